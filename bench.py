@@ -1,0 +1,288 @@
+"""S-CGIB pretrain-step throughput on MI355X (BASELINE.json metric).
+
+One step = on-device ego-net build (k-hop in-subgraphs of every node) +
+forward (transfer_d, GIN-64x5 x 2 encoders, fused compression/attention,
+MLP, KL + contrastive + reconstruction losses) + backward + gradient
+all-reduce (N > 1) + Adam(lr 1e-4, wd 5e-5) — exp_pretraining.py:290-333 with
+the Mainmodel_continue wrapper it trains (:109-113).
+
+Workload (config.workload): QM9-like synthetic molecules, B = 512 per GPU,
+k = 1, F = 11 (BASELINE.json configs[1]); weak scaling across GPUs.
+Inputs are resident in HBM before the timed region: a pool of distinct
+collated batches, cycled so consecutive steps see different molecules.
+
+Prints ONE JSON line on rank 0 (see README/DESIGN.md for the fields).
+"""
+from __future__ import annotations
+
+import argparse
+import importlib
+import json
+import os
+import statistics
+import sys
+import time
+from types import SimpleNamespace
+
+import numpy as np
+import torch
+import torch.distributed as dist
+import torch.nn.functional as F
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+pkg = importlib.import_module("s-cgib_amd")
+
+HBM_PEAK_GBS = 8000.0       # MI355X spec (MI355X_MICROARCH.md:36)
+HBM_MEASURED_GBS = 6290.0   # float4 copy, same file
+METRIC = "graphs/sec (pretrain step, GIN-64×5, k=1) at 1/2/4/8 MI355X; % HBM roofline"
+
+
+def agg_bytes(n, e, d):
+    """Algorithmic bytes of one GIN aggregation launch:
+    neighbour + self rows read, output written, col + rowptr read."""
+    return 4 * d * (e + n) + 4 * d * n + 4 * e + 4 * (n + 1)
+
+
+def make_model(F_in, k, gin_layers, dev):
+    args = SimpleNamespace(recons_type="adj", useAtt=1, readout_f="sum", d_transfer=32,
+                           batch_size=512, gin_layers=gin_layers, task="graph_classification")
+    inner = pkg.models.Mainmodel(args, F_in, 64, 4, 4, k, "GIN")
+    model = pkg.models.Mainmodel_continue(args, F_in, 64, 4, 4, k, 1, inner, "GIN")
+    return model.to(dev).train()
+
+
+class AggTimer:
+    """HIP-event timing of every GIN aggregation launch (fwd and bwd) on the
+    stream it is launched on (torch's current stream)."""
+
+    def __init__(self):
+        self.records = []  # (start_event, end_event, bytes)
+        self._orig = None
+
+    def __enter__(self):
+        ops = pkg.ops
+        self._orig = ops._aggregate
+        rec = self.records
+
+        def timed(h, rowptr, col, ope):
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record()
+            out = self._orig(h, rowptr, col, ope)
+            e.record()
+            rec.append((s, e, agg_bytes(h.shape[0], int(col.shape[0]), h.shape[1])))
+            return out
+
+        ops._aggregate = timed
+        return self
+
+    def __exit__(self, *exc):
+        pkg.ops._aggregate = self._orig
+
+    def summary(self):
+        torch.cuda.synchronize()
+        ms = [s.elapsed_time(e) for s, e, _ in self.records]
+        byts = [b for _, _, b in self.records]
+        return sum(byts) / len(byts), sum(ms) / len(ms), len(ms)
+
+
+def superbatch_roofline(dev, n_target=1_200_000, reps=20):
+    """GIN aggregation on a ZINC-scale superbatch whose [N,64] fp32 features
+    exceed the 256 MiB Infinity Cache (north_star's >=40 % target)."""
+    mols = pkg.synth.molecules(int(n_target / 23.2) + 1, "zinc", seed=123)
+    g, _ = pkg.graph.collate_pyg(mols)
+    g = g.to(dev)
+    n, e = g.num_nodes(), g.num_edges()
+    h = torch.randn(n, 64, device=dev)
+    out = torch.empty_like(h)
+    for _ in range(3):
+        out = pkg.ops._aggregate(h, g.rowptr, g.col, 1.0)
+    torch.cuda.synchronize()
+    s, t = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(reps):
+        out = pkg.ops._aggregate(h, g.rowptr, g.col, 1.0)
+    t.record()
+    torch.cuda.synchronize()
+    ms = s.elapsed_time(t) / reps
+    byts = agg_bytes(n, e, 64)
+    del out, h
+    return {"nodes": n, "edges": e, "bytes": byts, "us": ms * 1e3,
+            "gbs": byts / (ms * 1e-3) / 1e9}
+
+
+def cpu_baseline(pool_host, k, gin_layers, F_in, seconds=20.0):
+    """The oracle (literal restatement of the reference's CPU path: per-graph
+    loops, dense N x N recon) timed on this host's cores, bounded sample."""
+    from oracle import egonet
+    from oracle import scgib_ref as R
+
+    torch.manual_seed(0)
+    model = make_model(F_in, k, gin_layers, "cpu")
+    params = {kk: v.detach().clone().requires_grad_(v.is_floating_point() and "running" not in kk
+                                                    and not kk.endswith(".eps"))
+              for kk, v in R.strip_continue(
+                  {kk: v for kk, v in model.state_dict().items()
+                   if kk.startswith(("transfer_d.", "MLP.", "model.Encoder", "model.compressor.",
+                                     "model.attn_layer."))}).items()}
+    buffers = {kk: v for kk, v in params.items() if "running" in kk or "num_batches" in kk}
+    opt = torch.optim.Adam([v for v in params.values() if v.requires_grad], lr=1e-4,
+                           weight_decay=5e-5)
+    times, ego_times = [], []
+    t_end = time.perf_counter() + seconds
+    i = 0
+    while time.perf_counter() < t_end or i < 2:
+        gh = pool_host[i % len(pool_host)]
+        t0 = time.perf_counter()
+        sizes, ecount, nodes, esrc, edst = egonet.egonets(gh.rowptr.numpy(), gh.col.numpy(), k)
+        t1 = time.perf_counter()
+        off = np.repeat(np.concatenate([[0], np.cumsum(sizes)[:-1]]), ecount)
+        counts = torch.from_numpy(gh.batch_num_nodes_host())
+        src, dst = gh.edges()
+        batch = {"src": src, "dst": dst, "counts": counts}
+        ego = {"src": torch.from_numpy(esrc + off), "dst": torch.from_numpy(edst + off),
+               "counts": torch.from_numpy(sizes)}
+        x = F.normalize(gh.ndata["x"].float())
+        xs = x[torch.from_numpy(nodes)]
+        t2 = time.perf_counter()
+        opt.zero_grad(set_to_none=True)
+        out = R.pretrain_forward(params, batch, ego, x, xs, torch.rand(len(x)),
+                                 torch.rand(len(x), 64), 512, buffers)
+        out["loss_total"].backward()
+        opt.step()
+        t3 = time.perf_counter()
+        if i > 0:  # first step is warm-up
+            times.append(t3 - t2)
+            ego_times.append(t1 - t0)
+        i += 1
+    B = gh.batch_size
+    step = statistics.median(times)
+    return {"value": round(B / step, 2), "unit": "graphs/s", "cores": torch.get_num_threads(),
+            "kind": "port",
+            "sample": (f"oracle/scgib_ref.py pretrain step (fwd+bwd+Adam, dense NxN recon, "
+                       f"per-graph loops) on {B}-molecule QM9-like batches, median of "
+                       f"{len(times)} steps after 1 warm-up, torch CPU threads="
+                       f"{torch.get_num_threads()}, os.cpu_count={os.cpu_count()}; ego-nets "
+                       f"pre-extracted as in the reference (oracle/egonet_ref.c, "
+                       f"{statistics.median(ego_times) * 1e3:.1f} ms/batch, not in value)"),
+            "ms_per_step": round(step * 1e3, 2)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--workload", default="qm9")
+    ap.add_argument("--batch", type=int, default=512)
+    ap.add_argument("--k", type=int, default=1)
+    ap.add_argument("--gin-layers", type=int, default=5)
+    ap.add_argument("--pool", type=int, default=8)
+    ap.add_argument("--cpu-seconds", type=float, default=20.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-superbatch", action="store_true")
+    a = ap.parse_args()
+
+    rank, world, local = pkg.dist.init_from_env()
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+    torch.manual_seed(1234 + rank)
+    F_in = pkg.synth.WORKLOADS[a.workload][2]
+
+    # per-rank pool of distinct batches, resident in HBM
+    pool_host, pool = [], []
+    for i in range(a.pool):
+        mols = pkg.synth.molecules(a.batch, a.workload, seed=100_000 * rank + i)
+        gh, _ = pkg.graph.collate_pyg(mols)
+        pool_host.append(gh)
+        g = gh.to(dev)
+        dict.__setitem__(g.ndata, "x", F.normalize(g.ndata["x"].float()))  # exp_pretraining.py:312
+        pool.append(g)
+
+    model = make_model(F_in, a.k, a.gin_layers, dev)
+    opt = torch.optim.Adam(model.parameters(), lr=1e-4, weight_decay=5e-5)
+    reducer = pkg.dist.GradAllReducer(model.parameters())
+
+    def step(i):
+        g = pool[i % len(pool)]
+        opt.zero_grad(set_to_none=True)
+        _, kl, con, rec = model(g, g.ndata["x"], None, None, None, 1, None, a.k, dev, a.batch)
+        loss = kl + rec + con
+        loss.backward()
+        reducer()
+        opt.step()
+        return loss
+
+    for i in range(a.warmup):
+        step(i)
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    barrier()
+    t0 = time.perf_counter()
+    for i in range(a.steps):
+        loss = step(a.warmup + i)
+    barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    final_loss = float(loss.item())
+
+    # instrumented replay of the same steps: HIP events around every GIN
+    # aggregation launch (the dominant HBM kernel) for the roofline figure
+    with AggTimer() as timer:
+        for i in range(min(a.steps, 20)):
+            step(a.warmup + i)
+    avg_bytes, avg_ms, n_launch = timer.summary()
+    achieved = avg_bytes / (avg_ms * 1e-3) / 1e9
+
+    sb = None if a.no_superbatch or rank != 0 else superbatch_roofline(dev)
+    cpu = None
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        cpu = cpu_baseline(pool_host[:2], a.k, a.gin_layers, F_in, a.cpu_seconds)
+
+    if rank == 0:
+        total_graphs = world * a.batch * a.steps
+        n_nodes = statistics.mean(g.num_nodes() for g in pool)
+        line = {
+            "metric": METRIC,
+            "value": round(total_graphs / elapsed, 1),
+            "unit": "graphs/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(elapsed / a.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "fp32",
+            "data": "synthetic (seeded QM9-like molecules, SURVEY.md §8(d)); random-init weights",
+            "config": {"workload": f"{a.workload} pretrain step GIN-64x{a.gin_layers} "
+                                   f"k={a.k}, batch {a.batch}/GPU, Mainmodel_continue + Adam",
+                       "global_batch": world * a.batch, "nodes_per_batch": round(n_nodes, 1),
+                       "parallelism": f"dp{world}", "final_loss": round(final_loss, 4)},
+            "roofline": {"bound": "hbm", "kernel": "gin_aggregate_k (fwd+bwd launches)",
+                         "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4),
+                         "frac_vs_measured_copy": round(achieved / HBM_MEASURED_GBS, 4),
+                         "traffic": None, "avg_launch_us": round(avg_ms * 1e3, 3),
+                         "avg_bytes_per_launch": int(avg_bytes), "launches_timed": n_launch},
+            "roofline_superbatch": None if sb is None else {
+                "bound": "hbm", "kernel": "gin_aggregate_k d=64", "nodes": sb["nodes"],
+                "edges": sb["edges"], "achieved": round(sb["gbs"], 1), "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "frac": round(sb["gbs"] / HBM_PEAK_GBS, 4),
+                "avg_launch_us": round(sb["us"], 2)},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

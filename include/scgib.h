@@ -1,0 +1,163 @@
+/* scgib.h — C-ABI of the MI355X-native S-CGIB hot path (libscgib.so).
+ *
+ * The reference (O-JounLee/S-CGIB) is pure Python on PyTorch + DGL and has no
+ * FFI of its own; each entry point below replaces the
+ * library kernel the reference reaches through DGL / torch at the cited line.
+ * The Python host mirror (s-cgib_amd/ops.py, models.py) binds them with
+ * ctypes; INTEGRATION.md shows the binding.
+ *
+ * Conventions (every function):
+ *   - all pointers are DEVICE pointers (hipMalloc / torch CUDA tensors),
+ *     caller-allocated; indices int32, features fp32 row-major;
+ *   - `stream` is a hipStream_t (NULL = legacy default stream); every launch
+ *     is asynchronous on it, nothing synchronises, nothing allocates — so a
+ *     caller may capture any of them into a HIP graph;
+ *   - return 0 (SCGIB_OK), a negative SCGIB_E* argument error, or a positive
+ *     hipError_t from the launch; nothing throws across the ABI;
+ *   - deterministic: no floating-point atomics; every reduction has a fixed
+ *     order for a given shape.
+ */
+#ifndef SCGIB_H
+#define SCGIB_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef void *scgib_stream_t; /* hipStream_t */
+
+enum {
+    SCGIB_OK = 0,
+    SCGIB_EINVAL = -1,       /* null pointer / negative size / bad dim      */
+    SCGIB_EUNSUPPORTED = -2, /* shape outside what the kernels implement    */
+};
+
+#define SCGIB_HIDDEN 64     /* S-CGIB hidden width (args.dims, exp_pretraining.py:386) */
+#define SCGIB_STATS_STRIDE 260 /* floats per graph in the interaction stats slab */
+#define SCGIB_PGRAD_STRIDE 324 /* floats per graph in the parameter-gradient slab */
+
+int scgib_abi_version(void);
+const char *scgib_strerror(int code);
+
+/* ---- A5: GIN neighbourhood aggregation (DGL GINConv, sum aggregator) ------
+ * out[v,:] = one_plus_eps * h[v,:] + sum_{j in [rowptr[v], rowptr[v+1])} h[col[j],:]
+ * CSR is dst-major (row v lists the SOURCES of v's in-edges).  With the
+ * transposed CSR this is also the backward (grad_h from grad_out).
+ * Replaces DGL GINConv.forward -> update_all(copy_u, sum) (models.py:69).
+ * dim % 4 == 0, 4 <= dim <= 256. */
+int scgib_gin_aggregate(const float *h, const int32_t *rowptr, const int32_t *col,
+                        int64_t n_nodes, int32_t dim, float one_plus_eps, float *out,
+                        scgib_stream_t stream);
+
+/* ---- A6: per-segment readouts (dgl.sum_nodes) -------------------------------
+ * out[s,:] = sum_{i in [ptr[s], ptr[s+1])} x[i,:]   (models.py:716, 725, 733)
+ * segment_broadcast is its adjoint: out[i,:] = g[s,:] for every row i of s. */
+int scgib_segment_sum(const float *x, const int32_t *ptr, int64_t n_seg, int32_t dim,
+                      float *out, scgib_stream_t stream);
+int scgib_segment_broadcast(const float *g, const int32_t *ptr, int64_t n_seg, int32_t dim,
+                            float *out, scgib_stream_t stream);
+
+/* ---- A2: k-hop ego-net builder (dgl.khop_in_subgraph for every node) -------
+ * Replaces the per-node Python loop of exp_pretraining.py:269-272 (+ the
+ * per-step dgl.batch of the ego-nets, exp_pretraining.py:308-309).
+ * Graph: dst-major CSR (rowptr/col) of a batch of graphs whose node ranges are
+ * [graph_ptr[g], graph_ptr[g+1]); edges must stay inside their graph, column
+ * lists sorted ascending, the graph symmetric (to_bidirected output).
+ * max_graph_nodes <= 512.
+ *
+ * Step 1, scgib_egonet_count: fills ego_ptr[0..n] and ego_eptr[0..n] with the
+ * exclusive prefix sums of the ego-net node / edge counts (ego_ptr[n] = N_s,
+ * ego_eptr[n] = E_s).  `workspace` holds scgib_egonet_workspace_bytes(n).
+ * err (device int32, zeroed by the caller) becomes non-zero if an edge leaves
+ * its graph or a graph exceeds max_graph_nodes.
+ * Step 2, scgib_egonet_fill: writes, for the batched ego graph (ego j <-> node j,
+ * ego nodes sorted ascending, DGL node_subgraph edge order):
+ *   ego_nodes[N_s]   parent node id of every ego node (DGL's ndata['_ID'] + offset)
+ *   sub_rowptr[N_s+1], sub_col[E_s]  dst-major CSR in ego-batch node ids. */
+int64_t scgib_egonet_workspace_bytes(int64_t n_nodes);
+int scgib_egonet_count(const int32_t *rowptr, const int32_t *col, const int32_t *graph_ptr,
+                       int64_t n_graphs, int64_t n_nodes, int32_t k, int32_t max_graph_nodes,
+                       int32_t *ego_ptr, int32_t *ego_eptr, void *workspace, int32_t *err,
+                       scgib_stream_t stream);
+int scgib_egonet_fill(const int32_t *rowptr, const int32_t *col, const int32_t *graph_ptr,
+                      int64_t n_graphs, int64_t n_nodes, int32_t k, int32_t max_graph_nodes,
+                      const int32_t *ego_ptr, const int32_t *ego_eptr, int32_t *ego_nodes,
+                      int32_t *sub_rowptr, int32_t *sub_col, int32_t *err,
+                      scgib_stream_t stream);
+
+/* ---- A6-A8 + A10/A11 inputs: core <-> subgraph interaction, fused ----------
+ * One wavefront per molecule.  Restates, per graph i (models.py:595-604,
+ * 631-660, 714-749):
+ *   z2[i]   = sum_nodes(f)                                  (graph readout)
+ *   p       = W2 . relu(BN_i(t)) + b2   with t = f W1^T + b1 given, BN_i the
+ *             compressor BatchNorm over graph i's rows (train) or running
+ *             stats (eval)
+ *   lambda  = sigmoid(log(e) - log(1-e) + p),  e = 0.9999 - 0.9998 * u_gate
+ *   (sigma, mu) = std_mean(f_i) (unbiased), noisy = lambda f + (1-lambda) mu
+ *             + u_feat (1-lambda) sigma                    -> im[:, 0:64]
+ *   z1[i]   = sum_nodes(noisy)
+ *   logit_v = w_att[0:64].z1[i] + w_att[64:128].s_v + b_att, alpha = softmax_i
+ *   im[:, 64:128] = alpha * s
+ *   kl_tensor[2*n_last, 64]: the last graph's KL term, twice (models.py:659)
+ * Saved for backward: lam[N], logit[N], stats[B, SCGIB_STATS_STRIDE].
+ * Scalars b2, b_att are device pointers (no host sync). */
+int scgib_interaction_fwd(const float *f, const float *t, const float *s,
+                          const float *u_gate, const float *u_feat, const int32_t *graph_ptr,
+                          int64_t n_graphs, int64_t n_nodes, const float *bn_gamma,
+                          const float *bn_beta, const float *bn_running_mean,
+                          const float *bn_running_var, float bn_eps, int32_t training,
+                          const float *w2, const float *b2, const float *w_att,
+                          const float *b_att, float *im, float *z1, float *z2, float *lam,
+                          float *logit, float *stats, float *kl_tensor,
+                          scgib_stream_t stream);
+
+/* Sequential running-stat update of the per-graph compressor BatchNorm: one
+ * nn.BatchNorm1d call per graph in graph order (models.py:642 inside the loop
+ * of :639), i.e. B momentum updates with each graph's mean and unbiased var,
+ * and num_batches_tracked += B. */
+int scgib_bn_running_update(const float *stats, const int32_t *graph_ptr, int64_t n_graphs,
+                            float momentum, float *running_mean, float *running_var,
+                            int64_t *num_batches_tracked, scgib_stream_t stream);
+
+/* Backward of scgib_interaction_fwd.  g_kl may be NULL (no KL gradient).
+ * Outputs df, dt, ds [N,64] and per-graph parameter-gradient partials
+ * pgrad[B, SCGIB_PGRAD_STRIDE] laid out as
+ *   [0,64) dW2 | 64 db2 | [65,129) dgamma | [129,193) dbeta |
+ *   [193,321) dW_att | 321 db_att
+ * (sum them over graphs for the parameter gradients). */
+int scgib_interaction_bwd(const float *g_im, const float *g_z1, const float *g_z2,
+                          const float *g_kl, const float *f, const float *t, const float *s,
+                          const float *u_feat, const int32_t *graph_ptr, int64_t n_graphs,
+                          int64_t n_nodes, const float *bn_gamma, const float *bn_beta,
+                          const float *bn_running_mean, const float *bn_running_var,
+                          float bn_eps, int32_t training, const float *w2,
+                          const float *w_att, const float *z1, const float *lam,
+                          const float *logit, const float *stats, float *df, float *dt,
+                          float *ds, float *pgrad, scgib_stream_t stream);
+
+/* ---- A12: adjacency reconstruction loss, Gram form ------------------------
+ * loss = sum_{u,v} (<im_u, im_v> - A_uv)^2 / N
+ *      = (||IM^T IM||_F^2 - 2 sum_{(u,v) in E} <im_u, im_v> + |E|) / N
+ * exactly (A 0/1, simple graph) — replaces the dense N x N form of
+ * loss_recon_adj (models.py:762-768).  Two launches: partial Gram slabs
+ * (MFMA f32 32x32x2) + edge dot products, then a fixed-order fp64 finalize.
+ * `partials` holds scgib_recon_partials_floats(n) floats.
+ * Outputs: gram[64*64] (for backward) and loss[1]. */
+int64_t scgib_recon_partials_floats(int64_t n_nodes);
+int scgib_recon_fwd(const float *im, const int32_t *rowptr, const int32_t *col,
+                    int64_t n_nodes, int64_t n_edges, float *partials, float *gram,
+                    float *loss, scgib_stream_t stream);
+/* d loss / d im = (g_loss / N) * (4 IM G - 2 (A + A^T) IM); pass the in-CSR and
+ * the out-CSR (the same arrays for a symmetric graph).  g_loss is a device
+ * scalar. */
+int scgib_recon_bwd(const float *im, const float *gram, const int32_t *rowptr_in,
+                    const int32_t *col_in, const int32_t *rowptr_out, const int32_t *col_out,
+                    int64_t n_nodes, const float *g_loss, float *grad_im,
+                    scgib_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SCGIB_H */

@@ -1,0 +1,206 @@
+"""CPU restatement of the S-CGIB pretrain hot path (torch fp32, literal semantics).
+
+TEST INFRASTRUCTURE ONLY: imported by ``tests/``, ``__graft_entry__.smoke()``
+and ``bench.py``'s ``cpu_baseline`` leg, never by the product path.
+
+It restates, in its own code, what ``/root/reference/models.py`` computes, and
+keeps the reference's *structure* (per-graph Python loops, dense N x N
+reconstruction) so it doubles as the "reference CPU path" baseline:
+
+  GIN / GINConv / MLP ............ models.py:38-72  (+ DGL GINConv, eps buffer)
+  transfer_d on x and x_subs ...... models.py:668-669, 1164-1165
+  sum_nodes readouts .............. models.py:714-716, 724-726
+  compress / compression .......... models.py:595-604, 631-660
+  attention interaction ........... models.py:729-749
+  MLP on the interaction map ...... models.py:676, 1174
+  KL mean ......................... models.py:679
+  batched_semi_loss / sim ......... models.py:606-629
+  loss_recon_adj .................. models.py:762-768
+  forward (A13) / continue (A14) .. models.py:662-700, 1158-1195
+
+Quirks kept on purpose: per-graph compressor BatchNorm (one
+running-stat update per graph), uniform noise, only the last graph's KL,
+z-bar term of the attention logit included (it cancels in the softmax).
+
+Randomness is explicit: ``u_gate`` [N] and ``u_feat`` [N, 64] replace the
+reference's ``torch.rand(n_i, 1)`` / ``torch.rand_like`` draws per graph, in
+the same order (models.py:599, 650).
+
+Parameters are a dict keyed like ``Mainmodel.state_dict()`` (``model.``
+prefixes of the ``Mainmodel_continue`` wrapper stripped by
+``strip_continue``).
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn.functional as F
+
+BN_EPS = 1e-5
+BN_MOMENTUM = 0.1
+KL_EPS = 1e-7
+
+
+def strip_continue(params):
+    """Map Mainmodel_continue keys onto Mainmodel keys (A14 == A13 math)."""
+    return {(k[6:] if k.startswith("model.") else k): v for k, v in params.items()}
+
+
+def _linear(x, p, name, bias=True):
+    w = p[name + ".weight"]
+    b = p.get(name + ".bias") if bias else None
+    return F.linear(x, w, b)
+
+
+def _batchnorm_train(x, p, name, buffers):
+    """nn.BatchNorm1d in train mode (torch's own batch_norm kernel, as the
+    reference): batch stats for the output, unbiased var into the running
+    estimate, momentum 0.1, eps 1e-5."""
+    if x.shape[0] <= 1:
+        raise ValueError("Expected more than 1 value per channel when training")
+    if buffers is not None:
+        rm, rv = buffers[name + ".running_mean"], buffers[name + ".running_var"]
+        buffers[name + ".num_batches_tracked"] += 1
+    else:
+        rm = rv = None
+    return F.batch_norm(x, rm, rv, p[name + ".weight"], p[name + ".bias"], True,
+                        BN_MOMENTUM, BN_EPS)
+
+
+def gin_encoder(p, prefix, src, dst, h, buffers, num_layers):
+    """GIN.forward with DGL GINConv semantics (sum aggregation, (1+eps)*h)."""
+    for i in range(num_layers):
+        lp = f"{prefix}.ginlayers.{i}"
+        neigh = torch.zeros_like(h).index_add(0, dst, h[src])
+        eps = p.get(lp + ".eps", torch.zeros(1))
+        rst = (1 + eps) * h + neigh
+        z = F.relu(_linear(rst, p, lp + ".apply_func.mlp.0"))
+        z = _linear(z, p, lp + ".apply_func.mlp.2")
+        z = _batchnorm_train(z, p, f"{prefix}.batch_norms.{i}", buffers)
+        h = F.relu(z)
+    return h
+
+
+def num_gin_layers(p, prefix="Encoder1"):
+    i = 0
+    while f"{prefix}.ginlayers.{i}.apply_func.mlp.0.weight" in p:
+        i += 1
+    return i
+
+
+def sum_nodes(x, counts):
+    seg = torch.repeat_interleave(torch.arange(len(counts)), counts)
+    return torch.zeros(len(counts), x.shape[1], dtype=x.dtype).index_add(0, seg, x)
+
+
+def compression(p, graph_features, counts, u_gate, u_feat, buffers):
+    """Per-graph loop of models.py:631-660 with explicit noise."""
+    noisy_all, p_all, kl_all = [], [], None
+    off = 0
+    for n_i in counts.tolist():
+        feats = graph_features[off:off + n_i]
+        # compress(): compressor = Linear-BN-ReLU-Linear (models.py:589-596)
+        t = _linear(feats, p, "compressor.0")
+        t = _batchnorm_train(t, p, "compressor.1", buffers)
+        pv = _linear(F.relu(t), p, "compressor.3")
+        bias = 0.0 + 0.0001
+        eps = (bias - (1 - bias)) * u_gate[off:off + n_i].reshape(-1, 1) + (1 - bias)
+        gate = torch.log(eps) - torch.log(1 - eps)
+        lam = torch.sigmoid((gate + pv) / 1.0).squeeze().reshape(-1, 1)
+        lam_neg = 1 - lam
+        static = feats.clone().detach()
+        std, mean = torch.std_mean(static, dim=0)
+        noisy_mean = lam * feats + lam_neg * mean
+        noisy_std = lam_neg * std
+        noisy = noisy_mean + u_feat[off:off + n_i] * noisy_std
+        noisy_all.append(noisy)
+        p_all.append(pv)
+        kl = 0.5 * ((noisy_std ** 2) / (std + KL_EPS) ** 2) + torch.sum(
+            ((noisy_mean - mean) / (std + KL_EPS)) ** 2, dim=0)
+        kl_all = torch.cat((kl, kl), 0)  # only the last graph survives (models.py:659)
+        off += n_i
+    return torch.cat(noisy_all, 0), torch.cat(p_all, 0), kl_all
+
+
+def attention(p, noisy, sub_readout, counts):
+    """models.py:729-749 (readout == 'sum', useAtt == 1)."""
+    zbar = sum_nodes(noisy, counts)
+    outs, off = [], 0
+    for i, n_i in enumerate(counts.tolist()):
+        s_i = sub_readout[off:off + n_i]
+        inter = torch.cat((zbar[i].repeat(n_i, 1), s_i), -1)
+        logits = _linear(inter, p, "attn_layer")
+        alpha = F.softmax(logits, dim=0)
+        outs.append(s_i * alpha)
+        off += n_i
+    return torch.cat((noisy, torch.cat(outs, 0)), -1)
+
+
+def semi_loss(z1, z2, chunk):
+    """batched_semi_loss with tau = 1 (models.py:606-629)."""
+    n = z1.shape[0]
+    nb = (n - 1) // chunk + 1
+    z1n, z2n = F.normalize(z1), F.normalize(z2)
+    losses = []
+    for i in range(nb):
+        a, b = i * chunk, min((i + 1) * chunk, n)
+        refl = torch.exp(z1n[a:b] @ z1n.t())
+        betw = torch.exp(z1n[a:b] @ z2n.t())
+        losses.append(-torch.log(betw[:, a:b].diag() /
+                                 (refl.sum(1) + betw.sum(1) - refl[:, a:b].diag())))
+    return torch.cat(losses).mean()
+
+
+def recon_adj_dense(im, src, dst):
+    """Dense N x N restatement of loss_recon_adj (models.py:762-768)."""
+    n = im.shape[0]
+    adj = torch.zeros(n, n).index_put_((src, dst), torch.ones(len(src)), accumulate=True)
+    return torch.sum((im @ im.t() - adj) ** 2) / n
+
+
+def extract_features(p, batch, ego, h0, hs0, u_gate, u_feat, buffers):
+    L = num_gin_layers(p)
+    gf = gin_encoder(p, "Encoder1", batch["src"], batch["dst"], h0, buffers, L)
+    sf = gin_encoder(p, "Encoder2", ego["src"], ego["dst"], hs0, buffers, L)
+    readout = sum_nodes(gf, batch["counts"])
+    noisy, _, kl_tensor = compression(p, gf, batch["counts"], u_gate, u_feat, buffers)
+    sub_readout = sum_nodes(sf, ego["counts"])
+    im = attention(p, noisy, sub_readout, batch["counts"])
+    return {"graph_features": gf, "subgraph_features": sf, "graph_readout": readout,
+            "noisy": noisy, "kl_tensor": kl_tensor, "interaction_map": im}
+
+
+def pretrain_forward(p, batch, ego, x, x_subs, u_gate, u_feat, chunk, buffers=None,
+                     dense_recon=True):
+    """Mainmodel.forward (A13) == Mainmodel_continue.forward (A14).
+
+    ``x`` / ``x_subs`` are the already-normalised features, as the training loop
+    passes them (exp_pretraining.py:312-314).  Returns a dict with the three
+    losses, their sum and the intermediate activations.
+    """
+    h0 = _linear(x, p, "transfer_d", bias=False)
+    hs0 = _linear(x_subs, p, "transfer_d", bias=False)
+    acts = extract_features(p, batch, ego, h0, hs0, u_gate, u_feat, buffers)
+    im = _linear(F.relu(_linear(acts["interaction_map"], p, "MLP.0")), p, "MLP.2")
+    kl = torch.mean(acts["kl_tensor"])
+    z1 = sum_nodes(acts["noisy"], batch["counts"])
+    con = semi_loss(z1, acts["graph_readout"], chunk)
+    if dense_recon:
+        rec = recon_adj_dense(im, batch["src"], batch["dst"])
+    else:  # Gram form (exact restatement, used for large oracle runs)
+        g = im.t() @ im
+        e = (im[batch["src"]] * im[batch["dst"]]).sum()
+        rec = (torch.sum(g * g) - 2 * e + len(batch["src"])) / im.shape[0]
+    acts.update(im_mlp=im, loss_kl=kl, loss_contrastive=con, loss_recon=rec,
+                loss_total=kl + rec + con)
+    return acts
+
+
+def make_params(arrays, requires_grad=True):
+    """Tensors (fp32 leaf params, int buffers) from a fixture's ``param_*``."""
+    out = {}
+    for k, v in arrays.items():
+        t = torch.tensor(v)
+        if t.is_floating_point() and "running" not in k and not k.endswith(".eps"):
+            t.requires_grad_(requires_grad)
+        out[k] = t
+    return out

@@ -1,0 +1,25 @@
+"""S-CGIB hot path, MI355X-native.
+
+The package directory is ``s-cgib_amd`` (not a Python identifier), so import it
+with ``importlib.import_module("s-cgib_amd")`` and reach submodules as
+attributes (``pkg.models``, ``pkg.graph`` ...) — they load lazily.
+
+Layout:
+  csrc/        hand-written HIP kernels for gfx950 + the C-ABI (include/scgib.h)
+  _lib.py      ctypes binding of libscgib.so (fails loudly when missing)
+  graph.py     DGL-duck-typed graph batch (CSR int32, dst-major) + ingest
+  ops.py       autograd Functions over the C-ABI
+  models.py    models.py-compatible Mainmodel / Mainmodel_continue / GIN
+  dgl.py       drop-in ``dgl`` surface (graph, batch, sum_nodes, khop...)
+  dist.py      one-process-per-GPU data parallel (RCCL all-reduce)
+  synth.py     seeded synthetic molecules
+"""
+import importlib
+
+__all__ = ["graph", "ops", "models", "dgl", "dist", "synth", "_lib"]
+
+
+def __getattr__(name):
+    if name in __all__:
+        return importlib.import_module(f"{__name__}.{name}")
+    raise AttributeError(name)

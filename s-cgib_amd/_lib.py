@@ -1,0 +1,82 @@
+"""ctypes binding of libscgib.so (the C-ABI declared in include/scgib.h).
+
+There is no fallback: if the library is missing or cannot be loaded, every
+op raises.  Build it with ``__graft_entry__.build()`` or
+``make -C s-cgib_amd/csrc``.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libscgib.so")
+
+_P, _I64, _I32, _F = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32, ctypes.c_float
+
+# name -> (restype, argtypes); mirrors include/scgib.h exactly
+SIGNATURES = {
+    "scgib_abi_version": (ctypes.c_int, []),
+    "scgib_strerror": (ctypes.c_char_p, [ctypes.c_int]),
+    "scgib_gin_aggregate": (ctypes.c_int, [_P, _P, _P, _I64, _I32, _F, _P, _P]),
+    "scgib_segment_sum": (ctypes.c_int, [_P, _P, _I64, _I32, _P, _P]),
+    "scgib_segment_broadcast": (ctypes.c_int, [_P, _P, _I64, _I32, _P, _P]),
+    "scgib_egonet_workspace_bytes": (_I64, [_I64]),
+    "scgib_egonet_count": (ctypes.c_int, [_P, _P, _P, _I64, _I64, _I32, _I32, _P, _P, _P, _P, _P]),
+    "scgib_egonet_fill": (ctypes.c_int, [_P, _P, _P, _I64, _I64, _I32, _I32, _P, _P, _P, _P, _P,
+                                         _P, _P]),
+    "scgib_interaction_fwd": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _I64, _I64, _P, _P, _P, _P,
+                                             _F, _I32, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P,
+                                             _P, _P]),
+    "scgib_bn_running_update": (ctypes.c_int, [_P, _P, _I64, _F, _P, _P, _P, _P]),
+    "scgib_interaction_bwd": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _I64, _I64, _P,
+                                             _P, _P, _P, _F, _I32, _P, _P, _P, _P, _P, _P, _P,
+                                             _P, _P, _P, _P]),
+    "scgib_recon_partials_floats": (_I64, [_I64]),
+    "scgib_recon_fwd": (ctypes.c_int, [_P, _P, _P, _I64, _I64, _P, _P, _P, _P]),
+    "scgib_recon_bwd": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _I64, _P, _P, _P]),
+}
+
+STATS_STRIDE = 260
+PGRAD_STRIDE = 324
+HIDDEN = 64
+
+_lib = None
+
+
+class ScgibError(RuntimeError):
+    pass
+
+
+def load():
+    """Load libscgib.so once; raises ScgibError if it is absent or broken."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ScgibError(f"{LIB_PATH} not found: the HIP extension is not built "
+                         "(run __graft_entry__.build()); there is no CPU fallback")
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if lib.scgib_abi_version() != 1:
+        raise ScgibError("libscgib.so ABI version mismatch")
+    _lib = lib
+    return lib
+
+
+def call(name, *args):
+    """Invoke an int-returning C-ABI function and raise on a non-zero status."""
+    lib = load()
+    rc = getattr(lib, name)(*args)
+    if rc != 0:
+        msg = lib.scgib_strerror(rc).decode()
+        raise ScgibError(f"{name} failed: {msg} (code {rc})")
+    return rc
+
+
+def query(name, *args):
+    """Invoke a value-returning C-ABI function (sizes)."""
+    return getattr(load(), name)(*args)

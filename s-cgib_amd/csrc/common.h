@@ -1,0 +1,47 @@
+// Shared device helpers for the gfx950 kernels of libscgib.so.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/scgib.h"
+
+namespace scgib {
+
+constexpr int kWave = 64;  // CDNA wavefront
+constexpr int kHidden = SCGIB_HIDDEN;
+
+inline hipStream_t as_stream(scgib_stream_t s) { return reinterpret_cast<hipStream_t>(s); }
+
+// Launch status: the launch error of the last kernel, as a positive code.
+inline int launch_status() {
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? SCGIB_OK : static_cast<int>(e);
+}
+
+// Full-wave sum; every lane receives the total.  Fixed butterfly order, so
+// the result is bitwise identical on every lane and every run.
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, kWave);
+    return v;
+}
+
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) v = fmaxf(v, __shfl_xor(v, off, kWave));
+    return v;
+}
+
+// Bijective XCD-aware remap of a 1-D grid (cdna_hip_programming.md §5
+// "XCD swizzle must be bijective"): logical tiles t and t+1 land on the same
+// XCD, so neighbouring node ranges (same molecules, shared neighbour rows)
+// share that XCD's L2.  Speed only: any placement is correct.
+__device__ __forceinline__ int64_t xcd_remap(int64_t orig, int64_t nwg) {
+    if (nwg <= 8) return orig;
+    const int64_t xcd = orig % 8, q = nwg / 8, r = nwg % 8;
+    const int64_t base = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+    return base + orig / 8;
+}
+
+}  // namespace scgib

@@ -1,0 +1,311 @@
+// Fused k-hop ego-net builder (gfx950): dgl.khop_in_subgraph(g, v, k) for
+// every node v of a molecule batch, plus the dgl.batch of all of them, in
+// three launches (count + block scan, scan fix-up, fill).
+//
+// Reference call sites: exp_pretraining.py:269-272 (one libdgl call per
+// node, offline) and :308-309 (dgl.batch of the Σ n_i ego-nets every step).
+// Semantics restated in oracle/egonet_ref.c; bit-exact parity is tested.
+//
+// Design: molecules are small, so an ego-net never leaves its molecule and a
+// ball fits in a per-thread bitmap over the molecule's local node ids
+// (W 64-bit words in registers, n_graph <= 64 W, W in {1,2,4,8}).  One thread
+// builds one ego-net:
+//   ball = {v}; frontier = {v}; k times: frontier = ∪ in-nbrs(frontier),
+//   ball |= frontier                        (DGL: unique(cat(frontiers)))
+// The bitmap gives DGL's sorted node order for free (ascending set bits) and
+// the relabelling of an induced edge (u, w) is popcount(ball below w), so
+// the fill pass writes ego nodes and CSR rows directly in DGL order
+// (node_subgraph: rows in ball order, columns in CSR order).
+// Integer/pointer-chasing work: no MFMA, all index reads L2-resident.
+#include "common.h"
+
+namespace scgib {
+
+template <int W>
+__device__ __forceinline__ void bm_set(uint64_t (&b)[W], int32_t idx) {
+#pragma unroll
+    for (int i = 0; i < W; ++i) b[i] |= (i == (idx >> 6)) ? (1ull << (idx & 63)) : 0ull;
+}
+
+template <int W>
+__device__ __forceinline__ bool bm_test(const uint64_t (&b)[W], int32_t idx) {
+    uint64_t word = 0;
+#pragma unroll
+    for (int i = 0; i < W; ++i) word = (i == (idx >> 6)) ? b[i] : word;
+    return (word >> (idx & 63)) & 1ull;
+}
+
+// number of set bits strictly below idx
+template <int W>
+__device__ __forceinline__ int32_t bm_rank(const uint64_t (&b)[W], int32_t idx) {
+    int32_t r = 0;
+    const int wi = idx >> 6;
+    const uint64_t mask = (1ull << (idx & 63)) - 1ull;
+#pragma unroll
+    for (int i = 0; i < W; ++i) {
+        if (i < wi) r += __popcll(b[i]);
+        else if (i == wi) r += __popcll(b[i] & mask);
+    }
+    return r;
+}
+
+__device__ __forceinline__ int64_t graph_of(const int32_t *__restrict__ gptr, int64_t ng,
+                                            int64_t v) {
+    // largest g with gptr[g] <= v (graphs may be empty)
+    int64_t lo = 0, hi = ng - 1;
+    while (lo < hi) {
+        const int64_t mid = (lo + hi + 1) >> 1;
+        if (gptr[mid] <= v) lo = mid;
+        else hi = mid - 1;
+    }
+    return lo;
+}
+
+enum : int32_t { kErrEdgeLeavesGraph = 1, kErrGraphTooLarge = 2 };
+
+template <int W>
+__device__ __forceinline__ void build_ball(int32_t lv, int32_t base, int32_t ng, int k,
+                                           const int32_t *__restrict__ rowptr,
+                                           const int32_t *__restrict__ col,
+                                           uint64_t (&ball)[W], int32_t *err) {
+    uint64_t fr[W];
+#pragma unroll
+    for (int i = 0; i < W; ++i) ball[i] = fr[i] = 0ull;
+    bm_set<W>(ball, lv);
+    bm_set<W>(fr, lv);
+    for (int hop = 0; hop < k; ++hop) {
+        uint64_t nx[W];
+#pragma unroll
+        for (int i = 0; i < W; ++i) nx[i] = 0ull;
+#pragma unroll
+        for (int wi = 0; wi < W; ++wi) {
+            uint64_t m = fr[wi];
+            while (m) {
+                const int32_t u = wi * 64 + (__ffsll(static_cast<unsigned long long>(m)) - 1);
+                m &= m - 1ull;
+                const int32_t e1 = rowptr[base + u + 1];
+                for (int32_t j = rowptr[base + u]; j < e1; ++j) {
+                    const int32_t w = col[j] - base;
+                    if (w < 0 || w >= ng) {
+                        atomicOr(err, kErrEdgeLeavesGraph);
+                        continue;
+                    }
+                    bm_set<W>(nx, w);
+                }
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < W; ++i) {
+            ball[i] |= nx[i];
+            fr[i] = nx[i];
+        }
+    }
+}
+
+template <int W>
+__global__ __launch_bounds__(256) void egonet_count_k(
+    const int32_t *__restrict__ rowptr, const int32_t *__restrict__ col,
+    const int32_t *__restrict__ gptr, int64_t n_graphs, int64_t n, int k,
+    int32_t *__restrict__ ego_ptr, int32_t *__restrict__ ego_eptr,
+    int32_t *__restrict__ blk_tot, int32_t *err) {
+    __shared__ int32_t sn[256], se[256];
+    const int64_t v = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
+    int32_t nb = 0, ne = 0;
+    if (v < n) {
+        const int64_t g = graph_of(gptr, n_graphs, v);
+        const int32_t base = gptr[g], ng = gptr[g + 1] - base;
+        if (ng > 64 * W) {
+            atomicOr(err, kErrGraphTooLarge);
+        } else {
+            uint64_t ball[W];
+            build_ball<W>(static_cast<int32_t>(v - base), base, ng, k, rowptr, col, ball, err);
+#pragma unroll
+            for (int wi = 0; wi < W; ++wi) {
+                uint64_t m = ball[wi];
+                nb += __popcll(ball[wi]);
+                while (m) {
+                    const int32_t u = wi * 64 + (__ffsll(static_cast<unsigned long long>(m)) - 1);
+                    m &= m - 1ull;
+                    const int32_t e1 = rowptr[base + u + 1];
+                    for (int32_t j = rowptr[base + u]; j < e1; ++j) {
+                        const int32_t w = col[j] - base;
+                        if (w >= 0 && w < ng && bm_test<W>(ball, w)) ++ne;
+                    }
+                }
+            }
+        }
+    }
+    // block-inclusive scan of (nb, ne), Hillis-Steele in LDS
+    sn[threadIdx.x] = nb;
+    se[threadIdx.x] = ne;
+    __syncthreads();
+    for (int off = 1; off < 256; off <<= 1) {
+        int32_t an = 0, ae = 0;
+        if (threadIdx.x >= off) {
+            an = sn[threadIdx.x - off];
+            ae = se[threadIdx.x - off];
+        }
+        __syncthreads();
+        sn[threadIdx.x] += an;
+        se[threadIdx.x] += ae;
+        __syncthreads();
+    }
+    if (v < n) {
+        ego_ptr[v + 1] = sn[threadIdx.x];
+        ego_eptr[v + 1] = se[threadIdx.x];
+    }
+    if (threadIdx.x == 255) {
+        blk_tot[blockIdx.x] = sn[255];
+        blk_tot[gridDim.x + blockIdx.x] = se[255];
+    }
+}
+
+// Adds the exclusive prefix of the block totals to every element; each block
+// sums its predecessors itself (fixed order, no second scan launch).
+__global__ __launch_bounds__(256) void egonet_scan_fixup_k(int64_t n, int32_t nblk,
+                                                           const int32_t *__restrict__ blk_tot,
+                                                           int32_t *__restrict__ ego_ptr,
+                                                           int32_t *__restrict__ ego_eptr) {
+    __shared__ int32_t rn[256], re[256];
+    int32_t an = 0, ae = 0;
+    for (int32_t j = threadIdx.x; j < static_cast<int32_t>(blockIdx.x); j += 256) {
+        an += blk_tot[j];
+        ae += blk_tot[nblk + j];
+    }
+    rn[threadIdx.x] = an;
+    re[threadIdx.x] = ae;
+    __syncthreads();
+    for (int off = 128; off >= 1; off >>= 1) {
+        if (threadIdx.x < off) {
+            rn[threadIdx.x] += rn[threadIdx.x + off];
+            re[threadIdx.x] += re[threadIdx.x + off];
+        }
+        __syncthreads();
+    }
+    const int64_t v = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
+    if (v < n) {
+        ego_ptr[v + 1] += rn[0];
+        ego_eptr[v + 1] += re[0];
+    }
+    if (v == 0) {
+        ego_ptr[0] = 0;
+        ego_eptr[0] = 0;
+    }
+}
+
+template <int W>
+__global__ __launch_bounds__(256) void egonet_fill_k(
+    const int32_t *__restrict__ rowptr, const int32_t *__restrict__ col,
+    const int32_t *__restrict__ gptr, int64_t n_graphs, int64_t n, int k,
+    const int32_t *__restrict__ ego_ptr, const int32_t *__restrict__ ego_eptr,
+    int32_t *__restrict__ ego_nodes, int32_t *__restrict__ sub_rowptr,
+    int32_t *__restrict__ sub_col, int32_t *err) {
+    const int64_t v = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
+    if (v >= n) return;
+    if (v == n - 1) sub_rowptr[ego_ptr[n]] = ego_eptr[n];
+    const int64_t g = graph_of(gptr, n_graphs, v);
+    const int32_t base = gptr[g], ng = gptr[g + 1] - base;
+    if (ng > 64 * W) return;  // flagged by the count pass
+    uint64_t ball[W];
+    build_ball<W>(static_cast<int32_t>(v - base), base, ng, k, rowptr, col, ball, err);
+    const int32_t noff = ego_ptr[v];
+    int32_t eo = ego_eptr[v];
+    int32_t r = 0;
+#pragma unroll
+    for (int wi = 0; wi < W; ++wi) {
+        uint64_t m = ball[wi];
+        while (m) {
+            const int32_t u = wi * 64 + (__ffsll(static_cast<unsigned long long>(m)) - 1);
+            m &= m - 1ull;
+            ego_nodes[noff + r] = base + u;
+            sub_rowptr[noff + r] = eo;
+            const int32_t e1 = rowptr[base + u + 1];
+            for (int32_t j = rowptr[base + u]; j < e1; ++j) {
+                const int32_t w = col[j] - base;
+                if (w >= 0 && w < ng && bm_test<W>(ball, w)) sub_col[eo++] = noff + bm_rank<W>(ball, w);
+            }
+            ++r;
+        }
+    }
+}
+
+static int words_for(int32_t max_graph_nodes) {
+    if (max_graph_nodes <= 64) return 1;
+    if (max_graph_nodes <= 128) return 2;
+    if (max_graph_nodes <= 256) return 4;
+    if (max_graph_nodes <= 512) return 8;
+    return 0;
+}
+
+}  // namespace scgib
+
+using namespace scgib;
+
+extern "C" int64_t scgib_egonet_workspace_bytes(int64_t n_nodes) {
+    const int64_t nblk = (n_nodes + 255) / 256;
+    return 2 * sizeof(int32_t) * (nblk > 0 ? nblk : 1);
+}
+
+extern "C" int scgib_egonet_count(const int32_t *rowptr, const int32_t *col,
+                                  const int32_t *graph_ptr, int64_t n_graphs, int64_t n_nodes,
+                                  int32_t k, int32_t max_graph_nodes, int32_t *ego_ptr,
+                                  int32_t *ego_eptr, void *workspace, int32_t *err,
+                                  scgib_stream_t stream) {
+    if (n_nodes < 0 || n_graphs < 0 || k < 0) return SCGIB_EINVAL;
+    if (!ego_ptr || !ego_eptr || !err || !workspace) return SCGIB_EINVAL;
+    if (n_nodes > 0 && (!rowptr || !col || !graph_ptr || n_graphs == 0)) return SCGIB_EINVAL;
+    if (n_nodes >= (int64_t(1) << 31)) return SCGIB_EUNSUPPORTED;
+    const int W = words_for(max_graph_nodes);
+    if (W == 0) return SCGIB_EUNSUPPORTED;
+    hipStream_t st = as_stream(stream);
+    if (n_nodes == 0) {
+        hipError_t e = hipMemsetAsync(ego_ptr, 0, sizeof(int32_t), st);
+        if (e == hipSuccess) e = hipMemsetAsync(ego_eptr, 0, sizeof(int32_t), st);
+        return e == hipSuccess ? SCGIB_OK : static_cast<int>(e);
+    }
+    const int32_t nblk = static_cast<int32_t>((n_nodes + 255) / 256);
+    int32_t *blk_tot = static_cast<int32_t *>(workspace);
+#define SCGIB_EGO_COUNT(WW)                                                                     \
+    egonet_count_k<WW><<<nblk, 256, 0, st>>>(rowptr, col, graph_ptr, n_graphs, n_nodes, k,    \
+                                             ego_ptr, ego_eptr, blk_tot, err)
+    switch (W) {
+        case 1: SCGIB_EGO_COUNT(1); break;
+        case 2: SCGIB_EGO_COUNT(2); break;
+        case 4: SCGIB_EGO_COUNT(4); break;
+        default: SCGIB_EGO_COUNT(8); break;
+    }
+#undef SCGIB_EGO_COUNT
+    egonet_scan_fixup_k<<<nblk, 256, 0, st>>>(n_nodes, nblk, blk_tot, ego_ptr, ego_eptr);
+    return launch_status();
+}
+
+extern "C" int scgib_egonet_fill(const int32_t *rowptr, const int32_t *col,
+                                 const int32_t *graph_ptr, int64_t n_graphs, int64_t n_nodes,
+                                 int32_t k, int32_t max_graph_nodes, const int32_t *ego_ptr,
+                                 const int32_t *ego_eptr, int32_t *ego_nodes,
+                                 int32_t *sub_rowptr, int32_t *sub_col, int32_t *err,
+                                 scgib_stream_t stream) {
+    if (n_nodes < 0 || n_graphs < 0 || k < 0) return SCGIB_EINVAL;
+    if (!ego_ptr || !ego_eptr || !sub_rowptr || !err) return SCGIB_EINVAL;
+    if (n_nodes == 0) {
+        const hipError_t e = hipMemsetAsync(sub_rowptr, 0, sizeof(int32_t), as_stream(stream));
+        return e == hipSuccess ? SCGIB_OK : static_cast<int>(e);
+    }
+    if (!rowptr || !col || !graph_ptr || !ego_nodes || !sub_col) return SCGIB_EINVAL;
+    const int W = words_for(max_graph_nodes);
+    if (W == 0) return SCGIB_EUNSUPPORTED;
+    hipStream_t st = as_stream(stream);
+    const int64_t nblk = (n_nodes + 255) / 256;
+#define SCGIB_EGO_FILL(WW)                                                                      \
+    egonet_fill_k<WW><<<dim3((unsigned)nblk), 256, 0, st>>>(rowptr, col, graph_ptr, n_graphs,  \
+                                                            n_nodes, k, ego_ptr, ego_eptr,     \
+                                                            ego_nodes, sub_rowptr, sub_col, err)
+    switch (W) {
+        case 1: SCGIB_EGO_FILL(1); break;
+        case 2: SCGIB_EGO_FILL(2); break;
+        case 4: SCGIB_EGO_FILL(4); break;
+        default: SCGIB_EGO_FILL(8); break;
+    }
+#undef SCGIB_EGO_FILL
+    return launch_status();
+}

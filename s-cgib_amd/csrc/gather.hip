@@ -1,0 +1,154 @@
+// GIN neighbourhood aggregation and per-segment readouts (gfx950).
+//
+// Both are HBM/L2-bound gathers of fp32 rows.  A row of `dim` floats is
+// split into dim/4 float4 lanes (LPR lanes per row, 16 for dim 64), so one
+// wave instruction moves 64 x 16 B = 1 KiB of 4 (dim 64) or 8 (dim 32)
+// different rows: every load is a full 16-B-per-lane coalesced access and
+// several neighbour rows are in flight per wave.  Neighbour loads are issued
+// four at a time before they are consumed (latency hiding, Guideline 7).
+// Sums run in CSR order, so results are deterministic.
+#include <type_traits>
+
+#include "common.h"
+
+namespace scgib {
+
+__device__ __forceinline__ float4 f4add(float4 a, float4 b) {
+    return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
+}
+
+template <int LPR>
+__global__ __launch_bounds__(256) void gin_aggregate_k(const float4 *__restrict__ h,
+                                                       const int32_t *__restrict__ rowptr,
+                                                       const int32_t *__restrict__ col,
+                                                       int64_t n, float ope,
+                                                       float4 *__restrict__ out) {
+    constexpr int RPB = 256 / LPR;
+    const int64_t blk = xcd_remap(blockIdx.x, gridDim.x);
+    const int64_t v = blk * RPB + threadIdx.x / LPR;
+    const int c = threadIdx.x % LPR;
+    if (v >= n) return;
+    const int32_t beg = rowptr[v], end = rowptr[v + 1];
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    int32_t j = beg;
+    for (; j + 4 <= end; j += 4) {
+        const int64_t u0 = col[j], u1 = col[j + 1], u2 = col[j + 2], u3 = col[j + 3];
+        const float4 a0 = h[u0 * LPR + c], a1 = h[u1 * LPR + c];
+        const float4 a2 = h[u2 * LPR + c], a3 = h[u3 * LPR + c];
+        acc = f4add(f4add(f4add(f4add(acc, a0), a1), a2), a3);
+    }
+    for (; j < end; ++j) acc = f4add(acc, h[static_cast<int64_t>(col[j]) * LPR + c]);
+    const float4 self = h[v * LPR + c];
+    // DGL GINConv: rst = (1 + eps) * feat_dst + neigh
+    out[v * LPR + c] = make_float4(ope * self.x + acc.x, ope * self.y + acc.y,
+                                   ope * self.z + acc.z, ope * self.w + acc.w);
+}
+
+template <int LPR>
+__global__ __launch_bounds__(256) void segment_sum_k(const float4 *__restrict__ x,
+                                                     const int32_t *__restrict__ ptr,
+                                                     int64_t nseg, float4 *__restrict__ out) {
+    constexpr int RPB = 256 / LPR;
+    const int64_t blk = xcd_remap(blockIdx.x, gridDim.x);
+    const int64_t s = blk * RPB + threadIdx.x / LPR;
+    const int c = threadIdx.x % LPR;
+    if (s >= nseg) return;
+    const int64_t beg = ptr[s], end = ptr[s + 1];
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    int64_t i = beg;
+    for (; i + 4 <= end; i += 4) {
+        const float4 a0 = x[i * LPR + c], a1 = x[(i + 1) * LPR + c];
+        const float4 a2 = x[(i + 2) * LPR + c], a3 = x[(i + 3) * LPR + c];
+        acc = f4add(f4add(f4add(f4add(acc, a0), a1), a2), a3);
+    }
+    for (; i < end; ++i) acc = f4add(acc, x[i * LPR + c]);
+    out[s * LPR + c] = acc;
+}
+
+template <int LPR>
+__global__ __launch_bounds__(256) void segment_broadcast_k(const float4 *__restrict__ g,
+                                                           const int32_t *__restrict__ ptr,
+                                                           int64_t nseg,
+                                                           float4 *__restrict__ out) {
+    constexpr int RPB = 256 / LPR;
+    const int64_t blk = xcd_remap(blockIdx.x, gridDim.x);
+    const int64_t s = blk * RPB + threadIdx.x / LPR;
+    const int c = threadIdx.x % LPR;
+    if (s >= nseg) return;
+    const float4 val = g[s * LPR + c];
+    for (int64_t i = ptr[s]; i < ptr[s + 1]; ++i) out[i * LPR + c] = val;
+}
+
+
+#define SCGIB_DISPATCH_LPR(dim, KERNEL, GRID_ROWS, ...)                                    \
+    do {                                                                                    \
+        const int lpr_ = (dim) / 4;                                                         \
+        auto launch_ = [&](auto tag) {                                                      \
+            constexpr int L = decltype(tag)::value;                                         \
+            const int64_t rpb = 256 / L;                                                    \
+            const int64_t grid = ((GRID_ROWS) + rpb - 1) / rpb;                             \
+            if (grid > 0) KERNEL<L><<<dim3((unsigned)grid), dim3(256), 0, st>>>(__VA_ARGS__); \
+        };                                                                                  \
+        switch (lpr_) {                                                                     \
+            case 1: launch_(std::integral_constant<int, 1>{}); break;                       \
+            case 2: launch_(std::integral_constant<int, 2>{}); break;                       \
+            case 4: launch_(std::integral_constant<int, 4>{}); break;                       \
+            case 8: launch_(std::integral_constant<int, 8>{}); break;                       \
+            case 16: launch_(std::integral_constant<int, 16>{}); break;                     \
+            case 32: launch_(std::integral_constant<int, 32>{}); break;                     \
+            case 64: launch_(std::integral_constant<int, 64>{}); break;                     \
+            default: return SCGIB_EUNSUPPORTED;                                             \
+        }                                                                                   \
+    } while (0)
+
+static bool dim_ok(int32_t dim) {
+    return dim >= 4 && dim <= 256 && dim % 4 == 0 && ((dim / 4) & (dim / 4 - 1)) == 0;
+}
+
+}  // namespace scgib
+
+using namespace scgib;
+
+extern "C" int scgib_gin_aggregate(const float *h, const int32_t *rowptr, const int32_t *col,
+                                   int64_t n_nodes, int32_t dim, float one_plus_eps,
+                                   float *out, scgib_stream_t stream) {
+    if (n_nodes < 0 || !dim_ok(dim)) return SCGIB_EINVAL;
+    if (n_nodes == 0) return SCGIB_OK;
+    if (!h || !rowptr || !col || !out) return SCGIB_EINVAL;
+    hipStream_t st = as_stream(stream);
+    SCGIB_DISPATCH_LPR(dim, gin_aggregate_k, n_nodes, reinterpret_cast<const float4 *>(h),
+                       rowptr, col, n_nodes, one_plus_eps, reinterpret_cast<float4 *>(out));
+    return launch_status();
+}
+
+extern "C" int scgib_segment_sum(const float *x, const int32_t *ptr, int64_t n_seg,
+                                 int32_t dim, float *out, scgib_stream_t stream) {
+    if (n_seg < 0 || !dim_ok(dim)) return SCGIB_EINVAL;
+    if (n_seg == 0) return SCGIB_OK;
+    if (!x || !ptr || !out) return SCGIB_EINVAL;
+    hipStream_t st = as_stream(stream);
+    SCGIB_DISPATCH_LPR(dim, segment_sum_k, n_seg, reinterpret_cast<const float4 *>(x), ptr,
+                       n_seg, reinterpret_cast<float4 *>(out));
+    return launch_status();
+}
+
+extern "C" int scgib_segment_broadcast(const float *g, const int32_t *ptr, int64_t n_seg,
+                                       int32_t dim, float *out, scgib_stream_t stream) {
+    if (n_seg < 0 || !dim_ok(dim)) return SCGIB_EINVAL;
+    if (n_seg == 0) return SCGIB_OK;
+    if (!g || !ptr || !out) return SCGIB_EINVAL;
+    hipStream_t st = as_stream(stream);
+    SCGIB_DISPATCH_LPR(dim, segment_broadcast_k, n_seg, reinterpret_cast<const float4 *>(g),
+                       ptr, n_seg, reinterpret_cast<float4 *>(out));
+    return launch_status();
+}
+
+extern "C" int scgib_abi_version(void) { return 1; }
+
+extern "C" const char *scgib_strerror(int code) {
+    if (code == SCGIB_OK) return "ok";
+    if (code == SCGIB_EINVAL) return "invalid argument (null pointer, negative size or bad dim)";
+    if (code == SCGIB_EUNSUPPORTED) return "shape not supported by the kernels";
+    if (code > 0) return hipGetErrorString(static_cast<hipError_t>(code));
+    return "unknown scgib error";
+}

@@ -1,0 +1,198 @@
+// Adjacency-reconstruction loss in Gram form (gfx950).
+//
+// Reference: loss_recon_adj (models.py:762-768, :1256-1262) materialises the
+// dense N x N matrix IM IM^T - A of the whole batch (0.3 GB at QM9 B=512,
+// ~3 GB at B >= 1024) and reduces it.  For a 0/1 adjacency of a simple graph
+//   sum_{u,v} (<im_u,im_v> - A_uv)^2 = ||IM^T IM||_F^2 - 2 sum_E <im_u,im_v> + |E|
+// exactly, so the loss needs the 64 x 64 Gram matrix G = IM^T IM plus one dot
+// product per edge: O(N d^2) flops over one read of IM (HBM-bound), no N^2.
+//
+// recon_partial_k: each workgroup reduces a contiguous row range; its four
+//   wavefronts each own one 32x32 quadrant of G and accumulate it with the
+//   exact-f32 MFMA v_mfma_f32_32x32x2_f32 (two rows per instruction: lane l
+//   feeds row l>>5, channel l&31 of the quadrant's A and B halves), then
+//   the same wavefronts sum <im_v, sum_{u->v} im_u> for their rows.
+// recon_finalize_k: 16 workgroups each reduce 256 Gram entries over the
+//   partial slabs in fp64 (fixed order) and publish a partial ||G||^2; the
+//   last-arriving workgroup (agent-scope release/acquire, Guideline 16)
+//   forms the loss.  Deterministic for a given N.
+// recon_bwd_k: grad_v = (g/N) (4 (IM G)_v - 2 ((A + A^T) IM)_v), G staged in
+//   LDS, the row of IM broadcast from LDS.
+#include "common.h"
+
+namespace scgib {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+constexpr int kGram = 64 * 64;
+constexpr int kFinBlocks = 16;  // 16 x 256 threads = one Gram entry per thread
+
+__host__ __device__ __forceinline__ int64_t recon_blocks(int64_t n) {
+    int64_t g = (n + 255) / 256;
+    return g < 1 ? 1 : (g > 256 ? 256 : g);
+}
+
+// partials layout (floats): [G][4096] gram slabs | edge sums [G, padded to a
+// multiple of 4] | 16 doubles ||G||^2 partials | uint32 arrival counter (+pad)
+__host__ __device__ __forceinline__ int64_t off_edge(int64_t G) { return G * kGram; }
+__host__ __device__ __forceinline__ int64_t off_gsq(int64_t G) { return G * kGram + ((G + 3) & ~int64_t(3)); }
+__host__ __device__ __forceinline__ int64_t off_cnt(int64_t G) { return off_gsq(G) + 2 * kFinBlocks; }
+__global__ __launch_bounds__(256) void recon_partial_k(const float *__restrict__ im,
+                                                       const int32_t *__restrict__ rowptr,
+                                                       const int32_t *__restrict__ col,
+                                                       int64_t n, int64_t rows_per_blk,
+                                                       float *__restrict__ partials) {
+    const int G = gridDim.x;
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int64_t rb = static_cast<int64_t>(blockIdx.x) * rows_per_blk;
+    const int64_t re = rb + rows_per_blk < n ? rb + rows_per_blk : n;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        // arrival counter of the finalize kernel (stream-ordered before it)
+        *reinterpret_cast<unsigned *>(partials + off_cnt(G)) = 0u;
+    }
+    const int ta = w >> 1, tb = w & 1;
+    const int kk = lane >> 5, ch = lane & 31;
+    f32x16 acc;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+    int64_t r = rb;
+    for (; r + 8 <= re; r += 8) {
+        float a[4], b[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int64_t row = r + 2 * q + kk;
+            a[q] = im[row * 64 + ta * 32 + ch];
+            b[q] = im[row * 64 + tb * 32 + ch];
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[q], b[q], acc, 0, 0, 0);
+    }
+    for (; r < re; r += 2) {
+        const int64_t row = r + kk;
+        const float a = row < re ? im[row * 64 + ta * 32 + ch] : 0.f;
+        const float b = row < re ? im[row * 64 + tb * 32 + ch] : 0.f;
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc, 0, 0, 0);
+    }
+    float *slab = partials + static_cast<int64_t>(blockIdx.x) * kGram;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+        const int row = (j & 3) + 8 * (j >> 2) + 4 * (lane >> 5);
+        slab[(ta * 32 + row) * 64 + tb * 32 + (lane & 31)] = acc[j];
+    }
+    // edge term: sum over rows v of this block of <im_v, sum_{u->v} im_u>
+    float e = 0.f;
+    for (int64_t v = rb + w; v < re; v += 4) {
+        float nb = 0.f;
+        for (int32_t j = rowptr[v]; j < rowptr[v + 1]; ++j) nb += im[static_cast<int64_t>(col[j]) * 64 + lane];
+        e += im[v * 64 + lane] * nb;
+    }
+    e = wave_sum(e);
+    __shared__ float we[4];
+    if (lane == 0) we[w] = e;
+    __syncthreads();
+    if (threadIdx.x == 0) partials[off_edge(G) + blockIdx.x] = ((we[0] + we[1]) + we[2]) + we[3];
+}
+
+__global__ __launch_bounds__(256) void recon_finalize_k(float *__restrict__ partials, int G,
+                                                        int64_t n, int64_t n_edges,
+                                                        float *__restrict__ gram,
+                                                        float *__restrict__ loss) {
+    const int e = blockIdx.x * 256 + threadIdx.x;  // Gram entry
+    double acc = 0.0;
+    for (int b = 0; b < G; ++b) acc += static_cast<double>(partials[(int64_t)b * kGram + e]);
+    gram[e] = static_cast<float>(acc);
+    __shared__ double red[256];
+    red[threadIdx.x] = acc * acc;
+    __syncthreads();
+    for (int off = 128; off >= 1; off >>= 1) {
+        if (threadIdx.x < off) red[threadIdx.x] += red[threadIdx.x + off];
+        __syncthreads();
+    }
+    double *gsq = reinterpret_cast<double *>(partials + off_gsq(G));
+    unsigned *cnt = reinterpret_cast<unsigned *>(partials + off_cnt(G));
+    __shared__ unsigned ticket;
+    if (threadIdx.x == 0) {
+        gsq[blockIdx.x] = red[0];
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        ticket = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    if (ticket != kFinBlocks - 1) return;  // not the last arriver
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        double g2 = 0.0;
+        for (int b = 0; b < kFinBlocks; ++b) g2 += __hip_atomic_load(&gsq[b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        double es = 0.0;
+        const float *ep = partials + off_edge(G);
+        for (int b = 0; b < G; ++b) es += static_cast<double>(ep[b]);
+        *loss = static_cast<float>((g2 - 2.0 * es + static_cast<double>(n_edges)) / static_cast<double>(n));
+    }
+}
+
+__global__ __launch_bounds__(256) void recon_bwd_k(const float *__restrict__ im,
+                                                   const float *__restrict__ gram,
+                                                   const int32_t *__restrict__ rp_in,
+                                                   const int32_t *__restrict__ c_in,
+                                                   const int32_t *__restrict__ rp_out,
+                                                   const int32_t *__restrict__ c_out, int64_t n,
+                                                   const float *__restrict__ g_loss,
+                                                   float *__restrict__ out) {
+    __shared__ float sg[kGram];
+    __shared__ float srow[4][64];
+    for (int i = threadIdx.x; i < kGram; i += 256) sg[i] = gram[i];
+    __syncthreads();
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const float scale = *g_loss / static_cast<float>(n);
+    const int64_t rows_per_blk = 64;
+    const int64_t rb = xcd_remap(blockIdx.x, gridDim.x) * rows_per_blk;
+    for (int64_t v = rb + w; v < rb + rows_per_blk && v < n; v += 4) {
+        const float iv = im[v * 64 + lane];
+        srow[w][lane] = iv;
+        __builtin_amdgcn_wave_barrier();
+        float acc = 0.f;
+#pragma unroll 16
+        for (int k = 0; k < 64; ++k) acc += srow[w][k] * sg[k * 64 + lane];
+        float nb = 0.f;
+        for (int32_t j = rp_in[v]; j < rp_in[v + 1]; ++j) nb += im[static_cast<int64_t>(c_in[j]) * 64 + lane];
+        for (int32_t j = rp_out[v]; j < rp_out[v + 1]; ++j) nb += im[static_cast<int64_t>(c_out[j]) * 64 + lane];
+        out[v * 64 + lane] = scale * (4.f * acc - 2.f * nb);
+        __builtin_amdgcn_wave_barrier();
+    }
+}
+
+}  // namespace scgib
+
+using namespace scgib;
+
+extern "C" int64_t scgib_recon_partials_floats(int64_t n_nodes) {
+    return off_cnt(recon_blocks(n_nodes)) + 4;
+}
+
+extern "C" int scgib_recon_fwd(const float *im, const int32_t *rowptr, const int32_t *col,
+                               int64_t n_nodes, int64_t n_edges, float *partials, float *gram,
+                               float *loss, scgib_stream_t stream) {
+    if (n_nodes <= 0 || n_edges < 0) return SCGIB_EINVAL;
+    if (!im || !rowptr || (n_edges > 0 && !col) || !partials || !gram || !loss) return SCGIB_EINVAL;
+    const int64_t G = recon_blocks(n_nodes);
+    int64_t rows = (n_nodes + G - 1) / G;
+    rows += rows & 1;  // even: the MFMA consumes rows in pairs
+    hipStream_t st = as_stream(stream);
+    recon_partial_k<<<dim3((unsigned)G), 256, 0, st>>>(im, rowptr, col, n_nodes, rows, partials);
+    recon_finalize_k<<<kFinBlocks, 256, 0, st>>>(partials, (int)G, n_nodes, n_edges, gram, loss);
+    return launch_status();
+}
+
+extern "C" int scgib_recon_bwd(const float *im, const float *gram, const int32_t *rowptr_in,
+                               const int32_t *col_in, const int32_t *rowptr_out,
+                               const int32_t *col_out, int64_t n_nodes, const float *g_loss,
+                               float *grad_im, scgib_stream_t stream) {
+    if (n_nodes <= 0) return SCGIB_EINVAL;
+    if (!im || !gram || !rowptr_in || !rowptr_out || !g_loss || !grad_im) return SCGIB_EINVAL;
+    const int64_t grid = (n_nodes + 63) / 64;
+    recon_bwd_k<<<dim3((unsigned)grid), 256, 0, as_stream(stream)>>>(
+        im, gram, rowptr_in, col_in, rowptr_out, col_out, n_nodes, g_loss, grad_im);
+    return launch_status();
+}

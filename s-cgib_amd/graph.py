@@ -1,0 +1,357 @@
+"""Batched molecular graphs for the S-CGIB hot path (DGL-duck-typed).
+
+Reference surface reproduced: the model consumes a DGL
+graph — ``batch_num_nodes()`` (models.py:665), ``ndata`` reads/writes
+(exp_pretraining.py:304, models.py:683), ``edges()``, ``.to(device)``,
+``adj().to_dense()`` (models.py:764), ``nodes()`` / ``num_nodes()``.
+
+Storage, MI355X-first:
+  * ``rowptr`` [N+1] / ``col`` [E] int32: dst-major CSR (row v lists the
+    sources of v's in-edges, columns ascending) — the layout the GIN gather
+    kernel reads; 4-byte indices halve index traffic vs int64;
+  * ``rowptr_t`` / ``col_t``: the src-major CSR (the same tensors when the
+    graph is symmetric, i.e. every to_bidirected molecule);
+  * ``graph_ptr`` [B+1] int32: node range of every molecule;
+  * host copies of the per-graph node/edge counts, so shape decisions never
+    synchronise with the device.
+
+Ingest restates ``util.load_dgl_fromPyG`` (util.py:277-325): ``dgl.graph``
+infers ``num_nodes = max id + 1``, ``to_bidirected`` adds reverse edges and
+rebuilds a simple graph with edges sorted by (src, dst); a molecule whose
+``x`` row count differs from that node count (trailing isolated atoms, no
+bonds) raises, which the reference's bare ``except`` turns into "skip"
+(exp_pretraining.py:276-278).
+"""
+from __future__ import annotations
+
+import contextlib
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _lib
+
+
+class GraphIngestError(ValueError):
+    """Raised where DGL raises on ``g.ndata['x'] = x`` (row-count mismatch)."""
+
+
+class _NData(dict):
+    def __init__(self, graph):
+        super().__init__()
+        self._g = graph
+
+    def __setitem__(self, key, value):
+        if value.shape[0] != self._g.num_nodes():
+            raise GraphIngestError(
+                f"Expect number of features to match number of nodes. Got {value.shape[0]} "
+                f"and {self._g.num_nodes()} instead.")
+        super().__setitem__(key, value)
+
+
+class _Adj:
+    def __init__(self, g):
+        self._g = g
+
+    def to_dense(self):
+        src, dst = self._g.edges()
+        n = self._g.num_nodes()
+        a = torch.zeros(n, n, dtype=torch.float32, device=src.device)
+        a[src, dst] = 1.0
+        return a
+
+
+def _csr_from_sorted(keys_major, minor, n):
+    """CSR from edges already sorted by (major, minor)."""
+    counts = np.bincount(keys_major, minlength=n) if n else np.zeros(0, np.int64)
+    rowptr = np.zeros(n + 1, dtype=np.int64)
+    np.cumsum(counts, out=rowptr[1:])
+    return rowptr.astype(np.int32), minor.astype(np.int32)
+
+
+class GraphBatch:
+    """A batch of B graphs with N nodes and E directed edges."""
+
+    def __init__(self, rowptr, col, graph_ptr, batch_num_nodes, batch_num_edges=None,
+                 rowptr_t=None, col_t=None, max_graph_nodes=None, n_edges=None):
+        self.rowptr = rowptr
+        self.col = col
+        self.rowptr_t = rowptr if rowptr_t is None else rowptr_t
+        self.col_t = col if col_t is None else col_t
+        self.symmetric = rowptr_t is None
+        self.graph_ptr = graph_ptr
+        self._bnn = None if batch_num_nodes is None else np.asarray(batch_num_nodes, np.int64)
+        self._bne = None if batch_num_edges is None else np.asarray(batch_num_edges, np.int64)
+        self._n = int(rowptr.shape[0] - 1)
+        self._e = int(col.shape[0]) if n_edges is None else int(n_edges)
+        self._B = int(graph_ptr.shape[0] - 1)
+        if max_graph_nodes is None:
+            max_graph_nodes = int(self._bnn.max()) if self._bnn is not None and len(self._bnn) else 0
+        self.max_graph_nodes = int(max_graph_nodes)
+        self.ndata = _NData(self)
+        self.edata = {}
+
+    # ----- construction ---------------------------------------------------
+    @classmethod
+    def from_edges(cls, src, dst, num_nodes, symmetric_hint=False, batch_num_nodes=None,
+                   batch_num_edges=None):
+        """Graph from a COO edge list (kept as a multigraph-free CSR)."""
+        src = np.asarray(src, np.int64)
+        dst = np.asarray(dst, np.int64)
+        n = int(num_nodes)
+        order_out = np.lexsort((dst, src))
+        rp_t, col_t = _csr_from_sorted(src[order_out], dst[order_out], n)
+        if symmetric_hint:
+            rp, col, rp_t2, col_t2 = rp_t, col_t, None, None
+        else:
+            order_in = np.lexsort((src, dst))
+            rp, col = _csr_from_sorted(dst[order_in], src[order_in], n)
+            rp_t2, col_t2 = torch.from_numpy(rp_t), torch.from_numpy(col_t)
+        if batch_num_nodes is None:
+            batch_num_nodes = np.array([n], np.int64)
+            batch_num_edges = np.array([len(src)], np.int64)
+        gptr = np.zeros(len(batch_num_nodes) + 1, np.int64)
+        np.cumsum(batch_num_nodes, out=gptr[1:])
+        return cls(torch.from_numpy(rp), torch.from_numpy(col),
+                   torch.from_numpy(gptr.astype(np.int32)), batch_num_nodes, batch_num_edges,
+                   rp_t2, col_t2)
+
+    # ----- DGL surface ------------------------------------------------------
+    def num_nodes(self, ntype=None):
+        return self._n
+
+    number_of_nodes = num_nodes
+
+    def num_edges(self, etype=None):
+        return self._e
+
+    number_of_edges = num_edges
+
+    @property
+    def batch_size(self):
+        return self._B
+
+    @property
+    def device(self):
+        return self.rowptr.device
+
+    def batch_num_nodes(self, ntype=None):
+        if self._bnn is None:
+            gp = self.graph_ptr.to("cpu", torch.int64)
+            self._bnn = (gp[1:] - gp[:-1]).numpy()
+        return torch.from_numpy(self._bnn)
+
+    def batch_num_nodes_host(self):
+        """Per-graph node counts as a host numpy array (no device sync)."""
+        self.batch_num_nodes()
+        return self._bnn
+
+    def batch_num_edges(self, etype=None):
+        if self._bne is None:
+            rp_t = self.rowptr_t.to("cpu", torch.int64)
+            gp = self.graph_ptr.to("cpu", torch.int64)
+            self._bne = (rp_t[gp[1:]] - rp_t[gp[:-1]]).numpy()
+        return torch.from_numpy(self._bne)
+
+    def nodes(self, ntype=None):
+        return torch.arange(self._n, dtype=torch.int64, device=self.device)
+
+    def edges(self, form="uv", order="eid", etype=None):
+        """(src, dst) int64 in DGL's order for to_bidirected graphs: (src, dst) sorted."""
+        deg = (self.rowptr_t[1:] - self.rowptr_t[:-1]).to(torch.int64)
+        src = torch.repeat_interleave(torch.arange(self._n, device=self.device), deg)
+        return src, self.col_t[: self._e].to(torch.int64)
+
+    def in_degrees(self):
+        return (self.rowptr[1:] - self.rowptr[:-1]).to(torch.int64)
+
+    def adj(self, etype=None, eweight_name=None):
+        return _Adj(self)
+
+    def to(self, device, non_blocking=False):
+        def mv(t):
+            return None if t is None else t.to(device, non_blocking=non_blocking)
+
+        g = GraphBatch(mv(self.rowptr), mv(self.col), mv(self.graph_ptr), self._bnn, self._bne,
+                       None if self.symmetric else mv(self.rowptr_t),
+                       None if self.symmetric else mv(self.col_t), self.max_graph_nodes,
+                       self._e)
+        for k, v in self.ndata.items():
+            dict.__setitem__(g.ndata, k, v.to(device, non_blocking=non_blocking))
+        return g
+
+    @contextlib.contextmanager
+    def local_scope(self):
+        saved = dict(self.ndata)
+        try:
+            yield
+        finally:
+            dict.clear(self.ndata)
+            dict.update(self.ndata, saved)
+
+    def __repr__(self):
+        return (f"GraphBatch(num_graphs={self._B}, num_nodes={self._n}, num_edges={self._e}, "
+                f"device={self.device})")
+
+
+# ---------------------------------------------------------------------------
+# ingest (A1) and collate (A3)
+# ---------------------------------------------------------------------------
+def bidirected_simple(src, dst, n):
+    """dgl.to_bidirected(dgl.graph((src, dst))) edges: unique, (src, dst)-sorted."""
+    src = np.asarray(src, np.int64)
+    dst = np.asarray(dst, np.int64)
+    if len(src) == 0:
+        return src, dst
+    key = np.unique(np.concatenate([src * n + dst, dst * n + src]))
+    return key // n, key % n
+
+
+def pyg_num_nodes(edge_index):
+    ei = np.asarray(edge_index)
+    return int(ei.max()) + 1 if ei.size else 0
+
+
+def from_pyg(edge_index, x=None):
+    """util.load_dgl_fromPyG (util.py:277-325) for one molecule."""
+    ei = np.asarray(edge_index, np.int64).reshape(2, -1)
+    n = pyg_num_nodes(ei)
+    if x is not None and np.asarray(x).shape[0] != n:
+        raise GraphIngestError(f"x has {np.asarray(x).shape[0]} rows, graph has {n} nodes")
+    s, d = bidirected_simple(ei[0], ei[1], n)
+    g = GraphBatch.from_edges(s, d, n, symmetric_hint=True)
+    if x is not None:
+        g.ndata["x"] = torch.as_tensor(np.asarray(x))
+    return g
+
+
+def collate_pyg(molecules, device=None, skip_invalid=True):
+    """Batch a list of PyG-style ``(edge_index, x)`` molecules in one pass.
+
+    Equivalent to ``dgl.batch([load_dgl_fromPyG(m) for m in molecules])`` with
+    the reference's skip rule; vectorised over the batch (edges never cross
+    molecules, so one global unique == per-molecule to_bidirected).
+    Returns (GraphBatch, kept_indices).
+    """
+    srcs, dsts, xs, counts, kept = [], [], [], [], []
+    off = 0
+    for i, (ei, x) in enumerate(molecules):
+        ei = np.asarray(ei, np.int64).reshape(2, -1)
+        n = pyg_num_nodes(ei)
+        if np.asarray(x).shape[0] != n:
+            if skip_invalid:
+                continue
+            raise GraphIngestError(f"molecule {i}: x rows != inferred node count")
+        srcs.append(ei[0] + off)
+        dsts.append(ei[1] + off)
+        xs.append(np.asarray(x, np.float32))
+        counts.append(n)
+        kept.append(i)
+        off += n
+    counts = np.asarray(counts, np.int64)
+    src = np.concatenate(srcs) if srcs else np.zeros(0, np.int64)
+    dst = np.concatenate(dsts) if dsts else np.zeros(0, np.int64)
+    s, d = bidirected_simple(src, dst, max(off, 1))
+    gptr = np.zeros(len(counts) + 1, np.int64)
+    np.cumsum(counts, out=gptr[1:])
+    e_counts = np.diff(np.searchsorted(s, gptr)) if len(counts) else np.zeros(0, np.int64)
+    g = GraphBatch.from_edges(s, d, off, symmetric_hint=True, batch_num_nodes=counts,
+                              batch_num_edges=e_counts)
+    g.ndata["x"] = torch.from_numpy(np.concatenate(xs) if xs else np.zeros((0, 1), np.float32))
+    if device is not None:
+        g = g.to(device)
+    return g, kept
+
+
+def batch(graphs):
+    """dgl.batch: concatenate GraphBatches with node-id offsets (host side)."""
+    graphs = list(graphs)
+    rps, cols, rpts, colts, bnn, bne = [], [], [], [], [], []
+    noff = eoff = 0
+    sym = all(g.symmetric for g in graphs)
+    for g in graphs:
+        rp = g.rowptr.cpu().numpy().astype(np.int64)
+        rps.append(rp[:-1] + eoff)
+        cols.append(g.col.cpu().numpy().astype(np.int64)[: g.num_edges()] + noff)
+        if not sym:
+            rpt = g.rowptr_t.cpu().numpy().astype(np.int64)
+            rpts.append(rpt[:-1] + eoff)
+            colts.append(g.col_t.cpu().numpy().astype(np.int64)[: g.num_edges()] + noff)
+        bnn.append(g.batch_num_nodes_host())
+        bne.append(g.batch_num_edges().numpy())
+        noff += g.num_nodes()
+        eoff += g.num_edges()
+    rowptr = np.concatenate(rps + [np.array([eoff])]).astype(np.int32)
+    col = (np.concatenate(cols) if cols else np.zeros(0)).astype(np.int32)
+    bnn = np.concatenate(bnn) if bnn else np.zeros(0, np.int64)
+    bne = np.concatenate(bne) if bne else np.zeros(0, np.int64)
+    gptr = np.zeros(len(bnn) + 1, np.int64)
+    np.cumsum(bnn, out=gptr[1:])
+    rp_t = col_t = None
+    if not sym:
+        rp_t = torch.from_numpy(np.concatenate(rpts + [np.array([eoff])]).astype(np.int32))
+        col_t = torch.from_numpy(np.concatenate(colts).astype(np.int32))
+    out = GraphBatch(torch.from_numpy(rowptr), torch.from_numpy(col),
+                     torch.from_numpy(gptr.astype(np.int32)), bnn, bne, rp_t, col_t)
+    if graphs:
+        for k in graphs[0].ndata.keys():
+            dict.__setitem__(out.ndata, k, torch.cat([g.ndata[k].cpu() for g in graphs], 0))
+    dev = graphs[0].device if graphs else None
+    return out.to(dev) if dev is not None and dev.type != "cpu" else out
+
+
+# ---------------------------------------------------------------------------
+# on-device ego-net builder (A2 + the per-step dgl.batch of A3)
+# ---------------------------------------------------------------------------
+def _ptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+
+def _stream():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def egonet_batch(g: GraphBatch, k: int, x=None):
+    """All k-hop in-subgraphs of ``g``, batched: ego j <-> node j of ``g``.
+
+    Equivalent to ``dgl.batch(chain(*[[dgl.khop_in_subgraph(m, v, k)[0] for v
+    in m.nodes()] for m in molecules]))`` (exp_pretraining.py:269-272,
+    308-309).  Runs on ``g``'s HIP device through scgib_egonet_count/fill; one
+    3-integer device->host read (the ego batch's size) sizes the outputs.
+    The result carries ``ndata['_ID']`` (parent node id of every ego node)
+    and, if ``x`` is given, ``ndata['x'] = x[_ID]``.
+    """
+    if g.device.type != "cuda":
+        raise _lib.ScgibError("egonet_batch needs the graph on a HIP device (no CPU fallback)")
+    if not g.symmetric:
+        raise _lib.ScgibError("egonet_batch expects a symmetric (to_bidirected) graph")
+    dev = g.device
+    n = g.num_nodes()
+    i32 = torch.int32
+    ego_ptr = torch.empty(n + 1, dtype=i32, device=dev)
+    ego_eptr = torch.empty(n + 1, dtype=i32, device=dev)
+    ws = torch.empty(int(_lib.query("scgib_egonet_workspace_bytes", n)), dtype=torch.uint8,
+                     device=dev)
+    err = torch.zeros(1, dtype=i32, device=dev)
+    st = _stream()
+    mgn = max(g.max_graph_nodes, 1)
+    _lib.call("scgib_egonet_count", _ptr(g.rowptr), _ptr(g.col), _ptr(g.graph_ptr), g.batch_size,
+              n, k, mgn, _ptr(ego_ptr), _ptr(ego_eptr), _ptr(ws), _ptr(err), st)
+    tot = torch.stack([ego_ptr[n], ego_eptr[n], err[0]]).cpu().tolist()
+    n_s, e_s, e_code = int(tot[0]), int(tot[1]), int(tot[2])
+    if e_code:
+        raise _lib.ScgibError(f"scgib_egonet_count flagged error bits {e_code} "
+                              "(1: edge leaves its graph, 2: graph larger than max_graph_nodes)")
+    ego_nodes = torch.empty(n_s, dtype=i32, device=dev)
+    sub_rowptr = torch.empty(n_s + 1, dtype=i32, device=dev)
+    sub_col = torch.empty(max(e_s, 1), dtype=i32, device=dev)
+    _lib.call("scgib_egonet_fill", _ptr(g.rowptr), _ptr(g.col), _ptr(g.graph_ptr), g.batch_size, n,
+              k, mgn, _ptr(ego_ptr), _ptr(ego_eptr), _ptr(ego_nodes), _ptr(sub_rowptr),
+              _ptr(sub_col), _ptr(err), st)
+    ego = GraphBatch(sub_rowptr, sub_col, ego_ptr, None, None, n_edges=e_s,
+                     max_graph_nodes=mgn)
+    dict.__setitem__(ego.ndata, "_ID", ego_nodes)
+    if x is not None:
+        dict.__setitem__(ego.ndata, "x", x.index_select(0, ego_nodes))
+    return ego

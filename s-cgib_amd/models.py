@@ -1,0 +1,331 @@
+"""``models.py``-compatible S-CGIB pretraining model on the HIP path.
+
+Drop-in for the reference's classes on the north-star path, same
+constructor/forward signatures and the same ``state_dict`` keys:
+
+  MLP ................ models.py:38-49
+  GIN ................ models.py:52-72   (GINConv sum aggregation -> HIP kernel)
+  Mainmodel .......... models.py:546-782 (forward :662-700,
+                                          extract_features :702-750)
+  Mainmodel_continue . models.py:1010-1276 (the wrapper exp_pretraining.py
+                                            actually trains, :109-113)
+
+Differences from the reference, all deliberate:
+  * the GIN depth is explicit: ``args.gin_layers`` (default 5, the shipped
+    checkpoint's and the paper's depth; the shipped code builds 4 —
+    models.py:57-58 — use ``gin_layers=4`` for code-as-shipped parity);
+  * the compression + attention loops, the readouts and the dense N x N
+    reconstruction loss run as fused HIP kernels (ops.py);
+  * randomness: the reference draws the gate/feature noise from the CPU
+    generator per graph (models.py:599, 650); here it is drawn on the device
+    in one call, or passed explicitly with ``noise=(u_gate[N], u_feat[N,64])``
+    for parity with a recorded run;
+  * ``flatten_batch_subgraphs`` may be ``None``: the ego-nets are then built
+    on the device from ``batch_g`` (scgib_egonet_*), replacing the offline
+    khop_in_subgraph pass and the per-step dgl.batch of the reference;
+  * only the GIN encoder is implemented (the north-star path); GCN /
+    GraphSAGE / Transformer encoders raise.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from . import graph as G
+from . import ops
+
+
+class MLP(nn.Module):
+    """Linear-ReLU-Linear (models.py:38-49)."""
+
+    def __init__(self, num_features, num_classes, dims=16):
+        super().__init__()
+        self.mlp = nn.Sequential(nn.Linear(num_features, dims), nn.ReLU(),
+                                 nn.Linear(dims, num_classes))
+
+    def forward(self, x):
+        return self.mlp(x)
+
+
+class GINConv(nn.Module):
+    """DGL GINConv, sum aggregator, non-learnt eps buffer (models.py:63)."""
+
+    def __init__(self, apply_func=None, aggregator_type="sum", init_eps=0.0, learn_eps=False,
+                 activation=None):
+        super().__init__()
+        if aggregator_type != "sum" or learn_eps:
+            raise NotImplementedError("only the reference's GINConv(sum, learn_eps=False)")
+        self.apply_func = apply_func
+        self.activation = activation
+        self.register_buffer("eps", torch.FloatTensor([init_eps]))
+        self._one_plus_eps = 1.0 + float(init_eps)  # host mirror: no device sync per call
+
+    def _load_from_state_dict(self, state_dict, prefix, *args, **kwargs):
+        key = prefix + "eps"
+        if key in state_dict:
+            self._one_plus_eps = 1.0 + float(state_dict[key].reshape(-1)[0])
+        super()._load_from_state_dict(state_dict, prefix, *args, **kwargs)
+
+    def forward(self, graph, feat, edge_weight=None):
+        rst = ops.gin_aggregate(feat, graph, self._one_plus_eps)
+        if self.apply_func is not None:
+            rst = self.apply_func(rst)
+        if self.activation is not None:
+            rst = self.activation(rst)
+        return rst
+
+
+class GIN(nn.Module):
+    """GIN encoder: L x [GINConv(MLP) -> BatchNorm1d -> ReLU] (models.py:52-72)."""
+
+    def __init__(self, input_dim, hidden_dim=64, num_gin_layers=5):
+        super().__init__()
+        self.ginlayers = nn.ModuleList()
+        self.batch_norms = nn.ModuleList()
+        for layer in range(num_gin_layers):
+            d_in = input_dim if layer == 0 else hidden_dim
+            self.ginlayers.append(GINConv(MLP(d_in, hidden_dim, hidden_dim), learn_eps=False))
+            self.batch_norms.append(nn.BatchNorm1d(hidden_dim))
+
+    def forward(self, g, h):
+        for conv, bn in zip(self.ginlayers, self.batch_norms):
+            h = F.relu(bn(conv(g, h)))
+        return h
+
+
+class Set2Set(nn.Module):
+    """DGL Set2Set (LSTM(2d -> d), n_iters rounds) — held for state_dict parity
+    with the reference (models.py:565); not on the pretraining hot path."""
+
+    def __init__(self, input_dim, n_iters, n_layers):
+        super().__init__()
+        self.input_dim, self.output_dim = input_dim, 2 * input_dim
+        self.n_iters, self.n_layers = n_iters, n_layers
+        self.lstm = nn.LSTM(self.output_dim, self.input_dim, n_layers)
+
+    def forward(self, graph, feat):
+        bs = graph.batch_size
+        h = (feat.new_zeros((self.n_layers, bs, self.input_dim)),
+             feat.new_zeros((self.n_layers, bs, self.input_dim)))
+        q_star = feat.new_zeros(bs, self.output_dim)
+        seg = torch.repeat_interleave(torch.arange(bs, device=feat.device),
+                                      graph.batch_num_nodes().to(feat.device))
+        for _ in range(self.n_iters):
+            q, h = self.lstm(q_star.unsqueeze(0), h)
+            q = q.view(bs, self.input_dim)
+            e = (feat * q[seg]).sum(dim=-1, keepdim=True)
+            emax = torch.full((bs, 1), float("-inf"), device=feat.device).scatter_reduce(
+                0, seg.view(-1, 1), e, "amax")
+            a = torch.exp(e - emax[seg])
+            den = torch.zeros(bs, 1, device=feat.device).index_add(0, seg, a)
+            readout = ops.sum_nodes_graph(graph, feat * (a / den[seg]))
+            q_star = torch.cat([q, readout], dim=-1)
+        return q_star
+
+
+def _gin_layers(args):
+    return int(getattr(args, "gin_layers", 5))
+
+
+def semi_loss(z1, z2, chunk):
+    """batched_semi_loss, tau = 1 (models.py:606-629).  The per-row value does
+    not depend on the chunking, so the B x B similarities are formed at once."""
+    z1n, z2n = F.normalize(z1), F.normalize(z2)
+    refl = torch.exp(z1n @ z1n.t())
+    betw = torch.exp(z1n @ z2n.t())
+    return (-torch.log(betw.diagonal() / (refl.sum(1) + betw.sum(1) - refl.diagonal()))).mean()
+
+
+class _SCGIBCore(nn.Module):
+    """Shared hot-path logic of Mainmodel / Mainmodel_continue."""
+
+    def _prepare_ego(self, batch_g, flatten_batch_subgraphs, batch_x, x_subs):
+        if flatten_batch_subgraphs is None:
+            ego = G.egonet_batch(batch_g, self.k_transition)
+            if x_subs is None:
+                x_subs = batch_x.index_select(0, ego.ndata["_ID"])
+            return ego, x_subs
+        return flatten_batch_subgraphs, x_subs
+
+    def _noise(self, n, device, noise):
+        if noise is not None:
+            u_gate, u_feat = noise
+            return u_gate.reshape(-1), u_feat
+        return (torch.rand(n, device=device, dtype=torch.float32),
+                torch.rand(n, self.hidden_dim, device=device, dtype=torch.float32))
+
+    def _extract(self, enc_owner, batch_g, batch_x, ego, x_subs, noise):
+        """extract_features of ``enc_owner`` (models.py:702-750); returns the
+        reference's 4-tuple plus z1 = sum_nodes(noisy) (computed in-kernel)."""
+        graph_features = enc_owner.Encoder1(batch_g, batch_x)
+        subgraphs_features = enc_owner.Encoder2(ego, x_subs)
+        enc_owner.graph_features = graph_features
+        enc_owner.subgraphs_features = subgraphs_features
+        sub_readout = ops.segment_sum(subgraphs_features, ego.graph_ptr, ego.batch_size)
+        t = enc_owner.compressor[0](graph_features)
+        u_gate, u_feat = self._noise(graph_features.shape[0], graph_features.device, noise)
+        im, z1, z2, kl = ops.interaction(graph_features, t, sub_readout, u_gate, u_feat,
+                                         enc_owner.compressor[1], enc_owner.compressor[3],
+                                         enc_owner.attn_layer, batch_g, enc_owner.training)
+        noisy = im[:, : self.hidden_dim]
+        return im, kl, noisy, z2, z1
+
+    def _losses(self, batch_g, im, kl, z1, z2, mlp, batch_size):
+        im = mlp(im)
+        kl_loss = torch.mean(kl)
+        con = semi_loss(z1, z2, batch_size)
+        if self.recons_type == "adj":
+            rec = ops.recon_adj(im, batch_g)
+        else:
+            raise NotImplementedError("recons_type='logM' is a next-tier path (SURVEY.md §8(f) #3)")
+        return kl_loss, con, rec
+
+
+class Mainmodel(_SCGIBCore):
+    def __init__(self, args, in_dim, hidden_dim, num_layers, num_heads, k_transition, encoder):
+        super().__init__()
+        self.tau = 1.0
+        self.recons_type = args.recons_type
+        self.useAtt = args.useAtt
+        self.readout = args.readout_f
+        if self.readout != "sum" or not self.useAtt:
+            raise NotImplementedError("the hot path implements readout_f='sum', useAtt=1")
+        self.hidden_dim = hidden_dim
+        self.k_transition = k_transition
+        self.fc1 = nn.Linear(hidden_dim, 1)
+        self.in_dim = args.d_transfer
+        self.transfer_d = nn.Linear(in_dim, self.in_dim, bias=False)
+        self.embedding_h = nn.Linear(self.in_dim, hidden_dim, bias=False)
+        self.attn_layer = nn.Linear(self.hidden_dim * 2, 1)
+        self.reduce_d = nn.Linear(2 * self.hidden_dim, self.hidden_dim)
+        self.device = getattr(args, "device", None)
+        self.s2s = Set2Set(hidden_dim, 2, 1)
+        self.reconstructX = nn.Sequential(nn.Linear(self.hidden_dim, self.in_dim))
+        self.MLP = nn.Sequential(nn.Linear(2 * hidden_dim, hidden_dim), nn.ReLU(),
+                                 nn.Linear(hidden_dim, hidden_dim))
+        if encoder != "GIN":
+            raise NotImplementedError(f"encoder {encoder!r}: only GIN is on the hot path")
+        self.Encoder1 = GIN(self.in_dim, hidden_dim, _gin_layers(args))
+        self.Encoder2 = GIN(self.in_dim, hidden_dim, _gin_layers(args))
+        self.compressor = nn.Sequential(nn.Linear(hidden_dim, hidden_dim),
+                                        nn.BatchNorm1d(hidden_dim), nn.ReLU(),
+                                        nn.Linear(hidden_dim, 1))
+
+    def extract_features(self, nodes_list, batch_g, batch_x, flatten_batch_subgraphs, x_subs,
+                         device=None, noise=None):
+        ego, x_subs = self._prepare_ego(batch_g, flatten_batch_subgraphs, batch_x, x_subs)
+        im, kl, noisy, z2, z1 = self._extract(self, batch_g, batch_x, ego, x_subs, noise)
+        self._last_z1 = z1
+        return im, kl, noisy, z2
+
+    def forward(self, batch_g, batch_x, flatten_batch_subgraphs, batch_logMs, x_subs,
+                current_epoch=None, edge_index=None, k_transition=None, device=None,
+                batch_size=16, noise=None):
+        self.batch_size = batch_size
+        if flatten_batch_subgraphs is None:
+            flatten_batch_subgraphs, x_subs = self._prepare_ego(batch_g, None, batch_x, x_subs)
+        batch_x = self.transfer_d(batch_x)
+        x_subs = self.transfer_d(x_subs)
+        im, kl, noisy, z2 = self.extract_features(None, batch_g, batch_x,
+                                                  flatten_batch_subgraphs, x_subs, device, noise)
+        kl_loss, con, rec = self._losses(batch_g, im, kl, self._last_z1, z2, self.MLP,
+                                         batch_size)
+        return None, kl_loss, con, rec
+
+
+class Mainmodel_continue(_SCGIBCore):
+    """The pretraining wrapper (models.py:1010-1276): its own transfer_d and
+    MLP around the wrapped model's extract_features (models.py:1167)."""
+
+    def __init__(self, args, in_dim, hidden_dim, num_layers, num_heads, k_transition,
+                 num_classes, cp_filename, encoder):
+        super().__init__()
+        self.tau = 1.0
+        self.readout = args.readout_f
+        self.s2s = Set2Set(hidden_dim, 2, 1)
+        self.s2s_rev = Set2Set(in_dim, 2, 1)
+        self.in_dim = args.d_transfer
+        self.transfer_d = nn.Linear(in_dim, self.in_dim, bias=False)
+        self.recons_type = args.recons_type
+        self.batch_size = getattr(args, "batch_size", 16)
+        self.useAtt = args.useAtt
+        self.embedding_h = nn.Linear(self.in_dim, hidden_dim, bias=False)
+        self.hidden_dim = hidden_dim
+        self.k_transition = k_transition
+        self.reduce_d = nn.Linear(2 * hidden_dim, hidden_dim)
+        self.attn_layer = nn.Linear(2 * hidden_dim, 1)
+        self.num_nodes = -1
+        self.device = getattr(args, "device", None)
+        self.r_transfer_d = nn.Sequential(nn.Linear(2 * hidden_dim, hidden_dim), nn.ReLU(),
+                                          nn.Linear(hidden_dim, in_dim * 2))
+        out_dim = 1 if getattr(args, "task", "graph_classification") == "graph_regression" \
+            else num_classes
+        self.predict = nn.Sequential(nn.Linear(2 * hidden_dim, hidden_dim), nn.ReLU(),
+                                     nn.Linear(hidden_dim, out_dim))
+        self.MLP = nn.Sequential(nn.Linear(2 * hidden_dim, hidden_dim), nn.ReLU(),
+                                 nn.Linear(hidden_dim, hidden_dim))
+        if encoder != "GIN":
+            raise NotImplementedError(f"encoder {encoder!r}: only GIN is on the hot path")
+        self.Encoder1 = GIN(self.in_dim, hidden_dim, _gin_layers(args))
+        self.Encoder2 = GIN(self.in_dim, hidden_dim, _gin_layers(args))
+        self.model = load_checkpoint(cp_filename, args)
+        for p in self.model.parameters():
+            p.requires_grad = True
+        self.compressor = nn.Sequential(nn.Linear(hidden_dim, hidden_dim),
+                                        nn.BatchNorm1d(hidden_dim), nn.ReLU(),
+                                        nn.Linear(hidden_dim, 1))
+        self.reconstructX = nn.Sequential(nn.Linear(hidden_dim, hidden_dim), nn.ReLU(),
+                                          nn.Linear(hidden_dim, in_dim))
+
+    def extract_features(self, nodes_list, batch_g, batch_x, flatten_batch_subgraphs, x_subs,
+                         device=None, noise=None):
+        ego, x_subs = self._prepare_ego(batch_g, flatten_batch_subgraphs, batch_x, x_subs)
+        im, kl, noisy, z2, z1 = self._extract(self, batch_g, batch_x, ego, x_subs, noise)
+        self._last_z1 = z1
+        return im, kl, noisy, z2
+
+    def forward(self, batch_g, batch_x, flatten_batch_subgraphs, batch_logMs, x_subs,
+                current_epoch=None, edge_index=None, k_transition=None, device=None,
+                batch_size=16, noise=None):
+        self.batch_size = batch_size
+        if flatten_batch_subgraphs is None:
+            flatten_batch_subgraphs, x_subs = self._prepare_ego(batch_g, None, batch_x, x_subs)
+        batch_x = self.transfer_d(batch_x)
+        x_subs = self.transfer_d(x_subs)
+        im, kl, noisy, z2 = self.model.extract_features(None, batch_g, batch_x,
+                                                        flatten_batch_subgraphs, x_subs, device,
+                                                        noise)
+        kl_loss, con, rec = self._losses(batch_g, im, kl, self.model._last_z1, z2, self.MLP,
+                                         batch_size)
+        return None, kl_loss, con, rec
+
+
+# ---------------------------------------------------------------------------
+# checkpoints: state_dict based (the reference pickles whole modules,
+# exp_pretraining.py:107; such files are not loaded here)
+# ---------------------------------------------------------------------------
+def save_checkpoint(model, path, args=None, in_dim=None):
+    cfg = {}
+    if args is not None:
+        cfg = {k: getattr(args, k) for k in ("recons_type", "useAtt", "readout_f", "d_transfer",
+                                             "gin_layers") if hasattr(args, k)}
+    cfg.update(kind=type(model).__name__, in_dim=in_dim, hidden_dim=model.hidden_dim,
+               k_transition=model.k_transition)
+    torch.save({"config": cfg, "state_dict": model.state_dict()}, path)
+
+
+def load_checkpoint(cp, args):
+    """A Mainmodel from an in-memory module or a save_checkpoint() file."""
+    if isinstance(cp, nn.Module):
+        return cp
+    blob = torch.load(cp, map_location="cpu", weights_only=True)
+    cfg = blob["config"]
+    ns = type("Args", (), {})()
+    for k in ("recons_type", "useAtt", "readout_f", "d_transfer", "gin_layers"):
+        setattr(ns, k, cfg.get(k, getattr(args, k, None)))
+    if cfg.get("kind") != "Mainmodel":
+        raise NotImplementedError("nested Mainmodel_continue checkpoints: load the inner model")
+    m = Mainmodel(ns, cfg["in_dim"], cfg["hidden_dim"], 4, 4, cfg["k_transition"], "GIN")
+    m.load_state_dict(blob["state_dict"])
+    return m

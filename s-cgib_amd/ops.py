@@ -1,0 +1,221 @@
+"""Autograd ops over the C-ABI (include/scgib.h).  HIP only — no fallback.
+
+Each op checks that its tensors are fp32/int32, contiguous and on a HIP
+device, launches on torch's current stream (so torch's caching allocator and
+stream semantics apply) and raises ``ScgibError`` on any non-zero status.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+
+from . import _lib
+from ._lib import HIDDEN, PGRAD_STRIDE, STATS_STRIDE
+
+_NULL = None
+
+
+def _p(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else _NULL
+
+
+def _stream():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def _f32(t, name):
+    if not t.is_cuda:
+        raise _lib.ScgibError(f"{name}: tensor is on {t.device}; the S-CGIB ops run on the HIP "
+                              "device only (no CPU fallback)")
+    if t.dtype != torch.float32:
+        t = t.float()
+    return t.contiguous()
+
+
+# ---------------------------------------------------------------------------
+# A5: GIN aggregation
+# ---------------------------------------------------------------------------
+def _aggregate(h, rowptr, col, ope):
+    n, d = h.shape
+    out = torch.empty_like(h)
+    _lib.call("scgib_gin_aggregate", _p(h), _p(rowptr), _p(col), n, d, float(ope), _p(out),
+              _stream())
+    return out
+
+
+class _GinAggregate(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, h, graph, ope):
+        h = _f32(h, "gin_aggregate")
+        ctx.graph, ctx.ope = graph, ope
+        return _aggregate(h, graph.rowptr, graph.col, ope)
+
+    @staticmethod
+    def backward(ctx, g):
+        g = _f32(g, "gin_aggregate.backward")
+        gr = ctx.graph
+        # d/dh of sum_{u->v} h_u is the aggregation over the transposed CSR
+        return _aggregate(g, gr.rowptr_t, gr.col_t, ctx.ope), None, None
+
+
+def gin_aggregate(h, graph, one_plus_eps=1.0):
+    """out[v] = (1 + eps) h[v] + sum_{u -> v} h[u]  (DGL GINConv, models.py:69)."""
+    return _GinAggregate.apply(h, graph, float(one_plus_eps))
+
+
+# ---------------------------------------------------------------------------
+# A6: segment sums (dgl.sum_nodes)
+# ---------------------------------------------------------------------------
+class _SegmentSum(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, ptr, nseg):
+        x = _f32(x, "segment_sum")
+        out = torch.empty(nseg, x.shape[1], dtype=torch.float32, device=x.device)
+        _lib.call("scgib_segment_sum", _p(x), _p(ptr), nseg, x.shape[1], _p(out), _stream())
+        ctx.ptr, ctx.nrows = ptr, x.shape[0]
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        g = _f32(g, "segment_sum.backward")
+        out = torch.empty(ctx.nrows, g.shape[1], dtype=torch.float32, device=g.device)
+        _lib.call("scgib_segment_broadcast", _p(g), _p(ctx.ptr), g.shape[0], g.shape[1],
+                  _p(out), _stream())
+        return out, None, None
+
+
+def segment_sum(x, ptr, nseg):
+    return _SegmentSum.apply(x, ptr, int(nseg))
+
+
+def sum_nodes_graph(graph, x):
+    """dgl.sum_nodes(graph, feat) on a GraphBatch."""
+    return segment_sum(x, graph.graph_ptr, graph.batch_size)
+
+
+# ---------------------------------------------------------------------------
+# A6-A8: fused core <-> subgraph interaction
+# ---------------------------------------------------------------------------
+class _Interaction(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, f, t, s, u_gate, u_feat, gamma, beta, w2, b2, w_att, b_att, graph, bn,
+                training):
+        f = _f32(f, "interaction")
+        t, s = _f32(t, "interaction"), _f32(s, "interaction")
+        u_gate, u_feat = _f32(u_gate, "interaction"), _f32(u_feat, "interaction")
+        n, d = f.shape
+        if d != HIDDEN:
+            raise _lib.ScgibError(f"interaction kernels are built for hidden={HIDDEN}, got {d}")
+        B = graph.batch_size
+        counts = graph.batch_num_nodes_host()
+        if training and B and counts.min() < 2:
+            # nn.BatchNorm1d raises on a 1-row batch in train mode (models.py:642)
+            raise ValueError("Expected more than 1 value per channel when training "
+                             "(a graph with a single node in the per-graph compressor BN)")
+        dev = f.device
+        im = torch.empty(n, 2 * HIDDEN, dtype=torch.float32, device=dev)
+        z1 = torch.empty(B, HIDDEN, dtype=torch.float32, device=dev)
+        z2 = torch.empty(B, HIDDEN, dtype=torch.float32, device=dev)
+        lam = torch.empty(n, dtype=torch.float32, device=dev)
+        logit = torch.empty(n, dtype=torch.float32, device=dev)
+        stats = torch.empty(max(B, 1), STATS_STRIDE, dtype=torch.float32, device=dev)
+        n_last = int(counts[-1]) if B else 0
+        kl = torch.empty(2 * n_last, HIDDEN, dtype=torch.float32, device=dev)
+        gamma, beta = _f32(gamma, "bn.weight"), _f32(beta, "bn.bias")
+        w2, b2 = _f32(w2, "w2"), _f32(b2, "b2")
+        w_att, b_att = _f32(w_att, "w_att"), _f32(b_att, "b_att")
+        rm, rv = bn.running_mean, bn.running_var
+        st = _stream()
+        _lib.call("scgib_interaction_fwd", _p(f), _p(t), _p(s), _p(u_gate), _p(u_feat),
+                  _p(graph.graph_ptr), B, n, _p(gamma), _p(beta), _p(rm), _p(rv), float(bn.eps),
+                  int(training), _p(w2), _p(b2), _p(w_att), _p(b_att), _p(im), _p(z1), _p(z2),
+                  _p(lam), _p(logit), _p(stats), _p(kl), st)
+        if training and bn.track_running_stats:
+            nbt = bn.num_batches_tracked
+            _lib.call("scgib_bn_running_update", _p(stats), _p(graph.graph_ptr), B,
+                      float(bn.momentum), _p(rm), _p(rv), _p(nbt), st)
+        ctx.save_for_backward(f, t, s, u_feat, gamma, beta, w2, w_att, z1, lam, logit, stats)
+        ctx.graph, ctx.training = graph, training
+        ctx.bn_eps = float(bn.eps)
+        ctx.rm, ctx.rv = (None, None) if training else (rm.clone(), rv.clone())
+        return im, z1, z2, kl
+
+    @staticmethod
+    def backward(ctx, g_im, g_z1, g_z2, g_kl):
+        f, t, s, u_feat, gamma, beta, w2, w_att, z1, lam, logit, stats = ctx.saved_tensors
+        n = f.shape[0]
+        B = ctx.graph.batch_size
+        dev = f.device
+        zeros = lambda *shape: torch.zeros(*shape, dtype=torch.float32, device=dev)  # noqa: E731
+        g_im = zeros(n, 2 * HIDDEN) if g_im is None else _f32(g_im, "g_im")
+        g_z1 = zeros(B, HIDDEN) if g_z1 is None else _f32(g_z1, "g_z1")
+        g_z2 = zeros(B, HIDDEN) if g_z2 is None else _f32(g_z2, "g_z2")
+        g_kl = None if g_kl is None else _f32(g_kl, "g_kl")
+        df = torch.empty_like(f)
+        dt = torch.empty_like(t)
+        ds = torch.empty_like(s)
+        pgrad = torch.empty(max(B, 1), PGRAD_STRIDE, dtype=torch.float32, device=dev)
+        _lib.call("scgib_interaction_bwd", _p(g_im), _p(g_z1), _p(g_z2), _p(g_kl), _p(f), _p(t),
+                  _p(s), _p(u_feat), _p(ctx.graph.graph_ptr), B, n, _p(gamma), _p(beta),
+                  _p(ctx.rm), _p(ctx.rv), ctx.bn_eps, int(ctx.training), _p(w2), _p(w_att),
+                  _p(z1), _p(lam), _p(logit), _p(stats), _p(df), _p(dt), _p(ds), _p(pgrad),
+                  _stream())
+        pg = pgrad[:B].sum(0)
+        dw2 = pg[0:64].view(1, 64)
+        db2 = pg[64:65]
+        dgamma = pg[65:129]
+        dbeta = pg[129:193]
+        dwatt = pg[193:321].view(1, 128)
+        dbatt = pg[321:322]
+        return (df, dt, ds, None, None, dgamma, dbeta, dw2, db2, dwatt, dbatt, None, None, None)
+
+
+def interaction(f, t, s, u_gate, u_feat, bn, lin2, attn, graph, training):
+    """Fused compression + attention (models.py:595-660, 714-749).
+
+    ``bn`` is the compressor BatchNorm1d (its running stats are updated in
+    place in train mode, once per graph), ``lin2`` the compressor's
+    Linear(64, 1), ``attn`` the attn_layer Linear(128, 1).
+    Returns (interaction_map [N,128], z1 = sum_nodes(noisy) [B,64],
+    z2 = sum_nodes(f) [B,64], kl_tensor [2 n_last, 64]).
+    """
+    return _Interaction.apply(f, t, s, u_gate, u_feat, bn.weight, bn.bias, lin2.weight,
+                              lin2.bias, attn.weight, attn.bias, graph, bn, bool(training))
+
+
+# ---------------------------------------------------------------------------
+# A12: adjacency reconstruction loss (Gram form)
+# ---------------------------------------------------------------------------
+class _ReconAdj(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, im, graph):
+        im = _f32(im, "recon_adj")
+        n, d = im.shape
+        if d != HIDDEN:
+            raise _lib.ScgibError(f"recon kernels are built for width {HIDDEN}, got {d}")
+        dev = im.device
+        partials = torch.empty(int(_lib.query("scgib_recon_partials_floats", n)),
+                               dtype=torch.float32, device=dev)
+        gram = torch.empty(HIDDEN * HIDDEN, dtype=torch.float32, device=dev)
+        loss = torch.empty((), dtype=torch.float32, device=dev)
+        _lib.call("scgib_recon_fwd", _p(im), _p(graph.rowptr), _p(graph.col), n,
+                  graph.num_edges(), _p(partials), _p(gram), _p(loss), _stream())
+        ctx.save_for_backward(im, gram)
+        ctx.graph = graph
+        return loss
+
+    @staticmethod
+    def backward(ctx, g_loss):
+        im, gram = ctx.saved_tensors
+        gr = ctx.graph
+        g_loss = _f32(g_loss.reshape(1), "g_loss")
+        out = torch.empty_like(im)
+        _lib.call("scgib_recon_bwd", _p(im), _p(gram), _p(gr.rowptr), _p(gr.col), _p(gr.rowptr_t),
+                  _p(gr.col_t), im.shape[0], _p(g_loss), _p(out), _stream())
+        return out, None
+
+
+def recon_adj(im, graph):
+    """sum((IM IM^T - A)^2) / N without the N x N matrix (models.py:762-768)."""
+    return _ReconAdj.apply(im, graph)

@@ -1,0 +1,145 @@
+"""CPU-only tests: C-ABI exports, ego-net oracle vs goldens, host ingest/collate.
+
+No compute call touches the GPU here."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import ROOT, load_golden
+from oracle import dgl_semantics as D
+from oracle import egonet
+
+
+# ---------------------------------------------------------------------------
+def header_symbols():
+    src = open(os.path.join(ROOT, "include", "scgib.h")).read()
+    return sorted(set(re.findall(r"^\s*(?:int|int64_t|const char \*)\s*(scgib_\w+)\(", src,
+                                 re.M)))
+
+
+def test_library_exports_every_header_symbol(pkg):
+    lib_mod = pkg._lib
+    lib = ctypes.CDLL(lib_mod.LIB_PATH)  # loads without a GPU: nothing is launched
+    syms = header_symbols()
+    assert len(syms) >= 14
+    for s in syms:
+        assert hasattr(lib, s), s
+    assert set(syms) == set(lib_mod.SIGNATURES), "ctypes signature table out of sync"
+    loaded = lib_mod.load()
+    assert loaded.scgib_abi_version() == 1
+    assert loaded.scgib_strerror(-1).decode().startswith("invalid")
+
+
+def test_argument_errors_do_not_launch(pkg):
+    lib = pkg._lib.load()
+    # negative / invalid sizes and null pointers are rejected before any launch
+    assert lib.scgib_gin_aggregate(None, None, None, -1, 64, 1.0, None, None) == -1
+    assert lib.scgib_gin_aggregate(None, None, None, 10, 63, 1.0, None, None) == -1
+    assert lib.scgib_gin_aggregate(None, None, None, 0, 64, 1.0, None, None) == 0
+    assert lib.scgib_segment_sum(None, None, 5, 64, None, None) == -1
+    assert lib.scgib_egonet_count(None, None, None, 1, 10, 1, 1000, None, None, None, None,
+                                  None) == -1
+    assert lib.scgib_recon_fwd(None, None, None, 0, 0, None, None, None, None) == -1
+    assert lib.scgib_egonet_workspace_bytes(1000) >= 8
+    assert lib.scgib_recon_partials_floats(9000) > 36 * 4096
+
+
+# ---------------------------------------------------------------------------
+def test_egonet_oracle_matches_reference_goldens():
+    d = load_golden("ingest_egonet")
+    checked = 0
+    for i in range(int(d["num_mols"])):
+        if not d[f"m{i}_kept"]:
+            continue
+        g = D.Graph(d[f"m{i}_src"], d[f"m{i}_dst"], int(d[f"m{i}_n"]))
+        rp, col = D.csr_from_graph(g)
+        for k in (1, 2, 3):
+            s, e, nodes, es, ed = egonet.egonets(rp, col, k)
+            np.testing.assert_array_equal(s, d[f"m{i}_k{k}_sizes"])
+            np.testing.assert_array_equal(nodes, d[f"m{i}_k{k}_nodes"])
+            np.testing.assert_array_equal(e, d[f"m{i}_k{k}_ecount"])
+            np.testing.assert_array_equal(es, d[f"m{i}_k{k}_esrc"])
+            np.testing.assert_array_equal(ed, d[f"m{i}_k{k}_edst"])
+            checked += 1
+    assert checked >= 30
+
+
+def test_egonet_oracle_k1_size_identity(pkg):
+    # k = 1 on a simple graph: |ball(v)| = 1 + deg(v)  =>  N_s = N + E
+    mols = pkg.synth.molecules(64, "qm9", seed=5)
+    g, _ = pkg.graph.collate_pyg(mols)
+    s, e, *_ = egonet.egonets(g.rowptr.numpy(), g.col.numpy(), 1)
+    assert s.sum() == g.num_nodes() + g.num_edges()
+
+
+# ---------------------------------------------------------------------------
+def test_ingest_matches_reference_load_dgl_fromPyG(pkg):
+    """A1: graph + to_bidirected + the skip rule, against util.load_dgl_fromPyG."""
+    d = load_golden("ingest_egonet")
+    for i in range(int(d["num_mols"])):
+        ei, x = d[f"m{i}_edge_index"], d[f"m{i}_x"]
+        if not d[f"m{i}_kept"]:
+            with pytest.raises(pkg.graph.GraphIngestError):
+                pkg.graph.from_pyg(ei, x)
+            continue
+        g = pkg.graph.from_pyg(ei, x)
+        assert g.num_nodes() == int(d[f"m{i}_n"])
+        s, t = g.edges()
+        np.testing.assert_array_equal(s.numpy(), d[f"m{i}_src"])
+        np.testing.assert_array_equal(t.numpy(), d[f"m{i}_dst"])
+
+
+def test_collate_equals_batch_of_singles(pkg):
+    mols = pkg.synth.molecules(40, "pcqm4mv2", seed=3)
+    bad = (np.array([[0, 1], [1, 0]]), np.zeros((3, 9), np.float32))  # trailing isolated atom
+    mols.insert(7, bad)
+    g, kept = pkg.graph.collate_pyg(mols)
+    assert 7 not in kept and len(kept) == 40
+    singles = [pkg.graph.from_pyg(*mols[i]) for i in kept]
+    gb = pkg.graph.batch(singles)
+    np.testing.assert_array_equal(g.rowptr.numpy(), gb.rowptr.numpy())
+    np.testing.assert_array_equal(g.col.numpy(), gb.col.numpy())
+    np.testing.assert_array_equal(g.graph_ptr.numpy(), gb.graph_ptr.numpy())
+    np.testing.assert_array_equal(g.batch_num_nodes().numpy(), gb.batch_num_nodes().numpy())
+    np.testing.assert_array_equal(g.batch_num_edges().numpy(), gb.batch_num_edges().numpy())
+    assert torch.equal(g.ndata["x"], gb.ndata["x"])
+    # DGL edge order of the batch: (src, dst) sorted
+    s, t = g.edges()
+    key = s.numpy() * g.num_nodes() + t.numpy()
+    assert (np.diff(key) > 0).all()
+
+
+def test_adj_to_dense_and_symmetry(pkg):
+    g, _ = pkg.graph.collate_pyg(pkg.synth.molecules(5, "qm9", seed=1))
+    a = g.adj().to_dense()
+    assert torch.equal(a, a.t())
+    assert int(a.sum()) == g.num_edges()
+
+
+def test_ndata_rowcount_checked(pkg):
+    g, _ = pkg.graph.collate_pyg(pkg.synth.molecules(3, "qm9", seed=1))
+    with pytest.raises(pkg.graph.GraphIngestError):
+        g.ndata["h"] = torch.zeros(g.num_nodes() + 1, 4)
+
+
+def test_product_ops_refuse_cpu_tensors(pkg):
+    g, _ = pkg.graph.collate_pyg(pkg.synth.molecules(3, "qm9", seed=1))
+    with pytest.raises(pkg._lib.ScgibError):
+        pkg.ops.gin_aggregate(torch.zeros(g.num_nodes(), 64), g)
+    with pytest.raises(pkg._lib.ScgibError):
+        pkg.graph.egonet_batch(g, 1)
+
+
+@pytest.mark.parametrize("workload", ["qm9", "molpcba", "pcqm4mv2", "mutagenicity"])
+def test_synthetic_shapes(pkg, workload):
+    mols = pkg.synth.molecules(256, workload, seed=0)
+    g, kept = pkg.graph.collate_pyg(mols)
+    assert len(kept) == 256  # the generator never emits molecules the reference would skip
+    mu = pkg.synth.WORKLOADS[workload][0]
+    assert abs(g.num_nodes() / 256 - mu) < 0.15 * mu
+    deg = np.diff(g.rowptr.numpy())
+    assert deg.min() >= 1

@@ -1,0 +1,53 @@
+"""The oracle (CPU restatement) against the goldens produced by the reference's
+own models.py (oracle/gen_golden.py).  Pins the restatement before it is used
+as the checker of the HIP path."""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from conftest import MODEL_GOLDENS, check_grads, load_golden
+from oracle import scgib_ref as R
+
+
+def golden_inputs(g):
+    counts = torch.tensor(g["batch_num_nodes"])
+    batch = {"src": torch.tensor(g["src"]), "dst": torch.tensor(g["dst"]), "counts": counts}
+    ego = {"src": torch.tensor(g["ego_src"]), "dst": torch.tensor(g["ego_dst"]),
+           "counts": torch.tensor(g["ego_batch_num_nodes"])}
+    x_raw = torch.tensor(g["x_raw"]).float()
+    x = F.normalize(x_raw)
+    x_subs = F.normalize(x_raw[torch.tensor(g["ego_nodes_global"])])
+    return batch, ego, x, x_subs
+
+
+def golden_params(g):
+    raw = {k[6:]: v for k, v in g.items() if k.startswith("param_")}
+    return R.make_params(R.strip_continue(raw)), raw
+
+
+def rel(a, b):
+    a, b = np.asarray(a, np.float64), np.asarray(b, np.float64)
+    return np.abs(a - b).max() / max(np.abs(b).max(), 1e-30)
+
+
+@pytest.mark.parametrize("name", MODEL_GOLDENS)
+def test_oracle_matches_reference_golden(name):
+    g = load_golden(name)
+    batch, ego, x, x_subs = golden_inputs(g)
+    params, raw = golden_params(g)
+    buffers = {k: v.clone() for k, v in params.items() if "running" in k or "num_batches" in k}
+    out = R.pretrain_forward(params, batch, ego, x, x_subs, torch.tensor(g["u_gate"]),
+                             torch.tensor(g["u_feat"]), int(g["chunk"]), buffers)
+    for key in ("loss_kl", "loss_contrastive", "loss_recon", "loss_total"):
+        assert rel(out[key].item(), g[key]) < 1e-5, key
+    for key in ("graph_features", "subgraph_features", "noisy", "kl_tensor",
+                "interaction_map", "graph_readout", "im_mlp"):
+        assert rel(out[key].detach(), g["act_" + key]) < 1e-5, key
+    out["loss_total"].backward()
+    check_grads({k[5:]: v for k, v in g.items() if k.startswith("grad_")},
+                lambda n: params[R.strip_continue({n: 0}).popitem()[0]].grad)
+    for k, v in g.items():
+        if k.startswith("after_"):
+            assert np.allclose(buffers[R.strip_continue({k[6:]: 0}).popitem()[0]].numpy(), v,
+                               rtol=1e-5, atol=1e-6), k

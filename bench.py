@@ -54,7 +54,12 @@ def make_model(F_in, k, gin_layers, dev):
 
 class AggTimer:
     """HIP-event timing of every GIN aggregation launch (fwd and bwd) on the
-    stream it is launched on (torch's current stream)."""
+    stream it is launched on (torch's current stream).
+
+    A ~170 us spin kernel is queued ahead of each bracketed launch so the
+    GPU is still busy while the host submits [start event, kernel, end
+    event]; the events then bracket the kernel itself rather than the host's
+    launch latency (the step is launch-bound at these sizes)."""
 
     def __init__(self):
         self.records = []  # (start_event, end_event, bytes)
@@ -67,6 +72,7 @@ class AggTimer:
 
         def timed(h, rowptr, col, ope):
             s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            torch.cuda._sleep(400_000)
             s.record()
             out = self._orig(h, rowptr, col, ope)
             e.record()
@@ -183,6 +189,10 @@ def main():
     ap.add_argument("--no-superbatch", action="store_true")
     a = ap.parse_args()
 
+    # hipBLASLt's heuristics pick 2-workgroup kernels for the tall-skinny
+    # [N,64]^T x [N,64] weight-gradient GEMMs (~90 us each, profiles/r01_baseline);
+    # rocBLAS is ~2-3x faster on them.  (Process-wide torch setting.)
+    torch.backends.cuda.preferred_blas_library("cublas")
     rank, world, local = pkg.dist.init_from_env()
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)

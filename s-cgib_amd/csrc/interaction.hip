@@ -8,50 +8,74 @@
 // each, plus a host->device copy of the gate noise per graph); here the B
 // graphs are B independent wavefronts of one launch.
 //
-// Mapping: lane c of the wavefront owns hidden channel c (hidden = 64 =
-// wavefront width), so every per-node row access is one 256-B coalesced
-// load, every per-channel statistic (means, stds, BN stats, readouts) lives
-// in a register, and every per-node dot product over channels (compressor
-// output p, attention logit) is one butterfly wave_sum.  Graph rows are
-// re-read from L1/L2 between passes (a molecule is a few KB).
+// Lane mapping inside the wavefront: lane = 16 q + c4.  Row group q (0..3)
+// takes rows r0+q, r0+q+4, ...; lane c4 (0..15) holds hidden channels
+// 4c4..4c4+3 as a float4.  So every wave instruction touches four node rows
+// with 16-B-per-lane coalesced accesses (4 x 256 B), a dot product over the
+// 64 channels of a row is a 16-lane butterfly (red16), and a per-channel
+// statistic over the graph's rows is a per-lane float4 accumulator folded
+// across the four row groups at the end (red_q).  Every shuffle is executed
+// by all 64 lanes (rows past the end are masked, not skipped), so the
+// butterflies stay well defined.
 //
 // The attention logit keeps the z-bar half (w_att[0:64] . z1_i + b_att),
 // which is constant per graph and cancels in the softmax:
-// computing it costs one wave_sum per graph and keeps the parameter
-// gradients identical in exact arithmetic to the reference's.
+// computing it costs one red16 per graph and keeps the parameter gradients
+// identical in exact arithmetic to the reference's.
 //
-// This is latency-bound VALU/shuffle work (a few hundred FLOP per row), not
-// GEMM-shaped: no MFMA.
+// Latency-bound VALU/shuffle work (a few hundred FLOP per row): no MFMA.
 #include "common.h"
 
 namespace scgib {
 
-constexpr float kKlEps = 1e-7f;             // models.py:632
-constexpr float kGateLo = 0.0001f;          // models.py:598: bias = 0.0 + 0.0001
-// (bias - (1 - bias)) and (1 - bias) are evaluated in double by Python and
-// rounded to fp32 by torch's scalar multiply/add, as here.
+constexpr float kKlEps = 1e-7f;  // models.py:632
+// (bias - (1 - bias)) and (1 - bias) with bias = 0.0001 (models.py:598) are
+// evaluated in double by Python and rounded to fp32 by torch, as here.
 constexpr float kGateScale = static_cast<float>(0.0001 - (1.0 - 0.0001));
 constexpr float kGateShift = static_cast<float>(1.0 - 0.0001);
 
 // stats slab layout per graph (SCGIB_STATS_STRIDE floats)
 enum : int {
-    kStMeanT = 0,     // compressor-BN batch mean of t            [64]
-    kStSsqT = 64,     // centred sum of squares of t              [64]
-    kStMu = 128,      // std_mean(f).mean                        [64]
-    kStSigma = 192,   // std_mean(f).std (unbiased)              [64]
-    kStSoftMax = 256, // softmax running max M
-    kStSoftSum = 257, // softmax denominator S (relative to M)
-    kStConst = 258,   // z-bar logit constant
+    kStMeanT = 0,      // compressor-BN batch mean of t             [64]
+    kStSsqT = 64,      // centred sum of squares of t               [64]
+    kStMu = 128,       // std_mean(f).mean                         [64]
+    kStSigma = 192,    // std_mean(f).std (unbiased)               [64]
+    kStSoftMax = 256,  // softmax max M
+    kStSoftSum = 257,  // softmax denominator S (relative to M)
+    kStConst = 258,    // z-bar logit constant
 };
 // pgrad slab layout per graph (SCGIB_PGRAD_STRIDE floats)
 enum : int { kPgW2 = 0, kPgB2 = 64, kPgGamma = 65, kPgBeta = 129, kPgWatt = 193, kPgBatt = 321 };
 
-struct GraphCtx {
-    int64_t r0, r1;
-    int n;
-    float mt, rstd;  // BN stats used for normalisation (batch or running)
-    float mu, sig;   // std_mean of f
-};
+__device__ __forceinline__ float red16(float v) {
+    v += __shfl_xor(v, 1, kWave);
+    v += __shfl_xor(v, 2, kWave);
+    v += __shfl_xor(v, 4, kWave);
+    v += __shfl_xor(v, 8, kWave);
+    return v;
+}
+
+__device__ __forceinline__ float red_q(float v) {
+    v += __shfl_xor(v, 16, kWave);
+    v += __shfl_xor(v, 32, kWave);
+    return v;
+}
+
+__device__ __forceinline__ float4 red_q4(float4 v) {
+    return make_float4(red_q(v.x), red_q(v.y), red_q(v.z), red_q(v.w));
+}
+
+__device__ __forceinline__ float4 ld4(const float *p) { return *reinterpret_cast<const float4 *>(p); }
+__device__ __forceinline__ void st4(float *p, float4 v) { *reinterpret_cast<float4 *>(p) = v; }
+__device__ __forceinline__ float4 f4(float a) { return make_float4(a, a, a, a); }
+__device__ __forceinline__ float4 operator+(float4 a, float4 b) { return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w); }
+__device__ __forceinline__ float4 operator-(float4 a, float4 b) { return make_float4(a.x - b.x, a.y - b.y, a.z - b.z, a.w - b.w); }
+__device__ __forceinline__ float4 operator*(float4 a, float4 b) { return make_float4(a.x * b.x, a.y * b.y, a.z * b.z, a.w * b.w); }
+__device__ __forceinline__ float4 operator*(float s, float4 a) { return make_float4(s * a.x, s * a.y, s * a.z, s * a.w); }
+__device__ __forceinline__ float dot4(float4 a, float4 b) { return a.x * b.x + a.y * b.y + a.z * b.z + a.w * b.w; }
+__device__ __forceinline__ float4 relu4(float4 a) { return make_float4(fmaxf(a.x, 0.f), fmaxf(a.y, 0.f), fmaxf(a.z, 0.f), fmaxf(a.w, 0.f)); }
+__device__ __forceinline__ float4 sqrt4(float4 a) { return make_float4(sqrtf(a.x), sqrtf(a.y), sqrtf(a.z), sqrtf(a.w)); }
+__device__ __forceinline__ float4 rcp_sqrt4(float4 a) { return make_float4(1.f / sqrtf(a.x), 1.f / sqrtf(a.y), 1.f / sqrtf(a.z), 1.f / sqrtf(a.w)); }
 
 __device__ __forceinline__ float gate_lambda(float u, float p) {
     const float e = kGateScale * u + kGateShift;
@@ -59,7 +83,16 @@ __device__ __forceinline__ float gate_lambda(float u, float p) {
     return 1.f / (1.f + expf(-(g + p)));
 }
 
-__global__ __launch_bounds__(256) void interaction_fwd_k(
+struct Lanes {
+    int q, c4, ch;  // row group, channel quad, first channel
+};
+
+__device__ __forceinline__ Lanes lanes() {
+    const int l = threadIdx.x & 63;
+    return {l >> 4, l & 15, (l & 15) * 4};
+}
+
+__global__ __launch_bounds__(64) void interaction_fwd_k(
     const float *__restrict__ f, const float *__restrict__ t, const float *__restrict__ s,
     const float *__restrict__ u_gate, const float *__restrict__ u_feat,
     const int32_t *__restrict__ gptr, int64_t B, const float *__restrict__ gamma,
@@ -69,119 +102,189 @@ __global__ __launch_bounds__(256) void interaction_fwd_k(
     const float *__restrict__ battp, float *__restrict__ im, float *__restrict__ z1,
     float *__restrict__ z2, float *__restrict__ lam, float *__restrict__ logit,
     float *__restrict__ stats, float *__restrict__ kl) {
-    const int c = threadIdx.x & 63;
-    const int64_t gi = static_cast<int64_t>(blockIdx.x) * 4 + (threadIdx.x >> 6);
-    if (gi >= B) return;
+    const Lanes L = lanes();
+    const int64_t gi = blockIdx.x;
     const int64_t r0 = gptr[gi], r1 = gptr[gi + 1];
     const int n = static_cast<int>(r1 - r0);
     if (n <= 0) {
-        z1[gi * 64 + c] = 0.f;
-        z2[gi * 64 + c] = 0.f;
+        if (L.q == 0) {
+            st4(z1 + gi * 64 + L.ch, f4(0.f));
+            st4(z2 + gi * 64 + L.ch, f4(0.f));
+        }
         return;
     }
-    // pass 1: readout of f (= graph_features_readout) and means
-    float sf = 0.f, st = 0.f;
-    for (int64_t r = r0; r < r1; ++r) {
-        sf += f[r * 64 + c];
-        st += t[r * 64 + c];
+    // ---- pass 1: sums (readout of f, means) and shifted second moments ----
+    const float4 f0 = ld4(f + r0 * 64 + L.ch), t0 = ld4(t + r0 * 64 + L.ch);
+    float4 zf = f4(0.f), zt = f4(0.f), sf = f4(0.f), st = f4(0.f), qf = f4(0.f), qt = f4(0.f);
+    for (int64_t base = r0; base < r1; base += 4) {
+        const int64_t r = base + L.q;
+        if (r < r1) {
+            const float4 fv = ld4(f + r * 64 + L.ch), tv = ld4(t + r * 64 + L.ch);
+            zf = zf + fv;
+            zt = zt + tv;
+            const float4 df = fv - f0, dt = tv - t0;
+            sf = sf + df;
+            st = st + dt;
+            qf = qf + df * df;
+            qt = qt + dt * dt;
+        }
     }
-    const float mu = sf / n, mt = st / n;
-    // pass 2: centred second moments (two-pass, as torch's std/var)
-    float qf = 0.f, qt = 0.f;
-    for (int64_t r = r0; r < r1; ++r) {
-        const float df = f[r * 64 + c] - mu, dt = t[r * 64 + c] - mt;
-        qf += df * df;
-        qt += dt * dt;
-    }
-    const float sig = sqrtf(qf / static_cast<float>(n - 1));  // n == 1 -> NaN, as torch
-    const float m_use = training ? mt : rmean[c];
-    const float v_use = training ? qt / n : rvar[c];
-    const float rstd = 1.f / sqrtf(v_use + bn_eps);
-    const float gm = gamma[c], bt = beta[c], w2c = w2[c], b2 = *b2p;
-    z2[gi * 64 + c] = sf;
+    zf = red_q4(zf); zt = red_q4(zt); sf = red_q4(sf); st = red_q4(st);
+    qf = red_q4(qf); qt = red_q4(qt);
+    const float inv_n = 1.f / n;
+    const float4 mu = inv_n * zf, mt = inv_n * zt;
+    // centred sums of squares (shifted formula); n == 1 -> 0 / 0 -> NaN std, as torch
+    const float4 cf = qf - inv_n * (sf * sf), ct = qt - inv_n * (st * st);
+    const float4 sig = sqrt4(make_float4(fmaxf(cf.x, 0.f), fmaxf(cf.y, 0.f), fmaxf(cf.z, 0.f),
+                                         fmaxf(cf.w, 0.f)) * f4(1.f / static_cast<float>(n - 1)));
+    const float4 ctp = make_float4(fmaxf(ct.x, 0.f), fmaxf(ct.y, 0.f), fmaxf(ct.z, 0.f), fmaxf(ct.w, 0.f));
+    const float4 m_use = training ? mt : ld4(rmean + L.ch);
+    const float4 v_use = training ? inv_n * ctp : ld4(rvar + L.ch);
+    const float4 rstd = rcp_sqrt4(v_use + f4(bn_eps));
+    const float4 gm = ld4(gamma + L.ch), bt = ld4(beta + L.ch), w2c = ld4(w2 + L.ch);
+    const float b2 = *b2p;
     float *sl = stats + gi * SCGIB_STATS_STRIDE;
-    sl[kStMeanT + c] = mt;
-    sl[kStSsqT + c] = qt;
-    sl[kStMu + c] = mu;
-    sl[kStSigma + c] = sig;
-    // pass 3: compressor logit p, gate lambda, noisy features
-    float zacc = 0.f;
-    for (int64_t r = r0; r < r1; ++r) {
-        const float y = gm * (t[r * 64 + c] - m_use) * rstd + bt;
-        const float p = wave_sum(w2c * fmaxf(y, 0.f)) + b2;
-        const float lm = gate_lambda(u_gate[r], p);
-        const float fv = f[r * 64 + c];
-        const float ln = 1.f - lm;
-        const float nz = (lm * fv + ln * mu) + u_feat[r * 64 + c] * (ln * sig);
-        im[r * 128 + c] = nz;
-        zacc += nz;
-        if (c == 0) lam[r] = lm;
+    if (L.q == 0) {
+        st4(z2 + gi * 64 + L.ch, zf);
+        st4(sl + kStMeanT + L.ch, mt);
+        st4(sl + kStSsqT + L.ch, ctp);
+        st4(sl + kStMu + L.ch, mu);
+        st4(sl + kStSigma + L.ch, sig);
     }
-    z1[gi * 64 + c] = zacc;
-    // KL of the last graph only, duplicated (models.py:657-659)
+    // ---- pass 2: compressor logit p, gate lambda, noisy features ----
+    float4 zacc = f4(0.f);
+    for (int64_t base = r0; base < r1; base += 4) {
+        const int64_t r = base + L.q;
+        const bool ok = r < r1;
+        const int64_t rr = ok ? r : r0;
+        const float4 y = gm * ((ld4(t + rr * 64 + L.ch) - m_use) * rstd) + bt;
+        const float p = red16(dot4(w2c, relu4(y))) + b2;
+        if (ok) {
+            const float lm = gate_lambda(u_gate[r], p), ln = 1.f - lm;
+            const float4 fv = ld4(f + r * 64 + L.ch);
+            const float4 nz = (lm * fv + ln * mu) + ld4(u_feat + r * 64 + L.ch) * (ln * sig);
+            st4(im + r * 128 + L.ch, nz);
+            zacc = zacc + nz;
+            if (L.c4 == 0) lam[r] = lm;
+        }
+    }
+    zacc = red_q4(zacc);
+    if (L.q == 0) st4(z1 + gi * 64 + L.ch, zacc);
+    // ---- KL of the last graph only, duplicated (models.py:657-659) ----
     if (gi == B - 1) {
-        const float den = (sig + kKlEps) * (sig + kKlEps);
-        float q = 0.f;
-        for (int64_t r = r0; r < r1; ++r) {
-            const float y = gm * (t[r * 64 + c] - m_use) * rstd + bt;
-            const float lm = gate_lambda(u_gate[r], wave_sum(w2c * fmaxf(y, 0.f)) + b2);
-            const float d = (lm * f[r * 64 + c] + (1.f - lm) * mu) - mu;
-            q += (d / (sig + kKlEps)) * (d / (sig + kKlEps));
+        const float4 se = sig + f4(kKlEps);
+        const float4 den = se * se;
+        float4 qacc = f4(0.f);
+        for (int64_t base = r0; base < r1; base += 4) {
+            const int64_t r = base + L.q;
+            const bool ok = r < r1;
+            const int64_t rr = ok ? r : r0;
+            const float4 y = gm * ((ld4(t + rr * 64 + L.ch) - m_use) * rstd) + bt;
+            const float p = red16(dot4(w2c, relu4(y))) + b2;
+            if (ok) {
+                const float lm = gate_lambda(u_gate[r], p);
+                const float4 d = (lm * ld4(f + r * 64 + L.ch) + (1.f - lm) * mu) - mu;
+                const float4 z = make_float4(d.x / se.x, d.y / se.y, d.z / se.z, d.w / se.w);
+                qacc = qacc + z * z;
+            }
         }
-        for (int64_t r = r0; r < r1; ++r) {
-            const float y = gm * (t[r * 64 + c] - m_use) * rstd + bt;
-            const float lm = gate_lambda(u_gate[r], wave_sum(w2c * fmaxf(y, 0.f)) + b2);
-            const float ns = (1.f - lm) * sig;
-            const float v = 0.5f * ((ns * ns) / den) + q;
-            kl[(r - r0) * 64 + c] = v;
-            kl[(r - r0 + n) * 64 + c] = v;
+        qacc = red_q4(qacc);
+        for (int64_t base = r0; base < r1; base += 4) {
+            const int64_t r = base + L.q;
+            const bool ok = r < r1;
+            const int64_t rr = ok ? r : r0;
+            const float4 y = gm * ((ld4(t + rr * 64 + L.ch) - m_use) * rstd) + bt;
+            const float p = red16(dot4(w2c, relu4(y))) + b2;
+            if (ok) {
+                const float lm = gate_lambda(u_gate[r], p);
+                const float4 ns = (1.f - lm) * sig;
+                const float4 nn = ns * ns;
+                const float4 v = f4(0.5f) * make_float4(nn.x / den.x, nn.y / den.y, nn.z / den.z,
+                                                        nn.w / den.w) + qacc;
+                st4(kl + (r - r0) * 64 + L.ch, v);
+                st4(kl + (r - r0 + n) * 64 + L.ch, v);
+            }
         }
     }
-    // attention: logit_v = w_lo . z1 + w_hi . s_v + b ; softmax over the graph
-    const float cst = wave_sum(watt[c] * zacc) + *battp;
-    const float whi = watt[64 + c];
-    float M = -INFINITY, S = 0.f;
-    for (int64_t r = r0; r < r1; ++r) {
-        const float lg = wave_sum(whi * s[r * 64 + c]) + cst;
-        if (c == 0) logit[r] = lg;
-        const float Mn = fmaxf(M, lg);
-        S = S * expf(M - Mn) + expf(lg - Mn);
+    // ---- attention: logit_v = w_lo . z1 + w_hi . s_v + b; softmax per graph ----
+    const float cst = red16(dot4(ld4(watt + L.ch), zacc)) + *battp;
+    const float4 whi = ld4(watt + 64 + L.ch);
+    float M = -INFINITY, S = 0.f;  // per row group, merged below
+    for (int64_t base = r0; base < r1; base += 4) {
+        const int64_t r = base + L.q;
+        const bool ok = r < r1;
+        const int64_t rr = ok ? r : r0;
+        const float lg = red16(dot4(whi, ld4(s + rr * 64 + L.ch))) + cst;
+        if (ok) {
+            if (L.c4 == 0) logit[r] = lg;
+            const float Mn = fmaxf(M, lg);
+            S = S * expf(M - Mn) + expf(lg - Mn);
+            M = Mn;
+        }
+    }
+#pragma unroll
+    for (int off = 16; off <= 32; off <<= 1) {  // merge the four row groups
+        const float Mo = __shfl_xor(M, off, kWave), So = __shfl_xor(S, off, kWave);
+        const float Mn = fmaxf(M, Mo);
+        S = (S == 0.f ? 0.f : S * expf(M - Mn)) + (So == 0.f ? 0.f : So * expf(Mo - Mn));
         M = Mn;
     }
     const float invS = 1.f / S;
-    for (int64_t r = r0; r < r1; ++r) {
-        const float sv = s[r * 64 + c];
-        const float lg = wave_sum(whi * sv) + cst;
-        im[r * 128 + 64 + c] = (expf(lg - M) * invS) * sv;
+    for (int64_t base = r0; base < r1; base += 4) {
+        const int64_t r = base + L.q;
+        const bool ok = r < r1;
+        const int64_t rr = ok ? r : r0;
+        const float4 sv = ld4(s + rr * 64 + L.ch);
+        const float lg = red16(dot4(whi, sv)) + cst;
+        if (ok) st4(im + r * 128 + 64 + L.ch, (expf(lg - M) * invS) * sv);
     }
-    if (c == 0) {
+    if (threadIdx.x == 0) {
         sl[kStSoftMax] = M;
         sl[kStSoftSum] = S;
         sl[kStConst] = cst;
     }
 }
 
-__global__ __launch_bounds__(64) void bn_running_update_k(const float *__restrict__ stats,
-                                                          const int32_t *__restrict__ gptr,
-                                                          int64_t B, float momentum,
-                                                          float *__restrict__ rm,
-                                                          float *__restrict__ rv,
-                                                          int64_t *__restrict__ nbt) {
-    const int c = threadIdx.x;
-    float m = rm[c], v = rv[c];
-    for (int64_t i = 0; i < B; ++i) {
+// Closed form of the B sequential momentum updates of the per-graph
+// compressor BatchNorm (one nn.BatchNorm1d call per graph, models.py:642):
+//   r_B = (1-m)^B r_0 + sum_i m (1-m)^(B-1-i) x_i
+// evaluated in fp64 by 16 partitions x 64 channels, partials folded in a
+// fixed order (deterministic; closer to the exact recurrence than an fp32
+// sequential loop).
+__global__ __launch_bounds__(1024) void bn_running_update_k(const float *__restrict__ stats,
+                                                            const int32_t *__restrict__ gptr,
+                                                            int64_t B, float momentum,
+                                                            float *__restrict__ rm,
+                                                            float *__restrict__ rv,
+                                                            int64_t *__restrict__ nbt) {
+    const int c = threadIdx.x & 63, part = threadIdx.x >> 6;  // 16 partitions
+    const double m = momentum, lk = log1p(-m);
+    double am = 0.0, av = 0.0;
+    for (int64_t i = part; i < B; i += 16) {
         const int n = gptr[i + 1] - gptr[i];
         const float *sl = stats + i * SCGIB_STATS_STRIDE;
-        const float uv = sl[kStSsqT + c] / static_cast<float>(n - 1);
-        m = momentum * sl[kStMeanT + c] + (1.f - momentum) * m;
-        v = momentum * uv + (1.f - momentum) * v;
+        const double w = m * exp(static_cast<double>(B - 1 - i) * lk);
+        am += w * sl[kStMeanT + c];
+        av += w * (static_cast<double>(sl[kStSsqT + c]) / (n - 1));
     }
-    rm[c] = m;
-    rv[c] = v;
-    if (c == 0 && nbt) *nbt += B;
+    __shared__ double pm[16][64], pv[16][64];
+    pm[part][c] = am;
+    pv[part][c] = av;
+    __syncthreads();
+    if (part == 0) {
+        double sm = 0.0, sv = 0.0;
+        for (int p = 0; p < 16; ++p) {
+            sm += pm[p][c];
+            sv += pv[p][c];
+        }
+        const double decay = exp(static_cast<double>(B) * lk);
+        rm[c] = static_cast<float>(decay * rm[c] + sm);
+        rv[c] = static_cast<float>(decay * rv[c] + sv);
+        if (c == 0 && nbt) *nbt += B;
+    }
 }
 
-__global__ __launch_bounds__(256) void interaction_bwd_k(
+__global__ __launch_bounds__(64) void interaction_bwd_k(
     const float *__restrict__ g_im, const float *__restrict__ g_z1,
     const float *__restrict__ g_z2, const float *__restrict__ g_kl,
     const float *__restrict__ f, const float *__restrict__ t, const float *__restrict__ s,
@@ -192,94 +295,131 @@ __global__ __launch_bounds__(256) void interaction_bwd_k(
     const float *__restrict__ z1, const float *__restrict__ lam,
     const float *__restrict__ logit, const float *__restrict__ stats, float *__restrict__ df,
     float *__restrict__ dt, float *__restrict__ ds, float *__restrict__ pgrad) {
-    const int c = threadIdx.x & 63;
-    const int64_t gi = static_cast<int64_t>(blockIdx.x) * 4 + (threadIdx.x >> 6);
-    if (gi >= B) return;
+    const Lanes L = lanes();
+    const int64_t gi = blockIdx.x;
     const int64_t r0 = gptr[gi], r1 = gptr[gi + 1];
     const int n = static_cast<int>(r1 - r0);
     float *pg = pgrad + gi * SCGIB_PGRAD_STRIDE;
     if (n <= 0) {
-        for (int j = c; j < SCGIB_PGRAD_STRIDE; j += 64) pg[j] = 0.f;
+        for (int j = threadIdx.x; j < SCGIB_PGRAD_STRIDE; j += 64) pg[j] = 0.f;
         return;
     }
     const float *sl = stats + gi * SCGIB_STATS_STRIDE;
-    const float mt = sl[kStMeanT + c], qt = sl[kStSsqT + c];
-    const float mu = sl[kStMu + c], sig = sl[kStSigma + c];
+    const float inv_n = 1.f / n;
+    const float4 mt = ld4(sl + kStMeanT + L.ch), ssq = ld4(sl + kStSsqT + L.ch);
+    const float4 mu = ld4(sl + kStMu + L.ch), sig = ld4(sl + kStSigma + L.ch);
     const float M = sl[kStSoftMax], invS = 1.f / sl[kStSoftSum];
-    const float m_use = training ? mt : rmean[c];
-    const float v_use = training ? qt / n : rvar[c];
-    const float rstd = 1.f / sqrtf(v_use + bn_eps);
-    const float gm = gamma[c], bt = beta[c], w2c = w2[c];
-    const float wlo = watt[c], whi = watt[64 + c], zb = z1[gi * 64 + c];
+    const float4 m_use = training ? mt : ld4(rmean + L.ch);
+    const float4 v_use = training ? inv_n * ssq : ld4(rvar + L.ch);
+    const float4 rstd = rcp_sqrt4(v_use + f4(bn_eps));
+    const float4 gm = ld4(gamma + L.ch), bt = ld4(beta + L.ch), w2c = ld4(w2 + L.ch);
+    const float4 wlo = ld4(watt + L.ch), whi = ld4(watt + 64 + L.ch), zb = ld4(z1 + gi * 64 + L.ch);
 
     // ---- attention backward: a_v = alpha_v s_v, alpha = softmax(logit) ----
-    float SA = 0.f;
-    for (int64_t r = r0; r < r1; ++r) {
-        const float al = expf(logit[r] - M) * invS;
-        SA += al * wave_sum(g_im[r * 128 + 64 + c] * s[r * 64 + c]);
+    float sa = 0.f;  // sum alpha * dalpha of this row group (uniform over its lanes)
+    for (int64_t base = r0; base < r1; base += 4) {
+        const int64_t r = base + L.q;
+        const bool ok = r < r1;
+        const int64_t rr = ok ? r : r0;
+        const float da = red16(dot4(ld4(g_im + rr * 128 + 64 + L.ch), ld4(s + rr * 64 + L.ch)));
+        if (ok) sa += expf(logit[r] - M) * invS * da;
     }
-    float dwhi = 0.f, dc = 0.f;
-    for (int64_t r = r0; r < r1; ++r) {
-        const float al = expf(logit[r] - M) * invS;
-        const float ga = g_im[r * 128 + 64 + c], sv = s[r * 64 + c];
-        const float dl = al * (wave_sum(ga * sv) - SA);
-        ds[r * 64 + c] = al * ga + dl * whi;
-        dwhi += dl * sv;
-        dc += dl;
+    const float SA = red_q(sa);
+    float4 dwhi = f4(0.f);
+    float dcq = 0.f;
+    for (int64_t base = r0; base < r1; base += 4) {
+        const int64_t r = base + L.q;
+        const bool ok = r < r1;
+        const int64_t rr = ok ? r : r0;
+        const float4 ga = ld4(g_im + rr * 128 + 64 + L.ch), sv = ld4(s + rr * 64 + L.ch);
+        const float da = red16(dot4(ga, sv));
+        if (ok) {
+            const float al = expf(logit[r] - M) * invS;
+            const float dl = al * (da - SA);
+            st4(ds + r * 64 + L.ch, al * ga + dl * whi);
+            dwhi = dwhi + dl * sv;
+            dcq += dl;
+        }
     }
-    const float gb = g_z1[gi * 64 + c] + dc * wlo;  // d z-bar -> every node's noisy
-    const float gz2 = g_z2[gi * 64 + c];            // d readout(f) -> every node's f
+    dwhi = red_q4(dwhi);
+    const float dc = red_q(dcq);
+    const float4 gb = ld4(g_z1 + gi * 64 + L.ch) + dc * wlo;  // d z-bar -> every node's noisy
+    const float4 gz2 = ld4(g_z2 + gi * 64 + L.ch);            // d readout(f) -> every node's f
 
     // ---- KL (last graph) ----
     const bool has_kl = (g_kl != nullptr) && (gi == B - 1);
-    float Gc = 0.f;
-    if (has_kl)
-        for (int r = 0; r < n; ++r) Gc += g_kl[r * 64 + c] + g_kl[(r + n) * 64 + c];
-    const float inv2 = 1.f / ((sig + kKlEps) * (sig + kKlEps));
+    float4 Gc = f4(0.f);
+    if (has_kl) {
+        for (int base = 0; base < n; base += 4) {
+            const int rl = base + L.q;
+            if (rl < n) Gc = Gc + ld4(g_kl + rl * 64 + L.ch) + ld4(g_kl + (rl + n) * 64 + L.ch);
+        }
+        Gc = red_q4(Gc);
+    }
+    const float4 se = sig + f4(kKlEps);
+    const float4 inv2 = make_float4(1.f / (se.x * se.x), 1.f / (se.y * se.y), 1.f / (se.z * se.z),
+                                    1.f / (se.w * se.w));
 
     // ---- compression backward ----
-    float dw2 = 0.f, db2 = 0.f, dg = 0.f, dbe = 0.f;
-    for (int64_t r = r0; r < r1; ++r) {
-        const float lm = lam[r];
-        const float fv = f[r * 64 + c];
-        const float gn = g_im[r * 128 + c] + gb;
-        float part = gn * (fv - mu - u_feat[r * 64 + c] * sig);
-        float dfv = gn * lm + gz2;
+    float4 dw2 = f4(0.f), dg = f4(0.f), dbe = f4(0.f);
+    float db2q = 0.f;
+    for (int64_t base = r0; base < r1; base += 4) {
+        const int64_t r = base + L.q;
+        const bool ok = r < r1;
+        const int64_t rr = ok ? r : r0;
+        const float lm = lam[rr];
+        const float4 fv = ld4(f + rr * 64 + L.ch);
+        const float4 gn = ld4(g_im + rr * 128 + L.ch) + gb;
+        const float4 fm = fv - mu;
+        float part = dot4(gn, fm - ld4(u_feat + rr * 64 + L.ch) * sig);
+        float4 dfv = lm * gn + gz2;
         if (has_kl) {
-            const int rl = static_cast<int>(r - r0);
-            const float gk = g_kl[rl * 64 + c] + g_kl[(rl + n) * 64 + c];
-            const float fm = fv - mu;
-            part += gk * (-(1.f - lm) * sig * sig * inv2) + Gc * 2.f * lm * fm * fm * inv2;
-            dfv += Gc * 2.f * lm * lm * fm * inv2;
+            const int rl = static_cast<int>(rr - r0);
+            const float4 gk = ld4(g_kl + rl * 64 + L.ch) + ld4(g_kl + (rl + n) * 64 + L.ch);
+            part += dot4(gk, (-(1.f - lm)) * (sig * sig * inv2)) + dot4(Gc, (2.f * lm) * (fm * fm * inv2));
+            dfv = dfv + (2.f * lm * lm) * (Gc * fm * inv2);
         }
-        const float dp = wave_sum(part) * lm * (1.f - lm);
-        const float xh = (t[r * 64 + c] - m_use) * rstd;
-        const float y = gm * xh + bt;
-        dw2 += dp * fmaxf(y, 0.f);
-        db2 += dp;
-        const float dy = y > 0.f ? dp * w2c : 0.f;
-        dg += dy * xh;
-        dbe += dy;
-        df[r * 64 + c] = dfv;
-        dt[r * 64 + c] = dy;
-    }
-    // BatchNorm backward (batch statistics of this graph, or running stats)
-    const float inv_n = 1.f / n;
-    for (int64_t r = r0; r < r1; ++r) {
-        const float dy = dt[r * 64 + c];
-        if (training) {
-            const float xh = (t[r * 64 + c] - m_use) * rstd;
-            dt[r * 64 + c] = gm * rstd * (dy - dbe * inv_n - xh * dg * inv_n);
-        } else {
-            dt[r * 64 + c] = gm * rstd * dy;
+        const float dp = red16(part) * lm * (1.f - lm);
+        if (ok) {
+            const float4 xh = (ld4(t + r * 64 + L.ch) - m_use) * rstd;
+            const float4 y = gm * xh + bt;
+            dw2 = dw2 + dp * relu4(y);
+            db2q += dp;
+            const float4 dy = make_float4(y.x > 0.f ? dp * w2c.x : 0.f, y.y > 0.f ? dp * w2c.y : 0.f,
+                                          y.z > 0.f ? dp * w2c.z : 0.f, y.w > 0.f ? dp * w2c.w : 0.f);
+            dg = dg + dy * xh;
+            dbe = dbe + dy;
+            st4(df + r * 64 + L.ch, dfv);
+            st4(dt + r * 64 + L.ch, dy);
         }
     }
-    pg[kPgW2 + c] = dw2;
-    pg[kPgGamma + c] = dg;
-    pg[kPgBeta + c] = dbe;
-    pg[kPgWatt + c] = dc * zb;
-    pg[kPgWatt + 64 + c] = dwhi;
-    if (c == 0) {
+    dw2 = red_q4(dw2);
+    dg = red_q4(dg);
+    dbe = red_q4(dbe);
+    const float db2 = red_q(db2q);
+    // BatchNorm backward (this graph's batch statistics, or running stats);
+    // each lane re-reads only the dt entries it wrote itself
+    const float4 gr = gm * rstd;
+    for (int64_t base = r0; base < r1; base += 4) {
+        const int64_t r = base + L.q;
+        if (r < r1) {
+            const float4 dy = ld4(dt + r * 64 + L.ch);
+            if (training) {
+                const float4 xh = (ld4(t + r * 64 + L.ch) - m_use) * rstd;
+                st4(dt + r * 64 + L.ch, gr * (dy - inv_n * dbe - xh * (inv_n * dg)));
+            } else {
+                st4(dt + r * 64 + L.ch, gr * dy);
+            }
+        }
+    }
+    if (L.q == 0) {
+        st4(pg + kPgW2 + L.ch, dw2);
+        st4(pg + kPgGamma + L.ch, dg);
+        st4(pg + kPgBeta + L.ch, dbe);
+        st4(pg + kPgWatt + L.ch, dc * zb);
+        st4(pg + kPgWatt + 64 + L.ch, dwhi);
+    }
+    if (threadIdx.x == 0) {
         pg[kPgB2] = db2;
         pg[kPgBatt] = dc;
         pg[SCGIB_PGRAD_STRIDE - 2] = 0.f;
@@ -300,14 +440,14 @@ extern "C" int scgib_interaction_fwd(
     float *stats, float *kl_tensor, scgib_stream_t stream) {
     if (n_graphs < 0 || n_nodes < 0) return SCGIB_EINVAL;
     if (n_graphs == 0) return SCGIB_OK;
+    if (n_graphs > 0x7fffffff) return SCGIB_EUNSUPPORTED;
     if (!graph_ptr || !bn_gamma || !bn_beta || !w2 || !b2 || !w_att || !b_att || !z1 ||
         !z2 || !stats || !kl_tensor)
         return SCGIB_EINVAL;
     if (n_nodes > 0 && (!f || !t || !s || !u_gate || !u_feat || !im || !lam || !logit))
         return SCGIB_EINVAL;
     if (!training && (!bn_running_mean || !bn_running_var)) return SCGIB_EINVAL;
-    const int64_t grid = (n_graphs + 3) / 4;
-    interaction_fwd_k<<<dim3((unsigned)grid), 256, 0, as_stream(stream)>>>(
+    interaction_fwd_k<<<dim3((unsigned)n_graphs), 64, 0, as_stream(stream)>>>(
         f, t, s, u_gate, u_feat, graph_ptr, n_graphs, bn_gamma, bn_beta, bn_running_mean,
         bn_running_var, bn_eps, training, w2, b2, w_att, b_att, im, z1, z2, lam, logit, stats,
         kl_tensor);
@@ -321,9 +461,9 @@ extern "C" int scgib_bn_running_update(const float *stats, const int32_t *graph_
     if (n_graphs < 0) return SCGIB_EINVAL;
     if (n_graphs == 0) return SCGIB_OK;
     if (!stats || !graph_ptr || !running_mean || !running_var) return SCGIB_EINVAL;
-    bn_running_update_k<<<1, 64, 0, as_stream(stream)>>>(stats, graph_ptr, n_graphs, momentum,
-                                                         running_mean, running_var,
-                                                         num_batches_tracked);
+    bn_running_update_k<<<1, 1024, 0, as_stream(stream)>>>(stats, graph_ptr, n_graphs, momentum,
+                                                           running_mean, running_var,
+                                                           num_batches_tracked);
     return launch_status();
 }
 
@@ -337,6 +477,7 @@ extern "C" int scgib_interaction_bwd(
     scgib_stream_t stream) {
     if (n_graphs < 0 || n_nodes < 0) return SCGIB_EINVAL;
     if (n_graphs == 0) return SCGIB_OK;
+    if (n_graphs > 0x7fffffff) return SCGIB_EUNSUPPORTED;
     if (!graph_ptr || !g_z1 || !g_z2 || !bn_gamma || !bn_beta || !w2 || !w_att || !z1 ||
         !stats || !pgrad)
         return SCGIB_EINVAL;
@@ -344,8 +485,7 @@ extern "C" int scgib_interaction_bwd(
                         !ds))
         return SCGIB_EINVAL;
     if (!training && (!bn_running_mean || !bn_running_var)) return SCGIB_EINVAL;
-    const int64_t grid = (n_graphs + 3) / 4;
-    interaction_bwd_k<<<dim3((unsigned)grid), 256, 0, as_stream(stream)>>>(
+    interaction_bwd_k<<<dim3((unsigned)n_graphs), 64, 0, as_stream(stream)>>>(
         g_im, g_z1, g_z2, g_kl, f, t, s, u_feat, graph_ptr, n_graphs, bn_gamma, bn_beta,
         bn_running_mean, bn_running_var, bn_eps, training, w2, w_att, z1, lam, logit, stats,
         df, dt, ds, pgrad);

@@ -7,7 +7,7 @@
 // exactly, so the loss needs the 64 x 64 Gram matrix G = IM^T IM plus one dot
 // product per edge: O(N d^2) flops over one read of IM (HBM-bound), no N^2.
 //
-// recon_partial_k: each workgroup reduces a contiguous row range; its four
+// recon_partial_k: each workgroup reduces a contiguous ~64-row range; its four
 //   wavefronts each own one 32x32 quadrant of G and accumulate it with the
 //   exact-f32 MFMA v_mfma_f32_32x32x2_f32 (two rows per instruction: lane l
 //   feeds row l>>5, channel l&31 of the quadrant's A and B halves), then
@@ -27,9 +27,11 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 constexpr int kGram = 64 * 64;
 constexpr int kFinBlocks = 16;  // 16 x 256 threads = one Gram entry per thread
 
+// ~64 rows per partial workgroup (short dependent MFMA/load chains, enough
+// workgroups to spread over the CUs), at most 1024 slabs
 __host__ __device__ __forceinline__ int64_t recon_blocks(int64_t n) {
-    int64_t g = (n + 255) / 256;
-    return g < 1 ? 1 : (g > 256 ? 256 : g);
+    int64_t g = (n + 63) / 64;
+    return g < 1 ? 1 : (g > 1024 ? 1024 : g);
 }
 
 // partials layout (floats): [G][4096] gram slabs | edge sums [G, padded to a
@@ -99,7 +101,15 @@ __global__ __launch_bounds__(256) void recon_finalize_k(float *__restrict__ part
                                                         float *__restrict__ loss) {
     const int e = blockIdx.x * 256 + threadIdx.x;  // Gram entry
     double acc = 0.0;
-    for (int b = 0; b < G; ++b) acc += static_cast<double>(partials[(int64_t)b * kGram + e]);
+    int b = 0;
+    for (; b + 8 <= G; b += 8) {  // 8 independent loads in flight, summed in order
+        float v[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = partials[(int64_t)(b + j) * kGram + e];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc += static_cast<double>(v[j]);
+    }
+    for (; b < G; ++b) acc += static_cast<double>(partials[(int64_t)b * kGram + e]);
     gram[e] = static_cast<float>(acc);
     __shared__ double red[256];
     red[threadIdx.x] = acc * acc;
@@ -146,7 +156,7 @@ __global__ __launch_bounds__(256) void recon_bwd_k(const float *__restrict__ im,
     __syncthreads();
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const float scale = *g_loss / static_cast<float>(n);
-    const int64_t rows_per_blk = 64;
+    const int64_t rows_per_blk = 32;
     const int64_t rb = xcd_remap(blockIdx.x, gridDim.x) * rows_per_blk;
     for (int64_t v = rb + w; v < rb + rows_per_blk && v < n; v += 4) {
         const float iv = im[v * 64 + lane];
@@ -191,7 +201,7 @@ extern "C" int scgib_recon_bwd(const float *im, const float *gram, const int32_t
                                float *grad_im, scgib_stream_t stream) {
     if (n_nodes <= 0) return SCGIB_EINVAL;
     if (!im || !gram || !rowptr_in || !rowptr_out || !g_loss || !grad_im) return SCGIB_EINVAL;
-    const int64_t grid = (n_nodes + 63) / 64;
+    const int64_t grid = (n_nodes + 31) / 32;
     recon_bwd_k<<<dim3((unsigned)grid), 256, 0, as_stream(stream)>>>(
         im, gram, rowptr_in, col_in, rowptr_out, col_out, n_nodes, g_loss, grad_im);
     return launch_status();

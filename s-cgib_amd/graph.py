@@ -74,7 +74,8 @@ class GraphBatch:
     """A batch of B graphs with N nodes and E directed edges."""
 
     def __init__(self, rowptr, col, graph_ptr, batch_num_nodes, batch_num_edges=None,
-                 rowptr_t=None, col_t=None, max_graph_nodes=None, n_edges=None):
+                 rowptr_t=None, col_t=None, max_graph_nodes=None, n_edges=None,
+                 host_info=None):
         self.rowptr = rowptr
         self.col = col
         self.rowptr_t = rowptr if rowptr_t is None else rowptr_t
@@ -84,11 +85,15 @@ class GraphBatch:
         self._bnn = None if batch_num_nodes is None else np.asarray(batch_num_nodes, np.int64)
         self._bne = None if batch_num_edges is None else np.asarray(batch_num_edges, np.int64)
         self._n = int(rowptr.shape[0] - 1)
-        self._e = int(col.shape[0]) if n_edges is None else int(n_edges)
+        self._e = int(col.shape[0]) if n_edges is None else (None if n_edges < 0 else int(n_edges))
         self._B = int(graph_ptr.shape[0] - 1)
         if max_graph_nodes is None:
             max_graph_nodes = int(self._bnn.max()) if self._bnn is not None and len(self._bnn) else 0
         self.max_graph_nodes = int(max_graph_nodes)
+        # host-side facts known at construction (no device sync to get them):
+        # {"deg": in-degree per node (np.int64), "selfloops": per-node 0/1,
+        #  "validated": edges never leave their graph}
+        self.host_info = host_info
         self.ndata = _NData(self)
         self.edata = {}
 
@@ -113,9 +118,15 @@ class GraphBatch:
             batch_num_edges = np.array([len(src)], np.int64)
         gptr = np.zeros(len(batch_num_nodes) + 1, np.int64)
         np.cumsum(batch_num_nodes, out=gptr[1:])
+        # edges must stay inside their graph (the ego-net builder relies on it)
+        owner = np.searchsorted(gptr, np.arange(n), side="right") - 1 if n else np.zeros(0, np.int64)
+        validated = bool(len(src) == 0 or (owner[src] == owner[dst]).all())
+        sl = np.zeros(n, np.int64)
+        np.add.at(sl, src[src == dst], 1)
+        info = {"deg": np.diff(rp.astype(np.int64)), "selfloops": sl, "validated": validated}
         return cls(torch.from_numpy(rp), torch.from_numpy(col),
                    torch.from_numpy(gptr.astype(np.int32)), batch_num_nodes, batch_num_edges,
-                   rp_t2, col_t2)
+                   rp_t2, col_t2, host_info=info)
 
     # ----- DGL surface ------------------------------------------------------
     def num_nodes(self, ntype=None):
@@ -124,6 +135,8 @@ class GraphBatch:
     number_of_nodes = num_nodes
 
     def num_edges(self, etype=None):
+        if self._e is None:  # ego batches sized by capacity: read the exact count once
+            self._e = int(self.rowptr[-1].item())
         return self._e
 
     number_of_edges = num_edges
@@ -161,7 +174,7 @@ class GraphBatch:
         """(src, dst) int64 in DGL's order for to_bidirected graphs: (src, dst) sorted."""
         deg = (self.rowptr_t[1:] - self.rowptr_t[:-1]).to(torch.int64)
         src = torch.repeat_interleave(torch.arange(self._n, device=self.device), deg)
-        return src, self.col_t[: self._e].to(torch.int64)
+        return src, self.col_t[: self.num_edges()].to(torch.int64)
 
     def in_degrees(self):
         return (self.rowptr[1:] - self.rowptr[:-1]).to(torch.int64)
@@ -176,7 +189,7 @@ class GraphBatch:
         g = GraphBatch(mv(self.rowptr), mv(self.col), mv(self.graph_ptr), self._bnn, self._bne,
                        None if self.symmetric else mv(self.rowptr_t),
                        None if self.symmetric else mv(self.col_t), self.max_graph_nodes,
-                       self._e)
+                       -1 if self._e is None else self._e, self.host_info)
         for k, v in self.ndata.items():
             dict.__setitem__(g.ndata, k, v.to(device, non_blocking=non_blocking))
         return g
@@ -317,8 +330,9 @@ def egonet_batch(g: GraphBatch, k: int, x=None):
 
     Equivalent to ``dgl.batch(chain(*[[dgl.khop_in_subgraph(m, v, k)[0] for v
     in m.nodes()] for m in molecules]))`` (exp_pretraining.py:269-272,
-    308-309).  Runs on ``g``'s HIP device through scgib_egonet_count/fill; one
-    3-integer device->host read (the ego batch's size) sizes the outputs.
+    308-309).  Runs on ``g``'s HIP device through scgib_egonet_count/fill.  For
+    k = 1 on a host-validated graph the output sizes are known on the host
+    (no device sync); otherwise one 3-integer device->host read sizes them.
     The result carries ``ndata['_ID']`` (parent node id of every ego node)
     and, if ``x`` is given, ``ndata['x'] = x[_ID]``.
     """
@@ -336,16 +350,26 @@ def egonet_batch(g: GraphBatch, k: int, x=None):
     err = torch.zeros(1, dtype=i32, device=dev)
     st = _stream()
     mgn = max(g.max_graph_nodes, 1)
+    info = g.host_info
     _lib.call("scgib_egonet_count", _ptr(g.rowptr), _ptr(g.col), _ptr(g.graph_ptr), g.batch_size,
               n, k, mgn, _ptr(ego_ptr), _ptr(ego_eptr), _ptr(ws), _ptr(err), st)
-    tot = torch.stack([ego_ptr[n], ego_eptr[n], err[0]]).cpu().tolist()
-    n_s, e_s, e_code = int(tot[0]), int(tot[1]), int(tot[2])
-    if e_code:
-        raise _lib.ScgibError(f"scgib_egonet_count flagged error bits {e_code} "
-                              "(1: edge leaves its graph, 2: graph larger than max_graph_nodes)")
+    if k == 1 and info is not None and info["validated"] and mgn <= 512:
+        # sizes known on the host, no device sync: |ball(v)| = 1 + deg(v) - selfloop(v);
+        # the induced-edge count is bounded by sum_{u in ball(v)} deg(u)
+        ball = 1 + info["deg"] - info["selfloops"]
+        n_s = int(ball.sum())
+        e_cap = int((info["deg"] * ball).sum())
+        e_s = -1  # exact count read lazily (GraphBatch.num_edges)
+    else:
+        tot = torch.stack([ego_ptr[n], ego_eptr[n], err[0]]).cpu().tolist()
+        n_s, e_s, e_code = int(tot[0]), int(tot[1]), int(tot[2])
+        if e_code:
+            raise _lib.ScgibError(f"scgib_egonet_count flagged error bits {e_code} "
+                                  "(1: edge leaves its graph, 2: graph larger than max_graph_nodes)")
+        e_cap = e_s
     ego_nodes = torch.empty(n_s, dtype=i32, device=dev)
     sub_rowptr = torch.empty(n_s + 1, dtype=i32, device=dev)
-    sub_col = torch.empty(max(e_s, 1), dtype=i32, device=dev)
+    sub_col = torch.empty(max(e_cap, 1), dtype=i32, device=dev)
     _lib.call("scgib_egonet_fill", _ptr(g.rowptr), _ptr(g.col), _ptr(g.graph_ptr), g.batch_size, n,
               k, mgn, _ptr(ego_ptr), _ptr(ego_eptr), _ptr(ego_nodes), _ptr(sub_rowptr),
               _ptr(sub_col), _ptr(err), st)

@@ -51,6 +51,52 @@ int scgib_gin_aggregate(const float *h, const int32_t *rowptr, const int32_t *co
                         int64_t n_nodes, int32_t dim, float one_plus_eps, float *out,
                         scgib_stream_t stream);
 
+/* ---- A5 fused: one GIN layer = GINConv(MLP) + BatchNorm1d + ReLU -----------
+ * Replaces, per layer, DGL GINConv + nn.Linear x2 + ReLU + nn.BatchNorm1d +
+ * F.relu of GIN.forward (models.py:63-71) and their autograd backward.
+ * Tiles of 64 rows; scgib_gin_tiles(n) tiles; tile_stats holds 128 floats per
+ * tile.  `stat` is the layer's [4][64] BN record: mean, invstd, scale
+ * (= gamma*invstd), shift (= beta - mean*scale).
+ *
+ * scgib_gin_layer_fwd: agg = (1+eps) x_v + sum_{u->v} x_u with x = h_in, or
+ *   x = relu(in_stat.scale * h_in + in_stat.shift) when in_stat != NULL
+ *   (the previous layer's BN+ReLU applied on load; d_in must be 64);
+ *   r = relu(agg W1^T + b1); z2 = r W2^T + b2; per-tile (sum, centred M2).
+ *   d_in in {32, 64}; hidden 64.  Outputs agg [n,d_in], r, z2 [n,64].
+ * scgib_bn_finalize: training: batch mean/var from the tile stats (fp64
+ *   Chan combine), running stats updated (momentum, unbiased var,
+ *   num_batches_tracked += 1); eval: running stats.  Writes `stat`.
+ * scgib_bn_relu_apply: out = relu(stat.scale * z + stat.shift)  [n,64].
+ * scgib_gin_bwd_stats: dy = dh * [stat.scale z2 + stat.shift > 0], dh given,
+ *   or, with (rowptr_t, col_t), gathered from the next layer's d(agg):
+ *   dh_v = (1+eps) g_v + sum_{u in out(v)} g_u.  Per-tile sum(dy), sum(dy xhat).
+ * scgib_bn_bwd_finalize: dgamma, dbeta [64] and coef [2][64] for dz2.
+ * scgib_gin_layer_bwd: d(agg) [n,d_in] and wgrad = dW2[64*64] | dW1[64*d_in]
+ *   | db2[64] | db1[64] through per-workgroup slabs
+ *   (scgib_gin_slab_floats(n, d_in) floats) reduced in a fixed order. */
+int64_t scgib_gin_tiles(int64_t n_nodes);
+int64_t scgib_gin_slab_floats(int64_t n_nodes, int32_t d_in);
+int scgib_gin_layer_fwd(const float *h_in, int32_t d_in, const float *in_stat,
+                        const int32_t *rowptr, const int32_t *col, int64_t n_nodes,
+                        float one_plus_eps, const float *w1, const float *b1, const float *w2,
+                        const float *b2, float *agg, float *r, float *z2, float *tile_stats,
+                        scgib_stream_t stream);
+int scgib_bn_finalize(const float *tile_stats, int64_t n_nodes, const float *gamma,
+                      const float *beta, float eps, float momentum, int32_t training,
+                      float *running_mean, float *running_var, int64_t *num_batches_tracked,
+                      float *stat, scgib_stream_t stream);
+int scgib_bn_relu_apply(const float *z, const float *stat, int64_t n_nodes, float *out,
+                        scgib_stream_t stream);
+int scgib_gin_bwd_stats(const float *dh, const int32_t *rowptr_t, const int32_t *col_t,
+                        float one_plus_eps, const float *z2, const float *stat, int64_t n_nodes,
+                        float *dy, float *tile_stats, scgib_stream_t stream);
+int scgib_bn_bwd_finalize(const float *tile_stats, int64_t n_nodes, int32_t training,
+                          float *dgamma, float *dbeta, float *coef, scgib_stream_t stream);
+int scgib_gin_layer_bwd(const float *dy, const float *z2, const float *r, const float *agg,
+                        int32_t d_in, const float *stat, const float *coef, const float *w1,
+                        const float *w2, int64_t n_nodes, float *dagg, float *slab,
+                        float *wgrad, scgib_stream_t stream);
+
 /* ---- A6: per-segment readouts (dgl.sum_nodes) -------------------------------
  * out[s,:] = sum_{i in [ptr[s], ptr[s+1])} x[i,:]   (models.py:716, 725, 733)
  * segment_broadcast is its adjoint: out[i,:] = g[s,:] for every row i of s. */

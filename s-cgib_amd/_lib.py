@@ -32,6 +32,16 @@ SIGNATURES = {
     "scgib_interaction_bwd": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _I64, _I64, _P,
                                              _P, _P, _P, _F, _I32, _P, _P, _P, _P, _P, _P, _P,
                                              _P, _P, _P, _P]),
+    "scgib_gin_tiles": (_I64, [_I64]),
+    "scgib_gin_slab_floats": (_I64, [_I64, _I32]),
+    "scgib_gin_layer_fwd": (ctypes.c_int, [_P, _I32, _P, _P, _P, _I64, _F, _P, _P, _P, _P, _P, _P,
+                                           _P, _P, _P]),
+    "scgib_bn_finalize": (ctypes.c_int, [_P, _I64, _P, _P, _F, _F, _I32, _P, _P, _P, _P, _P]),
+    "scgib_bn_relu_apply": (ctypes.c_int, [_P, _P, _I64, _P, _P]),
+    "scgib_gin_bwd_stats": (ctypes.c_int, [_P, _P, _P, _F, _P, _P, _I64, _P, _P, _P]),
+    "scgib_bn_bwd_finalize": (ctypes.c_int, [_P, _I64, _I32, _P, _P, _P, _P]),
+    "scgib_gin_layer_bwd": (ctypes.c_int, [_P, _P, _P, _P, _I32, _P, _P, _P, _P, _I64, _P, _P,
+                                           _P, _P]),
     "scgib_recon_partials_floats": (_I64, [_I64]),
     "scgib_recon_fwd": (ctypes.c_int, [_P, _P, _P, _I64, _I64, _P, _P, _P, _P]),
     "scgib_recon_bwd": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _I64, _P, _P, _P]),

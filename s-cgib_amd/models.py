@@ -79,8 +79,12 @@ class GINConv(nn.Module):
 class GIN(nn.Module):
     """GIN encoder: L x [GINConv(MLP) -> BatchNorm1d -> ReLU] (models.py:52-72)."""
 
-    def __init__(self, input_dim, hidden_dim=64, num_gin_layers=5):
+    def __init__(self, input_dim, hidden_dim=64, num_gin_layers=5, fused=True):
         super().__init__()
+        # fused: every layer runs as the fused HIP kernels of gin_layer.hip;
+        # otherwise GINConv (HIP gather) + torch Linear/BatchNorm per layer.
+        # Both paths run on the HIP device only.
+        self.fused = fused and hidden_dim == 64 and input_dim in (32, 64)
         self.ginlayers = nn.ModuleList()
         self.batch_norms = nn.ModuleList()
         for layer in range(num_gin_layers):
@@ -89,6 +93,8 @@ class GIN(nn.Module):
             self.batch_norms.append(nn.BatchNorm1d(hidden_dim))
 
     def forward(self, g, h):
+        if self.fused:
+            return ops.gin_encoder(h, g, self)
         for conv, bn in zip(self.ginlayers, self.batch_norms):
             h = F.relu(bn(conv(g, h)))
         return h

@@ -65,6 +65,117 @@ def gin_aggregate(h, graph, one_plus_eps=1.0):
 
 
 # ---------------------------------------------------------------------------
+# A5 fused: the whole GIN encoder (L x GINConv(MLP) + BN + ReLU)
+# ---------------------------------------------------------------------------
+def _gin_layer_params(gin):
+    """Per layer (W1, b1, W2, b2, gamma, beta) of a models.GIN, flattened."""
+    out = []
+    for conv, bn in zip(gin.ginlayers, gin.batch_norms):
+        mlp = conv.apply_func.mlp
+        out += [mlp[0].weight, mlp[0].bias, mlp[2].weight, mlp[2].bias, bn.weight, bn.bias]
+    return out
+
+
+class _GinEncoder(torch.autograd.Function):
+    """GIN.forward (models.py:66-72) as fused HIP layers; see gin_layer.hip."""
+
+    @staticmethod
+    def forward(ctx, h0, graph, gin, training, *params):
+        h0 = _f32(h0, "gin_encoder")
+        n, d0 = h0.shape
+        dev = h0.device
+        st = _stream()
+        L = len(gin.ginlayers)
+        ntiles = int(_lib.query("scgib_gin_tiles", n))
+        tstats = torch.empty(max(ntiles, 1), 128, dtype=torch.float32, device=dev)
+        saved, h, stat_prev = [], h0, None
+        for l in range(L):
+            conv, bn = gin.ginlayers[l], gin.batch_norms[l]
+            w1, b1, w2, b2, gamma, beta = (_f32(p, "gin param") for p in params[6 * l: 6 * l + 6])
+            d_in = h.shape[1]
+            if w1.shape != (HIDDEN, d_in) or w2.shape != (HIDDEN, HIDDEN):
+                raise _lib.ScgibError(f"fused GIN layer needs Linear({d_in},64)/Linear(64,64), got "
+                                      f"{tuple(w1.shape)}/{tuple(w2.shape)}")
+            agg = torch.empty(n, d_in, dtype=torch.float32, device=dev)
+            r = torch.empty(n, HIDDEN, dtype=torch.float32, device=dev)
+            z2 = torch.empty(n, HIDDEN, dtype=torch.float32, device=dev)
+            _lib.call("scgib_gin_layer_fwd", _p(h), d_in, _p(stat_prev), _p(graph.rowptr),
+                      _p(graph.col), n, conv._one_plus_eps, _p(w1), _p(b1), _p(w2), _p(b2),
+                      _p(agg), _p(r), _p(z2), _p(tstats), st)
+            stat = torch.empty(4, HIDDEN, dtype=torch.float32, device=dev)
+            track = training and bn.track_running_stats
+            _lib.call("scgib_bn_finalize", _p(tstats), n, _p(gamma), _p(beta), float(bn.eps),
+                      float(bn.momentum if bn.momentum is not None else 0.1), int(training),
+                      _p(bn.running_mean) if (track or not training) else None,
+                      _p(bn.running_var) if (track or not training) else None,
+                      _p(bn.num_batches_tracked) if track else None, _p(stat), st)
+            saved += [agg, r, z2, stat]
+            h, stat_prev = z2, stat
+        out = torch.empty(n, HIDDEN, dtype=torch.float32, device=dev)
+        _lib.call("scgib_bn_relu_apply", _p(h), _p(stat_prev), n, _p(out), st)
+        ctx.save_for_backward(*saved, *params)
+        ctx.graph, ctx.L, ctx.training = graph, L, training
+        ctx.opes = [c._one_plus_eps for c in gin.ginlayers]
+        return out
+
+    @staticmethod
+    def backward(ctx, g_out):
+        g_out = _f32(g_out, "gin_encoder.backward")
+        L, gr = ctx.L, ctx.graph
+        t = ctx.saved_tensors
+        saved, params = t[: 4 * L], t[4 * L:]
+        n = g_out.shape[0]
+        dev = g_out.device
+        st = _stream()
+        ntiles = int(_lib.query("scgib_gin_tiles", n))
+        tstats = torch.empty(max(ntiles, 1), 128, dtype=torch.float32, device=dev)
+        grads = [None] * (6 * L)
+        dagg_next = None
+        for l in reversed(range(L)):
+            agg, r, z2, stat = saved[4 * l: 4 * l + 4]
+            w1, _, w2 = params[6 * l], params[6 * l + 1], params[6 * l + 2]
+            d_in = agg.shape[1]
+            dy = torch.empty(n, HIDDEN, dtype=torch.float32, device=dev)
+            if dagg_next is None:
+                _lib.call("scgib_gin_bwd_stats", _p(g_out), None, None, 1.0, _p(z2), _p(stat), n,
+                          _p(dy), _p(tstats), st)
+            else:
+                _lib.call("scgib_gin_bwd_stats", _p(dagg_next), _p(gr.rowptr_t), _p(gr.col_t),
+                          ctx.opes[l + 1], _p(z2), _p(stat), n, _p(dy), _p(tstats), st)
+            bn_g = torch.empty(2, HIDDEN, dtype=torch.float32, device=dev)  # dgamma, dbeta
+            coef = torch.empty(2, HIDDEN, dtype=torch.float32, device=dev)
+            _lib.call("scgib_bn_bwd_finalize", _p(tstats), n, int(ctx.training), _p(bn_g[0]),
+                      _p(bn_g[1]), _p(coef), st)
+            dagg = torch.empty(n, d_in, dtype=torch.float32, device=dev)
+            slab = torch.empty(int(_lib.query("scgib_gin_slab_floats", n, d_in)),
+                               dtype=torch.float32, device=dev)
+            wgrad = torch.empty(HIDDEN * HIDDEN + HIDDEN * d_in + 2 * HIDDEN,
+                                dtype=torch.float32, device=dev)
+            _lib.call("scgib_gin_layer_bwd", _p(dy), _p(z2), _p(r), _p(agg), d_in, _p(stat),
+                      _p(coef), _p(_f32(w1, "w1")), _p(_f32(w2, "w2")), n, _p(dagg), _p(slab),
+                      _p(wgrad), st)
+            o = HIDDEN * HIDDEN
+            grads[6 * l + 2] = wgrad[:o].view(HIDDEN, HIDDEN)
+            grads[6 * l + 0] = wgrad[o:o + HIDDEN * d_in].view(HIDDEN, d_in)
+            o += HIDDEN * d_in
+            grads[6 * l + 3] = wgrad[o:o + HIDDEN]
+            grads[6 * l + 1] = wgrad[o + HIDDEN:o + 2 * HIDDEN]
+            grads[6 * l + 4] = bn_g[0]
+            grads[6 * l + 5] = bn_g[1]
+            dagg_next = dagg
+        # d h0 = (1+eps_0) d(agg_0) + sum over out-edges (transposed aggregation)
+        dh0 = _aggregate(dagg_next, gr.rowptr_t, gr.col_t, ctx.opes[0])
+        return (dh0, None, None, None, *grads)
+
+
+def gin_encoder(h, graph, gin):
+    """models.GIN.forward on the fused HIP layers (train or eval BN)."""
+    if graph.num_nodes() == 0:
+        raise _lib.ScgibError("gin_encoder on an empty graph")
+    return _GinEncoder.apply(h, graph, gin, bool(gin.training), *_gin_layer_params(gin))
+
+
+# ---------------------------------------------------------------------------
 # A6: segment sums (dgl.sum_nodes)
 # ---------------------------------------------------------------------------
 class _SegmentSum(torch.autograd.Function):

@@ -47,7 +47,16 @@ def golden_graph_arrays(g):
 CANCELLED = ("mlp.2.bias", "compressor.0.bias", "attn_layer.bias")
 
 
-def check_grads(golden_grads, mine_of, tol=1e-4, cancelled=CANCELLED):
+def rel_l2(a, b):
+    """||a - b|| / ||b||: robust to the isolated fp32 ReLU-mask flips that make
+    two correct fp32 implementations differ by a whole upstream gradient at a
+    handful of elements (pre-activations within rounding of 0)."""
+    a = np.asarray(a, np.float64)
+    b = np.asarray(b, np.float64)
+    return float(np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30)) if b.size else 0.0
+
+
+def check_grads(golden_grads, mine_of, tol=1e-4, cancelled=CANCELLED, metric="max"):
     for name, ref in golden_grads.items():
         mine = mine_of(name)
         assert mine is not None, name
@@ -61,5 +70,39 @@ def check_grads(golden_grads, mine_of, tol=1e-4, cancelled=CANCELLED):
             floor = 1e-3 * np.abs(ref[:, 64:]).max()
             assert np.abs(mine[:, :64]).max() <= floor, name
             mine, ref = mine[:, 64:], ref[:, 64:]
-        err = np.abs(mine - ref).max() / max(np.abs(ref).max(), 1e-30)
+        if metric == "l2":
+            err = rel_l2(mine, ref)
+        else:
+            err = np.abs(mine - ref).max() / max(np.abs(ref).max(), 1e-30)
         assert err < tol, (name, err)
+
+
+def check_grads_model(golden_grads, mine_of, tol=1e-3, cos_min=0.999, cancelled=CANCELLED):
+    """Whole-model gradient parity that is robust to fp32 ReLU-kink flips.
+
+    Two correct fp32 evaluations of the step can put a pre-activation that
+    sits within rounding of 0 (e.g. |z| = 3e-7 for a K=64 dot product of O(1)
+    terms) on opposite sides of a ReLU; that changes the gradient by a whole
+    upstream value at one element, which on a small tensor (a 64-bias) is a
+    percent-level per-tensor error (tools/diag_chain.py shows such a case in
+    the L5 golden).  So: the concatenation of all hot-path gradients must
+    agree within ``tol`` relative L2, and every tensor must point the same
+    way (cosine >= cos_min), which a sign/layout/indexing bug would break."""
+    num = den = 0.0
+    for name, ref in golden_grads.items():
+        mine = mine_of(name)
+        assert mine is not None, name
+        mine = mine.detach().cpu().numpy().astype(np.float64)
+        ref = np.asarray(ref, np.float64)
+        if name.endswith(cancelled):
+            sib = np.asarray(golden_grads[name.rsplit(".", 1)[0] + ".weight"])
+            assert np.abs(mine).max() <= 1e-3 * np.abs(sib).max(), name
+            continue
+        if name.endswith("attn_layer.weight"):
+            assert np.abs(mine[:, :64]).max() <= 1e-3 * np.abs(ref[:, 64:]).max(), name
+            mine, ref = mine[:, 64:], ref[:, 64:]
+        num += float(((mine - ref) ** 2).sum())
+        den += float((ref ** 2).sum())
+        cos = float((mine * ref).sum() / max(np.linalg.norm(mine) * np.linalg.norm(ref), 1e-300))
+        assert cos >= cos_min, (name, cos)
+    assert (num / max(den, 1e-300)) ** 0.5 < tol, (num / den) ** 0.5

@@ -71,7 +71,9 @@ def _worker(rank, world, port, molecules, q):
     reducer = pkg.dist.GradAllReducer(holder)
     reducer()
     if r == 0:
-        q.put({k: params[k].grad.clone() for k in grads})
+        # numpy (pickled by value): torch tensors would travel as shared fds that
+        # race with this process's exit
+        q.put({k: params[k].grad.numpy().copy() for k in grads})
     dist.barrier()
     dist.destroy_process_group()
 
@@ -97,7 +99,7 @@ def test_grad_allreduce_matches_mean_of_shards(pkg):
             expect[k] = expect.get(k, 0) + v / world
     assert set(got) == set(expect)
     for k in expect:
-        assert torch.allclose(got[k], expect[k], rtol=1e-5, atol=1e-7), k
+        assert torch.allclose(torch.from_numpy(got[k]), expect[k], rtol=1e-5, atol=1e-7), k
 
 
 def test_shard_covers_everything_once(pkg):

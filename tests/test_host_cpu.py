@@ -143,3 +143,39 @@ def test_synthetic_shapes(pkg, workload):
     assert abs(g.num_nodes() / 256 - mu) < 0.15 * mu
     deg = np.diff(g.rowptr.numpy())
     assert deg.min() >= 1
+
+
+def test_dgl_dropin_khop_and_ingest(pkg):
+    """s-cgib_amd/dgl.py (the drop-in DGL surface) against the reference goldens:
+    graph -> to_bidirected -> ndata['x'] (util.py:317-321) and khop_in_subgraph
+    per node (exp_pretraining.py:269-272)."""
+    dgl = pkg.dgl
+    d = load_golden("ingest_egonet")
+    for i in range(int(d["num_mols"])):
+        ei, x = d[f"m{i}_edge_index"], d[f"m{i}_x"]
+        try:
+            g = dgl.to_bidirected(dgl.graph((torch.from_numpy(ei[0]), torch.from_numpy(ei[1]))))
+            g.ndata["x"] = torch.from_numpy(x)
+            kept = True
+        except (pkg.graph.GraphIngestError, ValueError):
+            kept = False
+        assert kept == bool(d[f"m{i}_kept"]), i
+        if not kept:
+            continue
+        s, t = g.edges()
+        np.testing.assert_array_equal(s.numpy(), d[f"m{i}_src"])
+        np.testing.assert_array_equal(t.numpy(), d[f"m{i}_dst"])
+        for k in (1, 2):
+            nodes, es, ed, sizes = [], [], [], []
+            for v in range(g.num_nodes()):
+                sg, _ = dgl.khop_in_subgraph(g, v, k)
+                nodes.append(sg.ndata["_ID"].numpy())
+                a, b = sg.edges()
+                es.append(a.numpy())
+                ed.append(b.numpy())
+                sizes.append(sg.num_nodes())
+                assert torch.equal(sg.ndata["x"], g.ndata["x"][sg.ndata["_ID"]])
+            np.testing.assert_array_equal(np.array(sizes), d[f"m{i}_k{k}_sizes"])
+            np.testing.assert_array_equal(np.concatenate(nodes), d[f"m{i}_k{k}_nodes"])
+            np.testing.assert_array_equal(np.concatenate(es), d[f"m{i}_k{k}_esrc"])
+            np.testing.assert_array_equal(np.concatenate(ed), d[f"m{i}_k{k}_edst"])

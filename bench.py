@@ -35,6 +35,9 @@ pkg = importlib.import_module("s-cgib_amd")
 
 HBM_PEAK_GBS = 8000.0       # MI355X spec (MI355X_MICROARCH.md:36)
 HBM_MEASURED_GBS = 6290.0   # float4 copy, same file
+# HBM bytes per launch from rocprofv3 PMC passes (profiles/, corrected per
+# MI355X_MICROARCH.md: 2 x FETCH_SIZE + WRITE_SIZE); filled by tools/pmc_summary.py
+TRAFFIC = {}
 METRIC = "graphs/sec (pretrain step, GIN-64×5, k=1) at 1/2/4/8 MI355X; % HBM roofline"
 
 
@@ -52,44 +55,55 @@ def make_model(F_in, k, gin_layers, dev):
     return model.to(dev).train()
 
 
-class AggTimer:
-    """HIP-event timing of every GIN aggregation launch (fwd and bwd) on the
-    stream it is launched on (torch's current stream).
+def layer_fwd_bytes(n, e, d_in):
+    """Algorithmic bytes of one gin_fwd_k launch: the gather (neighbour + self
+    rows, col + rowptr), the MLP weights, and the agg / r / z2 / tile-stat
+    writes."""
+    return (agg_bytes(n, e, d_in) - 4 * d_in * n          # gather reads + indices
+            + 4 * (64 * d_in + 64 + 64 * 64 + 64)          # W1, b1, W2, b2
+            + 4 * n * (d_in + 64 + 64) + 512 * ((n + 63) // 64))
 
-    A ~170 us spin kernel is queued ahead of each bracketed launch so the
-    GPU is still busy while the host submits [start event, kernel, end
-    event]; the events then bracket the kernel itself rather than the host's
-    launch latency (the step is launch-bound at these sizes)."""
 
-    def __init__(self):
-        self.records = []  # (start_event, end_event, bytes)
-        self._orig = None
+def layer_fwd_flops(n, d_in):
+    return 2 * n * 64 * (d_in + 64)
+
+
+class KernelTimer:
+    """HIP-event timing of every launch of one C-ABI entry point (routed
+    through ops._launch) on the stream it is launched on (torch's current
+    stream).  A ~170 us spin kernel is queued ahead of each bracketed launch
+    so the GPU is still busy while the host submits [start event, kernel, end
+    event]: the events bracket the kernel, not the host's launch latency."""
+
+    def __init__(self, name):
+        self.name = name
+        self.records = []  # (start_event, end_event, meta)
 
     def __enter__(self):
-        ops = pkg.ops
-        self._orig = ops._aggregate
-        rec = self.records
-
-        def timed(h, rowptr, col, ope):
+        def observe(name, meta, launch):
+            if name != self.name:
+                return launch()
             s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             torch.cuda._sleep(400_000)
             s.record()
-            out = self._orig(h, rowptr, col, ope)
+            rc = launch()
             e.record()
-            rec.append((s, e, agg_bytes(h.shape[0], int(col.shape[0]), h.shape[1])))
-            return out
+            self.records.append((s, e, meta))
+            return rc
 
-        ops._aggregate = timed
+        pkg.ops.OBSERVER = observe
         return self
 
     def __exit__(self, *exc):
-        pkg.ops._aggregate = self._orig
+        pkg.ops.OBSERVER = None
 
-    def summary(self):
+    def summary(self, bytes_fn, flops_fn):
         torch.cuda.synchronize()
         ms = [s.elapsed_time(e) for s, e, _ in self.records]
-        byts = [b for _, _, b in self.records]
-        return sum(byts) / len(byts), sum(ms) / len(ms), len(ms)
+        byts = [bytes_fn(m["n"], m["e"], m["d_in"]) for _, _, m in self.records]
+        fl = [flops_fn(m["n"], m["d_in"]) for _, _, m in self.records]
+        k = len(ms)
+        return sum(byts) / k, sum(fl) / k, sum(ms) / k, k
 
 
 def superbatch_roofline(dev, n_target=1_200_000, reps=20):
@@ -187,6 +201,8 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=20.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-superbatch", action="store_true")
+    ap.add_argument("--eager", action="store_true",
+                    help="launch every kernel from Python (no HIP-graph capture)")
     a = ap.parse_args()
 
     # hipBLASLt's heuristics pick 2-workgroup kernels for the tall-skinny
@@ -210,18 +226,66 @@ def main():
         pool.append(g)
 
     model = make_model(F_in, a.k, a.gin_layers, dev)
-    opt = torch.optim.Adam(model.parameters(), lr=1e-4, weight_decay=5e-5)
     reducer = pkg.dist.GradAllReducer(model.parameters())
 
-    def step(i):
-        g = pool[i % len(pool)]
+    if a.eager:
+        opt = torch.optim.Adam(model.parameters(), lr=1e-4, weight_decay=5e-5)
+
+        def step(i):
+            g = pool[i % len(pool)]
+            opt.zero_grad(set_to_none=True)
+            _, kl, con, rec = model(g, g.ndata["x"], None, None, None, 1, None, a.k, dev, a.batch)
+            loss = kl + rec + con
+            loss.backward()
+            reducer()
+            opt.step()
+            return loss
+    else:
+        # capacity mode + HIP graph: one capture of (ego build, forward,
+        # backward[, Adam]) on static buffers; each step copies the next batch
+        # in (5 device-to-device copies) and replays.  Every kernel reads the
+        # batch's actual sizes from the device.
+        opt = torch.optim.Adam(model.parameters(), lr=1e-4, weight_decay=5e-5, capturable=True)
+        n_cap, e_cap, mgn, ego_caps = pkg.graph.StaticBatch.capacities(pool_host, a.k, slack=1.02)
+        static = pkg.graph.StaticBatch(a.batch, n_cap, e_cap, F_in, mgn, ego_caps, dev)
+        padded = []
+        for gh in pool_host:
+            gx = pkg.graph.GraphBatch.from_edges(*[t.numpy() for t in gh.edges()], gh.num_nodes(),
+                                                 True, gh.batch_num_nodes_host())
+            dict.__setitem__(gx.ndata, "x", F.normalize(gh.ndata["x"].float()))
+            padded.append(static.pad(gx))
+
+        def body():
+            _, kl, con, rec = model(static.graph, static.x, None, None, None, 1, None, a.k, dev,
+                                    a.batch)
+            loss = kl + rec + con
+            loss.backward()
+            return loss
+
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):  # warm-up (allocator, Adam state) off the capture
+            for i in range(3):
+                static.load(padded[i % len(padded)])
+                opt.zero_grad(set_to_none=True)
+                body()
+                reducer()
+                opt.step()
+        torch.cuda.current_stream().wait_stream(side)
+        graph = torch.cuda.CUDAGraph()
         opt.zero_grad(set_to_none=True)
-        _, kl, con, rec = model(g, g.ndata["x"], None, None, None, 1, None, a.k, dev, a.batch)
-        loss = kl + rec + con
-        loss.backward()
-        reducer()
-        opt.step()
-        return loss
+        with torch.cuda.graph(graph):
+            static_loss = body()
+            if world == 1:
+                opt.step()
+
+        def step(i):
+            static.load(padded[i % len(padded)])
+            graph.replay()
+            if world > 1:  # gradient all-reduce over RCCL outside the graph
+                reducer()
+                opt.step()
+            return static_loss
 
     for i in range(a.warmup):
         step(i)
@@ -243,12 +307,15 @@ def main():
         elapsed = float(t.item())
     final_loss = float(loss.item())
 
-    # instrumented replay of the same steps: HIP events around every GIN
-    # aggregation launch (the dominant HBM kernel) for the roofline figure
-    with AggTimer() as timer:
-        for i in range(min(a.steps, 20)):
-            step(a.warmup + i)
-    avg_bytes, avg_ms, n_launch = timer.summary()
+    # instrumented eager pass over the same batches: HIP events around every
+    # launch of the measured kernel (forward+backward of the same model)
+    with KernelTimer("scgib_gin_layer_fwd") as timer:
+        for i in range(min(a.steps, 10)):
+            g = pool[i % len(pool)]
+            model.zero_grad(set_to_none=True)
+            _, kl, con, rec = model(g, g.ndata["x"], None, None, None, 1, None, a.k, dev, a.batch)
+            (kl + rec + con).backward()
+    avg_bytes, avg_flops, avg_ms, n_launch = timer.summary(layer_fwd_bytes, layer_fwd_flops)
     achieved = avg_bytes / (avg_ms * 1e-3) / 1e9
 
     sb = None if a.no_superbatch or rank != 0 else superbatch_roofline(dev)
@@ -274,14 +341,20 @@ def main():
             "data": "synthetic (seeded QM9-like molecules, SURVEY.md §8(d)); random-init weights",
             "config": {"workload": f"{a.workload} pretrain step GIN-64x{a.gin_layers} "
                                    f"k={a.k}, batch {a.batch}/GPU, Mainmodel_continue + Adam",
+                       "launch": "eager" if a.eager else "hip-graph replay (capacity mode)",
                        "global_batch": world * a.batch, "nodes_per_batch": round(n_nodes, 1),
                        "parallelism": f"dp{world}", "final_loss": round(final_loss, 4)},
-            "roofline": {"bound": "hbm", "kernel": "gin_aggregate_k (fwd+bwd launches)",
+            "roofline": {"bound": "hbm", "kernel": "gin_fwd_k (fused GIN layer: gather + "
+                                                   "2 f32-MFMA GEMMs + BN tile stats)",
                          "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "frac_vs_measured_copy": round(achieved / HBM_MEASURED_GBS, 4),
-                         "traffic": None, "avg_launch_us": round(avg_ms * 1e3, 3),
-                         "avg_bytes_per_launch": int(avg_bytes), "launches_timed": n_launch},
+                         "traffic": TRAFFIC.get("gin_fwd_k"),
+                         "avg_launch_us": round(avg_ms * 1e3, 3),
+                         "avg_bytes_per_launch": int(avg_bytes),
+                         "mfma_tflops": round(avg_flops / (avg_ms * 1e-3) / 1e12, 2),
+                         "mfma_frac_f32": round(avg_flops / (avg_ms * 1e-3) / 1e12 / 157.3, 4),
+                         "launches_timed": n_launch},
             "roofline_superbatch": None if sb is None else {
                 "bound": "hbm", "kernel": "gin_aggregate_k d=64", "nodes": sb["nodes"],
                 "edges": sb["edges"], "achieved": round(sb["gbs"], 1), "peak": HBM_PEAK_GBS,

@@ -15,7 +15,13 @@
  *   - return 0 (SCGIB_OK), a negative SCGIB_E* argument error, or a positive
  *     hipError_t from the launch; nothing throws across the ABI;
  *   - deterministic: no floating-point atomics; every reduction has a fixed
- *     order for a given shape.
+ *     order for a given shape;
+ *   - capacity mode (HIP-graph replay): functions taking `const int32_t *dims`
+ *     accept it NULL (the host sizes are exact) or a DEVICE array with the
+ *     actual counts, dims[0] = nodes (or segments), dims[1] = edges, each <=
+ *     the host size, which then only sizes the launch.  Rows past the actual
+ *     count are written as zeros, so capacity-padded buffers stay finite and
+ *     one captured graph serves every batch that fits.
  */
 #ifndef SCGIB_H
 #define SCGIB_H
@@ -49,7 +55,7 @@ const char *scgib_strerror(int code);
  * dim % 4 == 0, 4 <= dim <= 256. */
 int scgib_gin_aggregate(const float *h, const int32_t *rowptr, const int32_t *col,
                         int64_t n_nodes, int32_t dim, float one_plus_eps, float *out,
-                        scgib_stream_t stream);
+                        const int32_t *dims, scgib_stream_t stream);
 
 /* ---- A5 fused: one GIN layer = GINConv(MLP) + BatchNorm1d + ReLU -----------
  * Replaces, per layer, DGL GINConv + nn.Linear x2 + ReLU + nn.BatchNorm1d +
@@ -80,30 +86,34 @@ int scgib_gin_layer_fwd(const float *h_in, int32_t d_in, const float *in_stat,
                         const int32_t *rowptr, const int32_t *col, int64_t n_nodes,
                         float one_plus_eps, const float *w1, const float *b1, const float *w2,
                         const float *b2, float *agg, float *r, float *z2, float *tile_stats,
-                        scgib_stream_t stream);
+                        const int32_t *dims, scgib_stream_t stream);
 int scgib_bn_finalize(const float *tile_stats, int64_t n_nodes, const float *gamma,
                       const float *beta, float eps, float momentum, int32_t training,
                       float *running_mean, float *running_var, int64_t *num_batches_tracked,
-                      float *stat, scgib_stream_t stream);
+                      float *stat, const int32_t *dims, scgib_stream_t stream);
 int scgib_bn_relu_apply(const float *z, const float *stat, int64_t n_nodes, float *out,
-                        scgib_stream_t stream);
+                        const int32_t *dims, scgib_stream_t stream);
 int scgib_gin_bwd_stats(const float *dh, const int32_t *rowptr_t, const int32_t *col_t,
                         float one_plus_eps, const float *z2, const float *stat, int64_t n_nodes,
-                        float *dy, float *tile_stats, scgib_stream_t stream);
+                        float *dy, float *tile_stats, const int32_t *dims,
+                        scgib_stream_t stream);
 int scgib_bn_bwd_finalize(const float *tile_stats, int64_t n_nodes, int32_t training,
-                          float *dgamma, float *dbeta, float *coef, scgib_stream_t stream);
+                          float *dgamma, float *dbeta, float *coef, const int32_t *dims,
+                          scgib_stream_t stream);
 int scgib_gin_layer_bwd(const float *dy, const float *z2, const float *r, const float *agg,
                         int32_t d_in, const float *stat, const float *coef, const float *w1,
                         const float *w2, int64_t n_nodes, float *dagg, float *slab,
-                        float *wgrad, scgib_stream_t stream);
+                        float *wgrad, const int32_t *dims, scgib_stream_t stream);
 
 /* ---- A6: per-segment readouts (dgl.sum_nodes) -------------------------------
  * out[s,:] = sum_{i in [ptr[s], ptr[s+1])} x[i,:]   (models.py:716, 725, 733)
  * segment_broadcast is its adjoint: out[i,:] = g[s,:] for every row i of s. */
 int scgib_segment_sum(const float *x, const int32_t *ptr, int64_t n_seg, int32_t dim,
-                      float *out, scgib_stream_t stream);
+                      float *out, const int32_t *dims, scgib_stream_t stream);
+/* n_rows: rows of `out` (rows past ptr[actual n_seg] are zeroed in capacity mode) */
 int scgib_segment_broadcast(const float *g, const int32_t *ptr, int64_t n_seg, int32_t dim,
-                            float *out, scgib_stream_t stream);
+                            float *out, int64_t n_rows, const int32_t *dims,
+                            scgib_stream_t stream);
 
 /* ---- A2: k-hop ego-net builder (dgl.khop_in_subgraph for every node) -------
  * Replaces the per-node Python loop of exp_pretraining.py:269-272 (+ the
@@ -121,17 +131,20 @@ int scgib_segment_broadcast(const float *g, const int32_t *ptr, int64_t n_seg, i
  * Step 2, scgib_egonet_fill: writes, for the batched ego graph (ego j <-> node j,
  * ego nodes sorted ascending, DGL node_subgraph edge order):
  *   ego_nodes[N_s]   parent node id of every ego node (DGL's ndata['_ID'] + offset)
- *   sub_rowptr[N_s+1], sub_col[E_s]  dst-major CSR in ego-batch node ids. */
+ *   sub_rowptr[N_s+1], sub_col[E_s]  dst-major CSR in ego-batch node ids.
+ * n_ego_cap = length of ego_nodes (>= N_s): entries [N_s, n_ego_cap) get
+ * parent id 0 and empty CSR rows.  ego_dims (nullable, device int32[2])
+ * receives [N_s, E_s] (the ego batch's `dims` in capacity mode). */
 int64_t scgib_egonet_workspace_bytes(int64_t n_nodes);
 int scgib_egonet_count(const int32_t *rowptr, const int32_t *col, const int32_t *graph_ptr,
                        int64_t n_graphs, int64_t n_nodes, int32_t k, int32_t max_graph_nodes,
                        int32_t *ego_ptr, int32_t *ego_eptr, void *workspace, int32_t *err,
-                       scgib_stream_t stream);
+                       const int32_t *dims, scgib_stream_t stream);
 int scgib_egonet_fill(const int32_t *rowptr, const int32_t *col, const int32_t *graph_ptr,
                       int64_t n_graphs, int64_t n_nodes, int32_t k, int32_t max_graph_nodes,
                       const int32_t *ego_ptr, const int32_t *ego_eptr, int32_t *ego_nodes,
-                      int32_t *sub_rowptr, int32_t *sub_col, int32_t *err,
-                      scgib_stream_t stream);
+                      int32_t *sub_rowptr, int32_t *sub_col, int32_t *err, int64_t n_ego_cap,
+                      const int32_t *dims, int32_t *ego_dims, scgib_stream_t stream);
 
 /* ---- A6-A8 + A10/A11 inputs: core <-> subgraph interaction, fused ----------
  * One wavefront per molecule.  Restates, per graph i (models.py:595-604,
@@ -147,6 +160,9 @@ int scgib_egonet_fill(const int32_t *rowptr, const int32_t *col, const int32_t *
  *   logit_v = w_att[0:64].z1[i] + w_att[64:128].s_v + b_att, alpha = softmax_i
  *   im[:, 64:128] = alpha * s
  *   kl_tensor[2*n_last, 64]: the last graph's KL term, twice (models.py:659)
+ * kl_mean (scalar) = mean(kl_tensor); either output may be NULL (not both).
+ * pad_rows != 0: n_nodes is a row capacity and rows [graph_ptr[B], n_nodes)
+ * of im, lam, logit are zeroed (capacity mode; B stays exact).
  * Saved for backward: lam[N], logit[N], stats[B, SCGIB_STATS_STRIDE].
  * Scalars b2, b_att are device pointers (no host sync). */
 int scgib_interaction_fwd(const float *f, const float *t, const float *s,
@@ -156,8 +172,8 @@ int scgib_interaction_fwd(const float *f, const float *t, const float *s,
                           const float *bn_running_var, float bn_eps, int32_t training,
                           const float *w2, const float *b2, const float *w_att,
                           const float *b_att, float *im, float *z1, float *z2, float *lam,
-                          float *logit, float *stats, float *kl_tensor,
-                          scgib_stream_t stream);
+                          float *logit, float *stats, float *kl_tensor, float *kl_mean,
+                          int32_t pad_rows, scgib_stream_t stream);
 
 /* Sequential running-stat update of the per-graph compressor BatchNorm: one
  * nn.BatchNorm1d call per graph in graph order (models.py:642 inside the loop
@@ -167,7 +183,9 @@ int scgib_bn_running_update(const float *stats, const int32_t *graph_ptr, int64_
                             float momentum, float *running_mean, float *running_var,
                             int64_t *num_batches_tracked, scgib_stream_t stream);
 
-/* Backward of scgib_interaction_fwd.  g_kl may be NULL (no KL gradient).
+/* Backward of scgib_interaction_fwd.  The KL gradient is g_kl [2 n_last, 64],
+ * or g_klmean (device scalar, gradient of kl_mean), or neither (both NULL).
+ * pad_rows: zero rows [graph_ptr[B], n_nodes) of df, dt, ds.
  * Outputs df, dt, ds [N,64] and per-graph parameter-gradient partials
  * pgrad[B, SCGIB_PGRAD_STRIDE] laid out as
  *   [0,64) dW2 | 64 db2 | [65,129) dgamma | [129,193) dbeta |
@@ -181,7 +199,8 @@ int scgib_interaction_bwd(const float *g_im, const float *g_z1, const float *g_z
                           float bn_eps, int32_t training, const float *w2,
                           const float *w_att, const float *z1, const float *lam,
                           const float *logit, const float *stats, float *df, float *dt,
-                          float *ds, float *pgrad, scgib_stream_t stream);
+                          float *ds, float *pgrad, const float *g_klmean, int32_t pad_rows,
+                          scgib_stream_t stream);
 
 /* ---- A12: adjacency reconstruction loss, Gram form ------------------------
  * loss = sum_{u,v} (<im_u, im_v> - A_uv)^2 / N
@@ -194,14 +213,14 @@ int scgib_interaction_bwd(const float *g_im, const float *g_z1, const float *g_z
 int64_t scgib_recon_partials_floats(int64_t n_nodes);
 int scgib_recon_fwd(const float *im, const int32_t *rowptr, const int32_t *col,
                     int64_t n_nodes, int64_t n_edges, float *partials, float *gram,
-                    float *loss, scgib_stream_t stream);
+                    float *loss, const int32_t *dims, scgib_stream_t stream);
 /* d loss / d im = (g_loss / N) * (4 IM G - 2 (A + A^T) IM); pass the in-CSR and
  * the out-CSR (the same arrays for a symmetric graph).  g_loss is a device
  * scalar. */
 int scgib_recon_bwd(const float *im, const float *gram, const int32_t *rowptr_in,
                     const int32_t *col_in, const int32_t *rowptr_out, const int32_t *col_out,
                     int64_t n_nodes, const float *g_loss, float *grad_im,
-                    scgib_stream_t stream);
+                    const int32_t *dims, scgib_stream_t stream);
 
 #ifdef __cplusplus
 }

@@ -18,35 +18,37 @@ _P, _I64, _I32, _F = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32, ctypes.c_f
 SIGNATURES = {
     "scgib_abi_version": (ctypes.c_int, []),
     "scgib_strerror": (ctypes.c_char_p, [ctypes.c_int]),
-    "scgib_gin_aggregate": (ctypes.c_int, [_P, _P, _P, _I64, _I32, _F, _P, _P]),
-    "scgib_segment_sum": (ctypes.c_int, [_P, _P, _I64, _I32, _P, _P]),
-    "scgib_segment_broadcast": (ctypes.c_int, [_P, _P, _I64, _I32, _P, _P]),
+    "scgib_gin_aggregate": (ctypes.c_int, [_P, _P, _P, _I64, _I32, _F, _P, _P, _P]),
+    "scgib_segment_sum": (ctypes.c_int, [_P, _P, _I64, _I32, _P, _P, _P]),
+    "scgib_segment_broadcast": (ctypes.c_int, [_P, _P, _I64, _I32, _P, _I64, _P, _P]),
     "scgib_egonet_workspace_bytes": (_I64, [_I64]),
-    "scgib_egonet_count": (ctypes.c_int, [_P, _P, _P, _I64, _I64, _I32, _I32, _P, _P, _P, _P, _P]),
+    "scgib_egonet_count": (ctypes.c_int, [_P, _P, _P, _I64, _I64, _I32, _I32, _P, _P, _P, _P, _P,
+                                          _P]),
     "scgib_egonet_fill": (ctypes.c_int, [_P, _P, _P, _I64, _I64, _I32, _I32, _P, _P, _P, _P, _P,
-                                         _P, _P]),
+                                         _P, _I64, _P, _P, _P]),
     "scgib_interaction_fwd": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _I64, _I64, _P, _P, _P, _P,
                                              _F, _I32, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P,
-                                             _P, _P]),
+                                             _P, _P, _I32, _P]),
     "scgib_bn_running_update": (ctypes.c_int, [_P, _P, _I64, _F, _P, _P, _P, _P]),
     "scgib_interaction_bwd": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _I64, _I64, _P,
                                              _P, _P, _P, _F, _I32, _P, _P, _P, _P, _P, _P, _P,
-                                             _P, _P, _P, _P]),
+                                             _P, _P, _P, _P, _I32, _P]),
     "scgib_gin_tiles": (_I64, [_I64]),
     "scgib_gin_slab_floats": (_I64, [_I64, _I32]),
     "scgib_gin_layer_fwd": (ctypes.c_int, [_P, _I32, _P, _P, _P, _I64, _F, _P, _P, _P, _P, _P, _P,
-                                           _P, _P, _P]),
-    "scgib_bn_finalize": (ctypes.c_int, [_P, _I64, _P, _P, _F, _F, _I32, _P, _P, _P, _P, _P]),
-    "scgib_bn_relu_apply": (ctypes.c_int, [_P, _P, _I64, _P, _P]),
-    "scgib_gin_bwd_stats": (ctypes.c_int, [_P, _P, _P, _F, _P, _P, _I64, _P, _P, _P]),
-    "scgib_bn_bwd_finalize": (ctypes.c_int, [_P, _I64, _I32, _P, _P, _P, _P]),
+                                           _P, _P, _P, _P]),
+    "scgib_bn_finalize": (ctypes.c_int, [_P, _I64, _P, _P, _F, _F, _I32, _P, _P, _P, _P, _P, _P]),
+    "scgib_bn_relu_apply": (ctypes.c_int, [_P, _P, _I64, _P, _P, _P]),
+    "scgib_gin_bwd_stats": (ctypes.c_int, [_P, _P, _P, _F, _P, _P, _I64, _P, _P, _P, _P]),
+    "scgib_bn_bwd_finalize": (ctypes.c_int, [_P, _I64, _I32, _P, _P, _P, _P, _P]),
     "scgib_gin_layer_bwd": (ctypes.c_int, [_P, _P, _P, _P, _I32, _P, _P, _P, _P, _I64, _P, _P,
-                                           _P, _P]),
+                                           _P, _P, _P]),
     "scgib_recon_partials_floats": (_I64, [_I64]),
-    "scgib_recon_fwd": (ctypes.c_int, [_P, _P, _P, _I64, _I64, _P, _P, _P, _P]),
-    "scgib_recon_bwd": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _I64, _P, _P, _P]),
+    "scgib_recon_fwd": (ctypes.c_int, [_P, _P, _P, _I64, _I64, _P, _P, _P, _P, _P]),
+    "scgib_recon_bwd": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _I64, _P, _P, _P, _P]),
 }
 
+ABI_VERSION = 2
 STATS_STRIDE = 260
 PGRAD_STRIDE = 324
 HIDDEN = 64
@@ -71,7 +73,7 @@ def load():
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    if lib.scgib_abi_version() != 1:
+    if lib.scgib_abi_version() != ABI_VERSION:
         raise ScgibError("libscgib.so ABI version mismatch")
     _lib = lib
     return lib

@@ -44,4 +44,11 @@ __device__ __forceinline__ int64_t xcd_remap(int64_t orig, int64_t nwg) {
     return base + orig / 8;
 }
 
+// Capacity mode: when `dims` (device int32) is given, dims[idx] is the actual
+// count and `cap` (host) only sizes the grid; rows in [actual, cap) are
+// written as zeros so padded buffers stay finite under graph replay.
+__device__ __forceinline__ int64_t eff_count(const int32_t *dims, int idx, int64_t cap) {
+    return dims ? static_cast<int64_t>(dims[idx]) : cap;
+}
+
 }  // namespace scgib

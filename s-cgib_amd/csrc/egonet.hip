@@ -107,11 +107,11 @@ __global__ __launch_bounds__(256) void egonet_count_k(
     const int32_t *__restrict__ rowptr, const int32_t *__restrict__ col,
     const int32_t *__restrict__ gptr, int64_t n_graphs, int64_t n, int k,
     int32_t *__restrict__ ego_ptr, int32_t *__restrict__ ego_eptr,
-    int32_t *__restrict__ blk_tot, int32_t *err) {
+    int32_t *__restrict__ blk_tot, int32_t *err, const int32_t *__restrict__ dims) {
     __shared__ int32_t sn[256], se[256];
     const int64_t v = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
     int32_t nb = 0, ne = 0;
-    if (v < n) {
+    if (v < eff_count(dims, 0, n)) {
         const int64_t g = graph_of(gptr, n_graphs, v);
         const int32_t base = gptr[g], ng = gptr[g + 1] - base;
         if (ng > 64 * W) {
@@ -199,10 +199,23 @@ __global__ __launch_bounds__(256) void egonet_fill_k(
     const int32_t *__restrict__ gptr, int64_t n_graphs, int64_t n, int k,
     const int32_t *__restrict__ ego_ptr, const int32_t *__restrict__ ego_eptr,
     int32_t *__restrict__ ego_nodes, int32_t *__restrict__ sub_rowptr,
-    int32_t *__restrict__ sub_col, int32_t *err) {
+    int32_t *__restrict__ sub_col, int32_t *err, int64_t n_ego_cap,
+    const int32_t *__restrict__ dims, int32_t *__restrict__ ego_dims) {
     const int64_t v = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
-    if (v >= n) return;
-    if (v == n - 1) sub_rowptr[ego_ptr[n]] = ego_eptr[n];
+    if (v == 0 && ego_dims) {  // the ego batch's actual [N_s, E_s], device-resident
+        ego_dims[0] = ego_ptr[n];
+        ego_dims[1] = ego_eptr[n];
+    }
+    // tail of the ego batch: [N_s, n_ego_cap) gets parent id 0 and empty CSR
+    // rows, and sub_rowptr[N_s] = E_s (capacity-sized buffers stay valid)
+    {
+        const int64_t ns = ego_ptr[n], es = ego_eptr[n];
+        for (int64_t i = ns + v; i <= n_ego_cap; i += static_cast<int64_t>(gridDim.x) * 256) {
+            sub_rowptr[i] = static_cast<int32_t>(es);
+            if (i < n_ego_cap) ego_nodes[i] = 0;
+        }
+    }
+    if (v >= eff_count(dims, 0, n)) return;
     const int64_t g = graph_of(gptr, n_graphs, v);
     const int32_t base = gptr[g], ng = gptr[g + 1] - base;
     if (ng > 64 * W) return;  // flagged by the count pass
@@ -250,7 +263,7 @@ extern "C" int scgib_egonet_count(const int32_t *rowptr, const int32_t *col,
                                   const int32_t *graph_ptr, int64_t n_graphs, int64_t n_nodes,
                                   int32_t k, int32_t max_graph_nodes, int32_t *ego_ptr,
                                   int32_t *ego_eptr, void *workspace, int32_t *err,
-                                  scgib_stream_t stream) {
+                                  const int32_t *dims, scgib_stream_t stream) {
     if (n_nodes < 0 || n_graphs < 0 || k < 0) return SCGIB_EINVAL;
     if (!ego_ptr || !ego_eptr || !err || !workspace) return SCGIB_EINVAL;
     if (n_nodes > 0 && (!rowptr || !col || !graph_ptr || n_graphs == 0)) return SCGIB_EINVAL;
@@ -267,7 +280,7 @@ extern "C" int scgib_egonet_count(const int32_t *rowptr, const int32_t *col,
     int32_t *blk_tot = static_cast<int32_t *>(workspace);
 #define SCGIB_EGO_COUNT(WW)                                                                     \
     egonet_count_k<WW><<<nblk, 256, 0, st>>>(rowptr, col, graph_ptr, n_graphs, n_nodes, k,    \
-                                             ego_ptr, ego_eptr, blk_tot, err)
+                                             ego_ptr, ego_eptr, blk_tot, err, dims)
     switch (W) {
         case 1: SCGIB_EGO_COUNT(1); break;
         case 2: SCGIB_EGO_COUNT(2); break;
@@ -284,6 +297,7 @@ extern "C" int scgib_egonet_fill(const int32_t *rowptr, const int32_t *col,
                                  int32_t k, int32_t max_graph_nodes, const int32_t *ego_ptr,
                                  const int32_t *ego_eptr, int32_t *ego_nodes,
                                  int32_t *sub_rowptr, int32_t *sub_col, int32_t *err,
+                                 int64_t n_ego_cap, const int32_t *dims, int32_t *ego_dims,
                                  scgib_stream_t stream) {
     if (n_nodes < 0 || n_graphs < 0 || k < 0) return SCGIB_EINVAL;
     if (!ego_ptr || !ego_eptr || !sub_rowptr || !err) return SCGIB_EINVAL;
@@ -299,7 +313,8 @@ extern "C" int scgib_egonet_fill(const int32_t *rowptr, const int32_t *col,
 #define SCGIB_EGO_FILL(WW)                                                                      \
     egonet_fill_k<WW><<<dim3((unsigned)nblk), 256, 0, st>>>(rowptr, col, graph_ptr, n_graphs,  \
                                                             n_nodes, k, ego_ptr, ego_eptr,     \
-                                                            ego_nodes, sub_rowptr, sub_col, err)
+                                                            ego_nodes, sub_rowptr, sub_col, err, \
+                                                            n_ego_cap, dims, ego_dims)
     switch (W) {
         case 1: SCGIB_EGO_FILL(1); break;
         case 2: SCGIB_EGO_FILL(2); break;

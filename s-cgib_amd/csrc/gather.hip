@@ -21,13 +21,18 @@ template <int LPR>
 __global__ __launch_bounds__(256) void gin_aggregate_k(const float4 *__restrict__ h,
                                                        const int32_t *__restrict__ rowptr,
                                                        const int32_t *__restrict__ col,
-                                                       int64_t n, float ope,
-                                                       float4 *__restrict__ out) {
+                                                       int64_t ncap, float ope,
+                                                       float4 *__restrict__ out,
+                                                       const int32_t *__restrict__ dims) {
     constexpr int RPB = 256 / LPR;
     const int64_t blk = xcd_remap(blockIdx.x, gridDim.x);
     const int64_t v = blk * RPB + threadIdx.x / LPR;
     const int c = threadIdx.x % LPR;
-    if (v >= n) return;
+    if (v >= ncap) return;
+    if (v >= eff_count(dims, 0, ncap)) {
+        out[v * LPR + c] = make_float4(0.f, 0.f, 0.f, 0.f);
+        return;
+    }
     const int32_t beg = rowptr[v], end = rowptr[v + 1];
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
     int32_t j = beg;
@@ -47,12 +52,17 @@ __global__ __launch_bounds__(256) void gin_aggregate_k(const float4 *__restrict_
 template <int LPR>
 __global__ __launch_bounds__(256) void segment_sum_k(const float4 *__restrict__ x,
                                                      const int32_t *__restrict__ ptr,
-                                                     int64_t nseg, float4 *__restrict__ out) {
+                                                     int64_t nseg, float4 *__restrict__ out,
+                                                     const int32_t *__restrict__ dims) {
     constexpr int RPB = 256 / LPR;
     const int64_t blk = xcd_remap(blockIdx.x, gridDim.x);
     const int64_t s = blk * RPB + threadIdx.x / LPR;
     const int c = threadIdx.x % LPR;
     if (s >= nseg) return;
+    if (s >= eff_count(dims, 0, nseg)) {
+        out[s * LPR + c] = make_float4(0.f, 0.f, 0.f, 0.f);
+        return;
+    }
     const int64_t beg = ptr[s], end = ptr[s + 1];
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
     int64_t i = beg;
@@ -69,12 +79,22 @@ template <int LPR>
 __global__ __launch_bounds__(256) void segment_broadcast_k(const float4 *__restrict__ g,
                                                            const int32_t *__restrict__ ptr,
                                                            int64_t nseg,
-                                                           float4 *__restrict__ out) {
+                                                           float4 *__restrict__ out,
+                                                           int64_t nrows,
+                                                           const int32_t *__restrict__ dims) {
     constexpr int RPB = 256 / LPR;
     const int64_t blk = xcd_remap(blockIdx.x, gridDim.x);
     const int64_t s = blk * RPB + threadIdx.x / LPR;
     const int c = threadIdx.x % LPR;
-    if (s >= nseg) return;
+    const int64_t ns = eff_count(dims, 0, nseg);
+    if (dims) {  // zero the rows past the last valid segment (grid-stride)
+        const int64_t r0 = ptr[ns];
+        const int64_t tot = (nrows - r0) * LPR;
+        for (int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x; i < tot;
+             i += static_cast<int64_t>(gridDim.x) * 256)
+            out[r0 * LPR + i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    if (s >= ns) return;
     const float4 val = g[s * LPR + c];
     for (int64_t i = ptr[s]; i < ptr[s + 1]; ++i) out[i * LPR + c] = val;
 }
@@ -111,39 +131,41 @@ using namespace scgib;
 
 extern "C" int scgib_gin_aggregate(const float *h, const int32_t *rowptr, const int32_t *col,
                                    int64_t n_nodes, int32_t dim, float one_plus_eps,
-                                   float *out, scgib_stream_t stream) {
+                                   float *out, const int32_t *dims, scgib_stream_t stream) {
     if (n_nodes < 0 || !dim_ok(dim)) return SCGIB_EINVAL;
     if (n_nodes == 0) return SCGIB_OK;
     if (!h || !rowptr || !col || !out) return SCGIB_EINVAL;
     hipStream_t st = as_stream(stream);
     SCGIB_DISPATCH_LPR(dim, gin_aggregate_k, n_nodes, reinterpret_cast<const float4 *>(h),
-                       rowptr, col, n_nodes, one_plus_eps, reinterpret_cast<float4 *>(out));
+                       rowptr, col, n_nodes, one_plus_eps, reinterpret_cast<float4 *>(out), dims);
     return launch_status();
 }
 
 extern "C" int scgib_segment_sum(const float *x, const int32_t *ptr, int64_t n_seg,
-                                 int32_t dim, float *out, scgib_stream_t stream) {
+                                 int32_t dim, float *out, const int32_t *dims,
+                                 scgib_stream_t stream) {
     if (n_seg < 0 || !dim_ok(dim)) return SCGIB_EINVAL;
     if (n_seg == 0) return SCGIB_OK;
     if (!x || !ptr || !out) return SCGIB_EINVAL;
     hipStream_t st = as_stream(stream);
     SCGIB_DISPATCH_LPR(dim, segment_sum_k, n_seg, reinterpret_cast<const float4 *>(x), ptr,
-                       n_seg, reinterpret_cast<float4 *>(out));
+                       n_seg, reinterpret_cast<float4 *>(out), dims);
     return launch_status();
 }
 
 extern "C" int scgib_segment_broadcast(const float *g, const int32_t *ptr, int64_t n_seg,
-                                       int32_t dim, float *out, scgib_stream_t stream) {
-    if (n_seg < 0 || !dim_ok(dim)) return SCGIB_EINVAL;
+                                       int32_t dim, float *out, int64_t n_rows,
+                                       const int32_t *dims, scgib_stream_t stream) {
+    if (n_seg < 0 || n_rows < 0 || !dim_ok(dim)) return SCGIB_EINVAL;
     if (n_seg == 0) return SCGIB_OK;
     if (!g || !ptr || !out) return SCGIB_EINVAL;
     hipStream_t st = as_stream(stream);
     SCGIB_DISPATCH_LPR(dim, segment_broadcast_k, n_seg, reinterpret_cast<const float4 *>(g),
-                       ptr, n_seg, reinterpret_cast<float4 *>(out));
+                       ptr, n_seg, reinterpret_cast<float4 *>(out), n_rows, dims);
     return launch_status();
 }
 
-extern "C" int scgib_abi_version(void) { return 1; }
+extern "C" int scgib_abi_version(void) { return 2; }
 
 extern "C" const char *scgib_strerror(int code) {
     if (code == SCGIB_OK) return "ok";

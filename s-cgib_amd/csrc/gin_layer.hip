@@ -102,11 +102,12 @@ template <int DIN, bool XFORM>
 __global__ __launch_bounds__(256) void gin_fwd_k(
     const float *__restrict__ h, const float *__restrict__ in_scale,
     const float *__restrict__ in_shift, const int32_t *__restrict__ rowptr,
-    const int32_t *__restrict__ col, int64_t n, float ope, const float *__restrict__ w1,
+    const int32_t *__restrict__ col, int64_t ncap, float ope, const float *__restrict__ w1,
     const float *__restrict__ b1, const float *__restrict__ w2, const float *__restrict__ b2,
     float *__restrict__ agg_out, float *__restrict__ r_out, float *__restrict__ z2_out,
-    float *__restrict__ part) {
+    float *__restrict__ part, const int32_t *__restrict__ dims) {
     constexpr int LDA = DIN + 1, LPR = DIN / 4, RPP = 256 / LPR;
+    const int64_t n = eff_count(dims, 0, ncap);
     __shared__ float sA[TM * LDA];
     __shared__ float sW1[64 * LDA];
     __shared__ float sW2[64 * LDH];
@@ -115,7 +116,19 @@ __global__ __launch_bounds__(256) void gin_fwd_k(
     const int tid = threadIdx.x, l = tid & 63, w = tid >> 6;
     const int64_t tile = blockIdx.x;
     const int64_t row0 = tile * TM;
-    const int nv = static_cast<int>(n - row0 < TM ? n - row0 : TM);  // valid rows
+    const int nv = static_cast<int>(n - row0 < TM ? (n - row0 > 0 ? n - row0 : 0) : TM);  // valid rows
+    if (dims) {  // capacity mode: zero this tile's padded rows [nv, rows in capacity)
+        const int ncr = static_cast<int>(ncap - row0 < TM ? ncap - row0 : TM);
+        for (int idx = nv * 64 + tid; idx < ncr * 64; idx += 256) {
+            r_out[row0 * 64 + idx] = 0.f;
+            z2_out[row0 * 64 + idx] = 0.f;
+        }
+        for (int idx = nv * DIN + tid; idx < ncr * DIN; idx += 256) agg_out[row0 * DIN + idx] = 0.f;
+        if (nv == 0) {
+            if (tid < 128) part[tile * 128 + tid] = 0.f;
+            return;
+        }
+    }
 
     for (int idx = tid; idx < 64 * DIN; idx += 256) sW1[(idx / DIN) * LDA + idx % DIN] = w1[idx];
     for (int idx = tid; idx < 64 * 64; idx += 256) sW2[(idx >> 6) * LDH + (idx & 63)] = w2[idx];
@@ -215,11 +228,13 @@ __global__ __launch_bounds__(256) void gin_fwd_k(
 // (exact decomposition of the centred sum of squares).  Loads are issued four
 // at a time so the partition loops are not latency chains.
 __global__ __launch_bounds__(1024) void bn_finalize_k(
-    const float *__restrict__ part, int64_t n, int64_t ntiles, const float *__restrict__ gamma,
+    const float *__restrict__ part, int64_t ncap, const float *__restrict__ gamma,
     const float *__restrict__ beta, float eps, float momentum, int training,
     float *__restrict__ rmean, float *__restrict__ rvar, int64_t *__restrict__ nbt,
-    float *__restrict__ stat /* [4][64]: mean, invstd, scale, shift */) {
+    float *__restrict__ stat /* [4][64]: mean, invstd, scale, shift */,
+    const int32_t *__restrict__ dims) {
     const int c = threadIdx.x & 63, p = threadIdx.x >> 6;
+    const int64_t n = eff_count(dims, 0, ncap), ntiles = (n + TM - 1) / TM;
     __shared__ double sh[16][64];
     __shared__ double s_mean[64];
     double mean = 0.0, var = 0.0, M2 = 0.0;
@@ -277,9 +292,14 @@ __global__ __launch_bounds__(1024) void bn_finalize_k(
 
 __global__ __launch_bounds__(256) void bn_relu_apply_k(const float4 *__restrict__ z,
                                                        const float *__restrict__ stat,
-                                                       int64_t n4, float4 *__restrict__ out) {
+                                                       int64_t n4, float4 *__restrict__ out,
+                                                       const int32_t *__restrict__ dims) {
     const int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
     if (i >= n4) return;
+    if (dims && i >= static_cast<int64_t>(dims[0]) * 16) {
+        out[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+        return;
+    }
     const int c = static_cast<int>(i & 15) * 4;
     out[i] = xform4(z[i], ld4(stat + 128 + c), ld4(stat + 192 + c));
 }
@@ -294,9 +314,10 @@ template <bool GATHER>
 __global__ __launch_bounds__(256) void gin_bwd_stats_k(
     const float *__restrict__ dh, const int32_t *__restrict__ rowptr_t,
     const int32_t *__restrict__ col_t, float ope, const float *__restrict__ z2,
-    const float *__restrict__ stat, int64_t n, float *__restrict__ dy_out,
-    float *__restrict__ part) {
+    const float *__restrict__ stat, int64_t ncap, float *__restrict__ dy_out,
+    float *__restrict__ part, const int32_t *__restrict__ dims) {
     __shared__ float sRed[2][16][64];
+    const int64_t n = eff_count(dims, 0, ncap);
     const int tid = threadIdx.x, c = tid & 15, slot = tid >> 4;
     const int64_t tile = blockIdx.x, row0 = tile * TM;
     const float4 mean = ld4(stat + 4 * c), istd = ld4(stat + 64 + 4 * c);
@@ -305,7 +326,11 @@ __global__ __launch_bounds__(256) void gin_bwd_stats_k(
     float4 sdy = make_float4(0.f, 0.f, 0.f, 0.f), sdx = sdy;
     for (int rr = slot; rr < TM; rr += 16) {
         const int64_t v = row0 + rr;
-        if (v >= n) break;
+        if (v >= ncap) break;
+        if (v >= n) {
+            st4(dy_out + v * 64 + 4 * c, make_float4(0.f, 0.f, 0.f, 0.f));
+            continue;
+        }
         float4 g;
         if (GATHER) {
             float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -346,12 +371,13 @@ __global__ __launch_bounds__(256) void gin_bwd_stats_k(
 // dbeta = sum dy, dgamma = sum dy xhat (fp64, fixed order); coefficients of
 // dz2 = scale (dy - c1 - xhat c2): training c1 = dbeta/N, c2 = dgamma/N.
 __global__ __launch_bounds__(1024) void bn_bwd_finalize_k(const float *__restrict__ part,
-                                                          int64_t n, int64_t ntiles,
-                                                          int training,
+                                                          int64_t ncap, int training,
                                                           float *__restrict__ dgamma,
                                                           float *__restrict__ dbeta,
-                                                          float *__restrict__ coef) {
+                                                          float *__restrict__ coef,
+                                                          const int32_t *__restrict__ dims) {
     const int c = threadIdx.x & 63, p = threadIdx.x >> 6;
+    const int64_t n = eff_count(dims, 0, ncap), ntiles = (n + TM - 1) / TM;
     __shared__ double s1[16][64], s2[16][64];
     double a = 0.0, b = 0.0;
     int64_t t = p;
@@ -386,7 +412,9 @@ __global__ __launch_bounds__(256) void gin_bwd_k(
     const float *__restrict__ dy, const float *__restrict__ z2, const float *__restrict__ r,
     const float *__restrict__ agg, const float *__restrict__ stat,
     const float *__restrict__ coef, const float *__restrict__ w1, const float *__restrict__ w2,
-    int64_t n, int64_t ntiles, float *__restrict__ dagg_out, float *__restrict__ slab) {
+    int64_t ncap, int64_t ntiles, float *__restrict__ dagg_out, float *__restrict__ slab,
+    const int32_t *__restrict__ dims) {
+    const int64_t n = eff_count(dims, 0, ncap);
     constexpr int LDA = DIN + 1;
     constexpr int SLAB = 64 * 64 + 64 * DIN + 128;
     __shared__ float sD[TM * LDH];   // dz2, then dz1
@@ -406,7 +434,12 @@ __global__ __launch_bounds__(256) void gin_bwd_k(
     constexpr int NSUB1 = 2 * (DIN / 32);  // 32x32 sub-tiles of dW1 / d(agg)
     for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
         const int64_t row0 = tile * TM;
-        const int nv = static_cast<int>(n - row0 < TM ? n - row0 : TM);
+        const int nv = static_cast<int>(n - row0 < TM ? (n - row0 > 0 ? n - row0 : 0) : TM);
+        if (dims) {  // capacity mode: zero this tile's padded rows of d(agg)
+            const int ncr = static_cast<int>(ncap - row0 < TM ? ncap - row0 : TM);
+            for (int idx = nv * DIN + tid; idx < ncr * DIN; idx += 256) dagg_out[row0 * DIN + idx] = 0.f;
+            if (nv == 0) continue;  // block-uniform
+        }
         __syncthreads();  // previous tile's LDS reads are done
         // stage dz2 (computed), r and agg tiles; rows past n are zero
         for (int rr = q; rr < TM; rr += 4) {
@@ -531,7 +564,8 @@ extern "C" int scgib_gin_layer_fwd(const float *h_in, int32_t d_in, const float 
                                    const int32_t *rowptr, const int32_t *col, int64_t n_nodes,
                                    float one_plus_eps, const float *w1, const float *b1,
                                    const float *w2, const float *b2, float *agg, float *r,
-                                   float *z2, float *tile_stats, scgib_stream_t stream) {
+                                   float *z2, float *tile_stats, const int32_t *dims,
+                                   scgib_stream_t stream) {
     if (n_nodes < 0 || (d_in != 32 && d_in != 64)) return SCGIB_EINVAL;
     if (n_nodes == 0) return SCGIB_OK;
     if (!h_in || !rowptr || !col || !w1 || !b1 || !w2 || !b2 || !agg || !r || !z2 || !tile_stats)
@@ -541,44 +575,44 @@ extern "C" int scgib_gin_layer_fwd(const float *h_in, int32_t d_in, const float 
     hipStream_t st = as_stream(stream);
     const float *isc = in_stat ? in_stat + 128 : nullptr, *ish = in_stat ? in_stat + 192 : nullptr;
     if (d_in == 32)
-        gin_fwd_k<32, false><<<dim3((unsigned)nt), 256, 0, st>>>(h_in, isc, ish, rowptr, col, n_nodes, one_plus_eps, w1, b1, w2, b2, agg, r, z2, tile_stats);
+        gin_fwd_k<32, false><<<dim3((unsigned)nt), 256, 0, st>>>(h_in, isc, ish, rowptr, col, n_nodes, one_plus_eps, w1, b1, w2, b2, agg, r, z2, tile_stats, dims);
     else if (in_stat)
-        gin_fwd_k<64, true><<<dim3((unsigned)nt), 256, 0, st>>>(h_in, isc, ish, rowptr, col, n_nodes, one_plus_eps, w1, b1, w2, b2, agg, r, z2, tile_stats);
+        gin_fwd_k<64, true><<<dim3((unsigned)nt), 256, 0, st>>>(h_in, isc, ish, rowptr, col, n_nodes, one_plus_eps, w1, b1, w2, b2, agg, r, z2, tile_stats, dims);
     else
-        gin_fwd_k<64, false><<<dim3((unsigned)nt), 256, 0, st>>>(h_in, isc, ish, rowptr, col, n_nodes, one_plus_eps, w1, b1, w2, b2, agg, r, z2, tile_stats);
+        gin_fwd_k<64, false><<<dim3((unsigned)nt), 256, 0, st>>>(h_in, isc, ish, rowptr, col, n_nodes, one_plus_eps, w1, b1, w2, b2, agg, r, z2, tile_stats, dims);
     return launch_status();
 }
 
 extern "C" int scgib_bn_finalize(const float *tile_stats, int64_t n_nodes, const float *gamma,
                                  const float *beta, float eps, float momentum, int32_t training,
                                  float *running_mean, float *running_var,
-                                 int64_t *num_batches_tracked, float *stat,
+                                 int64_t *num_batches_tracked, float *stat, const int32_t *dims,
                                  scgib_stream_t stream) {
     if (n_nodes < 0 || !gamma || !beta || !stat) return SCGIB_EINVAL;
     if (training && (n_nodes == 0 || !tile_stats)) return SCGIB_EINVAL;
     if (!training && (!running_mean || !running_var)) return SCGIB_EINVAL;
-    bn_finalize_k<<<1, 1024, 0, as_stream(stream)>>>(tile_stats, n_nodes, scgib_gin_tiles(n_nodes),
-                                                     gamma, beta, eps, momentum, training,
-                                                     running_mean, running_var,
-                                                     num_batches_tracked, stat);
+    bn_finalize_k<<<1, 1024, 0, as_stream(stream)>>>(tile_stats, n_nodes, gamma, beta, eps,
+                                                     momentum, training, running_mean,
+                                                     running_var, num_batches_tracked, stat, dims);
     return launch_status();
 }
 
 extern "C" int scgib_bn_relu_apply(const float *z, const float *stat, int64_t n_nodes,
-                                   float *out, scgib_stream_t stream) {
+                                   float *out, const int32_t *dims, scgib_stream_t stream) {
     if (n_nodes < 0) return SCGIB_EINVAL;
     if (n_nodes == 0) return SCGIB_OK;
     if (!z || !stat || !out) return SCGIB_EINVAL;
     const int64_t n4 = n_nodes * 16;
     bn_relu_apply_k<<<dim3((unsigned)((n4 + 255) / 256)), 256, 0, as_stream(stream)>>>(
-        reinterpret_cast<const float4 *>(z), stat, n4, reinterpret_cast<float4 *>(out));
+        reinterpret_cast<const float4 *>(z), stat, n4, reinterpret_cast<float4 *>(out), dims);
     return launch_status();
 }
 
 extern "C" int scgib_gin_bwd_stats(const float *dh, const int32_t *rowptr_t,
                                    const int32_t *col_t, float one_plus_eps, const float *z2,
                                    const float *stat, int64_t n_nodes, float *dy,
-                                   float *tile_stats, scgib_stream_t stream) {
+                                   float *tile_stats, const int32_t *dims,
+                                   scgib_stream_t stream) {
     if (n_nodes < 0) return SCGIB_EINVAL;
     if (n_nodes == 0) return SCGIB_OK;
     if (!dh || !z2 || !stat || !dy || !tile_stats) return SCGIB_EINVAL;
@@ -586,19 +620,18 @@ extern "C" int scgib_gin_bwd_stats(const float *dh, const int32_t *rowptr_t,
     const int64_t nt = scgib_gin_tiles(n_nodes);
     hipStream_t st = as_stream(stream);
     if (rowptr_t)
-        gin_bwd_stats_k<true><<<dim3((unsigned)nt), 256, 0, st>>>(dh, rowptr_t, col_t, one_plus_eps, z2, stat, n_nodes, dy, tile_stats);
+        gin_bwd_stats_k<true><<<dim3((unsigned)nt), 256, 0, st>>>(dh, rowptr_t, col_t, one_plus_eps, z2, stat, n_nodes, dy, tile_stats, dims);
     else
-        gin_bwd_stats_k<false><<<dim3((unsigned)nt), 256, 0, st>>>(dh, rowptr_t, col_t, one_plus_eps, z2, stat, n_nodes, dy, tile_stats);
+        gin_bwd_stats_k<false><<<dim3((unsigned)nt), 256, 0, st>>>(dh, rowptr_t, col_t, one_plus_eps, z2, stat, n_nodes, dy, tile_stats, dims);
     return launch_status();
 }
 
 extern "C" int scgib_bn_bwd_finalize(const float *tile_stats, int64_t n_nodes, int32_t training,
                                      float *dgamma, float *dbeta, float *coef,
-                                     scgib_stream_t stream) {
+                                     const int32_t *dims, scgib_stream_t stream) {
     if (n_nodes <= 0 || !tile_stats || !dgamma || !dbeta || !coef) return SCGIB_EINVAL;
-    bn_bwd_finalize_k<<<1, 1024, 0, as_stream(stream)>>>(tile_stats, n_nodes,
-                                                         scgib_gin_tiles(n_nodes), training,
-                                                         dgamma, dbeta, coef);
+    bn_bwd_finalize_k<<<1, 1024, 0, as_stream(stream)>>>(tile_stats, n_nodes, training, dgamma,
+                                                         dbeta, coef, dims);
     return launch_status();
 }
 
@@ -606,7 +639,7 @@ extern "C" int scgib_gin_layer_bwd(const float *dy, const float *z2, const float
                                    const float *agg, int32_t d_in, const float *stat,
                                    const float *coef, const float *w1, const float *w2,
                                    int64_t n_nodes, float *dagg, float *slab, float *wgrad,
-                                   scgib_stream_t stream) {
+                                   const int32_t *dims, scgib_stream_t stream) {
     if (n_nodes <= 0 || (d_in != 32 && d_in != 64)) return SCGIB_EINVAL;
     if (!dy || !z2 || !r || !agg || !stat || !coef || !w1 || !w2 || !dagg || !slab || !wgrad)
         return SCGIB_EINVAL;
@@ -614,9 +647,9 @@ extern "C" int scgib_gin_layer_bwd(const float *dy, const float *z2, const float
     const int grid = bwd_grid(nt);
     hipStream_t st = as_stream(stream);
     if (d_in == 32)
-        gin_bwd_k<32><<<grid, 256, 0, st>>>(dy, z2, r, agg, stat, coef, w1, w2, n_nodes, nt, dagg, slab);
+        gin_bwd_k<32><<<grid, 256, 0, st>>>(dy, z2, r, agg, stat, coef, w1, w2, n_nodes, nt, dagg, slab, dims);
     else
-        gin_bwd_k<64><<<grid, 256, 0, st>>>(dy, z2, r, agg, stat, coef, w1, w2, n_nodes, nt, dagg, slab);
+        gin_bwd_k<64><<<grid, 256, 0, st>>>(dy, z2, r, agg, stat, coef, w1, w2, n_nodes, nt, dagg, slab, dims);
     const int64_t width = 64 * 64 + 64 * d_in + 128;
     const int groups = (grid + kSlabGroup - 1) / kSlabGroup;
     float *partial = slab + static_cast<int64_t>(grid) * width;

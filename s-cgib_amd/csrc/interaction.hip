@@ -101,9 +101,18 @@ __global__ __launch_bounds__(64) void interaction_fwd_k(
     const float *__restrict__ b2p, const float *__restrict__ watt,
     const float *__restrict__ battp, float *__restrict__ im, float *__restrict__ z1,
     float *__restrict__ z2, float *__restrict__ lam, float *__restrict__ logit,
-    float *__restrict__ stats, float *__restrict__ kl) {
+    float *__restrict__ stats, float *__restrict__ kl, float *__restrict__ kl_mean,
+    int64_t n_rows_cap, int pad) {
     const Lanes L = lanes();
     const int64_t gi = blockIdx.x;
+    if (gi >= B) {  // padding blocks: zero rows [N, n_rows_cap) of im, lam, logit
+        const int64_t r_beg = gptr[B];
+        for (int64_t r = r_beg + (gi - B); r < n_rows_cap; r += gridDim.x - B) {
+            if (threadIdx.x < 32) st4(im + r * 128 + threadIdx.x * 4, f4(0.f));
+            if (threadIdx.x == 0) { lam[r] = 0.f; logit[r] = 0.f; }
+        }
+        return;
+    }
     const int64_t r0 = gptr[gi], r1 = gptr[gi + 1];
     const int n = static_cast<int>(r1 - r0);
     if (n <= 0) {
@@ -111,6 +120,7 @@ __global__ __launch_bounds__(64) void interaction_fwd_k(
             st4(z1 + gi * 64 + L.ch, f4(0.f));
             st4(z2 + gi * 64 + L.ch, f4(0.f));
         }
+        if (gi == B - 1 && kl_mean && threadIdx.x == 0) *kl_mean = 0.f;
         return;
     }
     // ---- pass 1: sums (readout of f, means) and shifted second moments ----
@@ -189,6 +199,7 @@ __global__ __launch_bounds__(64) void interaction_fwd_k(
             }
         }
         qacc = red_q4(qacc);
+        float ksum = 0.f;
         for (int64_t base = r0; base < r1; base += 4) {
             const int64_t r = base + L.q;
             const bool ok = r < r1;
@@ -201,10 +212,16 @@ __global__ __launch_bounds__(64) void interaction_fwd_k(
                 const float4 nn = ns * ns;
                 const float4 v = f4(0.5f) * make_float4(nn.x / den.x, nn.y / den.y, nn.z / den.z,
                                                         nn.w / den.w) + qacc;
-                st4(kl + (r - r0) * 64 + L.ch, v);
-                st4(kl + (r - r0 + n) * 64 + L.ch, v);
+                if (kl) {
+                    st4(kl + (r - r0) * 64 + L.ch, v);
+                    st4(kl + (r - r0 + n) * 64 + L.ch, v);
+                }
+                ksum += (v.x + v.y) + (v.z + v.w);
             }
         }
+        // mean over the duplicated [2n, 64] tensor == mean over [n, 64]
+        ksum = red_q(red16(ksum));
+        if (kl_mean && threadIdx.x == 0) *kl_mean = ksum / (static_cast<float>(n) * 64.f);
     }
     // ---- attention: logit_v = w_lo . z1 + w_hi . s_v + b; softmax per graph ----
     const float cst = red16(dot4(ld4(watt + L.ch), zacc)) + *battp;
@@ -294,9 +311,21 @@ __global__ __launch_bounds__(64) void interaction_bwd_k(
     int training, const float *__restrict__ w2, const float *__restrict__ watt,
     const float *__restrict__ z1, const float *__restrict__ lam,
     const float *__restrict__ logit, const float *__restrict__ stats, float *__restrict__ df,
-    float *__restrict__ dt, float *__restrict__ ds, float *__restrict__ pgrad) {
+    float *__restrict__ dt, float *__restrict__ ds, float *__restrict__ pgrad,
+    const float *__restrict__ g_klmean, int64_t n_rows_cap) {
     const Lanes L = lanes();
     const int64_t gi = blockIdx.x;
+    if (gi >= B) {  // padding blocks: zero rows [N, n_rows_cap) of df, dt, ds
+        const int64_t r_beg = gptr[B];
+        for (int64_t r = r_beg + (gi - B); r < n_rows_cap; r += gridDim.x - B) {
+            if (threadIdx.x < 16) {
+                st4(df + r * 64 + threadIdx.x * 4, f4(0.f));
+                st4(dt + r * 64 + threadIdx.x * 4, f4(0.f));
+                st4(ds + r * 64 + threadIdx.x * 4, f4(0.f));
+            }
+        }
+        return;
+    }
     const int64_t r0 = gptr[gi], r1 = gptr[gi + 1];
     const int n = static_cast<int>(r1 - r0);
     float *pg = pgrad + gi * SCGIB_PGRAD_STRIDE;
@@ -347,15 +376,19 @@ __global__ __launch_bounds__(64) void interaction_bwd_k(
     const float4 gz2 = ld4(g_z2 + gi * 64 + L.ch);            // d readout(f) -> every node's f
 
     // ---- KL (last graph) ----
-    const bool has_kl = (g_kl != nullptr) && (gi == B - 1);
+    // gradient of the KL term: a tensor g_kl [2n, 64] (both copies), or the
+    // scalar gradient of KL_Loss = mean(KL_tensor): g / (2n 64) per entry
+    const bool has_kl = (g_kl != nullptr || g_klmean != nullptr) && (gi == B - 1);
+    const float gk_uniform = g_klmean ? *g_klmean / (static_cast<float>(n) * 64.f) : 0.f;
     float4 Gc = f4(0.f);
-    if (has_kl) {
+    if (has_kl && g_kl) {
         for (int base = 0; base < n; base += 4) {
             const int rl = base + L.q;
             if (rl < n) Gc = Gc + ld4(g_kl + rl * 64 + L.ch) + ld4(g_kl + (rl + n) * 64 + L.ch);
         }
         Gc = red_q4(Gc);
     }
+    if (has_kl && !g_kl) Gc = f4(gk_uniform * n);
     const float4 se = sig + f4(kKlEps);
     const float4 inv2 = make_float4(1.f / (se.x * se.x), 1.f / (se.y * se.y), 1.f / (se.z * se.z),
                                     1.f / (se.w * se.w));
@@ -375,7 +408,8 @@ __global__ __launch_bounds__(64) void interaction_bwd_k(
         float4 dfv = lm * gn + gz2;
         if (has_kl) {
             const int rl = static_cast<int>(rr - r0);
-            const float4 gk = ld4(g_kl + rl * 64 + L.ch) + ld4(g_kl + (rl + n) * 64 + L.ch);
+            const float4 gk = g_kl ? ld4(g_kl + rl * 64 + L.ch) + ld4(g_kl + (rl + n) * 64 + L.ch)
+                                   : f4(gk_uniform);
             part += dot4(gk, (-(1.f - lm)) * (sig * sig * inv2)) + dot4(Gc, (2.f * lm) * (fm * fm * inv2));
             dfv = dfv + (2.f * lm * lm) * (Gc * fm * inv2);
         }
@@ -437,20 +471,21 @@ extern "C" int scgib_interaction_fwd(
     const float *bn_beta, const float *bn_running_mean, const float *bn_running_var,
     float bn_eps, int32_t training, const float *w2, const float *b2, const float *w_att,
     const float *b_att, float *im, float *z1, float *z2, float *lam, float *logit,
-    float *stats, float *kl_tensor, scgib_stream_t stream) {
+    float *stats, float *kl_tensor, float *kl_mean, int32_t pad_rows, scgib_stream_t stream) {
     if (n_graphs < 0 || n_nodes < 0) return SCGIB_EINVAL;
     if (n_graphs == 0) return SCGIB_OK;
     if (n_graphs > 0x7fffffff) return SCGIB_EUNSUPPORTED;
     if (!graph_ptr || !bn_gamma || !bn_beta || !w2 || !b2 || !w_att || !b_att || !z1 ||
-        !z2 || !stats || !kl_tensor)
+        !z2 || !stats || (!kl_tensor && !kl_mean))
         return SCGIB_EINVAL;
     if (n_nodes > 0 && (!f || !t || !s || !u_gate || !u_feat || !im || !lam || !logit))
         return SCGIB_EINVAL;
     if (!training && (!bn_running_mean || !bn_running_var)) return SCGIB_EINVAL;
-    interaction_fwd_k<<<dim3((unsigned)n_graphs), 64, 0, as_stream(stream)>>>(
+    const unsigned grid = static_cast<unsigned>(n_graphs + (pad_rows ? 64 : 0));
+    interaction_fwd_k<<<dim3(grid), 64, 0, as_stream(stream)>>>(
         f, t, s, u_gate, u_feat, graph_ptr, n_graphs, bn_gamma, bn_beta, bn_running_mean,
         bn_running_var, bn_eps, training, w2, b2, w_att, b_att, im, z1, z2, lam, logit, stats,
-        kl_tensor);
+        kl_tensor, kl_mean, n_nodes, pad_rows);
     return launch_status();
 }
 
@@ -474,7 +509,7 @@ extern "C" int scgib_interaction_bwd(
     const float *bn_running_mean, const float *bn_running_var, float bn_eps, int32_t training,
     const float *w2, const float *w_att, const float *z1, const float *lam,
     const float *logit, const float *stats, float *df, float *dt, float *ds, float *pgrad,
-    scgib_stream_t stream) {
+    const float *g_klmean, int32_t pad_rows, scgib_stream_t stream) {
     if (n_graphs < 0 || n_nodes < 0) return SCGIB_EINVAL;
     if (n_graphs == 0) return SCGIB_OK;
     if (n_graphs > 0x7fffffff) return SCGIB_EUNSUPPORTED;
@@ -485,9 +520,10 @@ extern "C" int scgib_interaction_bwd(
                         !ds))
         return SCGIB_EINVAL;
     if (!training && (!bn_running_mean || !bn_running_var)) return SCGIB_EINVAL;
-    interaction_bwd_k<<<dim3((unsigned)n_graphs), 64, 0, as_stream(stream)>>>(
+    const unsigned grid = static_cast<unsigned>(n_graphs + (pad_rows ? 64 : 0));
+    interaction_bwd_k<<<dim3(grid), 64, 0, as_stream(stream)>>>(
         g_im, g_z1, g_z2, g_kl, f, t, s, u_feat, graph_ptr, n_graphs, bn_gamma, bn_beta,
         bn_running_mean, bn_running_var, bn_eps, training, w2, w_att, z1, lam, logit, stats,
-        df, dt, ds, pgrad);
+        df, dt, ds, pgrad, g_klmean, n_nodes);
     return launch_status();
 }

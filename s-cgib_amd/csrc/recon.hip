@@ -42,10 +42,12 @@ __host__ __device__ __forceinline__ int64_t off_cnt(int64_t G) { return off_gsq(
 __global__ __launch_bounds__(256) void recon_partial_k(const float *__restrict__ im,
                                                        const int32_t *__restrict__ rowptr,
                                                        const int32_t *__restrict__ col,
-                                                       int64_t n, int64_t rows_per_blk,
-                                                       float *__restrict__ partials) {
+                                                       int64_t ncap, int64_t rows_per_blk,
+                                                       float *__restrict__ partials,
+                                                       const int32_t *__restrict__ dims) {
     const int G = gridDim.x;
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int64_t n = eff_count(dims, 0, ncap);
     const int64_t rb = static_cast<int64_t>(blockIdx.x) * rows_per_blk;
     const int64_t re = rb + rows_per_blk < n ? rb + rows_per_blk : n;
     if (blockIdx.x == 0 && threadIdx.x == 0) {
@@ -96,9 +98,11 @@ __global__ __launch_bounds__(256) void recon_partial_k(const float *__restrict__
 }
 
 __global__ __launch_bounds__(256) void recon_finalize_k(float *__restrict__ partials, int G,
-                                                        int64_t n, int64_t n_edges,
+                                                        int64_t ncap, int64_t ecap,
                                                         float *__restrict__ gram,
-                                                        float *__restrict__ loss) {
+                                                        float *__restrict__ loss,
+                                                        const int32_t *__restrict__ dims) {
+    const int64_t n = eff_count(dims, 0, ncap), n_edges = eff_count(dims, 1, ecap);
     const int e = blockIdx.x * 256 + threadIdx.x;  // Gram entry
     double acc = 0.0;
     int b = 0;
@@ -147,9 +151,11 @@ __global__ __launch_bounds__(256) void recon_bwd_k(const float *__restrict__ im,
                                                    const int32_t *__restrict__ rp_in,
                                                    const int32_t *__restrict__ c_in,
                                                    const int32_t *__restrict__ rp_out,
-                                                   const int32_t *__restrict__ c_out, int64_t n,
+                                                   const int32_t *__restrict__ c_out, int64_t ncap,
                                                    const float *__restrict__ g_loss,
-                                                   float *__restrict__ out) {
+                                                   float *__restrict__ out,
+                                                   const int32_t *__restrict__ dims) {
+    const int64_t n = eff_count(dims, 0, ncap);
     __shared__ float sg[kGram];
     __shared__ float srow[4][64];
     for (int i = threadIdx.x; i < kGram; i += 256) sg[i] = gram[i];
@@ -158,7 +164,11 @@ __global__ __launch_bounds__(256) void recon_bwd_k(const float *__restrict__ im,
     const float scale = *g_loss / static_cast<float>(n);
     const int64_t rows_per_blk = 32;
     const int64_t rb = xcd_remap(blockIdx.x, gridDim.x) * rows_per_blk;
-    for (int64_t v = rb + w; v < rb + rows_per_blk && v < n; v += 4) {
+    for (int64_t v = rb + w; v < rb + rows_per_blk && v < ncap; v += 4) {
+        if (v >= n) {
+            out[v * 64 + lane] = 0.f;
+            continue;
+        }
         const float iv = im[v * 64 + lane];
         srow[w][lane] = iv;
         __builtin_amdgcn_wave_barrier();
@@ -183,26 +193,26 @@ extern "C" int64_t scgib_recon_partials_floats(int64_t n_nodes) {
 
 extern "C" int scgib_recon_fwd(const float *im, const int32_t *rowptr, const int32_t *col,
                                int64_t n_nodes, int64_t n_edges, float *partials, float *gram,
-                               float *loss, scgib_stream_t stream) {
+                               float *loss, const int32_t *dims, scgib_stream_t stream) {
     if (n_nodes <= 0 || n_edges < 0) return SCGIB_EINVAL;
     if (!im || !rowptr || (n_edges > 0 && !col) || !partials || !gram || !loss) return SCGIB_EINVAL;
     const int64_t G = recon_blocks(n_nodes);
     int64_t rows = (n_nodes + G - 1) / G;
     rows += rows & 1;  // even: the MFMA consumes rows in pairs
     hipStream_t st = as_stream(stream);
-    recon_partial_k<<<dim3((unsigned)G), 256, 0, st>>>(im, rowptr, col, n_nodes, rows, partials);
-    recon_finalize_k<<<kFinBlocks, 256, 0, st>>>(partials, (int)G, n_nodes, n_edges, gram, loss);
+    recon_partial_k<<<dim3((unsigned)G), 256, 0, st>>>(im, rowptr, col, n_nodes, rows, partials, dims);
+    recon_finalize_k<<<kFinBlocks, 256, 0, st>>>(partials, (int)G, n_nodes, n_edges, gram, loss, dims);
     return launch_status();
 }
 
 extern "C" int scgib_recon_bwd(const float *im, const float *gram, const int32_t *rowptr_in,
                                const int32_t *col_in, const int32_t *rowptr_out,
                                const int32_t *col_out, int64_t n_nodes, const float *g_loss,
-                               float *grad_im, scgib_stream_t stream) {
+                               float *grad_im, const int32_t *dims, scgib_stream_t stream) {
     if (n_nodes <= 0) return SCGIB_EINVAL;
     if (!im || !gram || !rowptr_in || !rowptr_out || !g_loss || !grad_im) return SCGIB_EINVAL;
     const int64_t grid = (n_nodes + 31) / 32;
     recon_bwd_k<<<dim3((unsigned)grid), 256, 0, as_stream(stream)>>>(
-        im, gram, rowptr_in, col_in, rowptr_out, col_out, n_nodes, g_loss, grad_im);
+        im, gram, rowptr_in, col_in, rowptr_out, col_out, n_nodes, g_loss, grad_im, dims);
     return launch_status();
 }

@@ -94,6 +94,11 @@ class GraphBatch:
         # {"deg": in-degree per node (np.int64), "selfloops": per-node 0/1,
         #  "validated": edges never leave their graph}
         self.host_info = host_info
+        # capacity mode: device int32 [actual nodes, actual edges]; the host
+        # sizes above are then capacities (see StaticBatch)
+        self.dims = None
+        self.ego_caps = None  # (ego nodes cap, ego edges cap) for capacity mode
+        self.seg_dims = None  # ego batches: device count of segments (= parent nodes)
         self.ndata = _NData(self)
         self.edata = {}
 
@@ -133,6 +138,10 @@ class GraphBatch:
         return self._n
 
     number_of_nodes = num_nodes
+
+    def edge_capacity(self):
+        """Host edge count to size launches: exact, or the capacity in capacity mode."""
+        return int(self.col.shape[0]) if self.dims is not None else self.num_edges()
 
     def num_edges(self, etype=None):
         if self._e is None:  # ego batches sized by capacity: read the exact count once
@@ -190,6 +199,9 @@ class GraphBatch:
                        None if self.symmetric else mv(self.rowptr_t),
                        None if self.symmetric else mv(self.col_t), self.max_graph_nodes,
                        -1 if self._e is None else self._e, self.host_info)
+        g.dims = mv(self.dims)
+        g.ego_caps = self.ego_caps
+        g.seg_dims = mv(self.seg_dims)
         for k, v in self.ndata.items():
             dict.__setitem__(g.ndata, k, v.to(device, non_blocking=non_blocking))
         return g
@@ -352,8 +364,17 @@ def egonet_batch(g: GraphBatch, k: int, x=None):
     mgn = max(g.max_graph_nodes, 1)
     info = g.host_info
     _lib.call("scgib_egonet_count", _ptr(g.rowptr), _ptr(g.col), _ptr(g.graph_ptr), g.batch_size,
-              n, k, mgn, _ptr(ego_ptr), _ptr(ego_eptr), _ptr(ws), _ptr(err), st)
-    if k == 1 and info is not None and info["validated"] and mgn <= 512:
+              n, k, mgn, _ptr(ego_ptr), _ptr(ego_eptr), _ptr(ws), _ptr(err), _ptr(g.dims), st)
+    ego_dims = None
+    if g.dims is not None:
+        # capacity mode: outputs sized by the graph's capacities, actual sizes
+        # stay on the device (ego_dims) — nothing is read back
+        if g.ego_caps is None:
+            raise _lib.ScgibError("capacity-mode graph without ego capacities (StaticBatch)")
+        n_s, e_cap = g.ego_caps
+        e_s = -1
+        ego_dims = torch.empty(2, dtype=i32, device=dev)
+    elif k == 1 and info is not None and info["validated"] and mgn <= 512:
         # sizes known on the host, no device sync: |ball(v)| = 1 + deg(v) - selfloop(v);
         # the induced-edge count is bounded by sum_{u in ball(v)} deg(u)
         ball = 1 + info["deg"] - info["selfloops"]
@@ -372,10 +393,90 @@ def egonet_batch(g: GraphBatch, k: int, x=None):
     sub_col = torch.empty(max(e_cap, 1), dtype=i32, device=dev)
     _lib.call("scgib_egonet_fill", _ptr(g.rowptr), _ptr(g.col), _ptr(g.graph_ptr), g.batch_size, n,
               k, mgn, _ptr(ego_ptr), _ptr(ego_eptr), _ptr(ego_nodes), _ptr(sub_rowptr),
-              _ptr(sub_col), _ptr(err), st)
+              _ptr(sub_col), _ptr(err), n_s, _ptr(g.dims), _ptr(ego_dims), st)
     ego = GraphBatch(sub_rowptr, sub_col, ego_ptr, None, None, n_edges=e_s,
                      max_graph_nodes=mgn)
+    ego.dims = ego_dims
+    ego.seg_dims = g.dims  # the ego batch's segments are g's nodes
     dict.__setitem__(ego.ndata, "_ID", ego_nodes)
     if x is not None:
         dict.__setitem__(ego.ndata, "x", x.index_select(0, ego_nodes))
     return ego
+
+
+class StaticBatch:
+    """Capacity-sized device buffers of one molecule batch, for HIP-graph
+    replay of the training step: every kernel reads the actual node/edge
+    counts from ``dims`` (device), so a graph captured on these buffers
+    serves every batch of ``B`` molecules that fits the capacities.
+
+    ``load(src)`` copies a padded device batch (``pad(...)``) in with five
+    device-to-device copies; nothing is read back to the host.
+    """
+
+    def __init__(self, B, n_cap, e_cap, n_feat, max_graph_nodes, ego_caps, device):
+        i32 = torch.int32
+        self.B, self.n_cap, self.e_cap, self.n_feat = B, n_cap, e_cap, n_feat
+        self.rowptr = torch.zeros(n_cap + 1, dtype=i32, device=device)
+        self.col = torch.zeros(max(e_cap, 1), dtype=i32, device=device)
+        self.graph_ptr = torch.zeros(B + 1, dtype=i32, device=device)
+        self.dims = torch.zeros(2, dtype=i32, device=device)
+        self.x = torch.zeros(n_cap, n_feat, dtype=torch.float32, device=device)
+        self.graph = GraphBatch(self.rowptr, self.col, self.graph_ptr, None, None,
+                                max_graph_nodes=max_graph_nodes, n_edges=-1)
+        self.graph.dims = self.dims
+        self.graph.ego_caps = tuple(int(c) for c in ego_caps)
+
+    @staticmethod
+    def capacities(host_batches, k, slack=1.0):
+        """(n_cap, e_cap, max_graph_nodes, (ego nodes cap, ego edges cap)) covering
+        every host-collated batch given (k = 1 bounds)."""
+        if k != 1:
+            raise NotImplementedError("capacity mode is implemented for k = 1 ego-nets")
+        n = max(g.num_nodes() for g in host_batches)
+        e = max(g.num_edges() for g in host_batches)
+        mgn = max(g.max_graph_nodes for g in host_batches)
+        ns = es = 0
+        for g in host_batches:
+            info = g.host_info
+            ball = 1 + info["deg"] - info["selfloops"]
+            ns = max(ns, int(ball.sum()))
+            es = max(es, int((info["deg"] * ball).sum()))
+        f = lambda v: int(v * slack) + 1  # noqa: E731
+        return f(n), f(e), mgn, (f(ns), f(es))
+
+    def pad(self, g):
+        """Device copy of host batch ``g`` padded to this batch's capacities."""
+        n, e = g.num_nodes(), g.num_edges()
+        if n > self.n_cap or e > self.e_cap or g.batch_size != self.B:
+            raise _lib.ScgibError(f"batch (B={g.batch_size}, N={n}, E={e}) does not fit the "
+                                  f"capacities (B={self.B}, N={self.n_cap}, E={self.e_cap})")
+        if g.max_graph_nodes > self.graph.max_graph_nodes:
+            raise _lib.ScgibError("batch has a larger molecule than the captured bitmap width")
+        if not g.host_info["validated"]:
+            raise _lib.ScgibError("batch edges leave their molecule")
+        ball = 1 + g.host_info["deg"] - g.host_info["selfloops"]
+        ns, es = self.graph.ego_caps
+        if int(ball.sum()) > ns or int((g.host_info["deg"] * ball).sum()) > es:
+            raise _lib.ScgibError("batch's ego-nets exceed the ego capacities")
+        if self.B and g.batch_num_nodes_host().min() < 2:
+            raise ValueError("Expected more than 1 value per channel when training "
+                             "(a molecule with one atom; the reference skips those)")
+        rp = np.full(self.n_cap + 1, e, np.int32)
+        rp[: n + 1] = g.rowptr.cpu().numpy()
+        col = np.zeros(max(self.e_cap, 1), np.int32)
+        col[:e] = g.col.cpu().numpy()[:e]
+        x = np.zeros((self.n_cap, self.n_feat), np.float32)
+        x[:n] = g.ndata["x"].cpu().numpy()
+        dev = self.rowptr.device
+        return {"rowptr": torch.from_numpy(rp).to(dev), "col": torch.from_numpy(col).to(dev),
+                "graph_ptr": g.graph_ptr.to(dev), "dims": torch.tensor([n, e], dtype=torch.int32,
+                                                                       device=dev),
+                "x": torch.from_numpy(x).to(dev), "n": n, "e": e}
+
+    def load(self, padded):
+        self.rowptr.copy_(padded["rowptr"], non_blocking=True)
+        self.col.copy_(padded["col"], non_blocking=True)
+        self.graph_ptr.copy_(padded["graph_ptr"], non_blocking=True)
+        self.dims.copy_(padded["dims"], non_blocking=True)
+        self.x.copy_(padded["x"], non_blocking=True)

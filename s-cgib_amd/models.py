@@ -168,18 +168,21 @@ class _SCGIBCore(nn.Module):
         subgraphs_features = enc_owner.Encoder2(ego, x_subs)
         enc_owner.graph_features = graph_features
         enc_owner.subgraphs_features = subgraphs_features
-        sub_readout = ops.segment_sum(subgraphs_features, ego.graph_ptr, ego.batch_size)
+        sub_readout = ops.segment_sum(subgraphs_features, ego.graph_ptr, ego.batch_size,
+                                      ego.seg_dims)
         t = enc_owner.compressor[0](graph_features)
         u_gate, u_feat = self._noise(graph_features.shape[0], graph_features.device, noise)
-        im, z1, z2, kl = ops.interaction(graph_features, t, sub_readout, u_gate, u_feat,
-                                         enc_owner.compressor[1], enc_owner.compressor[3],
-                                         enc_owner.attn_layer, batch_g, enc_owner.training)
+        im, z1, z2, kl, kl_mean = ops.interaction(graph_features, t, sub_readout, u_gate, u_feat,
+                                                  enc_owner.compressor[1], enc_owner.compressor[3],
+                                                  enc_owner.attn_layer, batch_g,
+                                                  enc_owner.training)
+        enc_owner._last_kl_mean = kl_mean
         noisy = im[:, : self.hidden_dim]
         return im, kl, noisy, z2, z1
 
-    def _losses(self, batch_g, im, kl, z1, z2, mlp, batch_size):
+    def _losses(self, batch_g, im, kl_mean, z1, z2, mlp, batch_size):
         im = mlp(im)
-        kl_loss = torch.mean(kl)
+        kl_loss = kl_mean  # == torch.mean(KL_tensor) (models.py:679), computed in-kernel
         con = semi_loss(z1, z2, batch_size)
         if self.recons_type == "adj":
             rec = ops.recon_adj(im, batch_g)
@@ -235,8 +238,8 @@ class Mainmodel(_SCGIBCore):
         x_subs = self.transfer_d(x_subs)
         im, kl, noisy, z2 = self.extract_features(None, batch_g, batch_x,
                                                   flatten_batch_subgraphs, x_subs, device, noise)
-        kl_loss, con, rec = self._losses(batch_g, im, kl, self._last_z1, z2, self.MLP,
-                                         batch_size)
+        kl_loss, con, rec = self._losses(batch_g, im, self._last_kl_mean, self._last_z1, z2,
+                                         self.MLP, batch_size)
         return None, kl_loss, con, rec
 
 
@@ -302,8 +305,8 @@ class Mainmodel_continue(_SCGIBCore):
         im, kl, noisy, z2 = self.model.extract_features(None, batch_g, batch_x,
                                                         flatten_batch_subgraphs, x_subs, device,
                                                         noise)
-        kl_loss, con, rec = self._losses(batch_g, im, kl, self.model._last_z1, z2, self.MLP,
-                                         batch_size)
+        kl_loss, con, rec = self._losses(batch_g, im, self.model._last_kl_mean,
+                                         self.model._last_z1, z2, self.MLP, batch_size)
         return None, kl_loss, con, rec
 
 

@@ -15,6 +15,17 @@ from ._lib import HIDDEN, PGRAD_STRIDE, STATS_STRIDE
 
 _NULL = None
 
+# Instrumentation hook (bench.py): when set, OBSERVER(name, meta, launch) is
+# called instead of launch() for the launches routed through _launch, with
+# meta = the sizes needed to price the launch.  None in production.
+OBSERVER = None
+
+
+def _launch(name, meta, *args):
+    if OBSERVER is None:
+        return _lib.call(name, *args)
+    return OBSERVER(name, meta, lambda: _lib.call(name, *args))
+
 
 def _p(t):
     return ctypes.c_void_p(t.data_ptr()) if t is not None else _NULL
@@ -36,11 +47,11 @@ def _f32(t, name):
 # ---------------------------------------------------------------------------
 # A5: GIN aggregation
 # ---------------------------------------------------------------------------
-def _aggregate(h, rowptr, col, ope):
+def _aggregate(h, rowptr, col, ope, dims=None):
     n, d = h.shape
     out = torch.empty_like(h)
     _lib.call("scgib_gin_aggregate", _p(h), _p(rowptr), _p(col), n, d, float(ope), _p(out),
-              _stream())
+              _p(dims), _stream())
     return out
 
 
@@ -49,14 +60,14 @@ class _GinAggregate(torch.autograd.Function):
     def forward(ctx, h, graph, ope):
         h = _f32(h, "gin_aggregate")
         ctx.graph, ctx.ope = graph, ope
-        return _aggregate(h, graph.rowptr, graph.col, ope)
+        return _aggregate(h, graph.rowptr, graph.col, ope, graph.dims)
 
     @staticmethod
     def backward(ctx, g):
         g = _f32(g, "gin_aggregate.backward")
         gr = ctx.graph
         # d/dh of sum_{u->v} h_u is the aggregation over the transposed CSR
-        return _aggregate(g, gr.rowptr_t, gr.col_t, ctx.ope), None, None
+        return _aggregate(g, gr.rowptr_t, gr.col_t, ctx.ope, gr.dims), None, None
 
 
 def gin_aggregate(h, graph, one_plus_eps=1.0):
@@ -99,20 +110,22 @@ class _GinEncoder(torch.autograd.Function):
             agg = torch.empty(n, d_in, dtype=torch.float32, device=dev)
             r = torch.empty(n, HIDDEN, dtype=torch.float32, device=dev)
             z2 = torch.empty(n, HIDDEN, dtype=torch.float32, device=dev)
-            _lib.call("scgib_gin_layer_fwd", _p(h), d_in, _p(stat_prev), _p(graph.rowptr),
+            meta = {"n": n, "e": graph.edge_capacity(), "d_in": d_in}
+            _launch("scgib_gin_layer_fwd", meta, _p(h), d_in, _p(stat_prev), _p(graph.rowptr),
                       _p(graph.col), n, conv._one_plus_eps, _p(w1), _p(b1), _p(w2), _p(b2),
-                      _p(agg), _p(r), _p(z2), _p(tstats), st)
+                      _p(agg), _p(r), _p(z2), _p(tstats), _p(graph.dims), st)
             stat = torch.empty(4, HIDDEN, dtype=torch.float32, device=dev)
             track = training and bn.track_running_stats
             _lib.call("scgib_bn_finalize", _p(tstats), n, _p(gamma), _p(beta), float(bn.eps),
                       float(bn.momentum if bn.momentum is not None else 0.1), int(training),
                       _p(bn.running_mean) if (track or not training) else None,
                       _p(bn.running_var) if (track or not training) else None,
-                      _p(bn.num_batches_tracked) if track else None, _p(stat), st)
+                      _p(bn.num_batches_tracked) if track else None, _p(stat),
+                      _p(graph.dims), st)
             saved += [agg, r, z2, stat]
             h, stat_prev = z2, stat
         out = torch.empty(n, HIDDEN, dtype=torch.float32, device=dev)
-        _lib.call("scgib_bn_relu_apply", _p(h), _p(stat_prev), n, _p(out), st)
+        _lib.call("scgib_bn_relu_apply", _p(h), _p(stat_prev), n, _p(out), _p(graph.dims), st)
         ctx.save_for_backward(*saved, *params)
         ctx.graph, ctx.L, ctx.training = graph, L, training
         ctx.opes = [c._one_plus_eps for c in gin.ginlayers]
@@ -138,22 +151,24 @@ class _GinEncoder(torch.autograd.Function):
             dy = torch.empty(n, HIDDEN, dtype=torch.float32, device=dev)
             if dagg_next is None:
                 _lib.call("scgib_gin_bwd_stats", _p(g_out), None, None, 1.0, _p(z2), _p(stat), n,
-                          _p(dy), _p(tstats), st)
+                          _p(dy), _p(tstats), _p(gr.dims), st)
             else:
                 _lib.call("scgib_gin_bwd_stats", _p(dagg_next), _p(gr.rowptr_t), _p(gr.col_t),
-                          ctx.opes[l + 1], _p(z2), _p(stat), n, _p(dy), _p(tstats), st)
+                          ctx.opes[l + 1], _p(z2), _p(stat), n, _p(dy), _p(tstats), _p(gr.dims),
+                          st)
             bn_g = torch.empty(2, HIDDEN, dtype=torch.float32, device=dev)  # dgamma, dbeta
             coef = torch.empty(2, HIDDEN, dtype=torch.float32, device=dev)
             _lib.call("scgib_bn_bwd_finalize", _p(tstats), n, int(ctx.training), _p(bn_g[0]),
-                      _p(bn_g[1]), _p(coef), st)
+                      _p(bn_g[1]), _p(coef), _p(gr.dims), st)
             dagg = torch.empty(n, d_in, dtype=torch.float32, device=dev)
             slab = torch.empty(int(_lib.query("scgib_gin_slab_floats", n, d_in)),
                                dtype=torch.float32, device=dev)
             wgrad = torch.empty(HIDDEN * HIDDEN + HIDDEN * d_in + 2 * HIDDEN,
                                 dtype=torch.float32, device=dev)
-            _lib.call("scgib_gin_layer_bwd", _p(dy), _p(z2), _p(r), _p(agg), d_in, _p(stat),
+            meta = {"n": n, "e": gr.edge_capacity(), "d_in": d_in}
+            _launch("scgib_gin_layer_bwd", meta, _p(dy), _p(z2), _p(r), _p(agg), d_in, _p(stat),
                       _p(coef), _p(_f32(w1, "w1")), _p(_f32(w2, "w2")), n, _p(dagg), _p(slab),
-                      _p(wgrad), st)
+                      _p(wgrad), _p(gr.dims), st)
             o = HIDDEN * HIDDEN
             grads[6 * l + 2] = wgrad[:o].view(HIDDEN, HIDDEN)
             grads[6 * l + 0] = wgrad[o:o + HIDDEN * d_in].view(HIDDEN, d_in)
@@ -164,7 +179,7 @@ class _GinEncoder(torch.autograd.Function):
             grads[6 * l + 5] = bn_g[1]
             dagg_next = dagg
         # d h0 = (1+eps_0) d(agg_0) + sum over out-edges (transposed aggregation)
-        dh0 = _aggregate(dagg_next, gr.rowptr_t, gr.col_t, ctx.opes[0])
+        dh0 = _aggregate(dagg_next, gr.rowptr_t, gr.col_t, ctx.opes[0], gr.dims)
         return (dh0, None, None, None, *grads)
 
 
@@ -180,11 +195,12 @@ def gin_encoder(h, graph, gin):
 # ---------------------------------------------------------------------------
 class _SegmentSum(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, ptr, nseg):
+    def forward(ctx, x, ptr, nseg, dims):
         x = _f32(x, "segment_sum")
         out = torch.empty(nseg, x.shape[1], dtype=torch.float32, device=x.device)
-        _lib.call("scgib_segment_sum", _p(x), _p(ptr), nseg, x.shape[1], _p(out), _stream())
-        ctx.ptr, ctx.nrows = ptr, x.shape[0]
+        _lib.call("scgib_segment_sum", _p(x), _p(ptr), nseg, x.shape[1], _p(out), _p(dims),
+                  _stream())
+        ctx.ptr, ctx.nrows, ctx.dims = ptr, x.shape[0], dims
         return out
 
     @staticmethod
@@ -192,12 +208,14 @@ class _SegmentSum(torch.autograd.Function):
         g = _f32(g, "segment_sum.backward")
         out = torch.empty(ctx.nrows, g.shape[1], dtype=torch.float32, device=g.device)
         _lib.call("scgib_segment_broadcast", _p(g), _p(ctx.ptr), g.shape[0], g.shape[1],
-                  _p(out), _stream())
-        return out, None, None
+                  _p(out), ctx.nrows, _p(ctx.dims), _stream())
+        return out, None, None, None
 
 
-def segment_sum(x, ptr, nseg):
-    return _SegmentSum.apply(x, ptr, int(nseg))
+def segment_sum(x, ptr, nseg, dims=None):
+    """out[s] = sum of rows [ptr[s], ptr[s+1]) (dgl.sum_nodes); ``dims`` (device,
+    capacity mode) holds the actual segment count."""
+    return _SegmentSum.apply(x, ptr, int(nseg), dims)
 
 
 def sum_nodes_graph(graph, x):
@@ -219,11 +237,14 @@ class _Interaction(torch.autograd.Function):
         if d != HIDDEN:
             raise _lib.ScgibError(f"interaction kernels are built for hidden={HIDDEN}, got {d}")
         B = graph.batch_size
-        counts = graph.batch_num_nodes_host()
-        if training and B and counts.min() < 2:
-            # nn.BatchNorm1d raises on a 1-row batch in train mode (models.py:642)
-            raise ValueError("Expected more than 1 value per channel when training "
-                             "(a graph with a single node in the per-graph compressor BN)")
+        pad = graph.dims is not None  # capacity mode: n is the row capacity
+        if not pad:
+            counts = graph.batch_num_nodes_host()
+            if training and B and counts.min() < 2:
+                # nn.BatchNorm1d raises on a 1-row batch in train mode (models.py:642)
+                raise ValueError("Expected more than 1 value per channel when training "
+                                 "(a graph with a single node in the per-graph compressor BN)")
+            n_last = int(counts[-1]) if B else 0
         dev = f.device
         im = torch.empty(n, 2 * HIDDEN, dtype=torch.float32, device=dev)
         z1 = torch.empty(B, HIDDEN, dtype=torch.float32, device=dev)
@@ -231,8 +252,8 @@ class _Interaction(torch.autograd.Function):
         lam = torch.empty(n, dtype=torch.float32, device=dev)
         logit = torch.empty(n, dtype=torch.float32, device=dev)
         stats = torch.empty(max(B, 1), STATS_STRIDE, dtype=torch.float32, device=dev)
-        n_last = int(counts[-1]) if B else 0
-        kl = torch.empty(2 * n_last, HIDDEN, dtype=torch.float32, device=dev)
+        kl = None if pad else torch.empty(2 * n_last, HIDDEN, dtype=torch.float32, device=dev)
+        kl_mean = torch.empty((), dtype=torch.float32, device=dev)
         gamma, beta = _f32(gamma, "bn.weight"), _f32(beta, "bn.bias")
         w2, b2 = _f32(w2, "w2"), _f32(b2, "b2")
         w_att, b_att = _f32(w_att, "w_att"), _f32(b_att, "b_att")
@@ -241,19 +262,22 @@ class _Interaction(torch.autograd.Function):
         _lib.call("scgib_interaction_fwd", _p(f), _p(t), _p(s), _p(u_gate), _p(u_feat),
                   _p(graph.graph_ptr), B, n, _p(gamma), _p(beta), _p(rm), _p(rv), float(bn.eps),
                   int(training), _p(w2), _p(b2), _p(w_att), _p(b_att), _p(im), _p(z1), _p(z2),
-                  _p(lam), _p(logit), _p(stats), _p(kl), st)
+                  _p(lam), _p(logit), _p(stats), _p(kl), _p(kl_mean), int(pad), st)
         if training and bn.track_running_stats:
             nbt = bn.num_batches_tracked
             _lib.call("scgib_bn_running_update", _p(stats), _p(graph.graph_ptr), B,
                       float(bn.momentum), _p(rm), _p(rv), _p(nbt), st)
         ctx.save_for_backward(f, t, s, u_feat, gamma, beta, w2, w_att, z1, lam, logit, stats)
-        ctx.graph, ctx.training = graph, training
+        ctx.graph, ctx.training, ctx.pad = graph, training, pad
+        ctx.n_last = None if pad else n_last
         ctx.bn_eps = float(bn.eps)
         ctx.rm, ctx.rv = (None, None) if training else (rm.clone(), rv.clone())
-        return im, z1, z2, kl
+        if kl is None:
+            kl = torch.zeros(0, HIDDEN, dtype=torch.float32, device=dev)
+        return im, z1, z2, kl, kl_mean
 
     @staticmethod
-    def backward(ctx, g_im, g_z1, g_z2, g_kl):
+    def backward(ctx, g_im, g_z1, g_z2, g_kl, g_klmean):
         f, t, s, u_feat, gamma, beta, w2, w_att, z1, lam, logit, stats = ctx.saved_tensors
         n = f.shape[0]
         B = ctx.graph.batch_size
@@ -262,7 +286,15 @@ class _Interaction(torch.autograd.Function):
         g_im = zeros(n, 2 * HIDDEN) if g_im is None else _f32(g_im, "g_im")
         g_z1 = zeros(B, HIDDEN) if g_z1 is None else _f32(g_z1, "g_z1")
         g_z2 = zeros(B, HIDDEN) if g_z2 is None else _f32(g_z2, "g_z2")
-        g_kl = None if g_kl is None else _f32(g_kl, "g_kl")
+        if g_kl is not None and g_kl.numel() == 0:
+            g_kl = None
+        if g_kl is not None:
+            g_kl = _f32(g_kl, "g_kl")
+            if g_klmean is not None:  # fold the mean's gradient into the tensor's
+                g_kl = g_kl + g_klmean / (2 * ctx.n_last * HIDDEN)
+                g_klmean = None
+        if g_klmean is not None:
+            g_klmean = _f32(g_klmean.reshape(1), "g_klmean")
         df = torch.empty_like(f)
         dt = torch.empty_like(t)
         ds = torch.empty_like(s)
@@ -271,7 +303,7 @@ class _Interaction(torch.autograd.Function):
                   _p(s), _p(u_feat), _p(ctx.graph.graph_ptr), B, n, _p(gamma), _p(beta),
                   _p(ctx.rm), _p(ctx.rv), ctx.bn_eps, int(ctx.training), _p(w2), _p(w_att),
                   _p(z1), _p(lam), _p(logit), _p(stats), _p(df), _p(dt), _p(ds), _p(pgrad),
-                  _stream())
+                  _p(g_klmean), int(ctx.pad), _stream())
         pg = pgrad[:B].sum(0)
         dw2 = pg[0:64].view(1, 64)
         db2 = pg[64:65]
@@ -289,7 +321,8 @@ def interaction(f, t, s, u_gate, u_feat, bn, lin2, attn, graph, training):
     place in train mode, once per graph), ``lin2`` the compressor's
     Linear(64, 1), ``attn`` the attn_layer Linear(128, 1).
     Returns (interaction_map [N,128], z1 = sum_nodes(noisy) [B,64],
-    z2 = sum_nodes(f) [B,64], kl_tensor [2 n_last, 64]).
+    z2 = sum_nodes(f) [B,64], kl_tensor [2 n_last, 64] (empty in capacity
+    mode), kl_mean = mean(kl_tensor) [scalar]).
     """
     return _Interaction.apply(f, t, s, u_gate, u_feat, bn.weight, bn.bias, lin2.weight,
                               lin2.bias, attn.weight, attn.bias, graph, bn, bool(training))
@@ -311,7 +344,8 @@ class _ReconAdj(torch.autograd.Function):
         gram = torch.empty(HIDDEN * HIDDEN, dtype=torch.float32, device=dev)
         loss = torch.empty((), dtype=torch.float32, device=dev)
         _lib.call("scgib_recon_fwd", _p(im), _p(graph.rowptr), _p(graph.col), n,
-                  graph.num_edges(), _p(partials), _p(gram), _p(loss), _stream())
+                  graph.edge_capacity(), _p(partials), _p(gram), _p(loss), _p(graph.dims),
+                  _stream())
         ctx.save_for_backward(im, gram)
         ctx.graph = graph
         return loss
@@ -323,7 +357,7 @@ class _ReconAdj(torch.autograd.Function):
         g_loss = _f32(g_loss.reshape(1), "g_loss")
         out = torch.empty_like(im)
         _lib.call("scgib_recon_bwd", _p(im), _p(gram), _p(gr.rowptr), _p(gr.col), _p(gr.rowptr_t),
-                  _p(gr.col_t), im.shape[0], _p(g_loss), _p(out), _stream())
+                  _p(gr.col_t), im.shape[0], _p(g_loss), _p(out), _p(gr.dims), _stream())
         return out, None
 
 

@@ -1,0 +1,157 @@
+"""Capacity mode and whole-step HIP-graph replay.
+
+A ``graph.StaticBatch`` holds capacity-sized buffers; every kernel reads the
+batch's actual node / edge counts from the device (``dims``), so one captured
+step serves every batch that fits.  The bar: the same pretrain step (ego-net
+build, both GIN encoders, interaction, losses, backward) on the same batch and
+noise gives the exact-mode losses, gradients and BN running statistics —
+eager on the static buffers, and replayed from a captured graph over several
+different batches.  Exact mode itself is pinned to the reference goldens by
+test_gpu_parity.py; the two modes differ only in grid sizes, hence in fp32
+reduction grouping, and fp32 ReLU-kink flips are tolerated as there.
+"""
+import copy
+from types import SimpleNamespace
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+from conftest import check_grads_model, rel_err
+
+pytestmark = pytest.mark.gpu
+
+B = 48
+F_IN = 11
+LOSS_TOL = 2e-5
+
+
+@pytest.fixture(scope="module")
+def dev():
+    if not torch.cuda.is_available():
+        pytest.skip("needs a GPU")
+    return torch.device("cuda", 0)
+
+
+def _model(pkg, dev, layers=5):
+    args = SimpleNamespace(recons_type="adj", useAtt=1, readout_f="sum", d_transfer=32,
+                           batch_size=B, gin_layers=layers)
+    torch.manual_seed(11)
+    m = pkg.models.Mainmodel(args, F_IN, 64, 4, 4, 1, "GIN").to(dev).train()
+    with torch.no_grad():  # non-trivial BN affine so the BN paths are exercised
+        for enc in (m.Encoder1, m.Encoder2):
+            for bn in enc.batch_norms:
+                bn.weight.add_(0.2 * torch.randn(64, device=dev))
+                bn.bias.add_(0.2 * torch.randn(64, device=dev))
+    return m
+
+
+def _batches(pkg, seeds):
+    out = []
+    for s in seeds:
+        gh, _ = pkg.graph.collate_pyg(pkg.synth.molecules(B, "qm9", seed=s))
+        dict.__setitem__(gh.ndata, "x", F.normalize(gh.ndata["x"].float()))
+        out.append(gh)
+    return out
+
+
+def _step(model, g, x, noise, dev):
+    model.zero_grad(set_to_none=True)
+    _, kl, con, rec = model(g, x, None, None, None, 1, None, 1, dev, B, noise=noise)
+    loss = kl + rec + con
+    loss.backward()
+    return torch.stack([kl, con, rec, loss]).detach()
+
+
+def _compare(exact_model, cap_model, exact_losses, cap_losses):
+    for a, b in zip(exact_losses.tolist(), cap_losses.tolist()):
+        assert rel_err(b, a) < LOSS_TOL, (a, b)
+    ref = {k: p.grad.detach().double().cpu() for k, p in exact_model.named_parameters()
+           if p.grad is not None}
+    mine = dict(cap_model.named_parameters())
+    check_grads_model(ref, lambda n: mine[n].grad, tol=1e-3)
+    bufs = dict(cap_model.named_buffers())
+    for k, v in exact_model.named_buffers():
+        if "running" in k:
+            assert rel_err(bufs[k].cpu(), v.cpu()) < 1e-5, k
+        elif "num_batches" in k:
+            assert int(bufs[k]) == int(v), k
+
+
+def _noise(n_cap, dev, seed):
+    gen = torch.Generator(device=dev).manual_seed(seed)
+    return (torch.rand(n_cap, device=dev, generator=gen),
+            torch.rand(n_cap, 64, device=dev, generator=gen))
+
+
+def test_capacity_mode_eager_matches_exact(pkg, dev):
+    hosts = _batches(pkg, (1, 2, 3))
+    n_cap, e_cap, mgn, caps = pkg.graph.StaticBatch.capacities(hosts, 1, slack=1.05)
+    static = pkg.graph.StaticBatch(B, n_cap, e_cap, F_IN, mgn, caps, dev)
+    exact_m = _model(pkg, dev)
+    cap_m = copy.deepcopy(exact_m)
+    for i, gh in enumerate(hosts):
+        n = gh.num_nodes()
+        ug, uf = _noise(n_cap, dev, 100 + i)
+        g = gh.to(dev)
+        le = _step(exact_m, g, g.ndata["x"], (ug[:n], uf[:n]), dev)
+        static.load(static.pad(gh))
+        lc = _step(cap_m, static.graph, static.x, (ug, uf), dev)
+        torch.cuda.synchronize()
+        _compare(exact_m, cap_m, le, lc)
+
+
+def test_graph_replay_matches_exact_over_batches(pkg, dev):
+    hosts = _batches(pkg, (4, 5, 6, 7))
+    n_cap, e_cap, mgn, caps = pkg.graph.StaticBatch.capacities(hosts, 1, slack=1.02)
+    static = pkg.graph.StaticBatch(B, n_cap, e_cap, F_IN, mgn, caps, dev)
+    padded = [static.pad(gh) for gh in hosts]
+    exact_m = _model(pkg, dev)
+    cap_m = copy.deepcopy(exact_m)
+    s_ug = torch.zeros(n_cap, device=dev)
+    s_uf = torch.zeros(n_cap, 64, device=dev)
+
+    # warm-up on a side stream (allocator), then capture one step
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    snap = copy.deepcopy(cap_m.state_dict())
+    with torch.cuda.stream(side):
+        static.load(padded[0])
+        _step(cap_m, static.graph, static.x, (s_ug, s_uf), dev)
+    torch.cuda.current_stream().wait_stream(side)
+    cap_m.load_state_dict(snap)  # undo the warm-up's BN running updates
+    cap_m.zero_grad(set_to_none=True)
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        _, kl, con, rec = cap_m(static.graph, static.x, None, None, None, 1, None, 1, dev, B,
+                                noise=(s_ug, s_uf))
+        loss = kl + rec + con
+        loss.backward()
+        static_losses = torch.stack([kl, con, rec, loss]).detach()
+
+    for i in (0, 1, 2, 3, 1):  # includes a batch seen before (replay is stateless)
+        gh = hosts[i]
+        n = gh.num_nodes()
+        ug, uf = _noise(n_cap, dev, 200 + i)
+        g = gh.to(dev)
+        le = _step(exact_m, g, g.ndata["x"], (ug[:n], uf[:n]), dev)
+        s_ug.copy_(ug)
+        s_uf.copy_(uf)
+        static.load(padded[i])
+        graph.replay()
+        torch.cuda.synchronize()
+        _compare(exact_m, cap_m, le, static_losses.clone())
+
+
+def test_static_batch_rejects_oversized(pkg, dev):
+    small, big = _batches(pkg, (8,)), None
+    n_cap, e_cap, mgn, caps = pkg.graph.StaticBatch.capacities(small, 1)
+    static = pkg.graph.StaticBatch(B, n_cap, e_cap, F_IN, mgn, caps, dev)
+    for seed in range(9, 40):
+        cand = _batches(pkg, (seed,))[0]
+        if cand.num_nodes() > n_cap or cand.num_edges() > e_cap:
+            big = cand
+            break
+    assert big is not None
+    with pytest.raises(pkg._lib.ScgibError):
+        static.pad(big)

@@ -211,19 +211,22 @@ def test_interaction_fwd_bwd(pkg, dev, training):
     fd = f.to(dev).requires_grad_(True)
     sd = s.to(dev).requires_grad_(True)
     t = comp_d[0](fd)
-    im, z1, z2, kl = pkg.ops.interaction(fd, t, sd, u_gate.to(dev), u_feat.to(dev), comp_d[1],
-                                         comp_d[3], attn_d, g, training)
-    for a, b, nm in ((im, im_r, "im"), (z1, z1_r, "z1"), (z2, z2_r, "z2"), (kl, kl_r, "kl")):
+    im, z1, z2, kl, kl_mean = pkg.ops.interaction(fd, t, sd, u_gate.to(dev), u_feat.to(dev),
+                                                  comp_d[1], comp_d[3], attn_d, g, training)
+    for a, b, nm in ((im, im_r, "im"), (z1, z1_r, "z1"), (z2, z2_r, "z2"), (kl, kl_r, "kl"),
+                     (kl_mean, kl_r.mean(), "kl_mean")):
         assert rel_err(a.detach().cpu(), b.detach()) < ACT_TOL, nm
     if training:
         for k in ("running_mean", "running_var"):
             assert rel_err(getattr(comp_d[1], k).cpu(), bn_state["compressor.1." + k]) < 1e-5
         assert int(comp_d[1].num_batches_tracked) == B
     # backward through a random linear functional of every output
-    ws = [torch.randn_like(x) for x in (im_r, z1_r, z2_r, kl_r)]
-    lr = sum((w * x).sum() for w, x in zip(ws, (im_r, z1_r, z2_r, kl_r)))
+    # (kl and its in-kernel mean both carry gradient: exercises the fold in
+    # _Interaction.backward)
+    ws = [torch.randn_like(x) for x in (im_r, z1_r, z2_r, kl_r, kl_r.mean())]
+    lr = sum((w * x).sum() for w, x in zip(ws, (im_r, z1_r, z2_r, kl_r, kl_r.mean())))
     lr.backward()
-    ld = sum((w.to(dev) * x).sum() for w, x in zip(ws, (im, z1, z2, kl)))
+    ld = sum((w.to(dev) * x).sum() for w, x in zip(ws, (im, z1, z2, kl, kl_mean)))
     ld.backward()
     assert rel_l2(fd.grad.cpu(), fo.grad) < GRAD_TOL
     assert rel_l2(sd.grad.cpu(), so.grad) < GRAD_TOL

@@ -30,20 +30,22 @@ def test_library_exports_every_header_symbol(pkg):
         assert hasattr(lib, s), s
     assert set(syms) == set(lib_mod.SIGNATURES), "ctypes signature table out of sync"
     loaded = lib_mod.load()
-    assert loaded.scgib_abi_version() == 1
+    assert loaded.scgib_abi_version() == lib_mod.ABI_VERSION
     assert loaded.scgib_strerror(-1).decode().startswith("invalid")
 
 
 def test_argument_errors_do_not_launch(pkg):
     lib = pkg._lib.load()
     # negative / invalid sizes and null pointers are rejected before any launch
-    assert lib.scgib_gin_aggregate(None, None, None, -1, 64, 1.0, None, None) == -1
-    assert lib.scgib_gin_aggregate(None, None, None, 10, 63, 1.0, None, None) == -1
-    assert lib.scgib_gin_aggregate(None, None, None, 0, 64, 1.0, None, None) == 0
-    assert lib.scgib_segment_sum(None, None, 5, 64, None, None) == -1
+    assert lib.scgib_gin_aggregate(None, None, None, -1, 64, 1.0, None, None, None) == -1
+    assert lib.scgib_gin_aggregate(None, None, None, 10, 63, 1.0, None, None, None) == -1
+    assert lib.scgib_gin_aggregate(None, None, None, 0, 64, 1.0, None, None, None) == 0
+    assert lib.scgib_segment_sum(None, None, 5, 64, None, None, None) == -1
     assert lib.scgib_egonet_count(None, None, None, 1, 10, 1, 1000, None, None, None, None,
-                                  None) == -1
-    assert lib.scgib_recon_fwd(None, None, None, 0, 0, None, None, None, None) == -1
+                                  None, None) == -1
+    assert lib.scgib_recon_fwd(None, None, None, 0, 0, None, None, None, None, None) == -1
+    assert lib.scgib_gin_layer_fwd(None, 48, None, None, None, 10, 1.0, None, None, None, None,
+                                   None, None, None, None, None, None) == -1
     assert lib.scgib_egonet_workspace_bytes(1000) >= 8
     assert lib.scgib_recon_partials_floats(9000) > 36 * 4096
 
@@ -179,3 +181,35 @@ def test_dgl_dropin_khop_and_ingest(pkg):
             np.testing.assert_array_equal(np.concatenate(nodes), d[f"m{i}_k{k}_nodes"])
             np.testing.assert_array_equal(np.concatenate(es), d[f"m{i}_k{k}_esrc"])
             np.testing.assert_array_equal(np.concatenate(ed), d[f"m{i}_k{k}_edst"])
+
+
+def _header_prototypes():
+    """{name: [param kind]} from include/scgib.h; kind in P (pointer), I64, I32, F."""
+    src = open(os.path.join(ROOT, "include", "scgib.h")).read()
+    src = re.sub(r"/\*.*?\*/|//[^\n]*", "", src, flags=re.S)
+    out = {}
+    for m in re.finditer(r"(?:int|int64_t|const char \*)\s*(scgib_\w+)\(([^)]*)\)\s*;", src):
+        params = [p.strip() for p in m.group(2).split(",") if p.strip() not in ("", "void")]
+        kinds = []
+        for p in params:
+            if "*" in p or p.startswith("scgib_stream_t"):
+                kinds.append("P")
+            elif p.startswith("int64_t"):
+                kinds.append("I64")
+            elif p.startswith("int32_t") or p.startswith("int "):
+                kinds.append("I32")
+            elif p.startswith("float"):
+                kinds.append("F")
+            else:
+                raise AssertionError(f"unparsed parameter {p!r} of {m.group(1)}")
+        out[m.group(1)] = kinds
+    return out
+
+
+def test_ctypes_table_matches_header_prototypes(pkg):
+    L = pkg._lib
+    kind = {L._P: "P", L._I64: "I64", L._I32: "I32", L._F: "F"}
+    protos = _header_prototypes()
+    assert set(protos) == set(L.SIGNATURES)
+    for name, (_, argtypes) in L.SIGNATURES.items():
+        assert [kind[t] for t in argtypes] == protos[name], name

@@ -229,7 +229,7 @@ def main():
     reducer = pkg.dist.GradAllReducer(model.parameters())
 
     if a.eager:
-        opt = torch.optim.Adam(model.parameters(), lr=1e-4, weight_decay=5e-5)
+        opt = torch.optim.Adam(model.parameters(), lr=1e-4, weight_decay=5e-5, fused=True)
 
         def step(i):
             g = pool[i % len(pool)]
@@ -245,7 +245,8 @@ def main():
         # backward[, Adam]) on static buffers; each step copies the next batch
         # in (5 device-to-device copies) and replays.  Every kernel reads the
         # batch's actual sizes from the device.
-        opt = torch.optim.Adam(model.parameters(), lr=1e-4, weight_decay=5e-5, capturable=True)
+        opt = torch.optim.Adam(model.parameters(), lr=1e-4, weight_decay=5e-5, capturable=True,
+                               fused=True)
         n_cap, e_cap, mgn, ego_caps = pkg.graph.StaticBatch.capacities(pool_host, a.k, slack=1.02)
         static = pkg.graph.StaticBatch(a.batch, n_cap, e_cap, F_in, mgn, ego_caps, dev)
         padded = []

@@ -222,6 +222,24 @@ int scgib_recon_bwd(const float *im, const float *gram, const int32_t *rowptr_in
                     int64_t n_nodes, const float *g_loss, float *grad_im,
                     const int32_t *dims, scgib_stream_t stream);
 
+/* ---- A11: contrastive loss (batched_semi_loss, tau = 1) --------------------
+ * models.py:606-629 (sim :606-609, semi_loss :611-616, batched :618-629;
+ * called at models.py:695 with z1 = sum_nodes(noisy), z2 = graph readout).
+ * loss = mean_i -log(exp(z1n_i.z2n_i) / (sum_j exp(z1n_i.z1n_j)
+ *        + sum_j exp(z1n_i.z2n_j) - exp(z1n_i.z1n_i))),  zn = F.normalize(z).
+ * The value is independent of the reference's chunk size.  z1, z2: [B][64].
+ * `workspace` holds scgib_contrastive_workspace_floats(B) floats and must be
+ * passed unchanged from forward to backward.  `counters` holds
+ * scgib_contrastive_counters(B) uint32 that are zero on entry; both launches
+ * leave them zero (graph-replay safe).  loss and g_loss are device scalars. */
+int64_t scgib_contrastive_workspace_floats(int64_t n_graphs);
+int64_t scgib_contrastive_counters(int64_t n_graphs);
+int scgib_contrastive_fwd(const float *z1, const float *z2, int64_t n_graphs, float *workspace,
+                          float *loss, uint32_t *counters, scgib_stream_t stream);
+int scgib_contrastive_bwd(const float *z1, const float *z2, int64_t n_graphs, float *workspace,
+                          const float *g_loss, float *dz1, float *dz2, uint32_t *counters,
+                          scgib_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

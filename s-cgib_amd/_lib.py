@@ -33,6 +33,10 @@ SIGNATURES = {
     "scgib_interaction_bwd": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _I64, _I64, _P,
                                              _P, _P, _P, _F, _I32, _P, _P, _P, _P, _P, _P, _P,
                                              _P, _P, _P, _P, _I32, _P]),
+    "scgib_contrastive_workspace_floats": (_I64, [_I64]),
+    "scgib_contrastive_counters": (_I64, [_I64]),
+    "scgib_contrastive_fwd": (ctypes.c_int, [_P, _P, _I64, _P, _P, _P, _P]),
+    "scgib_contrastive_bwd": (ctypes.c_int, [_P, _P, _I64, _P, _P, _P, _P, _P, _P]),
     "scgib_gin_tiles": (_I64, [_I64]),
     "scgib_gin_slab_floats": (_I64, [_I64, _I32]),
     "scgib_gin_layer_fwd": (ctypes.c_int, [_P, _I32, _P, _P, _P, _I64, _F, _P, _P, _P, _P, _P, _P,

@@ -130,17 +130,26 @@ class Set2Set(nn.Module):
         return q_star
 
 
+_SIDE_STREAMS = {}
+
+
+def _side_stream(device):
+    """The second HIP stream of ``device`` used by the forked encoder branch."""
+    key = torch.device(device).index
+    if key not in _SIDE_STREAMS:
+        _SIDE_STREAMS[key] = torch.cuda.Stream(device)
+    return _SIDE_STREAMS[key]
+
+
 def _gin_layers(args):
     return int(getattr(args, "gin_layers", 5))
 
 
 def semi_loss(z1, z2, chunk):
-    """batched_semi_loss, tau = 1 (models.py:606-629).  The per-row value does
-    not depend on the chunking, so the B x B similarities are formed at once."""
-    z1n, z2n = F.normalize(z1), F.normalize(z2)
-    refl = torch.exp(z1n @ z1n.t())
-    betw = torch.exp(z1n @ z2n.t())
-    return (-torch.log(betw.diagonal() / (refl.sum(1) + betw.sum(1) - refl.diagonal()))).mean()
+    """batched_semi_loss, tau = 1 (models.py:606-629), fused on the device
+    (scgib_contrastive_*).  The per-row value does not depend on the
+    chunking."""
+    return ops.contrastive(z1, z2)
 
 
 class _SCGIBCore(nn.Module):
@@ -161,15 +170,20 @@ class _SCGIBCore(nn.Module):
         return (torch.rand(n, device=device, dtype=torch.float32),
                 torch.rand(n, self.hidden_dim, device=device, dtype=torch.float32))
 
-    def _extract(self, enc_owner, batch_g, batch_x, ego, x_subs, noise):
+    def _extract(self, enc_owner, batch_g, batch_x, ego, x_subs, noise, encoded=None):
         """extract_features of ``enc_owner`` (models.py:702-750); returns the
-        reference's 4-tuple plus z1 = sum_nodes(noisy) (computed in-kernel)."""
-        graph_features = enc_owner.Encoder1(batch_g, batch_x)
-        subgraphs_features = enc_owner.Encoder2(ego, x_subs)
+        reference's 4-tuple plus z1 = sum_nodes(noisy) (computed in-kernel).
+        ``encoded`` = (graph_features, subgraphs_features, sub_readout) when the
+        encoders already ran (_encode_forked)."""
+        if encoded is None:
+            graph_features = enc_owner.Encoder1(batch_g, batch_x)
+            subgraphs_features = enc_owner.Encoder2(ego, x_subs)
+            sub_readout = ops.segment_sum(subgraphs_features, ego.graph_ptr, ego.batch_size,
+                                          ego.seg_dims)
+        else:
+            graph_features, subgraphs_features, sub_readout = encoded
         enc_owner.graph_features = graph_features
         enc_owner.subgraphs_features = subgraphs_features
-        sub_readout = ops.segment_sum(subgraphs_features, ego.graph_ptr, ego.batch_size,
-                                      ego.seg_dims)
         t = enc_owner.compressor[0](graph_features)
         u_gate, u_feat = self._noise(graph_features.shape[0], graph_features.device, noise)
         im, z1, z2, kl, kl_mean = ops.interaction(graph_features, t, sub_readout, u_gate, u_feat,
@@ -179,6 +193,29 @@ class _SCGIBCore(nn.Module):
         enc_owner._last_kl_mean = kl_mean
         noisy = im[:, : self.hidden_dim]
         return im, kl, noisy, z2, z1
+
+    def _encode_forked(self, enc_owner, batch_g, batch_x):
+        """Fast path of forward() when the ego-nets are built on the device:
+        the ego branch (ego-net build, x_subs gather, transfer_d, Encoder2,
+        readout) runs on a second HIP stream, concurrently with Encoder1 on the
+        current one (Encoder1's ~N/64 tiles leave most of the 256 CUs idle).
+        Captured into a HIP graph this is a fork/join; autograd runs each
+        branch's backward on the stream its forward ran on, so the two
+        encoders' backward chains overlap as well."""
+        main = torch.cuda.current_stream(batch_x.device)
+        side = _side_stream(batch_x.device)
+        side.wait_stream(main)
+        batch_x.record_stream(side)
+        with torch.cuda.stream(side):
+            ego, x_subs = self._prepare_ego(batch_g, None, batch_x, None)
+            subgraphs_features = enc_owner.Encoder2(ego, self.transfer_d(x_subs))
+            sub_readout = ops.segment_sum(subgraphs_features, ego.graph_ptr, ego.batch_size,
+                                          ego.seg_dims)
+        graph_features = enc_owner.Encoder1(batch_g, self.transfer_d(batch_x))
+        main.wait_stream(side)
+        subgraphs_features.record_stream(main)
+        sub_readout.record_stream(main)
+        return ego, (graph_features, subgraphs_features, sub_readout)
 
     def _losses(self, batch_g, im, kl_mean, z1, z2, mlp, batch_size):
         im = mlp(im)
@@ -232,12 +269,19 @@ class Mainmodel(_SCGIBCore):
                 current_epoch=None, edge_index=None, k_transition=None, device=None,
                 batch_size=16, noise=None):
         self.batch_size = batch_size
-        if flatten_batch_subgraphs is None:
-            flatten_batch_subgraphs, x_subs = self._prepare_ego(batch_g, None, batch_x, x_subs)
-        batch_x = self.transfer_d(batch_x)
-        x_subs = self.transfer_d(x_subs)
-        im, kl, noisy, z2 = self.extract_features(None, batch_g, batch_x,
-                                                  flatten_batch_subgraphs, x_subs, device, noise)
+        if flatten_batch_subgraphs is None and x_subs is None and batch_x.is_cuda:
+            ego, enc = self._encode_forked(self, batch_g, batch_x)
+            im, _, _, z2, z1 = self._extract(self, batch_g, None, ego, None, noise, enc)
+            self._last_z1 = z1
+        else:
+            if flatten_batch_subgraphs is None:
+                flatten_batch_subgraphs, x_subs = self._prepare_ego(batch_g, None, batch_x,
+                                                                    x_subs)
+            batch_x = self.transfer_d(batch_x)
+            x_subs = self.transfer_d(x_subs)
+            im, kl, noisy, z2 = self.extract_features(None, batch_g, batch_x,
+                                                      flatten_batch_subgraphs, x_subs, device,
+                                                      noise)
         kl_loss, con, rec = self._losses(batch_g, im, self._last_kl_mean, self._last_z1, z2,
                                          self.MLP, batch_size)
         return None, kl_loss, con, rec
@@ -298,13 +342,21 @@ class Mainmodel_continue(_SCGIBCore):
                 current_epoch=None, edge_index=None, k_transition=None, device=None,
                 batch_size=16, noise=None):
         self.batch_size = batch_size
-        if flatten_batch_subgraphs is None:
-            flatten_batch_subgraphs, x_subs = self._prepare_ego(batch_g, None, batch_x, x_subs)
-        batch_x = self.transfer_d(batch_x)
-        x_subs = self.transfer_d(x_subs)
-        im, kl, noisy, z2 = self.model.extract_features(None, batch_g, batch_x,
-                                                        flatten_batch_subgraphs, x_subs, device,
-                                                        noise)
+        if flatten_batch_subgraphs is None and x_subs is None and batch_x.is_cuda:
+            # the wrapper's transfer_d feeds the wrapped model's encoders
+            ego, enc = self._encode_forked(self.model, batch_g, batch_x)
+            im, _, _, z2, z1 = self.model._extract(self.model, batch_g, None, ego, None, noise,
+                                                   enc)
+            self.model._last_z1 = z1
+        else:
+            if flatten_batch_subgraphs is None:
+                flatten_batch_subgraphs, x_subs = self._prepare_ego(batch_g, None, batch_x,
+                                                                    x_subs)
+            batch_x = self.transfer_d(batch_x)
+            x_subs = self.transfer_d(x_subs)
+            im, kl, noisy, z2 = self.model.extract_features(None, batch_g, batch_x,
+                                                            flatten_batch_subgraphs, x_subs,
+                                                            device, noise)
         kl_loss, con, rec = self._losses(batch_g, im, self.model._last_kl_mean,
                                          self.model._last_z1, z2, self.MLP, batch_size)
         return None, kl_loss, con, rec

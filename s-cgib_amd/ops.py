@@ -364,3 +364,70 @@ class _ReconAdj(torch.autograd.Function):
 def recon_adj(im, graph):
     """sum((IM IM^T - A)^2) / N without the N x N matrix (models.py:762-768)."""
     return _ReconAdj.apply(im, graph)
+
+
+# ---------------------------------------------------------------------------
+# Arrival counters for last-arriver reductions: one persistent zeroed int32
+# buffer per device, carved into fixed ranges per call site.  Kernels leave
+# their counters zero, so a range is reused by every launch and graph replay.
+# ---------------------------------------------------------------------------
+_COUNTER_CAP = 1 << 16
+_COUNTERS = {}   # device index -> tensor
+_COUNTER_RANGES = {}  # (device index, key) -> (offset, size)
+
+
+def counters(device, key, n):
+    """``n`` zeroed uint32 counters reserved for call site ``key`` on ``device``
+    (allocate outside graph capture: the first call per device allocates)."""
+    idx = torch.device(device).index or 0
+    buf = _COUNTERS.get(idx)
+    if buf is None:
+        buf = _COUNTERS[idx] = torch.zeros(_COUNTER_CAP, dtype=torch.int32, device=device)
+    rk = (idx, key)
+    off, size = _COUNTER_RANGES.get(rk, (None, 0))
+    if size < n:
+        used = max((o + s for (d, _), (o, s) in _COUNTER_RANGES.items() if d == idx), default=0)
+        if used + n > _COUNTER_CAP:
+            raise _lib.ScgibError("arrival-counter pool exhausted")
+        off, size = used, n
+        _COUNTER_RANGES[rk] = (off, size)
+    return buf[off: off + n]
+
+
+# ---------------------------------------------------------------------------
+# A11: contrastive loss (batched_semi_loss, tau = 1)
+# ---------------------------------------------------------------------------
+class _Contrastive(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, z1, z2):
+        z1 = _f32(z1, "contrastive z1")
+        z2 = _f32(z2, "contrastive z2")
+        B = z1.shape[0]
+        if z1.shape != (B, HIDDEN) or z2.shape != (B, HIDDEN):
+            raise _lib.ScgibError(f"contrastive: z1 {tuple(z1.shape)} / z2 {tuple(z2.shape)} "
+                                  f"must both be [B, {HIDDEN}]")
+        ws = torch.empty(int(_lib.query("scgib_contrastive_workspace_floats", B)),
+                         dtype=torch.float32, device=z1.device)
+        loss = torch.empty((), dtype=torch.float32, device=z1.device)
+        cnt = counters(z1.device, "contrastive", int(_lib.query("scgib_contrastive_counters", B)))
+        _lib.call("scgib_contrastive_fwd", _p(z1), _p(z2), B, _p(ws), _p(loss), _p(cnt),
+                  _stream())
+        ctx.save_for_backward(z1, z2, ws)
+        return loss
+
+    @staticmethod
+    def backward(ctx, g):
+        z1, z2, ws = ctx.saved_tensors
+        B = z1.shape[0]
+        g = _f32(g, "contrastive.backward").reshape(1)
+        dz1, dz2 = torch.empty_like(z1), torch.empty_like(z2)
+        cnt = counters(z1.device, "contrastive", int(_lib.query("scgib_contrastive_counters", B)))
+        _lib.call("scgib_contrastive_bwd", _p(z1), _p(z2), B, _p(ws), _p(g), _p(dz1), _p(dz2),
+                  _p(cnt), _stream())
+        return dz1, dz2
+
+
+def contrastive(z1, z2):
+    """batched_semi_loss(z1, z2, chunk) with tau = 1 (models.py:606-629); the
+    value does not depend on the chunk size."""
+    return _Contrastive.apply(z1, z2)

@@ -365,3 +365,31 @@ def test_fused_gin_encoder(pkg, dev, training, layers, n_mols):
                 assert int(sd[kk]) == int(v), kk
             else:
                 assert rel_err(sd[kk].cpu(), v) < 1e-5, kk
+
+
+# ---------------------------------------------------------------------------
+# A11: contrastive loss (batched_semi_loss) vs the oracle in fp64
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("B", [1, 7, 64, 100, 512, 1500])
+def test_contrastive_fwd_bwd(pkg, dev, B):
+    gen = torch.Generator().manual_seed(B)
+    z1 = torch.randn(B, 64, generator=gen) * 2
+    z2 = torch.randn(B, 64, generator=gen) + 0.5 * z1
+    if B > 7:
+        z2[3] = 0.0  # a zero readout row (F.normalize eps branch)
+    z1r = z1.double().requires_grad_(True)
+    z2r = z2.double().requires_grad_(True)
+    lr = R.semi_loss(z1r, z2r, 16)
+    lr.backward()
+    z1d = z1.to(dev).requires_grad_(True)
+    z2d = z2.to(dev).requires_grad_(True)
+    for rep in range(2):  # the arrival counters must be left reusable
+        z1d.grad = z2d.grad = None
+        ld = pkg.ops.contrastive(z1d, z2d)
+        (3.0 * ld).backward()
+        # B = 1: the loss and its gradient are 0 in exact arithmetic (D = e12)
+        assert abs(ld.item() - lr.item()) <= 1e-5 * max(1.0, abs(lr.item())), rep
+        for mine, ref in ((z1d.grad, z1r.grad), (z2d.grad, z2r.grad)):
+            ref = 3.0 * ref
+            err = (mine.cpu().double() - ref).norm()
+            assert err <= 1e-5 * max(ref.norm().item(), 1e-2), rep

@@ -190,7 +190,8 @@ int scgib_bn_running_update(const float *stats, const int32_t *graph_ptr, int64_
  * pgrad[B, SCGIB_PGRAD_STRIDE] laid out as
  *   [0,64) dW2 | 64 db2 | [65,129) dgamma | [129,193) dbeta |
  *   [193,321) dW_att | 321 db_att
- * (sum them over graphs for the parameter gradients). */
+ * If pgrad_total (SCGIB_PGRAD_STRIDE floats) is given, the fixed-order sum
+ * over graphs (the parameter gradients) is written there as well. */
 int scgib_interaction_bwd(const float *g_im, const float *g_z1, const float *g_z2,
                           const float *g_kl, const float *f, const float *t, const float *s,
                           const float *u_feat, const int32_t *graph_ptr, int64_t n_graphs,
@@ -200,7 +201,7 @@ int scgib_interaction_bwd(const float *g_im, const float *g_z1, const float *g_z
                           const float *w_att, const float *z1, const float *lam,
                           const float *logit, const float *stats, float *df, float *dt,
                           float *ds, float *pgrad, const float *g_klmean, int32_t pad_rows,
-                          scgib_stream_t stream);
+                          float *pgrad_total, scgib_stream_t stream);
 
 /* ---- A12: adjacency reconstruction loss, Gram form ------------------------
  * loss = sum_{u,v} (<im_u, im_v> - A_uv)^2 / N
@@ -239,6 +240,31 @@ int scgib_contrastive_fwd(const float *z1, const float *z2, int64_t n_graphs, fl
 int scgib_contrastive_bwd(const float *z1, const float *z2, int64_t n_graphs, float *workspace,
                           const float *g_loss, float *dz1, float *dz2, uint32_t *counters,
                           scgib_stream_t stream);
+
+/* ---- A10 head: fused dense layers (exact-f32 MFMA tiles) -----------------
+ * mlp2: out = relu(x W1^T + b1) W2^T + b2, x [N][d_in] (d_in 64 or 128),
+ * W1 [64][d_in], W2 [64][64] — the interaction-map MLP of Mainmodel /
+ * Mainmodel_continue (models.py:569-571 / :1055-1057, applied at :676 /
+ * :1174).  Forward saves r = relu(x W1^T + b1) [N][64] for backward.
+ * Backward: dx [N][d_in] and wgrad = dW2[64*64] | dW1[64*d_in] | db2 | db1
+ * (fixed-order, deterministic); `slab` holds scgib_mlp2_slab_floats(n, d_in).
+ * linear: out = x W^T (+ b), 64 -> 64 — compressor[0] (models.py:589-592 /
+ * :1081-1084, applied at :596 / :1092).  Backward writes dx = add + dy W
+ * (`add` may be NULL) and wgrad = dW[64*64] | db[64]; `slab` holds
+ * scgib_linear_slab_floats(n).  Capacity mode as above (dims). */
+int64_t scgib_mlp2_slab_floats(int64_t n_nodes, int32_t d_in);
+int scgib_mlp2_fwd(const float *x, int32_t d_in, int64_t n_nodes, const float *w1,
+                   const float *b1, const float *w2, const float *b2, float *r, float *out,
+                   const int32_t *dims, scgib_stream_t stream);
+int scgib_mlp2_bwd(const float *dout, const float *x, const float *r, int32_t d_in,
+                   const float *w1, const float *w2, int64_t n_nodes, float *dx, float *slab,
+                   float *wgrad, const int32_t *dims, scgib_stream_t stream);
+int64_t scgib_linear_slab_floats(int64_t n_nodes);
+int scgib_linear_fwd(const float *x, int64_t n_nodes, const float *w, const float *b, float *out,
+                     const int32_t *dims, scgib_stream_t stream);
+int scgib_linear_bwd(const float *dy, const float *x, const float *w, int64_t n_nodes,
+                     const float *add, float *dx, float *slab, float *wgrad,
+                     const int32_t *dims, scgib_stream_t stream);
 
 #ifdef __cplusplus
 }

@@ -32,11 +32,17 @@ SIGNATURES = {
     "scgib_bn_running_update": (ctypes.c_int, [_P, _P, _I64, _F, _P, _P, _P, _P]),
     "scgib_interaction_bwd": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _I64, _I64, _P,
                                              _P, _P, _P, _F, _I32, _P, _P, _P, _P, _P, _P, _P,
-                                             _P, _P, _P, _P, _I32, _P]),
+                                             _P, _P, _P, _P, _I32, _P, _P]),
     "scgib_contrastive_workspace_floats": (_I64, [_I64]),
     "scgib_contrastive_counters": (_I64, [_I64]),
     "scgib_contrastive_fwd": (ctypes.c_int, [_P, _P, _I64, _P, _P, _P, _P]),
     "scgib_contrastive_bwd": (ctypes.c_int, [_P, _P, _I64, _P, _P, _P, _P, _P, _P]),
+    "scgib_mlp2_slab_floats": (_I64, [_I64, _I32]),
+    "scgib_mlp2_fwd": (ctypes.c_int, [_P, _I32, _I64, _P, _P, _P, _P, _P, _P, _P, _P]),
+    "scgib_mlp2_bwd": (ctypes.c_int, [_P, _P, _P, _I32, _P, _P, _I64, _P, _P, _P, _P, _P]),
+    "scgib_linear_slab_floats": (_I64, [_I64]),
+    "scgib_linear_fwd": (ctypes.c_int, [_P, _I64, _P, _P, _P, _P, _P]),
+    "scgib_linear_bwd": (ctypes.c_int, [_P, _P, _P, _I64, _P, _P, _P, _P, _P, _P]),
     "scgib_gin_tiles": (_I64, [_I64]),
     "scgib_gin_slab_floats": (_I64, [_I64, _I32]),
     "scgib_gin_layer_fwd": (ctypes.c_int, [_P, _I32, _P, _P, _P, _I64, _F, _P, _P, _P, _P, _P, _P,
@@ -52,7 +58,7 @@ SIGNATURES = {
     "scgib_recon_bwd": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _I64, _P, _P, _P, _P]),
 }
 
-ABI_VERSION = 2
+ABI_VERSION = 3
 STATS_STRIDE = 260
 PGRAD_STRIDE = 324
 HIDDEN = 64

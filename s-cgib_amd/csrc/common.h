@@ -51,4 +51,8 @@ __device__ __forceinline__ int64_t eff_count(const int32_t *dims, int idx, int64
     return dims ? static_cast<int64_t>(dims[idx]) : cap;
 }
 
+// Fixed-order sum of `nslab` per-workgroup slabs of `width` floats into out
+// (slab.hip); deterministic.
+int launch_slab_reduce(const float *slab, int nslab, int64_t width, float *out, hipStream_t st);
+
 }  // namespace scgib

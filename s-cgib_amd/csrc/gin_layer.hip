@@ -28,77 +28,22 @@
 //                    dW2 += dz2^T r; dr = dz2 W2; dz1 = dr [r > 0];
 //                    dW1 += dz1^T agg; d(agg) = dz1 W1.  Workgroups loop over
 //                    tiles and keep dW in MFMA accumulators; one slab each.
-//   slab_reduce1/2 : fixed-order two-stage sum of the per-workgroup slabs.
+//   slab_reduce_k  : fixed-order sum of the per-workgroup slabs.
 //
 // LDS tiles are row-major with a +1-float row pad (stride 65 / 33), which
 // makes every MFMA operand read (32 lanes: 32 rows of one column, or 32
 // columns of one row) bank-conflict free for ds_read_b32.
-#include "common.h"
+#include "mfma_tile.h"
 
 namespace scgib {
-
-typedef float f32x16 __attribute__((ext_vector_type(16)));
-
-constexpr int TM = 64;   // rows per tile
-constexpr int LDH = 65;  // LDS stride of 64-wide tiles
-
-__device__ __forceinline__ f32x16 zero16() {
-    f32x16 a;
-#pragma unroll
-    for (int i = 0; i < 16; ++i) a[i] = 0.f;
-    return a;
-}
-
-// C(i, j) += sum_k A(i, k) B(k, j) over K, 32x32 tile, with
-//   NT: A(i,k) = As[i*lda + k],   B(k,j) = Bs[j*ldb + k]
-//   NN: A(i,k) = As[i*lda + k],   B(k,j) = Bs[k*ldb + j]
-//   TN: A(i,k) = As[k*lda + i],   B(k,j) = Bs[k*ldb + j]   (sum over rows k)
-// (lane l supplies i or j = l & 31 and k-offset l >> 5 of each K=2 step)
-template <int K>
-__device__ __forceinline__ f32x16 mma_nt(const float *As, int lda, const float *Bs, int ldb,
-                                         f32x16 acc) {
-    const int l = threadIdx.x & 63, i = l & 31, kk = l >> 5;
-#pragma unroll 8
-    for (int k = 0; k < K; k += 2)
-        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(As[i * lda + k + kk], Bs[i * ldb + k + kk], acc, 0, 0, 0);
-    return acc;
-}
-
-template <int K>
-__device__ __forceinline__ f32x16 mma_nn(const float *As, int lda, const float *Bs, int ldb,
-                                         f32x16 acc) {
-    const int l = threadIdx.x & 63, i = l & 31, kk = l >> 5;
-#pragma unroll 8
-    for (int k = 0; k < K; k += 2)
-        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(As[i * lda + k + kk], Bs[(k + kk) * ldb + i], acc, 0, 0, 0);
-    return acc;
-}
-
-template <int K>
-__device__ __forceinline__ f32x16 mma_tn(const float *As, int lda, const float *Bs, int ldb,
-                                         f32x16 acc) {
-    const int l = threadIdx.x & 63, i = l & 31, kk = l >> 5;
-#pragma unroll 8
-    for (int k = 0; k < K; k += 2)
-        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(As[(k + kk) * lda + i], Bs[(k + kk) * ldb + i], acc, 0, 0, 0);
-    return acc;
-}
-
-// row of accumulator register `reg` of the 32x32 output tile held by lane l
-__device__ __forceinline__ int acc_row(int reg, int l) { return (reg & 3) + 8 * (reg >> 2) + 4 * (l >> 5); }
-
-__device__ __forceinline__ float4 ld4(const float *p) { return *reinterpret_cast<const float4 *>(p); }
-__device__ __forceinline__ void st4(float *p, float4 v) { *reinterpret_cast<float4 *>(p) = v; }
-__device__ __forceinline__ float4 add4(float4 a, float4 b) { return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w); }
-__device__ __forceinline__ float4 xform4(float4 z, float4 a, float4 b) {
-    return make_float4(fmaxf(a.x * z.x + b.x, 0.f), fmaxf(a.y * z.y + b.y, 0.f),
-                       fmaxf(a.z * z.z + b.z, 0.f), fmaxf(a.w * z.w + b.w, 0.f));
-}
 
 // ---------------------------------------------------------------------------
 // forward
 // ---------------------------------------------------------------------------
-template <int DIN, bool XFORM>
+// GATHER = false is the dense two-layer MLP of the head (models.py:1055-1057,
+// applied at :1174): the tile's input rows are staged directly, agg_out and
+// the BN tile statistics are not written, z2_out is the MLP output.
+template <int DIN, bool XFORM, bool GATHER = true>
 __global__ __launch_bounds__(256) void gin_fwd_k(
     const float *__restrict__ h, const float *__restrict__ in_scale,
     const float *__restrict__ in_shift, const int32_t *__restrict__ rowptr,
@@ -123,51 +68,53 @@ __global__ __launch_bounds__(256) void gin_fwd_k(
             r_out[row0 * 64 + idx] = 0.f;
             z2_out[row0 * 64 + idx] = 0.f;
         }
-        for (int idx = nv * DIN + tid; idx < ncr * DIN; idx += 256) agg_out[row0 * DIN + idx] = 0.f;
+        if (GATHER)
+            for (int idx = nv * DIN + tid; idx < ncr * DIN; idx += 256) agg_out[row0 * DIN + idx] = 0.f;
         if (nv == 0) {
-            if (tid < 128) part[tile * 128 + tid] = 0.f;
+            if (GATHER && tid < 128) part[tile * 128 + tid] = 0.f;
             return;
         }
     }
 
-    for (int idx = tid; idx < 64 * DIN; idx += 256) sW1[(idx / DIN) * LDA + idx % DIN] = w1[idx];
-    for (int idx = tid; idx < 64 * 64; idx += 256) sW2[(idx >> 6) * LDH + (idx & 63)] = w2[idx];
+    stage_weights<DIN>(w1, w2, sW1, sW2);
+    if constexpr (!GATHER) {  // dense: the input rows themselves
+        constexpr int AQ = DIN / 4, AK = TM * AQ / 256;
+        float4 va[AK];
+#pragma unroll
+        for (int k = 0; k < AK; ++k) {
+            const int idx = tid + 256 * k, rr = idx / AQ, cq = idx % AQ;
+            va[k] = rr < nv ? ld4(h + (row0 + rr) * DIN + 4 * cq) : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+#pragma unroll
+        for (int k = 0; k < AK; ++k) {
+            const int idx = tid + 256 * k, rr = idx / AQ, cq = idx % AQ;
+            float *d = sA + rr * LDA + 4 * cq;
+            d[0] = va[k].x; d[1] = va[k].y; d[2] = va[k].z; d[3] = va[k].w;
+        }
+    } else
 
-    // gather: agg[v] = ope * x[v] + sum_{u->v} x[u], x = relu(scale*h + shift) if XFORM
+    // gather: agg[v] = ope * x[v] + sum_{u->v} x[u], x = relu(scale*h + shift) if XFORM.
+    // Each thread owns RPT rows of one 4-channel chunk; the loads of all its
+    // rows are issued together (row pointers + self rows, then up to 4
+    // neighbour indices per row, then those neighbour rows), so a tile costs
+    // ~3 memory latencies instead of 3 per row.
     {
-        const int c = tid % LPR;
+        constexpr int RPT = TM / RPP;
+        const int c = tid % LPR, rbase = tid / LPR;
         float4 sc = make_float4(1.f, 1.f, 1.f, 1.f), sh = make_float4(0.f, 0.f, 0.f, 0.f);
         if (XFORM) {
             sc = ld4(in_scale + 4 * c);
             sh = ld4(in_shift + 4 * c);
         }
         const float4 *h4 = reinterpret_cast<const float4 *>(h);
-        for (int rr = tid / LPR; rr < TM; rr += RPP) {
-            const int64_t v = row0 + rr;
-            float4 out = make_float4(0.f, 0.f, 0.f, 0.f);
-            if (rr < nv) {
-                const int32_t beg = rowptr[v], end = rowptr[v + 1];
-                float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-                int32_t j = beg;
-                for (; j + 2 <= end; j += 2) {
-                    const int64_t u0 = col[j], u1 = col[j + 1];
-                    float4 a0 = h4[u0 * LPR + c], a1 = h4[u1 * LPR + c];
-                    if (XFORM) { a0 = xform4(a0, sc, sh); a1 = xform4(a1, sc, sh); }
-                    acc = add4(add4(acc, a0), a1);
-                }
-                if (j < end) {
-                    float4 a0 = h4[static_cast<int64_t>(col[j]) * LPR + c];
-                    if (XFORM) a0 = xform4(a0, sc, sh);
-                    acc = add4(acc, a0);
-                }
-                float4 self = h4[v * LPR + c];
-                if (XFORM) self = xform4(self, sc, sh);
-                out = make_float4(ope * self.x + acc.x, ope * self.y + acc.y, ope * self.z + acc.z,
-                                  ope * self.w + acc.w);
-                st4(agg_out + v * DIN + 4 * c, out);
-            }
+        float4 acc[RPT];
+        gather_rows<RPT, RPP, LPR, XFORM>(h4, rowptr, col, row0, nv, rbase, c, ope, sc, sh, acc);
+#pragma unroll
+        for (int k = 0; k < RPT; ++k) {
+            const int rr = rbase + k * RPP;
+            if (rr < nv) st4(agg_out + (row0 + rr) * DIN + 4 * c, acc[k]);
             float *d = sA + rr * LDA + 4 * c;
-            d[0] = out.x; d[1] = out.y; d[2] = out.z; d[3] = out.w;
+            d[0] = acc[k].x; d[1] = acc[k].y; d[2] = acc[k].z; d[3] = acc[k].w;
         }
     }
     __syncthreads();
@@ -200,6 +147,7 @@ __global__ __launch_bounds__(256) void gin_fwd_k(
             s += acc[reg];
         }
     }
+    if constexpr (!GATHER) return;
     s += __shfl_xor(s, 32, kWave);
     if (l < 32) sRed[wr][ccol] = s;
     __syncthreads();
@@ -222,11 +170,19 @@ __global__ __launch_bounds__(256) void gin_fwd_k(
     }
 }
 
-// Batch mean / biased variance from the per-tile (sum, centred M2): two
-// parallel fixed-order passes (fp64), 16 partitions x 64 channels:
-//   mean = sum_b S_b / N ;  M2 = sum_b [M2_b + n_b (S_b/n_b - mean)^2]
-// (exact decomposition of the centred sum of squares).  Loads are issued four
-// at a time so the partition loops are not latency chains.
+// Batch mean / biased variance from the per-tile (sum, centred M2), fp64,
+// two passes over the tile statistics with 8 tiles' loads in flight per
+// thread (16 partitions x 64 channels, partitions combined in fixed order):
+//   mean = sum_b S_b / N ;  M2 = sum_b [M2_b + (S_b - n_b mean)^2 / n_b]
+// (exact decomposition of the centred sum of squares; n_b = 64 except the
+// last tile, so only that one divides).
+__device__ __forceinline__ double sum16_lds(double (*sh)[64], int c) {
+    double s = 0.0;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) s += sh[k][c];
+    return s;
+}
+
 __global__ __launch_bounds__(1024) void bn_finalize_k(
     const float *__restrict__ part, int64_t ncap, const float *__restrict__ gamma,
     const float *__restrict__ beta, float eps, float momentum, int training,
@@ -240,33 +196,42 @@ __global__ __launch_bounds__(1024) void bn_finalize_k(
     double mean = 0.0, var = 0.0, M2 = 0.0;
     if (training) {
         double a = 0.0;
-        int64_t t = p;
-        for (; t + 48 < ntiles; t += 64) {
-            const float v0 = part[t * 128 + c], v1 = part[(t + 16) * 128 + c];
-            const float v2 = part[(t + 32) * 128 + c], v3 = part[(t + 48) * 128 + c];
-            a += v0; a += v1; a += v2; a += v3;
+        for (int64_t t0 = p; t0 < ntiles; t0 += 16 * 8) {
+            float S[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) S[u] = t0 + 16 * u < ntiles ? part[(t0 + 16 * u) * 128 + c] : 0.f;
+#pragma unroll
+            for (int u = 0; u < 8; ++u) a += static_cast<double>(S[u]);
         }
-        for (; t < ntiles; t += 16) a += part[t * 128 + c];
         sh[p][c] = a;
         __syncthreads();
-        if (p == 0) {
-            double s = 0.0;
-            for (int k = 0; k < 16; ++k) s += sh[k][c];
-            s_mean[c] = s / static_cast<double>(n);
-        }
+        if (p == 0) s_mean[c] = sum16_lds(sh, c) / static_cast<double>(n);
         __syncthreads();
         mean = s_mean[c];
         double q = 0.0;
-        for (t = p; t < ntiles; t += 16) {
-            const double nb = static_cast<double>(n - t * TM < TM ? n - t * TM : TM);
-            const double d = part[t * 128 + c] / nb - mean;
-            q += part[t * 128 + 64 + c] + nb * d * d;
+        for (int64_t t0 = p; t0 < ntiles; t0 += 16 * 8) {
+            float S[8], Q[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int64_t t = t0 + 16 * u;
+                S[u] = t < ntiles ? part[t * 128 + c] : 0.f;
+                Q[u] = t < ntiles ? part[t * 128 + 64 + c] : 0.f;
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int64_t t = t0 + 16 * u;
+                if (t < ntiles) {
+                    const int64_t nb = n - t * TM < TM ? n - t * TM : TM;
+                    const double d = static_cast<double>(S[u]) - static_cast<double>(nb) * mean;
+                    const double inv_nb = nb == TM ? 1.0 / TM : 1.0 / static_cast<double>(nb);
+                    q += static_cast<double>(Q[u]) + d * d * inv_nb;
+                }
+            }
         }
         __syncthreads();
         sh[p][c] = q;
         __syncthreads();
-        if (p == 0)
-            for (int k = 0; k < 16; ++k) M2 += sh[k][c];
+        if (p == 0) M2 = sum16_lds(sh, c);
         var = M2 / static_cast<double>(n);
     }
     if (p == 0) {
@@ -323,37 +288,36 @@ __global__ __launch_bounds__(256) void gin_bwd_stats_k(
     const float4 mean = ld4(stat + 4 * c), istd = ld4(stat + 64 + 4 * c);
     const float4 sc = ld4(stat + 128 + 4 * c), sh = ld4(stat + 192 + 4 * c);
     const float4 *g4 = reinterpret_cast<const float4 *>(dh);
+    const int nv = static_cast<int>(n - row0 < TM ? (n - row0 > 0 ? n - row0 : 0) : TM);
+    float4 g[4];
+    if (GATHER) {
+        gather_rows<4, 16, 16, false>(g4, rowptr_t, col_t, row0, nv, slot, c, ope, sc, sh, g);
+    } else {
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            g[k] = slot + 16 * k < nv ? g4[(row0 + slot + 16 * k) * 16 + c] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    float4 z[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+        z[k] = slot + 16 * k < nv ? ld4(z2 + (row0 + slot + 16 * k) * 64 + 4 * c) : make_float4(0.f, 0.f, 0.f, 0.f);
     float4 sdy = make_float4(0.f, 0.f, 0.f, 0.f), sdx = sdy;
-    for (int rr = slot; rr < TM; rr += 16) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int rr = slot + 16 * k;
         const int64_t v = row0 + rr;
         if (v >= ncap) break;
-        if (v >= n) {
+        if (rr >= nv) {
             st4(dy_out + v * 64 + 4 * c, make_float4(0.f, 0.f, 0.f, 0.f));
             continue;
         }
-        float4 g;
-        if (GATHER) {
-            float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-            const int32_t beg = rowptr_t[v], end = rowptr_t[v + 1];
-            int32_t j = beg;
-            for (; j + 2 <= end; j += 2) {
-                const int64_t u0 = col_t[j], u1 = col_t[j + 1];
-                acc = add4(add4(acc, g4[u0 * 16 + c]), g4[u1 * 16 + c]);
-            }
-            if (j < end) acc = add4(acc, g4[static_cast<int64_t>(col_t[j]) * 16 + c]);
-            const float4 self = g4[v * 16 + c];
-            g = make_float4(ope * self.x + acc.x, ope * self.y + acc.y, ope * self.z + acc.z,
-                            ope * self.w + acc.w);
-        } else {
-            g = g4[v * 16 + c];
-        }
-        const float4 z = ld4(z2 + v * 64 + 4 * c);
-        const float4 dy = make_float4(sc.x * z.x + sh.x > 0.f ? g.x : 0.f, sc.y * z.y + sh.y > 0.f ? g.y : 0.f,
-                                      sc.z * z.z + sh.z > 0.f ? g.z : 0.f, sc.w * z.w + sh.w > 0.f ? g.w : 0.f);
+        const float4 zz = z[k], gg = g[k];
+        const float4 dy = make_float4(sc.x * zz.x + sh.x > 0.f ? gg.x : 0.f, sc.y * zz.y + sh.y > 0.f ? gg.y : 0.f,
+                                      sc.z * zz.z + sh.z > 0.f ? gg.z : 0.f, sc.w * zz.w + sh.w > 0.f ? gg.w : 0.f);
         st4(dy_out + v * 64 + 4 * c, dy);
         sdy = add4(sdy, dy);
-        sdx = add4(sdx, make_float4(dy.x * (z.x - mean.x) * istd.x, dy.y * (z.y - mean.y) * istd.y,
-                                    dy.z * (z.z - mean.z) * istd.z, dy.w * (z.w - mean.w) * istd.w));
+        sdx = add4(sdx, make_float4(dy.x * (zz.x - mean.x) * istd.x, dy.y * (zz.y - mean.y) * istd.y,
+                                    dy.z * (zz.z - mean.z) * istd.z, dy.w * (zz.w - mean.w) * istd.w));
     }
     float *a = &sRed[0][slot][4 * c];
     a[0] = sdy.x; a[1] = sdy.y; a[2] = sdy.z; a[3] = sdy.w;
@@ -380,15 +344,19 @@ __global__ __launch_bounds__(1024) void bn_bwd_finalize_k(const float *__restric
     const int64_t n = eff_count(dims, 0, ncap), ntiles = (n + TM - 1) / TM;
     __shared__ double s1[16][64], s2[16][64];
     double a = 0.0, b = 0.0;
-    int64_t t = p;
-    for (; t + 16 < ntiles; t += 32) {
-        const float a0 = part[t * 128 + c], a1 = part[(t + 16) * 128 + c];
-        const float b0 = part[t * 128 + 64 + c], b1 = part[(t + 16) * 128 + 64 + c];
-        a += a0; a += a1; b += b0; b += b1;
-    }
-    for (; t < ntiles; t += 16) {
-        a += part[t * 128 + c];
-        b += part[t * 128 + 64 + c];
+    for (int64_t t0 = p; t0 < ntiles; t0 += 16 * 8) {
+        float A[8], Bv[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int64_t t = t0 + 16 * u;
+            A[u] = t < ntiles ? part[t * 128 + c] : 0.f;
+            Bv[u] = t < ntiles ? part[t * 128 + 64 + c] : 0.f;
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            a += static_cast<double>(A[u]);
+            b += static_cast<double>(Bv[u]);
+        }
     }
     s1[p][c] = a;
     s2[p][c] = b;
@@ -407,7 +375,9 @@ __global__ __launch_bounds__(1024) void bn_bwd_finalize_k(const float *__restric
 }
 
 // slab layout per workgroup: dW2[64*64] | dW1[64*DIN] | db2[64] | db1[64]
-template <int DIN>
+// BN = false is the backward of the dense head MLP: dz2 = dy (the gradient
+// of the MLP output); z2 / stat / coef are not read.
+template <int DIN, bool BN = true>
 __global__ __launch_bounds__(256) void gin_bwd_k(
     const float *__restrict__ dy, const float *__restrict__ z2, const float *__restrict__ r,
     const float *__restrict__ agg, const float *__restrict__ stat,
@@ -424,14 +394,26 @@ __global__ __launch_bounds__(256) void gin_bwd_k(
     __shared__ float sW2[64 * LDH];
     const int tid = threadIdx.x, l = tid & 63, w = tid >> 6;
     const int wr = w >> 1, wc = w & 1;
-    for (int idx = tid; idx < 64 * DIN; idx += 256) sW1[(idx / DIN) * LDA + idx % DIN] = w1[idx];
-    for (int idx = tid; idx < 64 * 64; idx += 256) sW2[(idx >> 6) * LDH + (idx & 63)] = w2[idx];
+    stage_weights<DIN>(w1, w2, sW1, sW2);
     const int ch = tid & 63, q = tid >> 6;  // column-sum roles: channel, row quarter
-    const float s_mean = stat[ch], s_istd = stat[64 + ch], s_sc = stat[128 + ch];
-    const float c1 = coef[ch], c2 = coef[64 + ch];
-    f32x16 accW2 = zero16(), accW1 = zero16();
-    float db2 = 0.f, db1 = 0.f;
+    // staging roles: 4-channel chunk c4, rows rs + 16 k
+    const int c4 = tid & 15, rs = tid >> 4;
+    const float4 zero = make_float4(0.f, 0.f, 0.f, 0.f);
+    float4 s_mean = zero, s_istd = zero, s_sc = zero, c1 = zero, c2 = zero;
+    if (BN) {
+        s_mean = ld4(stat + 4 * c4);
+        s_istd = ld4(stat + 64 + 4 * c4);
+        s_sc = ld4(stat + 128 + 4 * c4);
+        c1 = ld4(coef + 4 * c4);
+        c2 = ld4(coef + 64 + 4 * c4);
+    }
     constexpr int NSUB1 = 2 * (DIN / 32);  // 32x32 sub-tiles of dW1 / d(agg)
+    constexpr int NW1 = (NSUB1 + 3) / 4;   // per wave
+    f32x16 accW2 = zero16(), accW1[NW1];
+#pragma unroll
+    for (int q1 = 0; q1 < NW1; ++q1) accW1[q1] = zero16();
+    float db2 = 0.f, db1 = 0.f;
+    constexpr int AQ = DIN / 4, AK = TM * AQ / 256;  // agg tile: float4 per row, per thread
     for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
         const int64_t row0 = tile * TM;
         const int nv = static_cast<int>(n - row0 < TM ? (n - row0 > 0 ? n - row0 : 0) : TM);
@@ -440,23 +422,44 @@ __global__ __launch_bounds__(256) void gin_bwd_k(
             for (int idx = nv * DIN + tid; idx < ncr * DIN; idx += 256) dagg_out[row0 * DIN + idx] = 0.f;
             if (nv == 0) continue;  // block-uniform
         }
-        __syncthreads();  // previous tile's LDS reads are done
-        // stage dz2 (computed), r and agg tiles; rows past n are zero
-        for (int rr = q; rr < TM; rr += 4) {
-            float d = 0.f, rv = 0.f;
-            if (rr < nv) {
-                const int64_t v = row0 + rr;
-                const float z = z2[v * 64 + ch];
-                const float xh = (z - s_mean) * s_istd;
-                d = s_sc * (dy[v * 64 + ch] - c1 - xh * c2);
-                rv = r[v * 64 + ch];
-            }
-            sD[rr * LDH + ch] = d;
-            sR[rr * LDH + ch] = rv;
+        // global loads of the whole tile first (16-byte, all in flight)
+        float4 vz[4], vd[4], vr[4], va[AK];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int rr = rs + 16 * k;
+            const int64_t o = (row0 + rr) * 64 + 4 * c4;
+            vz[k] = BN && rr < nv ? ld4(z2 + o) : zero;
+            vd[k] = rr < nv ? ld4(dy + o) : zero;
+            vr[k] = rr < nv ? ld4(r + o) : zero;
         }
-        for (int idx = tid; idx < TM * DIN; idx += 256) {
-            const int rr = idx / DIN, k = idx % DIN;
-            sA[rr * LDA + k] = rr < nv ? agg[(row0 + rr) * DIN + k] : 0.f;
+#pragma unroll
+        for (int k = 0; k < AK; ++k) {
+            const int idx = tid + 256 * k, rr = idx / AQ, cq = idx % AQ;
+            va[k] = rr < nv ? ld4(agg + (row0 + rr) * DIN + 4 * cq) : zero;
+        }
+        __syncthreads();  // previous tile's LDS reads are done
+        // dz2 = scale (dy - c1 - xhat c2); rows past n are zero
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int rr = rs + 16 * k;
+            float4 d = zero;
+            if (!BN) {
+                d = vd[k];
+            } else if (rr < nv) {
+                d.x = s_sc.x * (vd[k].x - c1.x - (vz[k].x - s_mean.x) * s_istd.x * c2.x);
+                d.y = s_sc.y * (vd[k].y - c1.y - (vz[k].y - s_mean.y) * s_istd.y * c2.y);
+                d.z = s_sc.z * (vd[k].z - c1.z - (vz[k].z - s_mean.z) * s_istd.z * c2.z);
+                d.w = s_sc.w * (vd[k].w - c1.w - (vz[k].w - s_mean.w) * s_istd.w * c2.w);
+            }
+            float *pd = sD + rr * LDH + 4 * c4, *pr = sR + rr * LDH + 4 * c4;
+            pd[0] = d.x; pd[1] = d.y; pd[2] = d.z; pd[3] = d.w;
+            pr[0] = vr[k].x; pr[1] = vr[k].y; pr[2] = vr[k].z; pr[3] = vr[k].w;
+        }
+#pragma unroll
+        for (int k = 0; k < AK; ++k) {
+            const int idx = tid + 256 * k, rr = idx / AQ, cq = idx % AQ;
+            float *pa = sA + rr * LDA + 4 * cq;
+            pa[0] = va[k].x; pa[1] = va[k].y; pa[2] = va[k].z; pa[3] = va[k].w;
         }
         __syncthreads();
         // dW2 += dz2^T r  (sub-tile j-block wr, k-block wc)
@@ -473,19 +476,19 @@ __global__ __launch_bounds__(256) void gin_bwd_k(
         }
         __syncthreads();
         for (int rr = q; rr < TM; rr += 4) db1 += sD[rr * LDH + ch];
-        // dW1 += dz1^T agg  (64 x DIN)
-        if (w < NSUB1) {
-            const int jb = w & 1, kb = w >> 1;  // j-block, k-block
-            accW1 = mma_tn<TM>(sD + jb * 32, LDH, sA + kb * 32, LDA, accW1);
-        }
-        // d(agg) = dz1 W1  (TM x DIN)
-        if (w < NSUB1) {
-            const int rb = w & 1, kb = w >> 1;
-            f32x16 da = mma_nn<64>(sD + rb * 32 * LDH, LDH, sW1 + kb * 32, LDA, zero16());
+        // dW1 += dz1^T agg  (64 x DIN) ; d(agg) = dz1 W1  (TM x DIN)
 #pragma unroll
-            for (int reg = 0; reg < 16; ++reg) {
-                const int row = rb * 32 + acc_row(reg, l);
-                if (row < nv) dagg_out[(row0 + row) * DIN + kb * 32 + (l & 31)] = da[reg];
+        for (int q1 = 0; q1 < NW1; ++q1) {
+            const int sub = w + 4 * q1;
+            if (sub < NSUB1) {
+                const int jb = sub & 1, kb = sub >> 1;  // j-block (rows of dW1 / d(agg)), k-block
+                accW1[q1] = mma_tn<TM>(sD + jb * 32, LDH, sA + kb * 32, LDA, accW1[q1]);
+                f32x16 da = mma_nn<64>(sD + jb * 32 * LDH, LDH, sW1 + kb * 32, LDA, zero16());
+#pragma unroll
+                for (int reg = 0; reg < 16; ++reg) {
+                    const int row = jb * 32 + acc_row(reg, l);
+                    if (row < nv) dagg_out[(row0 + row) * DIN + kb * 32 + (l & 31)] = da[reg];
+                }
             }
         }
     }
@@ -496,12 +499,16 @@ __global__ __launch_bounds__(256) void gin_bwd_k(
         const int j = wr * 32 + acc_row(reg, l), k = wc * 32 + (l & 31);
         sl[j * 64 + k] = accW2[reg];
     }
-    if (w < NSUB1) {
-        const int jb = w & 1, kb = w >> 1;
 #pragma unroll
-        for (int reg = 0; reg < 16; ++reg) {
-            const int j = jb * 32 + acc_row(reg, l), k = kb * 32 + (l & 31);
-            sl[64 * 64 + j * DIN + k] = accW1[reg];
+    for (int q1 = 0; q1 < NW1; ++q1) {
+        const int sub = w + 4 * q1;
+        if (sub < NSUB1) {
+            const int jb = sub & 1, kb = sub >> 1;
+#pragma unroll
+            for (int reg = 0; reg < 16; ++reg) {
+                const int j = jb * 32 + acc_row(reg, l), kk = kb * 32 + (l & 31);
+                sl[64 * 64 + j * DIN + kk] = accW1[q1][reg];
+            }
         }
     }
     __shared__ float sB[2][4][64];
@@ -515,37 +522,6 @@ __global__ __launch_bounds__(256) void gin_bwd_k(
     }
 }
 
-// Fixed-order sum of the per-workgroup weight-gradient slabs in two stages:
-// stage 1 = (column block, group of kSlabGroup slabs) -> partial; stage 2 sums
-// the partials in group order.  Enough workgroups to spread over the chip and
-// at most 16 dependent adds per thread.
-constexpr int kSlabGroup = 16;
-
-__global__ __launch_bounds__(256) void slab_reduce1_k(const float *__restrict__ slab, int nslab,
-                                                      int64_t width, float *__restrict__ partial) {
-    const int64_t e = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
-    if (e >= width) return;
-    const int b0 = blockIdx.y * kSlabGroup;
-    const int b1 = b0 + kSlabGroup < nslab ? b0 + kSlabGroup : nslab;
-    float v[kSlabGroup];
-#pragma unroll
-    for (int j = 0; j < kSlabGroup; ++j) v[j] = (b0 + j < b1) ? slab[(int64_t)(b0 + j) * width + e] : 0.f;
-    float acc = 0.f;
-#pragma unroll
-    for (int j = 0; j < kSlabGroup; ++j) acc += v[j];
-    partial[(int64_t)blockIdx.y * width + e] = acc;
-}
-
-__global__ __launch_bounds__(256) void slab_reduce2_k(const float *__restrict__ partial,
-                                                      int ngroups, int64_t width,
-                                                      float *__restrict__ out) {
-    const int64_t e = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
-    if (e >= width) return;
-    double acc = 0.0;
-    for (int g = 0; g < ngroups; ++g) acc += partial[(int64_t)g * width + e];
-    out[e] = static_cast<float>(acc);
-}
-
 static int bwd_grid(int64_t ntiles) { return static_cast<int>(ntiles < 256 ? ntiles : 256); }
 
 }  // namespace scgib
@@ -555,9 +531,7 @@ using namespace scgib;
 extern "C" int64_t scgib_gin_tiles(int64_t n_nodes) { return (n_nodes + TM - 1) / TM; }
 
 extern "C" int64_t scgib_gin_slab_floats(int64_t n_nodes, int32_t d_in) {
-    const int64_t g = bwd_grid(scgib_gin_tiles(n_nodes));
-    const int64_t groups = (g + kSlabGroup - 1) / kSlabGroup;
-    return (g + groups) * (64 * 64 + 64 * d_in + 128);  // slabs + stage-1 partials
+    return static_cast<int64_t>(bwd_grid(scgib_gin_tiles(n_nodes))) * (64 * 64 + 64 * d_in + 128);
 }
 
 extern "C" int scgib_gin_layer_fwd(const float *h_in, int32_t d_in, const float *in_stat,
@@ -651,10 +625,47 @@ extern "C" int scgib_gin_layer_bwd(const float *dy, const float *z2, const float
     else
         gin_bwd_k<64><<<grid, 256, 0, st>>>(dy, z2, r, agg, stat, coef, w1, w2, n_nodes, nt, dagg, slab, dims);
     const int64_t width = 64 * 64 + 64 * d_in + 128;
-    const int groups = (grid + kSlabGroup - 1) / kSlabGroup;
-    float *partial = slab + static_cast<int64_t>(grid) * width;
-    const unsigned cb = static_cast<unsigned>((width + 255) / 256);
-    slab_reduce1_k<<<dim3(cb, groups), 256, 0, st>>>(slab, grid, width, partial);
-    slab_reduce2_k<<<dim3(cb), 256, 0, st>>>(partial, groups, width, wgrad);
+    launch_slab_reduce(slab, grid, width, wgrad, st);
     return launch_status();
+}
+
+// ---------------------------------------------------------------------------
+// Dense two-layer MLP of the head: the same tile kernels without the gather
+// and without BatchNorm (models.py:1055-1057, applied at :1174).
+// ---------------------------------------------------------------------------
+extern "C" int64_t scgib_mlp2_slab_floats(int64_t n_nodes, int32_t d_in) {
+    return scgib_gin_slab_floats(n_nodes, d_in);
+}
+
+extern "C" int scgib_mlp2_fwd(const float *x, int32_t d_in, int64_t n_nodes, const float *w1,
+                              const float *b1, const float *w2, const float *b2, float *r,
+                              float *out, const int32_t *dims, scgib_stream_t stream) {
+    if (n_nodes < 0 || (d_in != 64 && d_in != 128)) return SCGIB_EINVAL;
+    if (n_nodes == 0) return SCGIB_OK;
+    if (!x || !w1 || !b1 || !w2 || !b2 || !r || !out) return SCGIB_EINVAL;
+    const unsigned nt = static_cast<unsigned>(scgib_gin_tiles(n_nodes));
+    hipStream_t st = as_stream(stream);
+    if (d_in == 128)
+        gin_fwd_k<128, false, false><<<nt, 256, 0, st>>>(x, nullptr, nullptr, nullptr, nullptr, n_nodes, 0.f, w1, b1, w2, b2, nullptr, r, out, nullptr, dims);
+    else
+        gin_fwd_k<64, false, false><<<nt, 256, 0, st>>>(x, nullptr, nullptr, nullptr, nullptr, n_nodes, 0.f, w1, b1, w2, b2, nullptr, r, out, nullptr, dims);
+    return launch_status();
+}
+
+extern "C" int scgib_mlp2_bwd(const float *dout, const float *x, const float *r, int32_t d_in,
+                              const float *w1, const float *w2, int64_t n_nodes, float *dx,
+                              float *slab, float *wgrad, const int32_t *dims,
+                              scgib_stream_t stream) {
+    if (n_nodes <= 0 || (d_in != 64 && d_in != 128)) return SCGIB_EINVAL;
+    if (!dout || !x || !r || !w1 || !w2 || !dx || !slab || !wgrad) return SCGIB_EINVAL;
+    const int64_t nt = scgib_gin_tiles(n_nodes);
+    const int grid = bwd_grid(nt);
+    hipStream_t st = as_stream(stream);
+    if (d_in == 128)
+        gin_bwd_k<128, false><<<grid, 256, 0, st>>>(dout, nullptr, r, x, nullptr, nullptr, w1, w2, n_nodes, nt, dx, slab, dims);
+    else
+        gin_bwd_k<64, false><<<grid, 256, 0, st>>>(dout, nullptr, r, x, nullptr, nullptr, w1, w2, n_nodes, nt, dx, slab, dims);
+    const int rc = launch_status();
+    if (rc != SCGIB_OK) return rc;
+    return launch_slab_reduce(slab, grid, 64 * 64 + 64 * static_cast<int64_t>(d_in) + 128, wgrad, st);
 }

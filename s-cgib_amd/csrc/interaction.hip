@@ -509,7 +509,7 @@ extern "C" int scgib_interaction_bwd(
     const float *bn_running_mean, const float *bn_running_var, float bn_eps, int32_t training,
     const float *w2, const float *w_att, const float *z1, const float *lam,
     const float *logit, const float *stats, float *df, float *dt, float *ds, float *pgrad,
-    const float *g_klmean, int32_t pad_rows, scgib_stream_t stream) {
+    const float *g_klmean, int32_t pad_rows, float *pgrad_total, scgib_stream_t stream) {
     if (n_graphs < 0 || n_nodes < 0) return SCGIB_EINVAL;
     if (n_graphs == 0) return SCGIB_OK;
     if (n_graphs > 0x7fffffff) return SCGIB_EUNSUPPORTED;
@@ -525,5 +525,11 @@ extern "C" int scgib_interaction_bwd(
         g_im, g_z1, g_z2, g_kl, f, t, s, u_feat, graph_ptr, n_graphs, bn_gamma, bn_beta,
         bn_running_mean, bn_running_var, bn_eps, training, w2, w_att, z1, lam, logit, stats,
         df, dt, ds, pgrad, g_klmean, n_nodes);
+    if (pgrad_total) {
+        const int rc = launch_status();
+        if (rc != SCGIB_OK) return rc;
+        return launch_slab_reduce(pgrad, static_cast<int>(n_graphs), SCGIB_PGRAD_STRIDE,
+                                  pgrad_total, as_stream(stream));
+    }
     return launch_status();
 }

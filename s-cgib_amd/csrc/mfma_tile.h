@@ -1,0 +1,168 @@
+// Shared device helpers of the fp32 MFMA tile kernels (gin_layer.hip,
+// dense.hip): 64-row tiles in padded LDS, exact-f32 v_mfma_f32_32x32x2_f32
+// sub-tile products, latency-batched CSR gathers, weight staging.
+#pragma once
+
+#include "common.h"
+
+namespace scgib {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+constexpr int TM = 64;   // rows per tile
+constexpr int LDH = 65;  // LDS stride of 64-wide tiles
+
+__device__ __forceinline__ f32x16 zero16() {
+    f32x16 a;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) a[i] = 0.f;
+    return a;
+}
+
+__device__ __forceinline__ float4 ld4(const float *p) { return *reinterpret_cast<const float4 *>(p); }
+__device__ __forceinline__ void st4(float *p, float4 v) { *reinterpret_cast<float4 *>(p) = v; }
+__device__ __forceinline__ float4 add4(float4 a, float4 b) { return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w); }
+__device__ __forceinline__ float4 xform4(float4 z, float4 a, float4 b) {
+    return make_float4(fmaxf(a.x * z.x + b.x, 0.f), fmaxf(a.y * z.y + b.y, 0.f),
+                       fmaxf(a.z * z.z + b.z, 0.f), fmaxf(a.w * z.w + b.w, 0.f));
+}
+
+// Stage a [64][COLS] row-major matrix into LDS (row stride COLS + 1).
+template <int COLS>
+__device__ __forceinline__ void stage_matrix(const float *__restrict__ w, float *s) {
+    constexpr int LD = COLS + 1, N = 64 * COLS / 4 / 256;
+    const int tid = threadIdx.x;
+    float4 a[N];
+#pragma unroll
+    for (int k = 0; k < N; ++k) a[k] = reinterpret_cast<const float4 *>(w)[tid + 256 * k];
+#pragma unroll
+    for (int k = 0; k < N; ++k) {
+        const int idx = 4 * (tid + 256 * k), row = idx / COLS, cc = idx % COLS;
+        float *d = s + row * LD + cc;
+        d[0] = a[k].x; d[1] = a[k].y; d[2] = a[k].z; d[3] = a[k].w;
+    }
+}
+
+// Stage W1 [64][DIN] and W2 [64][64] (torch Linear layout) into padded LDS
+// tiles with 16-byte global loads, all issued before the first store.
+template <int DIN>
+__device__ __forceinline__ void stage_weights(const float *__restrict__ w1,
+                                              const float *__restrict__ w2, float *sW1,
+                                              float *sW2) {
+    constexpr int LDA = DIN + 1, N1 = 64 * DIN / 4 / 256, N2 = 64 * 64 / 4 / 256;
+    const int tid = threadIdx.x;
+    float4 a[N1], b[N2];
+#pragma unroll
+    for (int k = 0; k < N1; ++k) a[k] = reinterpret_cast<const float4 *>(w1)[tid + 256 * k];
+#pragma unroll
+    for (int k = 0; k < N2; ++k) b[k] = reinterpret_cast<const float4 *>(w2)[tid + 256 * k];
+#pragma unroll
+    for (int k = 0; k < N1; ++k) {
+        const int idx = 4 * (tid + 256 * k), row = idx / DIN, cc = idx % DIN;
+        float *d = sW1 + row * LDA + cc;
+        d[0] = a[k].x; d[1] = a[k].y; d[2] = a[k].z; d[3] = a[k].w;
+    }
+#pragma unroll
+    for (int k = 0; k < N2; ++k) {
+        const int idx = 4 * (tid + 256 * k), row = idx >> 6, cc = idx & 63;
+        float *d = sW2 + row * LDH + cc;
+        d[0] = b[k].x; d[1] = b[k].y; d[2] = b[k].z; d[3] = b[k].w;
+    }
+}
+
+
+// Sum aggregation of RPT rows (row0 + rbase + k * RPP) for one 4-channel
+// chunk c: out = ope * x[v] + sum_{u in N(v)} x[u] in CSR order, x optionally
+// relu(sc * h + sh).  Neighbour indices are fetched 4 per row per round with
+// all rows' loads in flight; rows >= nv give 0.
+template <int RPT, int RPP, int LPR, bool XFORM>
+__device__ __forceinline__ void gather_rows(const float4 *__restrict__ h4,
+                                            const int32_t *__restrict__ rowptr,
+                                            const int32_t *__restrict__ col, int64_t row0, int nv,
+                                            int rbase, int c, float ope, float4 sc, float4 sh,
+                                            float4 (&acc)[RPT]) {
+    int32_t beg[RPT], deg[RPT];
+    float4 self[RPT];
+    int maxdeg = 0;
+#pragma unroll
+    for (int k = 0; k < RPT; ++k) {
+        const int rr = rbase + k * RPP;
+        const int64_t v = row0 + rr;
+        beg[k] = 0;
+        deg[k] = 0;
+        self[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (rr < nv) {
+            beg[k] = rowptr[v];
+            deg[k] = rowptr[v + 1] - beg[k];
+            self[k] = h4[v * LPR + c];
+        }
+        acc[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int k = 0; k < RPT; ++k) maxdeg = deg[k] > maxdeg ? deg[k] : maxdeg;
+    for (int j0 = 0; j0 < maxdeg; j0 += 4) {
+        int64_t u[RPT][4];
+#pragma unroll
+        for (int k = 0; k < RPT; ++k)
+#pragma unroll
+            for (int t = 0; t < 4; ++t) u[k][t] = j0 + t < deg[k] ? col[beg[k] + j0 + t] : -1;
+        float4 a[RPT][4];
+#pragma unroll
+        for (int k = 0; k < RPT; ++k)
+#pragma unroll
+            for (int t = 0; t < 4; ++t) a[k][t] = u[k][t] >= 0 ? h4[u[k][t] * LPR + c] : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+        for (int k = 0; k < RPT; ++k)
+#pragma unroll
+            for (int t = 0; t < 4; ++t)
+                if (u[k][t] >= 0) acc[k] = add4(acc[k], XFORM ? xform4(a[k][t], sc, sh) : a[k][t]);
+    }
+#pragma unroll
+    for (int k = 0; k < RPT; ++k) {
+        const float4 x = XFORM ? xform4(self[k], sc, sh) : self[k];
+        acc[k] = make_float4(ope * x.x + acc[k].x, ope * x.y + acc[k].y, ope * x.z + acc[k].z,
+                             ope * x.w + acc[k].w);
+        if (rbase + k * RPP >= nv) acc[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+}
+
+// C(i, j) += sum_k A(i, k) B(k, j) over K, 32x32 tile, with
+//   NT: A(i,k) = As[i*lda + k],   B(k,j) = Bs[j*ldb + k]
+//   NN: A(i,k) = As[i*lda + k],   B(k,j) = Bs[k*ldb + j]
+//   TN: A(i,k) = As[k*lda + i],   B(k,j) = Bs[k*ldb + j]   (sum over rows k)
+// (lane l supplies i or j = l & 31 and k-offset l >> 5 of each K=2 step)
+template <int K>
+__device__ __forceinline__ f32x16 mma_nt(const float *As, int lda, const float *Bs, int ldb,
+                                         f32x16 acc) {
+    const int l = threadIdx.x & 63, i = l & 31, kk = l >> 5;
+#pragma unroll 8
+    for (int k = 0; k < K; k += 2)
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(As[i * lda + k + kk], Bs[i * ldb + k + kk], acc, 0, 0, 0);
+    return acc;
+}
+
+template <int K>
+__device__ __forceinline__ f32x16 mma_nn(const float *As, int lda, const float *Bs, int ldb,
+                                         f32x16 acc) {
+    const int l = threadIdx.x & 63, i = l & 31, kk = l >> 5;
+#pragma unroll 8
+    for (int k = 0; k < K; k += 2)
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(As[i * lda + k + kk], Bs[(k + kk) * ldb + i], acc, 0, 0, 0);
+    return acc;
+}
+
+template <int K>
+__device__ __forceinline__ f32x16 mma_tn(const float *As, int lda, const float *Bs, int ldb,
+                                         f32x16 acc) {
+    const int l = threadIdx.x & 63, i = l & 31, kk = l >> 5;
+#pragma unroll 8
+    for (int k = 0; k < K; k += 2)
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(As[(k + kk) * lda + i], Bs[(k + kk) * ldb + i], acc, 0, 0, 0);
+    return acc;
+}
+
+// row of accumulator register `reg` of the 32x32 output tile held by lane l
+__device__ __forceinline__ int acc_row(int reg, int l) { return (reg & 3) + 8 * (reg >> 2) + 4 * (l >> 5); }
+
+
+}  // namespace scgib

@@ -184,12 +184,11 @@ class _SCGIBCore(nn.Module):
             graph_features, subgraphs_features, sub_readout = encoded
         enc_owner.graph_features = graph_features
         enc_owner.subgraphs_features = subgraphs_features
-        t = enc_owner.compressor[0](graph_features)
         u_gate, u_feat = self._noise(graph_features.shape[0], graph_features.device, noise)
-        im, z1, z2, kl, kl_mean = ops.interaction(graph_features, t, sub_readout, u_gate, u_feat,
-                                                  enc_owner.compressor[1], enc_owner.compressor[3],
-                                                  enc_owner.attn_layer, batch_g,
-                                                  enc_owner.training)
+        # compressor[0] (models.py:1092) runs fused in front of the interaction
+        im, z1, z2, kl, kl_mean = ops.interaction_lin(graph_features, sub_readout, u_gate, u_feat,
+                                                      enc_owner.compressor, enc_owner.attn_layer,
+                                                      batch_g, enc_owner.training)
         enc_owner._last_kl_mean = kl_mean
         noisy = im[:, : self.hidden_dim]
         return im, kl, noisy, z2, z1
@@ -218,7 +217,7 @@ class _SCGIBCore(nn.Module):
         return ego, (graph_features, subgraphs_features, sub_readout)
 
     def _losses(self, batch_g, im, kl_mean, z1, z2, mlp, batch_size):
-        im = mlp(im)
+        im = ops.mlp2(im, mlp, batch_g.dims)  # models.py:1174, fused
         kl_loss = kl_mean  # == torch.mean(KL_tensor) (models.py:679), computed in-kernel
         con = semi_loss(z1, z2, batch_size)
         if self.recons_type == "adj":

@@ -393,3 +393,26 @@ def test_contrastive_fwd_bwd(pkg, dev, B):
             ref = 3.0 * ref
             err = (mine.cpu().double() - ref).norm()
             assert err <= 1e-5 * max(ref.norm().item(), 1e-2), rep
+
+
+# ---------------------------------------------------------------------------
+# A10 head: fused interaction-map MLP vs fp64 torch
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("d_in,n", [(128, 1), (128, 63), (128, 9300), (64, 1000)])
+def test_mlp2_fwd_bwd(pkg, dev, d_in, n):
+    torch.manual_seed(n + d_in)
+    mlp = torch.nn.Sequential(torch.nn.Linear(d_in, 64), torch.nn.ReLU(), torch.nn.Linear(64, 64))
+    x = torch.randn(n, d_in)
+    gout = torch.randn(n, 64)
+    ref = [p.detach().double().clone().requires_grad_(True) for p in mlp.parameters()]
+    xr = x.double().requires_grad_(True)
+    out_r = F.linear(F.relu(F.linear(xr, ref[0], ref[1])), ref[2], ref[3])
+    (out_r * gout.double()).sum().backward()
+    mlp_d = mlp.to(dev)
+    xd = x.to(dev).requires_grad_(True)
+    out = pkg.ops.mlp2(xd, mlp_d)
+    (out * gout.to(dev)).sum().backward()
+    assert rel_l2(out.detach().cpu(), out_r.detach()) < 1e-6
+    assert rel_l2(xd.grad.cpu(), xr.grad) < 1e-5
+    for p, r in zip(mlp_d.parameters(), ref):
+        assert rel_l2(p.grad.cpu(), r.grad) < 1e-5

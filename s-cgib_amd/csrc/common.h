@@ -44,6 +44,16 @@ __device__ __forceinline__ int64_t xcd_remap(int64_t orig, int64_t nwg) {
     return base + orig / 8;
 }
 
+// Batched loads: a load written as `ok ? p[i] : 0` is compiled into its own
+// branch with an s_waitcnt inside, which serialises a batch of such loads.
+// The kernels instead load unconditionally from a clamped, always-valid index
+// and apply the predicate to the value (ld_ok), so a batch stays in flight.
+template <class T>
+__device__ __forceinline__ T ld_ok(const T *p, int64_t i, int64_t safe, bool ok, T zero) {
+    const T v = p[ok ? i : safe];
+    return ok ? v : zero;
+}
+
 // Capacity mode: when `dims` (device int32) is given, dims[idx] is the actual
 // count and `cap` (host) only sizes the grid; rows in [actual, cap) are
 // written as zeros so padded buffers stay finite under graph replay.

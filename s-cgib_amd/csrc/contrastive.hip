@@ -50,8 +50,8 @@ __device__ __forceinline__ void stage_tile(const float *__restrict__ x, int64_t 
     float ss = 0.f;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-        v[k] = j < B ? reinterpret_cast<const float4 *>(x + j * 64 + 16 * q)[k]
-                     : make_float4(0.f, 0.f, 0.f, 0.f);
+        v[k] = ld_ok(reinterpret_cast<const float4 *>(x), j * 16 + 4 * q + k, 4 * q + k, j < B,
+                     make_float4(0.f, 0.f, 0.f, 0.f));
         ss += v[k].x * v[k].x + v[k].y * v[k].y + v[k].z * v[k].z + v[k].w * v[k].w;
     }
     ss += __shfl_xor(ss, 1, kWave);
@@ -69,7 +69,7 @@ __device__ __forceinline__ float load_row(const float *__restrict__ x, int64_t i
     float ss = 0.f;
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
-        q[k] = i < B ? reinterpret_cast<const float4 *>(x + i * 64)[k] : make_float4(0.f, 0.f, 0.f, 0.f);
+        q[k] = ld_ok(reinterpret_cast<const float4 *>(x), i * 16 + k, k, i < B, make_float4(0.f, 0.f, 0.f, 0.f));
         ss += q[k].x * q[k].x + q[k].y * q[k].y + q[k].z * q[k].z + q[k].w * q[k].w;
     }
     const float inv = 1.f / fmaxf(sqrtf(ss), kNormEps);

@@ -34,7 +34,8 @@ __global__ __launch_bounds__(256) void linear_fwd_k(const float *__restrict__ x,
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             const int idx = tid + 256 * k, rr = idx >> 4, cq = idx & 15;
-            v[k] = rr < nv ? ld4(x + (row0 + rr) * 64 + 4 * cq) : make_float4(0.f, 0.f, 0.f, 0.f);
+            v[k] = ld_ok(reinterpret_cast<const float4 *>(x), (row0 + rr) * 16 + cq, row0 * 16 + cq,
+                         rr < nv, make_float4(0.f, 0.f, 0.f, 0.f));
         }
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
@@ -82,9 +83,10 @@ __global__ __launch_bounds__(256) void linear_bwd_k(
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             const int idx = tid + 256 * k, rr = idx >> 4, cq = idx & 15;
-            const int64_t o = (row0 + rr) * 64 + 4 * cq;
-            vd[k] = rr < nv ? ld4(dy + o) : make_float4(0.f, 0.f, 0.f, 0.f);
-            va[k] = rr < nv ? ld4(x + o) : make_float4(0.f, 0.f, 0.f, 0.f);
+            const int64_t o = (row0 + rr) * 16 + cq, so = row0 * 16 + cq;
+            const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+            vd[k] = ld_ok(reinterpret_cast<const float4 *>(dy), o, so, rr < nv, z4);
+            va[k] = ld_ok(reinterpret_cast<const float4 *>(x), o, so, rr < nv, z4);
         }
         __syncthreads();  // previous tile's LDS reads are done
 #pragma unroll

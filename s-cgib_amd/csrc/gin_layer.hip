@@ -83,7 +83,8 @@ __global__ __launch_bounds__(256) void gin_fwd_k(
 #pragma unroll
         for (int k = 0; k < AK; ++k) {
             const int idx = tid + 256 * k, rr = idx / AQ, cq = idx % AQ;
-            va[k] = rr < nv ? ld4(h + (row0 + rr) * DIN + 4 * cq) : make_float4(0.f, 0.f, 0.f, 0.f);
+            va[k] = ld_ok(reinterpret_cast<const float4 *>(h), (row0 + rr) * AQ + cq, row0 * AQ + cq,
+                          rr < nv, make_float4(0.f, 0.f, 0.f, 0.f));
         }
 #pragma unroll
         for (int k = 0; k < AK; ++k) {
@@ -199,7 +200,7 @@ __global__ __launch_bounds__(1024) void bn_finalize_k(
         for (int64_t t0 = p; t0 < ntiles; t0 += 16 * 8) {
             float S[8];
 #pragma unroll
-            for (int u = 0; u < 8; ++u) S[u] = t0 + 16 * u < ntiles ? part[(t0 + 16 * u) * 128 + c] : 0.f;
+            for (int u = 0; u < 8; ++u) S[u] = ld_ok(part, (t0 + 16 * u) * 128 + c, c, t0 + 16 * u < ntiles, 0.f);
 #pragma unroll
             for (int u = 0; u < 8; ++u) a += static_cast<double>(S[u]);
         }
@@ -214,8 +215,8 @@ __global__ __launch_bounds__(1024) void bn_finalize_k(
 #pragma unroll
             for (int u = 0; u < 8; ++u) {
                 const int64_t t = t0 + 16 * u;
-                S[u] = t < ntiles ? part[t * 128 + c] : 0.f;
-                Q[u] = t < ntiles ? part[t * 128 + 64 + c] : 0.f;
+                S[u] = ld_ok(part, t * 128 + c, c, t < ntiles, 0.f);
+                Q[u] = ld_ok(part, t * 128 + 64 + c, 64 + c, t < ntiles, 0.f);
             }
 #pragma unroll
             for (int u = 0; u < 8; ++u) {
@@ -289,32 +290,41 @@ __global__ __launch_bounds__(256) void gin_bwd_stats_k(
     const float4 sc = ld4(stat + 128 + 4 * c), sh = ld4(stat + 192 + 4 * c);
     const float4 *g4 = reinterpret_cast<const float4 *>(dh);
     const int nv = static_cast<int>(n - row0 < TM ? (n - row0 > 0 ? n - row0 : 0) : TM);
+    if (nv == 0) {  // capacity mode: a tile of padding rows (block-uniform)
+        for (int rr = slot; rr < TM && row0 + rr < ncap; rr += 16)
+            st4(dy_out + (row0 + rr) * 64 + 4 * c, make_float4(0.f, 0.f, 0.f, 0.f));
+        return;
+    }
     float4 g[4];
     if (GATHER) {
         gather_rows<4, 16, 16, false>(g4, rowptr_t, col_t, row0, nv, slot, c, ope, sc, sh, g);
     } else {
 #pragma unroll
-        for (int k = 0; k < 4; ++k)
-            g[k] = slot + 16 * k < nv ? g4[(row0 + slot + 16 * k) * 16 + c] : make_float4(0.f, 0.f, 0.f, 0.f);
+        for (int k = 0; k < 4; ++k) {
+            const int rr = slot + 16 * k;
+            g[k] = g4[(row0 + (rr < nv ? rr : nv - 1)) * 16 + c];
+        }
     }
+    // rows past nv: the gather duplicated row nv - 1; z is read at that row
+    // and dy is multiplied by 0 (no predicate, so the loads stay batched)
     float4 z[4];
 #pragma unroll
-    for (int k = 0; k < 4; ++k)
-        z[k] = slot + 16 * k < nv ? ld4(z2 + (row0 + slot + 16 * k) * 64 + 4 * c) : make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int k = 0; k < 4; ++k) {
+        const int rr = slot + 16 * k;
+        z[k] = ld4(z2 + (row0 + (rr < nv ? rr : nv - 1)) * 64 + 4 * c);
+    }
     float4 sdy = make_float4(0.f, 0.f, 0.f, 0.f), sdx = sdy;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
         const int rr = slot + 16 * k;
         const int64_t v = row0 + rr;
-        if (v >= ncap) break;
-        if (rr >= nv) {
-            st4(dy_out + v * 64 + 4 * c, make_float4(0.f, 0.f, 0.f, 0.f));
-            continue;
-        }
+        const float valid = rr < nv ? 1.f : 0.f;
         const float4 zz = z[k], gg = g[k];
-        const float4 dy = make_float4(sc.x * zz.x + sh.x > 0.f ? gg.x : 0.f, sc.y * zz.y + sh.y > 0.f ? gg.y : 0.f,
-                                      sc.z * zz.z + sh.z > 0.f ? gg.z : 0.f, sc.w * zz.w + sh.w > 0.f ? gg.w : 0.f);
-        st4(dy_out + v * 64 + 4 * c, dy);
+        const float4 dy = make_float4((sc.x * zz.x + sh.x > 0.f ? gg.x : 0.f) * valid,
+                                      (sc.y * zz.y + sh.y > 0.f ? gg.y : 0.f) * valid,
+                                      (sc.z * zz.z + sh.z > 0.f ? gg.z : 0.f) * valid,
+                                      (sc.w * zz.w + sh.w > 0.f ? gg.w : 0.f) * valid);
+        if (v < ncap) st4(dy_out + v * 64 + 4 * c, dy);
         sdy = add4(sdy, dy);
         sdx = add4(sdx, make_float4(dy.x * (zz.x - mean.x) * istd.x, dy.y * (zz.y - mean.y) * istd.y,
                                     dy.z * (zz.z - mean.z) * istd.z, dy.w * (zz.w - mean.w) * istd.w));
@@ -349,8 +359,8 @@ __global__ __launch_bounds__(1024) void bn_bwd_finalize_k(const float *__restric
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
             const int64_t t = t0 + 16 * u;
-            A[u] = t < ntiles ? part[t * 128 + c] : 0.f;
-            Bv[u] = t < ntiles ? part[t * 128 + 64 + c] : 0.f;
+            A[u] = ld_ok(part, t * 128 + c, c, t < ntiles, 0.f);
+            Bv[u] = ld_ok(part, t * 128 + 64 + c, 64 + c, t < ntiles, 0.f);
         }
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
@@ -427,15 +437,17 @@ __global__ __launch_bounds__(256) void gin_bwd_k(
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             const int rr = rs + 16 * k;
-            const int64_t o = (row0 + rr) * 64 + 4 * c4;
-            vz[k] = BN && rr < nv ? ld4(z2 + o) : zero;
-            vd[k] = rr < nv ? ld4(dy + o) : zero;
-            vr[k] = rr < nv ? ld4(r + o) : zero;
+            const int64_t o = (row0 + rr) * 16 + c4, so = row0 * 16 + c4;
+            if (BN) vz[k] = ld_ok(reinterpret_cast<const float4 *>(z2), o, so, rr < nv, zero);
+            else vz[k] = zero;
+            vd[k] = ld_ok(reinterpret_cast<const float4 *>(dy), o, so, rr < nv, zero);
+            vr[k] = ld_ok(reinterpret_cast<const float4 *>(r), o, so, rr < nv, zero);
         }
 #pragma unroll
         for (int k = 0; k < AK; ++k) {
             const int idx = tid + 256 * k, rr = idx / AQ, cq = idx % AQ;
-            va[k] = rr < nv ? ld4(agg + (row0 + rr) * DIN + 4 * cq) : zero;
+            va[k] = ld_ok(reinterpret_cast<const float4 *>(agg), (row0 + rr) * AQ + cq, row0 * AQ + cq,
+                          rr < nv, zero);
         }
         __syncthreads();  // previous tile's LDS reads are done
         // dz2 = scale (dy - c1 - xhat c2); rows past n are zero

@@ -71,10 +71,23 @@ __device__ __forceinline__ void stage_weights(const float *__restrict__ w1,
 }
 
 
+__device__ __forceinline__ float4 fma4(float4 a, float w, float4 acc) {
+    return make_float4(fmaf(a.x, w, acc.x), fmaf(a.y, w, acc.y), fmaf(a.z, w, acc.z),
+                       fmaf(a.w, w, acc.w));
+}
+
 // Sum aggregation of RPT rows (row0 + rbase + k * RPP) for one 4-channel
 // chunk c: out = ope * x[v] + sum_{u in N(v)} x[u] in CSR order, x optionally
-// relu(sc * h + sh).  Neighbour indices are fetched 4 per row per round with
-// all rows' loads in flight; rows >= nv give 0.
+// relu(sc * h + sh).  Requires nv >= 1.
+//
+// Latency: all rows' row pointers and self rows are loaded together, then per
+// round 4 neighbour indices per row, then those neighbour rows — every load
+// unconditional so that each batch stays in flight (a load whose value is only
+// used under a predicate gets sunk into a branch with its own s_waitcnt):
+//   * rows past nv duplicate row nv - 1 (computed, never stored by callers);
+//   * neighbour slots past a row's degree read a clamped valid edge of this
+//     thread's rows and enter through fmaf(x, 0, acc) — exact: x * 1 and
+//     acc + x * 0 round like the plain add for finite x.
 template <int RPT, int RPP, int LPR, bool XFORM>
 __device__ __forceinline__ void gather_rows(const float4 *__restrict__ h4,
                                             const int32_t *__restrict__ rowptr,
@@ -83,46 +96,50 @@ __device__ __forceinline__ void gather_rows(const float4 *__restrict__ h4,
                                             float4 (&acc)[RPT]) {
     int32_t beg[RPT], deg[RPT];
     float4 self[RPT];
-    int maxdeg = 0;
+    int64_t vrow[RPT];
 #pragma unroll
     for (int k = 0; k < RPT; ++k) {
         const int rr = rbase + k * RPP;
-        const int64_t v = row0 + rr;
-        beg[k] = 0;
-        deg[k] = 0;
-        self[k] = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (rr < nv) {
-            beg[k] = rowptr[v];
-            deg[k] = rowptr[v + 1] - beg[k];
-            self[k] = h4[v * LPR + c];
-        }
+        vrow[k] = row0 + (rr < nv ? rr : nv - 1);
+        beg[k] = rowptr[vrow[k]];
+        deg[k] = rowptr[vrow[k] + 1];
+        self[k] = h4[vrow[k] * LPR + c];
         acc[k] = make_float4(0.f, 0.f, 0.f, 0.f);
     }
+    int maxdeg = 0, maxend = 0;
 #pragma unroll
-    for (int k = 0; k < RPT; ++k) maxdeg = deg[k] > maxdeg ? deg[k] : maxdeg;
+    for (int k = 0; k < RPT; ++k) {
+        maxend = deg[k] > maxend ? deg[k] : maxend;
+        deg[k] -= beg[k];
+        maxdeg = deg[k] > maxdeg ? deg[k] : maxdeg;
+    }
     for (int j0 = 0; j0 < maxdeg; j0 += 4) {
-        int64_t u[RPT][4];
+        int32_t u[RPT][4];
 #pragma unroll
         for (int k = 0; k < RPT; ++k)
 #pragma unroll
-            for (int t = 0; t < 4; ++t) u[k][t] = j0 + t < deg[k] ? col[beg[k] + j0 + t] : -1;
+            for (int t = 0; t < 4; ++t) {
+                const int32_t e = beg[k] + j0 + t;
+                u[k][t] = col[e < maxend ? e : maxend - 1];
+            }
         float4 a[RPT][4];
 #pragma unroll
         for (int k = 0; k < RPT; ++k)
 #pragma unroll
-            for (int t = 0; t < 4; ++t) a[k][t] = u[k][t] >= 0 ? h4[u[k][t] * LPR + c] : make_float4(0.f, 0.f, 0.f, 0.f);
+            for (int t = 0; t < 4; ++t) a[k][t] = h4[static_cast<int64_t>(u[k][t]) * LPR + c];
 #pragma unroll
         for (int k = 0; k < RPT; ++k)
 #pragma unroll
-            for (int t = 0; t < 4; ++t)
-                if (u[k][t] >= 0) acc[k] = add4(acc[k], XFORM ? xform4(a[k][t], sc, sh) : a[k][t]);
+            for (int t = 0; t < 4; ++t) {
+                const float w = j0 + t < deg[k] ? 1.f : 0.f;
+                acc[k] = fma4(XFORM ? xform4(a[k][t], sc, sh) : a[k][t], w, acc[k]);
+            }
     }
 #pragma unroll
     for (int k = 0; k < RPT; ++k) {
         const float4 x = XFORM ? xform4(self[k], sc, sh) : self[k];
         acc[k] = make_float4(ope * x.x + acc[k].x, ope * x.y + acc[k].y, ope * x.z + acc[k].z,
                              ope * x.w + acc[k].w);
-        if (rbase + k * RPP >= nv) acc[k] = make_float4(0.f, 0.f, 0.f, 0.f);
     }
 }
 

@@ -18,7 +18,8 @@ __global__ __launch_bounds__(1024) void slab_reduce_k(const float *__restrict__ 
         for (int b0 = sp; b0 < nslab; b0 += 16 * 8) {
             float v[8];
 #pragma unroll
-            for (int u = 0; u < 8; ++u) v[u] = b0 + 16 * u < nslab ? slab[static_cast<int64_t>(b0 + 16 * u) * width + e] : 0.f;
+            for (int u = 0; u < 8; ++u)
+                v[u] = ld_ok(slab, static_cast<int64_t>(b0 + 16 * u) * width + e, e, b0 + 16 * u < nslab, 0.f);
 #pragma unroll
             for (int u = 0; u < 8; ++u) acc += v[u];
         }

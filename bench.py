@@ -35,9 +35,31 @@ pkg = importlib.import_module("s-cgib_amd")
 
 HBM_PEAK_GBS = 8000.0       # MI355X spec (MI355X_MICROARCH.md:36)
 HBM_MEASURED_GBS = 6290.0   # float4 copy, same file
-# HBM bytes per launch from rocprofv3 PMC passes (profiles/, corrected per
-# MI355X_MICROARCH.md: 2 x FETCH_SIZE + WRITE_SIZE); filled by tools/pmc_summary.py
-TRAFFIC = {}
+# HBM bytes per launch of each kernel from the rocprofv3 PMC passes of
+# tools/gpu_pmc.sh (2 x FETCH_SIZE + WRITE_SIZE, MI355X_MICROARCH.md "HBM
+# [CDNA4]"), committed under profiles/ — the bench itself runs unprofiled.
+TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r01_pmc", "traffic.json")
+
+
+def _traffic():
+    try:
+        with open(TRAFFIC_FILE) as fh:
+            return json.load(fh)
+    except (OSError, ValueError):
+        return {}
+
+
+TRAFFIC = _traffic()
+
+
+def traffic_of(variants):
+    """Dispatch-weighted mean HBM bytes per launch over the given template
+    instantiations (e.g. the GIN variants of gin_bwd_k, not the MLP one)."""
+    got = [TRAFFIC[v] for v in variants if v in TRAFFIC]
+    n = sum(g["dispatches"] for g in got)
+    if not n:
+        return None
+    return round(sum(g["traffic_bytes"] * g["dispatches"] for g in got) / n)
 METRIC = "graphs/sec (pretrain step, GIN-64×5, k=1) at 1/2/4/8 MI355X; % HBM roofline"
 
 
@@ -55,40 +77,63 @@ def make_model(F_in, k, gin_layers, dev):
     return model.to(dev).train()
 
 
+F32_MFMA_PEAK_TFLOPS = 157.3  # dense fp32 MFMA (MI355X_MICROARCH.md)
+
+
 def layer_fwd_bytes(n, e, d_in):
-    """Algorithmic bytes of one gin_fwd_k launch: the gather (neighbour + self
-    rows, col + rowptr), the MLP weights, and the agg / r / z2 / tile-stat
-    writes."""
-    return (agg_bytes(n, e, d_in) - 4 * d_in * n          # gather reads + indices
-            + 4 * (64 * d_in + 64 + 64 * 64 + 64)          # W1, b1, W2, b2
+    """Algorithmic bytes of one gin_fwd_k launch: the gather
+    (neighbour + self rows, col + rowptr), W1/b1/W2/b2, the agg / r / z2
+    writes and the per-tile BN statistics."""
+    return (4 * d_in * (e + n) + 4 * e + 4 * (n + 1)
+            + 4 * (64 * d_in + 64 + 64 * 64 + 64)
             + 4 * n * (d_in + 64 + 64) + 512 * ((n + 63) // 64))
 
 
-def layer_fwd_flops(n, d_in):
+def layer_fwd_flops(n, e, d_in):
     return 2 * n * 64 * (d_in + 64)
 
 
-class KernelTimer:
-    """HIP-event timing of every launch of one C-ABI entry point (routed
-    through ops._launch) on the stream it is launched on (torch's current
-    stream).  A ~170 us spin kernel is queued ahead of each bracketed launch
-    so the GPU is still busy while the host submits [start event, kernel, end
-    event]: the events bracket the kernel, not the host's launch latency."""
+def layer_bwd_bytes(n, e, d_in):
+    """Algorithmic bytes of one gin_bwd_k launch: dy, z2, r and
+    agg tiles read, W1/W2 + BN coefficients, d(agg) written, one dW/db slab
+    per workgroup written."""
+    slabs = min((n + 63) // 64, 256)
+    return (4 * n * (3 * 64 + d_in) + 4 * (64 * d_in + 64 * 64 + 6 * 64)
+            + 4 * n * d_in + 4 * slabs * (64 * 64 + 64 * d_in + 128))
 
-    def __init__(self, name):
-        self.name = name
-        self.records = []  # (start_event, end_event, meta)
+
+def layer_bwd_flops(n, e, d_in):
+    return 4 * n * 64 * (64 + d_in)  # dW2, dr, dW1, d(agg)
+
+
+class KernelTimer:
+    """HIP-event timing of every launch of the given C-ABI entry points
+    (routed through ops._launch) on the stream they are launched on (torch's
+    current stream).  A ~170 us spin kernel is queued ahead of each bracketed
+    launch so the GPU is still busy while the host submits [start event,
+    kernel, end event]: the events bracket the kernel, not the host's launch
+    latency."""
+
+    REPEAT = 10  # back-to-back launches per bracket (the kernels are idempotent)
+
+    def __init__(self, *names):
+        self.names = set(names)
+        self.records = {n: [] for n in names}  # name -> [(start, end, meta)]
 
     def __enter__(self):
         def observe(name, meta, launch):
-            if name != self.name:
+            if name not in self.names:
                 return launch()
             s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             torch.cuda._sleep(400_000)
             s.record()
-            rc = launch()
+            # the timed kernels read only their inputs and overwrite their
+            # outputs, so repeating the launch leaves the results unchanged;
+            # REPEAT launches per bracket amortise the event/dispatch latency
+            for _ in range(self.REPEAT):
+                rc = launch()
             e.record()
-            self.records.append((s, e, meta))
+            self.records[name].append((s, e, meta))
             return rc
 
         pkg.ops.OBSERVER = observe
@@ -97,13 +142,38 @@ class KernelTimer:
     def __exit__(self, *exc):
         pkg.ops.OBSERVER = None
 
-    def summary(self, bytes_fn, flops_fn):
+    def summary(self, name, bytes_fn, flops_fn):
         torch.cuda.synchronize()
-        ms = [s.elapsed_time(e) for s, e, _ in self.records]
-        byts = [bytes_fn(m["n"], m["e"], m["d_in"]) for _, _, m in self.records]
-        fl = [flops_fn(m["n"], m["d_in"]) for _, _, m in self.records]
+        rec = self.records[name]
+        ms = [s.elapsed_time(e) / self.REPEAT for s, e, _ in rec]
+        byts = [bytes_fn(m["n"], m["e"], m["d_in"]) for _, _, m in rec]
+        fl = [flops_fn(m["n"], m["e"], m["d_in"]) for _, _, m in rec]
         k = len(ms)
-        return sum(byts) / k, sum(fl) / k, sum(ms) / k, k
+        avg_ms = sum(ms) / k
+        avg_b, avg_f = sum(byts) / k, sum(fl) / k
+        gbs = avg_b / (avg_ms * 1e-3) / 1e9
+        tfs = avg_f / (avg_ms * 1e-3) / 1e12
+        hbm_frac, mfma_frac = gbs / HBM_PEAK_GBS, tfs / F32_MFMA_PEAK_TFLOPS
+        return {"avg_bytes": avg_b, "avg_flops": avg_f, "avg_ms": avg_ms, "launches": k,
+                "gbs": gbs, "tflops": tfs, "hbm_frac": hbm_frac, "mfma_frac": mfma_frac}
+
+
+def roofline_entry(kernel, desc, r, variants):
+    """`roofline` object: bound = the resource this kernel is closer to
+    saturating (the two fractions are both reported)."""
+    if r["mfma_frac"] > r["hbm_frac"]:
+        bound, ach, peak, unit = "mfma", r["tflops"], F32_MFMA_PEAK_TFLOPS, "TFLOP/s"
+    else:
+        bound, ach, peak, unit = "hbm", r["gbs"], HBM_PEAK_GBS, "GB/s"
+    return {"bound": bound, "kernel": f"{kernel} ({desc})", "achieved": round(ach, 2),
+            "peak": peak, "unit": unit, "frac": round(ach / peak, 4),
+            "traffic": traffic_of(variants),
+            "hbm_gbs": round(r["gbs"], 1), "hbm_frac": round(r["hbm_frac"], 4),
+            "hbm_frac_vs_measured_copy": round(r["gbs"] / HBM_MEASURED_GBS, 4),
+            "mfma_f32_tflops": round(r["tflops"], 2), "mfma_frac": round(r["mfma_frac"], 4),
+            "avg_launch_us": round(r["avg_ms"] * 1e3, 3),
+            "avg_bytes_per_launch": int(r["avg_bytes"]),
+            "avg_flops_per_launch": int(r["avg_flops"]), "launches_timed": r["launches"]}
 
 
 def superbatch_roofline(dev, n_target=1_200_000, reps=20):
@@ -201,6 +271,8 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=20.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-superbatch", action="store_true")
+    ap.add_argument("--no-kernel-timer", action="store_true",
+                    help="skip the event-timed kernel pass (PMC runs: only real step launches)")
     ap.add_argument("--eager", action="store_true",
                     help="launch every kernel from Python (no HIP-graph capture)")
     a = ap.parse_args()
@@ -310,14 +382,21 @@ def main():
 
     # instrumented eager pass over the same batches: HIP events around every
     # launch of the measured kernel (forward+backward of the same model)
-    with KernelTimer("scgib_gin_layer_fwd") as timer:
-        for i in range(min(a.steps, 10)):
-            g = pool[i % len(pool)]
-            model.zero_grad(set_to_none=True)
-            _, kl, con, rec = model(g, g.ndata["x"], None, None, None, 1, None, a.k, dev, a.batch)
-            (kl + rec + con).backward()
-    avg_bytes, avg_flops, avg_ms, n_launch = timer.summary(layer_fwd_bytes, layer_fwd_flops)
-    achieved = avg_bytes / (avg_ms * 1e-3) / 1e9
+    # (one stream: the encoder branches are not forked here, so no other
+    # kernel runs inside a bracket)
+    r_bwd = r_fwd = None
+    if not a.no_kernel_timer:
+        pkg.models.FORK_ENCODERS = False
+        with KernelTimer("scgib_gin_layer_fwd", "scgib_gin_layer_bwd") as timer:
+            for i in range(min(a.steps, 10)):
+                g = pool[i % len(pool)]
+                model.zero_grad(set_to_none=True)
+                _, kl, con, rec = model(g, g.ndata["x"], None, None, None, 1, None, a.k, dev,
+                                        a.batch)
+                (kl + rec + con).backward()
+        pkg.models.FORK_ENCODERS = True
+        r_bwd = timer.summary("scgib_gin_layer_bwd", layer_bwd_bytes, layer_bwd_flops)
+        r_fwd = timer.summary("scgib_gin_layer_fwd", layer_fwd_bytes, layer_fwd_flops)
 
     sb = None if a.no_superbatch or rank != 0 else superbatch_roofline(dev)
     cpu = None
@@ -345,17 +424,15 @@ def main():
                        "launch": "eager" if a.eager else "hip-graph replay (capacity mode)",
                        "global_batch": world * a.batch, "nodes_per_batch": round(n_nodes, 1),
                        "parallelism": f"dp{world}", "final_loss": round(final_loss, 4)},
-            "roofline": {"bound": "hbm", "kernel": "gin_fwd_k (fused GIN layer: gather + "
-                                                   "2 f32-MFMA GEMMs + BN tile stats)",
-                         "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4),
-                         "frac_vs_measured_copy": round(achieved / HBM_MEASURED_GBS, 4),
-                         "traffic": TRAFFIC.get("gin_fwd_k"),
-                         "avg_launch_us": round(avg_ms * 1e3, 3),
-                         "avg_bytes_per_launch": int(avg_bytes),
-                         "mfma_tflops": round(avg_flops / (avg_ms * 1e-3) / 1e12, 2),
-                         "mfma_frac_f32": round(avg_flops / (avg_ms * 1e-3) / 1e12 / 157.3, 4),
-                         "launches_timed": n_launch},
+            # dominant kernel by total time per step (profiles/): gin_bwd_k
+            "roofline": None if r_bwd is None else roofline_entry("gin_bwd_k", "fused GIN layer backward: BN-backward "
+                                       "apply + 4 f32-MFMA GEMMs + dW slabs", r_bwd,
+                                       ["gin_bwd_k<32, true>", "gin_bwd_k<64, true>"]),
+            "roofline_gin_fwd": None if r_fwd is None else roofline_entry("gin_fwd_k", "fused GIN layer: gather + 2 "
+                                               "f32-MFMA GEMMs + BN tile stats", r_fwd,
+                                               ["gin_fwd_k<32, false, true>",
+                                                "gin_fwd_k<64, true, true>",
+                                                "gin_fwd_k<64, false, true>"]),
             "roofline_superbatch": None if sb is None else {
                 "bound": "hbm", "kernel": "gin_aggregate_k d=64", "nodes": sb["nodes"],
                 "edges": sb["edges"], "achieved": round(sb["gbs"], 1), "peak": HBM_PEAK_GBS,

@@ -78,10 +78,16 @@ int scgib_gin_aggregate(const float *h, const int32_t *rowptr, const int32_t *co
  *   dh_v = (1+eps) g_v + sum_{u in out(v)} g_u.  Per-tile sum(dy), sum(dy xhat).
  * scgib_bn_bwd_finalize: dgamma, dbeta [64] and coef [2][64] for dz2.
  * scgib_gin_layer_bwd: d(agg) [n,d_in] and wgrad = dW2[64*64] | dW1[64*d_in]
- *   | db2[64] | db1[64] through per-workgroup slabs
- *   (scgib_gin_slab_floats(n, d_in) floats) reduced in a fixed order. */
+ *   | db2[64] | db1[64] through scgib_gin_bwd_slabs(n) per-workgroup slabs of
+ *   64*64 + 64*d_in + 128 floats (scgib_gin_slab_floats(n, d_in) in total),
+ *   reduced in a fixed order.  With wgrad NULL the slabs are left for the
+ *   caller's scgib_slab_reduce (so the GEMM kernel can be timed alone).
+ * scgib_slab_reduce: out[w] = sum_s slab[s*width + w], fixed order. */
 int64_t scgib_gin_tiles(int64_t n_nodes);
 int64_t scgib_gin_slab_floats(int64_t n_nodes, int32_t d_in);
+int64_t scgib_gin_bwd_slabs(int64_t n_nodes);
+int scgib_slab_reduce(const float *slab, int32_t n_slabs, int64_t width, float *out,
+                      scgib_stream_t stream);
 int scgib_gin_layer_fwd(const float *h_in, int32_t d_in, const float *in_stat,
                         const int32_t *rowptr, const int32_t *col, int64_t n_nodes,
                         float one_plus_eps, const float *w1, const float *b1, const float *w2,

@@ -388,7 +388,7 @@ __global__ __launch_bounds__(1024) void bn_bwd_finalize_k(const float *__restric
 // BN = false is the backward of the dense head MLP: dz2 = dy (the gradient
 // of the MLP output); z2 / stat / coef are not read.
 template <int DIN, bool BN = true>
-__global__ __launch_bounds__(256) void gin_bwd_k(
+__global__ __launch_bounds__(256, 2) void gin_bwd_k(
     const float *__restrict__ dy, const float *__restrict__ z2, const float *__restrict__ r,
     const float *__restrict__ agg, const float *__restrict__ stat,
     const float *__restrict__ coef, const float *__restrict__ w1, const float *__restrict__ w2,
@@ -397,11 +397,14 @@ __global__ __launch_bounds__(256) void gin_bwd_k(
     const int64_t n = eff_count(dims, 0, ncap);
     constexpr int LDA = DIN + 1;
     constexpr int SLAB = 64 * 64 + 64 * DIN + 128;
+    // r is dead once dz1 is formed, so the agg tile reuses its buffer: 66.5 KB
+    // for DIN <= 64, two workgroups per CU (loads of one overlap the other's MFMA)
+    constexpr int RA = (LDA > LDH ? LDA : LDH);
     __shared__ float sD[TM * LDH];   // dz2, then dz1
-    __shared__ float sR[TM * LDH];
-    __shared__ float sA[TM * LDA];
+    __shared__ float sRA[TM * RA];   // r, then agg
     __shared__ float sW1[64 * LDA];
     __shared__ float sW2[64 * LDH];
+    float *const sR = sRA, *const sA = sRA;
     const int tid = threadIdx.x, l = tid & 63, w = tid >> 6;
     const int wr = w >> 1, wc = w & 1;
     stage_weights<DIN>(w1, w2, sW1, sW2);
@@ -467,12 +470,6 @@ __global__ __launch_bounds__(256) void gin_bwd_k(
             pd[0] = d.x; pd[1] = d.y; pd[2] = d.z; pd[3] = d.w;
             pr[0] = vr[k].x; pr[1] = vr[k].y; pr[2] = vr[k].z; pr[3] = vr[k].w;
         }
-#pragma unroll
-        for (int k = 0; k < AK; ++k) {
-            const int idx = tid + 256 * k, rr = idx / AQ, cq = idx % AQ;
-            float *pa = sA + rr * LDA + 4 * cq;
-            pa[0] = va[k].x; pa[1] = va[k].y; pa[2] = va[k].z; pa[3] = va[k].w;
-        }
         __syncthreads();
         // dW2 += dz2^T r  (sub-tile j-block wr, k-block wc)
         accW2 = mma_tn<TM>(sD + wr * 32, LDH, sR + wc * 32, LDH, accW2);
@@ -485,6 +482,13 @@ __global__ __launch_bounds__(256) void gin_bwd_k(
         for (int reg = 0; reg < 16; ++reg) {
             const int row = wr * 32 + acc_row(reg, l), cc = wc * 32 + (l & 31);
             sD[row * LDH + cc] = sR[row * LDH + cc] > 0.f ? dr[reg] : 0.f;
+        }
+        __syncthreads();  // r is dead: the agg tile (held in registers) takes its buffer
+#pragma unroll
+        for (int k = 0; k < AK; ++k) {
+            const int idx = tid + 256 * k, rr = idx / AQ, cq = idx % AQ;
+            float *pa = sA + rr * LDA + 4 * cq;
+            pa[0] = va[k].x; pa[1] = va[k].y; pa[2] = va[k].z; pa[3] = va[k].w;
         }
         __syncthreads();
         for (int rr = q; rr < TM; rr += 4) db1 += sD[rr * LDH + ch];
@@ -534,7 +538,9 @@ __global__ __launch_bounds__(256) void gin_bwd_k(
     }
 }
 
-static int bwd_grid(int64_t ntiles) { return static_cast<int>(ntiles < 256 ? ntiles : 256); }
+// up to two workgroups per CU (66.5 KB LDS each): one tile per workgroup for
+// batches up to 512 tiles, so every tile of an encoder layer runs at once
+static int bwd_grid(int64_t ntiles) { return static_cast<int>(ntiles < 512 ? ntiles : 512); }
 
 }  // namespace scgib
 
@@ -544,6 +550,10 @@ extern "C" int64_t scgib_gin_tiles(int64_t n_nodes) { return (n_nodes + TM - 1) 
 
 extern "C" int64_t scgib_gin_slab_floats(int64_t n_nodes, int32_t d_in) {
     return static_cast<int64_t>(bwd_grid(scgib_gin_tiles(n_nodes))) * (64 * 64 + 64 * d_in + 128);
+}
+
+extern "C" int64_t scgib_gin_bwd_slabs(int64_t n_nodes) {
+    return n_nodes <= 0 ? 0 : bwd_grid(scgib_gin_tiles(n_nodes));
 }
 
 extern "C" int scgib_gin_layer_fwd(const float *h_in, int32_t d_in, const float *in_stat,
@@ -627,7 +637,7 @@ extern "C" int scgib_gin_layer_bwd(const float *dy, const float *z2, const float
                                    int64_t n_nodes, float *dagg, float *slab, float *wgrad,
                                    const int32_t *dims, scgib_stream_t stream) {
     if (n_nodes <= 0 || (d_in != 32 && d_in != 64)) return SCGIB_EINVAL;
-    if (!dy || !z2 || !r || !agg || !stat || !coef || !w1 || !w2 || !dagg || !slab || !wgrad)
+    if (!dy || !z2 || !r || !agg || !stat || !coef || !w1 || !w2 || !dagg || !slab)
         return SCGIB_EINVAL;
     const int64_t nt = scgib_gin_tiles(n_nodes);
     const int grid = bwd_grid(nt);
@@ -636,9 +646,9 @@ extern "C" int scgib_gin_layer_bwd(const float *dy, const float *z2, const float
         gin_bwd_k<32><<<grid, 256, 0, st>>>(dy, z2, r, agg, stat, coef, w1, w2, n_nodes, nt, dagg, slab, dims);
     else
         gin_bwd_k<64><<<grid, 256, 0, st>>>(dy, z2, r, agg, stat, coef, w1, w2, n_nodes, nt, dagg, slab, dims);
-    const int64_t width = 64 * 64 + 64 * d_in + 128;
-    launch_slab_reduce(slab, grid, width, wgrad, st);
-    return launch_status();
+    const int rc = launch_status();
+    if (rc != SCGIB_OK || !wgrad) return rc;  // wgrad NULL: the caller reduces the slabs
+    return launch_slab_reduce(slab, grid, 64 * 64 + 64 * static_cast<int64_t>(d_in) + 128, wgrad, st);
 }
 
 // ---------------------------------------------------------------------------

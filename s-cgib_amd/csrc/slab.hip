@@ -40,3 +40,9 @@ int launch_slab_reduce(const float *slab, int nslab, int64_t width, float *out, 
 }
 
 }  // namespace scgib
+
+extern "C" int scgib_slab_reduce(const float *slab, int32_t n_slabs, int64_t width, float *out,
+                                 scgib_stream_t stream) {
+    if (n_slabs <= 0 || width <= 0 || !slab || !out) return SCGIB_EINVAL;
+    return scgib::launch_slab_reduce(slab, n_slabs, width, out, scgib::as_stream(stream));
+}

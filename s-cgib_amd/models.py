@@ -131,6 +131,9 @@ class Set2Set(nn.Module):
 
 
 _SIDE_STREAMS = {}
+# forward() runs the ego branch on a second stream (see _encode_forked);
+# bench.py turns it off for its single-stream event-timed kernel pass
+FORK_ENCODERS = True
 
 
 def _side_stream(device):
@@ -193,7 +196,7 @@ class _SCGIBCore(nn.Module):
         noisy = im[:, : self.hidden_dim]
         return im, kl, noisy, z2, z1
 
-    def _encode_forked(self, enc_owner, batch_g, batch_x):
+    def _encode_forked(self, enc_owner, batch_g, batch_x, fork=True):
         """Fast path of forward() when the ego-nets are built on the device:
         the ego branch (ego-net build, x_subs gather, transfer_d, Encoder2,
         readout) runs on a second HIP stream, concurrently with Encoder1 on the
@@ -202,7 +205,7 @@ class _SCGIBCore(nn.Module):
         branch's backward on the stream its forward ran on, so the two
         encoders' backward chains overlap as well."""
         main = torch.cuda.current_stream(batch_x.device)
-        side = _side_stream(batch_x.device)
+        side = _side_stream(batch_x.device) if fork else main
         side.wait_stream(main)
         batch_x.record_stream(side)
         with torch.cuda.stream(side):
@@ -269,7 +272,7 @@ class Mainmodel(_SCGIBCore):
                 batch_size=16, noise=None):
         self.batch_size = batch_size
         if flatten_batch_subgraphs is None and x_subs is None and batch_x.is_cuda:
-            ego, enc = self._encode_forked(self, batch_g, batch_x)
+            ego, enc = self._encode_forked(self, batch_g, batch_x, FORK_ENCODERS)
             im, _, _, z2, z1 = self._extract(self, batch_g, None, ego, None, noise, enc)
             self._last_z1 = z1
         else:
@@ -343,7 +346,7 @@ class Mainmodel_continue(_SCGIBCore):
         self.batch_size = batch_size
         if flatten_batch_subgraphs is None and x_subs is None and batch_x.is_cuda:
             # the wrapper's transfer_d feeds the wrapped model's encoders
-            ego, enc = self._encode_forked(self.model, batch_g, batch_x)
+            ego, enc = self._encode_forked(self.model, batch_g, batch_x, FORK_ENCODERS)
             im, _, _, z2, z1 = self.model._extract(self.model, batch_g, None, ego, None, noise,
                                                    enc)
             self.model._last_z1 = z1

@@ -167,8 +167,10 @@ class _GinEncoder(torch.autograd.Function):
                                 dtype=torch.float32, device=dev)
             meta = {"n": n, "e": gr.edge_capacity(), "d_in": d_in}
             _launch("scgib_gin_layer_bwd", meta, _p(dy), _p(z2), _p(r), _p(agg), d_in, _p(stat),
-                      _p(coef), _p(_f32(w1, "w1")), _p(_f32(w2, "w2")), n, _p(dagg), _p(slab),
-                      _p(wgrad), _p(gr.dims), st)
+                    _p(coef), _p(_f32(w1, "w1")), _p(_f32(w2, "w2")), n, _p(dagg), _p(slab),
+                    _NULL, _p(gr.dims), st)
+            _lib.call("scgib_slab_reduce", _p(slab), int(_lib.query("scgib_gin_bwd_slabs", n)),
+                      wgrad.numel(), _p(wgrad), st)
             o = HIDDEN * HIDDEN
             grads[6 * l + 2] = wgrad[:o].view(HIDDEN, HIDDEN)
             grads[6 * l + 0] = wgrad[o:o + HIDDEN * d_in].view(HIDDEN, d_in)

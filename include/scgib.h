@@ -106,6 +106,30 @@ int scgib_gin_bwd_stats(const float *dh, const int32_t *rowptr_t, const int32_t 
 int scgib_bn_bwd_finalize(const float *tile_stats, int64_t n_nodes, int32_t training,
                           float *dgamma, float *dbeta, float *coef, const int32_t *dims,
                           scgib_stream_t stream);
+/* Training-mode fused variants: the BatchNorm finalize is folded into the
+ * tile kernel (hierarchical last-arriver over 16-tile groups, fp64, fixed
+ * order) — one launch per layer instead of two.  `bn_ws` holds
+ * scgib_gin_bn_ws_floats(n) floats (tile statistics + group partials);
+ * `counters` holds scgib_gin_counters(n) uint32 that are zero on entry and
+ * left zero (graph-replay safe; one set per concurrently running encoder).
+ * scgib_gin_layer_fwd_bn = scgib_gin_layer_fwd + scgib_bn_finalize(training);
+ * running_mean/var/num_batches_tracked may be NULL (track_running_stats off).
+ * scgib_gin_bwd_stats_bn = scgib_gin_bwd_stats + scgib_bn_bwd_finalize. */
+int64_t scgib_gin_bn_ws_floats(int64_t n_nodes);
+int64_t scgib_gin_counters(int64_t n_nodes);
+int scgib_gin_layer_fwd_bn(const float *h_in, int32_t d_in, const float *in_stat,
+                           const int32_t *rowptr, const int32_t *col, int64_t n_nodes,
+                           float one_plus_eps, const float *w1, const float *b1, const float *w2,
+                           const float *b2, float *agg, float *r, float *z2, const float *gamma,
+                           const float *beta, float bn_eps, float momentum, float *running_mean,
+                           float *running_var, int64_t *num_batches_tracked, float *stat,
+                           float *bn_ws, uint32_t *counters, const int32_t *dims,
+                           scgib_stream_t stream);
+int scgib_gin_bwd_stats_bn(const float *dh, const int32_t *rowptr_t, const int32_t *col_t,
+                           float one_plus_eps, const float *z2, const float *stat,
+                           int64_t n_nodes, int32_t training, float *dy, float *dgamma,
+                           float *dbeta, float *coef, float *bn_ws, uint32_t *counters,
+                           const int32_t *dims, scgib_stream_t stream);
 int scgib_gin_layer_bwd(const float *dy, const float *z2, const float *r, const float *agg,
                         int32_t d_in, const float *stat, const float *coef, const float *w1,
                         const float *w2, int64_t n_nodes, float *dagg, float *slab,

@@ -112,10 +112,6 @@ __device__ __forceinline__ bool last_arriver(unsigned *counter, unsigned expecte
     return true;
 }
 
-__device__ __forceinline__ float ld_acq(const float *p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
 // workspace (floats): D[B] | fwd partials [NS][B][4] | bwd partials [NS][B][128]
 __global__ __launch_bounds__(256) void contrast_fwd_k(const float *__restrict__ z1,
                                                       const float *__restrict__ z2, int64_t B,
@@ -159,10 +155,20 @@ __global__ __launch_bounds__(256) void contrast_fwd_k(const float *__restrict__ 
     __shared__ double red[256];
     double acc = 0.0;
     for (int64_t k = tid; k < B; k += 256) {
-        float s[4] = {0.f, 0.f, 0.f, 0.f};
-        for (int y = 0; y < NS; ++y)
+        // all splits' partials in flight (clamped split index), summed in order
+        float4 v[kMaxSplit];
 #pragma unroll
-            for (int c = 0; c < 4; ++c) s[c] += ld_acq(pf + (y * B + k) * 4 + c);
+        for (int y = 0; y < kMaxSplit; ++y)
+            v[y] = *reinterpret_cast<const float4 *>(pf + ((y < NS ? y : 0) * B + k) * 4);
+        float s[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int y = 0; y < kMaxSplit; ++y) {
+            const float w = y < NS ? 1.f : 0.f;
+            s[0] = fmaf(v[y].x, w, s[0]);
+            s[1] = fmaf(v[y].y, w, s[1]);
+            s[2] = fmaf(v[y].z, w, s[2]);
+            s[3] = fmaf(v[y].w, w, s[3]);
+        }
         const float D = s[0] + s[1] - s[2];
         Dv[k] = D;
         acc += static_cast<double>(-logf(s[3] / D));
@@ -245,10 +251,20 @@ __global__ __launch_bounds__(256) void contrast_bwd_k(const float *__restrict__ 
     if (!last_arriver(counters + blockIdx.x, NS)) return;
     if (i < B) {
         d1 = d2 = make_float4(0.f, 0.f, 0.f, 0.f);
-        for (int y = 0; y < NS; ++y) {
-            const float *p = pb + (static_cast<int64_t>(y) * B + i) * 128 + 4 * cl;
-            d1.x += ld_acq(p); d1.y += ld_acq(p + 1); d1.z += ld_acq(p + 2); d1.w += ld_acq(p + 3);
-            d2.x += ld_acq(p + 64); d2.y += ld_acq(p + 65); d2.z += ld_acq(p + 66); d2.w += ld_acq(p + 67);
+        float4 v1[kMaxSplit], v2[kMaxSplit];
+#pragma unroll
+        for (int y = 0; y < kMaxSplit; ++y) {  // all splits in flight (clamped), summed in order
+            const float *p = pb + (static_cast<int64_t>(y < NS ? y : 0) * B + i) * 128 + 4 * cl;
+            v1[y] = *reinterpret_cast<const float4 *>(p);
+            v2[y] = *reinterpret_cast<const float4 *>(p + 64);
+        }
+#pragma unroll
+        for (int y = 0; y < kMaxSplit; ++y) {
+            const float w = y < NS ? 1.f : 0.f;
+            d1.x = fmaf(v1[y].x, w, d1.x); d1.y = fmaf(v1[y].y, w, d1.y);
+            d1.z = fmaf(v1[y].z, w, d1.z); d1.w = fmaf(v1[y].w, w, d1.w);
+            d2.x = fmaf(v2[y].x, w, d2.x); d2.y = fmaf(v2[y].y, w, d2.y);
+            d2.z = fmaf(v2[y].z, w, d2.z); d2.w = fmaf(v2[y].w, w, d2.w);
         }
         // this lane's channels of the normalised rows
         float4 a1 = q1[0], a2 = q2[0];

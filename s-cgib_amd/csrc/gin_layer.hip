@@ -40,6 +40,229 @@ namespace scgib {
 // ---------------------------------------------------------------------------
 // forward
 // ---------------------------------------------------------------------------
+// ---------------------------------------------------------------------------
+// BatchNorm finalize folded into the producing tile kernel (training mode).
+// Hierarchical last-arriver: the tiles of a layer arrive in groups of 16; the
+// last tile of a group combines the group's 16 tile statistics (fp64) into a
+// group partial, then arrives at the layer counter; the last group combines
+// the groups and writes the BN record / coefficients.  Two short load rounds
+// at the tail of the kernel replace a separate 1-workgroup finalize launch.
+// Fixed combination order -> deterministic.  Counters: caller-provided, zero
+// on entry; each is reset by its last arriver (graph-replay safe).
+// ---------------------------------------------------------------------------
+constexpr int kGroup = 16;
+
+struct BnFwdFuse {          // gin_fwd_k: BN statistics + running update
+    unsigned *counters;     // [ngr_cap + 1]; nullptr: not fused (separate finalize)
+    double *gpart;          // [ngr_cap][128]: group sum, group centred M2
+    const float *gamma, *beta;
+    float *rmean, *rvar, *stat;
+    int64_t *nbt;
+    float eps, momentum;
+    int ngr_cap;
+};
+
+struct BnBwdFuse {          // gin_bwd_stats_k: dgamma, dbeta, dz2 coefficients
+    unsigned *counters;
+    double *gpart;          // [ngr_cap][128]: group sum dy, group sum dy * xhat
+    float *dgamma, *dbeta, *coef;
+    int training, ngr_cap;
+};
+
+// release this workgroup's prior global writes, count it in, and return
+// whether it is the last of `expected` arrivals (then with acquire)
+// Cross-workgroup data of the finalize (tile stats, group partials) is
+// written with agent-scope atomic stores and read with agent-scope atomic
+// loads, which are coherent across the XCDs' L2s without an L2 write-back.
+// An agent-scope release fence would write back the whole L2 — including
+// the tile outputs this kernel just produced — and measured 5-10 us per
+// workgroup, more than the separate finalize launch it replaces.  So:
+// every wave waits for its stores to be acknowledged (vmcnt(0)), the barrier
+// collects the waves, and one thread counts the workgroup in.
+__device__ __forceinline__ void st_agent(float *p, float v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_agent(double *p, double v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ float ld_agent(const float *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double ld_agent(const double *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ bool block_arrive(unsigned *counter, unsigned expected) {
+    __shared__ unsigned s_ticket;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0)
+        s_ticket = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    return s_ticket == expected - 1;
+}
+
+// rows of tile t / group g of an n-row layer
+__device__ __forceinline__ double rows_in(int64_t n, int64_t first, int64_t span) {
+    const int64_t r = n - first;
+    return static_cast<double>(r < span ? r : span);
+}
+
+// 256 threads: channel c = tid & 63, partition p = tid >> 6 (4 partitions).
+// Per-tile (S, M2) -> group (S_g, M2_g) -> layer (mean, M2); exact
+// decomposition M2 = sum_b [M2_b + (S_b - n_b mean)^2 / n_b] at each level.
+__device__ void bn_fwd_hier(const float *__restrict__ part, int64_t n, int64_t tile,
+                            const BnFwdFuse &fz) {
+    const int64_t nt = (n + TM - 1) / TM;
+    const int ngr = static_cast<int>((nt + kGroup - 1) / kGroup);
+    const int g = static_cast<int>(tile / kGroup);
+    const int gsize = static_cast<int>(nt - int64_t(g) * kGroup < kGroup ? nt - int64_t(g) * kGroup : kGroup);
+    if (!block_arrive(&fz.counters[g], gsize)) return;
+    const int c = threadIdx.x & 63, p = threadIdx.x >> 6;
+    __shared__ double sh[4][64];
+    __shared__ double smean[64];
+    {   // group combine: partition p takes tiles g*16 + p + 4u
+        float S[4], Q[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int64_t t = int64_t(g) * kGroup + p + 4 * u;
+            const int64_t tc = p + 4 * u < gsize ? t : int64_t(g) * kGroup;
+            S[u] = ld_agent(part + tc * 128 + c);
+            Q[u] = ld_agent(part + tc * 128 + 64 + c);
+        }
+        double a = 0.0;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) a += p + 4 * u < gsize ? static_cast<double>(S[u]) : 0.0;
+        sh[p][c] = a;
+        __syncthreads();
+        if (p == 0) {
+            const double sg = ((sh[0][c] + sh[1][c]) + sh[2][c]) + sh[3][c];
+            smean[c] = sg / rows_in(n, int64_t(g) * kGroup * TM, kGroup * TM);
+            st_agent(fz.gpart + int64_t(g) * 128 + c, sg);
+        }
+        __syncthreads();
+        const double mg = smean[c];
+        double q = 0.0;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            if (p + 4 * u < gsize) {
+                const int64_t t = int64_t(g) * kGroup + p + 4 * u;
+                const double nb = rows_in(n, t * TM, TM);
+                const double d = static_cast<double>(S[u]) - nb * mg;
+                q += static_cast<double>(Q[u]) + d * d / nb;
+            }
+        }
+        __syncthreads();
+        sh[p][c] = q;
+        __syncthreads();
+        if (p == 0) st_agent(fz.gpart + int64_t(g) * 128 + 64 + c, ((sh[0][c] + sh[1][c]) + sh[2][c]) + sh[3][c]);
+        if (threadIdx.x == 0) fz.counters[g] = 0u;
+    }
+    if (!block_arrive(&fz.counters[fz.ngr_cap], ngr)) return;
+    // layer combine over the ngr groups (8 groups' loads in flight per thread)
+    double a = 0.0;
+    for (int g0 = p; g0 < ngr; g0 += 4 * 8) {
+        double v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = ld_agent(fz.gpart + int64_t(g0 + 4 * u < ngr ? g0 + 4 * u : p) * 128 + c);
+#pragma unroll
+        for (int u = 0; u < 8; ++u) a += g0 + 4 * u < ngr ? v[u] : 0.0;
+    }
+    sh[p][c] = a;
+    __syncthreads();
+    if (p == 0) smean[c] = (((sh[0][c] + sh[1][c]) + sh[2][c]) + sh[3][c]) / static_cast<double>(n);
+    __syncthreads();
+    const double mean = smean[c];
+    double q = 0.0;
+    for (int g0 = p; g0 < ngr; g0 += 4 * 8) {
+        double vs[8], vq[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int64_t gg = g0 + 4 * u < ngr ? g0 + 4 * u : p;
+            vs[u] = ld_agent(fz.gpart + gg * 128 + c);
+            vq[u] = ld_agent(fz.gpart + gg * 128 + 64 + c);
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            if (g0 + 4 * u < ngr) {
+                const double ng = rows_in(n, int64_t(g0 + 4 * u) * kGroup * TM, kGroup * TM);
+                const double d = vs[u] - ng * mean;
+                q += vq[u] + d * d / ng;
+            }
+        }
+    }
+    __syncthreads();
+    sh[p][c] = q;
+    __syncthreads();
+    if (p == 0) {
+        const double M2 = ((sh[0][c] + sh[1][c]) + sh[2][c]) + sh[3][c];
+        const double var = M2 / static_cast<double>(n);
+        if (fz.rmean) {
+            fz.rmean[c] = static_cast<float>((1.0 - fz.momentum) * fz.rmean[c] + fz.momentum * mean);
+            fz.rvar[c] = static_cast<float>((1.0 - fz.momentum) * fz.rvar[c] +
+                                            fz.momentum * (n > 1 ? M2 / static_cast<double>(n - 1) : M2));
+            if (c == 0 && fz.nbt) *fz.nbt += 1;
+        }
+        const double istd = 1.0 / sqrt(var + static_cast<double>(fz.eps));
+        const double sc = fz.gamma[c] * istd;
+        fz.stat[c] = static_cast<float>(mean);
+        fz.stat[64 + c] = static_cast<float>(istd);
+        fz.stat[128 + c] = static_cast<float>(sc);
+        fz.stat[192 + c] = static_cast<float>(fz.beta[c] - mean * sc);
+    }
+    if (threadIdx.x == 0) fz.counters[fz.ngr_cap] = 0u;
+}
+
+// backward: tile (sum dy, sum dy xhat) -> group -> layer sums (fp64)
+__device__ void bn_bwd_hier(const float *__restrict__ part, int64_t n, int64_t tile,
+                            const BnBwdFuse &bz) {
+    const int64_t nt = (n + TM - 1) / TM;
+    const int ngr = static_cast<int>((nt + kGroup - 1) / kGroup);
+    const int g = static_cast<int>(tile / kGroup);
+    const int gsize = static_cast<int>(nt - int64_t(g) * kGroup < kGroup ? nt - int64_t(g) * kGroup : kGroup);
+    if (!block_arrive(&bz.counters[g], gsize)) return;
+    const int c = threadIdx.x & 127, p = threadIdx.x >> 7;  // 128 sums x 2 partitions
+    __shared__ double sh[2][128];
+    {
+        float v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int k = p + 2 * u;
+            v[u] = ld_agent(part + (int64_t(g) * kGroup + (k < gsize ? k : 0)) * 128 + c);
+        }
+        double a = 0.0;
+#pragma unroll
+        for (int u = 0; u < 8; ++u) a += p + 2 * u < gsize ? static_cast<double>(v[u]) : 0.0;
+        sh[p][c] = a;
+        __syncthreads();
+        if (p == 0) st_agent(bz.gpart + int64_t(g) * 128 + c, sh[0][c] + sh[1][c]);
+        if (threadIdx.x == 0) bz.counters[g] = 0u;
+    }
+    if (!block_arrive(&bz.counters[bz.ngr_cap], ngr)) return;
+    double a = 0.0;
+    for (int g0 = p; g0 < ngr; g0 += 2 * 8) {
+        double v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = ld_agent(bz.gpart + int64_t(g0 + 2 * u < ngr ? g0 + 2 * u : p) * 128 + c);
+#pragma unroll
+        for (int u = 0; u < 8; ++u) a += g0 + 2 * u < ngr ? v[u] : 0.0;
+    }
+    __syncthreads();
+    sh[p][c] = a;
+    __syncthreads();
+    if (p == 0) {
+        const double tot = sh[0][c] + sh[1][c];
+        if (c < 64) {
+            bz.dbeta[c] = static_cast<float>(tot);
+            bz.coef[c] = bz.training ? static_cast<float>(tot / static_cast<double>(n)) : 0.f;
+        } else {
+            bz.dgamma[c - 64] = static_cast<float>(tot);
+            bz.coef[c] = bz.training ? static_cast<float>(tot / static_cast<double>(n)) : 0.f;
+        }
+    }
+    if (threadIdx.x == 0) bz.counters[bz.ngr_cap] = 0u;
+}
+
 // GATHER = false is the dense two-layer MLP of the head (models.py:1055-1057,
 // applied at :1174): the tile's input rows are staged directly, agg_out and
 // the BN tile statistics are not written, z2_out is the MLP output.
@@ -50,7 +273,7 @@ __global__ __launch_bounds__(256) void gin_fwd_k(
     const int32_t *__restrict__ col, int64_t ncap, float ope, const float *__restrict__ w1,
     const float *__restrict__ b1, const float *__restrict__ w2, const float *__restrict__ b2,
     float *__restrict__ agg_out, float *__restrict__ r_out, float *__restrict__ z2_out,
-    float *__restrict__ part, const int32_t *__restrict__ dims) {
+    float *__restrict__ part, const int32_t *__restrict__ dims, BnFwdFuse fz) {
     constexpr int LDA = DIN + 1, LPR = DIN / 4, RPP = 256 / LPR;
     const int64_t n = eff_count(dims, 0, ncap);
     __shared__ float sA[TM * LDA];
@@ -166,9 +389,10 @@ __global__ __launch_bounds__(256) void gin_fwd_k(
     if (l < 32) sRed[wr][ccol] = m2;
     __syncthreads();
     if (wr == 0 && l < 32) {
-        part[tile * 128 + ccol] = csum;
-        part[tile * 128 + 64 + ccol] = sRed[0][ccol] + sRed[1][ccol];
+        st_agent(part + tile * 128 + ccol, csum);
+        st_agent(part + tile * 128 + 64 + ccol, sRed[0][ccol] + sRed[1][ccol]);
     }
+    if (fz.counters) bn_fwd_hier(part, n, tile, fz);
 }
 
 // Batch mean / biased variance from the per-tile (sum, centred M2), fp64,
@@ -281,7 +505,7 @@ __global__ __launch_bounds__(256) void gin_bwd_stats_k(
     const float *__restrict__ dh, const int32_t *__restrict__ rowptr_t,
     const int32_t *__restrict__ col_t, float ope, const float *__restrict__ z2,
     const float *__restrict__ stat, int64_t ncap, float *__restrict__ dy_out,
-    float *__restrict__ part, const int32_t *__restrict__ dims) {
+    float *__restrict__ part, const int32_t *__restrict__ dims, BnBwdFuse bz) {
     __shared__ float sRed[2][16][64];
     const int64_t n = eff_count(dims, 0, ncap);
     const int tid = threadIdx.x, c = tid & 15, slot = tid >> 4;
@@ -338,8 +562,9 @@ __global__ __launch_bounds__(256) void gin_bwd_stats_k(
         const int which = tid >> 6, ch = tid & 63;
         float s = 0.f;
         for (int k = 0; k < 16; ++k) s += sRed[which][k][ch];
-        part[tile * 128 + which * 64 + ch] = s;
+        st_agent(part + tile * 128 + which * 64 + ch, s);
     }
+    if (bz.counters) bn_bwd_hier(part, n, tile, bz);
 }
 
 // dbeta = sum dy, dgamma = sum dy xhat (fp64, fixed order); coefficients of
@@ -388,7 +613,7 @@ __global__ __launch_bounds__(1024) void bn_bwd_finalize_k(const float *__restric
 // BN = false is the backward of the dense head MLP: dz2 = dy (the gradient
 // of the MLP output); z2 / stat / coef are not read.
 template <int DIN, bool BN = true>
-__global__ __launch_bounds__(256, 2) void gin_bwd_k(
+__global__ __launch_bounds__(256, (DIN <= 64 ? 2 : 1)) void gin_bwd_k(
     const float *__restrict__ dy, const float *__restrict__ z2, const float *__restrict__ r,
     const float *__restrict__ agg, const float *__restrict__ stat,
     const float *__restrict__ coef, const float *__restrict__ w1, const float *__restrict__ w2,
@@ -556,27 +781,83 @@ extern "C" int64_t scgib_gin_bwd_slabs(int64_t n_nodes) {
     return n_nodes <= 0 ? 0 : bwd_grid(scgib_gin_tiles(n_nodes));
 }
 
+static int launch_gin_fwd(const float *h_in, int32_t d_in, const float *in_stat,
+                          const int32_t *rowptr, const int32_t *col, int64_t n_nodes,
+                          float one_plus_eps, const float *w1, const float *b1, const float *w2,
+                          const float *b2, float *agg, float *r, float *z2, float *tile_stats,
+                          const int32_t *dims, const BnFwdFuse &fz, hipStream_t st) {
+    const int64_t nt = scgib_gin_tiles(n_nodes);
+    const float *isc = in_stat ? in_stat + 128 : nullptr, *ish = in_stat ? in_stat + 192 : nullptr;
+    if (d_in == 32)
+        gin_fwd_k<32, false><<<dim3((unsigned)nt), 256, 0, st>>>(h_in, isc, ish, rowptr, col, n_nodes, one_plus_eps, w1, b1, w2, b2, agg, r, z2, tile_stats, dims, fz);
+    else if (in_stat)
+        gin_fwd_k<64, true><<<dim3((unsigned)nt), 256, 0, st>>>(h_in, isc, ish, rowptr, col, n_nodes, one_plus_eps, w1, b1, w2, b2, agg, r, z2, tile_stats, dims, fz);
+    else
+        gin_fwd_k<64, false><<<dim3((unsigned)nt), 256, 0, st>>>(h_in, isc, ish, rowptr, col, n_nodes, one_plus_eps, w1, b1, w2, b2, agg, r, z2, tile_stats, dims, fz);
+    return launch_status();
+}
+
+static int gin_fwd_args_ok(const float *h_in, int32_t d_in, const float *in_stat,
+                           const int32_t *rowptr, const int32_t *col, int64_t n_nodes,
+                           const float *w1, const float *b1, const float *w2, const float *b2,
+                           const float *agg, const float *r, const float *z2,
+                           const float *tile_stats) {
+    if (n_nodes < 0 || (d_in != 32 && d_in != 64)) return SCGIB_EINVAL;
+    if (n_nodes == 0) return SCGIB_OK;
+    if (!h_in || !rowptr || !col || !w1 || !b1 || !w2 || !b2 || !agg || !r || !z2 || !tile_stats)
+        return SCGIB_EINVAL;
+    if (in_stat && d_in != 64) return SCGIB_EUNSUPPORTED;
+    return 1;  // go
+}
+
 extern "C" int scgib_gin_layer_fwd(const float *h_in, int32_t d_in, const float *in_stat,
                                    const int32_t *rowptr, const int32_t *col, int64_t n_nodes,
                                    float one_plus_eps, const float *w1, const float *b1,
                                    const float *w2, const float *b2, float *agg, float *r,
                                    float *z2, float *tile_stats, const int32_t *dims,
                                    scgib_stream_t stream) {
-    if (n_nodes < 0 || (d_in != 32 && d_in != 64)) return SCGIB_EINVAL;
-    if (n_nodes == 0) return SCGIB_OK;
-    if (!h_in || !rowptr || !col || !w1 || !b1 || !w2 || !b2 || !agg || !r || !z2 || !tile_stats)
+    const int ok = gin_fwd_args_ok(h_in, d_in, in_stat, rowptr, col, n_nodes, w1, b1, w2, b2, agg,
+                                   r, z2, tile_stats);
+    if (ok != 1) return ok;
+    BnFwdFuse fz{};
+    return launch_gin_fwd(h_in, d_in, in_stat, rowptr, col, n_nodes, one_plus_eps, w1, b1, w2, b2,
+                          agg, r, z2, tile_stats, dims, fz, as_stream(stream));
+}
+
+static int64_t bn_groups(int64_t n_nodes) { return (scgib_gin_tiles(n_nodes) + kGroup - 1) / kGroup; }
+
+extern "C" int64_t scgib_gin_bn_ws_floats(int64_t n_nodes) {
+    if (n_nodes <= 0) return 0;
+    // tile stats [tiles][128] f32 | (8-byte aligned) group partials [groups][128] f64
+    return ((scgib_gin_tiles(n_nodes) * 128 + 1) & ~int64_t(1)) + 2 * 128 * bn_groups(n_nodes);
+}
+
+extern "C" int64_t scgib_gin_counters(int64_t n_nodes) {
+    return n_nodes <= 0 ? 0 : bn_groups(n_nodes) + 1;
+}
+
+static double *bn_gpart(float *ws, int64_t n_nodes) {
+    return reinterpret_cast<double *>(ws + ((scgib_gin_tiles(n_nodes) * 128 + 1) & ~int64_t(1)));
+}
+
+extern "C" int scgib_gin_layer_fwd_bn(const float *h_in, int32_t d_in, const float *in_stat,
+                                      const int32_t *rowptr, const int32_t *col, int64_t n_nodes,
+                                      float one_plus_eps, const float *w1, const float *b1,
+                                      const float *w2, const float *b2, float *agg, float *r,
+                                      float *z2, const float *gamma, const float *beta,
+                                      float bn_eps, float momentum, float *running_mean,
+                                      float *running_var, int64_t *num_batches_tracked,
+                                      float *stat, float *bn_ws, uint32_t *counters,
+                                      const int32_t *dims, scgib_stream_t stream) {
+    const int ok = gin_fwd_args_ok(h_in, d_in, in_stat, rowptr, col, n_nodes, w1, b1, w2, b2, agg,
+                                   r, z2, bn_ws);
+    if (ok != 1) return ok == SCGIB_OK ? SCGIB_EINVAL : ok;  // BN needs rows
+    if (!gamma || !beta || !stat || !counters || ((running_mean == nullptr) != (running_var == nullptr)))
         return SCGIB_EINVAL;
-    if (in_stat && d_in != 64) return SCGIB_EUNSUPPORTED;
-    const int64_t nt = scgib_gin_tiles(n_nodes);
-    hipStream_t st = as_stream(stream);
-    const float *isc = in_stat ? in_stat + 128 : nullptr, *ish = in_stat ? in_stat + 192 : nullptr;
-    if (d_in == 32)
-        gin_fwd_k<32, false><<<dim3((unsigned)nt), 256, 0, st>>>(h_in, isc, ish, rowptr, col, n_nodes, one_plus_eps, w1, b1, w2, b2, agg, r, z2, tile_stats, dims);
-    else if (in_stat)
-        gin_fwd_k<64, true><<<dim3((unsigned)nt), 256, 0, st>>>(h_in, isc, ish, rowptr, col, n_nodes, one_plus_eps, w1, b1, w2, b2, agg, r, z2, tile_stats, dims);
-    else
-        gin_fwd_k<64, false><<<dim3((unsigned)nt), 256, 0, st>>>(h_in, isc, ish, rowptr, col, n_nodes, one_plus_eps, w1, b1, w2, b2, agg, r, z2, tile_stats, dims);
-    return launch_status();
+    BnFwdFuse fz{counters, bn_gpart(bn_ws, n_nodes), gamma, beta, running_mean, running_var,
+                 stat, num_batches_tracked, bn_eps, momentum, static_cast<int>(bn_groups(n_nodes))};
+    return launch_gin_fwd(h_in, d_in, in_stat, rowptr, col, n_nodes, one_plus_eps, w1, b1, w2, b2,
+                          agg, r, z2, bn_ws, dims, fz, as_stream(stream));
 }
 
 extern "C" int scgib_bn_finalize(const float *tile_stats, int64_t n_nodes, const float *gamma,
@@ -604,6 +885,18 @@ extern "C" int scgib_bn_relu_apply(const float *z, const float *stat, int64_t n_
     return launch_status();
 }
 
+static int launch_gin_bwd_stats(const float *dh, const int32_t *rowptr_t, const int32_t *col_t,
+                                float one_plus_eps, const float *z2, const float *stat,
+                                int64_t n_nodes, float *dy, float *tile_stats,
+                                const int32_t *dims, const BnBwdFuse &bz, hipStream_t st) {
+    const int64_t nt = scgib_gin_tiles(n_nodes);
+    if (rowptr_t)
+        gin_bwd_stats_k<true><<<dim3((unsigned)nt), 256, 0, st>>>(dh, rowptr_t, col_t, one_plus_eps, z2, stat, n_nodes, dy, tile_stats, dims, bz);
+    else
+        gin_bwd_stats_k<false><<<dim3((unsigned)nt), 256, 0, st>>>(dh, rowptr_t, col_t, one_plus_eps, z2, stat, n_nodes, dy, tile_stats, dims, bz);
+    return launch_status();
+}
+
 extern "C" int scgib_gin_bwd_stats(const float *dh, const int32_t *rowptr_t,
                                    const int32_t *col_t, float one_plus_eps, const float *z2,
                                    const float *stat, int64_t n_nodes, float *dy,
@@ -613,13 +906,25 @@ extern "C" int scgib_gin_bwd_stats(const float *dh, const int32_t *rowptr_t,
     if (n_nodes == 0) return SCGIB_OK;
     if (!dh || !z2 || !stat || !dy || !tile_stats) return SCGIB_EINVAL;
     if ((rowptr_t == nullptr) != (col_t == nullptr)) return SCGIB_EINVAL;
-    const int64_t nt = scgib_gin_tiles(n_nodes);
-    hipStream_t st = as_stream(stream);
-    if (rowptr_t)
-        gin_bwd_stats_k<true><<<dim3((unsigned)nt), 256, 0, st>>>(dh, rowptr_t, col_t, one_plus_eps, z2, stat, n_nodes, dy, tile_stats, dims);
-    else
-        gin_bwd_stats_k<false><<<dim3((unsigned)nt), 256, 0, st>>>(dh, rowptr_t, col_t, one_plus_eps, z2, stat, n_nodes, dy, tile_stats, dims);
-    return launch_status();
+    BnBwdFuse bz{};
+    return launch_gin_bwd_stats(dh, rowptr_t, col_t, one_plus_eps, z2, stat, n_nodes, dy,
+                                tile_stats, dims, bz, as_stream(stream));
+}
+
+extern "C" int scgib_gin_bwd_stats_bn(const float *dh, const int32_t *rowptr_t,
+                                      const int32_t *col_t, float one_plus_eps, const float *z2,
+                                      const float *stat, int64_t n_nodes, int32_t training,
+                                      float *dy, float *dgamma, float *dbeta, float *coef,
+                                      float *bn_ws, uint32_t *counters, const int32_t *dims,
+                                      scgib_stream_t stream) {
+    if (n_nodes <= 0 || !dh || !z2 || !stat || !dy || !dgamma || !dbeta || !coef || !bn_ws ||
+        !counters)
+        return SCGIB_EINVAL;
+    if ((rowptr_t == nullptr) != (col_t == nullptr)) return SCGIB_EINVAL;
+    BnBwdFuse bz{counters, bn_gpart(bn_ws, n_nodes), dgamma, dbeta, coef, training,
+                 static_cast<int>(bn_groups(n_nodes))};
+    return launch_gin_bwd_stats(dh, rowptr_t, col_t, one_plus_eps, z2, stat, n_nodes, dy, bn_ws,
+                                dims, bz, as_stream(stream));
 }
 
 extern "C" int scgib_bn_bwd_finalize(const float *tile_stats, int64_t n_nodes, int32_t training,
@@ -668,9 +973,9 @@ extern "C" int scgib_mlp2_fwd(const float *x, int32_t d_in, int64_t n_nodes, con
     const unsigned nt = static_cast<unsigned>(scgib_gin_tiles(n_nodes));
     hipStream_t st = as_stream(stream);
     if (d_in == 128)
-        gin_fwd_k<128, false, false><<<nt, 256, 0, st>>>(x, nullptr, nullptr, nullptr, nullptr, n_nodes, 0.f, w1, b1, w2, b2, nullptr, r, out, nullptr, dims);
+        gin_fwd_k<128, false, false><<<nt, 256, 0, st>>>(x, nullptr, nullptr, nullptr, nullptr, n_nodes, 0.f, w1, b1, w2, b2, nullptr, r, out, nullptr, dims, BnFwdFuse{});
     else
-        gin_fwd_k<64, false, false><<<nt, 256, 0, st>>>(x, nullptr, nullptr, nullptr, nullptr, n_nodes, 0.f, w1, b1, w2, b2, nullptr, r, out, nullptr, dims);
+        gin_fwd_k<64, false, false><<<nt, 256, 0, st>>>(x, nullptr, nullptr, nullptr, nullptr, n_nodes, 0.f, w1, b1, w2, b2, nullptr, r, out, nullptr, dims, BnFwdFuse{});
     return launch_status();
 }
 

@@ -265,9 +265,11 @@ __global__ __launch_bounds__(64) void interaction_fwd_k(
 // Closed form of the B sequential momentum updates of the per-graph
 // compressor BatchNorm (one nn.BatchNorm1d call per graph, models.py:642):
 //   r_B = (1-m)^B r_0 + sum_i m (1-m)^(B-1-i) x_i
-// evaluated in fp64 by 16 partitions x 64 channels, partials folded in a
-// fixed order (deterministic; closer to the exact recurrence than an fp32
-// sequential loop).
+// in fp64, 16 contiguous partitions x 64 channels.  Partition p runs the
+// recurrence S = (1-m) S + m x_i over its graphs (Horner form: no exp/pow
+// per graph, loads of 8 graphs in flight), then partition 0 chains the
+// partitions in order, T = (1-m)^len_p T + S_p, and applies the decay of r_0.
+// Deterministic; closer to the exact recurrence than an fp32 sequential loop.
 __global__ __launch_bounds__(1024) void bn_running_update_k(const float *__restrict__ stats,
                                                             const int32_t *__restrict__ gptr,
                                                             int64_t B, float momentum,
@@ -275,26 +277,45 @@ __global__ __launch_bounds__(1024) void bn_running_update_k(const float *__restr
                                                             float *__restrict__ rv,
                                                             int64_t *__restrict__ nbt) {
     const int c = threadIdx.x & 63, part = threadIdx.x >> 6;  // 16 partitions
-    const double m = momentum, lk = log1p(-m);
+    const double m = momentum, keep = 1.0 - static_cast<double>(momentum);
+    const int64_t chunk = (B + 15) / 16;
+    const int64_t i0 = part * chunk, i1 = i0 + chunk < B ? i0 + chunk : B;
     double am = 0.0, av = 0.0;
-    for (int64_t i = part; i < B; i += 16) {
-        const int n = gptr[i + 1] - gptr[i];
-        const float *sl = stats + i * SCGIB_STATS_STRIDE;
-        const double w = m * exp(static_cast<double>(B - 1 - i) * lk);
-        am += w * sl[kStMeanT + c];
-        av += w * (static_cast<double>(sl[kStSsqT + c]) / (n - 1));
+    for (int64_t ib = i0; ib < i1; ib += 8) {
+        float xm[8], xs[8];
+        int32_t g0[8], g1[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int64_t i = ib + u < i1 ? ib + u : i1 - 1;  // clamped: loads stay unconditional
+            const float *sl = stats + i * SCGIB_STATS_STRIDE;
+            xm[u] = sl[kStMeanT + c];
+            xs[u] = sl[kStSsqT + c];
+            g0[u] = gptr[i];
+            g1[u] = gptr[i + 1];
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            if (ib + u < i1) {
+                am = keep * am + m * static_cast<double>(xm[u]);
+                av = keep * av + m * (static_cast<double>(xs[u]) / (g1[u] - g0[u] - 1));
+            }
+        }
     }
     __shared__ double pm[16][64], pv[16][64];
     pm[part][c] = am;
     pv[part][c] = av;
     __syncthreads();
     if (part == 0) {
+        const double dchunk = pow(keep, static_cast<double>(chunk));
         double sm = 0.0, sv = 0.0;
         for (int p = 0; p < 16; ++p) {
-            sm += pm[p][c];
-            sv += pv[p][c];
+            const int64_t b0 = p * chunk, b1 = b0 + chunk < B ? b0 + chunk : B;
+            if (b1 <= b0) continue;
+            const double d = b1 - b0 == chunk ? dchunk : pow(keep, static_cast<double>(b1 - b0));
+            sm = d * sm + pm[p][c];
+            sv = d * sv + pv[p][c];
         }
-        const double decay = exp(static_cast<double>(B) * lk);
+        const double decay = pow(keep, static_cast<double>(B));
         rm[c] = static_cast<float>(decay * rm[c] + sm);
         rv[c] = static_cast<float>(decay * rv[c] + sv);
         if (c == 0 && nbt) *nbt += B;

@@ -12,8 +12,9 @@
 //   exact-f32 MFMA v_mfma_f32_32x32x2_f32 (two rows per instruction: lane l
 //   feeds row l>>5, channel l&31 of the quadrant's A and B halves), then
 //   the same wavefronts sum <im_v, sum_{u->v} im_u> for their rows.
-// recon_finalize_k: 16 workgroups each reduce 256 Gram entries over the
-//   partial slabs in fp64 (fixed order) and publish a partial ||G||^2; the
+// recon_finalize_k: 256 workgroups each reduce 16 Gram entries over the
+//   partial slabs (16 partitions per entry, a few loads each, combined in
+//   fixed order in fp64) and publish a partial ||G||^2; the
 //   last-arriving workgroup (agent-scope release/acquire, Guideline 16)
 //   forms the loss.  Deterministic for a given N.
 // recon_bwd_k: grad_v = (g/N) (4 (IM G)_v - 2 ((A + A^T) IM)_v), G staged in
@@ -25,7 +26,8 @@ namespace scgib {
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 constexpr int kGram = 64 * 64;
-constexpr int kFinBlocks = 16;  // 16 x 256 threads = one Gram entry per thread
+// finalize: 256 workgroups x (16 Gram entries x 16 slab partitions)
+constexpr int kFinBlocks = kGram / 16;
 
 // ~64 rows per partial workgroup (short dependent MFMA/load chains, enough
 // workgroups to spread over the CUs), at most 1024 slabs
@@ -103,25 +105,38 @@ __global__ __launch_bounds__(256) void recon_finalize_k(float *__restrict__ part
                                                         float *__restrict__ loss,
                                                         const int32_t *__restrict__ dims) {
     const int64_t n = eff_count(dims, 0, ncap), n_edges = eff_count(dims, 1, ecap);
-    const int e = blockIdx.x * 256 + threadIdx.x;  // Gram entry
+    const int el = threadIdx.x & 15, sp = threadIdx.x >> 4;
+    const int e = blockIdx.x * 16 + el;  // Gram entry
     double acc = 0.0;
-    int b = 0;
-    for (; b + 8 <= G; b += 8) {  // 8 independent loads in flight, summed in order
+    for (int b0 = sp; b0 < G; b0 += 16 * 8) {  // 8 independent loads in flight
         float v[8];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] = partials[(int64_t)(b + j) * kGram + e];
+        for (int j = 0; j < 8; ++j) {
+            const int b = b0 + 16 * j < G ? b0 + 16 * j : sp;  // clamped: unconditional loads
+            v[j] = partials[(int64_t)b * kGram + e];
+        }
 #pragma unroll
-        for (int j = 0; j < 8; ++j) acc += static_cast<double>(v[j]);
+        for (int j = 0; j < 8; ++j)
+            if (b0 + 16 * j < G) acc += static_cast<double>(v[j]);
     }
-    for (; b < G; ++b) acc += static_cast<double>(partials[(int64_t)b * kGram + e]);
-    gram[e] = static_cast<float>(acc);
-    __shared__ double red[256];
-    red[threadIdx.x] = acc * acc;
+    __shared__ double part[16][17];
+    __shared__ double red[16];
+    part[sp][el] = acc;
     __syncthreads();
-    for (int off = 128; off >= 1; off >>= 1) {
-        if (threadIdx.x < off) red[threadIdx.x] += red[threadIdx.x + off];
-        __syncthreads();
+    if (threadIdx.x < 16) {
+        double g = 0.0;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) g += part[k][threadIdx.x];
+        gram[blockIdx.x * 16 + threadIdx.x] = static_cast<float>(g);
+        red[threadIdx.x] = g * g;
     }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double q = 0.0;
+        for (int k = 0; k < 16; ++k) q += red[k];
+        red[0] = q;
+    }
+    __syncthreads();
     double *gsq = reinterpret_cast<double *>(partials + off_gsq(G));
     unsigned *cnt = reinterpret_cast<unsigned *>(partials + off_cnt(G));
     __shared__ unsigned ticket;
@@ -134,16 +149,25 @@ __global__ __launch_bounds__(256) void recon_finalize_k(float *__restrict__ part
     }
     __syncthreads();
     if (ticket != kFinBlocks - 1) return;  // not the last arriver
-    if (threadIdx.x == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        double g2 = 0.0;
-        for (int b = 0; b < kFinBlocks; ++b) g2 += __hip_atomic_load(&gsq[b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        double es = 0.0;
-        const float *ep = partials + off_edge(G);
-        for (int b = 0; b < G; ++b) es += static_cast<double>(ep[b]);
-        *loss = static_cast<float>((g2 - 2.0 * es + static_cast<double>(n_edges)) / static_cast<double>(n));
+    // last arriver: ||G||^2 from the 256 partials and the edge term, fixed order
+    __shared__ double fin[2][256];
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    fin[0][threadIdx.x] = __hip_atomic_load(&gsq[threadIdx.x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    double es = 0.0;
+    const float *ep = partials + off_edge(G);
+    for (int b = threadIdx.x; b < G; b += 256) es += static_cast<double>(ep[b]);
+    fin[1][threadIdx.x] = es;
+    __syncthreads();
+    for (int off = 128; off >= 1; off >>= 1) {
+        if (threadIdx.x < off) {
+            fin[0][threadIdx.x] += fin[0][threadIdx.x + off];
+            fin[1][threadIdx.x] += fin[1][threadIdx.x + off];
+        }
+        __syncthreads();
     }
+    if (threadIdx.x == 0)
+        *loss = static_cast<float>((fin[0][0] - 2.0 * fin[1][0] + static_cast<double>(n_edges)) /
+                                   static_cast<double>(n));
 }
 
 __global__ __launch_bounds__(256) void recon_bwd_k(const float *__restrict__ im,

@@ -99,6 +99,13 @@ class _GinEncoder(torch.autograd.Function):
         L = len(gin.ginlayers)
         ntiles = int(_lib.query("scgib_gin_tiles", n))
         tstats = torch.empty(max(ntiles, 1), 128, dtype=torch.float32, device=dev)
+        # training: BN finalize folded into the layer kernel (one counter set
+        # per encoder module: the two encoders run on concurrent streams)
+        fused = training and n > 0
+        if fused:
+            bn_ws = torch.empty(int(_lib.query("scgib_gin_bn_ws_floats", n)), dtype=torch.float32,
+                                device=dev)
+            cnt = counters(dev, ("gin", id(gin)), int(_lib.query("scgib_gin_counters", n)))
         saved, h, stat_prev = [], h0, None
         for l in range(L):
             conv, bn = gin.ginlayers[l], gin.batch_norms[l]
@@ -111,17 +118,27 @@ class _GinEncoder(torch.autograd.Function):
             r = torch.empty(n, HIDDEN, dtype=torch.float32, device=dev)
             z2 = torch.empty(n, HIDDEN, dtype=torch.float32, device=dev)
             meta = {"n": n, "e": graph.edge_capacity(), "d_in": d_in}
-            _launch("scgib_gin_layer_fwd", meta, _p(h), d_in, _p(stat_prev), _p(graph.rowptr),
-                      _p(graph.col), n, conv._one_plus_eps, _p(w1), _p(b1), _p(w2), _p(b2),
-                      _p(agg), _p(r), _p(z2), _p(tstats), _p(graph.dims), st)
             stat = torch.empty(4, HIDDEN, dtype=torch.float32, device=dev)
             track = training and bn.track_running_stats
-            _lib.call("scgib_bn_finalize", _p(tstats), n, _p(gamma), _p(beta), float(bn.eps),
-                      float(bn.momentum if bn.momentum is not None else 0.1), int(training),
-                      _p(bn.running_mean) if (track or not training) else None,
-                      _p(bn.running_var) if (track or not training) else None,
-                      _p(bn.num_batches_tracked) if track else None, _p(stat),
-                      _p(graph.dims), st)
+            momentum = float(bn.momentum if bn.momentum is not None else 0.1)
+            if fused:
+                _launch("scgib_gin_layer_fwd_bn", meta, _p(h), d_in, _p(stat_prev),
+                        _p(graph.rowptr), _p(graph.col), n, conv._one_plus_eps, _p(w1), _p(b1),
+                        _p(w2), _p(b2), _p(agg), _p(r), _p(z2), _p(gamma), _p(beta),
+                        float(bn.eps), momentum, _p(bn.running_mean) if track else None,
+                        _p(bn.running_var) if track else None,
+                        _p(bn.num_batches_tracked) if track else None, _p(stat), _p(bn_ws),
+                        _p(cnt), _p(graph.dims), st)
+            else:
+                _launch("scgib_gin_layer_fwd", meta, _p(h), d_in, _p(stat_prev),
+                        _p(graph.rowptr), _p(graph.col), n, conv._one_plus_eps, _p(w1), _p(b1),
+                        _p(w2), _p(b2), _p(agg), _p(r), _p(z2), _p(tstats), _p(graph.dims), st)
+                _lib.call("scgib_bn_finalize", _p(tstats), n, _p(gamma), _p(beta), float(bn.eps),
+                          momentum, int(training),
+                          _p(bn.running_mean) if (track or not training) else None,
+                          _p(bn.running_var) if (track or not training) else None,
+                          _p(bn.num_batches_tracked) if track else None, _p(stat),
+                          _p(graph.dims), st)
             saved += [agg, r, z2, stat]
             h, stat_prev = z2, stat
         out = torch.empty(n, HIDDEN, dtype=torch.float32, device=dev)
@@ -129,6 +146,7 @@ class _GinEncoder(torch.autograd.Function):
         ctx.save_for_backward(*saved, *params)
         ctx.graph, ctx.L, ctx.training = graph, L, training
         ctx.opes = [c._one_plus_eps for c in gin.ginlayers]
+        ctx.cnt_key = ("gin_bwd", id(gin))
         return out
 
     @staticmethod
@@ -140,8 +158,9 @@ class _GinEncoder(torch.autograd.Function):
         n = g_out.shape[0]
         dev = g_out.device
         st = _stream()
-        ntiles = int(_lib.query("scgib_gin_tiles", n))
-        tstats = torch.empty(max(ntiles, 1), 128, dtype=torch.float32, device=dev)
+        bn_ws = torch.empty(int(_lib.query("scgib_gin_bn_ws_floats", n)), dtype=torch.float32,
+                            device=dev)
+        cnt = counters(dev, ctx.cnt_key, int(_lib.query("scgib_gin_counters", n)))
         grads = [None] * (6 * L)
         dagg_next = None
         for l in reversed(range(L)):
@@ -149,17 +168,18 @@ class _GinEncoder(torch.autograd.Function):
             w1, _, w2 = params[6 * l], params[6 * l + 1], params[6 * l + 2]
             d_in = agg.shape[1]
             dy = torch.empty(n, HIDDEN, dtype=torch.float32, device=dev)
-            if dagg_next is None:
-                _lib.call("scgib_gin_bwd_stats", _p(g_out), None, None, 1.0, _p(z2), _p(stat), n,
-                          _p(dy), _p(tstats), _p(gr.dims), st)
-            else:
-                _lib.call("scgib_gin_bwd_stats", _p(dagg_next), _p(gr.rowptr_t), _p(gr.col_t),
-                          ctx.opes[l + 1], _p(z2), _p(stat), n, _p(dy), _p(tstats), _p(gr.dims),
-                          st)
             bn_g = torch.empty(2, HIDDEN, dtype=torch.float32, device=dev)  # dgamma, dbeta
             coef = torch.empty(2, HIDDEN, dtype=torch.float32, device=dev)
-            _lib.call("scgib_bn_bwd_finalize", _p(tstats), n, int(ctx.training), _p(bn_g[0]),
-                      _p(bn_g[1]), _p(coef), _p(gr.dims), st)
+            # dy, tile sums and the BN-backward finalize in one launch
+            if dagg_next is None:
+                _lib.call("scgib_gin_bwd_stats_bn", _p(g_out), None, None, 1.0, _p(z2),
+                          _p(stat), n, int(ctx.training), _p(dy), _p(bn_g[0]), _p(bn_g[1]),
+                          _p(coef), _p(bn_ws), _p(cnt), _p(gr.dims), st)
+            else:
+                _lib.call("scgib_gin_bwd_stats_bn", _p(dagg_next), _p(gr.rowptr_t),
+                          _p(gr.col_t), ctx.opes[l + 1], _p(z2), _p(stat), n, int(ctx.training),
+                          _p(dy), _p(bn_g[0]), _p(bn_g[1]), _p(coef), _p(bn_ws), _p(cnt),
+                          _p(gr.dims), st)
             dagg = torch.empty(n, d_in, dtype=torch.float32, device=dev)
             slab = torch.empty(int(_lib.query("scgib_gin_slab_floats", n, d_in)),
                                dtype=torch.float32, device=dev)

@@ -9,6 +9,7 @@ What runs from the reference (imported behind ``oracle/refshim.py``):
   * ``util.load_dgl_fromPyG``                       util.py:277-325
   * ``models.Mainmodel``  forward/backward          models.py:546-782
   * ``models.Mainmodel_continue`` forward/backward  models.py:1010-1276
+  * ``models.Mainmodel_finetuning`` forward + loss  models.py:358-543
 The DGL primitives underneath are the restatements in
 ``oracle/dgl_semantics.py`` (DGL itself is absent: parity at the DGL boundary
 is unpinned).
@@ -257,6 +258,88 @@ def gen_model_golden(models, util_mod, name, *, workload, F, B, L, k, continue_w
           f"losses kl={kl.item():.6g} con={con.item():.6g} rec={rec_loss.item():.6g}")
 
 
+def gen_finetune_golden(models, util_mod, name, *, workload, F, B, k, dataset, num_classes,
+                        loss_kind, seed):
+    """Mainmodel_finetuning (models.py:358-543) on a pretrained
+    Mainmodel_continue: scores, loss, trainable-parameter gradients (the
+    freezing quirk decides which), with recorded noise."""
+    torch.manual_seed(seed)
+    mols = synth.molecules(B, workload, seed=seed, mu=12.0, sigma=4.0, F=F)
+    graphs, subgraphs = [], []
+    for ei, x in mols:
+        g = util_mod.load_dgl_fromPyG(SimpleNamespace(edge_index=torch.from_numpy(ei),
+                                                      x=torch.from_numpy(x)))
+        graphs.append(g)
+        subgraphs.append([D.khop_in_subgraph(g, v, k=k)[0] for v in g.nodes()])
+    batch_g = D.batch(graphs)
+    ego_g = D.batch(list(chain.from_iterable(subgraphs)))
+    batch_x = F_normalize(batch_g.ndata["x"].float())                 # train_tudataset.py:139
+    x_subs = F_normalize(ego_g.ndata["x"].float())                    # :140
+    args = SimpleNamespace(recons_type="adj", useAtt=1, readout_f="sum", d_transfer=32,
+                           device="cpu", batch_size=B, task="graph_classification",
+                           dataset=dataset)
+    inner = models.Mainmodel(args, F, hidden_dim=64, num_layers=4, num_heads=4,
+                             k_transition=k, encoder="GIN")
+    real_load = models.torch.load
+    try:
+        models.torch.load = lambda *a, **kw: inner  # in-memory: nothing is unpickled
+        pre = models.Mainmodel_continue(args, F, hidden_dim=64, num_layers=4, num_heads=4,
+                                        k_transition=k, num_classes=num_classes,
+                                        cp_filename="<mem>", encoder="GIN")
+        models.torch.load = lambda *a, **kw: pre
+        model = models.Mainmodel_finetuning(args, F, hidden_dim=64, num_layers=4, num_heads=4,
+                                            k_transition=k, num_classes=num_classes,
+                                            cp_filename="<mem>", encoder="GIN")
+    finally:
+        models.torch.load = real_load
+    model.train()
+    with torch.no_grad():
+        for n_, p_ in model.named_parameters():
+            if "batch_norms" in n_ or "compressor.1" in n_:
+                p_.add_(0.1 * torch.randn_like(p_))
+    state0 = {kk: v.detach().clone() for kk, v in model.state_dict().items()}
+    trainable = [kk for kk, p in model.named_parameters() if p.requires_grad]
+    targets = torch.randint(0, 2, (B,)) if loss_kind == "ce" else \
+        torch.randint(0, 2, (B, 1)).float()
+    torch.manual_seed(seed + 1000)
+    with _NoiseRecorder() as rec:
+        scores, *_ = model.forward(batch_g, batch_x, ego_g, x_subs, 1, batch_g.edges(), 2, "cpu",
+                                   B)
+    loss = model.loss_CrossEntropy(scores, targets) if loss_kind == "ce" else \
+        model.loss(scores, targets)
+    loss.backward()
+    draws = rec.draws
+    assert len(draws) == 2 * B, len(draws)
+    u_gate = torch.cat([draws[2 * i].reshape(-1) for i in range(B)])
+    u_feat = torch.cat([draws[2 * i + 1] for i in range(B)])
+    out = {
+        "B": np.array(B), "k": np.array(k), "F": np.array(F),
+        "num_classes": np.array(num_classes), "dataset": np.array(dataset),
+        "loss_kind": np.array(loss_kind),
+        "batch_num_nodes": batch_g.batch_num_nodes().numpy(),
+        "src": batch_g.src.numpy(), "dst": batch_g.dst.numpy(),
+        "x_raw": batch_g.ndata["x"].numpy(),
+        "ego_batch_num_nodes": ego_g.batch_num_nodes().numpy(),
+        "ego_src": ego_g.src.numpy(), "ego_dst": ego_g.dst.numpy(),
+        "u_gate": u_gate.numpy(), "u_feat": u_feat.numpy(),
+        "targets": targets.numpy(), "scores": scores.detach().numpy(),
+        "loss": loss.detach().numpy(),
+        "trainable": np.array(trainable),
+    }
+    gptr = np.concatenate([[0], np.cumsum(out["batch_num_nodes"])])
+    node_graph = np.repeat(np.arange(B), out["batch_num_nodes"])
+    ego_owner = np.repeat(np.arange(len(out["ego_batch_num_nodes"])), out["ego_batch_num_nodes"])
+    out["ego_nodes_global"] = ego_g.ndata["_ID"].numpy() + gptr[node_graph[ego_owner]]
+    for kk, v in state0.items():
+        out["param_" + kk] = v.numpy()
+    for kk, p in model.named_parameters():
+        if p.grad is not None:
+            out["grad_" + kk] = p.grad.numpy()
+    np.savez_compressed(os.path.join(OUT, f"{name}.npz"), **out)
+    print(f"wrote {name}.npz  N={len(out['x_raw'])} loss={loss.item():.6g} "
+          f"trainable={len(trainable)}")
+
+
 def F_normalize(x):
     return F.normalize(x)
 
@@ -273,6 +356,12 @@ def main():
                      k=1, continue_wrapper=True, seed=2, **common)
     gen_model_golden(models, util, "pretrain_L5_k2_ogb_continue", workload="pcqm4mv2", F=9,
                      L=5, k=2, continue_wrapper=True, seed=3, **common)
+    # fine-tune head: Mutagenicity (CE on sigmoid scores, train_tudataset.py:146) and
+    # molhiv (BCE, train_molhiv.py:144), k = 1 as hard-coded in exp_tudataset/exp_molhiv
+    gen_finetune_golden(models, util, "finetune_mutag_ce", workload="mutagenicity", F=14, B=8,
+                        k=1, dataset="Mutagenicity", num_classes=2, loss_kind="ce", seed=4)
+    gen_finetune_golden(models, util, "finetune_molhiv_bce", workload="molhiv", F=9, B=8, k=1,
+                        dataset="ogbg-molhiv", num_classes=1, loss_kind="bce", seed=5)
 
 
 if __name__ == "__main__":

@@ -204,3 +204,55 @@ def make_params(arrays, requires_grad=True):
             t.requires_grad_(requires_grad)
         out[k] = t
     return out
+
+
+# ---------------------------------------------------------------------------
+# Fine-tune head: Mainmodel_finetuning, models.py:358-543
+# ---------------------------------------------------------------------------
+FINETUNE_TASKS = ("ZINC", "Peptides-struct", "FreeSolv", "ESOL")  # models.py:384
+
+
+def set2set(p, prefix, feat, counts, n_iters=2):
+    """DGL Set2Set(d, n_iters, 1) (models.py:565 / :362): LSTM(2d -> d) on
+    q_star, per-graph softmax attention, readout = sum(alpha * feat);
+    q_star = [q || readout].  Functional single-layer LSTM, PyTorch gate order
+    (i, f, g, o)."""
+    B, d = len(counts), feat.shape[1]
+    seg = torch.repeat_interleave(torch.arange(B), counts)
+    w_ih, w_hh = p[prefix + ".lstm.weight_ih_l0"], p[prefix + ".lstm.weight_hh_l0"]
+    b = p[prefix + ".lstm.bias_ih_l0"] + p[prefix + ".lstm.bias_hh_l0"]
+    hx = feat.new_zeros(B, d)
+    cx = feat.new_zeros(B, d)
+    q_star = feat.new_zeros(B, 2 * d)
+    for _ in range(n_iters):
+        gates = q_star @ w_ih.t() + hx @ w_hh.t() + b
+        i, f, g, o = gates.chunk(4, dim=1)
+        cx = torch.sigmoid(f) * cx + torch.sigmoid(i) * torch.tanh(g)
+        hx = torch.sigmoid(o) * torch.tanh(cx)
+        q = hx
+        e = (feat * q[seg]).sum(dim=-1)
+        emax = torch.stack([e[seg == k].max() for k in range(B)])
+        a = torch.exp(e - emax[seg])
+        den = torch.zeros(B, dtype=feat.dtype).index_add(0, seg, a)
+        alpha = (a / den[seg]).unsqueeze(-1)
+        readout = sum_nodes(feat * alpha, counts)
+        q_star = torch.cat([q, readout], dim=-1)
+    return q_star
+
+
+def finetune_forward(p, batch, ego, x, x_subs, u_gate, u_feat, dataset, buffers=None):
+    """Mainmodel_finetuning.forward: own transfer_d -> the pretrained model's
+    extract_features (its wrapper-level encoders, "model." prefix) -> own MLP
+    -> Set2Set -> predict -> sigmoid (unless a regression dataset)."""
+    h0 = _linear(x, p, "transfer_d", bias=False)
+    hs0 = _linear(x_subs, p, "transfer_d", bias=False)
+    pre = {k[6:]: v for k, v in p.items() if k.startswith("model.")}
+    bufs = None if buffers is None else {k[6:]: v for k, v in buffers.items()
+                                         if k.startswith("model.")}
+    acts = extract_features(pre, batch, ego, h0, hs0, u_gate, u_feat, bufs)
+    im = _linear(F.relu(_linear(acts["interaction_map"], p, "MLP.0")), p, "MLP.2")
+    g = set2set(p, "s2s", im, batch["counts"])
+    scores = _linear(F.relu(_linear(g, p, "predict.0")), p, "predict.2")
+    if dataset not in FINETUNE_TASKS:
+        scores = torch.sigmoid(scores)
+    return scores

@@ -9,14 +9,16 @@ Layout:
   _lib.py      ctypes binding of libscgib.so (fails loudly when missing)
   graph.py     DGL-duck-typed graph batch (CSR int32, dst-major) + ingest
   ops.py       autograd Functions over the C-ABI
-  models.py    models.py-compatible Mainmodel / Mainmodel_continue / GIN
+  models.py    models.py-compatible Mainmodel / Mainmodel_continue /
+               Mainmodel_finetuning / GIN / Set2Set
+  metrics.py   ROC-AUC (OGB semantics) and TU accuracy of the fine-tune configs
   dgl.py       drop-in ``dgl`` surface (graph, batch, sum_nodes, khop...)
   dist.py      one-process-per-GPU data parallel (RCCL all-reduce)
   synth.py     seeded synthetic molecules
 """
 import importlib
 
-__all__ = ["graph", "ops", "models", "dgl", "dist", "synth", "_lib"]
+__all__ = ["graph", "ops", "models", "dgl", "dist", "synth", "metrics", "_lib"]
 
 
 def __getattr__(name):

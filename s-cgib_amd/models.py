@@ -365,30 +365,161 @@ class Mainmodel_continue(_SCGIBCore):
 
 
 # ---------------------------------------------------------------------------
+# Fine-tuning head (boundary §8(b))
+# ---------------------------------------------------------------------------
+class Mainmodel_finetuning(nn.Module):
+    """models.py:358-543: a pretrained model's extract_features (frozen except
+    the reference's freezing quirk) -> MLP -> Set2Set -> predict [-> sigmoid].
+
+    Same constructor/forward signatures and state_dict keys as the reference.
+    ``cp_filename`` is an in-memory pretrained module or a ``save_checkpoint``
+    file (the reference unpickles a whole module, models.py:425; such files
+    are not loaded here — INTEGRATION.md).  Kept quirks:
+      * freezing (models.py:427-436): every parameter of the pretrained model
+        is frozen, then the loop over ["layers.4", "layers.3", "layers.2"]
+        re-assigns requires_grad for each entry, so only the LAST entry wins —
+        exactly the names containing "layers.2" stay trainable;
+      * the pretrained Mainmodel_continue's own (wrapper-level) encoders run
+        in extract_features (models.py:1204-1252), and the compression noise
+        is applied in eval mode too;
+      * scores are sigmoid(predict(.)) unless the dataset is one of
+        ZINC / Peptides-struct / FreeSolv / ESOL (models.py:517-520).
+    Own Encoder1/Encoder2/compressor/embedding_h/reduce_d/attn_layer are
+    created for state_dict parity only (unused by forward, as in the reference).
+    """
+
+    TASKS = ["ZINC", "Peptides-struct", "FreeSolv", "ESOL"]
+
+    def __init__(self, args, in_dim, hidden_dim, num_layers, num_heads, k_transition,
+                 num_classes, cp_filename, encoder):
+        super().__init__()
+        self.tau = 1.0
+        self.dataset = getattr(args, "dataset", None)
+        self.readout = args.readout_f
+        self.s2s = Set2Set(hidden_dim, 2, 1)
+        self.in_dim = args.d_transfer
+        self.transfer_d = nn.Linear(in_dim, self.in_dim, bias=False)
+        self.batch_size = getattr(args, "batch_size", 16)
+        self.useAtt = args.useAtt
+        self.embedding_h = nn.Linear(self.in_dim, hidden_dim, bias=False)
+        self.hidden_dim = hidden_dim
+        self.k_transition = k_transition
+        self.reduce_d = nn.Linear(2 * hidden_dim, hidden_dim)
+        self.attn_layer = nn.Linear(2 * hidden_dim, 1)
+        self.num_nodes = -1
+        self.device = getattr(args, "device", None)
+        self.tasks = list(self.TASKS)
+        task = getattr(args, "task", "graph_classification")
+        if task not in ("graph_regression", "graph_classification"):
+            raise ValueError(f"task {task!r}: the reference builds no predict head for it")
+        out_dim = 1 if task == "graph_regression" else num_classes
+        self.predict = nn.Sequential(nn.Linear(2 * hidden_dim, hidden_dim), nn.ReLU(),
+                                     nn.Linear(hidden_dim, out_dim))
+        self.MLP = nn.Sequential(nn.Linear(2 * hidden_dim, hidden_dim), nn.ReLU(),
+                                 nn.Linear(hidden_dim, hidden_dim))
+        if encoder != "GIN":
+            raise NotImplementedError(f"encoder {encoder!r}: only GIN is on the hot path")
+        self.Encoder1 = GIN(self.in_dim, hidden_dim, _gin_layers(args))
+        self.Encoder2 = GIN(self.in_dim, hidden_dim, _gin_layers(args))
+        self.model = load_checkpoint(cp_filename, args)
+        freeze_like_reference(self.model)
+        self.compressor = nn.Sequential(nn.Linear(hidden_dim, hidden_dim),
+                                        nn.BatchNorm1d(hidden_dim), nn.ReLU(),
+                                        nn.Linear(hidden_dim, 1))
+
+    def forward(self, batch_g, batch_x, flatten_batch_subgraphs, x_subs, current_epoch=None,
+                edge_index=None, k_transition=None, device=None, batch_size=2, noise=None):
+        self.batch_size = batch_size
+        self.device = device
+        if flatten_batch_subgraphs is None:  # ego-nets built on the device
+            flatten_batch_subgraphs, x_subs = self._prepare_ego(batch_g, batch_x, x_subs)
+        batch_x = self.transfer_d(batch_x)
+        x_subs = self.transfer_d(x_subs)
+        im = self.model.extract_features(None, batch_g, batch_x, flatten_batch_subgraphs, x_subs,
+                                         device, noise)[0]
+        im = ops.mlp2(im, self.MLP, batch_g.dims)
+        im = self.s2s(batch_g, im)
+        scores = self.predict(im)
+        if self.dataset in self.tasks:
+            return scores, 0, 0, 0
+        return torch.sigmoid(scores), 0, 0, 0
+
+    def _prepare_ego(self, batch_g, batch_x, x_subs):
+        k = getattr(self.model, "k_transition", self.k_transition)
+        ego = G.egonet_batch(batch_g, k)
+        if x_subs is None:
+            x_subs = batch_x.index_select(0, ego.ndata["_ID"])
+        return ego, x_subs
+
+    # losses (models.py:522-543)
+    def loss(self, scores, targets):
+        return F.binary_cross_entropy(scores.float(), targets.float())
+
+    def loss_CrossEntropy(self, scores, targets):
+        return F.cross_entropy(scores.to(torch.float32), targets.squeeze(dim=-1))
+
+    def loss_RMSE(self, scores, targets):
+        return torch.sqrt(F.mse_loss(scores, targets))
+
+    def BCEWithLogitsLoss(self, scores, targets):
+        return F.binary_cross_entropy_with_logits(scores, targets)
+
+    def lossMAE(self, scores, targets):
+        return F.l1_loss(scores, targets)
+
+
+def freeze_like_reference(model, num_layers=4):
+    """The reference's freezing loop (models.py:427-436), literally: for every
+    parameter, requires_grad is re-assigned once per entry of
+    unfrezz_layers, so the last entry ("layers.2") decides."""
+    for p in model.parameters():
+        p.requires_grad = False
+    unfrezz_layers = ["layers." + str(num_layers), "layers." + str(num_layers - 1),
+                      "layers." + str(num_layers - 2)]
+    for name, para in model.named_parameters():
+        for layer in unfrezz_layers:
+            para.requires_grad = layer in name
+
+
+# ---------------------------------------------------------------------------
 # checkpoints: state_dict based (the reference pickles whole modules,
 # exp_pretraining.py:107; such files are not loaded here, see INTEGRATION.md)
 # ---------------------------------------------------------------------------
-def save_checkpoint(model, path, args=None, in_dim=None):
+_CKPT_ARGS = ("recons_type", "useAtt", "readout_f", "d_transfer", "gin_layers", "task",
+              "batch_size")
+
+
+def save_checkpoint(model, path, args=None, in_dim=None, num_classes=1):
+    """state_dict checkpoint of a Mainmodel or Mainmodel_continue (the nested
+    inner model included), loadable with weights_only=True."""
     cfg = {}
     if args is not None:
-        cfg = {k: getattr(args, k) for k in ("recons_type", "useAtt", "readout_f", "d_transfer",
-                                             "gin_layers") if hasattr(args, k)}
+        cfg = {k: getattr(args, k) for k in _CKPT_ARGS if hasattr(args, k)}
     cfg.update(kind=type(model).__name__, in_dim=in_dim, hidden_dim=model.hidden_dim,
-               k_transition=model.k_transition)
+               k_transition=model.k_transition, num_classes=num_classes)
     torch.save({"config": cfg, "state_dict": model.state_dict()}, path)
 
 
 def load_checkpoint(cp, args):
-    """A Mainmodel from an in-memory module or a save_checkpoint() file."""
+    """A Mainmodel / Mainmodel_continue from an in-memory module or a
+    save_checkpoint() file (weights only: nothing is unpickled)."""
     if isinstance(cp, nn.Module):
         return cp
     blob = torch.load(cp, map_location="cpu", weights_only=True)
     cfg = blob["config"]
     ns = type("Args", (), {})()
-    for k in ("recons_type", "useAtt", "readout_f", "d_transfer", "gin_layers"):
+    for k in _CKPT_ARGS:
         setattr(ns, k, cfg.get(k, getattr(args, k, None)))
-    if cfg.get("kind") != "Mainmodel":
-        raise NotImplementedError("nested Mainmodel_continue checkpoints: load the inner model")
-    m = Mainmodel(ns, cfg["in_dim"], cfg["hidden_dim"], 4, 4, cfg["k_transition"], "GIN")
+    if ns.task is None:
+        ns.task = "graph_classification"
+    kind = cfg.get("kind")
+    inner = Mainmodel(ns, cfg["in_dim"], cfg["hidden_dim"], 4, 4, cfg["k_transition"], "GIN")
+    if kind == "Mainmodel":
+        m = inner
+    elif kind == "Mainmodel_continue":
+        m = Mainmodel_continue(ns, cfg["in_dim"], cfg["hidden_dim"], 4, 4, cfg["k_transition"],
+                               cfg.get("num_classes", 1), inner, "GIN")
+    else:
+        raise NotImplementedError(f"checkpoint kind {kind!r}")
     m.load_state_dict(blob["state_dict"])
     return m

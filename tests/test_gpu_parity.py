@@ -416,3 +416,52 @@ def test_mlp2_fwd_bwd(pkg, dev, d_in, n):
     assert rel_l2(xd.grad.cpu(), xr.grad) < 1e-5
     for p, r in zip(mlp_d.parameters(), ref):
         assert rel_l2(p.grad.cpu(), r.grad) < 1e-5
+
+
+# ---------------------------------------------------------------------------
+# Fine-tune head (Mainmodel_finetuning) vs the reference's own outputs
+# ---------------------------------------------------------------------------
+def _finetune_model(pkg, g, dev):
+    from types import SimpleNamespace
+    args = SimpleNamespace(recons_type="adj", useAtt=1, readout_f="sum", d_transfer=32,
+                           batch_size=int(g["B"]), gin_layers=4, task="graph_classification",
+                           dataset=str(g["dataset"]), device=dev)
+    F_in, C, k = int(g["F"]), int(g["num_classes"]), int(g["k"])
+    inner = pkg.models.Mainmodel(args, F_in, 64, 4, 4, k, "GIN")
+    pre = pkg.models.Mainmodel_continue(args, F_in, 64, 4, 4, k, C, inner, "GIN")
+    ft = pkg.models.Mainmodel_finetuning(args, F_in, 64, 4, 4, k, C, pre, "GIN")
+    state = {k_[6:]: torch.tensor(v) for k_, v in g.items() if k_.startswith("param_")}
+    missing, unexpected = ft.load_state_dict(state, strict=False)
+    assert not missing and not unexpected, (missing, unexpected)
+    return ft.to(dev).train()
+
+
+@pytest.mark.parametrize("name", ["finetune_mutag_ce", "finetune_molhiv_bce"])
+@pytest.mark.parametrize("device_ego", [True, False])
+def test_finetune_matches_reference(pkg, dev, name, device_ego):
+    g = load_golden(name)
+    ft = _finetune_model(pkg, g, dev)
+    trainable = {n for n, p in ft.named_parameters() if p.requires_grad}
+    assert trainable == set(str(s) for s in g["trainable"])  # the freezing quirk
+    bg = pkg.graph.GraphBatch.from_edges(g["src"], g["dst"], len(g["x_raw"]), True,
+                                         g["batch_num_nodes"]).to(dev)
+    x = F.normalize(torch.tensor(g["x_raw"]).float()).to(dev)
+    if device_ego:
+        ego, x_subs = None, None
+    else:
+        ego = pkg.graph.GraphBatch.from_edges(g["ego_src"], g["ego_dst"],
+                                              int(g["ego_batch_num_nodes"].sum()), True,
+                                              g["ego_batch_num_nodes"]).to(dev)
+        x_subs = x[torch.tensor(g["ego_nodes_global"], device=dev)]
+    noise = (torch.tensor(g["u_gate"], device=dev), torch.tensor(g["u_feat"], device=dev))
+    scores, *_ = ft(bg, x, ego, x_subs, 1, None, 2, dev, int(g["B"]), noise=noise)
+    assert rel_err(scores.detach().cpu(), g["scores"]) < 1e-4
+    t = torch.tensor(g["targets"], device=dev)
+    loss = ft.loss_CrossEntropy(scores, t) if str(g["loss_kind"]) == "ce" else ft.loss(scores, t)
+    assert rel_err(loss.item(), g["loss"]) < 1e-4
+    loss.backward()
+    params = dict(ft.named_parameters())
+    check_grads_model({k[5:]: v for k, v in g.items() if k.startswith("grad_")},
+                      lambda n: params[n].grad, tol=1e-3)
+    # frozen parameters never receive a gradient
+    assert all(p.grad is None for n, p in params.items() if n not in trainable)

@@ -213,3 +213,24 @@ def test_ctypes_table_matches_header_prototypes(pkg):
     assert set(protos) == set(L.SIGNATURES)
     for name, (_, argtypes) in L.SIGNATURES.items():
         assert [kind[t] for t in argtypes] == protos[name], name
+
+
+def test_checkpoint_roundtrip_continue(pkg, tmp_path):
+    """save_checkpoint / load_checkpoint of a nested Mainmodel_continue (weights
+    only, nothing unpickled) and the fine-tune freezing quirk on top of it."""
+    from types import SimpleNamespace
+    args = SimpleNamespace(recons_type="adj", useAtt=1, readout_f="sum", d_transfer=32,
+                           batch_size=8, gin_layers=4, task="graph_classification",
+                           dataset="Mutagenicity")
+    inner = pkg.models.Mainmodel(args, 14, 64, 4, 4, 1, "GIN")
+    pre = pkg.models.Mainmodel_continue(args, 14, 64, 4, 4, 1, 2, inner, "GIN")
+    path = str(tmp_path / "pre.pt")
+    pkg.models.save_checkpoint(pre, path, args, in_dim=14, num_classes=2)
+    back = pkg.models.load_checkpoint(path, args)
+    a, b = pre.state_dict(), back.state_dict()
+    assert set(a) == set(b) and all(torch.equal(a[k], b[k]) for k in a)
+    ft = pkg.models.Mainmodel_finetuning(args, 14, 64, 4, 4, 1, 2, path, "GIN")
+    frozen = {n for n, p in ft.named_parameters() if not p.requires_grad}
+    assert frozen and all(n.startswith("model.") and "layers.2" not in n for n in frozen)
+    assert all(p.requires_grad for n, p in ft.named_parameters()
+               if n.startswith("model.") and "layers.2" in n)

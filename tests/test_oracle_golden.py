@@ -6,7 +6,7 @@ import pytest
 import torch
 import torch.nn.functional as F
 
-from conftest import MODEL_GOLDENS, check_grads, load_golden
+from conftest import MODEL_GOLDENS, check_grads, load_golden, rel_err, rel_l2
 from oracle import scgib_ref as R
 
 
@@ -51,3 +51,41 @@ def test_oracle_matches_reference_golden(name):
         if k.startswith("after_"):
             assert np.allclose(buffers[R.strip_continue({k[6:]: 0}).popitem()[0]].numpy(), v,
                                rtol=1e-5, atol=1e-6), k
+
+
+# ---------------------------------------------------------------------------
+# Fine-tune head: oracle restatement vs the reference's Mainmodel_finetuning
+# ---------------------------------------------------------------------------
+FINETUNE_GOLDENS = ["finetune_mutag_ce", "finetune_molhiv_bce"]
+
+
+def finetune_inputs(g):
+    counts = torch.tensor(g["batch_num_nodes"])
+    batch = {"src": torch.tensor(g["src"]), "dst": torch.tensor(g["dst"]), "counts": counts}
+    ego = {"src": torch.tensor(g["ego_src"]), "dst": torch.tensor(g["ego_dst"]),
+           "counts": torch.tensor(g["ego_batch_num_nodes"])}
+    x = F.normalize(torch.tensor(g["x_raw"]).float())
+    x_subs = x[torch.tensor(g["ego_nodes_global"])]
+    return batch, ego, x, x_subs
+
+
+@pytest.mark.parametrize("name", FINETUNE_GOLDENS)
+def test_oracle_finetune_matches_reference(name):
+    g = load_golden(name)
+    batch, ego, x, x_subs = finetune_inputs(g)
+    p = R.make_params({k[6:]: v for k, v in g.items() if k.startswith("param_")})
+    buffers = {k: v.clone() for k, v in p.items() if "running" in k or "num_batches" in k}
+    scores = R.finetune_forward(p, batch, ego, x, x_subs, torch.tensor(g["u_gate"]),
+                                torch.tensor(g["u_feat"]), str(g["dataset"]), buffers)
+    assert rel_err(scores.detach(), g["scores"]) < 1e-5
+    t = torch.tensor(g["targets"])
+    loss = (F.cross_entropy(scores, t.squeeze(-1)) if str(g["loss_kind"]) == "ce"
+            else F.binary_cross_entropy(scores, t.float()))
+    assert rel_err(loss.item(), g["loss"]) < 1e-5
+    loss.backward()
+    trainable = set(str(s) for s in g["trainable"])
+    golden_grads = {k[5:]: v for k, v in g.items() if k.startswith("grad_")}
+    assert set(golden_grads) <= trainable
+    # frozen by the quirk: pretrained parameters outside "layers.2"
+    assert not any(k.startswith("model.") and "layers.2" not in k for k in golden_grads)
+    check_grads(golden_grads, lambda n_: p[n_].grad, tol=1e-4, metric="l2")

@@ -253,6 +253,20 @@ int scgib_recon_bwd(const float *im, const float *gram, const int32_t *rowptr_in
                     int64_t n_nodes, const float *g_loss, float *grad_im,
                     const int32_t *dims, scgib_stream_t stream);
 
+/* ---- A15: logM reconstruction loss (models.py:770-782) --------------------
+ * loss = (1/k) sum_g sum_i ||X_g X_g^T - logM_g,i||_F^2 / n_g^2, X_g = the rows
+ * of `im` [N][64] of molecule g (graph_ptr).  Targets per molecule, packed at
+ * int64 s_offsets[B+1] (n_g^2 floats each): S = sum_i logM_i, and
+ * C[g] = sum_i ||logM_i||^2 (fp64).  loss_graphs [B] holds per-molecule terms;
+ * loss is a device scalar (fixed-order sum).  Backward: grad_im [N][64] =
+ * 2 g_loss (2k X X^T - S - S^T) X / (k n_g^2) per molecule. */
+int scgib_recon_logm_fwd(const float *im, const int32_t *graph_ptr, int64_t n_graphs,
+                         const float *S, const int64_t *s_offsets, const double *C,
+                         int32_t kstep, float *loss_graphs, float *loss, scgib_stream_t stream);
+int scgib_recon_logm_bwd(const float *im, const int32_t *graph_ptr, int64_t n_graphs,
+                         const float *S, const int64_t *s_offsets, int32_t kstep,
+                         const float *g_loss, float *grad_im, scgib_stream_t stream);
+
 /* ---- A11: contrastive loss (batched_semi_loss, tau = 1) --------------------
  * models.py:606-629 (sim :606-609, semi_loss :611-616, batched :618-629;
  * called at models.py:695 with z1 = sum_nodes(noisy), z2 = graph readout).

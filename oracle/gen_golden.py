@@ -148,7 +148,7 @@ def _grow_gin(models, gin, layers):
 
 
 def gen_model_golden(models, util_mod, name, *, workload, F, B, L, k, continue_wrapper,
-                     chunk, seed):
+                     chunk, seed, recons_type="adj"):
     torch.manual_seed(seed)
     mols = synth.molecules(B - 1, workload, seed=seed, mu=12.0, sigma=4.0, F=F)
     # always include the smallest legal molecule (2 atoms) in the middle
@@ -166,9 +166,14 @@ def gen_model_golden(models, util_mod, name, *, workload, F, B, L, k, continue_w
     batch_x = F_normalize(batch_g.ndata["x"].float())                  # exp_pretraining.py:312
     x_subs = F_normalize(ego_g.ndata["x"].float())                     # exp_pretraining.py:314
 
-    args = SimpleNamespace(recons_type="adj", useAtt=1, readout_f="sum", d_transfer=32,
+    args = SimpleNamespace(recons_type=recons_type, useAtt=1, readout_f="sum", d_transfer=32,
                            device="cpu", batch_size=chunk, task="graph_classification",
                            dataset="pre-train")
+    batch_logMs = None
+    if recons_type == "logM":
+        # util.getM_logM (util.py:74-91) per molecule, as exp_tudataset.py:430-433 does
+        batch_logMs = [torch.from_numpy(np.array(util_mod.getM_logM(g, kstep=k)[1])).float()
+                       for g in graphs]
     inner = models.Mainmodel(args, F, hidden_dim=64, num_layers=4, num_heads=4,
                              k_transition=k, encoder="GIN")
     _grow_gin(models, inner.Encoder1, L)
@@ -207,7 +212,7 @@ def gen_model_golden(models, util_mod, name, *, workload, F, B, L, k, continue_w
 
     torch.manual_seed(seed + 1000)
     with _NoiseRecorder() as rec:
-        _, kl, con, rec_loss = model.forward(batch_g, batch_x, ego_g, None, x_subs, 1,
+        _, kl, con, rec_loss = model.forward(batch_g, batch_x, ego_g, batch_logMs, x_subs, 1,
                                              batch_g.edges(), 2, "cpu", chunk)
     for h in hooks:
         h.remove()
@@ -231,7 +236,10 @@ def gen_model_golden(models, util_mod, name, *, workload, F, B, L, k, continue_w
         "u_gate": u_gate.numpy(), "u_feat": u_feat.numpy(),
         "loss_kl": kl.detach().numpy(), "loss_contrastive": con.detach().numpy(),
         "loss_recon": rec_loss.detach().numpy(), "loss_total": loss.detach().numpy(),
+        "recons_type": np.array(recons_type),
     }
+    if batch_logMs is not None:  # ragged [k, n_i, n_i] per molecule, flattened
+        out["logm_flat"] = np.concatenate([m.numpy().reshape(-1) for m in batch_logMs])
     # ego node ids in the batched ego graph are local to each molecule: make
     # them global (ego j belongs to molecule graph_of(j))
     gptr = np.concatenate([[0], np.cumsum(out["batch_num_nodes"])])
@@ -356,6 +364,10 @@ def main():
                      k=1, continue_wrapper=True, seed=2, **common)
     gen_model_golden(models, util, "pretrain_L5_k2_ogb_continue", workload="pcqm4mv2", F=9,
                      L=5, k=2, continue_wrapper=True, seed=3, **common)
+    # logM reconstruction (A15): Mutagenicity's pretraining default
+    # (exp_tudataset.py:538), k_transition 2 -> two transition powers
+    gen_model_golden(models, util, "pretrain_L4_k2_logm", workload="mutagenicity", F=14, L=4,
+                     k=2, continue_wrapper=False, seed=6, recons_type="logM", **common)
     # fine-tune head: Mutagenicity (CE on sigmoid scores, train_tudataset.py:146) and
     # molhiv (BCE, train_molhiv.py:144), k = 1 as hard-coded in exp_tudataset/exp_molhiv
     gen_finetune_golden(models, util, "finetune_mutag_ce", workload="mutagenicity", F=14, B=8,

@@ -157,6 +157,18 @@ def recon_adj_dense(im, src, dst):
     return torch.sum((im @ im.t() - adj) ** 2) / n
 
 
+def recon_logm(im, logms, counts, kstep):
+    """loss_recon (models.py:770-782), literally: per molecule h = X X^T and
+    sum over the k targets of sum((h - logM_i)^2) / (n^2), then / k."""
+    loss = 0
+    for X, L in zip(torch.split(im, tuple(int(c) for c in counts)), logms):
+        h = X @ X.t()
+        n = h.shape[0]
+        for i in range(kstep):
+            loss = loss + torch.sum((h - L[i]) ** 2) / (n * n)
+    return loss / kstep
+
+
 def extract_features(p, batch, ego, h0, hs0, u_gate, u_feat, buffers):
     L = num_gin_layers(p)
     gf = gin_encoder(p, "Encoder1", batch["src"], batch["dst"], h0, buffers, L)
@@ -170,7 +182,7 @@ def extract_features(p, batch, ego, h0, hs0, u_gate, u_feat, buffers):
 
 
 def pretrain_forward(p, batch, ego, x, x_subs, u_gate, u_feat, chunk, buffers=None,
-                     dense_recon=True):
+                     dense_recon=True, logms=None, kstep=None):
     """Mainmodel.forward (A13) == Mainmodel_continue.forward (A14).
 
     ``x`` / ``x_subs`` are the already-normalised features, as the training loop
@@ -184,7 +196,9 @@ def pretrain_forward(p, batch, ego, x, x_subs, u_gate, u_feat, chunk, buffers=No
     kl = torch.mean(acts["kl_tensor"])
     z1 = sum_nodes(acts["noisy"], batch["counts"])
     con = semi_loss(z1, acts["graph_readout"], chunk)
-    if dense_recon:
+    if logms is not None:  # recons_type == 'logM'
+        rec = recon_logm(im, logms, batch["counts"], kstep)
+    elif dense_recon:
         rec = recon_adj_dense(im, batch["src"], batch["dst"])
     else:  # Gram form (exact restatement, used for large oracle runs)
         g = im.t() @ im

@@ -33,6 +33,8 @@ SIGNATURES = {
     "scgib_interaction_bwd": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _I64, _I64, _P,
                                              _P, _P, _P, _F, _I32, _P, _P, _P, _P, _P, _P, _P,
                                              _P, _P, _P, _P, _I32, _P, _P]),
+    "scgib_recon_logm_fwd": (ctypes.c_int, [_P, _P, _I64, _P, _P, _P, _I32, _P, _P, _P]),
+    "scgib_recon_logm_bwd": (ctypes.c_int, [_P, _P, _I64, _P, _P, _I32, _P, _P, _P]),
     "scgib_contrastive_workspace_floats": (_I64, [_I64]),
     "scgib_contrastive_counters": (_I64, [_I64]),
     "scgib_contrastive_fwd": (ctypes.c_int, [_P, _P, _I64, _P, _P, _P, _P]),

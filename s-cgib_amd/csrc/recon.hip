@@ -207,9 +207,117 @@ __global__ __launch_bounds__(256) void recon_bwd_k(const float *__restrict__ im,
     }
 }
 
+// ---------------------------------------------------------------------------
+// A15: logM reconstruction loss (models.py:770-782), per molecule g with
+// X = IM rows of g, h = X X^T and the k targets L_i [n, n]:
+//   loss = (1/k) sum_g sum_i sum_uv (h_uv - L_i,uv)^2 / n_g^2
+//        = sum_g [k ||h||^2 - 2 <h, S_g> + C_g] / (k n_g^2),
+//   S_g = sum_i L_i, C_g = sum_i ||L_i||^2 (precomputed, graph.LogMBatch);
+//   d loss / d X = 2 g (2k h - S - S^T) X / (k n_g^2).
+// One workgroup per molecule; 16 row groups x 16 lanes (float4 channels):
+// h_uv = 16-lane butterfly of the row dots, never materialised.  fp64
+// accumulation of the expanded loss (the terms cancel when h ~ L).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ float red16_sum(float v) {
+    v += __shfl_xor(v, 1, kWave);
+    v += __shfl_xor(v, 2, kWave);
+    v += __shfl_xor(v, 4, kWave);
+    v += __shfl_xor(v, 8, kWave);
+    return v;
+}
+
+__global__ __launch_bounds__(256) void recon_logm_fwd_k(const float *__restrict__ im,
+                                                        const int32_t *__restrict__ gptr,
+                                                        const float *__restrict__ S,
+                                                        const int64_t *__restrict__ soff,
+                                                        const double *__restrict__ C, int kstep,
+                                                        float *__restrict__ lossg) {
+    const int64_t g = blockIdx.x;
+    const int64_t r0 = gptr[g];
+    const int n = gptr[g + 1] - static_cast<int>(r0);
+    const int grp = threadIdx.x >> 4, lane = threadIdx.x & 15;
+    const float *Sg = S + soff[g];
+    const float4 *x4 = reinterpret_cast<const float4 *>(im);
+    const float k = static_cast<float>(kstep);
+    double acc = 0.0;
+    for (int u = grp; u < n; u += 16) {
+        const float4 xu = x4[(r0 + u) * 16 + lane];
+        for (int v = 0; v < n; ++v) {
+            const float4 xv = x4[(r0 + v) * 16 + lane];
+            const float h = red16_sum(xu.x * xv.x + xu.y * xv.y + xu.z * xv.z + xu.w * xv.w);
+            acc += static_cast<double>(k * h * h) - 2.0 * static_cast<double>(h) * Sg[int64_t(u) * n + v];
+        }
+    }
+    __shared__ double red[16];
+    if (lane == 0) red[grp] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double t = 0.0;
+        for (int q = 0; q < 16; ++q) t += red[q];
+        lossg[g] = n > 0 ? static_cast<float>((t + C[g]) / (static_cast<double>(kstep) * n * n)) : 0.f;
+    }
+}
+
+__global__ __launch_bounds__(256) void recon_logm_bwd_k(const float *__restrict__ im,
+                                                        const int32_t *__restrict__ gptr,
+                                                        const float *__restrict__ S,
+                                                        const int64_t *__restrict__ soff,
+                                                        int kstep,
+                                                        const float *__restrict__ g_loss,
+                                                        float *__restrict__ grad) {
+    const int64_t g = blockIdx.x;
+    const int64_t r0 = gptr[g];
+    const int n = gptr[g + 1] - static_cast<int>(r0);
+    const int grp = threadIdx.x >> 4, lane = threadIdx.x & 15;
+    const float *Sg = S + soff[g];
+    const float4 *x4 = reinterpret_cast<const float4 *>(im);
+    const float k2 = 2.f * static_cast<float>(kstep);
+    const float coef = n > 0 ? 2.f * *g_loss / (static_cast<float>(kstep) * n * n) : 0.f;
+    for (int u = grp; u < n; u += 16) {
+        const float4 xu = x4[(r0 + u) * 16 + lane];
+        float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+        for (int v = 0; v < n; ++v) {
+            const float4 xv = x4[(r0 + v) * 16 + lane];
+            const float h = red16_sum(xu.x * xv.x + xu.y * xv.y + xu.z * xv.z + xu.w * xv.w);
+            const float w = k2 * h - Sg[int64_t(u) * n + v] - Sg[int64_t(v) * n + u];
+            acc.x += w * xv.x; acc.y += w * xv.y; acc.z += w * xv.z; acc.w += w * xv.w;
+        }
+        reinterpret_cast<float4 *>(grad)[(r0 + u) * 16 + lane] =
+            make_float4(coef * acc.x, coef * acc.y, coef * acc.z, coef * acc.w);
+    }
+}
+
 }  // namespace scgib
 
 using namespace scgib;
+
+extern "C" int scgib_recon_logm_fwd(const float *im, const int32_t *graph_ptr, int64_t n_graphs,
+                                    const float *S, const int64_t *s_offsets, const double *C,
+                                    int32_t kstep, float *loss_graphs, float *loss,
+                                    scgib_stream_t stream) {
+    if (n_graphs <= 0 || kstep <= 0 || !im || !graph_ptr || !S || !s_offsets || !C ||
+        !loss_graphs || !loss)
+        return SCGIB_EINVAL;
+    if (n_graphs > 0x7fffffff) return SCGIB_EUNSUPPORTED;
+    hipStream_t st = as_stream(stream);
+    recon_logm_fwd_k<<<static_cast<unsigned>(n_graphs), 256, 0, st>>>(im, graph_ptr, S, s_offsets,
+                                                                      C, kstep, loss_graphs);
+    const int rc = launch_status();
+    if (rc != SCGIB_OK) return rc;
+    return launch_slab_reduce(loss_graphs, static_cast<int>(n_graphs), 1, loss, st);
+}
+
+extern "C" int scgib_recon_logm_bwd(const float *im, const int32_t *graph_ptr, int64_t n_graphs,
+                                    const float *S, const int64_t *s_offsets, int32_t kstep,
+                                    const float *g_loss, float *grad_im, scgib_stream_t stream) {
+    if (n_graphs <= 0 || kstep <= 0 || !im || !graph_ptr || !S || !s_offsets || !g_loss ||
+        !grad_im)
+        return SCGIB_EINVAL;
+    if (n_graphs > 0x7fffffff) return SCGIB_EUNSUPPORTED;
+    recon_logm_bwd_k<<<static_cast<unsigned>(n_graphs), 256, 0, as_stream(stream)>>>(
+        im, graph_ptr, S, s_offsets, kstep, g_loss, grad_im);
+    return launch_status();
+}
 
 extern "C" int64_t scgib_recon_partials_floats(int64_t n_nodes) {
     return off_cnt(recon_blocks(n_nodes)) + 4;

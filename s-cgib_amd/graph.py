@@ -480,3 +480,55 @@ class StaticBatch:
         self.graph_ptr.copy_(padded["graph_ptr"], non_blocking=True)
         self.dims.copy_(padded["dims"], non_blocking=True)
         self.x.copy_(padded["x"], non_blocking=True)
+
+
+# ---------------------------------------------------------------------------
+# A15: logM reconstruction targets (host data preparation, like the
+# reference's offline pass exp_tudataset.py:416-449)
+# ---------------------------------------------------------------------------
+def trans_logM(g, kstep):
+    """util.getM_logM (util.py:74-91) + GetProbTranMat (:60-71) of one molecule:
+    A^1..A^k of the dense adjacency, each column-normalised,
+    log(A^i / colsum) - log(1/n), negatives / -inf / NaN set to 0; computed in
+    float64 like the reference's numpy and returned as float32 [k, n, n]
+    (exp_tudataset.py:433)."""
+    n = g.num_nodes()
+    A = g.adj().to_dense().cpu().numpy().astype(np.float32)
+    Ak = np.identity(n)
+    out = []
+    with np.errstate(divide="ignore", invalid="ignore"):
+        for _ in range(kstep):
+            Ak = Ak @ A
+            colsum = np.repeat(Ak.sum(axis=0).reshape(1, -1), n, axis=0)
+            P = np.log(np.divide(Ak, colsum)) - np.log(1.0 / n)
+            P[P < 0] = 0
+            P[np.isnan(P)] = 0
+            out.append(P)
+    return torch.from_numpy(np.array(out)).float()
+
+
+class LogMBatch:
+    """Device form of a batch's logM targets for scgib_recon_logm_*: per molecule
+    S = sum_i logM_i ([n, n] fp32, packed at int64 offsets) and
+    C = sum_i ||logM_i||_F^2 (fp64); kstep = k."""
+
+    def __init__(self, logms, device):
+        logms = [torch.as_tensor(m) for m in logms]
+        if not logms:
+            raise GraphIngestError("empty logM batch")
+        self.kstep = int(logms[0].shape[0])
+        sizes, S, C = [], [], []
+        for m in logms:
+            if m.dim() != 3 or m.shape[0] != self.kstep or m.shape[1] != m.shape[2]:
+                raise GraphIngestError(f"logM target of shape {tuple(m.shape)}: expected "
+                                       f"[{self.kstep}, n, n]")
+            m64 = m.double()
+            sizes.append(m.shape[1])
+            S.append(m64.sum(0).float().reshape(-1))
+            C.append(float((m64 * m64).sum()))
+        off = np.zeros(len(sizes) + 1, np.int64)
+        np.cumsum(np.asarray(sizes, np.int64) ** 2, out=off[1:])
+        self.sizes = np.asarray(sizes, np.int64)
+        self.S = torch.cat(S).to(device)
+        self.offsets = torch.from_numpy(off).to(device)
+        self.C = torch.tensor(C, dtype=torch.float64, device=device)

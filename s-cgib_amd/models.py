@@ -219,14 +219,19 @@ class _SCGIBCore(nn.Module):
         sub_readout.record_stream(main)
         return ego, (graph_features, subgraphs_features, sub_readout)
 
-    def _losses(self, batch_g, im, kl_mean, z1, z2, mlp, batch_size):
+    def _losses(self, batch_g, im, kl_mean, z1, z2, mlp, batch_size, batch_logMs=None):
         im = ops.mlp2(im, mlp, batch_g.dims)  # models.py:1174, fused
         kl_loss = kl_mean  # == torch.mean(KL_tensor) (models.py:679), computed in-kernel
         con = semi_loss(z1, z2, batch_size)
         if self.recons_type == "adj":
             rec = ops.recon_adj(im, batch_g)
-        else:
-            raise NotImplementedError("recons_type='logM' is a next-tier path (SURVEY.md §8(f) #3)")
+        elif self.recons_type == "logM":  # models.py:692-693 / 770-782
+            if batch_logMs is None:
+                raise ValueError("recons_type='logM' needs batch_logMs (graph.trans_logM per "
+                                 "molecule, or a graph.LogMBatch)")
+            rec = ops.recon_logm(im, batch_g, batch_logMs)
+        else:  # the reference returns -1.0 (models.py:694-695)
+            rec = torch.tensor(-1.0, device=im.device)
         return kl_loss, con, rec
 
 
@@ -285,7 +290,7 @@ class Mainmodel(_SCGIBCore):
                                                       flatten_batch_subgraphs, x_subs, device,
                                                       noise)
         kl_loss, con, rec = self._losses(batch_g, im, self._last_kl_mean, self._last_z1, z2,
-                                         self.MLP, batch_size)
+                                         self.MLP, batch_size, batch_logMs)
         return None, kl_loss, con, rec
 
 
@@ -360,7 +365,8 @@ class Mainmodel_continue(_SCGIBCore):
                                                             flatten_batch_subgraphs, x_subs,
                                                             device, noise)
         kl_loss, con, rec = self._losses(batch_g, im, self.model._last_kl_mean,
-                                         self.model._last_z1, z2, self.MLP, batch_size)
+                                         self.model._last_z1, z2, self.MLP, batch_size,
+                                         batch_logMs)
         return None, kl_loss, con, rec
 
 

@@ -8,9 +8,11 @@ from __future__ import annotations
 
 import ctypes
 
+import numpy as np
 import torch
 
 from . import _lib
+from . import graph as _graph
 from ._lib import HIDDEN, PGRAD_STRIDE, STATS_STRIDE
 
 _NULL = None
@@ -561,3 +563,45 @@ def mlp2(x, mlp, dims=None):
     """``mlp`` = Sequential(Linear(d, 64), ReLU(), Linear(64, 64)) applied by
     the fused tile kernels (models.py:1055-1057, :1174)."""
     return _Mlp2.apply(x, mlp[0].weight, mlp[0].bias, mlp[2].weight, mlp[2].bias, dims)
+
+
+# ---------------------------------------------------------------------------
+# A15: logM reconstruction loss (models.py:770-782)
+# ---------------------------------------------------------------------------
+class _ReconLogM(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, im, graph, logm):
+        im = _f32(im, "recon_logm")
+        if im.shape[1] != HIDDEN:
+            raise _lib.ScgibError(f"recon_logm kernels are built for width {HIDDEN}")
+        if graph.dims is not None:
+            raise _lib.ScgibError("recon_logm: capacity mode is not supported")
+        B = graph.batch_size
+        if len(logm.sizes) != B or not np.array_equal(logm.sizes, graph.batch_num_nodes_host()):
+            raise _lib.ScgibError("logM targets do not match the molecules of the batch")
+        lossg = torch.empty(B, dtype=torch.float32, device=im.device)
+        loss = torch.empty((), dtype=torch.float32, device=im.device)
+        _lib.call("scgib_recon_logm_fwd", _p(im), _p(graph.graph_ptr), B, _p(logm.S),
+                  _p(logm.offsets), _p(logm.C), logm.kstep, _p(lossg), _p(loss), _stream())
+        ctx.save_for_backward(im)
+        ctx.graph, ctx.logm = graph, logm
+        return loss
+
+    @staticmethod
+    def backward(ctx, g):
+        (im,) = ctx.saved_tensors
+        g = _f32(g, "recon_logm.backward").reshape(1)
+        grad = torch.empty_like(im)
+        lm = ctx.logm
+        _lib.call("scgib_recon_logm_bwd", _p(im), _p(ctx.graph.graph_ptr), ctx.graph.batch_size,
+                  _p(lm.S), _p(lm.offsets), lm.kstep, _p(g), _p(grad), _stream())
+        return grad, None, None
+
+
+def recon_logm(im, graph, logm):
+    """loss_recon (models.py:770-782) on the device.  ``logm`` is a
+    graph.LogMBatch or the reference's list of per-molecule [k, n, n]
+    targets (packed here)."""
+    if not isinstance(logm, _graph.LogMBatch):
+        logm = _graph.LogMBatch(list(logm), im.device)
+    return _ReconLogM.apply(im, graph, logm)

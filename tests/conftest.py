@@ -11,7 +11,19 @@ if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 GOLDEN = os.path.join(ROOT, "tests", "golden")
 MODEL_GOLDENS = ["pretrain_L4_k1_qm9", "pretrain_L5_k1_qm9_continue",
-                 "pretrain_L5_k2_ogb_continue"]
+                 "pretrain_L5_k2_ogb_continue", "pretrain_L4_k2_logm"]
+
+
+def golden_logms(g):
+    """The ragged [k, n_i, n_i] logM targets of a golden (None for 'adj')."""
+    if "logm_flat" not in g:
+        return None
+    k, flat, out, o = int(g["k"]), g["logm_flat"], [], 0
+    for n in g["batch_num_nodes"]:
+        n = int(n)
+        out.append(flat[o:o + k * n * n].reshape(k, n, n))
+        o += k * n * n
+    return out
 
 
 def pytest_configure(config):

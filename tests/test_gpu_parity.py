@@ -8,8 +8,8 @@ import pytest
 import torch
 import torch.nn.functional as F
 
-from conftest import (CANCELLED, MODEL_GOLDENS, check_grads, check_grads_model, load_golden,
-                      rel_err, rel_l2)
+from conftest import (CANCELLED, MODEL_GOLDENS, check_grads, check_grads_model, golden_logms,
+                      load_golden, rel_err, rel_l2)
 from oracle import egonet
 from oracle import scgib_ref as R
 
@@ -243,16 +243,16 @@ def test_interaction_fwd_bwd(pkg, dev, training):
 # ---------------------------------------------------------------------------
 # A4-A14: the whole pretrain step vs the reference goldens
 # ---------------------------------------------------------------------------
-def _args(L, chunk):
+def _args(L, chunk, recons_type="adj"):
     from types import SimpleNamespace
-    return SimpleNamespace(recons_type="adj", useAtt=1, readout_f="sum", d_transfer=32,
+    return SimpleNamespace(recons_type=recons_type, useAtt=1, readout_f="sum", d_transfer=32,
                            device="cuda", batch_size=chunk, task="graph_classification",
                            dataset="pre-train", gin_layers=L)
 
 
 def build_model_from_golden(pkg, g, dev):
     L, k, F_, chunk = int(g["L"]), int(g["k"]), int(g["F"]), int(g["chunk"])
-    args = _args(L, chunk)
+    args = _args(L, chunk, str(g["recons_type"]) if "recons_type" in g else "adj")
     inner = pkg.models.Mainmodel(args, F_, 64, 4, 4, k, "GIN")
     if bool(g["continue_wrapper"]):
         model = pkg.models.Mainmodel_continue(args, F_, 64, 4, 4, k, 1, inner, "GIN")
@@ -288,7 +288,8 @@ def test_pretrain_step_matches_reference(pkg, dev, name, device_ego):
                                               g["ego_batch_num_nodes"]).to(dev)
         x_subs = x[torch.tensor(g["ego_nodes_global"], device=dev)]
     noise = (torch.tensor(g["u_gate"], device=dev), torch.tensor(g["u_feat"], device=dev))
-    _, kl, con, rec = model.forward(bg, x, ego, None, x_subs, 1, None, 2, dev,
+    logms = golden_logms(g)
+    _, kl, con, rec = model.forward(bg, x, ego, logms, x_subs, 1, None, 2, dev,
                                     int(g["chunk"]), noise=noise)
     assert rel_err(kl.item(), g["loss_kl"]) < LOSS_TOL
     assert rel_err(con.item(), g["loss_contrastive"]) < LOSS_TOL

@@ -6,7 +6,7 @@ import pytest
 import torch
 import torch.nn.functional as F
 
-from conftest import MODEL_GOLDENS, check_grads, load_golden, rel_err, rel_l2
+from conftest import MODEL_GOLDENS, check_grads, golden_logms, load_golden, rel_err, rel_l2
 from oracle import scgib_ref as R
 
 
@@ -37,8 +37,11 @@ def test_oracle_matches_reference_golden(name):
     batch, ego, x, x_subs = golden_inputs(g)
     params, raw = golden_params(g)
     buffers = {k: v.clone() for k, v in params.items() if "running" in k or "num_batches" in k}
+    logms = golden_logms(g)
     out = R.pretrain_forward(params, batch, ego, x, x_subs, torch.tensor(g["u_gate"]),
-                             torch.tensor(g["u_feat"]), int(g["chunk"]), buffers)
+                             torch.tensor(g["u_feat"]), int(g["chunk"]), buffers,
+                             logms=None if logms is None else [torch.tensor(m) for m in logms],
+                             kstep=int(g["k"]))
     for key in ("loss_kl", "loss_contrastive", "loss_recon", "loss_total"):
         assert rel(out[key].item(), g[key]) < 1e-5, key
     for key in ("graph_features", "subgraph_features", "noisy", "kl_tensor",
@@ -89,3 +92,17 @@ def test_oracle_finetune_matches_reference(name):
     # frozen by the quirk: pretrained parameters outside "layers.2"
     assert not any(k.startswith("model.") and "layers.2" not in k for k in golden_grads)
     check_grads(golden_grads, lambda n_: p[n_].grad, tol=1e-4, metric="l2")
+
+
+def test_trans_logM_matches_reference_targets(pkg):
+    """graph.trans_logM (restated util.getM_logM) == the reference's targets, bit-exact."""
+    g = load_golden("pretrain_L4_k2_logm")
+    k = int(g["k"])
+    src, dst, counts = g["src"], g["dst"], g["batch_num_nodes"]
+    gptr = np.concatenate([[0], np.cumsum(counts)])
+    for i, want in enumerate(golden_logms(g)):
+        m = (src >= gptr[i]) & (src < gptr[i + 1])
+        gi = pkg.graph.GraphBatch.from_edges(src[m] - gptr[i], dst[m] - gptr[i], int(counts[i]),
+                                             True)
+        got = pkg.graph.trans_logM(gi, k).numpy()
+        np.testing.assert_array_equal(got, want)

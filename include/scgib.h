@@ -130,6 +130,28 @@ int scgib_gin_bwd_stats_bn(const float *dh, const int32_t *rowptr_t, const int32
                            int64_t n_nodes, int32_t training, float *dy, float *dgamma,
                            float *dbeta, float *coef, float *bn_ws, uint32_t *counters,
                            const int32_t *dims, scgib_stream_t stream);
+/* Layer 0 with transfer_d folded in (models.py:668-669 / :1164-1165:
+ * h0 = x Wt^T, Wt = transfer_d.weight [32][F], F <= 16): the kernel gathers
+ * the raw rows x[node_map[v]] (node_map NULL = identity; ego batches pass
+ * the ego -> parent map, so x_subs is never built), aggx = ope x + sum_u x
+ * ([n][16] zero-padded, saved) and agg = aggx Wt^T ([n][32], saved), then the
+ * usual layer.  counters NULL: BN not fused (bn_ws then holds the tile
+ * statistics for scgib_bn_finalize).  Backward: one slab per workgroup of
+ * scgib_gin_layer0_slab_width() floats = dW2 | dW1[64*32] | db2 | db1 |
+ * dWt[32*16] (columns >= F are zero); d(agg0) is not produced. */
+int64_t scgib_gin_layer0_slab_width(void);
+int scgib_gin_layer0_fwd(const float *x, int32_t n_feat, const int32_t *node_map, const float *wt,
+                         const int32_t *rowptr, const int32_t *col, int64_t n_nodes,
+                         float one_plus_eps, const float *w1, const float *b1, const float *w2,
+                         const float *b2, float *agg, float *aggx, float *r, float *z2,
+                         const float *gamma, const float *beta, float bn_eps, float momentum,
+                         float *running_mean, float *running_var, int64_t *num_batches_tracked,
+                         float *stat, float *bn_ws, uint32_t *counters, const int32_t *dims,
+                         scgib_stream_t stream);
+int scgib_gin_layer0_bwd(const float *dy, const float *z2, const float *r, const float *agg,
+                         const float *aggx, const float *stat, const float *coef,
+                         const float *w1, const float *w2, int64_t n_nodes, float *slab,
+                         const int32_t *dims, scgib_stream_t stream);
 int scgib_gin_layer_bwd(const float *dy, const float *z2, const float *r, const float *agg,
                         int32_t d_in, const float *stat, const float *coef, const float *w1,
                         const float *w2, int64_t n_nodes, float *dagg, float *slab,

@@ -46,6 +46,12 @@ SIGNATURES = {
     "scgib_linear_fwd": (ctypes.c_int, [_P, _I64, _P, _P, _P, _P, _P]),
     "scgib_linear_bwd": (ctypes.c_int, [_P, _P, _P, _I64, _P, _P, _P, _P, _P, _P]),
     "scgib_gin_tiles": (_I64, [_I64]),
+    "scgib_gin_layer0_slab_width": (_I64, []),
+    "scgib_gin_layer0_fwd": (ctypes.c_int, [_P, _I32, _P, _P, _P, _P, _I64, _F, _P, _P, _P, _P,
+                                            _P, _P, _P, _P, _P, _P, _F, _F, _P, _P, _P, _P, _P,
+                                            _P, _P, _P]),
+    "scgib_gin_layer0_bwd": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _I64, _P, _P,
+                                            _P]),
     "scgib_gin_bn_ws_floats": (_I64, [_I64]),
     "scgib_gin_counters": (_I64, [_I64]),
     "scgib_gin_layer_fwd_bn": (ctypes.c_int, [_P, _I32, _P, _P, _P, _I64, _F, _P, _P, _P, _P, _P,

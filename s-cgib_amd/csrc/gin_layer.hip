@@ -263,24 +263,109 @@ __device__ void bn_bwd_hier(const float *__restrict__ part, int64_t n, int64_t t
     if (threadIdx.x == 0) bz.counters[bz.ngr_cap] = 0u;
 }
 
+// ---------------------------------------------------------------------------
+// transfer_d folded into the first GIN layer (PRE): the reference computes
+// h0 = x Wt^T per node (models.py:668-669, :1164-1165) and then aggregates h0;
+// by linearity agg0 = (ope x_v + sum_u x_u) Wt^T, so layer 0 gathers the raw
+// normalised features (F <= 16 floats per row, optionally through the
+// ego -> parent node map, i.e. x_subs = x[ego_nodes] is never materialised)
+// and applies Wt on the 64-row tile in LDS (K = 16 MFMA).  Backward adds
+// dWt += dagg0^T aggx in the same tile kernel; d(agg0) itself is never stored.
+// ---------------------------------------------------------------------------
+constexpr int kPreF = 16;       // max raw feature width
+constexpr int kPreLD = 17;      // LDS stride of the [64][16] aggx tile
+constexpr int kPreSlab = 32 * kPreF;
+
+struct PreArgs {
+    const float *x;         // [N_parent][F] raw (normalised) features
+    const int32_t *nmap;    // nullptr, or [N] row -> parent row (ego batches)
+    const float *wt;        // [32][F] transfer_d.weight
+    float *aggx;            // [N][16] saved gathered features (zero-padded)
+    int F;
+};
+
+// 16 lanes per row (lane c = feature c; c >= F contribute 0), 4 rows per
+// thread (rbase + 16 k).  Same latency scheme as gather_rows: every load
+// unconditional at a clamped valid address, masked lanes/slots enter through
+// fmaf(x, 0, acc).  Requires nv >= 1.
+__device__ __forceinline__ void gather_x_rows(const PreArgs &pre, const int32_t *__restrict__ rowptr,
+                                              const int32_t *__restrict__ col, int64_t row0,
+                                              int nv, int rbase, int c, float ope,
+                                              float (&acc)[4]) {
+    const int F = pre.F, cc = c < F ? c : F - 1;
+    const float cm = c < F ? 1.f : 0.f;
+    int32_t beg[4], deg[4];
+    int64_t vrow[4], sid[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int rr = rbase + 16 * k;
+        vrow[k] = row0 + (rr < nv ? rr : nv - 1);
+        beg[k] = rowptr[vrow[k]];
+        deg[k] = rowptr[vrow[k] + 1];
+        sid[k] = pre.nmap ? static_cast<int64_t>(pre.nmap[vrow[k]]) : vrow[k];
+    }
+    float self[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        self[k] = pre.x[sid[k] * F + cc];
+        acc[k] = 0.f;
+    }
+    int maxdeg = 0, maxend = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        maxend = deg[k] > maxend ? deg[k] : maxend;
+        deg[k] -= beg[k];
+        maxdeg = deg[k] > maxdeg ? deg[k] : maxdeg;
+    }
+    for (int j0 = 0; j0 < maxdeg; j0 += 4) {
+        int64_t u[4][4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                const int32_t e = beg[k] + j0 + t;
+                u[k][t] = col[e < maxend ? e : maxend - 1];
+            }
+        if (pre.nmap) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+#pragma unroll
+                for (int t = 0; t < 4; ++t) u[k][t] = pre.nmap[u[k][t]];
+        }
+        float a[4][4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+#pragma unroll
+            for (int t = 0; t < 4; ++t) a[k][t] = pre.x[u[k][t] * F + cc];
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+#pragma unroll
+            for (int t = 0; t < 4; ++t) acc[k] = fmaf(a[k][t], j0 + t < deg[k] ? cm : 0.f, acc[k]);
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) acc[k] = ope * (self[k] * cm) + acc[k];
+}
+
 // GATHER = false is the dense two-layer MLP of the head (models.py:1055-1057,
 // applied at :1174): the tile's input rows are staged directly, agg_out and
 // the BN tile statistics are not written, z2_out is the MLP output.
-template <int DIN, bool XFORM, bool GATHER = true>
+template <int DIN, bool XFORM, bool GATHER = true, bool PRE = false>
 __global__ __launch_bounds__(256) void gin_fwd_k(
     const float *__restrict__ h, const float *__restrict__ in_scale,
     const float *__restrict__ in_shift, const int32_t *__restrict__ rowptr,
     const int32_t *__restrict__ col, int64_t ncap, float ope, const float *__restrict__ w1,
     const float *__restrict__ b1, const float *__restrict__ w2, const float *__restrict__ b2,
     float *__restrict__ agg_out, float *__restrict__ r_out, float *__restrict__ z2_out,
-    float *__restrict__ part, const int32_t *__restrict__ dims, BnFwdFuse fz) {
+    float *__restrict__ part, const int32_t *__restrict__ dims, BnFwdFuse fz, PreArgs pre) {
     constexpr int LDA = DIN + 1, LPR = DIN / 4, RPP = 256 / LPR;
+    static_assert(!PRE || DIN == 32, "transfer_d fold produces the 32-wide layer-0 input");
     const int64_t n = eff_count(dims, 0, ncap);
     __shared__ float sA[TM * LDA];
     __shared__ float sW1[64 * LDA];
     __shared__ float sW2[64 * LDH];
     __shared__ float sR[TM * LDH];
     __shared__ float sRed[2][64];
+    __shared__ float sPre[PRE ? (TM + 32) * kPreLD : 1];  // aggx tile | Wt
     const int tid = threadIdx.x, l = tid & 63, w = tid >> 6;
     const int64_t tile = blockIdx.x;
     const int64_t row0 = tile * TM;
@@ -293,6 +378,8 @@ __global__ __launch_bounds__(256) void gin_fwd_k(
         }
         if (GATHER)
             for (int idx = nv * DIN + tid; idx < ncr * DIN; idx += 256) agg_out[row0 * DIN + idx] = 0.f;
+        if (PRE)
+            for (int idx = nv * kPreF + tid; idx < ncr * kPreF; idx += 256) pre.aggx[row0 * kPreF + idx] = 0.f;
         if (nv == 0) {
             if (GATHER && tid < 128) part[tile * 128 + tid] = 0.f;
             return;
@@ -300,7 +387,31 @@ __global__ __launch_bounds__(256) void gin_fwd_k(
     }
 
     stage_weights<DIN>(w1, w2, sW1, sW2);
-    if constexpr (!GATHER) {  // dense: the input rows themselves
+    if constexpr (PRE) {  // transfer_d folded: gather raw features, then agg0 = aggx Wt^T
+        float *sXg = sPre, *sWt = sPre + TM * kPreLD;
+        for (int idx = tid; idx < 32 * kPreF; idx += 256) {
+            const int j = idx / kPreF, k = idx % kPreF;
+            sWt[j * kPreLD + k] = pre.wt[j * pre.F + (k < pre.F ? k : 0)] * (k < pre.F ? 1.f : 0.f);
+        }
+        float ax[4];
+        gather_x_rows(pre, rowptr, col, row0, nv, tid >> 4, tid & 15, ope, ax);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int rr = (tid >> 4) + 16 * k;
+            sXg[rr * kPreLD + (tid & 15)] = ax[k];
+            if (rr < nv) pre.aggx[(row0 + rr) * kPreF + (tid & 15)] = ax[k];
+        }
+        __syncthreads();
+        if (w < 2) {  // rows 32w..32w+31, all 32 outputs
+            const f32x16 a0 = mma_nt<kPreF>(sXg + w * 32 * kPreLD, kPreLD, sWt, kPreLD, zero16());
+#pragma unroll
+            for (int reg = 0; reg < 16; ++reg) {
+                const int row = w * 32 + acc_row(reg, l), cc = l & 31;
+                sA[row * LDA + cc] = a0[reg];
+                if (row < nv) agg_out[(row0 + row) * DIN + cc] = a0[reg];
+            }
+        }
+    } else if constexpr (!GATHER) {  // dense: the input rows themselves
         constexpr int AQ = DIN / 4, AK = TM * AQ / 256;
         float4 va[AK];
 #pragma unroll
@@ -612,16 +723,22 @@ __global__ __launch_bounds__(1024) void bn_bwd_finalize_k(const float *__restric
 // slab layout per workgroup: dW2[64*64] | dW1[64*DIN] | db2[64] | db1[64]
 // BN = false is the backward of the dense head MLP: dz2 = dy (the gradient
 // of the MLP output); z2 / stat / coef are not read.
-template <int DIN, bool BN = true>
+// PRE: layer 0 with transfer_d folded in (see gather_x_rows): d(agg0) is not
+// stored; dWt += d(agg0)^T aggx is accumulated (slab tail of 32 x 16 floats).
+template <int DIN, bool BN = true, bool PRE = false>
 __global__ __launch_bounds__(256, (DIN <= 64 ? 2 : 1)) void gin_bwd_k(
     const float *__restrict__ dy, const float *__restrict__ z2, const float *__restrict__ r,
     const float *__restrict__ agg, const float *__restrict__ stat,
     const float *__restrict__ coef, const float *__restrict__ w1, const float *__restrict__ w2,
     int64_t ncap, int64_t ntiles, float *__restrict__ dagg_out, float *__restrict__ slab,
-    const int32_t *__restrict__ dims) {
+    const int32_t *__restrict__ dims, const float *__restrict__ aggx) {
+    static_assert(!PRE || DIN == 32, "transfer_d fold: layer 0 only");
     const int64_t n = eff_count(dims, 0, ncap);
     constexpr int LDA = DIN + 1;
-    constexpr int SLAB = 64 * 64 + 64 * DIN + 128;
+    constexpr int SLAB = 64 * 64 + 64 * DIN + 128 + (PRE ? kPreSlab : 0);
+    constexpr int LDP = 33;  // [64][32] tiles of d(agg0) and zero-padded aggx
+    __shared__ float sPre[PRE ? 2 * TM * LDP : 1];
+    float *const sPD = sPre, *const sPX = sPre + TM * LDP;
     // r is dead once dz1 is formed, so the agg tile reuses its buffer: 66.5 KB
     // for DIN <= 64, two workgroups per CU (loads of one overlap the other's MFMA)
     constexpr int RA = (LDA > LDH ? LDA : LDH);
@@ -650,6 +767,9 @@ __global__ __launch_bounds__(256, (DIN <= 64 ? 2 : 1)) void gin_bwd_k(
     f32x16 accW2 = zero16(), accW1[NW1];
 #pragma unroll
     for (int q1 = 0; q1 < NW1; ++q1) accW1[q1] = zero16();
+    f32x16 accWt = zero16();
+    if (PRE)  // columns 16..31 of the aggx tile stay zero
+        for (int idx = tid; idx < TM * 16; idx += 256) sPX[(idx >> 4) * LDP + 16 + (idx & 15)] = 0.f;
     float db2 = 0.f, db1 = 0.f;
     constexpr int AQ = DIN / 4, AK = TM * AQ / 256;  // agg tile: float4 per row, per thread
     for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
@@ -657,7 +777,8 @@ __global__ __launch_bounds__(256, (DIN <= 64 ? 2 : 1)) void gin_bwd_k(
         const int nv = static_cast<int>(n - row0 < TM ? (n - row0 > 0 ? n - row0 : 0) : TM);
         if (dims) {  // capacity mode: zero this tile's padded rows of d(agg)
             const int ncr = static_cast<int>(ncap - row0 < TM ? ncap - row0 : TM);
-            for (int idx = nv * DIN + tid; idx < ncr * DIN; idx += 256) dagg_out[row0 * DIN + idx] = 0.f;
+            if (!PRE)
+                for (int idx = nv * DIN + tid; idx < ncr * DIN; idx += 256) dagg_out[row0 * DIN + idx] = 0.f;
             if (nv == 0) continue;  // block-uniform
         }
         // global loads of the whole tile first (16-byte, all in flight)
@@ -677,7 +798,15 @@ __global__ __launch_bounds__(256, (DIN <= 64 ? 2 : 1)) void gin_bwd_k(
             va[k] = ld_ok(reinterpret_cast<const float4 *>(agg), (row0 + rr) * AQ + cq, row0 * AQ + cq,
                           rr < nv, zero);
         }
+        float4 vx = zero;
+        if (PRE)
+            vx = ld_ok(reinterpret_cast<const float4 *>(aggx), (row0 + (tid >> 2)) * 4 + (tid & 3),
+                       row0 * 4 + (tid & 3), (tid >> 2) < nv, zero);
         __syncthreads();  // previous tile's LDS reads are done
+        if (PRE) {
+            float *px = sPX + (tid >> 2) * LDP + 4 * (tid & 3);
+            px[0] = vx.x; px[1] = vx.y; px[2] = vx.z; px[3] = vx.w;
+        }
         // dz2 = scale (dy - c1 - xhat c2); rows past n are zero
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
@@ -728,9 +857,14 @@ __global__ __launch_bounds__(256, (DIN <= 64 ? 2 : 1)) void gin_bwd_k(
 #pragma unroll
                 for (int reg = 0; reg < 16; ++reg) {
                     const int row = jb * 32 + acc_row(reg, l);
-                    if (row < nv) dagg_out[(row0 + row) * DIN + kb * 32 + (l & 31)] = da[reg];
+                    if (PRE) sPD[row * LDP + kb * 32 + (l & 31)] = da[reg];
+                    else if (row < nv) dagg_out[(row0 + row) * DIN + kb * 32 + (l & 31)] = da[reg];
                 }
             }
+        }
+        if (PRE) {  // dWt += d(agg0)^T aggx (32 x 32, columns >= 16 are zero)
+            __syncthreads();
+            if (w == 0) accWt = mma_tn<TM>(sPD, LDP, sPX, LDP, accWt);
         }
     }
     // per-workgroup slab
@@ -750,6 +884,13 @@ __global__ __launch_bounds__(256, (DIN <= 64 ? 2 : 1)) void gin_bwd_k(
                 const int j = jb * 32 + acc_row(reg, l), kk = kb * 32 + (l & 31);
                 sl[64 * 64 + j * DIN + kk] = accW1[q1][reg];
             }
+        }
+    }
+    if (PRE && w == 0) {
+#pragma unroll
+        for (int reg = 0; reg < 16; ++reg) {
+            const int i = acc_row(reg, l), j = l & 31;
+            if (j < kPreF) sl[64 * 64 + 64 * DIN + 128 + i * kPreF + j] = accWt[reg];
         }
     }
     __shared__ float sB[2][4][64];
@@ -789,11 +930,11 @@ static int launch_gin_fwd(const float *h_in, int32_t d_in, const float *in_stat,
     const int64_t nt = scgib_gin_tiles(n_nodes);
     const float *isc = in_stat ? in_stat + 128 : nullptr, *ish = in_stat ? in_stat + 192 : nullptr;
     if (d_in == 32)
-        gin_fwd_k<32, false><<<dim3((unsigned)nt), 256, 0, st>>>(h_in, isc, ish, rowptr, col, n_nodes, one_plus_eps, w1, b1, w2, b2, agg, r, z2, tile_stats, dims, fz);
+        gin_fwd_k<32, false><<<dim3((unsigned)nt), 256, 0, st>>>(h_in, isc, ish, rowptr, col, n_nodes, one_plus_eps, w1, b1, w2, b2, agg, r, z2, tile_stats, dims, fz, PreArgs{});
     else if (in_stat)
-        gin_fwd_k<64, true><<<dim3((unsigned)nt), 256, 0, st>>>(h_in, isc, ish, rowptr, col, n_nodes, one_plus_eps, w1, b1, w2, b2, agg, r, z2, tile_stats, dims, fz);
+        gin_fwd_k<64, true><<<dim3((unsigned)nt), 256, 0, st>>>(h_in, isc, ish, rowptr, col, n_nodes, one_plus_eps, w1, b1, w2, b2, agg, r, z2, tile_stats, dims, fz, PreArgs{});
     else
-        gin_fwd_k<64, false><<<dim3((unsigned)nt), 256, 0, st>>>(h_in, isc, ish, rowptr, col, n_nodes, one_plus_eps, w1, b1, w2, b2, agg, r, z2, tile_stats, dims, fz);
+        gin_fwd_k<64, false><<<dim3((unsigned)nt), 256, 0, st>>>(h_in, isc, ish, rowptr, col, n_nodes, one_plus_eps, w1, b1, w2, b2, agg, r, z2, tile_stats, dims, fz, PreArgs{});
     return launch_status();
 }
 
@@ -948,9 +1089,9 @@ extern "C" int scgib_gin_layer_bwd(const float *dy, const float *z2, const float
     const int grid = bwd_grid(nt);
     hipStream_t st = as_stream(stream);
     if (d_in == 32)
-        gin_bwd_k<32><<<grid, 256, 0, st>>>(dy, z2, r, agg, stat, coef, w1, w2, n_nodes, nt, dagg, slab, dims);
+        gin_bwd_k<32><<<grid, 256, 0, st>>>(dy, z2, r, agg, stat, coef, w1, w2, n_nodes, nt, dagg, slab, dims, nullptr);
     else
-        gin_bwd_k<64><<<grid, 256, 0, st>>>(dy, z2, r, agg, stat, coef, w1, w2, n_nodes, nt, dagg, slab, dims);
+        gin_bwd_k<64><<<grid, 256, 0, st>>>(dy, z2, r, agg, stat, coef, w1, w2, n_nodes, nt, dagg, slab, dims, nullptr);
     const int rc = launch_status();
     if (rc != SCGIB_OK || !wgrad) return rc;  // wgrad NULL: the caller reduces the slabs
     return launch_slab_reduce(slab, grid, 64 * 64 + 64 * static_cast<int64_t>(d_in) + 128, wgrad, st);
@@ -973,9 +1114,9 @@ extern "C" int scgib_mlp2_fwd(const float *x, int32_t d_in, int64_t n_nodes, con
     const unsigned nt = static_cast<unsigned>(scgib_gin_tiles(n_nodes));
     hipStream_t st = as_stream(stream);
     if (d_in == 128)
-        gin_fwd_k<128, false, false><<<nt, 256, 0, st>>>(x, nullptr, nullptr, nullptr, nullptr, n_nodes, 0.f, w1, b1, w2, b2, nullptr, r, out, nullptr, dims, BnFwdFuse{});
+        gin_fwd_k<128, false, false><<<nt, 256, 0, st>>>(x, nullptr, nullptr, nullptr, nullptr, n_nodes, 0.f, w1, b1, w2, b2, nullptr, r, out, nullptr, dims, BnFwdFuse{}, PreArgs{});
     else
-        gin_fwd_k<64, false, false><<<nt, 256, 0, st>>>(x, nullptr, nullptr, nullptr, nullptr, n_nodes, 0.f, w1, b1, w2, b2, nullptr, r, out, nullptr, dims, BnFwdFuse{});
+        gin_fwd_k<64, false, false><<<nt, 256, 0, st>>>(x, nullptr, nullptr, nullptr, nullptr, n_nodes, 0.f, w1, b1, w2, b2, nullptr, r, out, nullptr, dims, BnFwdFuse{}, PreArgs{});
     return launch_status();
 }
 
@@ -989,10 +1130,59 @@ extern "C" int scgib_mlp2_bwd(const float *dout, const float *x, const float *r,
     const int grid = bwd_grid(nt);
     hipStream_t st = as_stream(stream);
     if (d_in == 128)
-        gin_bwd_k<128, false><<<grid, 256, 0, st>>>(dout, nullptr, r, x, nullptr, nullptr, w1, w2, n_nodes, nt, dx, slab, dims);
+        gin_bwd_k<128, false><<<grid, 256, 0, st>>>(dout, nullptr, r, x, nullptr, nullptr, w1, w2, n_nodes, nt, dx, slab, dims, nullptr);
     else
-        gin_bwd_k<64, false><<<grid, 256, 0, st>>>(dout, nullptr, r, x, nullptr, nullptr, w1, w2, n_nodes, nt, dx, slab, dims);
+        gin_bwd_k<64, false><<<grid, 256, 0, st>>>(dout, nullptr, r, x, nullptr, nullptr, w1, w2, n_nodes, nt, dx, slab, dims, nullptr);
     const int rc = launch_status();
     if (rc != SCGIB_OK) return rc;
     return launch_slab_reduce(slab, grid, 64 * 64 + 64 * static_cast<int64_t>(d_in) + 128, wgrad, st);
+}
+
+// ---------------------------------------------------------------------------
+// Layer 0 with transfer_d folded in (see gather_x_rows / gin_bwd_k<.., PRE>)
+// ---------------------------------------------------------------------------
+extern "C" int64_t scgib_gin_layer0_slab_width(void) {
+    return 64 * 64 + 64 * 32 + 128 + kPreSlab;
+}
+
+extern "C" int scgib_gin_layer0_fwd(const float *x, int32_t n_feat, const int32_t *node_map,
+                                    const float *wt, const int32_t *rowptr, const int32_t *col,
+                                    int64_t n_nodes, float one_plus_eps, const float *w1,
+                                    const float *b1, const float *w2, const float *b2, float *agg,
+                                    float *aggx, float *r, float *z2, const float *gamma,
+                                    const float *beta, float bn_eps, float momentum,
+                                    float *running_mean, float *running_var,
+                                    int64_t *num_batches_tracked, float *stat, float *bn_ws,
+                                    uint32_t *counters, const int32_t *dims,
+                                    scgib_stream_t stream) {
+    if (n_nodes <= 0 || n_feat < 1 || n_feat > kPreF) return n_nodes == 0 ? SCGIB_OK : SCGIB_EINVAL;
+    if (!x || !wt || !rowptr || !col || !w1 || !b1 || !w2 || !b2 || !agg || !aggx || !r || !z2 ||
+        !bn_ws)
+        return SCGIB_EINVAL;
+    if (counters && (!gamma || !beta || !stat || ((running_mean == nullptr) != (running_var == nullptr))))
+        return SCGIB_EINVAL;
+    BnFwdFuse fz{};
+    if (counters)
+        fz = BnFwdFuse{counters, bn_gpart(bn_ws, n_nodes), gamma, beta, running_mean, running_var,
+                       stat, num_batches_tracked, bn_eps, momentum,
+                       static_cast<int>(bn_groups(n_nodes))};
+    const PreArgs pre{x, node_map, wt, aggx, n_feat};
+    const int64_t nt = scgib_gin_tiles(n_nodes);
+    gin_fwd_k<32, false, true, true><<<dim3((unsigned)nt), 256, 0, as_stream(stream)>>>(
+        nullptr, nullptr, nullptr, rowptr, col, n_nodes, one_plus_eps, w1, b1, w2, b2, agg, r, z2,
+        bn_ws, dims, fz, pre);
+    return launch_status();
+}
+
+extern "C" int scgib_gin_layer0_bwd(const float *dy, const float *z2, const float *r,
+                                    const float *agg, const float *aggx, const float *stat,
+                                    const float *coef, const float *w1, const float *w2,
+                                    int64_t n_nodes, float *slab, const int32_t *dims,
+                                    scgib_stream_t stream) {
+    if (n_nodes <= 0 || !dy || !z2 || !r || !agg || !aggx || !stat || !coef || !w1 || !w2 || !slab)
+        return SCGIB_EINVAL;
+    const int64_t nt = scgib_gin_tiles(n_nodes);
+    gin_bwd_k<32, true, true><<<bwd_grid(nt), 256, 0, as_stream(stream)>>>(
+        dy, z2, r, agg, stat, coef, w1, w2, n_nodes, nt, nullptr, slab, dims, aggx);
+    return launch_status();
 }

@@ -206,14 +206,28 @@ class _SCGIBCore(nn.Module):
         encoders' backward chains overlap as well."""
         main = torch.cuda.current_stream(batch_x.device)
         side = _side_stream(batch_x.device) if fork else main
+        # transfer_d folded into both encoders' first layer (raw features are
+        # gathered in-kernel, through the ego -> parent map for Encoder2)
+        fold = (enc_owner.Encoder1.fused and enc_owner.Encoder2.fused
+                and self.transfer_d.bias is None and self.transfer_d.out_features == 32
+                and batch_x.shape[1] <= 16 and not batch_x.requires_grad)
         side.wait_stream(main)
         batch_x.record_stream(side)
         with torch.cuda.stream(side):
-            ego, x_subs = self._prepare_ego(batch_g, None, batch_x, None)
-            subgraphs_features = enc_owner.Encoder2(ego, self.transfer_d(x_subs))
+            if fold:
+                ego = G.egonet_batch(batch_g, self.k_transition)
+                subgraphs_features = ops.gin_encoder_x(batch_x, ego, enc_owner.Encoder2,
+                                                       self.transfer_d, ego.ndata["_ID"])
+            else:
+                ego, x_subs = self._prepare_ego(batch_g, None, batch_x, None)
+                subgraphs_features = enc_owner.Encoder2(ego, self.transfer_d(x_subs))
             sub_readout = ops.segment_sum(subgraphs_features, ego.graph_ptr, ego.batch_size,
                                           ego.seg_dims)
-        graph_features = enc_owner.Encoder1(batch_g, self.transfer_d(batch_x))
+        if fold:
+            graph_features = ops.gin_encoder_x(batch_x, batch_g, enc_owner.Encoder1,
+                                               self.transfer_d)
+        else:
+            graph_features = enc_owner.Encoder1(batch_g, self.transfer_d(batch_x))
         main.wait_stream(side)
         subgraphs_features.record_stream(main)
         sub_readout.record_stream(main)

@@ -90,13 +90,25 @@ def _gin_layer_params(gin):
 
 
 class _GinEncoder(torch.autograd.Function):
-    """GIN.forward (models.py:66-72) as fused HIP layers; see gin_layer.hip."""
+    """GIN.forward (models.py:66-72) as fused HIP layers; see gin_layer.hip.
+
+    With ``x`` / ``wt`` given (h0 = None), transfer_d (h0 = x Wt^T,
+    models.py:668-669) is folded into layer 0: the kernel gathers the raw
+    features — through ``nmap`` (ego -> parent row) when given, so x_subs is
+    never materialised — and d Wt comes out of the layer-0 backward."""
 
     @staticmethod
-    def forward(ctx, h0, graph, gin, training, *params):
-        h0 = _f32(h0, "gin_encoder")
-        n, d0 = h0.shape
-        dev = h0.device
+    def forward(ctx, h0, graph, gin, training, x, wt, nmap, *params):
+        pre = x is not None
+        if pre:
+            x = _f32(x, "gin_encoder x")
+            wt = _f32(wt, "transfer_d.weight")
+            n = graph.num_nodes()  # the row capacity in capacity mode
+            dev = x.device
+        else:
+            h0 = _f32(h0, "gin_encoder")
+            n = h0.shape[0]
+            dev = h0.device
         st = _stream()
         L = len(gin.ginlayers)
         ntiles = int(_lib.query("scgib_gin_tiles", n))
@@ -104,15 +116,15 @@ class _GinEncoder(torch.autograd.Function):
         # training: BN finalize folded into the layer kernel (one counter set
         # per encoder module: the two encoders run on concurrent streams)
         fused = training and n > 0
-        if fused:
-            bn_ws = torch.empty(int(_lib.query("scgib_gin_bn_ws_floats", n)), dtype=torch.float32,
-                                device=dev)
-            cnt = counters(dev, ("gin", id(gin)), int(_lib.query("scgib_gin_counters", n)))
-        saved, h, stat_prev = [], h0, None
+        bn_ws = torch.empty(max(int(_lib.query("scgib_gin_bn_ws_floats", n)), 1),
+                            dtype=torch.float32, device=dev)
+        cnt = counters(dev, ("gin", id(gin)), int(_lib.query("scgib_gin_counters", n))) \
+            if fused else None
+        saved, h, stat_prev, aggx = [], h0, None, None
         for l in range(L):
             conv, bn = gin.ginlayers[l], gin.batch_norms[l]
             w1, b1, w2, b2, gamma, beta = (_f32(p, "gin param") for p in params[6 * l: 6 * l + 6])
-            d_in = h.shape[1]
+            d_in = w1.shape[1] if (pre and l == 0) else h.shape[1]
             if w1.shape != (HIDDEN, d_in) or w2.shape != (HIDDEN, HIDDEN):
                 raise _lib.ScgibError(f"fused GIN layer needs Linear({d_in},64)/Linear(64,64), got "
                                       f"{tuple(w1.shape)}/{tuple(w2.shape)}")
@@ -123,30 +135,40 @@ class _GinEncoder(torch.autograd.Function):
             stat = torch.empty(4, HIDDEN, dtype=torch.float32, device=dev)
             track = training and bn.track_running_stats
             momentum = float(bn.momentum if bn.momentum is not None else 0.1)
-            if fused:
+            rm = _p(bn.running_mean) if track else None
+            rv = _p(bn.running_var) if track else None
+            nbt = _p(bn.num_batches_tracked) if track else None
+            if pre and l == 0:
+                aggx = torch.empty(n, 16, dtype=torch.float32, device=dev)
+                _launch("scgib_gin_layer0_fwd", meta, _p(x), x.shape[1], _p(nmap), _p(wt),
+                        _p(graph.rowptr), _p(graph.col), n, conv._one_plus_eps, _p(w1), _p(b1),
+                        _p(w2), _p(b2), _p(agg), _p(aggx), _p(r), _p(z2), _p(gamma), _p(beta),
+                        float(bn.eps), momentum, rm, rv, nbt, _p(stat), _p(bn_ws), _p(cnt),
+                        _p(graph.dims), st)
+            elif fused:
                 _launch("scgib_gin_layer_fwd_bn", meta, _p(h), d_in, _p(stat_prev),
                         _p(graph.rowptr), _p(graph.col), n, conv._one_plus_eps, _p(w1), _p(b1),
                         _p(w2), _p(b2), _p(agg), _p(r), _p(z2), _p(gamma), _p(beta),
-                        float(bn.eps), momentum, _p(bn.running_mean) if track else None,
-                        _p(bn.running_var) if track else None,
-                        _p(bn.num_batches_tracked) if track else None, _p(stat), _p(bn_ws),
-                        _p(cnt), _p(graph.dims), st)
+                        float(bn.eps), momentum, rm, rv, nbt, _p(stat), _p(bn_ws), _p(cnt),
+                        _p(graph.dims), st)
             else:
                 _launch("scgib_gin_layer_fwd", meta, _p(h), d_in, _p(stat_prev),
                         _p(graph.rowptr), _p(graph.col), n, conv._one_plus_eps, _p(w1), _p(b1),
                         _p(w2), _p(b2), _p(agg), _p(r), _p(z2), _p(tstats), _p(graph.dims), st)
-                _lib.call("scgib_bn_finalize", _p(tstats), n, _p(gamma), _p(beta), float(bn.eps),
+            if not fused:  # eval (running statistics) or untracked: separate finalize
+                src = bn_ws if (pre and l == 0) else tstats
+                _lib.call("scgib_bn_finalize", _p(src), n, _p(gamma), _p(beta), float(bn.eps),
                           momentum, int(training),
                           _p(bn.running_mean) if (track or not training) else None,
                           _p(bn.running_var) if (track or not training) else None,
-                          _p(bn.num_batches_tracked) if track else None, _p(stat),
-                          _p(graph.dims), st)
+                          nbt, _p(stat), _p(graph.dims), st)
             saved += [agg, r, z2, stat]
             h, stat_prev = z2, stat
         out = torch.empty(n, HIDDEN, dtype=torch.float32, device=dev)
         _lib.call("scgib_bn_relu_apply", _p(h), _p(stat_prev), n, _p(out), _p(graph.dims), st)
-        ctx.save_for_backward(*saved, *params)
-        ctx.graph, ctx.L, ctx.training = graph, L, training
+        ctx.save_for_backward(*saved, *params, *( (aggx,) if pre else ()))
+        ctx.graph, ctx.L, ctx.training, ctx.pre = graph, L, training, pre
+        ctx.n_feat = x.shape[1] if pre else None
         ctx.opes = [c._one_plus_eps for c in gin.ginlayers]
         ctx.cnt_key = ("gin_bwd", id(gin))
         return out
@@ -154,9 +176,10 @@ class _GinEncoder(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g_out):
         g_out = _f32(g_out, "gin_encoder.backward")
-        L, gr = ctx.L, ctx.graph
+        L, gr, pre = ctx.L, ctx.graph, ctx.pre
         t = ctx.saved_tensors
-        saved, params = t[: 4 * L], t[4 * L:]
+        saved, params = t[: 4 * L], t[4 * L: 4 * L + 6 * L]
+        aggx = t[-1] if pre else None
         n = g_out.shape[0]
         dev = g_out.device
         st = _stream()
@@ -164,7 +187,8 @@ class _GinEncoder(torch.autograd.Function):
                             device=dev)
         cnt = counters(dev, ctx.cnt_key, int(_lib.query("scgib_gin_counters", n)))
         grads = [None] * (6 * L)
-        dagg_next = None
+        dagg_next, dwt = None, None
+        nslab = int(_lib.query("scgib_gin_bwd_slabs", n))
         for l in reversed(range(L)):
             agg, r, z2, stat = saved[4 * l: 4 * l + 4]
             w1, _, w2 = params[6 * l], params[6 * l + 1], params[6 * l + 2]
@@ -182,36 +206,65 @@ class _GinEncoder(torch.autograd.Function):
                           _p(gr.col_t), ctx.opes[l + 1], _p(z2), _p(stat), n, int(ctx.training),
                           _p(dy), _p(bn_g[0]), _p(bn_g[1]), _p(coef), _p(bn_ws), _p(cnt),
                           _p(gr.dims), st)
-            dagg = torch.empty(n, d_in, dtype=torch.float32, device=dev)
-            slab = torch.empty(int(_lib.query("scgib_gin_slab_floats", n, d_in)),
-                               dtype=torch.float32, device=dev)
-            wgrad = torch.empty(HIDDEN * HIDDEN + HIDDEN * d_in + 2 * HIDDEN,
-                                dtype=torch.float32, device=dev)
             meta = {"n": n, "e": gr.edge_capacity(), "d_in": d_in}
-            _launch("scgib_gin_layer_bwd", meta, _p(dy), _p(z2), _p(r), _p(agg), d_in, _p(stat),
-                    _p(coef), _p(_f32(w1, "w1")), _p(_f32(w2, "w2")), n, _p(dagg), _p(slab),
-                    _NULL, _p(gr.dims), st)
-            _lib.call("scgib_slab_reduce", _p(slab), int(_lib.query("scgib_gin_bwd_slabs", n)),
-                      wgrad.numel(), _p(wgrad), st)
+            w1c, w2c = _f32(w1, "w1"), _f32(w2, "w2")
+            if pre and l == 0:
+                width = int(_lib.query("scgib_gin_layer0_slab_width"))
+                slab = torch.empty(nslab * width, dtype=torch.float32, device=dev)
+                _launch("scgib_gin_layer0_bwd", meta, _p(dy), _p(z2), _p(r), _p(agg), _p(aggx),
+                        _p(stat), _p(coef), _p(w1c), _p(w2c), n, _p(slab), _p(gr.dims), st)
+                dagg = None
+            else:
+                width = HIDDEN * HIDDEN + HIDDEN * d_in + 2 * HIDDEN
+                slab = torch.empty(int(_lib.query("scgib_gin_slab_floats", n, d_in)),
+                                   dtype=torch.float32, device=dev)
+                dagg = torch.empty(n, d_in, dtype=torch.float32, device=dev)
+                _launch("scgib_gin_layer_bwd", meta, _p(dy), _p(z2), _p(r), _p(agg), d_in,
+                        _p(stat), _p(coef), _p(w1c), _p(w2c), n, _p(dagg), _p(slab), _NULL,
+                        _p(gr.dims), st)
+            wgrad = torch.empty(width, dtype=torch.float32, device=dev)
+            _lib.call("scgib_slab_reduce", _p(slab), nslab, width, _p(wgrad), st)
             o = HIDDEN * HIDDEN
             grads[6 * l + 2] = wgrad[:o].view(HIDDEN, HIDDEN)
             grads[6 * l + 0] = wgrad[o:o + HIDDEN * d_in].view(HIDDEN, d_in)
             o += HIDDEN * d_in
             grads[6 * l + 3] = wgrad[o:o + HIDDEN]
             grads[6 * l + 1] = wgrad[o + HIDDEN:o + 2 * HIDDEN]
+            if pre and l == 0:
+                o += 2 * HIDDEN
+                dwt = wgrad[o:o + 32 * 16].view(32, 16)[:, : ctx.n_feat]
             grads[6 * l + 4] = bn_g[0]
             grads[6 * l + 5] = bn_g[1]
             dagg_next = dagg
+        if pre:
+            return (None, None, None, None, None, dwt, None, *grads)
         # d h0 = (1+eps_0) d(agg_0) + sum over out-edges (transposed aggregation)
         dh0 = _aggregate(dagg_next, gr.rowptr_t, gr.col_t, ctx.opes[0], gr.dims)
-        return (dh0, None, None, None, *grads)
+        return (dh0, None, None, None, None, None, None, *grads)
 
 
 def gin_encoder(h, graph, gin):
     """models.GIN.forward on the fused HIP layers (train or eval BN)."""
     if graph.num_nodes() == 0:
         raise _lib.ScgibError("gin_encoder on an empty graph")
-    return _GinEncoder.apply(h, graph, gin, bool(gin.training), *_gin_layer_params(gin))
+    return _GinEncoder.apply(h, graph, gin, bool(gin.training), None, None, None,
+                             *_gin_layer_params(gin))
+
+
+def gin_encoder_x(x, graph, gin, transfer, node_map=None):
+    """gin(graph, transfer(x[node_map])) with transfer_d (Linear(F, 32),
+    no bias) folded into the first fused layer.  ``x`` holds the raw
+    normalised features of the parent rows (F <= 16); ``node_map`` maps the
+    graph's rows to rows of ``x`` (ego batches: ego.ndata['_ID'])."""
+    if graph.num_nodes() == 0:
+        raise _lib.ScgibError("gin_encoder on an empty graph")
+    if transfer.bias is not None or transfer.weight.shape != (32, x.shape[1]) \
+            or x.shape[1] > 16:
+        raise _lib.ScgibError("transfer_d fold needs Linear(F <= 16, 32, bias=False)")
+    if x.requires_grad:
+        raise _lib.ScgibError("transfer_d fold: no gradient w.r.t. the raw features")
+    return _GinEncoder.apply(None, graph, gin, bool(gin.training), x, transfer.weight,
+                             node_map, *_gin_layer_params(gin))
 
 
 # ---------------------------------------------------------------------------

@@ -415,17 +415,33 @@ class StaticBatch:
     """
 
     def __init__(self, B, n_cap, e_cap, n_feat, max_graph_nodes, ego_caps, device):
-        i32 = torch.int32
         self.B, self.n_cap, self.e_cap, self.n_feat = B, n_cap, e_cap, n_feat
-        self.rowptr = torch.zeros(n_cap + 1, dtype=i32, device=device)
-        self.col = torch.zeros(max(e_cap, 1), dtype=i32, device=device)
-        self.graph_ptr = torch.zeros(B + 1, dtype=i32, device=device)
-        self.dims = torch.zeros(2, dtype=i32, device=device)
-        self.x = torch.zeros(n_cap, n_feat, dtype=torch.float32, device=device)
+        # one byte blob (rowptr | col | graph_ptr | dims | x, 256-B aligned
+        # sections) so that loading a batch is a single device copy
+        self.blob = torch.zeros(self._layout()[-1], dtype=torch.uint8, device=device)
+        self.rowptr, self.col, self.graph_ptr, self.dims, self.x = self._views(self.blob)
         self.graph = GraphBatch(self.rowptr, self.col, self.graph_ptr, None, None,
                                 max_graph_nodes=max_graph_nodes, n_edges=-1)
         self.graph.dims = self.dims
         self.graph.ego_caps = tuple(int(c) for c in ego_caps)
+
+    def _layout(self):
+        sizes = [4 * (self.n_cap + 1), 4 * max(self.e_cap, 1), 4 * (self.B + 1), 4 * 2,
+                 4 * self.n_cap * self.n_feat]
+        offs = [0]
+        for sz in sizes:
+            offs.append(offs[-1] + (sz + 255) // 256 * 256)
+        return offs
+
+    def _views(self, blob):
+        o = self._layout()
+        i32 = torch.int32
+        return (blob[o[0]:o[0] + 4 * (self.n_cap + 1)].view(i32),
+                blob[o[1]:o[1] + 4 * max(self.e_cap, 1)].view(i32),
+                blob[o[2]:o[2] + 4 * (self.B + 1)].view(i32),
+                blob[o[3]:o[3] + 8].view(i32),
+                blob[o[4]:o[4] + 4 * self.n_cap * self.n_feat].view(torch.float32)
+                .view(self.n_cap, self.n_feat))
 
     @staticmethod
     def capacities(host_batches, k, slack=1.0):
@@ -462,24 +478,24 @@ class StaticBatch:
         if self.B and g.batch_num_nodes_host().min() < 2:
             raise ValueError("Expected more than 1 value per channel when training "
                              "(a molecule with one atom; the reference skips those)")
+        blob = np.zeros(self._layout()[-1], np.uint8)
+        o = self._layout()
         rp = np.full(self.n_cap + 1, e, np.int32)
         rp[: n + 1] = g.rowptr.cpu().numpy()
-        col = np.zeros(max(self.e_cap, 1), np.int32)
-        col[:e] = g.col.cpu().numpy()[:e]
-        x = np.zeros((self.n_cap, self.n_feat), np.float32)
-        x[:n] = g.ndata["x"].cpu().numpy()
-        dev = self.rowptr.device
-        return {"rowptr": torch.from_numpy(rp).to(dev), "col": torch.from_numpy(col).to(dev),
-                "graph_ptr": g.graph_ptr.to(dev), "dims": torch.tensor([n, e], dtype=torch.int32,
-                                                                       device=dev),
-                "x": torch.from_numpy(x).to(dev), "n": n, "e": e}
+        blob[o[0]:o[0] + rp.nbytes] = rp.view(np.uint8)
+        col = g.col.cpu().numpy()[:e].astype(np.int32)
+        blob[o[1]:o[1] + col.nbytes] = col.view(np.uint8)
+        gp = g.graph_ptr.cpu().numpy().astype(np.int32)
+        blob[o[2]:o[2] + gp.nbytes] = gp.view(np.uint8)
+        blob[o[3]:o[3] + 8] = np.array([n, e], np.int32).view(np.uint8)
+        x = np.ascontiguousarray(g.ndata["x"].cpu().numpy().astype(np.float32))
+        blob[o[4]:o[4] + x.nbytes] = x.view(np.uint8).reshape(-1)
+        dev = self.blob.device
+        return {"blob": torch.from_numpy(blob).to(dev), "n": n, "e": e}
 
     def load(self, padded):
-        self.rowptr.copy_(padded["rowptr"], non_blocking=True)
-        self.col.copy_(padded["col"], non_blocking=True)
-        self.graph_ptr.copy_(padded["graph_ptr"], non_blocking=True)
-        self.dims.copy_(padded["dims"], non_blocking=True)
-        self.x.copy_(padded["x"], non_blocking=True)
+        """Copy a pad()-ed batch into the static buffers (one device copy)."""
+        self.blob.copy_(padded["blob"], non_blocking=True)
 
 
 # ---------------------------------------------------------------------------

@@ -284,6 +284,7 @@ class Mainmodel(_SCGIBCore):
         ego, x_subs = self._prepare_ego(batch_g, flatten_batch_subgraphs, batch_x, x_subs)
         im, kl, noisy, z2, z1 = self._extract(self, batch_g, batch_x, ego, x_subs, noise)
         self._last_z1 = z1
+        ops.join_aside()
         return im, kl, noisy, z2
 
     def forward(self, batch_g, batch_x, flatten_batch_subgraphs, batch_logMs, x_subs,
@@ -305,6 +306,7 @@ class Mainmodel(_SCGIBCore):
                                                       noise)
         kl_loss, con, rec = self._losses(batch_g, im, self._last_kl_mean, self._last_z1, z2,
                                          self.MLP, batch_size, batch_logMs)
+        ops.join_aside()
         return None, kl_loss, con, rec
 
 
@@ -357,6 +359,7 @@ class Mainmodel_continue(_SCGIBCore):
         ego, x_subs = self._prepare_ego(batch_g, flatten_batch_subgraphs, batch_x, x_subs)
         im, kl, noisy, z2, z1 = self._extract(self, batch_g, batch_x, ego, x_subs, noise)
         self._last_z1 = z1
+        ops.join_aside()
         return im, kl, noisy, z2
 
     def forward(self, batch_g, batch_x, flatten_batch_subgraphs, batch_logMs, x_subs,
@@ -381,6 +384,7 @@ class Mainmodel_continue(_SCGIBCore):
         kl_loss, con, rec = self._losses(batch_g, im, self.model._last_kl_mean,
                                          self.model._last_z1, z2, self.MLP, batch_size,
                                          batch_logMs)
+        ops.join_aside()
         return None, kl_loss, con, rec
 
 
@@ -460,6 +464,7 @@ class Mainmodel_finetuning(nn.Module):
         im = ops.mlp2(im, self.MLP, batch_g.dims)
         im = self.s2s(batch_g, im)
         scores = self.predict(im)
+        ops.join_aside()
         if self.dataset in self.tasks:
             return scores, 0, 0, 0
         return torch.sigmoid(scores), 0, 0, 0

@@ -29,6 +29,37 @@ def _launch(name, meta, *args):
     return OBSERVER(name, meta, lambda: _lib.call(name, *args))
 
 
+# Off-critical-path work (e.g. the compressor-BN running-stat update, which
+# nothing later in the step reads): launched on an auxiliary stream forked
+# from the current one, joined back by join_aside() (models call it at the
+# end of forward, so captured graphs stay closed).
+_AUX_STREAMS = {}
+_AUX_PENDING = set()
+
+
+def launch_aside(fn, *tensors):
+    main = torch.cuda.current_stream()
+    key = main.device.index
+    aux = _AUX_STREAMS.get(key)
+    if aux is None:
+        aux = _AUX_STREAMS[key] = torch.cuda.Stream(main.device)
+    aux.wait_stream(main)
+    for t in tensors:  # produced on main, consumed on aux
+        t.record_stream(aux)
+    with torch.cuda.stream(aux):
+        fn()
+    _AUX_PENDING.add(key)
+
+
+def join_aside():
+    if not _AUX_PENDING:
+        return
+    main = torch.cuda.current_stream()
+    for key in list(_AUX_PENDING):
+        main.wait_stream(_AUX_STREAMS[key])
+    _AUX_PENDING.clear()
+
+
 def _p(t):
     return ctypes.c_void_p(t.data_ptr()) if t is not None else _NULL
 
@@ -341,8 +372,11 @@ def _interaction_forward(ctx, f, t, s, u_gate, u_feat, gamma, beta, w2, b2, w_at
               _p(lam), _p(logit), _p(stats), _p(kl), _p(kl_mean), int(pad), st)
     if training and bn.track_running_stats:
         nbt = bn.num_batches_tracked
-        _lib.call("scgib_bn_running_update", _p(stats), _p(graph.graph_ptr), B,
-                  float(bn.momentum), _p(rm), _p(rv), _p(nbt), st)
+        # B sequential momentum updates in closed form; nothing in the step
+        # reads them, so they run beside the critical path (join_aside)
+        launch_aside(lambda: _lib.call("scgib_bn_running_update", _p(stats),
+                                       _p(graph.graph_ptr), B, float(bn.momentum), _p(rm),
+                                       _p(rv), _p(nbt), _stream()), stats, graph.graph_ptr)
     ctx.graph, ctx.training, ctx.pad, ctx.n_last = graph, training, pad, n_last
     ctx.bn_eps = float(bn.eps)
     ctx.rm, ctx.rv = (None, None) if training else (rm.clone(), rv.clone())

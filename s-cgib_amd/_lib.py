@@ -10,7 +10,8 @@ import ctypes
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libscgib.so")
+# SCGIB_LIB: debug builds only (tools/phase_trace.py loads libscgib_trace.so)
+LIB_PATH = os.environ.get("SCGIB_LIB") or os.path.join(HERE, "libscgib.so")
 
 _P, _I64, _I32, _F = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32, ctypes.c_float
 

@@ -385,6 +385,8 @@ __global__ __launch_bounds__(256) void gin_fwd_k(
             return;
         }
     }
+    SCGIB_MARK(0);
+    SCGIB_MARK_HWID();
 
     stage_weights<DIN>(w1, w2, sW1, sW2);
     if constexpr (PRE) {  // transfer_d folded: gather raw features, then agg0 = aggx Wt^T
@@ -453,6 +455,7 @@ __global__ __launch_bounds__(256) void gin_fwd_k(
         }
     }
     __syncthreads();
+    SCGIB_MARK(1);
 
     const int wr = w >> 1, wc = w & 1;
     const int ccol = wc * 32 + (l & 31);
@@ -469,6 +472,7 @@ __global__ __launch_bounds__(256) void gin_fwd_k(
         }
     }
     __syncthreads();
+    SCGIB_MARK(2);
     // z2 = r W2^T + b2 ; tile statistics of z2 (valid rows only)
     f32x16 acc = mma_nt<64>(sR + wr * 32 * LDH, LDH, sW2 + wc * 32 * LDH, LDH, zero16());
     const float bias2 = b2[ccol];
@@ -483,6 +487,7 @@ __global__ __launch_bounds__(256) void gin_fwd_k(
         }
     }
     if constexpr (!GATHER) return;
+    SCGIB_MARK(3);
     s += __shfl_xor(s, 32, kWave);
     if (l < 32) sRed[wr][ccol] = s;
     __syncthreads();
@@ -503,7 +508,11 @@ __global__ __launch_bounds__(256) void gin_fwd_k(
         st_agent(part + tile * 128 + ccol, csum);
         st_agent(part + tile * 128 + 64 + ccol, sRed[0][ccol] + sRed[1][ccol]);
     }
-    if (fz.counters) bn_fwd_hier(part, n, tile, fz);
+    SCGIB_MARK(4);
+    if (fz.counters) {
+        bn_fwd_hier(part, n, tile, fz);
+        SCGIB_MARK(5);
+    }
 }
 
 // Batch mean / biased variance from the per-tile (sum, centred M2), fp64,
@@ -630,6 +639,8 @@ __global__ __launch_bounds__(256) void gin_bwd_stats_k(
             st4(dy_out + (row0 + rr) * 64 + 4 * c, make_float4(0.f, 0.f, 0.f, 0.f));
         return;
     }
+    SCGIB_MARK(0);
+    SCGIB_MARK_HWID();
     float4 g[4];
     if (GATHER) {
         gather_rows<4, 16, 16, false>(g4, rowptr_t, col_t, row0, nv, slot, c, ope, sc, sh, g);
@@ -675,7 +686,11 @@ __global__ __launch_bounds__(256) void gin_bwd_stats_k(
         for (int k = 0; k < 16; ++k) s += sRed[which][k][ch];
         st_agent(part + tile * 128 + which * 64 + ch, s);
     }
-    if (bz.counters) bn_bwd_hier(part, n, tile, bz);
+    SCGIB_MARK(1);
+    if (bz.counters) {
+        bn_bwd_hier(part, n, tile, bz);
+        SCGIB_MARK(2);
+    }
 }
 
 // dbeta = sum dy, dgamma = sum dy xhat (fp64, fixed order); coefficients of
@@ -749,6 +764,8 @@ __global__ __launch_bounds__(256, (DIN <= 64 ? 2 : 1)) void gin_bwd_k(
     float *const sR = sRA, *const sA = sRA;
     const int tid = threadIdx.x, l = tid & 63, w = tid >> 6;
     const int wr = w >> 1, wc = w & 1;
+    SCGIB_MARK(0);
+    SCGIB_MARK_HWID();
     stage_weights<DIN>(w1, w2, sW1, sW2);
     const int ch = tid & 63, q = tid >> 6;  // column-sum roles: channel, row quarter
     // staging roles: 4-channel chunk c4, rows rs + 16 k
@@ -825,6 +842,7 @@ __global__ __launch_bounds__(256, (DIN <= 64 ? 2 : 1)) void gin_bwd_k(
             pr[0] = vr[k].x; pr[1] = vr[k].y; pr[2] = vr[k].z; pr[3] = vr[k].w;
         }
         __syncthreads();
+        if (tile == blockIdx.x) SCGIB_MARK(1);
         // dW2 += dz2^T r  (sub-tile j-block wr, k-block wc)
         accW2 = mma_tn<TM>(sD + wr * 32, LDH, sR + wc * 32, LDH, accW2);
         // dr = dz2 W2  (rows wr, cols wc)
@@ -838,6 +856,7 @@ __global__ __launch_bounds__(256, (DIN <= 64 ? 2 : 1)) void gin_bwd_k(
             sD[row * LDH + cc] = sR[row * LDH + cc] > 0.f ? dr[reg] : 0.f;
         }
         __syncthreads();  // r is dead: the agg tile (held in registers) takes its buffer
+        if (tile == blockIdx.x) SCGIB_MARK(2);
 #pragma unroll
         for (int k = 0; k < AK; ++k) {
             const int idx = tid + 256 * k, rr = idx / AQ, cq = idx % AQ;
@@ -866,6 +885,7 @@ __global__ __launch_bounds__(256, (DIN <= 64 ? 2 : 1)) void gin_bwd_k(
             __syncthreads();
             if (w == 0) accWt = mma_tn<TM>(sPD, LDP, sPX, LDP, accWt);
         }
+        if (tile == blockIdx.x) SCGIB_MARK(3);
     }
     // per-workgroup slab
     float *sl = slab + static_cast<int64_t>(blockIdx.x) * SLAB;
@@ -902,6 +922,7 @@ __global__ __launch_bounds__(256, (DIN <= 64 ? 2 : 1)) void gin_bwd_k(
         sl[64 * 64 + 64 * DIN + which * 64 + ch] =
             ((sB[which][0][ch] + sB[which][1][ch]) + sB[which][2][ch]) + sB[which][3][ch];
     }
+    SCGIB_MARK(4);
 }
 
 // up to two workgroups per CU (66.5 KB LDS each): one tile per workgroup for
@@ -913,6 +934,13 @@ static int bwd_grid(int64_t ntiles) { return static_cast<int>(ntiles < 512 ? nti
 using namespace scgib;
 
 extern "C" int64_t scgib_gin_tiles(int64_t n_nodes) { return (n_nodes + TM - 1) / TM; }
+
+#ifdef SCGIB_TRACE
+// debug build only: buffer of [grid][8] uint64 phase stamps (see common.h)
+extern "C" int scgib_trace_set(void *buf) {
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_trace), &buf, sizeof(buf)) == hipSuccess ? 0 : 1;
+}
+#endif
 
 extern "C" int64_t scgib_gin_slab_floats(int64_t n_nodes, int32_t d_in) {
     return static_cast<int64_t>(bwd_grid(scgib_gin_tiles(n_nodes))) * (64 * 64 + 64 * d_in + 128);

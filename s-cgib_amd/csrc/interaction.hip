@@ -77,6 +77,19 @@ __device__ __forceinline__ float4 relu4(float4 a) { return make_float4(fmaxf(a.x
 __device__ __forceinline__ float4 sqrt4(float4 a) { return make_float4(sqrtf(a.x), sqrtf(a.y), sqrtf(a.z), sqrtf(a.w)); }
 __device__ __forceinline__ float4 rcp_sqrt4(float4 a) { return make_float4(1.f / sqrtf(a.x), 1.f / sqrtf(a.y), 1.f / sqrtf(a.z), 1.f / sqrtf(a.w)); }
 
+// Rows are processed in chunks of 4 * CH (CH rows per row group): all loads
+// of a chunk are issued first at clamped, always-valid rows, then used with
+// 0/1 weights (macc: fmaf(x, w, acc) — exact for w = 1, and acc + x * 0 = acc
+// for finite x), so a chunk costs one memory latency instead of one per row
+// (a load consumed only under `if (row valid)` is sunk into that branch with
+// its own s_waitcnt).  Per-row-group accumulation order is unchanged.
+constexpr int CH = 8;
+
+__device__ __forceinline__ float4 macc(float4 x, float w, float4 acc) {
+    return make_float4(fmaf(x.x, w, acc.x), fmaf(x.y, w, acc.y), fmaf(x.z, w, acc.z),
+                       fmaf(x.w, w, acc.w));
+}
+
 __device__ __forceinline__ float gate_lambda(float u, float p) {
     const float e = kGateScale * u + kGateShift;
     const float g = logf(e) - logf(1.f - e);
@@ -126,17 +139,24 @@ __global__ __launch_bounds__(64) void interaction_fwd_k(
     // ---- pass 1: sums (readout of f, means) and shifted second moments ----
     const float4 f0 = ld4(f + r0 * 64 + L.ch), t0 = ld4(t + r0 * 64 + L.ch);
     float4 zf = f4(0.f), zt = f4(0.f), sf = f4(0.f), st = f4(0.f), qf = f4(0.f), qt = f4(0.f);
-    for (int64_t base = r0; base < r1; base += 4) {
-        const int64_t r = base + L.q;
-        if (r < r1) {
-            const float4 fv = ld4(f + r * 64 + L.ch), tv = ld4(t + r * 64 + L.ch);
-            zf = zf + fv;
-            zt = zt + tv;
-            const float4 df = fv - f0, dt = tv - t0;
-            sf = sf + df;
-            st = st + dt;
-            qf = qf + df * df;
-            qt = qt + dt * dt;
+    for (int64_t cb = r0; cb < r1; cb += 4 * CH) {
+        float4 fv[CH], tv[CH];
+#pragma unroll
+        for (int j = 0; j < CH; ++j) {
+            const int64_t r = cb + L.q + 4 * j, rr = r < r1 ? r : r0;
+            fv[j] = ld4(f + rr * 64 + L.ch);
+            tv[j] = ld4(t + rr * 64 + L.ch);
+        }
+#pragma unroll
+        for (int j = 0; j < CH; ++j) {
+            const float w = cb + L.q + 4 * j < r1 ? 1.f : 0.f;
+            zf = macc(fv[j], w, zf);
+            zt = macc(tv[j], w, zt);
+            const float4 df = fv[j] - f0, dt = tv[j] - t0;
+            sf = macc(df, w, sf);
+            st = macc(dt, w, st);
+            qf = macc(df * df, w, qf);
+            qt = macc(dt * dt, w, qt);
         }
     }
     zf = red_q4(zf); zt = red_q4(zt); sf = red_q4(sf); st = red_q4(st);
@@ -163,19 +183,29 @@ __global__ __launch_bounds__(64) void interaction_fwd_k(
     }
     // ---- pass 2: compressor logit p, gate lambda, noisy features ----
     float4 zacc = f4(0.f);
-    for (int64_t base = r0; base < r1; base += 4) {
-        const int64_t r = base + L.q;
-        const bool ok = r < r1;
-        const int64_t rr = ok ? r : r0;
-        const float4 y = gm * ((ld4(t + rr * 64 + L.ch) - m_use) * rstd) + bt;
-        const float p = red16(dot4(w2c, relu4(y))) + b2;
-        if (ok) {
-            const float lm = gate_lambda(u_gate[r], p), ln = 1.f - lm;
-            const float4 fv = ld4(f + r * 64 + L.ch);
-            const float4 nz = (lm * fv + ln * mu) + ld4(u_feat + r * 64 + L.ch) * (ln * sig);
-            st4(im + r * 128 + L.ch, nz);
-            zacc = zacc + nz;
-            if (L.c4 == 0) lam[r] = lm;
+    for (int64_t cb = r0; cb < r1; cb += 4 * CH) {
+        float4 tv[CH], fv[CH], uv[CH];
+        float ug[CH];
+#pragma unroll
+        for (int j = 0; j < CH; ++j) {
+            const int64_t r = cb + L.q + 4 * j, rr = r < r1 ? r : r0;
+            tv[j] = ld4(t + rr * 64 + L.ch);
+            fv[j] = ld4(f + rr * 64 + L.ch);
+            uv[j] = ld4(u_feat + rr * 64 + L.ch);
+            ug[j] = u_gate[rr];
+        }
+#pragma unroll
+        for (int j = 0; j < CH; ++j) {
+            const int64_t r = cb + L.q + 4 * j;
+            const float4 y = gm * ((tv[j] - m_use) * rstd) + bt;
+            const float p = red16(dot4(w2c, relu4(y))) + b2;
+            const float lm = gate_lambda(ug[j], p), ln = 1.f - lm;
+            const float4 nz = (lm * fv[j] + ln * mu) + uv[j] * (ln * sig);
+            zacc = macc(nz, r < r1 ? 1.f : 0.f, zacc);
+            if (r < r1) {
+                st4(im + r * 128 + L.ch, nz);
+                if (L.c4 == 0) lam[r] = lm;
+            }
         }
     }
     zacc = red_q4(zacc);
@@ -185,38 +215,54 @@ __global__ __launch_bounds__(64) void interaction_fwd_k(
         const float4 se = sig + f4(kKlEps);
         const float4 den = se * se;
         float4 qacc = f4(0.f);
-        for (int64_t base = r0; base < r1; base += 4) {
-            const int64_t r = base + L.q;
-            const bool ok = r < r1;
-            const int64_t rr = ok ? r : r0;
-            const float4 y = gm * ((ld4(t + rr * 64 + L.ch) - m_use) * rstd) + bt;
-            const float p = red16(dot4(w2c, relu4(y))) + b2;
-            if (ok) {
-                const float lm = gate_lambda(u_gate[r], p);
-                const float4 d = (lm * ld4(f + r * 64 + L.ch) + (1.f - lm) * mu) - mu;
+        for (int64_t cb = r0; cb < r1; cb += 4 * CH) {
+            float4 tv[CH], fv[CH];
+            float ug[CH];
+#pragma unroll
+            for (int j = 0; j < CH; ++j) {
+                const int64_t r = cb + L.q + 4 * j, rr = r < r1 ? r : r0;
+                tv[j] = ld4(t + rr * 64 + L.ch);
+                fv[j] = ld4(f + rr * 64 + L.ch);
+                ug[j] = u_gate[rr];
+            }
+#pragma unroll
+            for (int j = 0; j < CH; ++j) {
+                const float4 y = gm * ((tv[j] - m_use) * rstd) + bt;
+                const float p = red16(dot4(w2c, relu4(y))) + b2;
+                const float lm = gate_lambda(ug[j], p);
+                const float4 d = (lm * fv[j] + (1.f - lm) * mu) - mu;
                 const float4 z = make_float4(d.x / se.x, d.y / se.y, d.z / se.z, d.w / se.w);
-                qacc = qacc + z * z;
+                qacc = macc(z * z, cb + L.q + 4 * j < r1 ? 1.f : 0.f, qacc);
             }
         }
         qacc = red_q4(qacc);
         float ksum = 0.f;
-        for (int64_t base = r0; base < r1; base += 4) {
-            const int64_t r = base + L.q;
-            const bool ok = r < r1;
-            const int64_t rr = ok ? r : r0;
-            const float4 y = gm * ((ld4(t + rr * 64 + L.ch) - m_use) * rstd) + bt;
-            const float p = red16(dot4(w2c, relu4(y))) + b2;
-            if (ok) {
-                const float lm = gate_lambda(u_gate[r], p);
+        for (int64_t cb = r0; cb < r1; cb += 4 * CH) {
+            float4 tv[CH];
+            float ug[CH];
+#pragma unroll
+            for (int j = 0; j < CH; ++j) {
+                const int64_t r = cb + L.q + 4 * j, rr = r < r1 ? r : r0;
+                tv[j] = ld4(t + rr * 64 + L.ch);
+                ug[j] = u_gate[rr];
+            }
+#pragma unroll
+            for (int j = 0; j < CH; ++j) {
+                const int64_t r = cb + L.q + 4 * j;
+                const float4 y = gm * ((tv[j] - m_use) * rstd) + bt;
+                const float p = red16(dot4(w2c, relu4(y))) + b2;
+                const float lm = gate_lambda(ug[j], p);
                 const float4 ns = (1.f - lm) * sig;
                 const float4 nn = ns * ns;
                 const float4 v = f4(0.5f) * make_float4(nn.x / den.x, nn.y / den.y, nn.z / den.z,
                                                         nn.w / den.w) + qacc;
-                if (kl) {
-                    st4(kl + (r - r0) * 64 + L.ch, v);
-                    st4(kl + (r - r0 + n) * 64 + L.ch, v);
+                if (r < r1) {
+                    if (kl) {
+                        st4(kl + (r - r0) * 64 + L.ch, v);
+                        st4(kl + (r - r0 + n) * 64 + L.ch, v);
+                    }
+                    ksum += (v.x + v.y) + (v.z + v.w);
                 }
-                ksum += (v.x + v.y) + (v.z + v.w);
             }
         }
         // mean over the duplicated [2n, 64] tensor == mean over [n, 64]
@@ -227,16 +273,23 @@ __global__ __launch_bounds__(64) void interaction_fwd_k(
     const float cst = red16(dot4(ld4(watt + L.ch), zacc)) + *battp;
     const float4 whi = ld4(watt + 64 + L.ch);
     float M = -INFINITY, S = 0.f;  // per row group, merged below
-    for (int64_t base = r0; base < r1; base += 4) {
-        const int64_t r = base + L.q;
-        const bool ok = r < r1;
-        const int64_t rr = ok ? r : r0;
-        const float lg = red16(dot4(whi, ld4(s + rr * 64 + L.ch))) + cst;
-        if (ok) {
-            if (L.c4 == 0) logit[r] = lg;
-            const float Mn = fmaxf(M, lg);
-            S = S * expf(M - Mn) + expf(lg - Mn);
-            M = Mn;
+    for (int64_t cb = r0; cb < r1; cb += 4 * CH) {
+        float4 sv[CH];
+#pragma unroll
+        for (int j = 0; j < CH; ++j) {
+            const int64_t r = cb + L.q + 4 * j, rr = r < r1 ? r : r0;
+            sv[j] = ld4(s + rr * 64 + L.ch);
+        }
+#pragma unroll
+        for (int j = 0; j < CH; ++j) {
+            const int64_t r = cb + L.q + 4 * j;
+            const float lg = red16(dot4(whi, sv[j])) + cst;
+            if (r < r1) {
+                if (L.c4 == 0) logit[r] = lg;
+                const float Mn = fmaxf(M, lg);
+                S = S * expf(M - Mn) + expf(lg - Mn);
+                M = Mn;
+            }
         }
     }
 #pragma unroll
@@ -247,13 +300,19 @@ __global__ __launch_bounds__(64) void interaction_fwd_k(
         M = Mn;
     }
     const float invS = 1.f / S;
-    for (int64_t base = r0; base < r1; base += 4) {
-        const int64_t r = base + L.q;
-        const bool ok = r < r1;
-        const int64_t rr = ok ? r : r0;
-        const float4 sv = ld4(s + rr * 64 + L.ch);
-        const float lg = red16(dot4(whi, sv)) + cst;
-        if (ok) st4(im + r * 128 + 64 + L.ch, (expf(lg - M) * invS) * sv);
+    for (int64_t cb = r0; cb < r1; cb += 4 * CH) {
+        float4 sv[CH];
+#pragma unroll
+        for (int j = 0; j < CH; ++j) {
+            const int64_t r = cb + L.q + 4 * j, rr = r < r1 ? r : r0;
+            sv[j] = ld4(s + rr * 64 + L.ch);
+        }
+#pragma unroll
+        for (int j = 0; j < CH; ++j) {
+            const int64_t r = cb + L.q + 4 * j;
+            const float lg = red16(dot4(whi, sv[j])) + cst;
+            if (r < r1) st4(im + r * 128 + 64 + L.ch, (expf(lg - M) * invS) * sv[j]);
+        }
     }
     if (threadIdx.x == 0) {
         sl[kStSoftMax] = M;
@@ -366,30 +425,57 @@ __global__ __launch_bounds__(64) void interaction_bwd_k(
     const float4 wlo = ld4(watt + L.ch), whi = ld4(watt + 64 + L.ch), zb = ld4(z1 + gi * 64 + L.ch);
 
     // ---- attention backward: a_v = alpha_v s_v, alpha = softmax(logit) ----
+    // The first chunk (all rows of a typical molecule's ego-net batch slice)
+    // stays in registers across the passes; later chunks are re-loaded.
+    auto att_load = [&](int64_t cb, float4 *ga, float4 *sv, float *lg) {
+#pragma unroll
+        for (int j = 0; j < CH; ++j) {
+            const int64_t r = cb + L.q + 4 * j, rr = r < r1 ? r : r0;
+            ga[j] = ld4(g_im + rr * 128 + 64 + L.ch);
+            sv[j] = ld4(s + rr * 64 + L.ch);
+            lg[j] = logit[rr];
+        }
+    };
+    float4 ga0[CH], sv0[CH];
+    float lg0[CH];
+    att_load(r0, ga0, sv0, lg0);
     float sa = 0.f;  // sum alpha * dalpha of this row group (uniform over its lanes)
-    for (int64_t base = r0; base < r1; base += 4) {
-        const int64_t r = base + L.q;
-        const bool ok = r < r1;
-        const int64_t rr = ok ? r : r0;
-        const float da = red16(dot4(ld4(g_im + rr * 128 + 64 + L.ch), ld4(s + rr * 64 + L.ch)));
-        if (ok) sa += expf(logit[r] - M) * invS * da;
+    auto att_sum = [&](int64_t cb, const float4 *ga, const float4 *sv, const float *lg) {
+#pragma unroll
+        for (int j = 0; j < CH; ++j) {
+            const float da = red16(dot4(ga[j], sv[j]));
+            sa = fmaf(expf(lg[j] - M) * invS * da, cb + L.q + 4 * j < r1 ? 1.f : 0.f, sa);
+        }
+    };
+    att_sum(r0, ga0, sv0, lg0);
+    for (int64_t cb = r0 + 4 * CH; cb < r1; cb += 4 * CH) {
+        float4 ga[CH], sv[CH];
+        float lg[CH];
+        att_load(cb, ga, sv, lg);
+        att_sum(cb, ga, sv, lg);
     }
     const float SA = red_q(sa);
     float4 dwhi = f4(0.f);
     float dcq = 0.f;
-    for (int64_t base = r0; base < r1; base += 4) {
-        const int64_t r = base + L.q;
-        const bool ok = r < r1;
-        const int64_t rr = ok ? r : r0;
-        const float4 ga = ld4(g_im + rr * 128 + 64 + L.ch), sv = ld4(s + rr * 64 + L.ch);
-        const float da = red16(dot4(ga, sv));
-        if (ok) {
-            const float al = expf(logit[r] - M) * invS;
+    auto att_grad = [&](int64_t cb, const float4 *ga, const float4 *sv, const float *lg) {
+#pragma unroll
+        for (int j = 0; j < CH; ++j) {
+            const int64_t r = cb + L.q + 4 * j;
+            const float w = r < r1 ? 1.f : 0.f;
+            const float da = red16(dot4(ga[j], sv[j]));
+            const float al = expf(lg[j] - M) * invS;
             const float dl = al * (da - SA);
-            st4(ds + r * 64 + L.ch, al * ga + dl * whi);
-            dwhi = dwhi + dl * sv;
-            dcq += dl;
+            if (r < r1) st4(ds + r * 64 + L.ch, al * ga[j] + dl * whi);
+            dwhi = macc(dl * sv[j], w, dwhi);
+            dcq = fmaf(dl, w, dcq);
         }
+    };
+    att_grad(r0, ga0, sv0, lg0);
+    for (int64_t cb = r0 + 4 * CH; cb < r1; cb += 4 * CH) {
+        float4 ga[CH], sv[CH];
+        float lg[CH];
+        att_load(cb, ga, sv, lg);
+        att_grad(cb, ga, sv, lg);
     }
     dwhi = red_q4(dwhi);
     const float dc = red_q(dcq);
@@ -417,55 +503,85 @@ __global__ __launch_bounds__(64) void interaction_bwd_k(
     // ---- compression backward ----
     float4 dw2 = f4(0.f), dg = f4(0.f), dbe = f4(0.f);
     float db2q = 0.f;
-    for (int64_t base = r0; base < r1; base += 4) {
-        const int64_t r = base + L.q;
-        const bool ok = r < r1;
-        const int64_t rr = ok ? r : r0;
-        const float lm = lam[rr];
-        const float4 fv = ld4(f + rr * 64 + L.ch);
-        const float4 gn = ld4(g_im + rr * 128 + L.ch) + gb;
-        const float4 fm = fv - mu;
-        float part = dot4(gn, fm - ld4(u_feat + rr * 64 + L.ch) * sig);
-        float4 dfv = lm * gn + gz2;
-        if (has_kl) {
-            const int rl = static_cast<int>(rr - r0);
-            const float4 gk = g_kl ? ld4(g_kl + rl * 64 + L.ch) + ld4(g_kl + (rl + n) * 64 + L.ch)
-                                   : f4(gk_uniform);
-            part += dot4(gk, (-(1.f - lm)) * (sig * sig * inv2)) + dot4(Gc, (2.f * lm) * (fm * fm * inv2));
-            dfv = dfv + (2.f * lm * lm) * (Gc * fm * inv2);
+    float4 dy0[CH], xh0[CH];  // first chunk's BN-input gradient and normalised input
+    auto comp = [&](int64_t cb, float4 *dyo, float4 *xho) {
+        float lm[CH];
+        float4 fv[CH], gn[CH], uv[CH], tv[CH], gk[CH];
+#pragma unroll
+        for (int j = 0; j < CH; ++j) {
+            const int64_t r = cb + L.q + 4 * j, rr = r < r1 ? r : r0;
+            lm[j] = lam[rr];
+            fv[j] = ld4(f + rr * 64 + L.ch);
+            gn[j] = ld4(g_im + rr * 128 + L.ch);
+            uv[j] = ld4(u_feat + rr * 64 + L.ch);
+            tv[j] = ld4(t + rr * 64 + L.ch);
+            if (has_kl && g_kl) {
+                const int rl = static_cast<int>(rr - r0);
+                gk[j] = ld4(g_kl + rl * 64 + L.ch) + ld4(g_kl + (rl + n) * 64 + L.ch);
+            } else {
+                gk[j] = f4(gk_uniform);
+            }
         }
-        const float dp = red16(part) * lm * (1.f - lm);
-        if (ok) {
-            const float4 xh = (ld4(t + r * 64 + L.ch) - m_use) * rstd;
+#pragma unroll
+        for (int j = 0; j < CH; ++j) {
+            const int64_t r = cb + L.q + 4 * j;
+            const float w = r < r1 ? 1.f : 0.f;
+            const float4 g = gn[j] + gb;
+            const float4 fm = fv[j] - mu;
+            float part = dot4(g, fm - uv[j] * sig);
+            float4 dfv = lm[j] * g + gz2;
+            if (has_kl) {
+                part += dot4(gk[j], (-(1.f - lm[j])) * (sig * sig * inv2)) +
+                        dot4(Gc, (2.f * lm[j]) * (fm * fm * inv2));
+                dfv = dfv + (2.f * lm[j] * lm[j]) * (Gc * fm * inv2);
+            }
+            const float dp = red16(part) * lm[j] * (1.f - lm[j]);
+            const float4 xh = (tv[j] - m_use) * rstd;
             const float4 y = gm * xh + bt;
-            dw2 = dw2 + dp * relu4(y);
-            db2q += dp;
+            dw2 = macc(dp * relu4(y), w, dw2);
+            db2q = fmaf(dp, w, db2q);
             const float4 dy = make_float4(y.x > 0.f ? dp * w2c.x : 0.f, y.y > 0.f ? dp * w2c.y : 0.f,
                                           y.z > 0.f ? dp * w2c.z : 0.f, y.w > 0.f ? dp * w2c.w : 0.f);
-            dg = dg + dy * xh;
-            dbe = dbe + dy;
-            st4(df + r * 64 + L.ch, dfv);
-            st4(dt + r * 64 + L.ch, dy);
+            dg = macc(dy * xh, w, dg);
+            dbe = macc(dy, w, dbe);
+            if (dyo) {
+                dyo[j] = dy;
+                xho[j] = xh;
+            }
+            if (r < r1) {
+                st4(df + r * 64 + L.ch, dfv);
+                if (!dyo) st4(dt + r * 64 + L.ch, dy);
+            }
         }
-    }
+    };
+    comp(r0, dy0, xh0);
+    for (int64_t cb = r0 + 4 * CH; cb < r1; cb += 4 * CH) comp(cb, nullptr, nullptr);
     dw2 = red_q4(dw2);
     dg = red_q4(dg);
     dbe = red_q4(dbe);
     const float db2 = red_q(db2q);
     // BatchNorm backward (this graph's batch statistics, or running stats);
-    // each lane re-reads only the dt entries it wrote itself
+    // chunk 0 from registers, later chunks re-read the dt entries this lane wrote
     const float4 gr = gm * rstd;
-    for (int64_t base = r0; base < r1; base += 4) {
-        const int64_t r = base + L.q;
-        if (r < r1) {
-            const float4 dy = ld4(dt + r * 64 + L.ch);
-            if (training) {
-                const float4 xh = (ld4(t + r * 64 + L.ch) - m_use) * rstd;
-                st4(dt + r * 64 + L.ch, gr * (dy - inv_n * dbe - xh * (inv_n * dg)));
-            } else {
-                st4(dt + r * 64 + L.ch, gr * dy);
-            }
+    auto bn_bwd = [&](int64_t cb, const float4 *dy, const float4 *xh) {
+#pragma unroll
+        for (int j = 0; j < CH; ++j) {
+            const int64_t r = cb + L.q + 4 * j;
+            if (r < r1)
+                st4(dt + r * 64 + L.ch,
+                    training ? gr * (dy[j] - inv_n * dbe - xh[j] * (inv_n * dg)) : gr * dy[j]);
         }
+    };
+    bn_bwd(r0, dy0, xh0);
+    for (int64_t cb = r0 + 4 * CH; cb < r1; cb += 4 * CH) {
+        float4 dy[CH], xh[CH];
+#pragma unroll
+        for (int j = 0; j < CH; ++j) {
+            const int64_t r = cb + L.q + 4 * j, rr = r < r1 ? r : r0;
+            dy[j] = ld4(dt + rr * 64 + L.ch);  // valid rows: written by this lane above
+            xh[j] = (ld4(t + rr * 64 + L.ch) - m_use) * rstd;
+        }
+        bn_bwd(cb, dy, xh);
     }
     if (L.q == 0) {
         st4(pg + kPgW2 + L.ch, dw2);

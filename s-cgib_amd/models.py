@@ -28,6 +28,8 @@ Differences from the reference, all deliberate:
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
@@ -134,6 +136,8 @@ _SIDE_STREAMS = {}
 # forward() runs the ego branch on a second stream (see _encode_forked);
 # bench.py turns it off for its single-stream event-timed kernel pass
 FORK_ENCODERS = True
+# both folded encoders as one autograd node (ops.gin_encoder_pair_x)
+PAIR_ENCODERS = os.environ.get("SCGIB_PAIR_ENCODERS", "1") != "0"
 
 
 def _side_stream(device):
@@ -213,6 +217,20 @@ class _SCGIBCore(nn.Module):
                 and batch_x.shape[1] <= 16 and not batch_x.requires_grad)
         side.wait_stream(main)
         batch_x.record_stream(side)
+        if fold and fork and PAIR_ENCODERS:
+            # one autograd node for both encoders (ops._GinEncoderPair): the
+            # ego chain is enqueued first on ``side`` in forward AND backward
+            with torch.cuda.stream(side):
+                ego = G.egonet_batch(batch_g, self.k_transition)
+            subgraphs_features, graph_features = ops.gin_encoder_pair_x(
+                batch_x, ego, enc_owner.Encoder2, batch_g, enc_owner.Encoder1, self.transfer_d,
+                ego.ndata["_ID"], side)
+            with torch.cuda.stream(side):
+                sub_readout = ops.segment_sum(subgraphs_features, ego.graph_ptr, ego.batch_size,
+                                              ego.seg_dims)
+            main.wait_stream(side)
+            sub_readout.record_stream(main)
+            return ego, (graph_features, subgraphs_features, sub_readout)
         with torch.cuda.stream(side):
             if fold:
                 ego = G.egonet_batch(batch_g, self.k_transition)

@@ -229,11 +229,11 @@ class _GinEncoder(torch.autograd.Function):
             coef = torch.empty(2, HIDDEN, dtype=torch.float32, device=dev)
             # dy, tile sums and the BN-backward finalize in one launch
             if dagg_next is None:
-                _lib.call("scgib_gin_bwd_stats_bn", _p(g_out), None, None, 1.0, _p(z2),
+                _launch("scgib_gin_bwd_stats_bn", {"n": n}, _p(g_out), None, None, 1.0, _p(z2),
                           _p(stat), n, int(ctx.training), _p(dy), _p(bn_g[0]), _p(bn_g[1]),
                           _p(coef), _p(bn_ws), _p(cnt), _p(gr.dims), st)
             else:
-                _lib.call("scgib_gin_bwd_stats_bn", _p(dagg_next), _p(gr.rowptr_t),
+                _launch("scgib_gin_bwd_stats_bn", {"n": n}, _p(dagg_next), _p(gr.rowptr_t),
                           _p(gr.col_t), ctx.opes[l + 1], _p(z2), _p(stat), n, int(ctx.training),
                           _p(dy), _p(bn_g[0]), _p(bn_g[1]), _p(coef), _p(bn_ws), _p(cnt),
                           _p(gr.dims), st)
@@ -296,6 +296,81 @@ def gin_encoder_x(x, graph, gin, transfer, node_map=None):
         raise _lib.ScgibError("transfer_d fold: no gradient w.r.t. the raw features")
     return _GinEncoder.apply(None, graph, gin, bool(gin.training), x, transfer.weight,
                              node_map, *_gin_layer_params(gin))
+
+
+class _Ctx:
+    """Stand-in ctx so _GinEncoder's forward/backward can run inside another
+    Function (the tensors it saves stay referenced by the outer node)."""
+
+    def save_for_backward(self, *t):
+        self.saved_tensors = t
+
+
+class _GinEncoderPair(torch.autograd.Function):
+    """Encoder2 (ego-net batch, on ``side``) and Encoder1 (core batch, on the
+    current stream) with transfer_d folded into both first layers, as ONE
+    autograd node.  Two separate nodes would make the autograd engine run
+    Encoder1's backward first (it was created later), and the cross-stream
+    event then makes the ego chain — the longer one — wait for all of it.
+    Here the ego backward is enqueued first on ``side`` and the two chains
+    overlap in both directions; d Wt = d Wt(ego) + d Wt(core)."""
+
+    @staticmethod
+    def forward(ctx, x, wt, nmap, ego, core, gin_ego, gin_core, training, side, *params):
+        main = _torch_stream()
+        ne = 6 * len(gin_ego.ginlayers)
+        ctx.sub = (_Ctx(), _Ctx())
+        ctx.side, ctx.ne = side, ne
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
+            s = _GinEncoder.forward(ctx.sub[0], None, ego, gin_ego, training, x, wt, nmap,
+                                    *params[:ne])
+        f = _GinEncoder.forward(ctx.sub[1], None, core, gin_core, training, x, wt, None,
+                                *params[ne:])
+        main.wait_stream(side)
+        s.record_stream(main)
+        return s, f
+
+    @staticmethod
+    def backward(ctx, g_s, g_f):
+        # backward: the ego chain (the longer one) stays on the current stream,
+        # where its weight-gradient reduces can fork to the aux stream (a fork
+        # from an already-forked stream breaks HIP-graph capture on this
+        # runtime, tools/capture_probe.py); Encoder1 runs on ``side``
+        main, side = _torch_stream(), ctx.side
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
+            gc = _GinEncoder.backward(ctx.sub[1], g_f)
+        ge = _GinEncoder.backward(ctx.sub[0], g_s)
+        main.wait_stream(side)
+        for g in gc:
+            if isinstance(g, torch.Tensor):
+                g.record_stream(main)
+        g_f.record_stream(side)
+        dwt = ge[5] + gc[5]
+        return (None, dwt, None, None, None, None, None, None, None, *ge[7:], *gc[7:])
+
+
+def _torch_stream():
+    return torch.cuda.current_stream()
+
+
+def gin_encoder_pair_x(x, ego, gin_ego, core, gin_core, transfer, node_map, side):
+    """(gin_ego(ego, transfer(x[node_map])), gin_core(core, transfer(x))) —
+    the two encoders of Mainmodel.forward with transfer_d folded, the ego
+    chain on stream ``side`` (forward and backward)."""
+    if ego.num_nodes() == 0 or core.num_nodes() == 0:
+        raise _lib.ScgibError("gin_encoder on an empty graph")
+    if transfer.bias is not None or transfer.weight.shape != (32, x.shape[1]) \
+            or x.shape[1] > 16:
+        raise _lib.ScgibError("transfer_d fold needs Linear(F <= 16, 32, bias=False)")
+    if x.requires_grad:
+        raise _lib.ScgibError("transfer_d fold: no gradient w.r.t. the raw features")
+    if bool(gin_ego.training) != bool(gin_core.training):
+        raise _lib.ScgibError("gin_encoder_pair_x: encoders in different train/eval modes")
+    return _GinEncoderPair.apply(x, transfer.weight, node_map, ego, core, gin_ego, gin_core,
+                                 bool(gin_core.training), side, *_gin_layer_params(gin_ego),
+                                 *_gin_layer_params(gin_core))
 
 
 # ---------------------------------------------------------------------------

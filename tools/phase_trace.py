@@ -1,0 +1,104 @@
+"""Per-workgroup phase timeline of the fused GIN layer kernels (debug build).
+
+    make -C s-cgib_amd/csrc trace
+    SCGIB_LIB=$PWD/s-cgib_amd/libscgib_trace.so python tools/phase_trace.py
+
+Runs one eager pretrain step of the bench workload on one stream; every
+launch routed through ops._launch is synchronised and its [grid][8] wall-clock
+stamps (100 MHz, common.h SCGIB_MARK) are summarised: kernel span, spread of
+workgroup start times, and per-phase durations (median / p90 / max, us).
+"""
+import ctypes
+import importlib
+import os
+import sys
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+pkg = importlib.import_module("s-cgib_amd")
+import bench  # noqa: E402
+
+PHASES = {
+    "scgib_gin_layer_fwd_bn": ["gather", "gemm1", "gemm2+st", "tilestat", "bn_hier"],
+    "scgib_gin_layer0_fwd": ["gather", "gemm1", "gemm2+st", "tilestat", "bn_hier"],
+    "scgib_gin_layer_bwd": ["ld+dz2", "dW2,dr", "dW1,dagg", "slab"],
+    "scgib_gin_layer0_bwd": ["ld+dz2", "dW2,dr", "dW1,dagg", "slab"],
+    "scgib_gin_bwd_stats_bn": ["gather+dy", "bn_hier"],
+}
+MAXB = 4096
+
+
+def main():
+    assert os.environ.get("SCGIB_LIB", "").endswith("libscgib_trace.so"), "use the trace build"
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(1234)
+    lib = pkg._lib.load()
+    buf = torch.zeros(MAXB * 8, dtype=torch.int64, device=dev)
+    lib.scgib_trace_set.argtypes = [ctypes.c_void_p]
+    assert lib.scgib_trace_set(ctypes.c_void_p(buf.data_ptr())) == 0
+    F_in = pkg.synth.WORKLOADS["qm9"][2]
+    mols = pkg.synth.molecules(512, "qm9", seed=0)
+    gh, _ = pkg.graph.collate_pyg(mols)
+    g = gh.to(dev)
+    dict.__setitem__(g.ndata, "x", F.normalize(g.ndata["x"].float()))
+    model = bench.make_model(F_in, 1, 5, dev)
+    pkg.models.FORK_ENCODERS = False
+    recs = []
+
+    def observe(name, meta, launch):
+        if name not in PHASES:
+            return launch()
+        torch.cuda.synchronize()
+        buf.zero_()
+        out = launch()
+        torch.cuda.synchronize()
+        recs.append((name, meta, buf.view(MAXB, 8).cpu().numpy().copy()))
+        return out
+
+    for it in range(2):  # second iteration: warm caches / allocator
+        recs.clear()
+        pkg.ops.OBSERVER = observe if it == 1 else None
+        _, kl, con, rec = model(g, g.ndata["x"], None, None, None, 1, None, 1, dev, 512)
+        (kl + con + rec).backward()
+        torch.cuda.synchronize()
+    pkg.ops.OBSERVER = None
+    for name, meta, t in recs:
+        nb = int((t[:, 0] != 0).sum())
+        t = t[:nb]
+        ph = PHASES[name]
+        start = t[:, 0]
+        t0 = start.min()
+        ends = np.where(t[:, 1:1 + len(ph)] != 0, t[:, 1:1 + len(ph)], 0)
+        last = ends.max()
+        hw = t[:, 7]
+        xcc = (hw >> 32) & 0xF
+        cu = (hw >> 8) & 0xF
+        se = (hw >> 13) & 0x7
+        sh = (hw >> 12) & 1
+        ncu = len(set(zip(xcc.tolist(), se.tolist(), sh.tolist(), cu.tolist())))
+        print(f"{name} n={meta.get('n')} d_in={meta.get('d_in')} blocks={nb} distinct_CUs={ncu} "
+              f"span={(last - t0) / 100:.2f}us start_spread(p50/p90/max)="
+              f"{np.percentile(start - t0, 50) / 100:.2f}/{np.percentile(start - t0, 90) / 100:.2f}/"
+              f"{(start - t0).max() / 100:.2f}us")
+        prev = start
+        for k, pname in enumerate(ph):
+            col = t[:, 1 + k]
+            ok = col != 0
+            if not ok.any():
+                continue
+            d = (col[ok] - prev[ok]) / 100.0
+            print(f"    {pname:10s} n={ok.sum():4d} p50={np.percentile(d, 50):6.2f} "
+                  f"p90={np.percentile(d, 90):6.2f} max={d.max():6.2f} us")
+            prev = np.where(ok, col, prev)
+        per_cu = {}
+        for i in range(nb):
+            per_cu.setdefault((xcc[i], se[i], sh[i], cu[i]), []).append(i)
+        occ = np.bincount([len(v) for v in per_cu.values()])
+        print(f"    blocks/CU histogram: {occ.tolist()}")
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,19 @@
+"""Print the kernel timeline of one graph-replay step from a rocprofv3
+kernel trace (csv): python tools/prof_step.py gpurun_out/prof_kt/kt_kernel_trace.csv [k]"""
+import csv
+import sys
+
+rows = list(csv.DictReader(open(sys.argv[1])))
+rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+starts = [i for i, r in enumerate(rows) if "egonet_count_k" in r["Kernel_Name"]]
+k = int(sys.argv[2]) if len(sys.argv) > 2 else len(starts) // 2
+i0, i1 = starts[k], starts[k + 1]
+t0 = int(rows[i0]["Start_Timestamp"])
+last = 0
+for r in rows[i0:i1]:
+    s = int(r["Start_Timestamp"]) - t0
+    e = int(r["End_Timestamp"]) - t0
+    print(f"{s/1000:8.2f} {e/1000:8.2f} {(e-s)/1000:7.2f} gap{(s-last)/1000:7.2f} "
+          f"q{r['Queue_Id']} {r['Kernel_Name'][:48]} g{r['Grid_Size_X']}")
+    last = max(last, e)
+print("span", (int(rows[i1]["Start_Timestamp"]) - t0) / 1000)

@@ -278,6 +278,8 @@ def main():
                     help="skip the event-timed kernel pass (PMC runs: only real step launches)")
     ap.add_argument("--eager", action="store_true",
                     help="launch every kernel from Python (no HIP-graph capture)")
+    ap.add_argument("--torch-adam", action="store_true",
+                    help="torch's fused Adam instead of the one-launch scgib Adam")
     a = ap.parse_args()
 
     # hipBLASLt's heuristics pick 2-workgroup kernels for the tall-skinny
@@ -304,7 +306,8 @@ def main():
     reducer = pkg.dist.GradAllReducer(model.parameters())
 
     if a.eager:
-        opt = torch.optim.Adam(model.parameters(), lr=1e-4, weight_decay=5e-5, fused=True)
+        opt = (torch.optim.Adam(model.parameters(), lr=1e-4, weight_decay=5e-5, fused=True)
+               if a.torch_adam else pkg.optim.Adam(model.parameters(), lr=1e-4, weight_decay=5e-5))
 
         def step(i):
             g = pool[i % len(pool)]
@@ -320,8 +323,11 @@ def main():
         # backward[, Adam]) on static buffers; each step copies the next batch
         # in (5 device-to-device copies) and replays.  Every kernel reads the
         # batch's actual sizes from the device.
-        opt = torch.optim.Adam(model.parameters(), lr=1e-4, weight_decay=5e-5, capturable=True,
-                               fused=True)
+        if a.torch_adam:
+            opt = torch.optim.Adam(model.parameters(), lr=1e-4, weight_decay=5e-5,
+                                   capturable=True, fused=True)
+        else:  # one-launch device Adam, same arithmetic (tests/test_gpu_optim.py)
+            opt = pkg.optim.Adam(model.parameters(), lr=1e-4, weight_decay=5e-5)
         n_cap, e_cap, mgn, ego_caps = pkg.graph.StaticBatch.capacities(pool_host, a.k, slack=1.02)
         static = pkg.graph.StaticBatch(a.batch, n_cap, e_cap, F_in, mgn, ego_caps, dev)
         padded = []

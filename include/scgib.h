@@ -332,6 +332,31 @@ int scgib_linear_bwd(const float *dy, const float *x, const float *w, int64_t n_
                      const float *add, float *dx, float *slab, float *wgrad,
                      const int32_t *dims, scgib_stream_t stream);
 
+/* ---- optimizer: one-launch Adam over a tensor list ------------------------
+ * torch.optim.Adam(params, lr, betas, eps, weight_decay) as every reference
+ * training script builds it (exp_pretraining.py / exp_molhiv.py:53,
+ * weight_decay=5e-5; fine-tune :157 1e-5), fused-Adam arithmetic: per
+ * tensor t = *step + 1, g += wd p, m = b1 m + (1-b1) g, v = b2 v + (1-b2) g^2,
+ * p -= lr/(1-b1^t) * m / (sqrt(v)/sqrt(1-b2^t) + eps), *step = t (fp32
+ * device scalar per tensor, like torch's capturable state['step']); the
+ * hyper-parameters are doubles and enter the moment updates in double, as
+ * in torch's fused kernel.
+ * n_tensors <= scgib_adam_max_tensors(); the table is copied into the kernel
+ * arguments (HIP-graph capturable).  `counter`: one uint32, zero on entry,
+ * left zero. */
+typedef struct {
+    float *param;
+    const float *grad;
+    float *exp_avg;
+    float *exp_avg_sq;
+    float *step;
+    int64_t numel;
+} scgib_adam_tensor;
+int64_t scgib_adam_max_tensors(void);
+int scgib_adam_step(const scgib_adam_tensor *tensors, int32_t n_tensors, double lr,
+                    double beta1, double beta2, double eps, double weight_decay,
+                    uint32_t *counter, scgib_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

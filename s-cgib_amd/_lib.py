@@ -13,7 +13,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 # SCGIB_LIB: debug builds only (tools/phase_trace.py loads libscgib_trace.so)
 LIB_PATH = os.environ.get("SCGIB_LIB") or os.path.join(HERE, "libscgib.so")
 
-_P, _I64, _I32, _F = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32, ctypes.c_float
+_P, _I64, _I32, _F, _D = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32, ctypes.c_float, ctypes.c_double
 
 # name -> (restype, argtypes); mirrors include/scgib.h exactly
 SIGNATURES = {
@@ -74,9 +74,18 @@ SIGNATURES = {
     "scgib_recon_partials_floats": (_I64, [_I64]),
     "scgib_recon_fwd": (ctypes.c_int, [_P, _P, _P, _I64, _I64, _P, _P, _P, _P, _P]),
     "scgib_recon_bwd": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _I64, _P, _P, _P, _P]),
+    "scgib_adam_max_tensors": (_I64, []),
+    "scgib_adam_step": (ctypes.c_int, [_P, _I32, _D, _D, _D, _D, _D, _P, _P]),
 }
 
-ABI_VERSION = 3
+
+class AdamTensor(ctypes.Structure):
+    """scgib_adam_tensor (include/scgib.h)."""
+    _fields_ = [("param", ctypes.c_void_p), ("grad", ctypes.c_void_p),
+                ("exp_avg", ctypes.c_void_p), ("exp_avg_sq", ctypes.c_void_p),
+                ("step", ctypes.c_void_p), ("numel", ctypes.c_int64)]
+
+ABI_VERSION = 4
 STATS_STRIDE = 260
 PGRAD_STRIDE = 324
 HIDDEN = 64

@@ -1,0 +1,124 @@
+// One-launch Adam step over a list of fp32 tensors (gfx950) — the optimizer
+// of every reference training script (torch.optim.Adam(model.parameters(),
+// lr, weight_decay=5e-5), e.g. exp_pretraining.py / exp_molhiv.py:53), with
+// the arithmetic of torch's fused Adam (L2 weight decay added to the
+// gradient, no amsgrad / maximize):
+//   t = step + 1;  g += wd * p;  m = b1 m + (1 - b1) g;  v = b2 v + (1 - b2) g^2
+//   p -= (lr / (1 - b1^t)) * m / (sqrt(v) / sqrt(1 - b2^t) + eps);  step = t
+//
+// torch's fused / foreach paths need 4-5 launches per step for a model of
+// ~75 small tensors (step increments + chunked multi-tensor kernels); here
+// the tensor table travels by value in the kernel arguments (captured with
+// the launch in a HIP graph), every workgroup handles one 1024-element chunk
+// of one tensor, and the last workgroup to finish advances every tensor's
+// step counter (all workgroups read the step before they arrive).
+#include "common.h"
+
+namespace scgib {
+
+constexpr int kAdamMax = 48;       // tensors per launch (kernel-argument table)
+constexpr int kAdamChunk = 1024;   // elements per workgroup
+
+struct AdamTable {
+    scgib_adam_tensor t[kAdamMax];
+    int32_t chunk0[kAdamMax + 1];  // first chunk of tensor i; chunk0[n] = grid
+    int32_t n;
+};
+
+// Precision mirrors torch's fused Adam (ATen fused_adam_utils.cuh): the
+// hyper-parameters are doubles, so the weight decay, both moment updates and
+// eps enter in double and round to fp32 on assignment; the bias corrections
+// are computed in double and rounded to fp32; the final update is fp32.
+__device__ __forceinline__ void adam_chunk(const scgib_adam_tensor &T, int64_t base,
+                                           float step_size, float bc2_sqrt, double beta1,
+                                           double beta2, double eps, double wd) {
+    float p[4], g[4], m[4], v[4];
+    int64_t idx[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {  // clamped loads (all in flight), masked stores
+        const int64_t j = base + threadIdx.x + 256 * k;
+        idx[k] = j < T.numel ? j : T.numel - 1;
+        p[k] = T.param[idx[k]];
+        g[k] = T.grad[idx[k]];
+        m[k] = T.exp_avg[idx[k]];
+        v[k] = T.exp_avg_sq[idx[k]];
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        float gg = g[k];
+        if (wd != 0.0) gg = static_cast<float>(gg + p[k] * wd);
+        const float mm = static_cast<float>(beta1 * m[k] + (1 - beta1) * gg);
+        const float vv = static_cast<float>(beta2 * v[k] + (1 - beta2) * gg * gg);
+        const float denom = static_cast<float>(sqrtf(vv) / bc2_sqrt + eps);
+        const float pp = p[k] - step_size * mm / denom;
+        if (base + threadIdx.x + 256 * k < T.numel) {
+            T.param[idx[k]] = pp;
+            T.exp_avg[idx[k]] = mm;
+            T.exp_avg_sq[idx[k]] = vv;
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void adam_step_k(const AdamTable tab, double lr, double beta1,
+                                                   double beta2, double eps, double wd,
+                                                   unsigned *__restrict__ counter) {
+    const int b = blockIdx.x;
+    // tensor of this chunk: one parallel compare over the table (lane q holds
+    // chunk0[q]) instead of a dependent scalar-load chain
+    const int lane = threadIdx.x & 63;
+    const bool le = lane < tab.n && tab.chunk0[lane < tab.n ? lane : 0] <= b;
+    const int i = __popcll(__ballot(le)) - 1;
+    const scgib_adam_tensor &T = tab.t[i];
+    const float t = *T.step + 1.f;
+    const float bc1 = static_cast<float>(1 - pow(beta1, static_cast<double>(t)));
+    const float bc2_sqrt = static_cast<float>(sqrt(1 - pow(beta2, static_cast<double>(t))));
+    const float step_size = static_cast<float>(lr / bc1);
+    const int64_t base = static_cast<int64_t>(b - tab.chunk0[i]) * kAdamChunk;
+    if (T.numel > 0) adam_chunk(T, base, step_size, bc2_sqrt, beta1, beta2, eps, wd);
+    __shared__ unsigned s_last;
+    __syncthreads();
+    if (threadIdx.x == 0)
+        s_last = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                 gridDim.x - 1;
+    __syncthreads();
+    if (s_last) {  // every workgroup has read its step: advance all of them at once
+        if (threadIdx.x < tab.n) *tab.t[threadIdx.x].step += 1.f;
+        if (threadIdx.x == 0) *counter = 0u;
+    }
+}
+
+}  // namespace scgib
+
+using namespace scgib;
+
+extern "C" int64_t scgib_adam_max_tensors(void) { return kAdamMax; }
+
+extern "C" int scgib_adam_step(const scgib_adam_tensor *tensors, int32_t n_tensors, double lr,
+                               double beta1, double beta2, double eps, double weight_decay,
+                               uint32_t *counter, scgib_stream_t stream) {
+    if (n_tensors < 0 || n_tensors > kAdamMax) return SCGIB_EINVAL;
+    if (n_tensors == 0) return SCGIB_OK;
+    if (!tensors || !counter) return SCGIB_EINVAL;
+    AdamTable tab;
+    tab.n = n_tensors;
+    int64_t chunks = 0;
+    for (int i = 0; i < n_tensors; ++i) {
+        const scgib_adam_tensor &T = tensors[i];
+        if (T.numel < 0 || !T.step || (T.numel > 0 && (!T.param || !T.grad || !T.exp_avg ||
+                                                       !T.exp_avg_sq)))
+            return SCGIB_EINVAL;
+        tab.t[i] = T;
+        tab.chunk0[i] = static_cast<int32_t>(chunks);
+        chunks += (T.numel + kAdamChunk - 1) / kAdamChunk;
+        if (chunks > 0x7fffffff) return SCGIB_EUNSUPPORTED;
+    }
+    tab.chunk0[n_tensors] = static_cast<int32_t>(chunks);
+    if (chunks == 0) {  // only empty tensors: just advance the steps
+        tab.chunk0[n_tensors] = 1;
+        chunks = 1;
+    }
+    for (int i = n_tensors; i < kAdamMax; ++i) tab.t[i] = scgib_adam_tensor{};
+    adam_step_k<<<dim3(static_cast<unsigned>(chunks)), 256, 0, as_stream(stream)>>>(
+        tab, lr, beta1, beta2, eps, weight_decay, counter);
+    return launch_status();
+}

@@ -359,7 +359,9 @@ def egonet_batch(g: GraphBatch, k: int, x=None):
     ego_eptr = torch.empty(n + 1, dtype=i32, device=dev)
     ws = torch.empty(int(_lib.query("scgib_egonet_workspace_bytes", n)), dtype=torch.uint8,
                      device=dev)
-    err = torch.zeros(1, dtype=i32, device=dev)
+    err = getattr(g, "err_buf", None)
+    if err is None:
+        err = torch.zeros(1, dtype=i32, device=dev)
     st = _stream()
     mgn = max(g.max_graph_nodes, 1)
     info = g.host_info
@@ -419,14 +421,17 @@ class StaticBatch:
         # one byte blob (rowptr | col | graph_ptr | dims | x, 256-B aligned
         # sections) so that loading a batch is a single device copy
         self.blob = torch.zeros(self._layout()[-1], dtype=torch.uint8, device=device)
-        self.rowptr, self.col, self.graph_ptr, self.dims, self.x = self._views(self.blob)
+        self.rowptr, self.col, self.graph_ptr, self.dims, self.err, self.x = \
+            self._views(self.blob)
         self.graph = GraphBatch(self.rowptr, self.col, self.graph_ptr, None, None,
                                 max_graph_nodes=max_graph_nodes, n_edges=-1)
         self.graph.dims = self.dims
+        # ego-net error word, zeroed by every load (no fill launch in the step)
+        self.graph.err_buf = self.err
         self.graph.ego_caps = tuple(int(c) for c in ego_caps)
 
     def _layout(self):
-        sizes = [4 * (self.n_cap + 1), 4 * max(self.e_cap, 1), 4 * (self.B + 1), 4 * 2,
+        sizes = [4 * (self.n_cap + 1), 4 * max(self.e_cap, 1), 4 * (self.B + 1), 4 * 4,
                  4 * self.n_cap * self.n_feat]
         offs = [0]
         for sz in sizes:
@@ -440,6 +445,7 @@ class StaticBatch:
                 blob[o[1]:o[1] + 4 * max(self.e_cap, 1)].view(i32),
                 blob[o[2]:o[2] + 4 * (self.B + 1)].view(i32),
                 blob[o[3]:o[3] + 8].view(i32),
+                blob[o[3] + 8:o[3] + 12].view(i32),
                 blob[o[4]:o[4] + 4 * self.n_cap * self.n_feat].view(torch.float32)
                 .view(self.n_cap, self.n_feat))
 
@@ -496,6 +502,11 @@ class StaticBatch:
     def load(self, padded):
         """Copy a pad()-ed batch into the static buffers (one device copy)."""
         self.blob.copy_(padded["blob"], non_blocking=True)
+
+    def ego_error(self):
+        """Error bits the ego-net build of the last step flagged (0 = none; see
+        egonet_batch) — a device read, for checks outside the timed loop."""
+        return int(self.err.item())
 
 
 # ---------------------------------------------------------------------------

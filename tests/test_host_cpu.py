@@ -184,7 +184,7 @@ def test_dgl_dropin_khop_and_ingest(pkg):
 
 
 def _header_prototypes():
-    """{name: [param kind]} from include/scgib.h; kind in P (pointer), I64, I32, F."""
+    """{name: [param kind]} from include/scgib.h; kind in P (pointer), I64, I32, F, D."""
     src = open(os.path.join(ROOT, "include", "scgib.h")).read()
     src = re.sub(r"/\*.*?\*/|//[^\n]*", "", src, flags=re.S)
     out = {}
@@ -200,6 +200,8 @@ def _header_prototypes():
                 kinds.append("I32")
             elif p.startswith("float"):
                 kinds.append("F")
+            elif p.startswith("double"):
+                kinds.append("D")
             else:
                 raise AssertionError(f"unparsed parameter {p!r} of {m.group(1)}")
         out[m.group(1)] = kinds
@@ -208,7 +210,7 @@ def _header_prototypes():
 
 def test_ctypes_table_matches_header_prototypes(pkg):
     L = pkg._lib
-    kind = {L._P: "P", L._I64: "I64", L._I32: "I32", L._F: "F"}
+    kind = {L._P: "P", L._I64: "I64", L._I32: "I32", L._F: "F", L._D: "D"}
     protos = _header_prototypes()
     assert set(protos) == set(L.SIGNATURES)
     for name, (_, argtypes) in L.SIGNATURES.items():
@@ -234,3 +236,14 @@ def test_checkpoint_roundtrip_continue(pkg, tmp_path):
     assert frozen and all(n.startswith("model.") and "layers.2" not in n for n in frozen)
     assert all(p.requires_grad for n, p in ft.named_parameters()
                if n.startswith("model.") and "layers.2" in n)
+
+
+def test_adam_rejects_cpu_parameters(pkg):
+    """The device optimizer fails loudly on CPU tensors (no CPU fallback)."""
+    p = torch.zeros(4, requires_grad=True)
+    p.grad = torch.ones(4)
+    opt = pkg.optim.Adam([p], lr=1e-3)
+    with pytest.raises(pkg._lib.ScgibError):
+        opt.step()
+    with pytest.raises(NotImplementedError):
+        pkg.optim.Adam([p], amsgrad=True)

@@ -34,6 +34,28 @@ extern "C" {
 
 typedef void *scgib_stream_t; /* hipStream_t */
 
+/* Deferred BatchNorm finalize (training, fused layers).  A layer launched
+ * with defer = 1 leaves its batch statistics as group partials in its bn_ws
+ * (at scgib_gin_bn_gpart_offset(n) floats) and does not write `stat` /
+ * the running statistics; the NEXT kernel that needs them finishes the
+ * combination in every workgroup (workgroup 0 writes the outputs), which
+ * takes the serial last-arriver tail off the layer chain.  Layers up to
+ * scgib_gin_defer_max_nodes() rows. */
+typedef struct {
+    const double *gpart;          /* producer's bn_ws + scgib_gin_bn_gpart_offset(n) */
+    const float *gamma, *beta;    /* producer layer's BatchNorm affine */
+    float *running_mean, *running_var;  /* NULL: untracked */
+    int64_t *num_batches_tracked;
+    float *stat;                  /* producer's [4][64] record (mean, invstd, scale, shift) */
+    float eps, momentum;
+} scgib_bn_pending;
+
+typedef struct {
+    const double *gpart;          /* bwd-stats bn_ws + scgib_gin_bn_gpart_offset(n) */
+    float *dgamma, *dbeta;        /* written by workgroup 0 of the consumer */
+    int32_t training;
+} scgib_bn_bwd_pending;
+
 enum {
     SCGIB_OK = 0,
     SCGIB_EINVAL = -1,       /* null pointer / negative size / bad dim      */
@@ -124,12 +146,19 @@ int scgib_gin_layer_fwd_bn(const float *h_in, int32_t d_in, const float *in_stat
                            const float *beta, float bn_eps, float momentum, float *running_mean,
                            float *running_var, int64_t *num_batches_tracked, float *stat,
                            float *bn_ws, uint32_t *counters, const int32_t *dims,
+                           const scgib_bn_pending *in_pending, int32_t defer,
                            scgib_stream_t stream);
 int scgib_gin_bwd_stats_bn(const float *dh, const int32_t *rowptr_t, const int32_t *col_t,
                            float one_plus_eps, const float *z2, const float *stat,
                            int64_t n_nodes, int32_t training, float *dy, float *dgamma,
                            float *dbeta, float *coef, float *bn_ws, uint32_t *counters,
-                           const int32_t *dims, scgib_stream_t stream);
+                           const int32_t *dims, int32_t defer, scgib_stream_t stream);
+/* Deferred finalize (scgib_bn_pending above): in_pending (NULL: in_stat is
+ * used) names the previous layer's pending statistics — this layer finishes
+ * them; defer = 1 leaves this layer's own pending (stat / running stats /
+ * dgamma, dbeta, coef are then written by the consumer). */
+int64_t scgib_gin_bn_gpart_offset(int64_t n_nodes);
+int64_t scgib_gin_defer_max_nodes(void);
 /* Layer 0 with transfer_d folded in (models.py:668-669 / :1164-1165:
  * h0 = x Wt^T, Wt = transfer_d.weight [32][F], F <= 16): the kernel gathers
  * the raw rows x[node_map[v]] (node_map NULL = identity; ego batches pass
@@ -147,15 +176,19 @@ int scgib_gin_layer0_fwd(const float *x, int32_t n_feat, const int32_t *node_map
                          const float *gamma, const float *beta, float bn_eps, float momentum,
                          float *running_mean, float *running_var, int64_t *num_batches_tracked,
                          float *stat, float *bn_ws, uint32_t *counters, const int32_t *dims,
-                         scgib_stream_t stream);
+                         int32_t defer, scgib_stream_t stream);
+/* layer backward: `pending` (NULL: coef is read) finishes the deferred
+ * scgib_gin_bwd_stats_bn of the same layer (coef may then be NULL). */
 int scgib_gin_layer0_bwd(const float *dy, const float *z2, const float *r, const float *agg,
                          const float *aggx, const float *stat, const float *coef,
                          const float *w1, const float *w2, int64_t n_nodes, float *slab,
-                         const int32_t *dims, scgib_stream_t stream);
+                         const int32_t *dims, const scgib_bn_bwd_pending *pending,
+                         scgib_stream_t stream);
 int scgib_gin_layer_bwd(const float *dy, const float *z2, const float *r, const float *agg,
                         int32_t d_in, const float *stat, const float *coef, const float *w1,
                         const float *w2, int64_t n_nodes, float *dagg, float *slab,
-                        float *wgrad, const int32_t *dims, scgib_stream_t stream);
+                        float *wgrad, const int32_t *dims, const scgib_bn_bwd_pending *pending,
+                        scgib_stream_t stream);
 
 /* ---- A6: per-segment readouts (dgl.sum_nodes) -------------------------------
  * out[s,:] = sum_{i in [ptr[s], ptr[s+1])} x[i,:]   (models.py:716, 725, 733)

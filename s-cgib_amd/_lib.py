@@ -50,16 +50,18 @@ SIGNATURES = {
     "scgib_gin_layer0_slab_width": (_I64, []),
     "scgib_gin_layer0_fwd": (ctypes.c_int, [_P, _I32, _P, _P, _P, _P, _I64, _F, _P, _P, _P, _P,
                                             _P, _P, _P, _P, _P, _P, _F, _F, _P, _P, _P, _P, _P,
-                                            _P, _P, _P]),
+                                            _P, _P, _I32, _P]),
     "scgib_gin_layer0_bwd": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _I64, _P, _P,
-                                            _P]),
+                                            _P, _P]),
+    "scgib_gin_bn_gpart_offset": (_I64, [_I64]),
+    "scgib_gin_defer_max_nodes": (_I64, []),
     "scgib_gin_bn_ws_floats": (_I64, [_I64]),
     "scgib_gin_counters": (_I64, [_I64]),
     "scgib_gin_layer_fwd_bn": (ctypes.c_int, [_P, _I32, _P, _P, _P, _I64, _F, _P, _P, _P, _P, _P,
                                               _P, _P, _P, _P, _F, _F, _P, _P, _P, _P, _P, _P, _P,
-                                              _P]),
+                                              _P, _I32, _P]),
     "scgib_gin_bwd_stats_bn": (ctypes.c_int, [_P, _P, _P, _F, _P, _P, _I64, _I32, _P, _P, _P, _P,
-                                              _P, _P, _P, _P]),
+                                              _P, _P, _P, _I32, _P]),
     "scgib_gin_bwd_slabs": (_I64, [_I64]),
     "scgib_slab_reduce": (ctypes.c_int, [_P, _I32, _I64, _P, _P]),
     "scgib_gin_slab_floats": (_I64, [_I64, _I32]),
@@ -70,7 +72,7 @@ SIGNATURES = {
     "scgib_gin_bwd_stats": (ctypes.c_int, [_P, _P, _P, _F, _P, _P, _I64, _P, _P, _P, _P]),
     "scgib_bn_bwd_finalize": (ctypes.c_int, [_P, _I64, _I32, _P, _P, _P, _P, _P]),
     "scgib_gin_layer_bwd": (ctypes.c_int, [_P, _P, _P, _P, _I32, _P, _P, _P, _P, _I64, _P, _P,
-                                           _P, _P, _P]),
+                                           _P, _P, _P, _P]),
     "scgib_recon_partials_floats": (_I64, [_I64]),
     "scgib_recon_fwd": (ctypes.c_int, [_P, _P, _P, _I64, _I64, _P, _P, _P, _P, _P]),
     "scgib_recon_bwd": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _I64, _P, _P, _P, _P]),
@@ -79,13 +81,27 @@ SIGNATURES = {
 }
 
 
+class BnPending(ctypes.Structure):
+    """scgib_bn_pending (include/scgib.h)."""
+    _fields_ = [("gpart", ctypes.c_void_p), ("gamma", ctypes.c_void_p),
+                ("beta", ctypes.c_void_p), ("running_mean", ctypes.c_void_p),
+                ("running_var", ctypes.c_void_p), ("num_batches_tracked", ctypes.c_void_p),
+                ("stat", ctypes.c_void_p), ("eps", ctypes.c_float), ("momentum", ctypes.c_float)]
+
+
+class BnBwdPending(ctypes.Structure):
+    """scgib_bn_bwd_pending (include/scgib.h)."""
+    _fields_ = [("gpart", ctypes.c_void_p), ("dgamma", ctypes.c_void_p),
+                ("dbeta", ctypes.c_void_p), ("training", ctypes.c_int32)]
+
+
 class AdamTensor(ctypes.Structure):
     """scgib_adam_tensor (include/scgib.h)."""
     _fields_ = [("param", ctypes.c_void_p), ("grad", ctypes.c_void_p),
                 ("exp_avg", ctypes.c_void_p), ("exp_avg_sq", ctypes.c_void_p),
                 ("step", ctypes.c_void_p), ("numel", ctypes.c_int64)]
 
-ABI_VERSION = 4
+ABI_VERSION = 5
 STATS_STRIDE = 260
 PGRAD_STRIDE = 324
 HIDDEN = 64

@@ -67,18 +67,18 @@ int launch_slab_reduce(const float *slab, int nslab, int64_t width, float *out, 
 
 // Phase tracing (debug build only, `make trace` -> libscgib_trace.so):
 // thread 0 of each workgroup stamps the 100 MHz wall clock at phase marks
-// into g_trace[block * 8 + k]; slot 7 holds (XCC_ID << 32) | HW_ID.
+// into g_trace[block * 16 + k]; slot 15 holds (XCC_ID << 32) | HW_ID.
 #ifdef SCGIB_TRACE
 static __device__ unsigned long long *g_trace;
 #define SCGIB_MARK(k)                                                                     \
     do {                                                                                  \
         if (threadIdx.x == 0 && g_trace)                                                  \
-            g_trace[static_cast<uint64_t>(blockIdx.x) * 8 + (k)] = wall_clock64();        \
+            g_trace[static_cast<uint64_t>(blockIdx.x) * 16 + (k)] = wall_clock64();        \
     } while (0)
 #define SCGIB_MARK_HWID()                                                                 \
     do {                                                                                  \
         if (threadIdx.x == 0 && g_trace)                                                  \
-            g_trace[static_cast<uint64_t>(blockIdx.x) * 8 + 7] =                          \
+            g_trace[static_cast<uint64_t>(blockIdx.x) * 16 + 15] =                          \
                 (static_cast<unsigned long long>(__builtin_amdgcn_s_getreg((31 << 11) | 20)) << 32) | \
                 static_cast<unsigned>(__builtin_amdgcn_s_getreg((31 << 11) | 4));         \
     } while (0)

@@ -60,6 +60,7 @@ struct BnFwdFuse {          // gin_fwd_k: BN statistics + running update
     int64_t *nbt;
     float eps, momentum;
     int ngr_cap;
+    int defer;              // stop at the group partials (the consumer finishes)
 };
 
 struct BnBwdFuse {          // gin_bwd_stats_k: dgamma, dbeta, dz2 coefficients
@@ -67,6 +68,7 @@ struct BnBwdFuse {          // gin_bwd_stats_k: dgamma, dbeta, dz2 coefficients
     double *gpart;          // [ngr_cap][128]: group sum dy, group sum dy * xhat
     float *dgamma, *dbeta, *coef;
     int training, ngr_cap;
+    int defer;
 };
 
 // release this workgroup's prior global writes, count it in, and return
@@ -106,6 +108,127 @@ __device__ __forceinline__ bool block_arrive(unsigned *counter, unsigned expecte
 __device__ __forceinline__ double rows_in(int64_t n, int64_t first, int64_t span) {
     const int64_t r = n - first;
     return static_cast<double>(r < span ? r : span);
+}
+
+// Layer statistics from the ngr group partials (fp64, fixed order; 256
+// threads, channel c = tid & 63, partition p = tid >> 6 takes groups p, p + 4,
+// ...; one load round while ngr <= 64).  Every thread returns its channel's
+// mean and centred M2:  M2 = sum_g [M2_g + (S_g - n_g mean)^2 / n_g].
+// AGENT: the partials were written earlier in this kernel (agent-scope loads);
+// otherwise by a previous kernel (plain loads: L2-cached after the first
+// workgroup of an XCD, coherent across the kernel boundary).
+template <bool AGENT>
+__device__ __forceinline__ double ld_part(const double *p) {
+    if constexpr (AGENT) return ld_agent(p);
+    else return *p;
+}
+
+// Barrier-free layer combine (wave-local shuffles, no LDS): lane l of wave w
+// owns channel c = 16 w + (l & 15) and partition p = l >> 4, which takes
+// groups p, p + 4, ... (fp64, fixed order); the four partitions combine as
+// (p0 + p1) + (p2 + p3) through two xor shuffles (identical in every lane).
+// Split into the load (issue early, registers) and the combine, so other
+// loads can be in flight meanwhile; one load round for ngr <= kFinG.
+constexpr int kFinR = 16, kFinG = 4 * kFinR;
+
+struct FwdFin {
+    double vs[kFinR], vq[kFinR];
+};
+
+__device__ __forceinline__ int fin_channel() { return 16 * (threadIdx.x >> 6) + (threadIdx.x & 15); }
+
+template <bool AGENT>
+__device__ __forceinline__ void bn_fwd_fin_load(const double *__restrict__ gpart, int ngr, int g0,
+                                                FwdFin &f) {
+    const int c = fin_channel(), p = (threadIdx.x & 63) >> 4;
+#pragma unroll
+    for (int u = 0; u < kFinR; ++u) {
+        if (g0 + 4 * u < ngr) {  // wave-uniform: only rounds with a live group are loaded
+            const int64_t gg = g0 + p + 4 * u < ngr ? g0 + p + 4 * u : 0;  // group 0 always exists
+            f.vs[u] = ld_part<AGENT>(gpart + gg * 128 + c);
+            f.vq[u] = ld_part<AGENT>(gpart + gg * 128 + 64 + c);
+        }
+    }
+}
+
+__device__ __forceinline__ double quad_sum(double a) {
+    a = a + __shfl_xor(a, 16, kWave);
+    return a + __shfl_xor(a, 32, kWave);
+}
+
+// mean and centred M2 of channel fin_channel():
+//   mean = sum_g S_g / n,  M2 = sum_g [M2_g + (S_g - n_g mean)^2 / n_g]
+// n_g = 1024 for every group but possibly the last, and dividing by a power
+// of two equals multiplying by its reciprocal exactly, so only the last
+// group's term (added last by its owner, the same order) divides.
+template <bool AGENT>
+__device__ void bn_fwd_final(const double *__restrict__ gpart, int64_t n, int ngr, FwdFin &f,
+                             double &mean, double &M2) {
+    constexpr double kFull = kGroup * TM, kInvFull = 1.0 / kFull;
+    const int p = (threadIdx.x & 63) >> 4;
+    double a = 0.0;
+    for (int g0 = 0; g0 < ngr; g0 += kFinG) {
+        if (g0 > 0) bn_fwd_fin_load<AGENT>(gpart, ngr, g0, f);
+#pragma unroll
+        for (int u = 0; u < kFinR; ++u)
+            if (g0 + 4 * u < ngr) a += g0 + p + 4 * u < ngr ? f.vs[u] : 0.0;
+    }
+    mean = quad_sum(a) / static_cast<double>(n);
+    const int glast = ngr - 1;
+    const double nlast = rows_in(n, int64_t(glast) * kGroup * TM, kGroup * TM);
+    const bool last_partial = nlast != kFull;
+    double q = 0.0, last_vq = 0.0, last_d = 0.0;
+    bool owns_last = false;
+    for (int g0 = 0; g0 < ngr; g0 += kFinG) {
+        if (ngr > kFinG) bn_fwd_fin_load<AGENT>(gpart, ngr, g0, f);  // else still in registers
+#pragma unroll
+        for (int u = 0; u < kFinR; ++u) {
+            if (g0 + 4 * u < ngr) {
+                const int g = g0 + p + 4 * u;
+                if (g < ngr) {
+                    if (g == glast && last_partial) {
+                        owns_last = true;
+                        last_vq = f.vq[u];
+                        last_d = f.vs[u] - nlast * mean;
+                    } else {
+                        const double d = f.vs[u] - kFull * mean;
+                        q += f.vq[u] + d * d * kInvFull;
+                    }
+                }
+            }
+        }
+    }
+    if (owns_last) q += last_vq + last_d * last_d / nlast;
+    M2 = quad_sum(q);
+}
+
+// BN record of channel c from (mean, M2): returns scale / shift; with
+// `write`, also the [4][64] record and the running-statistics update
+// (momentum, unbiased variance, num_batches_tracked += 1).
+// (gamma_c / beta_c are passed as values: load them early, a dependent
+// global load here costs a full memory latency)
+__device__ __forceinline__ float2 bn_fwd_publish(int c, double mean, double M2, int64_t n,
+                                                 float gamma_c, float beta_c,
+                                                 float eps, float momentum, float *rmean,
+                                                 float *rvar, int64_t *nbt, float *stat,
+                                                 bool write) {
+    const double var = M2 / static_cast<double>(n);
+    if (write && rmean) {
+        rmean[c] = static_cast<float>((1.0 - momentum) * rmean[c] + momentum * mean);
+        rvar[c] = static_cast<float>((1.0 - momentum) * rvar[c] +
+                                     momentum * (n > 1 ? M2 / static_cast<double>(n - 1) : M2));
+        if (c == 0 && nbt) *nbt += 1;
+    }
+    const double istd = 1.0 / sqrt(var + static_cast<double>(eps));
+    const double sc = gamma_c * istd;
+    const float scale = static_cast<float>(sc), shift = static_cast<float>(beta_c - mean * sc);
+    if (write) {
+        stat[c] = static_cast<float>(mean);
+        stat[64 + c] = static_cast<float>(istd);
+        stat[128 + c] = scale;
+        stat[192 + c] = shift;
+    }
+    return make_float2(scale, shift);
 }
 
 // 256 threads: channel c = tid & 63, partition p = tid >> 6 (4 partitions).
@@ -158,59 +281,64 @@ __device__ void bn_fwd_hier(const float *__restrict__ part, int64_t n, int64_t t
         if (p == 0) st_agent(fz.gpart + int64_t(g) * 128 + 64 + c, ((sh[0][c] + sh[1][c]) + sh[2][c]) + sh[3][c]);
         if (threadIdx.x == 0) fz.counters[g] = 0u;
     }
+    if (fz.defer) return;  // the consumer kernel finishes (bn_fwd_final there)
     if (!block_arrive(&fz.counters[fz.ngr_cap], ngr)) return;
-    // layer combine over the ngr groups (8 groups' loads in flight per thread)
-    double a = 0.0;
-    for (int g0 = p; g0 < ngr; g0 += 4 * 8) {
-        double v[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) v[u] = ld_agent(fz.gpart + int64_t(g0 + 4 * u < ngr ? g0 + 4 * u : p) * 128 + c);
-#pragma unroll
-        for (int u = 0; u < 8; ++u) a += g0 + 4 * u < ngr ? v[u] : 0.0;
-    }
-    sh[p][c] = a;
-    __syncthreads();
-    if (p == 0) smean[c] = (((sh[0][c] + sh[1][c]) + sh[2][c]) + sh[3][c]) / static_cast<double>(n);
-    __syncthreads();
-    const double mean = smean[c];
-    double q = 0.0;
-    for (int g0 = p; g0 < ngr; g0 += 4 * 8) {
-        double vs[8], vq[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-            const int64_t gg = g0 + 4 * u < ngr ? g0 + 4 * u : p;
-            vs[u] = ld_agent(fz.gpart + gg * 128 + c);
-            vq[u] = ld_agent(fz.gpart + gg * 128 + 64 + c);
-        }
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-            if (g0 + 4 * u < ngr) {
-                const double ng = rows_in(n, int64_t(g0 + 4 * u) * kGroup * TM, kGroup * TM);
-                const double d = vs[u] - ng * mean;
-                q += vq[u] + d * d / ng;
-            }
-        }
-    }
-    __syncthreads();
-    sh[p][c] = q;
-    __syncthreads();
-    if (p == 0) {
-        const double M2 = ((sh[0][c] + sh[1][c]) + sh[2][c]) + sh[3][c];
-        const double var = M2 / static_cast<double>(n);
-        if (fz.rmean) {
-            fz.rmean[c] = static_cast<float>((1.0 - fz.momentum) * fz.rmean[c] + fz.momentum * mean);
-            fz.rvar[c] = static_cast<float>((1.0 - fz.momentum) * fz.rvar[c] +
-                                            fz.momentum * (n > 1 ? M2 / static_cast<double>(n - 1) : M2));
-            if (c == 0 && fz.nbt) *fz.nbt += 1;
-        }
-        const double istd = 1.0 / sqrt(var + static_cast<double>(fz.eps));
-        const double sc = fz.gamma[c] * istd;
-        fz.stat[c] = static_cast<float>(mean);
-        fz.stat[64 + c] = static_cast<float>(istd);
-        fz.stat[128 + c] = static_cast<float>(sc);
-        fz.stat[192 + c] = static_cast<float>(fz.beta[c] - mean * sc);
-    }
+    double mean, M2;
+    FwdFin fin;
+    const float gam = fz.gamma[fin_channel()], bet = fz.beta[fin_channel()];
+    bn_fwd_fin_load<true>(fz.gpart, ngr, 0, fin);
+    bn_fwd_final<true>(fz.gpart, n, ngr, fin, mean, M2);
+    bn_fwd_publish(fin_channel(), mean, M2, n, gam, bet, fz.eps, fz.momentum, fz.rmean,
+                   fz.rvar, fz.nbt, fz.stat, (threadIdx.x & 63) < 16);
     if (threadIdx.x == 0) fz.counters[fz.ngr_cap] = 0u;
+}
+
+// Layer sums (dbeta | dgamma, 128 values) from the ngr group partials,
+// barrier-free: lane l of wave w owns sum index cs = 32 w + (l & 31) and
+// partition p = l >> 5 (groups p, p + 2, ...); p0 + p1 via one xor shuffle.
+struct BwdFin {
+    double v[kFinR];
+};
+
+__device__ __forceinline__ int bfin_index() { return 32 * (threadIdx.x >> 6) + (threadIdx.x & 31); }
+
+template <bool AGENT>
+__device__ __forceinline__ void bn_bwd_fin_load(const double *__restrict__ gpart, int ngr, int g0,
+                                                BwdFin &f) {
+    const int cs = bfin_index(), p = (threadIdx.x & 63) >> 5;
+#pragma unroll
+    for (int u = 0; u < kFinR; ++u) {
+        if (g0 + 2 * u < ngr) {  // wave-uniform
+            const int64_t gg = g0 + p + 2 * u < ngr ? g0 + p + 2 * u : 0;  // group 0 always exists
+            f.v[u] = ld_part<AGENT>(gpart + gg * 128 + cs);
+        }
+    }
+}
+
+template <bool AGENT>
+__device__ double bn_bwd_final(const double *__restrict__ gpart, int ngr, BwdFin &f) {
+    const int p = (threadIdx.x & 63) >> 5;
+    double a = 0.0;
+    for (int g0 = 0; g0 < ngr; g0 += 2 * kFinR) {
+        if (g0 > 0) bn_bwd_fin_load<AGENT>(gpart, ngr, g0, f);
+#pragma unroll
+        for (int u = 0; u < kFinR; ++u)
+            if (g0 + 2 * u < ngr) a += g0 + p + 2 * u < ngr ? f.v[u] : 0.0;
+    }
+    return a + __shfl_xor(a, 32, kWave);
+}
+
+// dbeta = sum dy (c < 64), dgamma = sum dy xhat (c >= 64); dz2 coefficient
+// coef[c] = tot / N in training (0 in eval); coef may be nullptr
+__device__ __forceinline__ float bn_bwd_publish(int c, double tot, int64_t n, int training,
+                                                float *dgamma, float *dbeta, float *coef) {
+    const float cf = training ? static_cast<float>(tot / static_cast<double>(n)) : 0.f;
+    if (dbeta) {
+        if (c < 64) dbeta[c] = static_cast<float>(tot);
+        else dgamma[c - 64] = static_cast<float>(tot);
+    }
+    if (coef) coef[c] = cf;
+    return cf;
 }
 
 // backward: tile (sum dy, sum dy xhat) -> group -> layer sums (fp64)
@@ -238,28 +366,13 @@ __device__ void bn_bwd_hier(const float *__restrict__ part, int64_t n, int64_t t
         if (p == 0) st_agent(bz.gpart + int64_t(g) * 128 + c, sh[0][c] + sh[1][c]);
         if (threadIdx.x == 0) bz.counters[g] = 0u;
     }
+    if (bz.defer) return;  // the layer's gin_bwd_k finishes (bn_bwd_final there)
     if (!block_arrive(&bz.counters[bz.ngr_cap], ngr)) return;
-    double a = 0.0;
-    for (int g0 = p; g0 < ngr; g0 += 2 * 8) {
-        double v[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) v[u] = ld_agent(bz.gpart + int64_t(g0 + 2 * u < ngr ? g0 + 2 * u : p) * 128 + c);
-#pragma unroll
-        for (int u = 0; u < 8; ++u) a += g0 + 2 * u < ngr ? v[u] : 0.0;
-    }
-    __syncthreads();
-    sh[p][c] = a;
-    __syncthreads();
-    if (p == 0) {
-        const double tot = sh[0][c] + sh[1][c];
-        if (c < 64) {
-            bz.dbeta[c] = static_cast<float>(tot);
-            bz.coef[c] = bz.training ? static_cast<float>(tot / static_cast<double>(n)) : 0.f;
-        } else {
-            bz.dgamma[c - 64] = static_cast<float>(tot);
-            bz.coef[c] = bz.training ? static_cast<float>(tot / static_cast<double>(n)) : 0.f;
-        }
-    }
+    BwdFin fin;
+    bn_bwd_fin_load<true>(bz.gpart, ngr, 0, fin);
+    const double tot = bn_bwd_final<true>(bz.gpart, ngr, fin);
+    if ((threadIdx.x & 63) < 32)
+        bn_bwd_publish(bfin_index(), tot, n, bz.training, bz.dgamma, bz.dbeta, bz.coef);
     if (threadIdx.x == 0) bz.counters[bz.ngr_cap] = 0u;
 }
 
@@ -356,7 +469,8 @@ __global__ __launch_bounds__(256) void gin_fwd_k(
     const int32_t *__restrict__ col, int64_t ncap, float ope, const float *__restrict__ w1,
     const float *__restrict__ b1, const float *__restrict__ w2, const float *__restrict__ b2,
     float *__restrict__ agg_out, float *__restrict__ r_out, float *__restrict__ z2_out,
-    float *__restrict__ part, const int32_t *__restrict__ dims, BnFwdFuse fz, PreArgs pre) {
+    float *__restrict__ part, const int32_t *__restrict__ dims, BnFwdFuse fz, PreArgs pre,
+    scgib_bn_pending pend) {
     constexpr int LDA = DIN + 1, LPR = DIN / 4, RPP = 256 / LPR;
     static_assert(!PRE || DIN == 32, "transfer_d fold produces the 32-wide layer-0 input");
     const int64_t n = eff_count(dims, 0, ncap);
@@ -388,6 +502,15 @@ __global__ __launch_bounds__(256) void gin_fwd_k(
     SCGIB_MARK(0);
     SCGIB_MARK_HWID();
 
+    // the previous layer's deferred BN statistics: partial loads go out first
+    FwdFin fin;
+    float pend_gam = 0.f, pend_bet = 0.f;
+    const int pend_ngr = static_cast<int>(((n + TM - 1) / TM + kGroup - 1) / kGroup);
+    if (XFORM && pend.gpart) {
+        pend_gam = pend.gamma[fin_channel()];
+        pend_bet = pend.beta[fin_channel()];
+        bn_fwd_fin_load<false>(pend.gpart, pend_ngr, 0, fin);
+    }
     stage_weights<DIN>(w1, w2, sW1, sW2);
     if constexpr (PRE) {  // transfer_d folded: gather raw features, then agg0 = aggx Wt^T
         float *sXg = sPre, *sWt = sPre + TM * kPreLD;
@@ -439,13 +562,38 @@ __global__ __launch_bounds__(256) void gin_fwd_k(
         constexpr int RPT = TM / RPP;
         const int c = tid % LPR, rbase = tid / LPR;
         float4 sc = make_float4(1.f, 1.f, 1.f, 1.f), sh = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (XFORM) {
-            sc = ld4(in_scale + 4 * c);
-            sh = ld4(in_shift + 4 * c);
-        }
         const float4 *h4 = reinterpret_cast<const float4 *>(h);
         float4 acc[RPT];
-        gather_rows<RPT, RPP, LPR, XFORM>(h4, rowptr, col, row0, nv, rbase, c, ope, sc, sh, acc);
+        GatherHead<RPT> hd;
+        gather_head<RPT, RPP, LPR>(h4, rowptr, row0, nv, rbase, c, hd);  // in flight meanwhile
+        if (XFORM) {
+            if (pend.gpart) {  // finish the previous layer's deferred BatchNorm statistics
+                __shared__ float sScSh[128];
+                double mean, M2;
+                SCGIB_MARK(8);
+                bn_fwd_final<false>(pend.gpart, n, pend_ngr, fin, mean, M2);
+                SCGIB_MARK(9);
+                const int fc = fin_channel();
+                const bool lead = (tid & 63) < 16;
+                const float2 ss = bn_fwd_publish(
+                    fc, mean, M2, n, pend_gam, pend_bet, pend.eps, pend.momentum,
+                    pend.running_mean, pend.running_var, pend.num_batches_tracked, pend.stat,
+                    blockIdx.x == 0 && lead);
+                if (lead) {
+                    sScSh[fc] = ss.x;
+                    sScSh[64 + fc] = ss.y;
+                }
+                __syncthreads();
+                SCGIB_MARK(6);
+                sc = make_float4(sScSh[4 * c], sScSh[4 * c + 1], sScSh[4 * c + 2], sScSh[4 * c + 3]);
+                sh = make_float4(sScSh[64 + 4 * c], sScSh[65 + 4 * c], sScSh[66 + 4 * c],
+                                 sScSh[67 + 4 * c]);
+            } else {
+                sc = ld4(in_scale + 4 * c);
+                sh = ld4(in_shift + 4 * c);
+            }
+        }
+        gather_tail<RPT, LPR, XFORM>(h4, col, hd, c, ope, sc, sh, acc);
 #pragma unroll
         for (int k = 0; k < RPT; ++k) {
             const int rr = rbase + k * RPP;
@@ -746,7 +894,7 @@ __global__ __launch_bounds__(256, (DIN <= 64 ? 2 : 1)) void gin_bwd_k(
     const float *__restrict__ agg, const float *__restrict__ stat,
     const float *__restrict__ coef, const float *__restrict__ w1, const float *__restrict__ w2,
     int64_t ncap, int64_t ntiles, float *__restrict__ dagg_out, float *__restrict__ slab,
-    const int32_t *__restrict__ dims, const float *__restrict__ aggx) {
+    const int32_t *__restrict__ dims, const float *__restrict__ aggx, scgib_bn_bwd_pending pend) {
     static_assert(!PRE || DIN == 32, "transfer_d fold: layer 0 only");
     const int64_t n = eff_count(dims, 0, ncap);
     constexpr int LDA = DIN + 1;
@@ -766,6 +914,10 @@ __global__ __launch_bounds__(256, (DIN <= 64 ? 2 : 1)) void gin_bwd_k(
     const int wr = w >> 1, wc = w & 1;
     SCGIB_MARK(0);
     SCGIB_MARK_HWID();
+    // this layer's deferred BN-backward sums: partial loads go out with the weights
+    BwdFin bfin;
+    const int pend_ngr = static_cast<int>(((n + TM - 1) / TM + kGroup - 1) / kGroup);
+    if (BN && pend.gpart) bn_bwd_fin_load<false>(pend.gpart, pend_ngr, 0, bfin);
     stage_weights<DIN>(w1, w2, sW1, sW2);
     const int ch = tid & 63, q = tid >> 6;  // column-sum roles: channel, row quarter
     // staging roles: 4-channel chunk c4, rows rs + 16 k
@@ -776,8 +928,22 @@ __global__ __launch_bounds__(256, (DIN <= 64 ? 2 : 1)) void gin_bwd_k(
         s_mean = ld4(stat + 4 * c4);
         s_istd = ld4(stat + 64 + 4 * c4);
         s_sc = ld4(stat + 128 + 4 * c4);
-        c1 = ld4(coef + 4 * c4);
-        c2 = ld4(coef + 64 + 4 * c4);
+        if (!pend.gpart) {
+            c1 = ld4(coef + 4 * c4);
+            c2 = ld4(coef + 64 + 4 * c4);
+        } else {  // finish the sums; workgroup 0 writes dgamma, dbeta
+            __shared__ float sCoef[128];
+            const double tot = bn_bwd_final<false>(pend.gpart, pend_ngr, bfin);
+            const int cs = bfin_index();
+            const bool lead = (tid & 63) < 32, w0 = blockIdx.x == 0 && lead;
+            const float cf = bn_bwd_publish(cs, tot, n, pend.training, w0 ? pend.dgamma : nullptr,
+                                            w0 ? pend.dbeta : nullptr, nullptr);
+            if (lead) sCoef[cs] = cf;
+            __syncthreads();
+            c1 = make_float4(sCoef[4 * c4], sCoef[4 * c4 + 1], sCoef[4 * c4 + 2], sCoef[4 * c4 + 3]);
+            c2 = make_float4(sCoef[64 + 4 * c4], sCoef[65 + 4 * c4], sCoef[66 + 4 * c4],
+                             sCoef[67 + 4 * c4]);
+        }
     }
     constexpr int NSUB1 = 2 * (DIN / 32);  // 32x32 sub-tiles of dW1 / d(agg)
     constexpr int NW1 = (NSUB1 + 3) / 4;   // per wave
@@ -936,7 +1102,7 @@ using namespace scgib;
 extern "C" int64_t scgib_gin_tiles(int64_t n_nodes) { return (n_nodes + TM - 1) / TM; }
 
 #ifdef SCGIB_TRACE
-// debug build only: buffer of [grid][8] uint64 phase stamps (see common.h)
+// debug build only: buffer of [grid][16] uint64 phase stamps (see common.h)
 extern "C" int scgib_trace_set(void *buf) {
     return hipMemcpyToSymbol(HIP_SYMBOL(g_trace), &buf, sizeof(buf)) == hipSuccess ? 0 : 1;
 }
@@ -954,15 +1120,17 @@ static int launch_gin_fwd(const float *h_in, int32_t d_in, const float *in_stat,
                           const int32_t *rowptr, const int32_t *col, int64_t n_nodes,
                           float one_plus_eps, const float *w1, const float *b1, const float *w2,
                           const float *b2, float *agg, float *r, float *z2, float *tile_stats,
-                          const int32_t *dims, const BnFwdFuse &fz, hipStream_t st) {
+                          const int32_t *dims, const BnFwdFuse &fz,
+                          const scgib_bn_pending *pend, hipStream_t st) {
     const int64_t nt = scgib_gin_tiles(n_nodes);
     const float *isc = in_stat ? in_stat + 128 : nullptr, *ish = in_stat ? in_stat + 192 : nullptr;
+    const scgib_bn_pending pd = pend ? *pend : scgib_bn_pending{};
     if (d_in == 32)
-        gin_fwd_k<32, false><<<dim3((unsigned)nt), 256, 0, st>>>(h_in, isc, ish, rowptr, col, n_nodes, one_plus_eps, w1, b1, w2, b2, agg, r, z2, tile_stats, dims, fz, PreArgs{});
-    else if (in_stat)
-        gin_fwd_k<64, true><<<dim3((unsigned)nt), 256, 0, st>>>(h_in, isc, ish, rowptr, col, n_nodes, one_plus_eps, w1, b1, w2, b2, agg, r, z2, tile_stats, dims, fz, PreArgs{});
+        gin_fwd_k<32, false><<<dim3((unsigned)nt), 256, 0, st>>>(h_in, isc, ish, rowptr, col, n_nodes, one_plus_eps, w1, b1, w2, b2, agg, r, z2, tile_stats, dims, fz, PreArgs{}, pd);
+    else if (in_stat || pend)
+        gin_fwd_k<64, true><<<dim3((unsigned)nt), 256, 0, st>>>(h_in, isc, ish, rowptr, col, n_nodes, one_plus_eps, w1, b1, w2, b2, agg, r, z2, tile_stats, dims, fz, PreArgs{}, pd);
     else
-        gin_fwd_k<64, false><<<dim3((unsigned)nt), 256, 0, st>>>(h_in, isc, ish, rowptr, col, n_nodes, one_plus_eps, w1, b1, w2, b2, agg, r, z2, tile_stats, dims, fz, PreArgs{});
+        gin_fwd_k<64, false><<<dim3((unsigned)nt), 256, 0, st>>>(h_in, isc, ish, rowptr, col, n_nodes, one_plus_eps, w1, b1, w2, b2, agg, r, z2, tile_stats, dims, fz, PreArgs{}, pd);
     return launch_status();
 }
 
@@ -990,7 +1158,7 @@ extern "C" int scgib_gin_layer_fwd(const float *h_in, int32_t d_in, const float 
     if (ok != 1) return ok;
     BnFwdFuse fz{};
     return launch_gin_fwd(h_in, d_in, in_stat, rowptr, col, n_nodes, one_plus_eps, w1, b1, w2, b2,
-                          agg, r, z2, tile_stats, dims, fz, as_stream(stream));
+                          agg, r, z2, tile_stats, dims, fz, nullptr, as_stream(stream));
 }
 
 static int64_t bn_groups(int64_t n_nodes) { return (scgib_gin_tiles(n_nodes) + kGroup - 1) / kGroup; }
@@ -1005,8 +1173,15 @@ extern "C" int64_t scgib_gin_counters(int64_t n_nodes) {
     return n_nodes <= 0 ? 0 : bn_groups(n_nodes) + 1;
 }
 
+extern "C" int64_t scgib_gin_bn_gpart_offset(int64_t n_nodes) {
+    return n_nodes <= 0 ? 0 : ((scgib_gin_tiles(n_nodes) * 128 + 1) & ~int64_t(1));
+}
+
+// 64 groups of 16 tiles: the consumers' one-round finish (bn_fwd_final)
+extern "C" int64_t scgib_gin_defer_max_nodes(void) { return int64_t(64) * kGroup * TM; }
+
 static double *bn_gpart(float *ws, int64_t n_nodes) {
-    return reinterpret_cast<double *>(ws + ((scgib_gin_tiles(n_nodes) * 128 + 1) & ~int64_t(1)));
+    return reinterpret_cast<double *>(ws + scgib_gin_bn_gpart_offset(n_nodes));
 }
 
 extern "C" int scgib_gin_layer_fwd_bn(const float *h_in, int32_t d_in, const float *in_stat,
@@ -1017,16 +1192,22 @@ extern "C" int scgib_gin_layer_fwd_bn(const float *h_in, int32_t d_in, const flo
                                       float bn_eps, float momentum, float *running_mean,
                                       float *running_var, int64_t *num_batches_tracked,
                                       float *stat, float *bn_ws, uint32_t *counters,
-                                      const int32_t *dims, scgib_stream_t stream) {
+                                      const int32_t *dims, const scgib_bn_pending *in_pending,
+                                      int32_t defer, scgib_stream_t stream) {
     const int ok = gin_fwd_args_ok(h_in, d_in, in_stat, rowptr, col, n_nodes, w1, b1, w2, b2, agg,
                                    r, z2, bn_ws);
     if (ok != 1) return ok == SCGIB_OK ? SCGIB_EINVAL : ok;  // BN needs rows
     if (!gamma || !beta || !stat || !counters || ((running_mean == nullptr) != (running_var == nullptr)))
         return SCGIB_EINVAL;
+    if (in_pending && (d_in != 64 || in_stat || !in_pending->gpart || !in_pending->gamma ||
+                       !in_pending->beta || !in_pending->stat ||
+                       ((in_pending->running_mean == nullptr) != (in_pending->running_var == nullptr))))
+        return SCGIB_EINVAL;
     BnFwdFuse fz{counters, bn_gpart(bn_ws, n_nodes), gamma, beta, running_mean, running_var,
-                 stat, num_batches_tracked, bn_eps, momentum, static_cast<int>(bn_groups(n_nodes))};
+                 stat, num_batches_tracked, bn_eps, momentum, static_cast<int>(bn_groups(n_nodes)),
+                 defer ? 1 : 0};
     return launch_gin_fwd(h_in, d_in, in_stat, rowptr, col, n_nodes, one_plus_eps, w1, b1, w2, b2,
-                          agg, r, z2, bn_ws, dims, fz, as_stream(stream));
+                          agg, r, z2, bn_ws, dims, fz, in_pending, as_stream(stream));
 }
 
 extern "C" int scgib_bn_finalize(const float *tile_stats, int64_t n_nodes, const float *gamma,
@@ -1085,13 +1266,12 @@ extern "C" int scgib_gin_bwd_stats_bn(const float *dh, const int32_t *rowptr_t,
                                       const float *stat, int64_t n_nodes, int32_t training,
                                       float *dy, float *dgamma, float *dbeta, float *coef,
                                       float *bn_ws, uint32_t *counters, const int32_t *dims,
-                                      scgib_stream_t stream) {
-    if (n_nodes <= 0 || !dh || !z2 || !stat || !dy || !dgamma || !dbeta || !coef || !bn_ws ||
-        !counters)
-        return SCGIB_EINVAL;
+                                      int32_t defer, scgib_stream_t stream) {
+    if (n_nodes <= 0 || !dh || !z2 || !stat || !dy || !bn_ws || !counters) return SCGIB_EINVAL;
+    if (!defer && (!dgamma || !dbeta || !coef)) return SCGIB_EINVAL;
     if ((rowptr_t == nullptr) != (col_t == nullptr)) return SCGIB_EINVAL;
     BnBwdFuse bz{counters, bn_gpart(bn_ws, n_nodes), dgamma, dbeta, coef, training,
-                 static_cast<int>(bn_groups(n_nodes))};
+                 static_cast<int>(bn_groups(n_nodes)), defer ? 1 : 0};
     return launch_gin_bwd_stats(dh, rowptr_t, col_t, one_plus_eps, z2, stat, n_nodes, dy, bn_ws,
                                 dims, bz, as_stream(stream));
 }
@@ -1109,17 +1289,20 @@ extern "C" int scgib_gin_layer_bwd(const float *dy, const float *z2, const float
                                    const float *agg, int32_t d_in, const float *stat,
                                    const float *coef, const float *w1, const float *w2,
                                    int64_t n_nodes, float *dagg, float *slab, float *wgrad,
-                                   const int32_t *dims, scgib_stream_t stream) {
+                                   const int32_t *dims, const scgib_bn_bwd_pending *pending,
+                                   scgib_stream_t stream) {
     if (n_nodes <= 0 || (d_in != 32 && d_in != 64)) return SCGIB_EINVAL;
-    if (!dy || !z2 || !r || !agg || !stat || !coef || !w1 || !w2 || !dagg || !slab)
+    if (!dy || !z2 || !r || !agg || !stat || (!coef && !pending) || !w1 || !w2 || !dagg || !slab)
         return SCGIB_EINVAL;
+    if (pending && (!pending->gpart || !pending->dgamma || !pending->dbeta)) return SCGIB_EINVAL;
+    const scgib_bn_bwd_pending pd = pending ? *pending : scgib_bn_bwd_pending{};
     const int64_t nt = scgib_gin_tiles(n_nodes);
     const int grid = bwd_grid(nt);
     hipStream_t st = as_stream(stream);
     if (d_in == 32)
-        gin_bwd_k<32><<<grid, 256, 0, st>>>(dy, z2, r, agg, stat, coef, w1, w2, n_nodes, nt, dagg, slab, dims, nullptr);
+        gin_bwd_k<32><<<grid, 256, 0, st>>>(dy, z2, r, agg, stat, coef, w1, w2, n_nodes, nt, dagg, slab, dims, nullptr, pd);
     else
-        gin_bwd_k<64><<<grid, 256, 0, st>>>(dy, z2, r, agg, stat, coef, w1, w2, n_nodes, nt, dagg, slab, dims, nullptr);
+        gin_bwd_k<64><<<grid, 256, 0, st>>>(dy, z2, r, agg, stat, coef, w1, w2, n_nodes, nt, dagg, slab, dims, nullptr, pd);
     const int rc = launch_status();
     if (rc != SCGIB_OK || !wgrad) return rc;  // wgrad NULL: the caller reduces the slabs
     return launch_slab_reduce(slab, grid, 64 * 64 + 64 * static_cast<int64_t>(d_in) + 128, wgrad, st);
@@ -1142,9 +1325,9 @@ extern "C" int scgib_mlp2_fwd(const float *x, int32_t d_in, int64_t n_nodes, con
     const unsigned nt = static_cast<unsigned>(scgib_gin_tiles(n_nodes));
     hipStream_t st = as_stream(stream);
     if (d_in == 128)
-        gin_fwd_k<128, false, false><<<nt, 256, 0, st>>>(x, nullptr, nullptr, nullptr, nullptr, n_nodes, 0.f, w1, b1, w2, b2, nullptr, r, out, nullptr, dims, BnFwdFuse{}, PreArgs{});
+        gin_fwd_k<128, false, false><<<nt, 256, 0, st>>>(x, nullptr, nullptr, nullptr, nullptr, n_nodes, 0.f, w1, b1, w2, b2, nullptr, r, out, nullptr, dims, BnFwdFuse{}, PreArgs{}, scgib_bn_pending{});
     else
-        gin_fwd_k<64, false, false><<<nt, 256, 0, st>>>(x, nullptr, nullptr, nullptr, nullptr, n_nodes, 0.f, w1, b1, w2, b2, nullptr, r, out, nullptr, dims, BnFwdFuse{}, PreArgs{});
+        gin_fwd_k<64, false, false><<<nt, 256, 0, st>>>(x, nullptr, nullptr, nullptr, nullptr, n_nodes, 0.f, w1, b1, w2, b2, nullptr, r, out, nullptr, dims, BnFwdFuse{}, PreArgs{}, scgib_bn_pending{});
     return launch_status();
 }
 
@@ -1158,9 +1341,9 @@ extern "C" int scgib_mlp2_bwd(const float *dout, const float *x, const float *r,
     const int grid = bwd_grid(nt);
     hipStream_t st = as_stream(stream);
     if (d_in == 128)
-        gin_bwd_k<128, false><<<grid, 256, 0, st>>>(dout, nullptr, r, x, nullptr, nullptr, w1, w2, n_nodes, nt, dx, slab, dims, nullptr);
+        gin_bwd_k<128, false><<<grid, 256, 0, st>>>(dout, nullptr, r, x, nullptr, nullptr, w1, w2, n_nodes, nt, dx, slab, dims, nullptr, scgib_bn_bwd_pending{});
     else
-        gin_bwd_k<64, false><<<grid, 256, 0, st>>>(dout, nullptr, r, x, nullptr, nullptr, w1, w2, n_nodes, nt, dx, slab, dims, nullptr);
+        gin_bwd_k<64, false><<<grid, 256, 0, st>>>(dout, nullptr, r, x, nullptr, nullptr, w1, w2, n_nodes, nt, dx, slab, dims, nullptr, scgib_bn_bwd_pending{});
     const int rc = launch_status();
     if (rc != SCGIB_OK) return rc;
     return launch_slab_reduce(slab, grid, 64 * 64 + 64 * static_cast<int64_t>(d_in) + 128, wgrad, st);
@@ -1181,7 +1364,7 @@ extern "C" int scgib_gin_layer0_fwd(const float *x, int32_t n_feat, const int32_
                                     const float *beta, float bn_eps, float momentum,
                                     float *running_mean, float *running_var,
                                     int64_t *num_batches_tracked, float *stat, float *bn_ws,
-                                    uint32_t *counters, const int32_t *dims,
+                                    uint32_t *counters, const int32_t *dims, int32_t defer,
                                     scgib_stream_t stream) {
     if (n_nodes <= 0 || n_feat < 1 || n_feat > kPreF) return n_nodes == 0 ? SCGIB_OK : SCGIB_EINVAL;
     if (!x || !wt || !rowptr || !col || !w1 || !b1 || !w2 || !b2 || !agg || !aggx || !r || !z2 ||
@@ -1193,12 +1376,12 @@ extern "C" int scgib_gin_layer0_fwd(const float *x, int32_t n_feat, const int32_
     if (counters)
         fz = BnFwdFuse{counters, bn_gpart(bn_ws, n_nodes), gamma, beta, running_mean, running_var,
                        stat, num_batches_tracked, bn_eps, momentum,
-                       static_cast<int>(bn_groups(n_nodes))};
+                       static_cast<int>(bn_groups(n_nodes)), defer ? 1 : 0};
     const PreArgs pre{x, node_map, wt, aggx, n_feat};
     const int64_t nt = scgib_gin_tiles(n_nodes);
     gin_fwd_k<32, false, true, true><<<dim3((unsigned)nt), 256, 0, as_stream(stream)>>>(
         nullptr, nullptr, nullptr, rowptr, col, n_nodes, one_plus_eps, w1, b1, w2, b2, agg, r, z2,
-        bn_ws, dims, fz, pre);
+        bn_ws, dims, fz, pre, scgib_bn_pending{});
     return launch_status();
 }
 
@@ -1206,11 +1389,14 @@ extern "C" int scgib_gin_layer0_bwd(const float *dy, const float *z2, const floa
                                     const float *agg, const float *aggx, const float *stat,
                                     const float *coef, const float *w1, const float *w2,
                                     int64_t n_nodes, float *slab, const int32_t *dims,
-                                    scgib_stream_t stream) {
-    if (n_nodes <= 0 || !dy || !z2 || !r || !agg || !aggx || !stat || !coef || !w1 || !w2 || !slab)
+                                    const scgib_bn_bwd_pending *pending, scgib_stream_t stream) {
+    if (n_nodes <= 0 || !dy || !z2 || !r || !agg || !aggx || !stat || (!coef && !pending) || !w1 ||
+        !w2 || !slab)
         return SCGIB_EINVAL;
+    if (pending && (!pending->gpart || !pending->dgamma || !pending->dbeta)) return SCGIB_EINVAL;
+    const scgib_bn_bwd_pending pd = pending ? *pending : scgib_bn_bwd_pending{};
     const int64_t nt = scgib_gin_tiles(n_nodes);
     gin_bwd_k<32, true, true><<<bwd_grid(nt), 256, 0, as_stream(stream)>>>(
-        dy, z2, r, agg, stat, coef, w1, w2, n_nodes, nt, nullptr, slab, dims, aggx);
+        dy, z2, r, agg, stat, coef, w1, w2, n_nodes, nt, nullptr, slab, dims, aggx, pd);
     return launch_status();
 }

@@ -76,6 +76,71 @@ __device__ __forceinline__ float4 fma4(float4 a, float w, float4 acc) {
                        fmaf(a.w, w, acc.w));
 }
 
+template <int RPT>
+struct GatherHead {  // per-row CSR range and self row, loaded up front
+    int32_t beg[RPT], deg[RPT];
+    float4 self[RPT];
+};
+
+// first load round of gather_rows (row pointers and self rows); split out so
+// a caller can put other independent loads in flight before the tail waits
+template <int RPT, int RPP, int LPR>
+__device__ __forceinline__ void gather_head(const float4 *__restrict__ h4,
+                                            const int32_t *__restrict__ rowptr, int64_t row0,
+                                            int nv, int rbase, int c, GatherHead<RPT> &hd) {
+#pragma unroll
+    for (int k = 0; k < RPT; ++k) {
+        const int rr = rbase + k * RPP;
+        const int64_t vrow = row0 + (rr < nv ? rr : nv - 1);
+        hd.beg[k] = rowptr[vrow];
+        hd.deg[k] = rowptr[vrow + 1];
+        hd.self[k] = h4[vrow * LPR + c];
+    }
+}
+
+template <int RPT, int LPR, bool XFORM>
+__device__ __forceinline__ void gather_tail(const float4 *__restrict__ h4,
+                                            const int32_t *__restrict__ col, GatherHead<RPT> &hd,
+                                            int c, float ope, float4 sc, float4 sh,
+                                            float4 (&acc)[RPT]) {
+    int maxdeg = 0, maxend = 0;
+#pragma unroll
+    for (int k = 0; k < RPT; ++k) {
+        acc[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+        maxend = hd.deg[k] > maxend ? hd.deg[k] : maxend;
+        hd.deg[k] -= hd.beg[k];
+        maxdeg = hd.deg[k] > maxdeg ? hd.deg[k] : maxdeg;
+    }
+    for (int j0 = 0; j0 < maxdeg; j0 += 4) {
+        int32_t u[RPT][4];
+#pragma unroll
+        for (int k = 0; k < RPT; ++k)
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                const int32_t e = hd.beg[k] + j0 + t;
+                u[k][t] = col[e < maxend ? e : maxend - 1];
+            }
+        float4 a[RPT][4];
+#pragma unroll
+        for (int k = 0; k < RPT; ++k)
+#pragma unroll
+            for (int t = 0; t < 4; ++t) a[k][t] = h4[static_cast<int64_t>(u[k][t]) * LPR + c];
+#pragma unroll
+        for (int k = 0; k < RPT; ++k)
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                const float w = j0 + t < hd.deg[k] ? 1.f : 0.f;
+                acc[k] = fma4(XFORM ? xform4(a[k][t], sc, sh) : a[k][t], w, acc[k]);
+            }
+    }
+#pragma unroll
+    for (int k = 0; k < RPT; ++k) {
+        const float4 x = XFORM ? xform4(hd.self[k], sc, sh) : hd.self[k];
+        acc[k] = make_float4(ope * x.x + acc[k].x, ope * x.y + acc[k].y, ope * x.z + acc[k].z,
+                             ope * x.w + acc[k].w);
+    }
+}
+
 // Sum aggregation of RPT rows (row0 + rbase + k * RPP) for one 4-channel
 // chunk c: out = ope * x[v] + sum_{u in N(v)} x[u] in CSR order, x optionally
 // relu(sc * h + sh).  Requires nv >= 1.
@@ -94,53 +159,9 @@ __device__ __forceinline__ void gather_rows(const float4 *__restrict__ h4,
                                             const int32_t *__restrict__ col, int64_t row0, int nv,
                                             int rbase, int c, float ope, float4 sc, float4 sh,
                                             float4 (&acc)[RPT]) {
-    int32_t beg[RPT], deg[RPT];
-    float4 self[RPT];
-    int64_t vrow[RPT];
-#pragma unroll
-    for (int k = 0; k < RPT; ++k) {
-        const int rr = rbase + k * RPP;
-        vrow[k] = row0 + (rr < nv ? rr : nv - 1);
-        beg[k] = rowptr[vrow[k]];
-        deg[k] = rowptr[vrow[k] + 1];
-        self[k] = h4[vrow[k] * LPR + c];
-        acc[k] = make_float4(0.f, 0.f, 0.f, 0.f);
-    }
-    int maxdeg = 0, maxend = 0;
-#pragma unroll
-    for (int k = 0; k < RPT; ++k) {
-        maxend = deg[k] > maxend ? deg[k] : maxend;
-        deg[k] -= beg[k];
-        maxdeg = deg[k] > maxdeg ? deg[k] : maxdeg;
-    }
-    for (int j0 = 0; j0 < maxdeg; j0 += 4) {
-        int32_t u[RPT][4];
-#pragma unroll
-        for (int k = 0; k < RPT; ++k)
-#pragma unroll
-            for (int t = 0; t < 4; ++t) {
-                const int32_t e = beg[k] + j0 + t;
-                u[k][t] = col[e < maxend ? e : maxend - 1];
-            }
-        float4 a[RPT][4];
-#pragma unroll
-        for (int k = 0; k < RPT; ++k)
-#pragma unroll
-            for (int t = 0; t < 4; ++t) a[k][t] = h4[static_cast<int64_t>(u[k][t]) * LPR + c];
-#pragma unroll
-        for (int k = 0; k < RPT; ++k)
-#pragma unroll
-            for (int t = 0; t < 4; ++t) {
-                const float w = j0 + t < deg[k] ? 1.f : 0.f;
-                acc[k] = fma4(XFORM ? xform4(a[k][t], sc, sh) : a[k][t], w, acc[k]);
-            }
-    }
-#pragma unroll
-    for (int k = 0; k < RPT; ++k) {
-        const float4 x = XFORM ? xform4(self[k], sc, sh) : self[k];
-        acc[k] = make_float4(ope * x.x + acc[k].x, ope * x.y + acc[k].y, ope * x.z + acc[k].z,
-                             ope * x.w + acc[k].w);
-    }
+    GatherHead<RPT> hd;
+    gather_head<RPT, RPP, LPR>(h4, rowptr, row0, nv, rbase, c, hd);
+    gather_tail<RPT, LPR, XFORM>(h4, col, hd, c, ope, sc, sh, acc);
 }
 
 // C(i, j) += sum_k A(i, k) B(k, j) over K, 32x32 tile, with

@@ -7,6 +7,7 @@ stream semantics apply) and raises ``ScgibError`` on any non-zero status.
 from __future__ import annotations
 
 import ctypes
+import os
 
 import numpy as np
 import torch
@@ -34,6 +35,9 @@ def _launch(name, meta, *args):
 # from the current one, joined back by join_aside() (models call it at the
 # end of forward, so captured graphs stay closed).
 _AUX_STREAMS = {}
+# deferred BatchNorm finalize in the fused GIN layers (scgib_bn_pending)
+DEFER_BN = os.environ.get("SCGIB_DEFER_BN", "1") != "0"
+DEFER_BN_FWD = os.environ.get("SCGIB_DEFER_BN_FWD", "1") != "0"
 _AUX_PENDING = set()
 
 
@@ -62,6 +66,12 @@ def join_aside():
 
 def _p(t):
     return ctypes.c_void_p(t.data_ptr()) if t is not None else _NULL
+
+
+def _byref(st):
+    """Pointer argument for a ctypes Structure (None -> NULL); the C side
+    copies it into the kernel arguments before returning."""
+    return ctypes.cast(ctypes.pointer(st), ctypes.c_void_p) if st is not None else _NULL
 
 
 def _stream():
@@ -147,11 +157,17 @@ class _GinEncoder(torch.autograd.Function):
         # training: BN finalize folded into the layer kernel (one counter set
         # per encoder module: the two encoders run on concurrent streams)
         fused = training and n > 0
-        bn_ws = torch.empty(max(int(_lib.query("scgib_gin_bn_ws_floats", n)), 1),
-                            dtype=torch.float32, device=dev)
+        # deferred BN finalize (scgib_bn_pending): layer l leaves its statistics
+        # as group partials and layer l + 1 finishes them (not the last layer)
+        defer_ok = fused and DEFER_BN and DEFER_BN_FWD and \
+            n <= int(_lib.query("scgib_gin_defer_max_nodes"))
+        ws_floats = max(int(_lib.query("scgib_gin_bn_ws_floats", n)), 1)
+        bn_wss = [torch.empty(ws_floats, dtype=torch.float32, device=dev)
+                  for _ in range(2 if defer_ok else 1)]
+        gpart_off = 4 * int(_lib.query("scgib_gin_bn_gpart_offset", n))
         cnt = counters(dev, ("gin", id(gin)), int(_lib.query("scgib_gin_counters", n))) \
             if fused else None
-        saved, h, stat_prev, aggx = [], h0, None, None
+        saved, h, stat_prev, aggx, pend = [], h0, None, None, None
         for l in range(L):
             conv, bn = gin.ginlayers[l], gin.batch_norms[l]
             w1, b1, w2, b2, gamma, beta = (_f32(p, "gin param") for p in params[6 * l: 6 * l + 6])
@@ -169,19 +185,22 @@ class _GinEncoder(torch.autograd.Function):
             rm = _p(bn.running_mean) if track else None
             rv = _p(bn.running_var) if track else None
             nbt = _p(bn.num_batches_tracked) if track else None
+            bn_ws = bn_wss[l % len(bn_wss)]
+            defer = int(defer_ok and l < L - 1)
             if pre and l == 0:
                 aggx = torch.empty(n, 16, dtype=torch.float32, device=dev)
                 _launch("scgib_gin_layer0_fwd", meta, _p(x), x.shape[1], _p(nmap), _p(wt),
                         _p(graph.rowptr), _p(graph.col), n, conv._one_plus_eps, _p(w1), _p(b1),
                         _p(w2), _p(b2), _p(agg), _p(aggx), _p(r), _p(z2), _p(gamma), _p(beta),
                         float(bn.eps), momentum, rm, rv, nbt, _p(stat), _p(bn_ws), _p(cnt),
-                        _p(graph.dims), st)
+                        _p(graph.dims), defer, st)
             elif fused:
-                _launch("scgib_gin_layer_fwd_bn", meta, _p(h), d_in, _p(stat_prev),
+                _launch("scgib_gin_layer_fwd_bn", meta, _p(h), d_in,
+                        None if pend is not None else _p(stat_prev),
                         _p(graph.rowptr), _p(graph.col), n, conv._one_plus_eps, _p(w1), _p(b1),
                         _p(w2), _p(b2), _p(agg), _p(r), _p(z2), _p(gamma), _p(beta),
                         float(bn.eps), momentum, rm, rv, nbt, _p(stat), _p(bn_ws), _p(cnt),
-                        _p(graph.dims), st)
+                        _p(graph.dims), _byref(pend), defer, st)
             else:
                 _launch("scgib_gin_layer_fwd", meta, _p(h), d_in, _p(stat_prev),
                         _p(graph.rowptr), _p(graph.col), n, conv._one_plus_eps, _p(w1), _p(b1),
@@ -195,6 +214,12 @@ class _GinEncoder(torch.autograd.Function):
                           nbt, _p(stat), _p(graph.dims), st)
             saved += [agg, r, z2, stat]
             h, stat_prev = z2, stat
+            pend = _lib.BnPending(
+                bn_ws.data_ptr() + gpart_off, gamma.data_ptr(), beta.data_ptr(),
+                bn.running_mean.data_ptr() if track else None,
+                bn.running_var.data_ptr() if track else None,
+                bn.num_batches_tracked.data_ptr() if track else None,
+                stat.data_ptr(), float(bn.eps), momentum) if defer else None
         out = torch.empty(n, HIDDEN, dtype=torch.float32, device=dev)
         _lib.call("scgib_bn_relu_apply", _p(h), _p(stat_prev), n, _p(out), _p(graph.dims), st)
         ctx.save_for_backward(*saved, *params, *( (aggx,) if pre else ()))
@@ -217,6 +242,9 @@ class _GinEncoder(torch.autograd.Function):
         bn_ws = torch.empty(int(_lib.query("scgib_gin_bn_ws_floats", n)), dtype=torch.float32,
                             device=dev)
         cnt = counters(dev, ctx.cnt_key, int(_lib.query("scgib_gin_counters", n)))
+        # deferred BN-backward finalize: each layer's gin_bwd_k finishes the sums
+        defer = int(DEFER_BN and n <= int(_lib.query("scgib_gin_defer_max_nodes")))
+        gpart = bn_ws.data_ptr() + 4 * int(_lib.query("scgib_gin_bn_gpart_offset", n))
         grads = [None] * (6 * L)
         dagg_next, dwt = None, None
         nslab = int(_lib.query("scgib_gin_bwd_slabs", n))
@@ -231,19 +259,22 @@ class _GinEncoder(torch.autograd.Function):
             if dagg_next is None:
                 _launch("scgib_gin_bwd_stats_bn", {"n": n}, _p(g_out), None, None, 1.0, _p(z2),
                           _p(stat), n, int(ctx.training), _p(dy), _p(bn_g[0]), _p(bn_g[1]),
-                          _p(coef), _p(bn_ws), _p(cnt), _p(gr.dims), st)
+                          _p(coef), _p(bn_ws), _p(cnt), _p(gr.dims), defer, st)
             else:
                 _launch("scgib_gin_bwd_stats_bn", {"n": n}, _p(dagg_next), _p(gr.rowptr_t),
                           _p(gr.col_t), ctx.opes[l + 1], _p(z2), _p(stat), n, int(ctx.training),
                           _p(dy), _p(bn_g[0]), _p(bn_g[1]), _p(coef), _p(bn_ws), _p(cnt),
-                          _p(gr.dims), st)
+                          _p(gr.dims), defer, st)
+            bpend = _lib.BnBwdPending(gpart, bn_g[0].data_ptr(), bn_g[1].data_ptr(),
+                                      int(ctx.training)) if defer else None
             meta = {"n": n, "e": gr.edge_capacity(), "d_in": d_in}
             w1c, w2c = _f32(w1, "w1"), _f32(w2, "w2")
             if pre and l == 0:
                 width = int(_lib.query("scgib_gin_layer0_slab_width"))
                 slab = torch.empty(nslab * width, dtype=torch.float32, device=dev)
                 _launch("scgib_gin_layer0_bwd", meta, _p(dy), _p(z2), _p(r), _p(agg), _p(aggx),
-                        _p(stat), _p(coef), _p(w1c), _p(w2c), n, _p(slab), _p(gr.dims), st)
+                        _p(stat), _p(coef), _p(w1c), _p(w2c), n, _p(slab), _p(gr.dims),
+                        _byref(bpend), st)
                 dagg = None
             else:
                 width = HIDDEN * HIDDEN + HIDDEN * d_in + 2 * HIDDEN
@@ -252,7 +283,7 @@ class _GinEncoder(torch.autograd.Function):
                 dagg = torch.empty(n, d_in, dtype=torch.float32, device=dev)
                 _launch("scgib_gin_layer_bwd", meta, _p(dy), _p(z2), _p(r), _p(agg), d_in,
                         _p(stat), _p(coef), _p(w1c), _p(w2c), n, _p(dagg), _p(slab), _NULL,
-                        _p(gr.dims), st)
+                        _p(gr.dims), _byref(bpend), st)
             wgrad = torch.empty(width, dtype=torch.float32, device=dev)
             _lib.call("scgib_slab_reduce", _p(slab), nslab, width, _p(wgrad), st)
             o = HIDDEN * HIDDEN

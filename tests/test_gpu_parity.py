@@ -555,3 +555,47 @@ def test_gin_encoder_transfer_fold_small_exact(pkg, dev, via_ego):
     h, _, h64, gw, _, gw64, _, _ = _fold_case(pkg, dev, 3, True, via_ego, seed=3)
     assert rel_l2(h.detach().cpu(), h64.detach()) < 1e-5
     assert rel_l2(gw.cpu(), gw64) < 1e-5
+
+
+@pytest.mark.parametrize("via_ego,n_mols", [(False, 40), (True, 200)])
+def test_gin_encoder_deferred_bn_bitwise(pkg, dev, via_ego, n_mols):
+    """Deferred BatchNorm finalize (scgib_bn_pending: the next kernel finishes
+    a layer's statistics) against the in-kernel last-arriver finalize: both
+    run the same fixed-order combine, so outputs, every gradient and the BN
+    running statistics are bitwise identical; n_mols = 200 ego-nets spans
+    several 16-tile groups with a partial last group."""
+    import copy
+    torch.manual_seed(5)
+    g, _ = rand_graph(pkg, n_mols, "qm9", 12, dev)
+    x = F.normalize(torch.rand(g.num_nodes(), 11)).to(dev)
+    lin = torch.nn.Linear(11, 32, bias=False).to(dev)
+    gin = pkg.models.GIN(32, 64, 5).to(dev).train()
+    with torch.no_grad():
+        for bn in gin.batch_norms:
+            bn.weight.add_(0.2 * torch.randn(64, device=dev))
+    if via_ego:
+        target = pkg.graph.egonet_batch(g, 1)
+        nmap = target.ndata["_ID"]
+    else:
+        target, nmap = g, None
+    w = torch.randn(target.num_nodes(), 64, device=dev)
+    outs = []
+    for defer in (True, False):
+        gin_c, lin_c = copy.deepcopy(gin), copy.deepcopy(lin)
+        old = pkg.ops.DEFER_BN, pkg.ops.DEFER_BN_FWD
+        pkg.ops.DEFER_BN = pkg.ops.DEFER_BN_FWD = defer
+        try:
+            h = pkg.ops.gin_encoder_x(x, target, gin_c, lin_c, nmap)
+            (h * w).sum().backward()
+        finally:
+            pkg.ops.DEFER_BN, pkg.ops.DEFER_BN_FWD = old
+        torch.cuda.synchronize()
+        outs.append((h.detach(), {k: p.grad for k, p in list(gin_c.named_parameters())
+                                  + [("wt", lin_c.weight)]},
+                     {k: b.clone() for k, b in gin_c.named_buffers()}))
+    (ha, ga, ba), (hb, gb, bb) = outs
+    assert torch.equal(ha, hb)
+    for k in ga:
+        assert torch.equal(ga[k], gb[k]), k
+    for k in ba:
+        assert torch.equal(ba[k], bb[k]), k

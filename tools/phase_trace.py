@@ -5,7 +5,7 @@
 
 Runs one eager pretrain step of the bench workload on one stream; every
 launch routed through ops._launch is synchronised and its [grid][8] wall-clock
-stamps (100 MHz, common.h SCGIB_MARK) are summarised: kernel span, spread of
+stamps (100 MHz, common.h SCGIB_MARK; [grid][16]) are summarised: kernel span, spread of
 workgroup start times, and per-phase durations (median / p90 / max, us).
 """
 import ctypes
@@ -36,7 +36,7 @@ def main():
     dev = torch.device("cuda", 0)
     torch.manual_seed(1234)
     lib = pkg._lib.load()
-    buf = torch.zeros(MAXB * 8, dtype=torch.int64, device=dev)
+    buf = torch.zeros(MAXB * 16, dtype=torch.int64, device=dev)
     lib.scgib_trace_set.argtypes = [ctypes.c_void_p]
     assert lib.scgib_trace_set(ctypes.c_void_p(buf.data_ptr())) == 0
     F_in = pkg.synth.WORKLOADS["qm9"][2]
@@ -55,7 +55,7 @@ def main():
         buf.zero_()
         out = launch()
         torch.cuda.synchronize()
-        recs.append((name, meta, buf.view(MAXB, 8).cpu().numpy().copy()))
+        recs.append((name, meta, buf.view(MAXB, 16).cpu().numpy().copy()))
         return out
 
     for it in range(2):  # second iteration: warm caches / allocator
@@ -73,7 +73,7 @@ def main():
         t0 = start.min()
         ends = np.where(t[:, 1:1 + len(ph)] != 0, t[:, 1:1 + len(ph)], 0)
         last = ends.max()
-        hw = t[:, 7]
+        hw = t[:, 15]
         xcc = (hw >> 32) & 0xF
         cu = (hw >> 8) & 0xF
         se = (hw >> 13) & 0x7
@@ -93,6 +93,14 @@ def main():
             print(f"    {pname:10s} n={ok.sum():4d} p50={np.percentile(d, 50):6.2f} "
                   f"p90={np.percentile(d, 90):6.2f} max={d.max():6.2f} us")
             prev = np.where(ok, col, prev)
+        if name == "scgib_gin_layer_fwd_bn" and (t[:, 6] != 0).any():
+            d = (t[:, 6] - start) / 100.0
+            print(f"    (finish prev BN: start->mark6 p50={np.percentile(d, 50):.2f} "
+                  f"p90={np.percentile(d, 90):.2f} max={d.max():.2f} us)")
+            if os.environ.get("FIN_MARKS"):  # debug build with marks 4/5 around the combine
+                for a_, b_, lab in ((0, 8, "start->fin"), (8, 9, "fin compute"), (9, 6, "barrier")):
+                    d = (t[:, b_] - t[:, a_]) / 100.0
+                    print(f"      {lab}: p50={np.percentile(d, 50):.2f} p90={np.percentile(d, 90):.2f}")
         per_cu = {}
         for i in range(nb):
             per_cu.setdefault((xcc[i], se[i], sh[i], cu[i]), []).append(i)

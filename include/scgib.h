@@ -192,7 +192,9 @@ int scgib_gin_layer_bwd(const float *dy, const float *z2, const float *r, const 
 
 /* ---- A6: per-segment readouts (dgl.sum_nodes) -------------------------------
  * out[s,:] = sum_{i in [ptr[s], ptr[s+1])} x[i,:]   (models.py:716, 725, 733)
- * segment_broadcast is its adjoint: out[i,:] = g[s,:] for every row i of s. */
+ * segment_broadcast is its adjoint: out[i,:] = g[s,:] for every row i of s.
+ * dim: any >= 1 (float4 lanes when dim is 4 x a power of two <= 256, else a
+ * scalar kernel, e.g. for raw node features). */
 int scgib_segment_sum(const float *x, const int32_t *ptr, int64_t n_seg, int32_t dim,
                       float *out, const int32_t *dims, scgib_stream_t stream);
 /* n_rows: rows of `out` (rows past ptr[actual n_seg] are zeroed in capacity mode) */

@@ -348,6 +348,101 @@ def gen_finetune_golden(models, util_mod, name, *, workload, F, B, k, dataset, n
           f"trainable={len(trainable)}")
 
 
+def gen_domainadapt_golden(models, util_mod, name, *, workload, F, B, k, num_classes, seed,
+                           then_finetune=False):
+    """Mainmodel_domainadapt (models.py:107-355) on a pretrained
+    Mainmodel_continue, as run_domain_adaptation drives it (exp_molhiv.py:50-68,
+    train_molhiv.py:74-105): X loss and the gradients of every parameter, with
+    recorded noise.  then_finetune: Mainmodel_finetuning on that adapted model
+    (exp_molhiv.py:129-157 loads the DA model), whose extract_features is the
+    DA model's OWN (models.py:283) — scores, loss and gradients."""
+    torch.manual_seed(seed)
+    mols = synth.molecules(B, workload, seed=seed, mu=12.0, sigma=4.0, F=F)
+    graphs, subgraphs = [], []
+    for ei, x in mols:
+        g = util_mod.load_dgl_fromPyG(SimpleNamespace(edge_index=torch.from_numpy(ei),
+                                                      x=torch.from_numpy(x)))
+        graphs.append(g)
+        subgraphs.append([D.khop_in_subgraph(g, v, k=k)[0] for v in g.nodes()])
+    batch_g = D.batch(graphs)
+    ego_g = D.batch(list(chain.from_iterable(subgraphs)))
+    batch_x = F_normalize(batch_g.ndata["x"].float())                 # train_molhiv.py:91
+    x_subs = F_normalize(ego_g.ndata["x"].float())                    # :92
+    args = SimpleNamespace(recons_type="adj", useAtt=1, readout_f="sum", d_transfer=32,
+                           device="cpu", batch_size=B, task="graph_classification",
+                           dataset="ogbg-molhiv")
+    inner = models.Mainmodel(args, F, hidden_dim=64, num_layers=4, num_heads=4,
+                             k_transition=k, encoder="GIN")
+    real_load = models.torch.load
+    try:
+        models.torch.load = lambda *a, **kw: inner  # in-memory: nothing is unpickled
+        pre = models.Mainmodel_continue(args, F, hidden_dim=64, num_layers=4, num_heads=4,
+                                        k_transition=k, num_classes=num_classes,
+                                        cp_filename="<mem>", encoder="GIN")
+        models.torch.load = lambda *a, **kw: pre
+        da = models.Mainmodel_domainadapt(args, F, hidden_dim=64, num_layers=4, num_heads=4,
+                                          k_transition=k, num_classes=num_classes,
+                                          cp_filename="<mem>", encoder="GIN")
+        model = da
+        if then_finetune:
+            models.torch.load = lambda *a, **kw: da
+            model = models.Mainmodel_finetuning(args, F, hidden_dim=64, num_layers=4,
+                                                num_heads=4, k_transition=k,
+                                                num_classes=num_classes, cp_filename="<mem>",
+                                                encoder="GIN")
+    finally:
+        models.torch.load = real_load
+    model.train()
+    with torch.no_grad():
+        for n_, p_ in model.named_parameters():
+            if "batch_norms" in n_ or "compressor.1" in n_:
+                p_.add_(0.1 * torch.randn_like(p_))
+    state0 = {kk: v.detach().clone() for kk, v in model.state_dict().items()}
+    trainable = [kk for kk, p in model.named_parameters() if p.requires_grad]
+    targets = torch.randint(0, 2, (B, 1)).float()
+    torch.manual_seed(seed + 1000)
+    with _NoiseRecorder() as rec:
+        if then_finetune:
+            scores, *_ = model.forward(batch_g, batch_x, ego_g, x_subs, 1, batch_g.edges(), 2,
+                                       "cpu", B)
+            loss = model.loss(scores, targets)
+        else:
+            loss = model.forward(batch_g, batch_x, ego_g, None, x_subs, 1, batch_g.edges(), 2,
+                                 "cpu", B)
+            scores = None
+    loss.backward()
+    draws = rec.draws
+    assert len(draws) == 2 * B, len(draws)
+    u_gate = torch.cat([draws[2 * i].reshape(-1) for i in range(B)])
+    u_feat = torch.cat([draws[2 * i + 1] for i in range(B)])
+    out = {
+        "B": np.array(B), "k": np.array(k), "F": np.array(F),
+        "num_classes": np.array(num_classes), "then_finetune": np.array(int(then_finetune)),
+        "batch_num_nodes": batch_g.batch_num_nodes().numpy(),
+        "src": batch_g.src.numpy(), "dst": batch_g.dst.numpy(),
+        "x_raw": batch_g.ndata["x"].numpy(),
+        "ego_batch_num_nodes": ego_g.batch_num_nodes().numpy(),
+        "ego_src": ego_g.src.numpy(), "ego_dst": ego_g.dst.numpy(),
+        "u_gate": u_gate.numpy(), "u_feat": u_feat.numpy(),
+        "targets": targets.numpy(), "loss": loss.detach().numpy(),
+        "trainable": np.array(trainable),
+    }
+    if scores is not None:
+        out["scores"] = scores.detach().numpy()
+    gptr = np.concatenate([[0], np.cumsum(out["batch_num_nodes"])])
+    node_graph = np.repeat(np.arange(B), out["batch_num_nodes"])
+    ego_owner = np.repeat(np.arange(len(out["ego_batch_num_nodes"])), out["ego_batch_num_nodes"])
+    out["ego_nodes_global"] = ego_g.ndata["_ID"].numpy() + gptr[node_graph[ego_owner]]
+    for kk, v in state0.items():
+        out["param_" + kk] = v.numpy()
+    for kk, p in model.named_parameters():
+        if p.grad is not None:
+            out["grad_" + kk] = p.grad.numpy()
+    np.savez_compressed(os.path.join(OUT, f"{name}.npz"), **out)
+    print(f"wrote {name}.npz  N={len(out['x_raw'])} loss={loss.item():.6g} "
+          f"trainable={len(trainable)} grads={sum(1 for k_ in out if k_.startswith('grad_'))}")
+
+
 def F_normalize(x):
     return F.normalize(x)
 
@@ -356,6 +451,9 @@ def main():
     os.makedirs(OUT, exist_ok=True)
     models = refshim.import_reference_models()
     import util  # the reference's util.py (behind the same shim)
+    if sys.argv[1:] == ["domainadapt"]:  # only the domain-adaptation goldens
+        gen_domain_adaptation(models, util)
+        return
     gen_ingest_and_ego(util)
     common = dict(B=8, chunk=4)
     gen_model_golden(models, util, "pretrain_L4_k1_qm9", workload="qm9", F=11, L=4, k=1,
@@ -374,6 +472,15 @@ def main():
                         k=1, dataset="Mutagenicity", num_classes=2, loss_kind="ce", seed=4)
     gen_finetune_golden(models, util, "finetune_molhiv_bce", workload="molhiv", F=9, B=8, k=1,
                         dataset="ogbg-molhiv", num_classes=1, loss_kind="bce", seed=5)
+    gen_domain_adaptation(models, util)
+
+
+def gen_domain_adaptation(models, util):
+    # domain adaptation: molhiv, k = 1 as in exp_molhiv.py
+    gen_domainadapt_golden(models, util, "domainadapt_molhiv", workload="molhiv", F=9, B=8, k=1,
+                           num_classes=1, seed=7)
+    gen_domainadapt_golden(models, util, "finetune_after_da_molhiv", workload="molhiv", F=9, B=8,
+                           k=1, num_classes=1, seed=8, then_finetune=True)
 
 
 if __name__ == "__main__":

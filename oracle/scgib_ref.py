@@ -254,6 +254,25 @@ def set2set(p, prefix, feat, counts, n_iters=2):
     return q_star
 
 
+def domainadapt_forward(p, batch, ego, x, x_subs, u_gate, u_feat, buffers=None):
+    """Mainmodel_domainadapt.forward (models.py:256-275): own transfer_d -> the
+    pretrained model's extract_features ("model." prefix: a Mainmodel_continue
+    runs its wrapper-level encoders) -> own MLP -> Set2Set -> r_transfer_d,
+    against s2s_rev(raw normalised features); loss_X = sum of squared
+    differences (models.py:277-282)."""
+    h0 = _linear(x, p, "transfer_d", bias=False)
+    hs0 = _linear(x_subs, p, "transfer_d", bias=False)
+    pre = {k[6:]: v for k, v in p.items() if k.startswith("model.")}
+    bufs = None if buffers is None else {k[6:]: v for k, v in buffers.items()
+                                         if k.startswith("model.")}
+    acts = extract_features(pre, batch, ego, h0, hs0, u_gate, u_feat, bufs)
+    im = _linear(F.relu(_linear(acts["interaction_map"], p, "MLP.0")), p, "MLP.2")
+    g = set2set(p, "s2s", im, batch["counts"])
+    rec = _linear(F.relu(_linear(g, p, "r_transfer_d.0")), p, "r_transfer_d.2")
+    org = set2set(p, "s2s_rev", x, batch["counts"])
+    return torch.sum((rec - org) ** 2)
+
+
 def finetune_forward(p, batch, ego, x, x_subs, u_gate, u_feat, dataset, buffers=None):
     """Mainmodel_finetuning.forward: own transfer_d -> the pretrained model's
     extract_features (its wrapper-level encoders, "model." prefix) -> own MLP

@@ -99,6 +99,45 @@ __global__ __launch_bounds__(256) void segment_broadcast_k(const float4 *__restr
     for (int64_t i = ptr[s]; i < ptr[s + 1]; ++i) out[i * LPR + c] = val;
 }
 
+// Widths that are not a power-of-two multiple of 4 (e.g. the raw 9- or
+// 11-wide node features the domain-adaptation Set2Set reads, models.py:114,
+// :273): one thread per (segment, column), rows in order — same fixed-order
+// sums, scalar loads (off the hot path).
+__global__ __launch_bounds__(256) void segment_sum_scalar_k(const float *__restrict__ x,
+                                                            const int32_t *__restrict__ ptr,
+                                                            int64_t nseg, int32_t dim,
+                                                            float *__restrict__ out,
+                                                            const int32_t *__restrict__ dims) {
+    const int64_t t = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
+    if (t >= nseg * dim) return;
+    const int64_t s = t / dim, c = t % dim;
+    if (s >= eff_count(dims, 0, nseg)) {
+        out[t] = 0.f;
+        return;
+    }
+    float acc = 0.f;
+    for (int64_t i = ptr[s]; i < ptr[s + 1]; ++i) acc += x[i * dim + c];
+    out[t] = acc;
+}
+
+__global__ __launch_bounds__(256) void segment_broadcast_scalar_k(
+    const float *__restrict__ g, const int32_t *__restrict__ ptr, int64_t nseg, int32_t dim,
+    float *__restrict__ out, int64_t nrows, const int32_t *__restrict__ dims) {
+    const int64_t t = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
+    if (t >= nrows * dim) return;
+    const int64_t r = t / dim, c = t % dim, ns = eff_count(dims, 0, nseg);
+    if (r >= ptr[ns]) {  // capacity-mode padding rows
+        out[t] = 0.f;
+        return;
+    }
+    int64_t lo = 0, hi = ns;  // segment of row r: ptr[s] <= r < ptr[s + 1]
+    while (hi - lo > 1) {
+        const int64_t mid = (lo + hi) / 2;
+        if (ptr[mid] <= r) lo = mid;
+        else hi = mid;
+    }
+    out[t] = g[lo * dim + c];
+}
 
 #define SCGIB_DISPATCH_LPR(dim, KERNEL, GRID_ROWS, ...)                                    \
     do {                                                                                    \
@@ -144,10 +183,16 @@ extern "C" int scgib_gin_aggregate(const float *h, const int32_t *rowptr, const 
 extern "C" int scgib_segment_sum(const float *x, const int32_t *ptr, int64_t n_seg,
                                  int32_t dim, float *out, const int32_t *dims,
                                  scgib_stream_t stream) {
-    if (n_seg < 0 || !dim_ok(dim)) return SCGIB_EINVAL;
+    if (n_seg < 0 || dim < 1) return SCGIB_EINVAL;
     if (n_seg == 0) return SCGIB_OK;
     if (!x || !ptr || !out) return SCGIB_EINVAL;
     hipStream_t st = as_stream(stream);
+    if (!dim_ok(dim)) {
+        const int64_t tot = n_seg * dim;
+        segment_sum_scalar_k<<<dim3((unsigned)((tot + 255) / 256)), 256, 0, st>>>(
+            x, ptr, n_seg, dim, out, dims);
+        return launch_status();
+    }
     SCGIB_DISPATCH_LPR(dim, segment_sum_k, n_seg, reinterpret_cast<const float4 *>(x), ptr,
                        n_seg, reinterpret_cast<float4 *>(out), dims);
     return launch_status();
@@ -156,10 +201,17 @@ extern "C" int scgib_segment_sum(const float *x, const int32_t *ptr, int64_t n_s
 extern "C" int scgib_segment_broadcast(const float *g, const int32_t *ptr, int64_t n_seg,
                                        int32_t dim, float *out, int64_t n_rows,
                                        const int32_t *dims, scgib_stream_t stream) {
-    if (n_seg < 0 || n_rows < 0 || !dim_ok(dim)) return SCGIB_EINVAL;
+    if (n_seg < 0 || n_rows < 0 || dim < 1) return SCGIB_EINVAL;
     if (n_seg == 0) return SCGIB_OK;
     if (!g || !ptr || !out) return SCGIB_EINVAL;
     hipStream_t st = as_stream(stream);
+    if (!dim_ok(dim)) {
+        const int64_t tot = n_rows * dim;
+        if (tot > 0)
+            segment_broadcast_scalar_k<<<dim3((unsigned)((tot + 255) / 256)), 256, 0, st>>>(
+                g, ptr, n_seg, dim, out, n_rows, dims);
+        return launch_status();
+    }
     SCGIB_DISPATCH_LPR(dim, segment_broadcast_k, n_seg, reinterpret_cast<const float4 *>(g),
                        ptr, n_seg, reinterpret_cast<float4 *>(out), n_rows, dims);
     return launch_status();

@@ -407,6 +407,105 @@ class Mainmodel_continue(_SCGIBCore):
 
 
 # ---------------------------------------------------------------------------
+# Domain adaptation
+# ---------------------------------------------------------------------------
+class Mainmodel_domainadapt(_SCGIBCore):
+    """models.py:107-355, driven by run_domain_adaptation (exp_molhiv.py:50-68,
+    train_molhiv.py:74-105): the pretrained model's extract_features (every
+    parameter trainable) -> MLP -> Set2Set -> r_transfer_d, regressed onto
+    Set2Set(raw normalised features) — loss_X = sum of squared differences.
+
+    Same constructor / forward signatures and state_dict keys as the
+    reference.  Kept quirks: the model's OWN Encoder1 / Encoder2 /
+    compressor / attn_layer are built but unused by forward, and its
+    extract_features (models.py:283) runs exactly those — so fine-tuning on
+    an adapted model (exp_molhiv.py:129, Mainmodel_finetuning loads it) runs
+    freshly initialised encoders, as the reference does."""
+
+    def __init__(self, args, in_dim, hidden_dim, num_layers, num_heads, k_transition,
+                 num_classes, cp_filename, encoder):
+        super().__init__()
+        self.tau = 1.0
+        self.readout = args.readout_f
+        self.s2s = Set2Set(hidden_dim, 2, 1)
+        self.s2s_rev = Set2Set(in_dim, 2, 1)
+        self.in_dim = args.d_transfer
+        self.transfer_d = nn.Linear(in_dim, self.in_dim, bias=False)
+        self.batch_size = getattr(args, "batch_size", 16)
+        self.useAtt = args.useAtt
+        if self.readout != "sum" or not self.useAtt:
+            raise NotImplementedError("the hot path implements readout_f='sum', useAtt=1")
+        self.embedding_h = nn.Linear(self.in_dim, hidden_dim, bias=False)
+        self.hidden_dim = hidden_dim
+        self.k_transition = k_transition
+        self.reduce_d = nn.Linear(2 * hidden_dim, hidden_dim)
+        self.attn_layer = nn.Linear(2 * hidden_dim, 1)
+        self.num_nodes = -1
+        self.device = getattr(args, "device", None)
+        self.r_transfer_d = nn.Sequential(nn.Linear(2 * hidden_dim, hidden_dim), nn.ReLU(),
+                                          nn.Linear(hidden_dim, in_dim * 2))
+        task = getattr(args, "task", "graph_classification")
+        if task in ("graph_regression", "graph_classification"):  # else: no head (:141)
+            out_dim = 1 if task == "graph_regression" else num_classes
+            self.predict = nn.Sequential(nn.Linear(2 * hidden_dim, hidden_dim), nn.ReLU(),
+                                         nn.Linear(hidden_dim, out_dim))
+        self.MLP = nn.Sequential(nn.Linear(2 * hidden_dim, hidden_dim), nn.ReLU(),
+                                 nn.Linear(hidden_dim, hidden_dim))
+        if encoder != "GIN":
+            raise NotImplementedError(f"encoder {encoder!r}: only GIN is on the hot path")
+        self.Encoder1 = GIN(self.in_dim, hidden_dim, _gin_layers(args))
+        self.Encoder2 = GIN(self.in_dim, hidden_dim, _gin_layers(args))
+        self.model = load_checkpoint(cp_filename, args)
+        for p in self.model.parameters():
+            p.requires_grad = True
+        self.compressor = nn.Sequential(nn.Linear(hidden_dim, hidden_dim),
+                                        nn.BatchNorm1d(hidden_dim), nn.ReLU(),
+                                        nn.Linear(hidden_dim, 1))
+        self.reconstructX = nn.Sequential(nn.Linear(hidden_dim, hidden_dim), nn.ReLU(),
+                                          nn.Linear(hidden_dim, in_dim))
+
+    def extract_features(self, nodes_list, batch_g, batch_x, flatten_batch_subgraphs, x_subs,
+                         device=None, noise=None):
+        """models.py:283-335: the DA model's own encoders / compressor /
+        attention (what fine-tuning on an adapted checkpoint runs)."""
+        ego, x_subs = self._prepare_ego(batch_g, flatten_batch_subgraphs, batch_x, x_subs)
+        im, kl, noisy, z2, z1 = self._extract(self, batch_g, batch_x, ego, x_subs, noise)
+        self._last_z1 = z1
+        ops.join_aside()
+        return im, kl, noisy, z2
+
+    def forward(self, batch_g, batch_x, flatten_batch_subgraphs, batch_logMs, x_subs,
+                current_epoch=None, edge_index=None, k_transition=None, device=None,
+                batch_size=16, noise=None):
+        self.batch_size = batch_size
+        self.device = device
+        batch_x_org = batch_x
+        inner = self.model
+        if flatten_batch_subgraphs is None and x_subs is None and batch_x.is_cuda:
+            # this model's transfer_d feeds the pretrained model's encoders
+            # (folded into their first layers), ego branch forked
+            ego, enc = self._encode_forked(inner, batch_g, batch_x, FORK_ENCODERS)
+            im = inner._extract(inner, batch_g, None, ego, None, noise, enc)[0]
+        else:
+            if flatten_batch_subgraphs is None:
+                flatten_batch_subgraphs, x_subs = self._prepare_ego(batch_g, None, batch_x,
+                                                                    x_subs)
+            im = inner.extract_features(None, batch_g, self.transfer_d(batch_x),
+                                        flatten_batch_subgraphs, self.transfer_d(x_subs),
+                                        device, noise)[0]
+        im = ops.mlp2(im, self.MLP, batch_g.dims)  # 2d -> d
+        im = self.r_transfer_d(self.s2s(batch_g, im))  # [B, 2 in_dim]
+        org_x = self.s2s_rev(batch_g, batch_x_org)  # [B, 2 in_dim]
+        loss = self.loss_X(org_x, im)
+        ops.join_aside()
+        return loss
+
+    def loss_X(self, batch_x_org, interaction_map):
+        """models.py:277-282: sum of squared differences (no mean)."""
+        return torch.sum((interaction_map - batch_x_org) ** 2)
+
+
+# ---------------------------------------------------------------------------
 # Fine-tuning head (SURVEY.md §8(f) #1, boundary §8(b))
 # ---------------------------------------------------------------------------
 class Mainmodel_finetuning(nn.Module):
@@ -533,13 +632,19 @@ _CKPT_ARGS = ("recons_type", "useAtt", "readout_f", "d_transfer", "gin_layers", 
 
 
 def save_checkpoint(model, path, args=None, in_dim=None, num_classes=1):
-    """state_dict checkpoint of a Mainmodel or Mainmodel_continue (the nested
-    inner model included), loadable with weights_only=True."""
+    """state_dict checkpoint of a Mainmodel, Mainmodel_continue or
+    Mainmodel_domainadapt (the nested wrapped models included), loadable with
+    weights_only=True."""
     cfg = {}
     if args is not None:
         cfg = {k: getattr(args, k) for k in _CKPT_ARGS if hasattr(args, k)}
     cfg.update(kind=type(model).__name__, in_dim=in_dim, hidden_dim=model.hidden_dim,
                k_transition=model.k_transition, num_classes=num_classes)
+    inner = getattr(model, "model", None)  # wrapped pretrained model (continue / DA)
+    if inner is not None:
+        cfg["inner_kind"] = type(inner).__name__
+        if getattr(inner, "model", None) is not None:
+            cfg["inner_inner_kind"] = type(inner.model).__name__
     torch.save({"config": cfg, "state_dict": model.state_dict()}, path)
 
 
@@ -556,13 +661,20 @@ def load_checkpoint(cp, args):
     if ns.task is None:
         ns.task = "graph_classification"
     kind = cfg.get("kind")
-    inner = Mainmodel(ns, cfg["in_dim"], cfg["hidden_dim"], 4, 4, cfg["k_transition"], "GIN")
-    if kind == "Mainmodel":
-        m = inner
-    elif kind == "Mainmodel_continue":
-        m = Mainmodel_continue(ns, cfg["in_dim"], cfg["hidden_dim"], 4, 4, cfg["k_transition"],
-                               cfg.get("num_classes", 1), inner, "GIN")
-    else:
-        raise NotImplementedError(f"checkpoint kind {kind!r}")
+    m = _build_kind(kind, ns, cfg, cfg.get("inner_kind"), cfg.get("inner_inner_kind"))
     m.load_state_dict(blob["state_dict"])
     return m
+
+
+def _build_kind(kind, ns, cfg, inner_kind=None, inner_inner_kind=None):
+    """An untrained module of checkpoint kind ``kind`` (nested wrappers are
+    rebuilt around the kinds they wrapped) for load_state_dict."""
+    dims = (cfg["in_dim"], cfg["hidden_dim"], 4, 4, cfg["k_transition"])
+    if kind == "Mainmodel":
+        return Mainmodel(ns, *dims, "GIN")
+    inner = _build_kind(inner_kind or "Mainmodel", ns, cfg, inner_inner_kind)
+    if kind == "Mainmodel_continue":
+        return Mainmodel_continue(ns, *dims, cfg.get("num_classes", 1), inner, "GIN")
+    if kind == "Mainmodel_domainadapt":
+        return Mainmodel_domainadapt(ns, *dims, cfg.get("num_classes", 1), inner, "GIN")
+    raise NotImplementedError(f"checkpoint kind {kind!r}")

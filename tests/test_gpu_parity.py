@@ -65,9 +65,10 @@ def test_gin_aggregate_eps_and_isolated(pkg, dev):
     assert rel_err(out.cpu(), ref) < 1e-6
 
 
-def test_segment_sum_and_broadcast(pkg, dev):
+@pytest.mark.parametrize("dim", [64, 9, 1])
+def test_segment_sum_and_broadcast(pkg, dev, dim):
     g, gh = rand_graph(pkg, 200, "molpcba", 2, dev)
-    x = torch.randn(g.num_nodes(), 64, device=dev, requires_grad=True)
+    x = torch.randn(g.num_nodes(), dim, device=dev, requires_grad=True)
     y = pkg.ops.sum_nodes_graph(g, x)
     ref = R.sum_nodes(x.detach().cpu(), torch.from_numpy(gh.batch_num_nodes_host()))
     assert rel_err(y.detach().cpu(), ref) < 1e-6
@@ -599,3 +600,71 @@ def test_gin_encoder_deferred_bn_bitwise(pkg, dev, via_ego, n_mols):
         assert torch.equal(ga[k], gb[k]), k
     for k in ba:
         assert torch.equal(ba[k], bb[k]), k
+
+
+# ---------------------------------------------------------------------------
+# Domain adaptation and fine-tuning on the adapted model
+# ---------------------------------------------------------------------------
+def _da_model(pkg, g, dev):
+    from types import SimpleNamespace
+    args = SimpleNamespace(recons_type="adj", useAtt=1, readout_f="sum", d_transfer=32,
+                           batch_size=int(g["B"]), gin_layers=4, task="graph_classification",
+                           dataset="ogbg-molhiv", device=dev)
+    F_in, C, k = int(g["F"]), int(g["num_classes"]), int(g["k"])
+    inner = pkg.models.Mainmodel(args, F_in, 64, 4, 4, k, "GIN")
+    pre = pkg.models.Mainmodel_continue(args, F_in, 64, 4, 4, k, C, inner, "GIN")
+    model = pkg.models.Mainmodel_domainadapt(args, F_in, 64, 4, 4, k, C, pre, "GIN")
+    if int(g["then_finetune"]):
+        model = pkg.models.Mainmodel_finetuning(args, F_in, 64, 4, 4, k, C, model, "GIN")
+    state = {k_[6:]: torch.tensor(v) for k_, v in g.items() if k_.startswith("param_")}
+    missing, unexpected = model.load_state_dict(state, strict=False)
+    assert not missing and not unexpected, (missing, unexpected)
+    return model.to(dev).train()
+
+
+def _golden_batch(pkg, g, dev, device_ego):
+    bg = pkg.graph.GraphBatch.from_edges(g["src"], g["dst"], len(g["x_raw"]), True,
+                                         g["batch_num_nodes"]).to(dev)
+    x = F.normalize(torch.tensor(g["x_raw"]).float()).to(dev)
+    if device_ego:
+        return bg, x, None, None
+    ego = pkg.graph.GraphBatch.from_edges(g["ego_src"], g["ego_dst"],
+                                          int(g["ego_batch_num_nodes"].sum()), True,
+                                          g["ego_batch_num_nodes"]).to(dev)
+    return bg, x, ego, x[torch.tensor(g["ego_nodes_global"], device=dev)]
+
+
+@pytest.mark.parametrize("device_ego", [True, False])
+def test_domainadapt_matches_reference(pkg, dev, device_ego):
+    g = load_golden("domainadapt_molhiv")
+    model = _da_model(pkg, g, dev)
+    assert {n for n, p in model.named_parameters() if p.requires_grad} == \
+        set(str(s) for s in g["trainable"])
+    bg, x, ego, x_subs = _golden_batch(pkg, g, dev, device_ego)
+    noise = (torch.tensor(g["u_gate"], device=dev), torch.tensor(g["u_feat"], device=dev))
+    loss = model(bg, x, ego, None, x_subs, 1, None, 2, dev, int(g["B"]), noise=noise)
+    assert rel_err(loss.item(), g["loss"]) < LOSS_TOL
+    loss.backward()
+    params = dict(model.named_parameters())
+    golden = {k[5:]: v for k, v in g.items() if k.startswith("grad_")}
+    check_grads_model(golden, lambda n: params[n].grad, tol=GRAD_TOL)
+    # parameters the reference leaves without a gradient stay without one
+    assert all(p.grad is None for n, p in params.items() if n not in golden)
+
+
+@pytest.mark.parametrize("device_ego", [True, False])
+def test_finetune_after_domainadapt_matches_reference(pkg, dev, device_ego):
+    g = load_golden("finetune_after_da_molhiv")
+    ft = _da_model(pkg, g, dev)
+    assert {n for n, p in ft.named_parameters() if p.requires_grad} == \
+        set(str(s) for s in g["trainable"])
+    bg, x, ego, x_subs = _golden_batch(pkg, g, dev, device_ego)
+    noise = (torch.tensor(g["u_gate"], device=dev), torch.tensor(g["u_feat"], device=dev))
+    scores, *_ = ft(bg, x, ego, x_subs, 1, None, 2, dev, int(g["B"]), noise=noise)
+    assert rel_err(scores.detach().cpu(), g["scores"]) < 1e-4
+    loss = ft.loss(scores, torch.tensor(g["targets"], device=dev))
+    assert rel_err(loss.item(), g["loss"]) < LOSS_TOL
+    loss.backward()
+    params = dict(ft.named_parameters())
+    check_grads_model({k[5:]: v for k, v in g.items() if k.startswith("grad_")},
+                      lambda n: params[n].grad, tol=GRAD_TOL)

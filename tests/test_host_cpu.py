@@ -247,3 +247,25 @@ def test_adam_rejects_cpu_parameters(pkg):
         opt.step()
     with pytest.raises(NotImplementedError):
         pkg.optim.Adam([p], amsgrad=True)
+
+
+def test_checkpoint_roundtrip_domainadapt(pkg, tmp_path):
+    """A domain-adapted model (wrapping a Mainmodel_continue wrapping a
+    Mainmodel) saves and loads weights-only, nesting rebuilt from the config."""
+    from types import SimpleNamespace
+    args = SimpleNamespace(recons_type="adj", useAtt=1, readout_f="sum", d_transfer=32,
+                           batch_size=8, gin_layers=4, task="graph_classification",
+                           dataset="ogbg-molhiv")
+    inner = pkg.models.Mainmodel(args, 9, 64, 4, 4, 1, "GIN")
+    pre = pkg.models.Mainmodel_continue(args, 9, 64, 4, 4, 1, 1, inner, "GIN")
+    da = pkg.models.Mainmodel_domainadapt(args, 9, 64, 4, 4, 1, 1, pre, "GIN")
+    assert all(p.requires_grad for p in da.parameters())
+    path = str(tmp_path / "da.pt")
+    pkg.models.save_checkpoint(da, path, args, in_dim=9, num_classes=1)
+    back = pkg.models.load_checkpoint(path, args)
+    assert type(back).__name__ == "Mainmodel_domainadapt"
+    assert type(back.model).__name__ == "Mainmodel_continue"
+    a, b = da.state_dict(), back.state_dict()
+    assert set(a) == set(b) and all(torch.equal(a[k], b[k]) for k in a)
+    ft = pkg.models.Mainmodel_finetuning(args, 9, 64, 4, 4, 1, 1, path, "GIN")
+    assert type(ft.model).__name__ == "Mainmodel_domainadapt"

@@ -94,6 +94,39 @@ def test_oracle_finetune_matches_reference(name):
     check_grads(golden_grads, lambda n_: p[n_].grad, tol=1e-4, metric="l2")
 
 
+def test_oracle_domainadapt_matches_reference():
+    """Mainmodel_domainadapt (models.py:107-355): X loss and every gradient."""
+    g = load_golden("domainadapt_molhiv")
+    batch, ego, x, x_subs = finetune_inputs(g)
+    p = R.make_params({k[6:]: v for k, v in g.items() if k.startswith("param_")})
+    buffers = {k: v.clone() for k, v in p.items() if "running" in k or "num_batches" in k}
+    loss = R.domainadapt_forward(p, batch, ego, x, x_subs, torch.tensor(g["u_gate"]),
+                                 torch.tensor(g["u_feat"]), buffers)
+    assert rel_err(loss.item(), g["loss"]) < 1e-5
+    loss.backward()
+    golden_grads = {k[5:]: v for k, v in g.items() if k.startswith("grad_")}
+    assert any(k.startswith("model.") for k in golden_grads)  # the pretrained model trains too
+    assert any(k.startswith("s2s_rev.") for k in golden_grads)
+    check_grads(golden_grads, lambda n_: p[n_].grad, tol=1e-4, metric="l2")
+
+
+def test_oracle_finetune_after_domainadapt_matches_reference():
+    """Fine-tuning on the adapted model runs the DA model's OWN extract_features
+    (models.py:283, its freshly built encoders) — the reference's quirk."""
+    g = load_golden("finetune_after_da_molhiv")
+    batch, ego, x, x_subs = finetune_inputs(g)
+    p = R.make_params({k[6:]: v for k, v in g.items() if k.startswith("param_")})
+    buffers = {k: v.clone() for k, v in p.items() if "running" in k or "num_batches" in k}
+    scores = R.finetune_forward(p, batch, ego, x, x_subs, torch.tensor(g["u_gate"]),
+                                torch.tensor(g["u_feat"]), "ogbg-molhiv", buffers)
+    assert rel_err(scores.detach(), g["scores"]) < 1e-5
+    loss = F.binary_cross_entropy(scores, torch.tensor(g["targets"]).float())
+    assert rel_err(loss.item(), g["loss"]) < 1e-5
+    loss.backward()
+    golden_grads = {k[5:]: v for k, v in g.items() if k.startswith("grad_")}
+    check_grads(golden_grads, lambda n_: p[n_].grad, tol=1e-4, metric="l2")
+
+
 def test_trans_logM_matches_reference_targets(pkg):
     """graph.trans_logM (restated util.getM_logM) == the reference's targets, bit-exact."""
     g = load_golden("pretrain_L4_k2_logm")

@@ -668,3 +668,14 @@ def test_finetune_after_domainadapt_matches_reference(pkg, dev, device_ego):
     params = dict(ft.named_parameters())
     check_grads_model({k[5:]: v for k, v in g.items() if k.startswith("grad_")},
                       lambda n: params[n].grad, tol=GRAD_TOL)
+
+
+def test_csr_cache_batches_egonets_bit_exact(pkg, dev, tmp_path):
+    """Batches collated from the on-disk CSR cache (§8(f) #2) feed the device
+    ego-net builder bit-exactly (the cache stores no ego-nets)."""
+    mols = pkg.synth.molecules(300, "molpcba", seed=21)
+    c = pkg.cache.write(mols, str(tmp_path), "ogbg-molpcba", cap=None)
+    c = pkg.cache.open_cache(str(tmp_path), "mol-PCBA")
+    for g, _, _ in c.batches(128, seed=2):
+        for k in (1, 2):
+            _check_ego(pkg, g, k, dev)

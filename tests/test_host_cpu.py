@@ -269,3 +269,74 @@ def test_checkpoint_roundtrip_domainadapt(pkg, tmp_path):
     assert set(a) == set(b) and all(torch.equal(a[k], b[k]) for k in a)
     ft = pkg.models.Mainmodel_finetuning(args, 9, 64, 4, 4, 1, 1, path, "GIN")
     assert type(ft.model).__name__ == "Mainmodel_domainadapt"
+
+
+# ---------------------------------------------------------------------------
+# §8(f) #2: on-disk CSR cache
+# ---------------------------------------------------------------------------
+def _records(pkg, n, seed, bad_at=()):
+    mols = pkg.synth.molecules(n, "qm9", seed=seed)
+    rng = np.random.default_rng(seed)
+    recs = [(ei, x, rng.integers(0, 2, size=(1, 3)).astype(np.float32)) for ei, x in mols]
+    for i in bad_at:  # trailing isolated atom: x has a row the edges never reach
+        ei, x, y = recs[i]
+        recs[i] = (ei, np.concatenate([x, x[:1]]), y)
+    return recs
+
+
+def test_csr_cache_roundtrip_matches_collate(pkg, tmp_path):
+    recs = _records(pkg, 60, 3, bad_at=(7, 31))
+    c = pkg.cache.write(recs, str(tmp_path), "QM9", cap=None, logm_k=(1, 2))
+    assert len(c) == 58 and c.meta["missing"] == 2 and c.meta["records_read"] == 60
+    kept = [i for i in range(60) if i not in (7, 31)]
+    np.testing.assert_array_equal(np.asarray(c.kept), kept)
+    c = pkg.cache.open_cache(str(tmp_path), "QM9")  # memory-mapped
+    order = np.random.default_rng(0).permutation(len(c))[:23]
+    g, y, logms = c.collate(order, k_logm=2)
+    ref, _ = pkg.graph.collate_pyg([recs[kept[i]][:2] for i in order])
+    for a in ("rowptr", "col", "graph_ptr"):
+        assert torch.equal(getattr(g, a), getattr(ref, a)), a
+    assert torch.equal(g.ndata["x"], ref.ndata["x"])
+    np.testing.assert_array_equal(g.batch_num_edges().numpy(), ref.batch_num_edges().numpy())
+    assert torch.equal(y, torch.from_numpy(np.stack([recs[kept[i]][2] for i in order])))
+    for j, i in enumerate(order):
+        gi = pkg.graph.from_pyg(*recs[kept[i]][:2])
+        np.testing.assert_array_equal(logms[j].numpy(), pkg.graph.trans_logM(gi, 2).numpy())
+    seen = np.concatenate([b[1].numpy()[:, 0, 0] * 0 + np.arange(len(b[1]))
+                           for b in c.batches(16, seed=1)])
+    assert len(seen) == len(c)
+
+
+def test_csr_cache_cap_and_name_alias(pkg, tmp_path):
+    """Records at index >= cap are never read; skipped records count towards
+    the cap (exp_molpcba.py:333); 'mol-PCBA' resolves to the cache the
+    molpcba preprocessor names 'ogbg-molpcba' (exp_molpcba.py:373 vs
+    exp_pretraining.py:218)."""
+    recs = _records(pkg, 30, 4, bad_at=(3,))
+
+    def gen():
+        for i, r in enumerate(recs):
+            if i >= 10:
+                raise AssertionError("record past the cap was read")
+            yield r
+    c = pkg.cache.write(gen(), str(tmp_path), "ogbg-molpcba", cap=10)
+    assert len(c) == 9 and c.meta["missing"] == 1
+    c2 = pkg.cache.open_cache(str(tmp_path), "mol-PCBA")
+    assert c2.path == c.path and len(c2) == 9
+    with pytest.raises(FileNotFoundError):
+        pkg.cache.open_cache(str(tmp_path), "QM9")
+
+
+def test_csr_cache_reference_ingest_goldens(pkg, tmp_path):
+    """The cache applies load_dgl_fromPyG + the skip rule exactly as the
+    reference did on its own inputs (golden ingest_egonet)."""
+    d = load_golden("ingest_egonet")
+    nm = int(d["num_mols"])
+    recs = [(d[f"m{i}_edge_index"], d[f"m{i}_x"]) for i in range(nm)]
+    c = pkg.cache.write(recs, str(tmp_path), "golden", cap=None)
+    kept = [i for i in range(nm) if d[f"m{i}_kept"]]
+    np.testing.assert_array_equal(np.asarray(c.kept), kept)
+    for j, i in enumerate(kept):
+        s, t = c.graph(j).edges()
+        np.testing.assert_array_equal(s.numpy(), d[f"m{i}_src"])
+        np.testing.assert_array_equal(t.numpy(), d[f"m{i}_dst"])

@@ -394,8 +394,9 @@ def main():
     # (one stream: the encoder branches are not forked here, so no other
     # kernel runs inside a bracket)
     r_bwd = r_fwd = None
+    fork_losses = pkg.models.FORK_LOSSES
     if not a.no_kernel_timer:
-        pkg.models.FORK_ENCODERS = False
+        pkg.models.FORK_ENCODERS = pkg.models.FORK_LOSSES = False
         with KernelTimer("scgib_gin_layer_fwd_bn", "scgib_gin_layer_bwd") as timer:
             for i in range(min(a.steps, 10)):
                 g = pool[i % len(pool)]
@@ -404,6 +405,7 @@ def main():
                                         a.batch)
                 (kl + rec + con).backward()
         pkg.models.FORK_ENCODERS = True
+        pkg.models.FORK_LOSSES = fork_losses
         r_bwd = timer.summary("scgib_gin_layer_bwd", layer_bwd_bytes, layer_bwd_flops)
         r_fwd = timer.summary("scgib_gin_layer_fwd_bn", layer_fwd_bytes, layer_fwd_flops)
 

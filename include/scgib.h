@@ -360,6 +360,26 @@ int scgib_mlp2_fwd(const float *x, int32_t d_in, int64_t n_nodes, const float *w
 int scgib_mlp2_bwd(const float *dout, const float *x, const float *r, int32_t d_in,
                    const float *w1, const float *w2, int64_t n_nodes, float *dx, float *slab,
                    float *wgrad, const int32_t *dims, scgib_stream_t stream);
+/* mlp2 + recon (fused): the interaction-map MLP followed by loss_recon_adj
+ * on its output (models.py:1174 then :1256-1262, i.e. Mainmodel_continue's
+ * forward with recons_type 'adj'; replaces scgib_mlp2_fwd + scgib_recon_fwd
+ * and their backward).  Forward: out (= IM), r, and loss; `ws` holds
+ * scgib_mlp2_recon_ws_floats(n) floats (per-tile Gram partials, G, loss
+ * partials) and must be passed unchanged to the backward; `counter` is one
+ * zeroed uint32, left zero.  Backward: dx = d loss / d x and wgrad as
+ * scgib_mlp2_bwd, for d loss / d recon = *g_loss; rowptr_t/col_t NULL for a
+ * symmetric graph (A = A^T). */
+int64_t scgib_mlp2_recon_ws_floats(int64_t n_nodes);
+int scgib_mlp2_recon_fwd(const float *x, int32_t d_in, int64_t n_nodes, const float *w1,
+                         const float *b1, const float *w2, const float *b2, float *r, float *out,
+                         const int32_t *rowptr, const int32_t *col, int64_t n_edges, float *ws,
+                         uint32_t *counter, float *loss, const int32_t *dims,
+                         scgib_stream_t stream);
+int scgib_mlp2_recon_bwd(const float *x, const float *r, const float *out, const float *ws,
+                         int32_t d_in, const float *w1, const float *w2, int64_t n_nodes,
+                         const int32_t *rowptr, const int32_t *col, const int32_t *rowptr_t,
+                         const int32_t *col_t, const float *g_loss, float *dx, float *slab,
+                         float *wgrad, const int32_t *dims, scgib_stream_t stream);
 int64_t scgib_linear_slab_floats(int64_t n_nodes);
 int scgib_linear_fwd(const float *x, int64_t n_nodes, const float *w, const float *b, float *out,
                      const int32_t *dims, scgib_stream_t stream);

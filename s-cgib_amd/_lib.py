@@ -43,6 +43,11 @@ SIGNATURES = {
     "scgib_mlp2_slab_floats": (_I64, [_I64, _I32]),
     "scgib_mlp2_fwd": (ctypes.c_int, [_P, _I32, _I64, _P, _P, _P, _P, _P, _P, _P, _P]),
     "scgib_mlp2_bwd": (ctypes.c_int, [_P, _P, _P, _I32, _P, _P, _I64, _P, _P, _P, _P, _P]),
+    "scgib_mlp2_recon_ws_floats": (_I64, [_I64]),
+    "scgib_mlp2_recon_fwd": (ctypes.c_int, [_P, _I32, _I64, _P, _P, _P, _P, _P, _P, _P, _P, _I64,
+                                            _P, _P, _P, _P, _P]),
+    "scgib_mlp2_recon_bwd": (ctypes.c_int, [_P, _P, _P, _P, _I32, _P, _P, _I64, _P, _P, _P, _P,
+                                            _P, _P, _P, _P, _P, _P]),
     "scgib_linear_slab_floats": (_I64, [_I64]),
     "scgib_linear_fwd": (ctypes.c_int, [_P, _I64, _P, _P, _P, _P, _P]),
     "scgib_linear_bwd": (ctypes.c_int, [_P, _P, _P, _I64, _P, _P, _P, _P, _P, _P]),

@@ -44,6 +44,54 @@ __device__ __forceinline__ int64_t xcd_remap(int64_t orig, int64_t nwg) {
     return base + orig / 8;
 }
 
+// Cross-workgroup data inside one kernel (last-arriver reductions): each
+// XCD has its own L2, and a plain store can sit in the writer's L2 while a
+// reader on another XCD misses to memory.  Agent-scope atomic stores/loads are
+// coherent across the XCDs without an L2 write-back; an agent-scope release
+// fence instead writes back the whole L2 (measured 5-10 us per workgroup).
+// Pattern: st_agent the data, block_arrive (vmcnt(0) + barrier + one counter
+// atomic), the last arriver ld_agent's it.
+__device__ __forceinline__ void st_agent(float *p, float v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_agent(double *p, double v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ float ld_agent(const float *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double ld_agent(const double *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// 16-byte variants (two 8-byte agent-scope accesses; p 16-byte aligned)
+__device__ __forceinline__ void st_agent4(float *p, float4 v) {
+    uint64_t *q = reinterpret_cast<uint64_t *>(p);
+    __hip_atomic_store(q, __builtin_bit_cast(uint64_t, make_float2(v.x, v.y)), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(q + 1, __builtin_bit_cast(uint64_t, make_float2(v.z, v.w)), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ float4 ld_agent4(const float *p) {
+    const uint64_t *q = reinterpret_cast<const uint64_t *>(p);
+    const float2 a = __builtin_bit_cast(float2, __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    const float2 b = __builtin_bit_cast(float2, __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    return make_float4(a.x, a.y, b.x, b.y);
+}
+
+// Count this workgroup in at `counter` and return whether it is the last of
+// `expected` arrivals.  Every wave first waits for its stores to be
+// acknowledged (vmcnt(0)); the barrier collects the waves; one thread counts
+// the workgroup in.  Data exchanged this way must use st_agent / ld_agent.
+__device__ __forceinline__ bool block_arrive(unsigned *counter, unsigned expected) {
+    __shared__ unsigned s_ticket;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0)
+        s_ticket = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    return s_ticket == expected - 1;
+}
+
 // Batched loads: a load written as `ok ? p[i] : 0` is compiled into its own
 // branch with an s_waitcnt inside, which serialises a batch of such loads.
 // The kernels instead load unconditionally from a clamped, always-valid index
@@ -64,6 +112,12 @@ __device__ __forceinline__ int64_t eff_count(const int32_t *dims, int idx, int64
 // Fixed-order sum of `nslab` per-workgroup slabs of `width` floats into out
 // (slab.hip); deterministic.
 int launch_slab_reduce(const float *slab, int nslab, int64_t width, float *out, hipStream_t st);
+
+// Fused recon loss, forward finish (recon.hip): Gram reduce over the head
+// MLP's tile partials + edge term + last-arriver loss.  wsd: 512 doubles.
+int launch_recon_fin(const float *gslab, const float *im, const int32_t *rowptr,
+                     const int32_t *col, int64_t n_nodes, int64_t n_edges, float *gram,
+                     double *wsd, unsigned *cnt, float *loss, const int32_t *dims, hipStream_t st);
 
 // Phase tracing (debug build only, `make trace` -> libscgib_trace.so):
 // thread 0 of each workgroup stamps the 100 MHz wall clock at phase marks

@@ -22,6 +22,8 @@
 //   per-split partials; the last split to arrive for a row block sums them in
 //   fixed order and applies the normalisation backward
 //     dz = (dzn - zn (zn . dzn)) / |z|   (|z| > eps; z / eps otherwise).
+// The split partials cross workgroups through agent-scope stores/loads and
+// block_arrive (common.h): no L2 write-back fence.
 //
 // Arrival counters: caller-provided, zero on entry, left zero on exit (the
 // last arriver resets them), so the launches replay from a HIP graph.
@@ -98,20 +100,6 @@ __device__ __forceinline__ float sum16(float v) {
     return v;
 }
 
-__device__ __forceinline__ bool last_arriver(unsigned *counter, unsigned expected) {
-    __shared__ unsigned ticket;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        ticket = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    __syncthreads();
-    if (ticket != expected - 1) return false;
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    return true;
-}
-
 // workspace (floats): D[B] | fwd partials [NS][B][4] | bwd partials [NS][B][128]
 __global__ __launch_bounds__(256) void contrast_fwd_k(const float *__restrict__ z1,
                                                       const float *__restrict__ z2, int64_t B,
@@ -149,9 +137,8 @@ __global__ __launch_bounds__(256) void contrast_fwd_k(const float *__restrict__ 
     e11d = sum16(e11d);
     e12d = sum16(e12d);
     float *Dv = ws, *pf = ws + B;
-    if (cl == 0 && i < B)
-        *reinterpret_cast<float4 *>(pf + (blockIdx.y * B + i) * 4) = make_float4(R, Bt, e11d, e12d);
-    if (!last_arriver(counter, gridDim.x * gridDim.y)) return;
+    if (cl == 0 && i < B) st_agent4(pf + (blockIdx.y * B + i) * 4, make_float4(R, Bt, e11d, e12d));
+    if (!block_arrive(counter, gridDim.x * gridDim.y)) return;
     __shared__ double red[256];
     double acc = 0.0;
     for (int64_t k = tid; k < B; k += 256) {
@@ -159,7 +146,7 @@ __global__ __launch_bounds__(256) void contrast_fwd_k(const float *__restrict__ 
         float4 v[kMaxSplit];
 #pragma unroll
         for (int y = 0; y < kMaxSplit; ++y)
-            v[y] = *reinterpret_cast<const float4 *>(pf + ((y < NS ? y : 0) * B + k) * 4);
+            v[y] = ld_agent4(pf + ((y < NS ? y : 0) * B + k) * 4);
         float s[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int y = 0; y < kMaxSplit; ++y) {
@@ -245,18 +232,18 @@ __global__ __launch_bounds__(256) void contrast_bwd_k(const float *__restrict__ 
     }
     if (i < B) {
         float *p = pb + (static_cast<int64_t>(blockIdx.y) * B + i) * 128;
-        reinterpret_cast<float4 *>(p)[cl] = d1;
-        reinterpret_cast<float4 *>(p + 64)[cl] = d2;
+        st_agent4(p + 4 * cl, d1);
+        st_agent4(p + 64 + 4 * cl, d2);
     }
-    if (!last_arriver(counters + blockIdx.x, NS)) return;
+    if (!block_arrive(counters + blockIdx.x, NS)) return;
     if (i < B) {
         d1 = d2 = make_float4(0.f, 0.f, 0.f, 0.f);
         float4 v1[kMaxSplit], v2[kMaxSplit];
 #pragma unroll
         for (int y = 0; y < kMaxSplit; ++y) {  // all splits in flight (clamped), summed in order
             const float *p = pb + (static_cast<int64_t>(y < NS ? y : 0) * B + i) * 128 + 4 * cl;
-            v1[y] = *reinterpret_cast<const float4 *>(p);
-            v2[y] = *reinterpret_cast<const float4 *>(p + 64);
+            v1[y] = ld_agent4(p);
+            v2[y] = ld_agent4(p + 64);
         }
 #pragma unroll
         for (int y = 0; y < kMaxSplit; ++y) {

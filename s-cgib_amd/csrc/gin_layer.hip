@@ -71,38 +71,7 @@ struct BnBwdFuse {          // gin_bwd_stats_k: dgamma, dbeta, dz2 coefficients
     int defer;
 };
 
-// release this workgroup's prior global writes, count it in, and return
-// whether it is the last of `expected` arrivals (then with acquire)
-// Cross-workgroup data of the finalize (tile stats, group partials) is
-// written with agent-scope atomic stores and read with agent-scope atomic
-// loads, which are coherent across the XCDs' L2s without an L2 write-back.
-// An agent-scope release fence would write back the whole L2 — including
-// the tile outputs this kernel just produced — and measured 5-10 us per
-// workgroup, more than the separate finalize launch it replaces.  So:
-// every wave waits for its stores to be acknowledged (vmcnt(0)), the barrier
-// collects the waves, and one thread counts the workgroup in.
-__device__ __forceinline__ void st_agent(float *p, float v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void st_agent(double *p, double v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ float ld_agent(const float *p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ double ld_agent(const double *p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-__device__ __forceinline__ bool block_arrive(unsigned *counter, unsigned expected) {
-    __shared__ unsigned s_ticket;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0)
-        s_ticket = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __syncthreads();
-    return s_ticket == expected - 1;
-}
+// Cross-workgroup exchange: st_agent / ld_agent / block_arrive (common.h).
 
 // rows of tile t / group g of an n-row layer
 __device__ __forceinline__ double rows_in(int64_t n, int64_t first, int64_t span) {
@@ -459,10 +428,23 @@ __device__ __forceinline__ void gather_x_rows(const PreArgs &pre, const int32_t 
     for (int k = 0; k < 4; ++k) acc[k] = ope * (self[k] * cm) + acc[k];
 }
 
+// Reconstruction loss fused into the head MLP (RECON, dense path only):
+// forward writes each tile's Gram partial out^T out of the MLP output (the
+// interaction map IM fed to loss_recon_adj, models.py:762-768) to gslab;
+// backward forms d IM = (g/N) (4 IM G - 2 (A + A^T) IM) of its tile in LDS
+// (recon.hip for the derivation) instead of reading dy.
+struct ReconArgs {
+    float *gslab;                       // fwd: [tiles][64*64] Gram partials
+    const float *im, *gram;             // bwd: MLP output [N][64], G [64][64]
+    const int32_t *rowptr, *col;        // bwd: dst-major CSR
+    const int32_t *rowptr_t, *col_t;    // bwd: src-major CSR, nullptr = symmetric
+    const float *g_loss;                // bwd: d loss / d recon (device scalar)
+};
+
 // GATHER = false is the dense two-layer MLP of the head (models.py:1055-1057,
 // applied at :1174): the tile's input rows are staged directly, agg_out and
 // the BN tile statistics are not written, z2_out is the MLP output.
-template <int DIN, bool XFORM, bool GATHER = true, bool PRE = false>
+template <int DIN, bool XFORM, bool GATHER = true, bool PRE = false, bool RECON = false>
 __global__ __launch_bounds__(256) void gin_fwd_k(
     const float *__restrict__ h, const float *__restrict__ in_scale,
     const float *__restrict__ in_shift, const int32_t *__restrict__ rowptr,
@@ -470,8 +452,9 @@ __global__ __launch_bounds__(256) void gin_fwd_k(
     const float *__restrict__ b1, const float *__restrict__ w2, const float *__restrict__ b2,
     float *__restrict__ agg_out, float *__restrict__ r_out, float *__restrict__ z2_out,
     float *__restrict__ part, const int32_t *__restrict__ dims, BnFwdFuse fz, PreArgs pre,
-    scgib_bn_pending pend) {
+    scgib_bn_pending pend, ReconArgs rec) {
     constexpr int LDA = DIN + 1, LPR = DIN / 4, RPP = 256 / LPR;
+    static_assert(!RECON || !GATHER, "the recon Gram partial is fused into the dense head MLP");
     static_assert(!PRE || DIN == 32, "transfer_d fold produces the 32-wide layer-0 input");
     const int64_t n = eff_count(dims, 0, ncap);
     __shared__ float sA[TM * LDA];
@@ -634,7 +617,22 @@ __global__ __launch_bounds__(256) void gin_fwd_k(
             s += acc[reg];
         }
     }
-    if constexpr (!GATHER) return;
+    if constexpr (!GATHER) {
+        if constexpr (RECON) {  // Gram partial of the tile: out^T out (valid rows)
+            // sA (the input tile) is dead since the first GEMM's barrier
+#pragma unroll
+            for (int reg = 0; reg < 16; ++reg) {
+                const int row = wr * 32 + acc_row(reg, l);
+                sA[row * LDH + ccol] = row < nv ? acc[reg] : 0.f;
+            }
+            __syncthreads();
+            const f32x16 g = mma_tn<TM>(sA + wr * 32, LDH, sA + wc * 32, LDH, zero16());
+            float *gs = rec.gslab + tile * 4096;
+#pragma unroll
+            for (int reg = 0; reg < 16; ++reg) gs[(wr * 32 + acc_row(reg, l)) * 64 + ccol] = g[reg];
+        }
+        return;
+    }
     SCGIB_MARK(3);
     s += __shfl_xor(s, 32, kWave);
     if (l < 32) sRed[wr][ccol] = s;
@@ -888,14 +886,16 @@ __global__ __launch_bounds__(1024) void bn_bwd_finalize_k(const float *__restric
 // of the MLP output); z2 / stat / coef are not read.
 // PRE: layer 0 with transfer_d folded in (see gather_x_rows): d(agg0) is not
 // stored; dWt += d(agg0)^T aggx is accumulated (slab tail of 32 x 16 floats).
-template <int DIN, bool BN = true, bool PRE = false>
-__global__ __launch_bounds__(256, (DIN <= 64 ? 2 : 1)) void gin_bwd_k(
+template <int DIN, bool BN = true, bool PRE = false, bool RECON = false>
+__global__ __launch_bounds__(256, (DIN <= 64 && !RECON ? 2 : 1)) void gin_bwd_k(
     const float *__restrict__ dy, const float *__restrict__ z2, const float *__restrict__ r,
     const float *__restrict__ agg, const float *__restrict__ stat,
     const float *__restrict__ coef, const float *__restrict__ w1, const float *__restrict__ w2,
     int64_t ncap, int64_t ntiles, float *__restrict__ dagg_out, float *__restrict__ slab,
-    const int32_t *__restrict__ dims, const float *__restrict__ aggx, scgib_bn_bwd_pending pend) {
+    const int32_t *__restrict__ dims, const float *__restrict__ aggx, scgib_bn_bwd_pending pend,
+    ReconArgs rec) {
     static_assert(!PRE || DIN == 32, "transfer_d fold: layer 0 only");
+    static_assert(!RECON || !BN, "the recon backward is fused into the dense head MLP");
     const int64_t n = eff_count(dims, 0, ncap);
     constexpr int LDA = DIN + 1;
     constexpr int SLAB = 64 * 64 + 64 * DIN + 128 + (PRE ? kPreSlab : 0);
@@ -909,11 +909,17 @@ __global__ __launch_bounds__(256, (DIN <= 64 ? 2 : 1)) void gin_bwd_k(
     __shared__ float sRA[TM * RA];   // r, then agg
     __shared__ float sW1[64 * LDA];
     __shared__ float sW2[64 * LDH];
+    __shared__ float sG[RECON ? 64 * LDH : 1];  // Gram matrix of the recon loss
     float *const sR = sRA, *const sA = sRA;
     const int tid = threadIdx.x, l = tid & 63, w = tid >> 6;
     const int wr = w >> 1, wc = w & 1;
     SCGIB_MARK(0);
     SCGIB_MARK_HWID();
+    float rscale = 0.f;  // recon: g / N
+    if constexpr (RECON) {
+        stage_matrix<64>(rec.gram, sG);
+        rscale = *rec.g_loss / static_cast<float>(n);
+    }
     // this layer's deferred BN-backward sums: partial loads go out with the weights
     BwdFin bfin;
     const int pend_ngr = static_cast<int>(((n + TM - 1) / TM + kGroup - 1) / kGroup);
@@ -972,8 +978,30 @@ __global__ __launch_bounds__(256, (DIN <= 64 ? 2 : 1)) void gin_bwd_k(
             const int64_t o = (row0 + rr) * 16 + c4, so = row0 * 16 + c4;
             if (BN) vz[k] = ld_ok(reinterpret_cast<const float4 *>(z2), o, so, rr < nv, zero);
             else vz[k] = zero;
-            vd[k] = ld_ok(reinterpret_cast<const float4 *>(dy), o, so, rr < nv, zero);
+            if (!RECON) vd[k] = ld_ok(reinterpret_cast<const float4 *>(dy), o, so, rr < nv, zero);
             vr[k] = ld_ok(reinterpret_cast<const float4 *>(r), o, so, rr < nv, zero);
+        }
+        // recon: own IM rows (vd) and nb = ((A + A^T) IM) rows, same layout
+        float4 nb[4];
+        if constexpr (RECON) {
+            const float4 *im4 = reinterpret_cast<const float4 *>(rec.im);
+            const float4 one = make_float4(1.f, 1.f, 1.f, 1.f);
+            GatherHead<4> hd;
+            gather_head<4, 16, 16>(im4, rec.rowptr, row0, nv, rs, c4, hd);
+            gather_tail<4, 16, false>(im4, rec.col, hd, c4, 0.f, one, zero, nb);
+            if (rec.rowptr_t) {
+                GatherHead<4> ht;
+                float4 nt[4];
+                gather_head<4, 16, 16>(im4, rec.rowptr_t, row0, nv, rs, c4, ht);
+                gather_tail<4, 16, false>(im4, rec.col_t, ht, c4, 0.f, one, zero, nt);
+#pragma unroll
+                for (int k = 0; k < 4; ++k) nb[k] = add4(nb[k], nt[k]);
+            } else {
+#pragma unroll
+                for (int k = 0; k < 4; ++k) nb[k] = add4(nb[k], nb[k]);  // A symmetric
+            }
+#pragma unroll
+            for (int k = 0; k < 4; ++k) vd[k] = rs + 16 * k < nv ? hd.self[k] : zero;
         }
 #pragma unroll
         for (int k = 0; k < AK; ++k) {
@@ -1008,6 +1036,24 @@ __global__ __launch_bounds__(256, (DIN <= 64 ? 2 : 1)) void gin_bwd_k(
             pr[0] = vr[k].x; pr[1] = vr[k].y; pr[2] = vr[k].z; pr[3] = vr[k].w;
         }
         __syncthreads();
+        if constexpr (RECON) {  // sD = IM tile -> dz2 = d IM = (g/N) (4 IM G - 2 nb)
+            const f32x16 p = mma_nn<64>(sD + wr * 32 * LDH, LDH, sG + wc * 32, LDH, zero16());
+            __syncthreads();
+#pragma unroll
+            for (int reg = 0; reg < 16; ++reg)
+                sD[(wr * 32 + acc_row(reg, l)) * LDH + wc * 32 + (l & 31)] = 4.f * rscale * p[reg];
+            __syncthreads();
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int rr = rs + 16 * k;
+                if (rr < nv) {  // rows past nv: IM = 0 there, so p = 0 already
+                    float *pd = sD + rr * LDH + 4 * c4;
+                    pd[0] -= 2.f * rscale * nb[k].x; pd[1] -= 2.f * rscale * nb[k].y;
+                    pd[2] -= 2.f * rscale * nb[k].z; pd[3] -= 2.f * rscale * nb[k].w;
+                }
+            }
+            __syncthreads();
+        }
         if (tile == blockIdx.x) SCGIB_MARK(1);
         // dW2 += dz2^T r  (sub-tile j-block wr, k-block wc)
         accW2 = mma_tn<TM>(sD + wr * 32, LDH, sR + wc * 32, LDH, accW2);
@@ -1126,11 +1172,11 @@ static int launch_gin_fwd(const float *h_in, int32_t d_in, const float *in_stat,
     const float *isc = in_stat ? in_stat + 128 : nullptr, *ish = in_stat ? in_stat + 192 : nullptr;
     const scgib_bn_pending pd = pend ? *pend : scgib_bn_pending{};
     if (d_in == 32)
-        gin_fwd_k<32, false><<<dim3((unsigned)nt), 256, 0, st>>>(h_in, isc, ish, rowptr, col, n_nodes, one_plus_eps, w1, b1, w2, b2, agg, r, z2, tile_stats, dims, fz, PreArgs{}, pd);
+        gin_fwd_k<32, false><<<dim3((unsigned)nt), 256, 0, st>>>(h_in, isc, ish, rowptr, col, n_nodes, one_plus_eps, w1, b1, w2, b2, agg, r, z2, tile_stats, dims, fz, PreArgs{}, pd, ReconArgs{});
     else if (in_stat || pend)
-        gin_fwd_k<64, true><<<dim3((unsigned)nt), 256, 0, st>>>(h_in, isc, ish, rowptr, col, n_nodes, one_plus_eps, w1, b1, w2, b2, agg, r, z2, tile_stats, dims, fz, PreArgs{}, pd);
+        gin_fwd_k<64, true><<<dim3((unsigned)nt), 256, 0, st>>>(h_in, isc, ish, rowptr, col, n_nodes, one_plus_eps, w1, b1, w2, b2, agg, r, z2, tile_stats, dims, fz, PreArgs{}, pd, ReconArgs{});
     else
-        gin_fwd_k<64, false><<<dim3((unsigned)nt), 256, 0, st>>>(h_in, isc, ish, rowptr, col, n_nodes, one_plus_eps, w1, b1, w2, b2, agg, r, z2, tile_stats, dims, fz, PreArgs{}, pd);
+        gin_fwd_k<64, false><<<dim3((unsigned)nt), 256, 0, st>>>(h_in, isc, ish, rowptr, col, n_nodes, one_plus_eps, w1, b1, w2, b2, agg, r, z2, tile_stats, dims, fz, PreArgs{}, pd, ReconArgs{});
     return launch_status();
 }
 
@@ -1300,9 +1346,9 @@ extern "C" int scgib_gin_layer_bwd(const float *dy, const float *z2, const float
     const int grid = bwd_grid(nt);
     hipStream_t st = as_stream(stream);
     if (d_in == 32)
-        gin_bwd_k<32><<<grid, 256, 0, st>>>(dy, z2, r, agg, stat, coef, w1, w2, n_nodes, nt, dagg, slab, dims, nullptr, pd);
+        gin_bwd_k<32><<<grid, 256, 0, st>>>(dy, z2, r, agg, stat, coef, w1, w2, n_nodes, nt, dagg, slab, dims, nullptr, pd, ReconArgs{});
     else
-        gin_bwd_k<64><<<grid, 256, 0, st>>>(dy, z2, r, agg, stat, coef, w1, w2, n_nodes, nt, dagg, slab, dims, nullptr, pd);
+        gin_bwd_k<64><<<grid, 256, 0, st>>>(dy, z2, r, agg, stat, coef, w1, w2, n_nodes, nt, dagg, slab, dims, nullptr, pd, ReconArgs{});
     const int rc = launch_status();
     if (rc != SCGIB_OK || !wgrad) return rc;  // wgrad NULL: the caller reduces the slabs
     return launch_slab_reduce(slab, grid, 64 * 64 + 64 * static_cast<int64_t>(d_in) + 128, wgrad, st);
@@ -1325,9 +1371,9 @@ extern "C" int scgib_mlp2_fwd(const float *x, int32_t d_in, int64_t n_nodes, con
     const unsigned nt = static_cast<unsigned>(scgib_gin_tiles(n_nodes));
     hipStream_t st = as_stream(stream);
     if (d_in == 128)
-        gin_fwd_k<128, false, false><<<nt, 256, 0, st>>>(x, nullptr, nullptr, nullptr, nullptr, n_nodes, 0.f, w1, b1, w2, b2, nullptr, r, out, nullptr, dims, BnFwdFuse{}, PreArgs{}, scgib_bn_pending{});
+        gin_fwd_k<128, false, false><<<nt, 256, 0, st>>>(x, nullptr, nullptr, nullptr, nullptr, n_nodes, 0.f, w1, b1, w2, b2, nullptr, r, out, nullptr, dims, BnFwdFuse{}, PreArgs{}, scgib_bn_pending{}, ReconArgs{});
     else
-        gin_fwd_k<64, false, false><<<nt, 256, 0, st>>>(x, nullptr, nullptr, nullptr, nullptr, n_nodes, 0.f, w1, b1, w2, b2, nullptr, r, out, nullptr, dims, BnFwdFuse{}, PreArgs{}, scgib_bn_pending{});
+        gin_fwd_k<64, false, false><<<nt, 256, 0, st>>>(x, nullptr, nullptr, nullptr, nullptr, n_nodes, 0.f, w1, b1, w2, b2, nullptr, r, out, nullptr, dims, BnFwdFuse{}, PreArgs{}, scgib_bn_pending{}, ReconArgs{});
     return launch_status();
 }
 
@@ -1341,9 +1387,70 @@ extern "C" int scgib_mlp2_bwd(const float *dout, const float *x, const float *r,
     const int grid = bwd_grid(nt);
     hipStream_t st = as_stream(stream);
     if (d_in == 128)
-        gin_bwd_k<128, false><<<grid, 256, 0, st>>>(dout, nullptr, r, x, nullptr, nullptr, w1, w2, n_nodes, nt, dx, slab, dims, nullptr, scgib_bn_bwd_pending{});
+        gin_bwd_k<128, false><<<grid, 256, 0, st>>>(dout, nullptr, r, x, nullptr, nullptr, w1, w2, n_nodes, nt, dx, slab, dims, nullptr, scgib_bn_bwd_pending{}, ReconArgs{});
     else
-        gin_bwd_k<64, false><<<grid, 256, 0, st>>>(dout, nullptr, r, x, nullptr, nullptr, w1, w2, n_nodes, nt, dx, slab, dims, nullptr, scgib_bn_bwd_pending{});
+        gin_bwd_k<64, false><<<grid, 256, 0, st>>>(dout, nullptr, r, x, nullptr, nullptr, w1, w2, n_nodes, nt, dx, slab, dims, nullptr, scgib_bn_bwd_pending{}, ReconArgs{});
+    const int rc = launch_status();
+    if (rc != SCGIB_OK) return rc;
+    return launch_slab_reduce(slab, grid, 64 * 64 + 64 * static_cast<int64_t>(d_in) + 128, wgrad, st);
+}
+
+// ---------------------------------------------------------------------------
+// Head MLP + adjacency reconstruction loss, fused (Mainmodel / _continue with
+// recons_type 'adj': models.py:1174 then :1256-1262).  Forward: mlp2 with a
+// Gram partial per tile, then recon_fin_k (Gram reduce + edge term + loss).
+// Backward: mlp2 backward whose tile dy is d IM of the recon loss.
+// ---------------------------------------------------------------------------
+extern "C" int64_t scgib_mlp2_recon_ws_floats(int64_t n_nodes) {
+    // gram slabs [tiles][4096] | gram [4096] | 512 doubles
+    return n_nodes <= 0 ? 0 : scgib_gin_tiles(n_nodes) * 4096 + 4096 + 2 * 512;
+}
+
+extern "C" int scgib_mlp2_recon_fwd(const float *x, int32_t d_in, int64_t n_nodes,
+                                    const float *w1, const float *b1, const float *w2,
+                                    const float *b2, float *r, float *out,
+                                    const int32_t *rowptr, const int32_t *col, int64_t n_edges,
+                                    float *ws, uint32_t *counter, float *loss,
+                                    const int32_t *dims, scgib_stream_t stream) {
+    if (n_nodes <= 0 || n_edges < 0 || (d_in != 64 && d_in != 128)) return SCGIB_EINVAL;
+    if (!x || !w1 || !b1 || !w2 || !b2 || !r || !out || !rowptr || (n_edges > 0 && !col) || !ws ||
+        !counter || !loss)
+        return SCGIB_EINVAL;
+    const int64_t nt = scgib_gin_tiles(n_nodes);
+    float *gram = ws + nt * 4096;
+    double *wsd = reinterpret_cast<double *>(gram + 4096);
+    ReconArgs rec{};
+    rec.gslab = ws;
+    hipStream_t st = as_stream(stream);
+    if (d_in == 128)
+        gin_fwd_k<128, false, false, false, true><<<(unsigned)nt, 256, 0, st>>>(x, nullptr, nullptr, nullptr, nullptr, n_nodes, 0.f, w1, b1, w2, b2, nullptr, r, out, nullptr, dims, BnFwdFuse{}, PreArgs{}, scgib_bn_pending{}, rec);
+    else
+        gin_fwd_k<64, false, false, false, true><<<(unsigned)nt, 256, 0, st>>>(x, nullptr, nullptr, nullptr, nullptr, n_nodes, 0.f, w1, b1, w2, b2, nullptr, r, out, nullptr, dims, BnFwdFuse{}, PreArgs{}, scgib_bn_pending{}, rec);
+    const int rc = launch_status();
+    if (rc != SCGIB_OK) return rc;
+    return launch_recon_fin(ws, out, rowptr, col, n_nodes, n_edges, gram, wsd, counter, loss, dims,
+                            st);
+}
+
+extern "C" int scgib_mlp2_recon_bwd(const float *x, const float *r, const float *out,
+                                    const float *ws, int32_t d_in, const float *w1,
+                                    const float *w2, int64_t n_nodes, const int32_t *rowptr,
+                                    const int32_t *col, const int32_t *rowptr_t,
+                                    const int32_t *col_t, const float *g_loss, float *dx,
+                                    float *slab, float *wgrad, const int32_t *dims,
+                                    scgib_stream_t stream) {
+    if (n_nodes <= 0 || (d_in != 64 && d_in != 128)) return SCGIB_EINVAL;
+    if (!x || !r || !out || !ws || !w1 || !w2 || !rowptr || !col || !g_loss || !dx || !slab ||
+        !wgrad || ((rowptr_t == nullptr) != (col_t == nullptr)))
+        return SCGIB_EINVAL;
+    const int64_t nt = scgib_gin_tiles(n_nodes);
+    const int grid = bwd_grid(nt);
+    ReconArgs rec{nullptr, out, ws + nt * 4096, rowptr, col, rowptr_t, col_t, g_loss};
+    hipStream_t st = as_stream(stream);
+    if (d_in == 128)
+        gin_bwd_k<128, false, false, true><<<grid, 256, 0, st>>>(nullptr, nullptr, r, x, nullptr, nullptr, w1, w2, n_nodes, nt, dx, slab, dims, nullptr, scgib_bn_bwd_pending{}, rec);
+    else
+        gin_bwd_k<64, false, false, true><<<grid, 256, 0, st>>>(nullptr, nullptr, r, x, nullptr, nullptr, w1, w2, n_nodes, nt, dx, slab, dims, nullptr, scgib_bn_bwd_pending{}, rec);
     const int rc = launch_status();
     if (rc != SCGIB_OK) return rc;
     return launch_slab_reduce(slab, grid, 64 * 64 + 64 * static_cast<int64_t>(d_in) + 128, wgrad, st);
@@ -1381,7 +1488,7 @@ extern "C" int scgib_gin_layer0_fwd(const float *x, int32_t n_feat, const int32_
     const int64_t nt = scgib_gin_tiles(n_nodes);
     gin_fwd_k<32, false, true, true><<<dim3((unsigned)nt), 256, 0, as_stream(stream)>>>(
         nullptr, nullptr, nullptr, rowptr, col, n_nodes, one_plus_eps, w1, b1, w2, b2, agg, r, z2,
-        bn_ws, dims, fz, pre, scgib_bn_pending{});
+        bn_ws, dims, fz, pre, scgib_bn_pending{}, ReconArgs{});
     return launch_status();
 }
 
@@ -1397,6 +1504,6 @@ extern "C" int scgib_gin_layer0_bwd(const float *dy, const float *z2, const floa
     const scgib_bn_bwd_pending pd = pending ? *pending : scgib_bn_bwd_pending{};
     const int64_t nt = scgib_gin_tiles(n_nodes);
     gin_bwd_k<32, true, true><<<bwd_grid(nt), 256, 0, as_stream(stream)>>>(
-        dy, z2, r, agg, stat, coef, w1, w2, n_nodes, nt, nullptr, slab, dims, aggx, pd);
+        dy, z2, r, agg, stat, coef, w1, w2, n_nodes, nt, nullptr, slab, dims, aggx, pd, ReconArgs{});
     return launch_status();
 }

@@ -138,6 +138,14 @@ _SIDE_STREAMS = {}
 FORK_ENCODERS = True
 # both folded encoders as one autograd node (ops.gin_encoder_pair_x)
 PAIR_ENCODERS = os.environ.get("SCGIB_PAIR_ENCODERS", "1") != "0"
+# contrastive loss on the side stream, beside the head MLP + recon chain (off:
+# measured 2-4 % slower — each cross-stream edge of a replayed graph costs more
+# than the ~34 us of contrastive kernels it hides)
+FORK_LOSSES = os.environ.get("SCGIB_FORK_LOSSES", "0") != "0"
+# compressor[0] computed at the end of the core encoder chain (ops.gin_encoder_pair_x)
+LIN_IN_PAIR = os.environ.get("SCGIB_LIN_IN_PAIR", "1") != "0"
+# head MLP + adjacency recon loss as one fused op (ops.mlp2_recon)
+FUSE_RECON = os.environ.get("SCGIB_FUSE_RECON", "1") != "0"
 
 
 def _side_stream(device):
@@ -180,22 +188,33 @@ class _SCGIBCore(nn.Module):
     def _extract(self, enc_owner, batch_g, batch_x, ego, x_subs, noise, encoded=None):
         """extract_features of ``enc_owner`` (models.py:702-750); returns the
         reference's 4-tuple plus z1 = sum_nodes(noisy) (computed in-kernel).
-        ``encoded`` = (graph_features, subgraphs_features, sub_readout) when the
-        encoders already ran (_encode_forked)."""
+        ``encoded`` = (graph_features, subgraphs_features, sub_readout[, t]) when
+        the encoders already ran (_encode_forked); t = compressor[0](graph
+        features) when the encoder pair computed it."""
+        t = None
         if encoded is None:
             graph_features = enc_owner.Encoder1(batch_g, batch_x)
             subgraphs_features = enc_owner.Encoder2(ego, x_subs)
             sub_readout = ops.segment_sum(subgraphs_features, ego.graph_ptr, ego.batch_size,
                                           ego.seg_dims)
         else:
-            graph_features, subgraphs_features, sub_readout = encoded
+            graph_features, subgraphs_features, sub_readout = encoded[:3]
+            t = encoded[3] if len(encoded) > 3 else None
         enc_owner.graph_features = graph_features
         enc_owner.subgraphs_features = subgraphs_features
         u_gate, u_feat = self._noise(graph_features.shape[0], graph_features.device, noise)
         # compressor[0] (models.py:1092) runs fused in front of the interaction
-        im, z1, z2, kl, kl_mean = ops.interaction_lin(graph_features, sub_readout, u_gate, u_feat,
-                                                      enc_owner.compressor, enc_owner.attn_layer,
-                                                      batch_g, enc_owner.training)
+        if t is not None:
+            comp = enc_owner.compressor
+            im, z1, z2, kl, kl_mean = ops.interaction(graph_features, t, sub_readout, u_gate,
+                                                      u_feat, comp[1], comp[3],
+                                                      enc_owner.attn_layer, batch_g,
+                                                      enc_owner.training)
+        else:
+            im, z1, z2, kl, kl_mean = ops.interaction_lin(graph_features, sub_readout, u_gate,
+                                                          u_feat, enc_owner.compressor,
+                                                          enc_owner.attn_layer, batch_g,
+                                                          enc_owner.training)
         enc_owner._last_kl_mean = kl_mean
         noisy = im[:, : self.hidden_dim]
         return im, kl, noisy, z2, z1
@@ -222,15 +241,17 @@ class _SCGIBCore(nn.Module):
             # ego chain is enqueued first on ``side`` in forward AND backward
             with torch.cuda.stream(side):
                 ego = G.egonet_batch(batch_g, self.k_transition)
-            subgraphs_features, graph_features = ops.gin_encoder_pair_x(
+            lin0 = enc_owner.compressor[0] if LIN_IN_PAIR else None
+            outs = ops.gin_encoder_pair_x(
                 batch_x, ego, enc_owner.Encoder2, batch_g, enc_owner.Encoder1, self.transfer_d,
-                ego.ndata["_ID"], side)
+                ego.ndata["_ID"], side, lin0)
+            subgraphs_features, graph_features = outs[0], outs[1]
             with torch.cuda.stream(side):
                 sub_readout = ops.segment_sum(subgraphs_features, ego.graph_ptr, ego.batch_size,
                                               ego.seg_dims)
             main.wait_stream(side)
             sub_readout.record_stream(main)
-            return ego, (graph_features, subgraphs_features, sub_readout)
+            return ego, (graph_features, subgraphs_features, sub_readout, *outs[2:])
         with torch.cuda.stream(side):
             if fold:
                 ego = G.egonet_batch(batch_g, self.k_transition)
@@ -252,9 +273,25 @@ class _SCGIBCore(nn.Module):
         return ego, (graph_features, subgraphs_features, sub_readout)
 
     def _losses(self, batch_g, im, kl_mean, z1, z2, mlp, batch_size, batch_logMs=None):
-        im = ops.mlp2(im, mlp, batch_g.dims)  # models.py:1174, fused
+        # the contrastive loss needs only the two readouts: on the side stream
+        # it (and, through autograd, its backward) overlaps the head MLP and
+        # the reconstruction loss, which form the critical path
+        side = _side_stream(im.device) if (FORK_LOSSES and im.is_cuda) else None
+        if side is not None:
+            main = torch.cuda.current_stream(im.device)
+            side.wait_stream(main)
+            z1.record_stream(side)
+            z2.record_stream(side)
+            with torch.cuda.stream(side):
+                con = semi_loss(z1, z2, batch_size)
         kl_loss = kl_mean  # == torch.mean(KL_tensor) (models.py:679), computed in-kernel
-        con = semi_loss(z1, z2, batch_size)
+        if side is None:
+            con = semi_loss(z1, z2, batch_size)
+        if self.recons_type == "adj" and FUSE_RECON:
+            # models.py:1174 + loss_recon_adj (:1256-1262): MLP and recon fused
+            rec = ops.mlp2_recon(im, mlp, batch_g)
+            return kl_loss, self._join_losses(side, con), rec
+        im = ops.mlp2(im, mlp, batch_g.dims)  # models.py:1174, fused
         if self.recons_type == "adj":
             rec = ops.recon_adj(im, batch_g)
         elif self.recons_type == "logM":  # models.py:692-693 / 770-782
@@ -264,7 +301,15 @@ class _SCGIBCore(nn.Module):
             rec = ops.recon_logm(im, batch_g, batch_logMs)
         else:  # the reference returns -1.0 (models.py:694-695)
             rec = torch.tensor(-1.0, device=im.device)
-        return kl_loss, con, rec
+        return kl_loss, self._join_losses(side, con), rec
+
+    @staticmethod
+    def _join_losses(side, con):
+        if side is not None:
+            main = torch.cuda.current_stream(con.device)
+            main.wait_stream(side)
+            con.record_stream(main)
+        return con
 
 
 class Mainmodel(_SCGIBCore):

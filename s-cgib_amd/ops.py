@@ -347,7 +347,7 @@ class _GinEncoderPair(torch.autograd.Function):
     overlap in both directions; d Wt = d Wt(ego) + d Wt(core)."""
 
     @staticmethod
-    def forward(ctx, x, wt, nmap, ego, core, gin_ego, gin_core, training, side, *params):
+    def forward(ctx, x, wt, w0, b0, nmap, ego, core, gin_ego, gin_core, training, side, *params):
         main = _torch_stream()
         ne = 6 * len(gin_ego.ginlayers)
         ctx.sub = (_Ctx(), _Ctx())
@@ -358,38 +358,71 @@ class _GinEncoderPair(torch.autograd.Function):
                                     *params[:ne])
         f = _GinEncoder.forward(ctx.sub[1], None, core, gin_core, training, x, wt, None,
                                 *params[ne:])
+        outs = (s, f)
+        ctx.lin = w0 is not None
+        if ctx.lin:  # compressor[0] on the (shorter) core chain, before the join
+            w0, b0 = _f32(w0, "compressor.0.weight"), _f32(b0, "compressor.0.bias")
+            if tuple(w0.shape) != (HIDDEN, HIDDEN):
+                raise _lib.ScgibError("compressor[0] must be Linear(64, 64)")
+            t = torch.empty_like(f)
+            _lib.call("scgib_linear_fwd", _p(f), f.shape[0], _p(w0), _p(b0), _p(t),
+                      _p(core.dims), _stream())
+            ctx.lin_saved = (f, w0)
+            ctx.core_dims = core.dims
+            outs = (s, f, t)
         main.wait_stream(side)
         s.record_stream(main)
-        return s, f
+        return outs
 
     @staticmethod
-    def backward(ctx, g_s, g_f):
+    def backward(ctx, g_s, g_f, g_t=None):
         # backward: the ego chain (the longer one) stays on the current stream,
         # where its weight-gradient reduces can fork to the aux stream (a fork
         # from an already-forked stream breaks HIP-graph capture on this
-        # runtime, tools/capture_probe.py); Encoder1 runs on ``side``
+        # runtime, tools/capture_probe.py); Encoder1 runs on ``side``, preceded
+        # by compressor[0]'s backward (d f += d t W0, dW0, db0)
         main, side = _torch_stream(), ctx.side
         side.wait_stream(main)
+        dw0 = db0 = None
+        g_f_in = g_f
         with torch.cuda.stream(side):
+            if ctx.lin and g_t is not None:
+                f, w0 = ctx.lin_saved
+                g_t = _f32(g_t, "compressor.0 grad")
+                n = f.shape[0]
+                slab = torch.empty(int(_lib.query("scgib_linear_slab_floats", n)),
+                                   dtype=torch.float32, device=f.device)
+                wg = torch.empty(HIDDEN * HIDDEN + HIDDEN, dtype=torch.float32, device=f.device)
+                df_total = torch.empty_like(f)
+                _lib.call("scgib_linear_bwd", _p(g_t), _p(f), _p(w0), n,
+                          _p(_f32(g_f, "g_f")) if g_f is not None else None, _p(df_total),
+                          _p(slab), _p(wg), _p(ctx.core_dims), _stream())
+                dw0, db0 = wg[: HIDDEN * HIDDEN].view(HIDDEN, HIDDEN), wg[HIDDEN * HIDDEN:]
+                g_f = df_total
             gc = _GinEncoder.backward(ctx.sub[1], g_f)
         ge = _GinEncoder.backward(ctx.sub[0], g_s)
         main.wait_stream(side)
-        for g in gc:
+        for g in (*gc, dw0, db0):
             if isinstance(g, torch.Tensor):
                 g.record_stream(main)
-        g_f.record_stream(side)
+        if g_f_in is not None:
+            g_f_in.record_stream(side)
+        if g_t is not None:
+            g_t.record_stream(side)
         dwt = ge[5] + gc[5]
-        return (None, dwt, None, None, None, None, None, None, None, *ge[7:], *gc[7:])
+        return (None, dwt, dw0, db0, None, None, None, None, None, None, None, *ge[7:], *gc[7:])
 
 
 def _torch_stream():
     return torch.cuda.current_stream()
 
 
-def gin_encoder_pair_x(x, ego, gin_ego, core, gin_core, transfer, node_map, side):
+def gin_encoder_pair_x(x, ego, gin_ego, core, gin_core, transfer, node_map, side, lin0=None):
     """(gin_ego(ego, transfer(x[node_map])), gin_core(core, transfer(x))) —
     the two encoders of Mainmodel.forward with transfer_d folded, the ego
-    chain on stream ``side`` (forward and backward)."""
+    chain on stream ``side`` (forward and backward).  With ``lin0`` (the
+    compressor's Linear(64, 64), models.py:596) also returns
+    t = lin0(gin_core(...)), computed at the end of the core chain."""
     if ego.num_nodes() == 0 or core.num_nodes() == 0:
         raise _lib.ScgibError("gin_encoder on an empty graph")
     if transfer.bias is not None or transfer.weight.shape != (32, x.shape[1]) \
@@ -399,9 +432,10 @@ def gin_encoder_pair_x(x, ego, gin_ego, core, gin_core, transfer, node_map, side
         raise _lib.ScgibError("transfer_d fold: no gradient w.r.t. the raw features")
     if bool(gin_ego.training) != bool(gin_core.training):
         raise _lib.ScgibError("gin_encoder_pair_x: encoders in different train/eval modes")
-    return _GinEncoderPair.apply(x, transfer.weight, node_map, ego, core, gin_ego, gin_core,
-                                 bool(gin_core.training), side, *_gin_layer_params(gin_ego),
-                                 *_gin_layer_params(gin_core))
+    w0, b0 = (lin0.weight, lin0.bias) if lin0 is not None else (None, None)
+    return _GinEncoderPair.apply(x, transfer.weight, w0, b0, node_map, ego, core, gin_ego,
+                                 gin_core, bool(gin_core.training), side,
+                                 *_gin_layer_params(gin_ego), *_gin_layer_params(gin_core))
 
 
 # ---------------------------------------------------------------------------
@@ -756,6 +790,63 @@ def mlp2(x, mlp, dims=None):
     """``mlp`` = Sequential(Linear(d, 64), ReLU(), Linear(64, 64)) applied by
     the fused tile kernels (models.py:1055-1057, :1174)."""
     return _Mlp2.apply(x, mlp[0].weight, mlp[0].bias, mlp[2].weight, mlp[2].bias, dims)
+
+
+class _Mlp2Recon(torch.autograd.Function):
+    """loss_recon_adj(MLP(x)) (models.py:1174 then :1256-1262) in two
+    launches forward (the MLP tiles also write Gram partials; one kernel
+    reduces them, adds the edge term and forms the loss) and one backward
+    (the MLP backward forms d IM of its tile itself) + the weight reduce."""
+
+    @staticmethod
+    def forward(ctx, x, w1, b1, w2, b2, graph):
+        x = _f32(x, "mlp2_recon")
+        n, d_in = x.shape
+        if tuple(w1.shape) != (HIDDEN, d_in) or tuple(w2.shape) != (HIDDEN, HIDDEN):
+            raise _lib.ScgibError(f"mlp2_recon: expects Linear({d_in},64) - Linear(64,64)")
+        w1, b1, w2, b2 = (_f32(t, "mlp2 params") for t in (w1, b1, w2, b2))
+        dev = x.device
+        r = torch.empty(n, HIDDEN, dtype=torch.float32, device=dev)
+        out = torch.empty(n, HIDDEN, dtype=torch.float32, device=dev)
+        ws = torch.empty(int(_lib.query("scgib_mlp2_recon_ws_floats", n)), dtype=torch.float32,
+                         device=dev)
+        loss = torch.empty((), dtype=torch.float32, device=dev)
+        cnt = counters(dev, "mlp2_recon", 1)
+        _lib.call("scgib_mlp2_recon_fwd", _p(x), d_in, n, _p(w1), _p(b1), _p(w2), _p(b2), _p(r),
+                  _p(out), _p(graph.rowptr), _p(graph.col), graph.edge_capacity(), _p(ws),
+                  _p(cnt), _p(loss), _p(graph.dims), _stream())
+        ctx.save_for_backward(x, r, out, ws, w1, w2)
+        ctx.graph = graph
+        return loss
+
+    @staticmethod
+    def backward(ctx, g_loss):
+        x, r, out, ws, w1, w2 = ctx.saved_tensors
+        gr = ctx.graph
+        g_loss = _f32(g_loss.reshape(1), "g_loss")
+        n, d_in = x.shape
+        dx = torch.empty_like(x)
+        slab = torch.empty(int(_lib.query("scgib_mlp2_slab_floats", n, d_in)),
+                           dtype=torch.float32, device=x.device)
+        wg = torch.empty(HIDDEN * HIDDEN + HIDDEN * d_in + 2 * HIDDEN, dtype=torch.float32,
+                         device=x.device)
+        sym = gr.symmetric
+        _lib.call("scgib_mlp2_recon_bwd", _p(x), _p(r), _p(out), _p(ws), d_in, _p(w1), _p(w2), n,
+                  _p(gr.rowptr), _p(gr.col), None if sym else _p(gr.rowptr_t),
+                  None if sym else _p(gr.col_t), _p(g_loss), _p(dx), _p(slab), _p(wg),
+                  _p(gr.dims), _stream())
+        o = HIDDEN * HIDDEN
+        dw2 = wg[:o].view(HIDDEN, HIDDEN)
+        dw1 = wg[o: o + HIDDEN * d_in].view(HIDDEN, d_in)
+        db2 = wg[o + HIDDEN * d_in: o + HIDDEN * d_in + HIDDEN]
+        db1 = wg[o + HIDDEN * d_in + HIDDEN:]
+        return dx, dw1, db1, dw2, db2, None
+
+
+def mlp2_recon(x, mlp, graph):
+    """recon_adj(mlp2(x, mlp), graph) fused (the pretraining model's head);
+    the MLP output itself is not returned (nothing else reads it)."""
+    return _Mlp2Recon.apply(x, mlp[0].weight, mlp[0].bias, mlp[2].weight, mlp[2].bias, graph)
 
 
 # ---------------------------------------------------------------------------

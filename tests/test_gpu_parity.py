@@ -421,6 +421,55 @@ def test_mlp2_fwd_bwd(pkg, dev, d_in, n):
 
 
 # ---------------------------------------------------------------------------
+# A9 + A12 fused: loss_recon_adj(MLP(x)) vs fp64 torch (dense N x N)
+# ---------------------------------------------------------------------------
+def _dense_adj(src, dst, n):
+    a = torch.zeros(n, n, dtype=torch.float64)
+    a.index_put_((dst, src), torch.ones(len(src), dtype=torch.float64))
+    return a
+
+
+@pytest.mark.parametrize("n_mols,symmetric", [(1, True), (7, True), (512, True), (40, False)])
+def test_mlp2_recon_fused(pkg, dev, n_mols, symmetric):
+    if symmetric:
+        g, gh = rand_graph(pkg, n_mols, "qm9", 5, dev)
+    else:  # a directed graph: A != A^T exercises the transposed gather
+        rng = np.random.default_rng(n_mols)
+        n = 600
+        src = rng.integers(0, n, 1500)
+        dst = rng.integers(0, n, 1500)
+        keep = src != dst
+        pairs = np.unique(np.stack([src[keep], dst[keep]], 1), axis=0)
+        gh = pkg.graph.GraphBatch.from_edges(pairs[:, 0], pairs[:, 1], n)
+        assert not gh.symmetric
+        g = gh.to(dev)
+    n = g.num_nodes()
+    torch.manual_seed(n_mols)
+    mlp = torch.nn.Sequential(torch.nn.Linear(128, 64), torch.nn.ReLU(), torch.nn.Linear(64, 64))
+    x = 0.3 * torch.randn(n, 128)
+    ref = [p.detach().double().clone().requires_grad_(True) for p in mlp.parameters()]
+    xr = x.double().requires_grad_(True)
+    im = F.linear(F.relu(F.linear(xr, ref[0], ref[1])), ref[2], ref[3])
+    src, dst = gh.edges()
+    loss_r = torch.sum((im @ im.t() - _dense_adj(src, dst, n)) ** 2) / n
+    loss_r.backward()
+    mlp_d = mlp.to(dev)
+    xd = x.to(dev).requires_grad_(True)
+    loss = pkg.ops.mlp2_recon(xd, mlp_d, g)
+    (3.0 * loss).backward()  # a non-unit upstream gradient
+    assert rel_err(loss.item(), loss_r.item()) < LOSS_TOL
+    assert rel_l2(xd.grad.cpu(), 3.0 * xr.grad) < 1e-5
+    for p, r in zip(mlp_d.parameters(), ref):
+        assert rel_l2(p.grad.cpu(), 3.0 * r.grad) < 1e-5
+    # equals the unfused composition (same kernels' arithmetic up to ordering)
+    xd2 = x.to(dev).requires_grad_(True)
+    loss2 = pkg.ops.recon_adj(pkg.ops.mlp2(xd2, mlp_d), g)
+    loss2.backward()
+    assert rel_err(loss.item(), loss2.item()) < 1e-5
+    assert rel_l2(xd.grad.cpu(), 3.0 * xd2.grad.cpu()) < 1e-5
+
+
+# ---------------------------------------------------------------------------
 # Fine-tune head (Mainmodel_finetuning) vs the reference's own outputs
 # ---------------------------------------------------------------------------
 def _finetune_model(pkg, g, dev):

@@ -17,9 +17,11 @@ Differences from the reference, all deliberate:
   * the compression + attention loops, the readouts and the dense N x N
     reconstruction loss run as fused HIP kernels (ops.py);
   * randomness: the reference draws the gate/feature noise from the CPU
-    generator per graph (models.py:599, 650); here it is drawn on the device
-    in one call, or passed explicitly with ``noise=(u_gate[N], u_feat[N,64])``
-    for parity with a recorded run;
+    generator per graph (models.py:599, 650); here it is drawn inside the
+    interaction kernel (counter-based Philox4x32-10 keyed by a device
+    seed/offset, ops.noise_state / ops.seed_noise; the draws are kept in
+    ``_last_noise``), or passed explicitly with
+    ``noise=(u_gate[N], u_feat[N,64])`` for parity with a recorded run;
   * ``flatten_batch_subgraphs`` may be ``None``: the ego-nets are then built
     on the device from ``batch_g`` (scgib_egonet_*), replacing the offline
     khop_in_subgraph pass and the per-step dgl.batch of the reference;
@@ -146,6 +148,9 @@ FORK_LOSSES = os.environ.get("SCGIB_FORK_LOSSES", "0") != "0"
 LIN_IN_PAIR = os.environ.get("SCGIB_LIN_IN_PAIR", "1") != "0"
 # head MLP + adjacency recon loss as one fused op (ops.mlp2_recon)
 FUSE_RECON = os.environ.get("SCGIB_FUSE_RECON", "1") != "0"
+# gate / feature noise drawn inside the interaction kernel (counter-based
+# Philox, ops.noise_state) instead of two torch.rand launches per step
+DEVICE_NOISE = os.environ.get("SCGIB_DEVICE_NOISE", "1") != "0"
 
 
 def _side_stream(device):
@@ -182,6 +187,8 @@ class _SCGIBCore(nn.Module):
         if noise is not None:
             u_gate, u_feat = noise
             return u_gate.reshape(-1), u_feat
+        if DEVICE_NOISE and self.hidden_dim == 64:
+            return None, None  # drawn inside the interaction kernel (device Philox)
         return (torch.rand(n, device=device, dtype=torch.float32),
                 torch.rand(n, self.hidden_dim, device=device, dtype=torch.float32))
 
@@ -216,6 +223,8 @@ class _SCGIBCore(nn.Module):
                                                           enc_owner.attn_layer, batch_g,
                                                           enc_owner.training)
         enc_owner._last_kl_mean = kl_mean
+        # the in-kernel draws when noise was None (replayable via noise=)
+        enc_owner._last_noise = ops.pop_last_noise() if noise is None else None
         noisy = im[:, : self.hidden_dim]
         return im, kl, noisy, z2, z1
 

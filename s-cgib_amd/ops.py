@@ -477,8 +477,14 @@ def sum_nodes_graph(graph, x):
 def _interaction_forward(ctx, f, t, s, u_gate, u_feat, gamma, beta, w2, b2, w_att, b_att, graph,
                          bn, training):
     """Launch scgib_interaction_fwd (+ the BN running update); stores on ctx
-    what the backward needs and returns (outputs, tensors to save)."""
-    u_gate, u_feat = _f32(u_gate, "interaction"), _f32(u_feat, "interaction")
+    what the backward needs and returns (outputs, tensors to save).  With
+    u_gate = u_feat = None the noise is drawn in-kernel (device Philox,
+    scgib_interaction_fwd_rng) and written to fresh u_gate / u_feat."""
+    rng = u_gate is None
+    if rng != (u_feat is None):
+        raise _lib.ScgibError("interaction: give both noise tensors or neither")
+    if not rng:
+        u_gate, u_feat = _f32(u_gate, "interaction"), _f32(u_feat, "interaction")
     n, d = f.shape
     if d != HIDDEN:
         raise _lib.ScgibError(f"interaction kernels are built for hidden={HIDDEN}, got {d}")
@@ -506,10 +512,22 @@ def _interaction_forward(ctx, f, t, s, u_gate, u_feat, gamma, beta, w2, b2, w_at
     w_att, b_att = _f32(w_att, "w_att"), _f32(b_att, "b_att")
     rm, rv = bn.running_mean, bn.running_var
     st = _stream()
-    _lib.call("scgib_interaction_fwd", _p(f), _p(t), _p(s), _p(u_gate), _p(u_feat),
-              _p(graph.graph_ptr), B, n, _p(gamma), _p(beta), _p(rm), _p(rv), float(bn.eps),
-              int(training), _p(w2), _p(b2), _p(w_att), _p(b_att), _p(im), _p(z1), _p(z2),
-              _p(lam), _p(logit), _p(stats), _p(kl), _p(kl_mean), int(pad), st)
+    if rng:
+        u_gate = torch.empty(n, dtype=torch.float32, device=dev)
+        u_feat = torch.empty(n, HIDDEN, dtype=torch.float32, device=dev)
+        _lib.call("scgib_interaction_fwd_rng", _p(f), _p(t), _p(s), _p(u_gate), _p(u_feat),
+                  _p(noise_state(dev)), _p(counters(dev, "interaction_rng", 1)),
+                  _p(graph.graph_ptr), B, n, _p(gamma), _p(beta), _p(rm), _p(rv), float(bn.eps),
+                  int(training), _p(w2), _p(b2), _p(w_att), _p(b_att), _p(im), _p(z1), _p(z2),
+                  _p(lam), _p(logit), _p(stats), _p(kl), _p(kl_mean), int(pad), st)
+    else:
+        _lib.call("scgib_interaction_fwd", _p(f), _p(t), _p(s), _p(u_gate), _p(u_feat),
+                  _p(graph.graph_ptr), B, n, _p(gamma), _p(beta), _p(rm), _p(rv), float(bn.eps),
+                  int(training), _p(w2), _p(b2), _p(w_att), _p(b_att), _p(im), _p(z1), _p(z2),
+                  _p(lam), _p(logit), _p(stats), _p(kl), _p(kl_mean), int(pad), st)
+    if rng:
+        global _LAST_NOISE
+        _LAST_NOISE = (u_gate, u_feat)
     if training and bn.track_running_stats:
         nbt = bn.num_batches_tracked
         # B sequential momentum updates in closed form; nothing in the step
@@ -706,6 +724,47 @@ def counters(device, key, n):
         off, size = used, n
         _COUNTER_RANGES[rk] = (off, size)
     return buf[off: off + n]
+
+
+# ---------------------------------------------------------------------------
+# Device noise state: {seed, offset} (int64) per device for the in-kernel
+# Philox draws of the interaction; the kernel advances the offset itself, so
+# a captured step draws fresh noise on every replay.
+# ---------------------------------------------------------------------------
+_NOISE_STATES = {}
+
+
+def noise_state(device):
+    """The device's noise state; created on first use with a seed drawn from
+    torch's default CPU generator (reproducible under torch.manual_seed).
+    Create it outside graph capture (any eager step does)."""
+    idx = torch.device(device).index or 0
+    st = _NOISE_STATES.get(idx)
+    if st is None:
+        if torch.cuda.is_current_stream_capturing():
+            raise _lib.ScgibError("device noise state must be created outside graph capture "
+                                  "(run one eager step or call ops.seed_noise first)")
+        seed = int(torch.randint(0, 2 ** 62, (1,)).item())
+        st = _NOISE_STATES[idx] = torch.tensor([seed, 0], dtype=torch.int64, device=device)
+    return st
+
+
+def seed_noise(device, seed, offset=0):
+    """Reset the device noise stream (seed, offset) in place."""
+    st = noise_state(device)
+    st.copy_(torch.tensor([int(seed), int(offset)], dtype=torch.int64))
+    return st
+
+
+_LAST_NOISE = None
+
+
+def pop_last_noise():
+    """(u_gate [N], u_feat [N, 64]) drawn in-kernel by the latest interaction
+    launch (None if that launch was given its noise); clears it."""
+    global _LAST_NOISE
+    out, _LAST_NOISE = _LAST_NOISE, None
+    return out
 
 
 # ---------------------------------------------------------------------------

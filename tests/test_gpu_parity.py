@@ -728,3 +728,49 @@ def test_csr_cache_batches_egonets_bit_exact(pkg, dev, tmp_path):
     for g, _, _ in c.batches(128, seed=2):
         for k in (1, 2):
             _check_ego(pkg, g, k, dev)
+
+
+# ---------------------------------------------------------------------------
+# Device noise (noise=None): in-kernel Philox draws
+# ---------------------------------------------------------------------------
+def test_device_noise_replays_through_explicit_path(pkg, dev):
+    """noise=None draws U[0,1) gate/feature noise in the interaction kernel;
+    feeding the recorded draws back through noise= gives the same losses and
+    gradients (to fp32 contraction order: the two kernel instances may fuse
+    the noise multiply-add differently), every launch draws fresh noise, and
+    re-seeding reproduces a draw bitwise."""
+    import copy
+    from types import SimpleNamespace
+    g, _ = rand_graph(pkg, 64, "qm9", 9, dev)
+    x = F.normalize(g.ndata["x"].float())
+    args = SimpleNamespace(recons_type="adj", useAtt=1, readout_f="sum", d_transfer=32,
+                           batch_size=64, gin_layers=5)
+    torch.manual_seed(3)
+    m1 = pkg.models.Mainmodel(args, 11, 64, 4, 4, 1, "GIN").to(dev).train()
+    m2 = copy.deepcopy(m1)
+    pkg.ops.seed_noise(dev, 1234)
+    _, kl, con, rec = m1(g, x, None, None, None, 1, None, 1, dev, 64)
+    (kl + con + rec).backward()
+    ug, uf = m1._last_noise
+    n = g.num_nodes()
+    assert ug.shape == (n,) and uf.shape == (n, 64)
+    for u in (ug, uf):
+        uc = u.cpu()
+        assert float(uc.min()) >= 0.0 and float(uc.max()) < 1.0
+    ufc = uf.cpu().double()
+    assert abs(float(ufc.mean()) - 0.5) < 0.01 and abs(float(ufc.var()) - 1 / 12) < 0.005
+    _, kl2, con2, rec2 = m2(g, x, None, None, None, 1, None, 1, dev, 64, noise=(ug.clone(), uf.clone()))
+    (kl2 + con2 + rec2).backward()
+    for a, b in ((kl, kl2), (con, con2), (rec, rec2)):
+        assert rel_err(a.item(), b.item()) < 1e-6
+    p2 = dict(m2.named_parameters())
+    ref = {k: p2[k].grad.detach().double().cpu() for k, p in m1.named_parameters()
+           if p.grad is not None}
+    mine = dict(m1.named_parameters())
+    check_grads_model(ref, lambda k: mine[k].grad, tol=1e-5)
+    # the offset advanced: a second draw differs; re-seeding reproduces the first
+    m1(g, x, None, None, None, 1, None, 1, dev, 64)
+    assert not torch.equal(m1._last_noise[1], uf)
+    pkg.ops.seed_noise(dev, 1234)
+    m1(g, x, None, None, None, 1, None, 1, dev, 64)
+    assert torch.equal(m1._last_noise[1], uf) and torch.equal(m1._last_noise[0], ug)

@@ -262,23 +262,15 @@ int scgib_interaction_fwd(const float *f, const float *t, const float *s,
                           float *logit, float *stats, float *kl_tensor, float *kl_mean,
                           int32_t pad_rows, scgib_stream_t stream);
 
-/* scgib_interaction_fwd with the noise drawn in-kernel instead of read: the
- * reference's torch.rand gate / feature draws (models.py:599, :650) become
- * counter-based Philox4x32-10 uniforms in [0, 1) keyed by rng_state[0]
- * (seed) and rng_state[1] (offset, uint64, device); u_gate [N] and
- * u_feat [N][64] are OUTPUTS (the draws; the backward reads u_feat).  The
- * last workgroup advances rng_state[1] by one, so every launch / graph replay
- * draws fresh noise.  counter: one zeroed uint32, left zero. */
-int scgib_interaction_fwd_rng(const float *f, const float *t, const float *s, float *u_gate,
-                              float *u_feat, uint64_t *rng_state, uint32_t *counter,
-                              const int32_t *graph_ptr, int64_t n_graphs, int64_t n_nodes,
-                              const float *bn_gamma, const float *bn_beta,
-                              const float *bn_running_mean, const float *bn_running_var,
-                              float bn_eps, int32_t training, const float *w2, const float *b2,
-                              const float *w_att, const float *b_att, float *im, float *z1,
-                              float *z2, float *lam, float *logit, float *stats,
-                              float *kl_tensor, float *kl_mean, int32_t pad_rows,
-                              scgib_stream_t stream);
+/* Device noise for the interaction (replaces the reference's torch.rand gate
+ * draw u [n,1], models.py:599, and feature draw u [n,64], :650, when no noise
+ * is given): counter-based Philox4x32-10 uniforms in [0, 1) keyed by
+ * rng_state[0] (seed) and rng_state[1] (offset; uint64, device) -> u_gate
+ * [n_rows], u_feat [n_rows][64], passed to scgib_interaction_fwd as noise.
+ * The last workgroup advances rng_state[1] by one, so every launch / graph
+ * replay draws fresh noise.  counter: one zeroed uint32, left zero. */
+int scgib_noise_uniform(float *u_gate, float *u_feat, int64_t n_rows, uint64_t *rng_state,
+                        uint32_t *counter, scgib_stream_t stream);
 
 /* Sequential running-stat update of the per-graph compressor BatchNorm: one
  * nn.BatchNorm1d call per graph in graph order (models.py:642 inside the loop

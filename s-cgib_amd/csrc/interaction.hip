@@ -96,23 +96,15 @@ __device__ __forceinline__ float gate_lambda(float u, float p) {
     return 1.f / (1.f + expf(-(g + p)));
 }
 
-struct Lanes {
-    int q, c4, ch;  // row group, channel quad, first channel
-};
-
-__device__ __forceinline__ Lanes lanes() {
-    const int l = threadIdx.x & 63;
-    return {l >> 4, l & 15, (l & 15) * 4};
-}
-
-// Device noise (RNG = true, pretraining with noise=None): the reference's
-// torch.rand draws (gate u [n,1], models.py:599; feature u [n,64], :650) are
-// replaced by counter-based Philox4x32-10 uniforms keyed by a device seed and
-// a per-launch offset (NoiseGen): gate of row r = stream 16 of counter
-// (r, 16, offset), channels 4c..4c+3 = stream c of (r, c, offset).  The draws
-// are written to u_gate / u_feat (the backward reads u_feat; tests replay
-// them through the explicit-noise path).  The last workgroup to finish
-// advances the offset, so every launch and graph replay draws fresh noise.
+// Device noise (pretraining with noise=None): the reference's torch.rand
+// draws (gate u [n,1], models.py:599; feature u [n,64], :650) are replaced by
+// counter-based Philox4x32-10 uniforms keyed by a device seed and a per-launch
+// offset (NoiseGen): gate of row r = word 0 of counter (r, 16, offset),
+// channels 4c..4c+3 = counter (r, c, offset).  noise_uniform_k writes them to
+// u_gate / u_feat, which the interaction then reads like explicit noise; it
+// runs on the core encoder's stream, off the critical path.  Its last
+// workgroup advances the offset, so every launch / graph replay draws fresh
+// noise.
 struct NoiseGen {
     uint32_t key0, key1, off0, off1;
 };
@@ -141,11 +133,41 @@ __device__ __forceinline__ float4 noise_feat(const NoiseGen &ng, int64_t r, int 
     return make_float4(u01(v.x), u01(v.y), u01(v.z), u01(v.w));
 }
 
-template <bool RNG>
-__device__ __forceinline__ void interaction_fwd_body(
+
+// one thread per (row, channel quad); 256 threads = 16 rows per workgroup
+__global__ __launch_bounds__(256) void noise_uniform_k(float *__restrict__ u_gate,
+                                                       float *__restrict__ u_feat, int64_t n,
+                                                       uint64_t *__restrict__ rng,
+                                                       unsigned *__restrict__ cnt) {
+    const uint64_t seed = rng[0];
+    const uint64_t off = __hip_atomic_load(rng + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const NoiseGen ng{static_cast<uint32_t>(seed), static_cast<uint32_t>(seed >> 32),
+                      static_cast<uint32_t>(off), static_cast<uint32_t>(off >> 32)};
+    const int64_t r = static_cast<int64_t>(blockIdx.x) * 16 + (threadIdx.x >> 4);
+    const int c4 = threadIdx.x & 15;
+    if (r < n) {
+        st4(u_feat + r * 64 + 4 * c4, noise_feat(ng, r, c4));
+        if (c4 == 0) u_gate[r] = noise_gate(ng, r);
+    }
+    // every workgroup has read the offset: the last one advances it
+    if (block_arrive(cnt, gridDim.x) && threadIdx.x == 0) {
+        __hip_atomic_store(rng + 1, off + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        *cnt = 0u;
+    }
+}
+
+struct Lanes {
+    int q, c4, ch;  // row group, channel quad, first channel
+};
+
+__device__ __forceinline__ Lanes lanes() {
+    const int l = threadIdx.x & 63;
+    return {l >> 4, l & 15, (l & 15) * 4};
+}
+
+__global__ __launch_bounds__(64) void interaction_fwd_k(
     const float *__restrict__ f, const float *__restrict__ t, const float *__restrict__ s,
     const float *__restrict__ u_gate, const float *__restrict__ u_feat,
-    float *__restrict__ u_gate_out, float *__restrict__ u_feat_out, const NoiseGen &ng,
     const int32_t *__restrict__ gptr, int64_t B, const float *__restrict__ gamma,
     const float *__restrict__ beta, const float *__restrict__ rmean,
     const float *__restrict__ rvar, float bn_eps, int training, const float *__restrict__ w2,
@@ -161,10 +183,6 @@ __device__ __forceinline__ void interaction_fwd_body(
         for (int64_t r = r_beg + (gi - B); r < n_rows_cap; r += gridDim.x - B) {
             if (threadIdx.x < 32) st4(im + r * 128 + threadIdx.x * 4, f4(0.f));
             if (threadIdx.x == 0) { lam[r] = 0.f; logit[r] = 0.f; }
-            if (RNG) {
-                if (threadIdx.x < 16) st4(u_feat_out + r * 64 + threadIdx.x * 4, f4(0.f));
-                if (threadIdx.x == 0) u_gate_out[r] = 0.f;
-            }
         }
         return;
     }
@@ -233,22 +251,8 @@ __device__ __forceinline__ void interaction_fwd_body(
             const int64_t r = cb + L.q + 4 * j, rr = r < r1 ? r : r0;
             tv[j] = ld4(t + rr * 64 + L.ch);
             fv[j] = ld4(f + rr * 64 + L.ch);
-            if (!RNG) {
-                uv[j] = ld4(u_feat + rr * 64 + L.ch);
-                ug[j] = u_gate[rr];
-            }
-        }
-        if (RNG) {  // device noise: computed while the loads are in flight
-#pragma unroll
-            for (int j = 0; j < CH; ++j) {
-                const int64_t r = cb + L.q + 4 * j;
-                uv[j] = noise_feat(ng, r, L.c4);
-                ug[j] = noise_gate(ng, r);
-                if (r < r1) {
-                    st4(u_feat_out + r * 64 + L.ch, uv[j]);
-                    if (L.c4 == 0) u_gate_out[r] = ug[j];
-                }
-            }
+            uv[j] = ld4(u_feat + rr * 64 + L.ch);
+            ug[j] = u_gate[rr];
         }
 #pragma unroll
         for (int j = 0; j < CH; ++j) {
@@ -279,7 +283,7 @@ __device__ __forceinline__ void interaction_fwd_body(
                 const int64_t r = cb + L.q + 4 * j, rr = r < r1 ? r : r0;
                 tv[j] = ld4(t + rr * 64 + L.ch);
                 fv[j] = ld4(f + rr * 64 + L.ch);
-                ug[j] = RNG ? noise_gate(ng, rr) : u_gate[rr];
+                ug[j] = u_gate[rr];
             }
 #pragma unroll
             for (int j = 0; j < CH; ++j) {
@@ -300,7 +304,7 @@ __device__ __forceinline__ void interaction_fwd_body(
             for (int j = 0; j < CH; ++j) {
                 const int64_t r = cb + L.q + 4 * j, rr = r < r1 ? r : r0;
                 tv[j] = ld4(t + rr * 64 + L.ch);
-                ug[j] = RNG ? noise_gate(ng, rr) : u_gate[rr];
+                ug[j] = u_gate[rr];
             }
 #pragma unroll
             for (int j = 0; j < CH; ++j) {
@@ -374,44 +378,6 @@ __device__ __forceinline__ void interaction_fwd_body(
         sl[kStSoftMax] = M;
         sl[kStSoftSum] = S;
         sl[kStConst] = cst;
-    }
-}
-
-#define SCGIB_INTERACTION_FWD_PARAMS                                                           \
-    const int32_t *__restrict__ gptr, int64_t B, const float *__restrict__ gamma,              \
-        const float *__restrict__ beta, const float *__restrict__ rmean,                       \
-        const float *__restrict__ rvar, float bn_eps, int training,                            \
-        const float *__restrict__ w2, const float *__restrict__ b2p,                           \
-        const float *__restrict__ watt, const float *__restrict__ battp, float *__restrict__ im, \
-        float *__restrict__ z1, float *__restrict__ z2, float *__restrict__ lam,                \
-        float *__restrict__ logit, float *__restrict__ stats, float *__restrict__ kl,          \
-        float *__restrict__ kl_mean, int64_t n_rows_cap, int pad
-#define SCGIB_INTERACTION_FWD_ARGS \
-    gptr, B, gamma, beta, rmean, rvar, bn_eps, training, w2, b2p, watt, battp, im, z1, z2, lam, \
-        logit, stats, kl, kl_mean, n_rows_cap, pad
-
-__global__ __launch_bounds__(64) void interaction_fwd_k(
-    const float *__restrict__ f, const float *__restrict__ t, const float *__restrict__ s,
-    const float *__restrict__ u_gate, const float *__restrict__ u_feat, SCGIB_INTERACTION_FWD_PARAMS) {
-    interaction_fwd_body<false>(f, t, s, u_gate, u_feat, nullptr, nullptr, NoiseGen{},
-                                SCGIB_INTERACTION_FWD_ARGS);
-}
-
-// rng = {seed, offset} (uint64, device); cnt: one zeroed uint32, left zero
-__global__ __launch_bounds__(64) void interaction_fwd_rng_k(
-    const float *__restrict__ f, const float *__restrict__ t, const float *__restrict__ s,
-    float *__restrict__ u_gate, float *__restrict__ u_feat, uint64_t *__restrict__ rng,
-    unsigned *__restrict__ cnt, SCGIB_INTERACTION_FWD_PARAMS) {
-    const uint64_t seed = rng[0];
-    const uint64_t off = __hip_atomic_load(rng + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const NoiseGen ng{static_cast<uint32_t>(seed), static_cast<uint32_t>(seed >> 32),
-                      static_cast<uint32_t>(off), static_cast<uint32_t>(off >> 32)};
-    interaction_fwd_body<true>(f, t, s, nullptr, nullptr, u_gate, u_feat, ng,
-                               SCGIB_INTERACTION_FWD_ARGS);
-    // every workgroup has read the offset: the last one advances it
-    if (block_arrive(cnt, gridDim.x) && threadIdx.x == 0) {
-        __hip_atomic_store(rng + 1, off + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        *cnt = 0u;
     }
 }
 
@@ -720,28 +686,15 @@ extern "C" int scgib_interaction_fwd(
     return launch_status();
 }
 
-extern "C" int scgib_interaction_fwd_rng(
-    const float *f, const float *t, const float *s, float *u_gate, float *u_feat,
-    uint64_t *rng_state, uint32_t *counter, const int32_t *graph_ptr, int64_t n_graphs,
-    int64_t n_nodes, const float *bn_gamma, const float *bn_beta, const float *bn_running_mean,
-    const float *bn_running_var, float bn_eps, int32_t training, const float *w2,
-    const float *b2, const float *w_att, const float *b_att, float *im, float *z1, float *z2,
-    float *lam, float *logit, float *stats, float *kl_tensor, float *kl_mean, int32_t pad_rows,
-    scgib_stream_t stream) {
-    if (n_graphs < 0 || n_nodes < 0) return SCGIB_EINVAL;
-    if (n_graphs == 0) return SCGIB_OK;
-    if (n_graphs > 0x7fffffff || n_nodes > 0xffffffffLL) return SCGIB_EUNSUPPORTED;
-    if (!graph_ptr || !bn_gamma || !bn_beta || !w2 || !b2 || !w_att || !b_att || !z1 ||
-        !z2 || !stats || (!kl_tensor && !kl_mean) || !rng_state || !counter)
-        return SCGIB_EINVAL;
-    if (n_nodes > 0 && (!f || !t || !s || !u_gate || !u_feat || !im || !lam || !logit))
-        return SCGIB_EINVAL;
-    if (!training && (!bn_running_mean || !bn_running_var)) return SCGIB_EINVAL;
-    const unsigned grid = static_cast<unsigned>(n_graphs + (pad_rows ? 64 : 0));
-    interaction_fwd_rng_k<<<dim3(grid), 64, 0, as_stream(stream)>>>(
-        f, t, s, u_gate, u_feat, rng_state, counter, graph_ptr, n_graphs, bn_gamma, bn_beta,
-        bn_running_mean, bn_running_var, bn_eps, training, w2, b2, w_att, b_att, im, z1, z2, lam,
-        logit, stats, kl_tensor, kl_mean, n_nodes, pad_rows);
+extern "C" int scgib_noise_uniform(float *u_gate, float *u_feat, int64_t n_rows,
+                                   uint64_t *rng_state, uint32_t *counter,
+                                   scgib_stream_t stream) {
+    if (n_rows < 0) return SCGIB_EINVAL;
+    if (n_rows == 0) return SCGIB_OK;
+    if (!u_gate || !u_feat || !rng_state || !counter) return SCGIB_EINVAL;
+    if (n_rows > 0xffffffffLL) return SCGIB_EUNSUPPORTED;
+    noise_uniform_k<<<dim3(static_cast<unsigned>((n_rows + 15) / 16)), 256, 0, as_stream(stream)>>>(
+        u_gate, u_feat, n_rows, rng_state, counter);
     return launch_status();
 }
 

@@ -17,9 +17,9 @@ Differences from the reference, all deliberate:
   * the compression + attention loops, the readouts and the dense N x N
     reconstruction loss run as fused HIP kernels (ops.py);
   * randomness: the reference draws the gate/feature noise from the CPU
-    generator per graph (models.py:599, 650); here it is drawn inside the
-    interaction kernel (counter-based Philox4x32-10 keyed by a device
-    seed/offset, ops.noise_state / ops.seed_noise; the draws are kept in
+    generator per graph (models.py:599, 650); here it is drawn on the device
+    (counter-based Philox4x32-10 keyed by a device seed/offset,
+    ops.device_noise / ops.seed_noise; the draws are kept in
     ``_last_noise``), or passed explicitly with
     ``noise=(u_gate[N], u_feat[N,64])`` for parity with a recorded run;
   * ``flatten_batch_subgraphs`` may be ``None``: the ego-nets are then built
@@ -148,8 +148,8 @@ FORK_LOSSES = os.environ.get("SCGIB_FORK_LOSSES", "0") != "0"
 LIN_IN_PAIR = os.environ.get("SCGIB_LIN_IN_PAIR", "1") != "0"
 # head MLP + adjacency recon loss as one fused op (ops.mlp2_recon)
 FUSE_RECON = os.environ.get("SCGIB_FUSE_RECON", "1") != "0"
-# gate / feature noise drawn inside the interaction kernel (counter-based
-# Philox, ops.noise_state) instead of two torch.rand launches per step
+# gate / feature noise drawn by one Philox kernel (ops.device_noise) on the
+# core encoder's chain instead of two torch.rand launches on the critical path
 DEVICE_NOISE = os.environ.get("SCGIB_DEVICE_NOISE", "1") != "0"
 
 
@@ -188,28 +188,31 @@ class _SCGIBCore(nn.Module):
             u_gate, u_feat = noise
             return u_gate.reshape(-1), u_feat
         if DEVICE_NOISE and self.hidden_dim == 64:
-            return None, None  # drawn inside the interaction kernel (device Philox)
+            return ops.device_noise(n, device)  # Philox on the device, one launch
         return (torch.rand(n, device=device, dtype=torch.float32),
                 torch.rand(n, self.hidden_dim, device=device, dtype=torch.float32))
 
     def _extract(self, enc_owner, batch_g, batch_x, ego, x_subs, noise, encoded=None):
         """extract_features of ``enc_owner`` (models.py:702-750); returns the
         reference's 4-tuple plus z1 = sum_nodes(noisy) (computed in-kernel).
-        ``encoded`` = (graph_features, subgraphs_features, sub_readout[, t]) when
-        the encoders already ran (_encode_forked); t = compressor[0](graph
-        features) when the encoder pair computed it."""
-        t = None
+        ``encoded`` = (graph_features, subgraphs_features, sub_readout, t, drawn)
+        when the encoders already ran (_encode_forked); t = compressor[0](graph
+        features) and drawn = the device noise when the encoder pair's core
+        chain computed them (else None)."""
+        t = drawn = None
         if encoded is None:
             graph_features = enc_owner.Encoder1(batch_g, batch_x)
             subgraphs_features = enc_owner.Encoder2(ego, x_subs)
             sub_readout = ops.segment_sum(subgraphs_features, ego.graph_ptr, ego.batch_size,
                                           ego.seg_dims)
         else:
-            graph_features, subgraphs_features, sub_readout = encoded[:3]
-            t = encoded[3] if len(encoded) > 3 else None
+            graph_features, subgraphs_features, sub_readout, t, drawn = encoded
         enc_owner.graph_features = graph_features
         enc_owner.subgraphs_features = subgraphs_features
-        u_gate, u_feat = self._noise(graph_features.shape[0], graph_features.device, noise)
+        if noise is None and drawn is not None:  # drawn on the core encoder's chain
+            u_gate, u_feat = drawn
+        else:
+            u_gate, u_feat = self._noise(graph_features.shape[0], graph_features.device, noise)
         # compressor[0] (models.py:1092) runs fused in front of the interaction
         if t is not None:
             comp = enc_owner.compressor
@@ -223,12 +226,12 @@ class _SCGIBCore(nn.Module):
                                                           enc_owner.attn_layer, batch_g,
                                                           enc_owner.training)
         enc_owner._last_kl_mean = kl_mean
-        # the in-kernel draws when noise was None (replayable via noise=)
-        enc_owner._last_noise = ops.pop_last_noise() if noise is None else None
+        # the draws when noise was None (replayable via noise=)
+        enc_owner._last_noise = (u_gate, u_feat) if noise is None else None
         noisy = im[:, : self.hidden_dim]
         return im, kl, noisy, z2, z1
 
-    def _encode_forked(self, enc_owner, batch_g, batch_x, fork=True):
+    def _encode_forked(self, enc_owner, batch_g, batch_x, fork=True, draw_noise=False):
         """Fast path of forward() when the ego-nets are built on the device:
         the ego branch (ego-net build, x_subs gather, transfer_d, Encoder2,
         readout) runs on a second HIP stream, concurrently with Encoder1 on the
@@ -251,16 +254,22 @@ class _SCGIBCore(nn.Module):
             with torch.cuda.stream(side):
                 ego = G.egonet_batch(batch_g, self.k_transition)
             lin0 = enc_owner.compressor[0] if LIN_IN_PAIR else None
+            drawn = {}
+            tail = None
+            if draw_noise and DEVICE_NOISE and self.hidden_dim == 64:
+                def tail():  # the interaction's noise, drawn beside the ego chain
+                    drawn["u"] = ops.device_noise(batch_g.num_nodes(), batch_x.device)
             outs = ops.gin_encoder_pair_x(
                 batch_x, ego, enc_owner.Encoder2, batch_g, enc_owner.Encoder1, self.transfer_d,
-                ego.ndata["_ID"], side, lin0)
+                ego.ndata["_ID"], side, lin0, tail)
             subgraphs_features, graph_features = outs[0], outs[1]
+            t = outs[2] if len(outs) > 2 else None
             with torch.cuda.stream(side):
                 sub_readout = ops.segment_sum(subgraphs_features, ego.graph_ptr, ego.batch_size,
                                               ego.seg_dims)
             main.wait_stream(side)
             sub_readout.record_stream(main)
-            return ego, (graph_features, subgraphs_features, sub_readout, *outs[2:])
+            return ego, (graph_features, subgraphs_features, sub_readout, t, drawn.get("u"))
         with torch.cuda.stream(side):
             if fold:
                 ego = G.egonet_batch(batch_g, self.k_transition)
@@ -279,7 +288,7 @@ class _SCGIBCore(nn.Module):
         main.wait_stream(side)
         subgraphs_features.record_stream(main)
         sub_readout.record_stream(main)
-        return ego, (graph_features, subgraphs_features, sub_readout)
+        return ego, (graph_features, subgraphs_features, sub_readout, None, None)
 
     def _losses(self, batch_g, im, kl_mean, z1, z2, mlp, batch_size, batch_logMs=None):
         # the contrastive loss needs only the two readouts: on the side stream
@@ -364,7 +373,8 @@ class Mainmodel(_SCGIBCore):
                 batch_size=16, noise=None):
         self.batch_size = batch_size
         if flatten_batch_subgraphs is None and x_subs is None and batch_x.is_cuda:
-            ego, enc = self._encode_forked(self, batch_g, batch_x, FORK_ENCODERS)
+            ego, enc = self._encode_forked(self, batch_g, batch_x, FORK_ENCODERS,
+                                           noise is None)
             im, _, _, z2, z1 = self._extract(self, batch_g, None, ego, None, noise, enc)
             self._last_z1 = z1
         else:
@@ -440,7 +450,8 @@ class Mainmodel_continue(_SCGIBCore):
         self.batch_size = batch_size
         if flatten_batch_subgraphs is None and x_subs is None and batch_x.is_cuda:
             # the wrapper's transfer_d feeds the wrapped model's encoders
-            ego, enc = self._encode_forked(self.model, batch_g, batch_x, FORK_ENCODERS)
+            ego, enc = self._encode_forked(self.model, batch_g, batch_x, FORK_ENCODERS,
+                                           noise is None)
             im, _, _, z2, z1 = self.model._extract(self.model, batch_g, None, ego, None, noise,
                                                    enc)
             self.model._last_z1 = z1
@@ -538,7 +549,8 @@ class Mainmodel_domainadapt(_SCGIBCore):
         if flatten_batch_subgraphs is None and x_subs is None and batch_x.is_cuda:
             # this model's transfer_d feeds the pretrained model's encoders
             # (folded into their first layers), ego branch forked
-            ego, enc = self._encode_forked(inner, batch_g, batch_x, FORK_ENCODERS)
+            ego, enc = self._encode_forked(inner, batch_g, batch_x, FORK_ENCODERS,
+                                           noise is None)
             im = inner._extract(inner, batch_g, None, ego, None, noise, enc)[0]
         else:
             if flatten_batch_subgraphs is None:

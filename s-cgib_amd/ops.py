@@ -347,7 +347,8 @@ class _GinEncoderPair(torch.autograd.Function):
     overlap in both directions; d Wt = d Wt(ego) + d Wt(core)."""
 
     @staticmethod
-    def forward(ctx, x, wt, w0, b0, nmap, ego, core, gin_ego, gin_core, training, side, *params):
+    def forward(ctx, x, wt, w0, b0, nmap, ego, core, gin_ego, gin_core, training, side, core_tail,
+                *params):
         main = _torch_stream()
         ne = 6 * len(gin_ego.ginlayers)
         ctx.sub = (_Ctx(), _Ctx())
@@ -370,6 +371,8 @@ class _GinEncoderPair(torch.autograd.Function):
             ctx.lin_saved = (f, w0)
             ctx.core_dims = core.dims
             outs = (s, f, t)
+        if core_tail is not None:  # extra non-differentiable work on the core chain
+            core_tail()
         main.wait_stream(side)
         s.record_stream(main)
         return outs
@@ -410,19 +413,23 @@ class _GinEncoderPair(torch.autograd.Function):
         if g_t is not None:
             g_t.record_stream(side)
         dwt = ge[5] + gc[5]
-        return (None, dwt, dw0, db0, None, None, None, None, None, None, None, *ge[7:], *gc[7:])
+        return (None, dwt, dw0, db0, None, None, None, None, None, None, None, None, *ge[7:],
+                *gc[7:])
 
 
 def _torch_stream():
     return torch.cuda.current_stream()
 
 
-def gin_encoder_pair_x(x, ego, gin_ego, core, gin_core, transfer, node_map, side, lin0=None):
+def gin_encoder_pair_x(x, ego, gin_ego, core, gin_core, transfer, node_map, side, lin0=None,
+                       core_tail=None):
     """(gin_ego(ego, transfer(x[node_map])), gin_core(core, transfer(x))) —
     the two encoders of Mainmodel.forward with transfer_d folded, the ego
     chain on stream ``side`` (forward and backward).  With ``lin0`` (the
     compressor's Linear(64, 64), models.py:596) also returns
-    t = lin0(gin_core(...)), computed at the end of the core chain."""
+    t = lin0(gin_core(...)), computed at the end of the core chain;
+    ``core_tail()`` (non-differentiable, e.g. the noise draw) runs there too,
+    before the join."""
     if ego.num_nodes() == 0 or core.num_nodes() == 0:
         raise _lib.ScgibError("gin_encoder on an empty graph")
     if transfer.bias is not None or transfer.weight.shape != (32, x.shape[1]) \
@@ -434,7 +441,7 @@ def gin_encoder_pair_x(x, ego, gin_ego, core, gin_core, transfer, node_map, side
         raise _lib.ScgibError("gin_encoder_pair_x: encoders in different train/eval modes")
     w0, b0 = (lin0.weight, lin0.bias) if lin0 is not None else (None, None)
     return _GinEncoderPair.apply(x, transfer.weight, w0, b0, node_map, ego, core, gin_ego,
-                                 gin_core, bool(gin_core.training), side,
+                                 gin_core, bool(gin_core.training), side, core_tail,
                                  *_gin_layer_params(gin_ego), *_gin_layer_params(gin_core))
 
 
@@ -477,14 +484,8 @@ def sum_nodes_graph(graph, x):
 def _interaction_forward(ctx, f, t, s, u_gate, u_feat, gamma, beta, w2, b2, w_att, b_att, graph,
                          bn, training):
     """Launch scgib_interaction_fwd (+ the BN running update); stores on ctx
-    what the backward needs and returns (outputs, tensors to save).  With
-    u_gate = u_feat = None the noise is drawn in-kernel (device Philox,
-    scgib_interaction_fwd_rng) and written to fresh u_gate / u_feat."""
-    rng = u_gate is None
-    if rng != (u_feat is None):
-        raise _lib.ScgibError("interaction: give both noise tensors or neither")
-    if not rng:
-        u_gate, u_feat = _f32(u_gate, "interaction"), _f32(u_feat, "interaction")
+    what the backward needs and returns (outputs, tensors to save)."""
+    u_gate, u_feat = _f32(u_gate, "interaction"), _f32(u_feat, "interaction")
     n, d = f.shape
     if d != HIDDEN:
         raise _lib.ScgibError(f"interaction kernels are built for hidden={HIDDEN}, got {d}")
@@ -512,22 +513,10 @@ def _interaction_forward(ctx, f, t, s, u_gate, u_feat, gamma, beta, w2, b2, w_at
     w_att, b_att = _f32(w_att, "w_att"), _f32(b_att, "b_att")
     rm, rv = bn.running_mean, bn.running_var
     st = _stream()
-    if rng:
-        u_gate = torch.empty(n, dtype=torch.float32, device=dev)
-        u_feat = torch.empty(n, HIDDEN, dtype=torch.float32, device=dev)
-        _lib.call("scgib_interaction_fwd_rng", _p(f), _p(t), _p(s), _p(u_gate), _p(u_feat),
-                  _p(noise_state(dev)), _p(counters(dev, "interaction_rng", 1)),
-                  _p(graph.graph_ptr), B, n, _p(gamma), _p(beta), _p(rm), _p(rv), float(bn.eps),
-                  int(training), _p(w2), _p(b2), _p(w_att), _p(b_att), _p(im), _p(z1), _p(z2),
-                  _p(lam), _p(logit), _p(stats), _p(kl), _p(kl_mean), int(pad), st)
-    else:
-        _lib.call("scgib_interaction_fwd", _p(f), _p(t), _p(s), _p(u_gate), _p(u_feat),
-                  _p(graph.graph_ptr), B, n, _p(gamma), _p(beta), _p(rm), _p(rv), float(bn.eps),
-                  int(training), _p(w2), _p(b2), _p(w_att), _p(b_att), _p(im), _p(z1), _p(z2),
-                  _p(lam), _p(logit), _p(stats), _p(kl), _p(kl_mean), int(pad), st)
-    if rng:
-        global _LAST_NOISE
-        _LAST_NOISE = (u_gate, u_feat)
+    _lib.call("scgib_interaction_fwd", _p(f), _p(t), _p(s), _p(u_gate), _p(u_feat),
+              _p(graph.graph_ptr), B, n, _p(gamma), _p(beta), _p(rm), _p(rv), float(bn.eps),
+              int(training), _p(w2), _p(b2), _p(w_att), _p(b_att), _p(im), _p(z1), _p(z2),
+              _p(lam), _p(logit), _p(stats), _p(kl), _p(kl_mean), int(pad), st)
     if training and bn.track_running_stats:
         nbt = bn.num_batches_tracked
         # B sequential momentum updates in closed form; nothing in the step
@@ -727,11 +716,11 @@ def counters(device, key, n):
 
 
 # ---------------------------------------------------------------------------
-# Device noise state: {seed, offset} (int64) per device for the in-kernel
-# Philox draws of the interaction; the kernel advances the offset itself, so
-# a captured step draws fresh noise on every replay.
+# Device noise: {seed, offset} (int64) per device for the Philox draws of
+# scgib_noise_uniform; the kernel advances the offset itself, so a captured
+# step draws fresh noise on every replay.
 # ---------------------------------------------------------------------------
-_NOISE_STATES = {}
+_NOISE_STATES = {}  # device index -> int64 [seed, offset]
 
 
 def noise_state(device):
@@ -756,15 +745,14 @@ def seed_noise(device, seed, offset=0):
     return st
 
 
-_LAST_NOISE = None
-
-
-def pop_last_noise():
-    """(u_gate [N], u_feat [N, 64]) drawn in-kernel by the latest interaction
-    launch (None if that launch was given its noise); clears it."""
-    global _LAST_NOISE
-    out, _LAST_NOISE = _LAST_NOISE, None
-    return out
+def device_noise(n, device):
+    """(u_gate [n], u_feat [n, 64]) ~ U[0, 1) drawn on the current stream by
+    scgib_noise_uniform from the device's noise state."""
+    u_gate = torch.empty(n, dtype=torch.float32, device=device)
+    u_feat = torch.empty(n, HIDDEN, dtype=torch.float32, device=device)
+    _lib.call("scgib_noise_uniform", _p(u_gate), _p(u_feat), n, _p(noise_state(device)),
+              _p(counters(device, "noise", 1)), _stream())
+    return u_gate, u_feat
 
 
 # ---------------------------------------------------------------------------

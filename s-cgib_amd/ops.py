@@ -39,6 +39,10 @@ _AUX_STREAMS = {}
 DEFER_BN = os.environ.get("SCGIB_DEFER_BN", "1") != "0"
 DEFER_BN_FWD = os.environ.get("SCGIB_DEFER_BN_FWD", "1") != "0"
 _AUX_PENDING = set()
+# compressor-BN running update on the aux stream (1) or inline (0): inline
+# avoids a fork/join in the captured step, whose cross-queue edges cost more
+# than the ~4 us kernel
+RU_ASIDE = os.environ.get("SCGIB_RU_ASIDE", "0") != "0"
 
 
 def launch_aside(fn, *tensors):
@@ -519,11 +523,14 @@ def _interaction_forward(ctx, f, t, s, u_gate, u_feat, gamma, beta, w2, b2, w_at
               _p(lam), _p(logit), _p(stats), _p(kl), _p(kl_mean), int(pad), st)
     if training and bn.track_running_stats:
         nbt = bn.num_batches_tracked
-        # B sequential momentum updates in closed form; nothing in the step
-        # reads them, so they run beside the critical path (join_aside)
-        launch_aside(lambda: _lib.call("scgib_bn_running_update", _p(stats),
-                                       _p(graph.graph_ptr), B, float(bn.momentum), _p(rm),
-                                       _p(rv), _p(nbt), _stream()), stats, graph.graph_ptr)
+
+        def upd():  # B sequential momentum updates in closed form
+            _lib.call("scgib_bn_running_update", _p(stats), _p(graph.graph_ptr), B,
+                      float(bn.momentum), _p(rm), _p(rv), _p(nbt), _stream())
+        if RU_ASIDE:  # nothing in the step reads them: beside the critical path
+            launch_aside(upd, stats, graph.graph_ptr)
+        else:
+            upd()
     ctx.graph, ctx.training, ctx.pad, ctx.n_last = graph, training, pad, n_last
     ctx.bn_eps = float(bn.eps)
     ctx.rm, ctx.rv = (None, None) if training else (rm.clone(), rv.clone())

@@ -494,7 +494,8 @@ __global__ __launch_bounds__(256) void gin_fwd_k(
         pend_bet = pend.beta[fin_channel()];
         bn_fwd_fin_load<false>(pend.gpart, pend_ngr, 0, fin);
     }
-    stage_weights<DIN>(w1, w2, sW1, sW2);
+    WeightRegs<DIN> wregs;  // in flight during the gather; to LDS before the first GEMM
+    load_weights<DIN>(w1, w2, wregs);
     if constexpr (PRE) {  // transfer_d folded: gather raw features, then agg0 = aggx Wt^T
         float *sXg = sPre, *sWt = sPre + TM * kPreLD;
         for (int idx = tid; idx < 32 * kPreF; idx += 256) {
@@ -585,6 +586,7 @@ __global__ __launch_bounds__(256) void gin_fwd_k(
             d[0] = acc[k].x; d[1] = acc[k].y; d[2] = acc[k].z; d[3] = acc[k].w;
         }
     }
+    store_weights<DIN>(wregs, sW1, sW2);
     __syncthreads();
     SCGIB_MARK(1);
 
@@ -924,7 +926,10 @@ __global__ __launch_bounds__(256, (DIN <= 64 && !RECON ? 2 : 1)) void gin_bwd_k(
     BwdFin bfin;
     const int pend_ngr = static_cast<int>(((n + TM - 1) / TM + kGroup - 1) / kGroup);
     if (BN && pend.gpart) bn_bwd_fin_load<false>(pend.gpart, pend_ngr, 0, bfin);
-    stage_weights<DIN>(w1, w2, sW1, sW2);
+    // weights: in flight during the BN finish and the first tile's loads
+    WeightRegs<DIN> wregs;
+    load_weights<DIN>(w1, w2, wregs);
+    bool wpending = true;
     const int ch = tid & 63, q = tid >> 6;  // column-sum roles: channel, row quarter
     // staging roles: 4-channel chunk c4, rows rs + 16 k
     const int c4 = tid & 15, rs = tid >> 4;
@@ -1013,6 +1018,10 @@ __global__ __launch_bounds__(256, (DIN <= 64 && !RECON ? 2 : 1)) void gin_bwd_k(
         if (PRE)
             vx = ld_ok(reinterpret_cast<const float4 *>(aggx), (row0 + (tid >> 2)) * 4 + (tid & 3),
                        row0 * 4 + (tid & 3), (tid >> 2) < nv, zero);
+        if (wpending) {  // first tile: its loads are in flight now
+            store_weights<DIN>(wregs, sW1, sW2);
+            wpending = false;
+        }
         __syncthreads();  // previous tile's LDS reads are done
         if (PRE) {
             float *px = sPX + (tid >> 2) * LDP + 4 * (tid & 3);

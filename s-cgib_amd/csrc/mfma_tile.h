@@ -43,31 +43,53 @@ __device__ __forceinline__ void stage_matrix(const float *__restrict__ w, float 
     }
 }
 
-// Stage W1 [64][DIN] and W2 [64][64] (torch Linear layout) into padded LDS
-// tiles with 16-byte global loads, all issued before the first store.
+// W1 [64][DIN] and W2 [64][64] (torch Linear layout) -> padded LDS tiles, in
+// two halves so the global loads can be in flight while the caller issues its
+// own loads (gathers, tile rows): load_weights issues 16-byte loads into
+// registers, store_weights (later) writes them to LDS.  The hardware counts
+// outstanding loads in order, so waiting for the weights does not wait for
+// loads issued after them.
 template <int DIN>
-__device__ __forceinline__ void stage_weights(const float *__restrict__ w1,
-                                              const float *__restrict__ w2, float *sW1,
-                                              float *sW2) {
+struct WeightRegs {
+    float4 a[64 * DIN / 4 / 256], b[64 * 64 / 4 / 256];
+};
+
+template <int DIN>
+__device__ __forceinline__ void load_weights(const float *__restrict__ w1,
+                                             const float *__restrict__ w2, WeightRegs<DIN> &r) {
+    constexpr int N1 = 64 * DIN / 4 / 256, N2 = 64 * 64 / 4 / 256;
+    const int tid = threadIdx.x;
+#pragma unroll
+    for (int k = 0; k < N1; ++k) r.a[k] = reinterpret_cast<const float4 *>(w1)[tid + 256 * k];
+#pragma unroll
+    for (int k = 0; k < N2; ++k) r.b[k] = reinterpret_cast<const float4 *>(w2)[tid + 256 * k];
+}
+
+template <int DIN>
+__device__ __forceinline__ void store_weights(const WeightRegs<DIN> &r, float *sW1, float *sW2) {
     constexpr int LDA = DIN + 1, N1 = 64 * DIN / 4 / 256, N2 = 64 * 64 / 4 / 256;
     const int tid = threadIdx.x;
-    float4 a[N1], b[N2];
-#pragma unroll
-    for (int k = 0; k < N1; ++k) a[k] = reinterpret_cast<const float4 *>(w1)[tid + 256 * k];
-#pragma unroll
-    for (int k = 0; k < N2; ++k) b[k] = reinterpret_cast<const float4 *>(w2)[tid + 256 * k];
 #pragma unroll
     for (int k = 0; k < N1; ++k) {
         const int idx = 4 * (tid + 256 * k), row = idx / DIN, cc = idx % DIN;
         float *d = sW1 + row * LDA + cc;
-        d[0] = a[k].x; d[1] = a[k].y; d[2] = a[k].z; d[3] = a[k].w;
+        d[0] = r.a[k].x; d[1] = r.a[k].y; d[2] = r.a[k].z; d[3] = r.a[k].w;
     }
 #pragma unroll
     for (int k = 0; k < N2; ++k) {
         const int idx = 4 * (tid + 256 * k), row = idx >> 6, cc = idx & 63;
         float *d = sW2 + row * LDH + cc;
-        d[0] = b[k].x; d[1] = b[k].y; d[2] = b[k].z; d[3] = b[k].w;
+        d[0] = r.b[k].x; d[1] = r.b[k].y; d[2] = r.b[k].z; d[3] = r.b[k].w;
     }
+}
+
+template <int DIN>
+__device__ __forceinline__ void stage_weights(const float *__restrict__ w1,
+                                              const float *__restrict__ w2, float *sW1,
+                                              float *sW2) {
+    WeightRegs<DIN> r;
+    load_weights<DIN>(w1, w2, r);
+    store_weights<DIN>(r, sW1, sW2);
 }
 
 

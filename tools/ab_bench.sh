@@ -2,7 +2,7 @@
 # A/B bench: bash tools/ab_bench.sh CFG1 CFG2 ...  (3 rounds, same box)
 # A config is "ENV=val" (environment) or "--flag" (extra bench.py argument).
 cd $GRAFT_REPO_ROOT && python -c "import __graft_entry__ as g; g.build()" > /dev/null 2>&1 || exit 3
-for i in 1 2 3; do
+for i in $(seq ${ROUNDS:-3}); do
   for cfg in "$@"; do
     if [[ "$cfg" == --* ]]; then envs="AB_NONE=1"; args="$cfg"; else envs="$cfg"; args=""; fi
     env $envs timeout -k 10 200 python bench.py --steps 300 --warmup 20 --no-cpu-baseline \

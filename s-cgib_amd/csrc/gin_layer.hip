@@ -42,7 +42,7 @@ namespace scgib {
 // ---------------------------------------------------------------------------
 // ---------------------------------------------------------------------------
 // BatchNorm finalize folded into the producing tile kernel (training mode).
-// Hierarchical last-arriver: the tiles of a layer arrive in groups of 16; the
+// Hierarchical last-arriver: the tiles of a layer arrive in groups of kGroup; the
 // last tile of a group combines the group's 16 tile statistics (fp64) into a
 // group partial, then arrives at the layer counter; the last group combines
 // the groups and writes the BN record / coefficients.  Two short load rounds
@@ -50,7 +50,12 @@ namespace scgib {
 // Fixed combination order -> deterministic.  Counters: caller-provided, zero
 // on entry; each is reset by its last arriver (graph-replay safe).
 // ---------------------------------------------------------------------------
-constexpr int kGroup = 16;
+// tiles per BatchNorm statistics group (SCGIB_BN_GROUP: build-time A/B knob)
+#ifndef SCGIB_BN_GROUP
+#define SCGIB_BN_GROUP 16
+#endif
+constexpr int kGroup = SCGIB_BN_GROUP;
+static_assert(kGroup % 4 == 0 && kGroup <= 64, "group combine: 4 partitions, <= 16 loads each");
 
 struct BnFwdFuse {          // gin_fwd_k: BN statistics + running update
     unsigned *counters;     // [ngr_cap + 1]; nullptr: not fused (separate finalize)
@@ -127,7 +132,7 @@ __device__ __forceinline__ double quad_sum(double a) {
 
 // mean and centred M2 of channel fin_channel():
 //   mean = sum_g S_g / n,  M2 = sum_g [M2_g + (S_g - n_g mean)^2 / n_g]
-// n_g = 1024 for every group but possibly the last, and dividing by a power
+// n_g = kGroup * 64 for every group but possibly the last, and dividing by a power
 // of two equals multiplying by its reciprocal exactly, so only the last
 // group's term (added last by its owner, the same order) divides.
 template <bool AGENT>
@@ -213,10 +218,11 @@ __device__ void bn_fwd_hier(const float *__restrict__ part, int64_t n, int64_t t
     const int c = threadIdx.x & 63, p = threadIdx.x >> 6;
     __shared__ double sh[4][64];
     __shared__ double smean[64];
-    {   // group combine: partition p takes tiles g*16 + p + 4u
-        float S[4], Q[4];
+    {   // group combine: partition p takes tiles g*kGroup + p + 4u
+        constexpr int U = kGroup / 4;
+        float S[U], Q[U];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
+        for (int u = 0; u < U; ++u) {
             const int64_t t = int64_t(g) * kGroup + p + 4 * u;
             const int64_t tc = p + 4 * u < gsize ? t : int64_t(g) * kGroup;
             S[u] = ld_agent(part + tc * 128 + c);
@@ -224,7 +230,7 @@ __device__ void bn_fwd_hier(const float *__restrict__ part, int64_t n, int64_t t
         }
         double a = 0.0;
 #pragma unroll
-        for (int u = 0; u < 4; ++u) a += p + 4 * u < gsize ? static_cast<double>(S[u]) : 0.0;
+        for (int u = 0; u < U; ++u) a += p + 4 * u < gsize ? static_cast<double>(S[u]) : 0.0;
         sh[p][c] = a;
         __syncthreads();
         if (p == 0) {
@@ -236,7 +242,7 @@ __device__ void bn_fwd_hier(const float *__restrict__ part, int64_t n, int64_t t
         const double mg = smean[c];
         double q = 0.0;
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
+        for (int u = 0; u < U; ++u) {
             if (p + 4 * u < gsize) {
                 const int64_t t = int64_t(g) * kGroup + p + 4 * u;
                 const double nb = rows_in(n, t * TM, TM);
@@ -321,15 +327,16 @@ __device__ void bn_bwd_hier(const float *__restrict__ part, int64_t n, int64_t t
     const int c = threadIdx.x & 127, p = threadIdx.x >> 7;  // 128 sums x 2 partitions
     __shared__ double sh[2][128];
     {
-        float v[8];
+        constexpr int U = kGroup / 2;
+        float v[U];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) {
+        for (int u = 0; u < U; ++u) {
             const int k = p + 2 * u;
             v[u] = ld_agent(part + (int64_t(g) * kGroup + (k < gsize ? k : 0)) * 128 + c);
         }
         double a = 0.0;
 #pragma unroll
-        for (int u = 0; u < 8; ++u) a += p + 2 * u < gsize ? static_cast<double>(v[u]) : 0.0;
+        for (int u = 0; u < U; ++u) a += p + 2 * u < gsize ? static_cast<double>(v[u]) : 0.0;
         sh[p][c] = a;
         __syncthreads();
         if (p == 0) st_agent(bz.gpart + int64_t(g) * 128 + c, sh[0][c] + sh[1][c]);
@@ -1232,7 +1239,7 @@ extern "C" int64_t scgib_gin_bn_gpart_offset(int64_t n_nodes) {
     return n_nodes <= 0 ? 0 : ((scgib_gin_tiles(n_nodes) * 128 + 1) & ~int64_t(1));
 }
 
-// 64 groups of 16 tiles: the consumers' one-round finish (bn_fwd_final)
+// 64 groups of kGroup tiles: the consumers' one-round finish (bn_fwd_final)
 extern "C" int64_t scgib_gin_defer_max_nodes(void) { return int64_t(64) * kGroup * TM; }
 
 static double *bn_gpart(float *ws, int64_t n_nodes) {

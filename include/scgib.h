@@ -153,6 +153,22 @@ int scgib_gin_bwd_stats_bn(const float *dh, const int32_t *rowptr_t, const int32
                            int64_t n_nodes, int32_t training, float *dy, float *dgamma,
                            float *dbeta, float *coef, float *bn_ws, uint32_t *counters,
                            const int32_t *dims, int32_t defer, scgib_stream_t stream);
+/* scgib_gin_bwd_stats_bn for an encoder output read by a segment-sum readout
+ * (dgl.sum_nodes of the ego-net features, models.py:724-726): dh[v] =
+ * (dh ? dh[v] : 0) + g_seg[seg[v]] (dh may be NULL), i.e. the readout's
+ * backward broadcast is folded in; seg from scgib_bn_relu_segment_sum. */
+int scgib_gin_bwd_stats_seg_bn(const float *dh, const float *g_seg, const int32_t *seg,
+                               const float *z2, const float *stat, int64_t n_nodes,
+                               int32_t training, float *dy, float *dgamma, float *dbeta,
+                               float *coef, float *bn_ws, uint32_t *counters,
+                               const int32_t *dims, int32_t defer, scgib_stream_t stream);
+/* Encoder output and its readout in one pass: out = relu(stat.scale z +
+ * stat.shift) [n_rows][64], readout[s] = sum of out rows [ptr[s], ptr[s+1])
+ * (same order as scgib_segment_sum), seg[row] = s.  seg_dims (device, may be
+ * NULL): actual segment count; rows past the last valid one are zeroed. */
+int scgib_bn_relu_segment_sum(const float *z, const float *stat, const int32_t *ptr,
+                              int64_t n_seg, int64_t n_rows, float *out, float *readout,
+                              int32_t *seg, const int32_t *seg_dims, scgib_stream_t stream);
 /* Deferred finalize (scgib_bn_pending above): in_pending (NULL: in_stat is
  * used) names the previous layer's pending statistics — this layer finishes
  * them; defer = 1 leaves this layer's own pending (stat / running stats /

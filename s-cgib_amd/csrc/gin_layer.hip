@@ -775,12 +775,17 @@ __global__ __launch_bounds__(256) void bn_relu_apply_k(const float4 *__restrict_
 // dy = dh * [scale z2 + shift > 0]; tile sums of dy and dy * xhat.
 // GATHER: dh[v] = ope g[v] + sum_{u in out(v)} g[u]   (transposed aggregation
 // of the next layer's d(agg), never materialised)
-template <bool GATHER>
+// SEG: dh[v] = (dh ? dh[v] : 0) + g_seg[seg[v]] — the encoder output feeds a
+// segment-sum readout (dgl.sum_nodes) whose gradient is broadcast here
+// instead of by a separate segment_broadcast launch.
+template <bool GATHER, bool SEG = false>
 __global__ __launch_bounds__(256) void gin_bwd_stats_k(
     const float *__restrict__ dh, const int32_t *__restrict__ rowptr_t,
     const int32_t *__restrict__ col_t, float ope, const float *__restrict__ z2,
     const float *__restrict__ stat, int64_t ncap, float *__restrict__ dy_out,
-    float *__restrict__ part, const int32_t *__restrict__ dims, BnBwdFuse bz) {
+    float *__restrict__ part, const int32_t *__restrict__ dims, BnBwdFuse bz,
+    const float *__restrict__ g_seg, const int32_t *__restrict__ seg) {
+    static_assert(!(GATHER && SEG), "segment broadcast only on the dense input path");
     __shared__ float sRed[2][16][64];
     const int64_t n = eff_count(dims, 0, ncap);
     const int tid = threadIdx.x, c = tid & 15, slot = tid >> 4;
@@ -799,6 +804,20 @@ __global__ __launch_bounds__(256) void gin_bwd_stats_k(
     float4 g[4];
     if (GATHER) {
         gather_rows<4, 16, 16, false>(g4, rowptr_t, col_t, row0, nv, slot, c, ope, sc, sh, g);
+    } else if (SEG) {
+        int32_t sg[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int rr = slot + 16 * k;
+            sg[k] = seg[row0 + (rr < nv ? rr : nv - 1)];
+        }
+        const float4 *gs4 = reinterpret_cast<const float4 *>(g_seg);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int rr = slot + 16 * k;
+            const float4 b = gs4[static_cast<int64_t>(sg[k]) * 16 + c];
+            g[k] = dh ? add4(g4[(row0 + (rr < nv ? rr : nv - 1)) * 16 + c], b) : b;
+        }
     } else {
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
@@ -1300,12 +1319,15 @@ extern "C" int scgib_bn_relu_apply(const float *z, const float *stat, int64_t n_
 static int launch_gin_bwd_stats(const float *dh, const int32_t *rowptr_t, const int32_t *col_t,
                                 float one_plus_eps, const float *z2, const float *stat,
                                 int64_t n_nodes, float *dy, float *tile_stats,
-                                const int32_t *dims, const BnBwdFuse &bz, hipStream_t st) {
+                                const int32_t *dims, const BnBwdFuse &bz, hipStream_t st,
+                                const float *g_seg = nullptr, const int32_t *seg = nullptr) {
     const int64_t nt = scgib_gin_tiles(n_nodes);
     if (rowptr_t)
-        gin_bwd_stats_k<true><<<dim3((unsigned)nt), 256, 0, st>>>(dh, rowptr_t, col_t, one_plus_eps, z2, stat, n_nodes, dy, tile_stats, dims, bz);
+        gin_bwd_stats_k<true><<<dim3((unsigned)nt), 256, 0, st>>>(dh, rowptr_t, col_t, one_plus_eps, z2, stat, n_nodes, dy, tile_stats, dims, bz, nullptr, nullptr);
+    else if (g_seg)
+        gin_bwd_stats_k<false, true><<<dim3((unsigned)nt), 256, 0, st>>>(dh, rowptr_t, col_t, one_plus_eps, z2, stat, n_nodes, dy, tile_stats, dims, bz, g_seg, seg);
     else
-        gin_bwd_stats_k<false><<<dim3((unsigned)nt), 256, 0, st>>>(dh, rowptr_t, col_t, one_plus_eps, z2, stat, n_nodes, dy, tile_stats, dims, bz);
+        gin_bwd_stats_k<false><<<dim3((unsigned)nt), 256, 0, st>>>(dh, rowptr_t, col_t, one_plus_eps, z2, stat, n_nodes, dy, tile_stats, dims, bz, nullptr, nullptr);
     return launch_status();
 }
 
@@ -1336,6 +1358,80 @@ extern "C" int scgib_gin_bwd_stats_bn(const float *dh, const int32_t *rowptr_t,
                  static_cast<int>(bn_groups(n_nodes)), defer ? 1 : 0};
     return launch_gin_bwd_stats(dh, rowptr_t, col_t, one_plus_eps, z2, stat, n_nodes, dy, bn_ws,
                                 dims, bz, as_stream(stream));
+}
+
+extern "C" int scgib_gin_bwd_stats_seg_bn(const float *dh, const float *g_seg,
+                                          const int32_t *seg, const float *z2, const float *stat,
+                                          int64_t n_nodes, int32_t training, float *dy,
+                                          float *dgamma, float *dbeta, float *coef, float *bn_ws,
+                                          uint32_t *counters, const int32_t *dims, int32_t defer,
+                                          scgib_stream_t stream) {
+    if (n_nodes <= 0 || !g_seg || !seg || !z2 || !stat || !dy || !bn_ws || !counters)
+        return SCGIB_EINVAL;
+    if (!defer && (!dgamma || !dbeta || !coef)) return SCGIB_EINVAL;
+    BnBwdFuse bz{counters, bn_gpart(bn_ws, n_nodes), dgamma, dbeta, coef, training,
+                 static_cast<int>(bn_groups(n_nodes)), defer ? 1 : 0};
+    return launch_gin_bwd_stats(dh, nullptr, nullptr, 1.f, z2, stat, n_nodes, dy, bn_ws, dims, bz,
+                                as_stream(stream), g_seg, seg);
+}
+
+// Encoder output + readout in one pass: out = relu(scale z + shift) (the last
+// layer's BatchNorm + ReLU), readout[s] = sum of out over rows [ptr[s],
+// ptr[s+1]) in the order of segment_sum_k (so bitwise equal to the two-kernel
+// path), seg[row] = s for the backward's broadcast.  16 lanes (float4) per
+// segment; capacity mode: rows past the last valid segment are zeroed.
+__global__ __launch_bounds__(256) void bn_relu_segsum_k(
+    const float4 *__restrict__ z, const float *__restrict__ stat, const int32_t *__restrict__ ptr,
+    int64_t nseg, int64_t nrows, float4 *__restrict__ out, float4 *__restrict__ readout,
+    int32_t *__restrict__ seg, const int32_t *__restrict__ seg_dims) {
+    const int64_t blk = xcd_remap(blockIdx.x, gridDim.x);
+    const int64_t s = blk * 16 + (threadIdx.x >> 4);
+    const int c = threadIdx.x & 15;
+    const int64_t ns = eff_count(seg_dims, 0, nseg);
+    if (seg_dims) {  // zero the rows past the last valid segment (grid-stride)
+        const int64_t r0 = ptr[ns];
+        const int64_t tot = (nrows - r0) * 16;
+        for (int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x; i < tot;
+             i += static_cast<int64_t>(gridDim.x) * 256)
+            out[r0 * 16 + i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    if (s >= nseg) return;
+    if (s >= ns) {
+        readout[s * 16 + c] = make_float4(0.f, 0.f, 0.f, 0.f);
+        return;
+    }
+    const float4 a = ld4(stat + 128 + 4 * c), b = ld4(stat + 192 + 4 * c);
+    const int64_t beg = ptr[s], end = ptr[s + 1];
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    int64_t i = beg;
+    for (; i + 4 <= end; i += 4) {
+        const float4 v0 = xform4(z[i * 16 + c], a, b), v1 = xform4(z[(i + 1) * 16 + c], a, b);
+        const float4 v2 = xform4(z[(i + 2) * 16 + c], a, b), v3 = xform4(z[(i + 3) * 16 + c], a, b);
+        out[i * 16 + c] = v0; out[(i + 1) * 16 + c] = v1;
+        out[(i + 2) * 16 + c] = v2; out[(i + 3) * 16 + c] = v3;
+        if (c == 0) { seg[i] = s; seg[i + 1] = s; seg[i + 2] = s; seg[i + 3] = s; }
+        acc = add4(add4(add4(add4(acc, v0), v1), v2), v3);
+    }
+    for (; i < end; ++i) {
+        const float4 v = xform4(z[i * 16 + c], a, b);
+        out[i * 16 + c] = v;
+        if (c == 0) seg[i] = s;
+        acc = add4(acc, v);
+    }
+    readout[s * 16 + c] = acc;
+}
+
+extern "C" int scgib_bn_relu_segment_sum(const float *z, const float *stat, const int32_t *ptr,
+                                         int64_t n_seg, int64_t n_rows, float *out,
+                                         float *readout, int32_t *seg, const int32_t *seg_dims,
+                                         scgib_stream_t stream) {
+    if (n_seg < 0 || n_rows < 0) return SCGIB_EINVAL;
+    if (n_seg == 0) return SCGIB_OK;
+    if (!z || !stat || !ptr || !out || !readout || !seg) return SCGIB_EINVAL;
+    bn_relu_segsum_k<<<dim3(static_cast<unsigned>((n_seg + 15) / 16)), 256, 0, as_stream(stream)>>>(
+        reinterpret_cast<const float4 *>(z), stat, ptr, n_seg, n_rows,
+        reinterpret_cast<float4 *>(out), reinterpret_cast<float4 *>(readout), seg, seg_dims);
+    return launch_status();
 }
 
 extern "C" int scgib_bn_bwd_finalize(const float *tile_stats, int64_t n_nodes, int32_t training,

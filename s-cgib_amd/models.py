@@ -262,13 +262,8 @@ class _SCGIBCore(nn.Module):
             outs = ops.gin_encoder_pair_x(
                 batch_x, ego, enc_owner.Encoder2, batch_g, enc_owner.Encoder1, self.transfer_d,
                 ego.ndata["_ID"], side, lin0, tail)
-            subgraphs_features, graph_features = outs[0], outs[1]
-            t = outs[2] if len(outs) > 2 else None
-            with torch.cuda.stream(side):
-                sub_readout = ops.segment_sum(subgraphs_features, ego.graph_ptr, ego.batch_size,
-                                              ego.seg_dims)
-            main.wait_stream(side)
-            sub_readout.record_stream(main)
+            subgraphs_features, sub_readout, graph_features = outs[0], outs[1], outs[2]
+            t = outs[3] if len(outs) > 3 else None
             return ego, (graph_features, subgraphs_features, sub_readout, t, drawn.get("u"))
         with torch.cuda.stream(side):
             if fold:

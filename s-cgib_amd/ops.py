@@ -143,7 +143,10 @@ class _GinEncoder(torch.autograd.Function):
     never materialised — and d Wt comes out of the layer-0 backward."""
 
     @staticmethod
-    def forward(ctx, h0, graph, gin, training, x, wt, nmap, *params):
+    def forward(ctx, h0, graph, gin, training, x, wt, nmap, *params, readout=None):
+        """readout = (ptr, nseg, seg_dims): also return the segment sums of
+        the output (dgl.sum_nodes, fused with the last BN + ReLU); the backward
+        then takes (g_out, g_readout)."""
         pre = x is not None
         if pre:
             x = _f32(x, "gin_encoder x")
@@ -225,23 +228,39 @@ class _GinEncoder(torch.autograd.Function):
                 bn.num_batches_tracked.data_ptr() if track else None,
                 stat.data_ptr(), float(bn.eps), momentum) if defer else None
         out = torch.empty(n, HIDDEN, dtype=torch.float32, device=dev)
-        _lib.call("scgib_bn_relu_apply", _p(h), _p(stat_prev), n, _p(out), _p(graph.dims), st)
+        ro = seg = None
+        if readout is not None:
+            ptr, nseg, seg_dims = readout
+            ro = torch.empty(nseg, HIDDEN, dtype=torch.float32, device=dev)
+            seg = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
+            _lib.call("scgib_bn_relu_segment_sum", _p(h), _p(stat_prev), _p(ptr), nseg, n,
+                      _p(out), _p(ro), _p(seg), _p(seg_dims), st)
+        else:
+            _lib.call("scgib_bn_relu_apply", _p(h), _p(stat_prev), n, _p(out), _p(graph.dims), st)
+        ctx.seg = seg
         ctx.save_for_backward(*saved, *params, *( (aggx,) if pre else ()))
         ctx.graph, ctx.L, ctx.training, ctx.pre = graph, L, training, pre
         ctx.n_feat = x.shape[1] if pre else None
         ctx.opes = [c._one_plus_eps for c in gin.ginlayers]
         ctx.cnt_key = ("gin_bwd", id(gin))
-        return out
+        return out if ro is None else (out, ro)
 
     @staticmethod
-    def backward(ctx, g_out):
-        g_out = _f32(g_out, "gin_encoder.backward")
+    def backward(ctx, g_out, g_readout=None):
         L, gr, pre = ctx.L, ctx.graph, ctx.pre
         t = ctx.saved_tensors
         saved, params = t[: 4 * L], t[4 * L: 4 * L + 6 * L]
         aggx = t[-1] if pre else None
-        n = g_out.shape[0]
-        dev = g_out.device
+        if g_readout is not None and ctx.seg is None:
+            raise _lib.ScgibError("gin_encoder.backward: readout gradient without a readout")
+        if g_out is not None:
+            g_out = _f32(g_out, "gin_encoder.backward")
+        elif g_readout is None:  # the output is unused
+            g_out = torch.zeros_like(saved[2])
+        if g_readout is not None:
+            g_readout = _f32(g_readout, "gin_encoder.backward readout")
+        n = saved[2].shape[0]
+        dev = saved[2].device
         st = _stream()
         bn_ws = torch.empty(int(_lib.query("scgib_gin_bn_ws_floats", n)), dtype=torch.float32,
                             device=dev)
@@ -260,7 +279,13 @@ class _GinEncoder(torch.autograd.Function):
             bn_g = torch.empty(2, HIDDEN, dtype=torch.float32, device=dev)  # dgamma, dbeta
             coef = torch.empty(2, HIDDEN, dtype=torch.float32, device=dev)
             # dy, tile sums and the BN-backward finalize in one launch
-            if dagg_next is None:
+            if dagg_next is None and g_readout is not None:
+                # the readout's broadcast backward folded into the last layer
+                _launch("scgib_gin_bwd_stats_seg_bn", {"n": n}, _p(g_out), _p(g_readout),
+                        _p(ctx.seg), _p(z2), _p(stat), n, int(ctx.training), _p(dy),
+                        _p(bn_g[0]), _p(bn_g[1]), _p(coef), _p(bn_ws), _p(cnt), _p(gr.dims),
+                        defer, st)
+            elif dagg_next is None:
                 _launch("scgib_gin_bwd_stats_bn", {"n": n}, _p(g_out), None, None, 1.0, _p(z2),
                           _p(stat), n, int(ctx.training), _p(dy), _p(bn_g[0]), _p(bn_g[1]),
                           _p(coef), _p(bn_ws), _p(cnt), _p(gr.dims), defer, st)
@@ -358,12 +383,13 @@ class _GinEncoderPair(torch.autograd.Function):
         ctx.sub = (_Ctx(), _Ctx())
         ctx.side, ctx.ne = side, ne
         side.wait_stream(main)
-        with torch.cuda.stream(side):
-            s = _GinEncoder.forward(ctx.sub[0], None, ego, gin_ego, training, x, wt, nmap,
-                                    *params[:ne])
+        with torch.cuda.stream(side):  # Encoder2 + its readout (dgl.sum_nodes per ego-net)
+            s, ro = _GinEncoder.forward(ctx.sub[0], None, ego, gin_ego, training, x, wt, nmap,
+                                        *params[:ne],
+                                        readout=(ego.graph_ptr, ego.batch_size, ego.seg_dims))
         f = _GinEncoder.forward(ctx.sub[1], None, core, gin_core, training, x, wt, None,
                                 *params[ne:])
-        outs = (s, f)
+        outs = (s, ro, f)
         ctx.lin = w0 is not None
         if ctx.lin:  # compressor[0] on the (shorter) core chain, before the join
             w0, b0 = _f32(w0, "compressor.0.weight"), _f32(b0, "compressor.0.bias")
@@ -374,15 +400,16 @@ class _GinEncoderPair(torch.autograd.Function):
                       _p(core.dims), _stream())
             ctx.lin_saved = (f, w0)
             ctx.core_dims = core.dims
-            outs = (s, f, t)
+            outs = (s, ro, f, t)
         if core_tail is not None:  # extra non-differentiable work on the core chain
             core_tail()
         main.wait_stream(side)
         s.record_stream(main)
+        ro.record_stream(main)
         return outs
 
     @staticmethod
-    def backward(ctx, g_s, g_f, g_t=None):
+    def backward(ctx, g_s, g_ro, g_f, g_t=None):
         # backward: the ego chain (the longer one) stays on the current stream,
         # where its weight-gradient reduces can fork to the aux stream (a fork
         # from an already-forked stream breaks HIP-graph capture on this
@@ -407,7 +434,7 @@ class _GinEncoderPair(torch.autograd.Function):
                 dw0, db0 = wg[: HIDDEN * HIDDEN].view(HIDDEN, HIDDEN), wg[HIDDEN * HIDDEN:]
                 g_f = df_total
             gc = _GinEncoder.backward(ctx.sub[1], g_f)
-        ge = _GinEncoder.backward(ctx.sub[0], g_s)
+        ge = _GinEncoder.backward(ctx.sub[0], g_s, g_ro)
         main.wait_stream(side)
         for g in (*gc, dw0, db0):
             if isinstance(g, torch.Tensor):
@@ -427,9 +454,10 @@ def _torch_stream():
 
 def gin_encoder_pair_x(x, ego, gin_ego, core, gin_core, transfer, node_map, side, lin0=None,
                        core_tail=None):
-    """(gin_ego(ego, transfer(x[node_map])), gin_core(core, transfer(x))) —
-    the two encoders of Mainmodel.forward with transfer_d folded, the ego
-    chain on stream ``side`` (forward and backward).  With ``lin0`` (the
+    """(s, sum_nodes(ego, s), f) with s = gin_ego(ego, transfer(x[node_map])) and
+    f = gin_core(core, transfer(x)) — the two encoders of Mainmodel.forward
+    with transfer_d folded, and the ego-net readout fused into Encoder2's last
+    BN + ReLU; the ego chain on stream ``side`` (forward and backward).  With ``lin0`` (the
     compressor's Linear(64, 64), models.py:596) also returns
     t = lin0(gin_core(...)), computed at the end of the core chain;
     ``core_tail()`` (non-differentiable, e.g. the noise draw) runs there too,

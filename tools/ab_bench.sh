@@ -1,12 +1,14 @@
 #!/bin/bash
 # A/B bench: bash tools/ab_bench.sh CFG1 CFG2 ...  (3 rounds, same box)
-# A config is "ENV=val" (environment) or "--flag" (extra bench.py argument).
+# A config is "ENV=val" (environment), "--flag" (extra bench.py argument) or
+# "DIR=ab_tree" (the bench of another revision, tools/make_ab_tree.sh).
 cd $GRAFT_REPO_ROOT && python -c "import __graft_entry__ as g; g.build()" > /dev/null 2>&1 || exit 3
 for i in $(seq ${ROUNDS:-3}); do
   for cfg in "$@"; do
     if [[ "$cfg" == --* ]]; then envs="AB_NONE=1"; args="$cfg"; else envs="$cfg"; args=""; fi
-    env $envs timeout -k 10 200 python bench.py --steps 300 --warmup 20 --no-cpu-baseline \
-      --no-superbatch --no-kernel-timer $args 2>/dev/null | tail -1 | \
+    dir=.; if [[ "$cfg" == DIR=* ]]; then dir=${cfg#DIR=}; envs="AB_NONE=1"; fi
+    (cd $dir && env $envs timeout -k 10 200 python bench.py --steps 300 --warmup 20 --no-cpu-baseline \
+      --no-superbatch --no-kernel-timer $args 2>/dev/null) | tail -1 | \
       python -c "import sys,json; d=json.loads(sys.stdin.read()); print('$cfg', d['ms_per_step'], d['value'])" || exit 1
   done
 done

@@ -38,7 +38,7 @@ HBM_MEASURED_GBS = 6290.0   # float4 copy, same file
 # HBM bytes per launch of each kernel from the rocprofv3 PMC passes of
 # tools/gpu_pmc.sh (2 x FETCH_SIZE + WRITE_SIZE, MI355X_MICROARCH.md "HBM
 # [CDNA4]"), committed under profiles/ — the bench itself runs unprofiled.
-TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r01_pmc", "traffic.json")
+TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r01_s2_pmc", "traffic.json")
 
 
 def _traffic():
@@ -53,9 +53,10 @@ TRAFFIC = _traffic()
 
 
 def traffic_of(variants):
-    """Dispatch-weighted mean HBM bytes per launch over the given template
-    instantiations (e.g. the GIN variants of gin_bwd_k, not the MLP one)."""
-    got = [TRAFFIC[v] for v in variants if v in TRAFFIC]
+    """Dispatch-weighted mean HBM bytes per launch over the template
+    instantiations whose names start with one of ``variants`` (e.g. the GIN
+    variants of gin_bwd_k, not the MLP one)."""
+    got = [t for k, t in TRAFFIC.items() if any(k.startswith(v) for v in variants)]
     n = sum(g["dispatches"] for g in got)
     if not n:
         return None
@@ -438,12 +439,12 @@ def main():
             # dominant kernel by total time per step (profiles/): gin_bwd_k
             "roofline": None if r_bwd is None else roofline_entry("gin_bwd_k", "fused GIN layer backward: BN-backward "
                                        "apply + 4 f32-MFMA GEMMs + dW slabs", r_bwd,
-                                       ["gin_bwd_k<32, true>", "gin_bwd_k<64, true>"]),
+                                       ["gin_bwd_k<32, true,", "gin_bwd_k<64, true,"]),
             "roofline_gin_fwd": None if r_fwd is None else roofline_entry("gin_fwd_k", "fused GIN layer: gather + 2 "
                                                "f32-MFMA GEMMs + BN tile stats", r_fwd,
-                                               ["gin_fwd_k<32, false, true>",
-                                                "gin_fwd_k<64, true, true>",
-                                                "gin_fwd_k<64, false, true>"]),
+                                               ["gin_fwd_k<32, false, true,",
+                                                "gin_fwd_k<64, true, true,",
+                                                "gin_fwd_k<64, false, true,"]),
             "roofline_superbatch": None if sb is None else {
                 "bound": "hbm", "kernel": "gin_aggregate_k d=64", "nodes": sb["nodes"],
                 "edges": sb["edges"], "achieved": round(sb["gbs"], 1), "peak": HBM_PEAK_GBS,

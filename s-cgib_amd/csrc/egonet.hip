@@ -242,6 +242,227 @@ __global__ __launch_bounds__(256) void egonet_fill_k(
     }
 }
 
+// ---------------------------------------------------------------------------
+// k = 1 fast path (the pretraining configuration): ball(v) = sorted unique
+// ({v} ∪ N(v)) — DGL's unique(cat(frontiers)) for one hop — held as a short
+// sorted list in registers instead of a bitmap over the molecule, so the
+// molecule's bounds (a binary search over graph_ptr) are not needed, and
+// every load round is batched: row pointers of v; its <= kK1Deg neighbour
+// ids; the row pointers of the <= kK1Deg + 1 ball members; their neighbour
+// ids (clamped, always-valid addresses, predicates applied to the values).
+// Requires max in-degree <= kK1Deg and edges inside their molecule
+// (host-checked, GraphBatch.host_info).  Two launches: count + block scan,
+// then fill with the cross-block scan fix-up folded in (each block sums the
+// <= a few hundred preceding block totals itself).
+// ---------------------------------------------------------------------------
+constexpr int kK1Deg = 6, kK1Ball = kK1Deg + 1;
+
+struct K1Ball {
+    int32_t node[kK1Ball];  // ascending; entries >= nb repeat the last member
+    int32_t nb;
+};
+
+__device__ __forceinline__ void k1_ball(const int32_t *__restrict__ rowptr,
+                                        const int32_t *__restrict__ col, int32_t v, K1Ball &b) {
+    const int32_t beg = rowptr[v], end = rowptr[v + 1];
+    const int32_t last = end > beg ? end - 1 : (beg > 0 ? beg - 1 : 0);  // a valid index
+    int32_t nbr[kK1Deg];
+#pragma unroll
+    for (int j = 0; j < kK1Deg; ++j) nbr[j] = col[beg + j < end ? beg + j : last];
+    const int32_t d = end - beg;
+    // merge v into the sorted neighbour list, dropping duplicates / a self-loop
+    int32_t nb = 0, prev = -1;
+    bool vin = false;
+#pragma unroll
+    for (int j = 0; j <= kK1Deg; ++j) {
+        const bool have = j < d;
+        const int32_t w = have ? nbr[j < kK1Deg ? j : kK1Deg - 1] : 0x7fffffff;
+        if (!vin && v <= w) {  // v goes before w (or equals it: a self-loop)
+            b.node[nb < kK1Ball ? nb : kK1Ball - 1] = v;
+            ++nb;
+            prev = v;
+            vin = true;
+        }
+        if (have && w != prev) {
+            b.node[nb < kK1Ball ? nb : kK1Ball - 1] = w;
+            ++nb;
+            prev = w;
+        }
+    }
+    b.nb = nb;
+#pragma unroll
+    for (int r = 0; r < kK1Ball; ++r)
+        if (r >= nb) b.node[r] = b.node[nb - 1];
+}
+
+// position of w in the ball, or -1
+__device__ __forceinline__ int32_t k1_rank(const K1Ball &b, int32_t w) {
+    int32_t rank = 0;
+    bool in = false;
+#pragma unroll
+    for (int r = 0; r < kK1Ball; ++r) {
+        const bool live = r < b.nb;
+        rank += live && b.node[r] < w ? 1 : 0;
+        in = in || (live && b.node[r] == w);
+    }
+    return in ? rank : -1;
+}
+
+// member rows and their neighbour ids, one batched round each
+struct K1Rows {
+    int32_t beg[kK1Ball], deg[kK1Ball];
+    int32_t w[kK1Ball][kK1Deg];
+};
+
+__device__ __forceinline__ void k1_rows(const int32_t *__restrict__ rowptr,
+                                        const int32_t *__restrict__ col, const K1Ball &b,
+                                        K1Rows &m) {
+    int32_t end[kK1Ball];
+#pragma unroll
+    for (int r = 0; r < kK1Ball; ++r) {
+        m.beg[r] = rowptr[b.node[r]];
+        end[r] = rowptr[b.node[r] + 1];
+    }
+#pragma unroll
+    for (int r = 0; r < kK1Ball; ++r) {
+        m.deg[r] = end[r] - m.beg[r];
+        const int32_t last = end[r] > m.beg[r] ? end[r] - 1 : (m.beg[r] > 0 ? m.beg[r] - 1 : 0);
+#pragma unroll
+        for (int t = 0; t < kK1Deg; ++t) m.w[r][t] = col[m.beg[r] + t < end[r] ? m.beg[r] + t : last];
+    }
+}
+
+// per-block inclusive scan of (a, b) over 256 threads (Hillis-Steele in LDS)
+__device__ __forceinline__ void block_scan2(int32_t &a, int32_t &b) {
+    __shared__ int32_t sa[256], sb[256];
+    sa[threadIdx.x] = a;
+    sb[threadIdx.x] = b;
+    __syncthreads();
+    for (int off = 1; off < 256; off <<= 1) {
+        int32_t xa = 0, xb = 0;
+        if (threadIdx.x >= off) {
+            xa = sa[threadIdx.x - off];
+            xb = sb[threadIdx.x - off];
+        }
+        __syncthreads();
+        sa[threadIdx.x] += xa;
+        sb[threadIdx.x] += xb;
+        __syncthreads();
+    }
+    a = sa[threadIdx.x];
+    b = sb[threadIdx.x];
+}
+
+__global__ __launch_bounds__(256) void egonet_k1_count_k(
+    const int32_t *__restrict__ rowptr, const int32_t *__restrict__ col, int64_t n,
+    int32_t *__restrict__ ego_ptr, int32_t *__restrict__ ego_eptr, int32_t *__restrict__ blk_tot,
+    const int32_t *__restrict__ dims) {
+    const int64_t v = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
+    int32_t nb = 0, ne = 0;
+    if (v < eff_count(dims, 0, n)) {
+        K1Ball b;
+        k1_ball(rowptr, col, static_cast<int32_t>(v), b);
+        K1Rows m;
+        k1_rows(rowptr, col, b, m);
+        nb = b.nb;
+#pragma unroll
+        for (int r = 0; r < kK1Ball; ++r)
+#pragma unroll
+            for (int t = 0; t < kK1Deg; ++t)
+                ne += (r < b.nb && t < m.deg[r] && k1_rank(b, m.w[r][t]) >= 0) ? 1 : 0;
+    }
+    block_scan2(nb, ne);
+    if (v < n) {
+        ego_ptr[v + 1] = nb;   // block-local inclusive; the fill adds the block prefix
+        ego_eptr[v + 1] = ne;
+    }
+    if (threadIdx.x == 255) {
+        blk_tot[blockIdx.x] = nb;
+        blk_tot[gridDim.x + blockIdx.x] = ne;
+    }
+}
+
+__global__ __launch_bounds__(256) void egonet_k1_fill_k(
+    const int32_t *__restrict__ rowptr, const int32_t *__restrict__ col, int64_t n,
+    int32_t *__restrict__ ego_ptr, int32_t *__restrict__ ego_eptr,
+    const int32_t *__restrict__ blk_tot, int32_t *__restrict__ ego_nodes,
+    int32_t *__restrict__ sub_rowptr, int32_t *__restrict__ sub_col, int64_t n_ego_cap,
+    const int32_t *__restrict__ dims, int32_t *__restrict__ ego_dims) {
+    const int nblk = gridDim.x;
+    const int64_t v = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
+    const bool live = v < eff_count(dims, 0, n);
+    // the ball's loads go out first; the scan fix-up below overlaps them
+    K1Ball b;
+    K1Rows m;
+    if (live) {
+        k1_ball(rowptr, col, static_cast<int32_t>(v), b);
+        k1_rows(rowptr, col, b, m);
+    }
+    // block prefix and grand total of (nodes, edges), fixed order
+    __shared__ int32_t rp[4][256];
+    int32_t pn = 0, pe = 0, tn = 0, te = 0;
+    for (int32_t j = threadIdx.x; j < nblk; j += 256) {
+        const int32_t a = blk_tot[j], c = blk_tot[nblk + j];
+        tn += a;
+        te += c;
+        if (j < static_cast<int32_t>(blockIdx.x)) {
+            pn += a;
+            pe += c;
+        }
+    }
+    rp[0][threadIdx.x] = pn; rp[1][threadIdx.x] = pe;
+    rp[2][threadIdx.x] = tn; rp[3][threadIdx.x] = te;
+    __syncthreads();
+    for (int off = 128; off >= 1; off >>= 1) {
+        if (threadIdx.x < off)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) rp[q][threadIdx.x] += rp[q][threadIdx.x + off];
+        __syncthreads();
+    }
+    const int32_t pre_n = rp[0][0], pre_e = rp[1][0], ns = rp[2][0], es = rp[3][0];
+    // this node's exclusive offsets from the count's block-local inclusive scan
+    int32_t noff = pre_n, eo = pre_e, incl_n = 0, incl_e = 0;
+    if (v < n) {
+        incl_n = ego_ptr[v + 1];
+        incl_e = ego_eptr[v + 1];
+        if (threadIdx.x > 0) {
+            noff += ego_ptr[v];
+            eo += ego_eptr[v];
+        }
+    }
+    __syncthreads();  // every read of the block-local values precedes the writes
+    if (v < n) {
+        ego_ptr[v + 1] = pre_n + incl_n;
+        ego_eptr[v + 1] = pre_e + incl_e;
+    }
+    if (v == 0) {
+        ego_ptr[0] = 0;
+        ego_eptr[0] = 0;
+        if (ego_dims) {  // the ego batch's actual [N_s, E_s], device-resident
+            ego_dims[0] = ns;
+            ego_dims[1] = es;
+        }
+    }
+    // tail of the ego batch: [N_s, n_ego_cap) gets parent id 0 and empty CSR rows
+    for (int64_t i = ns + v; i <= n_ego_cap; i += static_cast<int64_t>(nblk) * 256) {
+        sub_rowptr[i] = es;
+        if (i < n_ego_cap) ego_nodes[i] = 0;
+    }
+    if (!live) return;
+#pragma unroll
+    for (int r = 0; r < kK1Ball; ++r) {
+        if (r < b.nb) {
+            ego_nodes[noff + r] = b.node[r];
+            sub_rowptr[noff + r] = eo;
+#pragma unroll
+            for (int t = 0; t < kK1Deg; ++t) {
+                const int32_t q = k1_rank(b, m.w[r][t]);
+                if (t < m.deg[r] && q >= 0) sub_col[eo++] = noff + q;
+            }
+        }
+    }
+}
+
 static int words_for(int32_t max_graph_nodes) {
     if (max_graph_nodes <= 64) return 1;
     if (max_graph_nodes <= 128) return 2;
@@ -289,6 +510,27 @@ extern "C" int scgib_egonet_count(const int32_t *rowptr, const int32_t *col,
     }
 #undef SCGIB_EGO_COUNT
     egonet_scan_fixup_k<<<nblk, 256, 0, st>>>(n_nodes, nblk, blk_tot, ego_ptr, ego_eptr);
+    return launch_status();
+}
+
+extern "C" int64_t scgib_egonet_k1_max_degree(void) { return kK1Deg; }
+
+extern "C" int scgib_egonet_k1_build(const int32_t *rowptr, const int32_t *col, int64_t n_nodes,
+                                     int32_t *ego_ptr, int32_t *ego_eptr, void *workspace,
+                                     int32_t *ego_nodes, int32_t *sub_rowptr, int32_t *sub_col,
+                                     int64_t n_ego_cap, const int32_t *dims, int32_t *ego_dims,
+                                     scgib_stream_t stream) {
+    if (n_nodes <= 0 || !rowptr || !col || !ego_ptr || !ego_eptr || !workspace || !ego_nodes ||
+        !sub_rowptr || !sub_col)
+        return SCGIB_EINVAL;
+    if (n_nodes >= (int64_t(1) << 31)) return SCGIB_EUNSUPPORTED;
+    const int32_t nblk = static_cast<int32_t>((n_nodes + 255) / 256);
+    int32_t *blk_tot = static_cast<int32_t *>(workspace);
+    hipStream_t st = as_stream(stream);
+    egonet_k1_count_k<<<nblk, 256, 0, st>>>(rowptr, col, n_nodes, ego_ptr, ego_eptr, blk_tot, dims);
+    egonet_k1_fill_k<<<nblk, 256, 0, st>>>(rowptr, col, n_nodes, ego_ptr, ego_eptr, blk_tot,
+                                           ego_nodes, sub_rowptr, sub_col, n_ego_cap, dims,
+                                           ego_dims);
     return launch_status();
 }
 

@@ -359,12 +359,24 @@ def egonet_batch(g: GraphBatch, k: int, x=None):
     ego_eptr = torch.empty(n + 1, dtype=i32, device=dev)
     ws = torch.empty(int(_lib.query("scgib_egonet_workspace_bytes", n)), dtype=torch.uint8,
                      device=dev)
+    info = g.host_info
+    if k == 1 and EGO_K1_FAST and n > 0:
+        # two-launch k = 1 builder (sorted-list balls, batched loads): needs
+        # the max in-degree bound and in-molecule edges, checked on the host
+        kmax = int(_lib.query("scgib_egonet_k1_max_degree"))
+        if g.dims is not None:
+            caps = g.ego_caps or ()
+            fast = len(caps) > 2 and caps[2] <= kmax
+        else:
+            fast = (info is not None and info["validated"] and
+                    (len(info["deg"]) == 0 or int(info["deg"].max()) <= kmax))
+        if fast:
+            return _egonet_k1(g, ego_ptr, ego_eptr, ws, x)
     err = getattr(g, "err_buf", None)
     if err is None:
         err = torch.zeros(1, dtype=i32, device=dev)
     st = _stream()
     mgn = max(g.max_graph_nodes, 1)
-    info = g.host_info
     _lib.call("scgib_egonet_count", _ptr(g.rowptr), _ptr(g.col), _ptr(g.graph_ptr), g.batch_size,
               n, k, mgn, _ptr(ego_ptr), _ptr(ego_eptr), _ptr(ws), _ptr(err), _ptr(g.dims), st)
     ego_dims = None
@@ -373,7 +385,7 @@ def egonet_batch(g: GraphBatch, k: int, x=None):
         # stay on the device (ego_dims) — nothing is read back
         if g.ego_caps is None:
             raise _lib.ScgibError("capacity-mode graph without ego capacities (StaticBatch)")
-        n_s, e_cap = g.ego_caps
+        n_s, e_cap = g.ego_caps[:2]
         e_s = -1
         ego_dims = torch.empty(2, dtype=i32, device=dev)
     elif k == 1 and info is not None and info["validated"] and mgn <= 512:
@@ -403,6 +415,42 @@ def egonet_batch(g: GraphBatch, k: int, x=None):
     dict.__setitem__(ego.ndata, "_ID", ego_nodes)
     if x is not None:
         dict.__setitem__(ego.ndata, "x", x.index_select(0, ego_nodes))
+    return ego
+
+
+# k = 1 ego-nets through the two-launch builder when its degree bound holds
+# (tests switch it off to compare with the general bitmap builder)
+EGO_K1_FAST = True
+
+
+def _egonet_k1(g, ego_ptr, ego_eptr, ws, x):
+    """egonet_batch for k = 1 via scgib_egonet_k1_build (sizes known on the
+    host: |ball(v)| = 1 + deg(v) - selfloop(v); capacity mode: g.ego_caps)."""
+    dev = g.device
+    n = g.num_nodes()
+    i32 = torch.int32
+    ego_dims = None
+    if g.dims is not None:
+        n_s, e_cap = g.ego_caps[:2]
+        ego_dims = torch.empty(2, dtype=i32, device=dev)
+    else:
+        info = g.host_info
+        ball = 1 + info["deg"] - info["selfloops"]
+        n_s = int(ball.sum())
+        e_cap = int((info["deg"] * ball).sum())
+    ego_nodes = torch.empty(max(n_s, 1), dtype=i32, device=dev)
+    sub_rowptr = torch.empty(n_s + 1, dtype=i32, device=dev)
+    sub_col = torch.empty(max(e_cap, 1), dtype=i32, device=dev)
+    _lib.call("scgib_egonet_k1_build", _ptr(g.rowptr), _ptr(g.col), n, _ptr(ego_ptr),
+              _ptr(ego_eptr), _ptr(ws), _ptr(ego_nodes), _ptr(sub_rowptr), _ptr(sub_col), n_s,
+              _ptr(g.dims), _ptr(ego_dims), _stream())
+    ego = GraphBatch(sub_rowptr, sub_col, ego_ptr, None, None, n_edges=-1,
+                     max_graph_nodes=max(g.max_graph_nodes, 1))
+    ego.dims = ego_dims
+    ego.seg_dims = g.dims
+    dict.__setitem__(ego.ndata, "_ID", ego_nodes[:n_s])
+    if x is not None:
+        dict.__setitem__(ego.ndata, "x", x.index_select(0, ego_nodes[:n_s]))
     return ego
 
 
@@ -458,14 +506,16 @@ class StaticBatch:
         n = max(g.num_nodes() for g in host_batches)
         e = max(g.num_edges() for g in host_batches)
         mgn = max(g.max_graph_nodes for g in host_batches)
-        ns = es = 0
+        ns = es = dmax = 0
         for g in host_batches:
             info = g.host_info
             ball = 1 + info["deg"] - info["selfloops"]
             ns = max(ns, int(ball.sum()))
             es = max(es, int((info["deg"] * ball).sum()))
+            dmax = max(dmax, int(info["deg"].max()) if len(info["deg"]) else 0)
         f = lambda v: int(v * slack) + 1  # noqa: E731
-        return f(n), f(e), mgn, (f(ns), f(es))
+        # ego caps: (nodes, edges, max in-degree — selects the k = 1 builder)
+        return f(n), f(e), mgn, (f(ns), f(es), dmax)
 
     def pad(self, g):
         """Device copy of host batch ``g`` padded to this batch's capacities."""
@@ -478,9 +528,12 @@ class StaticBatch:
         if not g.host_info["validated"]:
             raise _lib.ScgibError("batch edges leave their molecule")
         ball = 1 + g.host_info["deg"] - g.host_info["selfloops"]
-        ns, es = self.graph.ego_caps
+        ns, es = self.graph.ego_caps[:2]
         if int(ball.sum()) > ns or int((g.host_info["deg"] * ball).sum()) > es:
             raise _lib.ScgibError("batch's ego-nets exceed the ego capacities")
+        if len(self.graph.ego_caps) > 2 and len(g.host_info["deg"]) and \
+                int(g.host_info["deg"].max()) > self.graph.ego_caps[2]:
+            raise _lib.ScgibError("batch's max degree exceeds the captured ego builder's bound")
         if self.B and g.batch_num_nodes_host().min() < 2:
             raise ValueError("Expected more than 1 value per channel when training "
                              "(a molecule with one atom; the reference skips those)")

@@ -128,6 +128,34 @@ def test_egonet_large_molecules_multiword_bitmaps(pkg, dev):
         _check_ego(pkg, gh, k, dev)
 
 
+@pytest.mark.parametrize("workload", ["qm9", "molpcba", "mutagenicity"])
+def test_egonet_k1_fast_path_equals_bitmap_builder(pkg, dev, workload):
+    """The two-launch k = 1 builder (sorted-list balls) produces exactly the
+    arrays of the general bitmap builder, incl. an isolated atom and a
+    self-loop (hand-made molecule appended to the batch)."""
+    mols = pkg.synth.molecules(300, workload, seed=21)
+    gh, _ = pkg.graph.collate_pyg(mols)
+    src, dst = (t.numpy() for t in gh.edges())
+    n = gh.num_nodes()
+    # extra molecule: 0-1-2 path, isolated atom 3, self-loop on 1
+    es = np.array([0, 1, 1, 2, 1]) + n
+    ed = np.array([1, 0, 2, 1, 1]) + n
+    counts = np.concatenate([gh.batch_num_nodes_host(), [4]])
+    g2 = pkg.graph.GraphBatch.from_edges(np.concatenate([src, es]), np.concatenate([dst, ed]),
+                                         n + 4, True, counts)
+    outs = []
+    for fast in (True, False):
+        pkg.graph.EGO_K1_FAST = fast
+        try:
+            ego = pkg.graph.egonet_batch(g2.to(dev), 1)
+            outs.append([ego.graph_ptr.cpu().numpy(), ego.ndata["_ID"].cpu().numpy(),
+                         ego.rowptr.cpu().numpy(), ego.col.cpu().numpy()[: ego.num_edges()]])
+        finally:
+            pkg.graph.EGO_K1_FAST = True
+    for a, b in zip(*outs):
+        np.testing.assert_array_equal(a, b)
+
+
 def test_egonet_rejects_oversized_graph(pkg, dev):
     mols = pkg.synth.molecules(2, "qm9", seed=4, mu=700.0, sigma=1.0)
     gh, _ = pkg.graph.collate_pyg(mols)

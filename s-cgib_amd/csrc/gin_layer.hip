@@ -1173,8 +1173,14 @@ __global__ __launch_bounds__(256, (DIN <= 64 && !RECON ? 2 : 1)) void gin_bwd_k(
 }
 
 // up to two workgroups per CU (66.5 KB LDS each): one tile per workgroup for
-// batches up to 512 tiles, so every tile of an encoder layer runs at once
-static int bwd_grid(int64_t ntiles) { return static_cast<int>(ntiles < 512 ? ntiles : 512); }
+// batches up to SCGIB_BWD_GRID_CAP tiles (build-time knob), so every tile of
+// an encoder layer runs at once; larger batches loop over tiles
+#ifndef SCGIB_BWD_GRID_CAP
+#define SCGIB_BWD_GRID_CAP 512
+#endif
+static int bwd_grid(int64_t ntiles) {
+    return static_cast<int>(ntiles < SCGIB_BWD_GRID_CAP ? ntiles : SCGIB_BWD_GRID_CAP);
+}
 
 }  // namespace scgib
 

@@ -288,7 +288,8 @@ def main():
     # rocBLAS is ~2-3x faster on them.  (Process-wide torch setting.)
     torch.backends.cuda.preferred_blas_library("cublas")
     rank, world, local = pkg.dist.init_from_env()
-    dev = torch.device("cuda", local)
+    # (more ranks than devices only in local gloo rehearsals: ranks share GPUs)
+    dev = torch.device("cuda", local % max(torch.cuda.device_count(), 1))
     torch.cuda.set_device(dev)
     torch.manual_seed(1234 + rank)
     F_in = pkg.synth.WORKLOADS[a.workload][2]
@@ -361,13 +362,20 @@ def main():
             static_loss = body()
             if world == 1:
                 opt.step()
+            else:  # gradients -> the flat all-reduce bucket, one launch
+                reducer.pack()
+        if world > 1:  # 1/world unpack + Adam, replayed after the all-reduce
+            graph2 = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(graph2):
+                reducer.unpack()
+                opt.step()
 
         def step(i):
             static.load(padded[i % len(padded)])
             graph.replay()
-            if world > 1:  # gradient all-reduce over RCCL outside the graph
-                reducer()
-                opt.step()
+            if world > 1:  # RCCL all-reduce of the bucket between the two replays
+                reducer.reduce()
+                graph2.replay()
             return static_loss
 
     for i in range(a.warmup):

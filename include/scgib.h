@@ -451,6 +451,22 @@ int scgib_adam_step(const scgib_adam_tensor *tensors, int32_t n_tensors, double 
                     double beta1, double beta2, double eps, double weight_decay,
                     uint32_t *counter, scgib_stream_t stream);
 
+
+/* ---- data parallelism: gradient bucket (dist.GradAllReducer) --------------
+ * scgib_grad_pack: flat[offset + i] = data[i] for every slice, one launch;
+ * scgib_grad_unpack: data[i] = scale * flat[offset + i] (scale = 1/world after
+ * the all-reduce SUM).  n_tensors <= scgib_grad_pack_max_tensors(); the table
+ * is copied into the kernel arguments (HIP-graph capturable). */
+typedef struct {
+    float *data;
+    int64_t numel;
+    int64_t offset;
+} scgib_grad_slice;
+int64_t scgib_grad_pack_max_tensors(void);
+int scgib_grad_pack(const scgib_grad_slice *tensors, int32_t n_tensors, float *flat,
+                    scgib_stream_t stream);
+int scgib_grad_unpack(const scgib_grad_slice *tensors, int32_t n_tensors, const float *flat,
+                      float scale, scgib_stream_t stream);
 #ifdef __cplusplus
 }
 #endif

@@ -88,6 +88,9 @@ SIGNATURES = {
     "scgib_recon_partials_floats": (_I64, [_I64]),
     "scgib_recon_fwd": (ctypes.c_int, [_P, _P, _P, _I64, _I64, _P, _P, _P, _P, _P]),
     "scgib_recon_bwd": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _I64, _P, _P, _P, _P]),
+    "scgib_grad_pack_max_tensors": (_I64, []),
+    "scgib_grad_pack": (ctypes.c_int, [_P, _I32, _P, _P]),
+    "scgib_grad_unpack": (ctypes.c_int, [_P, _I32, _P, _F, _P]),
     "scgib_adam_max_tensors": (_I64, []),
     "scgib_adam_step": (ctypes.c_int, [_P, _I32, _D, _D, _D, _D, _D, _P, _P]),
 }
@@ -112,6 +115,11 @@ class AdamTensor(ctypes.Structure):
     _fields_ = [("param", ctypes.c_void_p), ("grad", ctypes.c_void_p),
                 ("exp_avg", ctypes.c_void_p), ("exp_avg_sq", ctypes.c_void_p),
                 ("step", ctypes.c_void_p), ("numel", ctypes.c_int64)]
+
+class GradSlice(ctypes.Structure):
+    """scgib_grad_slice (include/scgib.h)."""
+    _fields_ = [("data", ctypes.c_void_p), ("numel", ctypes.c_int64), ("offset", ctypes.c_int64)]
+
 
 ABI_VERSION = 5
 STATS_STRIDE = 260

@@ -87,6 +87,70 @@ __global__ __launch_bounds__(256) void adam_step_k(const AdamTable tab, double l
     }
 }
 
+// ---------------------------------------------------------------------------
+// Gradient bucket for the data-parallel all-reduce (dist.GradAllReducer): all
+// gradients packed into one flat buffer in ONE launch (and unpacked, scaled
+// by 1 / world, in one more) instead of a copy launch per tensor.  Same
+// chunk -> tensor scheme as the Adam step; the table travels by value.
+// ---------------------------------------------------------------------------
+constexpr int kPackMax = 96;
+
+struct PackTable {
+    scgib_grad_slice t[kPackMax];
+    int32_t chunk0[kPackMax + 1];
+    int32_t n;
+};
+
+template <bool UNPACK>
+__global__ __launch_bounds__(256) void grad_pack_k(const PackTable tab, float *__restrict__ flat,
+                                                   float scale) {
+    const int b = blockIdx.x, lane = threadIdx.x & 63;
+    // tensor of this chunk: parallel compare over the table (two 64-wide rounds)
+    int i = -1;
+#pragma unroll
+    for (int r = 0; r < (kPackMax + 63) / 64; ++r) {
+        const int q = 64 * r + lane;
+        const bool le = q < tab.n && tab.chunk0[q < tab.n ? q : 0] <= b;
+        i += __popcll(__ballot(le));
+    }
+    const scgib_grad_slice &T = tab.t[i];
+    const int64_t base = static_cast<int64_t>(b - tab.chunk0[i]) * kAdamChunk;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int64_t j = base + threadIdx.x + 256 * k;
+        if (j < T.numel) {
+            if (UNPACK) T.data[j] = scale * flat[T.offset + j];
+            else flat[T.offset + j] = T.data[j];
+        }
+    }
+}
+
+static int launch_pack(const scgib_grad_slice *tensors, int32_t n, float *flat, float scale,
+                       bool unpack, hipStream_t st) {
+    if (n < 0 || n > kPackMax) return SCGIB_EINVAL;
+    if (n == 0) return SCGIB_OK;
+    if (!tensors || !flat) return SCGIB_EINVAL;
+    PackTable tab;
+    tab.n = n;
+    int64_t chunks = 0;
+    for (int i = 0; i < n; ++i) {
+        const scgib_grad_slice &T = tensors[i];
+        if (T.numel < 0 || T.offset < 0 || (T.numel > 0 && !T.data)) return SCGIB_EINVAL;
+        tab.t[i] = T;
+        tab.chunk0[i] = static_cast<int32_t>(chunks);
+        chunks += (T.numel + kAdamChunk - 1) / kAdamChunk;
+        if (chunks > 0x7fffffff) return SCGIB_EUNSUPPORTED;
+    }
+    tab.chunk0[n] = static_cast<int32_t>(chunks);
+    for (int i = n; i < kPackMax; ++i) tab.t[i] = scgib_grad_slice{};
+    if (chunks == 0) return SCGIB_OK;
+    if (unpack)
+        grad_pack_k<true><<<dim3(static_cast<unsigned>(chunks)), 256, 0, st>>>(tab, flat, scale);
+    else
+        grad_pack_k<false><<<dim3(static_cast<unsigned>(chunks)), 256, 0, st>>>(tab, flat, scale);
+    return launch_status();
+}
+
 }  // namespace scgib
 
 using namespace scgib;
@@ -121,4 +185,17 @@ extern "C" int scgib_adam_step(const scgib_adam_tensor *tensors, int32_t n_tenso
     adam_step_k<<<dim3(static_cast<unsigned>(chunks)), 256, 0, as_stream(stream)>>>(
         tab, lr, beta1, beta2, eps, weight_decay, counter);
     return launch_status();
+}
+
+extern "C" int64_t scgib_grad_pack_max_tensors(void) { return kPackMax; }
+
+extern "C" int scgib_grad_pack(const scgib_grad_slice *tensors, int32_t n_tensors, float *flat,
+                               scgib_stream_t stream) {
+    return launch_pack(tensors, n_tensors, flat, 1.f, false, as_stream(stream));
+}
+
+extern "C" int scgib_grad_unpack(const scgib_grad_slice *tensors, int32_t n_tensors,
+                                 const float *flat, float scale, scgib_stream_t stream) {
+    return launch_pack(tensors, n_tensors, const_cast<float *>(flat), scale, true,
+                       as_stream(stream));
 }

@@ -279,7 +279,9 @@ int scgib_egonet_fill(const int32_t *rowptr, const int32_t *col, const int32_t *
  * kl_mean (scalar) = mean(kl_tensor); either output may be NULL (not both).
  * pad_rows != 0: n_nodes is a row capacity and rows [graph_ptr[B], n_nodes)
  * of im, lam, logit are zeroed (capacity mode; B stays exact).
- * Saved for backward: lam[N], logit[N], stats[B, SCGIB_STATS_STRIDE].
+ * Saved for backward: lam[N], logit[N] (= w_att[64:128].s_v: the per-graph
+ * z-bar term cancels in the softmax, so it is kept out of the saved logits and
+ * their max/sum), stats[B, SCGIB_STATS_STRIDE].
  * Scalars b2, b_att are device pointers (no host sync). */
 int scgib_interaction_fwd(const float *f, const float *t, const float *s,
                           const float *u_gate, const float *u_feat, const int32_t *graph_ptr,

@@ -40,9 +40,9 @@ enum : int {
     kStSsqT = 64,      // centred sum of squares of t               [64]
     kStMu = 128,       // std_mean(f).mean                         [64]
     kStSigma = 192,    // std_mean(f).std (unbiased)               [64]
-    kStSoftMax = 256,  // softmax max M
+    kStSoftMax = 256,  // softmax max M (of the logits without the z-bar constant)
     kStSoftSum = 257,  // softmax denominator S (relative to M)
-    kStConst = 258,    // z-bar logit constant
+    kStConst = 258,    // z-bar logit constant w_lo . z1 + b (cancels in the softmax)
 };
 // pgrad slab layout per graph (SCGIB_PGRAD_STRIDE floats)
 enum : int { kPgW2 = 0, kPgB2 = 64, kPgGamma = 65, kPgBeta = 129, kPgWatt = 193, kPgBatt = 321 };
@@ -196,20 +196,33 @@ __global__ __launch_bounds__(64) void interaction_fwd_k(
         if (gi == B - 1 && kl_mean && threadIdx.x == 0) *kl_mean = 0.f;
         return;
     }
-    // ---- pass 1: sums (readout of f, means) and shifted second moments ----
+    // Two load passes (the first chunk of CH rows per row group — a whole
+    // typical molecule — stays in registers between them):
+    //   pass A: f / t sums and shifted second moments; the attention logit
+    //           w_hi . s_v and its online softmax (the per-graph constant
+    //           w_lo . z-bar + b cancels in the softmax, so the stored logit,
+    //           max and sum exclude it; the backward only uses differences);
+    //   pass B: compressor logit p, gate lambda, noisy features, the attended
+    //           s rows, z-bar, and (last graph) the KL sum of squares;
+    //   KL store pass for the last graph (lambda of the first chunk from
+    //   registers, later chunks recomputed).
     const float4 f0 = ld4(f + r0 * 64 + L.ch), t0 = ld4(t + r0 * 64 + L.ch);
+    const float4 whi = ld4(watt + 64 + L.ch);
     float4 zf = f4(0.f), zt = f4(0.f), sf = f4(0.f), st = f4(0.f), qf = f4(0.f), qt = f4(0.f);
-    for (int64_t cb = r0; cb < r1; cb += 4 * CH) {
-        float4 fv[CH], tv[CH];
+    float M = -INFINITY, S = 0.f;  // per row group, merged below
+    float4 fk[CH], tk[CH], sk[CH];  // first chunk, kept
+    auto pass_a = [&](int64_t cb, float4 *fv, float4 *tv, float4 *sv) {
 #pragma unroll
         for (int j = 0; j < CH; ++j) {
             const int64_t r = cb + L.q + 4 * j, rr = r < r1 ? r : r0;
             fv[j] = ld4(f + rr * 64 + L.ch);
             tv[j] = ld4(t + rr * 64 + L.ch);
+            sv[j] = ld4(s + rr * 64 + L.ch);
         }
 #pragma unroll
         for (int j = 0; j < CH; ++j) {
-            const float w = cb + L.q + 4 * j < r1 ? 1.f : 0.f;
+            const int64_t r = cb + L.q + 4 * j;
+            const float w = r < r1 ? 1.f : 0.f;
             zf = macc(fv[j], w, zf);
             zt = macc(tv[j], w, zt);
             const float4 df = fv[j] - f0, dt = tv[j] - t0;
@@ -217,10 +230,30 @@ __global__ __launch_bounds__(64) void interaction_fwd_k(
             st = macc(dt, w, st);
             qf = macc(df * df, w, qf);
             qt = macc(dt * dt, w, qt);
+            const float lg = red16(dot4(whi, sv[j]));
+            if (r < r1) {
+                if (L.c4 == 0) logit[r] = lg;
+                const float Mn = fmaxf(M, lg);
+                S = S * expf(M - Mn) + expf(lg - Mn);
+                M = Mn;
+            }
         }
+    };
+    pass_a(r0, fk, tk, sk);
+    for (int64_t cb = r0 + 4 * CH; cb < r1; cb += 4 * CH) {
+        float4 fv[CH], tv[CH], sv[CH];
+        pass_a(cb, fv, tv, sv);
     }
     zf = red_q4(zf); zt = red_q4(zt); sf = red_q4(sf); st = red_q4(st);
     qf = red_q4(qf); qt = red_q4(qt);
+#pragma unroll
+    for (int off = 16; off <= 32; off <<= 1) {  // merge the four row groups' softmax
+        const float Mo = __shfl_xor(M, off, kWave), So = __shfl_xor(S, off, kWave);
+        const float Mn = fmaxf(M, Mo);
+        S = (S == 0.f ? 0.f : S * expf(M - Mn)) + (So == 0.f ? 0.f : So * expf(Mo - Mn));
+        M = Mn;
+    }
+    const float invS = 1.f / S;
     const float inv_n = 1.f / n;
     const float4 mu = inv_n * zf, mt = inv_n * zt;
     // centred sums of squares (shifted formula); n == 1 -> 0 / 0 -> NaN std, as torch
@@ -241,78 +274,71 @@ __global__ __launch_bounds__(64) void interaction_fwd_k(
         st4(sl + kStMu + L.ch, mu);
         st4(sl + kStSigma + L.ch, sig);
     }
-    // ---- pass 2: compressor logit p, gate lambda, noisy features ----
-    float4 zacc = f4(0.f);
-    for (int64_t cb = r0; cb < r1; cb += 4 * CH) {
-        float4 tv[CH], fv[CH], uv[CH];
+    // ---- pass B: compressor logit p, gate lambda, noisy features, attention ----
+    const bool last = gi == B - 1;
+    const float4 se = sig + f4(kKlEps);
+    float4 zacc = f4(0.f), qacc = f4(0.f);
+    float lmk[CH];  // first chunk's lambda, kept for the KL store pass
+    auto pass_b = [&](int64_t cb, const float4 *fv, const float4 *tv, const float4 *sv,
+                      float *lmo) {
+        float4 uv[CH];
         float ug[CH];
 #pragma unroll
         for (int j = 0; j < CH; ++j) {
             const int64_t r = cb + L.q + 4 * j, rr = r < r1 ? r : r0;
-            tv[j] = ld4(t + rr * 64 + L.ch);
-            fv[j] = ld4(f + rr * 64 + L.ch);
             uv[j] = ld4(u_feat + rr * 64 + L.ch);
             ug[j] = u_gate[rr];
         }
 #pragma unroll
         for (int j = 0; j < CH; ++j) {
             const int64_t r = cb + L.q + 4 * j;
+            const float w = r < r1 ? 1.f : 0.f;
             const float4 y = gm * ((tv[j] - m_use) * rstd) + bt;
             const float p = red16(dot4(w2c, relu4(y))) + b2;
             const float lm = gate_lambda(ug[j], p), ln = 1.f - lm;
+            if (lmo) lmo[j] = lm;
             const float4 nz = (lm * fv[j] + ln * mu) + uv[j] * (ln * sig);
-            zacc = macc(nz, r < r1 ? 1.f : 0.f, zacc);
+            zacc = macc(nz, w, zacc);
+            if (last) {
+                const float4 d = (lm * fv[j] + ln * mu) - mu;
+                const float4 z = make_float4(d.x / se.x, d.y / se.y, d.z / se.z, d.w / se.w);
+                qacc = macc(z * z, w, qacc);
+            }
+            const float lg = red16(dot4(whi, sv[j]));
             if (r < r1) {
                 st4(im + r * 128 + L.ch, nz);
+                st4(im + r * 128 + 64 + L.ch, (expf(lg - M) * invS) * sv[j]);
                 if (L.c4 == 0) lam[r] = lm;
             }
         }
+    };
+    pass_b(r0, fk, tk, sk, lmk);
+    for (int64_t cb = r0 + 4 * CH; cb < r1; cb += 4 * CH) {
+        float4 fv[CH], tv[CH], sv[CH];
+#pragma unroll
+        for (int j = 0; j < CH; ++j) {
+            const int64_t r = cb + L.q + 4 * j, rr = r < r1 ? r : r0;
+            fv[j] = ld4(f + rr * 64 + L.ch);
+            tv[j] = ld4(t + rr * 64 + L.ch);
+            sv[j] = ld4(s + rr * 64 + L.ch);
+        }
+        pass_b(cb, fv, tv, sv, nullptr);
     }
     zacc = red_q4(zacc);
     if (L.q == 0) st4(z1 + gi * 64 + L.ch, zacc);
+    // the z-bar half of the attention logit (constant per graph; kept for the
+    // record, the softmax above and its backward do not depend on it)
+    const float cst = red16(dot4(ld4(watt + L.ch), zacc)) + *battp;
     // ---- KL of the last graph only, duplicated (models.py:657-659) ----
-    if (gi == B - 1) {
-        const float4 se = sig + f4(kKlEps);
-        const float4 den = se * se;
-        float4 qacc = f4(0.f);
-        for (int64_t cb = r0; cb < r1; cb += 4 * CH) {
-            float4 tv[CH], fv[CH];
-            float ug[CH];
-#pragma unroll
-            for (int j = 0; j < CH; ++j) {
-                const int64_t r = cb + L.q + 4 * j, rr = r < r1 ? r : r0;
-                tv[j] = ld4(t + rr * 64 + L.ch);
-                fv[j] = ld4(f + rr * 64 + L.ch);
-                ug[j] = u_gate[rr];
-            }
-#pragma unroll
-            for (int j = 0; j < CH; ++j) {
-                const float4 y = gm * ((tv[j] - m_use) * rstd) + bt;
-                const float p = red16(dot4(w2c, relu4(y))) + b2;
-                const float lm = gate_lambda(ug[j], p);
-                const float4 d = (lm * fv[j] + (1.f - lm) * mu) - mu;
-                const float4 z = make_float4(d.x / se.x, d.y / se.y, d.z / se.z, d.w / se.w);
-                qacc = macc(z * z, cb + L.q + 4 * j < r1 ? 1.f : 0.f, qacc);
-            }
-        }
+    if (last) {
         qacc = red_q4(qacc);
+        const float4 den = se * se;
         float ksum = 0.f;
-        for (int64_t cb = r0; cb < r1; cb += 4 * CH) {
-            float4 tv[CH];
-            float ug[CH];
-#pragma unroll
-            for (int j = 0; j < CH; ++j) {
-                const int64_t r = cb + L.q + 4 * j, rr = r < r1 ? r : r0;
-                tv[j] = ld4(t + rr * 64 + L.ch);
-                ug[j] = u_gate[rr];
-            }
+        auto kl_store = [&](int64_t cb, const float *lmv) {
 #pragma unroll
             for (int j = 0; j < CH; ++j) {
                 const int64_t r = cb + L.q + 4 * j;
-                const float4 y = gm * ((tv[j] - m_use) * rstd) + bt;
-                const float p = red16(dot4(w2c, relu4(y))) + b2;
-                const float lm = gate_lambda(ug[j], p);
-                const float4 ns = (1.f - lm) * sig;
+                const float4 ns = (1.f - lmv[j]) * sig;
                 const float4 nn = ns * ns;
                 const float4 v = f4(0.5f) * make_float4(nn.x / den.x, nn.y / den.y, nn.z / den.z,
                                                         nn.w / den.w) + qacc;
@@ -324,55 +350,27 @@ __global__ __launch_bounds__(64) void interaction_fwd_k(
                     ksum += (v.x + v.y) + (v.z + v.w);
                 }
             }
+        };
+        kl_store(r0, lmk);
+        for (int64_t cb = r0 + 4 * CH; cb < r1; cb += 4 * CH) {
+            float4 tv[CH];
+            float ug[CH], lmv[CH];
+#pragma unroll
+            for (int j = 0; j < CH; ++j) {
+                const int64_t r = cb + L.q + 4 * j, rr = r < r1 ? r : r0;
+                tv[j] = ld4(t + rr * 64 + L.ch);
+                ug[j] = u_gate[rr];
+            }
+#pragma unroll
+            for (int j = 0; j < CH; ++j) {
+                const float4 y = gm * ((tv[j] - m_use) * rstd) + bt;
+                lmv[j] = gate_lambda(ug[j], red16(dot4(w2c, relu4(y))) + b2);
+            }
+            kl_store(cb, lmv);
         }
         // mean over the duplicated [2n, 64] tensor == mean over [n, 64]
         ksum = red_q(red16(ksum));
         if (kl_mean && threadIdx.x == 0) *kl_mean = ksum / (static_cast<float>(n) * 64.f);
-    }
-    // ---- attention: logit_v = w_lo . z1 + w_hi . s_v + b; softmax per graph ----
-    const float cst = red16(dot4(ld4(watt + L.ch), zacc)) + *battp;
-    const float4 whi = ld4(watt + 64 + L.ch);
-    float M = -INFINITY, S = 0.f;  // per row group, merged below
-    for (int64_t cb = r0; cb < r1; cb += 4 * CH) {
-        float4 sv[CH];
-#pragma unroll
-        for (int j = 0; j < CH; ++j) {
-            const int64_t r = cb + L.q + 4 * j, rr = r < r1 ? r : r0;
-            sv[j] = ld4(s + rr * 64 + L.ch);
-        }
-#pragma unroll
-        for (int j = 0; j < CH; ++j) {
-            const int64_t r = cb + L.q + 4 * j;
-            const float lg = red16(dot4(whi, sv[j])) + cst;
-            if (r < r1) {
-                if (L.c4 == 0) logit[r] = lg;
-                const float Mn = fmaxf(M, lg);
-                S = S * expf(M - Mn) + expf(lg - Mn);
-                M = Mn;
-            }
-        }
-    }
-#pragma unroll
-    for (int off = 16; off <= 32; off <<= 1) {  // merge the four row groups
-        const float Mo = __shfl_xor(M, off, kWave), So = __shfl_xor(S, off, kWave);
-        const float Mn = fmaxf(M, Mo);
-        S = (S == 0.f ? 0.f : S * expf(M - Mn)) + (So == 0.f ? 0.f : So * expf(Mo - Mn));
-        M = Mn;
-    }
-    const float invS = 1.f / S;
-    for (int64_t cb = r0; cb < r1; cb += 4 * CH) {
-        float4 sv[CH];
-#pragma unroll
-        for (int j = 0; j < CH; ++j) {
-            const int64_t r = cb + L.q + 4 * j, rr = r < r1 ? r : r0;
-            sv[j] = ld4(s + rr * 64 + L.ch);
-        }
-#pragma unroll
-        for (int j = 0; j < CH; ++j) {
-            const int64_t r = cb + L.q + 4 * j;
-            const float lg = red16(dot4(whi, sv[j])) + cst;
-            if (r < r1) st4(im + r * 128 + 64 + L.ch, (expf(lg - M) * invS) * sv[j]);
-        }
     }
     if (threadIdx.x == 0) {
         sl[kStSoftMax] = M;

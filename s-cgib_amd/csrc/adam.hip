@@ -8,28 +8,44 @@
 //
 // torch's fused / foreach paths need 4-5 launches per step for a model of
 // ~75 small tensors (step increments + chunked multi-tensor kernels); here
-// the tensor table travels by value in the kernel arguments (captured with
-// the launch in a HIP graph), every workgroup handles one 1024-element chunk
+// the tensor table (up to 80 tensors: one launch for the pretraining model)
+// travels by value in the kernel arguments (captured with the launch in a
+// HIP graph), every workgroup handles one 1024-element chunk
 // of one tensor, and the last workgroup to finish advances every tensor's
 // step counter (all workgroups read the step before they arrive).
 #include "common.h"
 
 namespace scgib {
 
-constexpr int kAdamMax = 48;       // tensors per launch (kernel-argument table)
+constexpr int kAdamMax = 80;       // tensors per launch (kernel-argument table, < 4 KB)
 constexpr int kAdamChunk = 1024;   // elements per workgroup
 
+// structure of arrays (no per-entry padding): 80 tensors in 3.8 KB of kernel
+// arguments, so a whole model's ~75 hot-path tensors take one launch
 struct AdamTable {
-    scgib_adam_tensor t[kAdamMax];
+    float *param[kAdamMax];
+    const float *grad[kAdamMax];
+    float *exp_avg[kAdamMax];
+    float *exp_avg_sq[kAdamMax];
+    float *step[kAdamMax];
+    int32_t numel[kAdamMax];
     int32_t chunk0[kAdamMax + 1];  // first chunk of tensor i; chunk0[n] = grid
     int32_t n;
+};
+static_assert(sizeof(AdamTable) <= 4096, "kernel-argument table");
+
+struct AdamRef {
+    float *param;
+    const float *grad;
+    float *exp_avg, *exp_avg_sq;
+    int64_t numel;
 };
 
 // Precision mirrors torch's fused Adam (ATen fused_adam_utils.cuh): the
 // hyper-parameters are doubles, so the weight decay, both moment updates and
 // eps enter in double and round to fp32 on assignment; the bias corrections
 // are computed in double and rounded to fp32; the final update is fp32.
-__device__ __forceinline__ void adam_chunk(const scgib_adam_tensor &T, int64_t base,
+__device__ __forceinline__ void adam_chunk(const AdamRef &T, int64_t base,
                                            float step_size, float bc2_sqrt, double beta1,
                                            double beta2, double eps, double wd) {
     float p[4], g[4], m[4], v[4];
@@ -66,10 +82,15 @@ __global__ __launch_bounds__(256) void adam_step_k(const AdamTable tab, double l
     // tensor of this chunk: one parallel compare over the table (lane q holds
     // chunk0[q]) instead of a dependent scalar-load chain
     const int lane = threadIdx.x & 63;
-    const bool le = lane < tab.n && tab.chunk0[lane < tab.n ? lane : 0] <= b;
-    const int i = __popcll(__ballot(le)) - 1;
-    const scgib_adam_tensor &T = tab.t[i];
-    const float t = *T.step + 1.f;
+    int i = -1;
+#pragma unroll
+    for (int r = 0; r < (kAdamMax + 63) / 64; ++r) {
+        const int q = 64 * r + lane;
+        const bool le = q < tab.n && tab.chunk0[q < tab.n ? q : 0] <= b;
+        i += __popcll(__ballot(le));
+    }
+    const AdamRef T{tab.param[i], tab.grad[i], tab.exp_avg[i], tab.exp_avg_sq[i], tab.numel[i]};
+    const float t = *tab.step[i] + 1.f;
     const float bc1 = static_cast<float>(1 - pow(beta1, static_cast<double>(t)));
     const float bc2_sqrt = static_cast<float>(sqrt(1 - pow(beta2, static_cast<double>(t))));
     const float step_size = static_cast<float>(lr / bc1);
@@ -82,7 +103,7 @@ __global__ __launch_bounds__(256) void adam_step_k(const AdamTable tab, double l
                  gridDim.x - 1;
     __syncthreads();
     if (s_last) {  // every workgroup has read its step: advance all of them at once
-        if (threadIdx.x < tab.n) *tab.t[threadIdx.x].step += 1.f;
+        if (threadIdx.x < tab.n) *tab.step[threadIdx.x] += 1.f;
         if (threadIdx.x == 0) *counter = 0u;
     }
 }
@@ -171,7 +192,13 @@ extern "C" int scgib_adam_step(const scgib_adam_tensor *tensors, int32_t n_tenso
         if (T.numel < 0 || !T.step || (T.numel > 0 && (!T.param || !T.grad || !T.exp_avg ||
                                                        !T.exp_avg_sq)))
             return SCGIB_EINVAL;
-        tab.t[i] = T;
+        if (T.numel > 0x7fffffff) return SCGIB_EUNSUPPORTED;
+        tab.param[i] = T.param;
+        tab.grad[i] = T.grad;
+        tab.exp_avg[i] = T.exp_avg;
+        tab.exp_avg_sq[i] = T.exp_avg_sq;
+        tab.step[i] = T.step;
+        tab.numel[i] = static_cast<int32_t>(T.numel);
         tab.chunk0[i] = static_cast<int32_t>(chunks);
         chunks += (T.numel + kAdamChunk - 1) / kAdamChunk;
         if (chunks > 0x7fffffff) return SCGIB_EUNSUPPORTED;
@@ -181,7 +208,11 @@ extern "C" int scgib_adam_step(const scgib_adam_tensor *tensors, int32_t n_tenso
         tab.chunk0[n_tensors] = 1;
         chunks = 1;
     }
-    for (int i = n_tensors; i < kAdamMax; ++i) tab.t[i] = scgib_adam_tensor{};
+    for (int i = n_tensors; i < kAdamMax; ++i) {
+        tab.param[i] = tab.exp_avg[i] = tab.exp_avg_sq[i] = tab.step[i] = nullptr;
+        tab.grad[i] = nullptr;
+        tab.numel[i] = 0;
+    }
     adam_step_k<<<dim3(static_cast<unsigned>(chunks)), 256, 0, as_stream(stream)>>>(
         tab, lr, beta1, beta2, eps, weight_decay, counter);
     return launch_status();

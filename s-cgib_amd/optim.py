@@ -1,4 +1,4 @@
-"""Adam on the device in one launch per 48 tensors (scgib_adam_step).
+"""Adam on the device in one launch per 80 tensors (scgib_adam_step).
 
 Drop-in for the optimizer every reference script builds,
 ``torch.optim.Adam(model.parameters(), lr=args.lr, weight_decay=5e-5)``

@@ -4,7 +4,7 @@ optimizer of every reference script (exp_molhiv.py:53: lr, weight_decay=5e-5).
 Same random parameters and gradient sequence through both; parameters and
 the three state tensors agree with torch's fused Adam (the same formula at
 the same precisions: measured bit-identical; the bar is relative 1e-6).  Covers tensor counts above one
-launch's table (48), sizes that are not multiples of the 1024-element chunk,
+launch's table (80), sizes that are not multiples of the 1024-element chunk,
 empty tensors, parameters without gradients, several param groups, and
 replay from a captured HIP graph."""
 import copy
@@ -14,7 +14,7 @@ import torch
 
 pytestmark = pytest.mark.gpu
 
-SHAPES = [(64, 64), (64,), (64, 32), (1,), (0,), (3, 7), (2049,), (64, 128), (5, 1031)] * 6
+SHAPES = [(64, 64), (64,), (64, 32), (1,), (0,), (3, 7), (2049,), (64, 128), (5, 1031)] * 10
 
 
 @pytest.fixture(scope="module")

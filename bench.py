@@ -331,7 +331,7 @@ def main():
         else:  # one-launch device Adam, same arithmetic (tests/test_gpu_optim.py)
             opt = pkg.optim.Adam(model.parameters(), lr=1e-4, weight_decay=5e-5)
         n_cap, e_cap, mgn, ego_caps = pkg.graph.StaticBatch.capacities(pool_host, a.k, slack=1.02)
-        static = pkg.graph.StaticBatch(a.batch, n_cap, e_cap, F_in, mgn, ego_caps, dev)
+        static = pkg.graph.StaticBatch(a.batch, n_cap, e_cap, F_in, mgn, ego_caps, dev, k=a.k)
         padded = []
         for gh in pool_host:
             gx = pkg.graph.GraphBatch.from_edges(*[t.numpy() for t in gh.edges()], gh.num_nodes(),

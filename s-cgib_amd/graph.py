@@ -418,6 +418,29 @@ def egonet_batch(g: GraphBatch, k: int, x=None):
     return ego
 
 
+def ego_bounds(g, k):
+    """(ego-batch nodes, bound on ego-batch edges, max in-degree) of host
+    batch ``g``'s k-hop ego-nets: nodes = sum_v |ball_k(v)|, edges <= sum_v
+    sum_{u in ball_k(v)} deg(u).  k = 1: |ball(v)| = 1 + deg(v) - selfloop(v);
+    k > 1: boolean reachability (I + A)^k on the host."""
+    info = g.host_info
+    deg = info["deg"].astype(np.int64)
+    dmax = int(deg.max()) if len(deg) else 0
+    if k == 1:
+        ball = 1 + deg - info["selfloops"]
+        return int(ball.sum()), int((deg * ball).sum()), dmax
+    import scipy.sparse as sp
+    n = g.num_nodes()
+    rp = g.rowptr.cpu().numpy().astype(np.int64)
+    col = g.col.cpu().numpy()[: rp[-1]].astype(np.int64)
+    a = sp.csr_matrix((np.ones(len(col), np.int8), col, rp), shape=(n, n))
+    step = (a + sp.identity(n, dtype=np.int8, format="csr")).astype(bool).astype(np.int32)
+    r = step
+    for _ in range(k - 1):
+        r = (r @ step).astype(bool).astype(np.int32)
+    return int(r.nnz), int((r @ deg).sum()), dmax
+
+
 # k = 1 ego-nets through the two-launch builder when its degree bound holds
 # (tests switch it off to compare with the general bitmap builder)
 EGO_K1_FAST = True
@@ -464,8 +487,9 @@ class StaticBatch:
     device-to-device copies; nothing is read back to the host.
     """
 
-    def __init__(self, B, n_cap, e_cap, n_feat, max_graph_nodes, ego_caps, device):
+    def __init__(self, B, n_cap, e_cap, n_feat, max_graph_nodes, ego_caps, device, k=1):
         self.B, self.n_cap, self.e_cap, self.n_feat = B, n_cap, e_cap, n_feat
+        self.k = int(k)
         # one byte blob (rowptr | col | graph_ptr | dims | x, 256-B aligned
         # sections) so that loading a batch is a single device copy
         self.blob = torch.zeros(self._layout()[-1], dtype=torch.uint8, device=device)
@@ -499,23 +523,20 @@ class StaticBatch:
 
     @staticmethod
     def capacities(host_batches, k, slack=1.0):
-        """(n_cap, e_cap, max_graph_nodes, (ego nodes cap, ego edges cap)) covering
-        every host-collated batch given (k = 1 bounds)."""
-        if k != 1:
-            raise NotImplementedError("capacity mode is implemented for k = 1 ego-nets")
+        """(n_cap, e_cap, max_graph_nodes, (ego nodes cap, ego edges cap, max
+        in-degree)) covering every host-collated batch given,
+        for k-hop ego-nets (k = 1 in closed form, k > 1 from the host
+        reachability of each batch, as the reference's offline pass would)."""
         n = max(g.num_nodes() for g in host_batches)
         e = max(g.num_edges() for g in host_batches)
         mgn = max(g.max_graph_nodes for g in host_batches)
         ns = es = dmax = 0
         for g in host_batches:
-            info = g.host_info
-            ball = 1 + info["deg"] - info["selfloops"]
-            ns = max(ns, int(ball.sum()))
-            es = max(es, int((info["deg"] * ball).sum()))
-            dmax = max(dmax, int(info["deg"].max()) if len(info["deg"]) else 0)
+            bn, be, bd = ego_bounds(g, k)
+            ns, es, dmax = max(ns, bn), max(es, be), max(dmax, bd)
         f = lambda v: int(v * slack) + 1  # noqa: E731
         # ego caps: (nodes, edges, max in-degree — selects the k = 1 builder)
-        return f(n), f(e), mgn, (f(ns), f(es), dmax)
+        return f(n), f(e), mgn, (f(ns), f(es), dmax if k == 1 else 1 << 30)
 
     def pad(self, g):
         """Device copy of host batch ``g`` padded to this batch's capacities."""
@@ -527,9 +548,9 @@ class StaticBatch:
             raise _lib.ScgibError("batch has a larger molecule than the captured bitmap width")
         if not g.host_info["validated"]:
             raise _lib.ScgibError("batch edges leave their molecule")
-        ball = 1 + g.host_info["deg"] - g.host_info["selfloops"]
         ns, es = self.graph.ego_caps[:2]
-        if int(ball.sum()) > ns or int((g.host_info["deg"] * ball).sum()) > es:
+        bn, be, _ = ego_bounds(g, self.k)
+        if bn > ns or be > es:
             raise _lib.ScgibError("batch's ego-nets exceed the ego capacities")
         if len(self.graph.ego_caps) > 2 and len(g.host_info["deg"]) and \
                 int(g.host_info["deg"].max()) > self.graph.ego_caps[2]:

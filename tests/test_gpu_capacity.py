@@ -33,11 +33,11 @@ def dev():
     return torch.device("cuda", 0)
 
 
-def _model(pkg, dev, layers=5):
+def _model(pkg, dev, layers=5, k=1):
     args = SimpleNamespace(recons_type="adj", useAtt=1, readout_f="sum", d_transfer=32,
                            batch_size=B, gin_layers=layers)
     torch.manual_seed(11)
-    m = pkg.models.Mainmodel(args, F_IN, 64, 4, 4, 1, "GIN").to(dev).train()
+    m = pkg.models.Mainmodel(args, F_IN, 64, 4, 4, k, "GIN").to(dev).train()
     with torch.no_grad():  # non-trivial BN affine so the BN paths are exercised
         for enc in (m.Encoder1, m.Encoder2):
             for bn in enc.batch_norms:
@@ -55,9 +55,9 @@ def _batches(pkg, seeds):
     return out
 
 
-def _step(model, g, x, noise, dev):
+def _step(model, g, x, noise, dev, k=1):
     model.zero_grad(set_to_none=True)
-    _, kl, con, rec = model(g, x, None, None, None, 1, None, 1, dev, B, noise=noise)
+    _, kl, con, rec = model(g, x, None, None, None, 1, None, k, dev, B, noise=noise)
     loss = kl + rec + con
     loss.backward()
     return torch.stack([kl, con, rec, loss]).detach()
@@ -101,12 +101,13 @@ def test_capacity_mode_eager_matches_exact(pkg, dev):
         _compare(exact_m, cap_m, le, lc)
 
 
-def test_graph_replay_matches_exact_over_batches(pkg, dev):
+@pytest.mark.parametrize("k", [1, 2])
+def test_graph_replay_matches_exact_over_batches(pkg, dev, k):
     hosts = _batches(pkg, (4, 5, 6, 7))
-    n_cap, e_cap, mgn, caps = pkg.graph.StaticBatch.capacities(hosts, 1, slack=1.02)
-    static = pkg.graph.StaticBatch(B, n_cap, e_cap, F_IN, mgn, caps, dev)
+    n_cap, e_cap, mgn, caps = pkg.graph.StaticBatch.capacities(hosts, k, slack=1.02)
+    static = pkg.graph.StaticBatch(B, n_cap, e_cap, F_IN, mgn, caps, dev, k=k)
     padded = [static.pad(gh) for gh in hosts]
-    exact_m = _model(pkg, dev)
+    exact_m = _model(pkg, dev, k=k)
     cap_m = copy.deepcopy(exact_m)
     s_ug = torch.zeros(n_cap, device=dev)
     s_uf = torch.zeros(n_cap, 64, device=dev)
@@ -117,13 +118,13 @@ def test_graph_replay_matches_exact_over_batches(pkg, dev):
     snap = copy.deepcopy(cap_m.state_dict())
     with torch.cuda.stream(side):
         static.load(padded[0])
-        _step(cap_m, static.graph, static.x, (s_ug, s_uf), dev)
+        _step(cap_m, static.graph, static.x, (s_ug, s_uf), dev, k)
     torch.cuda.current_stream().wait_stream(side)
     cap_m.load_state_dict(snap)  # undo the warm-up's BN running updates
     cap_m.zero_grad(set_to_none=True)
     graph = torch.cuda.CUDAGraph()
     with torch.cuda.graph(graph):
-        _, kl, con, rec = cap_m(static.graph, static.x, None, None, None, 1, None, 1, dev, B,
+        _, kl, con, rec = cap_m(static.graph, static.x, None, None, None, 1, None, k, dev, B,
                                 noise=(s_ug, s_uf))
         loss = kl + rec + con
         loss.backward()
@@ -134,7 +135,7 @@ def test_graph_replay_matches_exact_over_batches(pkg, dev):
         n = gh.num_nodes()
         ug, uf = _noise(n_cap, dev, 200 + i)
         g = gh.to(dev)
-        le = _step(exact_m, g, g.ndata["x"], (ug[:n], uf[:n]), dev)
+        le = _step(exact_m, g, g.ndata["x"], (ug[:n], uf[:n]), dev, k)
         s_ug.copy_(ug)
         s_uf.copy_(uf)
         static.load(padded[i])

@@ -340,3 +340,17 @@ def test_csr_cache_reference_ingest_goldens(pkg, tmp_path):
         s, t = c.graph(j).edges()
         np.testing.assert_array_equal(s.numpy(), d[f"m{i}_src"])
         np.testing.assert_array_equal(t.numpy(), d[f"m{i}_dst"])
+
+
+def test_ego_bounds_match_oracle_sizes(pkg):
+    """graph.ego_bounds (capacity sizing for k-hop ego-nets) equals the oracle's
+    ego-net sizes for the node count and bounds the edge count."""
+    from oracle import egonet
+    mols = pkg.synth.molecules(40, "pcqm4mv2", seed=3)
+    g, _ = pkg.graph.collate_pyg(mols)
+    for k in (1, 2, 3):
+        ns, es, dmax = pkg.graph.ego_bounds(g, k)
+        sizes, ecount, _, _, _ = egonet.egonets(g.rowptr.numpy(), g.col.numpy(), k)
+        assert ns == int(sizes.sum())
+        assert es >= int(ecount.sum())
+        assert dmax == int(np.diff(g.rowptr.numpy()).max())

@@ -108,6 +108,17 @@ int scgib_gin_aggregate(const float *h, const int32_t *rowptr, const int32_t *co
 int64_t scgib_gin_tiles(int64_t n_nodes);
 int64_t scgib_gin_slab_floats(int64_t n_nodes, int32_t d_in);
 int64_t scgib_gin_bwd_slabs(int64_t n_nodes);
+/* Up to scgib_slab_reduce_max_jobs() independent scgib_slab_reduce's in one
+ * launch (same fixed order per job). */
+typedef struct {
+    const float *slab;
+    float *out;
+    int64_t width;
+    int32_t n_slabs;
+    int32_t pad_;
+} scgib_slab_job;
+int64_t scgib_slab_reduce_max_jobs(void);
+int scgib_slab_reduce_multi(const scgib_slab_job *jobs, int32_t n_jobs, scgib_stream_t stream);
 int scgib_slab_reduce(const float *slab, int32_t n_slabs, int64_t width, float *out,
                       scgib_stream_t stream);
 int scgib_gin_layer_fwd(const float *h_in, int32_t d_in, const float *in_stat,

@@ -88,6 +88,8 @@ SIGNATURES = {
     "scgib_recon_partials_floats": (_I64, [_I64]),
     "scgib_recon_fwd": (ctypes.c_int, [_P, _P, _P, _I64, _I64, _P, _P, _P, _P, _P]),
     "scgib_recon_bwd": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _I64, _P, _P, _P, _P]),
+    "scgib_slab_reduce_max_jobs": (_I64, []),
+    "scgib_slab_reduce_multi": (ctypes.c_int, [_P, _I32, _P]),
     "scgib_grad_pack_max_tensors": (_I64, []),
     "scgib_grad_pack": (ctypes.c_int, [_P, _I32, _P, _P]),
     "scgib_grad_unpack": (ctypes.c_int, [_P, _I32, _P, _F, _P]),
@@ -115,6 +117,12 @@ class AdamTensor(ctypes.Structure):
     _fields_ = [("param", ctypes.c_void_p), ("grad", ctypes.c_void_p),
                 ("exp_avg", ctypes.c_void_p), ("exp_avg_sq", ctypes.c_void_p),
                 ("step", ctypes.c_void_p), ("numel", ctypes.c_int64)]
+
+class SlabJob(ctypes.Structure):
+    """scgib_slab_job (include/scgib.h)."""
+    _fields_ = [("slab", ctypes.c_void_p), ("out", ctypes.c_void_p), ("width", ctypes.c_int64),
+                ("n_slabs", ctypes.c_int32), ("pad_", ctypes.c_int32)]
+
 
 class GradSlice(ctypes.Structure):
     """scgib_grad_slice (include/scgib.h)."""

@@ -43,6 +43,9 @@ _AUX_PENDING = set()
 # 1.5 % faster aside (the ~15 us single-workgroup kernel leaves the critical
 # path; its fork/join edges cost less)
 RU_ASIDE = os.environ.get("SCGIB_RU_ASIDE", "1") != "0"
+# encoder backward: all layers' weight-gradient slabs reduced by one launch at
+# the end (scgib_slab_reduce_multi) instead of one launch per layer
+BATCH_SLABS = os.environ.get("SCGIB_BATCH_SLABS", "1") != "0"
 # encoder-pair backward: capture the ego chain before the core chain (off:
 # measured 2 % slower — the replayed graph's queue assignment follows capture
 # order in ways that favour the core chain first)
@@ -275,6 +278,7 @@ class _GinEncoder(torch.autograd.Function):
         grads = [None] * (6 * L)
         dagg_next, dwt = None, None
         nslab = int(_lib.query("scgib_gin_bwd_slabs", n))
+        jobs, keep = [], []
         for l in reversed(range(L)):
             agg, r, z2, stat = saved[4 * l: 4 * l + 4]
             w1, _, w2 = params[6 * l], params[6 * l + 1], params[6 * l + 2]
@@ -318,7 +322,11 @@ class _GinEncoder(torch.autograd.Function):
                         _p(stat), _p(coef), _p(w1c), _p(w2c), n, _p(dagg), _p(slab), _NULL,
                         _p(gr.dims), _byref(bpend), st)
             wgrad = torch.empty(width, dtype=torch.float32, device=dev)
-            _lib.call("scgib_slab_reduce", _p(slab), nslab, width, _p(wgrad), st)
+            if BATCH_SLABS:  # reduced together after the last layer (one launch)
+                jobs.append(_lib.SlabJob(slab.data_ptr(), wgrad.data_ptr(), width, nslab, 0))
+                keep.append(slab)
+            else:
+                _lib.call("scgib_slab_reduce", _p(slab), nslab, width, _p(wgrad), st)
             o = HIDDEN * HIDDEN
             grads[6 * l + 2] = wgrad[:o].view(HIDDEN, HIDDEN)
             grads[6 * l + 0] = wgrad[o:o + HIDDEN * d_in].view(HIDDEN, d_in)
@@ -331,6 +339,14 @@ class _GinEncoder(torch.autograd.Function):
             grads[6 * l + 4] = bn_g[0]
             grads[6 * l + 5] = bn_g[1]
             dagg_next = dagg
+        if jobs:  # every layer's weight-gradient slabs, one fixed-order reduce launch
+            cap = int(_lib.query("scgib_slab_reduce_max_jobs"))
+            for i0 in range(0, len(jobs), cap):
+                chunk = jobs[i0:i0 + cap]
+                table = (_lib.SlabJob * len(chunk))(*chunk)
+                _lib.call("scgib_slab_reduce_multi", ctypes.cast(table, ctypes.c_void_p),
+                          len(chunk), st)
+            del keep  # slabs stay allocated until the launch is enqueued
         if pre:
             return (None, None, None, None, None, dwt, None, *grads)
         # d h0 = (1+eps_0) d(agg_0) + sum over out-edges (transposed aggregation)

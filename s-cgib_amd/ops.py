@@ -50,6 +50,9 @@ BATCH_SLABS = os.environ.get("SCGIB_BATCH_SLABS", "1") != "0"
 # measured 2 % slower — the replayed graph's queue assignment follows capture
 # order in ways that favour the core chain first)
 EGO_FIRST = os.environ.get("SCGIB_EGO_FIRST", "0") != "0"
+# encoder pair: enqueue the two chains layer by layer alternately (forward and
+# backward) instead of one whole chain after the other
+INTERLEAVE = os.environ.get("SCGIB_INTERLEAVE", "1") != "0"
 
 
 def launch_aside(fn, *tensors):
@@ -141,6 +144,34 @@ def _gin_layer_params(gin):
     return out
 
 
+def _drain(gen):
+    """Run a step generator to completion and return its value."""
+    while True:
+        try:
+            next(gen)
+        except StopIteration as stop:
+            return stop.value
+
+
+def _interleave(first, first_stream, second, second_stream):
+    """Advance two step generators alternately, each on its own stream (the
+    launches of two encoders enqueued layer by layer: in a replayed HIP graph
+    both chains then start without waiting for the other's submissions).
+    Returns (first's value, second's value)."""
+    out, live = [None, None], [True, True]
+    gens = ((first, first_stream), (second, second_stream))
+    while live[0] or live[1]:
+        for i, (gen, stream) in enumerate(gens):
+            if not live[i]:
+                continue
+            with torch.cuda.stream(stream):
+                try:
+                    next(gen)
+                except StopIteration as stop:
+                    out[i], live[i] = stop.value, False
+    return out[0], out[1]
+
+
 class _GinEncoder(torch.autograd.Function):
     """GIN.forward (models.py:66-72) as fused HIP layers; see gin_layer.hip.
 
@@ -154,6 +185,14 @@ class _GinEncoder(torch.autograd.Function):
         """readout = (ptr, nseg, seg_dims): also return the segment sums of
         the output (dgl.sum_nodes, fused with the last BN + ReLU); the backward
         then takes (g_out, g_readout)."""
+        return _drain(_GinEncoder.forward_steps(ctx, h0, graph, gin, training, x, wt, nmap,
+                                                *params, readout=readout))
+
+    @staticmethod
+    def forward_steps(ctx, h0, graph, gin, training, x, wt, nmap, *params, readout=None):
+        """forward as a generator that yields after each layer's launch, so
+        two encoders on two streams can be enqueued (captured) layer by layer
+        in alternation (_GinEncoderPair); returns forward's result."""
         pre = x is not None
         if pre:
             x = _f32(x, "gin_encoder x")
@@ -234,6 +273,7 @@ class _GinEncoder(torch.autograd.Function):
                 bn.running_var.data_ptr() if track else None,
                 bn.num_batches_tracked.data_ptr() if track else None,
                 stat.data_ptr(), float(bn.eps), momentum) if defer else None
+            yield
         out = torch.empty(n, HIDDEN, dtype=torch.float32, device=dev)
         ro = seg = None
         if readout is not None:
@@ -254,6 +294,11 @@ class _GinEncoder(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, g_out, g_readout=None):
+        return _drain(_GinEncoder.backward_steps(ctx, g_out, g_readout))
+
+    @staticmethod
+    def backward_steps(ctx, g_out, g_readout=None):
+        """backward as a generator (yields after each layer), see forward_steps."""
         L, gr, pre = ctx.L, ctx.graph, ctx.pre
         t = ctx.saved_tensors
         saved, params = t[: 4 * L], t[4 * L: 4 * L + 6 * L]
@@ -339,6 +384,7 @@ class _GinEncoder(torch.autograd.Function):
             grads[6 * l + 4] = bn_g[0]
             grads[6 * l + 5] = bn_g[1]
             dagg_next = dagg
+            yield
         if jobs:  # every layer's weight-gradient slabs, one fixed-order reduce launch
             cap = int(_lib.query("scgib_slab_reduce_max_jobs"))
             for i0 in range(0, len(jobs), cap):
@@ -404,12 +450,19 @@ class _GinEncoderPair(torch.autograd.Function):
         ctx.sub = (_Ctx(), _Ctx())
         ctx.side, ctx.ne = side, ne
         side.wait_stream(main)
-        with torch.cuda.stream(side):  # Encoder2 + its readout (dgl.sum_nodes per ego-net)
-            s, ro = _GinEncoder.forward(ctx.sub[0], None, ego, gin_ego, training, x, wt, nmap,
-                                        *params[:ne],
-                                        readout=(ego.graph_ptr, ego.batch_size, ego.seg_dims))
-        f = _GinEncoder.forward(ctx.sub[1], None, core, gin_core, training, x, wt, None,
-                                *params[ne:])
+        # Encoder2 + its readout (dgl.sum_nodes per ego-net) on ``side``,
+        # Encoder1 on the current stream, enqueued layer by layer alternately
+        ego_steps = _GinEncoder.forward_steps(
+            ctx.sub[0], None, ego, gin_ego, training, x, wt, nmap, *params[:ne],
+            readout=(ego.graph_ptr, ego.batch_size, ego.seg_dims))
+        core_steps = _GinEncoder.forward_steps(ctx.sub[1], None, core, gin_core, training, x, wt,
+                                               None, *params[ne:])
+        if INTERLEAVE:
+            (s, ro), f = _interleave(ego_steps, side, core_steps, main)
+        else:
+            with torch.cuda.stream(side):
+                s, ro = _drain(ego_steps)
+            f = _drain(core_steps)
         outs = (s, ro, f)
         ctx.lin = w0 is not None
         if ctx.lin:  # compressor[0] on the (shorter) core chain, before the join
@@ -440,7 +493,7 @@ class _GinEncoderPair(torch.autograd.Function):
         side.wait_stream(main)
         dw0 = db0 = None
         g_f_in = g_f
-        if EGO_FIRST:  # enqueue (capture) the critical ego chain before the core chain
+        if EGO_FIRST and not INTERLEAVE:  # capture the critical ego chain first
             ge = _GinEncoder.backward(ctx.sub[0], g_s, g_ro)
         with torch.cuda.stream(side):
             if ctx.lin and g_t is not None:
@@ -456,8 +509,12 @@ class _GinEncoderPair(torch.autograd.Function):
                           _p(slab), _p(wg), _p(ctx.core_dims), _stream())
                 dw0, db0 = wg[: HIDDEN * HIDDEN].view(HIDDEN, HIDDEN), wg[HIDDEN * HIDDEN:]
                 g_f = df_total
-            gc = _GinEncoder.backward(ctx.sub[1], g_f)
-        if not EGO_FIRST:
+            if not INTERLEAVE:
+                gc = _GinEncoder.backward(ctx.sub[1], g_f)
+        if INTERLEAVE:  # both chains enqueued layer by layer, the ego chain first
+            ge, gc = _interleave(_GinEncoder.backward_steps(ctx.sub[0], g_s, g_ro), main,
+                                 _GinEncoder.backward_steps(ctx.sub[1], g_f), side)
+        elif not EGO_FIRST:
             ge = _GinEncoder.backward(ctx.sub[0], g_s, g_ro)
         main.wait_stream(side)
         for g in (*gc, dw0, db0):

@@ -254,14 +254,16 @@ int scgib_egonet_count(const int32_t *rowptr, const int32_t *col, const int32_t 
                        int64_t n_graphs, int64_t n_nodes, int32_t k, int32_t max_graph_nodes,
                        int32_t *ego_ptr, int32_t *ego_eptr, void *workspace, int32_t *err,
                        const int32_t *dims, scgib_stream_t stream);
-/* k = 1 fast path, both passes in two launches: ball(v) = sorted unique
- * ({v} u N(v)) as a register list (no molecule bitmap, no graph_ptr search),
- * batched loads; same outputs as scgib_egonet_count + scgib_egonet_fill
- * (ego_ptr, ego_eptr exclusive scans; ego_nodes; sub_rowptr/sub_col in DGL
- * order; ego_dims).  Requires every in-degree <= scgib_egonet_k1_max_degree()
- * and edges inside their molecule (the caller checks both on the host).
+/* k = 1 fast path, both passes in two launches: ball(v) = {v} u N(v) as a
+ * 128-bit window bitmap centred on v (no molecule bitmap, no graph_ptr
+ * search), batched loads; same outputs as scgib_egonet_count +
+ * scgib_egonet_fill (ego_ptr, ego_eptr exclusive scans; ego_nodes;
+ * sub_rowptr/sub_col in DGL order; ego_dims).  Requires every in-degree <=
+ * scgib_egonet_k1_max_degree(), molecules <= scgib_egonet_k1_max_graph_nodes()
+ * atoms and edges inside their molecule (the caller checks them on the host).
  * workspace: scgib_egonet_workspace_bytes(n). */
 int64_t scgib_egonet_k1_max_degree(void);
+int64_t scgib_egonet_k1_max_graph_nodes(void);
 int scgib_egonet_k1_build(const int32_t *rowptr, const int32_t *col, int64_t n_nodes,
                           int32_t *ego_ptr, int32_t *ego_eptr, void *workspace,
                           int32_t *ego_nodes, int32_t *sub_rowptr, int32_t *sub_col,

@@ -17,6 +17,8 @@
 // the fill pass writes ego nodes and CSR rows directly in DGL order
 // (node_subgraph: rows in ball order, columns in CSR order).
 // Integer/pointer-chasing work: no MFMA, all index reads L2-resident.
+#include <type_traits>
+
 #include "common.h"
 
 namespace scgib {
@@ -243,88 +245,94 @@ __global__ __launch_bounds__(256) void egonet_fill_k(
 }
 
 // ---------------------------------------------------------------------------
-// k = 1 fast path (the pretraining configuration): ball(v) = sorted unique
-// ({v} ∪ N(v)) — DGL's unique(cat(frontiers)) for one hop — held as a short
-// sorted list in registers instead of a bitmap over the molecule, so the
-// molecule's bounds (a binary search over graph_ptr) are not needed, and
-// every load round is batched: row pointers of v; its <= kK1Deg neighbour
-// ids; the row pointers of the <= kK1Deg + 1 ball members; their neighbour
-// ids (clamped, always-valid addresses, predicates applied to the values).
-// Requires max in-degree <= kK1Deg and edges inside their molecule
-// (host-checked, GraphBatch.host_info).  Two launches: count + block scan,
-// then fill with the cross-block scan fix-up folded in (each block sums the
-// <= a few hundred preceding block totals itself).
+// k = 1 fast path (the pretraining configuration): ball(v) = {v} ∪ N(v) —
+// DGL's unique(cat(frontiers)) for one hop — as a 128-bit window bitmap
+// centred on v (bit 64 + u - v), so neither the molecule's bounds (a binary
+// search over graph_ptr) nor a per-molecule bitmap are needed: with every
+// molecule <= 64 atoms, |u - v| < 64 inside a molecule.  Ascending bits give
+// DGL's sorted order; the relabelled id of a member is a popcount.  Every
+// load round is batched: row pointers of v; its <= kK1Deg neighbour ids; the
+// row pointers of the ball members; their neighbour ids (members in groups of
+// kK1Grp, clamped always-valid addresses, predicates applied to the values).
+// Requires in-degree <= kK1Deg, molecules <= 64 atoms and edges inside their
+// molecule (host-checked).  Two launches: count + block scan, then fill with
+// the cross-block scan fix-up folded in.
 // ---------------------------------------------------------------------------
-constexpr int kK1Deg = 6, kK1Ball = kK1Deg + 1;
+constexpr int kK1Deg = 12, kK1Grp = 7, kK1Ball = kK1Deg + 1;
 
-struct K1Ball {
-    int32_t node[kK1Ball];  // ascending; entries >= nb repeat the last member
-    int32_t nb;
+struct K1Win {
+    uint64_t w[2];   // bit 64 + (u - v): u in ball(v)
+    int32_t v;
+    int32_t nb;      // |ball|
+    int32_t mem[kK1Ball];  // members, ascending (entries >= nb repeat the last)
 };
 
+__device__ __forceinline__ int32_t k1_index(const K1Win &b, int32_t u) {
+    const int32_t i = u - b.v + 64;
+    const uint64_t word = i < 64 ? b.w[0] : b.w[1];  // selects: no dynamic indexing
+    return (i >= 0 && i < 128 && ((word >> (i & 63)) & 1ull)) ? i : -1;
+}
+
+// members strictly below window index i
+__device__ __forceinline__ int32_t k1_rank(const K1Win &b, int32_t i) {
+    const uint64_t m = (1ull << (i & 63)) - 1ull;
+    return i < 64 ? __popcll(b.w[0] & m) : __popcll(b.w[0]) + __popcll(b.w[1] & m);
+}
+
 __device__ __forceinline__ void k1_ball(const int32_t *__restrict__ rowptr,
-                                        const int32_t *__restrict__ col, int32_t v, K1Ball &b) {
+                                        const int32_t *__restrict__ col, int32_t v, K1Win &b) {
     const int32_t beg = rowptr[v], end = rowptr[v + 1];
     const int32_t last = end > beg ? end - 1 : (beg > 0 ? beg - 1 : 0);  // a valid index
     int32_t nbr[kK1Deg];
 #pragma unroll
     for (int j = 0; j < kK1Deg; ++j) nbr[j] = col[beg + j < end ? beg + j : last];
-    const int32_t d = end - beg;
-    // merge v into the sorted neighbour list, dropping duplicates / a self-loop
-    int32_t nb = 0, prev = -1;
-    bool vin = false;
+    b.v = v;
+    b.w[0] = 0ull;
+    b.w[1] = 1ull;  // v itself: bit 64
 #pragma unroll
-    for (int j = 0; j <= kK1Deg; ++j) {
-        const bool have = j < d;
-        const int32_t w = have ? nbr[j < kK1Deg ? j : kK1Deg - 1] : 0x7fffffff;
-        if (!vin && v <= w) {  // v goes before w (or equals it: a self-loop)
-            b.node[nb < kK1Ball ? nb : kK1Ball - 1] = v;
-            ++nb;
-            prev = v;
-            vin = true;
-        }
-        if (have && w != prev) {
-            b.node[nb < kK1Ball ? nb : kK1Ball - 1] = w;
-            ++nb;
-            prev = w;
-        }
+    for (int j = 0; j < kK1Deg; ++j) {
+        const int32_t i = nbr[j] - v + 64;
+        const uint64_t bit = (beg + j < end && i >= 0 && i < 128) ? 1ull << (i & 63) : 0ull;
+        b.w[0] |= i < 64 ? bit : 0ull;
+        b.w[1] |= i < 64 ? 0ull : bit;
     }
-    b.nb = nb;
+    b.nb = __popcll(b.w[0]) + __popcll(b.w[1]);
+    // members in ascending order, statically indexed (registers, no scratch):
+    // member q = the lowest remaining bit; past the last, repeat it
+    uint64_t m0 = b.w[0], m1 = b.w[1];
+    int32_t prev = v;
 #pragma unroll
-    for (int r = 0; r < kK1Ball; ++r)
-        if (r >= nb) b.node[r] = b.node[nb - 1];
+    for (int q = 0; q < kK1Ball; ++q) {
+        const bool lo = m0 != 0ull, hi = m1 != 0ull;
+        const int32_t i = lo ? __ffsll(static_cast<unsigned long long>(m0)) - 1
+                             : 64 + __ffsll(static_cast<unsigned long long>(m1)) - 1;
+        const int32_t u = (lo || hi) ? v - 64 + i : prev;
+        b.mem[q] = u;
+        prev = u;
+        if (lo) m0 &= m0 - 1ull;
+        else if (hi) m1 &= m1 - 1ull;
+    }
 }
 
-// position of w in the ball, or -1
-__device__ __forceinline__ int32_t k1_rank(const K1Ball &b, int32_t w) {
-    int32_t rank = 0;
-    bool in = false;
-#pragma unroll
-    for (int r = 0; r < kK1Ball; ++r) {
-        const bool live = r < b.nb;
-        rank += live && b.node[r] < w ? 1 : 0;
-        in = in || (live && b.node[r] == w);
-    }
-    return in ? rank : -1;
-}
-
-// member rows and their neighbour ids, one batched round each
+// rows of members [g0, g0 + kK1Grp) and their neighbour ids, one batched round each
 struct K1Rows {
-    int32_t beg[kK1Ball], deg[kK1Ball];
-    int32_t w[kK1Ball][kK1Deg];
+    int32_t beg[kK1Grp], deg[kK1Grp];
+    int32_t w[kK1Grp][kK1Deg];
 };
 
+template <int G0>
 __device__ __forceinline__ void k1_rows(const int32_t *__restrict__ rowptr,
-                                        const int32_t *__restrict__ col, const K1Ball &b,
+                                        const int32_t *__restrict__ col, const K1Win &b,
                                         K1Rows &m) {
-    int32_t end[kK1Ball];
+    int32_t end[kK1Grp];
 #pragma unroll
-    for (int r = 0; r < kK1Ball; ++r) {
-        m.beg[r] = rowptr[b.node[r]];
-        end[r] = rowptr[b.node[r] + 1];
+    for (int r = 0; r < kK1Grp; ++r) {
+        const int32_t u = b.mem[G0 + r < kK1Ball ? G0 + r : kK1Ball - 1];
+        m.beg[r] = rowptr[u];
+        end[r] = rowptr[u + 1];
     }
 #pragma unroll
-    for (int r = 0; r < kK1Ball; ++r) {
+    for (int r = 0; r < kK1Grp; ++r) {
         m.deg[r] = end[r] - m.beg[r];
         const int32_t last = end[r] > m.beg[r] ? end[r] - 1 : (m.beg[r] > 0 ? m.beg[r] - 1 : 0);
 #pragma unroll
@@ -332,76 +340,79 @@ __device__ __forceinline__ void k1_rows(const int32_t *__restrict__ rowptr,
     }
 }
 
-// per-block inclusive scan of (a, b) over 256 threads (Hillis-Steele in LDS)
-__device__ __forceinline__ void block_scan2(int32_t &a, int32_t &b) {
-    __shared__ int32_t sa[256], sb[256];
-    sa[threadIdx.x] = a;
-    sb[threadIdx.x] = b;
-    __syncthreads();
-    for (int off = 1; off < 256; off <<= 1) {
-        int32_t xa = 0, xb = 0;
-        if (threadIdx.x >= off) {
-            xa = sa[threadIdx.x - off];
-            xb = sb[threadIdx.x - off];
+// inclusive scan of (a, b) over the 64 lanes of a wave (one workgroup)
+constexpr int kK1Block = 64;  // 64-thread workgroups: the ego-nets spread over 4x more CUs
+
+__device__ __forceinline__ void wave_scan2(int32_t &a, int32_t &b) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const int32_t xa = __shfl_up(a, off, kWave), xb = __shfl_up(b, off, kWave);
+        if (lane >= off) {
+            a += xa;
+            b += xb;
         }
-        __syncthreads();
-        sa[threadIdx.x] += xa;
-        sb[threadIdx.x] += xb;
-        __syncthreads();
     }
-    a = sa[threadIdx.x];
-    b = sb[threadIdx.x];
 }
 
-__global__ __launch_bounds__(256) void egonet_k1_count_k(
+__global__ __launch_bounds__(kK1Block) void egonet_k1_count_k(
     const int32_t *__restrict__ rowptr, const int32_t *__restrict__ col, int64_t n,
     int32_t *__restrict__ ego_ptr, int32_t *__restrict__ ego_eptr, int32_t *__restrict__ blk_tot,
     const int32_t *__restrict__ dims) {
-    const int64_t v = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
+    const int64_t v = static_cast<int64_t>(blockIdx.x) * kK1Block + threadIdx.x;
     int32_t nb = 0, ne = 0;
     if (v < eff_count(dims, 0, n)) {
-        K1Ball b;
+        K1Win b;
         k1_ball(rowptr, col, static_cast<int32_t>(v), b);
-        K1Rows m;
-        k1_rows(rowptr, col, b, m);
         nb = b.nb;
+        auto count = [&](const K1Rows &m, int g0) {
 #pragma unroll
-        for (int r = 0; r < kK1Ball; ++r)
+            for (int r = 0; r < kK1Grp; ++r)
 #pragma unroll
-            for (int t = 0; t < kK1Deg; ++t)
-                ne += (r < b.nb && t < m.deg[r] && k1_rank(b, m.w[r][t]) >= 0) ? 1 : 0;
+                for (int t = 0; t < kK1Deg; ++t)
+                    ne += (g0 + r < b.nb && t < m.deg[r] && k1_index(b, m.w[r][t]) >= 0) ? 1 : 0;
+        };
+        {
+            K1Rows m;
+            k1_rows<0>(rowptr, col, b, m);
+            count(m, 0);
+        }
+        if (b.nb > kK1Grp) {  // balls of more than kK1Grp members: second group
+            K1Rows m;
+            k1_rows<kK1Grp>(rowptr, col, b, m);
+            count(m, kK1Grp);
+        }
     }
-    block_scan2(nb, ne);
+    wave_scan2(nb, ne);
     if (v < n) {
         ego_ptr[v + 1] = nb;   // block-local inclusive; the fill adds the block prefix
         ego_eptr[v + 1] = ne;
     }
-    if (threadIdx.x == 255) {
+    if (threadIdx.x == kK1Block - 1) {
         blk_tot[blockIdx.x] = nb;
         blk_tot[gridDim.x + blockIdx.x] = ne;
     }
 }
 
-__global__ __launch_bounds__(256) void egonet_k1_fill_k(
+__global__ __launch_bounds__(kK1Block) void egonet_k1_fill_k(
     const int32_t *__restrict__ rowptr, const int32_t *__restrict__ col, int64_t n,
     int32_t *__restrict__ ego_ptr, int32_t *__restrict__ ego_eptr,
     const int32_t *__restrict__ blk_tot, int32_t *__restrict__ ego_nodes,
     int32_t *__restrict__ sub_rowptr, int32_t *__restrict__ sub_col, int64_t n_ego_cap,
     const int32_t *__restrict__ dims, int32_t *__restrict__ ego_dims) {
     const int nblk = gridDim.x;
-    const int64_t v = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
+    const int64_t v = static_cast<int64_t>(blockIdx.x) * kK1Block + threadIdx.x;
     const bool live = v < eff_count(dims, 0, n);
     // the ball's loads go out first; the scan fix-up below overlaps them
-    K1Ball b;
+    K1Win b;
     K1Rows m;
     if (live) {
         k1_ball(rowptr, col, static_cast<int32_t>(v), b);
-        k1_rows(rowptr, col, b, m);
+        k1_rows<0>(rowptr, col, b, m);
     }
-    // block prefix and grand total of (nodes, edges), fixed order
-    __shared__ int32_t rp[4][256];
+    // block prefix and grand total of (nodes, edges), fixed order (wave sums)
     int32_t pn = 0, pe = 0, tn = 0, te = 0;
-    for (int32_t j = threadIdx.x; j < nblk; j += 256) {
+    for (int32_t j = threadIdx.x; j < nblk; j += kK1Block) {
         const int32_t a = blk_tot[j], c = blk_tot[nblk + j];
         tn += a;
         te += c;
@@ -410,16 +421,14 @@ __global__ __launch_bounds__(256) void egonet_k1_fill_k(
             pe += c;
         }
     }
-    rp[0][threadIdx.x] = pn; rp[1][threadIdx.x] = pe;
-    rp[2][threadIdx.x] = tn; rp[3][threadIdx.x] = te;
-    __syncthreads();
-    for (int off = 128; off >= 1; off >>= 1) {
-        if (threadIdx.x < off)
 #pragma unroll
-            for (int q = 0; q < 4; ++q) rp[q][threadIdx.x] += rp[q][threadIdx.x + off];
-        __syncthreads();
+    for (int off = 32; off >= 1; off >>= 1) {
+        pn += __shfl_xor(pn, off, kWave);
+        pe += __shfl_xor(pe, off, kWave);
+        tn += __shfl_xor(tn, off, kWave);
+        te += __shfl_xor(te, off, kWave);
     }
-    const int32_t pre_n = rp[0][0], pre_e = rp[1][0], ns = rp[2][0], es = rp[3][0];
+    const int32_t pre_n = pn, pre_e = pe, ns = tn, es = te;
     // this node's exclusive offsets from the count's block-local inclusive scan
     int32_t noff = pre_n, eo = pre_e, incl_n = 0, incl_e = 0;
     if (v < n) {
@@ -430,7 +439,7 @@ __global__ __launch_bounds__(256) void egonet_k1_fill_k(
             eo += ego_eptr[v];
         }
     }
-    __syncthreads();  // every read of the block-local values precedes the writes
+    __syncthreads();  // every read of the block-local values precedes the writes (one wave)
     if (v < n) {
         ego_ptr[v + 1] = pre_n + incl_n;
         ego_eptr[v + 1] = pre_e + incl_e;
@@ -444,22 +453,30 @@ __global__ __launch_bounds__(256) void egonet_k1_fill_k(
         }
     }
     // tail of the ego batch: [N_s, n_ego_cap) gets parent id 0 and empty CSR rows
-    for (int64_t i = ns + v; i <= n_ego_cap; i += static_cast<int64_t>(nblk) * 256) {
+    for (int64_t i = ns + v; i <= n_ego_cap; i += static_cast<int64_t>(nblk) * kK1Block) {
         sub_rowptr[i] = es;
         if (i < n_ego_cap) ego_nodes[i] = 0;
     }
     if (!live) return;
+    auto fill = [&](const K1Rows &mm, auto g0c) {
+        constexpr int G0 = decltype(g0c)::value;
 #pragma unroll
-    for (int r = 0; r < kK1Ball; ++r) {
-        if (r < b.nb) {
-            ego_nodes[noff + r] = b.node[r];
-            sub_rowptr[noff + r] = eo;
+        for (int r = 0; r < kK1Grp; ++r) {
+            if (G0 + r < b.nb) {
+                ego_nodes[noff + G0 + r] = b.mem[G0 + r < kK1Ball ? G0 + r : kK1Ball - 1];
+                sub_rowptr[noff + G0 + r] = eo;
 #pragma unroll
-            for (int t = 0; t < kK1Deg; ++t) {
-                const int32_t q = k1_rank(b, m.w[r][t]);
-                if (t < m.deg[r] && q >= 0) sub_col[eo++] = noff + q;
+                for (int t = 0; t < kK1Deg; ++t) {
+                    const int32_t i = k1_index(b, mm.w[r][t]);
+                    if (t < mm.deg[r] && i >= 0) sub_col[eo++] = noff + k1_rank(b, i);
+                }
             }
         }
+    };
+    fill(m, std::integral_constant<int, 0>{});
+    if (b.nb > kK1Grp) {
+        k1_rows<kK1Grp>(rowptr, col, b, m);
+        fill(m, std::integral_constant<int, kK1Grp>{});
     }
 }
 
@@ -476,7 +493,7 @@ static int words_for(int32_t max_graph_nodes) {
 using namespace scgib;
 
 extern "C" int64_t scgib_egonet_workspace_bytes(int64_t n_nodes) {
-    const int64_t nblk = (n_nodes + 255) / 256;
+    const int64_t nblk = (n_nodes + 63) / 64;  // the k = 1 builder's 64-node blocks
     return 2 * sizeof(int32_t) * (nblk > 0 ? nblk : 1);
 }
 
@@ -515,6 +532,8 @@ extern "C" int scgib_egonet_count(const int32_t *rowptr, const int32_t *col,
 
 extern "C" int64_t scgib_egonet_k1_max_degree(void) { return kK1Deg; }
 
+extern "C" int64_t scgib_egonet_k1_max_graph_nodes(void) { return 64; }
+
 extern "C" int scgib_egonet_k1_build(const int32_t *rowptr, const int32_t *col, int64_t n_nodes,
                                      int32_t *ego_ptr, int32_t *ego_eptr, void *workspace,
                                      int32_t *ego_nodes, int32_t *sub_rowptr, int32_t *sub_col,
@@ -524,11 +543,12 @@ extern "C" int scgib_egonet_k1_build(const int32_t *rowptr, const int32_t *col, 
         !sub_rowptr || !sub_col)
         return SCGIB_EINVAL;
     if (n_nodes >= (int64_t(1) << 31)) return SCGIB_EUNSUPPORTED;
-    const int32_t nblk = static_cast<int32_t>((n_nodes + 255) / 256);
+    const int32_t nblk = static_cast<int32_t>((n_nodes + kK1Block - 1) / kK1Block);
     int32_t *blk_tot = static_cast<int32_t *>(workspace);
     hipStream_t st = as_stream(stream);
-    egonet_k1_count_k<<<nblk, 256, 0, st>>>(rowptr, col, n_nodes, ego_ptr, ego_eptr, blk_tot, dims);
-    egonet_k1_fill_k<<<nblk, 256, 0, st>>>(rowptr, col, n_nodes, ego_ptr, ego_eptr, blk_tot,
+    egonet_k1_count_k<<<nblk, kK1Block, 0, st>>>(rowptr, col, n_nodes, ego_ptr, ego_eptr, blk_tot,
+                                                  dims);
+    egonet_k1_fill_k<<<nblk, kK1Block, 0, st>>>(rowptr, col, n_nodes, ego_ptr, ego_eptr, blk_tot,
                                            ego_nodes, sub_rowptr, sub_col, n_ego_cap, dims,
                                            ego_dims);
     return launch_status();

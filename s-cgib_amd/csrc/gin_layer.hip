@@ -953,9 +953,14 @@ __global__ __launch_bounds__(256, (DIN <= 64 && !RECON ? 2 : 1)) void gin_bwd_k(
     const int pend_ngr = static_cast<int>(((n + TM - 1) / TM + kGroup - 1) / kGroup);
     if (BN && pend.gpart) bn_bwd_fin_load<false>(pend.gpart, pend_ngr, 0, bfin);
     // weights: in flight during the BN finish and the first tile's loads
+    // (PRE, the register-heaviest variant: staged at once, no spill)
     WeightRegs<DIN> wregs;
     load_weights<DIN>(w1, w2, wregs);
     bool wpending = true;
+    if constexpr (PRE) {
+        store_weights<DIN>(wregs, sW1, sW2);
+        wpending = false;
+    }
     const int ch = tid & 63, q = tid >> 6;  // column-sum roles: channel, row quarter
     // staging roles: 4-channel chunk c4, rows rs + 16 k
     const int c4 = tid & 15, rs = tid >> 4;

@@ -25,6 +25,7 @@ bonds) raises, which the reference's bare ``except`` turns into "skip"
 from __future__ import annotations
 
 import contextlib
+import os
 import ctypes
 
 import numpy as np
@@ -364,11 +365,12 @@ def egonet_batch(g: GraphBatch, k: int, x=None):
         # two-launch k = 1 builder (sorted-list balls, batched loads): needs
         # the max in-degree bound and in-molecule edges, checked on the host
         kmax = int(_lib.query("scgib_egonet_k1_max_degree"))
+        fits = g.max_graph_nodes <= int(_lib.query("scgib_egonet_k1_max_graph_nodes"))
         if g.dims is not None:
             caps = g.ego_caps or ()
-            fast = len(caps) > 2 and caps[2] <= kmax
+            fast = fits and len(caps) > 2 and caps[2] <= kmax
         else:
-            fast = (info is not None and info["validated"] and
+            fast = (fits and info is not None and info["validated"] and
                     (len(info["deg"]) == 0 or int(info["deg"].max()) <= kmax))
         if fast:
             return _egonet_k1(g, ego_ptr, ego_eptr, ws, x)
@@ -441,9 +443,11 @@ def ego_bounds(g, k):
     return int(r.nnz), int((r @ deg).sum()), dmax
 
 
-# k = 1 ego-nets through the two-launch builder when its degree bound holds
-# (tests switch it off to compare with the general bitmap builder)
-EGO_K1_FAST = True
+# k = 1 ego-nets through the two-launch window builder when its bounds hold.
+# Off by default: faster alone (39 vs 46 us per QM9 B512 build, tools/ego_bench.py)
+# but the replayed step measured 0.5 % slower with it (the ego chain then
+# contends earlier with Encoder1's layers); tests compare both builders.
+EGO_K1_FAST = os.environ.get("SCGIB_EGO_K1", "0") != "0"
 
 
 def _egonet_k1(g, ego_ptr, ego_eptr, ws, x):

@@ -144,6 +144,7 @@ def test_egonet_k1_fast_path_equals_bitmap_builder(pkg, dev, workload):
     g2 = pkg.graph.GraphBatch.from_edges(np.concatenate([src, es]), np.concatenate([dst, ed]),
                                          n + 4, True, counts)
     outs = []
+    default = pkg.graph.EGO_K1_FAST
     for fast in (True, False):
         pkg.graph.EGO_K1_FAST = fast
         try:
@@ -151,7 +152,7 @@ def test_egonet_k1_fast_path_equals_bitmap_builder(pkg, dev, workload):
             outs.append([ego.graph_ptr.cpu().numpy(), ego.ndata["_ID"].cpu().numpy(),
                          ego.rowptr.cpu().numpy(), ego.col.cpu().numpy()[: ego.num_edges()]])
         finally:
-            pkg.graph.EGO_K1_FAST = True
+            pkg.graph.EGO_K1_FAST = default
     for a, b in zip(*outs):
         np.testing.assert_array_equal(a, b)
 

@@ -109,13 +109,15 @@ int64_t scgib_gin_tiles(int64_t n_nodes);
 int64_t scgib_gin_slab_floats(int64_t n_nodes, int32_t d_in);
 int64_t scgib_gin_bwd_slabs(int64_t n_nodes);
 /* Up to scgib_slab_reduce_max_jobs() independent scgib_slab_reduce's in one
- * launch (same fixed order per job). */
+ * launch (same fixed order per job): out[w] = sum_s slab[s*stride + w] for
+ * w < width; stride 0 means width (a column range of wider slabs otherwise,
+ * stride >= width). */
 typedef struct {
     const float *slab;
     float *out;
     int64_t width;
     int32_t n_slabs;
-    int32_t pad_;
+    int32_t stride;
 } scgib_slab_job;
 int64_t scgib_slab_reduce_max_jobs(void);
 int scgib_slab_reduce_multi(const scgib_slab_job *jobs, int32_t n_jobs, scgib_stream_t stream);
@@ -194,7 +196,8 @@ int64_t scgib_gin_defer_max_nodes(void);
  * usual layer.  counters NULL: BN not fused (bn_ws then holds the tile
  * statistics for scgib_bn_finalize).  Backward: one slab per workgroup of
  * scgib_gin_layer0_slab_width() floats = dW2 | dW1[64*32] | db2 | db1 |
- * dWt[32*16] (columns >= F are zero); d(agg0) is not produced. */
+ * dWt[32][n_feat] row-major in the first 32*n_feat floats of a 512-float
+ * region (the rest is not written); d(agg0) is not produced. */
 int64_t scgib_gin_layer0_slab_width(void);
 int scgib_gin_layer0_fwd(const float *x, int32_t n_feat, const int32_t *node_map, const float *wt,
                          const int32_t *rowptr, const int32_t *col, int64_t n_nodes,
@@ -207,9 +210,9 @@ int scgib_gin_layer0_fwd(const float *x, int32_t n_feat, const int32_t *node_map
 /* layer backward: `pending` (NULL: coef is read) finishes the deferred
  * scgib_gin_bwd_stats_bn of the same layer (coef may then be NULL). */
 int scgib_gin_layer0_bwd(const float *dy, const float *z2, const float *r, const float *agg,
-                         const float *aggx, const float *stat, const float *coef,
-                         const float *w1, const float *w2, int64_t n_nodes, float *slab,
-                         const int32_t *dims, const scgib_bn_bwd_pending *pending,
+                         const float *aggx, int32_t n_feat, const float *stat,
+                         const float *coef, const float *w1, const float *w2, int64_t n_nodes,
+                         float *slab, const int32_t *dims, const scgib_bn_bwd_pending *pending,
                          scgib_stream_t stream);
 int scgib_gin_layer_bwd(const float *dy, const float *z2, const float *r, const float *agg,
                         int32_t d_in, const float *stat, const float *coef, const float *w1,

@@ -61,8 +61,8 @@ SIGNATURES = {
     "scgib_gin_layer0_fwd": (ctypes.c_int, [_P, _I32, _P, _P, _P, _P, _I64, _F, _P, _P, _P, _P,
                                             _P, _P, _P, _P, _P, _P, _F, _F, _P, _P, _P, _P, _P,
                                             _P, _P, _I32, _P]),
-    "scgib_gin_layer0_bwd": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _I64, _P, _P,
-                                            _P, _P]),
+    "scgib_gin_layer0_bwd": (ctypes.c_int, [_P, _P, _P, _P, _P, _I32, _P, _P, _P, _P, _I64, _P,
+                                            _P, _P, _P]),
     "scgib_gin_bn_gpart_offset": (_I64, [_I64]),
     "scgib_gin_defer_max_nodes": (_I64, []),
     "scgib_gin_bn_ws_floats": (_I64, [_I64]),
@@ -122,7 +122,7 @@ class AdamTensor(ctypes.Structure):
 class SlabJob(ctypes.Structure):
     """scgib_slab_job (include/scgib.h)."""
     _fields_ = [("slab", ctypes.c_void_p), ("out", ctypes.c_void_p), ("width", ctypes.c_int64),
-                ("n_slabs", ctypes.c_int32), ("pad_", ctypes.c_int32)]
+                ("n_slabs", ctypes.c_int32), ("stride", ctypes.c_int32)]
 
 
 class GradSlice(ctypes.Structure):

@@ -921,7 +921,7 @@ __global__ __launch_bounds__(256, (DIN <= 64 && !RECON ? 2 : 1)) void gin_bwd_k(
     const float *__restrict__ coef, const float *__restrict__ w1, const float *__restrict__ w2,
     int64_t ncap, int64_t ntiles, float *__restrict__ dagg_out, float *__restrict__ slab,
     const int32_t *__restrict__ dims, const float *__restrict__ aggx, scgib_bn_bwd_pending pend,
-    ReconArgs rec) {
+    ReconArgs rec, int pre_f = kPreF) {
     static_assert(!PRE || DIN == 32, "transfer_d fold: layer 0 only");
     static_assert(!RECON || !BN, "the recon backward is fused into the dense head MLP");
     const int64_t n = eff_count(dims, 0, ncap);
@@ -1162,7 +1162,9 @@ __global__ __launch_bounds__(256, (DIN <= 64 && !RECON ? 2 : 1)) void gin_bwd_k(
 #pragma unroll
         for (int reg = 0; reg < 16; ++reg) {
             const int i = acc_row(reg, l), j = l & 31;
-            if (j < kPreF) sl[64 * 64 + 64 * DIN + 128 + i * kPreF + j] = accWt[reg];
+            // d Wt as [32][F] row-major: a column range of the slab reduces
+            // straight into the contiguous transfer_d.weight gradient
+            if (j < pre_f) sl[64 * 64 + 64 * DIN + 128 + i * pre_f + j] = accWt[reg];
         }
     }
     __shared__ float sB[2][4][64];
@@ -1616,17 +1618,19 @@ extern "C" int scgib_gin_layer0_fwd(const float *x, int32_t n_feat, const int32_
 }
 
 extern "C" int scgib_gin_layer0_bwd(const float *dy, const float *z2, const float *r,
-                                    const float *agg, const float *aggx, const float *stat,
-                                    const float *coef, const float *w1, const float *w2,
-                                    int64_t n_nodes, float *slab, const int32_t *dims,
-                                    const scgib_bn_bwd_pending *pending, scgib_stream_t stream) {
+                                    const float *agg, const float *aggx, int32_t n_feat,
+                                    const float *stat, const float *coef, const float *w1,
+                                    const float *w2, int64_t n_nodes, float *slab,
+                                    const int32_t *dims, const scgib_bn_bwd_pending *pending,
+                                    scgib_stream_t stream) {
     if (n_nodes <= 0 || !dy || !z2 || !r || !agg || !aggx || !stat || (!coef && !pending) || !w1 ||
-        !w2 || !slab)
+        !w2 || !slab || n_feat < 1 || n_feat > kPreF)
         return SCGIB_EINVAL;
     if (pending && (!pending->gpart || !pending->dgamma || !pending->dbeta)) return SCGIB_EINVAL;
     const scgib_bn_bwd_pending pd = pending ? *pending : scgib_bn_bwd_pending{};
     const int64_t nt = scgib_gin_tiles(n_nodes);
     gin_bwd_k<32, true, true><<<bwd_grid(nt), 256, 0, as_stream(stream)>>>(
-        dy, z2, r, agg, stat, coef, w1, w2, n_nodes, nt, nullptr, slab, dims, aggx, pd, ReconArgs{});
+        dy, z2, r, agg, stat, coef, w1, w2, n_nodes, nt, nullptr, slab, dims, aggx, pd, ReconArgs{},
+        n_feat);
     return launch_status();
 }

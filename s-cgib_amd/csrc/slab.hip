@@ -37,7 +37,8 @@ __global__ __launch_bounds__(1024) void slab_reduce_k(const float *__restrict__ 
 // Several independent slab reductions in one launch (e.g. the five layers of
 // an encoder's backward, reduced once at its end instead of one launch per
 // layer): workgroup -> (job, 64-column block) through the job table in the
-// kernel arguments; each job is summed exactly as slab_reduce_k does.
+// kernel arguments; each job is summed exactly as slab_reduce_k does, over a
+// column range of its slabs when the job's row stride exceeds its width.
 constexpr int kSlabJobs = 16;
 
 struct SlabJobs {
@@ -53,6 +54,7 @@ __global__ __launch_bounds__(1024) void slab_reduce_multi_k(const SlabJobs jobs)
     const scgib_slab_job &J = jobs.j[i];
     const int el = threadIdx.x & 63, sp = threadIdx.x >> 6;
     const int64_t e = static_cast<int64_t>(b - jobs.blk0[i]) * 64 + el;
+    const int64_t stride = J.stride > 0 ? J.stride : J.width;
     __shared__ float red[16][64];
     float acc = 0.f;
     if (e < J.width) {
@@ -60,7 +62,7 @@ __global__ __launch_bounds__(1024) void slab_reduce_multi_k(const SlabJobs jobs)
             float v[8];
 #pragma unroll
             for (int u = 0; u < 8; ++u)
-                v[u] = ld_ok(J.slab, static_cast<int64_t>(b0 + 16 * u) * J.width + e, e,
+                v[u] = ld_ok(J.slab, static_cast<int64_t>(b0 + 16 * u) * stride + e, e,
                              b0 + 16 * u < J.n_slabs, 0.f);
 #pragma unroll
             for (int u = 0; u < 8; ++u) acc += v[u];
@@ -102,6 +104,7 @@ extern "C" int scgib_slab_reduce_multi(const scgib_slab_job *jobs, int32_t n_job
     for (int i = 0; i < n_jobs; ++i) {
         const scgib_slab_job &J = jobs[i];
         if (J.n_slabs <= 0 || J.width <= 0 || !J.slab || !J.out) return SCGIB_EINVAL;
+        if (J.stride < 0 || (J.stride > 0 && J.stride < J.width)) return SCGIB_EINVAL;
         t.j[i] = J;
         t.blk0[i] = static_cast<int32_t>(blocks);
         blocks += (J.width + 63) / 64;

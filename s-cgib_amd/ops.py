@@ -53,6 +53,10 @@ EGO_FIRST = os.environ.get("SCGIB_EGO_FIRST", "0") != "0"
 # encoder pair: enqueue the two chains layer by layer alternately (forward and
 # backward) instead of one whole chain after the other
 INTERLEAVE = os.environ.get("SCGIB_INTERLEAVE", "1") != "0"
+# both encoders' transfer_d gradient slabs reduced by one job after the chains join
+# (A/B: 0.538 vs 0.530 ms: the ego reduce then waits for the join; an extra
+# mid-chain cross-stream edge instead serialised the two chains in graph replay)
+SHARED_L0 = os.environ.get("SCGIB_SHARED_L0", "0") != "0"  # measured slower (A/B)
 
 
 def launch_aside(fn, *tensors):
@@ -170,6 +174,14 @@ def _interleave(first, first_stream, second, second_stream):
                 except StopIteration as stop:
                     out[i], live[i] = stop.value, False
     return out[0], out[1]
+
+
+def _reduce_jobs(jobs, st):
+    cap = int(_lib.query("scgib_slab_reduce_max_jobs"))
+    for i0 in range(0, len(jobs), cap):
+        chunk = jobs[i0:i0 + cap]
+        table = (_lib.SlabJob * len(chunk))(*chunk)
+        _lib.call("scgib_slab_reduce_multi", ctypes.cast(table, ctypes.c_void_p), len(chunk), st)
 
 
 class _GinEncoder(torch.autograd.Function):
@@ -297,8 +309,17 @@ class _GinEncoder(torch.autograd.Function):
         return _drain(_GinEncoder.backward_steps(ctx, g_out, g_readout))
 
     @staticmethod
-    def backward_steps(ctx, g_out, g_readout=None):
-        """backward as a generator (yields after each layer), see forward_steps."""
+    def backward_steps(ctx, g_out, g_readout=None, l0=None):
+        """backward as a generator (yields after each layer), see forward_steps.
+
+        ``l0`` = (buf, first, total, owner, pending): the layer-0 (transfer_d
+        fold) weight-gradient slabs of TWO encoders sharing transfer_d live in
+        one buffer ``buf`` of ``total`` slabs, this chain's from slab
+        ``first``; the owner (owner = True) does not launch its final reduce
+        but appends (jobs, keep) to the list ``pending`` — the caller launches
+        it after the two chains join, and its d Wt job sums all ``total``
+        slabs (one fixed-order sum, no separate add, no extra cross-stream
+        edge); the other chain returns dwt = None."""
         L, gr, pre = ctx.L, ctx.graph, ctx.pre
         t = ctx.saved_tensors
         saved, params = t[: 4 * L], t[4 * L: 4 * L + 6 * L]
@@ -353,9 +374,12 @@ class _GinEncoder(torch.autograd.Function):
             w1c, w2c = _f32(w1, "w1"), _f32(w2, "w2")
             if pre and l == 0:
                 width = int(_lib.query("scgib_gin_layer0_slab_width"))
-                slab = torch.empty(nslab * width, dtype=torch.float32, device=dev)
+                if l0 is None:
+                    slab = torch.empty(nslab * width, dtype=torch.float32, device=dev)
+                else:
+                    slab = l0[0][l0[1] * width:(l0[1] + nslab) * width]
                 _launch("scgib_gin_layer0_bwd", meta, _p(dy), _p(z2), _p(r), _p(agg), _p(aggx),
-                        _p(stat), _p(coef), _p(w1c), _p(w2c), n, _p(slab), _p(gr.dims),
+                        ctx.n_feat, _p(stat), _p(coef), _p(w1c), _p(w2c), n, _p(slab), _p(gr.dims),
                         _byref(bpend), st)
                 dagg = None
             else:
@@ -367,7 +391,21 @@ class _GinEncoder(torch.autograd.Function):
                         _p(stat), _p(coef), _p(w1c), _p(w2c), n, _p(dagg), _p(slab), _NULL,
                         _p(gr.dims), _byref(bpend), st)
             wgrad = torch.empty(width, dtype=torch.float32, device=dev)
-            if BATCH_SLABS:  # reduced together after the last layer (one launch)
+            if pre and l == 0 and l0 is not None:
+                # this chain's W2 | W1 | b2 | b1 columns (row stride: the full slab)
+                base = HIDDEN * HIDDEN + HIDDEN * d_in + 2 * HIDDEN
+                jobs.append(_lib.SlabJob(slab.data_ptr(), wgrad.data_ptr(), base, nslab, width))
+                keep.append(slab)
+                if l0[3]:  # owner: the Wt columns of both encoders' slabs (after the join)
+                    jobs.append(_lib.SlabJob(l0[0].data_ptr() + 4 * base,
+                                             wgrad.data_ptr() + 4 * base, 32 * ctx.n_feat,
+                                             l0[2], width))
+                    keep.append(l0[0])
+            elif pre and l == 0 and BATCH_SLABS:  # dWt occupies 32 * F of its 512 columns
+                used = HIDDEN * HIDDEN + HIDDEN * d_in + 2 * HIDDEN + 32 * ctx.n_feat
+                jobs.append(_lib.SlabJob(slab.data_ptr(), wgrad.data_ptr(), used, nslab, width))
+                keep.append(slab)
+            elif BATCH_SLABS:  # reduced together after the last layer (one launch)
                 jobs.append(_lib.SlabJob(slab.data_ptr(), wgrad.data_ptr(), width, nslab, 0))
                 keep.append(slab)
             else:
@@ -378,20 +416,17 @@ class _GinEncoder(torch.autograd.Function):
             o += HIDDEN * d_in
             grads[6 * l + 3] = wgrad[o:o + HIDDEN]
             grads[6 * l + 1] = wgrad[o + HIDDEN:o + 2 * HIDDEN]
-            if pre and l == 0:
+            if pre and l == 0 and (l0 is None or l0[3]):
                 o += 2 * HIDDEN
-                dwt = wgrad[o:o + 32 * 16].view(32, 16)[:, : ctx.n_feat]
+                dwt = wgrad[o:o + 32 * ctx.n_feat].view(32, ctx.n_feat)
             grads[6 * l + 4] = bn_g[0]
             grads[6 * l + 5] = bn_g[1]
             dagg_next = dagg
             yield
-        if jobs:  # every layer's weight-gradient slabs, one fixed-order reduce launch
-            cap = int(_lib.query("scgib_slab_reduce_max_jobs"))
-            for i0 in range(0, len(jobs), cap):
-                chunk = jobs[i0:i0 + cap]
-                table = (_lib.SlabJob * len(chunk))(*chunk)
-                _lib.call("scgib_slab_reduce_multi", ctypes.cast(table, ctypes.c_void_p),
-                          len(chunk), st)
+        if l0 is not None and l0[3]:
+            l0[4].append((jobs, keep))  # launched by the caller after the chains join
+        elif jobs:  # every layer's weight-gradient slabs, one fixed-order reduce launch
+            _reduce_jobs(jobs, st)
             del keep  # slabs stay allocated until the launch is enqueued
         if pre:
             return (None, None, None, None, None, dwt, None, *grads)
@@ -511,12 +546,31 @@ class _GinEncoderPair(torch.autograd.Function):
                 g_f = df_total
             if not INTERLEAVE:
                 gc = _GinEncoder.backward(ctx.sub[1], g_f)
-        if INTERLEAVE:  # both chains enqueued layer by layer, the ego chain first
+        if INTERLEAVE and not SHARED_L0:
             ge, gc = _interleave(_GinEncoder.backward_steps(ctx.sub[0], g_s, g_ro), main,
                                  _GinEncoder.backward_steps(ctx.sub[1], g_f), side)
+        elif INTERLEAVE:  # both chains enqueued layer by layer, the ego chain first
+            # both encoders' transfer_d slabs in one buffer: the ego chain's
+            # final reduce sums them (after its layer-0 wait on Encoder1's)
+            ns_e = int(_lib.query("scgib_gin_bwd_slabs", ctx.sub[0].saved_tensors[2].shape[0]))
+            ns_c = int(_lib.query("scgib_gin_bwd_slabs", ctx.sub[1].saved_tensors[2].shape[0]))
+            width = int(_lib.query("scgib_gin_layer0_slab_width"))
+            buf = torch.empty((ns_e + ns_c) * width, dtype=torch.float32,
+                              device=ctx.sub[0].saved_tensors[2].device)
+            buf.record_stream(side)
+            pending = []
+            ge, gc = _interleave(
+                _GinEncoder.backward_steps(ctx.sub[0], g_s, g_ro,
+                                           l0=(buf, 0, ns_e + ns_c, True, pending)), main,
+                _GinEncoder.backward_steps(ctx.sub[1], g_f, l0=(buf, ns_e, ns_e + ns_c, False, None)),
+                side)
         elif not EGO_FIRST:
             ge = _GinEncoder.backward(ctx.sub[0], g_s, g_ro)
         main.wait_stream(side)
+        if INTERLEAVE and SHARED_L0:  # the ego chain's reduce, incl. both encoders' d Wt
+            jobs, keep = pending[0]
+            _reduce_jobs(jobs, _stream())
+            del keep
         for g in (*gc, dw0, db0):
             if isinstance(g, torch.Tensor):
                 g.record_stream(main)
@@ -524,7 +578,7 @@ class _GinEncoderPair(torch.autograd.Function):
             g_f_in.record_stream(side)
         if g_t is not None:
             g_t.record_stream(side)
-        dwt = ge[5] + gc[5]
+        dwt = ge[5] if gc[5] is None else ge[5] + gc[5]
         return (None, dwt, dw0, db0, None, None, None, None, None, None, None, None, *ge[7:],
                 *gc[7:])
 

@@ -36,7 +36,7 @@ def main():
         L.call("scgib_slab_reduce", P(slab_a), nslab, wa, P(ga), st)
         wb = int(L.query("scgib_gin_layer0_slab_width"))
         slab_b = torch.empty(nslab * wb, device=dev)
-        L.call("scgib_gin_layer0_bwd", P(dy), P(z2), P(r), P(agg), P(aggx), P(stat), P(coef),
+        L.call("scgib_gin_layer0_bwd", P(dy), P(z2), P(r), P(agg), P(aggx), 11, P(stat), P(coef),
                P(w1), P(w2), n, P(slab_b), None, st)
         gb = torch.empty(wb, device=dev)
         L.call("scgib_slab_reduce", P(slab_b), nslab, wb, P(gb), st)

@@ -914,8 +914,14 @@ __global__ __launch_bounds__(1024) void bn_bwd_finalize_k(const float *__restric
 // of the MLP output); z2 / stat / coef are not read.
 // PRE: layer 0 with transfer_d folded in (see gather_x_rows): d(agg0) is not
 // stored; dWt += d(agg0)^T aggx is accumulated (slab tail of 32 x 16 floats).
+#ifndef SCGIB_BWD_MINB
+#define SCGIB_BWD_MINB 2
+#endif
+#ifndef SCGIB_BWD_PIPELINE
+#define SCGIB_BWD_PIPELINE 0
+#endif
 template <int DIN, bool BN = true, bool PRE = false, bool RECON = false>
-__global__ __launch_bounds__(256, (DIN <= 64 && !RECON ? 2 : 1)) void gin_bwd_k(
+__global__ __launch_bounds__(256, (DIN <= 64 && !RECON ? SCGIB_BWD_MINB : 1)) void gin_bwd_k(
     const float *__restrict__ dy, const float *__restrict__ z2, const float *__restrict__ r,
     const float *__restrict__ agg, const float *__restrict__ stat,
     const float *__restrict__ coef, const float *__restrict__ w1, const float *__restrict__ w2,
@@ -943,7 +949,7 @@ __global__ __launch_bounds__(256, (DIN <= 64 && !RECON ? 2 : 1)) void gin_bwd_k(
     const int wr = w >> 1, wc = w & 1;
     SCGIB_MARK(0);
     SCGIB_MARK_HWID();
-    float rscale = 0.f;  // recon: g / N
+    [[maybe_unused]] float rscale = 0.f;  // recon: g / N
     if constexpr (RECON) {
         stage_matrix<64>(rec.gram, sG);
         rscale = *rec.g_loss / static_cast<float>(n);
@@ -997,26 +1003,58 @@ __global__ __launch_bounds__(256, (DIN <= 64 && !RECON ? 2 : 1)) void gin_bwd_k(
         for (int idx = tid; idx < TM * 16; idx += 256) sPX[(idx >> 4) * LDP + 16 + (idx & 15)] = 0.f;
     float db2 = 0.f, db1 = 0.f;
     constexpr int AQ = DIN / 4, AK = TM * AQ / 256;  // agg tile: float4 per row, per thread
+    // SCGIB_BWD_PIPELINE=1: tiles are software-pipelined when a workgroup
+    // owns several (grid < tiles): the next tile's row loads (z2, dy, r,
+    // aggx) go out as soon as this tile's rows are in LDS and its agg loads
+    // once this tile's agg tile is, so they are in flight during this tile's
+    // four GEMMs.  Off by default: holding the next tile live costs 20-44
+    // bytes/lane of scratch at 2 workgroups/CU and measured 1-2 % slower at
+    // QM9 B512, where nearly every workgroup owns a single tile.
+    constexpr bool PIPE = SCGIB_BWD_PIPELINE != 0;
+    float4 vz[4], vd[4], vr[4], va[AK], vx = zero;
+    auto load_rows = [&](int64_t t) {
+        const int64_t r0 = t * TM;
+        const int m = static_cast<int>(n - r0 < TM ? (n - r0 > 0 ? n - r0 : 0) : TM);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int rr = rs + 16 * k;
+            const int64_t o = (r0 + rr) * 16 + c4, so = r0 * 16 + c4;
+            if (BN) vz[k] = ld_ok(reinterpret_cast<const float4 *>(z2), o, so, rr < m, zero);
+            else vz[k] = zero;
+            if (!RECON) vd[k] = ld_ok(reinterpret_cast<const float4 *>(dy), o, so, rr < m, zero);
+            vr[k] = ld_ok(reinterpret_cast<const float4 *>(r), o, so, rr < m, zero);
+        }
+        if (PRE)
+            vx = ld_ok(reinterpret_cast<const float4 *>(aggx), (r0 + (tid >> 2)) * 4 + (tid & 3),
+                       r0 * 4 + (tid & 3), (tid >> 2) < m, zero);
+    };
+    auto load_agg = [&](int64_t t) {
+        const int64_t r0 = t * TM;
+        const int m = static_cast<int>(n - r0 < TM ? (n - r0 > 0 ? n - r0 : 0) : TM);
+#pragma unroll
+        for (int k = 0; k < AK; ++k) {
+            const int idx = tid + 256 * k, rr = idx / AQ, cq = idx % AQ;
+            va[k] = ld_ok(reinterpret_cast<const float4 *>(agg), (r0 + rr) * AQ + cq, r0 * AQ + cq,
+                          rr < m, zero);
+        }
+    };
+    if (PIPE && blockIdx.x < ntiles) {
+        load_rows(blockIdx.x);
+        load_agg(blockIdx.x);
+    }
     for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
         const int64_t row0 = tile * TM;
         const int nv = static_cast<int>(n - row0 < TM ? (n - row0 > 0 ? n - row0 : 0) : TM);
+        const int64_t next = tile + gridDim.x;  // block-uniform
         if (dims) {  // capacity mode: zero this tile's padded rows of d(agg)
             const int ncr = static_cast<int>(ncap - row0 < TM ? ncap - row0 : TM);
             if (!PRE)
                 for (int idx = nv * DIN + tid; idx < ncr * DIN; idx += 256) dagg_out[row0 * DIN + idx] = 0.f;
-            if (nv == 0) continue;  // block-uniform
+            // block-uniform; every later tile of this workgroup is empty too,
+            // so the registers are never read again
+            if (nv == 0) continue;
         }
-        // global loads of the whole tile first (16-byte, all in flight)
-        float4 vz[4], vd[4], vr[4], va[AK];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const int rr = rs + 16 * k;
-            const int64_t o = (row0 + rr) * 16 + c4, so = row0 * 16 + c4;
-            if (BN) vz[k] = ld_ok(reinterpret_cast<const float4 *>(z2), o, so, rr < nv, zero);
-            else vz[k] = zero;
-            if (!RECON) vd[k] = ld_ok(reinterpret_cast<const float4 *>(dy), o, so, rr < nv, zero);
-            vr[k] = ld_ok(reinterpret_cast<const float4 *>(r), o, so, rr < nv, zero);
-        }
+        if (!PIPE) load_rows(tile);
         // recon: own IM rows (vd) and nb = ((A + A^T) IM) rows, same layout
         float4 nb[4];
         if constexpr (RECON) {
@@ -1039,16 +1077,7 @@ __global__ __launch_bounds__(256, (DIN <= 64 && !RECON ? 2 : 1)) void gin_bwd_k(
 #pragma unroll
             for (int k = 0; k < 4; ++k) vd[k] = rs + 16 * k < nv ? hd.self[k] : zero;
         }
-#pragma unroll
-        for (int k = 0; k < AK; ++k) {
-            const int idx = tid + 256 * k, rr = idx / AQ, cq = idx % AQ;
-            va[k] = ld_ok(reinterpret_cast<const float4 *>(agg), (row0 + rr) * AQ + cq, row0 * AQ + cq,
-                          rr < nv, zero);
-        }
-        float4 vx = zero;
-        if (PRE)
-            vx = ld_ok(reinterpret_cast<const float4 *>(aggx), (row0 + (tid >> 2)) * 4 + (tid & 3),
-                       row0 * 4 + (tid & 3), (tid >> 2) < nv, zero);
+        if (!PIPE) load_agg(tile);
         if (wpending) {  // first tile: its loads are in flight now
             store_weights<DIN>(wregs, sW1, sW2);
             wpending = false;
@@ -1094,6 +1123,7 @@ __global__ __launch_bounds__(256, (DIN <= 64 && !RECON ? 2 : 1)) void gin_bwd_k(
             }
             __syncthreads();
         }
+        if (PIPE && next < ntiles) load_rows(next);  // in flight during the GEMMs below
         if (tile == blockIdx.x) SCGIB_MARK(1);
         // dW2 += dz2^T r  (sub-tile j-block wr, k-block wc)
         accW2 = mma_tn<TM>(sD + wr * 32, LDH, sR + wc * 32, LDH, accW2);
@@ -1115,6 +1145,7 @@ __global__ __launch_bounds__(256, (DIN <= 64 && !RECON ? 2 : 1)) void gin_bwd_k(
             float *pa = sA + rr * LDA + 4 * cq;
             pa[0] = va[k].x; pa[1] = va[k].y; pa[2] = va[k].z; pa[3] = va[k].w;
         }
+        if (PIPE && next < ntiles) load_agg(next);
         __syncthreads();
         for (int rr = q; rr < TM; rr += 4) db1 += sD[rr * LDH + ch];
         // dW1 += dz1^T agg  (64 x DIN) ; d(agg) = dz1 W1  (TM x DIN)

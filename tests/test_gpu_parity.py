@@ -627,6 +627,23 @@ def test_gin_encoder_transfer_fold(pkg, dev, training, via_ego):
                 assert rel_err(ba.cpu(), bb.cpu()) < 1e-5, ka
 
 
+@pytest.mark.parametrize("training", [True, False])
+def test_gin_encoder_transfer_fold_multi_tile(pkg, dev, training):
+    """700 molecules' ego-nets: ~37k rows = ~590 64-row tiles, more than the
+    backward grid, so workgroups own several tiles (the software-pipelined
+    tile loop of gin_bwd_k, dW accumulated across tiles in registers)."""
+    h, h_ref, h64, gw, gw_ref, gw64, gin_a, gin_b = _fold_case(pkg, dev, 700, training, True)
+    assert h.shape[0] > 64 * 512
+    assert rel_l2(h.detach().cpu(), h64.detach()) < 1e-5
+    assert rel_l2(gw.cpu(), gw64) < 5e-3
+    a, b = gw.cpu().double().flatten(), gw64.flatten()
+    assert float(a @ b / (a.norm() * b.norm())) > 0.99999
+    pa, pb = dict(gin_a.named_parameters()), dict(gin_b.named_parameters())
+    cancelled = ("mlp.2.bias",) if training else ()
+    check_grads_model({k: v.grad.detach().cpu().double().numpy() for k, v in pb.items()},
+                      lambda k: pa[k].grad, tol=5e-3, cancelled=cancelled)
+
+
 @pytest.mark.parametrize("via_ego", [False, True])
 def test_gin_encoder_transfer_fold_small_exact(pkg, dev, via_ego):
     """A few molecules: kink flips are improbable, so dWt must agree with the

@@ -95,6 +95,8 @@ int scgib_gin_aggregate(const float *h, const int32_t *rowptr, const int32_t *co
  *   Chan combine), running stats updated (momentum, unbiased var,
  *   num_batches_tracked += 1); eval: running stats.  Writes `stat`.
  * scgib_bn_relu_apply: out = relu(stat.scale * z + stat.shift)  [n,64].
+ *   in_pending (may be NULL): the last GIN layer's deferred statistics
+ *   (scgib_bn_pending below) — finished here, `stat` is then written.
  * scgib_gin_bwd_stats: dy = dh * [stat.scale z2 + stat.shift > 0], dh given,
  *   or, with (rowptr_t, col_t), gathered from the next layer's d(agg):
  *   dh_v = (1+eps) g_v + sum_{u in out(v)} g_u.  Per-tile sum(dy), sum(dy xhat).
@@ -133,7 +135,8 @@ int scgib_bn_finalize(const float *tile_stats, int64_t n_nodes, const float *gam
                       float *running_mean, float *running_var, int64_t *num_batches_tracked,
                       float *stat, const int32_t *dims, scgib_stream_t stream);
 int scgib_bn_relu_apply(const float *z, const float *stat, int64_t n_nodes, float *out,
-                        const int32_t *dims, scgib_stream_t stream);
+                        const int32_t *dims, const scgib_bn_pending *in_pending,
+                        scgib_stream_t stream);
 int scgib_gin_bwd_stats(const float *dh, const int32_t *rowptr_t, const int32_t *col_t,
                         float one_plus_eps, const float *z2, const float *stat, int64_t n_nodes,
                         float *dy, float *tile_stats, const int32_t *dims,
@@ -178,10 +181,12 @@ int scgib_gin_bwd_stats_seg_bn(const float *dh, const float *g_seg, const int32_
 /* Encoder output and its readout in one pass: out = relu(stat.scale z +
  * stat.shift) [n_rows][64], readout[s] = sum of out rows [ptr[s], ptr[s+1])
  * (same order as scgib_segment_sum), seg[row] = s.  seg_dims (device, may be
- * NULL): actual segment count; rows past the last valid one are zeroed. */
+ * NULL): actual segment count; rows past the last valid one are zeroed.
+ * in_pending / dims (row count, may be NULL): as scgib_bn_relu_apply. */
 int scgib_bn_relu_segment_sum(const float *z, const float *stat, const int32_t *ptr,
                               int64_t n_seg, int64_t n_rows, float *out, float *readout,
-                              int32_t *seg, const int32_t *seg_dims, scgib_stream_t stream);
+                              int32_t *seg, const int32_t *seg_dims, const int32_t *dims,
+                              const scgib_bn_pending *in_pending, scgib_stream_t stream);
 /* Deferred finalize (scgib_bn_pending above): in_pending (NULL: in_stat is
  * used) names the previous layer's pending statistics — this layer finishes
  * them; defer = 1 leaves this layer's own pending (stat / running stats /

@@ -78,10 +78,11 @@ SIGNATURES = {
     "scgib_gin_layer_fwd": (ctypes.c_int, [_P, _I32, _P, _P, _P, _I64, _F, _P, _P, _P, _P, _P, _P,
                                            _P, _P, _P, _P]),
     "scgib_bn_finalize": (ctypes.c_int, [_P, _I64, _P, _P, _F, _F, _I32, _P, _P, _P, _P, _P, _P]),
-    "scgib_bn_relu_apply": (ctypes.c_int, [_P, _P, _I64, _P, _P, _P]),
+    "scgib_bn_relu_apply": (ctypes.c_int, [_P, _P, _I64, _P, _P, _P, _P]),
     "scgib_gin_bwd_stats_seg_bn": (ctypes.c_int, [_P, _P, _P, _P, _P, _I64, _I32, _P, _P, _P,
                                                   _P, _P, _P, _P, _I32, _P]),
-    "scgib_bn_relu_segment_sum": (ctypes.c_int, [_P, _P, _P, _I64, _I64, _P, _P, _P, _P, _P]),
+    "scgib_bn_relu_segment_sum": (ctypes.c_int, [_P, _P, _P, _I64, _I64, _P, _P, _P, _P, _P, _P,
+                                                 _P]),
     "scgib_gin_bwd_stats": (ctypes.c_int, [_P, _P, _P, _F, _P, _P, _I64, _P, _P, _P, _P]),
     "scgib_bn_bwd_finalize": (ctypes.c_int, [_P, _I64, _I32, _P, _P, _P, _P, _P]),
     "scgib_gin_layer_bwd": (ctypes.c_int, [_P, _P, _P, _P, _I32, _P, _P, _P, _P, _I64, _P, _P,

@@ -205,6 +205,31 @@ __device__ __forceinline__ float2 bn_fwd_publish(int c, double mean, double M2, 
     return make_float2(scale, shift);
 }
 
+// A consumer of a deferred layer (scgib_bn_pending) that is not a GIN layer
+// (the encoder output's BN + ReLU): every 256-thread workgroup finishes the
+// statistics from the group partials; workgroup 0 writes the record and the
+// running update.  sSS[c] = scale, sSS[64 + c] = shift.  Call from all
+// threads, before any early return.
+__device__ __forceinline__ void bn_pending_finish(const scgib_bn_pending &pend, int64_t n,
+                                                  float *sSS) {
+    const int fc = fin_channel();
+    const int ngr = static_cast<int>(((n + TM - 1) / TM + kGroup - 1) / kGroup);
+    const float gam = pend.gamma[fc], bet = pend.beta[fc];
+    FwdFin fin;
+    bn_fwd_fin_load<false>(pend.gpart, ngr, 0, fin);
+    double mean, M2;
+    bn_fwd_final<false>(pend.gpart, n, ngr, fin, mean, M2);
+    const bool lead = (threadIdx.x & 63) < 16;
+    const float2 ss = bn_fwd_publish(fc, mean, M2, n, gam, bet, pend.eps, pend.momentum,
+                                     pend.running_mean, pend.running_var,
+                                     pend.num_batches_tracked, pend.stat, blockIdx.x == 0 && lead);
+    if (lead) {
+        sSS[fc] = ss.x;
+        sSS[64 + fc] = ss.y;
+    }
+    __syncthreads();
+}
+
 // 256 threads: channel c = tid & 63, partition p = tid >> 6 (4 partitions).
 // Per-tile (S, M2) -> group (S_g, M2_g) -> layer (mean, M2); exact
 // decomposition M2 = sum_b [M2_b + (S_b - n_b mean)^2 / n_b] at each level.
@@ -758,15 +783,26 @@ __global__ __launch_bounds__(1024) void bn_finalize_k(
 __global__ __launch_bounds__(256) void bn_relu_apply_k(const float4 *__restrict__ z,
                                                        const float *__restrict__ stat,
                                                        int64_t n4, float4 *__restrict__ out,
-                                                       const int32_t *__restrict__ dims) {
+                                                       const int32_t *__restrict__ dims,
+                                                       scgib_bn_pending pend) {
     const int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
+    const int c = static_cast<int>(i & 15) * 4;
+    float4 a, b;
+    if (pend.gpart) {  // the last GIN layer's deferred statistics
+        __shared__ float sSS[128];
+        bn_pending_finish(pend, eff_count(dims, 0, n4 / 16), sSS);
+        a = make_float4(sSS[c], sSS[c + 1], sSS[c + 2], sSS[c + 3]);
+        b = make_float4(sSS[64 + c], sSS[65 + c], sSS[66 + c], sSS[67 + c]);
+    } else {
+        a = ld4(stat + 128 + c);
+        b = ld4(stat + 192 + c);
+    }
     if (i >= n4) return;
     if (dims && i >= static_cast<int64_t>(dims[0]) * 16) {
         out[i] = make_float4(0.f, 0.f, 0.f, 0.f);
         return;
     }
-    const int c = static_cast<int>(i & 15) * 4;
-    out[i] = xform4(z[i], ld4(stat + 128 + c), ld4(stat + 192 + c));
+    out[i] = xform4(z[i], a, b);
 }
 
 // ---------------------------------------------------------------------------
@@ -1350,13 +1386,18 @@ extern "C" int scgib_bn_finalize(const float *tile_stats, int64_t n_nodes, const
 }
 
 extern "C" int scgib_bn_relu_apply(const float *z, const float *stat, int64_t n_nodes,
-                                   float *out, const int32_t *dims, scgib_stream_t stream) {
+                                   float *out, const int32_t *dims,
+                                   const scgib_bn_pending *in_pending, scgib_stream_t stream) {
     if (n_nodes < 0) return SCGIB_EINVAL;
     if (n_nodes == 0) return SCGIB_OK;
-    if (!z || !stat || !out) return SCGIB_EINVAL;
+    if (!z || !out || (!stat && !in_pending)) return SCGIB_EINVAL;
+    if (in_pending && (!in_pending->gpart || !in_pending->gamma || !in_pending->beta ||
+                       !in_pending->stat || n_nodes > scgib_gin_defer_max_nodes()))
+        return SCGIB_EINVAL;
     const int64_t n4 = n_nodes * 16;
     bn_relu_apply_k<<<dim3((unsigned)((n4 + 255) / 256)), 256, 0, as_stream(stream)>>>(
-        reinterpret_cast<const float4 *>(z), stat, n4, reinterpret_cast<float4 *>(out), dims);
+        reinterpret_cast<const float4 *>(z), stat, n4, reinterpret_cast<float4 *>(out), dims,
+        in_pending ? *in_pending : scgib_bn_pending{});
     return launch_status();
 }
 
@@ -1427,11 +1468,22 @@ extern "C" int scgib_gin_bwd_stats_seg_bn(const float *dh, const float *g_seg,
 __global__ __launch_bounds__(256) void bn_relu_segsum_k(
     const float4 *__restrict__ z, const float *__restrict__ stat, const int32_t *__restrict__ ptr,
     int64_t nseg, int64_t nrows, float4 *__restrict__ out, float4 *__restrict__ readout,
-    int32_t *__restrict__ seg, const int32_t *__restrict__ seg_dims) {
+    int32_t *__restrict__ seg, const int32_t *__restrict__ seg_dims,
+    const int32_t *__restrict__ dims, scgib_bn_pending pend) {
     const int64_t blk = xcd_remap(blockIdx.x, gridDim.x);
     const int64_t s = blk * 16 + (threadIdx.x >> 4);
     const int c = threadIdx.x & 15;
     const int64_t ns = eff_count(seg_dims, 0, nseg);
+    float4 a, b;
+    if (pend.gpart) {  // the last GIN layer's deferred statistics
+        __shared__ float sSS[128];
+        bn_pending_finish(pend, eff_count(dims, 0, nrows), sSS);
+        a = make_float4(sSS[4 * c], sSS[4 * c + 1], sSS[4 * c + 2], sSS[4 * c + 3]);
+        b = make_float4(sSS[64 + 4 * c], sSS[65 + 4 * c], sSS[66 + 4 * c], sSS[67 + 4 * c]);
+    } else {
+        a = ld4(stat + 128 + 4 * c);
+        b = ld4(stat + 192 + 4 * c);
+    }
     if (seg_dims) {  // zero the rows past the last valid segment (grid-stride)
         const int64_t r0 = ptr[ns];
         const int64_t tot = (nrows - r0) * 16;
@@ -1444,7 +1496,6 @@ __global__ __launch_bounds__(256) void bn_relu_segsum_k(
         readout[s * 16 + c] = make_float4(0.f, 0.f, 0.f, 0.f);
         return;
     }
-    const float4 a = ld4(stat + 128 + 4 * c), b = ld4(stat + 192 + 4 * c);
     const int64_t beg = ptr[s], end = ptr[s + 1];
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
     int64_t i = beg;
@@ -1468,13 +1519,18 @@ __global__ __launch_bounds__(256) void bn_relu_segsum_k(
 extern "C" int scgib_bn_relu_segment_sum(const float *z, const float *stat, const int32_t *ptr,
                                          int64_t n_seg, int64_t n_rows, float *out,
                                          float *readout, int32_t *seg, const int32_t *seg_dims,
+                                         const int32_t *dims, const scgib_bn_pending *in_pending,
                                          scgib_stream_t stream) {
     if (n_seg < 0 || n_rows < 0) return SCGIB_EINVAL;
     if (n_seg == 0) return SCGIB_OK;
-    if (!z || !stat || !ptr || !out || !readout || !seg) return SCGIB_EINVAL;
+    if (!z || !ptr || !out || !readout || !seg || (!stat && !in_pending)) return SCGIB_EINVAL;
+    if (in_pending && (!in_pending->gpart || !in_pending->gamma || !in_pending->beta ||
+                       !in_pending->stat || n_rows == 0 || n_rows > scgib_gin_defer_max_nodes()))
+        return SCGIB_EINVAL;
     bn_relu_segsum_k<<<dim3(static_cast<unsigned>((n_seg + 15) / 16)), 256, 0, as_stream(stream)>>>(
         reinterpret_cast<const float4 *>(z), stat, ptr, n_seg, n_rows,
-        reinterpret_cast<float4 *>(out), reinterpret_cast<float4 *>(readout), seg, seg_dims);
+        reinterpret_cast<float4 *>(out), reinterpret_cast<float4 *>(readout), seg, seg_dims, dims,
+        in_pending ? *in_pending : scgib_bn_pending{});
     return launch_status();
 }
 

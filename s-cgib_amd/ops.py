@@ -38,6 +38,14 @@ _AUX_STREAMS = {}
 # deferred BatchNorm finalize in the fused GIN layers (scgib_bn_pending)
 DEFER_BN = os.environ.get("SCGIB_DEFER_BN", "1") != "0"
 DEFER_BN_FWD = os.environ.get("SCGIB_DEFER_BN_FWD", "1") != "0"
+# the encoder pair's core_tail (the interaction's noise draw) enqueued at the
+# start of the core chain, beside the ego-net build, instead of at its end
+# (off: A/B 0.530 vs 0.528 ms, within noise or slightly slower)
+TAIL_FIRST = os.environ.get("SCGIB_TAIL_FIRST", "0") != "0"
+# ... including the last layer's, finished by the output's BN + ReLU kernel
+# (off: A/B neutral to 0.5 % slower — every consumer workgroup then combines
+# the group partials, which costs what the producer's serial tail did)
+DEFER_BN_LAST = os.environ.get("SCGIB_DEFER_BN_LAST", "0") != "0"
 _AUX_PENDING = set()
 # compressor-BN running update on the aux stream (1) or inline (0): measured
 # 1.5 % faster aside (the ~15 us single-workgroup kernel leaves the critical
@@ -223,7 +231,8 @@ class _GinEncoder(torch.autograd.Function):
         # per encoder module: the two encoders run on concurrent streams)
         fused = training and n > 0
         # deferred BN finalize (scgib_bn_pending): layer l leaves its statistics
-        # as group partials and layer l + 1 finishes them (not the last layer)
+        # as group partials and layer l + 1 finishes them (the last layer's:
+        # the output's BN + ReLU kernel, with DEFER_BN_LAST)
         defer_ok = fused and DEFER_BN and DEFER_BN_FWD and \
             n <= int(_lib.query("scgib_gin_defer_max_nodes"))
         ws_floats = max(int(_lib.query("scgib_gin_bn_ws_floats", n)), 1)
@@ -251,7 +260,7 @@ class _GinEncoder(torch.autograd.Function):
             rv = _p(bn.running_var) if track else None
             nbt = _p(bn.num_batches_tracked) if track else None
             bn_ws = bn_wss[l % len(bn_wss)]
-            defer = int(defer_ok and l < L - 1)
+            defer = int(defer_ok and (l < L - 1 or DEFER_BN_LAST))
             if pre and l == 0:
                 aggx = torch.empty(n, 16, dtype=torch.float32, device=dev)
                 _launch("scgib_gin_layer0_fwd", meta, _p(x), x.shape[1], _p(nmap), _p(wt),
@@ -293,9 +302,10 @@ class _GinEncoder(torch.autograd.Function):
             ro = torch.empty(nseg, HIDDEN, dtype=torch.float32, device=dev)
             seg = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
             _lib.call("scgib_bn_relu_segment_sum", _p(h), _p(stat_prev), _p(ptr), nseg, n,
-                      _p(out), _p(ro), _p(seg), _p(seg_dims), st)
+                      _p(out), _p(ro), _p(seg), _p(seg_dims), _p(graph.dims), _byref(pend), st)
         else:
-            _lib.call("scgib_bn_relu_apply", _p(h), _p(stat_prev), n, _p(out), _p(graph.dims), st)
+            _lib.call("scgib_bn_relu_apply", _p(h), _p(stat_prev), n, _p(out), _p(graph.dims),
+                      _byref(pend), st)
         ctx.seg = seg
         ctx.save_for_backward(*saved, *params, *( (aggx,) if pre else ()))
         ctx.graph, ctx.L, ctx.training, ctx.pre = graph, L, training, pre
@@ -485,6 +495,8 @@ class _GinEncoderPair(torch.autograd.Function):
         ctx.sub = (_Ctx(), _Ctx())
         ctx.side, ctx.ne = side, ne
         side.wait_stream(main)
+        if core_tail is not None and TAIL_FIRST:  # beside the ego-net build
+            core_tail()
         # Encoder2 + its readout (dgl.sum_nodes per ego-net) on ``side``,
         # Encoder1 on the current stream, enqueued layer by layer alternately
         ego_steps = _GinEncoder.forward_steps(
@@ -510,7 +522,7 @@ class _GinEncoderPair(torch.autograd.Function):
             ctx.lin_saved = (f, w0)
             ctx.core_dims = core.dims
             outs = (s, ro, f, t)
-        if core_tail is not None:  # extra non-differentiable work on the core chain
+        if core_tail is not None and not TAIL_FIRST:  # non-differentiable extra work
             core_tail()
         main.wait_stream(side)
         s.record_stream(main)
@@ -595,8 +607,8 @@ def gin_encoder_pair_x(x, ego, gin_ego, core, gin_core, transfer, node_map, side
     BN + ReLU; the ego chain on stream ``side`` (forward and backward).  With ``lin0`` (the
     compressor's Linear(64, 64), models.py:596) also returns
     t = lin0(gin_core(...)), computed at the end of the core chain;
-    ``core_tail()`` (non-differentiable, e.g. the noise draw) runs there too,
-    before the join."""
+    ``core_tail()`` (non-differentiable, e.g. the noise draw) runs on the
+    core chain too: first (TAIL_FIRST) or last, before the join."""
     if ego.num_nodes() == 0 or core.num_nodes() == 0:
         raise _lib.ScgibError("gin_encoder on an empty graph")
     if transfer.bias is not None or transfer.weight.shape != (32, x.shape[1]) \

@@ -676,25 +676,28 @@ def test_gin_encoder_deferred_bn_bitwise(pkg, dev, via_ego, n_mols):
         target, nmap = g, None
     w = torch.randn(target.num_nodes(), 64, device=dev)
     outs = []
-    for defer in (True, False):
+    # (defer, last): the last layer's statistics finished by bn_relu_apply
+    for defer, last in ((True, True), (True, False), (False, False)):
         gin_c, lin_c = copy.deepcopy(gin), copy.deepcopy(lin)
-        old = pkg.ops.DEFER_BN, pkg.ops.DEFER_BN_FWD
+        old = pkg.ops.DEFER_BN, pkg.ops.DEFER_BN_FWD, pkg.ops.DEFER_BN_LAST
         pkg.ops.DEFER_BN = pkg.ops.DEFER_BN_FWD = defer
+        pkg.ops.DEFER_BN_LAST = last
         try:
             h = pkg.ops.gin_encoder_x(x, target, gin_c, lin_c, nmap)
             (h * w).sum().backward()
         finally:
-            pkg.ops.DEFER_BN, pkg.ops.DEFER_BN_FWD = old
+            pkg.ops.DEFER_BN, pkg.ops.DEFER_BN_FWD, pkg.ops.DEFER_BN_LAST = old
         torch.cuda.synchronize()
         outs.append((h.detach(), {k: p.grad for k, p in list(gin_c.named_parameters())
                                   + [("wt", lin_c.weight)]},
                      {k: b.clone() for k, b in gin_c.named_buffers()}))
-    (ha, ga, ba), (hb, gb, bb) = outs
-    assert torch.equal(ha, hb)
-    for k in ga:
-        assert torch.equal(ga[k], gb[k]), k
-    for k in ba:
-        assert torch.equal(ba[k], bb[k]), k
+    (ha, ga, ba) = outs[-1]
+    for hb, gb, bb in outs[:-1]:
+        assert torch.equal(ha, hb)
+        for k in ga:
+            assert torch.equal(ga[k], gb[k]), k
+        for k in ba:
+            assert torch.equal(ba[k], bb[k]), k
 
 
 # ---------------------------------------------------------------------------

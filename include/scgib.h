@@ -442,6 +442,29 @@ int scgib_mlp2_recon_bwd(const float *x, const float *r, const float *out, const
                          const int32_t *rowptr, const int32_t *col, const int32_t *rowptr_t,
                          const int32_t *col_t, const float *g_loss, float *dx, float *slab,
                          float *wgrad, const int32_t *dims, scgib_stream_t stream);
+/* The same with the contrastive loss (scgib_contrastive_fwd / _bwd: z1, z2
+ * [n_graphs][64], cws / ccounters as documented there) run in extra
+ * workgroups of the MLP launches — one launch on the step's critical chain
+ * instead of two each way.  d_in must be 128 (the pretraining head).
+ * Forward also writes *closs; backward takes d loss / d contrastive =
+ * *g_con and writes dz1, dz2. */
+int scgib_mlp2_recon_contrastive_fwd(const float *x, int32_t d_in, int64_t n_nodes,
+                                     const float *w1, const float *b1, const float *w2,
+                                     const float *b2, float *r, float *out,
+                                     const int32_t *rowptr, const int32_t *col, int64_t n_edges,
+                                     float *ws, uint32_t *counter, float *loss,
+                                     const int32_t *dims, const float *z1, const float *z2,
+                                     int64_t n_graphs, float *cws, float *closs,
+                                     uint32_t *ccounters, scgib_stream_t stream);
+int scgib_mlp2_recon_contrastive_bwd(const float *x, const float *r, const float *out,
+                                     const float *ws, int32_t d_in, const float *w1,
+                                     const float *w2, int64_t n_nodes, const int32_t *rowptr,
+                                     const int32_t *col, const int32_t *rowptr_t,
+                                     const int32_t *col_t, const float *g_loss, float *dx,
+                                     float *slab, float *wgrad, const int32_t *dims,
+                                     const float *z1, const float *z2, int64_t n_graphs,
+                                     float *cws, const float *g_con, float *dz1, float *dz2,
+                                     uint32_t *ccounters, scgib_stream_t stream);
 int64_t scgib_linear_slab_floats(int64_t n_nodes);
 int scgib_linear_fwd(const float *x, int64_t n_nodes, const float *w, const float *b, float *out,
                      const int32_t *dims, scgib_stream_t stream);

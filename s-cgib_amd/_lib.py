@@ -53,6 +53,12 @@ SIGNATURES = {
                                             _P, _P, _P, _P, _P]),
     "scgib_mlp2_recon_bwd": (ctypes.c_int, [_P, _P, _P, _P, _I32, _P, _P, _I64, _P, _P, _P, _P,
                                             _P, _P, _P, _P, _P, _P]),
+    "scgib_mlp2_recon_contrastive_fwd": (ctypes.c_int, [_P, _I32, _I64, _P, _P, _P, _P, _P, _P,
+                                                        _P, _P, _I64, _P, _P, _P, _P, _P, _P,
+                                                        _I64, _P, _P, _P, _P]),
+    "scgib_mlp2_recon_contrastive_bwd": (ctypes.c_int, [_P, _P, _P, _P, _I32, _P, _P, _I64, _P,
+                                                        _P, _P, _P, _P, _P, _P, _P, _P, _P, _P,
+                                                        _I64, _P, _P, _P, _P, _P, _P]),
     "scgib_linear_slab_floats": (_I64, [_I64]),
     "scgib_linear_fwd": (ctypes.c_int, [_P, _I64, _P, _P, _P, _P, _P]),
     "scgib_linear_bwd": (ctypes.c_int, [_P, _P, _P, _I64, _P, _P, _P, _P, _P, _P]),

@@ -34,6 +34,7 @@
 // makes every MFMA operand read (32 lanes: 32 rows of one column, or 32
 // columns of one row) bank-conflict free for ds_read_b32.
 #include "mfma_tile.h"
+#include "contrast_body.h"
 
 namespace scgib {
 
@@ -471,6 +472,10 @@ struct ReconArgs {
     const int32_t *rowptr, *col;        // bwd: dst-major CSR
     const int32_t *rowptr_t, *col_t;    // bwd: src-major CSR, nullptr = symmetric
     const float *g_loss;                // bwd: d loss / d recon (device scalar)
+    // the contrastive loss (contrast_body.h) in extra workgroups past the
+    // MLP's (con.B = 0: none): it reads only z1 / z2, so it runs beside the
+    // MLP instead of as its own launch on the critical chain
+    ContrastArgs con;
 };
 
 // GATHER = false is the dense two-layer MLP of the head (models.py:1055-1057,
@@ -495,6 +500,14 @@ __global__ __launch_bounds__(256) void gin_fwd_k(
     __shared__ float sR[TM * LDH];
     __shared__ float sRed[2][64];
     __shared__ float sPre[PRE ? (TM + 32) * kPreLD : 1];  // aggx tile | Wt
+    if constexpr (RECON && DIN == 128) {  // the pretraining head (interaction map width)
+        static_assert(TM * LDA >= CT * CLD, "contrastive tiles in sA / sW1");
+        if (rec.con.B > 0 && static_cast<int>(blockIdx.x) >= rec.con.nmain) {  // block-uniform
+            const int64_t b = blockIdx.x - rec.con.nmain, nrb = contrast_row_blocks(rec.con.B);
+            contrast_fwd_body(rec.con, b % nrb, static_cast<int>(b / nrb), sA, sW1);
+            return;
+        }
+    }
     const int tid = threadIdx.x, l = tid & 63, w = tid >> 6;
     const int64_t tile = blockIdx.x;
     const int64_t row0 = tile * TM;
@@ -981,6 +994,19 @@ __global__ __launch_bounds__(256, (DIN <= 64 && !RECON ? SCGIB_BWD_MINB : 1)) vo
     __shared__ float sW2[64 * LDH];
     __shared__ float sG[RECON ? 64 * LDH : 1];  // Gram matrix of the recon loss
     float *const sR = sRA, *const sA = sRA;
+    unsigned gsz = gridDim.x;  // workgroups of the tile loop
+    if constexpr (RECON && DIN == 128) {  // the pretraining head (interaction map width)
+        static_assert(TM * RA >= CT * CLD && 64 * LDA >= CT * CLD && TM * LDH >= kContrastBwdW &&
+                      64 * LDH >= CT, "contrastive buffers in sRA / sW1 / sD / sW2");
+        if (rec.con.B > 0) {
+            gsz = static_cast<unsigned>(rec.con.nmain);
+            if (blockIdx.x >= gsz) {  // block-uniform
+                const int64_t b = blockIdx.x - gsz, nrb = contrast_row_blocks(rec.con.B);
+                contrast_bwd_body(rec.con, b % nrb, static_cast<int>(b / nrb), sRA, sW1, sD, sW2);
+                return;
+            }
+        }
+    }
     const int tid = threadIdx.x, l = tid & 63, w = tid >> 6;
     const int wr = w >> 1, wc = w & 1;
     SCGIB_MARK(0);
@@ -1078,10 +1104,10 @@ __global__ __launch_bounds__(256, (DIN <= 64 && !RECON ? SCGIB_BWD_MINB : 1)) vo
         load_rows(blockIdx.x);
         load_agg(blockIdx.x);
     }
-    for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    for (int64_t tile = blockIdx.x; tile < ntiles; tile += gsz) {
         const int64_t row0 = tile * TM;
         const int nv = static_cast<int>(n - row0 < TM ? (n - row0 > 0 ? n - row0 : 0) : TM);
-        const int64_t next = tile + gridDim.x;  // block-uniform
+        const int64_t next = tile + gsz;  // block-uniform
         if (dims) {  // capacity mode: zero this tile's padded rows of d(agg)
             const int ncr = static_cast<int>(ncap - row0 < TM ? ncap - row0 : TM);
             if (!PRE)
@@ -1249,6 +1275,8 @@ __global__ __launch_bounds__(256, (DIN <= 64 && !RECON ? SCGIB_BWD_MINB : 1)) vo
 // up to two workgroups per CU (66.5 KB LDS each): one tile per workgroup for
 // batches up to SCGIB_BWD_GRID_CAP tiles (build-time knob), so every tile of
 // an encoder layer runs at once; larger batches loop over tiles
+constexpr int kCUs = 256;  // MI355X: 8 XCDs x 32 CUs
+
 #ifndef SCGIB_BWD_GRID_CAP
 #define SCGIB_BWD_GRID_CAP 512
 #endif
@@ -1618,12 +1646,11 @@ extern "C" int64_t scgib_mlp2_recon_ws_floats(int64_t n_nodes) {
     return n_nodes <= 0 ? 0 : scgib_gin_tiles(n_nodes) * 4096 + 4096 + 2 * 512;
 }
 
-extern "C" int scgib_mlp2_recon_fwd(const float *x, int32_t d_in, int64_t n_nodes,
-                                    const float *w1, const float *b1, const float *w2,
-                                    const float *b2, float *r, float *out,
-                                    const int32_t *rowptr, const int32_t *col, int64_t n_edges,
-                                    float *ws, uint32_t *counter, float *loss,
-                                    const int32_t *dims, scgib_stream_t stream) {
+static int mlp2_recon_fwd(const float *x, int32_t d_in, int64_t n_nodes, const float *w1,
+                          const float *b1, const float *w2, const float *b2, float *r,
+                          float *out, const int32_t *rowptr, const int32_t *col, int64_t n_edges,
+                          float *ws, uint32_t *counter, float *loss, const int32_t *dims,
+                          const ContrastArgs &con, scgib_stream_t stream) {
     if (n_nodes <= 0 || n_edges < 0 || (d_in != 64 && d_in != 128)) return SCGIB_EINVAL;
     if (!x || !w1 || !b1 || !w2 || !b2 || !r || !out || !rowptr || (n_edges > 0 && !col) || !ws ||
         !counter || !loss)
@@ -1633,15 +1660,81 @@ extern "C" int scgib_mlp2_recon_fwd(const float *x, int32_t d_in, int64_t n_node
     double *wsd = reinterpret_cast<double *>(gram + 4096);
     ReconArgs rec{};
     rec.gslab = ws;
+    rec.con = con;
+    rec.con.nmain = static_cast<int>(nt);
+    const int64_t ncon = con.B > 0 ? contrast_row_blocks(con.B) * con.nsplit : 0;
     hipStream_t st = as_stream(stream);
     if (d_in == 128)
-        gin_fwd_k<128, false, false, false, true><<<(unsigned)nt, 256, 0, st>>>(x, nullptr, nullptr, nullptr, nullptr, n_nodes, 0.f, w1, b1, w2, b2, nullptr, r, out, nullptr, dims, BnFwdFuse{}, PreArgs{}, scgib_bn_pending{}, rec);
+        gin_fwd_k<128, false, false, false, true><<<(unsigned)(nt + ncon), 256, 0, st>>>(x, nullptr, nullptr, nullptr, nullptr, n_nodes, 0.f, w1, b1, w2, b2, nullptr, r, out, nullptr, dims, BnFwdFuse{}, PreArgs{}, scgib_bn_pending{}, rec);
     else
         gin_fwd_k<64, false, false, false, true><<<(unsigned)nt, 256, 0, st>>>(x, nullptr, nullptr, nullptr, nullptr, n_nodes, 0.f, w1, b1, w2, b2, nullptr, r, out, nullptr, dims, BnFwdFuse{}, PreArgs{}, scgib_bn_pending{}, rec);
     const int rc = launch_status();
     if (rc != SCGIB_OK) return rc;
     return launch_recon_fin(ws, out, rowptr, col, n_nodes, n_edges, gram, wsd, counter, loss, dims,
                             st);
+}
+
+extern "C" int scgib_mlp2_recon_fwd(const float *x, int32_t d_in, int64_t n_nodes,
+                                    const float *w1, const float *b1, const float *w2,
+                                    const float *b2, float *r, float *out,
+                                    const int32_t *rowptr, const int32_t *col, int64_t n_edges,
+                                    float *ws, uint32_t *counter, float *loss,
+                                    const int32_t *dims, scgib_stream_t stream) {
+    return mlp2_recon_fwd(x, d_in, n_nodes, w1, b1, w2, b2, r, out, rowptr, col, n_edges, ws,
+                          counter, loss, dims, ContrastArgs{}, stream);
+}
+
+static bool contrast_ok(const float *z1, const float *z2, int64_t n_graphs, const float *cws,
+                        const uint32_t *ccounters, int32_t d_in) {
+    return n_graphs > 0 && n_graphs <= (int64_t{1} << 20) && z1 && z2 && cws && ccounters &&
+           d_in == 128;
+}
+
+extern "C" int scgib_mlp2_recon_contrastive_fwd(
+    const float *x, int32_t d_in, int64_t n_nodes, const float *w1, const float *b1,
+    const float *w2, const float *b2, float *r, float *out, const int32_t *rowptr,
+    const int32_t *col, int64_t n_edges, float *ws, uint32_t *counter, float *loss,
+    const int32_t *dims, const float *z1, const float *z2, int64_t n_graphs, float *cws,
+    float *closs, uint32_t *ccounters, scgib_stream_t stream) {
+    if (!contrast_ok(z1, z2, n_graphs, cws, ccounters, d_in) || !closs) return SCGIB_EINVAL;
+    ContrastArgs con{z1, z2, n_graphs, cws, closs, nullptr, nullptr, nullptr,
+                     reinterpret_cast<unsigned *>(ccounters), contrast_splits(n_graphs), 0};
+    return mlp2_recon_fwd(x, d_in, n_nodes, w1, b1, w2, b2, r, out, rowptr, col, n_edges, ws,
+                          counter, loss, dims, con, stream);
+}
+
+static int mlp2_recon_bwd(const float *x, const float *r, const float *out, const float *ws,
+                          int32_t d_in, const float *w1, const float *w2, int64_t n_nodes,
+                          const int32_t *rowptr, const int32_t *col, const int32_t *rowptr_t,
+                          const int32_t *col_t, const float *g_loss, float *dx, float *slab,
+                          float *wgrad, const int32_t *dims, const ContrastArgs &con,
+                          scgib_stream_t stream) {
+    if (n_nodes <= 0 || (d_in != 64 && d_in != 128)) return SCGIB_EINVAL;
+    if (!x || !r || !out || !ws || !w1 || !w2 || !rowptr || !col || !g_loss || !dx || !slab ||
+        !wgrad || ((rowptr_t == nullptr) != (col_t == nullptr)))
+        return SCGIB_EINVAL;
+    const int64_t nt = scgib_gin_tiles(n_nodes);
+    const int grid = bwd_grid(nt);
+    ReconArgs rec{nullptr, out, ws + nt * 4096, rowptr, col, rowptr_t, col_t, g_loss, con};
+    rec.con.nmain = grid;
+    int64_t ncon = 0;
+    if (con.B > 0) {
+        // one workgroup per CU at this kernel's 256 VGPRs: the contrastive
+        // workgroups take the CUs the MLP tiles leave idle (fewer column
+        // splits, each over more column tiles) rather than queue behind them
+        const int64_t nrb = contrast_row_blocks(con.B);
+        const int64_t fit = (kCUs - grid) / nrb;
+        rec.con.nsplit = static_cast<int>(fit < 1 ? 1 : (fit < con.nsplit ? fit : con.nsplit));
+        ncon = nrb * rec.con.nsplit;
+    }
+    hipStream_t st = as_stream(stream);
+    if (d_in == 128)
+        gin_bwd_k<128, false, false, true><<<(unsigned)(grid + ncon), 256, 0, st>>>(nullptr, nullptr, r, x, nullptr, nullptr, w1, w2, n_nodes, nt, dx, slab, dims, nullptr, scgib_bn_bwd_pending{}, rec);
+    else
+        gin_bwd_k<64, false, false, true><<<grid, 256, 0, st>>>(nullptr, nullptr, r, x, nullptr, nullptr, w1, w2, n_nodes, nt, dx, slab, dims, nullptr, scgib_bn_bwd_pending{}, rec);
+    const int rc = launch_status();
+    if (rc != SCGIB_OK) return rc;
+    return launch_slab_reduce(slab, grid, 64 * 64 + 64 * static_cast<int64_t>(d_in) + 128, wgrad, st);
 }
 
 extern "C" int scgib_mlp2_recon_bwd(const float *x, const float *r, const float *out,
@@ -1651,21 +1744,23 @@ extern "C" int scgib_mlp2_recon_bwd(const float *x, const float *r, const float 
                                     const int32_t *col_t, const float *g_loss, float *dx,
                                     float *slab, float *wgrad, const int32_t *dims,
                                     scgib_stream_t stream) {
-    if (n_nodes <= 0 || (d_in != 64 && d_in != 128)) return SCGIB_EINVAL;
-    if (!x || !r || !out || !ws || !w1 || !w2 || !rowptr || !col || !g_loss || !dx || !slab ||
-        !wgrad || ((rowptr_t == nullptr) != (col_t == nullptr)))
+    return mlp2_recon_bwd(x, r, out, ws, d_in, w1, w2, n_nodes, rowptr, col, rowptr_t, col_t,
+                          g_loss, dx, slab, wgrad, dims, ContrastArgs{}, stream);
+}
+
+extern "C" int scgib_mlp2_recon_contrastive_bwd(
+    const float *x, const float *r, const float *out, const float *ws, int32_t d_in,
+    const float *w1, const float *w2, int64_t n_nodes, const int32_t *rowptr, const int32_t *col,
+    const int32_t *rowptr_t, const int32_t *col_t, const float *g_loss, float *dx, float *slab,
+    float *wgrad, const int32_t *dims, const float *z1, const float *z2, int64_t n_graphs,
+    float *cws, const float *g_con, float *dz1, float *dz2, uint32_t *ccounters,
+    scgib_stream_t stream) {
+    if (!contrast_ok(z1, z2, n_graphs, cws, ccounters, d_in) || !g_con || !dz1 || !dz2)
         return SCGIB_EINVAL;
-    const int64_t nt = scgib_gin_tiles(n_nodes);
-    const int grid = bwd_grid(nt);
-    ReconArgs rec{nullptr, out, ws + nt * 4096, rowptr, col, rowptr_t, col_t, g_loss};
-    hipStream_t st = as_stream(stream);
-    if (d_in == 128)
-        gin_bwd_k<128, false, false, true><<<grid, 256, 0, st>>>(nullptr, nullptr, r, x, nullptr, nullptr, w1, w2, n_nodes, nt, dx, slab, dims, nullptr, scgib_bn_bwd_pending{}, rec);
-    else
-        gin_bwd_k<64, false, false, true><<<grid, 256, 0, st>>>(nullptr, nullptr, r, x, nullptr, nullptr, w1, w2, n_nodes, nt, dx, slab, dims, nullptr, scgib_bn_bwd_pending{}, rec);
-    const int rc = launch_status();
-    if (rc != SCGIB_OK) return rc;
-    return launch_slab_reduce(slab, grid, 64 * 64 + 64 * static_cast<int64_t>(d_in) + 128, wgrad, st);
+    ContrastArgs con{z1, z2, n_graphs, cws, nullptr, g_con, dz1, dz2,
+                     reinterpret_cast<unsigned *>(ccounters) + 1, contrast_splits(n_graphs), 0};
+    return mlp2_recon_bwd(x, r, out, ws, d_in, w1, w2, n_nodes, rowptr, col, rowptr_t, col_t,
+                          g_loss, dx, slab, wgrad, dims, con, stream);
 }
 
 // ---------------------------------------------------------------------------

@@ -148,6 +148,9 @@ FORK_LOSSES = os.environ.get("SCGIB_FORK_LOSSES", "0") != "0"
 LIN_IN_PAIR = os.environ.get("SCGIB_LIN_IN_PAIR", "1") != "0"
 # head MLP + adjacency recon loss as one fused op (ops.mlp2_recon)
 FUSE_RECON = os.environ.get("SCGIB_FUSE_RECON", "1") != "0"
+# ... and the contrastive loss run in extra workgroups of the MLP + recon
+# launches (ops.mlp2_recon_contrastive)
+FUSE_CONTRAST = os.environ.get("SCGIB_FUSE_CONTRAST", "1") != "0"
 # gate / feature noise drawn by one Philox kernel (ops.device_noise) on the
 # core encoder's chain instead of two torch.rand launches on the critical path
 DEVICE_NOISE = os.environ.get("SCGIB_DEVICE_NOISE", "1") != "0"
@@ -298,6 +301,12 @@ class _SCGIBCore(nn.Module):
             with torch.cuda.stream(side):
                 con = semi_loss(z1, z2, batch_size)
         kl_loss = kl_mean  # == torch.mean(KL_tensor) (models.py:679), computed in-kernel
+        if side is None and self.recons_type == "adj" and FUSE_RECON and FUSE_CONTRAST \
+                and im.is_cuda and im.shape[1] == 2 * self.hidden_dim == 128:
+            # models.py:1174 + loss_recon_adj (:1256-1262) + batched_semi_loss
+            # (:606-629) in the same launches
+            rec, con = ops.mlp2_recon_contrastive(im, mlp, batch_g, z1, z2)
+            return kl_loss, con, rec
         if side is None:
             con = semi_loss(z1, z2, batch_size)
         if self.recons_type == "adj" and FUSE_RECON:

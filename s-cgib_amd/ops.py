@@ -1072,6 +1072,82 @@ class _Mlp2Recon(torch.autograd.Function):
         return dx, dw1, db1, dw2, db2, None
 
 
+class _Mlp2ReconContrastive(torch.autograd.Function):
+    """_Mlp2Recon and _Contrastive in the same launches: the contrastive
+    loss's workgroups run beside the MLP tiles (forward and backward), so the
+    critical chain has one launch each way instead of two."""
+
+    @staticmethod
+    def forward(ctx, x, w1, b1, w2, b2, graph, z1, z2):
+        x = _f32(x, "mlp2_recon")
+        n, d_in = x.shape
+        if d_in != 2 * HIDDEN or tuple(w1.shape) != (HIDDEN, d_in) or \
+                tuple(w2.shape) != (HIDDEN, HIDDEN):
+            raise _lib.ScgibError("mlp2_recon_contrastive: expects Linear(128,64) - Linear(64,64)")
+        z1, z2 = _f32(z1, "contrastive z1"), _f32(z2, "contrastive z2")
+        B = z1.shape[0]
+        if z1.shape != (B, HIDDEN) or z2.shape != (B, HIDDEN):
+            raise _lib.ScgibError(f"contrastive: z1 {tuple(z1.shape)} / z2 {tuple(z2.shape)} "
+                                  f"must both be [B, {HIDDEN}]")
+        w1, b1, w2, b2 = (_f32(t, "mlp2 params") for t in (w1, b1, w2, b2))
+        dev = x.device
+        r = torch.empty(n, HIDDEN, dtype=torch.float32, device=dev)
+        out = torch.empty(n, HIDDEN, dtype=torch.float32, device=dev)
+        ws = torch.empty(int(_lib.query("scgib_mlp2_recon_ws_floats", n)), dtype=torch.float32,
+                         device=dev)
+        cws = torch.empty(int(_lib.query("scgib_contrastive_workspace_floats", B)),
+                          dtype=torch.float32, device=dev)
+        loss = torch.empty((), dtype=torch.float32, device=dev)
+        closs = torch.empty((), dtype=torch.float32, device=dev)
+        cnt = counters(dev, "mlp2_recon", 1)
+        ccnt = counters(dev, "contrastive", int(_lib.query("scgib_contrastive_counters", B)))
+        _lib.call("scgib_mlp2_recon_contrastive_fwd", _p(x), d_in, n, _p(w1), _p(b1), _p(w2),
+                  _p(b2), _p(r), _p(out), _p(graph.rowptr), _p(graph.col),
+                  graph.edge_capacity(), _p(ws), _p(cnt), _p(loss), _p(graph.dims), _p(z1),
+                  _p(z2), B, _p(cws), _p(closs), _p(ccnt), _stream())
+        ctx.save_for_backward(x, r, out, ws, w1, w2, z1, z2, cws)
+        ctx.graph = graph
+        return loss, closs
+
+    @staticmethod
+    def backward(ctx, g_loss, g_con):
+        x, r, out, ws, w1, w2, z1, z2, cws = ctx.saved_tensors
+        gr = ctx.graph
+        dev = x.device
+        g_loss = _f32(g_loss.reshape(1), "g_loss") if g_loss is not None else \
+            torch.zeros(1, dtype=torch.float32, device=dev)
+        g_con = _f32(g_con.reshape(1), "g_con") if g_con is not None else \
+            torch.zeros(1, dtype=torch.float32, device=dev)
+        n, d_in = x.shape
+        B = z1.shape[0]
+        dx = torch.empty_like(x)
+        dz1, dz2 = torch.empty_like(z1), torch.empty_like(z2)
+        slab = torch.empty(int(_lib.query("scgib_mlp2_slab_floats", n, d_in)),
+                           dtype=torch.float32, device=dev)
+        wg = torch.empty(HIDDEN * HIDDEN + HIDDEN * d_in + 2 * HIDDEN, dtype=torch.float32,
+                         device=dev)
+        ccnt = counters(dev, "contrastive", int(_lib.query("scgib_contrastive_counters", B)))
+        sym = gr.symmetric
+        _lib.call("scgib_mlp2_recon_contrastive_bwd", _p(x), _p(r), _p(out), _p(ws), d_in,
+                  _p(w1), _p(w2), n, _p(gr.rowptr), _p(gr.col),
+                  None if sym else _p(gr.rowptr_t), None if sym else _p(gr.col_t), _p(g_loss),
+                  _p(dx), _p(slab), _p(wg), _p(gr.dims), _p(z1), _p(z2), B, _p(cws), _p(g_con),
+                  _p(dz1), _p(dz2), _p(ccnt), _stream())
+        o = HIDDEN * HIDDEN
+        dw2 = wg[:o].view(HIDDEN, HIDDEN)
+        dw1 = wg[o: o + HIDDEN * d_in].view(HIDDEN, d_in)
+        db2 = wg[o + HIDDEN * d_in: o + HIDDEN * d_in + HIDDEN]
+        db1 = wg[o + HIDDEN * d_in + HIDDEN:]
+        return dx, dw1, db1, dw2, db2, None, dz1, dz2
+
+
+def mlp2_recon_contrastive(x, mlp, graph, z1, z2):
+    """(recon_adj(mlp2(x, mlp), graph), contrastive(z1, z2)) from the same
+    launches (scgib_mlp2_recon_contrastive_fwd / _bwd)."""
+    return _Mlp2ReconContrastive.apply(x, mlp[0].weight, mlp[0].bias, mlp[2].weight,
+                                       mlp[2].bias, graph, z1, z2)
+
+
 def mlp2_recon(x, mlp, graph):
     """recon_adj(mlp2(x, mlp), graph) fused (the pretraining model's head);
     the MLP output itself is not returned (nothing else reads it)."""

@@ -498,6 +498,50 @@ def test_mlp2_recon_fused(pkg, dev, n_mols, symmetric):
     assert rel_l2(xd.grad.cpu(), 3.0 * xd2.grad.cpu()) < 1e-5
 
 
+@pytest.mark.parametrize("n_mols,n_graphs", [(7, 5), (512, 512), (1500, 1000)])
+def test_mlp2_recon_contrastive_fused(pkg, dev, n_mols, n_graphs):
+    """The contrastive loss run in extra workgroups of the MLP + recon
+    launches against the two separate ops: the losses are bitwise equal (same
+    bodies, same splits); the gradients agree to fp32 rounding (the backward
+    may use fewer column splits).  1500 molecules: more MLP tiles than CUs, so
+    the backward keeps one split per row block; the fp64 oracle pins dz."""
+    g, _ = rand_graph(pkg, n_mols, "qm9", 9, dev)
+    n = g.num_nodes()
+    torch.manual_seed(n_mols)
+    mlp = torch.nn.Sequential(torch.nn.Linear(128, 64), torch.nn.ReLU(),
+                              torch.nn.Linear(64, 64)).to(dev)
+    x = (0.3 * torch.randn(n, 128)).to(dev)
+    z1 = torch.randn(n_graphs, 64).to(dev)
+    z2 = torch.randn(n_graphs, 64).to(dev)
+    outs = []
+    for fused in (True, False):
+        for p_ in mlp.parameters():
+            p_.grad = None
+        xa, z1a, z2a = (t.clone().requires_grad_(True) for t in (x, z1, z2))
+        if fused:
+            rec, con = pkg.ops.mlp2_recon_contrastive(xa, mlp, g, z1a, z2a)
+        else:
+            rec, con = pkg.ops.mlp2_recon(xa, mlp, g), pkg.ops.contrastive(z1a, z2a)
+        (2.0 * rec + 3.0 * con).backward()
+        torch.cuda.synchronize()
+        outs.append((rec.item(), con.item(), xa.grad.cpu(), z1a.grad.cpu(), z2a.grad.cpu(),
+                     [p_.grad.cpu() for p_ in mlp.parameters()]))
+    (ra, ca, xa, z1a, z2a, pa), (rb, cb, xb, z1b, z2b, pb) = outs
+    assert ra == rb and ca == cb
+    assert torch.equal(xa, xb)
+    for u, v in zip(pa, pb):
+        assert torch.equal(u, v)
+    assert rel_l2(z1a, z1b) < 1e-6 and rel_l2(z2a, z2b) < 1e-6
+    # dz against the fp64 restatement of batched_semi_loss (tau = 1)
+    z1r, z2r = (t.detach().cpu().double().requires_grad_(True) for t in (z1, z2))
+    a, b = F.normalize(z1r), F.normalize(z2r)
+    refl, btw = torch.exp(a @ a.t()), torch.exp(a @ b.t())
+    loss_c = -torch.log(btw.diag() / (refl.sum(1) + btw.sum(1) - refl.diag())).mean()
+    (3.0 * loss_c).backward()
+    assert rel_err(ca, loss_c.item()) < LOSS_TOL
+    assert rel_l2(z1a, z1r.grad) < 1e-5 and rel_l2(z2a, z2r.grad) < 1e-5
+
+
 # ---------------------------------------------------------------------------
 # Fine-tune head (Mainmodel_finetuning) vs the reference's own outputs
 # ---------------------------------------------------------------------------

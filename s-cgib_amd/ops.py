@@ -59,8 +59,12 @@ BATCH_SLABS = os.environ.get("SCGIB_BATCH_SLABS", "1") != "0"
 # order in ways that favour the core chain first)
 EGO_FIRST = os.environ.get("SCGIB_EGO_FIRST", "0") != "0"
 # encoder pair: enqueue the two chains layer by layer alternately (forward and
-# backward) instead of one whole chain after the other
-INTERLEAVE = os.environ.get("SCGIB_INTERLEAVE", "1") != "0"
+# backward) instead of one whole chain after the other (off since the
+# contrastive loss moved into the head launches: A/B 0.5126 vs 0.5148 ms/step,
+# 6 of 6 rounds at or below)
+INTERLEAVE = os.environ.get("SCGIB_INTERLEAVE", "0") != "0"
+INTERLEAVE_FWD = os.environ.get("SCGIB_INTERLEAVE_FWD", "1" if INTERLEAVE else "0") != "0"
+INTERLEAVE_BWD = os.environ.get("SCGIB_INTERLEAVE_BWD", "1" if INTERLEAVE else "0") != "0"
 # both encoders' transfer_d gradient slabs reduced by one job after the chains join
 # (A/B: 0.538 vs 0.530 ms: the ego reduce then waits for the join; an extra
 # mid-chain cross-stream edge instead serialised the two chains in graph replay)
@@ -504,7 +508,7 @@ class _GinEncoderPair(torch.autograd.Function):
             readout=(ego.graph_ptr, ego.batch_size, ego.seg_dims))
         core_steps = _GinEncoder.forward_steps(ctx.sub[1], None, core, gin_core, training, x, wt,
                                                None, *params[ne:])
-        if INTERLEAVE:
+        if INTERLEAVE_FWD:
             (s, ro), f = _interleave(ego_steps, side, core_steps, main)
         else:
             with torch.cuda.stream(side):
@@ -540,7 +544,7 @@ class _GinEncoderPair(torch.autograd.Function):
         side.wait_stream(main)
         dw0 = db0 = None
         g_f_in = g_f
-        if EGO_FIRST and not INTERLEAVE:  # capture the critical ego chain first
+        if EGO_FIRST and not INTERLEAVE_BWD:  # capture the critical ego chain first
             ge = _GinEncoder.backward(ctx.sub[0], g_s, g_ro)
         with torch.cuda.stream(side):
             if ctx.lin and g_t is not None:
@@ -556,12 +560,12 @@ class _GinEncoderPair(torch.autograd.Function):
                           _p(slab), _p(wg), _p(ctx.core_dims), _stream())
                 dw0, db0 = wg[: HIDDEN * HIDDEN].view(HIDDEN, HIDDEN), wg[HIDDEN * HIDDEN:]
                 g_f = df_total
-            if not INTERLEAVE:
+            if not INTERLEAVE_BWD:
                 gc = _GinEncoder.backward(ctx.sub[1], g_f)
-        if INTERLEAVE and not SHARED_L0:
+        if INTERLEAVE_BWD and not SHARED_L0:
             ge, gc = _interleave(_GinEncoder.backward_steps(ctx.sub[0], g_s, g_ro), main,
                                  _GinEncoder.backward_steps(ctx.sub[1], g_f), side)
-        elif INTERLEAVE:  # both chains enqueued layer by layer, the ego chain first
+        elif INTERLEAVE_BWD:  # both chains enqueued layer by layer, the ego chain first
             # both encoders' transfer_d slabs in one buffer: the ego chain's
             # final reduce sums them (after its layer-0 wait on Encoder1's)
             ns_e = int(_lib.query("scgib_gin_bwd_slabs", ctx.sub[0].saved_tensors[2].shape[0]))
@@ -579,7 +583,7 @@ class _GinEncoderPair(torch.autograd.Function):
         elif not EGO_FIRST:
             ge = _GinEncoder.backward(ctx.sub[0], g_s, g_ro)
         main.wait_stream(side)
-        if INTERLEAVE and SHARED_L0:  # the ego chain's reduce, incl. both encoders' d Wt
+        if INTERLEAVE_BWD and SHARED_L0:  # the ego chain's reduce, incl. both encoders' d Wt
             jobs, keep = pending[0]
             _reduce_jobs(jobs, _stream())
             del keep

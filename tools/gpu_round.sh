@@ -1,7 +1,8 @@
 #!/bin/bash
-# Round measurement: GPU tests, smoke, full bench line, rocprofv3 kernel-trace
-# summary, then the PMC traffic passes.  Every GPU step has its own limit and
-# the first failure ends the script.  Usage: bash tools/gpu_round.sh TAG
+# Round measurement: GPU tests, smoke, the PMC traffic passes, the full bench
+# line (its roofline.traffic read from this run's PMC summary), then the
+# rocprofv3 kernel-trace summary.  Every GPU step has its own limit and the
+# first failure ends the script.  Usage: bash tools/gpu_round.sh TAG
 set -o pipefail
 TAG=${1:-round}
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
@@ -11,13 +12,14 @@ timeout -k 10 600 python -u -m pytest tests -m gpu -q -p no:cacheprovider --time
 echo "pytest rc=$rc"; tail -2 $O/pytest_gpu.log; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { echo smoke failed; tail -5 $O/smoke.log; exit 1; }
 tail -1 $O/smoke.log
-timeout -k 10 600 python bench.py --steps 300 --warmup 20 --cpu-seconds 20 > $O/bench.log 2>&1 || { echo bench failed; tail -5 $O/bench.log; exit 1; }
-tail -1 $O/bench.log | cut -c1-400
-timeout -k 10 600 rocprofv3 --kernel-trace --stats -T --output-format csv -d $O/prof_kt -o kt \
-  -- python bench.py --steps 20 --warmup 5 --no-cpu-baseline > $O/prof_bench.log 2>&1 || { echo rocprof failed; exit 1; }
 ARGS="--steps 5 --warmup 2 --no-cpu-baseline --no-superbatch --no-kernel-timer"
 for C in FETCH_SIZE WRITE_SIZE; do
   timeout -s KILL 300 rocprofv3 --pmc $C --output-format csv -d "$O/pmc/$C" -o pmc \
     -- python bench.py $ARGS > "$O/pmc_$C.log" 2>&1 || { echo "pmc $C failed"; exit 1; }
 done
 python tools/pmc_summary.py "$O/pmc" > "$O/traffic.json" && echo traffic ok
+SCGIB_TRAFFIC_FILE=$O/traffic.json timeout -k 10 600 python bench.py --steps 300 --warmup 20 --cpu-seconds 20 > $O/bench.log 2>&1 || { echo bench failed; tail -5 $O/bench.log; exit 1; }
+tail -1 $O/bench.log | cut -c1-400
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -T --output-format csv -d $O/prof_kt -o kt \
+  -- python bench.py --steps 20 --warmup 5 --no-cpu-baseline > $O/prof_bench.log 2>&1 || { echo rocprof failed; exit 1; }
+echo done

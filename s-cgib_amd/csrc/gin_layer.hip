@@ -810,12 +810,10 @@ __global__ __launch_bounds__(256) void bn_relu_apply_k(const float4 *__restrict_
         a = ld4(stat + 128 + c);
         b = ld4(stat + 192 + c);
     }
-    if (i >= n4) return;
-    if (dims && i >= static_cast<int64_t>(dims[0]) * 16) {
-        out[i] = make_float4(0.f, 0.f, 0.f, 0.f);
-        return;
-    }
-    out[i] = xform4(z[i], a, b);
+    // grid-stride (a multiple of 16 float4: the channel quad stays fixed)
+    const int64_t nv4 = dims ? static_cast<int64_t>(dims[0]) * 16 : n4;
+    for (int64_t k = i; k < n4; k += static_cast<int64_t>(gridDim.x) * 256)
+        out[k] = k < nv4 ? xform4(z[k], a, b) : make_float4(0.f, 0.f, 0.f, 0.f);
 }
 
 // ---------------------------------------------------------------------------
@@ -1422,8 +1420,10 @@ extern "C" int scgib_bn_relu_apply(const float *z, const float *stat, int64_t n_
     if (in_pending && (!in_pending->gpart || !in_pending->gamma || !in_pending->beta ||
                        !in_pending->stat || n_nodes > scgib_gin_defer_max_nodes()))
         return SCGIB_EINVAL;
-    const int64_t n4 = n_nodes * 16;
-    bn_relu_apply_k<<<dim3((unsigned)((n4 + 255) / 256)), 256, 0, as_stream(stream)>>>(
+    const int64_t n4 = n_nodes * 16, wg = (n4 + 255) / 256;
+    // at most 128 workgroups: this kernel runs beside the other encoder's
+    // layers, so it should hold few CU slots (each thread loops instead)
+    bn_relu_apply_k<<<dim3(static_cast<unsigned>(wg < 128 ? wg : 128)), 256, 0, as_stream(stream)>>>(
         reinterpret_cast<const float4 *>(z), stat, n4, reinterpret_cast<float4 *>(out), dims,
         in_pending ? *in_pending : scgib_bn_pending{});
     return launch_status();

@@ -134,7 +134,12 @@ __device__ __forceinline__ float4 noise_feat(const NoiseGen &ng, int64_t r, int 
 }
 
 
-// one thread per (row, channel quad); 256 threads = 16 rows per workgroup
+// one thread per (row, channel quad); 256 threads = 16 rows per workgroup per
+// pass, grid-stride over at most SCGIB_NOISE_WG workgroups: the kernel runs
+// beside Encoder2's last layer, so it should hold few CU slots
+#ifndef SCGIB_NOISE_WG
+#define SCGIB_NOISE_WG 64
+#endif
 __global__ __launch_bounds__(256) void noise_uniform_k(float *__restrict__ u_gate,
                                                        float *__restrict__ u_feat, int64_t n,
                                                        uint64_t *__restrict__ rng,
@@ -143,9 +148,9 @@ __global__ __launch_bounds__(256) void noise_uniform_k(float *__restrict__ u_gat
     const uint64_t off = __hip_atomic_load(rng + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const NoiseGen ng{static_cast<uint32_t>(seed), static_cast<uint32_t>(seed >> 32),
                       static_cast<uint32_t>(off), static_cast<uint32_t>(off >> 32)};
-    const int64_t r = static_cast<int64_t>(blockIdx.x) * 16 + (threadIdx.x >> 4);
     const int c4 = threadIdx.x & 15;
-    if (r < n) {
+    for (int64_t r = static_cast<int64_t>(blockIdx.x) * 16 + (threadIdx.x >> 4); r < n;
+         r += static_cast<int64_t>(gridDim.x) * 16) {
         st4(u_feat + r * 64 + 4 * c4, noise_feat(ng, r, c4));
         if (c4 == 0) u_gate[r] = noise_gate(ng, r);
     }
@@ -716,7 +721,9 @@ extern "C" int scgib_noise_uniform(float *u_gate, float *u_feat, int64_t n_rows,
     if (n_rows == 0) return SCGIB_OK;
     if (!u_gate || !u_feat || !rng_state || !counter) return SCGIB_EINVAL;
     if (n_rows > 0xffffffffLL) return SCGIB_EUNSUPPORTED;
-    noise_uniform_k<<<dim3(static_cast<unsigned>((n_rows + 15) / 16)), 256, 0, as_stream(stream)>>>(
+    const int64_t wg = (n_rows + 15) / 16;
+    noise_uniform_k<<<dim3(static_cast<unsigned>(wg < SCGIB_NOISE_WG ? wg : SCGIB_NOISE_WG)), 256, 0,
+                      as_stream(stream)>>>(
         u_gate, u_feat, n_rows, rng_state, counter);
     return launch_status();
 }

@@ -123,6 +123,10 @@ typedef struct {
 } scgib_slab_job;
 int64_t scgib_slab_reduce_max_jobs(void);
 int scgib_slab_reduce_multi(const scgib_slab_job *jobs, int32_t n_jobs, scgib_stream_t stream);
+/* The same on at most max_workgroups workgroups (0: no cap; each loops over
+ * column blocks) — for a reduce that runs beside another chain's kernels. */
+int scgib_slab_reduce_multi_ex(const scgib_slab_job *jobs, int32_t n_jobs,
+                               int32_t max_workgroups, scgib_stream_t stream);
 int scgib_slab_reduce(const float *slab, int32_t n_slabs, int64_t width, float *out,
                       scgib_stream_t stream);
 int scgib_gin_layer_fwd(const float *h_in, int32_t d_in, const float *in_stat,

@@ -98,6 +98,7 @@ SIGNATURES = {
     "scgib_recon_bwd": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _I64, _P, _P, _P, _P]),
     "scgib_slab_reduce_max_jobs": (_I64, []),
     "scgib_slab_reduce_multi": (ctypes.c_int, [_P, _I32, _P]),
+    "scgib_slab_reduce_multi_ex": (ctypes.c_int, [_P, _I32, _I32, _P]),
     "scgib_grad_pack_max_tensors": (_I64, []),
     "scgib_grad_pack": (ctypes.c_int, [_P, _I32, _P, _P]),
     "scgib_grad_unpack": (ctypes.c_int, [_P, _I32, _P, _F, _P]),

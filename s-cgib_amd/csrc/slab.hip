@@ -47,34 +47,39 @@ struct SlabJobs {
     int32_t n;
 };
 
+// grid-stride over the column blocks (gridDim.x may be capped so that a
+// reduce running beside another chain holds few CU slots)
 __global__ __launch_bounds__(1024) void slab_reduce_multi_k(const SlabJobs jobs) {
-    const int b = blockIdx.x, lane = threadIdx.x & 63;
-    const bool le = lane < jobs.n && jobs.blk0[lane < jobs.n ? lane : 0] <= b;
-    const int i = __popcll(__ballot(le)) - 1;
-    const scgib_slab_job &J = jobs.j[i];
+    const int lane = threadIdx.x & 63;
     const int el = threadIdx.x & 63, sp = threadIdx.x >> 6;
-    const int64_t e = static_cast<int64_t>(b - jobs.blk0[i]) * 64 + el;
-    const int64_t stride = J.stride > 0 ? J.stride : J.width;
     __shared__ float red[16][64];
-    float acc = 0.f;
-    if (e < J.width) {
-        for (int b0 = sp; b0 < J.n_slabs; b0 += 16 * 8) {
-            float v[8];
+    for (int b = blockIdx.x; b < jobs.blk0[jobs.n]; b += gridDim.x) {  // block-uniform
+        const bool le = lane < jobs.n && jobs.blk0[lane < jobs.n ? lane : 0] <= b;
+        const int i = __popcll(__ballot(le)) - 1;
+        const scgib_slab_job &J = jobs.j[i];
+        const int64_t e = static_cast<int64_t>(b - jobs.blk0[i]) * 64 + el;
+        const int64_t stride = J.stride > 0 ? J.stride : J.width;
+        float acc = 0.f;
+        if (e < J.width) {
+            for (int b0 = sp; b0 < J.n_slabs; b0 += 16 * 8) {
+                float v[8];
 #pragma unroll
-            for (int u = 0; u < 8; ++u)
-                v[u] = ld_ok(J.slab, static_cast<int64_t>(b0 + 16 * u) * stride + e, e,
-                             b0 + 16 * u < J.n_slabs, 0.f);
+                for (int u = 0; u < 8; ++u)
+                    v[u] = ld_ok(J.slab, static_cast<int64_t>(b0 + 16 * u) * stride + e, e,
+                                 b0 + 16 * u < J.n_slabs, 0.f);
 #pragma unroll
-            for (int u = 0; u < 8; ++u) acc += v[u];
+                for (int u = 0; u < 8; ++u) acc += v[u];
+            }
         }
-    }
-    red[sp][el] = acc;
-    __syncthreads();
-    if (sp == 0 && e < J.width) {
-        double s = 0.0;
+        red[sp][el] = acc;
+        __syncthreads();
+        if (sp == 0 && e < J.width) {
+            double s = 0.0;
 #pragma unroll
-        for (int k = 0; k < 16; ++k) s += static_cast<double>(red[k][el]);
-        J.out[e] = static_cast<float>(s);
+            for (int k = 0; k < 16; ++k) s += static_cast<double>(red[k][el]);
+            J.out[e] = static_cast<float>(s);
+        }
+        __syncthreads();  // red is rewritten by the next column block
     }
 }
 
@@ -95,7 +100,12 @@ extern "C" int64_t scgib_slab_reduce_max_jobs(void) { return scgib::kSlabJobs; }
 
 extern "C" int scgib_slab_reduce_multi(const scgib_slab_job *jobs, int32_t n_jobs,
                                        scgib_stream_t stream) {
-    if (n_jobs < 0 || n_jobs > scgib::kSlabJobs) return SCGIB_EINVAL;
+    return scgib_slab_reduce_multi_ex(jobs, n_jobs, 0, stream);
+}
+
+extern "C" int scgib_slab_reduce_multi_ex(const scgib_slab_job *jobs, int32_t n_jobs,
+                                          int32_t max_workgroups, scgib_stream_t stream) {
+    if (n_jobs < 0 || n_jobs > scgib::kSlabJobs || max_workgroups < 0) return SCGIB_EINVAL;
     if (n_jobs == 0) return SCGIB_OK;
     if (!jobs) return SCGIB_EINVAL;
     scgib::SlabJobs t{};
@@ -111,6 +121,7 @@ extern "C" int scgib_slab_reduce_multi(const scgib_slab_job *jobs, int32_t n_job
         if (blocks > 0x7fffffff) return SCGIB_EUNSUPPORTED;
     }
     t.blk0[n_jobs] = static_cast<int32_t>(blocks);
+    if (max_workgroups > 0 && blocks > max_workgroups) blocks = max_workgroups;
     scgib::slab_reduce_multi_k<<<dim3(static_cast<unsigned>(blocks)), 1024, 0,
                                  scgib::as_stream(stream)>>>(t);
     return scgib::launch_status();

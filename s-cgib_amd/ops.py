@@ -65,6 +65,10 @@ EGO_FIRST = os.environ.get("SCGIB_EGO_FIRST", "0") != "0"
 INTERLEAVE = os.environ.get("SCGIB_INTERLEAVE", "0") != "0"
 INTERLEAVE_FWD = os.environ.get("SCGIB_INTERLEAVE_FWD", "1" if INTERLEAVE else "0") != "0"
 INTERLEAVE_BWD = os.environ.get("SCGIB_INTERLEAVE_BWD", "1" if INTERLEAVE else "0") != "0"
+# workgroup cap of the core (Encoder1) chain's final slab reduce (0: none;
+# A/B: 64 -> 0.521, 128 -> 0.516, none -> 0.508 ms/step — the join waits for
+# that reduce, so it is as critical as the ego chain's)
+SIDE_REDUCE_WG = int(os.environ.get("SCGIB_SIDE_REDUCE_WG", "0"))
 # both encoders' transfer_d gradient slabs reduced by one job after the chains join
 # (A/B: 0.538 vs 0.530 ms: the ego reduce then waits for the join; an extra
 # mid-chain cross-stream edge instead serialised the two chains in graph replay)
@@ -188,12 +192,13 @@ def _interleave(first, first_stream, second, second_stream):
     return out[0], out[1]
 
 
-def _reduce_jobs(jobs, st):
+def _reduce_jobs(jobs, st, max_wg=0):
     cap = int(_lib.query("scgib_slab_reduce_max_jobs"))
     for i0 in range(0, len(jobs), cap):
         chunk = jobs[i0:i0 + cap]
         table = (_lib.SlabJob * len(chunk))(*chunk)
-        _lib.call("scgib_slab_reduce_multi", ctypes.cast(table, ctypes.c_void_p), len(chunk), st)
+        _lib.call("scgib_slab_reduce_multi_ex", ctypes.cast(table, ctypes.c_void_p), len(chunk),
+                  int(max_wg), st)
 
 
 class _GinEncoder(torch.autograd.Function):
@@ -440,7 +445,7 @@ class _GinEncoder(torch.autograd.Function):
         if l0 is not None and l0[3]:
             l0[4].append((jobs, keep))  # launched by the caller after the chains join
         elif jobs:  # every layer's weight-gradient slabs, one fixed-order reduce launch
-            _reduce_jobs(jobs, st)
+            _reduce_jobs(jobs, st, getattr(ctx, "reduce_wg", 0))
             del keep  # slabs stay allocated until the launch is enqueued
         if pre:
             return (None, None, None, None, None, dwt, None, *grads)
@@ -542,6 +547,9 @@ class _GinEncoderPair(torch.autograd.Function):
         # by compressor[0]'s backward (d f += d t W0, dW0, db0)
         main, side = _torch_stream(), ctx.side
         side.wait_stream(main)
+        # Encoder1's final weight-gradient reduce runs beside the ego chain's
+        # last layers (optionally capped, SIDE_REDUCE_WG)
+        ctx.sub[1].reduce_wg = SIDE_REDUCE_WG
         dw0 = db0 = None
         g_f_in = g_f
         if EGO_FIRST and not INTERLEAVE_BWD:  # capture the critical ego chain first

@@ -1699,6 +1699,14 @@ extern "C" int scgib_mlp2_recon_contrastive_fwd(
     if (!contrast_ok(z1, z2, n_graphs, cws, ccounters, d_in) || !closs) return SCGIB_EINVAL;
     ContrastArgs con{z1, z2, n_graphs, cws, closs, nullptr, nullptr, nullptr,
                      reinterpret_cast<unsigned *>(ccounters), contrast_splits(n_graphs), 0};
+    if (n_nodes > 0 && scgib_gin_tiles(n_nodes) + contrast_row_blocks(n_graphs) * con.nsplit >
+                           2 * kCUs) {
+        // both would not be resident at once (two workgroups per CU): the
+        // two launches (the contrastive grid is then several waves anyway)
+        const int rc = scgib_contrastive_fwd(z1, z2, n_graphs, cws, closs, ccounters, stream);
+        if (rc != SCGIB_OK) return rc;
+        con = ContrastArgs{};
+    }
     return mlp2_recon_fwd(x, d_in, n_nodes, w1, b1, w2, b2, r, out, rowptr, col, n_edges, ws,
                           counter, loss, dims, con, stream);
 }
@@ -1724,7 +1732,7 @@ static int mlp2_recon_bwd(const float *x, const float *r, const float *out, cons
         // splits, each over more column tiles) rather than queue behind them
         // (sized for two per CU instead: 1.3 % slower)
         const int64_t nrb = contrast_row_blocks(con.B);
-        const int64_t fit = (kCUs - grid) / nrb;
+        const int64_t fit = (kCUs - grid) / nrb;  // >= 1 (scgib_mlp2_recon_contrastive_bwd)
         rec.con.nsplit = static_cast<int>(fit < 1 ? 1 : (fit < con.nsplit ? fit : con.nsplit));
         ncon = nrb * rec.con.nsplit;
     }
@@ -1760,6 +1768,14 @@ extern "C" int scgib_mlp2_recon_contrastive_bwd(
         return SCGIB_EINVAL;
     ContrastArgs con{z1, z2, n_graphs, cws, nullptr, g_con, dz1, dz2,
                      reinterpret_cast<unsigned *>(ccounters) + 1, contrast_splits(n_graphs), 0};
+    if (n_nodes > 0 && bwd_grid(scgib_gin_tiles(n_nodes)) + contrast_row_blocks(n_graphs) > kCUs) {
+        // not even one column split fits beside the MLP tiles (one workgroup
+        // per CU): the two launches, the contrastive one with all its splits
+        const int rc = mlp2_recon_bwd(x, r, out, ws, d_in, w1, w2, n_nodes, rowptr, col, rowptr_t,
+                                      col_t, g_loss, dx, slab, wgrad, dims, ContrastArgs{}, stream);
+        if (rc != SCGIB_OK) return rc;
+        return scgib_contrastive_bwd(z1, z2, n_graphs, cws, g_con, dz1, dz2, ccounters, stream);
+    }
     return mlp2_recon_bwd(x, r, out, ws, d_in, w1, w2, n_nodes, rowptr, col, rowptr_t, col_t,
                           g_loss, dx, slab, wgrad, dims, con, stream);
 }

@@ -217,17 +217,21 @@ class _SCGIBCore(nn.Module):
         else:
             u_gate, u_feat = self._noise(graph_features.shape[0], graph_features.device, noise)
         # compressor[0] (models.py:1092) runs fused in front of the interaction
-        if t is not None:
-            comp = enc_owner.compressor
-            im, z1, z2, kl, kl_mean = ops.interaction(graph_features, t, sub_readout, u_gate,
-                                                      u_feat, comp[1], comp[3],
-                                                      enc_owner.attn_layer, batch_g,
-                                                      enc_owner.training)
-        else:
-            im, z1, z2, kl, kl_mean = ops.interaction_lin(graph_features, sub_readout, u_gate,
-                                                          u_feat, enc_owner.compressor,
+        # its aside work (the compressor-BN running update) is enqueued at
+        # the model's join_aside(), after the losses (ops.LATE_FORK)
+        with ops.aside_deferred():
+            if t is not None:
+                comp = enc_owner.compressor
+                im, z1, z2, kl, kl_mean = ops.interaction(graph_features, t, sub_readout, u_gate,
+                                                          u_feat, comp[1], comp[3],
                                                           enc_owner.attn_layer, batch_g,
                                                           enc_owner.training)
+            else:
+                im, z1, z2, kl, kl_mean = ops.interaction_lin(graph_features, sub_readout,
+                                                              u_gate, u_feat,
+                                                              enc_owner.compressor,
+                                                              enc_owner.attn_layer, batch_g,
+                                                              enc_owner.training)
         enc_owner._last_kl_mean = kl_mean
         # the draws when noise was None (replayable via noise=)
         enc_owner._last_noise = (u_gate, u_feat) if noise is None else None

@@ -6,6 +6,7 @@ stream semantics apply) and raises ``ScgibError`` on any non-zero status.
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes
 import os
 
@@ -75,12 +76,44 @@ SIDE_REDUCE_WG = int(os.environ.get("SCGIB_SIDE_REDUCE_WG", "0"))
 SHARED_L0 = os.environ.get("SCGIB_SHARED_L0", "0") != "0"  # measured slower (A/B)
 
 
-def launch_aside(fn, *tensors):
-    main = torch.cuda.current_stream()
-    key = main.device.index
+# LATE_FORK: launch_aside records an event on the current stream now and
+# enqueues the aside work at join_aside() time, after it has waited on that
+# event — the same dependencies, but in a captured graph the main chain's
+# next kernel is then created first and so keeps the producer's hardware
+# queue (the replayed graph puts a node's first-created child on its queue)
+# Only inside aside_deferred() (model forwards, which always end with
+# join_aside()); elsewhere aside work is enqueued at once.
+LATE_FORK = os.environ.get("SCGIB_LATE_FORK", "1") != "0"
+_AUX_DEFERRED = []
+_DEFER_DEPTH = [0]
+
+
+@contextlib.contextmanager
+def aside_deferred():
+    _DEFER_DEPTH[0] += 1
+    try:
+        yield
+    finally:
+        _DEFER_DEPTH[0] -= 1
+
+
+def _aux_stream(device):
+    key = device.index
     aux = _AUX_STREAMS.get(key)
     if aux is None:
-        aux = _AUX_STREAMS[key] = torch.cuda.Stream(main.device)
+        aux = _AUX_STREAMS[key] = torch.cuda.Stream(device)
+    return key, aux
+
+
+def launch_aside(fn, *tensors):
+    main = torch.cuda.current_stream()
+    key, aux = _aux_stream(main.device)
+    if LATE_FORK and _DEFER_DEPTH[0] > 0:
+        ev = torch.cuda.Event()
+        ev.record(main)
+        _AUX_DEFERRED.append((key, ev, fn, tensors))
+        _AUX_PENDING.add(key)
+        return
     aux.wait_stream(main)
     for t in tensors:  # produced on main, consumed on aux
         t.record_stream(aux)
@@ -93,6 +126,14 @@ def join_aside():
     if not _AUX_PENDING:
         return
     main = torch.cuda.current_stream()
+    for key, ev, fn, tensors in _AUX_DEFERRED:  # LATE_FORK: enqueue now, after ev
+        aux = _AUX_STREAMS[key]
+        aux.wait_event(ev)
+        for t in tensors:
+            t.record_stream(aux)
+        with torch.cuda.stream(aux):
+            fn()
+    _AUX_DEFERRED.clear()
     for key in list(_AUX_PENDING):
         main.wait_stream(_AUX_STREAMS[key])
     _AUX_PENDING.clear()

@@ -74,6 +74,9 @@ SIDE_REDUCE_WG = int(os.environ.get("SCGIB_SIDE_REDUCE_WG", "0"))
 # (A/B: 0.538 vs 0.530 ms: the ego reduce then waits for the join; an extra
 # mid-chain cross-stream edge instead serialised the two chains in graph replay)
 SHARED_L0 = os.environ.get("SCGIB_SHARED_L0", "0") != "0"  # measured slower (A/B)
+# the same for the chain-after-chain order (the ego chain's final reduce then
+# follows the join; A/B 0.504 vs 0.494 ms: off)
+SHARED_L0_SEQ = os.environ.get("SCGIB_SHARED_L0_SEQ", "0") != "0"
 
 
 # LATE_FORK: launch_aside records an event on the current stream now and
@@ -595,6 +598,21 @@ class _GinEncoderPair(torch.autograd.Function):
         g_f_in = g_f
         if EGO_FIRST and not INTERLEAVE_BWD:  # capture the critical ego chain first
             ge = _GinEncoder.backward(ctx.sub[0], g_s, g_ro)
+        # shared layer-0 slabs: both encoders' transfer_d slabs in one buffer,
+        # the ego chain's final reduce (after the join) sums them — no add of
+        # the two d Wt after the join
+        shared = SHARED_L0 if INTERLEAVE_BWD else (SHARED_L0_SEQ and not EGO_FIRST)
+        l0_e = l0_c = None
+        if shared:
+            ns_e = int(_lib.query("scgib_gin_bwd_slabs", ctx.sub[0].saved_tensors[2].shape[0]))
+            ns_c = int(_lib.query("scgib_gin_bwd_slabs", ctx.sub[1].saved_tensors[2].shape[0]))
+            width = int(_lib.query("scgib_gin_layer0_slab_width"))
+            buf = torch.empty((ns_e + ns_c) * width, dtype=torch.float32,
+                              device=ctx.sub[0].saved_tensors[2].device)
+            buf.record_stream(side)
+            pending = []
+            l0_e = (buf, 0, ns_e + ns_c, True, pending)
+            l0_c = (buf, ns_e, ns_e + ns_c, False, None)
         with torch.cuda.stream(side):
             if ctx.lin and g_t is not None:
                 f, w0 = ctx.lin_saved
@@ -610,29 +628,14 @@ class _GinEncoderPair(torch.autograd.Function):
                 dw0, db0 = wg[: HIDDEN * HIDDEN].view(HIDDEN, HIDDEN), wg[HIDDEN * HIDDEN:]
                 g_f = df_total
             if not INTERLEAVE_BWD:
-                gc = _GinEncoder.backward(ctx.sub[1], g_f)
-        if INTERLEAVE_BWD and not SHARED_L0:
-            ge, gc = _interleave(_GinEncoder.backward_steps(ctx.sub[0], g_s, g_ro), main,
-                                 _GinEncoder.backward_steps(ctx.sub[1], g_f), side)
-        elif INTERLEAVE_BWD:  # both chains enqueued layer by layer, the ego chain first
-            # both encoders' transfer_d slabs in one buffer: the ego chain's
-            # final reduce sums them (after its layer-0 wait on Encoder1's)
-            ns_e = int(_lib.query("scgib_gin_bwd_slabs", ctx.sub[0].saved_tensors[2].shape[0]))
-            ns_c = int(_lib.query("scgib_gin_bwd_slabs", ctx.sub[1].saved_tensors[2].shape[0]))
-            width = int(_lib.query("scgib_gin_layer0_slab_width"))
-            buf = torch.empty((ns_e + ns_c) * width, dtype=torch.float32,
-                              device=ctx.sub[0].saved_tensors[2].device)
-            buf.record_stream(side)
-            pending = []
-            ge, gc = _interleave(
-                _GinEncoder.backward_steps(ctx.sub[0], g_s, g_ro,
-                                           l0=(buf, 0, ns_e + ns_c, True, pending)), main,
-                _GinEncoder.backward_steps(ctx.sub[1], g_f, l0=(buf, ns_e, ns_e + ns_c, False, None)),
-                side)
+                gc = _drain(_GinEncoder.backward_steps(ctx.sub[1], g_f, l0=l0_c))
+        if INTERLEAVE_BWD:  # both chains enqueued layer by layer, the ego chain first
+            ge, gc = _interleave(_GinEncoder.backward_steps(ctx.sub[0], g_s, g_ro, l0=l0_e), main,
+                                 _GinEncoder.backward_steps(ctx.sub[1], g_f, l0=l0_c), side)
         elif not EGO_FIRST:
-            ge = _GinEncoder.backward(ctx.sub[0], g_s, g_ro)
+            ge = _drain(_GinEncoder.backward_steps(ctx.sub[0], g_s, g_ro, l0=l0_e))
         main.wait_stream(side)
-        if INTERLEAVE_BWD and SHARED_L0:  # the ego chain's reduce, incl. both encoders' d Wt
+        if shared:  # the ego chain's reduce, incl. both encoders' d Wt
             jobs, keep = pending[0]
             _reduce_jobs(jobs, _stream())
             del keep

@@ -498,6 +498,32 @@ def test_mlp2_recon_fused(pkg, dev, n_mols, symmetric):
     assert rel_l2(xd.grad.cpu(), 3.0 * xd2.grad.cpu()) < 1e-5
 
 
+@pytest.mark.parametrize("max_wg", [1, 3, 64])
+def test_slab_reduce_multi_capped(pkg, dev, max_wg):
+    """scgib_slab_reduce_multi_ex on a capped grid (workgroups loop over the
+    column blocks) == the uncapped launch bitwise, and == the fp64 column sums
+    to fp32 rounding; three jobs incl. a strided column range."""
+    torch.manual_seed(max_wg)
+    a = torch.randn(37, 300, device=dev)
+    b = torch.randn(5, 64, device=dev)
+    c = torch.randn(150, 520, device=dev)  # columns [8, 8 + 200) of 520-wide slabs
+    outs = []
+    for cap in (0, max_wg):
+        o = [torch.empty(300, device=dev), torch.empty(64, device=dev),
+             torch.empty(200, device=dev)]
+        jobs = [pkg._lib.SlabJob(a.data_ptr(), o[0].data_ptr(), 300, 37, 0),
+                pkg._lib.SlabJob(b.data_ptr(), o[1].data_ptr(), 64, 5, 0),
+                pkg._lib.SlabJob(c.data_ptr() + 4 * 8, o[2].data_ptr(), 200, 150, 520)]
+        pkg.ops._reduce_jobs(jobs, pkg.ops._stream(), cap)
+        torch.cuda.synchronize()
+        outs.append([t.cpu() for t in o])
+    for u, v in zip(*outs):
+        assert torch.equal(u, v)
+    refs = [a.double().sum(0), b.double().sum(0), c.double()[:, 8:208].sum(0)]
+    for u, r in zip(outs[1], refs):
+        assert torch.allclose(u.double(), r.cpu(), rtol=1e-5, atol=1e-4)
+
+
 @pytest.mark.parametrize("n_mols,n_graphs", [(7, 5), (512, 512), (1000, 16), (1500, 1000)])
 def test_mlp2_recon_contrastive_fused(pkg, dev, n_mols, n_graphs):
     """The contrastive loss run in extra workgroups of the MLP + recon

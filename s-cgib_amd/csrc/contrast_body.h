@@ -156,33 +156,54 @@ __device__ __forceinline__ void contrast_fwd_body(const ContrastArgs &a, int64_t
     e12d = sum16(e12d);
     float *Dv = ws, *pf = ws + B;
     if (cl == 0 && i < B) st_agent4(pf + (by * B + i) * 4, make_float4(R, Bt, e11d, e12d));
+    // two-level combine: the last split of each row block finishes its 16
+    // rows (D, the -log terms, their fixed-order sum), then the last row
+    // block sums the row-block partials in order.  Counters: a.counters[0]
+    // (row blocks) and a.counters[1 + bx] (splits; the backward's counters,
+    // idle during the forward), each reset by its last arriver.
     unsigned *counter = a.counters;
-    if (!block_arrive(counter, static_cast<unsigned>(contrast_row_blocks(B) * NS))) return;
-    __shared__ double red[256];
-    double acc = 0.0;
-    for (int64_t k = tid; k < B; k += 256) {
-        // all splits' partials in flight (clamped split index), summed in order
+    const int64_t nrb = contrast_row_blocks(B);
+    int64_t off = B + static_cast<int64_t>(contrast_splits(B)) * B * 4;  // bwd partials, idle here
+    off += off & 1;
+    double *rbp = reinterpret_cast<double *>(ws + off);
+    if (!block_arrive(counter + 1 + bx, static_cast<unsigned>(NS))) return;
+    __shared__ double sRow[CR];
+    if (tid < CR) {
+        const int64_t k = bx * CR + tid;
+        const int64_t kc = k < B ? k : B - 1;  // clamped: the loads stay unconditional
         float4 v[kMaxSplit];
 #pragma unroll
         for (int y = 0; y < kMaxSplit; ++y)
-            v[y] = ld_agent4(pf + ((y < NS ? y : 0) * B + k) * 4);
-        float s[4] = {0.f, 0.f, 0.f, 0.f};
+            v[y] = ld_agent4(pf + ((y < NS ? y : 0) * B + kc) * 4);
+        float sm[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int y = 0; y < kMaxSplit; ++y) {
             const float w = y < NS ? 1.f : 0.f;
-            s[0] = fmaf(v[y].x, w, s[0]);
-            s[1] = fmaf(v[y].y, w, s[1]);
-            s[2] = fmaf(v[y].z, w, s[2]);
-            s[3] = fmaf(v[y].w, w, s[3]);
+            sm[0] = fmaf(v[y].x, w, sm[0]);
+            sm[1] = fmaf(v[y].y, w, sm[1]);
+            sm[2] = fmaf(v[y].z, w, sm[2]);
+            sm[3] = fmaf(v[y].w, w, sm[3]);
         }
-        const float D = s[0] + s[1] - s[2];
-        Dv[k] = D;
-        acc += static_cast<double>(-logf(s[3] / D));
+        const float D = sm[0] + sm[1] - sm[2];
+        if (k < B) Dv[k] = D;
+        sRow[tid] = k < B ? static_cast<double>(-logf(sm[3] / D)) : 0.0;
     }
-    red[tid] = acc;
     __syncthreads();
-    for (int off = 128; off >= 1; off >>= 1) {
-        if (tid < off) red[tid] += red[tid + off];
+    if (tid == 0) {
+        double t = 0.0;
+#pragma unroll
+        for (int r2 = 0; r2 < CR; ++r2) t += sRow[r2];
+        st_agent(rbp + bx, t);
+        counter[1 + bx] = 0u;
+    }
+    if (!block_arrive(counter, static_cast<unsigned>(nrb))) return;
+    __shared__ double red[256];
+    double t = 0.0;
+    for (int64_t b2 = tid; b2 < nrb; b2 += 256) t += ld_agent(rbp + b2);
+    red[tid] = t;
+    __syncthreads();
+    for (int o = 128; o >= 1; o >>= 1) {
+        if (tid < o) red[tid] += red[tid + o];
         __syncthreads();
     }
     if (tid == 0) {

@@ -368,6 +368,7 @@ class Mainmodel(_SCGIBCore):
                                         nn.BatchNorm1d(hidden_dim), nn.ReLU(),
                                         nn.Linear(hidden_dim, 1))
 
+    @ops.aside_guard
     def extract_features(self, nodes_list, batch_g, batch_x, flatten_batch_subgraphs, x_subs,
                          device=None, noise=None):
         ego, x_subs = self._prepare_ego(batch_g, flatten_batch_subgraphs, batch_x, x_subs)
@@ -376,6 +377,7 @@ class Mainmodel(_SCGIBCore):
         ops.join_aside()
         return im, kl, noisy, z2
 
+    @ops.aside_guard
     def forward(self, batch_g, batch_x, flatten_batch_subgraphs, batch_logMs, x_subs,
                 current_epoch=None, edge_index=None, k_transition=None, device=None,
                 batch_size=16, noise=None):
@@ -444,6 +446,7 @@ class Mainmodel_continue(_SCGIBCore):
         self.reconstructX = nn.Sequential(nn.Linear(hidden_dim, hidden_dim), nn.ReLU(),
                                           nn.Linear(hidden_dim, in_dim))
 
+    @ops.aside_guard
     def extract_features(self, nodes_list, batch_g, batch_x, flatten_batch_subgraphs, x_subs,
                          device=None, noise=None):
         ego, x_subs = self._prepare_ego(batch_g, flatten_batch_subgraphs, batch_x, x_subs)
@@ -452,6 +455,7 @@ class Mainmodel_continue(_SCGIBCore):
         ops.join_aside()
         return im, kl, noisy, z2
 
+    @ops.aside_guard
     def forward(self, batch_g, batch_x, flatten_batch_subgraphs, batch_logMs, x_subs,
                 current_epoch=None, edge_index=None, k_transition=None, device=None,
                 batch_size=16, noise=None):
@@ -537,6 +541,7 @@ class Mainmodel_domainadapt(_SCGIBCore):
         self.reconstructX = nn.Sequential(nn.Linear(hidden_dim, hidden_dim), nn.ReLU(),
                                           nn.Linear(hidden_dim, in_dim))
 
+    @ops.aside_guard
     def extract_features(self, nodes_list, batch_g, batch_x, flatten_batch_subgraphs, x_subs,
                          device=None, noise=None):
         """models.py:283-335: the DA model's own encoders / compressor /
@@ -547,6 +552,7 @@ class Mainmodel_domainadapt(_SCGIBCore):
         ops.join_aside()
         return im, kl, noisy, z2
 
+    @ops.aside_guard
     def forward(self, batch_g, batch_x, flatten_batch_subgraphs, batch_logMs, x_subs,
                 current_epoch=None, edge_index=None, k_transition=None, device=None,
                 batch_size=16, noise=None):
@@ -642,6 +648,7 @@ class Mainmodel_finetuning(nn.Module):
                                         nn.BatchNorm1d(hidden_dim), nn.ReLU(),
                                         nn.Linear(hidden_dim, 1))
 
+    @ops.aside_guard
     def forward(self, batch_g, batch_x, flatten_batch_subgraphs, x_subs, current_epoch=None,
                 edge_index=None, k_transition=None, device=None, batch_size=2, noise=None):
         self.batch_size = batch_size

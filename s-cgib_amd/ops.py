@@ -109,9 +109,17 @@ def _aux_stream(device):
 
 
 def launch_aside(fn, *tensors):
+    """Run ``fn`` (work nothing later in the step reads) off the critical path.
+    Only inside aside_deferred() — the model forwards, which always end with
+    join_aside() — does it go to the auxiliary stream; a standalone op call
+    (the C-ABI drop-in surface) runs it inline on the caller's stream, so the
+    op's in-place outputs are ordered before the caller's next read."""
+    if _DEFER_DEPTH[0] == 0:
+        fn()
+        return
     main = torch.cuda.current_stream()
     key, aux = _aux_stream(main.device)
-    if LATE_FORK and _DEFER_DEPTH[0] > 0:
+    if LATE_FORK:
         ev = torch.cuda.Event()
         ev.record(main)
         _AUX_DEFERRED.append((key, ev, fn, tensors))
@@ -123,6 +131,34 @@ def launch_aside(fn, *tensors):
     with torch.cuda.stream(aux):
         fn()
     _AUX_PENDING.add(key)
+
+
+def discard_aside():
+    """Error path of a model forward: drop aside work that was deferred but
+    never enqueued (replaying it with the next batch would apply that batch's
+    running-stat update twice) and join what already ran on the aux stream."""
+    _AUX_DEFERRED.clear()
+    if _AUX_PENDING:
+        main = torch.cuda.current_stream()
+        for key in list(_AUX_PENDING):
+            main.wait_stream(_AUX_STREAMS[key])
+        _AUX_PENDING.clear()
+
+
+def aside_guard(fn):
+    """Decorator for model forwards that end with join_aside(): an exception
+    raised between the deferred launch and the join discards the deferred
+    work instead of leaving it for the next forward."""
+    import functools
+
+    @functools.wraps(fn)
+    def wrapper(*args, **kwargs):
+        try:
+            return fn(*args, **kwargs)
+        except BaseException:
+            discard_aside()
+            raise
+    return wrapper
 
 
 def join_aside():
@@ -937,15 +973,18 @@ _COUNTER_RANGES = {}  # (device index, key) -> (offset, size)
 
 def counters(device, key, n):
     """``n`` zeroed uint32 counters reserved for call site ``key`` on ``device``
-    (allocate outside graph capture: the first call per device allocates)."""
+    and the current stream (allocate outside graph capture: the first call per
+    device allocates).  Keying by stream as well keeps two launches of one call
+    site that run concurrently on different streams (e.g. two contrastive ops)
+    on disjoint ranges; launches on one stream are ordered, so they share."""
     idx = torch.device(device).index or 0
     buf = _COUNTERS.get(idx)
     if buf is None:
         buf = _COUNTERS[idx] = torch.zeros(_COUNTER_CAP, dtype=torch.int32, device=device)
-    rk = (idx, key)
+    rk = (idx, key, torch.cuda.current_stream(device).cuda_stream)
     off, size = _COUNTER_RANGES.get(rk, (None, 0))
     if size < n:
-        used = max((o + s for (d, _), (o, s) in _COUNTER_RANGES.items() if d == idx), default=0)
+        used = max((o + s for (d, _, _), (o, s) in _COUNTER_RANGES.items() if d == idx), default=0)
         if used + n > _COUNTER_CAP:
             raise _lib.ScgibError("arrival-counter pool exhausted")
         off, size = used, n

@@ -96,7 +96,7 @@ def check_grads_model(golden_grads, mine_of, tol=1e-3, cos_min=0.999, cancelled=
     sits within rounding of 0 (e.g. |z| = 3e-7 for a K=64 dot product of O(1)
     terms) on opposite sides of a ReLU; that changes the gradient by a whole
     upstream value at one element, which on a small tensor (a 64-bias) is a
-    percent-level per-tensor error (tools/diag_chain.py shows such a case in
+    percent-level per-tensor error (a one-off chain diagnostic showed such a case in
     the L5 golden).  So: the concatenation of all hot-path gradients must
     agree within ``tol`` relative L2, and every tensor must point the same
     way (cosine >= cos_min), which a sign/layout/indexing bug would break."""

@@ -678,7 +678,7 @@ def test_gin_encoder_transfer_fold(pkg, dev, training, via_ego):
     sum(dy) and sum(dy * xhat), so ONE fp32 ReLU-kink flip anywhere (a
     pre-activation within rounding of 0 landing on the other side) shifts
     every gradient by ~1/N: at 200 molecules both fp32 paths — folded and
-    unfused alike — reach ~1e-3 rel-L2 on some seeds (tools/diag_fold5.py:
+    unfused alike — reach ~1e-3 rel-L2 on some seeds (measured with a one-off fold script:
     seed 7, L=1: 4.47e-4 for both, one flipped output each) and ~1e-6
     otherwise.  Bound: 5e-3 with direction intact; the exact check is
     test_gin_encoder_transfer_fold_small_exact."""

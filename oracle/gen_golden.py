@@ -267,7 +267,7 @@ def gen_model_golden(models, util_mod, name, *, workload, F, B, L, k, continue_w
 
 
 def gen_finetune_golden(models, util_mod, name, *, workload, F, B, k, dataset, num_classes,
-                        loss_kind, seed):
+                        loss_kind, seed, L=4):
     """Mainmodel_finetuning (models.py:358-543) on a pretrained
     Mainmodel_continue: scores, loss, trainable-parameter gradients (the
     freezing quirk decides which), with recorded noise."""
@@ -294,6 +294,10 @@ def gen_finetune_golden(models, util_mod, name, *, workload, F, B, k, dataset, n
         pre = models.Mainmodel_continue(args, F, hidden_dim=64, num_layers=4, num_heads=4,
                                         k_transition=k, num_classes=num_classes,
                                         cp_filename="<mem>", encoder="GIN")
+        # the shipped checkpoint's (and the paper's) 5-GINConv encoders: grown
+        # before the fine-tune model is built, so its freezing loop sees them
+        for enc in (inner.Encoder1, inner.Encoder2, pre.Encoder1, pre.Encoder2):
+            _grow_gin(models, enc, L)
         models.torch.load = lambda *a, **kw: pre
         model = models.Mainmodel_finetuning(args, F, hidden_dim=64, num_layers=4, num_heads=4,
                                             k_transition=k, num_classes=num_classes,
@@ -321,7 +325,7 @@ def gen_finetune_golden(models, util_mod, name, *, workload, F, B, k, dataset, n
     u_gate = torch.cat([draws[2 * i].reshape(-1) for i in range(B)])
     u_feat = torch.cat([draws[2 * i + 1] for i in range(B)])
     out = {
-        "B": np.array(B), "k": np.array(k), "F": np.array(F),
+        "B": np.array(B), "k": np.array(k), "F": np.array(F), "L": np.array(L),
         "num_classes": np.array(num_classes), "dataset": np.array(dataset),
         "loss_kind": np.array(loss_kind),
         "batch_num_nodes": batch_g.batch_num_nodes().numpy(),
@@ -454,6 +458,9 @@ def main():
     if sys.argv[1:] == ["domainadapt"]:  # only the domain-adaptation goldens
         gen_domain_adaptation(models, util)
         return
+    if sys.argv[1:] == ["round2"]:  # only the goldens added in round 2
+        gen_round2(models, util)
+        return
     gen_ingest_and_ego(util)
     common = dict(B=8, chunk=4)
     gen_model_golden(models, util, "pretrain_L4_k1_qm9", workload="qm9", F=11, L=4, k=1,
@@ -473,6 +480,17 @@ def main():
     gen_finetune_golden(models, util, "finetune_molhiv_bce", workload="molhiv", F=9, B=8, k=1,
                         dataset="ogbg-molhiv", num_classes=1, loss_kind="bce", seed=5)
     gen_domain_adaptation(models, util)
+    gen_round2(models, util)
+
+
+def gen_round2(models, util):
+    # molpcba-shaped pretrain step (BASELINE configs[2]: k = 1, OGB features F = 9)
+    gen_model_golden(models, util, "pretrain_L5_k1_ogb_continue", workload="molpcba", F=9, L=5,
+                     k=1, continue_wrapper=True, seed=9, B=8, chunk=4)
+    # BASELINE configs[0] names a 5-layer GIN for the Mutagenicity fine-tune
+    gen_finetune_golden(models, util, "finetune_mutag_ce_L5", workload="mutagenicity", F=14,
+                        B=8, k=1, dataset="Mutagenicity", num_classes=2, loss_kind="ce",
+                        seed=10, L=5)
 
 
 def gen_domain_adaptation(models, util):

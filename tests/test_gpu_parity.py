@@ -8,7 +8,7 @@ import pytest
 import torch
 import torch.nn.functional as F
 
-from conftest import (CANCELLED, MODEL_GOLDENS, check_grads, check_grads_model, golden_logms,
+from conftest import (CANCELLED, FINETUNE_GOLDENS, MODEL_GOLDENS, check_grads, check_grads_model, golden_logms,
                       load_golden, rel_err, rel_l2)
 from oracle import egonet
 from oracle import scgib_ref as R
@@ -575,8 +575,8 @@ def test_mlp2_recon_contrastive_fused(pkg, dev, n_mols, n_graphs):
 def _finetune_model(pkg, g, dev):
     from types import SimpleNamespace
     args = SimpleNamespace(recons_type="adj", useAtt=1, readout_f="sum", d_transfer=32,
-                           batch_size=int(g["B"]), gin_layers=4, task="graph_classification",
-                           dataset=str(g["dataset"]), device=dev)
+                           batch_size=int(g["B"]), gin_layers=int(g.get("L", 4)),
+                           task="graph_classification", dataset=str(g["dataset"]), device=dev)
     F_in, C, k = int(g["F"]), int(g["num_classes"]), int(g["k"])
     inner = pkg.models.Mainmodel(args, F_in, 64, 4, 4, k, "GIN")
     pre = pkg.models.Mainmodel_continue(args, F_in, 64, 4, 4, k, C, inner, "GIN")
@@ -587,7 +587,7 @@ def _finetune_model(pkg, g, dev):
     return ft.to(dev).train()
 
 
-@pytest.mark.parametrize("name", ["finetune_mutag_ce", "finetune_molhiv_bce"])
+@pytest.mark.parametrize("name", FINETUNE_GOLDENS)
 @pytest.mark.parametrize("device_ego", [True, False])
 def test_finetune_matches_reference(pkg, dev, name, device_ego):
     g = load_golden(name)

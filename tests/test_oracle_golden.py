@@ -6,7 +6,7 @@ import pytest
 import torch
 import torch.nn.functional as F
 
-from conftest import MODEL_GOLDENS, check_grads, golden_logms, load_golden, rel_err, rel_l2
+from conftest import FINETUNE_GOLDENS, MODEL_GOLDENS, check_grads, golden_logms, load_golden, rel_err, rel_l2
 from oracle import scgib_ref as R
 
 
@@ -59,7 +59,6 @@ def test_oracle_matches_reference_golden(name):
 # ---------------------------------------------------------------------------
 # Fine-tune head: oracle restatement vs the reference's Mainmodel_finetuning
 # ---------------------------------------------------------------------------
-FINETUNE_GOLDENS = ["finetune_mutag_ce", "finetune_molhiv_bce"]
 
 
 def finetune_inputs(g):

@@ -304,6 +304,9 @@ def gen_finetune_golden(models, util_mod, name, *, workload, F, B, k, dataset, n
                                             cp_filename="<mem>", encoder="GIN")
     finally:
         models.torch.load = real_load
+    # the fine-tune model's own (unused) encoders, as deep as the checkpoint's
+    for enc in (model.Encoder1, model.Encoder2):
+        _grow_gin(models, enc, L)
     model.train()
     with torch.no_grad():
         for n_, p_ in model.named_parameters():

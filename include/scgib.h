@@ -102,14 +102,16 @@ int scgib_gin_aggregate(const float *h, const int32_t *rowptr, const int32_t *co
  *   dh_v = (1+eps) g_v + sum_{u in out(v)} g_u.  Per-tile sum(dy), sum(dy xhat).
  * scgib_bn_bwd_finalize: dgamma, dbeta [64] and coef [2][64] for dz2.
  * scgib_gin_layer_bwd: d(agg) [n,d_in] and wgrad = dW2[64*64] | dW1[64*d_in]
- *   | db2[64] | db1[64] through scgib_gin_bwd_slabs(n) per-workgroup slabs of
- *   64*64 + 64*d_in + 128 floats (scgib_gin_slab_floats(n, d_in) in total),
+ *   | db2[64] | db1[64] through scgib_gin_layer_bwd_slabs(n, d_in) per-workgroup
+ *   slabs of 64*64 + 64*d_in + 128 floats (scgib_gin_slab_floats(n, d_in) in
+ *   total; d_in = 64: one workgroup per CU walking its tiles, LDS-DMA staged),
  *   reduced in a fixed order.  With wgrad NULL the slabs are left for the
  *   caller's scgib_slab_reduce (so the GEMM kernel can be timed alone).
  * scgib_slab_reduce: out[w] = sum_s slab[s*width + w], fixed order. */
 int64_t scgib_gin_tiles(int64_t n_nodes);
 int64_t scgib_gin_slab_floats(int64_t n_nodes, int32_t d_in);
-int64_t scgib_gin_bwd_slabs(int64_t n_nodes);
+int64_t scgib_gin_bwd_slabs(int64_t n_nodes);  /* layer-0 (transfer_d folded) slabs */
+int64_t scgib_gin_layer_bwd_slabs(int64_t n_nodes, int32_t d_in);
 /* Up to scgib_slab_reduce_max_jobs() independent scgib_slab_reduce's in one
  * launch (same fixed order per job): out[w] = sum_s slab[s*stride + w] for
  * w < width; stride 0 means width (a column range of wider slabs otherwise,

@@ -639,7 +639,7 @@ __global__ __launch_bounds__(256) void gin_fwd_k(
     const int ccol = wc * 32 + (l & 31);
     // z1 = agg W1^T + b1 ; r = relu(z1)
     {
-        f32x16 acc = mma_nt<DIN>(sA + wr * 32 * LDA, LDA, sW1 + wc * 32 * LDA, LDA, zero16());
+        f32x16 acc = mma_pf<DIN, false, false>(sA + wr * 32 * LDA, LDA, sW1 + wc * 32 * LDA, LDA, zero16());
         const float bias = b1[ccol];
 #pragma unroll
         for (int reg = 0; reg < 16; ++reg) {
@@ -652,7 +652,7 @@ __global__ __launch_bounds__(256) void gin_fwd_k(
     __syncthreads();
     SCGIB_MARK(2);
     // z2 = r W2^T + b2 ; tile statistics of z2 (valid rows only)
-    f32x16 acc = mma_nt<64>(sR + wr * 32 * LDH, LDH, sW2 + wc * 32 * LDH, LDH, zero16());
+    f32x16 acc = mma_pf<64, false, false>(sR + wr * 32 * LDH, LDH, sW2 + wc * 32 * LDH, LDH, zero16());
     const float bias2 = b2[ccol];
     float s = 0.f;
 #pragma unroll
@@ -673,7 +673,7 @@ __global__ __launch_bounds__(256) void gin_fwd_k(
                 sA[row * LDH + ccol] = row < nv ? acc[reg] : 0.f;
             }
             __syncthreads();
-            const f32x16 g = mma_tn<TM>(sA + wr * 32, LDH, sA + wc * 32, LDH, zero16());
+            const f32x16 g = mma_pf<TM, true, true>(sA + wr * 32, LDH, sA + wc * 32, LDH, zero16());
             float *gs = rec.gslab + tile * 4096;
 #pragma unroll
             for (int reg = 0; reg < 16; ++reg) gs[(wr * 32 + acc_row(reg, l)) * 64 + ccol] = g[reg];
@@ -1031,28 +1031,6 @@ __global__ __launch_bounds__(256, (DIN <= 64 && !RECON ? SCGIB_BWD_MINB : 1)) vo
     // staging roles: 4-channel chunk c4, rows rs + 16 k
     const int c4 = tid & 15, rs = tid >> 4;
     const float4 zero = make_float4(0.f, 0.f, 0.f, 0.f);
-    float4 s_mean = zero, s_istd = zero, s_sc = zero, c1 = zero, c2 = zero;
-    if (BN) {
-        s_mean = ld4(stat + 4 * c4);
-        s_istd = ld4(stat + 64 + 4 * c4);
-        s_sc = ld4(stat + 128 + 4 * c4);
-        if (!pend.gpart) {
-            c1 = ld4(coef + 4 * c4);
-            c2 = ld4(coef + 64 + 4 * c4);
-        } else {  // finish the sums; workgroup 0 writes dgamma, dbeta
-            __shared__ float sCoef[128];
-            const double tot = bn_bwd_final<false>(pend.gpart, pend_ngr, bfin);
-            const int cs = bfin_index();
-            const bool lead = (tid & 63) < 32, w0 = blockIdx.x == 0 && lead;
-            const float cf = bn_bwd_publish(cs, tot, n, pend.training, w0 ? pend.dgamma : nullptr,
-                                            w0 ? pend.dbeta : nullptr, nullptr);
-            if (lead) sCoef[cs] = cf;
-            __syncthreads();
-            c1 = make_float4(sCoef[4 * c4], sCoef[4 * c4 + 1], sCoef[4 * c4 + 2], sCoef[4 * c4 + 3]);
-            c2 = make_float4(sCoef[64 + 4 * c4], sCoef[65 + 4 * c4], sCoef[66 + 4 * c4],
-                             sCoef[67 + 4 * c4]);
-        }
-    }
     constexpr int NSUB1 = 2 * (DIN / 32);  // 32x32 sub-tiles of dW1 / d(agg)
     constexpr int NW1 = (NSUB1 + 3) / 4;   // per wave
     f32x16 accW2 = zero16(), accW1[NW1];
@@ -1098,6 +1076,28 @@ __global__ __launch_bounds__(256, (DIN <= 64 && !RECON ? SCGIB_BWD_MINB : 1)) vo
                           rr < m, zero);
         }
     };
+    float4 s_mean = zero, s_istd = zero, s_sc = zero, c1 = zero, c2 = zero;
+    if (BN) {
+        s_mean = ld4(stat + 4 * c4);
+        s_istd = ld4(stat + 64 + 4 * c4);
+        s_sc = ld4(stat + 128 + 4 * c4);
+        if (!pend.gpart) {
+            c1 = ld4(coef + 4 * c4);
+            c2 = ld4(coef + 64 + 4 * c4);
+        } else {  // finish the sums; workgroup 0 writes dgamma, dbeta
+            __shared__ float sCoef[128];
+            const double tot = bn_bwd_final<false>(pend.gpart, pend_ngr, bfin);
+            const int cs = bfin_index();
+            const bool lead = (tid & 63) < 32, w0 = blockIdx.x == 0 && lead;
+            const float cf = bn_bwd_publish(cs, tot, n, pend.training, w0 ? pend.dgamma : nullptr,
+                                            w0 ? pend.dbeta : nullptr, nullptr);
+            if (lead) sCoef[cs] = cf;
+            __syncthreads();
+            c1 = make_float4(sCoef[4 * c4], sCoef[4 * c4 + 1], sCoef[4 * c4 + 2], sCoef[4 * c4 + 3]);
+            c2 = make_float4(sCoef[64 + 4 * c4], sCoef[65 + 4 * c4], sCoef[66 + 4 * c4],
+                             sCoef[67 + 4 * c4]);
+        }
+    }
     if (PIPE && blockIdx.x < ntiles) {
         load_rows(blockIdx.x);
         load_agg(blockIdx.x);
@@ -1166,7 +1166,7 @@ __global__ __launch_bounds__(256, (DIN <= 64 && !RECON ? SCGIB_BWD_MINB : 1)) vo
         }
         __syncthreads();
         if constexpr (RECON) {  // sD = IM tile -> dz2 = d IM = (g/N) (4 IM G - 2 nb)
-            const f32x16 p = mma_nn<64>(sD + wr * 32 * LDH, LDH, sG + wc * 32, LDH, zero16());
+            const f32x16 p = mma_pf<64, false, true>(sD + wr * 32 * LDH, LDH, sG + wc * 32, LDH, zero16());
             __syncthreads();
 #pragma unroll
             for (int reg = 0; reg < 16; ++reg)
@@ -1186,9 +1186,10 @@ __global__ __launch_bounds__(256, (DIN <= 64 && !RECON ? SCGIB_BWD_MINB : 1)) vo
         if (PIPE && next < ntiles) load_rows(next);  // in flight during the GEMMs below
         if (tile == blockIdx.x) SCGIB_MARK(1);
         // dW2 += dz2^T r  (sub-tile j-block wr, k-block wc)
-        accW2 = mma_tn<TM>(sD + wr * 32, LDH, sR + wc * 32, LDH, accW2);
-        // dr = dz2 W2  (rows wr, cols wc)
-        f32x16 dr = mma_nn<64>(sD + wr * 32 * LDH, LDH, sW2 + wc * 32, LDH, zero16());
+        // dr = dz2 W2  (rows wr, cols wc); the two products alternate
+        f32x16 dr = zero16();
+        mma_pf2<64, true, true, false, true>(sD + wr * 32, LDH, sR + wc * 32, LDH, accW2,
+                                             sD + wr * 32 * LDH, LDH, sW2 + wc * 32, LDH, dr);
         for (int rr = q; rr < TM; rr += 4) db2 += sD[rr * LDH + ch];
         __syncthreads();  // all reads of dz2 done
         // dz1 = dr * [r > 0]  -> sD
@@ -1214,8 +1215,9 @@ __global__ __launch_bounds__(256, (DIN <= 64 && !RECON ? SCGIB_BWD_MINB : 1)) vo
             const int sub = w + 4 * q1;
             if (sub < NSUB1) {
                 const int jb = sub & 1, kb = sub >> 1;  // j-block (rows of dW1 / d(agg)), k-block
-                accW1[q1] = mma_tn<TM>(sD + jb * 32, LDH, sA + kb * 32, LDA, accW1[q1]);
-                f32x16 da = mma_nn<64>(sD + jb * 32 * LDH, LDH, sW1 + kb * 32, LDA, zero16());
+                f32x16 da = zero16();
+                mma_pf2<64, true, true, false, true>(sD + jb * 32, LDH, sA + kb * 32, LDA, accW1[q1],
+                                                     sD + jb * 32 * LDH, LDH, sW1 + kb * 32, LDA, da);
 #pragma unroll
                 for (int reg = 0; reg < 16; ++reg) {
                     const int row = jb * 32 + acc_row(reg, l);
@@ -1270,6 +1272,244 @@ __global__ __launch_bounds__(256, (DIN <= 64 && !RECON ? SCGIB_BWD_MINB : 1)) vo
     SCGIB_MARK(4);
 }
 
+// ---------------------------------------------------------------------------
+// gin_bwd2_k: the GIN layer backward (BN, d_in = 64) as a staging pipeline.
+//
+// gin_bwd_k stages each tile through registers, two workgroups per CU in
+// lockstep: both load (per-CU fetch bound, ~6 us at QM9 B512), then both
+// compute (MFMA, ~7 us) — nothing overlaps (phase trace r02).  Here ONE
+// workgroup per CU walks its tiles (blockIdx.x, + gridDim.x, ...): the
+// weights and the first tile arrive by LDS-DMA (global_load_lds_dwordx4, no
+// VGPRs) while the BN-backward sums are finished; the next tile is loaded
+// into registers at the start of this tile's GEMMs and written to LDS after
+// them (issue early / write late).  Not LDS-DMA in the loop: with a DMA in
+// flight hipcc models the LDS counter as out of order and waits lgkmcnt(0)
+// before every MFMA operand read (ISA: counted waits only without it).
+// The images are unpadded row-major: every GEMM reads them with 32 lanes on
+// consecutive floats of one row (TN operands over rows, the NN weight
+// operand), which is bank-conflict free at any row stride; only the
+// VALU-written dz tile (read along rows by the NN products) keeps the +1 pad.
+// Arithmetic, k order and slab layout are those of gin_bwd_k, so results are
+// bitwise gin_bwd_k's (dW: one slab per workgroup, fewer workgroups — the
+// slab reduce sums the same products in a different grouping).
+// LDS: weights 32 KB + dy, z2, r, agg 64 KB + dz 16.6 KB (one workgroup per CU).
+// ---------------------------------------------------------------------------
+// s_waitcnt through the builtin (the compiler's wait model sees it, an asm
+// statement it does not): vmcnt(0) = 0x0F70, lgkmcnt(0) alone = 0xC07F (gfx9
+// encoding: vmcnt [3:0] + [15:14], expcnt [6:4], lgkmcnt [11:8])
+__device__ __forceinline__ void vm_wait_all() { __builtin_amdgcn_s_waitcnt(0x0F70); }
+// barrier without the vmcnt(0) of a __syncthreads fence (global stores and
+// prefetch loads stay in flight across it)
+__device__ __forceinline__ void lds_barrier() {
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    __builtin_amdgcn_s_barrier();
+}
+
+// rows [r0, r0 + TM) x W floats of a row-major [*, W] array -> s[TM][W]
+// (unpadded), by 16-byte LDS-DMA: TM * W / 256 wave-instructions of 1 KiB,
+// spread over the 4 waves.  Source rows past `last` read row `last` (valid
+// memory; the consumer never lets them into a result).
+template <int W>
+__device__ __forceinline__ void glds_tile(const float *__restrict__ g, float *s, int64_t r0,
+                                          int64_t last) {
+    constexpr int NI = TM * W / 256 / 4;  // instructions per wave
+    const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+#pragma unroll
+    for (int k = 0; k < NI; ++k) {
+        const int e = (w * NI + k) * 256 + 4 * l;  // float offset in the tile image
+        int64_t row = r0 + e / W;
+        row = row < last ? row : last;
+        __builtin_amdgcn_global_load_lds(g + row * W + e % W, s + (w * NI + k) * 256, 16, 0, 0);
+    }
+}
+
+// a [64][W] matrix (weights) -> s, contiguous copy
+template <int W>
+__device__ __forceinline__ void glds_matrix(const float *__restrict__ g, float *s) {
+    constexpr int NI = 64 * W / 256 / 4;
+    const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+#pragma unroll
+    for (int k = 0; k < NI; ++k) {
+        const int e = (w * NI + k) * 256;
+        __builtin_amdgcn_global_load_lds(g + e + 4 * l, s + e, 16, 0, 0);
+    }
+}
+
+template <int DIN>
+__global__ __launch_bounds__(256, 1) void gin_bwd2_k(
+    const float *__restrict__ dy, const float *__restrict__ z2, const float *__restrict__ r,
+    const float *__restrict__ agg, const float *__restrict__ stat,
+    const float *__restrict__ coef, const float *__restrict__ w1, const float *__restrict__ w2,
+    int64_t ncap, int64_t ntiles, float *__restrict__ dagg_out, float *__restrict__ slab,
+    const int32_t *__restrict__ dims, scgib_bn_bwd_pending pend) {
+    static_assert(DIN == 64, "unpadded [TM][DIN] DMA images of whole 256-B rows");
+    constexpr int LDD = LDH;  // dz tile: VALU-written, read along rows
+    constexpr int SLAB = 64 * 64 + 64 * DIN + 128;
+    __shared__ __attribute__((aligned(16))) float sW2[64 * 64];
+    __shared__ __attribute__((aligned(16))) float sW1[64 * DIN];
+    __shared__ __attribute__((aligned(16))) float sDY[TM * 64];
+    __shared__ __attribute__((aligned(16))) float sZ2[TM * 64];
+    __shared__ __attribute__((aligned(16))) float sR[TM * 64];
+    __shared__ __attribute__((aligned(16))) float sA[TM * DIN];
+    __shared__ float sD[TM * LDD];
+    __shared__ float sCoef[128];
+    __shared__ float sB[2][4][64];
+    const int64_t n = eff_count(dims, 0, ncap);
+    const int tid = threadIdx.x, l = tid & 63, w = tid >> 6;
+    const int wr = w >> 1, wc = w & 1;
+    const int ch = tid & 63, q = tid >> 6;    // column-sum roles: channel, row quarter
+    const int c4 = tid & 15, rs = tid >> 4;   // elementwise roles: chunk c4, rows rs + 16 k
+    const int64_t last = ncap - 1;            // last row of the allocations
+    const unsigned gsz = gridDim.x;
+    SCGIB_MARK(0);
+    SCGIB_MARK_HWID();
+    // ordinary loads first (the BN finish and the stat rows), then the DMA
+    BwdFin bfin;
+    const int pend_ngr = static_cast<int>(((n + TM - 1) / TM + kGroup - 1) / kGroup);
+    if (pend.gpart) bn_bwd_fin_load<false>(pend.gpart, pend_ngr, 0, bfin);
+    const float4 s_mean = ld4(stat + 4 * c4), s_istd = ld4(stat + 64 + 4 * c4);
+    const float4 s_sc = ld4(stat + 128 + 4 * c4);
+    float4 c1 = make_float4(0.f, 0.f, 0.f, 0.f), c2 = c1;
+    if (!pend.gpart) {
+        c1 = ld4(coef + 4 * c4);
+        c2 = ld4(coef + 64 + 4 * c4);
+    }
+    glds_matrix<64>(w2, sW2);
+    glds_matrix<DIN>(w1, sW1);
+    int64_t tile = blockIdx.x;
+    if (tile < ntiles) {
+        const int64_t r0 = tile * TM;
+        glds_tile<64>(dy, sDY, r0, last);
+        glds_tile<64>(z2, sZ2, r0, last);
+        glds_tile<64>(r, sR, r0, last);
+        glds_tile<DIN>(agg, sA, r0, last);
+    }
+    if (pend.gpart) {  // finish the BN-backward sums; workgroup 0 writes dgamma, dbeta
+        const double tot = bn_bwd_final<false>(pend.gpart, pend_ngr, bfin);
+        const int cs = bfin_index();
+        const bool lead = (tid & 63) < 32, w0 = blockIdx.x == 0 && lead;
+        const float cf = bn_bwd_publish(cs, tot, n, pend.training, w0 ? pend.dgamma : nullptr,
+                                        w0 ? pend.dbeta : nullptr, nullptr);
+        if (lead) sCoef[cs] = cf;
+    }
+    vm_wait_all();
+    lds_barrier();
+    if (pend.gpart) {
+        c1 = make_float4(sCoef[4 * c4], sCoef[4 * c4 + 1], sCoef[4 * c4 + 2], sCoef[4 * c4 + 3]);
+        c2 = make_float4(sCoef[64 + 4 * c4], sCoef[65 + 4 * c4], sCoef[66 + 4 * c4],
+                         sCoef[67 + 4 * c4]);
+    }
+    f32x16 accW2 = zero16(), accW1 = zero16();
+    float db2 = 0.f, db1 = 0.f;
+    // the next tile in registers: dy, z2, r, agg rows rs + 16 k, chunk c4
+    float4 nx[4][4];
+    const float *const srcs[4] = {dy, z2, r, agg};
+    float *const dsts[4] = {sDY, sZ2, sR, sA};
+    for (; tile < ntiles; tile += gsz) {
+        const int64_t row0 = tile * TM;
+        const int nv = static_cast<int>(n - row0 < TM ? (n - row0 > 0 ? n - row0 : 0) : TM);
+        if (dims) {  // capacity mode: zero this tile's padded rows of d(agg)
+            const int ncr = static_cast<int>(ncap - row0 < TM ? ncap - row0 : TM);
+            for (int idx = nv * DIN + tid; idx < ncr * DIN; idx += 256) dagg_out[row0 * DIN + idx] = 0.f;
+            // block-uniform; every later tile of this workgroup is empty too
+            // (nothing was prefetched for it, nothing computes on it)
+            if (nv == 0) continue;
+        }
+        const int64_t next = tile + gsz;  // block-uniform
+        const bool more = next < ntiles;
+        // dz2 = scale (dy - c1 - xhat c2); rows past nv are zero
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int rr = rs + 16 * k;
+            const float4 vd = *reinterpret_cast<const float4 *>(sDY + rr * 64 + 4 * c4);
+            const float4 vz = *reinterpret_cast<const float4 *>(sZ2 + rr * 64 + 4 * c4);
+            float4 d = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (rr < nv) {
+                d.x = s_sc.x * (vd.x - c1.x - (vz.x - s_mean.x) * s_istd.x * c2.x);
+                d.y = s_sc.y * (vd.y - c1.y - (vz.y - s_mean.y) * s_istd.y * c2.y);
+                d.z = s_sc.z * (vd.z - c1.z - (vz.z - s_mean.z) * s_istd.z * c2.z);
+                d.w = s_sc.w * (vd.w - c1.w - (vz.w - s_mean.w) * s_istd.w * c2.w);
+            }
+            float *pd = sD + rr * LDD + 4 * c4;
+            pd[0] = d.x; pd[1] = d.y; pd[2] = d.z; pd[3] = d.w;
+        }
+        lds_barrier();  // dz2 complete; dy / z2 consumed
+        if (more) {     // the next tile: in flight during both GEMM pairs
+            const int64_t r1 = next * TM;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                int64_t row = r1 + rs + 16 * k;
+                row = row < last ? row : last;
+#pragma unroll
+                for (int t = 0; t < 4; ++t) nx[t][k] = ld4(srcs[t] + row * 64 + 4 * c4);
+            }
+        }
+        if (tile == blockIdx.x) SCGIB_MARK(1);
+        // dW2 += dz2^T r ; dr = dz2 W2  (rows wr, cols wc), the two products alternating
+        f32x16 dr = zero16();
+        mma_pf2<64, true, true, false, true>(sD + wr * 32, LDD, sR + wc * 32, 64, accW2,
+                                             sD + wr * 32 * LDD, LDD, sW2 + wc * 32, 64, dr);
+        for (int rr = q; rr < TM; rr += 4) db2 += sD[rr * LDD + ch];
+        lds_barrier();  // all reads of dz2 done
+        // dz1 = dr * [r > 0]  -> sD
+#pragma unroll
+        for (int reg = 0; reg < 16; ++reg) {
+            const int row = wr * 32 + acc_row(reg, l), cc = wc * 32 + (l & 31);
+            sD[row * LDD + cc] = sR[row * 64 + cc] > 0.f ? dr[reg] : 0.f;
+        }
+        lds_barrier();  // dz1 complete; r consumed
+        if (tile == blockIdx.x) SCGIB_MARK(2);
+        for (int rr = q; rr < TM; rr += 4) db1 += sD[rr * LDD + ch];
+        // dW1 += dz1^T agg (64 x DIN) ; d(agg) = dz1 W1 (TM x DIN): wave w owns
+        // sub-tile (jb, kb) = (w & 1, w >> 1) of both
+        {
+            const int jb = w & 1, kb = w >> 1;
+            f32x16 da = zero16();
+            mma_pf2<64, true, true, false, true>(sD + jb * 32, LDD, sA + kb * 32, DIN, accW1,
+                                                 sD + jb * 32 * LDD, LDD, sW1 + kb * 32, DIN, da);
+#pragma unroll
+            for (int reg = 0; reg < 16; ++reg) {
+                const int row = jb * 32 + acc_row(reg, l);
+                if (row < nv) dagg_out[(row0 + row) * DIN + kb * 32 + (l & 31)] = da[reg];
+            }
+        }
+        if (tile == blockIdx.x) SCGIB_MARK(3);
+        if (more) {
+            lds_barrier();  // every read of this tile's r / agg / dz1 done
+#pragma unroll
+            for (int t = 0; t < 4; ++t)
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    *reinterpret_cast<float4 *>(dsts[t] + (rs + 16 * k) * 64 + 4 * c4) = nx[t][k];
+            lds_barrier();
+        }
+    }
+    // per-workgroup slab: dW2 | dW1 | db2 | db1 (gin_bwd_k layout)
+    float *sl = slab + static_cast<int64_t>(blockIdx.x) * SLAB;
+#pragma unroll
+    for (int reg = 0; reg < 16; ++reg) {
+        const int j = wr * 32 + acc_row(reg, l), k = wc * 32 + (l & 31);
+        sl[j * 64 + k] = accW2[reg];
+    }
+    {
+        const int jb = w & 1, kb = w >> 1;
+#pragma unroll
+        for (int reg = 0; reg < 16; ++reg) {
+            const int j = jb * 32 + acc_row(reg, l), kk = kb * 32 + (l & 31);
+            sl[64 * 64 + j * DIN + kk] = accW1[reg];
+        }
+    }
+    sB[0][q][ch] = db2;
+    sB[1][q][ch] = db1;
+    __syncthreads();
+    if (tid < 128) {
+        const int which = tid >> 6;
+        sl[64 * 64 + 64 * DIN + which * 64 + ch] =
+            ((sB[which][0][ch] + sB[which][1][ch]) + sB[which][2][ch]) + sB[which][3][ch];
+    }
+    SCGIB_MARK(4);
+}
+
 // up to two workgroups per CU (66.5 KB LDS each): one tile per workgroup for
 // batches up to SCGIB_BWD_GRID_CAP tiles (build-time knob), so every tile of
 // an encoder layer runs at once; larger batches loop over tiles
@@ -1295,8 +1535,22 @@ extern "C" int scgib_trace_set(void *buf) {
 }
 #endif
 
+// scgib_gin_layer_bwd: d_in = 64 runs gin_bwd2_k (one workgroup per CU, each
+// walking its tiles), d_in = 32 gin_bwd_k (one workgroup per tile up to the cap)
+#ifndef SCGIB_BWD2
+#define SCGIB_BWD2 1
+#endif
+static constexpr bool kBwd2 = SCGIB_BWD2 != 0;
+
+extern "C" int64_t scgib_gin_layer_bwd_slabs(int64_t n_nodes, int32_t d_in) {
+    if (n_nodes <= 0) return 0;
+    const int64_t nt = scgib_gin_tiles(n_nodes);
+    if (d_in == 64 && kBwd2) return nt < kCUs ? nt : kCUs;
+    return bwd_grid(nt);
+}
+
 extern "C" int64_t scgib_gin_slab_floats(int64_t n_nodes, int32_t d_in) {
-    return static_cast<int64_t>(bwd_grid(scgib_gin_tiles(n_nodes))) * (64 * 64 + 64 * d_in + 128);
+    return scgib_gin_layer_bwd_slabs(n_nodes, d_in) * (64 * 64 + 64 * d_in + 128);
 }
 
 extern "C" int64_t scgib_gin_bwd_slabs(int64_t n_nodes) {
@@ -1583,10 +1837,12 @@ extern "C" int scgib_gin_layer_bwd(const float *dy, const float *z2, const float
     if (pending && (!pending->gpart || !pending->dgamma || !pending->dbeta)) return SCGIB_EINVAL;
     const scgib_bn_bwd_pending pd = pending ? *pending : scgib_bn_bwd_pending{};
     const int64_t nt = scgib_gin_tiles(n_nodes);
-    const int grid = bwd_grid(nt);
+    const int grid = static_cast<int>(scgib_gin_layer_bwd_slabs(n_nodes, d_in));
     hipStream_t st = as_stream(stream);
     if (d_in == 32)
         gin_bwd_k<32><<<grid, 256, 0, st>>>(dy, z2, r, agg, stat, coef, w1, w2, n_nodes, nt, dagg, slab, dims, nullptr, pd, ReconArgs{});
+    else if (kBwd2)
+        gin_bwd2_k<64><<<grid, 256, 0, st>>>(dy, z2, r, agg, stat, coef, w1, w2, n_nodes, nt, dagg, slab, dims, pd);
     else
         gin_bwd_k<64><<<grid, 256, 0, st>>>(dy, z2, r, agg, stat, coef, w1, w2, n_nodes, nt, dagg, slab, dims, nullptr, pd, ReconArgs{});
     const int rc = launch_status();
@@ -1599,7 +1855,7 @@ extern "C" int scgib_gin_layer_bwd(const float *dy, const float *z2, const float
 // and without BatchNorm (models.py:1055-1057, applied at :1174).
 // ---------------------------------------------------------------------------
 extern "C" int64_t scgib_mlp2_slab_floats(int64_t n_nodes, int32_t d_in) {
-    return scgib_gin_slab_floats(n_nodes, d_in);
+    return static_cast<int64_t>(bwd_grid(scgib_gin_tiles(n_nodes))) * (64 * 64 + 64 * d_in + 128);
 }
 
 extern "C" int scgib_mlp2_fwd(const float *x, int32_t d_in, int64_t n_nodes, const float *w1,

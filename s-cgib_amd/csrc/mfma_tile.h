@@ -221,6 +221,97 @@ __device__ __forceinline__ f32x16 mma_tn(const float *As, int lda, const float *
     return acc;
 }
 
+// ---------------------------------------------------------------------------
+// Operand-prefetching forms of the three products (same k order per output,
+// hence bitwise the results of mma_nt / mma_nn / mma_tn).  The loop forms
+// above let hipcc emit "2 x ds_read2_b32, s_waitcnt lgkmcnt(0), 2 MFMA": the
+// next reads issue only behind the dependent MFMA, so every MFMA pair pays an
+// LDS round trip (measured: ~130 cycles per 64-cycle MFMA, phase trace r02).
+// Here the operands of a chunk of C steps are read into registers one chunk
+// ahead and the MFMAs of up to two independent products alternate, so the
+// matrix pipe sees back-to-back issue.
+//   operand X(idx, k) = COL ? Xs[k * ld + idx] : Xs[idx * ld + k]
+//   NT = <false, false>, NN = <false, true>, TN = <true, true>
+// ---------------------------------------------------------------------------
+// pins the software pipeline: without it hipcc hoists every LDS read of the
+// product (IR level, across other loops) and the kernel spills
+__device__ __forceinline__ void mma_step_fence() {
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+}
+
+// lane base of operand X: step s then reads base[s * mma_step<COL>(ld)] — one
+// address register per operand, every step an immediate offset (an address
+// formed as ((2 s) | kk) * ld + i per step is hoisted per step and spills)
+template <bool COL>
+__device__ __forceinline__ const float *mma_base(const float *X, int ld) {
+    const int l = threadIdx.x & 63, i = l & 31, kk = l >> 5;
+    return COL ? X + kk * ld + i : X + i * ld + kk;
+}
+template <bool COL>
+__device__ __forceinline__ int mma_step(int ld) { return COL ? 2 * ld : 2; }
+
+template <int K, bool AC, bool BC, int D = 4>
+__device__ __forceinline__ f32x16 mma_pf(const float *As, int lda, const float *Bs, int ldb,
+                                         f32x16 acc) {
+    constexpr int S = K / 2, R = D + 1;
+    const float *pa = mma_base<AC>(As, lda), *pb = mma_base<BC>(Bs, ldb);
+    const int sa = mma_step<AC>(lda), sb = mma_step<BC>(ldb);
+    float a[R], b[R];
+#pragma unroll
+    for (int s = 0; s < D; ++s) {
+        a[s] = pa[s * sa];
+        b[s] = pb[s * sb];
+    }
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+        if (s + D < S) {
+            a[(s + D) % R] = pa[(s + D) * sa];
+            b[(s + D) % R] = pb[(s + D) * sb];
+        }
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[s % R], b[s % R], acc, 0, 0, 0);
+        mma_step_fence();
+    }
+    return acc;
+}
+
+// two independent products over the same K, MFMAs alternating
+template <int K, bool AC1, bool BC1, bool AC2, bool BC2, int D = 3>
+__device__ __forceinline__ void mma_pf2(const float *A1, int la1, const float *B1, int lb1,
+                                        f32x16 &c1, const float *A2, int la2, const float *B2,
+                                        int lb2, f32x16 &c2) {
+    constexpr int S = K / 2, R = D + 1;
+    const float *pa1 = mma_base<AC1>(A1, la1), *pb1 = mma_base<BC1>(B1, lb1);
+    const float *pa2 = mma_base<AC2>(A2, la2), *pb2 = mma_base<BC2>(B2, lb2);
+    const int sa1 = mma_step<AC1>(la1), sb1 = mma_step<BC1>(lb1);
+    const int sa2 = mma_step<AC2>(la2), sb2 = mma_step<BC2>(lb2);
+    float a1[R], b1[R], a2[R], b2[R];
+#pragma unroll
+    for (int s = 0; s < D; ++s) {
+        a1[s] = pa1[s * sa1];
+        b1[s] = pb1[s * sb1];
+        a2[s] = pa2[s * sa2];
+        b2[s] = pb2[s * sb2];
+    }
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+        if (s + D < S) {
+            const int r = (s + D) % R;
+            a1[r] = pa1[(s + D) * sa1];
+            b1[r] = pb1[(s + D) * sb1];
+            a2[r] = pa2[(s + D) * sa2];
+            b2[r] = pb2[(s + D) * sb2];
+        }
+        c1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1[s % R], b1[s % R], c1, 0, 0, 0);
+        c2 = __builtin_amdgcn_mfma_f32_32x32x2f32(a2[s % R], b2[s % R], c2, 0, 0, 0);
+        mma_step_fence();
+    }
+    // both chains complete here: otherwise hipcc sinks a chain whose result is
+    // only read after the tile loop (a dW accumulator) to the loop latch,
+    // behind the next barrier, with all its operands held live meanwhile
+    asm volatile("" ::"v"(c1[0]), "v"(c2[0]));
+}
+
 // row of accumulator register `reg` of the 32x32 output tile held by lane l
 __device__ __forceinline__ int acc_row(int reg, int l) { return (reg & 3) + 8 * (reg >> 2) + 4 * (l >> 5); }
 

@@ -505,10 +505,12 @@ class _GinEncoder(torch.autograd.Function):
                 jobs.append(_lib.SlabJob(slab.data_ptr(), wgrad.data_ptr(), used, nslab, width))
                 keep.append(slab)
             elif BATCH_SLABS:  # reduced together after the last layer (one launch)
-                jobs.append(_lib.SlabJob(slab.data_ptr(), wgrad.data_ptr(), width, nslab, 0))
+                ns = int(_lib.query("scgib_gin_layer_bwd_slabs", n, d_in))
+                jobs.append(_lib.SlabJob(slab.data_ptr(), wgrad.data_ptr(), width, ns, 0))
                 keep.append(slab)
             else:
-                _lib.call("scgib_slab_reduce", _p(slab), nslab, width, _p(wgrad), st)
+                ns = int(_lib.query("scgib_gin_layer_bwd_slabs", n, d_in))
+                _lib.call("scgib_slab_reduce", _p(slab), ns, width, _p(wgrad), st)
             o = HIDDEN * HIDDEN
             grads[6 * l + 2] = wgrad[:o].view(HIDDEN, HIDDEN)
             grads[6 * l + 0] = wgrad[o:o + HIDDEN * d_in].view(HIDDEN, d_in)

@@ -96,12 +96,23 @@ def layer_fwd_flops(n, e, d_in):
 
 
 def layer_bwd_bytes(n, e, d_in):
-    """Algorithmic bytes of one gin_bwd_k launch: dy, z2, r and
-    agg tiles read, W1/W2 + BN coefficients, d(agg) written, one dW/db slab
-    per workgroup written."""
-    slabs = min((n + 63) // 64, 256)
-    return (4 * n * (3 * 64 + d_in) + 4 * (64 * d_in + 64 * 64 + 6 * 64)
-            + 4 * n * d_in + 4 * slabs * (64 * 64 + 64 * d_in + 128))
+    """Algorithmic bytes of one GIN layer backward launch (gin_bwd2_k, DESIGN.md
+    §4): the dy, z2, r and agg rows read, W1/W2 + BN coefficients, d(agg)
+    written.  The per-workgroup dW slabs are NOT counted: they are partials of
+    a 33 KB gradient, not bytes the layer needs (their cost shows in
+    `traffic`)."""
+    return 4 * n * (3 * 64 + d_in) + 4 * (64 * d_in + 64 * 64 + 6 * 64) + 4 * n * d_in
+
+
+def stats_bytes(n, e, d):
+    """Algorithmic bytes of one gin_bwd_stats_k launch with the transposed
+    gather: d(agg) rows of every out-neighbour + self, col_t + rowptr_t,
+    z2 read, dy written (+ 128 floats of tile sums per 64 rows)."""
+    return 4 * d * (e + n) + 4 * e + 4 * (n + 1) + 4 * 64 * n * 2 + 512 * ((n + 63) // 64)
+
+
+def stats_flops(n, e, d):
+    return 0
 
 
 def layer_bwd_flops(n, e, d_in):
@@ -182,8 +193,16 @@ def roofline_entry(kernel, desc, r, variants):
 
 
 def superbatch_roofline(dev, n_target=1_200_000, reps=20):
-    """GIN aggregation on a ZINC-scale superbatch whose [N,64] fp32 features
-    exceed the 256 MiB Infinity Cache (north_star's >=40 % target)."""
+    """GIN gather-scatter on a ZINC-scale superbatch whose [N,64] fp32 features
+    (1.2 M nodes: 307 MB) exceed the 256 MiB Infinity Cache, so the rows come
+    from HBM (north_star's >= 40 % target).  Measured on the kernels the
+    pretrain step runs (models.py:69 GINConv gspmm is fused into them):
+    gin_fwd_k (gather + BN/ReLU of the previous layer on load + 2 GEMMs + BN
+    tile statistics, d = 64 layers) and gin_bwd_stats_k (the transposed
+    gather of d(agg) + mask + BN-backward sums) — one eager forward+backward
+    of a GIN-64x5 encoder on the superbatch, every launch HIP-event timed.
+    gin_aggregate_k (the plain aggregation, not in the replayed step) is
+    kept as a labelled reference kernel."""
     mols = pkg.synth.molecules(int(n_target / 23.2) + 1, "zinc", seed=123)
     g, _ = pkg.graph.collate_pyg(mols)
     g = g.to(dev)
@@ -200,13 +219,71 @@ def superbatch_roofline(dev, n_target=1_200_000, reps=20):
     t.record()
     torch.cuda.synchronize()
     ms = s.elapsed_time(t) / reps
-    byts = agg_bytes(n, e, 64)
-    del out, h
-    return {"nodes": n, "edges": e, "bytes": byts, "us": ms * 1e3,
-            "gbs": byts / (ms * 1e-3) / 1e9}
+    del out
+    res = {"nodes": n, "edges": e, "feature_mb": round(n * 64 * 4 / 1e6, 1),
+           "gin_aggregate_k": _frac_entry(agg_bytes(n, e, 64), ms)}
+    # the on-path kernels: a GIN-64x5 encoder forward + backward, events per launch
+    gin = pkg.models.GIN(64, 64, 5).to(dev).train()
+    x = h.requires_grad_(True)
+    torch.cuda.synchronize()
+    with KernelTimer("scgib_gin_layer_fwd_bn", "scgib_gin_bwd_stats_bn") as timer:
+        y = gin(g, x)
+        y.sum().backward()
+    fwd = timer.records["scgib_gin_layer_fwd_bn"]
+    st = [rec for rec in timer.records["scgib_gin_bwd_stats_bn"] if rec[2]["e"] > 0]
+    torch.cuda.synchronize()
+    for key, recs, fn in (("gin_fwd_k", fwd, layer_fwd_bytes), ("gin_bwd_stats_k", st, stats_bytes)):
+        if recs:
+            ms_k = statistics.mean(a.elapsed_time(b) / KernelTimer.REPEAT for a, b, _ in recs)
+            m = recs[0][2]
+            res[key] = _frac_entry(fn(m["n"], m["e"], m["d_in"]), ms_k)
+            res[key]["launches"] = len(recs)
+    del y, x, h, gin
+    return res
 
 
-def cpu_baseline(pool_host, k, gin_layers, F_in, seconds=20.0):
+def _frac_entry(byts, ms):
+    gbs = byts / (ms * 1e-3) / 1e9
+    return {"bytes": int(byts), "us": round(ms * 1e3, 2), "achieved_gbs": round(gbs, 1),
+            "frac": round(gbs / HBM_PEAK_GBS, 4),
+            "frac_vs_measured_copy": round(gbs / HBM_MEASURED_GBS, 4)}
+
+
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as fh:
+            for line in fh:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baselines(pool_host, k, gin_layers, F_in, seconds=20.0):
+    """the CPU path at all the cores this process may use and
+    at 1 core, with the CPU model, nproc and torch.get_num_threads()."""
+    threads = torch.get_num_threads()
+    allc = cpu_baseline(pool_host, k, gin_layers, F_in, seconds, warmup=3, min_steps=10)
+    torch.set_num_threads(1)
+    try:
+        one = cpu_baseline(pool_host, k, gin_layers, F_in, seconds, warmup=1, min_steps=3)
+    finally:
+        torch.set_num_threads(threads)
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except AttributeError:
+        affinity = None
+    out = dict(allc)
+    out.update({"cores": threads, "value_1core": one["value"],
+                "ms_per_step_1core": one["ms_per_step"], "cpu_model": cpu_model(),
+                "nproc": os.cpu_count(), "sched_affinity_cpus": affinity,
+                "torch_num_threads": threads,
+                "sample": allc["sample"] + f"; 1-core run: {one['steps']} steps after 1 warm-up"})
+    return out
+
+
+def cpu_baseline(pool_host, k, gin_layers, F_in, seconds=20.0, warmup=1, min_steps=2):
     """The oracle (literal restatement of the reference's CPU path: per-graph
     loops, dense N x N recon) timed on this host's cores, bounded sample."""
     from oracle import egonet
@@ -226,7 +303,7 @@ def cpu_baseline(pool_host, k, gin_layers, F_in, seconds=20.0):
     times, ego_times = [], []
     t_end = time.perf_counter() + seconds
     i = 0
-    while time.perf_counter() < t_end or i < 2:
+    while time.perf_counter() < t_end or i < warmup + min_steps:
         gh = pool_host[i % len(pool_host)]
         t0 = time.perf_counter()
         sizes, ecount, nodes, esrc, edst = egonet.egonets(gh.rowptr.numpy(), gh.col.numpy(), k)
@@ -246,7 +323,7 @@ def cpu_baseline(pool_host, k, gin_layers, F_in, seconds=20.0):
         out["loss_total"].backward()
         opt.step()
         t3 = time.perf_counter()
-        if i > 0:  # first step is warm-up
+        if i >= warmup:
             times.append(t3 - t2)
             ego_times.append(t1 - t0)
         i += 1
@@ -256,14 +333,17 @@ def cpu_baseline(pool_host, k, gin_layers, F_in, seconds=20.0):
             "kind": "port",
             "sample": (f"oracle/scgib_ref.py pretrain step (fwd+bwd+Adam, dense NxN recon, "
                        f"per-graph loops) on {B}-molecule QM9-like batches, median of "
-                       f"{len(times)} steps after 1 warm-up, torch CPU threads="
+                       f"{len(times)} steps after {warmup} warm-up, torch CPU threads="
                        f"{torch.get_num_threads()}, os.cpu_count={os.cpu_count()}; ego-nets "
                        f"pre-extracted as in the reference (oracle/egonet_ref.c, "
                        f"{statistics.median(ego_times) * 1e3:.1f} ms/batch, not in value)"),
-            "ms_per_step": round(step * 1e3, 2)}
+            "ms_per_step": round(step * 1e3, 2), "steps": len(times)}
 
 
 SUM_LOSS = os.environ.get("SCGIB_BENCH_SUM_LOSS", "0") != "0"
+# N > 1: capture the RCCL all-reduce inside the replayed step graph (falls back
+# to all-reduce between two replays if the capture raises)
+GRAPH_ALLREDUCE = os.environ.get("SCGIB_GRAPH_ALLREDUCE", "1") != "0"
 
 
 def main():
@@ -272,7 +352,14 @@ def main():
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--workload", default="qm9")
-    ap.add_argument("--batch", type=int, default=512)
+    ap.add_argument("--batch", type=int, default=512,
+                    help="molecules per GPU (weak scaling: per-GPU work fixed as N grows)")
+    ap.add_argument("--global-batch", type=int, default=0,
+                    help="strong scaling: this many molecules per step in total, "
+                         "split evenly over the ranks (BASELINE.md §3: 1024 = 128/rank at 8)")
+    ap.add_argument("--force-allreduce", action="store_true",
+                    help="run the gradient all-reduce (and its graph capture) even at N=1 "
+                         "(a 1-rank process group; exercises the collective path on one GPU)")
     ap.add_argument("--k", type=int, default=1)
     ap.add_argument("--gin-layers", type=int, default=5)
     ap.add_argument("--pool", type=int, default=8)
@@ -292,6 +379,17 @@ def main():
     # rocBLAS is ~2-3x faster on them.  (Process-wide torch setting.)
     torch.backends.cuda.preferred_blas_library("cublas")
     rank, world, local = pkg.dist.init_from_env()
+    if a.force_allreduce and world == 1 and not dist.is_initialized():
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29531")
+        torch.cuda.set_device(local)
+        dist.init_process_group(os.environ.get("SCGIB_DIST_BACKEND") or "nccl",
+                                rank=0, world_size=1)
+    collective = world > 1 or a.force_allreduce
+    if a.global_batch:
+        if a.global_batch % world:
+            raise SystemExit(f"--global-batch {a.global_batch} is not a multiple of {world} ranks")
+        a.batch = a.global_batch // world
     # (more ranks than devices only in local gloo rehearsals: ranks share GPUs)
     dev = torch.device("cuda", local % max(torch.cuda.device_count(), 1))
     torch.cuda.set_device(dev)
@@ -309,7 +407,8 @@ def main():
         pool.append(g)
 
     model = make_model(F_in, a.k, a.gin_layers, dev)
-    reducer = pkg.dist.GradAllReducer(model.parameters())
+    # gradients + the BN running statistics, averaged in one bucket per step
+    reducer = pkg.dist.GradAllReducer(model.parameters(), buffers=pkg.dist.bn_buffers(model))
 
     if a.eager:
         opt = (torch.optim.Adam(model.parameters(), lr=1e-4, weight_decay=5e-5, fused=True)
@@ -321,7 +420,10 @@ def main():
             _, kl, con, rec = model(g, g.ndata["x"], None, None, None, 1, None, a.k, dev, a.batch)
             loss = kl + rec + con
             loss.backward()
-            reducer()
+            if collective:
+                reducer.pack()
+                reducer.reduce(force=True)
+                reducer.unpack()
             opt.step()
             return loss
     else:
@@ -360,33 +462,60 @@ def main():
 
         side = torch.cuda.Stream()
         side.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(side):  # warm-up (allocator, Adam state) off the capture
+        with torch.cuda.stream(side):  # warm-up (allocator, Adam state, RCCL comm) off the capture
             for i in range(3):
                 static.load(padded[i % len(padded)])
                 opt.zero_grad(set_to_none=True)
                 body()
-                reducer()
+                if collective:
+                    reducer.pack()
+                    reducer.reduce(force=True)
+                    reducer.unpack()
                 opt.step()
         torch.cuda.current_stream().wait_stream(side)
+        torch.cuda.synchronize()
+        graph2 = None
         graph = torch.cuda.CUDAGraph()
         opt.zero_grad(set_to_none=True)
-        with torch.cuda.graph(graph):
-            static_loss = body()
-            if world == 1:
+        capture_ok = GRAPH_ALLREDUCE and dist.is_initialized() and dist.get_backend() == "nccl"
+        if collective and capture_ok:  # (gloo's all-reduce is a host round trip: not capturable)
+            # the whole step incl. the RCCL all-reduce of the bucket in ONE graph:
+            # no host enqueue between the backward and the optimizer step
+            try:
+                with torch.cuda.graph(graph):
+                    static_loss = body()
+                    reducer.pack()
+                    reducer.reduce(force=True)
+                    reducer.unpack()
+                    opt.step()
+                allreduce_mode = "captured in the step graph"
+            except Exception as exc:  # RCCL without graph-capture support: two graphs
+                print(f"bench: all-reduce capture failed ({exc!r}); two-graph fallback",
+                      file=sys.stderr, flush=True)
+                torch.cuda.synchronize()
+                graph = torch.cuda.CUDAGraph()
+                opt.zero_grad(set_to_none=True)
+                graph2 = "fallback"
+        if not collective:
+            with torch.cuda.graph(graph):
+                static_loss = body()
                 opt.step()
-            else:  # gradients -> the flat all-reduce bucket, one launch
+            allreduce_mode = None
+        elif graph2 is not None or not capture_ok:
+            with torch.cuda.graph(graph):  # gradients -> the flat bucket, one launch
+                static_loss = body()
                 reducer.pack()
-        if world > 1:  # 1/world unpack + Adam, replayed after the all-reduce
-            graph2 = torch.cuda.CUDAGraph()
+            graph2 = torch.cuda.CUDAGraph()  # 1/world unpack + Adam, after the all-reduce
             with torch.cuda.graph(graph2):
                 reducer.unpack()
                 opt.step()
+            allreduce_mode = "between two graph replays"
 
         def step(i):
             static.load(padded[i % len(padded)])
             graph.replay()
-            if world > 1:  # RCCL all-reduce of the bucket between the two replays
-                reducer.reduce()
+            if graph2 is not None:  # RCCL all-reduce of the bucket between the two replays
+                reducer.reduce(force=True)
                 graph2.replay()
             return static_loss
 
@@ -433,7 +562,7 @@ def main():
     sb = None if a.no_superbatch or rank != 0 else superbatch_roofline(dev)
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
-        cpu = cpu_baseline(pool_host[:2], a.k, a.gin_layers, F_in, a.cpu_seconds)
+        cpu = cpu_baselines(pool_host[:2], a.k, a.gin_layers, F_in, a.cpu_seconds)
 
     if rank == 0:
         total_graphs = world * a.batch * a.steps
@@ -447,29 +576,32 @@ def main():
             "warmup": a.warmup,
             "ms_per_step": round(elapsed / a.steps * 1e3, 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if a.global_batch else "weak",
             "vs_baseline": None,
             "dtype": "fp32",
             "data": "synthetic (seeded QM9-like molecules, SURVEY.md §8(d)); random-init weights",
             "config": {"workload": f"{a.workload} pretrain step GIN-64x{a.gin_layers} "
                                    f"k={a.k}, batch {a.batch}/GPU, Mainmodel_continue + Adam",
                        "launch": "eager" if a.eager else "hip-graph replay (capacity mode)",
+                       "allreduce": None if not collective else
+                       ("eager" if a.eager else allreduce_mode),
                        "global_batch": world * a.batch, "nodes_per_batch": round(n_nodes, 1),
                        "parallelism": f"dp{world}", "final_loss": round(final_loss, 4)},
             # dominant kernel by total time per step (profiles/): gin_bwd_k
-            "roofline": None if r_bwd is None else roofline_entry("gin_bwd_k", "fused GIN layer backward: BN-backward "
-                                       "apply + 4 f32-MFMA GEMMs + dW slabs", r_bwd,
-                                       ["gin_bwd_k<32, true,", "gin_bwd_k<64, true,"]),
+            "roofline": None if r_bwd is None else roofline_entry("gin_bwd2_k", "fused GIN layer backward: BN-backward "
+                                       "apply + 4 f32-MFMA GEMMs, one workgroup per CU walking its tiles", r_bwd,
+                                       ["gin_bwd2_k<64>"]),
             "roofline_gin_fwd": None if r_fwd is None else roofline_entry("gin_fwd_k", "fused GIN layer: gather + 2 "
                                                "f32-MFMA GEMMs + BN tile stats", r_fwd,
                                                ["gin_fwd_k<32, false, true,",
                                                 "gin_fwd_k<64, true, true,",
                                                 "gin_fwd_k<64, false, true,"]),
-            "roofline_superbatch": None if sb is None else {
-                "bound": "hbm", "kernel": "gin_aggregate_k d=64", "nodes": sb["nodes"],
-                "edges": sb["edges"], "achieved": round(sb["gbs"], 1), "peak": HBM_PEAK_GBS,
-                "unit": "GB/s", "frac": round(sb["gbs"] / HBM_PEAK_GBS, 4),
-                "avg_launch_us": round(sb["us"], 2)},
+            "roofline_superbatch": None if sb is None else dict(
+                sb, bound="hbm", peak=HBM_PEAK_GBS, unit="GB/s",
+                note="ZINC-like superbatch, [N,64] fp32 > 256 MiB Infinity Cache; frac = "
+                     "algorithmic bytes / launch time / 8.0 TB/s (north_star target >= 0.40 on "
+                     "the on-path gather kernels gin_fwd_k and gin_bwd_stats_k; "
+                     "gin_aggregate_k is a reference kernel, not in the step)"),
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)

@@ -39,8 +39,8 @@ def init_from_env(backend=None):
 
 
 class GradAllReducer:
-    """Averages the gradients of every parameter that received one, in one
-    flat all-reduce (SUM / world).  The set of parameters with gradients is
+    """Averages the gradients of every parameter that received one (and the
+    given float buffers), in one flat all-reduce (SUM / world).  The set of parameters with gradients is
     the same on every rank (same model, same path).
 
     HIP tensors: the gradients are packed into the flat bucket by ONE launch
@@ -51,8 +51,13 @@ class GradAllReducer:
     the RCCL all-reduce runs between the two replays.  CPU tensors (the gloo
     tests) take per-tensor copies."""
 
-    def __init__(self, params, group=None):
+    def __init__(self, params, group=None, buffers=()):
         self.params = [p for p in params if p.requires_grad]
+        # float buffers averaged with the gradients (BatchNorm running
+        # statistics, ``bn_buffers``): every replica then holds the same
+        # statistics after each step, so eval and a saved checkpoint do not
+        # depend on which rank wrote them
+        self.buffers = [b for b in buffers if b.dtype == torch.float32]
         self.group = group
         self._flat = None
 
@@ -62,7 +67,7 @@ class GradAllReducer:
         return dist.get_world_size(self.group)
 
     def _grads(self):
-        return [p.grad for p in self.params if p.grad is not None]
+        return [p.grad for p in self.params if p.grad is not None] + self.buffers
 
     def _buffer(self, grads):
         numel = sum(g.numel() for g in grads)
@@ -109,9 +114,12 @@ class GradAllReducer:
             return
         self._launch("scgib_grad_pack", grads)
 
-    def reduce(self):
-        """All-reduce (SUM) of the flat bucket over the group."""
-        if self._flat is not None and self._world() > 1:
+    def reduce(self, force=False):
+        """All-reduce (SUM) of the flat bucket over the group (``force``: also
+        over a 1-rank group, to exercise the collective path on one GPU)."""
+        if self._flat is None:
+            return
+        if self._world() > 1 or (force and dist.is_initialized()):
             dist.all_reduce(self._flat, op=dist.ReduceOp.SUM, group=self.group)
 
     def unpack(self):
@@ -134,6 +142,13 @@ class GradAllReducer:
         self.pack()
         self.reduce()
         self.unpack()
+
+
+def bn_buffers(model):
+    """The BatchNorm running means / variances of ``model`` (float buffers the
+    replicas average each step; num_batches_tracked is equal on every rank)."""
+    return [b for name, b in model.named_buffers()
+            if name.endswith(("running_mean", "running_var"))]
 
 
 def shard(items, rank, world):

@@ -454,16 +454,17 @@ class _GinEncoder(torch.autograd.Function):
             # dy, tile sums and the BN-backward finalize in one launch
             if dagg_next is None and g_readout is not None:
                 # the readout's broadcast backward folded into the last layer
-                _launch("scgib_gin_bwd_stats_seg_bn", {"n": n}, _p(g_out), _p(g_readout),
+                _launch("scgib_gin_bwd_stats_seg_bn", {"n": n, "e": 0, "d_in": HIDDEN}, _p(g_out), _p(g_readout),
                         _p(ctx.seg), _p(z2), _p(stat), n, int(ctx.training), _p(dy),
                         _p(bn_g[0]), _p(bn_g[1]), _p(coef), _p(bn_ws), _p(cnt), _p(gr.dims),
                         defer, st)
             elif dagg_next is None:
-                _launch("scgib_gin_bwd_stats_bn", {"n": n}, _p(g_out), None, None, 1.0, _p(z2),
+                _launch("scgib_gin_bwd_stats_bn", {"n": n, "e": 0, "d_in": HIDDEN}, _p(g_out), None, None, 1.0, _p(z2),
                           _p(stat), n, int(ctx.training), _p(dy), _p(bn_g[0]), _p(bn_g[1]),
                           _p(coef), _p(bn_ws), _p(cnt), _p(gr.dims), defer, st)
             else:
-                _launch("scgib_gin_bwd_stats_bn", {"n": n}, _p(dagg_next), _p(gr.rowptr_t),
+                _launch("scgib_gin_bwd_stats_bn", {"n": n, "e": gr.edge_capacity(), "d_in": HIDDEN},
+                        _p(dagg_next), _p(gr.rowptr_t),
                           _p(gr.col_t), ctx.opes[l + 1], _p(z2), _p(stat), n, int(ctx.training),
                           _p(dy), _p(bn_g[0]), _p(bn_g[1]), _p(coef), _p(bn_ws), _p(cnt),
                           _p(gr.dims), defer, st)

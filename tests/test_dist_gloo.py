@@ -26,7 +26,7 @@ def _free_port():
     return p
 
 
-def _shard_grads(molecules, seed):
+def _shard_grads(molecules, seed, buffers=None):
     """Oracle pretrain-step gradients for one shard of molecules."""
     import importlib
     sys.path.insert(0, ROOT)
@@ -51,9 +51,12 @@ def _shard_grads(molecules, seed):
                                                    and not k.endswith(".eps"))
               for k, v in model.state_dict().items()}
     gen = torch.Generator().manual_seed(seed)
+    if buffers is not None:  # BN running statistics, updated by this step
+        buffers.update({k: v.detach().clone() for k, v in params.items()
+                        if "running" in k or "num_batches" in k})
     out = R.pretrain_forward(params, batch, ego, x, x[torch.from_numpy(nodes)],
                              torch.rand(len(x), generator=gen), torch.rand(len(x), 64, generator=gen),
-                             64)
+                             64, buffers)
     out["loss_total"].backward()
     return {k: v.grad.clone() for k, v in params.items() if v.grad is not None}, params
 
@@ -107,3 +110,52 @@ def test_shard_covers_everything_once(pkg):
     parts = [pkg.dist.shard(items, r, 8) for r in range(8)]
     assert sum(parts, []) == items
     assert max(map(len, parts)) - min(map(len, parts)) <= 1
+
+
+def _buffer_worker(rank, world, port, molecules, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    sys.path.insert(0, ROOT)
+    import importlib
+    pkg = importlib.import_module("s-cgib_amd")
+    r, w, _ = pkg.dist.init_from_env(backend="gloo")
+    bufs = {}
+    _, params = _shard_grads(pkg.dist.shard(molecules, r, w), seed=100 + r, buffers=bufs)
+    holder = [p for p in params.values() if p.requires_grad]
+    running = [v for k, v in sorted(bufs.items()) if "running" in k]
+    pkg.dist.GradAllReducer(holder, buffers=running)()
+    out = {k: v.numpy().copy() for k, v in bufs.items() if "running" in k}
+    q.put((r, out))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_bn_buffers_identical_across_ranks(pkg):
+    """With the BN running statistics in the gradient bucket (GradAllReducer
+    buffers=), every rank holds the same statistics after each step — their
+    mean over the ranks' shards."""
+    mols = pkg.synth.molecules(12, "qm9", seed=22)
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_buffer_worker, args=(r, world, port, mols, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=240) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert set(got[0]) == set(got[1]) and len(got[0]) > 0
+    expect = {}
+    for r in range(world):
+        bufs = {}
+        _shard_grads(pkg.dist.shard(mols, r, world), seed=100 + r, buffers=bufs)
+        for k, v in bufs.items():
+            if "running" in k:
+                expect[k] = expect.get(k, 0) + v / world
+    for k in got[0]:
+        np.testing.assert_array_equal(got[0][k], got[1][k], err_msg=k)
+        assert torch.allclose(torch.from_numpy(got[0][k]), expect[k], rtol=1e-6, atol=1e-7), k

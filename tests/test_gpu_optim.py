@@ -144,10 +144,12 @@ def test_grad_pack_unpack_roundtrip(pkg):
     assert torch.equal(torch.cat([p.grad.reshape(-1) for p in params]), 4.0 * ref)
 
 
-def test_bench_two_ranks_gloo_on_one_gpu(tmp_path):
+@pytest.mark.parametrize("strong", [False, True])
+def test_bench_two_ranks_gloo_on_one_gpu(tmp_path, strong):
     """The N > 1 bench path (captured backward + bucket pack, all-reduce
     between replays, captured unpack + Adam) end to end with two ranks on one
-    GPU over gloo (the driver's 8-GPU runs use RCCL)."""
+    GPU over gloo (the driver's 8-GPU runs use RCCL), weak (64/rank) and
+    strong (--global-batch 128 split over the ranks) scaling."""
     import json
     import os
     import subprocess
@@ -156,11 +158,34 @@ def test_bench_two_ranks_gloo_on_one_gpu(tmp_path):
     env = dict(os.environ, SCGIB_DIST_BACKEND="gloo", MASTER_ADDR="127.0.0.1")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
            "--master-addr=127.0.0.1", "--master-port=29533", os.path.join(root, "bench.py"),
-           "--gpus", "2", "--steps", "4", "--warmup", "2", "--batch", "64", "--pool", "2",
+           "--gpus", "2", "--steps", "4", "--warmup", "2", "--pool", "2",
            "--no-cpu-baseline", "--no-superbatch", "--no-kernel-timer"]
+    cmd += ["--global-batch", "128"] if strong else ["--batch", "64"]
     out = subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=240)
     assert out.returncode == 0, out.stderr[-3000:]
     line = json.loads(out.stdout.strip().splitlines()[-1])
     assert line["n_gpus"] == 2 and line["value"] > 0
     assert line["config"]["parallelism"] == "dp2" and line["config"]["global_batch"] == 128
+    assert line["scaling"] == ("strong" if strong else "weak")
+    assert line["config"]["allreduce"] == "between two graph replays"
     assert line["config"]["final_loss"] == line["config"]["final_loss"]  # finite (not NaN)
+
+
+def test_bench_allreduce_captured_one_rank_rccl():
+    """The RCCL all-reduce of the gradient + BN-statistics bucket captured
+    inside the replayed step graph (the N > 1 default), exercised on one GPU
+    through a 1-rank nccl (RCCL) group: the capture succeeds and the step runs."""
+    import json
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT="29541")
+    cmd = [sys.executable, os.path.join(root, "bench.py"), "--force-allreduce", "--steps", "6",
+           "--warmup", "2", "--batch", "64", "--pool", "2", "--no-cpu-baseline",
+           "--no-superbatch", "--no-kernel-timer"]
+    out = subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=240)
+    assert out.returncode == 0, out.stderr[-3000:]
+    line = json.loads(out.stdout.strip().splitlines()[-1])
+    assert line["config"]["allreduce"] == "captured in the step graph", out.stderr[-2000:]
+    assert line["value"] > 0 and line["config"]["final_loss"] == line["config"]["final_loss"]

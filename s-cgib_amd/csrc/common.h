@@ -121,18 +121,23 @@ int launch_recon_fin(const float *gslab, const float *im, const int32_t *rowptr,
 
 // Phase tracing (debug build only, `make trace` -> libscgib_trace.so):
 // thread 0 of each workgroup stamps the 100 MHz wall clock at phase marks
-// into g_trace[block * 16 + k]; slot 15 holds (XCC_ID << 32) | HW_ID.
+// into g_trace[block * 32 + k] and the shader clock (s_memtime) into
+// g_trace[block * 32 + 16 + k] (their ratio: the clock the CU held over a
+// phase); slot 15 holds (XCC_ID << 32) | HW_ID.
 #ifdef SCGIB_TRACE
 static __device__ unsigned long long *g_trace;
 #define SCGIB_MARK(k)                                                                     \
     do {                                                                                  \
-        if (threadIdx.x == 0 && g_trace)                                                  \
-            g_trace[static_cast<uint64_t>(blockIdx.x) * 16 + (k)] = wall_clock64();        \
+        if (threadIdx.x == 0 && g_trace) {                                                \
+            g_trace[static_cast<uint64_t>(blockIdx.x) * 32 + (k)] = wall_clock64();        \
+            g_trace[static_cast<uint64_t>(blockIdx.x) * 32 + 16 + (k)] =                   \
+                __builtin_amdgcn_s_memtime();                                             \
+        }                                                                                 \
     } while (0)
 #define SCGIB_MARK_HWID()                                                                 \
     do {                                                                                  \
         if (threadIdx.x == 0 && g_trace)                                                  \
-            g_trace[static_cast<uint64_t>(blockIdx.x) * 16 + 15] =                          \
+            g_trace[static_cast<uint64_t>(blockIdx.x) * 32 + 15] =                          \
                 (static_cast<unsigned long long>(__builtin_amdgcn_s_getreg((31 << 11) | 20)) << 32) | \
                 static_cast<unsigned>(__builtin_amdgcn_s_getreg((31 << 11) | 4));         \
     } while (0)

@@ -98,7 +98,7 @@ __global__ __launch_bounds__(256) void linear_bwd_k(
         }
         __syncthreads();
         accW = mma_tn<TM>(sD + wr * 32, LDH, sA + wc * 32, LDH, accW);
-        for (int rr = q; rr < TM; rr += 4) db += sD[rr * LDH + ch];
+        db = col_sum16(db, sD + q * LDH + ch, 4 * LDH);
         f32x16 g = mma_nn<64>(sD + wr * 32 * LDH, LDH, sW + wc * 32, LDH, zero16());
         const int ccol = wc * 32 + (l & 31);
 #pragma unroll

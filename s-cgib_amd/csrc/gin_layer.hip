@@ -1190,7 +1190,7 @@ __global__ __launch_bounds__(256, (DIN <= 64 && !RECON ? SCGIB_BWD_MINB : 1)) vo
         f32x16 dr = zero16();
         mma_pf2<64, true, true, false, true>(sD + wr * 32, LDH, sR + wc * 32, LDH, accW2,
                                              sD + wr * 32 * LDH, LDH, sW2 + wc * 32, LDH, dr);
-        for (int rr = q; rr < TM; rr += 4) db2 += sD[rr * LDH + ch];
+        db2 = col_sum16(db2, sD + q * LDH + ch, 4 * LDH);
         __syncthreads();  // all reads of dz2 done
         // dz1 = dr * [r > 0]  -> sD
 #pragma unroll
@@ -1208,7 +1208,7 @@ __global__ __launch_bounds__(256, (DIN <= 64 && !RECON ? SCGIB_BWD_MINB : 1)) vo
         }
         if (PIPE && next < ntiles) load_agg(next);
         __syncthreads();
-        for (int rr = q; rr < TM; rr += 4) db1 += sD[rr * LDH + ch];
+        db1 = col_sum16(db1, sD + q * LDH + ch, 4 * LDH);
         // dW1 += dz1^T agg  (64 x DIN) ; d(agg) = dz1 W1  (TM x DIN)
 #pragma unroll
         for (int q1 = 0; q1 < NW1; ++q1) {
@@ -1353,11 +1353,9 @@ __global__ __launch_bounds__(256, 1) void gin_bwd2_k(
     __shared__ __attribute__((aligned(16))) float sA[TM * DIN];
     __shared__ float sD[TM * LDD];
     __shared__ float sCoef[128];
-    __shared__ float sB[2][4][64];
     const int64_t n = eff_count(dims, 0, ncap);
     const int tid = threadIdx.x, l = tid & 63, w = tid >> 6;
     const int wr = w >> 1, wc = w & 1;
-    const int ch = tid & 63, q = tid >> 6;    // column-sum roles: channel, row quarter
     const int c4 = tid & 15, rs = tid >> 4;   // elementwise roles: chunk c4, rows rs + 16 k
     const int64_t last = ncap - 1;            // last row of the allocations
     const unsigned gsz = gridDim.x;
@@ -1446,10 +1444,11 @@ __global__ __launch_bounds__(256, 1) void gin_bwd2_k(
         }
         if (tile == blockIdx.x) SCGIB_MARK(1);
         // dW2 += dz2^T r ; dr = dz2 W2  (rows wr, cols wc), the two products alternating
+        // (db2: column sums of dz2 from the TN product's A operand, waves wc == 0)
         f32x16 dr = zero16();
         mma_pf2<64, true, true, false, true>(sD + wr * 32, LDD, sR + wc * 32, 64, accW2,
-                                             sD + wr * 32 * LDD, LDD, sW2 + wc * 32, 64, dr);
-        for (int rr = q; rr < TM; rr += 4) db2 += sD[rr * LDD + ch];
+                                             sD + wr * 32 * LDD, LDD, sW2 + wc * 32, 64, dr, &db2);
+        if (tile == blockIdx.x) SCGIB_MARK(6);
         lds_barrier();  // all reads of dz2 done
         // dz1 = dr * [r > 0]  -> sD
 #pragma unroll
@@ -1459,19 +1458,29 @@ __global__ __launch_bounds__(256, 1) void gin_bwd2_k(
         }
         lds_barrier();  // dz1 complete; r consumed
         if (tile == blockIdx.x) SCGIB_MARK(2);
-        for (int rr = q; rr < TM; rr += 4) db1 += sD[rr * LDD + ch];
         // dW1 += dz1^T agg (64 x DIN) ; d(agg) = dz1 W1 (TM x DIN): wave w owns
-        // sub-tile (jb, kb) = (w & 1, w >> 1) of both
+        // sub-tile (jb, kb) = (w & 1, w >> 1) of both (db1: waves kb == 0)
         {
             const int jb = w & 1, kb = w >> 1;
             f32x16 da = zero16();
             mma_pf2<64, true, true, false, true>(sD + jb * 32, LDD, sA + kb * 32, DIN, accW1,
-                                                 sD + jb * 32 * LDD, LDD, sW1 + kb * 32, DIN, da);
+                                                 sD + jb * 32 * LDD, LDD, sW1 + kb * 32, DIN, da,
+                                                 &db1);
+            if (tile == blockIdx.x) SCGIB_MARK(7);
+            // d(agg) through LDS (sDY: consumed, refilled only after the next
+            // barrier) -> full-row float4 stores instead of 16 predicated
+            // dword stores per lane
 #pragma unroll
-            for (int reg = 0; reg < 16; ++reg) {
-                const int row = jb * 32 + acc_row(reg, l);
-                if (row < nv) dagg_out[(row0 + row) * DIN + kb * 32 + (l & 31)] = da[reg];
-            }
+            for (int reg = 0; reg < 16; ++reg)
+                sDY[(jb * 32 + acc_row(reg, l)) * DIN + kb * 32 + (l & 31)] = da[reg];
+        }
+        lds_barrier();
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int rr = rs + 16 * k;
+            if (rr < nv)
+                st4(dagg_out + (row0 + rr) * DIN + 4 * c4,
+                    *reinterpret_cast<const float4 *>(sDY + rr * DIN + 4 * c4));
         }
         if (tile == blockIdx.x) SCGIB_MARK(3);
         if (more) {
@@ -1499,14 +1508,12 @@ __global__ __launch_bounds__(256, 1) void gin_bwd2_k(
             sl[64 * 64 + j * DIN + kk] = accW1[reg];
         }
     }
-    sB[0][q][ch] = db2;
-    sB[1][q][ch] = db1;
-    __syncthreads();
-    if (tid < 128) {
-        const int which = tid >> 6;
-        sl[64 * 64 + 64 * DIN + which * 64 + ch] =
-            ((sB[which][0][ch] + sB[which][1][ch]) + sB[which][2][ch]) + sB[which][3][ch];
-    }
+    // bias gradients: lane l < 32 of the owning waves holds its column's two
+    // row halves (kk = 0 here, kk = 1 in lane l + 32)
+    db2 += __shfl_xor(db2, 32, kWave);
+    db1 += __shfl_xor(db1, 32, kWave);
+    if (wc == 0 && l < 32) sl[64 * 64 + 64 * DIN + wr * 32 + l] = db2;
+    if ((w >> 1) == 0 && l < 32) sl[64 * 64 + 64 * DIN + 64 + (w & 1) * 32 + l] = db1;
     SCGIB_MARK(4);
 }
 

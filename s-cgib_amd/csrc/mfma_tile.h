@@ -275,11 +275,15 @@ __device__ __forceinline__ f32x16 mma_pf(const float *As, int lda, const float *
     return acc;
 }
 
-// two independent products over the same K, MFMAs alternating
+// two independent products over the same K, MFMAs alternating.  asum (if
+// given) accumulates this lane's A1 operand values over k: for a TN first
+// product (A1 = a tile read by column) that is the column's sum over the
+// lane's half of the rows — the bias gradient, free beside the MFMAs
+// (add the xor-32 partner lane's value for the full column).
 template <int K, bool AC1, bool BC1, bool AC2, bool BC2, int D = 3>
 __device__ __forceinline__ void mma_pf2(const float *A1, int la1, const float *B1, int lb1,
                                         f32x16 &c1, const float *A2, int la2, const float *B2,
-                                        int lb2, f32x16 &c2) {
+                                        int lb2, f32x16 &c2, float *asum = nullptr) {
     constexpr int S = K / 2, R = D + 1;
     const float *pa1 = mma_base<AC1>(A1, la1), *pb1 = mma_base<BC1>(B1, lb1);
     const float *pa2 = mma_base<AC2>(A2, la2), *pb2 = mma_base<BC2>(B2, lb2);
@@ -303,6 +307,7 @@ __device__ __forceinline__ void mma_pf2(const float *A1, int la1, const float *B
             b2[r] = pb2[(s + D) * sb2];
         }
         c1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1[s % R], b1[s % R], c1, 0, 0, 0);
+        if (asum) *asum += a1[s % R];
         c2 = __builtin_amdgcn_mfma_f32_32x32x2f32(a2[s % R], b2[s % R], c2, 0, 0, 0);
         mma_step_fence();
     }
@@ -310,6 +315,19 @@ __device__ __forceinline__ void mma_pf2(const float *A1, int la1, const float *B
     // only read after the tile loop (a dW accumulator) to the loop latch,
     // behind the next barrier, with all its operands held live meanwhile
     asm volatile("" ::"v"(c1[0]), "v"(c2[0]));
+}
+
+// acc + p[0] + p[stride] + ... + p[15 stride], added in that order: the 16
+// LDS reads go out together (a loop over a runtime start row is not unrolled
+// by hipcc and pays one LDS round trip per row — ~2k cycles per call, phase
+// trace r02)
+__device__ __forceinline__ float col_sum16(float acc, const float *p, int stride) {
+    float v[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) v[k] = p[k * stride];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) acc += v[k];
+    return acc;
 }
 
 // row of accumulator register `reg` of the 32x32 output tile held by lane l

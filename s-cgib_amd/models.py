@@ -160,7 +160,7 @@ def _side_stream(device):
     """The second HIP stream of ``device`` used by the forked encoder branch."""
     key = torch.device(device).index
     if key not in _SIDE_STREAMS:
-        _SIDE_STREAMS[key] = torch.cuda.Stream(device)
+        _SIDE_STREAMS[key] = ops.register_fork_stream(torch.cuda.Stream(device))
     return _SIDE_STREAMS[key]
 
 
@@ -253,6 +253,8 @@ class _SCGIBCore(nn.Module):
         fold = (enc_owner.Encoder1.fused and enc_owner.Encoder2.fused
                 and self.transfer_d.bias is None and self.transfer_d.out_features == 32
                 and batch_x.shape[1] <= 16 and not batch_x.requires_grad)
+        if fork:
+            ops.check_fork(main)  # never a nested fork while capturing (ops.check_fork)
         side.wait_stream(main)
         batch_x.record_stream(side)
         if fold and fork and PAIR_ENCODERS:
@@ -299,6 +301,7 @@ class _SCGIBCore(nn.Module):
         side = _side_stream(im.device) if (FORK_LOSSES and im.is_cuda) else None
         if side is not None:
             main = torch.cuda.current_stream(im.device)
+            ops.check_fork(main)
             side.wait_stream(main)
             z1.record_stream(side)
             z2.record_stream(side)

@@ -100,11 +100,37 @@ def aside_deferred():
         _DEFER_DEPTH[0] -= 1
 
 
+# The library's forked streams (models' side stream, the aux stream above).
+# A fork taken FROM one of them while a HIP graph is being captured nests
+# forks; torch-ROCm's CUDAGraph::capture_end segfaults on any nested fork,
+# even one with no work or allocation on the inner stream, while the same
+# sequence of HIP stream/event calls captures, instantiates and replays in
+# plain HIP (tools/capture_probe.py, tools/nested_torch_repro.py,
+# tools/nested_capture_repro.hip).  check_fork() refuses it with an error
+# instead of the crash at the end of the capture.
+_FORK_STREAMS = set()
+
+
+def register_fork_stream(stream):
+    _FORK_STREAMS.add((stream.device_index, stream.stream_id))
+    return stream
+
+
+def check_fork(src):
+    """Raise if a fork from ``src`` would nest forks inside a HIP-graph capture."""
+    if (src.device_index, src.stream_id) in _FORK_STREAMS and \
+            torch.cuda.is_current_stream_capturing():
+        raise RuntimeError(
+            "stream fork from an already-forked stream during HIP-graph capture: "
+            "torch-ROCm's capture_end crashes on nested forks (DESIGN.md §3); fork from the "
+            "capture's origin stream instead")
+
+
 def _aux_stream(device):
     key = device.index
     aux = _AUX_STREAMS.get(key)
     if aux is None:
-        aux = _AUX_STREAMS[key] = torch.cuda.Stream(device)
+        aux = _AUX_STREAMS[key] = register_fork_stream(torch.cuda.Stream(device))
     return key, aux
 
 
@@ -118,6 +144,7 @@ def launch_aside(fn, *tensors):
         fn()
         return
     main = torch.cuda.current_stream()
+    check_fork(main)
     key, aux = _aux_stream(main.device)
     if LATE_FORK:
         ev = torch.cuda.Event()
@@ -586,6 +613,7 @@ class _GinEncoderPair(torch.autograd.Function):
         ctx.set_materialize_grads(False)  # unused outputs (e.g. s) get no zero-fill launch
         ctx.sub = (_Ctx(), _Ctx())
         ctx.side, ctx.ne = side, ne
+        check_fork(main)
         side.wait_stream(main)
         if core_tail is not None and TAIL_FIRST:  # beside the ego-net build
             core_tail()
@@ -629,6 +657,7 @@ class _GinEncoderPair(torch.autograd.Function):
         # runtime, tools/capture_probe.py); Encoder1 runs on ``side``, preceded
         # by compressor[0]'s backward (d f += d t W0, dW0, db0)
         main, side = _torch_stream(), ctx.side
+        check_fork(main)
         side.wait_stream(main)
         # Encoder1's final weight-gradient reduce runs beside the ego chain's
         # last layers (optionally capped, SIDE_REDUCE_WG)

@@ -101,8 +101,12 @@ def test_capacity_mode_eager_matches_exact(pkg, dev):
         _compare(exact_m, cap_m, le, lc)
 
 
-@pytest.mark.parametrize("k", [1, 2])
-def test_graph_replay_matches_exact_over_batches(pkg, dev, k):
+@pytest.mark.parametrize("k,fork_losses", [(1, False), (2, False), (1, True)])
+def test_graph_replay_matches_exact_over_batches(pkg, dev, k, fork_losses, monkeypatch):
+    """Graph replay over several batches == exact mode; fork_losses: the
+    contrastive loss on the side stream (SCGIB_FORK_LOSSES=1) together with
+    the forked encoder pair — flat forks only, captured and replayed."""
+    monkeypatch.setattr(pkg.models, "FORK_LOSSES", fork_losses)
     hosts = _batches(pkg, (4, 5, 6, 7))
     n_cap, e_cap, mgn, caps = pkg.graph.StaticBatch.capacities(hosts, k, slack=1.02)
     static = pkg.graph.StaticBatch(B, n_cap, e_cap, F_IN, mgn, caps, dev, k=k)
@@ -156,3 +160,22 @@ def test_static_batch_rejects_oversized(pkg, dev):
     assert big is not None
     with pytest.raises(pkg._lib.ScgibError):
         static.pad(big)
+
+
+def test_nested_fork_refused_while_capturing(pkg, dev, monkeypatch):
+    """ops.check_fork: a fork taken from one of the library's forked streams
+    while a HIP graph is being captured raises (torch-ROCm's capture_end
+    crashes on nested forks); from any other stream, or outside
+    a capture, it is allowed.  The capture state is simulated: a real nested
+    capture would end in the crash this guard exists to prevent."""
+    side = pkg.models._side_stream(dev)
+    other = torch.cuda.Stream(dev)
+    pkg.ops.check_fork(side)  # not capturing: fine
+    monkeypatch.setattr(torch.cuda, "is_current_stream_capturing", lambda: True)
+    pkg.ops.check_fork(other)
+    pkg.ops.check_fork(torch.cuda.current_stream(dev))
+    with pytest.raises(RuntimeError, match="nested forks"):
+        pkg.ops.check_fork(side)
+    _, aux = pkg.ops._aux_stream(dev)
+    with pytest.raises(RuntimeError, match="nested forks"):
+        pkg.ops.check_fork(aux)

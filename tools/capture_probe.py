@@ -7,10 +7,13 @@ import sys
 import torch
 
 CASES = ["bwd_fork_join", "bwd_fork_join_2streams", "bwd_fork_join_nested", "fwd_fork_join",
-         "fwd_nested", "bwd_flat2", "bwd_seq2", "bwd_nested_nokernel"]
+         "fwd_nested", "bwd_flat2", "bwd_seq2", "bwd_nested_nokernel", "bwd_nested_clone",
+         "bwd_nested_record", "bwd_nested_status", "bwd_flat_ret_side"]
 
 
 def run_case(name):
+    import faulthandler
+    faulthandler.enable()  # a segfault prints the Python frame it happened in
     dev = torch.device("cuda", 0)
     aux = torch.cuda.Stream(dev)
     side = torch.cuda.Stream(dev)
@@ -74,6 +77,32 @@ def run_case(name):
                     a = g * 2.0
                 cur.wait_stream(side)
                 return fork_join(a)
+            if name in ("bwd_nested_clone", "bwd_nested_record", "bwd_nested_status"):
+                # the nested case with the returned gradient re-homed on the
+                # current stream (clone) or its side-stream block recorded on it,
+                # and a probe of the capture status seen inside the nested fork
+                cur = torch.cuda.current_stream()
+                side.wait_stream(cur)
+                with torch.cuda.stream(side):
+                    aux.wait_stream(side)
+                    with torch.cuda.stream(aux):
+                        if name == "bwd_nested_status":
+                            print("capturing on nested aux:",
+                                  torch.cuda.is_current_stream_capturing(), flush=True)
+                        y = g * 2.0
+                    side.wait_stream(aux)
+                cur.wait_stream(side)
+                if name == "bwd_nested_record":
+                    y.record_stream(cur)
+                    return y
+                return y.clone()
+            if name == "bwd_flat_ret_side":  # flat fork, side-allocated result returned
+                cur = torch.cuda.current_stream()
+                side.wait_stream(cur)
+                with torch.cuda.stream(side):
+                    a = g * 2.0
+                cur.wait_stream(side)
+                return a
             if name == "bwd_nested_nokernel":
                 cur = torch.cuda.current_stream()
                 side.wait_stream(cur)
@@ -115,6 +144,6 @@ if __name__ == "__main__":
         for c in CASES:
             r = subprocess.run([sys.executable, __file__, c], capture_output=True, text=True,
                                timeout=120)
-            tail = (r.stdout.strip().splitlines() or [""])[-1]
-            err = (r.stderr.strip().splitlines() or [""])[-1]
-            print(f"{c}: rc={r.returncode} {tail} {err[:200] if r.returncode else ''}")
+            out = " | ".join(r.stdout.strip().splitlines()[-3:])
+            err = " | ".join(ln.strip() for ln in r.stderr.strip().splitlines()[-8:])
+            print(f"{c}: rc={r.returncode} {out} {err[:900] if r.returncode else ''}", flush=True)

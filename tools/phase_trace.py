@@ -5,7 +5,8 @@
 
 Runs one eager pretrain step of the bench workload on one stream; every
 launch routed through ops._launch is synchronised and its [grid][8] wall-clock
-stamps (100 MHz, common.h SCGIB_MARK; [grid][16]) are summarised: kernel span, spread of
+stamps (100 MHz, common.h SCGIB_MARK; [grid][32]: wall clock, then shader
+clock) are summarised: kernel span, spread of
 workgroup start times, and per-phase durations (median / p90 / max, us).
 """
 import ctypes
@@ -36,7 +37,7 @@ def main():
     dev = torch.device("cuda", 0)
     torch.manual_seed(1234)
     lib = pkg._lib.load()
-    buf = torch.zeros(MAXB * 16, dtype=torch.int64, device=dev)
+    buf = torch.zeros(MAXB * 32, dtype=torch.int64, device=dev)
     lib.scgib_trace_set.argtypes = [ctypes.c_void_p]
     assert lib.scgib_trace_set(ctypes.c_void_p(buf.data_ptr())) == 0
     F_in = pkg.synth.WORKLOADS["qm9"][2]
@@ -55,7 +56,7 @@ def main():
         buf.zero_()
         out = launch()
         torch.cuda.synchronize()
-        recs.append((name, meta, buf.view(MAXB, 16).cpu().numpy().copy()))
+        recs.append((name, meta, buf.view(MAXB, 32).cpu().numpy().copy()))
         return out
 
     for it in range(2):  # second iteration: warm caches / allocator
@@ -84,15 +85,20 @@ def main():
               f"{np.percentile(start - t0, 50) / 100:.2f}/{np.percentile(start - t0, 90) / 100:.2f}/"
               f"{(start - t0).max() / 100:.2f}us")
         prev = start
+        prevc = t[:, 16]
         for k, pname in enumerate(ph):
             col = t[:, 1 + k]
             ok = col != 0
             if not ok.any():
                 continue
             d = (col[ok] - prev[ok]) / 100.0
+            cyc = t[:, 17 + k][ok] - prevc[ok]
+            ghz = np.where(d > 0, cyc / np.maximum(d, 1e-9) / 1e3, 0)
             print(f"    {pname:10s} n={ok.sum():4d} p50={np.percentile(d, 50):6.2f} "
-                  f"p90={np.percentile(d, 90):6.2f} max={d.max():6.2f} us")
+                  f"p90={np.percentile(d, 90):6.2f} max={d.max():6.2f} us  "
+                  f"clock p50={np.percentile(ghz, 50):.2f} GHz  cycles p50={np.percentile(cyc, 50):.0f}")
             prev = np.where(ok, col, prev)
+            prevc = np.where(ok, t[:, 17 + k], prevc)
         if name == "scgib_gin_layer_fwd_bn" and (t[:, 6] != 0).any():
             d = (t[:, 6] - start) / 100.0
             print(f"    (finish prev BN: start->mark6 p50={np.percentile(d, 50):.2f} "
@@ -101,6 +107,13 @@ def main():
                 for a_, b_, lab in ((0, 8, "start->fin"), (8, 9, "fin compute"), (9, 6, "barrier")):
                     d = (t[:, b_] - t[:, a_]) / 100.0
                     print(f"      {lab}: p50={np.percentile(d, 50):.2f} p90={np.percentile(d, 90):.2f}")
+        if name == "scgib_gin_layer_bwd" and (t[:, 6] != 0).any():  # gin_bwd2_k sub-marks
+            for a_, b_, lab in ((1, 6, "GEMM1 MFMA"), (6, 2, "db2+dz1"), (2, 7, "db1+GEMM2 MFMA"),
+                                (7, 3, "dagg stores")):
+                d = (t[:, b_] - t[:, a_]) / 100.0
+                cyc = t[:, 16 + b_] - t[:, 16 + a_]
+                print(f"      {lab:16s}: p50={np.percentile(d, 50):.2f} us  "
+                      f"cycles p50={np.percentile(cyc, 50):.0f}")
         per_cu = {}
         for i in range(nb):
             per_cu.setdefault((xcc[i], se[i], sh[i], cu[i]), []).append(i)

@@ -39,7 +39,7 @@ HBM_MEASURED_GBS = 6290.0   # float4 copy, same file
 # tools/gpu_pmc.sh (2 x FETCH_SIZE + WRITE_SIZE, MI355X_MICROARCH.md "HBM
 # [CDNA4]"), committed under profiles/ — the bench itself runs unprofiled.
 TRAFFIC_FILE = os.environ.get("SCGIB_TRAFFIC_FILE",
-                              os.path.join(ROOT, "profiles", "r01_s6", "traffic.json"))
+                              os.path.join(ROOT, "profiles", "r02_s1", "traffic.json"))
 
 
 def _traffic():

@@ -96,7 +96,7 @@ def layer_fwd_flops(n, e, d_in):
 
 
 def layer_bwd_bytes(n, e, d_in):
-    """Algorithmic bytes of one GIN layer backward launch (gin_bwd2_k, DESIGN.md
+    """Algorithmic bytes of one GIN layer backward launch (gin_bwd5_k, DESIGN.md
     §4): the dy, z2, r and agg rows read, W1/W2 + BN coefficients, d(agg)
     written.  The per-workgroup dW slabs are NOT counted: they are partials of
     a 33 KB gradient, not bytes the layer needs (their cost shows in
@@ -588,9 +588,9 @@ def main():
                        "global_batch": world * a.batch, "nodes_per_batch": round(n_nodes, 1),
                        "parallelism": f"dp{world}", "final_loss": round(final_loss, 4)},
             # dominant kernel by total time per step (profiles/): gin_bwd_k
-            "roofline": None if r_bwd is None else roofline_entry("gin_bwd2_k", "fused GIN layer backward: BN-backward "
-                                       "apply + 4 f32-MFMA GEMMs, one workgroup per CU walking its tiles", r_bwd,
-                                       ["gin_bwd2_k<64>"]),
+            "roofline": None if r_bwd is None else roofline_entry("gin_bwd5_k", "fused GIN layer backward: BN-backward "
+                                       "apply + 4 f32-MFMA GEMMs on 32-row sub-tiles, two workgroups per CU, "
+                                       "b128-fed operands", r_bwd, ["gin_bwd5_k<64>"]),
             "roofline_gin_fwd": None if r_fwd is None else roofline_entry("gin_fwd_k", "fused GIN layer: gather + 2 "
                                                "f32-MFMA GEMMs + BN tile stats", r_fwd,
                                                ["gin_fwd_k<32, false, true,",

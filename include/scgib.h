@@ -104,8 +104,8 @@ int scgib_gin_aggregate(const float *h, const int32_t *rowptr, const int32_t *co
  * scgib_gin_layer_bwd: d(agg) [n,d_in] and wgrad = dW2[64*64] | dW1[64*d_in]
  *   | db2[64] | db1[64] through scgib_gin_layer_bwd_slabs(n, d_in) per-workgroup
  *   slabs of 64*64 + 64*d_in + 128 floats (scgib_gin_slab_floats(n, d_in) in
- *   total; d_in = 64: one workgroup per CU walking its tiles, LDS-DMA staged),
- *   reduced in a fixed order.  With wgrad NULL the slabs are left for the
+ *   total; d_in = 64: 32-row sub-tiles, up to two workgroups per CU each
+ *   walking its sub-tiles), reduced in a fixed order.  With wgrad NULL the slabs are left for the
  *   caller's scgib_slab_reduce (so the GEMM kernel can be timed alone).
  * scgib_slab_reduce: out[w] = sum_s slab[s*width + w], fixed order. */
 int64_t scgib_gin_tiles(int64_t n_nodes);

@@ -1517,6 +1517,227 @@ __global__ __launch_bounds__(256, 1) void gin_bwd2_k(
     SCGIB_MARK(4);
 }
 
+// ---------------------------------------------------------------------------
+// gin_bwd5_k: the GIN layer backward (BN, d_in = 64) on 32-row sub-tiles,
+// TWO workgroups per CU (63 KB LDS, <= 256 VGPRs).
+//
+// gin_bwd2_k walks 64-row tiles, one workgroup per CU, ~1.7 tiles per CU at
+// QM9 B512 (437 ego tiles on 256 CUs): its per-tile phases (dz2, dz1 mask,
+// d(agg) stores, barrier waits) leave the matrix pipe idle ~40 % of a tile and
+// its dword operand reads (2 ds_read_b32 per MFMA at one wave per SIMD) run
+// the GEMMs at ~80 % of the MFMA rate (phase trace r02).  Here:
+//   * 32-row sub-tiles, two workgroups per CU: one workgroup's non-MFMA
+//     phases run under the other's MFMAs; ~3.4 sub-tiles per CU balance
+//     better than 1.7 tiles;
+//   * no K split: waves take whole products, 32 MFMAs per wave and pair:
+//       pair A: waves 0,1 (N): dr block q = dz2 W2[:, 32q..] (K = 64, one
+//               chain), dz1 = dr [r > 0] written straight from the accumulator;
+//               waves 2,3 (T): dW2 rows 32q.. += dz2^T r (two blocks, K = 32 rows)
+//       pair B: N: dW1 rows 32q.. += dz1^T agg;  T: d(agg) block q = dz1 W1[:, 32q..]
+//   * every MFMA operand is fed four k values per ds_read_b128 (mma_rk4 /
+//     mma_kk4x2, permuted k order): NN products read dz row-major and take
+//     the wave's 32-column weight block from 32 VGPRs held for the whole
+//     kernel (no weight image in LDS); TN products read transposed dz, r and
+//     agg images [col][row];
+//   * the next sub-tile's rows are loaded into registers before pair A and
+//     written to the r^T / agg^T images once their last reader has passed a
+//     barrier (r after pair A, agg after pair B): three barriers per sub-tile.
+// The elementwise steps own one column and eight rows per thread (c = tid &
+// 63, rows 8 w..8 w+7), so the transposed images are written as float4 runs
+// and the row-major dz images as conflict-free dwords.
+// LDS: dz2, dz1 row-major + transposed, r^T, agg^T, d(agg) staging = 63 KB.
+// ---------------------------------------------------------------------------
+constexpr int SM = 32;   // rows per sub-tile
+constexpr int LDR = 68;  // row-major 64-wide images (= 4 mod 64: b128 reads conflict free)
+constexpr int LDT = 36;  // transposed [64][32] images (rows k-contiguous)
+
+template <int DIN>
+__global__ __launch_bounds__(256, 2) void gin_bwd5_k(
+    const float *__restrict__ dy, const float *__restrict__ z2, const float *__restrict__ r,
+    const float *__restrict__ agg, const float *__restrict__ stat,
+    const float *__restrict__ coef, const float *__restrict__ w1, const float *__restrict__ w2,
+    int64_t ncap, int64_t nsub, float *__restrict__ dagg_out, float *__restrict__ slab,
+    const int32_t *__restrict__ dims, scgib_bn_bwd_pending pend) {
+    static_assert(DIN == 64 && SM == 32, "64-wide rows, 32-row sub-tiles");
+    constexpr int SLAB = 64 * 64 + 64 * DIN + 128;
+    __shared__ __attribute__((aligned(16))) float sD[SM * LDR];   // dz2 [row][k]
+    __shared__ __attribute__((aligned(16))) float sDT[64 * LDT];  // dz2 [col][row]
+    __shared__ __attribute__((aligned(16))) float sE[SM * LDR];   // dz1
+    __shared__ __attribute__((aligned(16))) float sET[64 * LDT];
+    __shared__ __attribute__((aligned(16))) float sRT[64 * LDT];  // r [col][row]
+    __shared__ __attribute__((aligned(16))) float sAT[DIN * LDT]; // agg [col][row]
+    __shared__ float sG[SM * LDH];                                 // d(agg) staging
+    __shared__ float sCoef[128];
+    const int64_t n = eff_count(dims, 0, ncap);
+    const int tid = threadIdx.x, l = tid & 63, w = tid >> 6;
+    const int kk = l >> 5, li = l & 31;
+    const bool nw = w < 2;  // wave-uniform role: N (dr, dW1) or T (dW2, d(agg))
+    const int q = w & 1;    // the role's 32-wide block
+    const int c = l;        // elementwise: column c, rows 8 w .. 8 w + 7
+    const int64_t last = ncap - 1;
+    const int64_t G = gridDim.x;
+    SCGIB_MARK(0);
+    SCGIB_MARK_HWID();
+    BwdFin bfin;
+    const int pend_ngr = static_cast<int>(((n + TM - 1) / TM + kGroup - 1) / kGroup);
+    if (pend.gpart) bn_bwd_fin_load<false>(pend.gpart, pend_ngr, 0, bfin);
+    const float s_mean = stat[c], s_istd = stat[64 + c], s_sc = stat[128 + c];
+    float c1 = 0.f, c2 = 0.f;
+    if (!pend.gpart) {
+        c1 = coef[c];
+        c2 = coef[64 + c];
+    }
+    // the wave's weight block: N waves W2[:, 32q..] (dr), T waves W1[:, 32q..] (d(agg))
+    float wreg[32];
+    {
+        const float *wm = nw ? w2 : w1;
+#pragma unroll
+        for (int s = 0; s < 32; ++s) wreg[s] = wm[kperm(s, kk) * 64 + q * 32 + li];
+    }
+    float nx[4][8];  // a sub-tile's column c, rows 8 w + i: [0] dy, [1] z2, [2] r, [3] agg
+    auto load_sub = [&](int64_t s) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {  // in order of use: r, agg, then dy / z2
+            int64_t row = s * SM + 8 * w + i;
+            row = row < last ? row : last;
+            nx[2][i] = r[row * 64 + c];
+        }
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            int64_t row = s * SM + 8 * w + i;
+            row = row < last ? row : last;
+            nx[3][i] = agg[row * DIN + c];
+        }
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            int64_t row = s * SM + 8 * w + i;
+            row = row < last ? row : last;
+            nx[0][i] = dy[row * 64 + c];
+            nx[1][i] = z2[row * 64 + c];
+        }
+    };
+    auto put_t = [&](float *img, int a) {  // column c, rows 8w..8w+7 -> [c][row]
+        float4 *p = reinterpret_cast<float4 *>(img + c * LDT + 8 * w);
+        p[0] = make_float4(nx[a][0], nx[a][1], nx[a][2], nx[a][3]);
+        p[1] = make_float4(nx[a][4], nx[a][5], nx[a][6], nx[a][7]);
+    };
+    auto rows_of = [&](int64_t s) {
+        const int64_t v = n - s * SM;
+        return static_cast<int>(v < SM ? (v > 0 ? v : 0) : SM);
+    };
+    auto zero_pad = [&](int64_t s, int from) {
+        const int64_t row0 = s * SM;
+        const int ncr = static_cast<int>(ncap - row0 < SM ? ncap - row0 : SM);
+        for (int idx = from * DIN + tid; idx < ncr * DIN; idx += 256) dagg_out[row0 * DIN + idx] = 0.f;
+    };
+    int64_t s = blockIdx.x;
+    int nv = s < nsub ? rows_of(s) : 0;
+    if (nv > 0) load_sub(s);
+    if (pend.gpart) {  // finish the BN-backward sums; workgroup 0 writes dgamma, dbeta
+        const double tot = bn_bwd_final<false>(pend.gpart, pend_ngr, bfin);
+        const int cs = bfin_index();
+        const bool lead = (tid & 63) < 32, w0 = blockIdx.x == 0 && lead;
+        const float cf = bn_bwd_publish(cs, tot, n, pend.training, w0 ? pend.dgamma : nullptr,
+                                        w0 ? pend.dbeta : nullptr, nullptr);
+        if (lead) sCoef[cs] = cf;
+    }
+    if (nv > 0) {
+        put_t(sRT, 2);
+        put_t(sAT, 3);
+    }
+    // the weight registers complete here: a load still counted at the loop
+    // entry makes hipcc wait vmcnt(0..3) at their uses in EVERY iteration
+    // (then for the next sub-tile's rows)
+    vm_wait_all();
+    __syncthreads();
+    if (pend.gpart) {
+        c1 = sCoef[c];
+        c2 = sCoef[64 + c];
+    }
+    const float k1 = s_istd * c2;  // dz2 = sc (dy - c1 - (z2 - mean) istd c2)
+    SCGIB_MARK(1);
+    // N waves: dW1 blocks (q, 0), (q, 1) and db1; T waves: dW2 blocks and db2
+    f32x16 accA = zero16(), accB = zero16();
+    float dbias = 0.f;
+    for (int it = 0; s < nsub; s += G, ++it) {
+        if (nv == 0) {  // capacity tail: this and every later sub-tile is padding
+            for (int64_t t = s; t < nsub; t += G) zero_pad(t, rows_of(t));
+            break;
+        }
+        {   // dz2 (rows past nv zero) -> sD row-major and sDT transposed
+            float d[8];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const float v = s_sc * (nx[0][i] - c1 - (nx[1][i] - s_mean) * k1);
+                d[i] = 8 * w + i < nv ? v : 0.f;
+                sD[(8 * w + i) * LDR + c] = d[i];
+            }
+            float4 *p = reinterpret_cast<float4 *>(sDT + c * LDT + 8 * w);
+            p[0] = make_float4(d[0], d[1], d[2], d[3]);
+            p[1] = make_float4(d[4], d[5], d[6], d[7]);
+        }
+        const int64_t next = s + G;
+        const int next_nv = next < nsub ? rows_of(next) : 0;  // block-uniform
+        if (next_nv > 0) load_sub(next);  // in flight during both product pairs
+        lds_barrier();  // dz2 complete
+        if (it == 0) SCGIB_MARK(2);
+        if (nw) {  // dr block q, dz1 = dr [r > 0] -> sE, sET (mask by multiplication)
+            const f32x16 dr = mma_rk4<8>(sD + li * LDR + 4 * kk, wreg, zero16());
+#pragma unroll
+            for (int reg = 0; reg < 16; ++reg) {
+                const int row = acc_row(reg, l), col = q * 32 + li;
+                const float v = dr[reg] * (sRT[col * LDT + row] > 0.f ? 1.f : 0.f);
+                sE[row * LDR + col] = v;
+                sET[col * LDT + row] = v;
+            }
+        } else {   // dW2 rows 32q.. += dz2^T r (db2 from the A operand)
+            mma_kk4x2<4>(sDT + (q * 32 + li) * LDT + 4 * kk, sRT + li * LDT + 4 * kk,
+                         sRT + (32 + li) * LDT + 4 * kk, accA, accB, dbias);
+        }
+        lds_barrier();  // dz1 complete; r and dz2 consumed
+        if (it == 0) SCGIB_MARK(3);
+        if (next_nv > 0) put_t(sRT, 2);
+        if (nw) {  // dW1 rows 32q.. += dz1^T agg (db1 from the A operand)
+            mma_kk4x2<4>(sET + (q * 32 + li) * LDT + 4 * kk, sAT + li * LDT + 4 * kk,
+                         sAT + (32 + li) * LDT + 4 * kk, accA, accB, dbias);
+        } else {   // d(agg) block q = dz1 W1[:, 32q..] -> staging
+            const f32x16 da = mma_rk4<8>(sE + li * LDR + 4 * kk, wreg, zero16());
+#pragma unroll
+            for (int reg = 0; reg < 16; ++reg) sG[acc_row(reg, l) * LDH + q * 32 + li] = da[reg];
+        }
+        lds_barrier();  // d(agg) staged; agg and dz1 consumed
+        if (it == 0) SCGIB_MARK(4);
+        if (next_nv > 0) put_t(sAT, 3);
+        // d(agg) rows: full-row float4 stores (after the loads: in-order vmcnt)
+        {
+            const int c4 = tid & 15, rs = tid >> 4;
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+                const int rr = rs + 16 * k;
+                const float *pg = sG + rr * LDH + 4 * c4;
+                const float4 v = make_float4(pg[0], pg[1], pg[2], pg[3]);
+                if (rr < nv) st4(dagg_out + (s * SM + rr) * DIN + 4 * c4, v);
+            }
+        }
+        if (dims) zero_pad(s, nv);
+        nv = next_nv;
+    }
+    SCGIB_MARK(5);
+    // per-workgroup slab: dW2 | dW1 | db2 | db1 (gin_bwd_k layout)
+    float *sl = slab + static_cast<int64_t>(blockIdx.x) * SLAB;
+    float *dw = nw ? sl + 64 * 64 : sl;  // N: dW1 [64][DIN], T: dW2 [64][64]
+    const int ld = nw ? DIN : 64;
+#pragma unroll
+    for (int reg = 0; reg < 16; ++reg) {
+        const int j = q * 32 + acc_row(reg, l);
+        dw[j * ld + li] = accA[reg];
+        dw[j * ld + 32 + li] = accB[reg];
+    }
+    dbias += __shfl_xor(dbias, 32, kWave);
+    if (l < 32) sl[64 * 64 + 64 * DIN + (nw ? 64 : 0) + q * 32 + l] = dbias;
+    SCGIB_MARK(6);
+}
+
 // up to two workgroups per CU (66.5 KB LDS each): one tile per workgroup for
 // batches up to SCGIB_BWD_GRID_CAP tiles (build-time knob), so every tile of
 // an encoder layer runs at once; larger batches loop over tiles
@@ -1542,16 +1763,28 @@ extern "C" int scgib_trace_set(void *buf) {
 }
 #endif
 
-// scgib_gin_layer_bwd: d_in = 64 runs gin_bwd2_k (one workgroup per CU, each
-// walking its tiles), d_in = 32 gin_bwd_k (one workgroup per tile up to the cap)
-#ifndef SCGIB_BWD2
-#define SCGIB_BWD2 1
+// scgib_gin_layer_bwd: d_in = 32 runs gin_bwd_k (one workgroup per tile up
+// to the cap); d_in = 64 the variant SCGIB_BWD_V (build-time A/B knob):
+// 5 = gin_bwd5_k (default), 2 = gin_bwd2_k (64-row tiles, one workgroup per
+// CU).  gin_bwd5_k takes the fewest workgroups that reach the largest
+// per-workgroup count: the same finish time as the full two-per-CU grid,
+// fewer slabs.
+#ifndef SCGIB_BWD_V
+#define SCGIB_BWD_V 5
 #endif
-static constexpr bool kBwd2 = SCGIB_BWD2 != 0;
+static constexpr bool kBwd5 = SCGIB_BWD_V == 5;
+static constexpr bool kBwd2 = SCGIB_BWD_V == 2;
+
+static int64_t bwd5_subtiles(int64_t n_nodes) { return (n_nodes + SM - 1) / SM; }
+static int bwd5_grid(int64_t nsub) {
+    const int64_t per = (nsub + 2 * kCUs - 1) / (2 * kCUs);
+    return static_cast<int>((nsub + per - 1) / per);
+}
 
 extern "C" int64_t scgib_gin_layer_bwd_slabs(int64_t n_nodes, int32_t d_in) {
     if (n_nodes <= 0) return 0;
     const int64_t nt = scgib_gin_tiles(n_nodes);
+    if (d_in == 64 && kBwd5) return bwd5_grid(bwd5_subtiles(n_nodes));
     if (d_in == 64 && kBwd2) return nt < kCUs ? nt : kCUs;
     return bwd_grid(nt);
 }
@@ -1848,6 +2081,8 @@ extern "C" int scgib_gin_layer_bwd(const float *dy, const float *z2, const float
     hipStream_t st = as_stream(stream);
     if (d_in == 32)
         gin_bwd_k<32><<<grid, 256, 0, st>>>(dy, z2, r, agg, stat, coef, w1, w2, n_nodes, nt, dagg, slab, dims, nullptr, pd, ReconArgs{});
+    else if (kBwd5)
+        gin_bwd5_k<64><<<grid, 256, 0, st>>>(dy, z2, r, agg, stat, coef, w1, w2, n_nodes, bwd5_subtiles(n_nodes), dagg, slab, dims, pd);
     else if (kBwd2)
         gin_bwd2_k<64><<<grid, 256, 0, st>>>(dy, z2, r, agg, stat, coef, w1, w2, n_nodes, nt, dagg, slab, dims, pd);
     else

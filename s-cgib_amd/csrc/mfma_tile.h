@@ -330,6 +330,74 @@ __device__ __forceinline__ float col_sum16(float acc, const float *p, int stride
     return acc;
 }
 
+// ---------------------------------------------------------------------------
+// Wide-operand forms (gin_bwd5_k).  ds_read_b32 at one or two waves per SIMD
+// delivers a fraction of the LDS rate (MI355X_MICROARCH.md §LDS), so each
+// lane reads FOUR k values per ds_read_b128 instead: the k order of the K
+// sum is permuted — step s = 4 qb + t of lane half kk covers
+//   k(s, kk) = 8 qb + 4 kk + t            (kperm below)
+// — identically for both operands, so every product is still the exact
+// sum over k (only the association order differs from mma_nt/nn/tn).  An
+// operand is "k-contiguous" per lane: A row-major over k (NN / NT rows), or a
+// transposed image [col][k] for the TN products over rows.  With row strides
+// = 4 (mod 64) floats the 16-lane groups of ds_read_b128 are conflict free.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ int kperm(int s, int kk) { return 8 * (s >> 2) + 4 * kk + (s & 3); }
+
+__device__ __forceinline__ float f4at(const float4 &v, int t) {
+    return t == 0 ? v.x : t == 1 ? v.y : t == 2 ? v.z : v.w;
+}
+
+// acc += A B over K = 8 NB: A k-contiguous per lane (pa = this lane's row
+// start + 4 kk), B in registers (b[s] = B(kperm(s, kk), lane's column)).
+// One accumulation chain (64-cycle issue = dependent latency of the f32 MFMA).
+template <int NB>
+__device__ __forceinline__ f32x16 mma_rk4(const float *pa, const float (&b)[4 * NB], f32x16 acc) {
+    float4 a[2];
+    a[0] = *reinterpret_cast<const float4 *>(pa);
+#pragma unroll
+    for (int qb = 0; qb < NB; ++qb) {
+        if (qb + 1 < NB) a[(qb + 1) & 1] = *reinterpret_cast<const float4 *>(pa + 8 * (qb + 1));
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(f4at(a[qb & 1], t), b[4 * qb + t], acc, 0, 0, 0);
+        mma_step_fence();
+    }
+    return acc;
+}
+
+// two products sharing the A operand, K = 8 NB, both operands k-contiguous
+// per lane (pa, pb1, pb2 = lane starts + 4 kk); asum += the lane's A values
+// (for a transposed dz image: the column sum over the lane's half of the
+// rows — the bias gradient).  The two chains alternate.
+template <int NB>
+__device__ __forceinline__ void mma_kk4x2(const float *pa, const float *pb1, const float *pb2,
+                                          f32x16 &c1, f32x16 &c2, float &asum) {
+    float4 a[2], b1[2], b2[2];
+    a[0] = *reinterpret_cast<const float4 *>(pa);
+    b1[0] = *reinterpret_cast<const float4 *>(pb1);
+    b2[0] = *reinterpret_cast<const float4 *>(pb2);
+#pragma unroll
+    for (int qb = 0; qb < NB; ++qb) {
+        if (qb + 1 < NB) {
+            const int o = 8 * (qb + 1), x = (qb + 1) & 1;
+            a[x] = *reinterpret_cast<const float4 *>(pa + o);
+            b1[x] = *reinterpret_cast<const float4 *>(pb1 + o);
+            b2[x] = *reinterpret_cast<const float4 *>(pb2 + o);
+        }
+        const int x = qb & 1;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            const float av = f4at(a[x], t);
+            c1 = __builtin_amdgcn_mfma_f32_32x32x2f32(av, f4at(b1[x], t), c1, 0, 0, 0);
+            c2 = __builtin_amdgcn_mfma_f32_32x32x2f32(av, f4at(b2[x], t), c2, 0, 0, 0);
+            asum += av;
+        }
+        mma_step_fence();
+    }
+    asm volatile("" ::"v"(c1[0]), "v"(c2[0]));
+}
+
 // row of accumulator register `reg` of the 32x32 output tile held by lane l
 __device__ __forceinline__ int acc_row(int reg, int l) { return (reg & 3) + 8 * (reg >> 2) + 4 * (l >> 5); }
 

@@ -25,7 +25,8 @@ import bench  # noqa: E402
 PHASES = {
     "scgib_gin_layer_fwd_bn": ["gather", "gemm1", "gemm2+st", "tilestat", "bn_hier"],
     "scgib_gin_layer0_fwd": ["gather", "gemm1", "gemm2+st", "tilestat", "bn_hier"],
-    "scgib_gin_layer_bwd": ["ld+dz2", "dW2,dr", "dW1,dagg", "slab"],
+    # gin_bwd5_k: marks of the first sub-tile, then the remaining sub-tiles
+    "scgib_gin_layer_bwd": ["prologue", "dz2", "pairA", "pairB", "rest", "slab"],
     "scgib_gin_layer0_bwd": ["ld+dz2", "dW2,dr", "dW1,dagg", "slab"],
     "scgib_gin_bwd_stats_bn": ["gather+dy", "bn_hier"],
 }
@@ -107,7 +108,7 @@ def main():
                 for a_, b_, lab in ((0, 8, "start->fin"), (8, 9, "fin compute"), (9, 6, "barrier")):
                     d = (t[:, b_] - t[:, a_]) / 100.0
                     print(f"      {lab}: p50={np.percentile(d, 50):.2f} p90={np.percentile(d, 90):.2f}")
-        if name == "scgib_gin_layer_bwd" and (t[:, 6] != 0).any():  # gin_bwd2_k sub-marks
+        if name == "scgib_gin_layer_bwd" and os.environ.get("BWD2_MARKS"):  # gin_bwd2_k sub-marks
             for a_, b_, lab in ((1, 6, "GEMM1 MFMA"), (6, 2, "db2+dz1"), (2, 7, "db1+GEMM2 MFMA"),
                                 (7, 3, "dagg stores")):
                 d = (t[:, b_] - t[:, a_]) / 100.0

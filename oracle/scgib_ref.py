@@ -66,17 +66,32 @@ def _batchnorm_train(x, p, name, buffers):
                         BN_MOMENTUM, BN_EPS)
 
 
-def gin_encoder(p, prefix, src, dst, h, buffers, num_layers):
-    """GIN.forward with DGL GINConv semantics (sum aggregation, (1+eps)*h)."""
+def _relu(x, mask, tie):
+    """ReLU; with `mask` (the implementation under test's own decisions), the
+    elements within `tie` of 0 — where an fp32 implementation may decide
+    either way — follow the mask (x passes, or 0), all others the sign."""
+    if mask is None:
+        return F.relu(x)
+    amb = x.abs() < tie
+    return torch.where(amb, x * mask.to(x.dtype), F.relu(x))
+
+
+def gin_encoder(p, prefix, src, dst, h, buffers, num_layers, relu_masks=None, tie=1e-5):
+    """GIN.forward with DGL GINConv semantics (sum aggregation, (1+eps)*h).
+    relu_masks (test use): per layer (hidden ReLU mask, output ReLU mask) of
+    the fp32 implementation under test, applied only at pre-activations
+    within `tie` of 0 (_relu), so that a gradient comparison is not decided
+    by which way a rounding-level pre-activation fell."""
     for i in range(num_layers):
         lp = f"{prefix}.ginlayers.{i}"
         neigh = torch.zeros_like(h).index_add(0, dst, h[src])
         eps = p.get(lp + ".eps", torch.zeros(1))
         rst = (1 + eps) * h + neigh
-        z = F.relu(_linear(rst, p, lp + ".apply_func.mlp.0"))
+        m1, m2 = relu_masks[i] if relu_masks is not None else (None, None)
+        z = _relu(_linear(rst, p, lp + ".apply_func.mlp.0"), m1, tie)
         z = _linear(z, p, lp + ".apply_func.mlp.2")
         z = _batchnorm_train(z, p, f"{prefix}.batch_norms.{i}", buffers)
-        h = F.relu(z)
+        h = _relu(z, m2, tie)
     return h
 
 

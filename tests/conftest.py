@@ -70,6 +70,22 @@ def rel_l2(a, b):
     return float(np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30)) if b.size else 0.0
 
 
+def gin_relu_masks(out, layers):
+    """Per GIN layer (hidden ReLU mask, output ReLU mask) of a fused encoder
+    output `out` (ops._GinEncoder): r > 0 from the saved r, and
+    scale z2 + shift > 0 from the saved z2 and BN record — for the oracle's
+    relu_masks (scgib_ref.gin_encoder).  The latter in fp64: the exact
+    product plus one rounding has the sign of the kernels' fused multiply-add."""
+    t = out.grad_fn.saved_tensors
+    masks = []
+    for l in range(layers):
+        _, r, z2, stat = t[4 * l: 4 * l + 4]
+        stat = stat.double()
+        m2 = (stat[2] * z2.double() + stat[3]) > 0
+        masks.append(((r > 0).cpu(), m2.cpu()))
+    return masks
+
+
 def check_grads(golden_grads, mine_of, tol=1e-4, cancelled=CANCELLED, metric="max"):
     for name, ref in golden_grads.items():
         mine = mine_of(name)

@@ -9,7 +9,7 @@ import torch
 import torch.nn.functional as F
 
 from conftest import (CANCELLED, FINETUNE_GOLDENS, MODEL_GOLDENS, check_grads, check_grads_model, golden_logms,
-                      load_golden, rel_err, rel_l2)
+                      load_golden, rel_err, rel_l2, gin_relu_masks)
 from oracle import egonet
 from oracle import scgib_ref as R
 
@@ -363,21 +363,26 @@ def test_fused_gin_encoder(pkg, dev, training, layers, n_mols):
     n = g.num_nodes()
     h0 = torch.randn(n, 32)
     src, dst = gh.edges()
+    gd = gin.to(dev)
+    h0d = h0.to(dev).requires_grad_(True)
+    out = gd(g, h0d)
+    # ~3.5 M ReLU pre-activations at 5 x 300 molecules: a few lie within fp32
+    # rounding of 0, and a train-mode BatchNorm spreads one flipped decision
+    # to every row's gradient.  The oracle follows the kernels' own decisions
+    # at |pre-activation| < 1e-5 (and the sign everywhere else).
+    masks = gin_relu_masks(out, layers)
     h0c = h0.double().requires_grad_(True)
     if training:
-        ref = R.gin_encoder(p, "Encoder1", src, dst, h0c, bufs, layers)
+        ref = R.gin_encoder(p, "Encoder1", src, dst, h0c, bufs, layers, relu_masks=masks)
     else:
         orig = R._batchnorm_train
         R._batchnorm_train = lambda x, pp, name, buf: F.batch_norm(
             x, bufs[name + ".running_mean"], bufs[name + ".running_var"], pp[name + ".weight"],
             pp[name + ".bias"], False, 0.1, 1e-5)
         try:
-            ref = R.gin_encoder(p, "Encoder1", src, dst, h0c, None, layers)
+            ref = R.gin_encoder(p, "Encoder1", src, dst, h0c, None, layers, relu_masks=masks)
         finally:
             R._batchnorm_train = orig
-    gd = gin.to(dev)
-    h0d = h0.to(dev).requires_grad_(True)
-    out = gd(g, h0d)
     assert rel_err(out.detach().cpu(), ref.detach()) < ACT_TOL
     w = torch.randn_like(ref)
     (w * ref).sum().backward()

@@ -481,6 +481,11 @@ struct ReconArgs {
 // GATHER = false is the dense two-layer MLP of the head (models.py:1055-1057,
 // applied at :1174): the tile's input rows are staged directly, agg_out and
 // the BN tile statistics are not written, z2_out is the MLP output.
+#ifndef SCGIB_LATE_WEIGHTS
+#define SCGIB_LATE_WEIGHTS 1
+#endif
+constexpr bool kLateWeights = SCGIB_LATE_WEIGHTS != 0;
+
 template <int DIN, bool XFORM, bool GATHER = true, bool PRE = false, bool RECON = false>
 __global__ __launch_bounds__(256) void gin_fwd_k(
     const float *__restrict__ h, const float *__restrict__ in_scale,
@@ -539,8 +544,13 @@ __global__ __launch_bounds__(256) void gin_fwd_k(
         pend_bet = pend.beta[fin_channel()];
         bn_fwd_fin_load<false>(pend.gpart, pend_ngr, 0, fin);
     }
-    WeightRegs<DIN> wregs;  // in flight during the gather; to LDS before the first GEMM
-    load_weights<DIN>(w1, w2, wregs);
+    // weights: in flight during the gather, to LDS before the first GEMM; with
+    // kLateWeights (gathering layers) issued after the gather's loads instead,
+    // so the latency chain (BN partials -> neighbour indices -> rows) does not
+    // share the start-of-kernel fetch burst with 32 KB of weights
+    WeightRegs<DIN> wregs;
+    constexpr bool late_w = kLateWeights && GATHER && !PRE;
+    if (!late_w) load_weights<DIN>(w1, w2, wregs);
     if constexpr (PRE) {  // transfer_d folded: gather raw features, then agg0 = aggx Wt^T
         float *sXg = sPre, *sWt = sPre + TM * kPreLD;
         for (int idx = tid; idx < 32 * kPreF; idx += 256) {
@@ -623,6 +633,7 @@ __global__ __launch_bounds__(256) void gin_fwd_k(
             }
         }
         gather_tail<RPT, LPR, XFORM>(h4, col, hd, c, ope, sc, sh, acc);
+        if (late_w) load_weights<DIN>(w1, w2, wregs);  // before the agg stores (in-order vmcnt)
 #pragma unroll
         for (int k = 0; k < RPT; ++k) {
             const int rr = rbase + k * RPP;
@@ -1776,8 +1787,12 @@ static constexpr bool kBwd5 = SCGIB_BWD_V == 5;
 static constexpr bool kBwd2 = SCGIB_BWD_V == 2;
 
 static int64_t bwd5_subtiles(int64_t n_nodes) { return (n_nodes + SM - 1) / SM; }
+#ifndef SCGIB_BWD5_SLOTS
+#define SCGIB_BWD5_SLOTS 1  // workgroups per CU the grid is sized for (2: same isolated time, 1.8x the slabs)
+#endif
 static int bwd5_grid(int64_t nsub) {
-    const int64_t per = (nsub + 2 * kCUs - 1) / (2 * kCUs);
+    constexpr int64_t slots = SCGIB_BWD5_SLOTS * kCUs;
+    const int64_t per = (nsub + slots - 1) / slots;
     return static_cast<int>((nsub + per - 1) / per);
 }
 

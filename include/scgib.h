@@ -218,6 +218,17 @@ int scgib_gin_layer0_fwd(const float *x, int32_t n_feat, const int32_t *node_map
                          float *running_mean, float *running_var, int64_t *num_batches_tracked,
                          float *stat, float *bn_ws, uint32_t *counters, const int32_t *dims,
                          int32_t defer, scgib_stream_t stream);
+/* scgib_gin_bwd_stats_bn with a weight-gradient slab reduce folded in
+ * (`fold` NULL: none): extra workgroups past the tile grid compute
+ * fold->out[w] = sum_s fold->slab[s*stride + w] (fixed order, as
+ * scgib_slab_reduce_multi's job) — the previous layer's reduce runs in the
+ * bandwidth the gather-bound statistics tiles leave idle. */
+int scgib_gin_bwd_stats_bn_fold(const float *dh, const int32_t *rowptr_t, const int32_t *col_t,
+                                float one_plus_eps, const float *z2, const float *stat,
+                                int64_t n_nodes, int32_t training, float *dy, float *dgamma,
+                                float *dbeta, float *coef, float *bn_ws, uint32_t *counters,
+                                const int32_t *dims, int32_t defer, const scgib_slab_job *fold,
+                                scgib_stream_t stream);
 /* layer backward: `pending` (NULL: coef is read) finishes the deferred
  * scgib_gin_bwd_stats_bn of the same layer (coef may then be NULL). */
 int scgib_gin_layer0_bwd(const float *dy, const float *z2, const float *r, const float *agg,

@@ -78,6 +78,8 @@ SIGNATURES = {
                                               _P, _I32, _P]),
     "scgib_gin_bwd_stats_bn": (ctypes.c_int, [_P, _P, _P, _F, _P, _P, _I64, _I32, _P, _P, _P, _P,
                                               _P, _P, _P, _I32, _P]),
+    "scgib_gin_bwd_stats_bn_fold": (ctypes.c_int, [_P, _P, _P, _F, _P, _P, _I64, _I32, _P, _P,
+                                                   _P, _P, _P, _P, _P, _I32, _P, _P]),
     "scgib_gin_bwd_slabs": (_I64, [_I64]),
     "scgib_gin_layer_bwd_slabs": (_I64, [_I64, _I32]),
     "scgib_slab_reduce": (ctypes.c_int, [_P, _I32, _I64, _P, _P]),

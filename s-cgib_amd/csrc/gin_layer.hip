@@ -836,15 +836,55 @@ __global__ __launch_bounds__(256) void bn_relu_apply_k(const float4 *__restrict_
 // SEG: dh[v] = (dh ? dh[v] : 0) + g_seg[seg[v]] — the encoder output feeds a
 // segment-sum readout (dgl.sum_nodes) whose gradient is broadcast here
 // instead of by a separate segment_broadcast launch.
+// The previous layer's weight-gradient slab reduce folded into this launch:
+// workgroups past the tile grid each sum one 64-column block of `fold`
+// (every slab, fixed order: partition p = tid >> 6 of 4 takes slabs p, p + 4,
+// ... in fp32 with 16 loads in flight, then the 4 partials in order in fp64).
+// The stats tiles wait on gathers and leave HBM bandwidth idle; the reduce
+// fills it, and the chain loses a separate reduce launch at its end.
+constexpr int kFoldCols = 64;
+
+__host__ __device__ inline int slab_fold_blocks(const scgib_slab_job &J) {
+    return J.n_slabs > 0 ? static_cast<int>((J.width + kFoldCols - 1) / kFoldCols) : 0;
+}
+
+__device__ __forceinline__ void slab_fold_block(const scgib_slab_job &J, int b, float *red) {
+    const int el = threadIdx.x & 63, sp = threadIdx.x >> 6;
+    const int64_t e = static_cast<int64_t>(b) * kFoldCols + el;
+    const int64_t stride = J.stride > 0 ? J.stride : J.width;
+    const int64_t ec = e < J.width ? e : J.width - 1;  // clamped: loads stay unconditional
+    float acc = 0.f;
+    for (int b0 = sp; b0 < J.n_slabs; b0 += 4 * 16) {
+        float v[16];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {
+            const int sb = b0 + 4 * u;
+            v[u] = J.slab[static_cast<int64_t>(sb < J.n_slabs ? sb : sp) * stride + ec];
+        }
+#pragma unroll
+        for (int u = 0; u < 16; ++u) acc += b0 + 4 * u < J.n_slabs ? v[u] : 0.f;
+    }
+    red[sp * 64 + el] = acc;
+    __syncthreads();
+    if (sp == 0 && e < J.width)
+        J.out[e] = static_cast<float>(((static_cast<double>(red[el]) + red[64 + el]) + red[128 + el]) +
+                                      red[192 + el]);
+}
+
 template <bool GATHER, bool SEG = false>
 __global__ __launch_bounds__(256) void gin_bwd_stats_k(
     const float *__restrict__ dh, const int32_t *__restrict__ rowptr_t,
     const int32_t *__restrict__ col_t, float ope, const float *__restrict__ z2,
     const float *__restrict__ stat, int64_t ncap, float *__restrict__ dy_out,
     float *__restrict__ part, const int32_t *__restrict__ dims, BnBwdFuse bz,
-    const float *__restrict__ g_seg, const int32_t *__restrict__ seg) {
+    const float *__restrict__ g_seg, const int32_t *__restrict__ seg, scgib_slab_job fold) {
     static_assert(!(GATHER && SEG), "segment broadcast only on the dense input path");
     __shared__ float sRed[2][16][64];
+    const int64_t ntile = (ncap + TM - 1) / TM;
+    if (static_cast<int64_t>(blockIdx.x) >= ntile) {  // block-uniform: a folded reduce block
+        slab_fold_block(fold, static_cast<int>(blockIdx.x - ntile), &sRed[0][0][0]);
+        return;
+    }
     const int64_t n = eff_count(dims, 0, ncap);
     const int tid = threadIdx.x, c = tid & 15, slot = tid >> 4;
     const int64_t tile = blockIdx.x, row0 = tile * TM;
@@ -1942,15 +1982,22 @@ static int launch_gin_bwd_stats(const float *dh, const int32_t *rowptr_t, const 
                                 float one_plus_eps, const float *z2, const float *stat,
                                 int64_t n_nodes, float *dy, float *tile_stats,
                                 const int32_t *dims, const BnBwdFuse &bz, hipStream_t st,
-                                const float *g_seg = nullptr, const int32_t *seg = nullptr) {
-    const int64_t nt = scgib_gin_tiles(n_nodes);
+                                const float *g_seg = nullptr, const int32_t *seg = nullptr,
+                                const scgib_slab_job *fold = nullptr) {
+    const scgib_slab_job fj = fold ? *fold : scgib_slab_job{};
+    const unsigned grid = static_cast<unsigned>(scgib_gin_tiles(n_nodes) + slab_fold_blocks(fj));
     if (rowptr_t)
-        gin_bwd_stats_k<true><<<dim3((unsigned)nt), 256, 0, st>>>(dh, rowptr_t, col_t, one_plus_eps, z2, stat, n_nodes, dy, tile_stats, dims, bz, nullptr, nullptr);
+        gin_bwd_stats_k<true><<<dim3(grid), 256, 0, st>>>(dh, rowptr_t, col_t, one_plus_eps, z2, stat, n_nodes, dy, tile_stats, dims, bz, nullptr, nullptr, fj);
     else if (g_seg)
-        gin_bwd_stats_k<false, true><<<dim3((unsigned)nt), 256, 0, st>>>(dh, rowptr_t, col_t, one_plus_eps, z2, stat, n_nodes, dy, tile_stats, dims, bz, g_seg, seg);
+        gin_bwd_stats_k<false, true><<<dim3(grid), 256, 0, st>>>(dh, rowptr_t, col_t, one_plus_eps, z2, stat, n_nodes, dy, tile_stats, dims, bz, g_seg, seg, fj);
     else
-        gin_bwd_stats_k<false><<<dim3((unsigned)nt), 256, 0, st>>>(dh, rowptr_t, col_t, one_plus_eps, z2, stat, n_nodes, dy, tile_stats, dims, bz, nullptr, nullptr);
+        gin_bwd_stats_k<false><<<dim3(grid), 256, 0, st>>>(dh, rowptr_t, col_t, one_plus_eps, z2, stat, n_nodes, dy, tile_stats, dims, bz, nullptr, nullptr, fj);
     return launch_status();
+}
+
+static bool fold_ok(const scgib_slab_job *f) {
+    return !f || (f->n_slabs > 0 && f->width > 0 && f->slab && f->out &&
+                  (f->stride == 0 || f->stride >= f->width));
 }
 
 extern "C" int scgib_gin_bwd_stats(const float *dh, const int32_t *rowptr_t,
@@ -1967,19 +2014,33 @@ extern "C" int scgib_gin_bwd_stats(const float *dh, const int32_t *rowptr_t,
                                 tile_stats, dims, bz, as_stream(stream));
 }
 
+extern "C" int scgib_gin_bwd_stats_bn_fold(const float *dh, const int32_t *rowptr_t,
+                                           const int32_t *col_t, float one_plus_eps,
+                                           const float *z2, const float *stat, int64_t n_nodes,
+                                           int32_t training, float *dy, float *dgamma,
+                                           float *dbeta, float *coef, float *bn_ws,
+                                           uint32_t *counters, const int32_t *dims,
+                                           int32_t defer, const scgib_slab_job *fold,
+                                           scgib_stream_t stream) {
+    if (n_nodes <= 0 || !dh || !z2 || !stat || !dy || !bn_ws || !counters) return SCGIB_EINVAL;
+    if (!defer && (!dgamma || !dbeta || !coef)) return SCGIB_EINVAL;
+    if ((rowptr_t == nullptr) != (col_t == nullptr)) return SCGIB_EINVAL;
+    if (!fold_ok(fold)) return SCGIB_EINVAL;
+    BnBwdFuse bz{counters, bn_gpart(bn_ws, n_nodes), dgamma, dbeta, coef, training,
+                 static_cast<int>(bn_groups(n_nodes)), defer ? 1 : 0};
+    return launch_gin_bwd_stats(dh, rowptr_t, col_t, one_plus_eps, z2, stat, n_nodes, dy, bn_ws,
+                                dims, bz, as_stream(stream), nullptr, nullptr, fold);
+}
+
 extern "C" int scgib_gin_bwd_stats_bn(const float *dh, const int32_t *rowptr_t,
                                       const int32_t *col_t, float one_plus_eps, const float *z2,
                                       const float *stat, int64_t n_nodes, int32_t training,
                                       float *dy, float *dgamma, float *dbeta, float *coef,
                                       float *bn_ws, uint32_t *counters, const int32_t *dims,
                                       int32_t defer, scgib_stream_t stream) {
-    if (n_nodes <= 0 || !dh || !z2 || !stat || !dy || !bn_ws || !counters) return SCGIB_EINVAL;
-    if (!defer && (!dgamma || !dbeta || !coef)) return SCGIB_EINVAL;
-    if ((rowptr_t == nullptr) != (col_t == nullptr)) return SCGIB_EINVAL;
-    BnBwdFuse bz{counters, bn_gpart(bn_ws, n_nodes), dgamma, dbeta, coef, training,
-                 static_cast<int>(bn_groups(n_nodes)), defer ? 1 : 0};
-    return launch_gin_bwd_stats(dh, rowptr_t, col_t, one_plus_eps, z2, stat, n_nodes, dy, bn_ws,
-                                dims, bz, as_stream(stream));
+    return scgib_gin_bwd_stats_bn_fold(dh, rowptr_t, col_t, one_plus_eps, z2, stat, n_nodes,
+                                       training, dy, dgamma, dbeta, coef, bn_ws, counters, dims,
+                                       defer, nullptr, stream);
 }
 
 extern "C" int scgib_gin_bwd_stats_seg_bn(const float *dh, const float *g_seg,

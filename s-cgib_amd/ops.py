@@ -55,6 +55,10 @@ RU_ASIDE = os.environ.get("SCGIB_RU_ASIDE", "1") != "0"
 # encoder backward: all layers' weight-gradient slabs reduced by one launch at
 # the end (scgib_slab_reduce_multi) instead of one launch per layer
 BATCH_SLABS = os.environ.get("SCGIB_BATCH_SLABS", "1") != "0"
+# layer l's weight-gradient slab reduce folded into layer l-1's backward
+# statistics launch (extra workgroups, scgib_gin_bwd_stats_bn_fold) instead of
+# the chain's final reduce launch; only layer 0's slabs are left for the end
+FOLD_SLABS = os.environ.get("SCGIB_FOLD_SLABS", "1") != "0"
 # encoder-pair backward: capture the ego chain before the core chain (off:
 # measured 2 % slower — the replayed graph's queue assignment follows capture
 # order in ways that favour the core chain first)
@@ -471,6 +475,7 @@ class _GinEncoder(torch.autograd.Function):
         dagg_next, dwt = None, None
         nslab = int(_lib.query("scgib_gin_bwd_slabs", n))
         jobs, keep = [], []
+        fold = None  # the previous layer's slab job, reduced by the next stats launch
         for l in reversed(range(L)):
             agg, r, z2, stat = saved[4 * l: 4 * l + 4]
             w1, _, w2 = params[6 * l], params[6 * l + 1], params[6 * l + 2]
@@ -490,11 +495,12 @@ class _GinEncoder(torch.autograd.Function):
                           _p(stat), n, int(ctx.training), _p(dy), _p(bn_g[0]), _p(bn_g[1]),
                           _p(coef), _p(bn_ws), _p(cnt), _p(gr.dims), defer, st)
             else:
-                _launch("scgib_gin_bwd_stats_bn", {"n": n, "e": gr.edge_capacity(), "d_in": HIDDEN},
+                _launch("scgib_gin_bwd_stats_bn_fold", {"n": n, "e": gr.edge_capacity(), "d_in": HIDDEN},
                         _p(dagg_next), _p(gr.rowptr_t),
-                          _p(gr.col_t), ctx.opes[l + 1], _p(z2), _p(stat), n, int(ctx.training),
-                          _p(dy), _p(bn_g[0]), _p(bn_g[1]), _p(coef), _p(bn_ws), _p(cnt),
-                          _p(gr.dims), defer, st)
+                        _p(gr.col_t), ctx.opes[l + 1], _p(z2), _p(stat), n, int(ctx.training),
+                        _p(dy), _p(bn_g[0]), _p(bn_g[1]), _p(coef), _p(bn_ws), _p(cnt),
+                        _p(gr.dims), defer, _byref(fold), st)
+                fold = None
             bpend = _lib.BnBwdPending(gpart, bn_g[0].data_ptr(), bn_g[1].data_ptr(),
                                       int(ctx.training)) if defer else None
             meta = {"n": n, "e": gr.edge_capacity(), "d_in": d_in}
@@ -532,10 +538,14 @@ class _GinEncoder(torch.autograd.Function):
                 used = HIDDEN * HIDDEN + HIDDEN * d_in + 2 * HIDDEN + 32 * ctx.n_feat
                 jobs.append(_lib.SlabJob(slab.data_ptr(), wgrad.data_ptr(), used, nslab, width))
                 keep.append(slab)
-            elif BATCH_SLABS:  # reduced together after the last layer (one launch)
+            elif BATCH_SLABS:  # reduced by the next stats launch, or together at the end
                 ns = int(_lib.query("scgib_gin_layer_bwd_slabs", n, d_in))
-                jobs.append(_lib.SlabJob(slab.data_ptr(), wgrad.data_ptr(), width, ns, 0))
+                job = _lib.SlabJob(slab.data_ptr(), wgrad.data_ptr(), width, ns, 0)
                 keep.append(slab)
+                if FOLD_SLABS and l > 0:
+                    fold = job
+                else:
+                    jobs.append(job)
             else:
                 ns = int(_lib.query("scgib_gin_layer_bwd_slabs", n, d_in))
                 _lib.call("scgib_slab_reduce", _p(slab), ns, width, _p(wgrad), st)

@@ -29,6 +29,7 @@ PHASES = {
     "scgib_gin_layer_bwd": ["prologue", "dz2", "pairA", "pairB", "rest", "slab"],
     "scgib_gin_layer0_bwd": ["ld+dz2", "dW2,dr", "dW1,dagg", "slab"],
     "scgib_gin_bwd_stats_bn": ["gather+dy", "bn_hier"],
+    "scgib_gin_bwd_stats_bn_fold": ["gather+dy", "bn_hier"],
 }
 MAXB = 4096
 

@@ -212,72 +212,139 @@ __device__ __forceinline__ void contrast_fwd_body(const ContrastArgs &a, int64_t
     }
 }
 
-// backward body: sK1, sK2 >= CT * CLD floats, sWf >= 3 * CR * (CT + 1), sDj >= CT
-constexpr int kContrastBwdW = 3 * CR * (CT + 1);
+// backward body: sK1, sK2 >= CT * CLD floats, sWf >= 3 * CR * CLD, sDj unused.
+//
+// The similarity blocks and the weighted sums are matrix products, run on
+// the f32 MFMA v_mfma_f32_16x16x4_f32 (wave w takes columns 16w.. of each
+// 64-column tile for the similarities and channels 16w.. for the sums):
+//   S11 = Q1 K1^T, S12 = Q1 K2^T, S21 = Q2 K1^T   (16 x 64 per tile, K = 64)
+//   d1 += W11 K1 + W12 K2,  d2 += W21 K1          (16 x 64, K = the tile's 64 j)
+// with the weights W formed on the S accumulators and passed through LDS.
+// Each lane feeds four k values per ds_read_b128 (the k order of every sum
+// permuted identically for both operands, kperm16).  The earlier form (one
+// 64-long dependent VALU fma chain per dot product, one wave per SIMD inside
+// the head MLP's launch) took ~25 us per workgroup at B = 512 (phase trace).
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+constexpr int kContrastBwdW = 3 * CR * CLD;
+
+__device__ __forceinline__ int kperm16(int s, int kq) { return 16 * (s >> 2) + 4 * kq + (s & 3); }
+__device__ __forceinline__ float f4c(const float4 &v, int t) {
+    return t == 0 ? v.x : t == 1 ? v.y : t == 2 ? v.z : v.w;
+}
+
+// lane (row li, k quarter kq): the row's normalised values at kperm16(s, kq)
+__device__ __forceinline__ void load_row_k(const float *__restrict__ x, int64_t i, int64_t B,
+                                           int kq, float (&q)[16]) {
+    const int64_t ic = i < B ? i : 0;
+    const float m = i < B ? 1.f : 0.f;
+    float4 v[4];
+    float ss = 0.f;
+#pragma unroll
+    for (int mm = 0; mm < 4; ++mm) {
+        v[mm] = *reinterpret_cast<const float4 *>(x + ic * 64 + 16 * mm + 4 * kq);
+        ss += v[mm].x * v[mm].x + v[mm].y * v[mm].y + v[mm].z * v[mm].z + v[mm].w * v[mm].w;
+    }
+    ss += __shfl_xor(ss, 16, kWave);
+    ss += __shfl_xor(ss, 32, kWave);
+    const float inv = m / fmaxf(sqrtf(ss), kNormEps);
+#pragma unroll
+    for (int s = 0; s < 16; ++s) q[s] = f4c(v[s >> 2], s & 3) * inv;
+}
+
 __device__ __forceinline__ void contrast_bwd_body(const ContrastArgs &a, int64_t bx, int by,
                                                   float *sK1, float *sK2, float *sWf,
-                                                  float *sDj) {
+                                                  float * /*sDj*/) {
     const float *__restrict__ z1 = a.z1, *__restrict__ z2 = a.z2;
     const int64_t B = a.B;
     const float *__restrict__ ws = a.ws;
     float *__restrict__ dz1 = a.dz1, *__restrict__ dz2 = a.dz2;
     unsigned *counters = a.counters;
-    auto sW = reinterpret_cast<float (*)[CR][CT + 1]>(sWf);
-    const int tid = threadIdx.x, r = tid >> 4, cl = tid & 15;
+    const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, li = l & 15, kq = l >> 4;
     const int NS = a.nsplit;
-    const int64_t i = bx * CR + r;
+    const int64_t row0 = bx * CR;
     const float g = *a.g_loss / static_cast<float>(B);
     const float *Dv = ws;
     float *pb = a.ws + B + static_cast<int64_t>(contrast_splits(B)) * B * 4;
-    float4 q1[16], q2[16];
-    const float inv1 = load_row(z1, i, B, q1);
-    const float inv2 = load_row(z2, i, B, q2);
-    const float invDi = i < B ? 1.f / Dv[i] : 0.f;
-    float4 d1 = make_float4(0.f, 0.f, 0.f, 0.f), d2 = d1;
+    float q1[16], q2[16];  // A operands: row row0 + li, k = kperm16(s, kq)
+    load_row_k(z1, row0 + li, B, kq, q1);
+    load_row_k(z2, row0 + li, B, kq, q2);
+    float invDi[4];        // output rows 4 kq + r
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const int64_t i = row0 + 4 * kq + r;
+        invDi[r] = i < B ? 1.f / Dv[i] : 0.f;
+    }
+    float *sW = sWf;  // [3][CR][CLD]: W11, W12, W21
+    f32x4 d1 = {0.f, 0.f, 0.f, 0.f}, d2 = d1;  // rows 4 kq + r, channel 16 w + li
     for (int64_t j0 = static_cast<int64_t>(by) * CT; j0 < B; j0 += static_cast<int64_t>(NS) * CT) {
+        const int64_t j = j0 + 16 * w + li;  // this lane's similarity column
+        const float invDj = j < B ? 1.f / Dv[j] : 0.f;
         __syncthreads();
         stage_tile(z1, B, j0, sK1);
         stage_tile(z2, B, j0, sK2);
-        if (tid < CT) sDj[tid] = j0 + tid < B ? Dv[j0 + tid] : 1.f;
         __syncthreads();
+        f32x4 s11 = {0.f, 0.f, 0.f, 0.f}, s12 = s11, s21 = s11;
+        const float *pk1 = sK1 + (16 * w + li) * CLD + 4 * kq, *pk2 = sK2 + (16 * w + li) * CLD + 4 * kq;
 #pragma unroll
-        for (int cc = 0; cc < CT / 16; ++cc) {
-            const int jj = cl + 16 * cc;
-            const int64_t j = j0 + jj;
-            float w11 = 0.f, w12 = 0.f, w21 = 0.f;
-            if (j < B && i < B) {
-                const float invDj = 1.f / sDj[jj];
-                const float e11 = expf(dot_row(q1, sK1 + jj * CLD));
-                const float e12 = expf(dot_row(q1, sK2 + jj * CLD));
-                const float e21 = expf(dot_row(q2, sK1 + jj * CLD));
-                const float delta = j == i ? 1.f : 0.f;
-                w11 = j == i ? 0.f : g * e11 * (invDi + invDj);
-                w12 = g * (e12 * invDi - delta);
-                w21 = g * (e21 * invDj - delta);
+        for (int mm = 0; mm < 4; ++mm) {
+            const float4 b1 = *reinterpret_cast<const float4 *>(pk1 + 16 * mm);
+            const float4 b2 = *reinterpret_cast<const float4 *>(pk2 + 16 * mm);
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                const int s = 4 * mm + t;
+                s11 = __builtin_amdgcn_mfma_f32_16x16x4f32(q1[s], f4c(b1, t), s11, 0, 0, 0);
+                s12 = __builtin_amdgcn_mfma_f32_16x16x4f32(q1[s], f4c(b2, t), s12, 0, 0, 0);
+                s21 = __builtin_amdgcn_mfma_f32_16x16x4f32(q2[s], f4c(b1, t), s21, 0, 0, 0);
             }
-            sW[0][r][jj] = w11;
-            sW[1][r][jj] = w12;
-            sW[2][r][jj] = w21;
+        }
+        // weights at (row 4 kq + r, column 16 w + li of the tile)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int64_t i = row0 + 4 * kq + r;
+            const bool ok = i < B && j < B;
+            const float delta = j == i ? 1.f : 0.f;
+            const float e11 = expf(s11[r]), e12 = expf(s12[r]), e21 = expf(s21[r]);
+            const int o = (4 * kq + r) * CLD + 16 * w + li;
+            sW[o] = ok && j != i ? g * e11 * (invDi[r] + invDj) : 0.f;
+            sW[CR * CLD + o] = ok ? g * (e12 * invDi[r] - delta) : 0.f;
+            sW[2 * CR * CLD + o] = ok ? g * (e21 * invDj - delta) : 0.f;
         }
         __syncthreads();
-#pragma unroll 4
-        for (int jj = 0; jj < CT; ++jj) {
-            const float w11 = sW[0][r][jj], w12 = sW[1][r][jj], w21 = sW[2][r][jj];
-            const float4 k1 = *reinterpret_cast<const float4 *>(sK1 + jj * CLD + 4 * cl);
-            const float4 k2 = *reinterpret_cast<const float4 *>(sK2 + jj * CLD + 4 * cl);
-            d1.x += w11 * k1.x + w12 * k2.x; d1.y += w11 * k1.y + w12 * k2.y;
-            d1.z += w11 * k1.z + w12 * k2.z; d1.w += w11 * k1.w + w12 * k2.w;
-            d2.x += w21 * k1.x; d2.y += w21 * k1.y; d2.z += w21 * k1.z; d2.w += w21 * k1.w;
+        // d1 += W11 K1 + W12 K2, d2 += W21 K1 over the tile's 64 columns j
+        const float *pw = sW + li * CLD + 4 * kq;
+        const float *pc1 = sK1 + 16 * w + li, *pc2 = sK2 + 16 * w + li;
+#pragma unroll
+        for (int mm = 0; mm < 4; ++mm) {
+            const float4 w11 = *reinterpret_cast<const float4 *>(pw + 16 * mm);
+            const float4 w12 = *reinterpret_cast<const float4 *>(pw + CR * CLD + 16 * mm);
+            const float4 w21 = *reinterpret_cast<const float4 *>(pw + 2 * CR * CLD + 16 * mm);
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                const int jj = kperm16(4 * mm + t, kq);
+                const float k1 = pc1[jj * CLD], k2 = pc2[jj * CLD];
+                d1 = __builtin_amdgcn_mfma_f32_16x16x4f32(f4c(w11, t), k1, d1, 0, 0, 0);
+                d2 = __builtin_amdgcn_mfma_f32_16x16x4f32(f4c(w21, t), k1, d2, 0, 0, 0);
+                d1 = __builtin_amdgcn_mfma_f32_16x16x4f32(f4c(w12, t), k2, d1, 0, 0, 0);
+            }
         }
     }
-    if (i < B) {
-        float *p = pb + (static_cast<int64_t>(by) * B + i) * 128;
-        st_agent4(p + 4 * cl, d1);
-        st_agent4(p + 64 + 4 * cl, d2);
+    // this split's partial rows -> [split][B][128] (d1 | d2)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const int64_t i = row0 + 4 * kq + r;
+        if (i < B) {
+            float *p = pb + (static_cast<int64_t>(by) * B + i) * 128 + 16 * w + li;
+            st_agent(p, d1[r]);
+            st_agent(p + 64, d2[r]);
+        }
     }
     if (!block_arrive(counters + bx, NS)) return;
+    // last split of the row block: fixed-order sum over the splits, then the
+    // normalisation backward; row r = tid >> 4, channels 4 cl .. 4 cl + 3
+    const int r = tid >> 4, cl = tid & 15;
+    const int64_t i = row0 + r;
     if (i < B) {
-        d1 = d2 = make_float4(0.f, 0.f, 0.f, 0.f);
+        float4 e1 = make_float4(0.f, 0.f, 0.f, 0.f), e2 = e1;
         float4 v1[kMaxSplit], v2[kMaxSplit];
 #pragma unroll
         for (int y = 0; y < kMaxSplit; ++y) {  // all splits in flight (clamped), summed in order
@@ -287,27 +354,29 @@ __device__ __forceinline__ void contrast_bwd_body(const ContrastArgs &a, int64_t
         }
 #pragma unroll
         for (int y = 0; y < kMaxSplit; ++y) {
-            const float w = y < NS ? 1.f : 0.f;
-            d1.x = fmaf(v1[y].x, w, d1.x); d1.y = fmaf(v1[y].y, w, d1.y);
-            d1.z = fmaf(v1[y].z, w, d1.z); d1.w = fmaf(v1[y].w, w, d1.w);
-            d2.x = fmaf(v2[y].x, w, d2.x); d2.y = fmaf(v2[y].y, w, d2.y);
-            d2.z = fmaf(v2[y].z, w, d2.z); d2.w = fmaf(v2[y].w, w, d2.w);
+            const float wy = y < NS ? 1.f : 0.f;
+            e1.x = fmaf(v1[y].x, wy, e1.x); e1.y = fmaf(v1[y].y, wy, e1.y);
+            e1.z = fmaf(v1[y].z, wy, e1.z); e1.w = fmaf(v1[y].w, wy, e1.w);
+            e2.x = fmaf(v2[y].x, wy, e2.x); e2.y = fmaf(v2[y].y, wy, e2.y);
+            e2.z = fmaf(v2[y].z, wy, e2.z); e2.w = fmaf(v2[y].w, wy, e2.w);
         }
-        // this lane's channels of the normalised rows
-        float4 a1 = q1[0], a2 = q2[0];
-#pragma unroll
-        for (int k = 1; k < 16; ++k)
-            if (k == cl) { a1 = q1[k]; a2 = q2[k]; }
-        const float p1 = sum16(a1.x * d1.x + a1.y * d1.y + a1.z * d1.z + a1.w * d1.w);
-        const float p2 = sum16(a2.x * d2.x + a2.y * d2.y + a2.z * d2.z + a2.w * d2.w);
+        // this lane's channels of the normalised rows and the row norms
+        const float4 x1 = reinterpret_cast<const float4 *>(z1 + i * 64)[cl];
+        const float4 x2 = reinterpret_cast<const float4 *>(z2 + i * 64)[cl];
+        const float inv1 = 1.f / fmaxf(sqrtf(sum16(x1.x * x1.x + x1.y * x1.y + x1.z * x1.z + x1.w * x1.w)), kNormEps);
+        const float inv2 = 1.f / fmaxf(sqrtf(sum16(x2.x * x2.x + x2.y * x2.y + x2.z * x2.z + x2.w * x2.w)), kNormEps);
+        const float4 a1 = make_float4(x1.x * inv1, x1.y * inv1, x1.z * inv1, x1.w * inv1);
+        const float4 a2 = make_float4(x2.x * inv2, x2.y * inv2, x2.z * inv2, x2.w * inv2);
+        const float p1 = sum16(a1.x * e1.x + a1.y * e1.y + a1.z * e1.z + a1.w * e1.w);
+        const float p2 = sum16(a2.x * e2.x + a2.y * e2.y + a2.z * e2.z + a2.w * e2.w);
         const float s1 = inv1 < 1.f / kNormEps ? p1 : 0.f;  // |z| <= eps: z / eps, no projection
         const float s2 = inv2 < 1.f / kNormEps ? p2 : 0.f;
         reinterpret_cast<float4 *>(dz1 + i * 64)[cl] =
-            make_float4((d1.x - a1.x * s1) * inv1, (d1.y - a1.y * s1) * inv1,
-                        (d1.z - a1.z * s1) * inv1, (d1.w - a1.w * s1) * inv1);
+            make_float4((e1.x - a1.x * s1) * inv1, (e1.y - a1.y * s1) * inv1,
+                        (e1.z - a1.z * s1) * inv1, (e1.w - a1.w * s1) * inv1);
         reinterpret_cast<float4 *>(dz2 + i * 64)[cl] =
-            make_float4((d2.x - a2.x * s2) * inv2, (d2.y - a2.y * s2) * inv2,
-                        (d2.z - a2.z * s2) * inv2, (d2.w - a2.w * s2) * inv2);
+            make_float4((e2.x - a2.x * s2) * inv2, (e2.y - a2.y * s2) * inv2,
+                        (e2.z - a2.z * s2) * inv2, (e2.w - a2.w * s2) * inv2);
     }
     if (tid == 0) counters[bx] = 0u;
 }

@@ -5,15 +5,15 @@
 namespace scgib {
 
 __global__ __launch_bounds__(256) void contrast_fwd_k(ContrastArgs a) {
-    __shared__ float sK1[CT * CLD];
-    __shared__ float sK2[CT * CLD];
+    __shared__ __attribute__((aligned(16))) float sK1[CT * CLD];
+    __shared__ __attribute__((aligned(16))) float sK2[CT * CLD];
     contrast_fwd_body(a, blockIdx.x, blockIdx.y, sK1, sK2);
 }
 
 __global__ __launch_bounds__(256) void contrast_bwd_k(ContrastArgs a) {
-    __shared__ float sK1[CT * CLD];
-    __shared__ float sK2[CT * CLD];
-    __shared__ float sW[kContrastBwdW];
+    __shared__ __attribute__((aligned(16))) float sK1[CT * CLD];
+    __shared__ __attribute__((aligned(16))) float sK2[CT * CLD];
+    __shared__ __attribute__((aligned(16))) float sW[kContrastBwdW];
     __shared__ float sDj[CT];
     contrast_bwd_body(a, blockIdx.x, blockIdx.y, sK1, sK2, sW, sDj);
 }

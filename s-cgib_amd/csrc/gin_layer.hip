@@ -499,8 +499,8 @@ __global__ __launch_bounds__(256) void gin_fwd_k(
     static_assert(!RECON || !GATHER, "the recon Gram partial is fused into the dense head MLP");
     static_assert(!PRE || DIN == 32, "transfer_d fold produces the 32-wide layer-0 input");
     const int64_t n = eff_count(dims, 0, ncap);
-    __shared__ float sA[TM * LDA];
-    __shared__ float sW1[64 * LDA];
+    __shared__ __attribute__((aligned(16))) float sA[TM * LDA];   // (contrastive: float4 tiles)
+    __shared__ __attribute__((aligned(16))) float sW1[64 * LDA];
     __shared__ float sW2[64 * LDH];
     __shared__ float sR[TM * LDH];
     __shared__ float sRed[2][64];
@@ -509,7 +509,9 @@ __global__ __launch_bounds__(256) void gin_fwd_k(
         static_assert(TM * LDA >= CT * CLD, "contrastive tiles in sA / sW1");
         if (rec.con.B > 0 && static_cast<int>(blockIdx.x) >= rec.con.nmain) {  // block-uniform
             const int64_t b = blockIdx.x - rec.con.nmain, nrb = contrast_row_blocks(rec.con.B);
+            SCGIB_MARK(0);
             contrast_fwd_body(rec.con, b % nrb, static_cast<int>(b / nrb), sA, sW1);
+            SCGIB_MARK(5);
             return;
         }
     }
@@ -1037,10 +1039,11 @@ __global__ __launch_bounds__(256, (DIN <= 64 && !RECON ? SCGIB_BWD_MINB : 1)) vo
     // r is dead once dz1 is formed, so the agg tile reuses its buffer: 66.5 KB
     // for DIN <= 64, two workgroups per CU (loads of one overlap the other's MFMA)
     constexpr int RA = (LDA > LDH ? LDA : LDH);
-    __shared__ float sD[TM * LDH];   // dz2, then dz1
-    __shared__ float sRA[TM * RA];   // r, then agg
-    __shared__ float sW1[64 * LDA];
-    __shared__ float sW2[64 * LDH];
+    // 16-byte aligned: the contrastive workgroups read them by ds_read_b128
+    __shared__ __attribute__((aligned(16))) float sD[TM * LDH];   // dz2, then dz1
+    __shared__ __attribute__((aligned(16))) float sRA[TM * RA];   // r, then agg
+    __shared__ __attribute__((aligned(16))) float sW1[64 * LDA];
+    __shared__ __attribute__((aligned(16))) float sW2[64 * LDH];
     __shared__ float sG[RECON ? 64 * LDH : 1];  // Gram matrix of the recon loss
     float *const sR = sRA, *const sA = sRA;
     unsigned gsz = gridDim.x;  // workgroups of the tile loop
@@ -1051,7 +1054,9 @@ __global__ __launch_bounds__(256, (DIN <= 64 && !RECON ? SCGIB_BWD_MINB : 1)) vo
             gsz = static_cast<unsigned>(rec.con.nmain);
             if (blockIdx.x >= gsz) {  // block-uniform
                 const int64_t b = blockIdx.x - gsz, nrb = contrast_row_blocks(rec.con.B);
+                SCGIB_MARK(0);
                 contrast_bwd_body(rec.con, b % nrb, static_cast<int>(b / nrb), sRA, sW1, sD, sW2);
+                SCGIB_MARK(5);
                 return;
             }
         }

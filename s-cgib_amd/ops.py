@@ -1238,7 +1238,8 @@ class _Mlp2ReconContrastive(torch.autograd.Function):
         closs = torch.empty((), dtype=torch.float32, device=dev)
         cnt = counters(dev, "mlp2_recon", 1)
         ccnt = counters(dev, "contrastive", int(_lib.query("scgib_contrastive_counters", B)))
-        _lib.call("scgib_mlp2_recon_contrastive_fwd", _p(x), d_in, n, _p(w1), _p(b1), _p(w2),
+        _launch("scgib_mlp2_recon_contrastive_fwd", {"n": n, "d_in": d_in, "B": B}, _p(x), d_in, n,
+                _p(w1), _p(b1), _p(w2),
                   _p(b2), _p(r), _p(out), _p(graph.rowptr), _p(graph.col),
                   graph.edge_capacity(), _p(ws), _p(cnt), _p(loss), _p(graph.dims), _p(z1),
                   _p(z2), B, _p(cws), _p(closs), _p(ccnt), _stream())
@@ -1265,7 +1266,8 @@ class _Mlp2ReconContrastive(torch.autograd.Function):
                          device=dev)
         ccnt = counters(dev, "contrastive", int(_lib.query("scgib_contrastive_counters", B)))
         sym = gr.symmetric
-        _lib.call("scgib_mlp2_recon_contrastive_bwd", _p(x), _p(r), _p(out), _p(ws), d_in,
+        _launch("scgib_mlp2_recon_contrastive_bwd", {"n": n, "d_in": d_in, "B": B}, _p(x), _p(r),
+                _p(out), _p(ws), d_in,
                   _p(w1), _p(w2), n, _p(gr.rowptr), _p(gr.col),
                   None if sym else _p(gr.rowptr_t), None if sym else _p(gr.col_t), _p(g_loss),
                   _p(dx), _p(slab), _p(wg), _p(gr.dims), _p(z1), _p(z2), B, _p(cws), _p(g_con),

@@ -30,6 +30,9 @@ PHASES = {
     "scgib_gin_layer0_bwd": ["ld+dz2", "dW2,dr", "dW1,dagg", "slab"],
     "scgib_gin_bwd_stats_bn": ["gather+dy", "bn_hier"],
     "scgib_gin_bwd_stats_bn_fold": ["gather+dy", "bn_hier"],
+    # head MLP (+ recon) tiles mark 1..3, the contrastive workgroups 5
+    "scgib_mlp2_recon_contrastive_fwd": ["load", "gemm1", "-", "-", "contrast"],
+    "scgib_mlp2_recon_contrastive_bwd": ["dz2(recon)", "dW2,dr,dz1", "dW1,dx", "-", "contrast"],
 }
 MAXB = 4096
 

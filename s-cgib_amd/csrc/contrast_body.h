@@ -10,9 +10,11 @@
 // B x B similarity blocks are formed on the fly and never stored.
 //
 // Grid: (row blocks of 16) x (NS column splits); a workgroup takes its rows
-// against the 64-row column tiles of its split.  The 16 query rows are held in
-// registers (one row per 16 lanes), the column tile is normalised into LDS
-// (stride 68: 16-byte reads of 16 different rows hit disjoint banks).
+// against the 64-row column tiles of its split.  The column tile is
+// normalised into LDS (stride 68: 16-byte reads of 16 different rows hit
+// disjoint banks); the similarity blocks and the backward's weighted sums
+// are f32 MFMA products (v_mfma_f32_16x16x4_f32, the query rows' operand
+// values held in registers, the tiles read by ds_read_b128).
 //   forward : per (row, split) partial (R, Bt, e11_ii, e12_ii); the last
 //             workgroup to arrive combines the splits in fixed order, writes
 //             D_i and the mean (fp64) -> deterministic.
@@ -45,53 +47,44 @@ __host__ __device__ inline int contrast_splits(int64_t B) {
 
 // Stage rows [j0, j0 + 64) of x, normalised, into s (64 x CLD); rows >= B are
 // zero.  256 threads: row tid >> 2, 16 channels per thread.
-__device__ __forceinline__ void stage_tile(const float *__restrict__ x, int64_t B, int64_t j0,
-                                           float *s) {
+// stage_tile in two halves, so the next tile's loads can be in flight while
+// the current one is computed on: tile_load (rows -> registers, rows >= B
+// zero), tile_store (normalise -> LDS).  256 threads: row tid >> 2, 16
+// channels per thread.
+struct TileRegs {
+    float4 v[4];
+};
+
+__device__ __forceinline__ void tile_load(const float *__restrict__ x, int64_t B, int64_t j0,
+                                          TileRegs &t) {
     const int tid = threadIdx.x, r = tid >> 2, q = tid & 3;
     const int64_t j = j0 + r;
-    float4 v[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+        t.v[k] = ld_ok(reinterpret_cast<const float4 *>(x), j * 16 + 4 * q + k, 4 * q + k, j < B,
+                       make_float4(0.f, 0.f, 0.f, 0.f));
+}
+
+__device__ __forceinline__ void tile_store(const TileRegs &t, float *s) {
+    const int tid = threadIdx.x, r = tid >> 2, q = tid & 3;
     float ss = 0.f;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        v[k] = ld_ok(reinterpret_cast<const float4 *>(x), j * 16 + 4 * q + k, 4 * q + k, j < B,
-                     make_float4(0.f, 0.f, 0.f, 0.f));
-        ss += v[k].x * v[k].x + v[k].y * v[k].y + v[k].z * v[k].z + v[k].w * v[k].w;
-    }
+    for (int k = 0; k < 4; ++k) ss += t.v[k].x * t.v[k].x + t.v[k].y * t.v[k].y + t.v[k].z * t.v[k].z + t.v[k].w * t.v[k].w;
     ss += __shfl_xor(ss, 1, kWave);
     ss += __shfl_xor(ss, 2, kWave);
     const float inv = 1.f / fmaxf(sqrtf(ss), kNormEps);
 #pragma unroll
     for (int k = 0; k < 4; ++k)
         *reinterpret_cast<float4 *>(s + r * CLD + 16 * q + 4 * k) =
-            make_float4(v[k].x * inv, v[k].y * inv, v[k].z * inv, v[k].w * inv);
+            make_float4(t.v[k].x * inv, t.v[k].y * inv, t.v[k].z * inv, t.v[k].w * inv);
 }
 
-// a whole normalised row in registers; returns 1 / max(|x|, eps)
-__device__ __forceinline__ float load_row(const float *__restrict__ x, int64_t i, int64_t B,
-                                          float4 (&q)[16]) {
-    float ss = 0.f;
-#pragma unroll
-    for (int k = 0; k < 16; ++k) {
-        q[k] = ld_ok(reinterpret_cast<const float4 *>(x), i * 16 + k, k, i < B, make_float4(0.f, 0.f, 0.f, 0.f));
-        ss += q[k].x * q[k].x + q[k].y * q[k].y + q[k].z * q[k].z + q[k].w * q[k].w;
-    }
-    const float inv = 1.f / fmaxf(sqrtf(ss), kNormEps);
-#pragma unroll
-    for (int k = 0; k < 16; ++k) q[k] = make_float4(q[k].x * inv, q[k].y * inv, q[k].z * inv, q[k].w * inv);
-    return inv;
-}
-
-__device__ __forceinline__ float dot_row(const float4 (&q)[16], const float *s) {
-    float acc = 0.f;
-#pragma unroll
-    for (int k = 0; k < 16; ++k) {
-        const float4 b = *reinterpret_cast<const float4 *>(s + 4 * k);
-        acc += q[k].x * b.x;
-        acc += q[k].y * b.y;
-        acc += q[k].z * b.z;
-        acc += q[k].w * b.w;
-    }
-    return acc;
+// Stage rows [j0, j0 + 64) of x, normalised, into s (64 x CLD); rows >= B are zero.
+__device__ __forceinline__ void stage_tile(const float *__restrict__ x, int64_t B, int64_t j0,
+                                           float *s) {
+    TileRegs t;
+    tile_load(x, B, j0, t);
+    tile_store(t, s);
 }
 
 // sum over the 16 lanes of a row group (lanes 16m .. 16m+15 of the wave)
@@ -101,8 +94,35 @@ __device__ __forceinline__ float sum16(float v) {
     return v;
 }
 
-// workspace (floats): D[B] | fwd partials [S][B][4] | bwd partials [S][B][128],
-// S = contrast_splits(B); a launch may use NS <= S splits.
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+constexpr int kContrastBwdW = 3 * CR * CLD;
+
+__device__ __forceinline__ int kperm16(int s, int kq) { return 16 * (s >> 2) + 4 * kq + (s & 3); }
+__device__ __forceinline__ float f4c(const float4 &v, int t) {
+    return t == 0 ? v.x : t == 1 ? v.y : t == 2 ? v.z : v.w;
+}
+
+// lane (row li, k quarter kq): the row's normalised values at kperm16(s, kq)
+__device__ __forceinline__ void load_row_k(const float *__restrict__ x, int64_t i, int64_t B,
+                                           int kq, float (&q)[16]) {
+    const int64_t ic = i < B ? i : 0;
+    const float m = i < B ? 1.f : 0.f;
+    float4 v[4];
+    float ss = 0.f;
+#pragma unroll
+    for (int mm = 0; mm < 4; ++mm) {
+        v[mm] = *reinterpret_cast<const float4 *>(x + ic * 64 + 16 * mm + 4 * kq);
+        ss += v[mm].x * v[mm].x + v[mm].y * v[mm].y + v[mm].z * v[mm].z + v[mm].w * v[mm].w;
+    }
+    ss += __shfl_xor(ss, 16, kWave);
+    ss += __shfl_xor(ss, 32, kWave);
+    const float inv = m / fmaxf(sqrtf(ss), kNormEps);
+#pragma unroll
+    for (int s = 0; s < 16; ++s) q[s] = f4c(v[s >> 2], s & 3) * inv;
+}
+
+// workspace (floats): D[B] | fwd partials [T][B][4] | bwd partials [S][B][128],
+// T = contrast_tiles(B), S = contrast_splits(B); a launch may use NS <= S splits.
 // The bodies take their workgroup's (row block bx, split by) and LDS buffers
 // from the caller, so a kernel of another op can run them in extra
 // workgroups (the head MLP: gin_layer.hip, ContrastArgs).
@@ -119,51 +139,95 @@ struct ContrastArgs {
 };
 
 __host__ __device__ inline int64_t contrast_row_blocks(int64_t B) { return (B + CR - 1) / CR; }
+// column tiles; the forward keeps one partial per (tile, row), so the loss
+// does not depend on how a launch splits the tiles over workgroups
+__host__ __device__ inline int64_t contrast_tiles(int64_t B) { return (B + CT - 1) / CT; }
+// workspace offset of the backward's split partials (after D and the
+// forward's tile partials)
+__host__ __device__ inline int64_t contrast_pb_offset(int64_t B) { return B + 4 * contrast_tiles(B) * B; }
 
-// forward body: sK1, sK2 >= CT * CLD floats each
+// forward body: sK1, sK2 >= CT * CLD floats each.  S11 = Q1 K1^T and
+// S12 = Q1 K2^T per 64-column tile on the f32 MFMA (as the backward: wave w
+// takes columns 16w.. of the tile, lanes hold rows 4 kq + r), their
+// exponentials summed per lane over the tiles, then over the 16 columns of
+// a wave (shuffles) and the 4 waves (LDS, fixed order).
 __device__ __forceinline__ void contrast_fwd_body(const ContrastArgs &a, int64_t bx, int by,
                                                   float *sK1, float *sK2) {
     const float *__restrict__ z1 = a.z1, *__restrict__ z2 = a.z2;
     const int64_t B = a.B;
     float *__restrict__ ws = a.ws;
-    const int tid = threadIdx.x, r = tid >> 4, cl = tid & 15;
+    const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, li = l & 15, kq = l >> 4;
     const int NS = a.nsplit;
-    const int64_t i = bx * CR + r;
-    float4 q[16];
-    load_row(z1, i, B, q);
-    float R = 0.f, Bt = 0.f, e12d = 0.f, e11d = 0.f;
-    for (int64_t j0 = static_cast<int64_t>(by) * CT; j0 < B; j0 += static_cast<int64_t>(NS) * CT) {
+    const int64_t row0 = bx * CR;
+    float q1[16];
+    load_row_k(z1, row0 + li, B, kq, q1);
+    float *Dv = ws, *pf = ws + B;
+    __shared__ float sPart[4][CR][4];
+    const int64_t jstep = static_cast<int64_t>(NS) * CT;
+    TileRegs t1, t2;  // the next tile's rows, in flight during this tile
+    if (static_cast<int64_t>(by) * CT < B) {
+        tile_load(z1, B, static_cast<int64_t>(by) * CT, t1);
+        tile_load(z2, B, static_cast<int64_t>(by) * CT, t2);
+    }
+    for (int64_t j0 = static_cast<int64_t>(by) * CT; j0 < B; j0 += jstep) {
         __syncthreads();
-        stage_tile(z1, B, j0, sK1);
-        stage_tile(z2, B, j0, sK2);
+        tile_store(t1, sK1);
+        tile_store(t2, sK2);
+        if (j0 + jstep < B) {
+            tile_load(z1, B, j0 + jstep, t1);
+            tile_load(z2, B, j0 + jstep, t2);
+        }
         __syncthreads();
+        f32x4 s11 = {0.f, 0.f, 0.f, 0.f}, s12 = s11;
+        const float *pk1 = sK1 + (16 * w + li) * CLD + 4 * kq, *pk2 = sK2 + (16 * w + li) * CLD + 4 * kq;
 #pragma unroll
-        for (int cc = 0; cc < CT / 16; ++cc) {
-            const int jj = cl + 16 * cc;
-            const int64_t j = j0 + jj;
-            if (j < B) {
-                const float e11 = expf(dot_row(q, sK1 + jj * CLD));
-                const float e12 = expf(dot_row(q, sK2 + jj * CLD));
-                R += e11;
-                Bt += e12;
-                if (j == i) { e11d = e11; e12d = e12; }
+        for (int mm = 0; mm < 4; ++mm) {
+            const float4 b1 = *reinterpret_cast<const float4 *>(pk1 + 16 * mm);
+            const float4 b2 = *reinterpret_cast<const float4 *>(pk2 + 16 * mm);
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                s11 = __builtin_amdgcn_mfma_f32_16x16x4f32(q1[4 * mm + t], f4c(b1, t), s11, 0, 0, 0);
+                s12 = __builtin_amdgcn_mfma_f32_16x16x4f32(q1[4 * mm + t], f4c(b2, t), s12, 0, 0, 0);
             }
         }
+        // (R, Bt, e11_ii, e12_ii) of this tile for rows 4 kq + r: over the
+        // wave's 16 columns (shuffles), then over the waves in order
+        const int64_t j = j0 + 16 * w + li;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int64_t i = row0 + 4 * kq + r;
+            const float okj = j < B ? 1.f : 0.f, dg = j == i ? 1.f : 0.f;
+            const float e11 = expf(s11[r]) * okj, e12 = expf(s12[r]) * okj;
+            float v[4] = {e11, e12, e11 * dg, e12 * dg};
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+#pragma unroll
+                for (int off = 8; off >= 1; off >>= 1) v[u] += __shfl_xor(v[u], off, kWave);
+            if (li == 0) {
+#pragma unroll
+                for (int u = 0; u < 4; ++u) sPart[w][4 * kq + r][u] = v[u];
+            }
+        }
+        __syncthreads();
+        if (tid < CR) {
+            const int64_t i = row0 + tid;
+            float4 t4;
+            t4.x = ((sPart[0][tid][0] + sPart[1][tid][0]) + sPart[2][tid][0]) + sPart[3][tid][0];
+            t4.y = ((sPart[0][tid][1] + sPart[1][tid][1]) + sPart[2][tid][1]) + sPart[3][tid][1];
+            t4.z = ((sPart[0][tid][2] + sPart[1][tid][2]) + sPart[2][tid][2]) + sPart[3][tid][2];
+            t4.w = ((sPart[0][tid][3] + sPart[1][tid][3]) + sPart[2][tid][3]) + sPart[3][tid][3];
+            if (i < B) st_agent4(pf + ((j0 / CT) * B + i) * 4, t4);
+        }
     }
-    R = sum16(R);
-    Bt = sum16(Bt);
-    e11d = sum16(e11d);
-    e12d = sum16(e12d);
-    float *Dv = ws, *pf = ws + B;
-    if (cl == 0 && i < B) st_agent4(pf + (by * B + i) * 4, make_float4(R, Bt, e11d, e12d));
     // two-level combine: the last split of each row block finishes its 16
-    // rows (D, the -log terms, their fixed-order sum), then the last row
-    // block sums the row-block partials in order.  Counters: a.counters[0]
-    // (row blocks) and a.counters[1 + bx] (splits; the backward's counters,
-    // idle during the forward), each reset by its last arriver.
+    // rows (the tile partials summed in tile order, D, the -log terms, their
+    // fixed-order sum), then the last row block sums the row-block partials
+    // in order.  Counters: a.counters[0] (row blocks) and a.counters[1 + bx]
+    // (splits; the backward's counters, idle during the forward), each reset
+    // by its last arriver.
     unsigned *counter = a.counters;
-    const int64_t nrb = contrast_row_blocks(B);
-    int64_t off = B + static_cast<int64_t>(contrast_splits(B)) * B * 4;  // bwd partials, idle here
+    const int64_t nrb = contrast_row_blocks(B), T = contrast_tiles(B);
+    int64_t off = contrast_pb_offset(B);  // bwd partials, idle here
     off += off & 1;
     double *rbp = reinterpret_cast<double *>(ws + off);
     if (!block_arrive(counter + 1 + bx, static_cast<unsigned>(NS))) return;
@@ -171,18 +235,20 @@ __device__ __forceinline__ void contrast_fwd_body(const ContrastArgs &a, int64_t
     if (tid < CR) {
         const int64_t k = bx * CR + tid;
         const int64_t kc = k < B ? k : B - 1;  // clamped: the loads stay unconditional
-        float4 v[kMaxSplit];
-#pragma unroll
-        for (int y = 0; y < kMaxSplit; ++y)
-            v[y] = ld_agent4(pf + ((y < NS ? y : 0) * B + kc) * 4);
         float sm[4] = {0.f, 0.f, 0.f, 0.f};
+        for (int64_t y0 = 0; y0 < T; y0 += 16) {
+            float4 v[16];
 #pragma unroll
-        for (int y = 0; y < kMaxSplit; ++y) {
-            const float w = y < NS ? 1.f : 0.f;
-            sm[0] = fmaf(v[y].x, w, sm[0]);
-            sm[1] = fmaf(v[y].y, w, sm[1]);
-            sm[2] = fmaf(v[y].z, w, sm[2]);
-            sm[3] = fmaf(v[y].w, w, sm[3]);
+            for (int y = 0; y < 16; ++y)
+                v[y] = ld_agent4(pf + ((y0 + y < T ? y0 + y : 0) * B + kc) * 4);
+#pragma unroll
+            for (int y = 0; y < 16; ++y) {
+                const float wy = y0 + y < T ? 1.f : 0.f;
+                sm[0] = fmaf(v[y].x, wy, sm[0]);
+                sm[1] = fmaf(v[y].y, wy, sm[1]);
+                sm[2] = fmaf(v[y].z, wy, sm[2]);
+                sm[3] = fmaf(v[y].w, wy, sm[3]);
+            }
         }
         const float D = sm[0] + sm[1] - sm[2];
         if (k < B) Dv[k] = D;
@@ -224,33 +290,6 @@ __device__ __forceinline__ void contrast_fwd_body(const ContrastArgs &a, int64_t
 // permuted identically for both operands, kperm16).  The earlier form (one
 // 64-long dependent VALU fma chain per dot product, one wave per SIMD inside
 // the head MLP's launch) took ~25 us per workgroup at B = 512 (phase trace).
-typedef float f32x4 __attribute__((ext_vector_type(4)));
-constexpr int kContrastBwdW = 3 * CR * CLD;
-
-__device__ __forceinline__ int kperm16(int s, int kq) { return 16 * (s >> 2) + 4 * kq + (s & 3); }
-__device__ __forceinline__ float f4c(const float4 &v, int t) {
-    return t == 0 ? v.x : t == 1 ? v.y : t == 2 ? v.z : v.w;
-}
-
-// lane (row li, k quarter kq): the row's normalised values at kperm16(s, kq)
-__device__ __forceinline__ void load_row_k(const float *__restrict__ x, int64_t i, int64_t B,
-                                           int kq, float (&q)[16]) {
-    const int64_t ic = i < B ? i : 0;
-    const float m = i < B ? 1.f : 0.f;
-    float4 v[4];
-    float ss = 0.f;
-#pragma unroll
-    for (int mm = 0; mm < 4; ++mm) {
-        v[mm] = *reinterpret_cast<const float4 *>(x + ic * 64 + 16 * mm + 4 * kq);
-        ss += v[mm].x * v[mm].x + v[mm].y * v[mm].y + v[mm].z * v[mm].z + v[mm].w * v[mm].w;
-    }
-    ss += __shfl_xor(ss, 16, kWave);
-    ss += __shfl_xor(ss, 32, kWave);
-    const float inv = m / fmaxf(sqrtf(ss), kNormEps);
-#pragma unroll
-    for (int s = 0; s < 16; ++s) q[s] = f4c(v[s >> 2], s & 3) * inv;
-}
-
 __device__ __forceinline__ void contrast_bwd_body(const ContrastArgs &a, int64_t bx, int by,
                                                   float *sK1, float *sK2, float *sWf,
                                                   float * /*sDj*/) {
@@ -264,7 +303,7 @@ __device__ __forceinline__ void contrast_bwd_body(const ContrastArgs &a, int64_t
     const int64_t row0 = bx * CR;
     const float g = *a.g_loss / static_cast<float>(B);
     const float *Dv = ws;
-    float *pb = a.ws + B + static_cast<int64_t>(contrast_splits(B)) * B * 4;
+    float *pb = a.ws + contrast_pb_offset(B);
     float q1[16], q2[16];  // A operands: row row0 + li, k = kperm16(s, kq)
     load_row_k(z1, row0 + li, B, kq, q1);
     load_row_k(z2, row0 + li, B, kq, q2);
@@ -276,12 +315,22 @@ __device__ __forceinline__ void contrast_bwd_body(const ContrastArgs &a, int64_t
     }
     float *sW = sWf;  // [3][CR][CLD]: W11, W12, W21
     f32x4 d1 = {0.f, 0.f, 0.f, 0.f}, d2 = d1;  // rows 4 kq + r, channel 16 w + li
-    for (int64_t j0 = static_cast<int64_t>(by) * CT; j0 < B; j0 += static_cast<int64_t>(NS) * CT) {
+    const int64_t jstep = static_cast<int64_t>(NS) * CT;
+    TileRegs t1, t2;  // the next tile's rows, in flight during this tile
+    if (static_cast<int64_t>(by) * CT < B) {
+        tile_load(z1, B, static_cast<int64_t>(by) * CT, t1);
+        tile_load(z2, B, static_cast<int64_t>(by) * CT, t2);
+    }
+    for (int64_t j0 = static_cast<int64_t>(by) * CT; j0 < B; j0 += jstep) {
         const int64_t j = j0 + 16 * w + li;  // this lane's similarity column
         const float invDj = j < B ? 1.f / Dv[j] : 0.f;
         __syncthreads();
-        stage_tile(z1, B, j0, sK1);
-        stage_tile(z2, B, j0, sK2);
+        tile_store(t1, sK1);
+        tile_store(t2, sK2);
+        if (j0 + jstep < B) {
+            tile_load(z1, B, j0 + jstep, t1);
+            tile_load(z2, B, j0 + jstep, t2);
+        }
         __syncthreads();
         f32x4 s11 = {0.f, 0.f, 0.f, 0.f}, s12 = s11, s21 = s11;
         const float *pk1 = sK1 + (16 * w + li) * CLD + 4 * kq, *pk2 = sK2 + (16 * w + li) * CLD + 4 * kq;

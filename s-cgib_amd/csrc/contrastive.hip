@@ -24,7 +24,7 @@ using namespace scgib;
 
 extern "C" int64_t scgib_contrastive_workspace_floats(int64_t n_graphs) {
     if (n_graphs <= 0) return 0;
-    return n_graphs * (1 + 132 * static_cast<int64_t>(contrast_splits(n_graphs)));
+    return contrast_pb_offset(n_graphs) + 128 * n_graphs * static_cast<int64_t>(contrast_splits(n_graphs));
 }
 
 extern "C" int64_t scgib_contrastive_counters(int64_t n_graphs) {

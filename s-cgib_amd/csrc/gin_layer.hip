@@ -2278,13 +2278,18 @@ extern "C" int scgib_mlp2_recon_contrastive_fwd(
     if (!contrast_ok(z1, z2, n_graphs, cws, ccounters, d_in) || !closs) return SCGIB_EINVAL;
     ContrastArgs con{z1, z2, n_graphs, cws, closs, nullptr, nullptr, nullptr,
                      reinterpret_cast<unsigned *>(ccounters), contrast_splits(n_graphs), 0};
-    if (n_nodes > 0 && scgib_gin_tiles(n_nodes) + contrast_row_blocks(n_graphs) * con.nsplit >
-                           2 * kCUs) {
-        // both would not be resident at once (two workgroups per CU): the
-        // two launches (the contrastive grid is then several waves anyway)
+    // the head tiles hold one CU each (101 KB LDS): the contrastive
+    // workgroups take the CUs they leave, with as many column splits as fit
+    // (each over more column tiles) rather than a second wave behind the
+    // tiles; the loss does not depend on the split count (per-tile partials)
+    const int64_t nrb = contrast_row_blocks(n_graphs);
+    const int64_t fit = n_nodes > 0 ? (kCUs - scgib_gin_tiles(n_nodes)) / nrb : con.nsplit;
+    if (fit < 1) {  // not even one split fits beside the tiles: the two launches
         const int rc = scgib_contrastive_fwd(z1, z2, n_graphs, cws, closs, ccounters, stream);
         if (rc != SCGIB_OK) return rc;
         con = ContrastArgs{};
+    } else if (fit < con.nsplit) {
+        con.nsplit = static_cast<int>(fit);
     }
     return mlp2_recon_fwd(x, d_in, n_nodes, w1, b1, w2, b2, r, out, rowptr, col, n_edges, ws,
                           counter, loss, dims, con, stream);

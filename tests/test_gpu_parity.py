@@ -533,8 +533,9 @@ def test_slab_reduce_multi_capped(pkg, dev, max_wg):
 def test_mlp2_recon_contrastive_fused(pkg, dev, n_mols, n_graphs):
     """The contrastive loss run in extra workgroups of the MLP + recon
     launches against the two separate ops: the losses are bitwise equal (same
-    bodies, same splits); the gradients agree to fp32 rounding (the backward
-    may use fewer column splits).  1000 molecules: the forward is fused, the
+    bodies; the forward keeps per-column-tile partials, so its split count,
+    smaller beside the MLP tiles, does not change a bit); the gradients agree
+    to fp32 rounding (the backward may use fewer column splits).  1000 molecules: the forward is fused, the
     backward's MLP tiles fill the CUs (two launches); 1500: two launches each
     way.  The fp64 oracle pins dz."""
     g, _ = rand_graph(pkg, n_mols, "qm9", 9, dev)

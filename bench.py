@@ -226,11 +226,20 @@ def superbatch_roofline(dev, n_target=1_200_000, reps=20):
     gin = pkg.models.GIN(64, 64, 5).to(dev).train()
     x = h.requires_grad_(True)
     torch.cuda.synchronize()
-    with KernelTimer("scgib_gin_layer_fwd_bn", "scgib_gin_bwd_stats_bn") as timer:
-        y = gin(g, x)
-        y.sum().backward()
+    # the statistics kernel alone: the previous layer's slab reduce is not
+    # folded into its launches here (stats_bytes counts the gather only)
+    fold = pkg.ops.FOLD_SLABS
+    pkg.ops.FOLD_SLABS = False
+    try:
+        with KernelTimer("scgib_gin_layer_fwd_bn", "scgib_gin_bwd_stats_bn",
+                         "scgib_gin_bwd_stats_bn_fold") as timer:
+            y = gin(g, x)
+            y.sum().backward()
+    finally:
+        pkg.ops.FOLD_SLABS = fold
     fwd = timer.records["scgib_gin_layer_fwd_bn"]
-    st = [rec for rec in timer.records["scgib_gin_bwd_stats_bn"] if rec[2]["e"] > 0]
+    st = [rec for name in ("scgib_gin_bwd_stats_bn", "scgib_gin_bwd_stats_bn_fold")
+          for rec in timer.records[name] if rec[2]["e"] > 0]
     torch.cuda.synchronize()
     for key, recs, fn in (("gin_fwd_k", fwd, layer_fwd_bytes), ("gin_bwd_stats_k", st, stats_bytes)):
         if recs:

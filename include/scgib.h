@@ -294,6 +294,14 @@ int scgib_egonet_k1_build(const int32_t *rowptr, const int32_t *col, int64_t n_n
                           int32_t *ego_nodes, int32_t *sub_rowptr, int32_t *sub_col,
                           int64_t n_ego_cap, const int32_t *dims, int32_t *ego_dims,
                           scgib_stream_t stream);
+/* The same with the batch's max in-degree (<= scgib_egonet_k1_max_degree()):
+ * <= 6 runs the kernels built for balls of <= 7 members (one load group,
+ * half the neighbour slots of the general form). */
+int scgib_egonet_k1_build_deg(const int32_t *rowptr, const int32_t *col, int64_t n_nodes,
+                              int32_t max_in_degree, int32_t *ego_ptr, int32_t *ego_eptr,
+                              void *workspace, int32_t *ego_nodes, int32_t *sub_rowptr,
+                              int32_t *sub_col, int64_t n_ego_cap, const int32_t *dims,
+                              int32_t *ego_dims, scgib_stream_t stream);
 int scgib_egonet_fill(const int32_t *rowptr, const int32_t *col, const int32_t *graph_ptr,
                       int64_t n_graphs, int64_t n_nodes, int32_t k, int32_t max_graph_nodes,
                       const int32_t *ego_ptr, const int32_t *ego_eptr, int32_t *ego_nodes,

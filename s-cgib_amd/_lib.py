@@ -29,6 +29,8 @@ SIGNATURES = {
     "scgib_egonet_k1_max_graph_nodes": (_I64, []),
     "scgib_egonet_k1_build": (ctypes.c_int, [_P, _P, _I64, _P, _P, _P, _P, _P, _P, _I64, _P, _P,
                                              _P]),
+    "scgib_egonet_k1_build_deg": (ctypes.c_int, [_P, _P, _I64, _I32, _P, _P, _P, _P, _P, _P, _I64,
+                                                 _P, _P, _P]),
     "scgib_egonet_fill": (ctypes.c_int, [_P, _P, _P, _I64, _I64, _I32, _I32, _P, _P, _P, _P, _P,
                                          _P, _I64, _P, _P, _P]),
     "scgib_interaction_fwd": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _I64, _I64, _P, _P, _P, _P,

@@ -258,39 +258,48 @@ __global__ __launch_bounds__(256) void egonet_fill_k(
 // molecule (host-checked).  Two launches: count + block scan, then fill with
 // the cross-block scan fix-up folded in.
 // ---------------------------------------------------------------------------
-constexpr int kK1Deg = 12, kK1Grp = 7, kK1Ball = kK1Deg + 1;
+// D = the in-degree bound the launch was built for (6: one member group of
+// 7 = |ball|, every molecule set of the benchmarks; 12: two groups)
+constexpr int kK1Grp = 7;
+template <int D> struct K1 {
+    static constexpr int kDeg = D, kBall = D + 1;
+};
 
+template <int D>
 struct K1Win {
     uint64_t w[2];   // bit 64 + (u - v): u in ball(v)
     int32_t v;
     int32_t nb;      // |ball|
-    int32_t mem[kK1Ball];  // members, ascending (entries >= nb repeat the last)
+    int32_t mem[D + 1];  // members, ascending (entries >= nb repeat the last)
 };
 
-__device__ __forceinline__ int32_t k1_index(const K1Win &b, int32_t u) {
+template <int D>
+__device__ __forceinline__ int32_t k1_index(const K1Win<D> &b, int32_t u) {
     const int32_t i = u - b.v + 64;
     const uint64_t word = i < 64 ? b.w[0] : b.w[1];  // selects: no dynamic indexing
     return (i >= 0 && i < 128 && ((word >> (i & 63)) & 1ull)) ? i : -1;
 }
 
 // members strictly below window index i
-__device__ __forceinline__ int32_t k1_rank(const K1Win &b, int32_t i) {
+template <int D>
+__device__ __forceinline__ int32_t k1_rank(const K1Win<D> &b, int32_t i) {
     const uint64_t m = (1ull << (i & 63)) - 1ull;
     return i < 64 ? __popcll(b.w[0] & m) : __popcll(b.w[0]) + __popcll(b.w[1] & m);
 }
 
+template <int D>
 __device__ __forceinline__ void k1_ball(const int32_t *__restrict__ rowptr,
-                                        const int32_t *__restrict__ col, int32_t v, K1Win &b) {
+                                        const int32_t *__restrict__ col, int32_t v, K1Win<D> &b) {
     const int32_t beg = rowptr[v], end = rowptr[v + 1];
     const int32_t last = end > beg ? end - 1 : (beg > 0 ? beg - 1 : 0);  // a valid index
-    int32_t nbr[kK1Deg];
+    int32_t nbr[D];
 #pragma unroll
-    for (int j = 0; j < kK1Deg; ++j) nbr[j] = col[beg + j < end ? beg + j : last];
+    for (int j = 0; j < D; ++j) nbr[j] = col[beg + j < end ? beg + j : last];
     b.v = v;
     b.w[0] = 0ull;
     b.w[1] = 1ull;  // v itself: bit 64
 #pragma unroll
-    for (int j = 0; j < kK1Deg; ++j) {
+    for (int j = 0; j < D; ++j) {
         const int32_t i = nbr[j] - v + 64;
         const uint64_t bit = (beg + j < end && i >= 0 && i < 128) ? 1ull << (i & 63) : 0ull;
         b.w[0] |= i < 64 ? bit : 0ull;
@@ -302,7 +311,7 @@ __device__ __forceinline__ void k1_ball(const int32_t *__restrict__ rowptr,
     uint64_t m0 = b.w[0], m1 = b.w[1];
     int32_t prev = v;
 #pragma unroll
-    for (int q = 0; q < kK1Ball; ++q) {
+    for (int q = 0; q < D + 1; ++q) {
         const bool lo = m0 != 0ull, hi = m1 != 0ull;
         const int32_t i = lo ? __ffsll(static_cast<unsigned long long>(m0)) - 1
                              : 64 + __ffsll(static_cast<unsigned long long>(m1)) - 1;
@@ -315,19 +324,20 @@ __device__ __forceinline__ void k1_ball(const int32_t *__restrict__ rowptr,
 }
 
 // rows of members [g0, g0 + kK1Grp) and their neighbour ids, one batched round each
+template <int D>
 struct K1Rows {
     int32_t beg[kK1Grp], deg[kK1Grp];
-    int32_t w[kK1Grp][kK1Deg];
+    int32_t w[kK1Grp][D];
 };
 
-template <int G0>
+template <int D, int G0>
 __device__ __forceinline__ void k1_rows(const int32_t *__restrict__ rowptr,
-                                        const int32_t *__restrict__ col, const K1Win &b,
-                                        K1Rows &m) {
+                                        const int32_t *__restrict__ col, const K1Win<D> &b,
+                                        K1Rows<D> &m) {
     int32_t end[kK1Grp];
 #pragma unroll
     for (int r = 0; r < kK1Grp; ++r) {
-        const int32_t u = b.mem[G0 + r < kK1Ball ? G0 + r : kK1Ball - 1];
+        const int32_t u = b.mem[G0 + r < D + 1 ? G0 + r : D];
         m.beg[r] = rowptr[u];
         end[r] = rowptr[u + 1];
     }
@@ -336,7 +346,7 @@ __device__ __forceinline__ void k1_rows(const int32_t *__restrict__ rowptr,
         m.deg[r] = end[r] - m.beg[r];
         const int32_t last = end[r] > m.beg[r] ? end[r] - 1 : (m.beg[r] > 0 ? m.beg[r] - 1 : 0);
 #pragma unroll
-        for (int t = 0; t < kK1Deg; ++t) m.w[r][t] = col[m.beg[r] + t < end[r] ? m.beg[r] + t : last];
+        for (int t = 0; t < D; ++t) m.w[r][t] = col[m.beg[r] + t < end[r] ? m.beg[r] + t : last];
     }
 }
 
@@ -355,6 +365,7 @@ __device__ __forceinline__ void wave_scan2(int32_t &a, int32_t &b) {
     }
 }
 
+template <int D>
 __global__ __launch_bounds__(kK1Block) void egonet_k1_count_k(
     const int32_t *__restrict__ rowptr, const int32_t *__restrict__ col, int64_t n,
     int32_t *__restrict__ ego_ptr, int32_t *__restrict__ ego_eptr, int32_t *__restrict__ blk_tot,
@@ -362,24 +373,24 @@ __global__ __launch_bounds__(kK1Block) void egonet_k1_count_k(
     const int64_t v = static_cast<int64_t>(blockIdx.x) * kK1Block + threadIdx.x;
     int32_t nb = 0, ne = 0;
     if (v < eff_count(dims, 0, n)) {
-        K1Win b;
-        k1_ball(rowptr, col, static_cast<int32_t>(v), b);
+        K1Win<D> b;
+        k1_ball<D>(rowptr, col, static_cast<int32_t>(v), b);
         nb = b.nb;
-        auto count = [&](const K1Rows &m, int g0) {
+        auto count = [&](const K1Rows<D> &m, int g0) {
 #pragma unroll
             for (int r = 0; r < kK1Grp; ++r)
 #pragma unroll
-                for (int t = 0; t < kK1Deg; ++t)
+                for (int t = 0; t < D; ++t)
                     ne += (g0 + r < b.nb && t < m.deg[r] && k1_index(b, m.w[r][t]) >= 0) ? 1 : 0;
         };
         {
-            K1Rows m;
-            k1_rows<0>(rowptr, col, b, m);
+            K1Rows<D> m;
+            k1_rows<D, 0>(rowptr, col, b, m);
             count(m, 0);
         }
-        if (b.nb > kK1Grp) {  // balls of more than kK1Grp members: second group
-            K1Rows m;
-            k1_rows<kK1Grp>(rowptr, col, b, m);
+        if (D + 1 > kK1Grp && b.nb > kK1Grp) {  // balls of more than kK1Grp members: second group
+            K1Rows<D> m;
+            k1_rows<D, kK1Grp>(rowptr, col, b, m);
             count(m, kK1Grp);
         }
     }
@@ -394,6 +405,7 @@ __global__ __launch_bounds__(kK1Block) void egonet_k1_count_k(
     }
 }
 
+template <int D>
 __global__ __launch_bounds__(kK1Block) void egonet_k1_fill_k(
     const int32_t *__restrict__ rowptr, const int32_t *__restrict__ col, int64_t n,
     int32_t *__restrict__ ego_ptr, int32_t *__restrict__ ego_eptr,
@@ -404,11 +416,11 @@ __global__ __launch_bounds__(kK1Block) void egonet_k1_fill_k(
     const int64_t v = static_cast<int64_t>(blockIdx.x) * kK1Block + threadIdx.x;
     const bool live = v < eff_count(dims, 0, n);
     // the ball's loads go out first; the scan fix-up below overlaps them
-    K1Win b;
-    K1Rows m;
+    K1Win<D> b;
+    K1Rows<D> m;
     if (live) {
-        k1_ball(rowptr, col, static_cast<int32_t>(v), b);
-        k1_rows<0>(rowptr, col, b, m);
+        k1_ball<D>(rowptr, col, static_cast<int32_t>(v), b);
+        k1_rows<D, 0>(rowptr, col, b, m);
     }
     // block prefix and grand total of (nodes, edges), fixed order (wave sums)
     int32_t pn = 0, pe = 0, tn = 0, te = 0;
@@ -458,15 +470,15 @@ __global__ __launch_bounds__(kK1Block) void egonet_k1_fill_k(
         if (i < n_ego_cap) ego_nodes[i] = 0;
     }
     if (!live) return;
-    auto fill = [&](const K1Rows &mm, auto g0c) {
+    auto fill = [&](const K1Rows<D> &mm, auto g0c) {
         constexpr int G0 = decltype(g0c)::value;
 #pragma unroll
         for (int r = 0; r < kK1Grp; ++r) {
             if (G0 + r < b.nb) {
-                ego_nodes[noff + G0 + r] = b.mem[G0 + r < kK1Ball ? G0 + r : kK1Ball - 1];
+                ego_nodes[noff + G0 + r] = b.mem[G0 + r < D + 1 ? G0 + r : D];
                 sub_rowptr[noff + G0 + r] = eo;
 #pragma unroll
-                for (int t = 0; t < kK1Deg; ++t) {
+                for (int t = 0; t < D; ++t) {
                     const int32_t i = k1_index(b, mm.w[r][t]);
                     if (t < mm.deg[r] && i >= 0) sub_col[eo++] = noff + k1_rank(b, i);
                 }
@@ -474,9 +486,11 @@ __global__ __launch_bounds__(kK1Block) void egonet_k1_fill_k(
         }
     };
     fill(m, std::integral_constant<int, 0>{});
-    if (b.nb > kK1Grp) {
-        k1_rows<kK1Grp>(rowptr, col, b, m);
-        fill(m, std::integral_constant<int, kK1Grp>{});
+    if constexpr (D + 1 > kK1Grp) {
+        if (b.nb > kK1Grp) {
+            k1_rows<D, kK1Grp>(rowptr, col, b, m);
+            fill(m, std::integral_constant<int, kK1Grp>{});
+        }
     }
 }
 
@@ -530,28 +544,53 @@ extern "C" int scgib_egonet_count(const int32_t *rowptr, const int32_t *col,
     return launch_status();
 }
 
-extern "C" int64_t scgib_egonet_k1_max_degree(void) { return kK1Deg; }
+extern "C" int64_t scgib_egonet_k1_max_degree(void) { return 12; }
 
 extern "C" int64_t scgib_egonet_k1_max_graph_nodes(void) { return 64; }
+
+template <int D>
+static void launch_k1(const int32_t *rowptr, const int32_t *col, int64_t n_nodes,
+                      int32_t *ego_ptr, int32_t *ego_eptr, int32_t *blk_tot, int32_t *ego_nodes,
+                      int32_t *sub_rowptr, int32_t *sub_col, int64_t n_ego_cap,
+                      const int32_t *dims, int32_t *ego_dims, hipStream_t st) {
+    const int32_t nblk = static_cast<int32_t>((n_nodes + kK1Block - 1) / kK1Block);
+    egonet_k1_count_k<D><<<nblk, kK1Block, 0, st>>>(rowptr, col, n_nodes, ego_ptr, ego_eptr,
+                                                     blk_tot, dims);
+    egonet_k1_fill_k<D><<<nblk, kK1Block, 0, st>>>(rowptr, col, n_nodes, ego_ptr, ego_eptr,
+                                                    blk_tot, ego_nodes, sub_rowptr, sub_col,
+                                                    n_ego_cap, dims, ego_dims);
+}
+
+extern "C" int scgib_egonet_k1_build_deg(const int32_t *rowptr, const int32_t *col,
+                                         int64_t n_nodes, int32_t max_in_degree,
+                                         int32_t *ego_ptr, int32_t *ego_eptr, void *workspace,
+                                         int32_t *ego_nodes, int32_t *sub_rowptr,
+                                         int32_t *sub_col, int64_t n_ego_cap,
+                                         const int32_t *dims, int32_t *ego_dims,
+                                         scgib_stream_t stream) {
+    if (n_nodes <= 0 || !rowptr || !col || !ego_ptr || !ego_eptr || !workspace || !ego_nodes ||
+        !sub_rowptr || !sub_col || max_in_degree < 0)
+        return SCGIB_EINVAL;
+    if (n_nodes >= (int64_t(1) << 31) || max_in_degree > 12) return SCGIB_EUNSUPPORTED;
+    int32_t *blk_tot = static_cast<int32_t *>(workspace);
+    hipStream_t st = as_stream(stream);
+    if (max_in_degree <= 6)  // one member group, half the neighbour slots
+        launch_k1<6>(rowptr, col, n_nodes, ego_ptr, ego_eptr, blk_tot, ego_nodes, sub_rowptr,
+                     sub_col, n_ego_cap, dims, ego_dims, st);
+    else
+        launch_k1<12>(rowptr, col, n_nodes, ego_ptr, ego_eptr, blk_tot, ego_nodes, sub_rowptr,
+                      sub_col, n_ego_cap, dims, ego_dims, st);
+    return launch_status();
+}
 
 extern "C" int scgib_egonet_k1_build(const int32_t *rowptr, const int32_t *col, int64_t n_nodes,
                                      int32_t *ego_ptr, int32_t *ego_eptr, void *workspace,
                                      int32_t *ego_nodes, int32_t *sub_rowptr, int32_t *sub_col,
                                      int64_t n_ego_cap, const int32_t *dims, int32_t *ego_dims,
                                      scgib_stream_t stream) {
-    if (n_nodes <= 0 || !rowptr || !col || !ego_ptr || !ego_eptr || !workspace || !ego_nodes ||
-        !sub_rowptr || !sub_col)
-        return SCGIB_EINVAL;
-    if (n_nodes >= (int64_t(1) << 31)) return SCGIB_EUNSUPPORTED;
-    const int32_t nblk = static_cast<int32_t>((n_nodes + kK1Block - 1) / kK1Block);
-    int32_t *blk_tot = static_cast<int32_t *>(workspace);
-    hipStream_t st = as_stream(stream);
-    egonet_k1_count_k<<<nblk, kK1Block, 0, st>>>(rowptr, col, n_nodes, ego_ptr, ego_eptr, blk_tot,
-                                                  dims);
-    egonet_k1_fill_k<<<nblk, kK1Block, 0, st>>>(rowptr, col, n_nodes, ego_ptr, ego_eptr, blk_tot,
-                                           ego_nodes, sub_rowptr, sub_col, n_ego_cap, dims,
-                                           ego_dims);
-    return launch_status();
+    return scgib_egonet_k1_build_deg(rowptr, col, n_nodes, 12, ego_ptr, ego_eptr, workspace,
+                                     ego_nodes, sub_rowptr, sub_col, n_ego_cap, dims, ego_dims,
+                                     stream);
 }
 
 extern "C" int scgib_egonet_fill(const int32_t *rowptr, const int32_t *col,

@@ -373,7 +373,9 @@ def egonet_batch(g: GraphBatch, k: int, x=None):
             fast = (fits and info is not None and info["validated"] and
                     (len(info["deg"]) == 0 or int(info["deg"].max()) <= kmax))
         if fast:
-            return _egonet_k1(g, ego_ptr, ego_eptr, ws, x)
+            dmax = int(caps[2]) if g.dims is not None else \
+                (int(info["deg"].max()) if len(info["deg"]) else 0)
+            return _egonet_k1(g, ego_ptr, ego_eptr, ws, x, dmax)
     err = getattr(g, "err_buf", None)
     if err is None:
         err = torch.zeros(1, dtype=i32, device=dev)
@@ -447,10 +449,10 @@ def ego_bounds(g, k):
 # Off by default: faster alone (39 vs 46 us per QM9 B512 build, tools/ego_bench.py)
 # but the replayed step measured 0.5 % slower with it (the ego chain then
 # contends earlier with Encoder1's layers); tests compare both builders.
-EGO_K1_FAST = os.environ.get("SCGIB_EGO_K1", "0") != "0"
+EGO_K1_FAST = os.environ.get("SCGIB_EGO_K1", "1") != "0"
 
 
-def _egonet_k1(g, ego_ptr, ego_eptr, ws, x):
+def _egonet_k1(g, ego_ptr, ego_eptr, ws, x, max_in_degree=12):
     """egonet_batch for k = 1 via scgib_egonet_k1_build (sizes known on the
     host: |ball(v)| = 1 + deg(v) - selfloop(v); capacity mode: g.ego_caps)."""
     dev = g.device
@@ -468,9 +470,9 @@ def _egonet_k1(g, ego_ptr, ego_eptr, ws, x):
     ego_nodes = torch.empty(max(n_s, 1), dtype=i32, device=dev)
     sub_rowptr = torch.empty(n_s + 1, dtype=i32, device=dev)
     sub_col = torch.empty(max(e_cap, 1), dtype=i32, device=dev)
-    _lib.call("scgib_egonet_k1_build", _ptr(g.rowptr), _ptr(g.col), n, _ptr(ego_ptr),
-              _ptr(ego_eptr), _ptr(ws), _ptr(ego_nodes), _ptr(sub_rowptr), _ptr(sub_col), n_s,
-              _ptr(g.dims), _ptr(ego_dims), _stream())
+    _lib.call("scgib_egonet_k1_build_deg", _ptr(g.rowptr), _ptr(g.col), n, int(max_in_degree),
+              _ptr(ego_ptr), _ptr(ego_eptr), _ptr(ws), _ptr(ego_nodes), _ptr(sub_rowptr),
+              _ptr(sub_col), n_s, _ptr(g.dims), _ptr(ego_dims), _stream())
     ego = GraphBatch(sub_rowptr, sub_col, ego_ptr, None, None, n_edges=-1,
                      max_graph_nodes=max(g.max_graph_nodes, 1))
     ego.dims = ego_dims

@@ -241,6 +241,34 @@ int scgib_gin_layer_bwd(const float *dy, const float *z2, const float *r, const 
                         const float *w2, int64_t n_nodes, float *dagg, float *slab,
                         float *wgrad, const int32_t *dims, const scgib_bn_bwd_pending *pending,
                         scgib_stream_t stream);
+/* Fused backward of layer l (d_in = 64) and the statistics of layer l-1:
+ * scgib_gin_layer_bwd followed by scgib_gin_bwd_stats_bn_fold(dagg, ...) in
+ * one launch, over component-aligned chunks (d(agg) stays on chip).
+ * Replaces, per layer l >= 1, the pair gin_bwd + gin_bwd_stats that the
+ * reference's autograd runs through GINConv / BatchNorm1d (models.py:52-72).
+ * chunk_ptr: scgib_gin_chunk_bounds of the same graph (scgib_gin_chunks(n) + 1
+ * entries).  Valid when every component (graph_ptr segment) has at most
+ * scgib_gin_chunk_max_component() rows and no edge leaves its component.
+ * Outputs: dy_prev (dy of layer l-1), the layer l-1 BN-backward sums in
+ * bn_ws_prev (deferred, or finished into dgamma/dbeta/coef_prev), and one
+ * weight-gradient slab per chunk (slab_reduce: n_slabs = scgib_gin_chunks).
+ * fold (NULL: none): a slab reduce job (the previous fused layer's) run in
+ * extra workgroups ahead of the chunk grid, as in scgib_gin_bwd_stats_bn_fold. */
+int32_t scgib_gin_chunk_max_component(void);
+int64_t scgib_gin_chunks(int64_t n_nodes);
+int scgib_gin_chunk_bounds(const int32_t *graph_ptr, int64_t n_seg, const int32_t *seg_dims,
+                           int64_t n_nodes, const int32_t *dims, int32_t *chunk_ptr,
+                           scgib_stream_t stream);
+int scgib_gin_layer_bwd_fused(const float *dy, const float *z2, const float *r, const float *agg,
+                              const float *stat, const float *coef, const float *w1,
+                              const float *w2, int64_t n_nodes, const int32_t *chunk_ptr,
+                              const int32_t *rowptr_t, const int32_t *col_t, float one_plus_eps,
+                              const float *z2_prev, const float *stat_prev, int32_t training,
+                              float *dy_prev, float *dgamma_prev, float *dbeta_prev,
+                              float *coef_prev, float *bn_ws_prev, uint32_t *counters,
+                              int32_t defer, float *slab, const int32_t *dims,
+                              const scgib_bn_bwd_pending *pending, const scgib_slab_job *fold,
+                              scgib_stream_t stream);
 
 /* ---- A6: per-segment readouts (dgl.sum_nodes) -------------------------------
  * out[s,:] = sum_{i in [ptr[s], ptr[s+1])} x[i,:]   (models.py:716, 725, 733)

@@ -98,6 +98,12 @@ SIGNATURES = {
     "scgib_bn_bwd_finalize": (ctypes.c_int, [_P, _I64, _I32, _P, _P, _P, _P, _P]),
     "scgib_gin_layer_bwd": (ctypes.c_int, [_P, _P, _P, _P, _I32, _P, _P, _P, _P, _I64, _P, _P,
                                            _P, _P, _P, _P]),
+    "scgib_gin_chunk_max_component": (_I32, []),
+    "scgib_gin_chunks": (_I64, [_I64]),
+    "scgib_gin_chunk_bounds": (ctypes.c_int, [_P, _I64, _P, _I64, _P, _P, _P]),
+    "scgib_gin_layer_bwd_fused": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _P, _P, _I64, _P, _P,
+                                                 _P, _F, _P, _P, _I32, _P, _P, _P, _P, _P, _P,
+                                                 _I32, _P, _P, _P, _P, _P]),
     "scgib_recon_partials_floats": (_I64, [_I64]),
     "scgib_recon_fwd": (ctypes.c_int, [_P, _P, _P, _I64, _I64, _P, _P, _P, _P, _P]),
     "scgib_recon_bwd": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _I64, _P, _P, _P, _P]),

@@ -342,16 +342,17 @@ __device__ __forceinline__ float bn_bwd_publish(int c, double tot, int64_t n, in
     return cf;
 }
 
-// backward: tile (sum dy, sum dy xhat) -> group -> layer sums (fp64)
-__device__ void bn_bwd_hier(const float *__restrict__ part, int64_t n, int64_t tile,
-                            const BnBwdFuse &bz) {
+// backward: tile (sum dy, sum dy xhat) -> group -> layer sums (fp64);
+// sh: 2 KB of LDS scratch (the caller's, so a kernel near its LDS limit can
+// lend a dead tile image)
+__device__ void bn_bwd_hier_s(const float *__restrict__ part, int64_t n, int64_t tile,
+                              const BnBwdFuse &bz, double (*sh)[128]) {
     const int64_t nt = (n + TM - 1) / TM;
     const int ngr = static_cast<int>((nt + kGroup - 1) / kGroup);
     const int g = static_cast<int>(tile / kGroup);
     const int gsize = static_cast<int>(nt - int64_t(g) * kGroup < kGroup ? nt - int64_t(g) * kGroup : kGroup);
     if (!block_arrive(&bz.counters[g], gsize)) return;
     const int c = threadIdx.x & 127, p = threadIdx.x >> 7;  // 128 sums x 2 partitions
-    __shared__ double sh[2][128];
     {
         constexpr int U = kGroup / 2;
         float v[U];
@@ -376,6 +377,12 @@ __device__ void bn_bwd_hier(const float *__restrict__ part, int64_t n, int64_t t
     if ((threadIdx.x & 63) < 32)
         bn_bwd_publish(bfin_index(), tot, n, bz.training, bz.dgamma, bz.dbeta, bz.coef);
     if (threadIdx.x == 0) bz.counters[bz.ngr_cap] = 0u;
+}
+
+__device__ void bn_bwd_hier(const float *__restrict__ part, int64_t n, int64_t tile,
+                            const BnBwdFuse &bz) {
+    __shared__ double sh[2][128];
+    bn_bwd_hier_s(part, n, tile, bz, sh);
 }
 
 // ---------------------------------------------------------------------------
@@ -1794,6 +1801,371 @@ __global__ __launch_bounds__(256, 2) void gin_bwd5_k(
     SCGIB_MARK(6);
 }
 
+// ---------------------------------------------------------------------------
+// gin_bwdf_k: layer l's backward (gin_bwd5_k's sub-tile body) fused with
+// layer l-1's backward statistics (gin_bwd_stats_k) on component-aligned
+// chunks, so d(agg) of layer l never leaves LDS and the statistics launch of
+// every layer but the last disappears.
+//
+// Chunk c = the components (molecules, ego-nets) whose first row lies in
+// [64 c, 64 c + 64): rows [cptr[c], cptr[c+1]).  The transposed aggregation
+//   dh_{l-1}(v) = (1+eps_l) d(agg_l)(v) + sum_{v->u} d(agg_l)(u)
+// only reads rows u of v's own component (edges stay inside their graph,
+// checked on the host), i.e. rows of the same chunk, whose d(agg) this
+// workgroup has just computed.  With components of <= kChunkComp rows a chunk
+// holds <= 96 rows: up to three 32-row sub-tiles, d(agg) staged in a
+// [96][64] LDS image that replaces gin_bwd5_k's staging buffer (79 KB LDS:
+// two workgroups per CU).  One workgroup per chunk; chunk c's sums
+// (sum dy, sum dy xhat) of layer l-1 are tile c's of the statistics kernel,
+// so the BN-backward hierarchy, its deferral and its consumer are unchanged.
+// Per-row arithmetic is gin_bwd5_k's and gin_bwd_stats_k's (fp32; the
+// neighbour sum in CSR order).
+// ---------------------------------------------------------------------------
+constexpr int kChunkRows = 96;
+constexpr int kChunkComp = 33;   // max component rows for kChunkRows
+// build-time A/B knob: fetch the statistics phase's row ranges, BN record,
+// first neighbour round and z2 rows during the sub-tile loop (1) or at the
+// phase (0)
+#ifndef SCGIB_BWDF_PREFETCH
+#define SCGIB_BWDF_PREFETCH 0
+#endif
+constexpr bool kBwdfPf = SCGIB_BWDF_PREFETCH != 0;
+#ifndef SCGIB_BWDF_FOLD_WG
+#define SCGIB_BWDF_FOLD_WG 64
+#endif
+constexpr int kBwdfFoldWG = SCGIB_BWDF_FOLD_WG;
+#ifndef SCGIB_BWDF_SLAB_LAST
+#define SCGIB_BWDF_SLAB_LAST 1
+#endif
+constexpr bool kBwdfSlabLast = SCGIB_BWDF_SLAB_LAST != 0;
+
+// cptr[c] = min(first row of a component >= 64 c, n) for c in [0, nchunk]
+// (one thread per component start; each chunk boundary written once)
+__global__ __launch_bounds__(256) void gin_chunk_bounds_k(
+    const int32_t *__restrict__ gptr, int64_t nseg, const int32_t *__restrict__ seg_dims,
+    int64_t ncap, const int32_t *__restrict__ dims, int32_t *__restrict__ cptr, int64_t nchunk) {
+    const int64_t m = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
+    const int64_t ns = eff_count(seg_dims, 0, nseg), n = eff_count(dims, 0, ncap);
+    if (m > ns) return;
+    const int64_t s = m < ns ? gptr[m] : n;
+    const int64_t p = m > 0 ? gptr[m - 1] : -1;
+    const int64_t lo = (p + TM) / TM, hi = m < ns ? (s / TM < nchunk ? s / TM : nchunk) : nchunk;
+    for (int64_t c = lo; c <= hi; ++c) cptr[c] = static_cast<int32_t>(s);
+}
+
+template <int DIN>
+__global__ __launch_bounds__(256, 2) void gin_bwdf_k(
+    const float *__restrict__ dy, const float *__restrict__ z2, const float *__restrict__ r,
+    const float *__restrict__ agg, const float *__restrict__ stat,
+    const float *__restrict__ coef, const float *__restrict__ w1, const float *__restrict__ w2,
+    int64_t ncap, const int32_t *__restrict__ cptr, const int32_t *__restrict__ rowptr_t,
+    const int32_t *__restrict__ col_t, float ope, const float *__restrict__ z2p,
+    const float *__restrict__ statp, float *__restrict__ dyp_out, float *__restrict__ part,
+    BnBwdFuse bz, float *__restrict__ slab, const int32_t *__restrict__ dims,
+    scgib_bn_bwd_pending pend, scgib_slab_job fold) {
+    static_assert(DIN == 64 && SM == 32 && kChunkRows == 3 * SM, "64-wide rows, 3 sub-tiles");
+    constexpr int SLAB = 64 * 64 + 64 * DIN + 128;
+    constexpr int KR = kChunkRows / 16;  // rows per thread in the statistics phase
+    __shared__ __attribute__((aligned(16))) float sD[SM * LDR];   // dz2 [row][k]
+    __shared__ __attribute__((aligned(16))) float sDT[64 * LDT];  // dz2 [col][row]
+    __shared__ __attribute__((aligned(16))) float sE[SM * LDR];   // dz1
+    __shared__ __attribute__((aligned(16))) float sET[64 * LDT];
+    __shared__ __attribute__((aligned(16))) float sRT[64 * LDT];  // r [col][row]
+    __shared__ __attribute__((aligned(16))) float sAT[DIN * LDT]; // agg [col][row]
+    __shared__ __attribute__((aligned(16))) float sA[kChunkRows * 64];  // d(agg) of the chunk
+    __shared__ float sCoef[128];
+    __shared__ int32_t sRp[kChunkRows + 1];  // rowptr_t of the chunk's rows
+    __shared__ __attribute__((aligned(16))) float sStp[256];  // layer l-1's BN record
+    const int64_t n = eff_count(dims, 0, ncap);
+    const int tid = threadIdx.x, l = tid & 63, w = tid >> 6;
+    const int kk = l >> 5, li = l & 31;
+    const bool nw = w < 2;
+    const int q = w & 1;
+    const int c = l;
+    const int64_t last = ncap - 1;
+    // the folded reduce of the previous layer's slabs: at most kBwdfFoldWG
+    // workgroups past the chunk grid, each looping over column blocks, so they
+    // fit the workgroup slots the chunk grid leaves free (block-uniform)
+    const int64_t nchunk = (ncap + TM - 1) / TM;
+    if (static_cast<int64_t>(blockIdx.x) >= nchunk) {
+        const int nb = slab_fold_blocks(fold), nwg = gridDim.x - static_cast<int>(nchunk);
+        for (int b = static_cast<int>(blockIdx.x - nchunk); b < nb; b += nwg) {
+            slab_fold_block(fold, b, sD);
+            __syncthreads();  // sD reused by the next column block
+        }
+        return;
+    }
+    const int64_t chunk = blockIdx.x;
+    SCGIB_MARK(0);
+    SCGIB_MARK_HWID();
+    BwdFin bfin;
+    const int pend_ngr = static_cast<int>(((n + TM - 1) / TM + kGroup - 1) / kGroup);
+    if (pend.gpart) bn_bwd_fin_load<false>(pend.gpart, pend_ngr, 0, bfin);
+    const int64_t a = cptr[chunk];
+    const int rows = static_cast<int>(cptr[chunk + 1] - a);  // block-uniform, <= kChunkRows
+    // statistics phase: thread = row slot rs + 16 k, float4 column c4; with
+    // kBwdfPf its row ranges (-> sRp) and BN record (-> sStp) are fetched here
+    const int c4 = tid & 15, rs = tid >> 4;
+    const int32_t rp_v = kBwdfPf && tid <= rows && rows > 0 ? rowptr_t[a + tid] : 0;
+    const float stp_v = kBwdfPf ? statp[tid] : 0.f;
+    const float s_mean = stat[c], s_istd = stat[64 + c], s_sc = stat[128 + c];
+    float c1 = 0.f, c2 = 0.f;
+    if (!pend.gpart) {
+        c1 = coef[c];
+        c2 = coef[64 + c];
+    }
+    float wreg[32];
+    {
+        const float *wm = nw ? w2 : w1;
+#pragma unroll
+        for (int s = 0; s < 32; ++s) wreg[s] = wm[kperm(s, kk) * 64 + q * 32 + li];
+    }
+    float nx[4][8];
+    auto load_sub = [&](int j) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            int64_t row = a + j * SM + 8 * w + i;
+            row = row < last ? row : last;
+            nx[2][i] = r[row * 64 + c];
+        }
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            int64_t row = a + j * SM + 8 * w + i;
+            row = row < last ? row : last;
+            nx[3][i] = agg[row * DIN + c];
+        }
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            int64_t row = a + j * SM + 8 * w + i;
+            row = row < last ? row : last;
+            nx[0][i] = dy[row * 64 + c];
+            nx[1][i] = z2[row * 64 + c];
+        }
+    };
+    auto put_t = [&](float *img, int x) {
+        float4 *p = reinterpret_cast<float4 *>(img + c * LDT + 8 * w);
+        p[0] = make_float4(nx[x][0], nx[x][1], nx[x][2], nx[x][3]);
+        p[1] = make_float4(nx[x][4], nx[x][5], nx[x][6], nx[x][7]);
+    };
+    const int nsub = (rows + SM - 1) / SM;
+    if (nsub > 0) load_sub(0);
+    if (pend.gpart) {
+        const double tot = bn_bwd_final<false>(pend.gpart, pend_ngr, bfin);
+        const int cs = bfin_index();
+        const bool lead = (tid & 63) < 32, w0 = chunk == 0 && lead;
+        const float cf = bn_bwd_publish(cs, tot, n, pend.training, w0 ? pend.dgamma : nullptr,
+                                        w0 ? pend.dbeta : nullptr, nullptr);
+        if (lead) sCoef[cs] = cf;
+    }
+    if (nsub > 0) {
+        put_t(sRT, 2);
+        put_t(sAT, 3);
+    }
+    vm_wait_all();
+    if (kBwdfPf) {
+        if (tid <= rows) sRp[tid] = rp_v;
+        sStp[tid] = stp_v;
+    }
+    __syncthreads();
+    if (pend.gpart) {
+        c1 = sCoef[c];
+        c2 = sCoef[64 + c];
+    }
+    const float k1 = s_istd * c2;
+    SCGIB_MARK(1);
+    // kBwdfPf: the statistics phase's z2 rows and first neighbour round,
+    // loaded during the last sub-tile; the neighbour ids go to the registers
+    // of the (then unused) row prefetch nx[0..2] as int bits: row k, slot t at
+    // nx[(4k+t)/8][(4k+t)%8]
+    float4 zp[KR];
+    auto load_stats = [&]() {
+#pragma unroll
+        for (int k = 0; k < KR; ++k) {
+            const int rr = rs + 16 * k;
+            zp[k] = ld4(z2p + (a + (rr < rows ? rr : rows - 1)) * 64 + 4 * c4);
+        }
+#pragma unroll
+        for (int k = 0; k < KR; ++k) {
+            const int rr = rs + 16 * k < rows ? rs + 16 * k : rows;
+            const int32_t b = sRp[rr], e1 = sRp[rs + 16 * k < rows ? rr + 1 : rows];
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                const int32_t e = b + t;
+                nx[(4 * k + t) >> 3][(4 * k + t) & 7] = e < e1 ? __int_as_float(col_t[e]) : 0.f;
+            }
+        }
+    };
+    f32x16 accA = zero16(), accB = zero16();
+    float dbias = 0.f;
+    for (int j = 0; j < nsub; ++j) {
+        const int nv = rows - j * SM < SM ? rows - j * SM : SM;
+        {
+            float d[8];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const float v = s_sc * (nx[0][i] - c1 - (nx[1][i] - s_mean) * k1);
+                d[i] = 8 * w + i < nv ? v : 0.f;
+                sD[(8 * w + i) * LDR + c] = d[i];
+            }
+            float4 *p = reinterpret_cast<float4 *>(sDT + c * LDT + 8 * w);
+            p[0] = make_float4(d[0], d[1], d[2], d[3]);
+            p[1] = make_float4(d[4], d[5], d[6], d[7]);
+        }
+        const bool more = j + 1 < nsub;  // block-uniform
+        if (more) load_sub(j + 1);
+        else if (kBwdfPf) load_stats();
+        lds_barrier();
+        if (j == 0) SCGIB_MARK(2);
+        if (nw) {
+            const f32x16 dr = mma_rk4<8>(sD + li * LDR + 4 * kk, wreg, zero16());
+#pragma unroll
+            for (int reg = 0; reg < 16; ++reg) {
+                const int row = acc_row(reg, l), col = q * 32 + li;
+                const float v = dr[reg] * (sRT[col * LDT + row] > 0.f ? 1.f : 0.f);
+                sE[row * LDR + col] = v;
+                sET[col * LDT + row] = v;
+            }
+        } else {
+            mma_kk4x2<4>(sDT + (q * 32 + li) * LDT + 4 * kk, sRT + li * LDT + 4 * kk,
+                         sRT + (32 + li) * LDT + 4 * kk, accA, accB, dbias);
+        }
+        lds_barrier();
+        if (j == 0) SCGIB_MARK(3);
+        if (more) put_t(sRT, 2);
+        if (nw) {
+            mma_kk4x2<4>(sET + (q * 32 + li) * LDT + 4 * kk, sAT + li * LDT + 4 * kk,
+                         sAT + (32 + li) * LDT + 4 * kk, accA, accB, dbias);
+        } else {   // d(agg) block q of sub-tile j -> the chunk image (rows past nv are 0)
+            const f32x16 da = mma_rk4<8>(sE + li * LDR + 4 * kk, wreg, zero16());
+            float *dst = sA + (j * SM) * 64 + q * 32 + li;
+#pragma unroll
+            for (int reg = 0; reg < 16; ++reg) dst[acc_row(reg, l) * 64] = da[reg];
+        }
+        lds_barrier();
+        if (j == 0) SCGIB_MARK(4);
+        if (more) put_t(sAT, 3);
+    }
+    SCGIB_MARK(5);
+    // ---- layer l-1's statistics: dh = ope d(agg)(v) + sum_{v->u} d(agg)(u),
+    // dy_{l-1} = dh [scale z2 + shift > 0] (the neighbour sum in CSR order)
+    const float4 *st4p = reinterpret_cast<const float4 *>(kBwdfPf ? sStp : statp);
+    const float4 pmean = st4p[c4], pistd = st4p[16 + c4], psc = st4p[32 + c4], psh = st4p[48 + c4];
+    float4 sdy = make_float4(0.f, 0.f, 0.f, 0.f), sdx = sdy;
+    if (rows > 0) {  // block-uniform
+        float4 g[KR];
+        int32_t beg[KR], end[KR], u0[KR][4];
+        if constexpr (kBwdfPf) {
+#pragma unroll
+            for (int k = 0; k < KR; ++k) {
+                const int rr = rs + 16 * k;
+                beg[k] = sRp[rr < rows ? rr : rows];
+                end[k] = sRp[rr < rows ? rr + 1 : rows];
+#pragma unroll
+                for (int t = 0; t < 4; ++t) u0[k][t] = __float_as_int(nx[(4 * k + t) >> 3][(4 * k + t) & 7]);
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < KR; ++k) {
+                const int rr = rs + 16 * k;
+                const int64_t v = a + (rr < rows ? rr : rows - 1);
+                beg[k] = rowptr_t[v];
+                end[k] = rowptr_t[v + 1];
+            }
+#pragma unroll
+            for (int k = 0; k < KR; ++k) {
+                const int rr = rs + 16 * k;
+                zp[k] = ld4(z2p + (a + (rr < rows ? rr : rows - 1)) * 64 + 4 * c4);
+                if (rr >= rows) end[k] = beg[k];
+            }
+        }
+        int maxdeg = 0;
+#pragma unroll
+        for (int k = 0; k < KR; ++k) {
+            const int rr = rs + 16 * k;
+            maxdeg = end[k] - beg[k] > maxdeg ? end[k] - beg[k] : maxdeg;
+            const int sr = rr < rows ? rr : 0;
+            const float4 x = *reinterpret_cast<const float4 *>(sA + sr * 64 + 4 * c4);
+            g[k] = make_float4(ope * x.x, ope * x.y, ope * x.z, ope * x.w);
+        }
+        for (int j0 = 0; j0 < maxdeg; j0 += 4) {
+            if (j0 > 0 || !kBwdfPf) {  // (kBwdfPf: rows of degree > 4) a neighbour round
+#pragma unroll
+                for (int k = 0; k < KR; ++k)
+#pragma unroll
+                    for (int t = 0; t < 4; ++t) {
+                        const int32_t e = beg[k] + j0 + t;
+                        u0[k][t] = col_t[e < end[k] ? e : 0];
+                    }
+            }
+#pragma unroll
+            for (int k = 0; k < KR; ++k)
+#pragma unroll
+                for (int t = 0; t < 4; ++t) {
+                    int64_t sl = static_cast<int64_t>(u0[k][t]) - a;  // in-chunk (host-checked)
+                    sl = sl < 0 ? 0 : (sl < rows ? sl : rows - 1);
+                    const float4 x = *reinterpret_cast<const float4 *>(sA + sl * 64 + 4 * c4);
+                    if (beg[k] + j0 + t < end[k]) g[k] = add4(g[k], x);
+                }
+        }
+#pragma unroll
+        for (int k = 0; k < KR; ++k) {
+            const int rr = rs + 16 * k;
+            const float valid = rr < rows ? 1.f : 0.f;
+            const float4 zz = zp[k], gg = g[k];
+            const float4 d = make_float4((psc.x * zz.x + psh.x > 0.f ? gg.x : 0.f) * valid,
+                                         (psc.y * zz.y + psh.y > 0.f ? gg.y : 0.f) * valid,
+                                         (psc.z * zz.z + psh.z > 0.f ? gg.z : 0.f) * valid,
+                                         (psc.w * zz.w + psh.w > 0.f ? gg.w : 0.f) * valid);
+            if (rr < rows) st4(dyp_out + (a + rr) * 64 + 4 * c4, d);
+            sdy = add4(sdy, d);
+            sdx = add4(sdx, make_float4(d.x * (zz.x - pmean.x) * pistd.x, d.y * (zz.y - pmean.y) * pistd.y,
+                                        d.z * (zz.z - pmean.z) * pistd.z, d.w * (zz.w - pmean.w) * pistd.w));
+        }
+    }
+    {   // capacity mode: this chunk's share of the padding rows [n, ncap)
+        const int64_t p0 = chunk * TM > n ? chunk * TM : n;
+        const int64_t p1 = chunk * TM + TM < ncap ? chunk * TM + TM : ncap;
+        for (int64_t i = p0 * 16 + tid; i < p1 * 16; i += 256)
+            st4(dyp_out + i * 4, make_float4(0.f, 0.f, 0.f, 0.f));
+    }
+    // per-workgroup slab: dW2 | dW1 | db2 | db1 (gin_bwd_k layout), written
+    // after the statistics hierarchy (its arrival waits for every store)
+    auto write_slab = [&]() {
+        float *sl = slab + chunk * SLAB;
+        float *dw = nw ? sl + 64 * 64 : sl;
+        const int ld = nw ? DIN : 64;
+#pragma unroll
+        for (int reg = 0; reg < 16; ++reg) {
+            const int jr = q * 32 + acc_row(reg, l);
+            dw[jr * ld + li] = accA[reg];
+            dw[jr * ld + 32 + li] = accB[reg];
+        }
+        const float db = dbias + __shfl_xor(dbias, 32, kWave);
+        if (l < 32) sl[64 * 64 + 64 * DIN + (nw ? 64 : 0) + q * 32 + l] = db;
+    };
+    const int64_t nt = (n + TM - 1) / TM;
+    if (!kBwdfSlabLast || chunk >= nt) write_slab();
+    if (chunk >= nt) return;  // a chunk of padding rows only (block-uniform)
+    float *red = sDT;  // [2][16][64]: sDT's last reader passed the loop's barriers
+    {
+        float *x = red + rs * 64 + 4 * c4;
+        x[0] = sdy.x; x[1] = sdy.y; x[2] = sdy.z; x[3] = sdy.w;
+        float *y = red + (16 + rs) * 64 + 4 * c4;
+        y[0] = sdx.x; y[1] = sdx.y; y[2] = sdx.z; y[3] = sdx.w;
+    }
+    __syncthreads();
+    if (tid < 128) {
+        const int which = tid >> 6, ch = tid & 63;
+        float s = 0.f;
+        for (int k = 0; k < 16; ++k) s += red[(which * 16 + k) * 64 + ch];
+        st_agent(part + chunk * 128 + which * 64 + ch, s);
+    }
+    SCGIB_MARK(6);
+    bn_bwd_hier_s(part, n, chunk, bz, reinterpret_cast<double (*)[128]>(sD));
+    if (kBwdfSlabLast) write_slab();
+    SCGIB_MARK(7);
+}
+
 // up to two workgroups per CU (66.5 KB LDS each): one tile per workgroup for
 // batches up to SCGIB_BWD_GRID_CAP tiles (build-time knob), so every tile of
 // an encoder layer runs at once; larger batches loop over tiles
@@ -2171,6 +2543,49 @@ extern "C" int scgib_gin_layer_bwd(const float *dy, const float *z2, const float
     const int rc = launch_status();
     if (rc != SCGIB_OK || !wgrad) return rc;  // wgrad NULL: the caller reduces the slabs
     return launch_slab_reduce(slab, grid, 64 * 64 + 64 * static_cast<int64_t>(d_in) + 128, wgrad, st);
+}
+
+// ---- fused layer backward + previous layer's statistics (gin_bwdf_k) ----
+extern "C" int32_t scgib_gin_chunk_max_component() { return kChunkComp; }
+extern "C" int64_t scgib_gin_chunks(int64_t n_nodes) { return scgib_gin_tiles(n_nodes); }
+
+extern "C" int scgib_gin_chunk_bounds(const int32_t *graph_ptr, int64_t n_seg,
+                                      const int32_t *seg_dims, int64_t n_nodes,
+                                      const int32_t *dims, int32_t *chunk_ptr,
+                                      scgib_stream_t stream) {
+    if (n_seg < 0 || n_nodes <= 0 || !chunk_ptr || (n_seg > 0 && !graph_ptr)) return SCGIB_EINVAL;
+    const int64_t nchunk = scgib_gin_chunks(n_nodes);
+    gin_chunk_bounds_k<<<dim3(static_cast<unsigned>((n_seg + 1 + 255) / 256)), 256, 0,
+                         as_stream(stream)>>>(graph_ptr, n_seg, seg_dims, n_nodes, dims,
+                                              chunk_ptr, nchunk);
+    return launch_status();
+}
+
+extern "C" int scgib_gin_layer_bwd_fused(
+    const float *dy, const float *z2, const float *r, const float *agg, const float *stat,
+    const float *coef, const float *w1, const float *w2, int64_t n_nodes, const int32_t *chunk_ptr,
+    const int32_t *rowptr_t, const int32_t *col_t, float one_plus_eps, const float *z2_prev,
+    const float *stat_prev, int32_t training, float *dy_prev, float *dgamma_prev,
+    float *dbeta_prev, float *coef_prev, float *bn_ws_prev, uint32_t *counters, int32_t defer,
+    float *slab, const int32_t *dims, const scgib_bn_bwd_pending *pending,
+    const scgib_slab_job *fold, scgib_stream_t stream) {
+    if (!fold_ok(fold)) return SCGIB_EINVAL;
+    if (n_nodes <= 0 || !dy || !z2 || !r || !agg || !stat || (!coef && !pending) || !w1 || !w2 ||
+        !chunk_ptr || !rowptr_t || !col_t || !z2_prev || !stat_prev || !dy_prev || !bn_ws_prev ||
+        !counters || !slab)
+        return SCGIB_EINVAL;
+    if (pending && (!pending->gpart || !pending->dgamma || !pending->dbeta)) return SCGIB_EINVAL;
+    if (!defer && (!dgamma_prev || !dbeta_prev || !coef_prev)) return SCGIB_EINVAL;
+    const scgib_bn_bwd_pending pd = pending ? *pending : scgib_bn_bwd_pending{};
+    BnBwdFuse bz{counters, bn_gpart(bn_ws_prev, n_nodes), dgamma_prev, dbeta_prev, coef_prev,
+                 training, static_cast<int>(bn_groups(n_nodes)), defer ? 1 : 0};
+    const scgib_slab_job fj = fold ? *fold : scgib_slab_job{};
+    const int nfb = slab_fold_blocks(fj);
+    const int64_t grid = scgib_gin_chunks(n_nodes) + (nfb < kBwdfFoldWG ? nfb : kBwdfFoldWG);
+    gin_bwdf_k<64><<<dim3(static_cast<unsigned>(grid)), 256, 0, as_stream(stream)>>>(
+        dy, z2, r, agg, stat, coef, w1, w2, n_nodes, chunk_ptr, rowptr_t, col_t, one_plus_eps,
+        z2_prev, stat_prev, dy_prev, bn_ws_prev, bz, slab, dims, pd, fj);
+    return launch_status();
 }
 
 // ---------------------------------------------------------------------------

@@ -95,6 +95,9 @@ class GraphBatch:
         # {"deg": in-degree per node (np.int64), "selfloops": per-node 0/1,
         #  "validated": edges never leave their graph}
         self.host_info = host_info
+        # no edge leaves its graph_ptr segment (host-validated, or built so:
+        # ego batches, StaticBatch) -- the chunked fused GIN backward needs it
+        self.components_closed = bool(host_info is not None and host_info.get("validated"))
         # capacity mode: device int32 [actual nodes, actual edges]; the host
         # sizes above are then capacities (see StaticBatch)
         self.dims = None
@@ -201,6 +204,7 @@ class GraphBatch:
                        None if self.symmetric else mv(self.col_t), self.max_graph_nodes,
                        -1 if self._e is None else self._e, self.host_info)
         g.dims = mv(self.dims)
+        g.components_closed = self.components_closed
         g.ego_caps = self.ego_caps
         g.seg_dims = mv(self.seg_dims)
         for k, v in self.ndata.items():
@@ -320,6 +324,7 @@ def batch(graphs):
         col_t = torch.from_numpy(np.concatenate(colts).astype(np.int32))
     out = GraphBatch(torch.from_numpy(rowptr), torch.from_numpy(col),
                      torch.from_numpy(gptr.astype(np.int32)), bnn, bne, rp_t, col_t)
+    out.components_closed = bool(graphs) and all(g.components_closed for g in graphs)
     if graphs:
         for k in graphs[0].ndata.keys():
             dict.__setitem__(out.ndata, k, torch.cat([g.ndata[k].cpu() for g in graphs], 0))
@@ -415,6 +420,7 @@ def egonet_batch(g: GraphBatch, k: int, x=None):
     ego = GraphBatch(sub_rowptr, sub_col, ego_ptr, None, None, n_edges=e_s,
                      max_graph_nodes=mgn)
     ego.dims = ego_dims
+    ego.components_closed = True  # induced subgraphs: edges stay in their ego-net
     ego.seg_dims = g.dims  # the ego batch's segments are g's nodes
     dict.__setitem__(ego.ndata, "_ID", ego_nodes)
     if x is not None:
@@ -476,6 +482,7 @@ def _egonet_k1(g, ego_ptr, ego_eptr, ws, x, max_in_degree=12):
     ego = GraphBatch(sub_rowptr, sub_col, ego_ptr, None, None, n_edges=-1,
                      max_graph_nodes=max(g.max_graph_nodes, 1))
     ego.dims = ego_dims
+    ego.components_closed = True
     ego.seg_dims = g.dims
     dict.__setitem__(ego.ndata, "_ID", ego_nodes[:n_s])
     if x is not None:
@@ -504,6 +511,7 @@ class StaticBatch:
         self.graph = GraphBatch(self.rowptr, self.col, self.graph_ptr, None, None,
                                 max_graph_nodes=max_graph_nodes, n_edges=-1)
         self.graph.dims = self.dims
+        self.graph.components_closed = True  # pad() refuses batches whose edges leave a molecule
         # ego-net error word, zeroed by every load (no fill launch in the step)
         self.graph.err_buf = self.err
         self.graph.ego_caps = tuple(int(c) for c in ego_caps)

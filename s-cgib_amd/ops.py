@@ -59,6 +59,17 @@ BATCH_SLABS = os.environ.get("SCGIB_BATCH_SLABS", "1") != "0"
 # statistics launch (extra workgroups, scgib_gin_bwd_stats_bn_fold) instead of
 # the chain's final reduce launch; only layer 0's slabs are left for the end
 FOLD_SLABS = os.environ.get("SCGIB_FOLD_SLABS", "1") != "0"
+# encoder backward: layer l's backward and layer l-1's statistics in one
+# launch over component-aligned chunks (scgib_gin_layer_bwd_fused) when the
+# graph's components are closed and small enough; d(agg) then stays on chip.
+# Off: A/B within the box noise of the two-launch path (0.4632 vs 0.4652 ms,
+# three rounds) — the chunk kernel's per-workgroup chain (prologue, 2-3
+# sub-tiles at two workgroups per CU, then the statistics phase) is as long
+# as the two kernels it replaces, and its 437 slabs per layer move the
+# reduce to the chain's end
+FUSED_BWD = os.environ.get("SCGIB_FUSED_BWD", "0") != "0"
+# ... with layer l's slab reduce folded into layer l-1's fused launch
+FOLD_FUSED = os.environ.get("SCGIB_FOLD_FUSED", "1") != "0"
 # encoder-pair backward: capture the ego chain before the core chain (off:
 # measured 2 % slower — the replayed graph's queue assignment follows capture
 # order in ways that favour the core chain first)
@@ -303,6 +314,19 @@ def _interleave(first, first_stream, second, second_stream):
     return out[0], out[1]
 
 
+def _chunk_bounds(gr, n, L, st):
+    """Chunk table of the fused backward (scgib_gin_chunk_bounds), or None
+    when the fused path does not apply to this graph."""
+    if not (FUSED_BWD and L > 1 and n > 0 and gr.components_closed and
+            1 <= gr.max_graph_nodes <= int(_lib.query("scgib_gin_chunk_max_component"))):
+        return None
+    cp = torch.empty(int(_lib.query("scgib_gin_chunks", n)) + 1, dtype=torch.int32,
+                     device=gr.rowptr.device)
+    _lib.call("scgib_gin_chunk_bounds", _p(gr.graph_ptr), gr.batch_size, _p(gr.seg_dims), n,
+              _p(gr.dims), _p(cp), st)
+    return cp
+
+
 def _reduce_jobs(jobs, st, max_wg=0):
     cap = int(_lib.query("scgib_slab_reduce_max_jobs"))
     for i0 in range(0, len(jobs), cap):
@@ -476,15 +500,29 @@ class _GinEncoder(torch.autograd.Function):
         nslab = int(_lib.query("scgib_gin_bwd_slabs", n))
         jobs, keep = [], []
         fold = None  # the previous layer's slab job, reduced by the next stats launch
+        chunks = _chunk_bounds(gr, n, L, st)
+        # the fused launches alternate two BN-backward workspaces
+        ws_pair = (bn_ws, torch.empty_like(bn_ws)) if chunks is not None else (bn_ws,)
+        gpart_off = gpart - bn_ws.data_ptr()
+        carry = None  # (dy, bn_g, coef, ws) of layer l from layer l + 1's fused launch
         for l in reversed(range(L)):
             agg, r, z2, stat = saved[4 * l: 4 * l + 4]
             w1, _, w2 = params[6 * l], params[6 * l + 1], params[6 * l + 2]
             d_in = agg.shape[1]
-            dy = torch.empty(n, HIDDEN, dtype=torch.float32, device=dev)
-            bn_g = torch.empty(2, HIDDEN, dtype=torch.float32, device=dev)  # dgamma, dbeta
-            coef = torch.empty(2, HIDDEN, dtype=torch.float32, device=dev)
+            from_fused = carry is not None
+            if from_fused:
+                dy, bn_g, coef, ws_l = carry
+                carry = None
+            else:
+                dy = torch.empty(n, HIDDEN, dtype=torch.float32, device=dev)
+                bn_g = torch.empty(2, HIDDEN, dtype=torch.float32, device=dev)  # dgamma, dbeta
+                coef = torch.empty(2, HIDDEN, dtype=torch.float32, device=dev)
+                ws_l = bn_ws
+            gpart = ws_l.data_ptr() + gpart_off
             # dy, tile sums and the BN-backward finalize in one launch
-            if dagg_next is None and g_readout is not None:
+            if from_fused:
+                pass  # made by layer l + 1's fused launch
+            elif dagg_next is None and g_readout is not None:
                 # the readout's broadcast backward folded into the last layer
                 _launch("scgib_gin_bwd_stats_seg_bn", {"n": n, "e": 0, "d_in": HIDDEN}, _p(g_out), _p(g_readout),
                         _p(ctx.seg), _p(z2), _p(stat), n, int(ctx.training), _p(dy),
@@ -515,6 +553,24 @@ class _GinEncoder(torch.autograd.Function):
                         ctx.n_feat, _p(stat), _p(coef), _p(w1c), _p(w2c), n, _p(slab), _p(gr.dims),
                         _byref(bpend), st)
                 dagg = None
+            elif chunks is not None and l > 0 and d_in == HIDDEN:
+                # layer l's backward + layer l-1's dy and BN-backward sums
+                width = HIDDEN * HIDDEN + HIDDEN * d_in + 2 * HIDDEN
+                nch = int(_lib.query("scgib_gin_chunks", n))
+                slab = torch.empty(nch * width, dtype=torch.float32, device=dev)
+                z2p, statp = saved[4 * (l - 1) + 2], saved[4 * (l - 1) + 3]
+                ws_n = ws_pair[1] if ws_l is ws_pair[0] else ws_pair[0]
+                dyp = torch.empty(n, HIDDEN, dtype=torch.float32, device=dev)
+                bn_gp = torch.empty(2, HIDDEN, dtype=torch.float32, device=dev)
+                coefp = torch.empty(2, HIDDEN, dtype=torch.float32, device=dev)
+                _launch("scgib_gin_layer_bwd_fused", meta, _p(dy), _p(z2), _p(r), _p(agg),
+                        _p(stat), _p(coef), _p(w1c), _p(w2c), n, _p(chunks), _p(gr.rowptr_t),
+                        _p(gr.col_t), ctx.opes[l], _p(z2p), _p(statp), int(ctx.training),
+                        _p(dyp), _p(bn_gp[0]), _p(bn_gp[1]), _p(coefp), _p(ws_n), _p(cnt),
+                        defer, _p(slab), _p(gr.dims), _byref(bpend), _byref(fold), st)
+                fold = None
+                carry = (dyp, bn_gp, coefp, ws_n)
+                dagg = None
             else:
                 width = HIDDEN * HIDDEN + HIDDEN * d_in + 2 * HIDDEN
                 slab = torch.empty(int(_lib.query("scgib_gin_slab_floats", n, d_in)),
@@ -539,15 +595,22 @@ class _GinEncoder(torch.autograd.Function):
                 jobs.append(_lib.SlabJob(slab.data_ptr(), wgrad.data_ptr(), used, nslab, width))
                 keep.append(slab)
             elif BATCH_SLABS:  # reduced by the next stats launch, or together at the end
-                ns = int(_lib.query("scgib_gin_layer_bwd_slabs", n, d_in))
+                ns = int(_lib.query("scgib_gin_chunks", n)) if carry is not None else \
+                    int(_lib.query("scgib_gin_layer_bwd_slabs", n, d_in))
                 job = _lib.SlabJob(slab.data_ptr(), wgrad.data_ptr(), width, ns, 0)
                 keep.append(slab)
-                if FOLD_SLABS and l > 0:
+                if carry is not None:  # folded into the next fused launch, if any
+                    if FOLD_FUSED and l > 1:
+                        fold = job
+                    else:
+                        jobs.append(job)
+                elif FOLD_SLABS and l > 0:
                     fold = job
                 else:
                     jobs.append(job)
             else:
-                ns = int(_lib.query("scgib_gin_layer_bwd_slabs", n, d_in))
+                ns = int(_lib.query("scgib_gin_chunks", n)) if carry is not None else \
+                    int(_lib.query("scgib_gin_layer_bwd_slabs", n, d_in))
                 _lib.call("scgib_slab_reduce", _p(slab), ns, width, _p(wgrad), st)
             o = HIDDEN * HIDDEN
             grads[6 * l + 2] = wgrad[:o].view(HIDDEN, HIDDEN)

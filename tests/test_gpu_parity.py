@@ -339,11 +339,40 @@ def test_pretrain_step_matches_reference(pkg, dev, name, device_ego):
 
 
 # ---------------------------------------------------------------------------
+# chunk table of the fused backward: chunk c = components starting in [64c, 64c+64)
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("n_mols,workload,pad", [(300, "qm9", 0), (37, "qm9", 200), (1, "qm9", 0),
+                                                 (120, "zinc", 70)])
+def test_gin_chunk_bounds(pkg, dev, n_mols, workload, pad):
+    g, gh = rand_graph(pkg, n_mols, workload, 5, dev)
+    n = g.num_nodes()
+    gp = gh.graph_ptr.numpy().astype(np.int64)
+    ncap = n + pad
+    dims = torch.tensor([n, g.num_edges()], dtype=torch.int32, device=dev) if pad else None
+    nch = int(pkg._lib.query("scgib_gin_chunks", ncap))
+    cp = torch.full((nch + 1,), -7, dtype=torch.int32, device=dev)
+    pkg._lib.call("scgib_gin_chunk_bounds", pkg.ops._p(g.graph_ptr), g.batch_size, None, ncap,
+                  pkg.ops._p(dims), pkg.ops._p(cp), None)
+    starts = np.append(gp[:-1], n)
+    want = [int(starts[np.searchsorted(starts, 64 * c)]) if 64 * c <= n else n
+            for c in range(nch + 1)]
+    assert cp.cpu().tolist() == want
+    sizes = np.diff(np.array(want))
+    if gh.max_graph_nodes <= int(pkg._lib.query("scgib_gin_chunk_max_component")):
+        assert sizes.max() <= 96
+
+
+# ---------------------------------------------------------------------------
 # A5 fused: GIN encoder (fused HIP layers) vs the oracle's GIN
 # ---------------------------------------------------------------------------
+@pytest.mark.parametrize("fused_bwd", [True, False])
 @pytest.mark.parametrize("training", [True, False])
 @pytest.mark.parametrize("layers,n_mols", [(5, 300), (4, 37), (2, 1)])
-def test_fused_gin_encoder(pkg, dev, training, layers, n_mols):
+def test_fused_gin_encoder(pkg, dev, training, layers, n_mols, fused_bwd, monkeypatch):
+    """fused_bwd: layers >= 1 run backward + the previous layer's statistics
+    as one chunked launch (scgib_gin_layer_bwd_fused); False: the two-launch
+    path (gin_bwd5_k + gin_bwd_stats_k)."""
+    monkeypatch.setattr(pkg.ops, "FUSED_BWD", fused_bwd)
     torch.manual_seed(layers)
     g, gh = rand_graph(pkg, n_mols, "qm9", 11, dev)
     gin = pkg.models.GIN(32, 64, layers)

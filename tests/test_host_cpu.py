@@ -17,7 +17,7 @@ from oracle import egonet
 # ---------------------------------------------------------------------------
 def header_symbols():
     src = open(os.path.join(ROOT, "include", "scgib.h")).read()
-    return sorted(set(re.findall(r"^\s*(?:int|int64_t|const char \*)\s*(scgib_\w+)\(", src,
+    return sorted(set(re.findall(r"^\s*(?:int|int32_t|int64_t|const char \*)\s*(scgib_\w+)\(", src,
                                  re.M)))
 
 
@@ -188,7 +188,7 @@ def _header_prototypes():
     src = open(os.path.join(ROOT, "include", "scgib.h")).read()
     src = re.sub(r"/\*.*?\*/|//[^\n]*", "", src, flags=re.S)
     out = {}
-    for m in re.finditer(r"(?:int|int64_t|const char \*)\s*(scgib_\w+)\(([^)]*)\)\s*;", src):
+    for m in re.finditer(r"(?:int|int32_t|int64_t|const char \*)\s*(scgib_\w+)\(([^)]*)\)\s*;", src):
         params = [p.strip() for p in m.group(2).split(",") if p.strip() not in ("", "void")]
         kinds = []
         for p in params:

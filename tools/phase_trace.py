@@ -27,6 +27,8 @@ PHASES = {
     "scgib_gin_layer0_fwd": ["gather", "gemm1", "gemm2+st", "tilestat", "bn_hier"],
     # gin_bwd5_k: marks of the first sub-tile, then the remaining sub-tiles
     "scgib_gin_layer_bwd": ["prologue", "dz2", "pairA", "pairB", "rest", "slab"],
+    # gin_bwdf_k: + layer l-1's statistics (gather from the LDS d(agg) image)
+    "scgib_gin_layer_bwd_fused": ["prologue", "dz2", "pairA", "pairB", "rest", "stats", "bn_hier"],
     "scgib_gin_layer0_bwd": ["ld+dz2", "dW2,dr", "dW1,dagg", "slab"],
     "scgib_gin_bwd_stats_bn": ["gather+dy", "bn_hier"],
     "scgib_gin_bwd_stats_bn_fold": ["gather+dy", "bn_hier"],

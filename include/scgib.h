@@ -483,7 +483,10 @@ int scgib_mlp2_bwd(const float *dout, const float *x, const float *r, int32_t d_
  * partials) and must be passed unchanged to the backward; `counter` is one
  * zeroed uint32, left zero.  Backward: dx = d loss / d x and wgrad as
  * scgib_mlp2_bwd, for d loss / d recon = *g_loss; rowptr_t/col_t NULL for a
- * symmetric graph (A = A^T). */
+ * symmetric graph (A = A^T).  wgrad NULL: the per-workgroup slabs
+ * (scgib_mlp2_slab_floats(n, d_in) floats, width 64*64 + 64*d_in + 128) are
+ * left for the caller's scgib_slab_reduce(_multi) — the model path defers
+ * them into an encoder chain's final reduce, off the loss section. */
 int64_t scgib_mlp2_recon_ws_floats(int64_t n_nodes);
 int scgib_mlp2_recon_fwd(const float *x, int32_t d_in, int64_t n_nodes, const float *w1,
                          const float *b1, const float *w2, const float *b2, float *r, float *out,
@@ -521,6 +524,8 @@ int scgib_mlp2_recon_contrastive_bwd(const float *x, const float *r, const float
 int64_t scgib_linear_slab_floats(int64_t n_nodes);
 int scgib_linear_fwd(const float *x, int64_t n_nodes, const float *w, const float *b, float *out,
                      const int32_t *dims, scgib_stream_t stream);
+/* wgrad NULL: the slabs (scgib_linear_slab_floats(n) floats, width 64*64 + 64)
+ * are left for the caller's reduce. */
 int scgib_linear_bwd(const float *dy, const float *x, const float *w, int64_t n_nodes,
                      const float *add, float *dx, float *slab, float *wgrad,
                      const int32_t *dims, scgib_stream_t stream);

@@ -145,12 +145,12 @@ extern "C" int scgib_linear_fwd(const float *x, int64_t n_nodes, const float *w,
 extern "C" int scgib_linear_bwd(const float *dy, const float *x, const float *w, int64_t n_nodes,
                                 const float *add, float *dx, float *slab, float *wgrad,
                                 const int32_t *dims, scgib_stream_t stream) {
-    if (n_nodes <= 0 || !dy || !x || !w || !dx || !slab || !wgrad) return SCGIB_EINVAL;
+    if (n_nodes <= 0 || !dy || !x || !w || !dx || !slab) return SCGIB_EINVAL;
     const int64_t nt = (n_nodes + TM - 1) / TM;
     const int grid = lin_grid(nt);
     hipStream_t st = as_stream(stream);
     linear_bwd_k<<<grid, 256, 0, st>>>(dy, x, w, n_nodes, nt, add, dx, slab, dims);
     const int rc = launch_status();
-    if (rc != SCGIB_OK) return rc;
+    if (rc != SCGIB_OK || !wgrad) return rc;  // wgrad NULL: the caller reduces the slabs
     return launch_slab_reduce(slab, grid, kLinSlab, wgrad, st);
 }

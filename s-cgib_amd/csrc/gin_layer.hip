@@ -2718,7 +2718,7 @@ static int mlp2_recon_bwd(const float *x, const float *r, const float *out, cons
                           scgib_stream_t stream) {
     if (n_nodes <= 0 || (d_in != 64 && d_in != 128)) return SCGIB_EINVAL;
     if (!x || !r || !out || !ws || !w1 || !w2 || !rowptr || !col || !g_loss || !dx || !slab ||
-        !wgrad || ((rowptr_t == nullptr) != (col_t == nullptr)))
+        ((rowptr_t == nullptr) != (col_t == nullptr)))
         return SCGIB_EINVAL;
     const int64_t nt = scgib_gin_tiles(n_nodes);
     const int grid = bwd_grid(nt);
@@ -2741,7 +2741,7 @@ static int mlp2_recon_bwd(const float *x, const float *r, const float *out, cons
     else
         gin_bwd_k<64, false, false, true><<<grid, 256, 0, st>>>(nullptr, nullptr, r, x, nullptr, nullptr, w1, w2, n_nodes, nt, dx, slab, dims, nullptr, scgib_bn_bwd_pending{}, rec);
     const int rc = launch_status();
-    if (rc != SCGIB_OK) return rc;
+    if (rc != SCGIB_OK || !wgrad) return rc;  // wgrad NULL: the caller reduces the slabs
     return launch_slab_reduce(slab, grid, 64 * 64 + 64 * static_cast<int64_t>(d_in) + 128, wgrad, st);
 }
 

@@ -9,6 +9,7 @@ from __future__ import annotations
 import contextlib
 import ctypes
 import os
+import weakref
 
 import numpy as np
 import torch
@@ -106,6 +107,56 @@ _AUX_DEFERRED = []
 _DEFER_DEPTH = [0]
 
 
+# Loss-section weight-gradient reduces deferred into the encoder pair's
+# backward (the head MLP's, the interaction's and compressor[0]'s slabs are
+# summed by Encoder1's final scgib_slab_reduce_multi instead of one reduce
+# launch each on the loss chain).  The gradient tensors these backward
+# functions return are then written by a launch enqueued LATER in the same
+# backward pass, so a deferral is taken only when nothing can read them
+# before: every parameter's .grad is None (AccumulateGrad takes the tensor
+# without a kernel) and no other encoder-pair forward is awaiting its
+# backward (two forwards into one backward would make autograd add the two
+# gradients first).  Anything else reduces inline, as before.
+DEFER_LOSS_REDUCE = os.environ.get("SCGIB_DEFER_LOSS_REDUCE", "1") != "0"
+
+
+class SlabScope:
+    """Slab-reduce jobs collected between an encoder pair's forward and its
+    backward (which drains them into a chain's final reduce)."""
+
+    _live = weakref.WeakSet()
+
+    def __init__(self):
+        self.jobs, self.keep = [], []
+        self.open, self.ok = True, True
+        for other in list(SlabScope._live):
+            if other.open:  # two forwards awaiting one backward: defer nothing
+                other.ok = self.ok = False
+        SlabScope._live.add(self)
+
+    def usable(self, params):
+        return self.open and self.ok and all(p is None or p.grad is None for p in params)
+
+    def add(self, slab, wgrad, width, n_slabs):
+        self.jobs.append(_lib.SlabJob(slab.data_ptr(), wgrad.data_ptr(), width, n_slabs, 0))
+        self.keep += [slab, wgrad]
+
+    def take(self):
+        self.open = False
+        jobs, keep = self.jobs, self.keep
+        self.jobs, self.keep = [], []
+        return jobs, keep
+
+
+_SLAB_SCOPE = [None]  # the latest encoder pair's scope (captured by later loss ops)
+
+
+def _slab_scope_for(params):
+    """The current scope if a backward may defer its reduce into it."""
+    sc = _SLAB_SCOPE[0]  # (autograd Function forwards run with grad mode off)
+    return sc if (sc is not None and DEFER_LOSS_REDUCE) else None
+
+
 @contextlib.contextmanager
 def aside_deferred():
     _DEFER_DEPTH[0] += 1
@@ -179,6 +230,7 @@ def discard_aside():
     """Error path of a model forward: drop aside work that was deferred but
     never enqueued (replaying it with the next batch would apply that batch's
     running-stat update twice) and join what already ran on the aux stream."""
+    _SLAB_SCOPE[0] = None
     _AUX_DEFERRED.clear()
     if _AUX_PENDING:
         main = torch.cuda.current_stream()
@@ -204,6 +256,7 @@ def aside_guard(fn):
 
 
 def join_aside():
+    _SLAB_SCOPE[0] = None  # end of a model forward: later standalone ops never defer
     if not _AUX_PENDING:
         return
     main = torch.cuda.current_stream()
@@ -625,6 +678,11 @@ class _GinEncoder(torch.autograd.Function):
             grads[6 * l + 5] = bn_g[1]
             dagg_next = dagg
             yield
+        extra = getattr(ctx, "extra_jobs", None)
+        if extra is not None:  # deferred loss-section slabs (SlabScope), same launch
+            ctx.extra_jobs = None
+            jobs.extend(extra[0])
+            keep.extend(extra[1])
         if l0 is not None and l0[3]:
             l0[4].append((jobs, keep))  # launched by the caller after the chains join
         elif jobs:  # every layer's weight-gradient slabs, one fixed-order reduce launch
@@ -684,6 +742,11 @@ class _GinEncoderPair(torch.autograd.Function):
         main = _torch_stream()
         ne = 6 * len(gin_ego.ginlayers)
         ctx.set_materialize_grads(False)  # unused outputs (e.g. s) get no zero-fill launch
+        # the loss-section reduces of this step are deferred into this node's
+        # backward (SlabScope); only when the node will have a backward
+        grad = any(isinstance(p, torch.Tensor) and p.requires_grad for p in (wt, w0, b0, *params))
+        ctx.scope = SlabScope() if (DEFER_LOSS_REDUCE and grad) else None
+        _SLAB_SCOPE[0] = ctx.scope
         ctx.sub = (_Ctx(), _Ctx())
         ctx.side, ctx.ne = side, ne
         check_fork(main)
@@ -705,6 +768,7 @@ class _GinEncoderPair(torch.autograd.Function):
             f = _drain(core_steps)
         outs = (s, ro, f)
         ctx.lin = w0 is not None
+        ctx.lin_leaves = (w0, b0)
         if ctx.lin:  # compressor[0] on the (shorter) core chain, before the join
             w0, b0 = _f32(w0, "compressor.0.weight"), _f32(b0, "compressor.0.bias")
             if tuple(w0.shape) != (HIDDEN, HIDDEN):
@@ -733,8 +797,13 @@ class _GinEncoderPair(torch.autograd.Function):
         check_fork(main)
         side.wait_stream(main)
         # Encoder1's final weight-gradient reduce runs beside the ego chain's
-        # last layers (optionally capped, SIDE_REDUCE_WG)
+        # last layers (optionally capped, SIDE_REDUCE_WG); it also sums the
+        # loss section's deferred slabs (SlabScope: the head MLP's and the
+        # interaction's, enqueued on the main stream before this fork, and
+        # compressor[0]'s below) — Encoder1's chain ends well before the ego
+        # chain's, so they leave the critical path
         ctx.sub[1].reduce_wg = SIDE_REDUCE_WG
+        scope = ctx.scope if (ctx.scope is not None and ctx.scope.open) else None
         dw0 = db0 = None
         g_f_in = g_f
         if EGO_FIRST and not INTERLEAVE_BWD:  # capture the critical ego chain first
@@ -763,11 +832,19 @@ class _GinEncoderPair(torch.autograd.Function):
                                    dtype=torch.float32, device=f.device)
                 wg = torch.empty(HIDDEN * HIDDEN + HIDDEN, dtype=torch.float32, device=f.device)
                 df_total = torch.empty_like(f)
+                lin_defer = scope is not None and scope.usable(ctx.lin_leaves)
                 _lib.call("scgib_linear_bwd", _p(g_t), _p(f), _p(w0), n,
                           _p(_f32(g_f, "g_f")) if g_f is not None else None, _p(df_total),
-                          _p(slab), _p(wg), _p(ctx.core_dims), _stream())
+                          _p(slab), None if lin_defer else _p(wg), _p(ctx.core_dims), _stream())
+                if lin_defer:
+                    scope.add(slab, wg, wg.numel(), slab.numel() // wg.numel())
                 dw0, db0 = wg[: HIDDEN * HIDDEN].view(HIDDEN, HIDDEN), wg[HIDDEN * HIDDEN:]
                 g_f = df_total
+            if scope is not None:
+                jobs, keep = scope.take()
+                for tsr in keep:  # made on the main stream, reduced / written on side
+                    tsr.record_stream(side)
+                ctx.sub[1].extra_jobs = (jobs, keep)
             if not INTERLEAVE_BWD:
                 gc = _drain(_GinEncoder.backward_steps(ctx.sub[1], g_f, l0=l0_c))
         if INTERLEAVE_BWD:  # both chains enqueued layer by layer, the ego chain first
@@ -937,11 +1014,15 @@ def _interaction_backward(ctx, saved, g_im, g_z1, g_z2, g_kl, g_klmean):
     ds = torch.empty_like(s)
     pgrad = torch.empty(max(B, 1), PGRAD_STRIDE, dtype=torch.float32, device=dev)
     pg = torch.empty(PGRAD_STRIDE, dtype=torch.float32, device=dev)
+    scope = getattr(ctx, "scope", None)
+    defer = B > 0 and scope is not None and scope.usable(ctx.leaves)
     _lib.call("scgib_interaction_bwd", _p(g_im), _p(g_z1), _p(g_z2), _p(g_kl), _p(f), _p(t),
               _p(s), _p(u_feat), _p(ctx.graph.graph_ptr), B, n, _p(gamma), _p(beta),
               _p(ctx.rm), _p(ctx.rv), ctx.bn_eps, int(ctx.training), _p(w2), _p(w_att),
               _p(z1), _p(lam), _p(logit), _p(stats), _p(df), _p(dt), _p(ds), _p(pgrad),
-              _p(g_klmean), int(ctx.pad), _p(pg), _stream())
+              _p(g_klmean), int(ctx.pad), None if defer else _p(pg), _stream())
+    if defer:  # the per-graph partials are summed by the encoder pair's backward
+        scope.add(pgrad, pg, PGRAD_STRIDE, B)
     grads = (pg[65:129], pg[129:193], pg[0:64].view(1, 64), pg[64:65],
              pg[193:321].view(1, 128), pg[321:322])  # dgamma dbeta dW2 db2 dWatt dbatt
     return df, dt, ds, grads
@@ -951,6 +1032,8 @@ class _Interaction(torch.autograd.Function):
     @staticmethod
     def forward(ctx, f, t, s, u_gate, u_feat, gamma, beta, w2, b2, w_att, b_att, graph, bn,
                 training):
+        ctx.leaves = (gamma, beta, w2, b2, w_att, b_att)
+        ctx.scope = _slab_scope_for(ctx.leaves)
         f = _f32(f, "interaction")
         t, s = _f32(t, "interaction"), _f32(s, "interaction")
         outs, saved = _interaction_forward(ctx, f, t, s, u_gate, u_feat, gamma, beta, w2, b2,
@@ -1289,6 +1372,8 @@ class _Mlp2ReconContrastive(torch.autograd.Function):
         if z1.shape != (B, HIDDEN) or z2.shape != (B, HIDDEN):
             raise _lib.ScgibError(f"contrastive: z1 {tuple(z1.shape)} / z2 {tuple(z2.shape)} "
                                   f"must both be [B, {HIDDEN}]")
+        ctx.leaves = (w1, b1, w2, b2)
+        ctx.scope = _slab_scope_for(ctx.leaves)
         w1, b1, w2, b2 = (_f32(t, "mlp2 params") for t in (w1, b1, w2, b2))
         dev = x.device
         r = torch.empty(n, HIDDEN, dtype=torch.float32, device=dev)
@@ -1329,12 +1414,15 @@ class _Mlp2ReconContrastive(torch.autograd.Function):
                          device=dev)
         ccnt = counters(dev, "contrastive", int(_lib.query("scgib_contrastive_counters", B)))
         sym = gr.symmetric
+        defer = ctx.scope is not None and ctx.scope.usable(ctx.leaves)
         _launch("scgib_mlp2_recon_contrastive_bwd", {"n": n, "d_in": d_in, "B": B}, _p(x), _p(r),
                 _p(out), _p(ws), d_in,
                   _p(w1), _p(w2), n, _p(gr.rowptr), _p(gr.col),
                   None if sym else _p(gr.rowptr_t), None if sym else _p(gr.col_t), _p(g_loss),
-                  _p(dx), _p(slab), _p(wg), _p(gr.dims), _p(z1), _p(z2), B, _p(cws), _p(g_con),
-                  _p(dz1), _p(dz2), _p(ccnt), _stream())
+                  _p(dx), _p(slab), None if defer else _p(wg), _p(gr.dims), _p(z1), _p(z2), B,
+                  _p(cws), _p(g_con), _p(dz1), _p(dz2), _p(ccnt), _stream())
+        if defer:  # reduced by the encoder pair's backward (SlabScope)
+            ctx.scope.add(slab, wg, wg.numel(), slab.numel() // wg.numel())
         o = HIDDEN * HIDDEN
         dw2 = wg[:o].view(HIDDEN, HIDDEN)
         dw1 = wg[o: o + HIDDEN * d_in].view(HIDDEN, d_in)

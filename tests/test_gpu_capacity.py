@@ -179,3 +179,43 @@ def test_nested_fork_refused_while_capturing(pkg, dev, monkeypatch):
     _, aux = pkg.ops._aux_stream(dev)
     with pytest.raises(RuntimeError, match="nested forks"):
         pkg.ops.check_fork(aux)
+
+
+def test_deferred_loss_reduces_bitwise(pkg, dev, monkeypatch):
+    """SlabScope: the head MLP's, the interaction's and compressor[0]'s
+    weight-gradient slabs summed by Encoder1's final multi-job reduce give the
+    same gradients, bit for bit, as their own reduce launches (same fixed
+    order per job); and the deferral is actually taken (3 jobs per step)."""
+    gh = _batches(pkg, (9,))[0]
+    g = gh.to(dev)
+    n = g.num_nodes()
+    ug, uf = _noise(n, dev, 300)
+    m_inline = _model(pkg, dev)
+    m_defer = copy.deepcopy(m_inline)
+    added = []
+    orig_add = pkg.ops.SlabScope.add
+
+    def counting_add(self, *a):
+        added.append(a[2])
+        return orig_add(self, *a)
+
+    monkeypatch.setattr(pkg.ops.SlabScope, "add", counting_add)
+    monkeypatch.setattr(pkg.ops, "DEFER_LOSS_REDUCE", False)
+    l_inline = _step(m_inline, g, g.ndata["x"], (ug, uf), dev)
+    assert added == []
+    monkeypatch.setattr(pkg.ops, "DEFER_LOSS_REDUCE", True)
+    l_defer = _step(m_defer, g, g.ndata["x"], (ug, uf), dev)
+    torch.cuda.synchronize()
+    assert len(added) == 3, added  # head MLP, interaction, compressor[0]
+    assert torch.equal(l_inline, l_defer)
+    inline = dict(m_inline.named_parameters())
+    for k, p in m_defer.named_parameters():
+        if p.grad is not None:
+            assert torch.equal(p.grad, inline[k].grad), k
+    # a .grad already present (accumulation): the reduces stay inline
+    added.clear()
+    _, kl, con, rec = m_defer(g, g.ndata["x"], None, None, None, 1, None, 1, dev, B,
+                              noise=(ug, uf))
+    (kl + rec + con).backward()
+    torch.cuda.synchronize()
+    assert added == []

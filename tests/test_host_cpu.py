@@ -354,3 +354,27 @@ def test_ego_bounds_match_oracle_sizes(pkg):
         assert ns == int(sizes.sum())
         assert es >= int(ecount.sum())
         assert dmax == int(np.diff(g.rowptr.numpy()).max())
+
+
+def test_slab_scope_rules(pkg):
+    """ops.SlabScope (host logic, no launch): usable only while open, with
+    every parameter's .grad None, and with no other scope awaiting its
+    backward; take() closes it and hands over the jobs."""
+    ops = pkg.ops
+    w = torch.zeros(4, requires_grad=True)
+    a = ops.SlabScope()
+    assert a.usable((w, None))
+    slab, out = torch.zeros(8), torch.zeros(4)
+    a.add(slab, out, 4, 2)
+    w.grad = torch.zeros(4)
+    assert not a.usable((w,))
+    w.grad = None
+    b = ops.SlabScope()  # a second forward before a's backward: neither defers
+    assert not a.usable((w,)) and not b.usable((w,))
+    jobs, keep = a.take()
+    assert len(jobs) == 1 and jobs[0].n_slabs == 2 and jobs[0].width == 4
+    assert keep[0] is slab and keep[1] is out
+    assert not a.usable((w,))
+    del b
+    c = ops.SlabScope()  # a closed scope does not poison a new one
+    assert c.usable((w,))

@@ -330,6 +330,17 @@ int scgib_egonet_k1_build_deg(const int32_t *rowptr, const int32_t *col, int64_t
                               void *workspace, int32_t *ego_nodes, int32_t *sub_rowptr,
                               int32_t *sub_col, int64_t n_ego_cap, const int32_t *dims,
                               int32_t *ego_dims, scgib_stream_t stream);
+/* The same in ONE launch: each block of 64 parents takes its offsets by a
+ * decoupled look-back over the preceding blocks instead of a second launch.
+ * scan_state: scgib_egonet_k1_scan_words(n) ZEROED uint32 words, 4-byte
+ * aligned, left zeroed by the launch (reusable by the next one; one launch in
+ * flight per scan_state).  Output identical to scgib_egonet_k1_build_deg. */
+int64_t scgib_egonet_k1_scan_words(int64_t n_nodes);
+int scgib_egonet_k1_build_onepass(const int32_t *rowptr, const int32_t *col, int64_t n_nodes,
+                                  int32_t max_in_degree, int32_t *ego_ptr, int32_t *ego_eptr,
+                                  uint32_t *scan_state, int32_t *ego_nodes, int32_t *sub_rowptr,
+                                  int32_t *sub_col, int64_t n_ego_cap, const int32_t *dims,
+                                  int32_t *ego_dims, scgib_stream_t stream);
 int scgib_egonet_fill(const int32_t *rowptr, const int32_t *col, const int32_t *graph_ptr,
                       int64_t n_graphs, int64_t n_nodes, int32_t k, int32_t max_graph_nodes,
                       const int32_t *ego_ptr, const int32_t *ego_eptr, int32_t *ego_nodes,

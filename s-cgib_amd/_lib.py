@@ -31,6 +31,9 @@ SIGNATURES = {
                                              _P]),
     "scgib_egonet_k1_build_deg": (ctypes.c_int, [_P, _P, _I64, _I32, _P, _P, _P, _P, _P, _P, _I64,
                                                  _P, _P, _P]),
+    "scgib_egonet_k1_scan_words": (_I64, [_I64]),
+    "scgib_egonet_k1_build_onepass": (ctypes.c_int, [_P, _P, _I64, _I32, _P, _P, _P, _P, _P, _P,
+                                                     _I64, _P, _P, _P]),
     "scgib_egonet_fill": (ctypes.c_int, [_P, _P, _P, _I64, _I64, _I32, _I32, _P, _P, _P, _P, _P,
                                          _P, _I64, _P, _P, _P]),
     "scgib_interaction_fwd": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _I64, _I64, _P, _P, _P, _P,

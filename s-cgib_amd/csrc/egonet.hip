@@ -253,14 +253,15 @@ __global__ __launch_bounds__(256) void egonet_fill_k(
 // DGL's sorted order; the relabelled id of a member is a popcount.  Every
 // load round is batched: row pointers of v; its <= kK1Deg neighbour ids; the
 // row pointers of the ball members; their neighbour ids (members in groups of
-// kK1Grp, clamped always-valid addresses, predicates applied to the values).
+// K1G<D>, clamped always-valid addresses, predicates applied to the values).
 // Requires in-degree <= kK1Deg, molecules <= 64 atoms and edges inside their
 // molecule (host-checked).  Two launches: count + block scan, then fill with
 // the cross-block scan fix-up folded in.
 // ---------------------------------------------------------------------------
 // D = the in-degree bound the launch was built for (6: one member group of
 // 7 = |ball|, every molecule set of the benchmarks; 12: two groups)
-constexpr int kK1Grp = 7;
+// members per load group: the whole ball for D <= 8 (one rows round), else 7
+template <int D> constexpr int K1G = D <= 8 ? D + 1 : 7;
 template <int D> struct K1 {
     static constexpr int kDeg = D, kBall = D + 1;
 };
@@ -323,26 +324,26 @@ __device__ __forceinline__ void k1_ball(const int32_t *__restrict__ rowptr,
     }
 }
 
-// rows of members [g0, g0 + kK1Grp) and their neighbour ids, one batched round each
+// rows of members [g0, g0 + K1G<D>) and their neighbour ids, one batched round each
 template <int D>
 struct K1Rows {
-    int32_t beg[kK1Grp], deg[kK1Grp];
-    int32_t w[kK1Grp][D];
+    int32_t beg[K1G<D>], deg[K1G<D>];
+    int32_t w[K1G<D>][D];
 };
 
 template <int D, int G0>
 __device__ __forceinline__ void k1_rows(const int32_t *__restrict__ rowptr,
                                         const int32_t *__restrict__ col, const K1Win<D> &b,
                                         K1Rows<D> &m) {
-    int32_t end[kK1Grp];
+    int32_t end[K1G<D>];
 #pragma unroll
-    for (int r = 0; r < kK1Grp; ++r) {
+    for (int r = 0; r < K1G<D>; ++r) {
         const int32_t u = b.mem[G0 + r < D + 1 ? G0 + r : D];
         m.beg[r] = rowptr[u];
         end[r] = rowptr[u + 1];
     }
 #pragma unroll
-    for (int r = 0; r < kK1Grp; ++r) {
+    for (int r = 0; r < K1G<D>; ++r) {
         m.deg[r] = end[r] - m.beg[r];
         const int32_t last = end[r] > m.beg[r] ? end[r] - 1 : (m.beg[r] > 0 ? m.beg[r] - 1 : 0);
 #pragma unroll
@@ -378,7 +379,7 @@ __global__ __launch_bounds__(kK1Block) void egonet_k1_count_k(
         nb = b.nb;
         auto count = [&](const K1Rows<D> &m, int g0) {
 #pragma unroll
-            for (int r = 0; r < kK1Grp; ++r)
+            for (int r = 0; r < K1G<D>; ++r)
 #pragma unroll
                 for (int t = 0; t < D; ++t)
                     ne += (g0 + r < b.nb && t < m.deg[r] && k1_index(b, m.w[r][t]) >= 0) ? 1 : 0;
@@ -388,10 +389,10 @@ __global__ __launch_bounds__(kK1Block) void egonet_k1_count_k(
             k1_rows<D, 0>(rowptr, col, b, m);
             count(m, 0);
         }
-        if (D + 1 > kK1Grp && b.nb > kK1Grp) {  // balls of more than kK1Grp members: second group
+        if (D + 1 > K1G<D> && b.nb > K1G<D>) {  // balls of more than K1G<D> members: second group
             K1Rows<D> m;
-            k1_rows<D, kK1Grp>(rowptr, col, b, m);
-            count(m, kK1Grp);
+            k1_rows<D, K1G<D>>(rowptr, col, b, m);
+            count(m, K1G<D>);
         }
     }
     wave_scan2(nb, ne);
@@ -473,7 +474,7 @@ __global__ __launch_bounds__(kK1Block) void egonet_k1_fill_k(
     auto fill = [&](const K1Rows<D> &mm, auto g0c) {
         constexpr int G0 = decltype(g0c)::value;
 #pragma unroll
-        for (int r = 0; r < kK1Grp; ++r) {
+        for (int r = 0; r < K1G<D>; ++r) {
             if (G0 + r < b.nb) {
                 ego_nodes[noff + G0 + r] = b.mem[G0 + r < D + 1 ? G0 + r : D];
                 sub_rowptr[noff + G0 + r] = eo;
@@ -486,11 +487,146 @@ __global__ __launch_bounds__(kK1Block) void egonet_k1_fill_k(
         }
     };
     fill(m, std::integral_constant<int, 0>{});
-    if constexpr (D + 1 > kK1Grp) {
-        if (b.nb > kK1Grp) {
-            k1_rows<D, kK1Grp>(rowptr, col, b, m);
-            fill(m, std::integral_constant<int, kK1Grp>{});
+    if constexpr (D + 1 > K1G<D>) {
+        if (b.nb > K1G<D>) {
+            k1_rows<D, K1G<D>>(rowptr, col, b, m);
+            fill(m, std::integral_constant<int, K1G<D>>{});
         }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// k = 1 in ONE launch: each 64-parent block computes its balls, publishes its
+// (nodes, edges) aggregate and takes its exclusive prefix by a decoupled
+// look-back over the preceding blocks' published words, then fills — the
+// count kernel's four dependent load rounds are not repeated by a fill
+// launch.  state[b] packs (flag:2 | nodes:31 | edges:31) in one 64-bit word
+// (flag 1: the block's aggregate, 2: its inclusive prefix); a block waits
+// only on lower-numbered blocks, which the dispatcher starts first.  The last
+// block to finish zeroes every state word and the finish counter, so the
+// next launch (graph replay) starts from zeros.  Integer sums: exact.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t k1_pack(uint64_t flag, int32_t n, int32_t e) {
+    return (flag << 62) | (static_cast<uint64_t>(static_cast<uint32_t>(n)) << 31) |
+           static_cast<uint64_t>(static_cast<uint32_t>(e));
+}
+
+template <int D>
+__global__ __launch_bounds__(kK1Block) void egonet_k1_onepass_k(
+    const int32_t *__restrict__ rowptr, const int32_t *__restrict__ col, int64_t n,
+    int32_t *__restrict__ ego_ptr, int32_t *__restrict__ ego_eptr, uint64_t *__restrict__ state,
+    uint32_t *__restrict__ done, int32_t *__restrict__ ego_nodes,
+    int32_t *__restrict__ sub_rowptr, int32_t *__restrict__ sub_col, int64_t n_ego_cap,
+    const int32_t *__restrict__ dims, int32_t *__restrict__ ego_dims) {
+    const int nblk = gridDim.x, blk = blockIdx.x, lane = threadIdx.x;
+    const int64_t v = static_cast<int64_t>(blk) * kK1Block + lane;
+    const bool live = v < eff_count(dims, 0, n);
+    K1Win<D> b;
+    K1Rows<D> m;
+    int32_t nb = 0, ne = 0;
+    if (live) {
+        k1_ball<D>(rowptr, col, static_cast<int32_t>(v), b);
+        k1_rows<D, 0>(rowptr, col, b, m);
+        nb = b.nb;
+        auto count = [&](const K1Rows<D> &mm, int g0) {
+#pragma unroll
+            for (int r = 0; r < K1G<D>; ++r)
+#pragma unroll
+                for (int t = 0; t < D; ++t)
+                    ne += (g0 + r < b.nb && t < mm.deg[r] && k1_index(b, mm.w[r][t]) >= 0) ? 1 : 0;
+        };
+        count(m, 0);
+        if (D + 1 > K1G<D> && b.nb > K1G<D>) {
+            K1Rows<D> m2;
+            k1_rows<D, K1G<D>>(rowptr, col, b, m2);
+            count(m2, K1G<D>);
+        }
+    }
+    int32_t in_n = nb, in_e = ne;  // inclusive within the block
+    wave_scan2(in_n, in_e);
+    const int32_t agg_n = __shfl(in_n, kK1Block - 1, kWave), agg_e = __shfl(in_e, kK1Block - 1, kWave);
+    int32_t pre_n = 0, pre_e = 0;
+    if (lane == 0) {
+        if (blk == 0) {
+            __hip_atomic_store(&state[0], k1_pack(2, agg_n, agg_e), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            __hip_atomic_store(&state[blk], k1_pack(1, agg_n, agg_e), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+            for (int j = blk - 1;;) {
+                const uint64_t w = __hip_atomic_load(&state[j], __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_AGENT);
+                const uint64_t flag = w >> 62;
+                if (flag == 0) {
+                    __builtin_amdgcn_s_sleep(1);
+                    continue;
+                }
+                pre_n += static_cast<int32_t>((w >> 31) & 0x7fffffffull);
+                pre_e += static_cast<int32_t>(w & 0x7fffffffull);
+                if (flag == 2) break;
+                --j;
+            }
+            __hip_atomic_store(&state[blk], k1_pack(2, pre_n + agg_n, pre_e + agg_e),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+    pre_n = __shfl(pre_n, 0, kWave);
+    pre_e = __shfl(pre_e, 0, kWave);
+    const int32_t noff = pre_n + in_n - nb;
+    int32_t eo = pre_e + in_e - ne;
+    if (v < n) {
+        ego_ptr[v + 1] = pre_n + in_n;
+        ego_eptr[v + 1] = pre_e + in_e;
+    }
+    if (v == 0) {
+        ego_ptr[0] = 0;
+        ego_eptr[0] = 0;
+    }
+    if (blk == nblk - 1) {  // the totals: the ego batch's sizes and its tail
+        const int32_t ns = pre_n + agg_n, es = pre_e + agg_e;
+        if (lane == 0 && ego_dims) {
+            ego_dims[0] = ns;
+            ego_dims[1] = es;
+        }
+        for (int64_t i = ns + lane; i <= n_ego_cap; i += kK1Block) {
+            sub_rowptr[i] = es;
+            if (i < n_ego_cap) ego_nodes[i] = 0;
+        }
+    }
+    if (live) {
+        auto fill = [&](const K1Rows<D> &mm, auto g0c) {
+            constexpr int G0 = decltype(g0c)::value;
+#pragma unroll
+            for (int r = 0; r < K1G<D>; ++r) {
+                if (G0 + r < b.nb) {
+                    ego_nodes[noff + G0 + r] = b.mem[G0 + r < D + 1 ? G0 + r : D];
+                    sub_rowptr[noff + G0 + r] = eo;
+#pragma unroll
+                    for (int t = 0; t < D; ++t) {
+                        const int32_t i = k1_index(b, mm.w[r][t]);
+                        if (t < mm.deg[r] && i >= 0) sub_col[eo++] = noff + k1_rank(b, i);
+                    }
+                }
+            }
+        };
+        fill(m, std::integral_constant<int, 0>{});
+        if constexpr (D + 1 > K1G<D>) {
+            if (b.nb > K1G<D>) {
+                k1_rows<D, K1G<D>>(rowptr, col, b, m);
+                fill(m, std::integral_constant<int, K1G<D>>{});
+            }
+        }
+    }
+    // every look-back of this block is done: count it in; the last one resets
+    if (lane == 0) {
+        const uint32_t t = __hip_atomic_fetch_add(done, 1u, __ATOMIC_RELAXED,
+                                                  __HIP_MEMORY_SCOPE_AGENT);
+        pre_n = t == static_cast<uint32_t>(nblk - 1) ? 1 : 0;
+    }
+    if (__shfl(pre_n, 0, kWave)) {
+        for (int j = lane; j < nblk; j += kK1Block)
+            __hip_atomic_store(&state[j], uint64_t(0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (lane == 0) __hip_atomic_store(done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
 
@@ -577,9 +713,52 @@ extern "C" int scgib_egonet_k1_build_deg(const int32_t *rowptr, const int32_t *c
     if (max_in_degree <= 6)  // one member group, half the neighbour slots
         launch_k1<6>(rowptr, col, n_nodes, ego_ptr, ego_eptr, blk_tot, ego_nodes, sub_rowptr,
                      sub_col, n_ego_cap, dims, ego_dims, st);
+    else if (max_in_degree <= 8)  // one member group of 9
+        launch_k1<8>(rowptr, col, n_nodes, ego_ptr, ego_eptr, blk_tot, ego_nodes, sub_rowptr,
+                     sub_col, n_ego_cap, dims, ego_dims, st);
     else
         launch_k1<12>(rowptr, col, n_nodes, ego_ptr, ego_eptr, blk_tot, ego_nodes, sub_rowptr,
                       sub_col, n_ego_cap, dims, ego_dims, st);
+    return launch_status();
+}
+
+// one-launch form (egonet_k1_onepass_k): scan_state = scgib_egonet_k1_scan_words(n)
+// zeroed uint32 words, left zeroed for the next launch (one launch in flight
+// per scan_state)
+extern "C" int64_t scgib_egonet_k1_scan_words(int64_t n_nodes) {
+    return 2 * ((n_nodes + kK1Block - 1) / kK1Block) + 4;
+}
+
+extern "C" int scgib_egonet_k1_build_onepass(const int32_t *rowptr, const int32_t *col,
+                                             int64_t n_nodes, int32_t max_in_degree,
+                                             int32_t *ego_ptr, int32_t *ego_eptr,
+                                             uint32_t *scan_state, int32_t *ego_nodes,
+                                             int32_t *sub_rowptr, int32_t *sub_col,
+                                             int64_t n_ego_cap, const int32_t *dims,
+                                             int32_t *ego_dims, scgib_stream_t stream) {
+    if (n_nodes <= 0 || !rowptr || !col || !ego_ptr || !ego_eptr || !scan_state || !ego_nodes ||
+        !sub_rowptr || !sub_col || max_in_degree < 0)
+        return SCGIB_EINVAL;
+    if (n_nodes >= (int64_t(1) << 31) || max_in_degree > 12) return SCGIB_EUNSUPPORTED;
+    if (reinterpret_cast<uintptr_t>(scan_state) % 4) return SCGIB_EINVAL;
+    const int32_t nblk = static_cast<int32_t>((n_nodes + kK1Block - 1) / kK1Block);
+    uint32_t *done = scan_state;
+    uint64_t *state = reinterpret_cast<uint64_t *>(
+        (reinterpret_cast<uintptr_t>(scan_state) + sizeof(uint32_t) + 7) & ~uintptr_t(7));
+    hipStream_t st = as_stream(stream);
+    if (max_in_degree <= 6)
+        egonet_k1_onepass_k<6><<<nblk, kK1Block, 0, st>>>(rowptr, col, n_nodes, ego_ptr, ego_eptr,
+                                                          state, done, ego_nodes, sub_rowptr,
+                                                          sub_col, n_ego_cap, dims, ego_dims);
+    else if (max_in_degree <= 8)
+        egonet_k1_onepass_k<8><<<nblk, kK1Block, 0, st>>>(rowptr, col, n_nodes, ego_ptr, ego_eptr,
+                                                          state, done, ego_nodes, sub_rowptr,
+                                                          sub_col, n_ego_cap, dims, ego_dims);
+    else
+        egonet_k1_onepass_k<12><<<nblk, kK1Block, 0, st>>>(rowptr, col, n_nodes, ego_ptr,
+                                                           ego_eptr, state, done, ego_nodes,
+                                                           sub_rowptr, sub_col, n_ego_cap, dims,
+                                                           ego_dims);
     return launch_status();
 }
 

@@ -456,6 +456,8 @@ def ego_bounds(g, k):
 # but the replayed step measured 0.5 % slower with it (the ego chain then
 # contends earlier with Encoder1's layers); tests compare both builders.
 EGO_K1_FAST = os.environ.get("SCGIB_EGO_K1", "1") != "0"
+# ... in one launch (count + look-back scan + fill, egonet_k1_onepass_k)
+EGO_K1_ONEPASS = os.environ.get("SCGIB_EGO_K1_ONEPASS", "1") != "0"
 
 
 def _egonet_k1(g, ego_ptr, ego_eptr, ws, x, max_in_degree=12):
@@ -476,9 +478,16 @@ def _egonet_k1(g, ego_ptr, ego_eptr, ws, x, max_in_degree=12):
     ego_nodes = torch.empty(max(n_s, 1), dtype=i32, device=dev)
     sub_rowptr = torch.empty(n_s + 1, dtype=i32, device=dev)
     sub_col = torch.empty(max(e_cap, 1), dtype=i32, device=dev)
-    _lib.call("scgib_egonet_k1_build_deg", _ptr(g.rowptr), _ptr(g.col), n, int(max_in_degree),
-              _ptr(ego_ptr), _ptr(ego_eptr), _ptr(ws), _ptr(ego_nodes), _ptr(sub_rowptr),
-              _ptr(sub_col), n_s, _ptr(g.dims), _ptr(ego_dims), _stream())
+    if EGO_K1_ONEPASS:
+        from . import ops  # (ops imports this module)
+        state = ops.counters(dev, "egonet_k1_scan", int(_lib.query("scgib_egonet_k1_scan_words", n)))
+        _lib.call("scgib_egonet_k1_build_onepass", _ptr(g.rowptr), _ptr(g.col), n,
+                  int(max_in_degree), _ptr(ego_ptr), _ptr(ego_eptr), _ptr(state), _ptr(ego_nodes),
+                  _ptr(sub_rowptr), _ptr(sub_col), n_s, _ptr(g.dims), _ptr(ego_dims), _stream())
+    else:
+        _lib.call("scgib_egonet_k1_build_deg", _ptr(g.rowptr), _ptr(g.col), n,
+                  int(max_in_degree), _ptr(ego_ptr), _ptr(ego_eptr), _ptr(ws), _ptr(ego_nodes),
+                  _ptr(sub_rowptr), _ptr(sub_col), n_s, _ptr(g.dims), _ptr(ego_dims), _stream())
     ego = GraphBatch(sub_rowptr, sub_col, ego_ptr, None, None, n_edges=-1,
                      max_graph_nodes=max(g.max_graph_nodes, 1))
     ego.dims = ego_dims

@@ -128,33 +128,50 @@ def test_egonet_large_molecules_multiword_bitmaps(pkg, dev):
         _check_ego(pkg, gh, k, dev)
 
 
-@pytest.mark.parametrize("workload", ["qm9", "molpcba", "mutagenicity"])
-def test_egonet_k1_fast_path_equals_bitmap_builder(pkg, dev, workload):
-    """The two-launch k = 1 builder (sorted-list balls) produces exactly the
-    arrays of the general bitmap builder, incl. an isolated atom and a
-    self-loop (hand-made molecule appended to the batch)."""
-    mols = pkg.synth.molecules(300, workload, seed=21)
+@pytest.mark.parametrize("workload,star", [("qm9", False), ("molpcba", False),
+                                           ("mutagenicity", False), ("qm9", True),
+                                           ("qm9-lowdeg", False)])
+def test_egonet_k1_fast_path_equals_bitmap_builder(pkg, dev, workload, star, monkeypatch):
+    """The k = 1 builders (sorted-list balls: one launch with a look-back
+    scan, and two launches) produce exactly the arrays of the general bitmap
+    builder, incl. an isolated atom and a self-loop (hand-made molecule
+    appended to the batch).  The kernels are built per in-degree bound D:
+    qm9 (max in-degree 8) runs D = 8, molpcba / mutagenicity (9) D = 12,
+    star (a 12-atom star appended: in-degree 11) D = 12 with two member
+    groups, lowdeg (molecules of in-degree <= 6 only) D = 6.  The one-launch
+    builder runs three times in a row (its scan state must come back zeroed)."""
+    mols = pkg.synth.molecules(300, workload.split("-")[0], seed=21)
+    if workload.endswith("lowdeg"):
+        mols = [m for m in mols if pkg.graph.collate_pyg([m])[0].host_info["deg"].max() <= 6]
     gh, _ = pkg.graph.collate_pyg(mols)
     src, dst = (t.numpy() for t in gh.edges())
     n = gh.num_nodes()
     # extra molecule: 0-1-2 path, isolated atom 3, self-loop on 1
     es = np.array([0, 1, 1, 2, 1]) + n
     ed = np.array([1, 0, 2, 1, 1]) + n
-    counts = np.concatenate([gh.batch_num_nodes_host(), [4]])
+    counts = [gh.batch_num_nodes_host(), [4]]
+    n2 = n + 4
+    if star:
+        leaves = np.arange(1, 12) + n2
+        es = np.concatenate([es, np.full(11, n2), leaves])
+        ed = np.concatenate([ed, leaves, np.full(11, n2)])
+        counts.append([12])
+        n2 += 12
     g2 = pkg.graph.GraphBatch.from_edges(np.concatenate([src, es]), np.concatenate([dst, ed]),
-                                         n + 4, True, counts)
+                                         n2, True, np.concatenate(counts))
+    dmax = int(g2.host_info["deg"].max())
+    assert dmax == (11 if star else 6 if workload.endswith("lowdeg") else dmax)
     outs = []
-    default = pkg.graph.EGO_K1_FAST
-    for fast in (True, False):
-        pkg.graph.EGO_K1_FAST = fast
-        try:
+    for fast, onepass, reps in ((True, True, 3), (True, False, 1), (False, False, 1)):
+        monkeypatch.setattr(pkg.graph, "EGO_K1_FAST", fast)
+        monkeypatch.setattr(pkg.graph, "EGO_K1_ONEPASS", onepass)
+        for _ in range(reps):
             ego = pkg.graph.egonet_batch(g2.to(dev), 1)
             outs.append([ego.graph_ptr.cpu().numpy(), ego.ndata["_ID"].cpu().numpy(),
                          ego.rowptr.cpu().numpy(), ego.col.cpu().numpy()[: ego.num_edges()]])
-        finally:
-            pkg.graph.EGO_K1_FAST = default
-    for a, b in zip(*outs):
-        np.testing.assert_array_equal(a, b)
+    for other in outs[1:]:
+        for a, b in zip(outs[0], other):
+            np.testing.assert_array_equal(a, b)
 
 
 def test_egonet_rejects_oversized_graph(pkg, dev):

@@ -395,6 +395,14 @@ int scgib_noise_uniform(float *u_gate, float *u_feat, int64_t n_rows, uint64_t *
 int scgib_bn_running_update(const float *stats, const int32_t *graph_ptr, int64_t n_graphs,
                             float momentum, float *running_mean, float *running_var,
                             int64_t *num_batches_tracked, scgib_stream_t stream);
+/* The same over up to 16 workgroups (partition partials chained by the last
+ * workgroup to arrive): partials = scgib_bn_running_update_partials(B)
+ * doubles of scratch, counter = one ZEROED uint32, left zeroed. */
+int64_t scgib_bn_running_update_partials(int64_t n_graphs);
+int scgib_bn_running_update_multi(const float *stats, const int32_t *graph_ptr, int64_t n_graphs,
+                                  float momentum, float *running_mean, float *running_var,
+                                  int64_t *num_batches_tracked, double *partials,
+                                  uint32_t *counter, scgib_stream_t stream);
 
 /* Backward of scgib_interaction_fwd.  The KL gradient is g_kl [2 n_last, 64],
  * or g_klmean (device scalar, gradient of kl_mean), or neither (both NULL).

@@ -41,6 +41,8 @@ SIGNATURES = {
                                              _P, _P, _I32, _P]),
     "scgib_noise_uniform": (ctypes.c_int, [_P, _P, _I64, _P, _P, _P]),
     "scgib_bn_running_update": (ctypes.c_int, [_P, _P, _I64, _F, _P, _P, _P, _P]),
+    "scgib_bn_running_update_partials": (_I64, [_I64]),
+    "scgib_bn_running_update_multi": (ctypes.c_int, [_P, _P, _I64, _F, _P, _P, _P, _P, _P, _P]),
     "scgib_interaction_bwd": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _I64, _I64, _P,
                                              _P, _P, _P, _F, _I32, _P, _P, _P, _P, _P, _P, _P,
                                              _P, _P, _P, _P, _I32, _P, _P]),

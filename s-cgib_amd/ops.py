@@ -53,6 +53,10 @@ _AUX_PENDING = set()
 # 1.5 % faster aside (the ~15 us single-workgroup kernel leaves the critical
 # path; its fork/join edges cost less)
 RU_ASIDE = os.environ.get("SCGIB_RU_ASIDE", "1") != "0"
+# ... or, before both, the 16-workgroup form inline on the current stream
+# (off: 10 us inline vs the fork / join edges of the aside launch, A/B 0.4686
+# vs 0.4608 ms)
+RU_MULTI = os.environ.get("SCGIB_RU_MULTI", "0") != "0"
 # encoder backward: all layers' weight-gradient slabs reduced by one launch at
 # the end (scgib_slab_reduce_multi) instead of one launch per layer
 BATCH_SLABS = os.environ.get("SCGIB_BATCH_SLABS", "1") != "0"
@@ -976,7 +980,13 @@ def _interaction_forward(ctx, f, t, s, u_gate, u_feat, gamma, beta, w2, b2, w_at
         def upd():  # B sequential momentum updates in closed form
             _lib.call("scgib_bn_running_update", _p(stats), _p(graph.graph_ptr), B,
                       float(bn.momentum), _p(rm), _p(rv), _p(nbt), _stream())
-        if RU_ASIDE:  # nothing in the step reads them: beside the critical path
+        if RU_MULTI:  # a few microseconds inline: no fork / join around it
+            part = torch.empty(int(_lib.query("scgib_bn_running_update_partials", B)),
+                               dtype=torch.float64, device=dev)
+            _lib.call("scgib_bn_running_update_multi", _p(stats), _p(graph.graph_ptr), B,
+                      float(bn.momentum), _p(rm), _p(rv), _p(nbt), _p(part),
+                      _p(counters(dev, "bn_running_update", 1)), st)
+        elif RU_ASIDE:  # nothing in the step reads them: beside the critical path
             launch_aside(upd, stats, graph.graph_ptr)
         else:
             upd()

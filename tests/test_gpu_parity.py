@@ -212,6 +212,55 @@ def _interaction_oracle(p, f, s, counts, u_gate, u_feat, bn_state):
     return im, z1, z2, kl
 
 
+@pytest.mark.parametrize("B", [1, 7, 100, 512, 2048])
+def test_bn_running_update_multi_equals_single(pkg, dev, B):
+    """The compressor BatchNorm's B sequential momentum updates
+    (models.py:642, one BN call per graph) in closed form: the 16-workgroup
+    kernel (scgib_bn_running_update_multi, inline on the loss chain) vs the
+    one-workgroup kernel and vs an fp64 sequential loop; the counter comes
+    back zeroed (three launches in a row)."""
+    gen = torch.Generator().manual_seed(B)
+    stride = pkg._lib.STATS_STRIDE
+    stats = torch.randn(B, stride, generator=gen)
+    stats[:, 64:128] = stats[:, 64:128].abs() * 5
+    sizes = torch.randint(2, 30, (B,), generator=gen)
+    gptr = torch.zeros(B + 1, dtype=torch.int32)
+    gptr[1:] = torch.cumsum(sizes, 0)
+    rm0, rv0 = torch.randn(64, generator=gen), torch.rand(64, generator=gen) + 0.5
+    mom = 0.1
+    ref_m, ref_v = rm0.double().clone(), rv0.double().clone()
+    for i in range(B):  # the reference's loop
+        ref_m = (1 - mom) * ref_m + mom * stats[i, :64].double()
+        ref_v = (1 - mom) * ref_v + mom * stats[i, 64:128].double() / float(sizes[i] - 1)
+    sd, gd = stats.to(dev), gptr.to(dev)
+    outs = []
+    for multi in (False, True):
+        rm, rv = rm0.clone().to(dev), rv0.clone().to(dev)
+        nbt = torch.zeros((), dtype=torch.int64, device=dev)
+        reps = 3 if multi else 1
+        for _ in range(reps):
+            rm.copy_(rm0)
+            rv.copy_(rv0)
+            nbt.zero_()
+            if multi:
+                part = torch.empty(int(pkg._lib.query("scgib_bn_running_update_partials", B)),
+                                   dtype=torch.float64, device=dev)
+                cnt = pkg.ops.counters(dev, "test_bn_ru", 1)
+                pkg._lib.call("scgib_bn_running_update_multi", pkg.ops._p(sd), pkg.ops._p(gd), B,
+                              mom, pkg.ops._p(rm), pkg.ops._p(rv), pkg.ops._p(nbt),
+                              pkg.ops._p(part), pkg.ops._p(cnt), None)
+            else:
+                pkg._lib.call("scgib_bn_running_update", pkg.ops._p(sd), pkg.ops._p(gd), B, mom,
+                              pkg.ops._p(rm), pkg.ops._p(rv), pkg.ops._p(nbt), None)
+            torch.cuda.synchronize()
+            assert int(nbt) == B
+        outs.append((rm.cpu(), rv.cpu()))
+        assert rel_err(rm.cpu(), ref_m.float()) < 1e-6
+        assert rel_err(rv.cpu(), ref_v.float()) < 1e-6
+    assert int(cnt.cpu()[0]) == 0
+    assert rel_err(outs[0][0], outs[1][0]) < 1e-6 and rel_err(outs[0][1], outs[1][1]) < 1e-6
+
+
 @pytest.mark.parametrize("training", [True, False])
 def test_interaction_fwd_bwd(pkg, dev, training):
     torch.manual_seed(0)

@@ -235,6 +235,15 @@ __device__ __forceinline__ f32x16 mma_tn(const float *As, int lda, const float *
 // ---------------------------------------------------------------------------
 // pins the software pipeline: without it hipcc hoists every LDS read of the
 // product (IR level, across other loops) and the kernel spills
+// ds_read_b128-fed products: pin the next k block's operand reads ahead of
+// the current block's MFMAs (without the pin the scheduler sinks them behind
+// the block's MFMAs into the same registers, and each block then waits out an
+// LDS latency).  Build-time A/B knob.
+#ifndef SCGIB_MMA_PREFETCH_PIN
+#define SCGIB_MMA_PREFETCH_PIN 1
+#endif
+constexpr bool kMmaPrefetchPin = SCGIB_MMA_PREFETCH_PIN != 0;
+
 __device__ __forceinline__ void mma_step_fence() {
     asm volatile("" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
@@ -358,6 +367,7 @@ __device__ __forceinline__ f32x16 mma_rk4(const float *pa, const float (&b)[4 * 
 #pragma unroll
     for (int qb = 0; qb < NB; ++qb) {
         if (qb + 1 < NB) a[(qb + 1) & 1] = *reinterpret_cast<const float4 *>(pa + 8 * (qb + 1));
+        if (kMmaPrefetchPin) __builtin_amdgcn_sched_barrier(0);  // the next block's read goes out first
 #pragma unroll
         for (int t = 0; t < 4; ++t)
             acc = __builtin_amdgcn_mfma_f32_32x32x2f32(f4at(a[qb & 1], t), b[4 * qb + t], acc, 0, 0, 0);
@@ -385,6 +395,7 @@ __device__ __forceinline__ void mma_kk4x2(const float *pa, const float *pb1, con
             b1[x] = *reinterpret_cast<const float4 *>(pb1 + o);
             b2[x] = *reinterpret_cast<const float4 *>(pb2 + o);
         }
+        if (kMmaPrefetchPin) __builtin_amdgcn_sched_barrier(0);  // the next block's reads go out first
         const int x = qb & 1;
 #pragma unroll
         for (int t = 0; t < 4; ++t) {

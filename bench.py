@@ -232,7 +232,7 @@ def superbatch_roofline(dev, n_target=1_200_000, reps=20):
     pkg.ops.FOLD_SLABS = False
     try:
         with KernelTimer("scgib_gin_layer_fwd_bn", "scgib_gin_bwd_stats_bn",
-                         "scgib_gin_bwd_stats_bn_fold") as timer:
+                         "scgib_gin_bwd_stats_bn_fold", "scgib_gin_layer_bwd") as timer:
             y = gin(g, x)
             y.sum().backward()
     finally:
@@ -247,6 +247,19 @@ def superbatch_roofline(dev, n_target=1_200_000, reps=20):
             m = recs[0][2]
             res[key] = _frac_entry(fn(m["n"], m["e"], m["d_in"]), ms_k)
             res[key]["launches"] = len(recs)
+    # the step's dominant kernel (gin_bwd5_k, d_in = 64 layers) at this scale:
+    # ~37 k sub-tiles, ~146 per workgroup, so its start-of-kernel chain is
+    # amortised — the steady-state rate of the sub-tile loop
+    bw = [rec for rec in timer.records["scgib_gin_layer_bwd"] if rec[2]["d_in"] == 64]
+    if bw:
+        ms_k = statistics.mean(a.elapsed_time(b) / KernelTimer.REPEAT for a, b, _ in bw)
+        m = bw[0][2]
+        fl = layer_bwd_flops(m["n"], m["e"], m["d_in"])
+        ent = _frac_entry(layer_bwd_bytes(m["n"], m["e"], m["d_in"]), ms_k)
+        ent["tflops"] = round(fl / (ms_k * 1e-3) / 1e12, 2)
+        ent["mfma_frac"] = round(fl / (ms_k * 1e-3) / 1e12 / F32_MFMA_PEAK_TFLOPS, 4)
+        ent["launches"] = len(bw)
+        res["gin_bwd5_k"] = ent
     del y, x, h, gin
     return res
 
@@ -610,7 +623,9 @@ def main():
                 note="ZINC-like superbatch, [N,64] fp32 > 256 MiB Infinity Cache; frac = "
                      "algorithmic bytes / launch time / 8.0 TB/s (north_star target >= 0.40 on "
                      "the on-path gather kernels gin_fwd_k and gin_bwd_stats_k; "
-                     "gin_aggregate_k is a reference kernel, not in the step)"),
+                     "gin_aggregate_k is a reference kernel, not in the step); gin_bwd5_k: the "
+                     "step's dominant kernel at this scale (~146 sub-tiles per workgroup, its "
+                     "start-of-kernel chain amortised), mfma_frac = flops / time / 157.3 TF/s"),
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)

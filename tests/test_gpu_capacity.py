@@ -84,7 +84,12 @@ def _noise(n_cap, dev, seed):
             torch.rand(n_cap, 64, device=dev, generator=gen))
 
 
-def test_capacity_mode_eager_matches_exact(pkg, dev):
+@pytest.mark.parametrize("fused_bwd", [False, True])
+def test_capacity_mode_eager_matches_exact(pkg, dev, fused_bwd, monkeypatch):
+    """fused_bwd: the chunked fused GIN backward (scgib_gin_layer_bwd_fused)
+    in both modes — capacity mode adds chunks of padding rows only and the
+    zeroing of dy rows past the actual count."""
+    monkeypatch.setattr(pkg.ops, "FUSED_BWD", fused_bwd)
     hosts = _batches(pkg, (1, 2, 3))
     n_cap, e_cap, mgn, caps = pkg.graph.StaticBatch.capacities(hosts, 1, slack=1.05)
     static = pkg.graph.StaticBatch(B, n_cap, e_cap, F_IN, mgn, caps, dev)

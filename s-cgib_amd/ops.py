@@ -139,7 +139,12 @@ class SlabScope:
         SlabScope._live.add(self)
 
     def usable(self, params):
-        return self.open and self.ok and all(p is None or p.grad is None for p in params)
+        # no .grad to accumulate into, and no gradient hook that would read
+        # the tensor as soon as the engine hands it over
+        return self.open and self.ok and all(
+            p is None or (p.grad is None and not getattr(p, "_backward_hooks", None) and
+                          not getattr(p, "_post_accumulate_grad_hooks", None))
+            for p in params)
 
     def add(self, slab, wgrad, width, n_slabs):
         self.jobs.append(_lib.SlabJob(slab.data_ptr(), wgrad.data_ptr(), width, n_slabs, 0))

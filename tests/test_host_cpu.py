@@ -378,3 +378,7 @@ def test_slab_scope_rules(pkg):
     del b
     c = ops.SlabScope()  # a closed scope does not poison a new one
     assert c.usable((w,))
+    h = w.register_hook(lambda g: g)  # a gradient hook reads the tensor early: inline
+    assert not c.usable((w,))
+    h.remove()
+    assert c.usable((w,))

@@ -64,6 +64,9 @@ BATCH_SLABS = os.environ.get("SCGIB_BATCH_SLABS", "1") != "0"
 # statistics launch (extra workgroups, scgib_gin_bwd_stats_bn_fold) instead of
 # the chain's final reduce launch; only layer 0's slabs are left for the end
 FOLD_SLABS = os.environ.get("SCGIB_FOLD_SLABS", "1") != "0"
+# a folded slab is released once the launch that reduces it is enqueued (the
+# captured step then reuses its block instead of holding every layer's slabs)
+RELEASE_FOLDED = os.environ.get("SCGIB_RELEASE_FOLDED", "1") != "0"
 # encoder backward: layer l's backward and layer l-1's statistics in one
 # launch over component-aligned chunks (scgib_gin_layer_bwd_fused) when the
 # graph's components are closed and small enough; d(agg) then stays on chip.
@@ -562,6 +565,8 @@ class _GinEncoder(torch.autograd.Function):
         nslab = int(_lib.query("scgib_gin_bwd_slabs", n))
         jobs, keep = [], []
         fold = None  # the previous layer's slab job, reduced by the next stats launch
+        fold_slab = None  # its slab: released once that launch is enqueued (the
+        # allocator may then reuse the block for later tensors of this stream)
         chunks = _chunk_bounds(gr, n, L, st)
         # the fused launches alternate two BN-backward workspaces
         ws_pair = (bn_ws, torch.empty_like(bn_ws)) if chunks is not None else (bn_ws,)
@@ -600,7 +605,7 @@ class _GinEncoder(torch.autograd.Function):
                         _p(gr.col_t), ctx.opes[l + 1], _p(z2), _p(stat), n, int(ctx.training),
                         _p(dy), _p(bn_g[0]), _p(bn_g[1]), _p(coef), _p(bn_ws), _p(cnt),
                         _p(gr.dims), defer, _byref(fold), st)
-                fold = None
+                fold = fold_slab = None
             bpend = _lib.BnBwdPending(gpart, bn_g[0].data_ptr(), bn_g[1].data_ptr(),
                                       int(ctx.training)) if defer else None
             meta = {"n": n, "e": gr.edge_capacity(), "d_in": d_in}
@@ -630,7 +635,7 @@ class _GinEncoder(torch.autograd.Function):
                         _p(gr.col_t), ctx.opes[l], _p(z2p), _p(statp), int(ctx.training),
                         _p(dyp), _p(bn_gp[0]), _p(bn_gp[1]), _p(coefp), _p(ws_n), _p(cnt),
                         defer, _p(slab), _p(gr.dims), _byref(bpend), _byref(fold), st)
-                fold = None
+                fold = fold_slab = None
                 carry = (dyp, bn_gp, coefp, ws_n)
                 dagg = None
             else:
@@ -660,16 +665,14 @@ class _GinEncoder(torch.autograd.Function):
                 ns = int(_lib.query("scgib_gin_chunks", n)) if carry is not None else \
                     int(_lib.query("scgib_gin_layer_bwd_slabs", n, d_in))
                 job = _lib.SlabJob(slab.data_ptr(), wgrad.data_ptr(), width, ns, 0)
-                keep.append(slab)
-                if carry is not None:  # folded into the next fused launch, if any
-                    if FOLD_FUSED and l > 1:
-                        fold = job
-                    else:
-                        jobs.append(job)
-                elif FOLD_SLABS and l > 0:
-                    fold = job
+                if (carry is not None and FOLD_FUSED and l > 1) or \
+                        (carry is None and FOLD_SLABS and l > 0):
+                    fold, fold_slab = job, slab  # reduced by the next layer's launch
+                    if not RELEASE_FOLDED:
+                        keep.append(slab)
                 else:
                     jobs.append(job)
+                    keep.append(slab)
             else:
                 ns = int(_lib.query("scgib_gin_chunks", n)) if carry is not None else \
                     int(_lib.query("scgib_gin_layer_bwd_slabs", n, d_in))

@@ -504,7 +504,10 @@ def main():
             # the whole step incl. the RCCL all-reduce of the bucket in ONE graph:
             # no host enqueue between the backward and the optimizer step
             try:
-                with torch.cuda.graph(graph):
+                # thread_local: the process group's watchdog thread queries the
+                # warm-up all-reduce's event while this thread captures; under
+                # the default global mode that query invalidates the capture
+                with torch.cuda.graph(graph, capture_error_mode="thread_local"):
                     static_loss = body()
                     reducer.pack()
                     reducer.reduce(force=True)

@@ -581,6 +581,10 @@ class _GinEncoder(torch.autograd.Function):
                 dy, bn_g, coef, ws_l = carry
                 carry = None
             else:
+                # (the previous layer's dy and slab are no longer read by anything
+                # not yet enqueued: released before the new allocations, whose
+                # blocks the captured step can then reuse)
+                dy = slab = None
                 dy = torch.empty(n, HIDDEN, dtype=torch.float32, device=dev)
                 bn_g = torch.empty(2, HIDDEN, dtype=torch.float32, device=dev)  # dgamma, dbeta
                 coef = torch.empty(2, HIDDEN, dtype=torch.float32, device=dev)
@@ -605,7 +609,7 @@ class _GinEncoder(torch.autograd.Function):
                         _p(gr.col_t), ctx.opes[l + 1], _p(z2), _p(stat), n, int(ctx.training),
                         _p(dy), _p(bn_g[0]), _p(bn_g[1]), _p(coef), _p(bn_ws), _p(cnt),
                         _p(gr.dims), defer, _byref(fold), st)
-                fold = fold_slab = None
+                fold = fold_slab = dagg_next = None
             bpend = _lib.BnBwdPending(gpart, bn_g[0].data_ptr(), bn_g[1].data_ptr(),
                                       int(ctx.training)) if defer else None
             meta = {"n": n, "e": gr.edge_capacity(), "d_in": d_in}

@@ -67,6 +67,9 @@ FOLD_SLABS = os.environ.get("SCGIB_FOLD_SLABS", "1") != "0"
 # a folded slab is released once the launch that reduces it is enqueued (the
 # captured step then reuses its block instead of holding every layer's slabs)
 RELEASE_FOLDED = os.environ.get("SCGIB_RELEASE_FOLDED", "1") != "0"
+# the deferred head-MLP slab reduced by Encoder1's first backward launch (and
+# released there) instead of by its final reduce
+FOLD_LOSS_SLAB = os.environ.get("SCGIB_FOLD_LOSS_SLAB", "1") != "0"
 # encoder backward: layer l's backward and layer l-1's statistics in one
 # launch over component-aligned chunks (scgib_gin_layer_bwd_fused) when the
 # graph's components are closed and small enough; d(agg) then stays on chip.
@@ -600,9 +603,15 @@ class _GinEncoder(torch.autograd.Function):
                         _p(bn_g[0]), _p(bn_g[1]), _p(coef), _p(bn_ws), _p(cnt), _p(gr.dims),
                         defer, st)
             elif dagg_next is None:
-                _launch("scgib_gin_bwd_stats_bn", {"n": n, "e": 0, "d_in": HIDDEN}, _p(g_out), None, None, 1.0, _p(z2),
-                          _p(stat), n, int(ctx.training), _p(dy), _p(bn_g[0]), _p(bn_g[1]),
-                          _p(coef), _p(bn_ws), _p(cnt), _p(gr.dims), defer, st)
+                # (first_fold: a loss-section slab job handed over by the encoder
+                # pair — reduced in extra workgroups here, its slab then released)
+                ff = getattr(ctx, "first_fold", None)
+                ctx.first_fold = None
+                _launch("scgib_gin_bwd_stats_bn_fold", {"n": n, "e": 0, "d_in": HIDDEN}, _p(g_out),
+                        None, None, 1.0, _p(z2), _p(stat), n, int(ctx.training), _p(dy),
+                        _p(bn_g[0]), _p(bn_g[1]), _p(coef), _p(bn_ws), _p(cnt), _p(gr.dims),
+                        defer, _byref(ff[0] if ff else None), st)
+                ff = None
             else:
                 _launch("scgib_gin_bwd_stats_bn_fold", {"n": n, "e": gr.edge_capacity(), "d_in": HIDDEN},
                         _p(dagg_next), _p(gr.rowptr_t),
@@ -860,6 +869,11 @@ class _GinEncoderPair(torch.autograd.Function):
                 jobs, keep = scope.take()
                 for tsr in keep:  # made on the main stream, reduced / written on side
                     tsr.record_stream(side)
+                if jobs and FOLD_SLABS and FOLD_LOSS_SLAB:  # the largest (the head MLP's) into Encoder1's first launch
+                    big = max(range(len(jobs)), key=lambda i: jobs[i].width * jobs[i].n_slabs)
+                    ctx.sub[1].first_fold = (jobs[big], keep[2 * big: 2 * big + 2])
+                    jobs = jobs[:big] + jobs[big + 1:]
+                    keep = keep[:2 * big] + keep[2 * big + 2:]
                 ctx.sub[1].extra_jobs = (jobs, keep)
             if not INTERLEAVE_BWD:
                 gc = _drain(_GinEncoder.backward_steps(ctx.sub[1], g_f, l0=l0_c))

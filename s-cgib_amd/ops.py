@@ -829,6 +829,7 @@ class _GinEncoderPair(torch.autograd.Function):
         # chain's, so they leave the critical path
         ctx.sub[1].reduce_wg = SIDE_REDUCE_WG
         scope = ctx.scope if (ctx.scope is not None and ctx.scope.open) else None
+        held = None
         dw0 = db0 = None
         g_f_in = g_f
         if EGO_FIRST and not INTERLEAVE_BWD:  # capture the critical ego chain first
@@ -869,6 +870,11 @@ class _GinEncoderPair(torch.autograd.Function):
                 jobs, keep = scope.take()
                 for tsr in keep:  # made on the main stream, reduced / written on side
                     tsr.record_stream(side)
+                # ... and referenced until after the join below: a block made on
+                # main and read on side is not returned to the allocator while
+                # later main-stream work could be handed it unordered (in a
+                # captured step `record_stream` alone does not order the reuse)
+                held = list(keep)
                 if jobs and FOLD_SLABS and FOLD_LOSS_SLAB:  # the largest (the head MLP's) into Encoder1's first launch
                     big = max(range(len(jobs)), key=lambda i: jobs[i].width * jobs[i].n_slabs)
                     ctx.sub[1].first_fold = (jobs[big], keep[2 * big: 2 * big + 2])
@@ -883,6 +889,7 @@ class _GinEncoderPair(torch.autograd.Function):
         elif not EGO_FIRST:
             ge = _drain(_GinEncoder.backward_steps(ctx.sub[0], g_s, g_ro, l0=l0_e))
         main.wait_stream(side)
+        held = None  # after the join: main-stream reuse is ordered after side's reads
         if shared:  # the ego chain's reduce, incl. both encoders' d Wt
             jobs, keep = pending[0]
             _reduce_jobs(jobs, _stream())

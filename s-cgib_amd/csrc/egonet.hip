@@ -288,14 +288,49 @@ __device__ __forceinline__ int32_t k1_rank(const K1Win<D> &b, int32_t i) {
     return i < 64 ? __popcll(b.w[0] & m) : __popcll(b.w[0]) + __popcll(b.w[1] & m);
 }
 
-template <int D>
-__device__ __forceinline__ void k1_ball(const int32_t *__restrict__ rowptr,
-                                        const int32_t *__restrict__ col, int32_t v, K1Win<D> &b) {
-    const int32_t beg = rowptr[v], end = rowptr[v + 1];
+// CSR accessors of the k = 1 builders.  K1Global reads global memory and, for
+// the neighbour slots past a row's end (whose values the callers predicate
+// away), a clamped always-valid address so every slot is one batched load.
+struct K1Global {
+    const int32_t *__restrict__ rowptr;
+    const int32_t *__restrict__ col;
+    __device__ __forceinline__ int32_t rp(int32_t u) const { return rowptr[u]; }
+    __device__ __forceinline__ int32_t cl(int32_t e, bool valid, int32_t last) const {
+        return col[valid ? e : last];
+    }
+};
+
+// K1Lds: the block's CSR window staged in LDS by two coalesced rounds —
+// rowptr[lo .. lo + kK1WinRows] with lo = 64 b - 64 (the parents' rows and
+// every ball member's: |u - v| < 64), then col[rowptr[lo] .. rowptr[lo +
+// kK1WinRows]) up to the LDS capacity.  An index outside the window (none under
+// the host-checked bounds) reads global memory; the slots past a row's end
+// load nothing.
+constexpr int kK1WinRows = 192;
+struct K1Lds {
+    const int32_t *__restrict__ rowptr;
+    const int32_t *__restrict__ col;
+    const int32_t *sRp;
+    const int32_t *sCol;
+    int32_t lo, c0;
+    uint32_t ncol;
+    __device__ __forceinline__ int32_t rp(int32_t u) const {
+        const uint32_t i = static_cast<uint32_t>(u - lo);
+        return i <= static_cast<uint32_t>(kK1WinRows) ? sRp[i] : rowptr[u];
+    }
+    __device__ __forceinline__ int32_t cl(int32_t e, bool valid, int32_t) const {
+        const uint32_t i = static_cast<uint32_t>(e - c0);
+        return !valid ? 0 : (i < ncol ? sCol[i] : col[e]);
+    }
+};
+
+template <int D, class A>
+__device__ __forceinline__ void k1_ball(const A &acc, int32_t v, K1Win<D> &b) {
+    const int32_t beg = acc.rp(v), end = acc.rp(v + 1);
     const int32_t last = end > beg ? end - 1 : (beg > 0 ? beg - 1 : 0);  // a valid index
     int32_t nbr[D];
 #pragma unroll
-    for (int j = 0; j < D; ++j) nbr[j] = col[beg + j < end ? beg + j : last];
+    for (int j = 0; j < D; ++j) nbr[j] = acc.cl(beg + j, beg + j < end, last);
     b.v = v;
     b.w[0] = 0ull;
     b.w[1] = 1ull;  // v itself: bit 64
@@ -331,23 +366,21 @@ struct K1Rows {
     int32_t w[K1G<D>][D];
 };
 
-template <int D, int G0>
-__device__ __forceinline__ void k1_rows(const int32_t *__restrict__ rowptr,
-                                        const int32_t *__restrict__ col, const K1Win<D> &b,
-                                        K1Rows<D> &m) {
+template <int D, int G0, class A>
+__device__ __forceinline__ void k1_rows(const A &acc, const K1Win<D> &b, K1Rows<D> &m) {
     int32_t end[K1G<D>];
 #pragma unroll
     for (int r = 0; r < K1G<D>; ++r) {
         const int32_t u = b.mem[G0 + r < D + 1 ? G0 + r : D];
-        m.beg[r] = rowptr[u];
-        end[r] = rowptr[u + 1];
+        m.beg[r] = acc.rp(u);
+        end[r] = acc.rp(u + 1);
     }
 #pragma unroll
     for (int r = 0; r < K1G<D>; ++r) {
         m.deg[r] = end[r] - m.beg[r];
         const int32_t last = end[r] > m.beg[r] ? end[r] - 1 : (m.beg[r] > 0 ? m.beg[r] - 1 : 0);
 #pragma unroll
-        for (int t = 0; t < D; ++t) m.w[r][t] = col[m.beg[r] + t < end[r] ? m.beg[r] + t : last];
+        for (int t = 0; t < D; ++t) m.w[r][t] = acc.cl(m.beg[r] + t, m.beg[r] + t < end[r], last);
     }
 }
 
@@ -374,8 +407,9 @@ __global__ __launch_bounds__(kK1Block) void egonet_k1_count_k(
     const int64_t v = static_cast<int64_t>(blockIdx.x) * kK1Block + threadIdx.x;
     int32_t nb = 0, ne = 0;
     if (v < eff_count(dims, 0, n)) {
+        const K1Global acc{rowptr, col};
         K1Win<D> b;
-        k1_ball<D>(rowptr, col, static_cast<int32_t>(v), b);
+        k1_ball<D>(acc, static_cast<int32_t>(v), b);
         nb = b.nb;
         auto count = [&](const K1Rows<D> &m, int g0) {
 #pragma unroll
@@ -386,12 +420,12 @@ __global__ __launch_bounds__(kK1Block) void egonet_k1_count_k(
         };
         {
             K1Rows<D> m;
-            k1_rows<D, 0>(rowptr, col, b, m);
+            k1_rows<D, 0>(acc, b, m);
             count(m, 0);
         }
         if (D + 1 > K1G<D> && b.nb > K1G<D>) {  // balls of more than K1G<D> members: second group
             K1Rows<D> m;
-            k1_rows<D, K1G<D>>(rowptr, col, b, m);
+            k1_rows<D, K1G<D>>(acc, b, m);
             count(m, K1G<D>);
         }
     }
@@ -417,11 +451,12 @@ __global__ __launch_bounds__(kK1Block) void egonet_k1_fill_k(
     const int64_t v = static_cast<int64_t>(blockIdx.x) * kK1Block + threadIdx.x;
     const bool live = v < eff_count(dims, 0, n);
     // the ball's loads go out first; the scan fix-up below overlaps them
+    const K1Global acc{rowptr, col};
     K1Win<D> b;
     K1Rows<D> m;
     if (live) {
-        k1_ball<D>(rowptr, col, static_cast<int32_t>(v), b);
-        k1_rows<D, 0>(rowptr, col, b, m);
+        k1_ball<D>(acc, static_cast<int32_t>(v), b);
+        k1_rows<D, 0>(acc, b, m);
     }
     // block prefix and grand total of (nodes, edges), fixed order (wave sums)
     int32_t pn = 0, pe = 0, tn = 0, te = 0;
@@ -489,7 +524,7 @@ __global__ __launch_bounds__(kK1Block) void egonet_k1_fill_k(
     fill(m, std::integral_constant<int, 0>{});
     if constexpr (D + 1 > K1G<D>) {
         if (b.nb > K1G<D>) {
-            k1_rows<D, K1G<D>>(rowptr, col, b, m);
+            k1_rows<D, K1G<D>>(acc, b, m);
             fill(m, std::integral_constant<int, K1G<D>>{});
         }
     }
@@ -511,6 +546,11 @@ __device__ __forceinline__ uint64_t k1_pack(uint64_t flag, int32_t n, int32_t e)
            static_cast<uint64_t>(static_cast<uint32_t>(e));
 }
 
+// SCGIB_EGO_LDS (default 1): the CSR window staged in LDS and the look-back
+// by the whole wave; 0: scattered global loads and a one-lane look-back
+#ifndef SCGIB_EGO_LDS
+#define SCGIB_EGO_LDS 1
+#endif
 template <int D>
 __global__ __launch_bounds__(kK1Block) void egonet_k1_onepass_k(
     const int32_t *__restrict__ rowptr, const int32_t *__restrict__ col, int64_t n,
@@ -521,12 +561,70 @@ __global__ __launch_bounds__(kK1Block) void egonet_k1_onepass_k(
     const int nblk = gridDim.x, blk = blockIdx.x, lane = threadIdx.x;
     const int64_t v = static_cast<int64_t>(blk) * kK1Block + lane;
     const bool live = v < eff_count(dims, 0, n);
+#if SCGIB_EGO_LDS
+    // the block's CSR window -> LDS (K1Lds): two coalesced rounds instead of
+    // four dependent rounds of scattered loads per parent
+    constexpr int kColCap = kK1WinRows * D;
+    __shared__ int32_t sRp[kK1WinRows + 1];
+    __shared__ int32_t sCol[kColCap];
+    const int32_t lo = blk * kK1Block - 64;
+    for (int i = lane; i <= kK1WinRows; i += kK1Block) {
+        const int64_t u = lo + i;
+        sRp[i] = rowptr[u < 0 ? 0 : (u > n ? n : u)];
+    }
+    __syncthreads();
+    const int32_t c0 = sRp[0], dc = sRp[kK1WinRows] - c0;
+    const int32_t nc = dc < 0 ? 0 : (dc < kColCap ? dc : kColCap);
+    for (int i0 = 0; i0 < nc; i0 += 4 * kK1Block) {
+        int32_t t[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int i = i0 + k * kK1Block + lane;
+            t[k] = i < nc ? col[c0 + i] : 0;
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int i = i0 + k * kK1Block + lane;
+            if (i < nc) sCol[i] = t[k];
+        }
+    }
+    __syncthreads();
+    const K1Lds acc{rowptr, col, sRp, sCol, lo, c0, static_cast<uint32_t>(nc)};
+    // with the window in LDS the loops run over the actual members and
+    // degrees (not the D-slot predicated batches the global-load form needs)
+    K1Win<D> b;
+    int32_t nb = 0, ne = 0;
+    if (live) {
+        const int32_t vv = static_cast<int32_t>(v);
+        b.v = vv;
+        b.w[0] = 0ull;
+        b.w[1] = 1ull;  // v itself: bit 64
+        for (int32_t e = acc.rp(vv), e1 = acc.rp(vv + 1); e < e1; ++e) {
+            const int32_t i = acc.cl(e, true, 0) - vv + 64;
+            if (i >= 0 && i < 128) {
+                if (i < 64) b.w[0] |= 1ull << i;
+                else b.w[1] |= 1ull << (i - 64);
+            }
+        }
+        nb = b.nb = __popcll(b.w[0]) + __popcll(b.w[1]);
+        for (uint64_t m0 = b.w[0], m1 = b.w[1]; m0 | m1;) {  // members, any order
+            const int32_t i = m0 ? __ffsll(static_cast<unsigned long long>(m0)) - 1
+                                 : 64 + __ffsll(static_cast<unsigned long long>(m1)) - 1;
+            if (m0) m0 &= m0 - 1ull;
+            else m1 &= m1 - 1ull;
+            const int32_t u = vv - 64 + i;
+            for (int32_t e = acc.rp(u), e1 = acc.rp(u + 1); e < e1; ++e)
+                ne += k1_index(b, acc.cl(e, true, 0)) >= 0 ? 1 : 0;
+        }
+    }
+#else
+    const K1Global acc{rowptr, col};
     K1Win<D> b;
     K1Rows<D> m;
     int32_t nb = 0, ne = 0;
     if (live) {
-        k1_ball<D>(rowptr, col, static_cast<int32_t>(v), b);
-        k1_rows<D, 0>(rowptr, col, b, m);
+        k1_ball<D>(acc, static_cast<int32_t>(v), b);
+        k1_rows<D, 0>(acc, b, m);
         nb = b.nb;
         auto count = [&](const K1Rows<D> &mm, int g0) {
 #pragma unroll
@@ -538,10 +636,11 @@ __global__ __launch_bounds__(kK1Block) void egonet_k1_onepass_k(
         count(m, 0);
         if (D + 1 > K1G<D> && b.nb > K1G<D>) {
             K1Rows<D> m2;
-            k1_rows<D, K1G<D>>(rowptr, col, b, m2);
+            k1_rows<D, K1G<D>>(acc, b, m2);
             count(m2, K1G<D>);
         }
     }
+#endif
     int32_t in_n = nb, in_e = ne;  // inclusive within the block
     wave_scan2(in_n, in_e);
     const int32_t agg_n = __shfl(in_n, kK1Block - 1, kWave), agg_e = __shfl(in_e, kK1Block - 1, kWave);
@@ -553,6 +652,7 @@ __global__ __launch_bounds__(kK1Block) void egonet_k1_onepass_k(
         } else {
             __hip_atomic_store(&state[blk], k1_pack(1, agg_n, agg_e), __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);
+#if !SCGIB_EGO_LDS
             for (int j = blk - 1;;) {
                 const uint64_t w = __hip_atomic_load(&state[j], __ATOMIC_RELAXED,
                                                      __HIP_MEMORY_SCOPE_AGENT);
@@ -568,8 +668,43 @@ __global__ __launch_bounds__(kK1Block) void egonet_k1_onepass_k(
             }
             __hip_atomic_store(&state[blk], k1_pack(2, pre_n + agg_n, pre_e + agg_e),
                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#endif
         }
     }
+#if SCGIB_EGO_LDS
+    // look-back by the whole wave: lane i reads block (base - i)'s word; the
+    // nearest inclusive prefix ends it once every nearer block has published
+    if (blk > 0) {
+        for (int32_t base = blk - 1;;) {  // wave-uniform control flow (ballots)
+            const int32_t j = base - lane;
+            const uint64_t w = j >= 0 ? __hip_atomic_load(&state[j], __ATOMIC_RELAXED,
+                                                          __HIP_MEMORY_SCOPE_AGENT)
+                                      : k1_pack(2, 0, 0);
+            const uint64_t f = w >> 62;
+            const uint64_t inc = __ballot(f == 2), unset = __ballot(f == 0);
+            const int first = inc ? __ffsll(static_cast<unsigned long long>(inc)) - 1 : 64;
+            const uint64_t need = first >= 63 ? ~0ull : ((2ull << first) - 1ull);
+            if (unset & need) {
+                __builtin_amdgcn_s_sleep(1);
+                continue;
+            }
+            int32_t a = lane <= first ? static_cast<int32_t>((w >> 31) & 0x7fffffffull) : 0;
+            int32_t e = lane <= first ? static_cast<int32_t>(w & 0x7fffffffull) : 0;
+#pragma unroll
+            for (int off = 32; off >= 1; off >>= 1) {
+                a += __shfl_xor(a, off, kWave);
+                e += __shfl_xor(e, off, kWave);
+            }
+            pre_n += a;
+            pre_e += e;
+            if (first < 64) break;
+            base -= 64;
+        }
+        if (lane == 0)
+            __hip_atomic_store(&state[blk], k1_pack(2, pre_n + agg_n, pre_e + agg_e),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+#endif
     pre_n = __shfl(pre_n, 0, kWave);
     pre_e = __shfl(pre_e, 0, kWave);
     const int32_t noff = pre_n + in_n - nb;
@@ -593,6 +728,24 @@ __global__ __launch_bounds__(kK1Block) void egonet_k1_onepass_k(
             if (i < n_ego_cap) ego_nodes[i] = 0;
         }
     }
+#if SCGIB_EGO_LDS
+    if (live) {  // members ascending (DGL order), each row's columns in CSR order
+        int32_t r = 0;
+        for (uint64_t m0 = b.w[0], m1 = b.w[1]; m0 | m1; ++r) {
+            const int32_t i = m0 ? __ffsll(static_cast<unsigned long long>(m0)) - 1
+                                 : 64 + __ffsll(static_cast<unsigned long long>(m1)) - 1;
+            if (m0) m0 &= m0 - 1ull;
+            else m1 &= m1 - 1ull;
+            const int32_t u = b.v - 64 + i;
+            ego_nodes[noff + r] = u;
+            sub_rowptr[noff + r] = eo;
+            for (int32_t e = acc.rp(u), e1 = acc.rp(u + 1); e < e1; ++e) {
+                const int32_t j = k1_index(b, acc.cl(e, true, 0));
+                if (j >= 0) sub_col[eo++] = noff + k1_rank(b, j);
+            }
+        }
+    }
+#else
     if (live) {
         auto fill = [&](const K1Rows<D> &mm, auto g0c) {
             constexpr int G0 = decltype(g0c)::value;
@@ -612,11 +765,12 @@ __global__ __launch_bounds__(kK1Block) void egonet_k1_onepass_k(
         fill(m, std::integral_constant<int, 0>{});
         if constexpr (D + 1 > K1G<D>) {
             if (b.nb > K1G<D>) {
-                k1_rows<D, K1G<D>>(rowptr, col, b, m);
+                k1_rows<D, K1G<D>>(acc, b, m);
                 fill(m, std::integral_constant<int, K1G<D>>{});
             }
         }
     }
+#endif
     // every look-back of this block is done: count it in; the last one resets
     if (lane == 0) {
         const uint32_t t = __hip_atomic_fetch_add(done, 1u, __ATOMIC_RELAXED,

@@ -493,8 +493,18 @@ struct ReconArgs {
 #endif
 constexpr bool kLateWeights = SCGIB_LATE_WEIGHTS != 0;
 
+// SCGIB_FWD_ALIAS (default 1): the gathering d_in = 64 layers write r into
+// the agg tile's buffer once every wave's first GEMM is done (one more
+// barrier): 53 KB of LDS and <= 168 VGPRs, three workgroups per CU instead
+// of two, so an ego layer's 437 tiles and Encoder1's 145 fit the chip at once
+#ifndef SCGIB_FWD_ALIAS
+#define SCGIB_FWD_ALIAS 1
+#endif
+template <int DIN, bool GATHER, bool PRE>
+constexpr bool kFwdAlias = SCGIB_FWD_ALIAS != 0 && DIN == 64 && GATHER && !PRE;
+
 template <int DIN, bool XFORM, bool GATHER = true, bool PRE = false, bool RECON = false>
-__global__ __launch_bounds__(256) void gin_fwd_k(
+__global__ __launch_bounds__(256, (kFwdAlias<DIN, GATHER, PRE> ? 3 : 1)) void gin_fwd_k(
     const float *__restrict__ h, const float *__restrict__ in_scale,
     const float *__restrict__ in_shift, const int32_t *__restrict__ rowptr,
     const int32_t *__restrict__ col, int64_t ncap, float ope, const float *__restrict__ w1,
@@ -509,7 +519,10 @@ __global__ __launch_bounds__(256) void gin_fwd_k(
     __shared__ __attribute__((aligned(16))) float sA[TM * LDA];   // (contrastive: float4 tiles)
     __shared__ __attribute__((aligned(16))) float sW1[64 * LDA];
     __shared__ float sW2[64 * LDH];
-    __shared__ float sR[TM * LDH];
+    constexpr bool ALIAS = kFwdAlias<DIN, GATHER, PRE>;
+    static_assert(!ALIAS || LDA == LDH, "r takes the agg tile's buffer");
+    __shared__ float sROwn[ALIAS ? 1 : TM * LDH];
+    float *const sR = ALIAS ? sA : sROwn;
     __shared__ float sRed[2][64];
     __shared__ float sPre[PRE ? (TM + 32) * kPreLD : 1];  // aggx tile | Wt
     if constexpr (RECON && DIN == 128) {  // the pretraining head (interaction map width)
@@ -661,6 +674,7 @@ __global__ __launch_bounds__(256) void gin_fwd_k(
     {
         f32x16 acc = mma_pf<DIN, false, false>(sA + wr * 32 * LDA, LDA, sW1 + wc * 32 * LDA, LDA, zero16());
         const float bias = b1[ccol];
+        if constexpr (ALIAS) __syncthreads();  // every wave's reads of the agg tile are done
 #pragma unroll
         for (int reg = 0; reg < 16; ++reg) {
             const int row = wr * 32 + acc_row(reg, l);

@@ -42,8 +42,10 @@ DEFER_BN = os.environ.get("SCGIB_DEFER_BN", "1") != "0"
 DEFER_BN_FWD = os.environ.get("SCGIB_DEFER_BN_FWD", "1") != "0"
 # the encoder pair's core_tail (the interaction's noise draw) enqueued at the
 # start of the core chain, beside the ego-net build, instead of at its end
-# (off: A/B 0.530 vs 0.528 ms, within noise or slightly slower)
-TAIL_FIRST = os.environ.get("SCGIB_TAIL_FIRST", "0") != "0"
+# (round 1: A/B 0.530 vs 0.528 ms, off; re-checked in round 2 after the
+# 3-workgroup forward: 0.4349 vs 0.4437 ms over three rounds, on — the draw
+# no longer delays the core chain's join into the interaction)
+TAIL_FIRST = os.environ.get("SCGIB_TAIL_FIRST", "1") != "0"
 # ... including the last layer's, finished by the output's BN + ReLU kernel
 # (off: A/B neutral to 0.5 % slower — every consumer workgroup then combines
 # the group partials, which costs what the producer's serial tail did)

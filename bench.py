@@ -366,6 +366,9 @@ SUM_LOSS = os.environ.get("SCGIB_BENCH_SUM_LOSS", "0") != "0"
 # N > 1: capture the RCCL all-reduce inside the replayed step graph (falls back
 # to all-reduce between two replays if the capture raises)
 GRAPH_ALLREDUCE = os.environ.get("SCGIB_GRAPH_ALLREDUCE", "1") != "0"
+# k = 1 ego-net build of batch i+1 inside step i, beside the encoders
+# (graph.EgoPipeline): every step still builds one ego batch, off the chain
+EGO_PIPELINE = os.environ.get("SCGIB_EGO_PIPELINE", "0") != "0"
 
 
 def main():
@@ -468,8 +471,20 @@ def main():
             padded.append(static.pad(gx))
 
         one = torch.ones((), dtype=torch.float32, device=dev)
+        pipe = None
+        if EGO_PIPELINE and a.k == 1:
+            nxt = pkg.graph.StaticBatch(a.batch, n_cap, e_cap, F_in, mgn, ego_caps, dev, k=a.k)
+            pipe = pkg.graph.EgoPipeline(static, nxt, a.k)
+
+        def load(i):  # batch i into the step's inputs (the pipeline: batch i+1 into nxt)
+            if pipe is None:
+                static.load(padded[i % len(padded)])
+            else:
+                pipe.nxt.load(padded[(i + 1) % len(padded)])
 
         def body():
+            if pipe is not None:
+                pipe.build_next()
             _, kl, con, rec = model(static.graph, static.x, None, None, None, 1, None, a.k, dev,
                                     a.batch)
             # loss = KL + contrastive + recon (exp_pretraining.py:321): d loss / d part = 1,
@@ -478,15 +493,22 @@ def main():
             if SUM_LOSS:
                 loss = kl + rec + con
                 loss.backward()
-                return loss
-            torch.autograd.backward((kl, rec, con), (one, one, one))
-            return kl, rec, con
+                out = loss
+            else:
+                torch.autograd.backward((kl, rec, con), (one, one, one))
+                out = (kl, rec, con)
+            if pipe is not None:
+                pipe.hand_over()
+            return out
 
         side = torch.cuda.Stream()
         side.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(side):  # warm-up (allocator, Adam state, RCCL comm) off the capture
+            if pipe is not None:
+                static.load(padded[0])
+                pipe.prime()
             for i in range(3):
-                static.load(padded[i % len(padded)])
+                load(i)
                 opt.zero_grad(set_to_none=True)
                 body()
                 if collective:
@@ -536,8 +558,12 @@ def main():
                 opt.step()
             allreduce_mode = "between two graph replays"
 
+        if pipe is not None:  # step 0 trains on padded[0] with its ego-nets prebuilt
+            static.load(padded[0])
+            pipe.prime()
+
         def step(i):
-            static.load(padded[i % len(padded)])
+            load(i)
             graph.replay()
             if graph2 is not None:  # RCCL all-reduce of the bucket between the two replays
                 reducer.reduce(force=True)
@@ -611,7 +637,8 @@ def main():
                        "allreduce": None if not collective else
                        ("eager" if a.eager else allreduce_mode),
                        "global_batch": world * a.batch, "nodes_per_batch": round(n_nodes, 1),
-                       "parallelism": f"dp{world}", "final_loss": round(final_loss, 4)},
+                       "parallelism": f"dp{world}", "final_loss": round(final_loss, 4),
+                       "ego_pipeline": bool(EGO_PIPELINE and not a.eager and a.k == 1)},
             # dominant kernel by total time per step (profiles/): gin_bwd_k
             "roofline": None if r_bwd is None else roofline_entry("gin_bwd5_k", "fused GIN layer backward: BN-backward "
                                        "apply + 4 f32-MFMA GEMMs on 32-row sub-tiles, two workgroups per CU, "

@@ -131,6 +131,18 @@ int scgib_slab_reduce_multi_ex(const scgib_slab_job *jobs, int32_t n_jobs,
                                int32_t max_workgroups, scgib_stream_t stream);
 int scgib_slab_reduce(const float *slab, int32_t n_slabs, int64_t width, float *out,
                       scgib_stream_t stream);
+/* Up to scgib_copy_words_max_ranges() device-to-device copies of 4-byte
+ * words (dst[i] = src[i], i < words) in one launch; the table is copied into
+ * the kernel arguments (HIP-graph capturable), pointers 4-byte aligned, ranges
+ * must not overlap.  Replaces nothing in the reference: the bench's ego-net
+ * pipeline hands the next batch's ego-net buffers over with it. */
+typedef struct {
+    const void *src;
+    void *dst;
+    int64_t words;
+} scgib_copy_range;
+int64_t scgib_copy_words_max_ranges(void);
+int scgib_copy_words(const scgib_copy_range *ranges, int32_t n_ranges, scgib_stream_t stream);
 int scgib_gin_layer_fwd(const float *h_in, int32_t d_in, const float *in_stat,
                         const int32_t *rowptr, const int32_t *col, int64_t n_nodes,
                         float one_plus_eps, const float *w1, const float *b1, const float *w2,

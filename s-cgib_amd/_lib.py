@@ -115,6 +115,8 @@ SIGNATURES = {
     "scgib_slab_reduce_max_jobs": (_I64, []),
     "scgib_slab_reduce_multi": (ctypes.c_int, [_P, _I32, _P]),
     "scgib_slab_reduce_multi_ex": (ctypes.c_int, [_P, _I32, _I32, _P]),
+    "scgib_copy_words_max_ranges": (_I64, []),
+    "scgib_copy_words": (ctypes.c_int, [_P, _I32, _P]),
     "scgib_grad_pack_max_tensors": (_I64, []),
     "scgib_grad_pack": (ctypes.c_int, [_P, _I32, _P, _P]),
     "scgib_grad_unpack": (ctypes.c_int, [_P, _I32, _P, _F, _P]),
@@ -147,6 +149,11 @@ class SlabJob(ctypes.Structure):
     """scgib_slab_job (include/scgib.h)."""
     _fields_ = [("slab", ctypes.c_void_p), ("out", ctypes.c_void_p), ("width", ctypes.c_int64),
                 ("n_slabs", ctypes.c_int32), ("stride", ctypes.c_int32)]
+
+
+class CopyRange(ctypes.Structure):
+    """scgib_copy_range (include/scgib.h)."""
+    _fields_ = [("src", ctypes.c_void_p), ("dst", ctypes.c_void_p), ("words", ctypes.c_int64)]
 
 
 class GradSlice(ctypes.Structure):

@@ -356,6 +356,9 @@ def egonet_batch(g: GraphBatch, k: int, x=None):
     """
     if g.device.type != "cuda":
         raise _lib.ScgibError("egonet_batch needs the graph on a HIP device (no CPU fallback)")
+    pre = getattr(g, "ego_prebuilt", None)
+    if pre is not None and x is None:  # EgoPipeline: built by the previous step
+        return pre.view(g, k)
     if not g.symmetric:
         raise _lib.ScgibError("egonet_batch expects a symmetric (to_bidirected) graph")
     dev = g.device
@@ -488,15 +491,88 @@ def _egonet_k1(g, ego_ptr, ego_eptr, ws, x, max_in_degree=12):
         _lib.call("scgib_egonet_k1_build_deg", _ptr(g.rowptr), _ptr(g.col), n,
                   int(max_in_degree), _ptr(ego_ptr), _ptr(ego_eptr), _ptr(ws), _ptr(ego_nodes),
                   _ptr(sub_rowptr), _ptr(sub_col), n_s, _ptr(g.dims), _ptr(ego_dims), _stream())
+    ego = _ego_graph(g, sub_rowptr, sub_col, ego_ptr, ego_nodes, n_s, ego_dims)
+    ego._k1_buffers = (sub_rowptr, sub_col, ego_ptr, ego_nodes, ego_dims)
+    if x is not None:
+        dict.__setitem__(ego.ndata, "x", x.index_select(0, ego_nodes[:n_s]))
+    return ego
+
+
+def _ego_graph(g, sub_rowptr, sub_col, ego_ptr, ego_nodes, n_s, ego_dims):
     ego = GraphBatch(sub_rowptr, sub_col, ego_ptr, None, None, n_edges=-1,
                      max_graph_nodes=max(g.max_graph_nodes, 1))
     ego.dims = ego_dims
     ego.components_closed = True
     ego.seg_dims = g.dims
     dict.__setitem__(ego.ndata, "_ID", ego_nodes[:n_s])
-    if x is not None:
-        dict.__setitem__(ego.ndata, "x", x.index_select(0, ego_nodes[:n_s]))
     return ego
+
+
+class EgoPipeline:
+    """Software pipeline of the k = 1 ego-net build across captured steps
+    (bench): step i trains on ``cur`` (batch i) with the ego-nets built
+    during step i-1, and builds batch i+1's (``nxt``, loaded by the host
+    before the replay) on a stream of its own beside the encoders; after the
+    step's backward one launch (scgib_copy_words) hands ``nxt``'s inputs and
+    ego-net buffers over to ``cur``.  Each step still builds one ego batch;
+    the model reads it through egonet_batch (``cur.graph.ego_prebuilt``), as
+    the reference's forward receives flatten_batch_subgraphs built by its
+    loader (exp_pretraining.py:269-272, :308-309).  Capacity mode, k = 1."""
+
+    def __init__(self, cur, nxt, k):
+        if cur.graph.dims is None or nxt.graph.dims is None or int(k) != 1:
+            raise _lib.ScgibError("EgoPipeline: capacity-mode StaticBatch pair, k = 1")
+        self.cur, self.nxt, self.k = cur, nxt, 1
+        self.stream = torch.cuda.Stream(device=cur.blob.device)
+        self.bufs = None
+        self._pending = None
+
+    def prime(self):
+        """Build the ego-nets of ``cur``'s current batch into persistent buffers
+        (outside any capture; before the first step)."""
+        self.cur.graph.ego_prebuilt = None
+        ego = egonet_batch(self.cur.graph, self.k)
+        if not hasattr(ego, "_k1_buffers"):
+            raise _lib.ScgibError("EgoPipeline: the k = 1 builder did not take this batch")
+        if self.bufs is None:
+            self.bufs = ego._k1_buffers
+        else:
+            for d, s in zip(self.bufs, ego._k1_buffers):
+                d.copy_(s)
+        self.n_s = int(self.cur.graph.ego_caps[0])
+        self.cur.graph.ego_prebuilt = self
+
+    def view(self, g, k):
+        if g is not self.cur.graph or int(k) != self.k:
+            raise _lib.ScgibError("EgoPipeline: ego-nets requested for another batch")
+        sub_rowptr, sub_col, ego_ptr, ego_nodes, ego_dims = self.bufs
+        return _ego_graph(g, sub_rowptr, sub_col, ego_ptr, ego_nodes, self.n_s, ego_dims)
+
+    def build_next(self):
+        """Fork from the current stream: build ``nxt``'s ego-nets (call at the
+        start of the step)."""
+        main = torch.cuda.current_stream()
+        self.stream.wait_stream(main)
+        with torch.cuda.stream(self.stream):
+            self.nxt.graph.ego_prebuilt = None
+            ego = egonet_batch(self.nxt.graph, self.k)
+        if not hasattr(ego, "_k1_buffers"):
+            raise _lib.ScgibError("EgoPipeline: the k = 1 builder did not take this batch")
+        self._pending = ego._k1_buffers
+
+    def hand_over(self):
+        """After the step's last read of ``cur`` (its backward): join the
+        build and copy ``nxt`` -> ``cur`` (inputs + ego-net buffers), one launch."""
+        main = torch.cuda.current_stream()
+        main.wait_stream(self.stream)
+        pairs = [(self.nxt.blob, self.cur.blob)] + list(zip(self._pending, self.bufs))
+        tab = (_lib.CopyRange * len(pairs))()
+        for i, (s, d) in enumerate(pairs):
+            if s.numel() * s.element_size() != d.numel() * d.element_size():
+                raise _lib.ScgibError("EgoPipeline: buffer sizes differ")
+            s.record_stream(main)
+            tab[i] = _lib.CopyRange(s.data_ptr(), d.data_ptr(), s.numel() * s.element_size() // 4)
+        _lib.call("scgib_copy_words", ctypes.cast(tab, ctypes.c_void_p), len(pairs), _stream())
 
 
 class StaticBatch:

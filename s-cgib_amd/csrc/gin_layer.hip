@@ -500,8 +500,11 @@ constexpr bool kLateWeights = SCGIB_LATE_WEIGHTS != 0;
 #ifndef SCGIB_FWD_ALIAS
 #define SCGIB_FWD_ALIAS 1
 #endif
+// (layer 0 with transfer_d folded: the agg tile and W1 are 32 wide, so r
+// takes both of their buffers, contiguous: 59.8 -> 43 KB)
 template <int DIN, bool GATHER, bool PRE>
-constexpr bool kFwdAlias = SCGIB_FWD_ALIAS != 0 && DIN == 64 && GATHER && !PRE;
+constexpr bool kFwdAlias = SCGIB_FWD_ALIAS != 0 &&
+                           ((DIN == 64 && GATHER && !PRE) || (DIN == 32 && GATHER && PRE));
 
 template <int DIN, bool XFORM, bool GATHER = true, bool PRE = false, bool RECON = false>
 __global__ __launch_bounds__(256, (kFwdAlias<DIN, GATHER, PRE> ? 3 : 1)) void gin_fwd_k(
@@ -516,11 +519,12 @@ __global__ __launch_bounds__(256, (kFwdAlias<DIN, GATHER, PRE> ? 3 : 1)) void gi
     static_assert(!RECON || !GATHER, "the recon Gram partial is fused into the dense head MLP");
     static_assert(!PRE || DIN == 32, "transfer_d fold produces the 32-wide layer-0 input");
     const int64_t n = eff_count(dims, 0, ncap);
-    __shared__ __attribute__((aligned(16))) float sA[TM * LDA];   // (contrastive: float4 tiles)
-    __shared__ __attribute__((aligned(16))) float sW1[64 * LDA];
+    // sA | sW1 contiguous (contrastive: float4 tiles in each)
+    __shared__ __attribute__((aligned(16))) float sAW1[TM * LDA + 64 * LDA];
+    float *const sA = sAW1, *const sW1 = sAW1 + TM * LDA;
     __shared__ float sW2[64 * LDH];
     constexpr bool ALIAS = kFwdAlias<DIN, GATHER, PRE>;
-    static_assert(!ALIAS || LDA == LDH, "r takes the agg tile's buffer");
+    static_assert(!ALIAS || TM * LDA + 64 * LDA >= TM * LDH, "r takes the agg tile's (and W1's) buffer");
     __shared__ float sROwn[ALIAS ? 1 : TM * LDH];
     float *const sR = ALIAS ? sA : sROwn;
     __shared__ float sRed[2][64];
@@ -674,7 +678,7 @@ __global__ __launch_bounds__(256, (kFwdAlias<DIN, GATHER, PRE> ? 3 : 1)) void gi
     {
         f32x16 acc = mma_pf<DIN, false, false>(sA + wr * 32 * LDA, LDA, sW1 + wc * 32 * LDA, LDA, zero16());
         const float bias = b1[ccol];
-        if constexpr (ALIAS) __syncthreads();  // every wave's reads of the agg tile are done
+        if constexpr (ALIAS) __syncthreads();  // every wave's reads of the agg tile and W1 are done
 #pragma unroll
         for (int reg = 0; reg < 16; ++reg) {
             const int row = wr * 32 + acc_row(reg, l);

@@ -301,22 +301,21 @@ struct K1Global {
 };
 
 // K1Lds: the block's CSR window staged in LDS by two coalesced rounds —
-// rowptr[lo .. lo + kK1WinRows] with lo = 64 b - 64 (the parents' rows and
-// every ball member's: |u - v| < 64), then col[rowptr[lo] .. rowptr[lo +
-// kK1WinRows]) up to the LDS capacity.  An index outside the window (none under
-// the host-checked bounds) reads global memory; the slots past a row's end
-// load nothing.
-constexpr int kK1WinRows = 192;
+// rowptr[lo .. lo + win] with lo = P b - 64 for P parents per block, win = P +
+// 128 (the parents' rows and every ball member's: |u - v| < 64), then
+// col[rowptr[lo] .. rowptr[lo + win]) up to the LDS capacity.  An index
+// outside the window (none under the host-checked bounds) reads global
+// memory; the slots past a row's end load nothing.
 struct K1Lds {
     const int32_t *__restrict__ rowptr;
     const int32_t *__restrict__ col;
     const int32_t *sRp;
     const int32_t *sCol;
     int32_t lo, c0;
-    uint32_t ncol;
+    uint32_t ncol, win;  // win: rows in the window (kK1WinRows for 64-parent blocks)
     __device__ __forceinline__ int32_t rp(int32_t u) const {
         const uint32_t i = static_cast<uint32_t>(u - lo);
-        return i <= static_cast<uint32_t>(kK1WinRows) ? sRp[i] : rowptr[u];
+        return i <= win ? sRp[i] : rowptr[u];
     }
     __device__ __forceinline__ int32_t cl(int32_t e, bool valid, int32_t) const {
         const uint32_t i = static_cast<uint32_t>(e - c0);
@@ -551,45 +550,56 @@ __device__ __forceinline__ uint64_t k1_pack(uint64_t flag, int32_t n, int32_t e)
 #ifndef SCGIB_EGO_LDS
 #define SCGIB_EGO_LDS 1
 #endif
+// SCGIB_EGO_WAVES: waves (64 parents each) per workgroup of the LDS form
+#ifndef SCGIB_EGO_WAVES
+#define SCGIB_EGO_WAVES 1
+#endif
+constexpr int kK1Waves = SCGIB_EGO_LDS ? SCGIB_EGO_WAVES : 1;
+constexpr int kK1One = 64 * kK1Waves;  // parents per workgroup of the one-pass builder
 template <int D>
-__global__ __launch_bounds__(kK1Block) void egonet_k1_onepass_k(
+__global__ __launch_bounds__(kK1One) void egonet_k1_onepass_k(
     const int32_t *__restrict__ rowptr, const int32_t *__restrict__ col, int64_t n,
     int32_t *__restrict__ ego_ptr, int32_t *__restrict__ ego_eptr, uint64_t *__restrict__ state,
     uint32_t *__restrict__ done, int32_t *__restrict__ ego_nodes,
     int32_t *__restrict__ sub_rowptr, int32_t *__restrict__ sub_col, int64_t n_ego_cap,
     const int32_t *__restrict__ dims, int32_t *__restrict__ ego_dims) {
-    const int nblk = gridDim.x, blk = blockIdx.x, lane = threadIdx.x;
-    const int64_t v = static_cast<int64_t>(blk) * kK1Block + lane;
+    const int nblk = gridDim.x, blk = blockIdx.x, tid = threadIdx.x;
+    const int lane = tid & 63, wave = tid >> 6;
+    const int64_t v = static_cast<int64_t>(blk) * kK1One + tid;
     const bool live = v < eff_count(dims, 0, n);
+    __shared__ int32_t sScan[kK1Waves][2];  // wave totals, then the block's prefix
+    __shared__ int32_t sPre[3];
 #if SCGIB_EGO_LDS
     // the block's CSR window -> LDS (K1Lds): two coalesced rounds instead of
     // four dependent rounds of scattered loads per parent
-    constexpr int kColCap = kK1WinRows * D;
-    __shared__ int32_t sRp[kK1WinRows + 1];
+    constexpr int kWin = kK1One + 128;
+    constexpr int kColCap = kWin * D;
+    __shared__ int32_t sRp[kWin + 1];
     __shared__ int32_t sCol[kColCap];
-    const int32_t lo = blk * kK1Block - 64;
-    for (int i = lane; i <= kK1WinRows; i += kK1Block) {
+    const int32_t lo = blk * kK1One - 64;
+    for (int i = tid; i <= kWin; i += kK1One) {
         const int64_t u = lo + i;
         sRp[i] = rowptr[u < 0 ? 0 : (u > n ? n : u)];
     }
     __syncthreads();
-    const int32_t c0 = sRp[0], dc = sRp[kK1WinRows] - c0;
+    const int32_t c0 = sRp[0], dc = sRp[kWin] - c0;
     const int32_t nc = dc < 0 ? 0 : (dc < kColCap ? dc : kColCap);
-    for (int i0 = 0; i0 < nc; i0 += 4 * kK1Block) {
+    for (int i0 = 0; i0 < nc; i0 += 4 * kK1One) {
         int32_t t[4];
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-            const int i = i0 + k * kK1Block + lane;
+            const int i = i0 + k * kK1One + tid;
             t[k] = i < nc ? col[c0 + i] : 0;
         }
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-            const int i = i0 + k * kK1Block + lane;
+            const int i = i0 + k * kK1One + tid;
             if (i < nc) sCol[i] = t[k];
         }
     }
     __syncthreads();
-    const K1Lds acc{rowptr, col, sRp, sCol, lo, c0, static_cast<uint32_t>(nc)};
+    const K1Lds acc{rowptr, col, sRp, sCol, lo, c0, static_cast<uint32_t>(nc),
+                    static_cast<uint32_t>(kWin)};
     // with the window in LDS the loops run over the actual members and
     // degrees (not the D-slot predicated batches the global-load form needs)
     K1Win<D> b;
@@ -641,11 +651,30 @@ __global__ __launch_bounds__(kK1Block) void egonet_k1_onepass_k(
         }
     }
 #endif
-    int32_t in_n = nb, in_e = ne;  // inclusive within the block
+    int32_t in_n = nb, in_e = ne;  // inclusive within the wave, then the block
     wave_scan2(in_n, in_e);
-    const int32_t agg_n = __shfl(in_n, kK1Block - 1, kWave), agg_e = __shfl(in_e, kK1Block - 1, kWave);
+    int32_t agg_n = __shfl(in_n, 63, kWave), agg_e = __shfl(in_e, 63, kWave);
+    if constexpr (kK1Waves > 1) {  // waves' totals -> block-inclusive, block aggregate
+        if (lane == 63) {
+            sScan[wave][0] = agg_n;
+            sScan[wave][1] = agg_e;
+        }
+        __syncthreads();
+        int32_t wn = 0, we = 0, tn = 0, te = 0;
+#pragma unroll
+        for (int q = 0; q < kK1Waves; ++q) {
+            wn += q < wave ? sScan[q][0] : 0;
+            we += q < wave ? sScan[q][1] : 0;
+            tn += sScan[q][0];
+            te += sScan[q][1];
+        }
+        in_n += wn;
+        in_e += we;
+        agg_n = tn;
+        agg_e = te;
+    }
     int32_t pre_n = 0, pre_e = 0;
-    if (lane == 0) {
+    if (tid == 0) {
         if (blk == 0) {
             __hip_atomic_store(&state[0], k1_pack(2, agg_n, agg_e), __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);
@@ -672,9 +701,10 @@ __global__ __launch_bounds__(kK1Block) void egonet_k1_onepass_k(
         }
     }
 #if SCGIB_EGO_LDS
-    // look-back by the whole wave: lane i reads block (base - i)'s word; the
-    // nearest inclusive prefix ends it once every nearer block has published
-    if (blk > 0) {
+    // look-back by the whole wave (wave 0): lane i reads block (base - i)'s
+    // word; the nearest inclusive prefix ends it once every nearer block has
+    // published
+    if (blk > 0 && wave == 0) {
         for (int32_t base = blk - 1;;) {  // wave-uniform control flow (ballots)
             const int32_t j = base - lane;
             const uint64_t w = j >= 0 ? __hip_atomic_load(&state[j], __ATOMIC_RELAXED,
@@ -705,8 +735,18 @@ __global__ __launch_bounds__(kK1Block) void egonet_k1_onepass_k(
                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 #endif
-    pre_n = __shfl(pre_n, 0, kWave);
-    pre_e = __shfl(pre_e, 0, kWave);
+    if constexpr (kK1Waves > 1) {  // wave 0's prefix to every wave
+        if (tid == 0) {
+            sPre[0] = pre_n;
+            sPre[1] = pre_e;
+        }
+        __syncthreads();
+        pre_n = sPre[0];
+        pre_e = sPre[1];
+    } else {
+        pre_n = __shfl(pre_n, 0, kWave);
+        pre_e = __shfl(pre_e, 0, kWave);
+    }
     const int32_t noff = pre_n + in_n - nb;
     int32_t eo = pre_e + in_e - ne;
     if (v < n) {
@@ -719,11 +759,11 @@ __global__ __launch_bounds__(kK1Block) void egonet_k1_onepass_k(
     }
     if (blk == nblk - 1) {  // the totals: the ego batch's sizes and its tail
         const int32_t ns = pre_n + agg_n, es = pre_e + agg_e;
-        if (lane == 0 && ego_dims) {
+        if (tid == 0 && ego_dims) {
             ego_dims[0] = ns;
             ego_dims[1] = es;
         }
-        for (int64_t i = ns + lane; i <= n_ego_cap; i += kK1Block) {
+        for (int64_t i = ns + tid; i <= n_ego_cap; i += kK1One) {
             sub_rowptr[i] = es;
             if (i < n_ego_cap) ego_nodes[i] = 0;
         }
@@ -772,15 +812,19 @@ __global__ __launch_bounds__(kK1Block) void egonet_k1_onepass_k(
     }
 #endif
     // every look-back of this block is done: count it in; the last one resets
-    if (lane == 0) {
-        const uint32_t t = __hip_atomic_fetch_add(done, 1u, __ATOMIC_RELAXED,
-                                                  __HIP_MEMORY_SCOPE_AGENT);
-        pre_n = t == static_cast<uint32_t>(nblk - 1) ? 1 : 0;
-    }
-    if (__shfl(pre_n, 0, kWave)) {
-        for (int j = lane; j < nblk; j += kK1Block)
-            __hip_atomic_store(&state[j], uint64_t(0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (lane == 0) __hip_atomic_store(done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // (wave 0 only: its look-back is the block's)
+    if (wave == 0) {
+        if (lane == 0) {
+            const uint32_t t = __hip_atomic_fetch_add(done, 1u, __ATOMIC_RELAXED,
+                                                      __HIP_MEMORY_SCOPE_AGENT);
+            pre_n = t == static_cast<uint32_t>(nblk - 1) ? 1 : 0;
+        }
+        if (__shfl(pre_n, 0, kWave)) {
+            for (int j = lane; j < nblk; j += 64)
+                __hip_atomic_store(&state[j], uint64_t(0), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+            if (lane == 0) __hip_atomic_store(done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
     }
 }
 
@@ -895,21 +939,21 @@ extern "C" int scgib_egonet_k1_build_onepass(const int32_t *rowptr, const int32_
         return SCGIB_EINVAL;
     if (n_nodes >= (int64_t(1) << 31) || max_in_degree > 12) return SCGIB_EUNSUPPORTED;
     if (reinterpret_cast<uintptr_t>(scan_state) % 4) return SCGIB_EINVAL;
-    const int32_t nblk = static_cast<int32_t>((n_nodes + kK1Block - 1) / kK1Block);
+    const int32_t nblk = static_cast<int32_t>((n_nodes + kK1One - 1) / kK1One);
     uint32_t *done = scan_state;
     uint64_t *state = reinterpret_cast<uint64_t *>(
         (reinterpret_cast<uintptr_t>(scan_state) + sizeof(uint32_t) + 7) & ~uintptr_t(7));
     hipStream_t st = as_stream(stream);
     if (max_in_degree <= 6)
-        egonet_k1_onepass_k<6><<<nblk, kK1Block, 0, st>>>(rowptr, col, n_nodes, ego_ptr, ego_eptr,
+        egonet_k1_onepass_k<6><<<nblk, kK1One, 0, st>>>(rowptr, col, n_nodes, ego_ptr, ego_eptr,
                                                           state, done, ego_nodes, sub_rowptr,
                                                           sub_col, n_ego_cap, dims, ego_dims);
     else if (max_in_degree <= 8)
-        egonet_k1_onepass_k<8><<<nblk, kK1Block, 0, st>>>(rowptr, col, n_nodes, ego_ptr, ego_eptr,
+        egonet_k1_onepass_k<8><<<nblk, kK1One, 0, st>>>(rowptr, col, n_nodes, ego_ptr, ego_eptr,
                                                           state, done, ego_nodes, sub_rowptr,
                                                           sub_col, n_ego_cap, dims, ego_dims);
     else
-        egonet_k1_onepass_k<12><<<nblk, kK1Block, 0, st>>>(rowptr, col, n_nodes, ego_ptr,
+        egonet_k1_onepass_k<12><<<nblk, kK1One, 0, st>>>(rowptr, col, n_nodes, ego_ptr,
                                                            ego_eptr, state, done, ego_nodes,
                                                            sub_rowptr, sub_col, n_ego_cap, dims,
                                                            ego_dims);

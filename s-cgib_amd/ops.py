@@ -83,10 +83,11 @@ FOLD_LOSS_SLAB = os.environ.get("SCGIB_FOLD_LOSS_SLAB", "1") != "0"
 FUSED_BWD = os.environ.get("SCGIB_FUSED_BWD", "0") != "0"
 # ... with layer l's slab reduce folded into layer l-1's fused launch
 FOLD_FUSED = os.environ.get("SCGIB_FOLD_FUSED", "1") != "0"
-# encoder-pair backward: capture the ego chain before the core chain (off:
-# measured 2 % slower — the replayed graph's queue assignment follows capture
-# order in ways that favour the core chain first)
-EGO_FIRST = os.environ.get("SCGIB_EGO_FIRST", "0") != "0"
+# encoder-pair backward: capture the ego chain before the core chain (round
+# 1: 2 % slower, off; round 2 after the 3-workgroup forward and the early
+# noise draw: 0.4326 vs 0.4381 ms over five rounds, all GPU tests green with
+# it — on; the replayed graph's queue assignment follows capture order)
+EGO_FIRST = os.environ.get("SCGIB_EGO_FIRST", "1") != "0"
 # encoder pair: enqueue the two chains layer by layer alternately (forward and
 # backward) instead of one whole chain after the other (off since the
 # contrastive loss moved into the head launches: A/B 0.5126 vs 0.5148 ms/step,

@@ -35,11 +35,14 @@ pkg = importlib.import_module("s-cgib_amd")
 
 HBM_PEAK_GBS = 8000.0       # MI355X spec (MI355X_MICROARCH.md:36)
 HBM_MEASURED_GBS = 6290.0   # float4 copy, same file
+F32_MFMA_PEAK_TFLOPS = 157.3  # dense fp32 MFMA (MI355X_MICROARCH.md)
 # HBM bytes per launch of each kernel from the rocprofv3 PMC passes of
 # tools/gpu_pmc.sh (2 x FETCH_SIZE + WRITE_SIZE, MI355X_MICROARCH.md "HBM
-# [CDNA4]"), committed under profiles/ — the bench itself runs unprofiled.
+# [CDNA4]"), committed under profiles/ by the round measurement of the CURRENT
+# code (tools/gpu_round.sh) — the bench itself runs unprofiled.  A timed kernel
+# without an entry there is reported with traffic null and a traffic_note.
 TRAFFIC_FILE = os.environ.get("SCGIB_TRAFFIC_FILE",
-                              os.path.join(ROOT, "profiles", "r02_s1", "traffic.json"))
+                              os.path.join(ROOT, "profiles", "traffic_current.json"))
 
 
 def _traffic():
@@ -56,18 +59,17 @@ TRAFFIC = _traffic()
 def traffic_of(variants):
     """Dispatch-weighted mean HBM bytes per launch over the template
     instantiations whose names start with one of ``variants`` (e.g. the GIN
-    variants of gin_bwd_k, not the MLP one)."""
+    variants of gin_bwd_k, not the MLP one); None when none is in the file."""
     got = [t for k, t in TRAFFIC.items() if any(k.startswith(v) for v in variants)]
     n = sum(g["dispatches"] for g in got)
     if not n:
         return None
     return round(sum(g["traffic_bytes"] * g["dispatches"] for g in got) / n)
-METRIC = "graphs/sec (pretrain step, GIN-64×5, k=1) at 1/2/4/8 MI355X; % HBM roofline"
 
 
 def agg_bytes(n, e, d):
-    """Algorithmic bytes of one GIN aggregation launch:
-    neighbour + self rows read, output written, col + rowptr read."""
+    """Algorithmic bytes of one GIN aggregation: neighbour +
+    self rows read, output written, col + rowptr read."""
     return 4 * d * (e + n) + 4 * d * n + 4 * e + 4 * (n + 1)
 
 
@@ -79,13 +81,19 @@ def make_model(F_in, k, gin_layers, dev):
     return model.to(dev).train()
 
 
-F32_MFMA_PEAK_TFLOPS = 157.3  # dense fp32 MFMA (MI355X_MICROARCH.md)
+def agg_fwd_bytes(n, e, d_in):
+    """Algorithmic bytes of one gin_fwd_k launch = SURVEY.md §8(d)'s
+    aggregation figure for the layer (neighbour + self rows read, output
+    written, col + rowptr read).  The kernel's own saved-activation writes
+    (agg, r, z2) and the weights are NOT counted: they are this design's
+    choice, not bytes the algorithm needs (`layer_fwd_bytes_inclusive`)."""
+    return agg_bytes(n, e, d_in)
 
 
-def layer_fwd_bytes(n, e, d_in):
-    """Algorithmic bytes of one gin_fwd_k launch: the gather
-    (neighbour + self rows, col + rowptr), W1/b1/W2/b2, the agg / r / z2
-    writes and the per-tile BN statistics."""
+def layer_fwd_bytes_inclusive(n, e, d_in):
+    """Everything one gin_fwd_k launch moves: the gather (neighbour + self
+    rows, col + rowptr), W1/b1/W2/b2, the agg / r / z2 writes and the per-tile
+    BN statistics (reported beside the §8(d) figure as frac_inclusive)."""
     return (4 * d_in * (e + n) + 4 * e + 4 * (n + 1)
             + 4 * (64 * d_in + 64 + 64 * 64 + 64)
             + 4 * n * (d_in + 64 + 64) + 512 * ((n + 63) // 64))
@@ -105,18 +113,46 @@ def layer_bwd_bytes(n, e, d_in):
 
 
 def stats_bytes(n, e, d):
-    """Algorithmic bytes of one gin_bwd_stats_k launch with the transposed
-    gather: d(agg) rows of every out-neighbour + self, col_t + rowptr_t,
-    z2 read, dy written (+ 128 floats of tile sums per 64 rows)."""
-    return 4 * d * (e + n) + 4 * e + 4 * (n + 1) + 4 * 64 * n * 2 + 512 * ((n + 63) // 64)
+    """Algorithmic bytes of one gin_bwd_stats_k launch: the transposed
+    aggregation of d(agg) (§8(d)'s figure when it gathers, e > 0; the plain
+    dh read otherwise) + z2 read and dy written."""
+    gather = agg_bytes(n, e, d) - 4 * d * n if e > 0 else 4 * d * n
+    return gather + 4 * 64 * n * 2
 
 
-def stats_flops(n, e, d):
+def no_flops(n, e, d):
     return 0
 
 
 def layer_bwd_flops(n, e, d_in):
     return 4 * n * 64 * (64 + d_in)  # dW2, dr, dW1, d(agg)
+
+
+# The step's kernels timed by KernelTimer, by kernel (the C-ABI entries that
+# launch it, a filter on the launch sizes, §8(d) bytes, flops, and the PMC
+# name prefixes of its template instances in the traffic file)
+KERNELS = {
+    "gin_fwd_k": dict(entries=("scgib_gin_layer0_fwd", "scgib_gin_layer_fwd_bn"),
+                      keep=lambda m: True, bytes=agg_fwd_bytes, flops=layer_fwd_flops,
+                      pmc=["gin_fwd_k<32, false, true, true,", "gin_fwd_k<64, true, true,",
+                           "gin_fwd_k<64, false, true,"],
+                      desc="fused GIN layer forward: gather (+ previous BN + ReLU on load) + "
+                           "2 f32-MFMA GEMMs + BN tile statistics"),
+    "gin_bwd5_k": dict(entries=("scgib_gin_layer_bwd",), keep=lambda m: m["d_in"] == 64,
+                       bytes=layer_bwd_bytes, flops=layer_bwd_flops, pmc=["gin_bwd5_k<64>"],
+                       desc="fused GIN layer backward (d_in = 64): BN-backward apply + 4 "
+                            "f32-MFMA GEMMs on 32-row sub-tiles"),
+    "gin_bwd_stats_k": dict(entries=("scgib_gin_bwd_stats_bn_fold", "scgib_gin_bwd_stats_seg_bn",
+                                     "scgib_gin_bwd_stats_bn"),
+                            keep=lambda m: True, bytes=stats_bytes, flops=no_flops,
+                            pmc=["gin_bwd_stats_k<"],
+                            desc="GIN backward statistics: transposed gather of d(agg) + ReLU "
+                                 "mask + BN-backward sums"),
+    "gin_bwd_k": dict(entries=("scgib_gin_layer0_bwd",), keep=lambda m: True,
+                      bytes=layer_bwd_bytes, flops=layer_bwd_flops,
+                      pmc=["gin_bwd_k<32, true, true,"],
+                      desc="layer-0 backward with transfer_d folded (d_in = 32)"),
+}
 
 
 class KernelTimer:
@@ -156,40 +192,54 @@ class KernelTimer:
     def __exit__(self, *exc):
         pkg.ops.OBSERVER = None
 
-    def summary(self, name, bytes_fn, flops_fn):
+    def kernel_summary(self, spec, steps):
+        """Launch-averaged time, §8(d) bytes and flops of one KERNELS entry,
+        and its summed time per step over ``steps`` timed steps."""
         torch.cuda.synchronize()
-        rec = self.records[name]
+        rec = [r for name in spec["entries"] for r in self.records.get(name, ())
+               if spec["keep"](r[2])]
         if not rec:
             return None
         ms = [s.elapsed_time(e) / self.REPEAT for s, e, _ in rec]
-        byts = [bytes_fn(m["n"], m["e"], m["d_in"]) for _, _, m in rec]
-        fl = [flops_fn(m["n"], m["e"], m["d_in"]) for _, _, m in rec]
+        byts = [spec["bytes"](m["n"], m["e"], m["d_in"]) for _, _, m in rec]
+        fl = [spec["flops"](m["n"], m["e"], m["d_in"]) for _, _, m in rec]
         k = len(ms)
         avg_ms = sum(ms) / k
         avg_b, avg_f = sum(byts) / k, sum(fl) / k
         gbs = avg_b / (avg_ms * 1e-3) / 1e9
         tfs = avg_f / (avg_ms * 1e-3) / 1e12
-        hbm_frac, mfma_frac = gbs / HBM_PEAK_GBS, tfs / F32_MFMA_PEAK_TFLOPS
         return {"avg_bytes": avg_b, "avg_flops": avg_f, "avg_ms": avg_ms, "launches": k,
-                "gbs": gbs, "tflops": tfs, "hbm_frac": hbm_frac, "mfma_frac": mfma_frac}
+                "per_step_us": sum(ms) / steps * 1e3, "launches_per_step": k / steps,
+                "gbs": gbs, "tflops": tfs, "hbm_frac": gbs / HBM_PEAK_GBS,
+                "mfma_frac": tfs / F32_MFMA_PEAK_TFLOPS}
 
 
 def roofline_entry(kernel, desc, r, variants):
     """`roofline` object: bound = the resource this kernel is closer to
-    saturating (the two fractions are both reported)."""
+    saturating (both fractions are reported); traffic = PMC HBM bytes per
+    launch of the same kernel from TRAFFIC_FILE (null + a note if absent)."""
     if r["mfma_frac"] > r["hbm_frac"]:
         bound, ach, peak, unit = "mfma", r["tflops"], F32_MFMA_PEAK_TFLOPS, "TFLOP/s"
     else:
         bound, ach, peak, unit = "hbm", r["gbs"], HBM_PEAK_GBS, "GB/s"
-    return {"bound": bound, "kernel": f"{kernel} ({desc})", "achieved": round(ach, 2),
-            "peak": peak, "unit": unit, "frac": round(ach / peak, 4),
-            "traffic": traffic_of(variants),
-            "hbm_gbs": round(r["gbs"], 1), "hbm_frac": round(r["hbm_frac"], 4),
-            "hbm_frac_vs_measured_copy": round(r["gbs"] / HBM_MEASURED_GBS, 4),
-            "mfma_f32_tflops": round(r["tflops"], 2), "mfma_frac": round(r["mfma_frac"], 4),
-            "avg_launch_us": round(r["avg_ms"] * 1e3, 3),
-            "avg_bytes_per_launch": int(r["avg_bytes"]),
-            "avg_flops_per_launch": int(r["avg_flops"]), "launches_timed": r["launches"]}
+    traffic = traffic_of(variants)
+    out = {"bound": bound, "kernel": kernel, "kernel_desc": desc, "achieved": round(ach, 2),
+           "peak": peak, "unit": unit, "frac": round(ach / peak, 4), "traffic": traffic,
+           "traffic_file": os.path.relpath(TRAFFIC_FILE, ROOT),
+           "hbm_gbs": round(r["gbs"], 1), "hbm_frac": round(r["hbm_frac"], 4),
+           "hbm_frac_vs_measured_copy": round(r["gbs"] / HBM_MEASURED_GBS, 4),
+           "mfma_f32_tflops": round(r["tflops"], 2), "mfma_frac": round(r["mfma_frac"], 4),
+           "avg_launch_us": round(r["avg_ms"] * 1e3, 3),
+           "per_step_us": round(r["per_step_us"], 2),
+           "launches_per_step": round(r["launches_per_step"], 2),
+           "avg_bytes_per_launch": int(r["avg_bytes"]),
+           "avg_flops_per_launch": int(r["avg_flops"]), "launches_timed": r["launches"]}
+    if traffic is None:
+        out["traffic_note"] = (f"no PMC entry for {variants} in {out['traffic_file']}: "
+                               "run tools/gpu_round.sh on this code")
+    else:
+        out["traffic_over_algorithmic"] = round(traffic / r["avg_bytes"], 3)
+    return out
 
 
 def superbatch_roofline(dev, n_target=1_200_000, reps=20):
@@ -241,12 +291,22 @@ def superbatch_roofline(dev, n_target=1_200_000, reps=20):
     st = [rec for name in ("scgib_gin_bwd_stats_bn", "scgib_gin_bwd_stats_bn_fold")
           for rec in timer.records[name] if rec[2]["e"] > 0]
     torch.cuda.synchronize()
-    for key, recs, fn in (("gin_fwd_k", fwd, layer_fwd_bytes), ("gin_bwd_stats_k", st, stats_bytes)):
+    # gin_fwd_k over its d = 64 layers: frac on §8(d)'s aggregation bytes;
+    # frac_inclusive counts everything the launch moves (its own saved
+    # agg / r / z2 writes and the weights too); mfma_frac on its two GEMMs
+    fwd = [rec for rec in fwd if rec[2]["d_in"] == 64]
+    for key, recs, fn in (("gin_fwd_k", fwd, agg_fwd_bytes), ("gin_bwd_stats_k", st, stats_bytes)):
         if recs:
             ms_k = statistics.mean(a.elapsed_time(b) / KernelTimer.REPEAT for a, b, _ in recs)
             m = recs[0][2]
             res[key] = _frac_entry(fn(m["n"], m["e"], m["d_in"]), ms_k)
             res[key]["launches"] = len(recs)
+            if key == "gin_fwd_k":
+                inc = layer_fwd_bytes_inclusive(m["n"], m["e"], m["d_in"])
+                res[key]["bytes_inclusive"] = int(inc)
+                res[key]["frac_inclusive"] = round(inc / (ms_k * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+                fl = layer_fwd_flops(m["n"], m["e"], m["d_in"])
+                res[key]["mfma_frac"] = round(fl / (ms_k * 1e-3) / 1e12 / F32_MFMA_PEAK_TFLOPS, 4)
     # the step's dominant kernel (gin_bwd5_k, d_in = 64 layers) at this scale:
     # ~37 k sub-tiles, ~146 per workgroup, so its start-of-kernel chain is
     # amortised — the steady-state rate of the sub-tile loop
@@ -282,30 +342,43 @@ def cpu_model():
     return "unknown"
 
 
-def cpu_baselines(pool_host, k, gin_layers, F_in, seconds=20.0):
-    """the CPU path at all the cores this process may use and
-    at 1 core, with the CPU model, nproc and torch.get_num_threads()."""
+def cpu_baselines(pool_host, k, gin_layers, F_in, workload, seconds=20.0):
+    """the CPU path at all the CPUs this process may run on
+    (len(os.sched_getaffinity(0)) torch threads: `value`), at the box's CPU
+    share (torch's default thread count, OMP_NUM_THREADS) and at 1 core, with
+    the CPU model, nproc and the thread counts.  Each leg is a bounded sample
+    of ~seconds/2 of CPU work."""
     threads = torch.get_num_threads()
-    allc = cpu_baseline(pool_host, k, gin_layers, F_in, seconds, warmup=3, min_steps=10)
-    torch.set_num_threads(1)
-    try:
-        one = cpu_baseline(pool_host, k, gin_layers, F_in, seconds, warmup=1, min_steps=3)
-    finally:
-        torch.set_num_threads(threads)
     try:
         affinity = len(os.sched_getaffinity(0))
     except AttributeError:
-        affinity = None
+        affinity = os.cpu_count() or threads
+    leg = max(seconds / 2, 5.0)
+    legs = {}
+    try:
+        for name, nt, warm, mins in (("all_affinity", affinity, 2, 5), ("share", threads, 2, 5),
+                                     ("one_core", 1, 1, 3)):
+            torch.set_num_threads(nt)
+            legs[name] = cpu_baseline(pool_host, k, gin_layers, F_in, workload, leg, warmup=warm,
+                                      min_steps=mins)
+    finally:
+        torch.set_num_threads(threads)
+    allc = legs["all_affinity"]
     out = dict(allc)
-    out.update({"cores": threads, "value_1core": one["value"],
-                "ms_per_step_1core": one["ms_per_step"], "cpu_model": cpu_model(),
-                "nproc": os.cpu_count(), "sched_affinity_cpus": affinity,
-                "torch_num_threads": threads,
-                "sample": allc["sample"] + f"; 1-core run: {one['steps']} steps after 1 warm-up"})
+    out.update({"cores": allc["cores"], "cpu_model": cpu_model(), "nproc": os.cpu_count(),
+                "sched_affinity_cpus": affinity, "torch_default_threads": threads,
+                "value_share_threads": legs["share"]["value"],
+                "ms_per_step_share_threads": legs["share"]["ms_per_step"],
+                "value_1core": legs["one_core"]["value"],
+                "ms_per_step_1core": legs["one_core"]["ms_per_step"],
+                "sample": allc["sample"] + f"; legs: {affinity} threads (value), {threads} "
+                                           f"threads ({legs['share']['steps']} steps), 1 thread "
+                                           f"({legs['one_core']['steps']} steps)"})
     return out
 
 
-def cpu_baseline(pool_host, k, gin_layers, F_in, seconds=20.0, warmup=1, min_steps=2):
+def cpu_baseline(pool_host, k, gin_layers, F_in, workload, seconds=20.0, warmup=1,
+                 min_steps=2):
     """The oracle (literal restatement of the reference's CPU path: per-graph
     loops, dense N x N recon) timed on this host's cores, bounded sample."""
     from oracle import egonet
@@ -354,7 +427,7 @@ def cpu_baseline(pool_host, k, gin_layers, F_in, seconds=20.0, warmup=1, min_ste
     return {"value": round(B / step, 2), "unit": "graphs/s", "cores": torch.get_num_threads(),
             "kind": "port",
             "sample": (f"oracle/scgib_ref.py pretrain step (fwd+bwd+Adam, dense NxN recon, "
-                       f"per-graph loops) on {B}-molecule QM9-like batches, median of "
+                       f"per-graph loops) on {B}-molecule {workload}-like batches, k={k}, median of "
                        f"{len(times)} steps after {warmup} warm-up, torch CPU threads="
                        f"{torch.get_num_threads()}, os.cpu_count={os.cpu_count()}; ego-nets "
                        f"pre-extracted as in the reference (oracle/egonet_ref.c, "
@@ -366,9 +439,11 @@ SUM_LOSS = os.environ.get("SCGIB_BENCH_SUM_LOSS", "0") != "0"
 # N > 1: capture the RCCL all-reduce inside the replayed step graph (falls back
 # to all-reduce between two replays if the capture raises)
 GRAPH_ALLREDUCE = os.environ.get("SCGIB_GRAPH_ALLREDUCE", "1") != "0"
-# k = 1 ego-net build of batch i+1 inside step i, beside the encoders
-# (graph.EgoPipeline): every step still builds one ego batch, off the chain
-EGO_PIPELINE = os.environ.get("SCGIB_EGO_PIPELINE", "0") != "0"
+
+
+WORKLOAD_DESC = {"qm9": "QM9-like", "molpcba": "ogbg-molpcba-like", "pcqm4mv2": "PCQM4Mv2-like",
+                 "zinc": "ZINC-like", "mutagenicity": "Mutagenicity-like",
+                 "molhiv": "ogbg-molhiv-like"}
 
 
 def main():
@@ -399,10 +474,6 @@ def main():
                     help="torch's fused Adam instead of the one-launch scgib Adam")
     a = ap.parse_args()
 
-    # hipBLASLt's heuristics pick 2-workgroup kernels for the tall-skinny
-    # [N,64]^T x [N,64] weight-gradient GEMMs (~90 us each, profiles/r01_baseline);
-    # rocBLAS is ~2-3x faster on them.  (Process-wide torch setting.)
-    torch.backends.cuda.preferred_blas_library("cublas")
     rank, world, local = pkg.dist.init_from_env()
     if a.force_allreduce and world == 1 and not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
@@ -471,20 +542,11 @@ def main():
             padded.append(static.pad(gx))
 
         one = torch.ones((), dtype=torch.float32, device=dev)
-        pipe = None
-        if EGO_PIPELINE and a.k == 1:
-            nxt = pkg.graph.StaticBatch(a.batch, n_cap, e_cap, F_in, mgn, ego_caps, dev, k=a.k)
-            pipe = pkg.graph.EgoPipeline(static, nxt, a.k)
 
-        def load(i):  # batch i into the step's inputs (the pipeline: batch i+1 into nxt)
-            if pipe is None:
-                static.load(padded[i % len(padded)])
-            else:
-                pipe.nxt.load(padded[(i + 1) % len(padded)])
+        def load(i):  # batch i into the step's static inputs
+            static.load(padded[i % len(padded)])
 
         def body():
-            if pipe is not None:
-                pipe.build_next()
             _, kl, con, rec = model(static.graph, static.x, None, None, None, 1, None, a.k, dev,
                                     a.batch)
             # loss = KL + contrastive + recon (exp_pretraining.py:321): d loss / d part = 1,
@@ -497,16 +559,11 @@ def main():
             else:
                 torch.autograd.backward((kl, rec, con), (one, one, one))
                 out = (kl, rec, con)
-            if pipe is not None:
-                pipe.hand_over()
             return out
 
         side = torch.cuda.Stream()
         side.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(side):  # warm-up (allocator, Adam state, RCCL comm) off the capture
-            if pipe is not None:
-                static.load(padded[0])
-                pipe.prime()
             for i in range(3):
                 load(i)
                 opt.zero_grad(set_to_none=True)
@@ -558,10 +615,6 @@ def main():
                 opt.step()
             allreduce_mode = "between two graph replays"
 
-        if pipe is not None:  # step 0 trains on padded[0] with its ego-nets prebuilt
-            static.load(padded[0])
-            pipe.prime()
-
         def step(i):
             load(i)
             graph.replay()
@@ -594,32 +647,41 @@ def main():
     # launch of the measured kernel (forward+backward of the same model)
     # (one stream: the encoder branches are not forked here, so no other
     # kernel runs inside a bracket)
-    r_bwd = r_fwd = None
+    kernels = {}
     fork_losses = pkg.models.FORK_LOSSES
     if not a.no_kernel_timer:
+        entries = [e for spec in KERNELS.values() for e in spec["entries"]]
+        timed_steps = min(a.steps, 10)
         pkg.models.FORK_ENCODERS = pkg.models.FORK_LOSSES = False
-        with KernelTimer("scgib_gin_layer_fwd_bn", "scgib_gin_layer_bwd") as timer:
-            for i in range(min(a.steps, 10)):
-                g = pool[i % len(pool)]
-                model.zero_grad(set_to_none=True)
-                _, kl, con, rec = model(g, g.ndata["x"], None, None, None, 1, None, a.k, dev,
-                                        a.batch)
-                (kl + rec + con).backward()
-        pkg.models.FORK_ENCODERS = True
-        pkg.models.FORK_LOSSES = fork_losses
-        r_bwd = timer.summary("scgib_gin_layer_bwd", layer_bwd_bytes, layer_bwd_flops)
-        r_fwd = timer.summary("scgib_gin_layer_fwd_bn", layer_fwd_bytes, layer_fwd_flops)
+        try:
+            with KernelTimer(*entries) as timer:
+                for i in range(timed_steps):
+                    g = pool[i % len(pool)]
+                    model.zero_grad(set_to_none=True)
+                    _, kl, con, rec = model(g, g.ndata["x"], None, None, None, 1, None, a.k, dev,
+                                            a.batch)
+                    (kl + rec + con).backward()
+        finally:
+            pkg.models.FORK_ENCODERS = True
+            pkg.models.FORK_LOSSES = fork_losses
+        for name, spec in KERNELS.items():
+            r = timer.kernel_summary(spec, timed_steps)
+            if r is not None:
+                kernels[name] = roofline_entry(name, spec["desc"], r, spec["pmc"])
+    # the dominant kernel = the largest summed time per step (kernel-timer pass)
+    dominant = max(kernels, key=lambda k: kernels[k]["per_step_us"]) if kernels else None
 
     sb = None if a.no_superbatch or rank != 0 else superbatch_roofline(dev)
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
-        cpu = cpu_baselines(pool_host[:2], a.k, a.gin_layers, F_in, a.cpu_seconds)
+        cpu = cpu_baselines(pool_host[:2], a.k, a.gin_layers, F_in, a.workload, a.cpu_seconds)
 
     if rank == 0:
         total_graphs = world * a.batch * a.steps
         n_nodes = statistics.mean(g.num_nodes() for g in pool)
         line = {
-            "metric": METRIC,
+            "metric": f"graphs/sec (pretrain step, GIN-64×{a.gin_layers}, k={a.k}) at "
+                      f"1/2/4/8 MI355X; % HBM roofline",
             "value": round(total_graphs / elapsed, 1),
             "unit": "graphs/s",
             "n_gpus": world,
@@ -630,7 +692,8 @@ def main():
             "scaling": "strong" if a.global_batch else "weak",
             "vs_baseline": None,
             "dtype": "fp32",
-            "data": "synthetic (seeded QM9-like molecules, SURVEY.md §8(d)); random-init weights",
+            "data": f"synthetic (seeded {WORKLOAD_DESC.get(a.workload, a.workload)} molecules, "
+                    f"SURVEY.md §8(d)); random-init weights",
             "config": {"workload": f"{a.workload} pretrain step GIN-64x{a.gin_layers} "
                                    f"k={a.k}, batch {a.batch}/GPU, Mainmodel_continue + Adam",
                        "launch": "eager" if a.eager else "hip-graph replay (capacity mode)",
@@ -638,24 +701,27 @@ def main():
                        ("eager" if a.eager else allreduce_mode),
                        "global_batch": world * a.batch, "nodes_per_batch": round(n_nodes, 1),
                        "parallelism": f"dp{world}", "final_loss": round(final_loss, 4),
-                       "ego_pipeline": bool(EGO_PIPELINE and not a.eager and a.k == 1)},
-            # dominant kernel by total time per step (profiles/): gin_bwd_k
-            "roofline": None if r_bwd is None else roofline_entry("gin_bwd5_k", "fused GIN layer backward: BN-backward "
-                                       "apply + 4 f32-MFMA GEMMs on 32-row sub-tiles, two workgroups per CU, "
-                                       "b128-fed operands", r_bwd, ["gin_bwd5_k<64>"]),
-            "roofline_gin_fwd": None if r_fwd is None else roofline_entry("gin_fwd_k", "fused GIN layer: gather + 2 "
-                                               "f32-MFMA GEMMs + BN tile stats", r_fwd,
-                                               ["gin_fwd_k<32, false, true,",
-                                                "gin_fwd_k<64, true, true,",
-                                                "gin_fwd_k<64, false, true,"]),
+                       "bn_semantics": ("single rank: BatchNorm statistics over the whole batch"
+                                        if world == 1 else
+                                        "replica mode (DESIGN.md §6): each rank's BatchNorm, "
+                                        "contrastive, recon and last-graph KL over its own "
+                                        f"{a.batch}-molecule sub-batch (= the reference at batch "
+                                        f"{a.batch}); gradients and BN running statistics "
+                                        "averaged over ranks by the one all-reduce")},
+            # the kernel with the largest summed time per step in the kernel-timer
+            # pass; every timed kernel's entry is in roofline_kernels
+            "roofline": kernels.get(dominant),
+            "roofline_kernels": kernels or None,
             "roofline_superbatch": None if sb is None else dict(
                 sb, bound="hbm", peak=HBM_PEAK_GBS, unit="GB/s",
                 note="ZINC-like superbatch, [N,64] fp32 > 256 MiB Infinity Cache; frac = "
                      "algorithmic bytes / launch time / 8.0 TB/s (north_star target >= 0.40 on "
                      "the on-path gather kernels gin_fwd_k and gin_bwd_stats_k; "
-                     "gin_aggregate_k is a reference kernel, not in the step); gin_bwd5_k: the "
-                     "step's dominant kernel at this scale (~146 sub-tiles per workgroup, its "
-                     "start-of-kernel chain amortised), mfma_frac = flops / time / 157.3 TF/s"),
+                     "gin_aggregate_k is a reference kernel, not in the step); gin_fwd_k frac "
+                     "on §8(d) aggregation bytes, frac_inclusive on everything the launch moves "
+                     "(its saved agg / r / z2 writes too); gin_bwd5_k at this scale (~146 "
+                     "sub-tiles per workgroup, its start-of-kernel chain amortised), mfma_frac "
+                     "= flops / time / 157.3 TF/s"),
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)

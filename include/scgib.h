@@ -131,18 +131,6 @@ int scgib_slab_reduce_multi_ex(const scgib_slab_job *jobs, int32_t n_jobs,
                                int32_t max_workgroups, scgib_stream_t stream);
 int scgib_slab_reduce(const float *slab, int32_t n_slabs, int64_t width, float *out,
                       scgib_stream_t stream);
-/* Up to scgib_copy_words_max_ranges() device-to-device copies of 4-byte
- * words (dst[i] = src[i], i < words) in one launch; the table is copied into
- * the kernel arguments (HIP-graph capturable), pointers 4-byte aligned, ranges
- * must not overlap.  Replaces nothing in the reference: the bench's ego-net
- * pipeline hands the next batch's ego-net buffers over with it. */
-typedef struct {
-    const void *src;
-    void *dst;
-    int64_t words;
-} scgib_copy_range;
-int64_t scgib_copy_words_max_ranges(void);
-int scgib_copy_words(const scgib_copy_range *ranges, int32_t n_ranges, scgib_stream_t stream);
 int scgib_gin_layer_fwd(const float *h_in, int32_t d_in, const float *in_stat,
                         const int32_t *rowptr, const int32_t *col, int64_t n_nodes,
                         float one_plus_eps, const float *w1, const float *b1, const float *w2,
@@ -253,35 +241,6 @@ int scgib_gin_layer_bwd(const float *dy, const float *z2, const float *r, const 
                         const float *w2, int64_t n_nodes, float *dagg, float *slab,
                         float *wgrad, const int32_t *dims, const scgib_bn_bwd_pending *pending,
                         scgib_stream_t stream);
-/* Fused backward of layer l (d_in = 64) and the statistics of layer l-1:
- * scgib_gin_layer_bwd followed by scgib_gin_bwd_stats_bn_fold(dagg, ...) in
- * one launch, over component-aligned chunks (d(agg) stays on chip).
- * Replaces, per layer l >= 1, the pair gin_bwd + gin_bwd_stats that the
- * reference's autograd runs through GINConv / BatchNorm1d (models.py:52-72).
- * chunk_ptr: scgib_gin_chunk_bounds of the same graph (scgib_gin_chunks(n) + 1
- * entries).  Valid when every component (graph_ptr segment) has at most
- * scgib_gin_chunk_max_component() rows and no edge leaves its component.
- * Outputs: dy_prev (dy of layer l-1), the layer l-1 BN-backward sums in
- * bn_ws_prev (deferred, or finished into dgamma/dbeta/coef_prev), and one
- * weight-gradient slab per chunk (slab_reduce: n_slabs = scgib_gin_chunks).
- * fold (NULL: none): a slab reduce job (the previous fused layer's) run in
- * extra workgroups ahead of the chunk grid, as in scgib_gin_bwd_stats_bn_fold. */
-int32_t scgib_gin_chunk_max_component(void);
-int64_t scgib_gin_chunks(int64_t n_nodes);
-int scgib_gin_chunk_bounds(const int32_t *graph_ptr, int64_t n_seg, const int32_t *seg_dims,
-                           int64_t n_nodes, const int32_t *dims, int32_t *chunk_ptr,
-                           scgib_stream_t stream);
-int scgib_gin_layer_bwd_fused(const float *dy, const float *z2, const float *r, const float *agg,
-                              const float *stat, const float *coef, const float *w1,
-                              const float *w2, int64_t n_nodes, const int32_t *chunk_ptr,
-                              const int32_t *rowptr_t, const int32_t *col_t, float one_plus_eps,
-                              const float *z2_prev, const float *stat_prev, int32_t training,
-                              float *dy_prev, float *dgamma_prev, float *dbeta_prev,
-                              float *coef_prev, float *bn_ws_prev, uint32_t *counters,
-                              int32_t defer, float *slab, const int32_t *dims,
-                              const scgib_bn_bwd_pending *pending, const scgib_slab_job *fold,
-                              scgib_stream_t stream);
-
 /* ---- A6: per-segment readouts (dgl.sum_nodes) -------------------------------
  * out[s,:] = sum_{i in [ptr[s], ptr[s+1])} x[i,:]   (models.py:716, 725, 733)
  * segment_broadcast is its adjoint: out[i,:] = g[s,:] for every row i of s.
@@ -407,15 +366,6 @@ int scgib_noise_uniform(float *u_gate, float *u_feat, int64_t n_rows, uint64_t *
 int scgib_bn_running_update(const float *stats, const int32_t *graph_ptr, int64_t n_graphs,
                             float momentum, float *running_mean, float *running_var,
                             int64_t *num_batches_tracked, scgib_stream_t stream);
-/* The same over up to 16 workgroups (partition partials chained by the last
- * workgroup to arrive): partials = scgib_bn_running_update_partials(B)
- * doubles of scratch, counter = one ZEROED uint32, left zeroed. */
-int64_t scgib_bn_running_update_partials(int64_t n_graphs);
-int scgib_bn_running_update_multi(const float *stats, const int32_t *graph_ptr, int64_t n_graphs,
-                                  float momentum, float *running_mean, float *running_var,
-                                  int64_t *num_batches_tracked, double *partials,
-                                  uint32_t *counter, scgib_stream_t stream);
-
 /* Backward of scgib_interaction_fwd.  The KL gradient is g_kl [2 n_last, 64],
  * or g_klmean (device scalar, gradient of kl_mean), or neither (both NULL).
  * pad_rows: zero rows [graph_ptr[B], n_nodes) of df, dt, ds.

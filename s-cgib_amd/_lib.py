@@ -41,8 +41,6 @@ SIGNATURES = {
                                              _P, _P, _I32, _P]),
     "scgib_noise_uniform": (ctypes.c_int, [_P, _P, _I64, _P, _P, _P]),
     "scgib_bn_running_update": (ctypes.c_int, [_P, _P, _I64, _F, _P, _P, _P, _P]),
-    "scgib_bn_running_update_partials": (_I64, [_I64]),
-    "scgib_bn_running_update_multi": (ctypes.c_int, [_P, _P, _I64, _F, _P, _P, _P, _P, _P, _P]),
     "scgib_interaction_bwd": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _I64, _I64, _P,
                                              _P, _P, _P, _F, _I32, _P, _P, _P, _P, _P, _P, _P,
                                              _P, _P, _P, _P, _I32, _P, _P]),
@@ -103,20 +101,12 @@ SIGNATURES = {
     "scgib_bn_bwd_finalize": (ctypes.c_int, [_P, _I64, _I32, _P, _P, _P, _P, _P]),
     "scgib_gin_layer_bwd": (ctypes.c_int, [_P, _P, _P, _P, _I32, _P, _P, _P, _P, _I64, _P, _P,
                                            _P, _P, _P, _P]),
-    "scgib_gin_chunk_max_component": (_I32, []),
-    "scgib_gin_chunks": (_I64, [_I64]),
-    "scgib_gin_chunk_bounds": (ctypes.c_int, [_P, _I64, _P, _I64, _P, _P, _P]),
-    "scgib_gin_layer_bwd_fused": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _P, _P, _I64, _P, _P,
-                                                 _P, _F, _P, _P, _I32, _P, _P, _P, _P, _P, _P,
-                                                 _I32, _P, _P, _P, _P, _P]),
     "scgib_recon_partials_floats": (_I64, [_I64]),
     "scgib_recon_fwd": (ctypes.c_int, [_P, _P, _P, _I64, _I64, _P, _P, _P, _P, _P]),
     "scgib_recon_bwd": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _I64, _P, _P, _P, _P]),
     "scgib_slab_reduce_max_jobs": (_I64, []),
     "scgib_slab_reduce_multi": (ctypes.c_int, [_P, _I32, _P]),
     "scgib_slab_reduce_multi_ex": (ctypes.c_int, [_P, _I32, _I32, _P]),
-    "scgib_copy_words_max_ranges": (_I64, []),
-    "scgib_copy_words": (ctypes.c_int, [_P, _I32, _P]),
     "scgib_grad_pack_max_tensors": (_I64, []),
     "scgib_grad_pack": (ctypes.c_int, [_P, _I32, _P, _P]),
     "scgib_grad_unpack": (ctypes.c_int, [_P, _I32, _P, _F, _P]),
@@ -149,11 +139,6 @@ class SlabJob(ctypes.Structure):
     """scgib_slab_job (include/scgib.h)."""
     _fields_ = [("slab", ctypes.c_void_p), ("out", ctypes.c_void_p), ("width", ctypes.c_int64),
                 ("n_slabs", ctypes.c_int32), ("stride", ctypes.c_int32)]
-
-
-class CopyRange(ctypes.Structure):
-    """scgib_copy_range (include/scgib.h)."""
-    _fields_ = [("src", ctypes.c_void_p), ("dst", ctypes.c_void_p), ("words", ctypes.c_int64)]
 
 
 class GradSlice(ctypes.Structure):

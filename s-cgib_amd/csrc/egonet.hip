@@ -536,26 +536,29 @@ __global__ __launch_bounds__(kK1Block) void egonet_k1_fill_k(
 // count kernel's four dependent load rounds are not repeated by a fill
 // launch.  state[b] packs (flag:2 | nodes:31 | edges:31) in one 64-bit word
 // (flag 1: the block's aggregate, 2: its inclusive prefix); a block waits
-// only on lower-numbered blocks, which the dispatcher starts first.  The last
-// block to finish zeroes every state word and the finish counter, so the
-// next launch (graph replay) starts from zeros.  Integer sums: exact.
+// only on lower-numbered blocks.  HIP promises no dispatch order, so when the
+// grid may not be co-resident (more than kK1Resident blocks) each block takes
+// its logical index from an atomic ticket: every lower index then belongs to
+// a block that is already running, and the look-back always progresses.  Each
+// block drains its state stores (vmcnt(0)) before it counts itself done; the
+// last block to finish zeroes every state word, the ticket and the finish
+// counter, so the next launch (graph replay) starts from zeros.  Integer sums:
+// exact.
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ uint64_t k1_pack(uint64_t flag, int32_t n, int32_t e) {
     return (flag << 62) | (static_cast<uint64_t>(static_cast<uint32_t>(n)) << 31) |
            static_cast<uint64_t>(static_cast<uint32_t>(e));
 }
 
-// SCGIB_EGO_LDS (default 1): the CSR window staged in LDS and the look-back
-// by the whole wave; 0: scattered global loads and a one-lane look-back
-#ifndef SCGIB_EGO_LDS
-#define SCGIB_EGO_LDS 1
-#endif
-// SCGIB_EGO_WAVES: waves (64 parents each) per workgroup of the LDS form
-#ifndef SCGIB_EGO_WAVES
-#define SCGIB_EGO_WAVES 1
-#endif
-constexpr int kK1Waves = SCGIB_EGO_LDS ? SCGIB_EGO_WAVES : 1;
+// The CSR window is staged in LDS and the look-back done by the whole wave
+// (the scattered-global-load form with a one-lane look-back measured 2.7 %
+// slower in the step, round 2).  kK1Waves: waves (64 parents each) per
+// workgroup — 2 and 4 were parity-tested and measured no faster (round 2).
+constexpr int kK1Waves = 1;
 constexpr int kK1One = 64 * kK1Waves;  // parents per workgroup of the one-pass builder
+// grids up to this many blocks are co-resident (64-thread blocks, 256 CUs):
+// blockIdx.x serves as the logical index without the ticket's extra round trip
+constexpr int kK1Resident = 1024;
 template <int D>
 __global__ __launch_bounds__(kK1One) void egonet_k1_onepass_k(
     const int32_t *__restrict__ rowptr, const int32_t *__restrict__ col, int64_t n,
@@ -563,13 +566,21 @@ __global__ __launch_bounds__(kK1One) void egonet_k1_onepass_k(
     uint32_t *__restrict__ done, int32_t *__restrict__ ego_nodes,
     int32_t *__restrict__ sub_rowptr, int32_t *__restrict__ sub_col, int64_t n_ego_cap,
     const int32_t *__restrict__ dims, int32_t *__restrict__ ego_dims) {
-    const int nblk = gridDim.x, blk = blockIdx.x, tid = threadIdx.x;
+    const int nblk = gridDim.x, tid = threadIdx.x;
+    int blk = blockIdx.x;
+    if (nblk > kK1Resident) {  // block-uniform: the logical index from the ticket
+        __shared__ int sTicket;
+        if (tid == 0)
+            sTicket = static_cast<int>(__hip_atomic_fetch_add(done + 1, 1u, __ATOMIC_RELAXED,
+                                                              __HIP_MEMORY_SCOPE_AGENT));
+        __syncthreads();
+        blk = sTicket;
+    }
     const int lane = tid & 63, wave = tid >> 6;
     const int64_t v = static_cast<int64_t>(blk) * kK1One + tid;
     const bool live = v < eff_count(dims, 0, n);
     __shared__ int32_t sScan[kK1Waves][2];  // wave totals, then the block's prefix
     __shared__ int32_t sPre[3];
-#if SCGIB_EGO_LDS
     // the block's CSR window -> LDS (K1Lds): two coalesced rounds instead of
     // four dependent rounds of scattered loads per parent
     constexpr int kWin = kK1One + 128;
@@ -627,30 +638,6 @@ __global__ __launch_bounds__(kK1One) void egonet_k1_onepass_k(
                 ne += k1_index(b, acc.cl(e, true, 0)) >= 0 ? 1 : 0;
         }
     }
-#else
-    const K1Global acc{rowptr, col};
-    K1Win<D> b;
-    K1Rows<D> m;
-    int32_t nb = 0, ne = 0;
-    if (live) {
-        k1_ball<D>(acc, static_cast<int32_t>(v), b);
-        k1_rows<D, 0>(acc, b, m);
-        nb = b.nb;
-        auto count = [&](const K1Rows<D> &mm, int g0) {
-#pragma unroll
-            for (int r = 0; r < K1G<D>; ++r)
-#pragma unroll
-                for (int t = 0; t < D; ++t)
-                    ne += (g0 + r < b.nb && t < mm.deg[r] && k1_index(b, mm.w[r][t]) >= 0) ? 1 : 0;
-        };
-        count(m, 0);
-        if (D + 1 > K1G<D> && b.nb > K1G<D>) {
-            K1Rows<D> m2;
-            k1_rows<D, K1G<D>>(acc, b, m2);
-            count(m2, K1G<D>);
-        }
-    }
-#endif
     int32_t in_n = nb, in_e = ne;  // inclusive within the wave, then the block
     wave_scan2(in_n, in_e);
     int32_t agg_n = __shfl(in_n, 63, kWave), agg_e = __shfl(in_e, 63, kWave);
@@ -681,26 +668,8 @@ __global__ __launch_bounds__(kK1One) void egonet_k1_onepass_k(
         } else {
             __hip_atomic_store(&state[blk], k1_pack(1, agg_n, agg_e), __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);
-#if !SCGIB_EGO_LDS
-            for (int j = blk - 1;;) {
-                const uint64_t w = __hip_atomic_load(&state[j], __ATOMIC_RELAXED,
-                                                     __HIP_MEMORY_SCOPE_AGENT);
-                const uint64_t flag = w >> 62;
-                if (flag == 0) {
-                    __builtin_amdgcn_s_sleep(1);
-                    continue;
-                }
-                pre_n += static_cast<int32_t>((w >> 31) & 0x7fffffffull);
-                pre_e += static_cast<int32_t>(w & 0x7fffffffull);
-                if (flag == 2) break;
-                --j;
-            }
-            __hip_atomic_store(&state[blk], k1_pack(2, pre_n + agg_n, pre_e + agg_e),
-                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#endif
         }
     }
-#if SCGIB_EGO_LDS
     // look-back by the whole wave (wave 0): lane i reads block (base - i)'s
     // word; the nearest inclusive prefix ends it once every nearer block has
     // published
@@ -734,7 +703,6 @@ __global__ __launch_bounds__(kK1One) void egonet_k1_onepass_k(
             __hip_atomic_store(&state[blk], k1_pack(2, pre_n + agg_n, pre_e + agg_e),
                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-#endif
     if constexpr (kK1Waves > 1) {  // wave 0's prefix to every wave
         if (tid == 0) {
             sPre[0] = pre_n;
@@ -768,7 +736,6 @@ __global__ __launch_bounds__(kK1One) void egonet_k1_onepass_k(
             if (i < n_ego_cap) ego_nodes[i] = 0;
         }
     }
-#if SCGIB_EGO_LDS
     if (live) {  // members ascending (DGL order), each row's columns in CSR order
         int32_t r = 0;
         for (uint64_t m0 = b.w[0], m1 = b.w[1]; m0 | m1; ++r) {
@@ -785,36 +752,13 @@ __global__ __launch_bounds__(kK1One) void egonet_k1_onepass_k(
             }
         }
     }
-#else
-    if (live) {
-        auto fill = [&](const K1Rows<D> &mm, auto g0c) {
-            constexpr int G0 = decltype(g0c)::value;
-#pragma unroll
-            for (int r = 0; r < K1G<D>; ++r) {
-                if (G0 + r < b.nb) {
-                    ego_nodes[noff + G0 + r] = b.mem[G0 + r < D + 1 ? G0 + r : D];
-                    sub_rowptr[noff + G0 + r] = eo;
-#pragma unroll
-                    for (int t = 0; t < D; ++t) {
-                        const int32_t i = k1_index(b, mm.w[r][t]);
-                        if (t < mm.deg[r] && i >= 0) sub_col[eo++] = noff + k1_rank(b, i);
-                    }
-                }
-            }
-        };
-        fill(m, std::integral_constant<int, 0>{});
-        if constexpr (D + 1 > K1G<D>) {
-            if (b.nb > K1G<D>) {
-                k1_rows<D, K1G<D>>(acc, b, m);
-                fill(m, std::integral_constant<int, K1G<D>>{});
-            }
-        }
-    }
-#endif
     // every look-back of this block is done: count it in; the last one resets
     // (wave 0 only: its look-back is the block's)
     if (wave == 0) {
         if (lane == 0) {
+            // this block's state stores are performed before it counts itself
+            // done, so the last block's reset cannot be overtaken by one
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             const uint32_t t = __hip_atomic_fetch_add(done, 1u, __ATOMIC_RELAXED,
                                                       __HIP_MEMORY_SCOPE_AGENT);
             pre_n = t == static_cast<uint32_t>(nblk - 1) ? 1 : 0;
@@ -823,7 +767,10 @@ __global__ __launch_bounds__(kK1One) void egonet_k1_onepass_k(
             for (int j = lane; j < nblk; j += 64)
                 __hip_atomic_store(&state[j], uint64_t(0), __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_AGENT);
-            if (lane == 0) __hip_atomic_store(done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (lane == 0) {
+                __hip_atomic_store(done + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
         }
     }
 }
@@ -940,9 +887,9 @@ extern "C" int scgib_egonet_k1_build_onepass(const int32_t *rowptr, const int32_
     if (n_nodes >= (int64_t(1) << 31) || max_in_degree > 12) return SCGIB_EUNSUPPORTED;
     if (reinterpret_cast<uintptr_t>(scan_state) % 4) return SCGIB_EINVAL;
     const int32_t nblk = static_cast<int32_t>((n_nodes + kK1One - 1) / kK1One);
-    uint32_t *done = scan_state;
+    uint32_t *done = scan_state;  // [0]: finished blocks, [1]: ticket
     uint64_t *state = reinterpret_cast<uint64_t *>(
-        (reinterpret_cast<uintptr_t>(scan_state) + sizeof(uint32_t) + 7) & ~uintptr_t(7));
+        (reinterpret_cast<uintptr_t>(scan_state) + 2 * sizeof(uint32_t) + 7) & ~uintptr_t(7));
     hipStream_t st = as_stream(stream);
     if (max_in_degree <= 6)
         egonet_k1_onepass_k<6><<<nblk, kK1One, 0, st>>>(rowptr, col, n_nodes, ego_ptr, ego_eptr,

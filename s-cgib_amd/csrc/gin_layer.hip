@@ -51,11 +51,8 @@ namespace scgib {
 // Fixed combination order -> deterministic.  Counters: caller-provided, zero
 // on entry; each is reset by its last arriver (graph-replay safe).
 // ---------------------------------------------------------------------------
-// tiles per BatchNorm statistics group (SCGIB_BN_GROUP: build-time A/B knob)
-#ifndef SCGIB_BN_GROUP
-#define SCGIB_BN_GROUP 16
-#endif
-constexpr int kGroup = SCGIB_BN_GROUP;
+// tiles per BatchNorm statistics group (8 / 32 / 64 measured +1 %, round 1)
+constexpr int kGroup = 16;
 static_assert(kGroup % 4 == 0 && kGroup <= 64, "group combine: 4 partitions, <= 16 loads each");
 
 struct BnFwdFuse {          // gin_fwd_k: BN statistics + running update
@@ -488,23 +485,16 @@ struct ReconArgs {
 // GATHER = false is the dense two-layer MLP of the head (models.py:1055-1057,
 // applied at :1174): the tile's input rows are staged directly, agg_out and
 // the BN tile statistics are not written, z2_out is the MLP output.
-#ifndef SCGIB_LATE_WEIGHTS
-#define SCGIB_LATE_WEIGHTS 1
-#endif
-constexpr bool kLateWeights = SCGIB_LATE_WEIGHTS != 0;
+constexpr bool kLateWeights = true;  // (early: 0.4372 vs 0.4355 ms, round 2)
 
-// SCGIB_FWD_ALIAS (default 1): the gathering d_in = 64 layers write r into
+// r aliased onto the agg tile: the gathering d_in = 64 layers write r into
 // the agg tile's buffer once every wave's first GEMM is done (one more
 // barrier): 53 KB of LDS and <= 168 VGPRs, three workgroups per CU instead
 // of two, so an ego layer's 437 tiles and Encoder1's 145 fit the chip at once
-#ifndef SCGIB_FWD_ALIAS
-#define SCGIB_FWD_ALIAS 1
-#endif
 // (layer 0 with transfer_d folded: the agg tile and W1 are 32 wide, so r
 // takes both of their buffers, contiguous: 59.8 -> 43 KB)
 template <int DIN, bool GATHER, bool PRE>
-constexpr bool kFwdAlias = SCGIB_FWD_ALIAS != 0 &&
-                           ((DIN == 64 && GATHER && !PRE) || (DIN == 32 && GATHER && PRE));
+constexpr bool kFwdAlias = ((DIN == 64 && GATHER && !PRE) || (DIN == 32 && GATHER && PRE));
 
 template <int DIN, bool XFORM, bool GATHER = true, bool PRE = false, bool RECON = false>
 __global__ __launch_bounds__(256, (kFwdAlias<DIN, GATHER, PRE> ? 3 : 1)) void gin_fwd_k(
@@ -1039,14 +1029,8 @@ __global__ __launch_bounds__(1024) void bn_bwd_finalize_k(const float *__restric
 // of the MLP output); z2 / stat / coef are not read.
 // PRE: layer 0 with transfer_d folded in (see gather_x_rows): d(agg0) is not
 // stored; dWt += d(agg0)^T aggx is accumulated (slab tail of 32 x 16 floats).
-#ifndef SCGIB_BWD_MINB
-#define SCGIB_BWD_MINB 2
-#endif
-#ifndef SCGIB_BWD_PIPELINE
-#define SCGIB_BWD_PIPELINE 0
-#endif
 template <int DIN, bool BN = true, bool PRE = false, bool RECON = false>
-__global__ __launch_bounds__(256, (DIN <= 64 && !RECON ? SCGIB_BWD_MINB : 1)) void gin_bwd_k(
+__global__ __launch_bounds__(256, (DIN <= 64 && !RECON ? 2 : 1)) void gin_bwd_k(
     const float *__restrict__ dy, const float *__restrict__ z2, const float *__restrict__ r,
     const float *__restrict__ agg, const float *__restrict__ stat,
     const float *__restrict__ coef, const float *__restrict__ w1, const float *__restrict__ w2,
@@ -1122,14 +1106,9 @@ __global__ __launch_bounds__(256, (DIN <= 64 && !RECON ? SCGIB_BWD_MINB : 1)) vo
         for (int idx = tid; idx < TM * 16; idx += 256) sPX[(idx >> 4) * LDP + 16 + (idx & 15)] = 0.f;
     float db2 = 0.f, db1 = 0.f;
     constexpr int AQ = DIN / 4, AK = TM * AQ / 256;  // agg tile: float4 per row, per thread
-    // SCGIB_BWD_PIPELINE=1: tiles are software-pipelined when a workgroup
-    // owns several (grid < tiles): the next tile's row loads (z2, dy, r,
-    // aggx) go out as soon as this tile's rows are in LDS and its agg loads
-    // once this tile's agg tile is, so they are in flight during this tile's
-    // four GEMMs.  Off by default: holding the next tile live costs 20-44
-    // bytes/lane of scratch at 2 workgroups/CU and measured 1-2 % slower at
-    // QM9 B512, where nearly every workgroup owns a single tile.
-    constexpr bool PIPE = SCGIB_BWD_PIPELINE != 0;
+    // (software-pipelining the next tile's loads under this tile's GEMMs
+    // measured 1-2 % slower: 20-44 bytes/lane of scratch at 2 workgroups/CU,
+    // and at QM9 B512 nearly every workgroup owns a single tile)
     float4 vz[4], vd[4], vr[4], va[AK], vx = zero;
     auto load_rows = [&](int64_t t) {
         const int64_t r0 = t * TM;
@@ -1179,14 +1158,9 @@ __global__ __launch_bounds__(256, (DIN <= 64 && !RECON ? SCGIB_BWD_MINB : 1)) vo
                              sCoef[67 + 4 * c4]);
         }
     }
-    if (PIPE && blockIdx.x < ntiles) {
-        load_rows(blockIdx.x);
-        load_agg(blockIdx.x);
-    }
     for (int64_t tile = blockIdx.x; tile < ntiles; tile += gsz) {
         const int64_t row0 = tile * TM;
         const int nv = static_cast<int>(n - row0 < TM ? (n - row0 > 0 ? n - row0 : 0) : TM);
-        const int64_t next = tile + gsz;  // block-uniform
         if (dims) {  // capacity mode: zero this tile's padded rows of d(agg)
             const int ncr = static_cast<int>(ncap - row0 < TM ? ncap - row0 : TM);
             if (!PRE)
@@ -1195,7 +1169,7 @@ __global__ __launch_bounds__(256, (DIN <= 64 && !RECON ? SCGIB_BWD_MINB : 1)) vo
             // so the registers are never read again
             if (nv == 0) continue;
         }
-        if (!PIPE) load_rows(tile);
+        load_rows(tile);
         // recon: own IM rows (vd) and nb = ((A + A^T) IM) rows, same layout
         float4 nb[4];
         if constexpr (RECON) {
@@ -1218,7 +1192,7 @@ __global__ __launch_bounds__(256, (DIN <= 64 && !RECON ? SCGIB_BWD_MINB : 1)) vo
 #pragma unroll
             for (int k = 0; k < 4; ++k) vd[k] = rs + 16 * k < nv ? hd.self[k] : zero;
         }
-        if (!PIPE) load_agg(tile);
+        load_agg(tile);
         if (wpending) {  // first tile: its loads are in flight now
             store_weights<DIN>(wregs, sW1, sW2);
             wpending = false;
@@ -1264,7 +1238,6 @@ __global__ __launch_bounds__(256, (DIN <= 64 && !RECON ? SCGIB_BWD_MINB : 1)) vo
             }
             __syncthreads();
         }
-        if (PIPE && next < ntiles) load_rows(next);  // in flight during the GEMMs below
         if (tile == blockIdx.x) SCGIB_MARK(1);
         // dW2 += dz2^T r  (sub-tile j-block wr, k-block wc)
         // dr = dz2 W2  (rows wr, cols wc); the two products alternate
@@ -1287,7 +1260,6 @@ __global__ __launch_bounds__(256, (DIN <= 64 && !RECON ? SCGIB_BWD_MINB : 1)) vo
             float *pa = sA + rr * LDA + 4 * cq;
             pa[0] = va[k].x; pa[1] = va[k].y; pa[2] = va[k].z; pa[3] = va[k].w;
         }
-        if (PIPE && next < ntiles) load_agg(next);
         __syncthreads();
         db1 = col_sum16(db1, sD + q * LDH + ch, 4 * LDH);
         // dW1 += dz1^T agg  (64 x DIN) ; d(agg) = dz1 W1  (TM x DIN)
@@ -1353,28 +1325,6 @@ __global__ __launch_bounds__(256, (DIN <= 64 && !RECON ? SCGIB_BWD_MINB : 1)) vo
     SCGIB_MARK(4);
 }
 
-// ---------------------------------------------------------------------------
-// gin_bwd2_k: the GIN layer backward (BN, d_in = 64) as a staging pipeline.
-//
-// gin_bwd_k stages each tile through registers, two workgroups per CU in
-// lockstep: both load (per-CU fetch bound, ~6 us at QM9 B512), then both
-// compute (MFMA, ~7 us) — nothing overlaps (phase trace r02).  Here ONE
-// workgroup per CU walks its tiles (blockIdx.x, + gridDim.x, ...): the
-// weights and the first tile arrive by LDS-DMA (global_load_lds_dwordx4, no
-// VGPRs) while the BN-backward sums are finished; the next tile is loaded
-// into registers at the start of this tile's GEMMs and written to LDS after
-// them (issue early / write late).  Not LDS-DMA in the loop: with a DMA in
-// flight hipcc models the LDS counter as out of order and waits lgkmcnt(0)
-// before every MFMA operand read (ISA: counted waits only without it).
-// The images are unpadded row-major: every GEMM reads them with 32 lanes on
-// consecutive floats of one row (TN operands over rows, the NN weight
-// operand), which is bank-conflict free at any row stride; only the
-// VALU-written dz tile (read along rows by the NN products) keeps the +1 pad.
-// Arithmetic, k order and slab layout are those of gin_bwd_k, so results are
-// bitwise gin_bwd_k's (dW: one slab per workgroup, fewer workgroups — the
-// slab reduce sums the same products in a different grouping).
-// LDS: weights 32 KB + dy, z2, r, agg 64 KB + dz 16.6 KB (one workgroup per CU).
-// ---------------------------------------------------------------------------
 // s_waitcnt through the builtin (the compiler's wait model sees it, an asm
 // statement it does not): vmcnt(0) = 0x0F70, lgkmcnt(0) alone = 0xC07F (gfx9
 // encoding: vmcnt [3:0] + [15:14], expcnt [6:4], lgkmcnt [11:8])
@@ -1386,227 +1336,14 @@ __device__ __forceinline__ void lds_barrier() {
     __builtin_amdgcn_s_barrier();
 }
 
-// rows [r0, r0 + TM) x W floats of a row-major [*, W] array -> s[TM][W]
-// (unpadded), by 16-byte LDS-DMA: TM * W / 256 wave-instructions of 1 KiB,
-// spread over the 4 waves.  Source rows past `last` read row `last` (valid
-// memory; the consumer never lets them into a result).
-template <int W>
-__device__ __forceinline__ void glds_tile(const float *__restrict__ g, float *s, int64_t r0,
-                                          int64_t last) {
-    constexpr int NI = TM * W / 256 / 4;  // instructions per wave
-    const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
-#pragma unroll
-    for (int k = 0; k < NI; ++k) {
-        const int e = (w * NI + k) * 256 + 4 * l;  // float offset in the tile image
-        int64_t row = r0 + e / W;
-        row = row < last ? row : last;
-        __builtin_amdgcn_global_load_lds(g + row * W + e % W, s + (w * NI + k) * 256, 16, 0, 0);
-    }
-}
-
-// a [64][W] matrix (weights) -> s, contiguous copy
-template <int W>
-__device__ __forceinline__ void glds_matrix(const float *__restrict__ g, float *s) {
-    constexpr int NI = 64 * W / 256 / 4;
-    const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
-#pragma unroll
-    for (int k = 0; k < NI; ++k) {
-        const int e = (w * NI + k) * 256;
-        __builtin_amdgcn_global_load_lds(g + e + 4 * l, s + e, 16, 0, 0);
-    }
-}
-
-template <int DIN>
-__global__ __launch_bounds__(256, 1) void gin_bwd2_k(
-    const float *__restrict__ dy, const float *__restrict__ z2, const float *__restrict__ r,
-    const float *__restrict__ agg, const float *__restrict__ stat,
-    const float *__restrict__ coef, const float *__restrict__ w1, const float *__restrict__ w2,
-    int64_t ncap, int64_t ntiles, float *__restrict__ dagg_out, float *__restrict__ slab,
-    const int32_t *__restrict__ dims, scgib_bn_bwd_pending pend) {
-    static_assert(DIN == 64, "unpadded [TM][DIN] DMA images of whole 256-B rows");
-    constexpr int LDD = LDH;  // dz tile: VALU-written, read along rows
-    constexpr int SLAB = 64 * 64 + 64 * DIN + 128;
-    __shared__ __attribute__((aligned(16))) float sW2[64 * 64];
-    __shared__ __attribute__((aligned(16))) float sW1[64 * DIN];
-    __shared__ __attribute__((aligned(16))) float sDY[TM * 64];
-    __shared__ __attribute__((aligned(16))) float sZ2[TM * 64];
-    __shared__ __attribute__((aligned(16))) float sR[TM * 64];
-    __shared__ __attribute__((aligned(16))) float sA[TM * DIN];
-    __shared__ float sD[TM * LDD];
-    __shared__ float sCoef[128];
-    const int64_t n = eff_count(dims, 0, ncap);
-    const int tid = threadIdx.x, l = tid & 63, w = tid >> 6;
-    const int wr = w >> 1, wc = w & 1;
-    const int c4 = tid & 15, rs = tid >> 4;   // elementwise roles: chunk c4, rows rs + 16 k
-    const int64_t last = ncap - 1;            // last row of the allocations
-    const unsigned gsz = gridDim.x;
-    SCGIB_MARK(0);
-    SCGIB_MARK_HWID();
-    // ordinary loads first (the BN finish and the stat rows), then the DMA
-    BwdFin bfin;
-    const int pend_ngr = static_cast<int>(((n + TM - 1) / TM + kGroup - 1) / kGroup);
-    if (pend.gpart) bn_bwd_fin_load<false>(pend.gpart, pend_ngr, 0, bfin);
-    const float4 s_mean = ld4(stat + 4 * c4), s_istd = ld4(stat + 64 + 4 * c4);
-    const float4 s_sc = ld4(stat + 128 + 4 * c4);
-    float4 c1 = make_float4(0.f, 0.f, 0.f, 0.f), c2 = c1;
-    if (!pend.gpart) {
-        c1 = ld4(coef + 4 * c4);
-        c2 = ld4(coef + 64 + 4 * c4);
-    }
-    glds_matrix<64>(w2, sW2);
-    glds_matrix<DIN>(w1, sW1);
-    int64_t tile = blockIdx.x;
-    if (tile < ntiles) {
-        const int64_t r0 = tile * TM;
-        glds_tile<64>(dy, sDY, r0, last);
-        glds_tile<64>(z2, sZ2, r0, last);
-        glds_tile<64>(r, sR, r0, last);
-        glds_tile<DIN>(agg, sA, r0, last);
-    }
-    if (pend.gpart) {  // finish the BN-backward sums; workgroup 0 writes dgamma, dbeta
-        const double tot = bn_bwd_final<false>(pend.gpart, pend_ngr, bfin);
-        const int cs = bfin_index();
-        const bool lead = (tid & 63) < 32, w0 = blockIdx.x == 0 && lead;
-        const float cf = bn_bwd_publish(cs, tot, n, pend.training, w0 ? pend.dgamma : nullptr,
-                                        w0 ? pend.dbeta : nullptr, nullptr);
-        if (lead) sCoef[cs] = cf;
-    }
-    vm_wait_all();
-    lds_barrier();
-    if (pend.gpart) {
-        c1 = make_float4(sCoef[4 * c4], sCoef[4 * c4 + 1], sCoef[4 * c4 + 2], sCoef[4 * c4 + 3]);
-        c2 = make_float4(sCoef[64 + 4 * c4], sCoef[65 + 4 * c4], sCoef[66 + 4 * c4],
-                         sCoef[67 + 4 * c4]);
-    }
-    f32x16 accW2 = zero16(), accW1 = zero16();
-    float db2 = 0.f, db1 = 0.f;
-    // the next tile in registers: dy, z2, r, agg rows rs + 16 k, chunk c4
-    float4 nx[4][4];
-    const float *const srcs[4] = {dy, z2, r, agg};
-    float *const dsts[4] = {sDY, sZ2, sR, sA};
-    for (; tile < ntiles; tile += gsz) {
-        const int64_t row0 = tile * TM;
-        const int nv = static_cast<int>(n - row0 < TM ? (n - row0 > 0 ? n - row0 : 0) : TM);
-        if (dims) {  // capacity mode: zero this tile's padded rows of d(agg)
-            const int ncr = static_cast<int>(ncap - row0 < TM ? ncap - row0 : TM);
-            for (int idx = nv * DIN + tid; idx < ncr * DIN; idx += 256) dagg_out[row0 * DIN + idx] = 0.f;
-            // block-uniform; every later tile of this workgroup is empty too
-            // (nothing was prefetched for it, nothing computes on it)
-            if (nv == 0) continue;
-        }
-        const int64_t next = tile + gsz;  // block-uniform
-        const bool more = next < ntiles;
-        // dz2 = scale (dy - c1 - xhat c2); rows past nv are zero
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const int rr = rs + 16 * k;
-            const float4 vd = *reinterpret_cast<const float4 *>(sDY + rr * 64 + 4 * c4);
-            const float4 vz = *reinterpret_cast<const float4 *>(sZ2 + rr * 64 + 4 * c4);
-            float4 d = make_float4(0.f, 0.f, 0.f, 0.f);
-            if (rr < nv) {
-                d.x = s_sc.x * (vd.x - c1.x - (vz.x - s_mean.x) * s_istd.x * c2.x);
-                d.y = s_sc.y * (vd.y - c1.y - (vz.y - s_mean.y) * s_istd.y * c2.y);
-                d.z = s_sc.z * (vd.z - c1.z - (vz.z - s_mean.z) * s_istd.z * c2.z);
-                d.w = s_sc.w * (vd.w - c1.w - (vz.w - s_mean.w) * s_istd.w * c2.w);
-            }
-            float *pd = sD + rr * LDD + 4 * c4;
-            pd[0] = d.x; pd[1] = d.y; pd[2] = d.z; pd[3] = d.w;
-        }
-        lds_barrier();  // dz2 complete; dy / z2 consumed
-        if (more) {     // the next tile: in flight during both GEMM pairs
-            const int64_t r1 = next * TM;
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                int64_t row = r1 + rs + 16 * k;
-                row = row < last ? row : last;
-#pragma unroll
-                for (int t = 0; t < 4; ++t) nx[t][k] = ld4(srcs[t] + row * 64 + 4 * c4);
-            }
-        }
-        if (tile == blockIdx.x) SCGIB_MARK(1);
-        // dW2 += dz2^T r ; dr = dz2 W2  (rows wr, cols wc), the two products alternating
-        // (db2: column sums of dz2 from the TN product's A operand, waves wc == 0)
-        f32x16 dr = zero16();
-        mma_pf2<64, true, true, false, true>(sD + wr * 32, LDD, sR + wc * 32, 64, accW2,
-                                             sD + wr * 32 * LDD, LDD, sW2 + wc * 32, 64, dr, &db2);
-        if (tile == blockIdx.x) SCGIB_MARK(6);
-        lds_barrier();  // all reads of dz2 done
-        // dz1 = dr * [r > 0]  -> sD
-#pragma unroll
-        for (int reg = 0; reg < 16; ++reg) {
-            const int row = wr * 32 + acc_row(reg, l), cc = wc * 32 + (l & 31);
-            sD[row * LDD + cc] = sR[row * 64 + cc] > 0.f ? dr[reg] : 0.f;
-        }
-        lds_barrier();  // dz1 complete; r consumed
-        if (tile == blockIdx.x) SCGIB_MARK(2);
-        // dW1 += dz1^T agg (64 x DIN) ; d(agg) = dz1 W1 (TM x DIN): wave w owns
-        // sub-tile (jb, kb) = (w & 1, w >> 1) of both (db1: waves kb == 0)
-        {
-            const int jb = w & 1, kb = w >> 1;
-            f32x16 da = zero16();
-            mma_pf2<64, true, true, false, true>(sD + jb * 32, LDD, sA + kb * 32, DIN, accW1,
-                                                 sD + jb * 32 * LDD, LDD, sW1 + kb * 32, DIN, da,
-                                                 &db1);
-            if (tile == blockIdx.x) SCGIB_MARK(7);
-            // d(agg) through LDS (sDY: consumed, refilled only after the next
-            // barrier) -> full-row float4 stores instead of 16 predicated
-            // dword stores per lane
-#pragma unroll
-            for (int reg = 0; reg < 16; ++reg)
-                sDY[(jb * 32 + acc_row(reg, l)) * DIN + kb * 32 + (l & 31)] = da[reg];
-        }
-        lds_barrier();
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const int rr = rs + 16 * k;
-            if (rr < nv)
-                st4(dagg_out + (row0 + rr) * DIN + 4 * c4,
-                    *reinterpret_cast<const float4 *>(sDY + rr * DIN + 4 * c4));
-        }
-        if (tile == blockIdx.x) SCGIB_MARK(3);
-        if (more) {
-            lds_barrier();  // every read of this tile's r / agg / dz1 done
-#pragma unroll
-            for (int t = 0; t < 4; ++t)
-#pragma unroll
-                for (int k = 0; k < 4; ++k)
-                    *reinterpret_cast<float4 *>(dsts[t] + (rs + 16 * k) * 64 + 4 * c4) = nx[t][k];
-            lds_barrier();
-        }
-    }
-    // per-workgroup slab: dW2 | dW1 | db2 | db1 (gin_bwd_k layout)
-    float *sl = slab + static_cast<int64_t>(blockIdx.x) * SLAB;
-#pragma unroll
-    for (int reg = 0; reg < 16; ++reg) {
-        const int j = wr * 32 + acc_row(reg, l), k = wc * 32 + (l & 31);
-        sl[j * 64 + k] = accW2[reg];
-    }
-    {
-        const int jb = w & 1, kb = w >> 1;
-#pragma unroll
-        for (int reg = 0; reg < 16; ++reg) {
-            const int j = jb * 32 + acc_row(reg, l), kk = kb * 32 + (l & 31);
-            sl[64 * 64 + j * DIN + kk] = accW1[reg];
-        }
-    }
-    // bias gradients: lane l < 32 of the owning waves holds its column's two
-    // row halves (kk = 0 here, kk = 1 in lane l + 32)
-    db2 += __shfl_xor(db2, 32, kWave);
-    db1 += __shfl_xor(db1, 32, kWave);
-    if (wc == 0 && l < 32) sl[64 * 64 + 64 * DIN + wr * 32 + l] = db2;
-    if ((w >> 1) == 0 && l < 32) sl[64 * 64 + 64 * DIN + 64 + (w & 1) * 32 + l] = db1;
-    SCGIB_MARK(4);
-}
-
 // ---------------------------------------------------------------------------
 // gin_bwd5_k: the GIN layer backward (BN, d_in = 64) on 32-row sub-tiles,
 // TWO workgroups per CU (63 KB LDS, <= 256 VGPRs).
 //
-// gin_bwd2_k walks 64-row tiles, one workgroup per CU, ~1.7 tiles per CU at
-// QM9 B512 (437 ego tiles on 256 CUs): its per-tile phases (dz2, dz1 mask,
-// d(agg) stores, barrier waits) leave the matrix pipe idle ~40 % of a tile and
-// its dword operand reads (2 ds_read_b32 per MFMA at one wave per SIMD) run
-// the GEMMs at ~80 % of the MFMA rate (phase trace r02).  Here:
+// (Round 2 replaced gin_bwd2_k with it: 64-row tiles at one workgroup per
+// CU, ~1.7 tiles per CU at QM9 B512, whose per-tile phases left the matrix
+// pipe idle ~40 % of a tile and whose dword operand reads ran the GEMMs at
+// ~80 % of the MFMA rate; phase trace r02.)  Here:
 //   * 32-row sub-tiles, two workgroups per CU: one workgroup's non-MFMA
 //     phases run under the other's MFMAs; ~3.4 sub-tiles per CU balance
 //     better than 1.7 tiles;
@@ -1819,381 +1556,14 @@ __global__ __launch_bounds__(256, 2) void gin_bwd5_k(
     SCGIB_MARK(6);
 }
 
-// ---------------------------------------------------------------------------
-// gin_bwdf_k: layer l's backward (gin_bwd5_k's sub-tile body) fused with
-// layer l-1's backward statistics (gin_bwd_stats_k) on component-aligned
-// chunks, so d(agg) of layer l never leaves LDS and the statistics launch of
-// every layer but the last disappears.
-//
-// Chunk c = the components (molecules, ego-nets) whose first row lies in
-// [64 c, 64 c + 64): rows [cptr[c], cptr[c+1]).  The transposed aggregation
-//   dh_{l-1}(v) = (1+eps_l) d(agg_l)(v) + sum_{v->u} d(agg_l)(u)
-// only reads rows u of v's own component (edges stay inside their graph,
-// checked on the host), i.e. rows of the same chunk, whose d(agg) this
-// workgroup has just computed.  With components of <= kChunkComp rows a chunk
-// holds <= 96 rows: up to three 32-row sub-tiles, d(agg) staged in a
-// [96][64] LDS image that replaces gin_bwd5_k's staging buffer (79 KB LDS:
-// two workgroups per CU).  One workgroup per chunk; chunk c's sums
-// (sum dy, sum dy xhat) of layer l-1 are tile c's of the statistics kernel,
-// so the BN-backward hierarchy, its deferral and its consumer are unchanged.
-// Per-row arithmetic is gin_bwd5_k's and gin_bwd_stats_k's (fp32; the
-// neighbour sum in CSR order).
-// ---------------------------------------------------------------------------
-constexpr int kChunkRows = 96;
-constexpr int kChunkComp = 33;   // max component rows for kChunkRows
-// build-time A/B knob: fetch the statistics phase's row ranges, BN record,
-// first neighbour round and z2 rows during the sub-tile loop (1) or at the
-// phase (0)
-#ifndef SCGIB_BWDF_PREFETCH
-#define SCGIB_BWDF_PREFETCH 0
-#endif
-constexpr bool kBwdfPf = SCGIB_BWDF_PREFETCH != 0;
-#ifndef SCGIB_BWDF_FOLD_WG
-#define SCGIB_BWDF_FOLD_WG 64
-#endif
-constexpr int kBwdfFoldWG = SCGIB_BWDF_FOLD_WG;
-#ifndef SCGIB_BWDF_SLAB_LAST
-#define SCGIB_BWDF_SLAB_LAST 1
-#endif
-constexpr bool kBwdfSlabLast = SCGIB_BWDF_SLAB_LAST != 0;
-
-// cptr[c] = min(first row of a component >= 64 c, n) for c in [0, nchunk]
-// (one thread per component start; each chunk boundary written once)
-__global__ __launch_bounds__(256) void gin_chunk_bounds_k(
-    const int32_t *__restrict__ gptr, int64_t nseg, const int32_t *__restrict__ seg_dims,
-    int64_t ncap, const int32_t *__restrict__ dims, int32_t *__restrict__ cptr, int64_t nchunk) {
-    const int64_t m = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
-    const int64_t ns = eff_count(seg_dims, 0, nseg), n = eff_count(dims, 0, ncap);
-    if (m > ns) return;
-    const int64_t s = m < ns ? gptr[m] : n;
-    const int64_t p = m > 0 ? gptr[m - 1] : -1;
-    const int64_t lo = (p + TM) / TM, hi = m < ns ? (s / TM < nchunk ? s / TM : nchunk) : nchunk;
-    for (int64_t c = lo; c <= hi; ++c) cptr[c] = static_cast<int32_t>(s);
-}
-
-template <int DIN>
-__global__ __launch_bounds__(256, 2) void gin_bwdf_k(
-    const float *__restrict__ dy, const float *__restrict__ z2, const float *__restrict__ r,
-    const float *__restrict__ agg, const float *__restrict__ stat,
-    const float *__restrict__ coef, const float *__restrict__ w1, const float *__restrict__ w2,
-    int64_t ncap, const int32_t *__restrict__ cptr, const int32_t *__restrict__ rowptr_t,
-    const int32_t *__restrict__ col_t, float ope, const float *__restrict__ z2p,
-    const float *__restrict__ statp, float *__restrict__ dyp_out, float *__restrict__ part,
-    BnBwdFuse bz, float *__restrict__ slab, const int32_t *__restrict__ dims,
-    scgib_bn_bwd_pending pend, scgib_slab_job fold) {
-    static_assert(DIN == 64 && SM == 32 && kChunkRows == 3 * SM, "64-wide rows, 3 sub-tiles");
-    constexpr int SLAB = 64 * 64 + 64 * DIN + 128;
-    constexpr int KR = kChunkRows / 16;  // rows per thread in the statistics phase
-    __shared__ __attribute__((aligned(16))) float sD[SM * LDR];   // dz2 [row][k]
-    __shared__ __attribute__((aligned(16))) float sDT[64 * LDT];  // dz2 [col][row]
-    __shared__ __attribute__((aligned(16))) float sE[SM * LDR];   // dz1
-    __shared__ __attribute__((aligned(16))) float sET[64 * LDT];
-    __shared__ __attribute__((aligned(16))) float sRT[64 * LDT];  // r [col][row]
-    __shared__ __attribute__((aligned(16))) float sAT[DIN * LDT]; // agg [col][row]
-    __shared__ __attribute__((aligned(16))) float sA[kChunkRows * 64];  // d(agg) of the chunk
-    __shared__ float sCoef[128];
-    __shared__ int32_t sRp[kChunkRows + 1];  // rowptr_t of the chunk's rows
-    __shared__ __attribute__((aligned(16))) float sStp[256];  // layer l-1's BN record
-    const int64_t n = eff_count(dims, 0, ncap);
-    const int tid = threadIdx.x, l = tid & 63, w = tid >> 6;
-    const int kk = l >> 5, li = l & 31;
-    const bool nw = w < 2;
-    const int q = w & 1;
-    const int c = l;
-    const int64_t last = ncap - 1;
-    // the folded reduce of the previous layer's slabs: at most kBwdfFoldWG
-    // workgroups past the chunk grid, each looping over column blocks, so they
-    // fit the workgroup slots the chunk grid leaves free (block-uniform)
-    const int64_t nchunk = (ncap + TM - 1) / TM;
-    if (static_cast<int64_t>(blockIdx.x) >= nchunk) {
-        const int nb = slab_fold_blocks(fold), nwg = gridDim.x - static_cast<int>(nchunk);
-        for (int b = static_cast<int>(blockIdx.x - nchunk); b < nb; b += nwg) {
-            slab_fold_block(fold, b, sD);
-            __syncthreads();  // sD reused by the next column block
-        }
-        return;
-    }
-    const int64_t chunk = blockIdx.x;
-    SCGIB_MARK(0);
-    SCGIB_MARK_HWID();
-    BwdFin bfin;
-    const int pend_ngr = static_cast<int>(((n + TM - 1) / TM + kGroup - 1) / kGroup);
-    if (pend.gpart) bn_bwd_fin_load<false>(pend.gpart, pend_ngr, 0, bfin);
-    const int64_t a = cptr[chunk];
-    const int rows = static_cast<int>(cptr[chunk + 1] - a);  // block-uniform, <= kChunkRows
-    // statistics phase: thread = row slot rs + 16 k, float4 column c4; with
-    // kBwdfPf its row ranges (-> sRp) and BN record (-> sStp) are fetched here
-    const int c4 = tid & 15, rs = tid >> 4;
-    const int32_t rp_v = kBwdfPf && tid <= rows && rows > 0 ? rowptr_t[a + tid] : 0;
-    const float stp_v = kBwdfPf ? statp[tid] : 0.f;
-    const float s_mean = stat[c], s_istd = stat[64 + c], s_sc = stat[128 + c];
-    float c1 = 0.f, c2 = 0.f;
-    if (!pend.gpart) {
-        c1 = coef[c];
-        c2 = coef[64 + c];
-    }
-    float wreg[32];
-    {
-        const float *wm = nw ? w2 : w1;
-#pragma unroll
-        for (int s = 0; s < 32; ++s) wreg[s] = wm[kperm(s, kk) * 64 + q * 32 + li];
-    }
-    float nx[4][8];
-    auto load_sub = [&](int j) {
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            int64_t row = a + j * SM + 8 * w + i;
-            row = row < last ? row : last;
-            nx[2][i] = r[row * 64 + c];
-        }
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            int64_t row = a + j * SM + 8 * w + i;
-            row = row < last ? row : last;
-            nx[3][i] = agg[row * DIN + c];
-        }
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            int64_t row = a + j * SM + 8 * w + i;
-            row = row < last ? row : last;
-            nx[0][i] = dy[row * 64 + c];
-            nx[1][i] = z2[row * 64 + c];
-        }
-    };
-    auto put_t = [&](float *img, int x) {
-        float4 *p = reinterpret_cast<float4 *>(img + c * LDT + 8 * w);
-        p[0] = make_float4(nx[x][0], nx[x][1], nx[x][2], nx[x][3]);
-        p[1] = make_float4(nx[x][4], nx[x][5], nx[x][6], nx[x][7]);
-    };
-    const int nsub = (rows + SM - 1) / SM;
-    if (nsub > 0) load_sub(0);
-    if (pend.gpart) {
-        const double tot = bn_bwd_final<false>(pend.gpart, pend_ngr, bfin);
-        const int cs = bfin_index();
-        const bool lead = (tid & 63) < 32, w0 = chunk == 0 && lead;
-        const float cf = bn_bwd_publish(cs, tot, n, pend.training, w0 ? pend.dgamma : nullptr,
-                                        w0 ? pend.dbeta : nullptr, nullptr);
-        if (lead) sCoef[cs] = cf;
-    }
-    if (nsub > 0) {
-        put_t(sRT, 2);
-        put_t(sAT, 3);
-    }
-    vm_wait_all();
-    if (kBwdfPf) {
-        if (tid <= rows) sRp[tid] = rp_v;
-        sStp[tid] = stp_v;
-    }
-    __syncthreads();
-    if (pend.gpart) {
-        c1 = sCoef[c];
-        c2 = sCoef[64 + c];
-    }
-    const float k1 = s_istd * c2;
-    SCGIB_MARK(1);
-    // kBwdfPf: the statistics phase's z2 rows and first neighbour round,
-    // loaded during the last sub-tile; the neighbour ids go to the registers
-    // of the (then unused) row prefetch nx[0..2] as int bits: row k, slot t at
-    // nx[(4k+t)/8][(4k+t)%8]
-    float4 zp[KR];
-    auto load_stats = [&]() {
-#pragma unroll
-        for (int k = 0; k < KR; ++k) {
-            const int rr = rs + 16 * k;
-            zp[k] = ld4(z2p + (a + (rr < rows ? rr : rows - 1)) * 64 + 4 * c4);
-        }
-#pragma unroll
-        for (int k = 0; k < KR; ++k) {
-            const int rr = rs + 16 * k < rows ? rs + 16 * k : rows;
-            const int32_t b = sRp[rr], e1 = sRp[rs + 16 * k < rows ? rr + 1 : rows];
-#pragma unroll
-            for (int t = 0; t < 4; ++t) {
-                const int32_t e = b + t;
-                nx[(4 * k + t) >> 3][(4 * k + t) & 7] = e < e1 ? __int_as_float(col_t[e]) : 0.f;
-            }
-        }
-    };
-    f32x16 accA = zero16(), accB = zero16();
-    float dbias = 0.f;
-    for (int j = 0; j < nsub; ++j) {
-        const int nv = rows - j * SM < SM ? rows - j * SM : SM;
-        {
-            float d[8];
-#pragma unroll
-            for (int i = 0; i < 8; ++i) {
-                const float v = s_sc * (nx[0][i] - c1 - (nx[1][i] - s_mean) * k1);
-                d[i] = 8 * w + i < nv ? v : 0.f;
-                sD[(8 * w + i) * LDR + c] = d[i];
-            }
-            float4 *p = reinterpret_cast<float4 *>(sDT + c * LDT + 8 * w);
-            p[0] = make_float4(d[0], d[1], d[2], d[3]);
-            p[1] = make_float4(d[4], d[5], d[6], d[7]);
-        }
-        const bool more = j + 1 < nsub;  // block-uniform
-        if (more) load_sub(j + 1);
-        else if (kBwdfPf) load_stats();
-        lds_barrier();
-        if (j == 0) SCGIB_MARK(2);
-        if (nw) {
-            const f32x16 dr = mma_rk4<8>(sD + li * LDR + 4 * kk, wreg, zero16());
-#pragma unroll
-            for (int reg = 0; reg < 16; ++reg) {
-                const int row = acc_row(reg, l), col = q * 32 + li;
-                const float v = dr[reg] * (sRT[col * LDT + row] > 0.f ? 1.f : 0.f);
-                sE[row * LDR + col] = v;
-                sET[col * LDT + row] = v;
-            }
-        } else {
-            mma_kk4x2<4>(sDT + (q * 32 + li) * LDT + 4 * kk, sRT + li * LDT + 4 * kk,
-                         sRT + (32 + li) * LDT + 4 * kk, accA, accB, dbias);
-        }
-        lds_barrier();
-        if (j == 0) SCGIB_MARK(3);
-        if (more) put_t(sRT, 2);
-        if (nw) {
-            mma_kk4x2<4>(sET + (q * 32 + li) * LDT + 4 * kk, sAT + li * LDT + 4 * kk,
-                         sAT + (32 + li) * LDT + 4 * kk, accA, accB, dbias);
-        } else {   // d(agg) block q of sub-tile j -> the chunk image (rows past nv are 0)
-            const f32x16 da = mma_rk4<8>(sE + li * LDR + 4 * kk, wreg, zero16());
-            float *dst = sA + (j * SM) * 64 + q * 32 + li;
-#pragma unroll
-            for (int reg = 0; reg < 16; ++reg) dst[acc_row(reg, l) * 64] = da[reg];
-        }
-        lds_barrier();
-        if (j == 0) SCGIB_MARK(4);
-        if (more) put_t(sAT, 3);
-    }
-    SCGIB_MARK(5);
-    // ---- layer l-1's statistics: dh = ope d(agg)(v) + sum_{v->u} d(agg)(u),
-    // dy_{l-1} = dh [scale z2 + shift > 0] (the neighbour sum in CSR order)
-    const float4 *st4p = reinterpret_cast<const float4 *>(kBwdfPf ? sStp : statp);
-    const float4 pmean = st4p[c4], pistd = st4p[16 + c4], psc = st4p[32 + c4], psh = st4p[48 + c4];
-    float4 sdy = make_float4(0.f, 0.f, 0.f, 0.f), sdx = sdy;
-    if (rows > 0) {  // block-uniform
-        float4 g[KR];
-        int32_t beg[KR], end[KR], u0[KR][4];
-        if constexpr (kBwdfPf) {
-#pragma unroll
-            for (int k = 0; k < KR; ++k) {
-                const int rr = rs + 16 * k;
-                beg[k] = sRp[rr < rows ? rr : rows];
-                end[k] = sRp[rr < rows ? rr + 1 : rows];
-#pragma unroll
-                for (int t = 0; t < 4; ++t) u0[k][t] = __float_as_int(nx[(4 * k + t) >> 3][(4 * k + t) & 7]);
-            }
-        } else {
-#pragma unroll
-            for (int k = 0; k < KR; ++k) {
-                const int rr = rs + 16 * k;
-                const int64_t v = a + (rr < rows ? rr : rows - 1);
-                beg[k] = rowptr_t[v];
-                end[k] = rowptr_t[v + 1];
-            }
-#pragma unroll
-            for (int k = 0; k < KR; ++k) {
-                const int rr = rs + 16 * k;
-                zp[k] = ld4(z2p + (a + (rr < rows ? rr : rows - 1)) * 64 + 4 * c4);
-                if (rr >= rows) end[k] = beg[k];
-            }
-        }
-        int maxdeg = 0;
-#pragma unroll
-        for (int k = 0; k < KR; ++k) {
-            const int rr = rs + 16 * k;
-            maxdeg = end[k] - beg[k] > maxdeg ? end[k] - beg[k] : maxdeg;
-            const int sr = rr < rows ? rr : 0;
-            const float4 x = *reinterpret_cast<const float4 *>(sA + sr * 64 + 4 * c4);
-            g[k] = make_float4(ope * x.x, ope * x.y, ope * x.z, ope * x.w);
-        }
-        for (int j0 = 0; j0 < maxdeg; j0 += 4) {
-            if (j0 > 0 || !kBwdfPf) {  // (kBwdfPf: rows of degree > 4) a neighbour round
-#pragma unroll
-                for (int k = 0; k < KR; ++k)
-#pragma unroll
-                    for (int t = 0; t < 4; ++t) {
-                        const int32_t e = beg[k] + j0 + t;
-                        u0[k][t] = col_t[e < end[k] ? e : 0];
-                    }
-            }
-#pragma unroll
-            for (int k = 0; k < KR; ++k)
-#pragma unroll
-                for (int t = 0; t < 4; ++t) {
-                    int64_t sl = static_cast<int64_t>(u0[k][t]) - a;  // in-chunk (host-checked)
-                    sl = sl < 0 ? 0 : (sl < rows ? sl : rows - 1);
-                    const float4 x = *reinterpret_cast<const float4 *>(sA + sl * 64 + 4 * c4);
-                    if (beg[k] + j0 + t < end[k]) g[k] = add4(g[k], x);
-                }
-        }
-#pragma unroll
-        for (int k = 0; k < KR; ++k) {
-            const int rr = rs + 16 * k;
-            const float valid = rr < rows ? 1.f : 0.f;
-            const float4 zz = zp[k], gg = g[k];
-            const float4 d = make_float4((psc.x * zz.x + psh.x > 0.f ? gg.x : 0.f) * valid,
-                                         (psc.y * zz.y + psh.y > 0.f ? gg.y : 0.f) * valid,
-                                         (psc.z * zz.z + psh.z > 0.f ? gg.z : 0.f) * valid,
-                                         (psc.w * zz.w + psh.w > 0.f ? gg.w : 0.f) * valid);
-            if (rr < rows) st4(dyp_out + (a + rr) * 64 + 4 * c4, d);
-            sdy = add4(sdy, d);
-            sdx = add4(sdx, make_float4(d.x * (zz.x - pmean.x) * pistd.x, d.y * (zz.y - pmean.y) * pistd.y,
-                                        d.z * (zz.z - pmean.z) * pistd.z, d.w * (zz.w - pmean.w) * pistd.w));
-        }
-    }
-    {   // capacity mode: this chunk's share of the padding rows [n, ncap)
-        const int64_t p0 = chunk * TM > n ? chunk * TM : n;
-        const int64_t p1 = chunk * TM + TM < ncap ? chunk * TM + TM : ncap;
-        for (int64_t i = p0 * 16 + tid; i < p1 * 16; i += 256)
-            st4(dyp_out + i * 4, make_float4(0.f, 0.f, 0.f, 0.f));
-    }
-    // per-workgroup slab: dW2 | dW1 | db2 | db1 (gin_bwd_k layout), written
-    // after the statistics hierarchy (its arrival waits for every store)
-    auto write_slab = [&]() {
-        float *sl = slab + chunk * SLAB;
-        float *dw = nw ? sl + 64 * 64 : sl;
-        const int ld = nw ? DIN : 64;
-#pragma unroll
-        for (int reg = 0; reg < 16; ++reg) {
-            const int jr = q * 32 + acc_row(reg, l);
-            dw[jr * ld + li] = accA[reg];
-            dw[jr * ld + 32 + li] = accB[reg];
-        }
-        const float db = dbias + __shfl_xor(dbias, 32, kWave);
-        if (l < 32) sl[64 * 64 + 64 * DIN + (nw ? 64 : 0) + q * 32 + l] = db;
-    };
-    const int64_t nt = (n + TM - 1) / TM;
-    if (!kBwdfSlabLast || chunk >= nt) write_slab();
-    if (chunk >= nt) return;  // a chunk of padding rows only (block-uniform)
-    float *red = sDT;  // [2][16][64]: sDT's last reader passed the loop's barriers
-    {
-        float *x = red + rs * 64 + 4 * c4;
-        x[0] = sdy.x; x[1] = sdy.y; x[2] = sdy.z; x[3] = sdy.w;
-        float *y = red + (16 + rs) * 64 + 4 * c4;
-        y[0] = sdx.x; y[1] = sdx.y; y[2] = sdx.z; y[3] = sdx.w;
-    }
-    __syncthreads();
-    if (tid < 128) {
-        const int which = tid >> 6, ch = tid & 63;
-        float s = 0.f;
-        for (int k = 0; k < 16; ++k) s += red[(which * 16 + k) * 64 + ch];
-        st_agent(part + chunk * 128 + which * 64 + ch, s);
-    }
-    SCGIB_MARK(6);
-    bn_bwd_hier_s(part, n, chunk, bz, reinterpret_cast<double (*)[128]>(sD));
-    if (kBwdfSlabLast) write_slab();
-    SCGIB_MARK(7);
-}
-
 // up to two workgroups per CU (66.5 KB LDS each): one tile per workgroup for
-// batches up to SCGIB_BWD_GRID_CAP tiles (build-time knob), so every tile of
+// batches up to kBwdGridCap tiles, so every tile of
 // an encoder layer runs at once; larger batches loop over tiles
 constexpr int kCUs = 256;  // MI355X: 8 XCDs x 32 CUs
 
-#ifndef SCGIB_BWD_GRID_CAP
-#define SCGIB_BWD_GRID_CAP 512
-#endif
+constexpr int64_t kBwdGridCap = 512;
 static int bwd_grid(int64_t ntiles) {
-    return static_cast<int>(ntiles < SCGIB_BWD_GRID_CAP ? ntiles : SCGIB_BWD_GRID_CAP);
+    return static_cast<int>(ntiles < kBwdGridCap ? ntiles : kBwdGridCap);
 }
 
 }  // namespace scgib
@@ -2210,23 +1580,12 @@ extern "C" int scgib_trace_set(void *buf) {
 #endif
 
 // scgib_gin_layer_bwd: d_in = 32 runs gin_bwd_k (one workgroup per tile up
-// to the cap); d_in = 64 the variant SCGIB_BWD_V (build-time A/B knob):
-// 5 = gin_bwd5_k (default), 2 = gin_bwd2_k (64-row tiles, one workgroup per
-// CU).  gin_bwd5_k takes the fewest workgroups that reach the largest
-// per-workgroup count: the same finish time as the full two-per-CU grid,
-// fewer slabs.
-#ifndef SCGIB_BWD_V
-#define SCGIB_BWD_V 5
-#endif
-static constexpr bool kBwd5 = SCGIB_BWD_V == 5;
-static constexpr bool kBwd2 = SCGIB_BWD_V == 2;
-
+// to the cap); d_in = 64 gin_bwd5_k, on the fewest workgroups that reach the
+// largest per-workgroup count at one workgroup per CU: the same finish time
+// as the full two-per-CU grid (measured), half the slabs.
 static int64_t bwd5_subtiles(int64_t n_nodes) { return (n_nodes + SM - 1) / SM; }
-#ifndef SCGIB_BWD5_SLOTS
-#define SCGIB_BWD5_SLOTS 1  // workgroups per CU the grid is sized for (2: same isolated time, 1.8x the slabs)
-#endif
 static int bwd5_grid(int64_t nsub) {
-    constexpr int64_t slots = SCGIB_BWD5_SLOTS * kCUs;
+    constexpr int64_t slots = kCUs;
     const int64_t per = (nsub + slots - 1) / slots;
     return static_cast<int>((nsub + per - 1) / per);
 }
@@ -2234,8 +1593,7 @@ static int bwd5_grid(int64_t nsub) {
 extern "C" int64_t scgib_gin_layer_bwd_slabs(int64_t n_nodes, int32_t d_in) {
     if (n_nodes <= 0) return 0;
     const int64_t nt = scgib_gin_tiles(n_nodes);
-    if (d_in == 64 && kBwd5) return bwd5_grid(bwd5_subtiles(n_nodes));
-    if (d_in == 64 && kBwd2) return nt < kCUs ? nt : kCUs;
+    if (d_in == 64) return bwd5_grid(bwd5_subtiles(n_nodes));
     return bwd_grid(nt);
 }
 
@@ -2552,64 +1910,13 @@ extern "C" int scgib_gin_layer_bwd(const float *dy, const float *z2, const float
     hipStream_t st = as_stream(stream);
     if (d_in == 32)
         gin_bwd_k<32><<<grid, 256, 0, st>>>(dy, z2, r, agg, stat, coef, w1, w2, n_nodes, nt, dagg, slab, dims, nullptr, pd, ReconArgs{});
-    else if (kBwd5)
-        gin_bwd5_k<64><<<grid, 256, 0, st>>>(dy, z2, r, agg, stat, coef, w1, w2, n_nodes, bwd5_subtiles(n_nodes), dagg, slab, dims, pd);
-    else if (kBwd2)
-        gin_bwd2_k<64><<<grid, 256, 0, st>>>(dy, z2, r, agg, stat, coef, w1, w2, n_nodes, nt, dagg, slab, dims, pd);
     else
-        gin_bwd_k<64><<<grid, 256, 0, st>>>(dy, z2, r, agg, stat, coef, w1, w2, n_nodes, nt, dagg, slab, dims, nullptr, pd, ReconArgs{});
+        gin_bwd5_k<64><<<grid, 256, 0, st>>>(dy, z2, r, agg, stat, coef, w1, w2, n_nodes, bwd5_subtiles(n_nodes), dagg, slab, dims, pd);
     const int rc = launch_status();
     if (rc != SCGIB_OK || !wgrad) return rc;  // wgrad NULL: the caller reduces the slabs
     return launch_slab_reduce(slab, grid, 64 * 64 + 64 * static_cast<int64_t>(d_in) + 128, wgrad, st);
 }
 
-// ---- fused layer backward + previous layer's statistics (gin_bwdf_k) ----
-extern "C" int32_t scgib_gin_chunk_max_component() { return kChunkComp; }
-extern "C" int64_t scgib_gin_chunks(int64_t n_nodes) { return scgib_gin_tiles(n_nodes); }
-
-extern "C" int scgib_gin_chunk_bounds(const int32_t *graph_ptr, int64_t n_seg,
-                                      const int32_t *seg_dims, int64_t n_nodes,
-                                      const int32_t *dims, int32_t *chunk_ptr,
-                                      scgib_stream_t stream) {
-    if (n_seg < 0 || n_nodes <= 0 || !chunk_ptr || (n_seg > 0 && !graph_ptr)) return SCGIB_EINVAL;
-    const int64_t nchunk = scgib_gin_chunks(n_nodes);
-    gin_chunk_bounds_k<<<dim3(static_cast<unsigned>((n_seg + 1 + 255) / 256)), 256, 0,
-                         as_stream(stream)>>>(graph_ptr, n_seg, seg_dims, n_nodes, dims,
-                                              chunk_ptr, nchunk);
-    return launch_status();
-}
-
-extern "C" int scgib_gin_layer_bwd_fused(
-    const float *dy, const float *z2, const float *r, const float *agg, const float *stat,
-    const float *coef, const float *w1, const float *w2, int64_t n_nodes, const int32_t *chunk_ptr,
-    const int32_t *rowptr_t, const int32_t *col_t, float one_plus_eps, const float *z2_prev,
-    const float *stat_prev, int32_t training, float *dy_prev, float *dgamma_prev,
-    float *dbeta_prev, float *coef_prev, float *bn_ws_prev, uint32_t *counters, int32_t defer,
-    float *slab, const int32_t *dims, const scgib_bn_bwd_pending *pending,
-    const scgib_slab_job *fold, scgib_stream_t stream) {
-    if (!fold_ok(fold)) return SCGIB_EINVAL;
-    if (n_nodes <= 0 || !dy || !z2 || !r || !agg || !stat || (!coef && !pending) || !w1 || !w2 ||
-        !chunk_ptr || !rowptr_t || !col_t || !z2_prev || !stat_prev || !dy_prev || !bn_ws_prev ||
-        !counters || !slab)
-        return SCGIB_EINVAL;
-    if (pending && (!pending->gpart || !pending->dgamma || !pending->dbeta)) return SCGIB_EINVAL;
-    if (!defer && (!dgamma_prev || !dbeta_prev || !coef_prev)) return SCGIB_EINVAL;
-    const scgib_bn_bwd_pending pd = pending ? *pending : scgib_bn_bwd_pending{};
-    BnBwdFuse bz{counters, bn_gpart(bn_ws_prev, n_nodes), dgamma_prev, dbeta_prev, coef_prev,
-                 training, static_cast<int>(bn_groups(n_nodes)), defer ? 1 : 0};
-    const scgib_slab_job fj = fold ? *fold : scgib_slab_job{};
-    const int nfb = slab_fold_blocks(fj);
-    const int64_t grid = scgib_gin_chunks(n_nodes) + (nfb < kBwdfFoldWG ? nfb : kBwdfFoldWG);
-    gin_bwdf_k<64><<<dim3(static_cast<unsigned>(grid)), 256, 0, as_stream(stream)>>>(
-        dy, z2, r, agg, stat, coef, w1, w2, n_nodes, chunk_ptr, rowptr_t, col_t, one_plus_eps,
-        z2_prev, stat_prev, dy_prev, bn_ws_prev, bz, slab, dims, pd, fj);
-    return launch_status();
-}
-
-// ---------------------------------------------------------------------------
-// Dense two-layer MLP of the head: the same tile kernels without the gather
-// and without BatchNorm (models.py:1055-1057, applied at :1174).
-// ---------------------------------------------------------------------------
 extern "C" int64_t scgib_mlp2_slab_floats(int64_t n_nodes, int32_t d_in) {
     return static_cast<int64_t>(bwd_grid(scgib_gin_tiles(n_nodes))) * (64 * 64 + 64 * d_in + 128);
 }

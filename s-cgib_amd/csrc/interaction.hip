@@ -135,11 +135,9 @@ __device__ __forceinline__ float4 noise_feat(const NoiseGen &ng, int64_t r, int 
 
 
 // one thread per (row, channel quad); 256 threads = 16 rows per workgroup per
-// pass, grid-stride over at most SCGIB_NOISE_WG workgroups: the kernel runs
+// pass, grid-stride over at most kNoiseWG workgroups: the kernel runs
 // beside Encoder2's last layer, so it should hold few CU slots
-#ifndef SCGIB_NOISE_WG
-#define SCGIB_NOISE_WG 64
-#endif
+constexpr int kNoiseWG = 64;
 __global__ __launch_bounds__(256) void noise_uniform_k(float *__restrict__ u_gate,
                                                        float *__restrict__ u_feat, int64_t n,
                                                        uint64_t *__restrict__ rng,
@@ -406,98 +404,6 @@ __device__ __forceinline__ void horner4(D4 &a, double keep, double m, float4 v, 
     a.w = keep * a.w + m * (static_cast<double>(v.w) * scale);
 }
 
-// The same closed form over up to kRuMaxWG workgroups of 16 partitions x 16
-// float4 lanes (one load round per partition: <= 2 graphs each at B = 512),
-// each workgroup chaining its partitions into one fp64 partial; the last
-// workgroup to arrive chains the workgroups' partials in order and applies
-// the decay of r_0.  A few microseconds inline on the loss chain, where the
-// one-workgroup form needs its own stream (and the fork / join around it).
-constexpr int kRuMaxWG = 16;
-
-__device__ __forceinline__ double dpow(double b, int64_t e) {  // e >= 0, binary powering
-    double r = 1.0;
-    while (e > 0) {
-        if (e & 1) r *= b;
-        b *= b;
-        e >>= 1;
-    }
-    return r;
-}
-
-__global__ __launch_bounds__(256) void bn_running_update_multi_k(
-    const float *__restrict__ stats, const int32_t *__restrict__ gptr, int64_t B, float momentum,
-    float *__restrict__ rm, float *__restrict__ rv, int64_t *__restrict__ nbt,
-    double *__restrict__ partials, unsigned *__restrict__ counter) {
-    const int c4 = threadIdx.x & 15, part = threadIdx.x >> 4;
-    const int G = gridDim.x, wg = blockIdx.x;
-    const double m = momentum, keep = 1.0 - static_cast<double>(momentum);
-    const int64_t chunk = (B + 16 * G - 1) / (16 * G);
-    auto range = [&](int64_t q) {  // graphs of global partition q
-        const int64_t a = q * chunk < B ? q * chunk : B, b = a + chunk < B ? a + chunk : B;
-        return b - a;
-    };
-    const int64_t q = static_cast<int64_t>(wg) * 16 + part;
-    const int64_t i0 = q * chunk < B ? q * chunk : B, len = range(q);
-    D4 am{0.0, 0.0, 0.0, 0.0}, av{0.0, 0.0, 0.0, 0.0};
-    for (int64_t ib = 0; ib < len; ib += kRuRound) {
-        float4 xm[kRuRound], xs[kRuRound];
-        int32_t g0[kRuRound], g1[kRuRound];
-#pragma unroll
-        for (int u = 0; u < kRuRound; ++u) {
-            const int64_t i = i0 + (ib + u < len ? ib + u : len - 1);  // clamped: unconditional loads
-            const float *sl = stats + i * SCGIB_STATS_STRIDE;
-            xm[u] = ld4(sl + kStMeanT + 4 * c4);
-            xs[u] = ld4(sl + kStSsqT + 4 * c4);
-            g0[u] = gptr[i];
-            g1[u] = gptr[i + 1];
-        }
-#pragma unroll
-        for (int u = 0; u < kRuRound; ++u) {
-            if (ib + u < len) {
-                horner4(am, keep, m, xm[u], 1.f);
-                const double inv = 1.0 / static_cast<double>(g1[u] - g0[u] - 1);
-                av.x = keep * av.x + m * (static_cast<double>(xs[u].x) * inv);
-                av.y = keep * av.y + m * (static_cast<double>(xs[u].y) * inv);
-                av.z = keep * av.z + m * (static_cast<double>(xs[u].z) * inv);
-                av.w = keep * av.w + m * (static_cast<double>(xs[u].w) * inv);
-            }
-        }
-    }
-    __shared__ double pm[16][65], pv[16][65];
-    __shared__ double sPow[17];  // keep^len of this workgroup's 16 partitions, and of the workgroup
-    pm[part][4 * c4] = am.x; pm[part][4 * c4 + 1] = am.y; pm[part][4 * c4 + 2] = am.z; pm[part][4 * c4 + 3] = am.w;
-    pv[part][4 * c4] = av.x; pv[part][4 * c4 + 1] = av.y; pv[part][4 * c4 + 2] = av.z; pv[part][4 * c4 + 3] = av.w;
-    if (threadIdx.x < 16) sPow[threadIdx.x] = dpow(keep, range(static_cast<int64_t>(wg) * 16 + threadIdx.x));
-    __syncthreads();
-    if (threadIdx.x < 128) {  // chain the partitions in order: T = keep^len_p T + S_p
-        const int which = threadIdx.x >> 6, c = threadIdx.x & 63;
-        double t = 0.0;
-        for (int p = 0; p < 16; ++p) t = sPow[p] * t + (which ? pv[p][c] : pm[p][c]);
-        st_agent(partials + static_cast<int64_t>(wg) * 128 + threadIdx.x, t);
-    }
-    if (!block_arrive(counter, static_cast<unsigned>(G))) return;
-    if (threadIdx.x < 128) {  // the last workgroup: chain the workgroups, decay r_0
-        const int which = threadIdx.x >> 6, c = threadIdx.x & 63;
-        double v[kRuMaxWG];  // every partial's load in flight before the chain
-#pragma unroll
-        for (int w = 0; w < kRuMaxWG; ++w)
-            v[w] = ld_agent(partials + static_cast<int64_t>(w < G ? w : 0) * 128 + threadIdx.x);
-        double u = 0.0;
-#pragma unroll
-        for (int w = 0; w < kRuMaxWG; ++w) {
-            const int64_t a = 16 * w * chunk < B ? 16 * w * chunk : B;
-            const int64_t b = 16 * (w + 1) * chunk < B ? 16 * (w + 1) * chunk : B;
-            if (w < G) u = dpow(keep, b - a) * u + v[w];
-        }
-        const double kB = dpow(keep, B);
-        float *r = which ? rv : rm;
-        r[c] = static_cast<float>(kB * r[c] + u);
-        if (threadIdx.x == 0) {
-            if (nbt) *nbt += B;
-            *counter = 0u;
-        }
-    }
-}
 
 __global__ __launch_bounds__(1024) void bn_running_update_k(const float *__restrict__ stats,
                                                             const int32_t *__restrict__ gptr,
@@ -815,7 +721,7 @@ extern "C" int scgib_noise_uniform(float *u_gate, float *u_feat, int64_t n_rows,
     if (!u_gate || !u_feat || !rng_state || !counter) return SCGIB_EINVAL;
     if (n_rows > 0xffffffffLL) return SCGIB_EUNSUPPORTED;
     const int64_t wg = (n_rows + 15) / 16;
-    noise_uniform_k<<<dim3(static_cast<unsigned>(wg < SCGIB_NOISE_WG ? wg : SCGIB_NOISE_WG)), 256, 0,
+    noise_uniform_k<<<dim3(static_cast<unsigned>(wg < kNoiseWG ? wg : kNoiseWG)), 256, 0,
                       as_stream(stream)>>>(
         u_gate, u_feat, n_rows, rng_state, counter);
     return launch_status();
@@ -831,27 +737,6 @@ extern "C" int scgib_bn_running_update(const float *stats, const int32_t *graph_
     bn_running_update_k<<<1, 1024, 0, as_stream(stream)>>>(stats, graph_ptr, n_graphs, momentum,
                                                            running_mean, running_var,
                                                            num_batches_tracked);
-    return launch_status();
-}
-
-extern "C" int64_t scgib_bn_running_update_partials(int64_t n_graphs) {
-    return 128 * kRuMaxWG;  // doubles
-}
-
-extern "C" int scgib_bn_running_update_multi(const float *stats, const int32_t *graph_ptr,
-                                             int64_t n_graphs, float momentum,
-                                             float *running_mean, float *running_var,
-                                             int64_t *num_batches_tracked, double *partials,
-                                             uint32_t *counter, scgib_stream_t stream) {
-    if (n_graphs < 0) return SCGIB_EINVAL;
-    if (n_graphs == 0) return SCGIB_OK;
-    if (!stats || !graph_ptr || !running_mean || !running_var || !partials || !counter)
-        return SCGIB_EINVAL;
-    const int64_t g = (n_graphs + 31) / 32;
-    const unsigned grid = static_cast<unsigned>(g < kRuMaxWG ? g : kRuMaxWG);
-    bn_running_update_multi_k<<<grid, 256, 0, as_stream(stream)>>>(
-        stats, graph_ptr, n_graphs, momentum, running_mean, running_var, num_batches_tracked,
-        partials, reinterpret_cast<unsigned *>(counter));
     return launch_status();
 }
 

@@ -126,62 +126,3 @@ extern "C" int scgib_slab_reduce_multi_ex(const scgib_slab_job *jobs, int32_t n_
                                  scgib::as_stream(stream)>>>(t);
     return scgib::launch_status();
 }
-
-// ---------------------------------------------------------------------------
-// scgib_copy_words: up to kCopyRanges device-to-device copies of 4-byte words
-// in ONE launch (the bench's ego pipeline hands the next batch's ego-net
-// buffers and inputs over at the end of a captured step; one memcpy node per
-// tensor would cost a blit launch each).  Each workgroup takes 1024-word
-// blocks of the concatenated ranges; 16-byte vectors where both ends allow.
-// ---------------------------------------------------------------------------
-namespace scgib {
-constexpr int kCopyRanges = 8;
-struct CopyTable {
-    scgib_copy_range r[kCopyRanges];
-    int64_t blk0[kCopyRanges + 1];
-    int32_t n;
-};
-
-__global__ __launch_bounds__(256) void copy_words_k(const CopyTable t) {
-    const int64_t b = blockIdx.x;
-    int i = 0;
-    while (i + 1 < t.n && b >= t.blk0[i + 1]) ++i;  // <= 8 ranges: scalar scan
-    const scgib_copy_range R = t.r[i];
-    const int64_t w0 = (b - t.blk0[i]) * 1024, w1 = w0 + 1024 < R.words ? w0 + 1024 : R.words;
-    const uint32_t *src = static_cast<const uint32_t *>(R.src);
-    uint32_t *dst = static_cast<uint32_t *>(R.dst);
-    const bool vec = ((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst)) & 15) == 0;
-    if (vec && w1 - w0 == 1024) {
-        const int64_t q = w0 / 4 + threadIdx.x;
-        reinterpret_cast<uint4 *>(dst)[q] = reinterpret_cast<const uint4 *>(src)[q];
-    } else {
-        for (int64_t k = w0 + threadIdx.x; k < w1; k += 256) dst[k] = src[k];
-    }
-}
-}  // namespace scgib
-
-extern "C" int64_t scgib_copy_words_max_ranges(void) { return scgib::kCopyRanges; }
-
-extern "C" int scgib_copy_words(const scgib_copy_range *ranges, int32_t n_ranges,
-                                scgib_stream_t stream) {
-    if (n_ranges < 0 || n_ranges > scgib::kCopyRanges) return SCGIB_EINVAL;
-    if (n_ranges == 0) return SCGIB_OK;
-    if (!ranges) return SCGIB_EINVAL;
-    scgib::CopyTable t{};
-    int64_t blocks = 0;
-    for (int i = 0; i < n_ranges; ++i) {
-        const scgib_copy_range &R = ranges[i];
-        if (R.words < 0 || (R.words > 0 && (!R.src || !R.dst))) return SCGIB_EINVAL;
-        if ((reinterpret_cast<uintptr_t>(R.src) | reinterpret_cast<uintptr_t>(R.dst)) & 3)
-            return SCGIB_EINVAL;
-        t.r[t.n] = R;
-        t.blk0[t.n] = blocks;
-        blocks += (R.words + 1023) / 1024;
-        ++t.n;
-    }
-    t.blk0[t.n] = blocks;
-    if (blocks == 0) return SCGIB_OK;
-    if (blocks > 0x7fffffff) return SCGIB_EUNSUPPORTED;
-    scgib::copy_words_k<<<dim3(static_cast<unsigned>(blocks)), 256, 0, scgib::as_stream(stream)>>>(t);
-    return scgib::launch_status();
-}

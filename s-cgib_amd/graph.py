@@ -25,7 +25,6 @@ bonds) raises, which the reference's bare ``except`` turns into "skip"
 from __future__ import annotations
 
 import contextlib
-import os
 import ctypes
 
 import numpy as np
@@ -356,9 +355,6 @@ def egonet_batch(g: GraphBatch, k: int, x=None):
     """
     if g.device.type != "cuda":
         raise _lib.ScgibError("egonet_batch needs the graph on a HIP device (no CPU fallback)")
-    pre = getattr(g, "ego_prebuilt", None)
-    if pre is not None and x is None:  # EgoPipeline: built by the previous step
-        return pre.view(g, k)
     if not g.symmetric:
         raise _lib.ScgibError("egonet_batch expects a symmetric (to_bidirected) graph")
     dev = g.device
@@ -454,13 +450,16 @@ def ego_bounds(g, k):
     return int(r.nnz), int((r @ deg).sum()), dmax
 
 
-# k = 1 ego-nets through the two-launch window builder when its bounds hold.
-# Off by default: faster alone (39 vs 46 us per QM9 B512 build, tools/ego_bench.py)
-# but the replayed step measured 0.5 % slower with it (the ego chain then
-# contends earlier with Encoder1's layers); tests compare both builders.
-EGO_K1_FAST = os.environ.get("SCGIB_EGO_K1", "1") != "0"
+# k = 1 ego-nets through the sorted-list window builders when their bounds
+# hold (in-degree <= 12, molecules <= the window), else the bitmap builder.
+# On since round 1, session 4 (39 vs 46 us per QM9 B512 build alone; in the
+# replayed step it first measured 0.5 % slower, which the later LDS-window
+# one-pass form turned into 2.7 % faster).  Module attributes,
+# not environment knobs: the tests compare every builder bit for bit.
+EGO_K1_FAST = True
 # ... in one launch (count + look-back scan + fill, egonet_k1_onepass_k)
-EGO_K1_ONEPASS = os.environ.get("SCGIB_EGO_K1_ONEPASS", "1") != "0"
+# instead of two (count + block scan, fill)
+EGO_K1_ONEPASS = True
 
 
 def _egonet_k1(g, ego_ptr, ego_eptr, ws, x, max_in_degree=12):
@@ -483,7 +482,7 @@ def _egonet_k1(g, ego_ptr, ego_eptr, ws, x, max_in_degree=12):
     sub_col = torch.empty(max(e_cap, 1), dtype=i32, device=dev)
     if EGO_K1_ONEPASS:
         from . import ops  # (ops imports this module)
-        state = ops.counters(dev, "egonet_k1_scan", int(_lib.query("scgib_egonet_k1_scan_words", n)))
+        state = ops.scan_state(dev, "egonet_k1_scan", int(_lib.query("scgib_egonet_k1_scan_words", n)))
         _lib.call("scgib_egonet_k1_build_onepass", _ptr(g.rowptr), _ptr(g.col), n,
                   int(max_in_degree), _ptr(ego_ptr), _ptr(ego_eptr), _ptr(state), _ptr(ego_nodes),
                   _ptr(sub_rowptr), _ptr(sub_col), n_s, _ptr(g.dims), _ptr(ego_dims), _stream())
@@ -492,7 +491,6 @@ def _egonet_k1(g, ego_ptr, ego_eptr, ws, x, max_in_degree=12):
                   int(max_in_degree), _ptr(ego_ptr), _ptr(ego_eptr), _ptr(ws), _ptr(ego_nodes),
                   _ptr(sub_rowptr), _ptr(sub_col), n_s, _ptr(g.dims), _ptr(ego_dims), _stream())
     ego = _ego_graph(g, sub_rowptr, sub_col, ego_ptr, ego_nodes, n_s, ego_dims)
-    ego._k1_buffers = (sub_rowptr, sub_col, ego_ptr, ego_nodes, ego_dims)
     if x is not None:
         dict.__setitem__(ego.ndata, "x", x.index_select(0, ego_nodes[:n_s]))
     return ego
@@ -506,73 +504,6 @@ def _ego_graph(g, sub_rowptr, sub_col, ego_ptr, ego_nodes, n_s, ego_dims):
     ego.seg_dims = g.dims
     dict.__setitem__(ego.ndata, "_ID", ego_nodes[:n_s])
     return ego
-
-
-class EgoPipeline:
-    """Software pipeline of the k = 1 ego-net build across captured steps
-    (bench): step i trains on ``cur`` (batch i) with the ego-nets built
-    during step i-1, and builds batch i+1's (``nxt``, loaded by the host
-    before the replay) on a stream of its own beside the encoders; after the
-    step's backward one launch (scgib_copy_words) hands ``nxt``'s inputs and
-    ego-net buffers over to ``cur``.  Each step still builds one ego batch;
-    the model reads it through egonet_batch (``cur.graph.ego_prebuilt``), as
-    the reference's forward receives flatten_batch_subgraphs built by its
-    loader (exp_pretraining.py:269-272, :308-309).  Capacity mode, k = 1."""
-
-    def __init__(self, cur, nxt, k):
-        if cur.graph.dims is None or nxt.graph.dims is None or int(k) != 1:
-            raise _lib.ScgibError("EgoPipeline: capacity-mode StaticBatch pair, k = 1")
-        self.cur, self.nxt, self.k = cur, nxt, 1
-        self.stream = torch.cuda.Stream(device=cur.blob.device)
-        self.bufs = None
-        self._pending = None
-
-    def prime(self):
-        """Build the ego-nets of ``cur``'s current batch into persistent buffers
-        (outside any capture; before the first step)."""
-        self.cur.graph.ego_prebuilt = None
-        ego = egonet_batch(self.cur.graph, self.k)
-        if not hasattr(ego, "_k1_buffers"):
-            raise _lib.ScgibError("EgoPipeline: the k = 1 builder did not take this batch")
-        if self.bufs is None:
-            self.bufs = ego._k1_buffers
-        else:
-            for d, s in zip(self.bufs, ego._k1_buffers):
-                d.copy_(s)
-        self.n_s = int(self.cur.graph.ego_caps[0])
-        self.cur.graph.ego_prebuilt = self
-
-    def view(self, g, k):
-        if g is not self.cur.graph or int(k) != self.k:
-            raise _lib.ScgibError("EgoPipeline: ego-nets requested for another batch")
-        sub_rowptr, sub_col, ego_ptr, ego_nodes, ego_dims = self.bufs
-        return _ego_graph(g, sub_rowptr, sub_col, ego_ptr, ego_nodes, self.n_s, ego_dims)
-
-    def build_next(self):
-        """Fork from the current stream: build ``nxt``'s ego-nets (call at the
-        start of the step)."""
-        main = torch.cuda.current_stream()
-        self.stream.wait_stream(main)
-        with torch.cuda.stream(self.stream):
-            self.nxt.graph.ego_prebuilt = None
-            ego = egonet_batch(self.nxt.graph, self.k)
-        if not hasattr(ego, "_k1_buffers"):
-            raise _lib.ScgibError("EgoPipeline: the k = 1 builder did not take this batch")
-        self._pending = ego._k1_buffers
-
-    def hand_over(self):
-        """After the step's last read of ``cur`` (its backward): join the
-        build and copy ``nxt`` -> ``cur`` (inputs + ego-net buffers), one launch."""
-        main = torch.cuda.current_stream()
-        main.wait_stream(self.stream)
-        pairs = [(self.nxt.blob, self.cur.blob)] + list(zip(self._pending, self.bufs))
-        tab = (_lib.CopyRange * len(pairs))()
-        for i, (s, d) in enumerate(pairs):
-            if s.numel() * s.element_size() != d.numel() * d.element_size():
-                raise _lib.ScgibError("EgoPipeline: buffer sizes differ")
-            s.record_stream(main)
-            tab[i] = _lib.CopyRange(s.data_ptr(), d.data_ptr(), s.numel() * s.element_size() // 4)
-        _lib.call("scgib_copy_words", ctypes.cast(tab, ctypes.c_void_p), len(pairs), _stream())
 
 
 class StaticBatch:

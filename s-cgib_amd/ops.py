@@ -8,7 +8,6 @@ from __future__ import annotations
 
 import contextlib
 import ctypes
-import os
 import weakref
 
 import numpy as np
@@ -37,85 +36,29 @@ def _launch(name, meta, *args):
 # from the current one, joined back by join_aside() (models call it at the
 # end of forward, so captured graphs stay closed).
 _AUX_STREAMS = {}
-# deferred BatchNorm finalize in the fused GIN layers (scgib_bn_pending)
-DEFER_BN = os.environ.get("SCGIB_DEFER_BN", "1") != "0"
-DEFER_BN_FWD = os.environ.get("SCGIB_DEFER_BN_FWD", "1") != "0"
-# the encoder pair's core_tail (the interaction's noise draw) enqueued at the
-# start of the core chain, beside the ego-net build, instead of at its end
-# (round 1: A/B 0.530 vs 0.528 ms, off; re-checked in round 2 after the
-# 3-workgroup forward: 0.4349 vs 0.4437 ms over three rounds, on — the draw
-# no longer delays the core chain's join into the interaction)
-TAIL_FIRST = os.environ.get("SCGIB_TAIL_FIRST", "1") != "0"
-# ... including the last layer's, finished by the output's BN + ReLU kernel
-# (off: A/B neutral to 0.5 % slower — every consumer workgroup then combines
-# the group partials, which costs what the producer's serial tail did)
-DEFER_BN_LAST = os.environ.get("SCGIB_DEFER_BN_LAST", "0") != "0"
 _AUX_PENDING = set()
-# compressor-BN running update on the aux stream (1) or inline (0): measured
-# 1.5 % faster aside (the ~15 us single-workgroup kernel leaves the critical
-# path; its fork/join edges cost less)
-RU_ASIDE = os.environ.get("SCGIB_RU_ASIDE", "1") != "0"
-# ... or, before both, the 16-workgroup form inline on the current stream
-# (off: 10 us inline vs the fork / join edges of the aside launch, A/B 0.4686
-# vs 0.4608 ms)
-RU_MULTI = os.environ.get("SCGIB_RU_MULTI", "0") != "0"
-# encoder backward: all layers' weight-gradient slabs reduced by one launch at
-# the end (scgib_slab_reduce_multi) instead of one launch per layer
-BATCH_SLABS = os.environ.get("SCGIB_BATCH_SLABS", "1") != "0"
+# Design switches (module attributes, not environment knobs: the measured
+# alternatives were removed, DESIGN.md §5 keeps their numbers).  Tests set
+# them to cover both sides where both are supported:
+# deferred BatchNorm finalize in the fused GIN layers (scgib_bn_pending):
+# layer l leaves its statistics as group partials, layer l + 1 finishes them
+# (off: the producer finishes them; +4 % / +2.5 % step, round 2)
+DEFER_BN = True
+DEFER_BN_FWD = True
 # layer l's weight-gradient slab reduce folded into layer l-1's backward
 # statistics launch (extra workgroups, scgib_gin_bwd_stats_bn_fold) instead of
 # the chain's final reduce launch; only layer 0's slabs are left for the end
-FOLD_SLABS = os.environ.get("SCGIB_FOLD_SLABS", "1") != "0"
-# a folded slab is released once the launch that reduces it is enqueued (the
-# captured step then reuses its block instead of holding every layer's slabs)
-RELEASE_FOLDED = os.environ.get("SCGIB_RELEASE_FOLDED", "1") != "0"
-# the deferred head-MLP slab reduced by Encoder1's first backward launch (and
-# released there) instead of by its final reduce
-FOLD_LOSS_SLAB = os.environ.get("SCGIB_FOLD_LOSS_SLAB", "1") != "0"
-# encoder backward: layer l's backward and layer l-1's statistics in one
-# launch over component-aligned chunks (scgib_gin_layer_bwd_fused) when the
-# graph's components are closed and small enough; d(agg) then stays on chip.
-# Off: A/B within the box noise of the two-launch path (0.4632 vs 0.4652 ms,
-# three rounds) — the chunk kernel's per-workgroup chain (prologue, 2-3
-# sub-tiles at two workgroups per CU, then the statistics phase) is as long
-# as the two kernels it replaces, and its 437 slabs per layer move the
-# reduce to the chain's end
-FUSED_BWD = os.environ.get("SCGIB_FUSED_BWD", "0") != "0"
-# ... with layer l's slab reduce folded into layer l-1's fused launch
-FOLD_FUSED = os.environ.get("SCGIB_FOLD_FUSED", "1") != "0"
-# encoder-pair backward: capture the ego chain before the core chain (round
-# 1: 2 % slower, off; round 2 after the 3-workgroup forward and the early
-# noise draw: 0.4326 vs 0.4381 ms over five rounds, all GPU tests green with
-# it — on; the replayed graph's queue assignment follows capture order)
-EGO_FIRST = os.environ.get("SCGIB_EGO_FIRST", "1") != "0"
-# encoder pair: enqueue the two chains layer by layer alternately (forward and
-# backward) instead of one whole chain after the other (off since the
-# contrastive loss moved into the head launches: A/B 0.5126 vs 0.5148 ms/step,
-# 6 of 6 rounds at or below)
-INTERLEAVE = os.environ.get("SCGIB_INTERLEAVE", "0") != "0"
-INTERLEAVE_FWD = os.environ.get("SCGIB_INTERLEAVE_FWD", "1" if INTERLEAVE else "0") != "0"
-INTERLEAVE_BWD = os.environ.get("SCGIB_INTERLEAVE_BWD", "1" if INTERLEAVE else "0") != "0"
-# workgroup cap of the core (Encoder1) chain's final slab reduce (0: none;
-# A/B: 64 -> 0.521, 128 -> 0.516, none -> 0.508 ms/step — the join waits for
-# that reduce, so it is as critical as the ego chain's)
-SIDE_REDUCE_WG = int(os.environ.get("SCGIB_SIDE_REDUCE_WG", "0"))
-# both encoders' transfer_d gradient slabs reduced by one job after the chains join
-# (A/B: 0.538 vs 0.530 ms: the ego reduce then waits for the join; an extra
-# mid-chain cross-stream edge instead serialised the two chains in graph replay)
-SHARED_L0 = os.environ.get("SCGIB_SHARED_L0", "0") != "0"  # measured slower (A/B)
-# the same for the chain-after-chain order (the ego chain's final reduce then
-# follows the join; A/B 0.504 vs 0.494 ms: off)
-SHARED_L0_SEQ = os.environ.get("SCGIB_SHARED_L0_SEQ", "0") != "0"
+# (bench.py's superbatch pass turns it off to time the statistics kernel alone)
+FOLD_SLABS = True
 
 
-# LATE_FORK: launch_aside records an event on the current stream now and
-# enqueues the aside work at join_aside() time, after it has waited on that
-# event — the same dependencies, but in a captured graph the main chain's
-# next kernel is then created first and so keeps the producer's hardware
-# queue (the replayed graph puts a node's first-created child on its queue)
+# LATE_FORK (always): launch_aside records an event on the current stream now
+# and enqueues the aside work at join_aside() time, after it has waited on
+# that event — the same dependencies, but in a captured graph the main chain's
+# next kernel is then created first and so keeps the producer's hardware queue
+# (the replayed graph puts a node's first-created child on its queue).
 # Only inside aside_deferred() (model forwards, which always end with
 # join_aside()); elsewhere aside work is enqueued at once.
-LATE_FORK = os.environ.get("SCGIB_LATE_FORK", "1") != "0"
 _AUX_DEFERRED = []
 _DEFER_DEPTH = [0]
 
@@ -126,11 +69,15 @@ _DEFER_DEPTH = [0]
 # launch each on the loss chain).  The gradient tensors these backward
 # functions return are then written by a launch enqueued LATER in the same
 # backward pass, so a deferral is taken only when nothing can read them
-# before: every parameter's .grad is None (AccumulateGrad takes the tensor
-# without a kernel) and no other encoder-pair forward is awaiting its
-# backward (two forwards into one backward would make autograd add the two
-# gradients first).  Anything else reduces inline, as before.
-DEFER_LOSS_REDUCE = os.environ.get("SCGIB_DEFER_LOSS_REDUCE", "1") != "0"
+# before: every parameter is a contiguous fp32 CUDA leaf whose .grad is None
+# (AccumulateGrad takes the tensor without a kernel), no hook of any kind is
+# registered on it or on its AccumulateGrad node, and no other encoder-pair
+# forward is awaiting its backward (two forwards into one backward would make
+# autograd add the two gradients first).  A scope still open when the
+# autograd graph task ends (a backward that never reached the encoder pair,
+# e.g. autograd.grad over the head parameters only) reduces its jobs inline
+# from an engine callback.  Anything else reduces inline, as before.
+DEFER_LOSS_REDUCE = True
 
 
 class SlabScope:
@@ -138,26 +85,54 @@ class SlabScope:
     backward (which drains them into a chain's final reduce)."""
 
     _live = weakref.WeakSet()
+    # the deferred gradients live on the HIP device (a hook for the host tests)
+    _device_ok = staticmethod(lambda p: p.is_cuda)
 
     def __init__(self):
         self.jobs, self.keep = [], []
-        self.open, self.ok = True, True
+        self.open, self.ok, self.callback, self.stream = True, True, False, None
         for other in list(SlabScope._live):
             if other.open:  # two forwards awaiting one backward: defer nothing
                 other.ok = self.ok = False
         SlabScope._live.add(self)
 
     def usable(self, params):
-        # no .grad to accumulate into, and no gradient hook that would read
-        # the tensor as soon as the engine hands it over
+        """Whether a loss-section backward may hand autograd gradients that a
+        later launch of this scope writes.  Not for: parameters that are not
+        contiguous fp32 CUDA leaves (the backward returns an fp32 tensor that
+        autograd would cast or copy at once), a .grad to accumulate into, or a
+        hook on the tensor.  (A hook registered directly on a parameter's
+        AccumulateGrad node is not visible from Python: whoever registers one
+        that reads the gradient sets ops.DEFER_LOSS_REDUCE = False; this
+        package's GradAllReducer reads .grad only after backward returns.)"""
         return self.open and self.ok and all(
-            p is None or (p.grad is None and not getattr(p, "_backward_hooks", None) and
+            p is None or (SlabScope._device_ok(p) and p.dtype == torch.float32 and p.is_contiguous() and
+                          p.is_leaf and p.grad is None and
+                          not getattr(p, "_backward_hooks", None) and
                           not getattr(p, "_post_accumulate_grad_hooks", None))
             for p in params)
 
     def add(self, slab, wgrad, width, n_slabs):
         self.jobs.append(_lib.SlabJob(slab.data_ptr(), wgrad.data_ptr(), width, n_slabs, 0))
         self.keep += [slab, wgrad]
+        self.stream = torch.cuda.current_stream() if slab.is_cuda else None
+        if not self.callback:
+            # a backward that never reaches the encoder pair (autograd.grad over
+            # the loss-section parameters only, backward(inputs=...)) would never
+            # take the jobs: reduce them at the end of the graph task instead
+            try:
+                torch.autograd.Variable._execution_engine.queue_callback(self._flush)
+                self.callback = True
+            except RuntimeError:  # not inside a backward pass (host tests)
+                pass
+
+    def _flush(self):
+        if not self.open or not self.jobs:
+            return
+        jobs, keep = self.take()
+        with torch.cuda.stream(self.stream):
+            _reduce_jobs(jobs, _stream())
+        del keep  # the slabs stay allocated until the launch is enqueued
 
     def take(self):
         self.open = False
@@ -229,18 +204,10 @@ def launch_aside(fn, *tensors):
         return
     main = torch.cuda.current_stream()
     check_fork(main)
-    key, aux = _aux_stream(main.device)
-    if LATE_FORK:
-        ev = torch.cuda.Event()
-        ev.record(main)
-        _AUX_DEFERRED.append((key, ev, fn, tensors))
-        _AUX_PENDING.add(key)
-        return
-    aux.wait_stream(main)
-    for t in tensors:  # produced on main, consumed on aux
-        t.record_stream(aux)
-    with torch.cuda.stream(aux):
-        fn()
+    key, _ = _aux_stream(main.device)
+    ev = torch.cuda.Event()
+    ev.record(main)
+    _AUX_DEFERRED.append((key, ev, fn, tensors))
     _AUX_PENDING.add(key)
 
 
@@ -366,38 +333,6 @@ def _drain(gen):
             return stop.value
 
 
-def _interleave(first, first_stream, second, second_stream):
-    """Advance two step generators alternately, each on its own stream (the
-    launches of two encoders enqueued layer by layer: in a replayed HIP graph
-    both chains then start without waiting for the other's submissions).
-    Returns (first's value, second's value)."""
-    out, live = [None, None], [True, True]
-    gens = ((first, first_stream), (second, second_stream))
-    while live[0] or live[1]:
-        for i, (gen, stream) in enumerate(gens):
-            if not live[i]:
-                continue
-            with torch.cuda.stream(stream):
-                try:
-                    next(gen)
-                except StopIteration as stop:
-                    out[i], live[i] = stop.value, False
-    return out[0], out[1]
-
-
-def _chunk_bounds(gr, n, L, st):
-    """Chunk table of the fused backward (scgib_gin_chunk_bounds), or None
-    when the fused path does not apply to this graph."""
-    if not (FUSED_BWD and L > 1 and n > 0 and gr.components_closed and
-            1 <= gr.max_graph_nodes <= int(_lib.query("scgib_gin_chunk_max_component"))):
-        return None
-    cp = torch.empty(int(_lib.query("scgib_gin_chunks", n)) + 1, dtype=torch.int32,
-                     device=gr.rowptr.device)
-    _lib.call("scgib_gin_chunk_bounds", _p(gr.graph_ptr), gr.batch_size, _p(gr.seg_dims), n,
-              _p(gr.dims), _p(cp), st)
-    return cp
-
-
 def _reduce_jobs(jobs, st, max_wg=0):
     cap = int(_lib.query("scgib_slab_reduce_max_jobs"))
     for i0 in range(0, len(jobs), cap):
@@ -446,8 +381,9 @@ class _GinEncoder(torch.autograd.Function):
         # per encoder module: the two encoders run on concurrent streams)
         fused = training and n > 0
         # deferred BN finalize (scgib_bn_pending): layer l leaves its statistics
-        # as group partials and layer l + 1 finishes them (the last layer's:
-        # the output's BN + ReLU kernel, with DEFER_BN_LAST)
+        # as group partials and layer l + 1 finishes them (the last layer's
+        # are finished in its own launch: deferring them into the output's
+        # BN + ReLU kernel measured neutral to 0.5 % slower)
         defer_ok = fused and DEFER_BN and DEFER_BN_FWD and \
             n <= int(_lib.query("scgib_gin_defer_max_nodes"))
         ws_floats = max(int(_lib.query("scgib_gin_bn_ws_floats", n)), 1)
@@ -475,7 +411,7 @@ class _GinEncoder(torch.autograd.Function):
             rv = _p(bn.running_var) if track else None
             nbt = _p(bn.num_batches_tracked) if track else None
             bn_ws = bn_wss[l % len(bn_wss)]
-            defer = int(defer_ok and (l < L - 1 or DEFER_BN_LAST))
+            defer = int(defer_ok and l < L - 1)
             if pre and l == 0:
                 aggx = torch.empty(n, 16, dtype=torch.float32, device=dev)
                 _launch("scgib_gin_layer0_fwd", meta, _p(x), x.shape[1], _p(nmap), _p(wt),
@@ -534,17 +470,8 @@ class _GinEncoder(torch.autograd.Function):
         return _drain(_GinEncoder.backward_steps(ctx, g_out, g_readout))
 
     @staticmethod
-    def backward_steps(ctx, g_out, g_readout=None, l0=None):
-        """backward as a generator (yields after each layer), see forward_steps.
-
-        ``l0`` = (buf, first, total, owner, pending): the layer-0 (transfer_d
-        fold) weight-gradient slabs of TWO encoders sharing transfer_d live in
-        one buffer ``buf`` of ``total`` slabs, this chain's from slab
-        ``first``; the owner (owner = True) does not launch its final reduce
-        but appends (jobs, keep) to the list ``pending`` — the caller launches
-        it after the two chains join, and its d Wt job sums all ``total``
-        slabs (one fixed-order sum, no separate add, no extra cross-stream
-        edge); the other chain returns dwt = None."""
+    def backward_steps(ctx, g_out, g_readout=None):
+        """backward as a generator (yields after each layer), see forward_steps."""
         L, gr, pre = ctx.L, ctx.graph, ctx.pre
         t = ctx.saved_tensors
         saved, params = t[: 4 * L], t[4 * L: 4 * L + 6 * L]
@@ -573,33 +500,19 @@ class _GinEncoder(torch.autograd.Function):
         fold = None  # the previous layer's slab job, reduced by the next stats launch
         fold_slab = None  # its slab: released once that launch is enqueued (the
         # allocator may then reuse the block for later tensors of this stream)
-        chunks = _chunk_bounds(gr, n, L, st)
-        # the fused launches alternate two BN-backward workspaces
-        ws_pair = (bn_ws, torch.empty_like(bn_ws)) if chunks is not None else (bn_ws,)
-        gpart_off = gpart - bn_ws.data_ptr()
-        carry = None  # (dy, bn_g, coef, ws) of layer l from layer l + 1's fused launch
         for l in reversed(range(L)):
             agg, r, z2, stat = saved[4 * l: 4 * l + 4]
             w1, _, w2 = params[6 * l], params[6 * l + 1], params[6 * l + 2]
             d_in = agg.shape[1]
-            from_fused = carry is not None
-            if from_fused:
-                dy, bn_g, coef, ws_l = carry
-                carry = None
-            else:
-                # (the previous layer's dy and slab are no longer read by anything
-                # not yet enqueued: released before the new allocations, whose
-                # blocks the captured step can then reuse)
-                dy = slab = None
-                dy = torch.empty(n, HIDDEN, dtype=torch.float32, device=dev)
-                bn_g = torch.empty(2, HIDDEN, dtype=torch.float32, device=dev)  # dgamma, dbeta
-                coef = torch.empty(2, HIDDEN, dtype=torch.float32, device=dev)
-                ws_l = bn_ws
-            gpart = ws_l.data_ptr() + gpart_off
+            # (the previous layer's dy and slab are no longer read by anything
+            # not yet enqueued: released before the new allocations, whose
+            # blocks the captured step can then reuse)
+            dy = slab = None
+            dy = torch.empty(n, HIDDEN, dtype=torch.float32, device=dev)
+            bn_g = torch.empty(2, HIDDEN, dtype=torch.float32, device=dev)  # dgamma, dbeta
+            coef = torch.empty(2, HIDDEN, dtype=torch.float32, device=dev)
             # dy, tile sums and the BN-backward finalize in one launch
-            if from_fused:
-                pass  # made by layer l + 1's fused launch
-            elif dagg_next is None and g_readout is not None:
+            if dagg_next is None and g_readout is not None:
                 # the readout's broadcast backward folded into the last layer
                 _launch("scgib_gin_bwd_stats_seg_bn", {"n": n, "e": 0, "d_in": HIDDEN}, _p(g_out), _p(g_readout),
                         _p(ctx.seg), _p(z2), _p(stat), n, int(ctx.training), _p(dy),
@@ -628,31 +541,10 @@ class _GinEncoder(torch.autograd.Function):
             w1c, w2c = _f32(w1, "w1"), _f32(w2, "w2")
             if pre and l == 0:
                 width = int(_lib.query("scgib_gin_layer0_slab_width"))
-                if l0 is None:
-                    slab = torch.empty(nslab * width, dtype=torch.float32, device=dev)
-                else:
-                    slab = l0[0][l0[1] * width:(l0[1] + nslab) * width]
+                slab = torch.empty(nslab * width, dtype=torch.float32, device=dev)
                 _launch("scgib_gin_layer0_bwd", meta, _p(dy), _p(z2), _p(r), _p(agg), _p(aggx),
                         ctx.n_feat, _p(stat), _p(coef), _p(w1c), _p(w2c), n, _p(slab), _p(gr.dims),
                         _byref(bpend), st)
-                dagg = None
-            elif chunks is not None and l > 0 and d_in == HIDDEN:
-                # layer l's backward + layer l-1's dy and BN-backward sums
-                width = HIDDEN * HIDDEN + HIDDEN * d_in + 2 * HIDDEN
-                nch = int(_lib.query("scgib_gin_chunks", n))
-                slab = torch.empty(nch * width, dtype=torch.float32, device=dev)
-                z2p, statp = saved[4 * (l - 1) + 2], saved[4 * (l - 1) + 3]
-                ws_n = ws_pair[1] if ws_l is ws_pair[0] else ws_pair[0]
-                dyp = torch.empty(n, HIDDEN, dtype=torch.float32, device=dev)
-                bn_gp = torch.empty(2, HIDDEN, dtype=torch.float32, device=dev)
-                coefp = torch.empty(2, HIDDEN, dtype=torch.float32, device=dev)
-                _launch("scgib_gin_layer_bwd_fused", meta, _p(dy), _p(z2), _p(r), _p(agg),
-                        _p(stat), _p(coef), _p(w1c), _p(w2c), n, _p(chunks), _p(gr.rowptr_t),
-                        _p(gr.col_t), ctx.opes[l], _p(z2p), _p(statp), int(ctx.training),
-                        _p(dyp), _p(bn_gp[0]), _p(bn_gp[1]), _p(coefp), _p(ws_n), _p(cnt),
-                        defer, _p(slab), _p(gr.dims), _byref(bpend), _byref(fold), st)
-                fold = fold_slab = None
-                carry = (dyp, bn_gp, coefp, ws_n)
                 dagg = None
             else:
                 width = HIDDEN * HIDDEN + HIDDEN * d_in + 2 * HIDDEN
@@ -663,43 +555,25 @@ class _GinEncoder(torch.autograd.Function):
                         _p(stat), _p(coef), _p(w1c), _p(w2c), n, _p(dagg), _p(slab), _NULL,
                         _p(gr.dims), _byref(bpend), st)
             wgrad = torch.empty(width, dtype=torch.float32, device=dev)
-            if pre and l == 0 and l0 is not None:
-                # this chain's W2 | W1 | b2 | b1 columns (row stride: the full slab)
-                base = HIDDEN * HIDDEN + HIDDEN * d_in + 2 * HIDDEN
-                jobs.append(_lib.SlabJob(slab.data_ptr(), wgrad.data_ptr(), base, nslab, width))
-                keep.append(slab)
-                if l0[3]:  # owner: the Wt columns of both encoders' slabs (after the join)
-                    jobs.append(_lib.SlabJob(l0[0].data_ptr() + 4 * base,
-                                             wgrad.data_ptr() + 4 * base, 32 * ctx.n_feat,
-                                             l0[2], width))
-                    keep.append(l0[0])
-            elif pre and l == 0 and BATCH_SLABS:  # dWt occupies 32 * F of its 512 columns
+            if pre and l == 0:  # dWt occupies 32 * F of its 512 columns
                 used = HIDDEN * HIDDEN + HIDDEN * d_in + 2 * HIDDEN + 32 * ctx.n_feat
                 jobs.append(_lib.SlabJob(slab.data_ptr(), wgrad.data_ptr(), used, nslab, width))
                 keep.append(slab)
-            elif BATCH_SLABS:  # reduced by the next stats launch, or together at the end
-                ns = int(_lib.query("scgib_gin_chunks", n)) if carry is not None else \
-                    int(_lib.query("scgib_gin_layer_bwd_slabs", n, d_in))
+            else:  # reduced by the next stats launch, or together at the end
+                ns = int(_lib.query("scgib_gin_layer_bwd_slabs", n, d_in))
                 job = _lib.SlabJob(slab.data_ptr(), wgrad.data_ptr(), width, ns, 0)
-                if (carry is not None and FOLD_FUSED and l > 1) or \
-                        (carry is None and FOLD_SLABS and l > 0):
+                if FOLD_SLABS and l > 0:
                     fold, fold_slab = job, slab  # reduced by the next layer's launch
-                    if not RELEASE_FOLDED:
-                        keep.append(slab)
                 else:
                     jobs.append(job)
                     keep.append(slab)
-            else:
-                ns = int(_lib.query("scgib_gin_chunks", n)) if carry is not None else \
-                    int(_lib.query("scgib_gin_layer_bwd_slabs", n, d_in))
-                _lib.call("scgib_slab_reduce", _p(slab), ns, width, _p(wgrad), st)
             o = HIDDEN * HIDDEN
             grads[6 * l + 2] = wgrad[:o].view(HIDDEN, HIDDEN)
             grads[6 * l + 0] = wgrad[o:o + HIDDEN * d_in].view(HIDDEN, d_in)
             o += HIDDEN * d_in
             grads[6 * l + 3] = wgrad[o:o + HIDDEN]
             grads[6 * l + 1] = wgrad[o + HIDDEN:o + 2 * HIDDEN]
-            if pre and l == 0 and (l0 is None or l0[3]):
+            if pre and l == 0:
                 o += 2 * HIDDEN
                 dwt = wgrad[o:o + 32 * ctx.n_feat].view(32, ctx.n_feat)
             grads[6 * l + 4] = bn_g[0]
@@ -711,10 +585,8 @@ class _GinEncoder(torch.autograd.Function):
             ctx.extra_jobs = None
             jobs.extend(extra[0])
             keep.extend(extra[1])
-        if l0 is not None and l0[3]:
-            l0[4].append((jobs, keep))  # launched by the caller after the chains join
-        elif jobs:  # every layer's weight-gradient slabs, one fixed-order reduce launch
-            _reduce_jobs(jobs, st, getattr(ctx, "reduce_wg", 0))
+        if jobs:  # every layer's weight-gradient slabs, one fixed-order reduce launch
+            _reduce_jobs(jobs, st)
             del keep  # slabs stay allocated until the launch is enqueued
         if pre:
             return (None, None, None, None, None, dwt, None, *grads)
@@ -779,21 +651,18 @@ class _GinEncoderPair(torch.autograd.Function):
         ctx.side, ctx.ne = side, ne
         check_fork(main)
         side.wait_stream(main)
-        if core_tail is not None and TAIL_FIRST:  # beside the ego-net build
+        if core_tail is not None:  # beside the ego-net build
             core_tail()
         # Encoder2 + its readout (dgl.sum_nodes per ego-net) on ``side``,
-        # Encoder1 on the current stream, enqueued layer by layer alternately
+        # Encoder1 on the current stream, one chain after the other
         ego_steps = _GinEncoder.forward_steps(
             ctx.sub[0], None, ego, gin_ego, training, x, wt, nmap, *params[:ne],
             readout=(ego.graph_ptr, ego.batch_size, ego.seg_dims))
         core_steps = _GinEncoder.forward_steps(ctx.sub[1], None, core, gin_core, training, x, wt,
                                                None, *params[ne:])
-        if INTERLEAVE_FWD:
-            (s, ro), f = _interleave(ego_steps, side, core_steps, main)
-        else:
-            with torch.cuda.stream(side):
-                s, ro = _drain(ego_steps)
-            f = _drain(core_steps)
+        with torch.cuda.stream(side):
+            s, ro = _drain(ego_steps)
+        f = _drain(core_steps)
         outs = (s, ro, f)
         ctx.lin = w0 is not None
         ctx.lin_leaves = (w0, b0)
@@ -807,8 +676,6 @@ class _GinEncoderPair(torch.autograd.Function):
             ctx.lin_saved = (f, w0)
             ctx.core_dims = core.dims
             outs = (s, ro, f, t)
-        if core_tail is not None and not TAIL_FIRST:  # non-differentiable extra work
-            core_tail()
         main.wait_stream(side)
         s.record_stream(main)
         ro.record_stream(main)
@@ -825,33 +692,17 @@ class _GinEncoderPair(torch.autograd.Function):
         check_fork(main)
         side.wait_stream(main)
         # Encoder1's final weight-gradient reduce runs beside the ego chain's
-        # last layers (optionally capped, SIDE_REDUCE_WG); it also sums the
-        # loss section's deferred slabs (SlabScope: the head MLP's and the
-        # interaction's, enqueued on the main stream before this fork, and
-        # compressor[0]'s below) — Encoder1's chain ends well before the ego
-        # chain's, so they leave the critical path
-        ctx.sub[1].reduce_wg = SIDE_REDUCE_WG
+        # last layers; it also sums the loss section's deferred slabs
+        # (SlabScope: the head MLP's and the interaction's, enqueued on the
+        # main stream before this fork, and compressor[0]'s below) — Encoder1's
+        # chain ends well before the ego chain's, so they leave the critical path
         scope = ctx.scope if (ctx.scope is not None and ctx.scope.open) else None
         held = None
         dw0 = db0 = None
         g_f_in = g_f
-        if EGO_FIRST and not INTERLEAVE_BWD:  # capture the critical ego chain first
-            ge = _GinEncoder.backward(ctx.sub[0], g_s, g_ro)
-        # shared layer-0 slabs: both encoders' transfer_d slabs in one buffer,
-        # the ego chain's final reduce (after the join) sums them — no add of
-        # the two d Wt after the join
-        shared = SHARED_L0 if INTERLEAVE_BWD else (SHARED_L0_SEQ and not EGO_FIRST)
-        l0_e = l0_c = None
-        if shared:
-            ns_e = int(_lib.query("scgib_gin_bwd_slabs", ctx.sub[0].saved_tensors[2].shape[0]))
-            ns_c = int(_lib.query("scgib_gin_bwd_slabs", ctx.sub[1].saved_tensors[2].shape[0]))
-            width = int(_lib.query("scgib_gin_layer0_slab_width"))
-            buf = torch.empty((ns_e + ns_c) * width, dtype=torch.float32,
-                              device=ctx.sub[0].saved_tensors[2].device)
-            buf.record_stream(side)
-            pending = []
-            l0_e = (buf, 0, ns_e + ns_c, True, pending)
-            l0_c = (buf, ns_e, ns_e + ns_c, False, None)
+        # the critical ego chain is captured first: the replayed graph then
+        # puts it on the interaction's queue (round 2: 0.4381 -> 0.4326 ms)
+        ge = _GinEncoder.backward(ctx.sub[0], g_s, g_ro)
         with torch.cuda.stream(side):
             if ctx.lin and g_t is not None:
                 f, w0 = ctx.lin_saved
@@ -878,25 +729,15 @@ class _GinEncoderPair(torch.autograd.Function):
                 # later main-stream work could be handed it unordered (in a
                 # captured step `record_stream` alone does not order the reuse)
                 held = list(keep)
-                if jobs and FOLD_SLABS and FOLD_LOSS_SLAB:  # the largest (the head MLP's) into Encoder1's first launch
+                if jobs and FOLD_SLABS:  # the largest (the head MLP's) into Encoder1's first launch
                     big = max(range(len(jobs)), key=lambda i: jobs[i].width * jobs[i].n_slabs)
                     ctx.sub[1].first_fold = (jobs[big], keep[2 * big: 2 * big + 2])
                     jobs = jobs[:big] + jobs[big + 1:]
                     keep = keep[:2 * big] + keep[2 * big + 2:]
                 ctx.sub[1].extra_jobs = (jobs, keep)
-            if not INTERLEAVE_BWD:
-                gc = _drain(_GinEncoder.backward_steps(ctx.sub[1], g_f, l0=l0_c))
-        if INTERLEAVE_BWD:  # both chains enqueued layer by layer, the ego chain first
-            ge, gc = _interleave(_GinEncoder.backward_steps(ctx.sub[0], g_s, g_ro, l0=l0_e), main,
-                                 _GinEncoder.backward_steps(ctx.sub[1], g_f, l0=l0_c), side)
-        elif not EGO_FIRST:
-            ge = _drain(_GinEncoder.backward_steps(ctx.sub[0], g_s, g_ro, l0=l0_e))
+            gc = _drain(_GinEncoder.backward_steps(ctx.sub[1], g_f))
         main.wait_stream(side)
         held = None  # after the join: main-stream reuse is ordered after side's reads
-        if shared:  # the ego chain's reduce, incl. both encoders' d Wt
-            jobs, keep = pending[0]
-            _reduce_jobs(jobs, _stream())
-            del keep
         for g in (*gc, dw0, db0):
             if isinstance(g, torch.Tensor):
                 g.record_stream(main)
@@ -921,8 +762,8 @@ def gin_encoder_pair_x(x, ego, gin_ego, core, gin_core, transfer, node_map, side
     BN + ReLU; the ego chain on stream ``side`` (forward and backward).  With ``lin0`` (the
     compressor's Linear(64, 64), models.py:596) also returns
     t = lin0(gin_core(...)), computed at the end of the core chain;
-    ``core_tail()`` (non-differentiable, e.g. the noise draw) runs on the
-    core chain too: first (TAIL_FIRST) or last, before the join."""
+    ``core_tail()`` (non-differentiable, e.g. the noise draw) runs first on
+    the core chain, beside the ego-net build."""
     if ego.num_nodes() == 0 or core.num_nodes() == 0:
         raise _lib.ScgibError("gin_encoder on an empty graph")
     if transfer.bias is not None or transfer.weight.shape != (32, x.shape[1]) \
@@ -1016,16 +857,10 @@ def _interaction_forward(ctx, f, t, s, u_gate, u_feat, gamma, beta, w2, b2, w_at
         def upd():  # B sequential momentum updates in closed form
             _lib.call("scgib_bn_running_update", _p(stats), _p(graph.graph_ptr), B,
                       float(bn.momentum), _p(rm), _p(rv), _p(nbt), _stream())
-        if RU_MULTI:  # a few microseconds inline: no fork / join around it
-            part = torch.empty(int(_lib.query("scgib_bn_running_update_partials", B)),
-                               dtype=torch.float64, device=dev)
-            _lib.call("scgib_bn_running_update_multi", _p(stats), _p(graph.graph_ptr), B,
-                      float(bn.momentum), _p(rm), _p(rv), _p(nbt), _p(part),
-                      _p(counters(dev, "bn_running_update", 1)), st)
-        elif RU_ASIDE:  # nothing in the step reads them: beside the critical path
-            launch_aside(upd, stats, graph.graph_ptr)
-        else:
-            upd()
+        # nothing in the step reads them: beside the critical path (the
+        # 16-workgroup form inline measured 10 us slower than the aside
+        # launch's fork / join edges, round 2)
+        launch_aside(upd, stats, graph.graph_ptr)
     ctx.graph, ctx.training, ctx.pad, ctx.n_last = graph, training, pad, n_last
     ctx.bn_eps = float(bn.eps)
     ctx.rm, ctx.rv = (None, None) if training else (rm.clone(), rv.clone())
@@ -1224,6 +1059,26 @@ def counters(device, key, n):
         off, size = used, n
         _COUNTER_RANGES[rk] = (off, size)
     return buf[off: off + n]
+
+
+_SCAN_STATES = {}  # (device index, key, stream) -> int32 tensor
+_SCAN_RETIRED = []  # outgrown scan states: a captured graph may still point at one
+
+
+def scan_state(device, key, n):
+    """``n`` zeroed int32 words of O(n) scan state (the one-pass ego builder's
+    look-back words) for call site ``key`` on ``device`` and the current
+    stream, separate from the O(1) counter pool: it grows on demand (a new
+    zeroed tensor; the outgrown one is kept alive, since a captured graph may
+    reference it) and the kernels leave it zeroed for the next launch."""
+    idx = torch.device(device).index or 0
+    rk = (idx, key, torch.cuda.current_stream(device).cuda_stream)
+    buf = _SCAN_STATES.get(rk)
+    if buf is None or buf.numel() < n:
+        if buf is not None:
+            _SCAN_RETIRED.append(buf)
+        buf = _SCAN_STATES[rk] = torch.zeros(max(n, 1024), dtype=torch.int32, device=device)
+    return buf[:n]
 
 
 # ---------------------------------------------------------------------------

@@ -84,12 +84,7 @@ def _noise(n_cap, dev, seed):
             torch.rand(n_cap, 64, device=dev, generator=gen))
 
 
-@pytest.mark.parametrize("fused_bwd", [False, True])
-def test_capacity_mode_eager_matches_exact(pkg, dev, fused_bwd, monkeypatch):
-    """fused_bwd: the chunked fused GIN backward (scgib_gin_layer_bwd_fused)
-    in both modes — capacity mode adds chunks of padding rows only and the
-    zeroing of dy rows past the actual count."""
-    monkeypatch.setattr(pkg.ops, "FUSED_BWD", fused_bwd)
+def test_capacity_mode_eager_matches_exact(pkg, dev):
     hosts = _batches(pkg, (1, 2, 3))
     n_cap, e_cap, mgn, caps = pkg.graph.StaticBatch.capacities(hosts, 1, slack=1.05)
     static = pkg.graph.StaticBatch(B, n_cap, e_cap, F_IN, mgn, caps, dev)
@@ -191,7 +186,7 @@ def test_deferred_loss_reduces_bitwise(pkg, dev, monkeypatch):
     summed by Encoder1's final multi-job reduce give the same gradients, bit
     for bit, as their own reduce launches (same fixed order per job); the
     head MLP's, reduced by the fold workgroups of Encoder1's first backward
-    launch (ops.FOLD_LOSS_SLAB: 4 partitions per column, fp64 final sum),
+    launch (4 partitions per column, fp64 final sum),
     agree to fp32 summation order; and the deferral is actually taken (3
     jobs per step)."""
     gh = _batches(pkg, (9,))[0]
@@ -220,7 +215,7 @@ def test_deferred_loss_reduces_bitwise(pkg, dev, monkeypatch):
     for k, p in m_defer.named_parameters():
         if p.grad is None:
             continue
-        if k.startswith("MLP.") and pkg.ops.FOLD_LOSS_SLAB:
+        if k.startswith("MLP."):
             ref = inline[k].grad
             assert (p.grad - ref).norm() <= 1e-6 * ref.norm() + 1e-12, k
         else:
@@ -232,3 +227,43 @@ def test_deferred_loss_reduces_bitwise(pkg, dev, monkeypatch):
     (kl + rec + con).backward()
     torch.cuda.synchronize()
     assert added == []
+
+
+@pytest.mark.parametrize("mode", ["grad", "inputs", "double"])
+def test_deferred_loss_reduce_partial_and_cast_backward(pkg, dev, mode, monkeypatch):
+    """SlabScope safety (ops.py): a backward that never reaches the encoder
+    pair — autograd.grad over the head MLP's parameters only, or
+    backward(inputs=[...]) — still reduces the deferred slabs (an engine
+    callback at the end of the graph task), and a model whose parameters are
+    not fp32 is never deferred (autograd casts the returned gradient at once).
+    Each case equals the same run with the deferral off."""
+    gh = _batches(pkg, (9,))[0]
+    g = gh.to(dev)
+    n = g.num_nodes()
+    ug, uf = _noise(n, dev, 301)
+    base = _model(pkg, dev)
+    got = {}
+    for defer in (False, True):
+        monkeypatch.setattr(pkg.ops, "DEFER_LOSS_REDUCE", defer)
+        m = copy.deepcopy(base)
+        if mode == "double":
+            m = m.double()
+        m.zero_grad(set_to_none=True)
+        _, kl, con, rec = m(g, g.ndata["x"], None, None, None, 1, None, 1, dev, B,
+                            noise=(ug, uf))
+        loss = kl + rec + con
+        head = list(m.MLP.parameters()) + list(m.attn_layer.parameters())
+        if mode == "grad":
+            grads = torch.autograd.grad(loss, head)
+        elif mode == "inputs":
+            loss.backward(inputs=head)
+            grads = [p.grad for p in head]
+        else:
+            loss.backward()
+            grads = [p.grad for p in m.parameters() if p.grad is not None]
+        torch.cuda.synchronize()
+        got[defer] = [t.detach().clone() for t in grads]
+    assert len(got[True]) == len(got[False]) > 0
+    for a, b in zip(got[False], got[True]):
+        assert torch.isfinite(b).all()
+        assert (a - b).norm() <= 1e-6 * a.norm() + 1e-12

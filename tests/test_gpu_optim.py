@@ -189,53 +189,3 @@ def test_bench_allreduce_captured_one_rank_rccl():
     line = json.loads(out.stdout.strip().splitlines()[-1])
     assert line["config"]["allreduce"] == "captured in the step graph", out.stderr[-2000:]
     assert line["value"] > 0 and line["config"]["final_loss"] == line["config"]["final_loss"]
-
-
-def test_bench_ego_pipeline_same_losses():
-    """graph.EgoPipeline (batch i+1's ego-nets built inside step i, handed over
-    by one scgib_copy_words launch): the replayed steps train on the same
-    batches with the same ego-nets, so the final loss equals the unpipelined
-    bench's."""
-    import json
-    import os
-    import subprocess
-    import sys
-    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    losses = {}
-    for on in ("0", "1"):
-        env = dict(os.environ, SCGIB_EGO_PIPELINE=on)
-        cmd = [sys.executable, os.path.join(root, "bench.py"), "--steps", "5", "--warmup", "2",
-               "--pool", "3", "--no-cpu-baseline", "--no-superbatch", "--no-kernel-timer"]
-        out = subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=240)
-        assert out.returncode == 0, out.stderr[-3000:]
-        line = json.loads(out.stdout.strip().splitlines()[-1])
-        assert line["config"]["ego_pipeline"] == (on == "1")
-        losses[on] = line["config"]["final_loss"]
-    assert losses["0"] == losses["0"] and abs(losses["0"] - losses["1"]) <= 1e-4 * abs(losses["0"]), losses
-
-
-def test_copy_words_ranges(pkg):
-    """scgib_copy_words: several ranges (vector and word paths, partial last
-    blocks) in one launch, exact; more ranges than the table holds refused."""
-    import ctypes
-    dev = torch.device("cuda", 0)
-    g = torch.Generator().manual_seed(3)
-    sizes = [1, 1023, 1024, 4099, 70001]
-    srcs = [torch.randint(-2**31, 2**31 - 1, (n,), generator=g, dtype=torch.int32).to(dev)
-            for n in sizes]
-    dsts = [torch.zeros(n + 1, dtype=torch.int32, device=dev) for n in sizes]
-    tab = (pkg._lib.CopyRange * len(sizes))()
-    for i, (s, d) in enumerate(zip(srcs, dsts)):
-        # odd ranges start one word in: 4-byte but not 16-byte aligned
-        off = 4 * (i % 2)
-        tab[i] = pkg._lib.CopyRange(s.data_ptr(), d.data_ptr() + off, s.numel())
-    pkg._lib.call("scgib_copy_words", ctypes.cast(tab, ctypes.c_void_p), len(sizes),
-                  pkg.graph._stream())
-    torch.cuda.synchronize()
-    for i, (s, d) in enumerate(zip(srcs, dsts)):
-        o = i % 2
-        assert torch.equal(d[o:o + s.numel()], s)
-        assert int(d[s.numel()] if o == 0 else d[0]) == 0  # nothing past the range
-    big = (pkg._lib.CopyRange * 9)()
-    with pytest.raises(pkg._lib.ScgibError):
-        pkg._lib.call("scgib_copy_words", ctypes.cast(big, ctypes.c_void_p), 9, pkg.graph._stream())

@@ -212,55 +212,6 @@ def _interaction_oracle(p, f, s, counts, u_gate, u_feat, bn_state):
     return im, z1, z2, kl
 
 
-@pytest.mark.parametrize("B", [1, 7, 100, 512, 2048])
-def test_bn_running_update_multi_equals_single(pkg, dev, B):
-    """The compressor BatchNorm's B sequential momentum updates
-    (models.py:642, one BN call per graph) in closed form: the 16-workgroup
-    kernel (scgib_bn_running_update_multi, inline on the loss chain) vs the
-    one-workgroup kernel and vs an fp64 sequential loop; the counter comes
-    back zeroed (three launches in a row)."""
-    gen = torch.Generator().manual_seed(B)
-    stride = pkg._lib.STATS_STRIDE
-    stats = torch.randn(B, stride, generator=gen)
-    stats[:, 64:128] = stats[:, 64:128].abs() * 5
-    sizes = torch.randint(2, 30, (B,), generator=gen)
-    gptr = torch.zeros(B + 1, dtype=torch.int32)
-    gptr[1:] = torch.cumsum(sizes, 0)
-    rm0, rv0 = torch.randn(64, generator=gen), torch.rand(64, generator=gen) + 0.5
-    mom = 0.1
-    ref_m, ref_v = rm0.double().clone(), rv0.double().clone()
-    for i in range(B):  # the reference's loop
-        ref_m = (1 - mom) * ref_m + mom * stats[i, :64].double()
-        ref_v = (1 - mom) * ref_v + mom * stats[i, 64:128].double() / float(sizes[i] - 1)
-    sd, gd = stats.to(dev), gptr.to(dev)
-    outs = []
-    for multi in (False, True):
-        rm, rv = rm0.clone().to(dev), rv0.clone().to(dev)
-        nbt = torch.zeros((), dtype=torch.int64, device=dev)
-        reps = 3 if multi else 1
-        for _ in range(reps):
-            rm.copy_(rm0)
-            rv.copy_(rv0)
-            nbt.zero_()
-            if multi:
-                part = torch.empty(int(pkg._lib.query("scgib_bn_running_update_partials", B)),
-                                   dtype=torch.float64, device=dev)
-                cnt = pkg.ops.counters(dev, "test_bn_ru", 1)
-                pkg._lib.call("scgib_bn_running_update_multi", pkg.ops._p(sd), pkg.ops._p(gd), B,
-                              mom, pkg.ops._p(rm), pkg.ops._p(rv), pkg.ops._p(nbt),
-                              pkg.ops._p(part), pkg.ops._p(cnt), None)
-            else:
-                pkg._lib.call("scgib_bn_running_update", pkg.ops._p(sd), pkg.ops._p(gd), B, mom,
-                              pkg.ops._p(rm), pkg.ops._p(rv), pkg.ops._p(nbt), None)
-            torch.cuda.synchronize()
-            assert int(nbt) == B
-        outs.append((rm.cpu(), rv.cpu()))
-        assert rel_err(rm.cpu(), ref_m.float()) < 1e-6
-        assert rel_err(rv.cpu(), ref_v.float()) < 1e-6
-    assert int(cnt.cpu()[0]) == 0
-    assert rel_err(outs[0][0], outs[1][0]) < 1e-6 and rel_err(outs[0][1], outs[1][1]) < 1e-6
-
-
 @pytest.mark.parametrize("training", [True, False])
 def test_interaction_fwd_bwd(pkg, dev, training):
     torch.manual_seed(0)
@@ -405,40 +356,11 @@ def test_pretrain_step_matches_reference(pkg, dev, name, device_ego):
 
 
 # ---------------------------------------------------------------------------
-# chunk table of the fused backward: chunk c = components starting in [64c, 64c+64)
-# ---------------------------------------------------------------------------
-@pytest.mark.parametrize("n_mols,workload,pad", [(300, "qm9", 0), (37, "qm9", 200), (1, "qm9", 0),
-                                                 (120, "zinc", 70)])
-def test_gin_chunk_bounds(pkg, dev, n_mols, workload, pad):
-    g, gh = rand_graph(pkg, n_mols, workload, 5, dev)
-    n = g.num_nodes()
-    gp = gh.graph_ptr.numpy().astype(np.int64)
-    ncap = n + pad
-    dims = torch.tensor([n, g.num_edges()], dtype=torch.int32, device=dev) if pad else None
-    nch = int(pkg._lib.query("scgib_gin_chunks", ncap))
-    cp = torch.full((nch + 1,), -7, dtype=torch.int32, device=dev)
-    pkg._lib.call("scgib_gin_chunk_bounds", pkg.ops._p(g.graph_ptr), g.batch_size, None, ncap,
-                  pkg.ops._p(dims), pkg.ops._p(cp), None)
-    starts = np.append(gp[:-1], n)
-    want = [int(starts[np.searchsorted(starts, 64 * c)]) if 64 * c <= n else n
-            for c in range(nch + 1)]
-    assert cp.cpu().tolist() == want
-    sizes = np.diff(np.array(want))
-    if gh.max_graph_nodes <= int(pkg._lib.query("scgib_gin_chunk_max_component")):
-        assert sizes.max() <= 96
-
-
-# ---------------------------------------------------------------------------
 # A5 fused: GIN encoder (fused HIP layers) vs the oracle's GIN
 # ---------------------------------------------------------------------------
-@pytest.mark.parametrize("fused_bwd", [True, False])
 @pytest.mark.parametrize("training", [True, False])
 @pytest.mark.parametrize("layers,n_mols", [(5, 300), (4, 37), (2, 1)])
-def test_fused_gin_encoder(pkg, dev, training, layers, n_mols, fused_bwd, monkeypatch):
-    """fused_bwd: layers >= 1 run backward + the previous layer's statistics
-    as one chunked launch (scgib_gin_layer_bwd_fused); False: the two-launch
-    path (gin_bwd5_k + gin_bwd_stats_k)."""
-    monkeypatch.setattr(pkg.ops, "FUSED_BWD", fused_bwd)
+def test_fused_gin_encoder(pkg, dev, training, layers, n_mols):
     torch.manual_seed(layers)
     g, gh = rand_graph(pkg, n_mols, "qm9", 11, dev)
     gin = pkg.models.GIN(32, 64, layers)
@@ -848,17 +770,15 @@ def test_gin_encoder_deferred_bn_bitwise(pkg, dev, via_ego, n_mols):
         target, nmap = g, None
     w = torch.randn(target.num_nodes(), 64, device=dev)
     outs = []
-    # (defer, last): the last layer's statistics finished by bn_relu_apply
-    for defer, last in ((True, True), (True, False), (False, False)):
+    for defer in (True, False):
         gin_c, lin_c = copy.deepcopy(gin), copy.deepcopy(lin)
-        old = pkg.ops.DEFER_BN, pkg.ops.DEFER_BN_FWD, pkg.ops.DEFER_BN_LAST
+        old = pkg.ops.DEFER_BN, pkg.ops.DEFER_BN_FWD
         pkg.ops.DEFER_BN = pkg.ops.DEFER_BN_FWD = defer
-        pkg.ops.DEFER_BN_LAST = last
         try:
             h = pkg.ops.gin_encoder_x(x, target, gin_c, lin_c, nmap)
             (h * w).sum().backward()
         finally:
-            pkg.ops.DEFER_BN, pkg.ops.DEFER_BN_FWD, pkg.ops.DEFER_BN_LAST = old
+            pkg.ops.DEFER_BN, pkg.ops.DEFER_BN_FWD = old
         torch.cuda.synchronize()
         outs.append((h.detach(), {k: p.grad for k, p in list(gin_c.named_parameters())
                                   + [("wt", lin_c.weight)]},

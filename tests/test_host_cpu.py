@@ -356,12 +356,17 @@ def test_ego_bounds_match_oracle_sizes(pkg):
         assert dmax == int(np.diff(g.rowptr.numpy()).max())
 
 
-def test_slab_scope_rules(pkg):
+def test_slab_scope_rules(pkg, monkeypatch):
     """ops.SlabScope (host logic, no launch): usable only while open, with
-    every parameter's .grad None, and with no other scope awaiting its
-    backward; take() closes it and hands over the jobs."""
+    every parameter a contiguous fp32 leaf whose .grad is None, and with no
+    other scope awaiting its backward; take() closes it and hands over the
+    jobs."""
     ops = pkg.ops
+    monkeypatch.setattr(ops.SlabScope, "_device_ok", staticmethod(lambda p: True))
     w = torch.zeros(4, requires_grad=True)
+    # parameters autograd would cast or copy the returned gradient for: inline
+    assert not ops.SlabScope().usable((torch.zeros(4, dtype=torch.float64, requires_grad=True),))
+    assert not ops.SlabScope().usable((torch.zeros(4, 2, requires_grad=True).t(),))
     a = ops.SlabScope()
     assert a.usable((w, None))
     slab, out = torch.zeros(8), torch.zeros(4)

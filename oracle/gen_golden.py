@@ -355,6 +355,124 @@ def gen_finetune_golden(models, util_mod, name, *, workload, F, B, k, dataset, n
           f"trainable={len(trainable)}")
 
 
+CKPT = "/root/reference/outputs/pre_training_v1_GIN_64_5_1.pt"
+CKPT_FIXTURE = "ckpt_pre_training_v1_GIN_64_5_1"
+
+
+def gen_checkpoint_fixture():
+    """The shipped checkpoint's 544 tensors and its wrapper chain, read
+    weights-only through inert stand-in classes (s-cgib_amd/refckpt.py — the
+    product's reader: this fixture pins it, tests/test_host_cpu.py re-reads
+    the file and compares), written as plain npz data for the GPU box."""
+    refckpt = importlib.import_module("s-cgib_amd.refckpt")
+    levels, cfg, sd = refckpt.read(CKPT)
+    out = {"sd/" + k: v.numpy() for k, v in sd.items()}
+    out["levels"] = np.array([f"{k}:{f}" for k, f in levels])
+    for k in ("hidden_dim", "k_transition", "gin_layers", "num_classes", "d_transfer",
+              "batch_size", "useAtt"):
+        out["cfg_" + k] = np.array(cfg[k])
+    for k in ("recons_type", "readout_f"):
+        out["cfg_" + k] = np.array(cfg[k])
+    np.savez_compressed(os.path.join(OUT, f"{CKPT_FIXTURE}.npz"), **out)
+    print(f"wrote {CKPT_FIXTURE}.npz  tensors={len(sd)} levels={levels}")
+    return levels, cfg, sd
+
+
+def gen_checkpoint_finetune_golden(models, util_mod, name, *, B, seed):
+    """BASELINE configs[4]: Mainmodel_finetuning (models.py:358-543) built on
+    the shipped pre_training_v1_GIN_64_5_1.pt — the reference's own classes
+    rebuilt in memory level by level (Mainmodel_continue x 3 around a
+    Mainmodel, each with its own transfer_d width, 5-GINConv encoders) and
+    loaded with the checkpoint's tensors (strict), then one ogbg-molhiv-like
+    fine-tune step (BCE) in train mode and a forward in eval mode (the
+    checkpoint's BatchNorm running statistics), with recorded noise."""
+    levels, cfg, sd = gen_checkpoint_fixture()
+    k, L, F = cfg["k_transition"], cfg["gin_layers"], levels[0][1]
+    torch.manual_seed(seed)
+    mols = synth.molecules(B, "molhiv", seed=seed, mu=12.0, sigma=4.0, F=F)
+    graphs, subgraphs = [], []
+    for ei, x in mols:
+        g = util_mod.load_dgl_fromPyG(SimpleNamespace(edge_index=torch.from_numpy(ei),
+                                                      x=torch.from_numpy(x)))
+        graphs.append(g)
+        subgraphs.append([D.khop_in_subgraph(g, v, k=k)[0] for v in g.nodes()])
+    batch_g = D.batch(graphs)
+    ego_g = D.batch(list(chain.from_iterable(subgraphs)))
+    batch_x = F_normalize(batch_g.ndata["x"].float())                 # train_molhiv.py
+    x_subs = F_normalize(ego_g.ndata["x"].float())
+    args = SimpleNamespace(recons_type=cfg["recons_type"], useAtt=cfg["useAtt"],
+                           readout_f=cfg["readout_f"], d_transfer=cfg["d_transfer"],
+                           device="cpu", batch_size=B, task="graph_classification",
+                           dataset="ogbg-molhiv")
+    real_load = models.torch.load
+    try:
+        m = None
+        for kind, f_in in reversed(levels):  # innermost first
+            if kind == "Mainmodel":
+                m = models.Mainmodel(args, f_in, hidden_dim=64, num_layers=4, num_heads=4,
+                                     k_transition=k, encoder="GIN")
+            else:
+                inner = m
+                models.torch.load = lambda *a, **kw: inner  # in-memory: nothing is unpickled
+                m = models.Mainmodel_continue(args, f_in, hidden_dim=64, num_layers=4,
+                                              num_heads=4, k_transition=k,
+                                              num_classes=cfg["num_classes"],
+                                              cp_filename="<mem>", encoder="GIN")
+        pre = m
+        for mod in pre.modules():  # the checkpoint's 5-GINConv encoders
+            if isinstance(mod, models.GIN):
+                _grow_gin(models, mod, L)
+        pre.load_state_dict(sd, strict=True)
+        models.torch.load = lambda *a, **kw: pre
+        model = models.Mainmodel_finetuning(args, F, hidden_dim=64, num_layers=4, num_heads=4,
+                                            k_transition=k, num_classes=1,
+                                            cp_filename="<mem>", encoder="GIN")
+    finally:
+        models.torch.load = real_load
+    for enc in (model.Encoder1, model.Encoder2):
+        _grow_gin(models, enc, L)
+    state0 = {kk: v.detach().clone() for kk, v in model.state_dict().items()
+              if not kk.startswith("model.")}  # model.*: the checkpoint fixture
+    trainable = [kk for kk, p in model.named_parameters() if p.requires_grad]
+    targets = torch.randint(0, 2, (B, 1)).float()
+    out = {"B": np.array(B), "k": np.array(k), "F": np.array(F), "L": np.array(L),
+           "num_classes": np.array(1), "dataset": np.array("ogbg-molhiv"),
+           "loss_kind": np.array("bce"), "checkpoint": np.array(CKPT_FIXTURE),
+           "batch_num_nodes": batch_g.batch_num_nodes().numpy(),
+           "src": batch_g.src.numpy(), "dst": batch_g.dst.numpy(),
+           "x_raw": batch_g.ndata["x"].numpy(),
+           "ego_batch_num_nodes": ego_g.batch_num_nodes().numpy(),
+           "ego_src": ego_g.src.numpy(), "ego_dst": ego_g.dst.numpy(),
+           "targets": targets.numpy(), "trainable": np.array(trainable)}
+    for mode in ("eval", "train"):  # eval first: the train step updates running stats
+        model.train(mode == "train")
+        torch.manual_seed(seed + (1000 if mode == "train" else 2000))
+        with _NoiseRecorder() as rec:
+            scores, *_ = model.forward(batch_g, batch_x, ego_g, x_subs, 1, batch_g.edges(), 2,
+                                       "cpu", B)
+        draws = rec.draws
+        assert len(draws) == 2 * B, len(draws)
+        out[f"{mode}_u_gate"] = torch.cat([draws[2 * i].reshape(-1) for i in range(B)]).numpy()
+        out[f"{mode}_u_feat"] = torch.cat([draws[2 * i + 1] for i in range(B)]).numpy()
+        out[f"{mode}_scores"] = scores.detach().numpy()
+        if mode == "train":
+            loss = model.loss(scores, targets)
+            loss.backward()
+            out["loss"] = loss.detach().numpy()
+    gptr = np.concatenate([[0], np.cumsum(out["batch_num_nodes"])])
+    node_graph = np.repeat(np.arange(B), out["batch_num_nodes"])
+    ego_owner = np.repeat(np.arange(len(out["ego_batch_num_nodes"])), out["ego_batch_num_nodes"])
+    out["ego_nodes_global"] = ego_g.ndata["_ID"].numpy() + gptr[node_graph[ego_owner]]
+    for kk, v in state0.items():
+        out["param_" + kk] = v.numpy()
+    for kk, p in model.named_parameters():
+        if p.grad is not None:
+            out["grad_" + kk] = p.grad.numpy()
+    np.savez_compressed(os.path.join(OUT, f"{name}.npz"), **out)
+    print(f"wrote {name}.npz  N={len(out['x_raw'])} loss={out['loss']:.6g} "
+          f"eval scores[:2]={out['eval_scores'][:2].ravel()} trainable={len(trainable)}")
+
+
 def gen_domainadapt_golden(models, util_mod, name, *, workload, F, B, k, num_classes, seed,
                            then_finetune=False):
     """Mainmodel_domainadapt (models.py:107-355) on a pretrained
@@ -464,6 +582,9 @@ def main():
     if sys.argv[1:] == ["round2"]:  # only the goldens added in round 2
         gen_round2(models, util)
         return
+    if sys.argv[1:] == ["checkpoint"]:  # only the shipped-checkpoint goldens (round 3)
+        gen_checkpoint_goldens(models, util)
+        return
     gen_ingest_and_ego(util)
     common = dict(B=8, chunk=4)
     gen_model_golden(models, util, "pretrain_L4_k1_qm9", workload="qm9", F=11, L=4, k=1,
@@ -484,6 +605,12 @@ def main():
                         dataset="ogbg-molhiv", num_classes=1, loss_kind="bce", seed=5)
     gen_domain_adaptation(models, util)
     gen_round2(models, util)
+    gen_checkpoint_goldens(models, util)
+
+
+def gen_checkpoint_goldens(models, util):
+    # BASELINE configs[4]: ogbg-molhiv fine-tune from pre_training_v1_GIN_64_5_1.pt
+    gen_checkpoint_finetune_golden(models, util, "finetune_molhiv_ckpt", B=8, seed=11)
 
 
 def gen_round2(models, util):

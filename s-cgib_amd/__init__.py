@@ -14,13 +14,15 @@ Layout:
   metrics.py   ROC-AUC (OGB semantics) and TU accuracy of the fine-tune configs
   optim.py     one-launch device Adam (drop-in for torch.optim.Adam as the scripts use it)
   cache.py     on-disk CSR cache of a molecule dataset (replaces the pts/ pickles)
+  refckpt.py   the reference's whole-module checkpoints, read weights-only
   dgl.py       drop-in ``dgl`` surface (graph, batch, sum_nodes, khop...)
   dist.py      one-process-per-GPU data parallel (RCCL all-reduce)
   synth.py     seeded synthetic molecules
 """
 import importlib
 
-__all__ = ["graph", "ops", "models", "dgl", "dist", "synth", "metrics", "optim", "cache", "_lib"]
+__all__ = ["graph", "ops", "models", "dgl", "dist", "synth", "metrics", "optim", "cache", "refckpt",
+           "_lib"]
 
 
 def __getattr__(name):

@@ -30,6 +30,7 @@ Differences from the reference, all deliberate:
 """
 from __future__ import annotations
 
+import os
 
 import torch
 import torch.nn as nn
@@ -37,6 +38,7 @@ import torch.nn.functional as F
 
 from . import graph as G
 from . import ops
+from . import refckpt
 
 
 class MLP(nn.Module):
@@ -708,8 +710,9 @@ def freeze_like_reference(model, num_layers=4):
 
 
 # ---------------------------------------------------------------------------
-# checkpoints: state_dict based (the reference pickles whole modules,
-# exp_pretraining.py:107; such files are not loaded here)
+# checkpoints: state_dict based.  The reference pickles whole modules
+# (exp_pretraining.py:107); those files are read weights-only through inert
+# stand-in classes (refckpt.py) and rebuilt from this package's classes.
 # ---------------------------------------------------------------------------
 _CKPT_ARGS = ("recons_type", "useAtt", "readout_f", "d_transfer", "gin_layers", "task",
               "batch_size")
@@ -724,39 +727,57 @@ def save_checkpoint(model, path, args=None, in_dim=None, num_classes=1):
         cfg = {k: getattr(args, k) for k in _CKPT_ARGS if hasattr(args, k)}
     cfg.update(kind=type(model).__name__, in_dim=in_dim, hidden_dim=model.hidden_dim,
                k_transition=model.k_transition, num_classes=num_classes)
-    inner = getattr(model, "model", None)  # wrapped pretrained model (continue / DA)
-    if inner is not None:
-        cfg["inner_kind"] = type(inner).__name__
-        if getattr(inner, "model", None) is not None:
-            cfg["inner_inner_kind"] = type(inner.model).__name__
+    levels, m = [], model  # the wrapper chain (continue / DA around a Mainmodel)
+    while m is not None:
+        levels.append([type(m).__name__, int(m.transfer_d.weight.shape[1])])
+        m = getattr(m, "model", None)
+    cfg["levels"] = levels
     torch.save({"config": cfg, "state_dict": model.state_dict()}, path)
 
 
 def load_checkpoint(cp, args):
-    """A Mainmodel / Mainmodel_continue from an in-memory module or a
-    save_checkpoint() file (weights only: nothing is unpickled)."""
+    """A Mainmodel / Mainmodel_continue / Mainmodel_domainadapt from an
+    in-memory module, a save_checkpoint() file, or one of the reference's
+    whole-module checkpoints (models.py:421, :1076; e.g. the shipped
+    pre_training_v1_GIN_64_5_1.pt) — all weights only: nothing in a file is
+    executed (refckpt.py)."""
     if isinstance(cp, nn.Module):
         return cp
-    blob = torch.load(cp, map_location="cpu", weights_only=True)
-    cfg = blob["config"]
+    if isinstance(cp, (str, os.PathLike)) and refckpt.is_reference_module_checkpoint(cp):
+        levels, cfg, sd = refckpt.read(cp)
+        cfg = dict(cfg, task=getattr(args, "task", None))
+    else:
+        blob = torch.load(cp, map_location="cpu", weights_only=True)
+        cfg, sd = blob["config"], blob["state_dict"]
+        levels = cfg.get("levels")
+        if levels is None:  # round-2 files: up to two wrapped levels, one F
+            kinds = [cfg.get("kind"), cfg.get("inner_kind"), cfg.get("inner_inner_kind")]
+            kinds = [k for k in kinds if k] + ([] if "Mainmodel" in kinds else ["Mainmodel"])
+            levels = [[k, cfg["in_dim"]] for k in kinds]
+    return model_from_state(levels, cfg, sd, args)
+
+
+def model_from_state(levels, cfg, sd, args=None):
+    """The wrapper chain ``levels`` = [(kind, F), ...] (outermost first) built
+    from this package's classes with ``cfg``'s sizes, ``sd`` loaded strictly."""
     ns = type("Args", (), {})()
     for k in _CKPT_ARGS:
         setattr(ns, k, cfg.get(k, getattr(args, k, None)))
     if ns.task is None:
         ns.task = "graph_classification"
-    kind = cfg.get("kind")
-    m = _build_kind(kind, ns, cfg, cfg.get("inner_kind"), cfg.get("inner_inner_kind"))
-    m.load_state_dict(blob["state_dict"])
+    m = _build_levels([(str(k), int(f)) for k, f in levels], ns, cfg)
+    m.load_state_dict(sd)
     return m
 
 
-def _build_kind(kind, ns, cfg, inner_kind=None, inner_inner_kind=None):
-    """An untrained module of checkpoint kind ``kind`` (nested wrappers are
-    rebuilt around the kinds they wrapped) for load_state_dict."""
-    dims = (cfg["in_dim"], cfg["hidden_dim"], 4, 4, cfg["k_transition"])
+def _build_levels(levels, ns, cfg):
+    """An untrained module for load_state_dict: levels = [(kind, F), ...] from
+    the outermost wrapper down to the Mainmodel it wraps."""
+    (kind, f_in), rest = levels[0], levels[1:]
+    dims = (f_in, cfg["hidden_dim"], 4, 4, cfg["k_transition"])
     if kind == "Mainmodel":
         return Mainmodel(ns, *dims, "GIN")
-    inner = _build_kind(inner_kind or "Mainmodel", ns, cfg, inner_inner_kind)
+    inner = _build_levels(rest or [("Mainmodel", f_in)], ns, cfg)
     if kind == "Mainmodel_continue":
         return Mainmodel_continue(ns, *dims, cfg.get("num_classes", 1), inner, "GIN")
     if kind == "Mainmodel_domainadapt":

@@ -915,3 +915,59 @@ def test_device_noise_replays_through_explicit_path(pkg, dev):
     pkg.ops.seed_noise(dev, 1234)
     m1(g, x, None, None, None, 1, None, 1, dev, 64)
     assert torch.equal(m1._last_noise[1], uf) and torch.equal(m1._last_noise[0], ug)
+
+
+# ---------------------------------------------------------------------------
+# BASELINE configs[4]: fine-tune from the shipped pre_training_v1_GIN_64_5_1.pt
+# (its 544 tensors read weights-only through refckpt.py into the fixture
+# ckpt_pre_training_v1_GIN_64_5_1.npz; the golden is the reference's own
+# Mainmodel_finetuning on the same tensors, oracle/gen_golden.py)
+# ---------------------------------------------------------------------------
+def checkpoint_fixture(pkg):
+    d = load_golden("ckpt_pre_training_v1_GIN_64_5_1")
+    levels = [(s.split(":")[0], int(s.split(":")[1])) for s in d["levels"].tolist()]
+    cfg = {k[4:]: (v.item() if v.dtype.kind in "iuf" else str(v)) for k, v in d.items()
+           if k.startswith("cfg_")}
+    sd = {k[3:]: torch.tensor(v) for k, v in d.items() if k.startswith("sd/")}
+    return levels, cfg, sd
+
+
+def test_finetune_from_shipped_checkpoint(pkg, dev):
+    from types import SimpleNamespace
+    g = load_golden("finetune_molhiv_ckpt")
+    levels, cfg, sd = checkpoint_fixture(pkg)
+    assert len(sd) == 544 and [k for k, _ in levels] == ["Mainmodel_continue"] * 3 + ["Mainmodel"]
+    args = SimpleNamespace(recons_type="adj", useAtt=1, readout_f="sum", d_transfer=32,
+                           batch_size=int(g["B"]), gin_layers=int(g["L"]),
+                           task="graph_classification", dataset=str(g["dataset"]), device=dev)
+    pre = pkg.models.model_from_state(levels, cfg, sd, args)
+    ft = pkg.models.Mainmodel_finetuning(args, int(g["F"]), 64, 4, 4, int(g["k"]), 1, pre, "GIN")
+    own = {k[6:]: torch.tensor(v) for k, v in g.items() if k.startswith("param_")}
+    missing, unexpected = ft.load_state_dict(own, strict=False)
+    assert not unexpected and all(k.startswith("model.") for k in missing), (missing, unexpected)
+    ft = ft.to(dev)
+    trainable = {n for n, p in ft.named_parameters() if p.requires_grad}
+    assert trainable == set(str(s) for s in g["trainable"])  # the freezing quirk
+    bg = pkg.graph.GraphBatch.from_edges(g["src"], g["dst"], len(g["x_raw"]), True,
+                                         g["batch_num_nodes"]).to(dev)
+    x = F.normalize(torch.tensor(g["x_raw"]).float()).to(dev)
+    B = int(g["B"])
+    # eval: the checkpoint's BatchNorm running statistics (noise still applied)
+    ft.eval()
+    noise = (torch.tensor(g["eval_u_gate"], device=dev), torch.tensor(g["eval_u_feat"], device=dev))
+    with torch.no_grad():
+        scores, *_ = ft(bg, x, None, None, 1, None, 2, dev, B, noise=noise)
+    assert rel_err(scores.cpu(), g["eval_scores"]) < 1e-4
+    # one train-mode fine-tune step: scores, BCE loss, the trainable gradients
+    ft.train()
+    noise = (torch.tensor(g["train_u_gate"], device=dev),
+             torch.tensor(g["train_u_feat"], device=dev))
+    scores, *_ = ft(bg, x, None, None, 1, None, 2, dev, B, noise=noise)
+    assert rel_err(scores.detach().cpu(), g["train_scores"]) < 1e-4
+    loss = ft.loss(scores, torch.tensor(g["targets"], device=dev))
+    assert rel_err(loss.item(), g["loss"]) < 1e-4
+    loss.backward()
+    params = dict(ft.named_parameters())
+    check_grads_model({k[5:]: v for k, v in g.items() if k.startswith("grad_")},
+                      lambda n: params[n].grad, tol=1e-3)
+    assert all(p.grad is None for n, p in params.items() if n not in trainable)

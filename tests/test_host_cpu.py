@@ -387,3 +387,56 @@ def test_slab_scope_rules(pkg, monkeypatch):
     assert not c.usable((w,))
     h.remove()
     assert c.usable((w,))
+
+
+REF_CKPT = "/root/reference/outputs/pre_training_v1_GIN_64_5_1.pt"
+
+
+def _ckpt_fixture():
+    d = load_golden("ckpt_pre_training_v1_GIN_64_5_1")
+    levels = [(s.split(":")[0], int(s.split(":")[1])) for s in d["levels"].tolist()]
+    cfg = {k[4:]: (v.item() if v.dtype.kind in "iuf" else str(v)) for k, v in d.items()
+           if k.startswith("cfg_")}
+    sd = {k[3:]: torch.tensor(v) for k, v in d.items() if k.startswith("sd/")}
+    return levels, cfg, sd
+
+
+@pytest.mark.skipif(not os.path.exists(REF_CKPT), reason="the reference tree is not here")
+def test_reference_checkpoint_reads_weights_only(pkg):
+    """refckpt.read on the shipped whole-module pickle (models.py:421):
+    weights-only through inert stand-ins, the same 544 tensors as the
+    committed fixture, and models.load_checkpoint rebuilds the 4-level
+    wrapper chain with them (strict)."""
+    levels, cfg, sd = pkg.refckpt.read(REF_CKPT)
+    f_levels, f_cfg, f_sd = _ckpt_fixture()
+    assert levels == f_levels and set(sd) == set(f_sd) and len(sd) == 544
+    for k, v in sd.items():
+        assert torch.equal(v, f_sd[k]), k
+    assert cfg["gin_layers"] == 5 and cfg["k_transition"] == 1 and cfg["in_dim"] == 9
+    args = type("A", (), {"task": "graph_classification"})()
+    m = pkg.models.load_checkpoint(REF_CKPT, args)
+    assert type(m).__name__ == "Mainmodel_continue"
+    assert type(m.model.model.model).__name__ == "Mainmodel"
+    got = m.state_dict()
+    assert all(torch.equal(got[k], v) for k, v in sd.items())
+
+
+def test_checkpoint_levels_roundtrip(pkg, tmp_path):
+    """The fixture's 4-level chain (each level its own transfer_d width)
+    through save_checkpoint / load_checkpoint (weights only), and a file
+    naming a class outside the known set is refused before loading."""
+    levels, cfg, sd = _ckpt_fixture()
+    m = pkg.models.model_from_state(levels, cfg, sd)
+    path = str(tmp_path / "ckpt.pt")
+    args = type("A", (), {"recons_type": "adj", "useAtt": 1, "readout_f": "sum",
+                          "d_transfer": 32, "gin_layers": 5, "task": "graph_classification",
+                          "batch_size": 16})()
+    pkg.models.save_checkpoint(m, path, args, in_dim=levels[0][1])
+    m2 = pkg.models.load_checkpoint(path, args)
+    s2 = m2.state_dict()
+    assert set(s2) == set(sd) and all(torch.equal(s2[k], v) for k, v in sd.items())
+    bad = str(tmp_path / "bad.pt")
+    torch.save({"x": torch.zeros(1)}, bad)
+    assert not pkg.refckpt.is_reference_module_checkpoint(bad)
+    with pytest.raises(pkg.refckpt.RefCheckpointError):
+        pkg.refckpt.read(bad)

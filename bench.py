@@ -132,6 +132,12 @@ def layer_bwd_flops(n, e, d_in):
 # launch it, a filter on the launch sizes, §8(d) bytes, flops, and the PMC
 # name prefixes of its template instances in the traffic file)
 KERNELS = {
+    "gin_pair_fwd_k": dict(entries=("scgib_gin_pair_fwd",), keep=lambda m: True,
+                           bytes=pair_fwd_bytes, flops=pair_fwd_flops, pmc=["gin_pair_fwd_k"],
+                           desc="persistent encoder-pair forward: both GIN-64xL encoders "
+                                "(transfer_d folded, ego readout, compressor[0]) in one launch, "
+                                "chunk-resident rows, f32 MFMA 16x16x4, in-kernel BatchNorm "
+                                "exchange"),
     "gin_fwd_k": dict(entries=("scgib_gin_layer0_fwd", "scgib_gin_layer_fwd_bn"),
                       keep=lambda m: True, bytes=agg_fwd_bytes, flops=layer_fwd_flops,
                       pmc=["gin_fwd_k<32, false, true, true,", "gin_fwd_k<64, true, true,",
@@ -153,6 +159,23 @@ KERNELS = {
                       pmc=["gin_bwd_k<32, true, true,"],
                       desc="layer-0 backward with transfer_d folded (d_in = 32)"),
 }
+
+
+def _call_meta(fn, m):
+    """bytes / flops of one launch from its meta: per-layer kernels take
+    (n, e, d_in); the persistent pair forward its own meta (layers list)."""
+    return fn(m) if "layers" in m else fn(m["n"], m["e"], m["d_in"])
+
+
+def pair_fwd_bytes(m):
+    """§8(d) aggregation bytes of every layer of both encoders (d = 32 for the
+    transfer_d-folded layer 0, 64 after): the algorithmic bytes of the
+    persistent encoder-pair forward launch."""
+    return sum(agg_bytes(n, e, d) for n, e, d in m["layers"])
+
+
+def pair_fwd_flops(m):
+    return sum(layer_fwd_flops(n, e, d) for n, e, d in m["layers"])
 
 
 class KernelTimer:
@@ -201,8 +224,8 @@ class KernelTimer:
         if not rec:
             return None
         ms = [s.elapsed_time(e) / self.REPEAT for s, e, _ in rec]
-        byts = [spec["bytes"](m["n"], m["e"], m["d_in"]) for _, _, m in rec]
-        fl = [spec["flops"](m["n"], m["e"], m["d_in"]) for _, _, m in rec]
+        byts = [_call_meta(spec["bytes"], m) for _, _, m in rec]
+        fl = [_call_meta(spec["flops"], m) for _, _, m in rec]
         k = len(ms)
         avg_ms = sum(ms) / k
         avg_b, avg_f = sum(byts) / k, sum(fl) / k

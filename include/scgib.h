@@ -241,6 +241,112 @@ int scgib_gin_layer_bwd(const float *dy, const float *z2, const float *r, const 
                         const float *w2, int64_t n_nodes, float *dagg, float *slab,
                         float *wgrad, const int32_t *dims, const scgib_bn_bwd_pending *pending,
                         scgib_stream_t stream);
+/* ---- A4+A5+A6 persistent: both encoders' forward in ONE launch ----------------
+ * Replaces, in training mode, the encoder pair of Mainmodel.extract_features
+ * (models.py:702-716 / :1204-1213): h = transfer_d(x) (:668-669) and
+ * Encoder1(batch_g, h), Encoder2(ego-nets, h[_ID]) — GIN-64 x L (models.py:
+ * 52-72: GINConv(MLP) + BatchNorm1d (batch statistics) + ReLU per layer) —
+ * the ego readout dgl.sum_nodes (:716) and compressor[0] on Encoder1's output
+ * (:596).  Each workgroup owns one CHUNK of one encoder: the components
+ * (molecules / ego-nets) whose first row lies in a 64-row window, at most
+ * scgib_gin_pair_max_component() rows each, so every neighbour a row gathers
+ * is a row the same workgroup computed; the chunk's rows stay in LDS across
+ * the layers.  BatchNorm's batch statistics are exchanged per layer through
+ * chunk -> group -> publisher partials (fp64, fixed order) with agent-scope
+ * atomics; every spin is bounded (timeout: sync[1] != 0).  The grid holds
+ * both encoders' chunks at once: valid only when scgib_gin_pair_chunks() of
+ * both fits scgib_gin_pair_slots() (co-resident workgroups).
+ * Writes exactly what the per-layer path saves for the backward (agg, r,
+ * z2, stat per layer, aggx), updates the running statistics, and the
+ * outputs: out = relu(BN(z2 of the last layer)), the per-component readout
+ * and row -> component map (readout != NULL), lin_out = Linear(out)
+ * (lin_w != NULL).  Capacity mode: dims = device [n, e], rows past n zeroed. */
+#define SCGIB_PAIR_MAX_LAYERS 6
+typedef struct {
+    const int32_t *rowptr, *col;  /* symmetric CSR (components closed) */
+    const int32_t *comp_ptr;      /* [n_comp + 1] component starts (entries past the
+                                     actual count equal the row count) */
+    int64_t n_comp;               /* components (capacity) */
+    const int32_t *dims;          /* device [n, e] or NULL */
+    int64_t n_cap;                /* rows (capacity) */
+    const int32_t *node_map;      /* layer-0 row -> row of x, or NULL (identity) */
+    const float *w1[SCGIB_PAIR_MAX_LAYERS], *b1[SCGIB_PAIR_MAX_LAYERS];
+    const float *w2[SCGIB_PAIR_MAX_LAYERS], *b2[SCGIB_PAIR_MAX_LAYERS];
+    const float *gamma[SCGIB_PAIR_MAX_LAYERS], *beta[SCGIB_PAIR_MAX_LAYERS];
+    float one_plus_eps[SCGIB_PAIR_MAX_LAYERS], bn_eps[SCGIB_PAIR_MAX_LAYERS];
+    float momentum[SCGIB_PAIR_MAX_LAYERS];
+    float *running_mean[SCGIB_PAIR_MAX_LAYERS], *running_var[SCGIB_PAIR_MAX_LAYERS];
+    int64_t *num_batches_tracked[SCGIB_PAIR_MAX_LAYERS];
+    float *agg[SCGIB_PAIR_MAX_LAYERS], *r[SCGIB_PAIR_MAX_LAYERS];
+    float *z2[SCGIB_PAIR_MAX_LAYERS], *stat[SCGIB_PAIR_MAX_LAYERS];
+    float *aggx;                  /* [n][16] layer-0 gathered raw features */
+    float *out;                   /* [n][64] */
+    float *readout;               /* [n_comp][64] or NULL */
+    int32_t *seg;                 /* [n] with readout */
+    const float *lin_w, *lin_b;   /* Linear(64, 64) on out, or NULL */
+    float *lin_out;
+    void *ws;                     /* scgib_gin_pair_ws_bytes(n_cap, n_layers) bytes */
+    uint32_t *counters;           /* scgib_gin_pair_counters(n_cap, n_layers) ZEROED words,
+                                     left zeroed */
+} scgib_pair_encoder;
+typedef struct {
+    scgib_pair_encoder enc[2];    /* enc[0] (the ego-nets) takes the first chunks */
+    const float *x;               /* [*][n_feat] raw (normalised) features */
+    int32_t n_feat;               /* <= 16 */
+    const float *wt;              /* transfer_d.weight [32][n_feat] */
+    int32_t n_layers;             /* <= SCGIB_PAIR_MAX_LAYERS */
+    uint32_t *sync;               /* 4 ZEROED words: [0] exit count (left zeroed),
+                                     [1] timeout code (0: none) */
+} scgib_pair_fwd_args;
+/* The backward of scgib_gin_pair_fwd, the same way: one workgroup per chunk,
+ * d h of the chunk's rows kept in LDS from layer to layer (the transposed
+ * aggregation never leaves the chunk), per layer the BatchNorm-backward sums
+ * (dbeta = sum dy, dgamma = sum dy xhat) exchanged as in the forward, then
+ * dz2 = scale (dy - dbeta/N - xhat dgamma/N), dW2 += dz2^T r, dr = dz2 W2,
+ * dz1 = dr [r > 0], dW1 += dz1^T agg, d(agg) = dz1 W1, and for layer 0
+ * dWt += d(agg0)^T aggx (models.py:52-72, :668-669 under autograd).  Incoming:
+ * g_out [n][64] and / or g_readout [n_comp][64] (the ego readout's gradient,
+ * broadcast to the component's rows); with lin_g, compressor[0]'s backward
+ * first: d out = g_out + lin_g W0, dW0 += lin_g^T lin_in (models.py:596).
+ * Weight gradients: one partial per chunk in slab[l] (row c at c * stride[l]:
+ * dW2[64*64] | dW1[64*d_in] | db2[64] | db1[64] | layer 0: dWt[32*16] at
+ * 64*64 + 64*32 + 128, i.e. scgib_gin_layer_bwd's wgrad layout), lin_slab
+ * (dW0[64*64] | db0[64]); summed afterwards by scgib_slab_reduce_multi. */
+typedef struct {
+    const int32_t *rowptr, *col, *comp_ptr;
+    int64_t n_comp;
+    const int32_t *dims;
+    int64_t n_cap;
+    const float *agg[SCGIB_PAIR_MAX_LAYERS], *r[SCGIB_PAIR_MAX_LAYERS];
+    const float *z2[SCGIB_PAIR_MAX_LAYERS], *stat[SCGIB_PAIR_MAX_LAYERS];
+    const float *w1[SCGIB_PAIR_MAX_LAYERS], *w2[SCGIB_PAIR_MAX_LAYERS];
+    float one_plus_eps[SCGIB_PAIR_MAX_LAYERS];
+    const float *aggx;
+    const float *g_out, *g_readout;
+    const float *lin_g, *lin_w, *lin_in;
+    float *dgamma[SCGIB_PAIR_MAX_LAYERS], *dbeta[SCGIB_PAIR_MAX_LAYERS];
+    float *slab[SCGIB_PAIR_MAX_LAYERS];
+    int64_t slab_stride[SCGIB_PAIR_MAX_LAYERS];
+    float *lin_slab;
+    void *ws;                     /* scgib_gin_pair_ws_bytes(n_cap, n_layers) bytes */
+    uint32_t *counters;           /* scgib_gin_pair_counters(...) ZEROED words, left zeroed */
+} scgib_pair_bwd_encoder;
+typedef struct {
+    scgib_pair_bwd_encoder enc[2];
+    int32_t n_layers;
+    int32_t n_feat;
+    uint32_t *sync;               /* as scgib_pair_fwd_args.sync */
+} scgib_pair_bwd_args;
+int64_t scgib_gin_pair_bwd_args_bytes(void);
+int scgib_gin_pair_bwd(const scgib_pair_bwd_args *args, scgib_stream_t stream);
+int64_t scgib_gin_pair_args_bytes(void);  /* sizeof(scgib_pair_fwd_args): binding check */
+int32_t scgib_gin_pair_max_component(void);
+int64_t scgib_gin_pair_chunks(int64_t n_cap);
+int64_t scgib_gin_pair_slots(void);
+int64_t scgib_gin_pair_ws_bytes(int64_t n_cap, int32_t n_layers);
+int64_t scgib_gin_pair_counters(int64_t n_cap, int32_t n_layers);
+int scgib_gin_pair_fwd(const scgib_pair_fwd_args *args, scgib_stream_t stream);
+
 /* ---- A6: per-segment readouts (dgl.sum_nodes) -------------------------------
  * out[s,:] = sum_{i in [ptr[s], ptr[s+1])} x[i,:]   (models.py:716, 725, 733)
  * segment_broadcast is its adjoint: out[i,:] = g[s,:] for every row i of s.

@@ -1,0 +1,1118 @@
+// Persistent forward of the encoder pair (include/scgib.h, scgib_gin_pair_fwd):
+// Encoder2 over the ego-nets and Encoder1 over the molecules (models.py:702-716,
+// GIN-64 x L of models.py:52-72 with transfer_d folded into layer 0, the ego
+// readout dgl.sum_nodes and compressor[0] on Encoder1's output) in ONE launch.
+//
+// Why: the per-layer kernels (gin_fwd_k) spend ~2/3 of each 18-20 us launch
+// outside their GEMMs at QM9 B512 — kernel boundary, the weights and the
+// deferred BatchNorm partials arriving at every workgroup's start, and the
+// dependent CSR -> neighbour-row gather chain — once per layer.  Here:
+//   * chunk c of an encoder = the components (molecules / ego-nets) whose
+//     first row lies in rows [64c, 64c + 64): <= 96 rows when no component
+//     exceeds 33 rows.  Every neighbour of a chunk row is a row of the same
+//     chunk (components are closed), so ONE workgroup per chunk owns all the
+//     rows it ever gathers: the chunk's local CSR is loaded once, its rows
+//     stay in LDS from layer to layer, and no row crosses a workgroup;
+//   * per layer: aggregation from LDS (BN + ReLU of the previous layer applied
+//     on read), z1 = agg W1^T, r = relu(z1 + b1), z2 = r W2^T + b2 on the f32
+//     MFMA v_mfma_f32_16x16x4_f32 (16-row blocks: a chunk pays for
+//     ceil(rows / 16) blocks), the wave's 16 weight columns held in VGPRs and
+//     the next layer's fetched during the BatchNorm exchange;
+//   * BatchNorm's batch statistics: each chunk's (n, sum, centred M2) ->
+//     16-chunk groups combined by the group's last arriver (fp64, fixed
+//     order) -> the last group's arriver combines the groups, updates the
+//     running statistics and publishes (scale, shift) behind a flag; every
+//     workgroup polls that one word.  All cross-workgroup words are
+//     agent-scope atomics on both sides (MI355X_MICROARCH.md, valid forms);
+//     every spin is bounded (timeout -> sync[1], never a hang).
+// The whole grid (both encoders' chunks) must be co-resident: the host
+// launches it only when it fits scgib_gin_pair_slots() (3 workgroups per CU:
+// 51 KB of LDS, <= 168 VGPRs) and falls back to the per-layer kernels
+// otherwise.  Writes what the per-layer path saves for the backward (agg, r,
+// z2, stat per layer, aggx), so the backward is unchanged.
+//
+// LDS images are [row][64] floats with the float4 slots XOR-swizzled by the
+// row (slot q of row r at q ^ (r & 15)): the MFMA operand reads (16 rows x one
+// float4 per lane, ds_read_b128) and the row-wise VALU accesses are both
+// bank-conflict free without padding.
+#include "mfma_tile.h"
+
+namespace scgib {
+namespace pair {
+
+constexpr int kWin = 64;                 // chunk window (rows)
+constexpr int kRows = 96;                // max rows per chunk
+constexpr int kMaxComp = kRows - kWin + 1;  // max component rows (33)
+constexpr int kNrb = kRows / 16;         // 16-row blocks
+constexpr int kMaxE = 256;               // chunk edges cached in LDS (else read from global)
+constexpr int kGrp = 16;                 // chunk partials per group
+constexpr int kPart = 132;               // floats per chunk partial: S[64] M2[64] n pad[3]
+constexpr int kGPart = 130;              // doubles per group partial: n S[64] M2[64] pad
+constexpr int kL = SCGIB_PAIR_MAX_LAYERS;
+constexpr uint64_t kTimeout = 20000000;  // 0.2 s of the 100 MHz wall clock per spin
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ int sidx(int row, int col) {
+    return row * 64 + ((((col >> 2) ^ (row & 15)) << 2) | (col & 3));
+}
+
+__host__ __device__ inline int64_t n_chunks(int64_t n_cap) { return (n_cap + kWin - 1) / kWin; }
+__host__ __device__ inline int64_t n_groups(int64_t n_cap) { return (n_chunks(n_cap) + kGrp - 1) / kGrp; }
+
+// workspace layout (per encoder): chunk partials | group partials | (scale, shift)
+struct Ws {
+    float *part;     // [L][nch][kPart]
+    double *gpart;   // [L][ngr][kGPart]
+    float *ss;       // [L][128]
+};
+__host__ __device__ inline int64_t ws_part_floats(int64_t n_cap) { return n_chunks(n_cap) * kPart; }
+__host__ __device__ inline int64_t ws_bytes(int64_t n_cap, int L) {
+    return L * (ws_part_floats(n_cap) * 4 + n_groups(n_cap) * kGPart * 8 + 128 * 4) + 64;
+}
+__device__ inline Ws ws_of(void *ws, int64_t n_cap, int L) {
+    char *p = reinterpret_cast<char *>((reinterpret_cast<uintptr_t>(ws) + 15) & ~uintptr_t(15));
+    Ws w;
+    w.gpart = reinterpret_cast<double *>(p);
+    p += static_cast<int64_t>(L) * n_groups(n_cap) * kGPart * 8;
+    w.part = reinterpret_cast<float *>(p);
+    p += static_cast<int64_t>(L) * ws_part_floats(n_cap) * 4;
+    w.ss = reinterpret_cast<float *>(p);
+    return w;
+}
+// counters (per encoder): group arrivals [kL][ngr] | publisher arrivals [kL] | flags [kL]
+__host__ __device__ inline int64_t n_counters(int64_t n_cap, int) { return kL * (n_groups(n_cap) + 2); }
+
+struct Smem {
+    alignas(16) float buf0[kRows * 64];   // z2 of the previous layer / aggx / r / z2
+    alignas(16) float buf1[kRows * 64];   // agg / the final output; scratch of the BN combines
+    int32_t rp[kRows + 1];    // chunk-local row pointers (edge offsets from the chunk's first)
+    int32_t colv[kMaxE];      // chunk-local neighbour rows
+    int32_t cs[kRows + 2];    // chunk-local component starts (readout)
+    float ss[128];            // (scale, shift) of the previous layer's BatchNorm
+    int32_t sb[2][4];         // bound searches: lo, hi, first hit
+    unsigned flag;            // block-wide broadcast of a ticket / last-arriver flag
+    alignas(16) float red[4][128];  // backward: the waves' column sums; exchange scratch
+};
+
+__device__ __forceinline__ uint64_t now() { return wall_clock64(); }
+
+__device__ __forceinline__ void set_err(uint32_t *sync, unsigned code) {
+    __hip_atomic_store(sync + 1, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Count this workgroup in (every wave's stores drained first) and return the
+// value the counter held before (block-uniform).
+__device__ __forceinline__ unsigned arrive(unsigned *counter, Smem &sm) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0)
+        sm.flag = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    return sm.flag;
+}
+
+// Two lower bounds at once: threads 0..127 find the first i in [0, C] with
+// gp[i] >= t0, threads 128..255 with gp[i] >= t1 (gp non-decreasing; C when
+// none), by 128-way sampling rounds.  Returns this half's index in sm.sb[h][0].
+__device__ void lower_bounds(const int32_t *__restrict__ gp, int64_t C, int t0, int t1, Smem &sm) {
+    const int h = threadIdx.x >> 7, j = threadIdx.x & 127;
+    const int tgt = h ? t1 : t0;
+    if (j == 0) {
+        sm.sb[h][0] = 0;
+        sm.sb[h][1] = static_cast<int>(C);
+    }
+    __syncthreads();
+    for (int round = 0; round < 5; ++round) {
+        const int lo = sm.sb[h][0], hi = sm.sb[h][1];
+        const bool more = sm.sb[0][0] < sm.sb[0][1] || sm.sb[1][0] < sm.sb[1][1];
+        __syncthreads();
+        if (!more) break;  // block-uniform
+        if (j == 0) sm.sb[h][2] = 128;
+        __syncthreads();
+        const int n = hi - lo, step = (n + 127) / 128;
+        const int p = lo + j * step;
+        if (lo < hi && p < hi && gp[p] >= tgt) atomicMin(&sm.sb[h][2], j);
+        __syncthreads();
+        if (j == 0 && lo < hi) {
+            const int f = sm.sb[h][2];
+            if (f < 128) {
+                sm.sb[h][1] = lo + f * step;
+                sm.sb[h][0] = f > 0 ? lo + (f - 1) * step + 1 : lo;
+            } else {
+                const int last = (n - 1) / step;  // the last sampled j
+                sm.sb[h][0] = lo + last * step + 1;
+            }
+        }
+        __syncthreads();
+    }
+}
+
+// weight fragments of wave w (output columns 16 w + (lane & 15)) for the
+// 16x16x4 MFMA with the k order permuted per ds_read_b128: step 4 j + t of
+// lane group g = lane >> 4 covers k = 16 j + 4 g + t
+template <int K>
+__device__ __forceinline__ void load_frag(const float *__restrict__ W, float (&f)[16]) {
+    const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const float *row = W + static_cast<int64_t>(16 * w + (l & 15)) * K + 4 * (l >> 4);
+#pragma unroll
+    for (int j = 0; j < K / 16; ++j) {
+        const float4 v = *reinterpret_cast<const float4 *>(row + 16 * j);
+        f[4 * j] = v.x; f[4 * j + 1] = v.y; f[4 * j + 2] = v.z; f[4 * j + 3] = v.w;
+    }
+}
+
+// acc[rb] = A[16 rb .. 16 rb + 15][0..K) W^T (wave's 16 columns), rb < nrb
+template <int K>
+__device__ __forceinline__ void gemm(const float *A, const float (&f)[16], int nrb, f32x4 (&acc)[kNrb]) {
+    const int l = threadIdx.x & 63, r16 = l & 15, g = l >> 4;
+#pragma unroll
+    for (int rb = 0; rb < kNrb; ++rb) {
+        acc[rb] = f32x4{0.f, 0.f, 0.f, 0.f};
+        if (rb < nrb) {  // block-uniform
+            const int row = 16 * rb + r16;
+#pragma unroll
+            for (int j = 0; j < K / 16; ++j) {
+                const float4 a = *reinterpret_cast<const float4 *>(A + sidx(row, 16 * j + 4 * g));
+                acc[rb] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, f[4 * j], acc[rb], 0, 0, 0);
+                acc[rb] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, f[4 * j + 1], acc[rb], 0, 0, 0);
+                acc[rb] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.z, f[4 * j + 2], acc[rb], 0, 0, 0);
+                acc[rb] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, f[4 * j + 3], acc[rb], 0, 0, 0);
+            }
+        }
+    }
+}
+
+// accumulator element i of row block rb: row 16 rb + 4 (lane >> 4) + i, column
+// 16 w + (lane & 15)
+__device__ __forceinline__ int acc_row16(int rb, int i) { return 16 * rb + 4 * ((threadIdx.x & 63) >> 4) + i; }
+__device__ __forceinline__ int acc_col16() { return 16 * (threadIdx.x >> 6) + (threadIdx.x & 15); }
+
+// copy rows [0, nr) of an LDS image (width cols) to global rows g0.. (float4 lanes)
+template <int COLS>
+__device__ __forceinline__ void lds_to_global(const float *S, float *__restrict__ dst, int64_t g0, int nr) {
+    constexpr int Q = COLS / 4;
+    for (int idx = threadIdx.x; idx < nr * Q; idx += 256) {
+        const int v = idx / Q, q = idx % Q;
+        st4(dst + (g0 + v) * COLS + 4 * q, *reinterpret_cast<const float4 *>(S + sidx(v, 4 * q)));
+    }
+}
+
+// zero rows [r0, r1) x COLS of a global array
+template <int COLS>
+__device__ __forceinline__ void zero_rows(float *__restrict__ dst, int64_t r0, int64_t r1) {
+    constexpr int Q = COLS / 4;
+    for (int64_t idx = threadIdx.x; idx < (r1 - r0) * Q; idx += 256)
+        st4(dst + (r0 + idx / Q) * COLS + 4 * (idx % Q), make_float4(0.f, 0.f, 0.f, 0.f));
+}
+
+struct Layer {  // this layer's per-encoder constants
+    float ope, eps, mom;
+    const float *gamma, *beta;
+    float *rmean, *rvar, *stat;
+    int64_t *nbt;
+};
+
+// The BatchNorm exchange of layer l for chunk c (rows nr): chunk partial from
+// the z2 accumulators -> group -> publisher -> (scale, shift) into sm.ss.
+__device__ void bn_exchange(const f32x4 (&z)[kNrb], int nrb, int nr, int64_t c, int64_t nch,
+                            int64_t ngr, int l, const Ws &ws, unsigned *cnt, const Layer &Ly,
+                            uint32_t *sync, Smem &sm) {
+    const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4;
+    const int col = acc_col16();
+    // ---- chunk partial: column sum and centred M2 over the valid rows (fp32)
+    float s = 0.f;
+#pragma unroll
+    for (int rb = 0; rb < kNrb; ++rb)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            if (rb < nrb && acc_row16(rb, i) < nr) s += z[rb][i];
+    s += __shfl_xor(s, 16, kWave);
+    s += __shfl_xor(s, 32, kWave);
+    const float mean = nr > 0 ? s / static_cast<float>(nr) : 0.f;
+    float q = 0.f;
+#pragma unroll
+    for (int rb = 0; rb < kNrb; ++rb)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            if (rb < nrb && acc_row16(rb, i) < nr) {
+                const float d = z[rb][i] - mean;
+                q += d * d;
+            }
+    q += __shfl_xor(q, 16, kWave);
+    q += __shfl_xor(q, 32, kWave);
+    float *part = ws.part + (static_cast<int64_t>(l) * nch + c) * kPart;
+    if (g == 0) {
+        st_agent(part + col, s);
+        st_agent(part + 64 + col, q);
+    }
+    if (tid == 0) st_agent(part + 128, static_cast<float>(nr));
+    // ---- group combine by the group's last arriving chunk
+    const int64_t grp = c / kGrp, g0 = grp * kGrp;
+    const int gsize = static_cast<int>(nch - g0 < kGrp ? nch - g0 : kGrp);
+    unsigned *gcnt = cnt + static_cast<int64_t>(l) * ngr + grp;
+    unsigned *pub = cnt + static_cast<int64_t>(ngr) * kL + l;           // publisher arrivals
+    unsigned *flag = cnt + static_cast<int64_t>(ngr) * kL + kL + l;     // published
+    double *dscr = reinterpret_cast<double *>(sm.buf1);                 // 4 KB of scratch
+    const int ch = tid & 63, p = tid >> 6;
+    const Ws &W = ws;
+    bool publisher = false;
+    if (arrive(gcnt, sm) == static_cast<unsigned>(gsize - 1)) {
+        // partition p takes chunks g0 + p + 4 u (fixed order), channel ch
+        float S[4], Q[4], N[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int k = p + 4 * u;
+            const float *pp = W.part + (static_cast<int64_t>(l) * nch + g0 + (k < gsize ? k : 0)) * kPart;
+            S[u] = ld_agent(pp + ch);
+            Q[u] = ld_agent(pp + 64 + ch);
+            N[u] = k < gsize ? ld_agent(pp + 128) : 0.f;
+        }
+        double ns = 0.0, ss = 0.0;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            ns += N[u];
+            ss += N[u] > 0.f ? static_cast<double>(S[u]) : 0.0;
+        }
+        dscr[p * 64 + ch] = ss;
+        dscr[256 + p * 64 + ch] = ns;
+        __syncthreads();
+        const double Sg = ((dscr[ch] + dscr[64 + ch]) + dscr[128 + ch]) + dscr[192 + ch];
+        const double Ng = ((dscr[256 + ch] + dscr[320 + ch]) + dscr[384 + ch]) + dscr[448 + ch];
+        const double mg = Ng > 0.0 ? Sg / Ng : 0.0;
+        double qq = 0.0;
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+            if (N[u] > 0.f) {
+                const double d = static_cast<double>(S[u]) - static_cast<double>(N[u]) * mg;
+                qq += static_cast<double>(Q[u]) + d * d / static_cast<double>(N[u]);
+            }
+        __syncthreads();
+        dscr[p * 64 + ch] = qq;
+        __syncthreads();
+        double *gp = W.gpart + (static_cast<int64_t>(l) * ngr + grp) * kGPart;
+        if (p == 0) {
+            st_agent(gp + 1 + ch, Sg);
+            st_agent(gp + 65 + ch, ((dscr[ch] + dscr[64 + ch]) + dscr[128 + ch]) + dscr[192 + ch]);
+            if (ch == 0) st_agent(gp, Ng);
+        }
+        if (tid == 0) __hip_atomic_store(gcnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        publisher = arrive(pub, sm) == static_cast<unsigned>(ngr - 1);
+    }
+    if (publisher) {  // block-uniform: the last group in combines every group
+        double a = 0.0, nn = 0.0;
+        for (int64_t g1 = p; g1 < ngr; g1 += 4) {
+            const double *gp = W.gpart + (static_cast<int64_t>(l) * ngr + g1) * kGPart;
+            a += ld_agent(gp + 1 + ch);
+            nn += ld_agent(gp);
+        }
+        __syncthreads();
+        dscr[p * 64 + ch] = a;
+        dscr[256 + p * 64 + ch] = nn;
+        __syncthreads();
+        const double S = ((dscr[ch] + dscr[64 + ch]) + dscr[128 + ch]) + dscr[192 + ch];
+        const double N = ((dscr[256 + ch] + dscr[320 + ch]) + dscr[384 + ch]) + dscr[448 + ch];
+        const double m = N > 0.0 ? S / N : 0.0;
+        double qq = 0.0;
+        for (int64_t g1 = p; g1 < ngr; g1 += 4) {
+            const double *gp = W.gpart + (static_cast<int64_t>(l) * ngr + g1) * kGPart;
+            const double ng = ld_agent(gp);
+            if (ng > 0.0) {
+                const double d = ld_agent(gp + 1 + ch) - ng * m;
+                qq += ld_agent(gp + 65 + ch) + d * d / ng;
+            }
+        }
+        __syncthreads();
+        dscr[p * 64 + ch] = qq;
+        __syncthreads();
+        if (p == 0) {
+            const double M2 = ((dscr[ch] + dscr[64 + ch]) + dscr[128 + ch]) + dscr[192 + ch];
+            const double var = N > 0.0 ? M2 / N : 0.0;
+            const double istd = 1.0 / sqrt(var + static_cast<double>(Ly.eps));
+            const double sc = static_cast<double>(Ly.gamma[ch]) * istd;
+            const float scale = static_cast<float>(sc);
+            const float shift = static_cast<float>(static_cast<double>(Ly.beta[ch]) - m * sc);
+            if (Ly.rmean) {
+                const double mo = static_cast<double>(Ly.mom);
+                Ly.rmean[ch] = static_cast<float>((1.0 - mo) * Ly.rmean[ch] + mo * m);
+                Ly.rvar[ch] = static_cast<float>((1.0 - mo) * Ly.rvar[ch] +
+                                                 mo * (N > 1.0 ? M2 / (N - 1.0) : M2));
+                if (ch == 0 && Ly.nbt) *Ly.nbt += 1;
+            }
+            Ly.stat[ch] = static_cast<float>(m);
+            Ly.stat[64 + ch] = static_cast<float>(istd);
+            Ly.stat[128 + ch] = scale;
+            Ly.stat[192 + ch] = shift;
+            st_agent(W.ss + l * 128 + ch, scale);
+            st_agent(W.ss + l * 128 + 64 + ch, shift);
+        }
+        if (tid == 0) __hip_atomic_store(pub, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (tid == 0) __hip_atomic_store(flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    // ---- every chunk: wait for the published (scale, shift)
+    if (tid == 0) {
+        const uint64_t t0 = now();
+        while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) {
+            __builtin_amdgcn_s_sleep(2);
+            if (now() - t0 > kTimeout) {
+                set_err(sync, 0x100u + l);
+                break;
+            }
+        }
+    }
+    __syncthreads();
+    if (tid < 128) sm.ss[tid] = ld_agent(W.ss + l * 128 + tid);
+    __syncthreads();
+}
+
+// This workgroup's chunk c of a graph: components [i0, i1), rows [rb0, rb1),
+// its CSR as chunk-local rows in LDS (sm.rp, sm.colv), the component starts
+// (sm.cs, ncomp entries + the end).  With node_map/par, par[v] = the x row of
+// chunk row v (layer 0 of the forward).
+struct Chunk {
+    int64_t i0, i1;
+    int rb0, rb1, nr, nrb, ncomp, e0;
+    bool lds_col;
+};
+
+__device__ Chunk load_chunk(const int32_t *__restrict__ rowptr, const int32_t *__restrict__ col,
+                            const int32_t *__restrict__ comp_ptr, int64_t n_comp, int64_t nch,
+                            int64_t c, uint32_t *sync, Smem &sm,
+                            const int32_t *__restrict__ node_map = nullptr, int32_t *par = nullptr) {
+    const int tid = threadIdx.x;
+    Chunk k;
+    const int win0 = static_cast<int>(c * kWin), win1 = static_cast<int>(c * kWin + kWin);
+    lower_bounds(comp_ptr, n_comp, win0, win1, sm);
+    k.i0 = sm.sb[0][0];
+    k.i1 = c == nch - 1 ? n_comp : sm.sb[1][0];
+    __syncthreads();
+    k.rb0 = static_cast<int>(comp_ptr[k.i0]);
+    k.rb1 = static_cast<int>(comp_ptr[k.i1]);
+    if (k.rb1 - k.rb0 > kRows || k.rb1 < k.rb0) {  // a component over kMaxComp rows: host-checked
+        if (tid == 0) set_err(sync, 0x10u);
+        k.rb1 = k.rb0;
+    }
+    k.nr = k.rb1 - k.rb0;
+    k.nrb = (k.nr + 15) / 16;
+    k.ncomp = static_cast<int>(k.i1 - k.i0 < kRows + 1 ? k.i1 - k.i0 : kRows + 1);
+    if (tid <= k.nr) sm.rp[tid] = rowptr[k.rb0 + tid];
+    if (par && tid < k.nr) par[tid] = node_map ? node_map[k.rb0 + tid] : k.rb0 + tid;
+    if (tid <= k.ncomp) sm.cs[tid] = (tid < k.ncomp ? comp_ptr[k.i0 + tid] : k.rb1) - k.rb0;
+    __syncthreads();
+    k.e0 = sm.rp[0];
+    const int ne = sm.rp[k.nr] - k.e0;
+    k.lds_col = ne <= kMaxE;  // block-uniform
+    if (k.lds_col)
+        for (int i = tid; i < ne; i += 256) sm.colv[i] = col[k.e0 + i] - k.rb0;
+    __syncthreads();
+    if (tid <= k.nr) sm.rp[tid] -= k.e0;
+    __syncthreads();
+    return k;
+}
+
+// chunk-local neighbour row of chunk edge ei (clamped into the chunk: a graph
+// whose edges left their component would read wrong rows, never outside the
+// images)
+__device__ __forceinline__ int nbr_of(const Chunk &k, const int32_t *__restrict__ col, const Smem &sm,
+                                      int ei) {
+    const int u = k.lds_col ? sm.colv[ei] : col[k.e0 + ei] - k.rb0;
+    return u < 0 ? 0 : (u < k.nr ? u : k.nr - 1);
+}
+
+__global__ __launch_bounds__(256, 3) void gin_pair_fwd_k(const scgib_pair_fwd_args A) {
+    __shared__ Smem sm;
+    const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
+    const int64_t nch0 = n_chunks(A.enc[0].n_cap);
+    const int e = static_cast<int64_t>(blockIdx.x) < nch0 ? 0 : 1;
+    const scgib_pair_encoder &E = A.enc[e];
+    const int64_t c = blockIdx.x - (e ? nch0 : 0);
+    const int64_t nch = n_chunks(E.n_cap), ngr = n_groups(E.n_cap);
+    const int L = A.n_layers;
+    const Ws ws = ws_of(E.ws, E.n_cap, L);
+    unsigned *cnt = E.counters;
+    const int64_t n = E.dims ? static_cast<int64_t>(E.dims[0]) : E.n_cap;
+    const int F = A.n_feat;
+
+    // ---- weights of layer 0 (in flight during the chunk search)
+    float fw1[16], fw2[16], fwt[4];
+    load_frag<32>(E.w1[0], fw1);
+    load_frag<64>(E.w2[0], fw2);
+    {
+        const int cb = wv & 1, g = lane >> 4;
+        const float *wr = A.wt + static_cast<int64_t>(16 * cb + (lane & 15)) * F;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            const int k = 4 * g + t;
+            fwt[t] = wr[k < F ? k : 0] * (k < F ? 1.f : 0.f);
+        }
+    }
+    float bias1 = E.b1[0][acc_col16()], bias2 = E.b2[0][acc_col16()];
+
+    // ---- this chunk: components [i0, i1), rows [rb0, rb1)
+    int32_t *par = reinterpret_cast<int32_t *>(sm.buf1);  // layer 0 only
+    const Chunk ck = load_chunk(E.rowptr, E.col, E.comp_ptr, E.n_comp, nch, c, A.sync, sm,
+                                E.node_map, par);
+    const int64_t i0 = ck.i0, i1 = ck.i1;
+    const int rb0 = ck.rb0, nr = ck.nr, nrb = ck.nrb, ncomp = ck.ncomp;
+    const int win0 = static_cast<int>(c * kWin), win1 = static_cast<int>(c * kWin + kWin);
+    auto nbr = [&](int ei) -> int { return nbr_of(ck, E.col, sm, ei); };
+
+    // capacity padding rows this window zeroes (every output, every layer)
+    const int64_t z0 = win0 > n ? win0 : n, z1 = win1 < E.n_cap ? win1 : E.n_cap;
+
+    // ---- layer 0: gather the raw features (ope x_v + sum of neighbours)
+    const float ope0 = E.one_plus_eps[0];
+    {
+        const int f = tid & 15, rs = tid >> 4;
+        const bool fok = f < F;
+        for (int v = rs; v < 16 * nrb; v += 16) {
+            float a = 0.f;
+            if (v < nr) {
+                a = ope0 * (fok ? A.x[static_cast<int64_t>(par[v]) * F + f] : 0.f);
+                const int b = sm.rp[v], d = sm.rp[v + 1] - b;
+                for (int j0 = 0; j0 < d; j0 += 4) {
+                    float xs[4];
+#pragma unroll
+                    for (int t = 0; t < 4; ++t) {
+                        const int j = j0 + t < d ? j0 + t : d - 1;
+                        xs[t] = A.x[static_cast<int64_t>(par[nbr(b + j)]) * F + (fok ? f : 0)];
+                    }
+#pragma unroll
+                    for (int t = 0; t < 4; ++t) a = fmaf(xs[t], (j0 + t < d && fok) ? 1.f : 0.f, a);
+                }
+                E.aggx[static_cast<int64_t>(rb0 + v) * 16 + f] = a;
+            }
+            sm.buf0[sidx(v, f)] = a;
+        }
+        for (int64_t idx = tid; idx < (z1 - z0) * 16; idx += 256) E.aggx[z0 * 16 + idx] = 0.f;
+    }
+    __syncthreads();
+    // agg0 = aggx Wt^T (32 columns): wave w takes column block w & 1, row blocks w >> 1 + 2 k
+    {
+        const int cb = wv & 1, r16 = lane & 15, g = lane >> 4;
+        for (int rb = wv >> 1; rb < nrb; rb += 2) {
+            const float4 a = *reinterpret_cast<const float4 *>(sm.buf0 + sidx(16 * rb + r16, 4 * g));
+            f32x4 acc{0.f, 0.f, 0.f, 0.f};
+            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, fwt[0], acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, fwt[1], acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.z, fwt[2], acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, fwt[3], acc, 0, 0, 0);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int row = 16 * rb + 4 * g + i, cc = 16 * cb + r16;
+                sm.buf1[sidx(row, cc)] = acc[i];
+                if (row < nr) E.agg[0][static_cast<int64_t>(rb0 + row) * 32 + cc] = acc[i];
+            }
+        }
+        zero_rows<32>(E.agg[0], z0, z1);
+    }
+    __syncthreads();
+
+    f32x4 z[kNrb];
+    for (int l = 0; l < L; ++l) {
+        const int din = l == 0 ? 32 : 64;
+        if (l > 0) {
+            // ---- aggregation from LDS: x = relu(scale z2 + shift) of the previous layer
+            const int q = tid & 15, rs = tid >> 4;
+            const float ope = E.one_plus_eps[l];
+            const float4 sc = make_float4(sm.ss[4 * q], sm.ss[4 * q + 1], sm.ss[4 * q + 2], sm.ss[4 * q + 3]);
+            const float4 sh = make_float4(sm.ss[64 + 4 * q], sm.ss[65 + 4 * q], sm.ss[66 + 4 * q],
+                                          sm.ss[67 + 4 * q]);
+            for (int v = rs; v < 16 * nrb; v += 16) {
+                float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+                if (v < nr) {
+                    const float4 xv = xform4(*reinterpret_cast<const float4 *>(sm.buf0 + sidx(v, 4 * q)), sc, sh);
+                    a = make_float4(ope * xv.x, ope * xv.y, ope * xv.z, ope * xv.w);
+                    for (int ei = sm.rp[v]; ei < sm.rp[v + 1]; ++ei) {
+                        const int u = nbr(ei);
+                        a = add4(a, xform4(*reinterpret_cast<const float4 *>(sm.buf0 + sidx(u, 4 * q)), sc, sh));
+                    }
+                    st4(E.agg[l] + static_cast<int64_t>(rb0 + v) * 64 + 4 * q, a);
+                }
+                *reinterpret_cast<float4 *>(sm.buf1 + sidx(v, 4 * q)) = a;
+            }
+            zero_rows<64>(E.agg[l], z0, z1);
+            __syncthreads();
+        }
+        // ---- z1 = agg W1^T; r = relu(z1 + b1) -> buf0 (its previous content is consumed)
+        if (din == 32) gemm<32>(sm.buf1, fw1, nrb, z);
+        else gemm<64>(sm.buf1, fw1, nrb, z);
+#pragma unroll
+        for (int rb = 0; rb < kNrb; ++rb)
+            if (rb < nrb)
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+                    sm.buf0[sidx(acc_row16(rb, i), acc_col16())] = fmaxf(z[rb][i] + bias1, 0.f);
+        __syncthreads();
+        lds_to_global<64>(sm.buf0, E.r[l], rb0, nr);
+        zero_rows<64>(E.r[l], z0, z1);
+        // ---- z2 = r W2^T + b2
+        gemm<64>(sm.buf0, fw2, nrb, z);
+#pragma unroll
+        for (int rb = 0; rb < kNrb; ++rb)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) z[rb][i] += bias2;
+        __syncthreads();  // every wave's reads of r done
+#pragma unroll
+        for (int rb = 0; rb < kNrb; ++rb)
+            if (rb < nrb)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) sm.buf0[sidx(acc_row16(rb, i), acc_col16())] = z[rb][i];
+        __syncthreads();
+        lds_to_global<64>(sm.buf0, E.z2[l], rb0, nr);
+        zero_rows<64>(E.z2[l], z0, z1);
+        // ---- the next layer's weights, in flight during the exchange
+        if (l + 1 < L) {
+            load_frag<64>(E.w1[l + 1], fw1);
+            load_frag<64>(E.w2[l + 1], fw2);
+            bias1 = E.b1[l + 1][acc_col16()];
+            bias2 = E.b2[l + 1][acc_col16()];
+        }
+        const Layer Ly{0.f, E.bn_eps[l], E.momentum[l], E.gamma[l], E.beta[l], E.running_mean[l],
+                       E.running_var[l], E.stat[l], E.num_batches_tracked[l]};
+        bn_exchange(z, nrb, nr, c, nch, ngr, l, ws, cnt, Ly, A.sync, sm);
+    }
+
+    // ---- encoder output: out = relu(BN(z2)) -> global and buf1
+    {
+        const int q = tid & 15, rs = tid >> 4;
+        const float4 sc = make_float4(sm.ss[4 * q], sm.ss[4 * q + 1], sm.ss[4 * q + 2], sm.ss[4 * q + 3]);
+        const float4 sh = make_float4(sm.ss[64 + 4 * q], sm.ss[65 + 4 * q], sm.ss[66 + 4 * q],
+                                      sm.ss[67 + 4 * q]);
+        for (int v = rs; v < 16 * nrb; v += 16) {
+            float4 o = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (v < nr) {
+                o = xform4(*reinterpret_cast<const float4 *>(sm.buf0 + sidx(v, 4 * q)), sc, sh);
+                st4(E.out + static_cast<int64_t>(rb0 + v) * 64 + 4 * q, o);
+            }
+            *reinterpret_cast<float4 *>(sm.buf1 + sidx(v, 4 * q)) = o;
+        }
+        zero_rows<64>(E.out, z0, z1);
+    }
+    __syncthreads();
+    if (E.readout) {
+        // per-component sums (dgl.sum_nodes): task = (component k, float4 slot q)
+        for (int t = tid; t < ncomp * 16; t += 256) {
+            const int k = t >> 4, q = t & 15;
+            float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+            for (int v = sm.cs[k]; v < sm.cs[k + 1]; ++v)
+                a = add4(a, *reinterpret_cast<const float4 *>(sm.buf1 + sidx(v, 4 * q)));
+            st4(E.readout + (i0 + k) * 64 + 4 * q, a);
+            if (q == 0)
+                for (int v = sm.cs[k]; v < sm.cs[k + 1]; ++v) E.seg[rb0 + v] = static_cast<int32_t>(i0 + k);
+        }
+        // (the last chunk only) trailing empty components past the LDS table
+        for (int64_t k = i0 + ncomp + (tid >> 4); k < i1; k += 16)
+            st4(E.readout + k * 64 + 4 * (tid & 15), make_float4(0.f, 0.f, 0.f, 0.f));
+        for (int64_t v = z0 + tid; v < z1; v += 256) E.seg[v] = 0;
+    }
+    if (E.lin_w) {  // compressor[0] (models.py:596) on the output
+        float fw0[16];
+        load_frag<64>(E.lin_w, fw0);
+        const float b0 = E.lin_b[acc_col16()];
+        gemm<64>(sm.buf1, fw0, nrb, z);
+#pragma unroll
+        for (int rb = 0; rb < kNrb; ++rb)
+            if (rb < nrb)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const int row = acc_row16(rb, i);
+                    if (row < nr) E.lin_out[static_cast<int64_t>(rb0 + row) * 64 + acc_col16()] = z[rb][i] + b0;
+                }
+        zero_rows<64>(E.lin_out, z0, z1);
+    }
+
+    // ---- exit: the last workgroup re-arms every flag of both encoders
+    if (arrive(A.sync, sm) == gridDim.x - 1) {
+        for (int ee = 0; ee < 2; ++ee) {
+            unsigned *cc = A.enc[ee].counters + n_groups(A.enc[ee].n_cap) * kL;
+            if (tid < 2 * kL) __hip_atomic_store(cc + tid, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        if (tid == 0) __hip_atomic_store(A.sync, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// backward (scgib_gin_pair_bwd)
+// ---------------------------------------------------------------------------
+// Row loads of the saved activations through a buffer resource: 32-bit
+// offsets (one VGPR per load instead of a 64-bit address each) and the
+// hardware range check returns zeros past the array's rows, so the loads of
+// a chunk's padding rows need no clamp.
+typedef __amdgpu_buffer_rsrc_t Rsrc;
+__device__ __forceinline__ Rsrc rows_rsrc(const float *base, int64_t rows, int width) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(base), 0,
+                                             static_cast<int>(rows * width * 4), 0x00020000);
+}
+// v, or zeros (per component: a select of whole float4 values is lowered
+// through scratch memory by hipcc)
+__device__ __forceinline__ float4 keep4(bool ok, float4 v) {
+    return make_float4(ok ? v.x : 0.f, ok ? v.y : 0.f, ok ? v.z : 0.f, ok ? v.w : 0.f);
+}
+__device__ __forceinline__ float4 ld_row(Rsrc r, int row, int width, int col) {
+    return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, (row * width + col) * 4, 0, 0));
+}
+// acc[jb] += X^T Y over rows [0, 4 ns): output rows = this wave's 16 columns
+// of X (16 w + lane & 15), output columns = Y's columns 16 jb + (lane & 15);
+// csum += the lane's X values (summed over lane >> 4: X's column sums)
+template <int JB>
+__device__ __forceinline__ void gemm_tn(const float *X, const float *Y, int ns, f32x4 (&acc)[4],
+                                        float &csum) {
+    const int l = threadIdx.x & 63, r16 = l & 15, g = l >> 4, w = threadIdx.x >> 6;
+    for (int s = 0; s < ns; ++s) {
+        const int row = 4 * s + g;
+        const float a = X[sidx(row, 16 * w + r16)];
+        float b[JB];
+#pragma unroll
+        for (int jb = 0; jb < JB; ++jb) b[jb] = Y[sidx(row, 16 * jb + r16)];
+        csum += a;
+#pragma unroll
+        for (int jb = 0; jb < JB; ++jb)
+            acc[jb] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b[jb], acc[jb], 0, 0, 0);
+    }
+}
+
+// B fragments of the product X W (W [K][N] row-major): column colbase + (lane
+// & 15), rows k = 16 j + 4 (lane >> 4) + t -> f[4 j + t] (gemm's convention)
+template <int K, int N>
+__device__ __forceinline__ void load_frag_col(const float *__restrict__ W, int colbase, float (&f)[16]) {
+    const int l = threadIdx.x & 63, c = l & 15, g = l >> 4;
+#pragma unroll
+    for (int j = 0; j < K / 16; ++j)
+#pragma unroll
+        for (int t = 0; t < 4; ++t) f[4 * j + t] = W[(16 * j + 4 * g + t) * N + colbase + c];
+}
+
+// for rb = rb0, rb0 + step, ... < nrb: epi(rb, A rows [16 rb, 16 rb + 16) x f)
+// (K = 64, b128 reads; one row block's accumulator live at a time)
+template <class Epi>
+__device__ __forceinline__ void gemm_each(const float *A, const float (&f)[16], int nrb, int rb0,
+                                          int step, Epi epi) {
+    const int l = threadIdx.x & 63, r16 = l & 15, g = l >> 4;
+    for (int rb = rb0; rb < nrb; rb += step) {
+        const int row = 16 * rb + r16;
+        f32x4 acc{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const float4 a = *reinterpret_cast<const float4 *>(A + sidx(row, 16 * j + 4 * g));
+            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, f[4 * j], acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, f[4 * j + 1], acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.z, f[4 * j + 2], acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, f[4 * j + 3], acc, 0, 0, 0);
+        }
+        epi(rb, acc);
+    }
+}
+
+// the BatchNorm-backward exchange of layer l: the chunk's 128 sums (sum dy,
+// sum dy xhat, already stored at its partial) -> groups -> publisher, which
+// writes dbeta / dgamma and publishes the dz2 coefficients tot / N into sm.ss
+__device__ void bwd_exchange(int l, int64_t c, int64_t nch, int64_t ngr, int64_t n, const Ws &W,
+                             unsigned *cnt, float *dgamma, float *dbeta, uint32_t *sync, Smem &sm,
+                             double *dscr) {
+    const int tid = threadIdx.x, ch = tid & 127, p = tid >> 7;  // 128 sums x 2 partitions
+    const int64_t grp = c / kGrp, g0 = grp * kGrp;
+    const int gsize = static_cast<int>(nch - g0 < kGrp ? nch - g0 : kGrp);
+    unsigned *gcnt = cnt + static_cast<int64_t>(l) * ngr + grp;
+    unsigned *pub = cnt + static_cast<int64_t>(ngr) * kL + l;
+    unsigned *flag = cnt + static_cast<int64_t>(ngr) * kL + kL + l;
+    bool publisher = false;
+    if (arrive(gcnt, sm) == static_cast<unsigned>(gsize - 1)) {
+        float v[kGrp / 2];
+#pragma unroll
+        for (int u = 0; u < kGrp / 2; ++u) {
+            const int k = p + 2 * u;
+            v[u] = ld_agent(W.part + (static_cast<int64_t>(l) * nch + g0 + (k < gsize ? k : 0)) * kPart + ch);
+        }
+        double a = 0.0;
+#pragma unroll
+        for (int u = 0; u < kGrp / 2; ++u) a += p + 2 * u < gsize ? static_cast<double>(v[u]) : 0.0;
+        dscr[p * 128 + ch] = a;
+        __syncthreads();
+        if (p == 0) st_agent(W.gpart + (static_cast<int64_t>(l) * ngr + grp) * kGPart + ch, dscr[ch] + dscr[128 + ch]);
+        if (tid == 0) __hip_atomic_store(gcnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        publisher = arrive(pub, sm) == static_cast<unsigned>(ngr - 1);
+    }
+    if (publisher) {
+        double a = 0.0;
+        for (int64_t g1 = p; g1 < ngr; g1 += 2) a += ld_agent(W.gpart + (static_cast<int64_t>(l) * ngr + g1) * kGPart + ch);
+        __syncthreads();
+        dscr[p * 128 + ch] = a;
+        __syncthreads();
+        if (p == 0) {
+            const double tot = dscr[ch] + dscr[128 + ch];
+            if (ch < 64) dbeta[ch] = static_cast<float>(tot);
+            else dgamma[ch - 64] = static_cast<float>(tot);
+            st_agent(W.ss + l * 128 + ch, static_cast<float>(tot / static_cast<double>(n)));
+        }
+        if (tid == 0) __hip_atomic_store(pub, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (tid == 0) __hip_atomic_store(flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (tid == 0) {
+        const uint64_t t0 = now();
+        while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) {
+            __builtin_amdgcn_s_sleep(2);
+            if (now() - t0 > kTimeout) {
+                set_err(sync, 0x200u + l);
+                break;
+            }
+        }
+    }
+    __syncthreads();
+    if (tid < 128) sm.ss[tid] = ld_agent(W.ss + l * 128 + tid);
+    __syncthreads();
+}
+
+__global__ __launch_bounds__(256, 3) void gin_pair_bwd_k(const scgib_pair_bwd_args A) {
+    __shared__ Smem sm;
+    const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63, r16 = lane & 15, g = lane >> 4;
+    const int64_t nch0 = n_chunks(A.enc[0].n_cap);
+    const int e = static_cast<int64_t>(blockIdx.x) < nch0 ? 0 : 1;
+    const scgib_pair_bwd_encoder &E = A.enc[e];
+    const int64_t c = blockIdx.x - (e ? nch0 : 0);
+    const int64_t nch = n_chunks(E.n_cap), ngr = n_groups(E.n_cap);
+    const int L = A.n_layers, F = A.n_feat;
+    const Ws ws = ws_of(E.ws, E.n_cap, L);
+    unsigned *cnt = E.counters;
+    const int64_t n = E.dims ? static_cast<int64_t>(E.dims[0]) : E.n_cap;
+
+    const Chunk ck = load_chunk(E.rowptr, E.col, E.comp_ptr, E.n_comp, nch, c, A.sync, sm);
+    const int rb0 = ck.rb0, nr = ck.nr, nrb = ck.nrb, ns = (ck.nr + 3) / 4;
+    const int q4 = tid & 15, rs = tid >> 4;  // thread-row-wise roles: float4 slot, rows rs + 16 k
+    float *P = sm.buf0, *Q = sm.buf1;
+    float fw[16];
+
+    // ---- d out of the chunk's rows -> P
+    if (E.lin_g) {  // compressor[0] backward first: d out = g_out + g_t W0, dW0 += g_t^T f
+        for (int v = rs; v < 16 * nrb; v += 16) {
+            const bool ok = v < nr;
+            const float4 gt = ld_row(rows_rsrc(E.lin_g, E.n_cap, 64), rb0 + v, 64, 4 * q4);
+            const float4 fi = ld_row(rows_rsrc(E.lin_in, E.n_cap, 64), rb0 + v, 64, 4 * q4);
+            *reinterpret_cast<float4 *>(Q + sidx(v, 4 * q4)) = keep4(ok, gt);
+            *reinterpret_cast<float4 *>(P + sidx(v, 4 * q4)) = keep4(ok, fi);
+        }
+        load_frag_col<64, 64>(E.lin_w, 16 * wv, fw);
+        __syncthreads();
+        f32x4 aw[4] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f},
+                       f32x4{0.f, 0.f, 0.f, 0.f}};
+        float cs = 0.f;
+        gemm_tn<4>(Q, P, ns, aw, cs);          // dW0 = g_t^T f, db0 = sum g_t
+        float *sl = E.lin_slab + c * (64 * 64 + 64);
+#pragma unroll
+        for (int jb = 0; jb < 4; ++jb)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) sl[(16 * wv + 4 * g + i) * 64 + 16 * jb + r16] = aw[jb][i];
+        cs += __shfl_xor(cs, 16, kWave);
+        cs += __shfl_xor(cs, 32, kWave);
+        if (g == 0) sl[64 * 64 + 16 * wv + r16] = cs;
+        __syncthreads();  // every read of P (f) done: d out = g_out + g_t W0 -> P
+        gemm_each(Q, fw, nrb, 0, 1, [&](int rb, const f32x4 &d) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int row = acc_row16(rb, i), col = acc_col16();
+                const float go = E.g_out && row < nr ? E.g_out[static_cast<int64_t>(rb0 + row) * 64 + col] : 0.f;
+                P[sidx(row, col)] = row < nr ? d[i] + go : 0.f;
+            }
+        });
+    } else {
+        for (int v = rs; v < 16 * nrb; v += 16) {
+            float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (v < nr && E.g_out) a = ld_row(rows_rsrc(E.g_out, E.n_cap, 64), rb0 + v, 64, 4 * q4);
+            *reinterpret_cast<float4 *>(P + sidx(v, 4 * q4)) = a;
+        }
+        __syncthreads();
+        if (E.g_readout)  // the readout's gradient, broadcast to its component's rows
+            for (int t = tid; t < ck.ncomp * 16; t += 256) {
+                const int k = t >> 4, q = t & 15;
+                if (sm.cs[k] < sm.cs[k + 1]) {
+                    const float4 gr = ld4(E.g_readout + (ck.i0 + k) * 64 + 4 * q);
+                    for (int v = sm.cs[k]; v < sm.cs[k + 1]; ++v) {
+                        float4 *d = reinterpret_cast<float4 *>(P + sidx(v, 4 * q));
+                        *d = add4(*d, gr);
+                    }
+                }
+            }
+    }
+    __syncthreads();
+
+    for (int l = L - 1; l >= 0; --l) {
+        const int din = l == 0 ? 32 : 64;
+        // ---- dy = dh [scale z2 + shift > 0] (in place), xhat, the chunk's sums
+        const float *st = E.stat[l];
+        const float4 mean = ld4(st + 4 * q4), istd = ld4(st + 64 + 4 * q4);
+        const float4 sc = ld4(st + 128 + 4 * q4), sh = ld4(st + 192 + 4 * q4);
+        float4 zv[kNrb];
+        {
+            const Rsrc rz = rows_rsrc(E.z2[l], E.n_cap, 64);
+#pragma unroll
+            for (int k = 0; k < kNrb; ++k) zv[k] = ld_row(rz, rb0 + rs + 16 * k, 64, 4 * q4);
+        }
+        // dy -> P (in place of dh), xhat -> Q
+        float4 sdy = make_float4(0.f, 0.f, 0.f, 0.f), sdx = sdy;
+#pragma unroll
+        for (int k = 0; k < kNrb; ++k) {
+            const int v = rs + 16 * k;
+            if (v < 16 * nrb) {
+                const float ok = v < nr ? 1.f : 0.f;
+                const float4 zz = zv[k];
+                float4 *pd = reinterpret_cast<float4 *>(P + sidx(v, 4 * q4));
+                const float4 dh = *pd;
+                const float4 dy = make_float4((sc.x * zz.x + sh.x > 0.f ? dh.x : 0.f) * ok,
+                                              (sc.y * zz.y + sh.y > 0.f ? dh.y : 0.f) * ok,
+                                              (sc.z * zz.z + sh.z > 0.f ? dh.z : 0.f) * ok,
+                                              (sc.w * zz.w + sh.w > 0.f ? dh.w : 0.f) * ok);
+                const float4 xh = make_float4((zz.x - mean.x) * istd.x, (zz.y - mean.y) * istd.y,
+                                              (zz.z - mean.z) * istd.z, (zz.w - mean.w) * istd.w);
+                *pd = dy;
+                *reinterpret_cast<float4 *>(Q + sidx(v, 4 * q4)) = xh;
+                sdy = add4(sdy, dy);
+                sdx = add4(sdx, make_float4(dy.x * xh.x, dy.y * xh.y, dy.z * xh.z, dy.w * xh.w));
+            }
+        }
+        {  // the row slots' sums: lane groups by shuffles, the 4 waves through red
+#pragma unroll
+            for (int off = 16; off <= 32; off <<= 1) {
+                sdy = make_float4(sdy.x + __shfl_xor(sdy.x, off, kWave), sdy.y + __shfl_xor(sdy.y, off, kWave),
+                                  sdy.z + __shfl_xor(sdy.z, off, kWave), sdy.w + __shfl_xor(sdy.w, off, kWave));
+                sdx = make_float4(sdx.x + __shfl_xor(sdx.x, off, kWave), sdx.y + __shfl_xor(sdx.y, off, kWave),
+                                  sdx.z + __shfl_xor(sdx.z, off, kWave), sdx.w + __shfl_xor(sdx.w, off, kWave));
+            }
+            if (lane < 16) {
+                *reinterpret_cast<float4 *>(&sm.red[wv][4 * lane]) = sdy;
+                *reinterpret_cast<float4 *>(&sm.red[wv][64 + 4 * lane]) = sdx;
+            }
+            __syncthreads();
+            if (tid < 128)
+                st_agent(ws.part + (static_cast<int64_t>(l) * nch + c) * kPart + tid,
+                         ((sm.red[0][tid] + sm.red[1][tid]) + sm.red[2][tid]) + sm.red[3][tid]);
+        }
+        // r rows in flight during the exchange
+        float4 rr[kNrb];
+        {
+            const Rsrc rrs = rows_rsrc(E.r[l], E.n_cap, 64);
+#pragma unroll
+            for (int k = 0; k < kNrb; ++k) rr[k] = ld_row(rrs, rb0 + rs + 16 * k, 64, 4 * q4);
+        }
+        bwd_exchange(l, c, nch, ngr, n, ws, cnt, E.dgamma[l], E.dbeta[l], A.sync, sm,
+                     reinterpret_cast<double *>(&sm.red[0][0]));
+        // ---- dz2 = scale (dy - c1 - xhat c2) -> P; r -> Q
+        {
+            const float4 c1 = make_float4(sm.ss[4 * q4], sm.ss[4 * q4 + 1], sm.ss[4 * q4 + 2], sm.ss[4 * q4 + 3]);
+            const float4 c2 = make_float4(sm.ss[64 + 4 * q4], sm.ss[65 + 4 * q4], sm.ss[66 + 4 * q4],
+                                          sm.ss[67 + 4 * q4]);
+#pragma unroll
+            for (int k = 0; k < kNrb; ++k) {
+                const int v = rs + 16 * k;
+                if (v < 16 * nrb) {
+                    const bool ok = v < nr;
+                    float4 *pd = reinterpret_cast<float4 *>(P + sidx(v, 4 * q4));
+                    float4 *qd = reinterpret_cast<float4 *>(Q + sidx(v, 4 * q4));
+                    const float4 dy = *pd, xh = *qd;
+                    *pd = keep4(ok, make_float4(sc.x * (dy.x - c1.x - xh.x * c2.x),
+                                                sc.y * (dy.y - c1.y - xh.y * c2.y),
+                                                sc.z * (dy.z - c1.z - xh.z * c2.z),
+                                                sc.w * (dy.w - c1.w - xh.w * c2.w)));
+                    *qd = keep4(ok, rr[k]);
+                }
+            }
+        }
+        __syncthreads();
+        // ---- dW2 += dz2^T r, db2 (slab); dr = dz2 W2, dz1 = dr [r > 0] -> Q (in place of r)
+        float *sl = E.slab[l] + c * E.slab_stride[l];
+        {
+            f32x4 a2[4] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f},
+                           f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+            float cs2 = 0.f;
+            gemm_tn<4>(P, Q, ns, a2, cs2);
+#pragma unroll
+            for (int jb = 0; jb < 4; ++jb)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) sl[(16 * wv + 4 * g + i) * 64 + 16 * jb + r16] = a2[jb][i];
+            cs2 += __shfl_xor(cs2, 16, kWave);
+            cs2 += __shfl_xor(cs2, 32, kWave);
+            if (g == 0) sl[64 * 64 + 64 * din + 16 * wv + r16] = cs2;
+        }
+        load_frag_col<64, 64>(E.w2[l], 16 * wv, fw);
+        // agg rows in flight meanwhile (din / 4 float4 slots per row)
+        float4 av[kNrb];
+        {
+            const int aq = q4 < din / 4 ? q4 : 0;
+            const Rsrc ra = rows_rsrc(E.agg[l], E.n_cap, din);
+#pragma unroll
+            for (int k = 0; k < kNrb; ++k) av[k] = ld_row(ra, rb0 + rs + 16 * k, din, 4 * aq);
+        }
+        __syncthreads();  // every wave's dW2 reads of Q (r) done
+        gemm_each(P, fw, nrb, 0, 1, [&](int rb, const f32x4 &d) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                float *q = Q + sidx(acc_row16(rb, i), acc_col16());
+                *q = *q > 0.f ? d[i] : 0.f;
+            }
+        });
+        __syncthreads();  // every read of P (dz2) done: agg -> P
+#pragma unroll
+        for (int k = 0; k < kNrb; ++k) {
+            const int v = rs + 16 * k;
+            if (v < 16 * nrb && q4 < din / 4)
+                *reinterpret_cast<float4 *>(P + sidx(v, 4 * q4)) = keep4(v < nr, av[k]);
+        }
+        __syncthreads();
+        // ---- dW1 += dz1^T agg, db1 (slab); d(agg) = dz1 W1 -> P (in place of agg)
+        {
+            f32x4 a1[4] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f},
+                           f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+            float cs1 = 0.f;
+            if (din == 64) gemm_tn<4>(Q, P, ns, a1, cs1);
+            else gemm_tn<2>(Q, P, ns, a1, cs1);
+#pragma unroll
+            for (int jb = 0; jb < 4; ++jb)
+                if (jb < din / 16)
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) sl[64 * 64 + (16 * wv + 4 * g + i) * din + 16 * jb + r16] = a1[jb][i];
+            cs1 += __shfl_xor(cs1, 16, kWave);
+            cs1 += __shfl_xor(cs1, 32, kWave);
+            if (g == 0) sl[64 * 64 + 64 * din + 64 + 16 * wv + r16] = cs1;
+        }
+        if (din == 64) load_frag_col<64, 64>(E.w1[l], 16 * wv, fw);
+        else load_frag_col<64, 32>(E.w1[l], 16 * (wv & 1), fw);
+        __syncthreads();  // every wave's dW1 reads of P (agg) done
+        {
+            const int ccol = din == 64 ? acc_col16() : 16 * (wv & 1) + r16;
+            gemm_each(Q, fw, nrb, din == 64 ? 0 : wv >> 1, din == 64 ? 1 : 2, [&](int rb, const f32x4 &d) {
+#pragma unroll
+                for (int i = 0; i < 4; ++i) P[sidx(acc_row16(rb, i), ccol)] = d[i];
+            });
+        }
+        __syncthreads();
+        if (l > 0) {
+            // dh of layer l-1: (1+eps) d(agg)[v] + sum over v's neighbours (P -> Q)
+            const float ope = E.one_plus_eps[l];
+            for (int v = rs; v < 16 * nrb; v += 16) {
+                float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+                if (v < nr) {
+                    const float4 s0 = *reinterpret_cast<const float4 *>(P + sidx(v, 4 * q4));
+                    a = make_float4(ope * s0.x, ope * s0.y, ope * s0.z, ope * s0.w);
+                    for (int ei = sm.rp[v]; ei < sm.rp[v + 1]; ++ei)
+                        a = add4(a, *reinterpret_cast<const float4 *>(P + sidx(nbr_of(ck, E.col, sm, ei), 4 * q4)));
+                }
+                *reinterpret_cast<float4 *>(Q + sidx(v, 4 * q4)) = a;
+            }
+            __syncthreads();
+            float *t = P;
+            P = Q;
+            Q = t;
+        } else {
+            // dWt += d(agg0)^T aggx: aggx rows -> Q (16 columns), waves 0, 1
+            for (int v = rs; v < 16 * nrb; v += 16)
+                if (q4 < 4)
+                    *reinterpret_cast<float4 *>(Q + sidx(v, 4 * q4)) =
+                        keep4(v < nr, ld_row(rows_rsrc(E.aggx, E.n_cap, 16), rb0 + v, 16, 4 * q4));
+            __syncthreads();
+            if (wv < 2) {
+                f32x4 at[4] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f},
+                               f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+                float dummy = 0.f;
+                gemm_tn<1>(P, Q, ns, at, dummy);
+                if (r16 < F)
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) sl[64 * 64 + 64 * 32 + 128 + (16 * wv + 4 * g + i) * F + r16] = at[0][i];
+            }
+        }
+    }
+
+    // ---- exit: the last workgroup re-arms every flag of both encoders
+    if (arrive(A.sync, sm) == gridDim.x - 1) {
+        for (int ee = 0; ee < 2; ++ee) {
+            unsigned *cc = A.enc[ee].counters + n_groups(A.enc[ee].n_cap) * kL;
+            if (tid < 2 * kL) __hip_atomic_store(cc + tid, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        if (tid == 0) __hip_atomic_store(A.sync, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
+}  // namespace pair
+}  // namespace scgib
+
+using namespace scgib;
+
+extern "C" int64_t scgib_gin_pair_args_bytes(void) { return sizeof(scgib_pair_fwd_args); }
+extern "C" int32_t scgib_gin_pair_max_component(void) { return pair::kMaxComp; }
+extern "C" int64_t scgib_gin_pair_chunks(int64_t n_cap) { return n_cap > 0 ? pair::n_chunks(n_cap) : 0; }
+extern "C" int64_t scgib_gin_pair_ws_bytes(int64_t n_cap, int32_t n_layers) {
+    return pair::ws_bytes(n_cap, n_layers);
+}
+extern "C" int64_t scgib_gin_pair_counters(int64_t n_cap, int32_t n_layers) {
+    return pair::n_counters(n_cap, n_layers);
+}
+
+// co-resident workgroups of gin_pair_fwd_k on the current device (the grid
+// must not exceed it: its workgroups wait on each other)
+extern "C" int64_t scgib_gin_pair_slots(void) {
+    static int64_t slots = -1;
+    if (slots < 0) {
+        int dev = 0, cus = 0, per = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, pair::gin_pair_fwd_k, 256, 0) !=
+                hipSuccess)
+            return 0;
+        slots = static_cast<int64_t>(cus) * (per < 3 ? per : 3);
+    }
+    return slots;
+}
+
+extern "C" int scgib_gin_pair_fwd(const scgib_pair_fwd_args *args, scgib_stream_t stream) {
+    if (!args || !args->x || !args->wt || !args->sync) return SCGIB_EINVAL;
+    const scgib_pair_fwd_args &A = *args;
+    if (A.n_layers < 1 || A.n_layers > SCGIB_PAIR_MAX_LAYERS || A.n_feat < 1 || A.n_feat > 16)
+        return SCGIB_EUNSUPPORTED;
+    int64_t grid = 0;
+    for (int e = 0; e < 2; ++e) {
+        const scgib_pair_encoder &E = A.enc[e];
+        if (E.n_cap <= 0 || E.n_comp <= 0 || !E.rowptr || !E.col || !E.comp_ptr || !E.aggx ||
+            !E.out || !E.ws || !E.counters || (E.readout && !E.seg) || (E.lin_w && (!E.lin_b || !E.lin_out)))
+            return SCGIB_EINVAL;
+        if (E.n_cap >= (int64_t(1) << 31) || E.n_comp >= (int64_t(1) << 31)) return SCGIB_EUNSUPPORTED;
+        for (int l = 0; l < A.n_layers; ++l)
+            if (!E.w1[l] || !E.b1[l] || !E.w2[l] || !E.b2[l] || !E.gamma[l] || !E.beta[l] ||
+                !E.agg[l] || !E.r[l] || !E.z2[l] || !E.stat[l] ||
+                ((E.running_mean[l] == nullptr) != (E.running_var[l] == nullptr)))
+                return SCGIB_EINVAL;
+        grid += pair::n_chunks(E.n_cap);
+    }
+    const int64_t slots = scgib_gin_pair_slots();
+    if (grid > slots) return SCGIB_EUNSUPPORTED;  // not co-resident: the per-layer path
+    pair::gin_pair_fwd_k<<<dim3(static_cast<unsigned>(grid)), 256, 0, as_stream(stream)>>>(A);
+    return launch_status();
+}
+
+extern "C" int64_t scgib_gin_pair_bwd_args_bytes(void) { return sizeof(scgib_pair_bwd_args); }
+
+extern "C" int scgib_gin_pair_bwd(const scgib_pair_bwd_args *args, scgib_stream_t stream) {
+    if (!args || !args->sync) return SCGIB_EINVAL;
+    const scgib_pair_bwd_args &A = *args;
+    if (A.n_layers < 1 || A.n_layers > SCGIB_PAIR_MAX_LAYERS || A.n_feat < 1 || A.n_feat > 16)
+        return SCGIB_EUNSUPPORTED;
+    int64_t grid = 0;
+    for (int e = 0; e < 2; ++e) {
+        const scgib_pair_bwd_encoder &E = A.enc[e];
+        if (E.n_cap <= 0 || E.n_comp <= 0 || !E.rowptr || !E.col || !E.comp_ptr || !E.aggx ||
+            !E.ws || !E.counters || (E.lin_g && (!E.lin_w || !E.lin_in || !E.lin_slab)))
+            return SCGIB_EINVAL;
+        if (E.n_cap >= (int64_t(1) << 31) || E.n_comp >= (int64_t(1) << 31)) return SCGIB_EUNSUPPORTED;
+        for (int l = 0; l < A.n_layers; ++l) {
+            const int64_t width = 64 * 64 + 64 * (l == 0 ? 32 : 64) + 128 + (l == 0 ? 32 * A.n_feat : 0);
+            if (!E.agg[l] || !E.r[l] || !E.z2[l] || !E.stat[l] || !E.w1[l] || !E.w2[l] ||
+                !E.dgamma[l] || !E.dbeta[l] || !E.slab[l] || E.slab_stride[l] < width)
+                return SCGIB_EINVAL;
+        }
+        grid += pair::n_chunks(E.n_cap);
+    }
+    if (grid > scgib_gin_pair_slots()) return SCGIB_EUNSUPPORTED;
+    pair::gin_pair_bwd_k<<<dim3(static_cast<unsigned>(grid)), 256, 0, as_stream(stream)>>>(A);
+    return launch_status();
+}

@@ -158,6 +158,23 @@ FUSE_CONTRAST = True
 DEVICE_NOISE = True
 
 
+_GRAPH_ATTRS = ("graph_features", "subgraphs_features", "_last_z1", "_last_kl_mean")
+
+
+def _drop_graph_refs(*owners):
+    """End of a training forward: the attributes the reference keeps
+    (self.graph_features, ...) are kept detached, so the model does not hold
+    this step's autograd graph — and with it the parameters' AccumulateGrad
+    nodes — into the next step: a node created on another stream (a warm-up
+    on a side stream before a HIP-graph capture) would then make torch warn
+    about a cross-stream AccumulateGrad in the captured backward."""
+    for o in owners:
+        for a in _GRAPH_ATTRS:
+            v = getattr(o, a, None)
+            if isinstance(v, torch.Tensor) and v.requires_grad:
+                setattr(o, a, v.detach())
+
+
 def _side_stream(device):
     """The second HIP stream of ``device`` used by the forked encoder branch."""
     key = torch.device(device).index
@@ -259,9 +276,10 @@ class _SCGIBCore(nn.Module):
             ops.check_fork(main)  # never a nested fork while capturing (ops.check_fork)
         side.wait_stream(main)
         batch_x.record_stream(side)
-        if fold and fork and PAIR_ENCODERS:
+        if fold and PAIR_ENCODERS:
             # one autograd node for both encoders (ops._GinEncoderPair): the
             # ego chain is enqueued first on ``side`` in forward AND backward
+            # (fork off: side is the current stream, the chains run in turn)
             with torch.cuda.stream(side):
                 ego = G.egonet_batch(batch_g, self.k_transition)
             lin0 = enc_owner.compressor[0] if LIN_IN_PAIR else None
@@ -404,6 +422,7 @@ class Mainmodel(_SCGIBCore):
         kl_loss, con, rec = self._losses(batch_g, im, self._last_kl_mean, self._last_z1, z2,
                                          self.MLP, batch_size, batch_logMs)
         ops.join_aside()
+        _drop_graph_refs(self)
         return None, kl_loss, con, rec
 
 
@@ -485,6 +504,7 @@ class Mainmodel_continue(_SCGIBCore):
                                          self.model._last_z1, z2, self.MLP, batch_size,
                                          batch_logMs)
         ops.join_aside()
+        _drop_graph_refs(self, self.model)
         return None, kl_loss, con, rec
 
 

@@ -650,6 +650,18 @@ class _GinEncoderPair(torch.autograd.Function):
         ctx.sub = (_Ctx(), _Ctx())
         ctx.side, ctx.ne = side, ne
         check_fork(main)
+        ctx.lin = w0 is not None
+        ctx.lin_leaves = (w0, b0)
+        if _pair_persistent_ok(x, ego, core, gin_ego, gin_core, training, w0):
+            # both encoders in ONE persistent launch on the current stream,
+            # after the ego-net build (``side``) and the noise draw (here)
+            if core_tail is not None:
+                core_tail()
+            main.wait_stream(side)
+            ctx.persistent = True
+            return _pair_forward_persistent(ctx, x, wt, w0, b0, nmap, ego, core, gin_ego,
+                                            gin_core, params)
+        ctx.persistent = False
         side.wait_stream(main)
         if core_tail is not None:  # beside the ego-net build
             core_tail()
@@ -664,8 +676,6 @@ class _GinEncoderPair(torch.autograd.Function):
             s, ro = _drain(ego_steps)
         f = _drain(core_steps)
         outs = (s, ro, f)
-        ctx.lin = w0 is not None
-        ctx.lin_leaves = (w0, b0)
         if ctx.lin:  # compressor[0] on the (shorter) core chain, before the join
             w0, b0 = _f32(w0, "compressor.0.weight"), _f32(b0, "compressor.0.bias")
             if tuple(w0.shape) != (HIDDEN, HIDDEN):
@@ -683,6 +693,8 @@ class _GinEncoderPair(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, g_s, g_ro, g_f, g_t=None):
+        if ctx.persistent:
+            return _pair_backward_persistent(ctx, g_s, g_ro, g_f, g_t)
         # backward: the ego chain (the longer one) stays on the current stream,
         # where its weight-gradient reduces can fork to the aux stream (a fork
         # from an already-forked stream breaks HIP-graph capture on this
@@ -752,6 +764,231 @@ class _GinEncoderPair(torch.autograd.Function):
 
 def _torch_stream():
     return torch.cuda.current_stream()
+
+
+# The encoder pair's forward as ONE persistent launch (scgib_gin_pair_fwd,
+# gin_pair.hip) when it applies: training with batch statistics, both graphs
+# made of closed components of <= scgib_gin_pair_max_component() rows, and
+# both encoders' chunks co-resident on the device.  Otherwise the per-layer
+# kernels.  (A module attribute: the tests run both paths.)
+PAIR_PERSISTENT = False  # (on once validated on the GPU)
+
+
+def pair_sync_error(device):
+    """The persistent pair forward's timeout word (0: none; a bounded spin
+    that gave up writes its code) — read by the tests, not in the step."""
+    return int(counters(device, ("gin_pair_sync",), 4)[1].item())
+
+
+def _pair_persistent_ok(x, ego, core, gin_ego, gin_core, training, w0):
+    L = len(gin_ego.ginlayers)
+    if not (PAIR_PERSISTENT and training and L == len(gin_core.ginlayers)
+            and 1 <= L <= _lib.PAIR_MAX_LAYERS and x.shape[1] <= 16):
+        return False
+    if w0 is not None and tuple(w0.shape) != (HIDDEN, HIDDEN):
+        return False
+    for gr, gin in ((ego, gin_ego), (core, gin_core)):
+        if not (getattr(gr, "components_closed", False) and gr.num_nodes() > 0
+                and gr.batch_size > 0):
+            return False
+        if not 1 <= gr.max_graph_nodes <= int(_lib.query("scgib_gin_pair_max_component")):
+            return False
+        for conv, bn in zip(gin.ginlayers, gin.batch_norms):
+            mlp = conv.apply_func.mlp
+            if not (bn.track_running_stats and bn.momentum is not None and bn.affine):
+                return False
+            if mlp[2].weight.shape != (HIDDEN, HIDDEN):
+                return False
+    chunks = sum(int(_lib.query("scgib_gin_pair_chunks", gr.num_nodes())) for gr in (ego, core))
+    return chunks <= int(_lib.query("scgib_gin_pair_slots"))
+
+
+def _pair_backward_persistent(ctx, g_s, g_ro, g_f, g_t):
+    """_GinEncoderPair.backward through scgib_gin_pair_bwd (one launch, both
+    encoders, compressor[0]'s backward first on Encoder1's chunks), then ONE
+    fixed-order reduce of every layer's per-chunk weight-gradient partials —
+    both encoders' transfer_d partials summed as one job (no add of two
+    d Wt), the loss section's deferred slabs (SlabScope) in the same launch."""
+    dev = ctx.sub[0].saved_tensors[2].device
+    L = ctx.sub[0].L
+    F = ctx.sub[0].n_feat
+    args = _lib.PairBwdArgs()
+    args.n_layers, args.n_feat = L, F
+    args.sync = counters(dev, ("gin_pair_sync",), 4).data_ptr()
+    keep, jobs = [], []
+    nchs = [int(_lib.query("scgib_gin_pair_chunks", ctx.sub[e].saved_tensors[2].shape[0]))
+            for e in (0, 1)]
+    w0_width = HIDDEN * HIDDEN + HIDDEN * 32 + 2 * HIDDEN      # layer 0: W2 | W1 | b2 | b1
+    l0_stride = int(_lib.query("scgib_gin_layer0_slab_width"))  # + the 32 x 16 dWt tail
+    slab0 = torch.empty((nchs[0] + nchs[1]) * l0_stride, dtype=torch.float32, device=dev)
+    keep.append(slab0)
+    dwt = torch.empty(32, F, dtype=torch.float32, device=dev)
+    jobs.append(_lib.SlabJob(slab0.data_ptr() + 4 * w0_width, dwt.data_ptr(), 32 * F,
+                             nchs[0] + nchs[1], l0_stride))
+    grads = ([None] * (6 * L), [None] * (6 * L))
+    dw0 = db0 = None
+    g_in = ((g_s, g_ro), (g_f, None))
+    for e in (0, 1):
+        sub = ctx.sub[e]
+        t = sub.saved_tensors
+        saved, params, aggx = t[: 4 * L], t[4 * L: 4 * L + 6 * L], t[-1]
+        gr = sub.graph
+        n = saved[2].shape[0]
+        E = args.enc[e]
+        E.rowptr, E.col = gr.rowptr.data_ptr(), gr.col.data_ptr()
+        E.comp_ptr, E.n_comp = gr.graph_ptr.data_ptr(), gr.batch_size
+        E.dims = gr.dims.data_ptr() if gr.dims is not None else None
+        E.n_cap = n
+        E.aggx = aggx.data_ptr()
+        g_out, g_read = g_in[e]
+        if g_out is not None:
+            g_out = _f32(g_out, "gin_encoder_pair.backward")
+            keep.append(g_out)
+            E.g_out = g_out.data_ptr()
+        if g_read is not None:
+            g_read = _f32(g_read, "gin_encoder_pair.backward readout")
+            keep.append(g_read)
+            E.g_readout = g_read.data_ptr()
+        for l in range(L):
+            agg, r, z2, stat = saved[4 * l: 4 * l + 4]
+            w1, w2 = _f32(params[6 * l], "w1"), _f32(params[6 * l + 2], "w2")
+            keep += [w1, w2]
+            E.agg[l], E.r[l], E.z2[l], E.stat[l] = (x.data_ptr() for x in (agg, r, z2, stat))
+            E.w1[l], E.w2[l] = w1.data_ptr(), w2.data_ptr()
+            E.one_plus_eps[l] = sub.opes[l]
+            bn_g = torch.empty(2, HIDDEN, dtype=torch.float32, device=dev)
+            E.dgamma[l], E.dbeta[l] = bn_g[0].data_ptr(), bn_g[1].data_ptr()
+            d_in = agg.shape[1]
+            width = HIDDEN * HIDDEN + HIDDEN * d_in + 2 * HIDDEN
+            wgrad = torch.empty(width, dtype=torch.float32, device=dev)
+            if l == 0:
+                E.slab[l] = slab0.data_ptr() + 4 * (nchs[0] * l0_stride if e else 0)
+                E.slab_stride[l] = l0_stride
+                jobs.append(_lib.SlabJob(E.slab[l], wgrad.data_ptr(), width, nchs[e], l0_stride))
+            else:
+                slab = torch.empty(nchs[e] * width, dtype=torch.float32, device=dev)
+                keep.append(slab)
+                E.slab[l], E.slab_stride[l] = slab.data_ptr(), width
+                jobs.append(_lib.SlabJob(slab.data_ptr(), wgrad.data_ptr(), width, nchs[e], 0))
+            o = HIDDEN * HIDDEN
+            gl = grads[e]
+            gl[6 * l + 2] = wgrad[:o].view(HIDDEN, HIDDEN)
+            gl[6 * l + 0] = wgrad[o:o + HIDDEN * d_in].view(HIDDEN, d_in)
+            o += HIDDEN * d_in
+            gl[6 * l + 3] = wgrad[o:o + HIDDEN]
+            gl[6 * l + 1] = wgrad[o + HIDDEN:o + 2 * HIDDEN]
+            gl[6 * l + 4] = bn_g[0]
+            gl[6 * l + 5] = bn_g[1]
+        ws = torch.empty(int(_lib.query("scgib_gin_pair_ws_bytes", n, L)), dtype=torch.uint8,
+                         device=dev)
+        keep.append(ws)
+        E.ws = ws.data_ptr()
+        E.counters = counters(dev, ("gin_pair_bwd", e), int(_lib.query("scgib_gin_pair_counters", n, L))).data_ptr()
+        if e == 1 and ctx.lin and g_t is not None:
+            f, w0 = ctx.lin_saved
+            g_t = _f32(g_t, "compressor.0 grad")
+            keep.append(g_t)
+            E.lin_g, E.lin_w, E.lin_in = g_t.data_ptr(), w0.data_ptr(), f.data_ptr()
+            lin_slab = torch.empty(nchs[1] * (HIDDEN * HIDDEN + HIDDEN), dtype=torch.float32,
+                                   device=dev)
+            keep.append(lin_slab)
+            E.lin_slab = lin_slab.data_ptr()
+            wg0 = torch.empty(HIDDEN * HIDDEN + HIDDEN, dtype=torch.float32, device=dev)
+            jobs.append(_lib.SlabJob(lin_slab.data_ptr(), wg0.data_ptr(), wg0.numel(), nchs[1], 0))
+            dw0, db0 = wg0[: HIDDEN * HIDDEN].view(HIDDEN, HIDDEN), wg0[HIDDEN * HIDDEN:]
+    _lib.call("scgib_gin_pair_bwd", ctypes.cast(ctypes.pointer(args), ctypes.c_void_p), _stream())
+    scope = ctx.scope if (ctx.scope is not None and ctx.scope.open) else None
+    if scope is not None:  # the loss section's deferred slabs: the same reduce launch
+        sj, sk = scope.take()
+        jobs += sj
+        keep += sk
+    _reduce_jobs(jobs, _stream())
+    del keep  # (slabs stay allocated until the reduce is enqueued)
+    return (None, dwt, dw0, db0, None, None, None, None, None, None, None, None, *grads[0],
+            *grads[1])
+
+
+def _pair_forward_persistent(ctx, x, wt, w0, b0, nmap, ego, core, gin_ego, gin_core, params):
+    """_GinEncoderPair.forward through scgib_gin_pair_fwd: fills ctx.sub[0]
+    (Encoder2, ego-nets) and ctx.sub[1] (Encoder1) with exactly what the
+    per-layer forward saves, so the backward is the same."""
+    x = _f32(x, "gin_encoder x")
+    wt = _f32(wt, "transfer_d.weight")
+    dev = x.device
+    L = len(gin_ego.ginlayers)
+    ne = 6 * L
+    args = _lib.PairFwdArgs()
+    args.x, args.n_feat, args.wt, args.n_layers = x.data_ptr(), x.shape[1], wt.data_ptr(), L
+    args.sync = counters(dev, ("gin_pair_sync",), 4).data_ptr()
+    keep = [x, wt]
+    outs = []
+    for e, (gr, gin, prm) in enumerate(((ego, gin_ego, params[:ne]), (core, gin_core, params[ne:]))):
+        n = gr.num_nodes()
+        E = args.enc[e]
+        E.rowptr, E.col = gr.rowptr.data_ptr(), gr.col.data_ptr()
+        E.comp_ptr, E.n_comp = gr.graph_ptr.data_ptr(), gr.batch_size
+        E.dims = gr.dims.data_ptr() if gr.dims is not None else None
+        E.n_cap = n
+        E.node_map = nmap.data_ptr() if (e == 0 and nmap is not None) else None
+        saved = []
+        for l in range(L):
+            conv, bn = gin.ginlayers[l], gin.batch_norms[l]
+            w1, b1, w2, b2, gamma, beta = (_f32(p, "gin param") for p in prm[6 * l: 6 * l + 6])
+            d_in = 32 if l == 0 else HIDDEN
+            if w1.shape != (HIDDEN, d_in):
+                raise _lib.ScgibError(f"fused GIN layer {l} needs Linear({d_in}, 64)")
+            keep += [w1, b1, w2, b2, gamma, beta]
+            E.w1[l], E.b1[l], E.w2[l], E.b2[l] = (t.data_ptr() for t in (w1, b1, w2, b2))
+            E.gamma[l], E.beta[l] = gamma.data_ptr(), beta.data_ptr()
+            E.one_plus_eps[l] = conv._one_plus_eps
+            E.bn_eps[l], E.momentum[l] = float(bn.eps), float(bn.momentum)
+            E.running_mean[l] = bn.running_mean.data_ptr()
+            E.running_var[l] = bn.running_var.data_ptr()
+            E.num_batches_tracked[l] = bn.num_batches_tracked.data_ptr()
+            agg = torch.empty(n, d_in, dtype=torch.float32, device=dev)
+            r = torch.empty(n, HIDDEN, dtype=torch.float32, device=dev)
+            z2 = torch.empty(n, HIDDEN, dtype=torch.float32, device=dev)
+            stat = torch.empty(4, HIDDEN, dtype=torch.float32, device=dev)
+            E.agg[l], E.r[l], E.z2[l], E.stat[l] = (t.data_ptr() for t in (agg, r, z2, stat))
+            saved += [agg, r, z2, stat]
+        aggx = torch.empty(n, 16, dtype=torch.float32, device=dev)
+        out = torch.empty(n, HIDDEN, dtype=torch.float32, device=dev)
+        E.aggx, E.out = aggx.data_ptr(), out.data_ptr()
+        ro = seg = t = None
+        if e == 0:
+            ro = torch.empty(gr.batch_size, HIDDEN, dtype=torch.float32, device=dev)
+            seg = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
+            E.readout, E.seg = ro.data_ptr(), seg.data_ptr()
+        elif w0 is not None:
+            w0c, b0c = _f32(w0, "compressor.0.weight"), _f32(b0, "compressor.0.bias")
+            keep += [w0c, b0c]
+            t = torch.empty(n, HIDDEN, dtype=torch.float32, device=dev)
+            E.lin_w, E.lin_b, E.lin_out = w0c.data_ptr(), b0c.data_ptr(), t.data_ptr()
+            ctx.lin_saved = (out, w0c)
+            ctx.core_dims = gr.dims
+        ws = torch.empty(int(_lib.query("scgib_gin_pair_ws_bytes", n, L)), dtype=torch.uint8,
+                         device=dev)
+        keep.append(ws)
+        E.ws = ws.data_ptr()
+        E.counters = counters(dev, ("gin_pair", id(gin)),
+                              int(_lib.query("scgib_gin_pair_counters", n, L))).data_ptr()
+        sub = ctx.sub[e]
+        sub.save_for_backward(*saved, *prm, aggx)
+        sub.graph, sub.L, sub.training, sub.pre = gr, L, True, True
+        sub.n_feat = x.shape[1]
+        sub.opes = [c._one_plus_eps for c in gin.ginlayers]
+        sub.cnt_key = ("gin_bwd", id(gin))
+        sub.seg = seg
+        outs += [out, ro] if e == 0 else [out] + ([t] if t is not None else [])
+    # (the sizes only for the bench's kernel timer: an exact-mode ego batch's
+    # edge count is a device read)
+    meta = None if OBSERVER is None else {
+        "layers": [(gr.num_nodes(), gr.edge_capacity(), 32 if l == 0 else HIDDEN)
+                   for gr in (ego, core) for l in range(L)]}
+    _launch("scgib_gin_pair_fwd", meta, ctypes.cast(ctypes.pointer(args), ctypes.c_void_p),
+            _stream())
+    del keep  # (every pointer is read into the kernel arguments at the launch)
+    return tuple(outs)
 
 
 def gin_encoder_pair_x(x, ego, gin_ego, core, gin_core, transfer, node_map, side, lin0=None,

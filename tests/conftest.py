@@ -108,7 +108,7 @@ def check_grads(golden_grads, mine_of, tol=1e-4, cancelled=CANCELLED, metric="ma
 
 
 def check_grads_model(golden_grads, mine_of, tol=1e-3, cos_min=0.999, cancelled=CANCELLED,
-                      big_tol=5e-3, big_min=4096):
+                      big_tol=5e-3, big_min=4096, each_tol=None):
     """Whole-model gradient parity that is robust to fp32 ReLU-kink flips.
 
     Two correct fp32 evaluations of the step can put a pre-activation that
@@ -121,7 +121,10 @@ def check_grads_model(golden_grads, mine_of, tol=1e-3, cos_min=0.999, cancelled=
     way (cosine >= cos_min), which a sign/layout/indexing bug would break.
     A flip moves a tensor of >= ``big_min`` elements by far less than a
     percent, so those (the GIN / MLP / compressor weight matrices) must each
-    also be within ``big_tol`` relative L2 on their own.  Returns the
+    also be within ``big_tol`` relative L2 on their own.  ``each_tol``: a
+    per-tensor relative-L2 bound on EVERY tensor, small ones included (the
+    config-size tests, whose batches are large enough that no single flip
+    moves a 64-element bias by more than a fraction of it).  Returns the
     per-tensor relative L2 errors (for diagnostics)."""
     num = den = 0.0
     errs = {}
@@ -144,5 +147,7 @@ def check_grads_model(golden_grads, mine_of, tol=1e-3, cos_min=0.999, cancelled=
         errs[name] = rel_l2(mine, ref)
         if ref.size >= big_min:
             assert errs[name] < big_tol, (name, errs[name])
+        if each_tol is not None:
+            assert errs[name] < each_tol, (name, errs[name])
     assert (num / max(den, 1e-300)) ** 0.5 < tol, (num / den) ** 0.5
     return errs

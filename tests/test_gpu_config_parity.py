@@ -19,7 +19,8 @@ the exact Gram form above B = 512 — the dense N x N matrix would be 2.7 GB).
 
 Bars (written here): losses within 1e-4 relative (north star); gradients by
 ``check_grads_model`` (concatenated rel-L2 1e-3, per-tensor cosine 0.999,
-per-tensor rel-L2 5e-3 on every tensor of >= 4096 elements); every BatchNorm
+per-tensor rel-L2 2e-3 on EVERY tensor, 64-element biases and BatchNorm
+gamma / beta included); every BatchNorm
 running statistic within 1e-4 relative and num_batches_tracked exact (the
 compressor BN: B sequential updates).
 """
@@ -37,6 +38,7 @@ pytestmark = pytest.mark.gpu
 
 LOSS_TOL = 1e-4
 BUF_TOL = 1e-4
+EACH_TOL = 2e-3  # per-tensor gradient rel-L2, every tensor (round 2 worst: 9.8e-4)
 CONFIGS = {  # id -> (workload, B, k)
     "qm9_B512_k1": ("qm9", 512, 1),
     "molpcba_B1024_k1": ("molpcba", 1024, 1),
@@ -124,7 +126,7 @@ def _check(c, model, losses):
     for name, a, b in zip(("kl", "contrastive", "recon", "total"), losses, c.ref["losses"]):
         assert rel_err(a, b) < LOSS_TOL, (c.name, name, a, b)
     params = dict(model.named_parameters())
-    errs = check_grads_model(c.ref["grads"], lambda n: params[n].grad)
+    errs = check_grads_model(c.ref["grads"], lambda n: params[n].grad, each_tol=EACH_TOL)
     worst = max(errs.items(), key=lambda kv: kv[1])
     print(f"{c.name}: worst per-tensor grad rel-L2 {worst[0]} {worst[1]:.2e}")
     bufs = dict(model.named_buffers())

@@ -32,6 +32,10 @@ def test_library_exports_every_header_symbol(pkg):
     loaded = lib_mod.load()
     assert loaded.scgib_abi_version() == lib_mod.ABI_VERSION
     assert loaded.scgib_strerror(-1).decode().startswith("invalid")
+    # the persistent pair forward takes its arguments as one struct: its ctypes
+    # mirror must have the C layout's size
+    assert loaded.scgib_gin_pair_args_bytes() == ctypes.sizeof(lib_mod.PairFwdArgs)
+    assert loaded.scgib_gin_pair_bwd_args_bytes() == ctypes.sizeof(lib_mod.PairBwdArgs)
 
 
 def test_argument_errors_do_not_launch(pkg):

@@ -788,7 +788,7 @@ def _pair_persistent_ok(x, ego, core, gin_ego, gin_core, training, w0):
     if w0 is not None and tuple(w0.shape) != (HIDDEN, HIDDEN):
         return False
     for gr, gin in ((ego, gin_ego), (core, gin_core)):
-        if not (getattr(gr, "components_closed", False) and gr.num_nodes() > 0
+        if not (getattr(gr, "components_closed", False) and gr.symmetric and gr.num_nodes() > 0
                 and gr.batch_size > 0):
             return False
         if not 1 <= gr.max_graph_nodes <= int(_lib.query("scgib_gin_pair_max_component")):

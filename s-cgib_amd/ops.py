@@ -896,7 +896,11 @@ def _pair_backward_persistent(ctx, g_s, g_ro, g_f, g_t):
             wg0 = torch.empty(HIDDEN * HIDDEN + HIDDEN, dtype=torch.float32, device=dev)
             jobs.append(_lib.SlabJob(lin_slab.data_ptr(), wg0.data_ptr(), wg0.numel(), nchs[1], 0))
             dw0, db0 = wg0[: HIDDEN * HIDDEN].view(HIDDEN, HIDDEN), wg0[HIDDEN * HIDDEN:]
-    _lib.call("scgib_gin_pair_bwd", ctypes.cast(ctypes.pointer(args), ctypes.c_void_p), _stream())
+    meta = None if OBSERVER is None else {
+        "layers": [(ctx.sub[e].graph.num_nodes(), ctx.sub[e].graph.edge_capacity(),
+                    32 if l == 0 else HIDDEN) for e in (0, 1) for l in range(L)]}
+    _launch("scgib_gin_pair_bwd", meta, ctypes.cast(ctypes.pointer(args), ctypes.c_void_p),
+            _stream())
     scope = ctx.scope if (ctx.scope is not None and ctx.scope.open) else None
     if scope is not None:  # the loss section's deferred slabs: the same reduce launch
         sj, sk = scope.take()

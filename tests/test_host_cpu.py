@@ -444,3 +444,20 @@ def test_checkpoint_levels_roundtrip(pkg, tmp_path):
     assert not pkg.refckpt.is_reference_module_checkpoint(bad)
     with pytest.raises(pkg.refckpt.RefCheckpointError):
         pkg.refckpt.read(bad)
+
+
+def test_bench_kernel_table_evaluates(pkg):
+    """bench.py imports on a CPU host and every KERNELS entry's bytes / flops
+    evaluate on a launch meta of its shape (per-layer or persistent pair)."""
+    import importlib
+    import sys
+    sys.path.insert(0, ROOT)
+    bench = importlib.import_module("bench")
+    layer = {"n": 1000, "e": 2000, "d_in": 64}
+    pair = {"layers": [(1000, 2000, 32)] + [(1000, 2000, 64)] * 4}
+    for name, spec in bench.KERNELS.items():
+        m = pair if "pair" in name else layer
+        b = bench._call_meta(spec["bytes"], m)
+        f = bench._call_meta(spec["flops"], m)
+        assert b > 0 and f >= 0, name
+    assert bench.pair_fwd_bytes(pair) == sum(bench.agg_bytes(n, e, d) for n, e, d in pair["layers"])

@@ -82,6 +82,14 @@ def test_pair_forward_graph_replay(pkg, dev, monkeypatch):
     ug = torch.empty(n_cap, device=dev)
     uf = torch.empty(n_cap, 64, device=dev)
     monkeypatch.setattr(pkg.ops, "PAIR_PERSISTENT", True)
+    calls = []
+    orig = pkg.ops._pair_forward_persistent
+
+    def counting(*a, **k):
+        calls.append(1)
+        return orig(*a, **k)
+
+    monkeypatch.setattr(pkg.ops, "_pair_forward_persistent", counting)
     # warm-up off the capture
     side = torch.cuda.Stream()
     side.wait_stream(torch.cuda.current_stream())
@@ -97,6 +105,7 @@ def test_pair_forward_graph_replay(pkg, dev, monkeypatch):
         _, kl, con, rec = m_cap(static.graph, static.x, None, None, None, 1, None, 1, dev, B,
                                 noise=(ug, uf))
         (kl + rec + con).backward()
+    assert len(calls) == 2, "the persistent path was not captured"
     for i, gh in enumerate(hosts):
         n = gh.num_nodes()
         nz = _noise(n_cap, dev, 500 + i)

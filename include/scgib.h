@@ -264,9 +264,11 @@ int scgib_gin_layer_bwd(const float *dy, const float *z2, const float *r, const 
 #define SCGIB_PAIR_MAX_LAYERS 6
 typedef struct {
     const int32_t *rowptr, *col;  /* symmetric CSR (components closed) */
-    const int32_t *comp_ptr;      /* [n_comp + 1] component starts (entries past the
-                                     actual count equal the row count) */
+    const int32_t *comp_ptr;      /* [n_comp + 1] component starts (only the first
+                                     actual count + 1 entries are read) */
     int64_t n_comp;               /* components (capacity) */
+    const int32_t *comp_dims;     /* device: [0] = the actual component count
+                                     (capacity mode), or NULL: n_comp */
     const int32_t *dims;          /* device [n, e] or NULL */
     int64_t n_cap;                /* rows (capacity) */
     const int32_t *node_map;      /* layer-0 row -> row of x, or NULL (identity) */
@@ -315,6 +317,7 @@ typedef struct {
 typedef struct {
     const int32_t *rowptr, *col, *comp_ptr;
     int64_t n_comp;
+    const int32_t *comp_dims;     /* as scgib_pair_encoder */
     const int32_t *dims;
     int64_t n_cap;
     const float *agg[SCGIB_PAIR_MAX_LAYERS], *r[SCGIB_PAIR_MAX_LAYERS];

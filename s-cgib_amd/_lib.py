@@ -163,6 +163,7 @@ class PairEncoder(ctypes.Structure):
     _L = PAIR_MAX_LAYERS
     _fields_ = [("rowptr", ctypes.c_void_p), ("col", ctypes.c_void_p),
                 ("comp_ptr", ctypes.c_void_p), ("n_comp", ctypes.c_int64),
+                ("comp_dims", ctypes.c_void_p),
                 ("dims", ctypes.c_void_p), ("n_cap", ctypes.c_int64),
                 ("node_map", ctypes.c_void_p),
                 ("w1", ctypes.c_void_p * _L), ("b1", ctypes.c_void_p * _L),
@@ -192,6 +193,7 @@ class PairBwdEncoder(ctypes.Structure):
     _L = PAIR_MAX_LAYERS
     _fields_ = [("rowptr", ctypes.c_void_p), ("col", ctypes.c_void_p),
                 ("comp_ptr", ctypes.c_void_p), ("n_comp", ctypes.c_int64),
+                ("comp_dims", ctypes.c_void_p),
                 ("dims", ctypes.c_void_p), ("n_cap", ctypes.c_int64),
                 ("agg", ctypes.c_void_p * _L), ("r", ctypes.c_void_p * _L),
                 ("z2", ctypes.c_void_p * _L), ("stat", ctypes.c_void_p * _L),
@@ -212,7 +214,7 @@ class PairBwdArgs(ctypes.Structure):
                 ("n_feat", ctypes.c_int32), ("sync", ctypes.c_void_p)]
 
 
-ABI_VERSION = 6
+ABI_VERSION = 7
 STATS_STRIDE = 260
 PGRAD_STRIDE = 324
 HIDDEN = 64

@@ -377,6 +377,13 @@ struct Chunk {
     bool lds_col;
 };
 
+// valid components: comp_dims[0] (capacity mode), clamped to the capacity
+__device__ __forceinline__ int64_t comp_count(const int32_t *comp_dims, int64_t n_comp) {
+    if (!comp_dims) return n_comp;
+    const int64_t k = comp_dims[0];
+    return k < 0 ? 0 : (k < n_comp ? k : n_comp);
+}
+
 __device__ Chunk load_chunk(const int32_t *__restrict__ rowptr, const int32_t *__restrict__ col,
                             const int32_t *__restrict__ comp_ptr, int64_t n_comp, int64_t nch,
                             int64_t c, uint32_t *sync, Smem &sm,
@@ -452,7 +459,8 @@ __global__ __launch_bounds__(256, 3) void gin_pair_fwd_k(const scgib_pair_fwd_ar
 
     // ---- this chunk: components [i0, i1), rows [rb0, rb1)
     int32_t *par = reinterpret_cast<int32_t *>(sm.buf1);  // layer 0 only
-    const Chunk ck = load_chunk(E.rowptr, E.col, E.comp_ptr, E.n_comp, nch, c, A.sync, sm,
+    const int64_t nce = comp_count(E.comp_dims, E.n_comp);
+    const Chunk ck = load_chunk(E.rowptr, E.col, E.comp_ptr, nce, nch, c, A.sync, sm,
                                 E.node_map, par);
     const int64_t i0 = ck.i0, i1 = ck.i1;
     const int rb0 = ck.rb0, nr = ck.nr, nrb = ck.nrb, ncomp = ck.ncomp;
@@ -607,6 +615,10 @@ __global__ __launch_bounds__(256, 3) void gin_pair_fwd_k(const scgib_pair_fwd_ar
         for (int64_t k = i0 + ncomp + (tid >> 4); k < i1; k += 16)
             st4(E.readout + k * 64 + 4 * (tid & 15), make_float4(0.f, 0.f, 0.f, 0.f));
         for (int64_t v = z0 + tid; v < z1; v += 256) E.seg[v] = 0;
+        // capacity mode: the components past the actual count, round robin
+        if (tid < 16)
+            for (int64_t k = nce + c; k < E.n_comp; k += nch)
+                st4(E.readout + k * 64 + 4 * tid, make_float4(0.f, 0.f, 0.f, 0.f));
     }
     if (E.lin_w) {  // compressor[0] (models.py:596) on the output
         float fw0[16];
@@ -780,7 +792,8 @@ __global__ __launch_bounds__(256, 3) void gin_pair_bwd_k(const scgib_pair_bwd_ar
     unsigned *cnt = E.counters;
     const int64_t n = E.dims ? static_cast<int64_t>(E.dims[0]) : E.n_cap;
 
-    const Chunk ck = load_chunk(E.rowptr, E.col, E.comp_ptr, E.n_comp, nch, c, A.sync, sm);
+    const Chunk ck = load_chunk(E.rowptr, E.col, E.comp_ptr, comp_count(E.comp_dims, E.n_comp),
+                                nch, c, A.sync, sm);
     const int rb0 = ck.rb0, nr = ck.nr, nrb = ck.nrb, ns = (ck.nr + 3) / 4;
     const int q4 = tid & 15, rs = tid >> 4;  // thread-row-wise roles: float4 slot, rows rs + 16 k
     float *P = sm.buf0, *Q = sm.buf1;

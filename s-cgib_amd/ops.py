@@ -803,6 +803,14 @@ def _pair_persistent_ok(x, ego, core, gin_ego, gin_core, training, w0):
     return chunks <= int(_lib.query("scgib_gin_pair_slots"))
 
 
+def _comp_dims(gr):
+    """Device count of gr's valid components in capacity mode: an ego batch
+    has one ego-net per actual molecule node (its seg_dims[0]); its
+    graph_ptr entries past that count are not maintained."""
+    sd = getattr(gr, "seg_dims", None)
+    return sd.data_ptr() if (gr.dims is not None and sd is not None) else None
+
+
 def _pair_backward_persistent(ctx, g_s, g_ro, g_f, g_t):
     """_GinEncoderPair.backward through scgib_gin_pair_bwd (one launch, both
     encoders, compressor[0]'s backward first on Encoder1's chunks), then ONE
@@ -837,6 +845,7 @@ def _pair_backward_persistent(ctx, g_s, g_ro, g_f, g_t):
         E = args.enc[e]
         E.rowptr, E.col = gr.rowptr.data_ptr(), gr.col.data_ptr()
         E.comp_ptr, E.n_comp = gr.graph_ptr.data_ptr(), gr.batch_size
+        E.comp_dims = _comp_dims(gr)
         E.dims = gr.dims.data_ptr() if gr.dims is not None else None
         E.n_cap = n
         E.aggx = aggx.data_ptr()
@@ -931,6 +940,7 @@ def _pair_forward_persistent(ctx, x, wt, w0, b0, nmap, ego, core, gin_ego, gin_c
         E = args.enc[e]
         E.rowptr, E.col = gr.rowptr.data_ptr(), gr.col.data_ptr()
         E.comp_ptr, E.n_comp = gr.graph_ptr.data_ptr(), gr.batch_size
+        E.comp_dims = _comp_dims(gr)
         E.dims = gr.dims.data_ptr() if gr.dims is not None else None
         E.n_cap = n
         E.node_map = nmap.data_ptr() if (e == 0 and nmap is not None) else None

@@ -299,6 +299,8 @@ typedef struct {
     int32_t n_layers;             /* <= SCGIB_PAIR_MAX_LAYERS */
     uint32_t *sync;               /* 4 ZEROED words: [0] exit count (left zeroed),
                                      [1] timeout code (0: none) */
+    uint64_t *trace;              /* diagnostics: NULL, or [grid][64] wall-clock stamps
+                                     of each workgroup's phases */
 } scgib_pair_fwd_args;
 /* The backward of scgib_gin_pair_fwd, the same way: one workgroup per chunk,
  * d h of the chunk's rows kept in LDS from layer to layer (the transposed
@@ -339,6 +341,7 @@ typedef struct {
     int32_t n_layers;
     int32_t n_feat;
     uint32_t *sync;               /* as scgib_pair_fwd_args.sync */
+    uint64_t *trace;              /* as scgib_pair_fwd_args.trace */
 } scgib_pair_bwd_args;
 int64_t scgib_gin_pair_bwd_args_bytes(void);
 int scgib_gin_pair_bwd(const scgib_pair_bwd_args *args, scgib_stream_t stream);

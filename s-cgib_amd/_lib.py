@@ -185,7 +185,8 @@ class PairEncoder(ctypes.Structure):
 class PairFwdArgs(ctypes.Structure):
     """scgib_pair_fwd_args (include/scgib.h)."""
     _fields_ = [("enc", PairEncoder * 2), ("x", ctypes.c_void_p), ("n_feat", ctypes.c_int32),
-                ("wt", ctypes.c_void_p), ("n_layers", ctypes.c_int32), ("sync", ctypes.c_void_p)]
+                ("wt", ctypes.c_void_p), ("n_layers", ctypes.c_int32), ("sync", ctypes.c_void_p),
+                ("trace", ctypes.c_void_p)]
 
 
 class PairBwdEncoder(ctypes.Structure):
@@ -211,7 +212,8 @@ class PairBwdEncoder(ctypes.Structure):
 class PairBwdArgs(ctypes.Structure):
     """scgib_pair_bwd_args (include/scgib.h)."""
     _fields_ = [("enc", PairBwdEncoder * 2), ("n_layers", ctypes.c_int32),
-                ("n_feat", ctypes.c_int32), ("sync", ctypes.c_void_p)]
+                ("n_feat", ctypes.c_int32), ("sync", ctypes.c_void_p),
+                ("trace", ctypes.c_void_p)]
 
 
 ABI_VERSION = 7

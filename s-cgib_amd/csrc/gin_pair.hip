@@ -40,11 +40,11 @@
 namespace scgib {
 namespace pair {
 
-constexpr int kWin = 64;                 // chunk window (rows)
-constexpr int kRows = 96;                // max rows per chunk
+constexpr int kWin = 80;                 // chunk window (rows)
+constexpr int kRows = 112;               // max rows per chunk
 constexpr int kMaxComp = kRows - kWin + 1;  // max component rows (33)
 constexpr int kNrb = kRows / 16;         // 16-row blocks
-constexpr int kMaxE = 256;               // chunk edges cached in LDS (else read from global)
+constexpr int kMaxE = 512;               // chunk edges cached in LDS (else read from global)
 constexpr int kGrp = 16;                 // chunk partials per group
 constexpr int kPart = 132;               // floats per chunk partial: S[64] M2[64] n pad[3]
 constexpr int kGPart = 130;              // doubles per group partial: n S[64] M2[64] pad
@@ -60,15 +60,27 @@ __device__ __forceinline__ int sidx(int row, int col) {
 __host__ __device__ inline int64_t n_chunks(int64_t n_cap) { return (n_cap + kWin - 1) / kWin; }
 __host__ __device__ inline int64_t n_groups(int64_t n_cap) { return (n_chunks(n_cap) + kGrp - 1) / kGrp; }
 
-// workspace layout (per encoder): chunk partials | group partials | (scale, shift)
+constexpr int kMaxGroups = 32;           // groups per encoder (512 co-resident chunks)
+constexpr int kPubB = 8;                 // group partials per load batch of the publisher
+
+// merge (nb rows, sum sb, centred M2 mb) into the running (n, mean, M2)
+__device__ __forceinline__ void chan_merge(double &n, double &mean, double &m2, double nb, double sb,
+                                           double mb) {
+    if (nb <= 0.0) return;
+    const double meanb = sb / nb, nn = n + nb, d = meanb - mean;
+    mean += d * (nb / nn);
+    m2 += mb + d * d * (n * nb / nn);
+    n = nn;
+}
+
+// workspace layout (per encoder): group partials | chunk partials
 struct Ws {
     float *part;     // [L][nch][kPart]
     double *gpart;   // [L][ngr][kGPart]
-    float *ss;       // [L][128]
 };
 __host__ __device__ inline int64_t ws_part_floats(int64_t n_cap) { return n_chunks(n_cap) * kPart; }
 __host__ __device__ inline int64_t ws_bytes(int64_t n_cap, int L) {
-    return L * (ws_part_floats(n_cap) * 4 + n_groups(n_cap) * kGPart * 8 + 128 * 4) + 64;
+    return L * (ws_part_floats(n_cap) * 4 + n_groups(n_cap) * kGPart * 8) + 64;
 }
 __device__ inline Ws ws_of(void *ws, int64_t n_cap, int L) {
     char *p = reinterpret_cast<char *>((reinterpret_cast<uintptr_t>(ws) + 15) & ~uintptr_t(15));
@@ -76,12 +88,28 @@ __device__ inline Ws ws_of(void *ws, int64_t n_cap, int L) {
     w.gpart = reinterpret_cast<double *>(p);
     p += static_cast<int64_t>(L) * n_groups(n_cap) * kGPart * 8;
     w.part = reinterpret_cast<float *>(p);
-    p += static_cast<int64_t>(L) * ws_part_floats(n_cap) * 4;
-    w.ss = reinterpret_cast<float *>(p);
     return w;
 }
-// counters (per encoder): group arrivals [kL][ngr] | publisher arrivals [kL] | flags [kL]
-__host__ __device__ inline int64_t n_counters(int64_t n_cap, int) { return kL * (n_groups(n_cap) + 2); }
+// counters (per encoder, zeroed once, kept across launches): group arrivals
+// [kL][ngr] | publisher arrivals [kL] | launch epoch | the published values
+// [kL][128] as tagged words (epoch + 1) << 32 | float bits, 8-byte aligned.
+// A published word carries its own launch tag, so readers poll the data
+// itself: no flag, nothing to re-arm, and a stale word never matches.
+struct Cnt {
+    unsigned *grp, *pub, *epoch;
+    uint64_t *ss;
+};
+__host__ __device__ inline int64_t n_counters(int64_t n_cap, int) {
+    return kL * (n_groups(n_cap) + 1) + 1 + 1 + 2 * kL * 128;
+}
+__device__ inline Cnt cnt_of(unsigned *base, int64_t ngr) {
+    Cnt k;
+    k.grp = base;
+    k.pub = base + kL * ngr;
+    k.epoch = k.pub + kL;
+    k.ss = reinterpret_cast<uint64_t *>((reinterpret_cast<uintptr_t>(k.epoch + 1) + 7) & ~uintptr_t(7));
+    return k;
+}
 
 struct Smem {
     alignas(16) float buf0[kRows * 64];   // z2 of the previous layer / aggx / r / z2
@@ -90,15 +118,46 @@ struct Smem {
     int32_t colv[kMaxE];      // chunk-local neighbour rows
     int32_t cs[kRows + 2];    // chunk-local component starts (readout)
     float ss[128];            // (scale, shift) of the previous layer's BatchNorm
-    int32_t sb[2][4];         // bound searches: lo, hi, first hit
+    int32_t sb[2][4];         // bound searches: lo, hi, first hit; sb[0][3]: max degree
     unsigned flag;            // block-wide broadcast of a ticket / last-arriver flag
     alignas(16) float red[4][128];  // backward: the waves' column sums; exchange scratch
 };
 
 __device__ __forceinline__ uint64_t now() { return wall_clock64(); }
 
+// diagnostics: wall-clock stamp i of this workgroup (trace != NULL)
+__device__ __forceinline__ void mark(uint64_t *tr, int i) {
+    if (tr && threadIdx.x == 0) tr[i] = now();
+}
+
 __device__ __forceinline__ void set_err(uint32_t *sync, unsigned code) {
     __hip_atomic_store(sync + 1, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ void st_tagged(uint64_t *p, unsigned tag, float v) {
+    __hip_atomic_store(p, (static_cast<uint64_t>(tag) << 32) | __float_as_uint(v), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// threads 0..127 wait for the 128 words of src carrying this launch's tag and
+// leave their values in dst (then a block barrier)
+__device__ void await_tagged(const uint64_t *src, unsigned tag, float *dst, uint32_t *sync, unsigned code) {
+    const int tid = threadIdx.x;
+    if (tid < 128) {
+        const uint64_t t0 = now();
+        uint64_t v;
+        while (true) {
+            v = __hip_atomic_load(src + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (__all(static_cast<unsigned>(v >> 32) == tag)) break;  // wave-uniform
+            __builtin_amdgcn_s_sleep(1);
+            if (now() - t0 > kTimeout) {
+                set_err(sync, code);
+                break;
+            }
+        }
+        dst[tid] = __uint_as_float(static_cast<unsigned>(v));
+    }
+    __syncthreads();
 }
 
 // Count this workgroup in (every wave's stores drained first) and return the
@@ -216,8 +275,8 @@ struct Layer {  // this layer's per-encoder constants
 // The BatchNorm exchange of layer l for chunk c (rows nr): chunk partial from
 // the z2 accumulators -> group -> publisher -> (scale, shift) into sm.ss.
 __device__ void bn_exchange(const f32x4 (&z)[kNrb], int nrb, int nr, int64_t c, int64_t nch,
-                            int64_t ngr, int l, const Ws &ws, unsigned *cnt, const Layer &Ly,
-                            uint32_t *sync, Smem &sm) {
+                            int64_t ngr, int l, const Ws &ws, const Cnt &cnt, unsigned tag,
+                            const Layer &Ly, uint32_t *sync, Smem &sm, uint64_t *tr) {
     const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4;
     const int col = acc_col16();
     // ---- chunk partial: column sum and centred M2 over the valid rows (fp32)
@@ -250,14 +309,15 @@ __device__ void bn_exchange(const f32x4 (&z)[kNrb], int nrb, int nr, int64_t c, 
     // ---- group combine by the group's last arriving chunk
     const int64_t grp = c / kGrp, g0 = grp * kGrp;
     const int gsize = static_cast<int>(nch - g0 < kGrp ? nch - g0 : kGrp);
-    unsigned *gcnt = cnt + static_cast<int64_t>(l) * ngr + grp;
-    unsigned *pub = cnt + static_cast<int64_t>(ngr) * kL + l;           // publisher arrivals
-    unsigned *flag = cnt + static_cast<int64_t>(ngr) * kL + kL + l;     // published
+    unsigned *gcnt = cnt.grp + static_cast<int64_t>(l) * ngr + grp;
+    unsigned *pub = cnt.pub + l;                                        // publisher arrivals
     double *dscr = reinterpret_cast<double *>(sm.buf1);                 // 4 KB of scratch
     const int ch = tid & 63, p = tid >> 6;
     const Ws &W = ws;
     bool publisher = false;
-    if (arrive(gcnt, sm) == static_cast<unsigned>(gsize - 1)) {
+    const bool last_in_group = arrive(gcnt, sm) == static_cast<unsigned>(gsize - 1);
+    mark(tr, 4);
+    if (last_in_group) {
         // partition p takes chunks g0 + p + 4 u (fixed order), channel ch
         float S[4], Q[4], N[4];
 #pragma unroll
@@ -298,40 +358,45 @@ __device__ void bn_exchange(const f32x4 (&z)[kNrb], int nrb, int nr, int64_t c, 
         }
         if (tid == 0) __hip_atomic_store(gcnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         publisher = arrive(pub, sm) == static_cast<unsigned>(ngr - 1);
+        mark(tr, 5);
     }
     if (publisher) {  // block-uniform: the last group in combines every group
-        double a = 0.0, nn = 0.0;
-        for (int64_t g1 = p; g1 < ngr; g1 += 4) {
-            const double *gp = W.gpart + (static_cast<int64_t>(l) * ngr + g1) * kGPart;
-            a += ld_agent(gp + 1 + ch);
-            nn += ld_agent(gp);
-        }
-        __syncthreads();
-        dscr[p * 64 + ch] = a;
-        dscr[256 + p * 64 + ch] = nn;
-        __syncthreads();
-        const double S = ((dscr[ch] + dscr[64 + ch]) + dscr[128 + ch]) + dscr[192 + ch];
-        const double N = ((dscr[256 + ch] + dscr[320 + ch]) + dscr[384 + ch]) + dscr[448 + ch];
-        const double m = N > 0.0 ? S / N : 0.0;
-        double qq = 0.0;
-        for (int64_t g1 = p; g1 < ngr; g1 += 4) {
-            const double *gp = W.gpart + (static_cast<int64_t>(l) * ngr + g1) * kGPart;
-            const double ng = ld_agent(gp);
-            if (ng > 0.0) {
-                const double d = ld_agent(gp + 1 + ch) - ng * m;
-                qq += ld_agent(gp + 65 + ch) + d * d / ng;
+        // partition p merges groups p + 4 u in order (Chan et al.'s pairwise
+        // update, fp64), loading kPubB groups per batch
+        double an = 0.0, am = 0.0, aq = 0.0;
+        for (int u0 = 0; u0 < kMaxGroups / 4 && p + 4 * u0 < ngr; u0 += kPubB) {
+            double Nv[kPubB], Sv[kPubB], Mv[kPubB];
+#pragma unroll
+            for (int u = 0; u < kPubB; ++u) {
+                const int64_t g1 = p + 4 * (u0 + u);
+                const double *gp = W.gpart + (static_cast<int64_t>(l) * ngr + (g1 < ngr ? g1 : 0)) * kGPart;
+                Nv[u] = ld_agent(gp);
+                Sv[u] = ld_agent(gp + 1 + ch);
+                Mv[u] = ld_agent(gp + 65 + ch);
             }
+#pragma unroll
+            for (int u = 0; u < kPubB; ++u)
+                if (p + 4 * (u0 + u) < ngr) chan_merge(an, am, aq, Nv[u], Sv[u], Mv[u]);
         }
         __syncthreads();
-        dscr[p * 64 + ch] = qq;
+        dscr[p * 64 + ch] = an;
+        dscr[256 + p * 64 + ch] = am;
+        dscr[512 + p * 64 + ch] = aq;
         __syncthreads();
+        double N = 0.0, m = 0.0, M2 = 0.0;
+#pragma unroll
+        for (int pp = 0; pp < 4; ++pp) {
+            const double nb = dscr[pp * 64 + ch];
+            chan_merge(N, m, M2, nb, dscr[256 + pp * 64 + ch] * nb, dscr[512 + pp * 64 + ch]);
+        }
         if (p == 0) {
-            const double M2 = ((dscr[ch] + dscr[64 + ch]) + dscr[128 + ch]) + dscr[192 + ch];
             const double var = N > 0.0 ? M2 / N : 0.0;
             const double istd = 1.0 / sqrt(var + static_cast<double>(Ly.eps));
             const double sc = static_cast<double>(Ly.gamma[ch]) * istd;
             const float scale = static_cast<float>(sc);
             const float shift = static_cast<float>(static_cast<double>(Ly.beta[ch]) - m * sc);
+            st_tagged(cnt.ss + l * 128 + ch, tag, scale);
+            st_tagged(cnt.ss + l * 128 + 64 + ch, tag, shift);
             if (Ly.rmean) {
                 const double mo = static_cast<double>(Ly.mom);
                 Ly.rmean[ch] = static_cast<float>((1.0 - mo) * Ly.rmean[ch] + mo * m);
@@ -343,28 +408,13 @@ __device__ void bn_exchange(const f32x4 (&z)[kNrb], int nrb, int nr, int64_t c, 
             Ly.stat[64 + ch] = static_cast<float>(istd);
             Ly.stat[128 + ch] = scale;
             Ly.stat[192 + ch] = shift;
-            st_agent(W.ss + l * 128 + ch, scale);
-            st_agent(W.ss + l * 128 + 64 + ch, shift);
         }
         if (tid == 0) __hip_atomic_store(pub, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        if (tid == 0) __hip_atomic_store(flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        mark(tr, 6);
     }
-    // ---- every chunk: wait for the published (scale, shift)
-    if (tid == 0) {
-        const uint64_t t0 = now();
-        while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) {
-            __builtin_amdgcn_s_sleep(2);
-            if (now() - t0 > kTimeout) {
-                set_err(sync, 0x100u + l);
-                break;
-            }
-        }
-    }
-    __syncthreads();
-    if (tid < 128) sm.ss[tid] = ld_agent(W.ss + l * 128 + tid);
-    __syncthreads();
+    // ---- every chunk: the published (scale, shift)
+    await_tagged(cnt.ss + l * 128, tag, sm.ss, sync, 0x100u + l);
+    mark(tr, 7);
 }
 
 // This workgroup's chunk c of a graph: components [i0, i1), rows [rb0, rb1),
@@ -374,6 +424,7 @@ __device__ void bn_exchange(const f32x4 (&z)[kNrb], int nrb, int nr, int64_t c, 
 struct Chunk {
     int64_t i0, i1;
     int rb0, rb1, nr, nrb, ncomp, e0;
+    int maxdeg;  // the largest row degree of the chunk
     bool lds_col;
 };
 
@@ -415,7 +466,11 @@ __device__ Chunk load_chunk(const int32_t *__restrict__ rowptr, const int32_t *_
         for (int i = tid; i < ne; i += 256) sm.colv[i] = col[k.e0 + i] - k.rb0;
     __syncthreads();
     if (tid <= k.nr) sm.rp[tid] -= k.e0;
+    if (tid == 0) sm.sb[0][3] = 0;
     __syncthreads();
+    if (tid < k.nr) atomicMax(&sm.sb[0][3], sm.rp[tid + 1] - sm.rp[tid]);
+    __syncthreads();
+    k.maxdeg = sm.sb[0][3];
     return k;
 }
 
@@ -428,7 +483,47 @@ __device__ __forceinline__ int nbr_of(const Chunk &k, const int32_t *__restrict_
     return u < 0 ? 0 : (u < k.nr ? u : k.nr - 1);
 }
 
-__global__ __launch_bounds__(256, 3) void gin_pair_fwd_k(const scgib_pair_fwd_args A) {
+// out[v] = ope f(S[v]) + sum over v's neighbours u of f(S[u]) for the rows
+// v = rs + 16 k (k < kNrb) of this thread's float4 slot q (f: per-column
+// transform, e.g. the previous BatchNorm + ReLU); rows >= nr give zeros.  All
+// rows' neighbour reads of one degree step go out together (the chunk's max
+// degree bounds the steps; a missing neighbour enters as fmaf(x, 0, acc), so
+// the sum equals the CSR-order sum bit for bit).  epi(k, v, value).
+template <class Fn, class Epi>
+__device__ __forceinline__ void aggregate_rows(const Chunk &ck, const int32_t *__restrict__ col,
+                                               const Smem &sm, const float *S, float ope, int q,
+                                               int rs, Fn f, Epi epi) {
+    float4 acc[kNrb];
+    int e0[kNrb], dg[kNrb];
+#pragma unroll
+    for (int k = 0; k < kNrb; ++k) {
+        const int v = rs + 16 * k, vv = v < ck.nr ? v : 0;
+        e0[k] = sm.rp[vv];
+        dg[k] = v < ck.nr ? sm.rp[vv + 1] - e0[k] : 0;
+        const float4 x = f(*reinterpret_cast<const float4 *>(S + sidx(vv, 4 * q)));
+        acc[k] = make_float4(ope * x.x, ope * x.y, ope * x.z, ope * x.w);
+    }
+    const int elast = sm.rp[ck.nr] - 1;  // (>= 0 whenever maxdeg > 0)
+    for (int j = 0; j < ck.maxdeg; ++j) {
+        int u[kNrb];
+#pragma unroll
+        for (int k = 0; k < kNrb; ++k) u[k] = nbr_of(ck, col, sm, j < dg[k] ? e0[k] + j : elast);
+#pragma unroll
+        for (int k = 0; k < kNrb; ++k) {
+            const float w = j < dg[k] ? 1.f : 0.f;
+            const float4 x = f(*reinterpret_cast<const float4 *>(S + sidx(u[k], 4 * q)));
+            acc[k] = make_float4(fmaf(x.x, w, acc[k].x), fmaf(x.y, w, acc[k].y), fmaf(x.z, w, acc[k].z),
+                                 fmaf(x.w, w, acc[k].w));
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < kNrb; ++k) {
+        const int v = rs + 16 * k;
+        epi(k, v, v < ck.nr ? acc[k] : make_float4(0.f, 0.f, 0.f, 0.f));
+    }
+}
+
+__global__ __launch_bounds__(256, 2) void gin_pair_fwd_k(const scgib_pair_fwd_args A) {
     __shared__ Smem sm;
     const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
     const int64_t nch0 = n_chunks(A.enc[0].n_cap);
@@ -438,9 +533,12 @@ __global__ __launch_bounds__(256, 3) void gin_pair_fwd_k(const scgib_pair_fwd_ar
     const int64_t nch = n_chunks(E.n_cap), ngr = n_groups(E.n_cap);
     const int L = A.n_layers;
     const Ws ws = ws_of(E.ws, E.n_cap, L);
-    unsigned *cnt = E.counters;
+    const Cnt cnt = cnt_of(E.counters, ngr);
+    const unsigned tag = __hip_atomic_load(cnt.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
     const int64_t n = E.dims ? static_cast<int64_t>(E.dims[0]) : E.n_cap;
     const int F = A.n_feat;
+    uint64_t *tr = A.trace ? A.trace + static_cast<int64_t>(blockIdx.x) * 64 : nullptr;
+    mark(tr, 56);
 
     // ---- weights of layer 0 (in flight during the chunk search)
     float fw1[16], fw2[16], fwt[4];
@@ -466,6 +564,10 @@ __global__ __launch_bounds__(256, 3) void gin_pair_fwd_k(const scgib_pair_fwd_ar
     const int rb0 = ck.rb0, nr = ck.nr, nrb = ck.nrb, ncomp = ck.ncomp;
     const int win0 = static_cast<int>(c * kWin), win1 = static_cast<int>(c * kWin + kWin);
     auto nbr = [&](int ei) -> int { return nbr_of(ck, E.col, sm, ei); };
+    mark(tr, 57);
+    if (tr && tid == 0)
+        tr[61] = static_cast<uint64_t>(nr) | (static_cast<uint64_t>(sm.rp[nr]) << 8) |
+                 (static_cast<uint64_t>(ck.lds_col) << 30) | (static_cast<uint64_t>(e) << 31);
 
     // capacity padding rows this window zeroes (every output, every layer)
     const int64_t z0 = win0 > n ? win0 : n, z1 = win1 < E.n_cap ? win1 : E.n_cap;
@@ -517,10 +619,13 @@ __global__ __launch_bounds__(256, 3) void gin_pair_fwd_k(const scgib_pair_fwd_ar
         zero_rows<32>(E.agg[0], z0, z1);
     }
     __syncthreads();
+    mark(tr, 58);
 
     f32x4 z[kNrb];
     for (int l = 0; l < L; ++l) {
         const int din = l == 0 ? 32 : 64;
+        uint64_t *tl = tr ? tr + 8 * l : nullptr;
+        mark(tl, 0);
         if (l > 0) {
             // ---- aggregation from LDS: x = relu(scale z2 + shift) of the previous layer
             const int q = tid & 15, rs = tid >> 4;
@@ -528,22 +633,16 @@ __global__ __launch_bounds__(256, 3) void gin_pair_fwd_k(const scgib_pair_fwd_ar
             const float4 sc = make_float4(sm.ss[4 * q], sm.ss[4 * q + 1], sm.ss[4 * q + 2], sm.ss[4 * q + 3]);
             const float4 sh = make_float4(sm.ss[64 + 4 * q], sm.ss[65 + 4 * q], sm.ss[66 + 4 * q],
                                           sm.ss[67 + 4 * q]);
-            for (int v = rs; v < 16 * nrb; v += 16) {
-                float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
-                if (v < nr) {
-                    const float4 xv = xform4(*reinterpret_cast<const float4 *>(sm.buf0 + sidx(v, 4 * q)), sc, sh);
-                    a = make_float4(ope * xv.x, ope * xv.y, ope * xv.z, ope * xv.w);
-                    for (int ei = sm.rp[v]; ei < sm.rp[v + 1]; ++ei) {
-                        const int u = nbr(ei);
-                        a = add4(a, xform4(*reinterpret_cast<const float4 *>(sm.buf0 + sidx(u, 4 * q)), sc, sh));
-                    }
-                    st4(E.agg[l] + static_cast<int64_t>(rb0 + v) * 64 + 4 * q, a);
-                }
-                *reinterpret_cast<float4 *>(sm.buf1 + sidx(v, 4 * q)) = a;
-            }
+            aggregate_rows(ck, E.col, sm, sm.buf0, ope, q, rs,
+                           [&](float4 x) { return xform4(x, sc, sh); },
+                           [&](int, int v, float4 a) {
+                               if (v < nr) st4(E.agg[l] + static_cast<int64_t>(rb0 + v) * 64 + 4 * q, a);
+                               if (v < 16 * nrb) *reinterpret_cast<float4 *>(sm.buf1 + sidx(v, 4 * q)) = a;
+                           });
             zero_rows<64>(E.agg[l], z0, z1);
             __syncthreads();
         }
+        mark(tl, 1);
         // ---- z1 = agg W1^T; r = relu(z1 + b1) -> buf0 (its previous content is consumed)
         if (din == 32) gemm<32>(sm.buf1, fw1, nrb, z);
         else gemm<64>(sm.buf1, fw1, nrb, z);
@@ -556,6 +655,7 @@ __global__ __launch_bounds__(256, 3) void gin_pair_fwd_k(const scgib_pair_fwd_ar
         __syncthreads();
         lds_to_global<64>(sm.buf0, E.r[l], rb0, nr);
         zero_rows<64>(E.r[l], z0, z1);
+        mark(tl, 2);
         // ---- z2 = r W2^T + b2
         gemm<64>(sm.buf0, fw2, nrb, z);
 #pragma unroll
@@ -580,7 +680,8 @@ __global__ __launch_bounds__(256, 3) void gin_pair_fwd_k(const scgib_pair_fwd_ar
         }
         const Layer Ly{0.f, E.bn_eps[l], E.momentum[l], E.gamma[l], E.beta[l], E.running_mean[l],
                        E.running_var[l], E.stat[l], E.num_batches_tracked[l]};
-        bn_exchange(z, nrb, nr, c, nch, ngr, l, ws, cnt, Ly, A.sync, sm);
+        mark(tl, 3);
+        bn_exchange(z, nrb, nr, c, nch, ngr, l, ws, cnt, tag, Ly, A.sync, sm, tl);
     }
 
     // ---- encoder output: out = relu(BN(z2)) -> global and buf1
@@ -636,11 +737,18 @@ __global__ __launch_bounds__(256, 3) void gin_pair_fwd_k(const scgib_pair_fwd_ar
         zero_rows<64>(E.lin_out, z0, z1);
     }
 
-    // ---- exit: the last workgroup re-arms every flag of both encoders
+    // ---- exit: the last workgroup advances both encoders' epochs (the next
+    // launch's tag) and re-arms the publisher counters (already zero unless a
+    // spin timed out)
+    mark(tr, 60);
     if (arrive(A.sync, sm) == gridDim.x - 1) {
         for (int ee = 0; ee < 2; ++ee) {
-            unsigned *cc = A.enc[ee].counters + n_groups(A.enc[ee].n_cap) * kL;
-            if (tid < 2 * kL) __hip_atomic_store(cc + tid, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const Cnt k = cnt_of(A.enc[ee].counters, n_groups(A.enc[ee].n_cap));
+            if (tid < kL) __hip_atomic_store(k.pub + tid, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (tid == 64) {
+                const unsigned ep = __hip_atomic_load(k.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(k.epoch, ep + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
         }
         if (tid == 0) __hip_atomic_store(A.sync, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
@@ -673,17 +781,28 @@ template <int JB>
 __device__ __forceinline__ void gemm_tn(const float *X, const float *Y, int ns, f32x4 (&acc)[4],
                                         float &csum) {
     const int l = threadIdx.x & 63, r16 = l & 15, g = l >> 4, w = threadIdx.x >> 6;
-    for (int s = 0; s < ns; ++s) {
-        const int row = 4 * s + g;
-        const float a = X[sidx(row, 16 * w + r16)];
-        float b[JB];
+    auto step = [&](int s0, int cnt) {  // cnt (1 or 2) row steps, their LDS reads issued together
+        float a[2], b[2][JB];
 #pragma unroll
-        for (int jb = 0; jb < JB; ++jb) b[jb] = Y[sidx(row, 16 * jb + r16)];
-        csum += a;
+        for (int u = 0; u < 2; ++u)
+            if (u < cnt) {
+                const int row = 4 * (s0 + u) + g;
+                a[u] = X[sidx(row, 16 * w + r16)];
 #pragma unroll
-        for (int jb = 0; jb < JB; ++jb)
-            acc[jb] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b[jb], acc[jb], 0, 0, 0);
-    }
+                for (int jb = 0; jb < JB; ++jb) b[u][jb] = Y[sidx(row, 16 * jb + r16)];
+            }
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+            if (u < cnt) {
+                csum += a[u];
+#pragma unroll
+                for (int jb = 0; jb < JB; ++jb)
+                    acc[jb] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u], b[u][jb], acc[jb], 0, 0, 0);
+            }
+    };
+    int s = 0;
+    for (; s + 1 < ns; s += 2) step(s, 2);
+    if (s < ns) step(s, 1);
 }
 
 // B fragments of the product X W (W [K][N] row-major): column colbase + (lane
@@ -722,16 +841,17 @@ __device__ __forceinline__ void gemm_each(const float *A, const float (&f)[16], 
 // sum dy xhat, already stored at its partial) -> groups -> publisher, which
 // writes dbeta / dgamma and publishes the dz2 coefficients tot / N into sm.ss
 __device__ void bwd_exchange(int l, int64_t c, int64_t nch, int64_t ngr, int64_t n, const Ws &W,
-                             unsigned *cnt, float *dgamma, float *dbeta, uint32_t *sync, Smem &sm,
-                             double *dscr) {
+                             const Cnt &cnt, unsigned tag, float *dgamma, float *dbeta, uint32_t *sync, Smem &sm,
+                             double *dscr, uint64_t *tr) {
     const int tid = threadIdx.x, ch = tid & 127, p = tid >> 7;  // 128 sums x 2 partitions
     const int64_t grp = c / kGrp, g0 = grp * kGrp;
     const int gsize = static_cast<int>(nch - g0 < kGrp ? nch - g0 : kGrp);
-    unsigned *gcnt = cnt + static_cast<int64_t>(l) * ngr + grp;
-    unsigned *pub = cnt + static_cast<int64_t>(ngr) * kL + l;
-    unsigned *flag = cnt + static_cast<int64_t>(ngr) * kL + kL + l;
+    unsigned *gcnt = cnt.grp + static_cast<int64_t>(l) * ngr + grp;
+    unsigned *pub = cnt.pub + l;
     bool publisher = false;
-    if (arrive(gcnt, sm) == static_cast<unsigned>(gsize - 1)) {
+    const bool last_in_group = arrive(gcnt, sm) == static_cast<unsigned>(gsize - 1);
+    mark(tr, 2);
+    if (last_in_group) {
         float v[kGrp / 2];
 #pragma unroll
         for (int u = 0; u < kGrp / 2; ++u) {
@@ -746,40 +866,38 @@ __device__ void bwd_exchange(int l, int64_t c, int64_t nch, int64_t ngr, int64_t
         if (p == 0) st_agent(W.gpart + (static_cast<int64_t>(l) * ngr + grp) * kGPart + ch, dscr[ch] + dscr[128 + ch]);
         if (tid == 0) __hip_atomic_store(gcnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         publisher = arrive(pub, sm) == static_cast<unsigned>(ngr - 1);
+        mark(tr, 3);
     }
-    if (publisher) {
+    if (publisher) {  // partition p: groups p + 2 u in order, 16 loads per batch
         double a = 0.0;
-        for (int64_t g1 = p; g1 < ngr; g1 += 2) a += ld_agent(W.gpart + (static_cast<int64_t>(l) * ngr + g1) * kGPart + ch);
+        for (int u0 = 0; u0 < kMaxGroups / 2 && p + 2 * u0 < ngr; u0 += 16) {
+            double v[16];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int64_t g1 = p + 2 * (u0 + u);
+                v[u] = ld_agent(W.gpart + (static_cast<int64_t>(l) * ngr + (g1 < ngr ? g1 : 0)) * kGPart + ch);
+            }
+#pragma unroll
+            for (int u = 0; u < 16; ++u)
+                if (p + 2 * (u0 + u) < ngr) a += v[u];
+        }
         __syncthreads();
         dscr[p * 128 + ch] = a;
         __syncthreads();
         if (p == 0) {
             const double tot = dscr[ch] + dscr[128 + ch];
+            st_tagged(cnt.ss + l * 128 + ch, tag, static_cast<float>(tot / static_cast<double>(n)));
             if (ch < 64) dbeta[ch] = static_cast<float>(tot);
             else dgamma[ch - 64] = static_cast<float>(tot);
-            st_agent(W.ss + l * 128 + ch, static_cast<float>(tot / static_cast<double>(n)));
         }
         if (tid == 0) __hip_atomic_store(pub, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        if (tid == 0) __hip_atomic_store(flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        mark(tr, 4);
     }
-    if (tid == 0) {
-        const uint64_t t0 = now();
-        while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) {
-            __builtin_amdgcn_s_sleep(2);
-            if (now() - t0 > kTimeout) {
-                set_err(sync, 0x200u + l);
-                break;
-            }
-        }
-    }
-    __syncthreads();
-    if (tid < 128) sm.ss[tid] = ld_agent(W.ss + l * 128 + tid);
-    __syncthreads();
+    await_tagged(cnt.ss + l * 128, tag, sm.ss, sync, 0x200u + l);
+    mark(tr, 5);
 }
 
-__global__ __launch_bounds__(256, 3) void gin_pair_bwd_k(const scgib_pair_bwd_args A) {
+__global__ __launch_bounds__(256, 2) void gin_pair_bwd_k(const scgib_pair_bwd_args A) {
     __shared__ Smem sm;
     const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63, r16 = lane & 15, g = lane >> 4;
     const int64_t nch0 = n_chunks(A.enc[0].n_cap);
@@ -789,8 +907,11 @@ __global__ __launch_bounds__(256, 3) void gin_pair_bwd_k(const scgib_pair_bwd_ar
     const int64_t nch = n_chunks(E.n_cap), ngr = n_groups(E.n_cap);
     const int L = A.n_layers, F = A.n_feat;
     const Ws ws = ws_of(E.ws, E.n_cap, L);
-    unsigned *cnt = E.counters;
+    const Cnt cnt = cnt_of(E.counters, ngr);
+    const unsigned tag = __hip_atomic_load(cnt.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
     const int64_t n = E.dims ? static_cast<int64_t>(E.dims[0]) : E.n_cap;
+    uint64_t *tr = A.trace ? A.trace + static_cast<int64_t>(blockIdx.x) * 64 : nullptr;
+    mark(tr, 56);
 
     const Chunk ck = load_chunk(E.rowptr, E.col, E.comp_ptr, comp_count(E.comp_dims, E.n_comp),
                                 nch, c, A.sync, sm);
@@ -851,9 +972,12 @@ __global__ __launch_bounds__(256, 3) void gin_pair_bwd_k(const scgib_pair_bwd_ar
             }
     }
     __syncthreads();
+    mark(tr, 57);
 
     for (int l = L - 1; l >= 0; --l) {
         const int din = l == 0 ? 32 : 64;
+        uint64_t *tl = tr ? tr + 8 * l : nullptr;
+        mark(tl, 0);
         // ---- dy = dh [scale z2 + shift > 0] (in place), xhat, the chunk's sums
         const float *st = E.stat[l];
         const float4 mean = ld4(st + 4 * q4), istd = ld4(st + 64 + 4 * q4);
@@ -910,8 +1034,9 @@ __global__ __launch_bounds__(256, 3) void gin_pair_bwd_k(const scgib_pair_bwd_ar
 #pragma unroll
             for (int k = 0; k < kNrb; ++k) rr[k] = ld_row(rrs, rb0 + rs + 16 * k, 64, 4 * q4);
         }
-        bwd_exchange(l, c, nch, ngr, n, ws, cnt, E.dgamma[l], E.dbeta[l], A.sync, sm,
-                     reinterpret_cast<double *>(&sm.red[0][0]));
+        mark(tl, 1);
+        bwd_exchange(l, c, nch, ngr, n, ws, cnt, tag, E.dgamma[l], E.dbeta[l], A.sync, sm,
+                     reinterpret_cast<double *>(&sm.red[0][0]), tl);
         // ---- dz2 = scale (dy - c1 - xhat c2) -> P; r -> Q
         {
             const float4 c1 = make_float4(sm.ss[4 * q4], sm.ss[4 * q4 + 1], sm.ss[4 * q4 + 2], sm.ss[4 * q4 + 3]);
@@ -966,6 +1091,7 @@ __global__ __launch_bounds__(256, 3) void gin_pair_bwd_k(const scgib_pair_bwd_ar
                 *q = *q > 0.f ? d[i] : 0.f;
             }
         });
+        mark(tl, 6);
         __syncthreads();  // every read of P (dz2) done: agg -> P
 #pragma unroll
         for (int k = 0; k < kNrb; ++k) {
@@ -1004,16 +1130,10 @@ __global__ __launch_bounds__(256, 3) void gin_pair_bwd_k(const scgib_pair_bwd_ar
         if (l > 0) {
             // dh of layer l-1: (1+eps) d(agg)[v] + sum over v's neighbours (P -> Q)
             const float ope = E.one_plus_eps[l];
-            for (int v = rs; v < 16 * nrb; v += 16) {
-                float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
-                if (v < nr) {
-                    const float4 s0 = *reinterpret_cast<const float4 *>(P + sidx(v, 4 * q4));
-                    a = make_float4(ope * s0.x, ope * s0.y, ope * s0.z, ope * s0.w);
-                    for (int ei = sm.rp[v]; ei < sm.rp[v + 1]; ++ei)
-                        a = add4(a, *reinterpret_cast<const float4 *>(P + sidx(nbr_of(ck, E.col, sm, ei), 4 * q4)));
-                }
-                *reinterpret_cast<float4 *>(Q + sidx(v, 4 * q4)) = a;
-            }
+            aggregate_rows(ck, E.col, sm, P, ope, q4, rs, [](float4 x) { return x; },
+                           [&](int, int v, float4 a) {
+                               if (v < 16 * nrb) *reinterpret_cast<float4 *>(Q + sidx(v, 4 * q4)) = a;
+                           });
             __syncthreads();
             float *t = P;
             P = Q;
@@ -1037,11 +1157,18 @@ __global__ __launch_bounds__(256, 3) void gin_pair_bwd_k(const scgib_pair_bwd_ar
         }
     }
 
-    // ---- exit: the last workgroup re-arms every flag of both encoders
+    // ---- exit: the last workgroup advances both encoders' epochs (the next
+    // launch's tag) and re-arms the publisher counters (already zero unless a
+    // spin timed out)
+    mark(tr, 60);
     if (arrive(A.sync, sm) == gridDim.x - 1) {
         for (int ee = 0; ee < 2; ++ee) {
-            unsigned *cc = A.enc[ee].counters + n_groups(A.enc[ee].n_cap) * kL;
-            if (tid < 2 * kL) __hip_atomic_store(cc + tid, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const Cnt k = cnt_of(A.enc[ee].counters, n_groups(A.enc[ee].n_cap));
+            if (tid < kL) __hip_atomic_store(k.pub + tid, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (tid == 64) {
+                const unsigned ep = __hip_atomic_load(k.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(k.epoch, ep + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
         }
         if (tid == 0) __hip_atomic_store(A.sync, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
@@ -1067,13 +1194,16 @@ extern "C" int64_t scgib_gin_pair_counters(int64_t n_cap, int32_t n_layers) {
 extern "C" int64_t scgib_gin_pair_slots(void) {
     static int64_t slots = -1;
     if (slots < 0) {
-        int dev = 0, cus = 0, per = 0;
+        int dev = 0, cus = 0, per = 0, per_b = 0;
         if (hipGetDevice(&dev) != hipSuccess ||
             hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
             hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, pair::gin_pair_fwd_k, 256, 0) !=
+                hipSuccess ||
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_b, pair::gin_pair_bwd_k, 256, 0) !=
                 hipSuccess)
             return 0;
-        slots = static_cast<int64_t>(cus) * (per < 3 ? per : 3);
+        per = per < per_b ? per : per_b;
+        slots = static_cast<int64_t>(cus) * (per < 2 ? per : 2);
     }
     return slots;
 }
@@ -1089,7 +1219,9 @@ extern "C" int scgib_gin_pair_fwd(const scgib_pair_fwd_args *args, scgib_stream_
         if (E.n_cap <= 0 || E.n_comp <= 0 || !E.rowptr || !E.col || !E.comp_ptr || !E.aggx ||
             !E.out || !E.ws || !E.counters || (E.readout && !E.seg) || (E.lin_w && (!E.lin_b || !E.lin_out)))
             return SCGIB_EINVAL;
-        if (E.n_cap >= (int64_t(1) << 31) || E.n_comp >= (int64_t(1) << 31)) return SCGIB_EUNSUPPORTED;
+        if (E.n_cap >= (int64_t(1) << 31) || E.n_comp >= (int64_t(1) << 31) ||
+            pair::n_groups(E.n_cap) > pair::kMaxGroups)
+            return SCGIB_EUNSUPPORTED;
         for (int l = 0; l < A.n_layers; ++l)
             if (!E.w1[l] || !E.b1[l] || !E.w2[l] || !E.b2[l] || !E.gamma[l] || !E.beta[l] ||
                 !E.agg[l] || !E.r[l] || !E.z2[l] || !E.stat[l] ||
@@ -1116,7 +1248,9 @@ extern "C" int scgib_gin_pair_bwd(const scgib_pair_bwd_args *args, scgib_stream_
         if (E.n_cap <= 0 || E.n_comp <= 0 || !E.rowptr || !E.col || !E.comp_ptr || !E.aggx ||
             !E.ws || !E.counters || (E.lin_g && (!E.lin_w || !E.lin_in || !E.lin_slab)))
             return SCGIB_EINVAL;
-        if (E.n_cap >= (int64_t(1) << 31) || E.n_comp >= (int64_t(1) << 31)) return SCGIB_EUNSUPPORTED;
+        if (E.n_cap >= (int64_t(1) << 31) || E.n_comp >= (int64_t(1) << 31) ||
+            pair::n_groups(E.n_cap) > pair::kMaxGroups)
+            return SCGIB_EUNSUPPORTED;
         for (int l = 0; l < A.n_layers; ++l) {
             const int64_t width = 64 * 64 + 64 * (l == 0 ? 32 : 64) + 128 + (l == 0 ? 32 * A.n_feat : 0);
             if (!E.agg[l] || !E.r[l] || !E.z2[l] || !E.stat[l] || !E.w1[l] || !E.w2[l] ||

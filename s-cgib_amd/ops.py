@@ -772,6 +772,9 @@ def _torch_stream():
 # both encoders' chunks co-resident on the device.  Otherwise the per-layer
 # kernels.  (A module attribute: the tests run both paths.)
 PAIR_PERSISTENT = False  # (on once validated on the GPU)
+# diagnostics (tools/pair_trace.py): None, or two int64 device tensors
+# [grid * 64] receiving the forward's / backward's per-workgroup phase stamps
+PAIR_TRACE = None
 
 
 def pair_sync_error(device):
@@ -823,6 +826,8 @@ def _pair_backward_persistent(ctx, g_s, g_ro, g_f, g_t):
     args = _lib.PairBwdArgs()
     args.n_layers, args.n_feat = L, F
     args.sync = counters(dev, ("gin_pair_sync",), 4).data_ptr()
+    if PAIR_TRACE is not None:
+        args.trace = PAIR_TRACE[1].data_ptr()
     keep, jobs = [], []
     nchs = [int(_lib.query("scgib_gin_pair_chunks", ctx.sub[e].saved_tensors[2].shape[0]))
             for e in (0, 1)]
@@ -933,6 +938,8 @@ def _pair_forward_persistent(ctx, x, wt, w0, b0, nmap, ego, core, gin_ego, gin_c
     args = _lib.PairFwdArgs()
     args.x, args.n_feat, args.wt, args.n_layers = x.data_ptr(), x.shape[1], wt.data_ptr(), L
     args.sync = counters(dev, ("gin_pair_sync",), 4).data_ptr()
+    if PAIR_TRACE is not None:
+        args.trace = PAIR_TRACE[0].data_ptr()
     keep = [x, wt]
     outs = []
     for e, (gr, gin, prm) in enumerate(((ego, gin_ego, params[:ne]), (core, gin_core, params[ne:]))):

@@ -288,6 +288,8 @@ typedef struct {
     const float *lin_w, *lin_b;   /* Linear(64, 64) on out, or NULL */
     float *lin_out;
     void *ws;                     /* scgib_gin_pair_ws_bytes(n_cap, n_layers) bytes */
+    int32_t *chunk_rec;           /* [chunks][scgib_gin_pair_chunk_rec_ints()]: each chunk's
+                                     bounds and local CSR, written for the backward; or NULL */
     uint32_t *counters;           /* scgib_gin_pair_counters(n_cap, n_layers) ZEROED words,
                                      left zeroed */
 } scgib_pair_encoder;
@@ -334,6 +336,7 @@ typedef struct {
     int64_t slab_stride[SCGIB_PAIR_MAX_LAYERS];
     float *lin_slab;
     void *ws;                     /* scgib_gin_pair_ws_bytes(n_cap, n_layers) bytes */
+    const int32_t *chunk_rec;     /* the forward's chunk records, or NULL (derived again) */
     uint32_t *counters;           /* scgib_gin_pair_counters(...) ZEROED words, left zeroed */
 } scgib_pair_bwd_encoder;
 typedef struct {
@@ -351,6 +354,7 @@ int64_t scgib_gin_pair_chunks(int64_t n_cap);
 int64_t scgib_gin_pair_slots(void);
 int64_t scgib_gin_pair_ws_bytes(int64_t n_cap, int32_t n_layers);
 int64_t scgib_gin_pair_counters(int64_t n_cap, int32_t n_layers);
+int64_t scgib_gin_pair_chunk_rec_ints(void);
 int scgib_gin_pair_fwd(const scgib_pair_fwd_args *args, scgib_stream_t stream);
 
 /* ---- A6: per-segment readouts (dgl.sum_nodes) -------------------------------

@@ -115,6 +115,7 @@ SIGNATURES = {
     "scgib_gin_pair_bwd": (ctypes.c_int, [_P, _P]),
     "scgib_gin_pair_max_component": (_I32, []),
     "scgib_gin_pair_chunks": (_I64, [_I64]),
+    "scgib_gin_pair_chunk_rec_ints": (_I64, []),
     "scgib_gin_pair_slots": (_I64, []),
     "scgib_gin_pair_ws_bytes": (_I64, [_I64, _I32]),
     "scgib_gin_pair_counters": (_I64, [_I64, _I32]),
@@ -179,7 +180,7 @@ class PairEncoder(ctypes.Structure):
                 ("readout", ctypes.c_void_p), ("seg", ctypes.c_void_p),
                 ("lin_w", ctypes.c_void_p), ("lin_b", ctypes.c_void_p),
                 ("lin_out", ctypes.c_void_p), ("ws", ctypes.c_void_p),
-                ("counters", ctypes.c_void_p)]
+                ("chunk_rec", ctypes.c_void_p), ("counters", ctypes.c_void_p)]
 
 
 class PairFwdArgs(ctypes.Structure):
@@ -206,7 +207,7 @@ class PairBwdEncoder(ctypes.Structure):
                 ("dgamma", ctypes.c_void_p * _L), ("dbeta", ctypes.c_void_p * _L),
                 ("slab", ctypes.c_void_p * _L), ("slab_stride", ctypes.c_int64 * _L),
                 ("lin_slab", ctypes.c_void_p), ("ws", ctypes.c_void_p),
-                ("counters", ctypes.c_void_p)]
+                ("chunk_rec", ctypes.c_void_p), ("counters", ctypes.c_void_p)]
 
 
 class PairBwdArgs(ctypes.Structure):
@@ -216,7 +217,7 @@ class PairBwdArgs(ctypes.Structure):
                 ("trace", ctypes.c_void_p)]
 
 
-ABI_VERSION = 7
+ABI_VERSION = 8
 STATS_STRIDE = 260
 PGRAD_STRIDE = 324
 HIDDEN = 64

@@ -8,28 +8,32 @@
 // deferred BatchNorm partials arriving at every workgroup's start, and the
 // dependent CSR -> neighbour-row gather chain — once per layer.  Here:
 //   * chunk c of an encoder = the components (molecules / ego-nets) whose
-//     first row lies in rows [64c, 64c + 64): <= 96 rows when no component
+//     first row lies in rows [80c, 80c + 80): <= 112 rows when no component
 //     exceeds 33 rows.  Every neighbour of a chunk row is a row of the same
 //     chunk (components are closed), so ONE workgroup per chunk owns all the
-//     rows it ever gathers: the chunk's local CSR is loaded once, its rows
-//     stay in LDS from layer to layer, and no row crosses a workgroup;
+//     rows it ever gathers: the chunk's local CSR is loaded once (and handed
+//     to the backward as a chunk record), its rows stay in LDS from layer to
+//     layer, and no row crosses a workgroup;
 //   * per layer: aggregation from LDS (BN + ReLU of the previous layer applied
-//     on read), z1 = agg W1^T, r = relu(z1 + b1), z2 = r W2^T + b2 on the f32
-//     MFMA v_mfma_f32_16x16x4_f32 (16-row blocks: a chunk pays for
-//     ceil(rows / 16) blocks), the wave's 16 weight columns held in VGPRs and
-//     the next layer's fetched during the BatchNorm exchange;
-//   * BatchNorm's batch statistics: each chunk's (n, sum, centred M2) ->
-//     16-chunk groups combined by the group's last arriver (fp64, fixed
-//     order) -> the last group's arriver combines the groups, updates the
-//     running statistics and publishes (scale, shift) behind a flag; every
-//     workgroup polls that one word.  All cross-workgroup words are
-//     agent-scope atomics on both sides (MI355X_MICROARCH.md, valid forms);
-//     every spin is bounded (timeout -> sync[1], never a hang).
+//     once per row in place, then every row's neighbour reads of one degree
+//     step in flight together), z1 = agg W1^T, r = relu(z1 + b1),
+//     z2 = r W2^T + b2 on the f32 MFMA v_mfma_f32_16x16x4_f32 (16-row
+//     blocks), the wave's 16 weight columns held in VGPRs and the next
+//     layer's fetched during the BatchNorm exchange, as are the z2 row stores;
+//   * BatchNorm's batch statistics: each chunk's (n, mean, centred M2) ->
+//     32-chunk groups combined by the group's last arriver (fp64, fixed
+//     order) into tagged words ((launch epoch + 1) << 32 | float bits) ->
+//     every chunk polls the groups' words and merges them itself (fp64, fixed
+//     order, one division): no publisher, no flag, nothing to re-arm.  Chunk
+//     0 writes the stat record and the running statistics.  All
+//     cross-workgroup words are agent-scope atomics on both sides
+//     (MI355X_MICROARCH.md, valid forms); every spin is bounded (timeout ->
+//     sync[1], never a hang).
 // The whole grid (both encoders' chunks) must be co-resident: the host
-// launches it only when it fits scgib_gin_pair_slots() (3 workgroups per CU:
-// 51 KB of LDS, <= 168 VGPRs) and falls back to the per-layer kernels
+// launches it only when it fits scgib_gin_pair_slots() (2 workgroups per CU:
+// 63 KB of LDS, <= 256 VGPRs) and falls back to the per-layer kernels
 // otherwise.  Writes what the per-layer path saves for the backward (agg, r,
-// z2, stat per layer, aggx), so the backward is unchanged.
+// z2, stat per layer, aggx).
 //
 // LDS images are [row][64] floats with the float4 slots XOR-swizzled by the
 // row (slot q of row r at q ^ (r & 15)): the MFMA operand reads (16 rows x one
@@ -45,9 +49,8 @@ constexpr int kRows = 112;               // max rows per chunk
 constexpr int kMaxComp = kRows - kWin + 1;  // max component rows (33)
 constexpr int kNrb = kRows / 16;         // 16-row blocks
 constexpr int kMaxE = 512;               // chunk edges cached in LDS (else read from global)
-constexpr int kGrp = 16;                 // chunk partials per group
-constexpr int kPart = 132;               // floats per chunk partial: S[64] M2[64] n pad[3]
-constexpr int kGPart = 130;              // doubles per group partial: n S[64] M2[64] pad
+constexpr int kGrp = 32;                 // chunk partials per group
+constexpr int kPart = 132;               // floats per chunk partial: mean[64] M2[64] n pad[3]
 constexpr int kL = SCGIB_PAIR_MAX_LAYERS;
 constexpr uint64_t kTimeout = 20000000;  // 0.2 s of the 100 MHz wall clock per spin
 
@@ -60,8 +63,8 @@ __device__ __forceinline__ int sidx(int row, int col) {
 __host__ __device__ inline int64_t n_chunks(int64_t n_cap) { return (n_cap + kWin - 1) / kWin; }
 __host__ __device__ inline int64_t n_groups(int64_t n_cap) { return (n_chunks(n_cap) + kGrp - 1) / kGrp; }
 
-constexpr int kMaxGroups = 32;           // groups per encoder (512 co-resident chunks)
-constexpr int kPubB = 8;                 // group partials per load batch of the publisher
+constexpr int kMaxGroups = 16;           // groups per encoder (512 co-resident chunks)
+constexpr int kGT = 130;                 // tagged words per group partial
 
 // merge (nb rows, sum sb, centred M2 mb) into the running (n, mean, M2)
 __device__ __forceinline__ void chan_merge(double &n, double &mean, double &m2, double nb, double sb,
@@ -73,41 +76,32 @@ __device__ __forceinline__ void chan_merge(double &n, double &mean, double &m2, 
     n = nn;
 }
 
-// workspace layout (per encoder): group partials | chunk partials
-struct Ws {
-    float *part;     // [L][nch][kPart]
-    double *gpart;   // [L][ngr][kGPart]
-};
-__host__ __device__ inline int64_t ws_part_floats(int64_t n_cap) { return n_chunks(n_cap) * kPart; }
+// workspace (per encoder, any memory): the chunk partials [L][nch][kPart]
 __host__ __device__ inline int64_t ws_bytes(int64_t n_cap, int L) {
-    return L * (ws_part_floats(n_cap) * 4 + n_groups(n_cap) * kGPart * 8) + 64;
+    return static_cast<int64_t>(L) * n_chunks(n_cap) * kPart * 4 + 64;
 }
-__device__ inline Ws ws_of(void *ws, int64_t n_cap, int L) {
-    char *p = reinterpret_cast<char *>((reinterpret_cast<uintptr_t>(ws) + 15) & ~uintptr_t(15));
-    Ws w;
-    w.gpart = reinterpret_cast<double *>(p);
-    p += static_cast<int64_t>(L) * n_groups(n_cap) * kGPart * 8;
-    w.part = reinterpret_cast<float *>(p);
-    return w;
+__device__ inline float *ws_of(void *ws) {
+    return reinterpret_cast<float *>((reinterpret_cast<uintptr_t>(ws) + 15) & ~uintptr_t(15));
 }
-// counters (per encoder, zeroed once, kept across launches): group arrivals
-// [kL][ngr] | publisher arrivals [kL] | launch epoch | the published values
-// [kL][128] as tagged words (epoch + 1) << 32 | float bits, 8-byte aligned.
-// A published word carries its own launch tag, so readers poll the data
+// state (per encoder and call site, zeroed once, kept across launches; a
+// fixed layout whatever the graph size): [0] launch epoch | group arrival
+// counters [kL][kMaxGroups] | group partials [kL][kMaxGroups][kGT] as tagged
+// words (epoch + 1) << 32 | float bits, 8-byte aligned.  A group partial
+// carries its launch's tag in every word, so the chunks poll the data
 // itself: no flag, nothing to re-arm, and a stale word never matches.
 struct Cnt {
-    unsigned *grp, *pub, *epoch;
-    uint64_t *ss;
+    unsigned *epoch, *grp;
+    uint64_t *gt;
 };
-__host__ __device__ inline int64_t n_counters(int64_t n_cap, int) {
-    return kL * (n_groups(n_cap) + 1) + 1 + 1 + 2 * kL * 128;
+__host__ __device__ inline int64_t n_counters(int64_t, int) {
+    return 2 + kL * kMaxGroups + 2 + 2 * kL * kMaxGroups * kGT;
 }
-__device__ inline Cnt cnt_of(unsigned *base, int64_t ngr) {
+__device__ inline Cnt cnt_of(unsigned *base) {
     Cnt k;
-    k.grp = base;
-    k.pub = base + kL * ngr;
-    k.epoch = k.pub + kL;
-    k.ss = reinterpret_cast<uint64_t *>((reinterpret_cast<uintptr_t>(k.epoch + 1) + 7) & ~uintptr_t(7));
+    k.epoch = base;
+    k.grp = base + 2;
+    k.gt = reinterpret_cast<uint64_t *>((reinterpret_cast<uintptr_t>(k.grp + kL * kMaxGroups) + 7) &
+                                        ~uintptr_t(7));
     return k;
 }
 
@@ -120,6 +114,7 @@ struct Smem {
     float ss[128];            // (scale, shift) of the previous layer's BatchNorm
     int32_t sb[2][4];         // bound searches: lo, hi, first hit; sb[0][3]: max degree
     unsigned flag;            // block-wide broadcast of a ticket / last-arriver flag
+    int32_t hdr[16];          // backward: the chunk record's header
     alignas(16) float red[4][128];  // backward: the waves' column sums; exchange scratch
 };
 
@@ -139,26 +134,6 @@ __device__ __forceinline__ void st_tagged(uint64_t *p, unsigned tag, float v) {
                        __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// threads 0..127 wait for the 128 words of src carrying this launch's tag and
-// leave their values in dst (then a block barrier)
-__device__ void await_tagged(const uint64_t *src, unsigned tag, float *dst, uint32_t *sync, unsigned code) {
-    const int tid = threadIdx.x;
-    if (tid < 128) {
-        const uint64_t t0 = now();
-        uint64_t v;
-        while (true) {
-            v = __hip_atomic_load(src + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (__all(static_cast<unsigned>(v >> 32) == tag)) break;  // wave-uniform
-            __builtin_amdgcn_s_sleep(1);
-            if (now() - t0 > kTimeout) {
-                set_err(sync, code);
-                break;
-            }
-        }
-        dst[tid] = __uint_as_float(static_cast<unsigned>(v));
-    }
-    __syncthreads();
-}
 
 // Count this workgroup in (every wave's stores drained first) and return the
 // value the counter held before (block-uniform).
@@ -272,13 +247,61 @@ struct Layer {  // this layer's per-encoder constants
     int64_t *nbt;
 };
 
-// The BatchNorm exchange of layer l for chunk c (rows nr): chunk partial from
-// the z2 accumulators -> group -> publisher -> (scale, shift) into sm.ss.
+// wait until word w of every group partial of layer l carries this launch's
+// tag (wave 0's lanes < ngr poll one word each), then a block barrier
+__device__ void await_groups(const Cnt &cnt, int l, int64_t ngr, int w, unsigned tag, uint32_t *sync,
+                             unsigned code) {
+    const int tid = threadIdx.x;
+    if (tid < 64) {
+        const uint64_t *q = cnt.gt + (static_cast<int64_t>(l) * kMaxGroups + (tid < ngr ? tid : 0)) * kGT + w;
+        const uint64_t t0 = now();
+        while (true) {
+            const uint64_t v = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (__all(tid >= ngr || static_cast<unsigned>(v >> 32) == tag)) break;  // wave-uniform
+            __builtin_amdgcn_s_sleep(1);
+            if (now() - t0 > kTimeout) {
+                set_err(sync, code);
+                break;
+            }
+        }
+    }
+    __syncthreads();
+}
+
+// a tagged word's value once it carries tag (re-polled otherwise; bounded)
+__device__ __forceinline__ float ld_tagged(const uint64_t *q, unsigned tag, uint32_t *sync, unsigned code) {
+    uint64_t v = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (static_cast<unsigned>(v >> 32) != tag) {  // (rare: the group's marker word landed first)
+        const uint64_t t0 = now();
+        do {
+            __builtin_amdgcn_s_sleep(1);
+            v = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (now() - t0 > kTimeout) {
+                set_err(sync, code);
+                break;
+            }
+        } while (static_cast<unsigned>(v >> 32) != tag);
+    }
+    return __uint_as_float(static_cast<unsigned>(v));
+}
+
+// The BatchNorm exchange of layer l for chunk c (rows nr), two levels with no
+// publisher: chunk partial (n, column means, centred M2; fp32) -> the 32-chunk
+// group's last arriver combines them (fp64, fixed order) and stores the group
+// partial (n, mean, centred M2) as tagged words -> EVERY chunk reads all
+// group partials and merges them itself (fp64, fixed order, one division:
+// every chunk gets the same bits), so the
+// statistics cost one arrival and two tagged hand-offs.  Chunk 0 also writes
+// the stat record and the running statistics.  (scale, shift) -> sm.ss.
+template <class Mid>
 __device__ void bn_exchange(const f32x4 (&z)[kNrb], int nrb, int nr, int64_t c, int64_t nch,
-                            int64_t ngr, int l, const Ws &ws, const Cnt &cnt, unsigned tag,
-                            const Layer &Ly, uint32_t *sync, Smem &sm, uint64_t *tr) {
+                            int64_t ngr, int l, float *ws, const Cnt &cnt, unsigned tag,
+                            const Layer &Ly, uint32_t *sync, Smem &sm, uint64_t *tr, Mid mid) {
     const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4;
     const int col = acc_col16();
+    const int ch = tid & 63, p = tid >> 6;
+    // (gamma, beta) in flight during the exchange
+    const float gam = Ly.gamma[ch], bet = Ly.beta[ch];
     // ---- chunk partial: column sum and centred M2 over the valid rows (fp32)
     float s = 0.f;
 #pragma unroll
@@ -300,39 +323,37 @@ __device__ void bn_exchange(const f32x4 (&z)[kNrb], int nrb, int nr, int64_t c, 
             }
     q += __shfl_xor(q, 16, kWave);
     q += __shfl_xor(q, 32, kWave);
-    float *part = ws.part + (static_cast<int64_t>(l) * nch + c) * kPart;
+    float *part = ws + (static_cast<int64_t>(l) * nch + c) * kPart;
     if (g == 0) {
-        st_agent(part + col, s);
+        st_agent(part + col, mean);
         st_agent(part + 64 + col, q);
     }
     if (tid == 0) st_agent(part + 128, static_cast<float>(nr));
-    // ---- group combine by the group's last arriving chunk
+    // ---- group combine by the group's last arriving chunk -> tagged partial
     const int64_t grp = c / kGrp, g0 = grp * kGrp;
     const int gsize = static_cast<int>(nch - g0 < kGrp ? nch - g0 : kGrp);
-    unsigned *gcnt = cnt.grp + static_cast<int64_t>(l) * ngr + grp;
-    unsigned *pub = cnt.pub + l;                                        // publisher arrivals
-    double *dscr = reinterpret_cast<double *>(sm.buf1);                 // 4 KB of scratch
-    const int ch = tid & 63, p = tid >> 6;
-    const Ws &W = ws;
-    bool publisher = false;
+    unsigned *gcnt = cnt.grp + l * kMaxGroups + grp;
+    double *dscr = reinterpret_cast<double *>(sm.buf1);                 // 6 KB of scratch
     const bool last_in_group = arrive(gcnt, sm) == static_cast<unsigned>(gsize - 1);
     mark(tr, 4);
     if (last_in_group) {
-        // partition p takes chunks g0 + p + 4 u (fixed order), channel ch
-        float S[4], Q[4], N[4];
+        // partition p takes chunks g0 + p + 4 u (fixed order), channel ch:
+        // (rows, mean, centred M2) of each
+        constexpr int U = kGrp / 4;
+        float M[U], Q[U], N[U];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
+        for (int u = 0; u < U; ++u) {
             const int k = p + 4 * u;
-            const float *pp = W.part + (static_cast<int64_t>(l) * nch + g0 + (k < gsize ? k : 0)) * kPart;
-            S[u] = ld_agent(pp + ch);
+            const float *pp = ws + (static_cast<int64_t>(l) * nch + g0 + (k < gsize ? k : 0)) * kPart;
+            M[u] = ld_agent(pp + ch);
             Q[u] = ld_agent(pp + 64 + ch);
             N[u] = k < gsize ? ld_agent(pp + 128) : 0.f;
         }
         double ns = 0.0, ss = 0.0;
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
+        for (int u = 0; u < U; ++u) {
             ns += N[u];
-            ss += N[u] > 0.f ? static_cast<double>(S[u]) : 0.0;
+            ss += static_cast<double>(N[u]) * M[u];
         }
         dscr[p * 64 + ch] = ss;
         dscr[256 + p * 64 + ch] = ns;
@@ -342,61 +363,91 @@ __device__ void bn_exchange(const f32x4 (&z)[kNrb], int nrb, int nr, int64_t c, 
         const double mg = Ng > 0.0 ? Sg / Ng : 0.0;
         double qq = 0.0;
 #pragma unroll
-        for (int u = 0; u < 4; ++u)
-            if (N[u] > 0.f) {
-                const double d = static_cast<double>(S[u]) - static_cast<double>(N[u]) * mg;
-                qq += static_cast<double>(Q[u]) + d * d / static_cast<double>(N[u]);
-            }
+        for (int u = 0; u < U; ++u) {
+            const double d = static_cast<double>(M[u]) - mg;
+            qq += N[u] > 0.f ? static_cast<double>(Q[u]) + static_cast<double>(N[u]) * d * d : 0.0;
+        }
         __syncthreads();
         dscr[p * 64 + ch] = qq;
         __syncthreads();
-        double *gp = W.gpart + (static_cast<int64_t>(l) * ngr + grp) * kGPart;
+        uint64_t *gp = cnt.gt + (static_cast<int64_t>(l) * kMaxGroups + grp) * kGT;
         if (p == 0) {
-            st_agent(gp + 1 + ch, Sg);
-            st_agent(gp + 65 + ch, ((dscr[ch] + dscr[64 + ch]) + dscr[128 + ch]) + dscr[192 + ch]);
-            if (ch == 0) st_agent(gp, Ng);
+            st_tagged(gp + ch, tag, static_cast<float>(mg));
+            st_tagged(gp + 64 + ch, tag,
+                      static_cast<float>(((dscr[ch] + dscr[64 + ch]) + dscr[128 + ch]) + dscr[192 + ch]));
+            if (ch == 0) st_tagged(gp + 128, tag, static_cast<float>(Ng));
         }
         if (tid == 0) __hip_atomic_store(gcnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        publisher = arrive(pub, sm) == static_cast<unsigned>(ngr - 1);
         mark(tr, 5);
     }
-    if (publisher) {  // block-uniform: the last group in combines every group
-        // partition p merges groups p + 4 u in order (Chan et al.'s pairwise
-        // update, fp64), loading kPubB groups per batch
-        double an = 0.0, am = 0.0, aq = 0.0;
-        for (int u0 = 0; u0 < kMaxGroups / 4 && p + 4 * u0 < ngr; u0 += kPubB) {
-            double Nv[kPubB], Sv[kPubB], Mv[kPubB];
+    mid();  // work that needs no statistics (the z2 row stores) while the groups finish
+    // ---- every chunk: all group partials (row counts first), merged in order
+    await_groups(cnt, l, ngr, 128, tag, sync, 0x100u + l);
+    mark(tr, 6);
+    constexpr int U = kMaxGroups / 4;
+    float gN[U], gm[U], gq[U];  // this thread's groups p + 4 u: rows, mean, centred M2
+    {
+        uint64_t w[3][U];  // every load in flight at once, tags checked after
+        const uint64_t *base = cnt.gt + static_cast<int64_t>(l) * kMaxGroups * kGT;
+        auto addr = [&](int u, int k) {
+            const int64_t g1 = p + 4 * u;
+            return base + (g1 < ngr ? g1 : 0) * kGT + (k == 0 ? 128 : k == 1 ? ch : 64 + ch);
+        };
 #pragma unroll
-            for (int u = 0; u < kPubB; ++u) {
-                const int64_t g1 = p + 4 * (u0 + u);
-                const double *gp = W.gpart + (static_cast<int64_t>(l) * ngr + (g1 < ngr ? g1 : 0)) * kGPart;
-                Nv[u] = ld_agent(gp);
-                Sv[u] = ld_agent(gp + 1 + ch);
-                Mv[u] = ld_agent(gp + 65 + ch);
-            }
+        for (int u = 0; u < U; ++u)
 #pragma unroll
-            for (int u = 0; u < kPubB; ++u)
-                if (p + 4 * (u0 + u) < ngr) chan_merge(an, am, aq, Nv[u], Sv[u], Mv[u]);
+            for (int k = 0; k < 3; ++k) w[k][u] = __hip_atomic_load(addr(u, k), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        bool ok = true;
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+            for (int k = 0; k < 3; ++k) ok = ok && (p + 4 * u >= ngr || static_cast<unsigned>(w[k][u] >> 32) == tag);
+        if (!ok)  // (rare: a group's marker word landed before its other words)
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+                if (p + 4 * u < ngr)
+#pragma unroll
+                    for (int k = 0; k < 3; ++k)
+                        w[k][u] = static_cast<uint64_t>(__float_as_uint(ld_tagged(addr(u, k), tag, sync, 0x100u + l)));
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const bool in = p + 4 * u < ngr;
+            gN[u] = in ? __uint_as_float(static_cast<unsigned>(w[0][u])) : 0.f;
+            gm[u] = in ? __uint_as_float(static_cast<unsigned>(w[1][u])) : 0.f;
+            gq[u] = in ? __uint_as_float(static_cast<unsigned>(w[2][u])) : 0.f;
         }
-        __syncthreads();
-        dscr[p * 64 + ch] = an;
-        dscr[256 + p * 64 + ch] = am;
-        dscr[512 + p * 64 + ch] = aq;
-        __syncthreads();
-        double N = 0.0, m = 0.0, M2 = 0.0;
+    }
+    // N and the mean: partition sums in order, then the 4 partitions in order
+    double pn = 0.0, ps = 0.0;
 #pragma unroll
-        for (int pp = 0; pp < 4; ++pp) {
-            const double nb = dscr[pp * 64 + ch];
-            chan_merge(N, m, M2, nb, dscr[256 + pp * 64 + ch] * nb, dscr[512 + pp * 64 + ch]);
-        }
-        if (p == 0) {
-            const double var = N > 0.0 ? M2 / N : 0.0;
-            const double istd = 1.0 / sqrt(var + static_cast<double>(Ly.eps));
-            const double sc = static_cast<double>(Ly.gamma[ch]) * istd;
-            const float scale = static_cast<float>(sc);
-            const float shift = static_cast<float>(static_cast<double>(Ly.beta[ch]) - m * sc);
-            st_tagged(cnt.ss + l * 128 + ch, tag, scale);
-            st_tagged(cnt.ss + l * 128 + 64 + ch, tag, shift);
+    for (int u = 0; u < U; ++u) {
+        pn += gN[u];
+        ps += static_cast<double>(gN[u]) * gm[u];
+    }
+    dscr[p * 64 + ch] = pn;
+    dscr[256 + p * 64 + ch] = ps;
+    __syncthreads();
+    const double N = ((dscr[ch] + dscr[64 + ch]) + dscr[128 + ch]) + dscr[192 + ch];
+    const double m = N > 0.0 ? (((dscr[256 + ch] + dscr[320 + ch]) + dscr[384 + ch]) + dscr[448 + ch]) / N : 0.0;
+    // the centred M2 about the batch mean: sum of M2_g + N_g (mean_g - mean)^2
+    double pq = 0.0;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const double d = static_cast<double>(gm[u]) - m;
+        pq += static_cast<double>(gq[u]) + static_cast<double>(gN[u]) * d * d;
+    }
+    dscr[512 + p * 64 + ch] = pq;
+    __syncthreads();
+    if (p == 0) {
+        const double M2 = ((dscr[512 + ch] + dscr[576 + ch]) + dscr[640 + ch]) + dscr[704 + ch];
+        const double var = N > 0.0 ? M2 / N : 0.0;
+        const double istd = 1.0 / sqrt(var + static_cast<double>(Ly.eps));
+        const double sc = static_cast<double>(gam) * istd;
+        const float scale = static_cast<float>(sc);
+        const float shift = static_cast<float>(static_cast<double>(bet) - m * sc);
+        sm.ss[ch] = scale;
+        sm.ss[64 + ch] = shift;
+        if (c == 0) {  // one chunk per encoder: the layer's record and running statistics
             if (Ly.rmean) {
                 const double mo = static_cast<double>(Ly.mom);
                 Ly.rmean[ch] = static_cast<float>((1.0 - mo) * Ly.rmean[ch] + mo * m);
@@ -409,11 +460,8 @@ __device__ void bn_exchange(const f32x4 (&z)[kNrb], int nrb, int nr, int64_t c, 
             Ly.stat[128 + ch] = scale;
             Ly.stat[192 + ch] = shift;
         }
-        if (tid == 0) __hip_atomic_store(pub, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        mark(tr, 6);
     }
-    // ---- every chunk: the published (scale, shift)
-    await_tagged(cnt.ss + l * 128, tag, sm.ss, sync, 0x100u + l);
+    __syncthreads();
     mark(tr, 7);
 }
 
@@ -474,6 +522,60 @@ __device__ Chunk load_chunk(const int32_t *__restrict__ rowptr, const int32_t *_
     return k;
 }
 
+// The chunk's description as the forward derived it (header, local row
+// pointers, component starts, local columns), saved for the backward so that
+// it loads one record instead of repeating the searches and the CSR reads.
+constexpr int kRecHdr = 16, kRecRp = kRecHdr, kRecCs = kRecRp + kRows + 1, kRecCol = kRecCs + kRows + 2;
+constexpr int kRec = 768;  // ints per chunk record (3 x 256)
+static_assert(kRecCol + kMaxE <= kRec, "chunk record");
+
+__device__ void save_chunk(const Chunk &k, const Smem &sm, int32_t *__restrict__ rec) {
+    const int tid = threadIdx.x;
+    if (tid == 0) {
+        rec[0] = static_cast<int32_t>(k.i0);
+        rec[1] = static_cast<int32_t>(k.i1);
+        rec[2] = k.rb0;
+        rec[3] = k.rb1;
+        rec[4] = k.nr;
+        rec[5] = k.ncomp;
+        rec[6] = k.e0;
+        rec[7] = k.maxdeg;
+        rec[8] = k.lds_col ? 1 : 0;
+    }
+    if (tid <= k.nr) rec[kRecRp + tid] = sm.rp[tid];
+    if (tid <= k.ncomp) rec[kRecCs + tid] = sm.cs[tid];
+    if (k.lds_col)
+        for (int i = tid; i < sm.rp[k.nr]; i += 256) rec[kRecCol + i] = sm.colv[i];
+}
+
+__device__ Chunk load_chunk_rec(const int32_t *__restrict__ rec, Smem &sm) {
+    const int tid = threadIdx.x;
+    int32_t v[3];
+#pragma unroll
+    for (int t = 0; t < 3; ++t) v[t] = rec[tid + 256 * t];
+#pragma unroll
+    for (int t = 0; t < 3; ++t) {
+        const int i = tid + 256 * t;
+        if (i < kRecHdr) sm.hdr[i] = v[t];
+        else if (i < kRecCs) sm.rp[i - kRecRp] = v[t];
+        else if (i < kRecCol) sm.cs[i - kRecCs] = v[t];
+        else if (i - kRecCol < kMaxE) sm.colv[i - kRecCol] = v[t];
+    }
+    __syncthreads();
+    Chunk k;
+    k.i0 = sm.hdr[0];
+    k.i1 = sm.hdr[1];
+    k.rb0 = sm.hdr[2];
+    k.rb1 = sm.hdr[3];
+    k.nr = sm.hdr[4];
+    k.nrb = (k.nr + 15) / 16;
+    k.ncomp = sm.hdr[5];
+    k.e0 = sm.hdr[6];
+    k.maxdeg = sm.hdr[7];
+    k.lds_col = sm.hdr[8] != 0;
+    return k;
+}
+
 // chunk-local neighbour row of chunk edge ei (clamped into the chunk: a graph
 // whose edges left their component would read wrong rows, never outside the
 // images)
@@ -504,7 +606,10 @@ __device__ __forceinline__ void aggregate_rows(const Chunk &ck, const int32_t *_
         acc[k] = make_float4(ope * x.x, ope * x.y, ope * x.z, ope * x.w);
     }
     const int elast = sm.rp[ck.nr] - 1;  // (>= 0 whenever maxdeg > 0)
-    for (int j = 0; j < ck.maxdeg; ++j) {
+    int md = 0;  // this lane's steps: the largest degree of its rows
+#pragma unroll
+    for (int k = 0; k < kNrb; ++k) md = dg[k] > md ? dg[k] : md;
+    for (int j = 0; j < md; ++j) {
         int u[kNrb];
 #pragma unroll
         for (int k = 0; k < kNrb; ++k) u[k] = nbr_of(ck, col, sm, j < dg[k] ? e0[k] + j : elast);
@@ -532,8 +637,8 @@ __global__ __launch_bounds__(256, 2) void gin_pair_fwd_k(const scgib_pair_fwd_ar
     const int64_t c = blockIdx.x - (e ? nch0 : 0);
     const int64_t nch = n_chunks(E.n_cap), ngr = n_groups(E.n_cap);
     const int L = A.n_layers;
-    const Ws ws = ws_of(E.ws, E.n_cap, L);
-    const Cnt cnt = cnt_of(E.counters, ngr);
+    float *ws = ws_of(E.ws);
+    const Cnt cnt = cnt_of(E.counters);
     const unsigned tag = __hip_atomic_load(cnt.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
     const int64_t n = E.dims ? static_cast<int64_t>(E.dims[0]) : E.n_cap;
     const int F = A.n_feat;
@@ -564,6 +669,7 @@ __global__ __launch_bounds__(256, 2) void gin_pair_fwd_k(const scgib_pair_fwd_ar
     const int rb0 = ck.rb0, nr = ck.nr, nrb = ck.nrb, ncomp = ck.ncomp;
     const int win0 = static_cast<int>(c * kWin), win1 = static_cast<int>(c * kWin + kWin);
     auto nbr = [&](int ei) -> int { return nbr_of(ck, E.col, sm, ei); };
+    if (E.chunk_rec) save_chunk(ck, sm, E.chunk_rec + c * kRec);
     mark(tr, 57);
     if (tr && tid == 0)
         tr[61] = static_cast<uint64_t>(nr) | (static_cast<uint64_t>(sm.rp[nr]) << 8) |
@@ -575,26 +681,48 @@ __global__ __launch_bounds__(256, 2) void gin_pair_fwd_k(const scgib_pair_fwd_ar
     // ---- layer 0: gather the raw features (ope x_v + sum of neighbours)
     const float ope0 = E.one_plus_eps[0];
     {
+        // the chunk rows' raw features -> X [kRows][16] in LDS (one round of
+        // loads), then the aggregation from LDS as in the later layers
         const int f = tid & 15, rs = tid >> 4;
-        const bool fok = f < F;
-        for (int v = rs; v < 16 * nrb; v += 16) {
-            float a = 0.f;
-            if (v < nr) {
-                a = ope0 * (fok ? A.x[static_cast<int64_t>(par[v]) * F + f] : 0.f);
-                const int b = sm.rp[v], d = sm.rp[v + 1] - b;
-                for (int j0 = 0; j0 < d; j0 += 4) {
-                    float xs[4];
+        float *X = sm.buf1 + 128;  // (after par)
+        if (nr > 0) {  // block-uniform
+            float xv[kNrb];
 #pragma unroll
-                    for (int t = 0; t < 4; ++t) {
-                        const int j = j0 + t < d ? j0 + t : d - 1;
-                        xs[t] = A.x[static_cast<int64_t>(par[nbr(b + j)]) * F + (fok ? f : 0)];
-                    }
-#pragma unroll
-                    for (int t = 0; t < 4; ++t) a = fmaf(xs[t], (j0 + t < d && fok) ? 1.f : 0.f, a);
-                }
-                E.aggx[static_cast<int64_t>(rb0 + v) * 16 + f] = a;
+            for (int k = 0; k < kNrb; ++k) {
+                const int v = rs + 16 * k;
+                xv[k] = A.x[static_cast<int64_t>(par[v < nr ? v : 0]) * F + (f < F ? f : 0)];
             }
-            sm.buf0[sidx(v, f)] = a;
+#pragma unroll
+            for (int k = 0; k < kNrb; ++k) {
+                const int v = rs + 16 * k;
+                if (v < nr) X[v * 16 + f] = f < F ? xv[k] : 0.f;
+            }
+        }
+        __syncthreads();
+        float acc[kNrb];
+        int e0[kNrb], dg[kNrb], md = 0;
+#pragma unroll
+        for (int k = 0; k < kNrb; ++k) {
+            const int v = rs + 16 * k, vv = v < nr ? v : 0;
+            e0[k] = sm.rp[vv];
+            dg[k] = v < nr ? sm.rp[vv + 1] - e0[k] : 0;
+            md = dg[k] > md ? dg[k] : md;
+            acc[k] = ope0 * X[vv * 16 + f];
+        }
+        const int elast = sm.rp[nr] - 1;
+        for (int j = 0; j < md; ++j) {
+            int u[kNrb];
+#pragma unroll
+            for (int k = 0; k < kNrb; ++k) u[k] = nbr(j < dg[k] ? e0[k] + j : elast);
+#pragma unroll
+            for (int k = 0; k < kNrb; ++k) acc[k] = fmaf(X[u[k] * 16 + f], j < dg[k] ? 1.f : 0.f, acc[k]);
+        }
+#pragma unroll
+        for (int k = 0; k < kNrb; ++k) {
+            const int v = rs + 16 * k;
+            const float a = v < nr ? acc[k] : 0.f;
+            if (v < nr) E.aggx[static_cast<int64_t>(rb0 + v) * 16 + f] = a;
+            if (v < 16 * nrb) sm.buf0[sidx(v, f)] = a;
         }
         for (int64_t idx = tid; idx < (z1 - z0) * 16; idx += 256) E.aggx[z0 * 16 + idx] = 0.f;
     }
@@ -633,8 +761,13 @@ __global__ __launch_bounds__(256, 2) void gin_pair_fwd_k(const scgib_pair_fwd_ar
             const float4 sc = make_float4(sm.ss[4 * q], sm.ss[4 * q + 1], sm.ss[4 * q + 2], sm.ss[4 * q + 3]);
             const float4 sh = make_float4(sm.ss[64 + 4 * q], sm.ss[65 + 4 * q], sm.ss[66 + 4 * q],
                                           sm.ss[67 + 4 * q]);
-            aggregate_rows(ck, E.col, sm, sm.buf0, ope, q, rs,
-                           [&](float4 x) { return xform4(x, sc, sh); },
+            // x = relu(scale z2 + shift) in place, once per row
+            for (int v = rs; v < nr; v += 16) {
+                float4 *px = reinterpret_cast<float4 *>(sm.buf0 + sidx(v, 4 * q));
+                *px = xform4(*px, sc, sh);
+            }
+            __syncthreads();
+            aggregate_rows(ck, E.col, sm, sm.buf0, ope, q, rs, [](float4 x) { return x; },
                            [&](int, int v, float4 a) {
                                if (v < nr) st4(E.agg[l] + static_cast<int64_t>(rb0 + v) * 64 + 4 * q, a);
                                if (v < 16 * nrb) *reinterpret_cast<float4 *>(sm.buf1 + sidx(v, 4 * q)) = a;
@@ -669,19 +802,21 @@ __global__ __launch_bounds__(256, 2) void gin_pair_fwd_k(const scgib_pair_fwd_ar
 #pragma unroll
                 for (int i = 0; i < 4; ++i) sm.buf0[sidx(acc_row16(rb, i), acc_col16())] = z[rb][i];
         __syncthreads();
-        lds_to_global<64>(sm.buf0, E.z2[l], rb0, nr);
-        zero_rows<64>(E.z2[l], z0, z1);
-        // ---- the next layer's weights, in flight during the exchange
-        if (l + 1 < L) {
-            load_frag<64>(E.w1[l + 1], fw1);
-            load_frag<64>(E.w2[l + 1], fw2);
-            bias1 = E.b1[l + 1][acc_col16()];
-            bias2 = E.b2[l + 1][acc_col16()];
-        }
         const Layer Ly{0.f, E.bn_eps[l], E.momentum[l], E.gamma[l], E.beta[l], E.running_mean[l],
                        E.running_var[l], E.stat[l], E.num_batches_tracked[l]};
         mark(tl, 3);
-        bn_exchange(z, nrb, nr, c, nch, ngr, l, ws, cnt, tag, Ly, A.sync, sm, tl);
+        // the chunk's statistics go out first; the z2 rows and the next
+        // layer's weights during the exchange
+        bn_exchange(z, nrb, nr, c, nch, ngr, l, ws, cnt, tag, Ly, A.sync, sm, tl, [&]() {
+            lds_to_global<64>(sm.buf0, E.z2[l], rb0, nr);
+            zero_rows<64>(E.z2[l], z0, z1);
+            if (l + 1 < L) {
+                load_frag<64>(E.w1[l + 1], fw1);
+                load_frag<64>(E.w2[l + 1], fw2);
+                bias1 = E.b1[l + 1][acc_col16()];
+                bias2 = E.b2[l + 1][acc_col16()];
+            }
+        });
     }
 
     // ---- encoder output: out = relu(BN(z2)) -> global and buf1
@@ -738,13 +873,11 @@ __global__ __launch_bounds__(256, 2) void gin_pair_fwd_k(const scgib_pair_fwd_ar
     }
 
     // ---- exit: the last workgroup advances both encoders' epochs (the next
-    // launch's tag) and re-arms the publisher counters (already zero unless a
-    // spin timed out)
+    // launch's tag)
     mark(tr, 60);
     if (arrive(A.sync, sm) == gridDim.x - 1) {
         for (int ee = 0; ee < 2; ++ee) {
-            const Cnt k = cnt_of(A.enc[ee].counters, n_groups(A.enc[ee].n_cap));
-            if (tid < kL) __hip_atomic_store(k.pub + tid, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const Cnt k = cnt_of(A.enc[ee].counters);
             if (tid == 64) {
                 const unsigned ep = __hip_atomic_load(k.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 __hip_atomic_store(k.epoch, ep + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -837,18 +970,18 @@ __device__ __forceinline__ void gemm_each(const float *A, const float (&f)[16], 
     }
 }
 
-// the BatchNorm-backward exchange of layer l: the chunk's 128 sums (sum dy,
-// sum dy xhat, already stored at its partial) -> groups -> publisher, which
-// writes dbeta / dgamma and publishes the dz2 coefficients tot / N into sm.ss
-__device__ void bwd_exchange(int l, int64_t c, int64_t nch, int64_t ngr, int64_t n, const Ws &W,
+// the BatchNorm-backward exchange of layer l, as the forward's: the chunk's
+// 128 sums (sum dy, sum dy xhat, already stored at its partial) -> the
+// group's last arriver (fp64, fixed order) -> tagged group sums -> every
+// chunk adds all groups in order (fp64) and keeps the dz2 coefficients
+// tot / N in sm.ss; chunk 0 writes dbeta / dgamma.
+__device__ void bwd_exchange(int l, int64_t c, int64_t nch, int64_t ngr, int64_t n, float *ws,
                              const Cnt &cnt, unsigned tag, float *dgamma, float *dbeta, uint32_t *sync, Smem &sm,
                              double *dscr, uint64_t *tr) {
     const int tid = threadIdx.x, ch = tid & 127, p = tid >> 7;  // 128 sums x 2 partitions
     const int64_t grp = c / kGrp, g0 = grp * kGrp;
     const int gsize = static_cast<int>(nch - g0 < kGrp ? nch - g0 : kGrp);
-    unsigned *gcnt = cnt.grp + static_cast<int64_t>(l) * ngr + grp;
-    unsigned *pub = cnt.pub + l;
-    bool publisher = false;
+    unsigned *gcnt = cnt.grp + l * kMaxGroups + grp;
     const bool last_in_group = arrive(gcnt, sm) == static_cast<unsigned>(gsize - 1);
     mark(tr, 2);
     if (last_in_group) {
@@ -856,44 +989,56 @@ __device__ void bwd_exchange(int l, int64_t c, int64_t nch, int64_t ngr, int64_t
 #pragma unroll
         for (int u = 0; u < kGrp / 2; ++u) {
             const int k = p + 2 * u;
-            v[u] = ld_agent(W.part + (static_cast<int64_t>(l) * nch + g0 + (k < gsize ? k : 0)) * kPart + ch);
+            v[u] = ld_agent(ws + (static_cast<int64_t>(l) * nch + g0 + (k < gsize ? k : 0)) * kPart + ch);
         }
         double a = 0.0;
 #pragma unroll
         for (int u = 0; u < kGrp / 2; ++u) a += p + 2 * u < gsize ? static_cast<double>(v[u]) : 0.0;
         dscr[p * 128 + ch] = a;
         __syncthreads();
-        if (p == 0) st_agent(W.gpart + (static_cast<int64_t>(l) * ngr + grp) * kGPart + ch, dscr[ch] + dscr[128 + ch]);
-        if (tid == 0) __hip_atomic_store(gcnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        publisher = arrive(pub, sm) == static_cast<unsigned>(ngr - 1);
+        uint64_t *gp = cnt.gt + (static_cast<int64_t>(l) * kMaxGroups + grp) * kGT;
+        if (p == 0) st_tagged(gp + ch, tag, static_cast<float>(dscr[ch] + dscr[128 + ch]));
+        if (tid == 0) {
+            st_tagged(gp + 128, tag, 1.f);  // the group's marker word
+            __hip_atomic_store(gcnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
         mark(tr, 3);
     }
-    if (publisher) {  // partition p: groups p + 2 u in order, 16 loads per batch
-        double a = 0.0;
-        for (int u0 = 0; u0 < kMaxGroups / 2 && p + 2 * u0 < ngr; u0 += 16) {
-            double v[16];
+    await_groups(cnt, l, ngr, 128, tag, sync, 0x200u + l);
+    mark(tr, 4);
+    double a = 0.0;
+    const uint64_t *base = cnt.gt + static_cast<int64_t>(l) * kMaxGroups * kGT + ch;
+    for (int u0 = 0; p + 2 * u0 < ngr; u0 += 8) {  // groups p + 2 u, 8 per batch
+        uint64_t w[8];
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const int64_t g1 = p + 2 * (u0 + u);
-                v[u] = ld_agent(W.gpart + (static_cast<int64_t>(l) * ngr + (g1 < ngr ? g1 : 0)) * kGPart + ch);
-            }
-#pragma unroll
-            for (int u = 0; u < 16; ++u)
-                if (p + 2 * (u0 + u) < ngr) a += v[u];
+        for (int u = 0; u < 8; ++u) {
+            const int64_t g1 = p + 2 * (u0 + u);
+            w[u] = __hip_atomic_load(base + (g1 < ngr ? g1 : 0) * kGT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
-        __syncthreads();
-        dscr[p * 128 + ch] = a;
-        __syncthreads();
-        if (p == 0) {
-            const double tot = dscr[ch] + dscr[128 + ch];
-            st_tagged(cnt.ss + l * 128 + ch, tag, static_cast<float>(tot / static_cast<double>(n)));
+        bool ok = true;
+#pragma unroll
+        for (int u = 0; u < 8; ++u) ok = ok && (p + 2 * (u0 + u) >= ngr || static_cast<unsigned>(w[u] >> 32) == tag);
+        if (!ok)
+#pragma unroll
+            for (int u = 0; u < 8; ++u)
+                if (p + 2 * (u0 + u) < ngr)
+                    w[u] = __float_as_uint(ld_tagged(base + (p + 2 * (u0 + u)) * kGT, tag, sync, 0x200u + l));
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+            if (p + 2 * (u0 + u) < ngr) a += static_cast<double>(__uint_as_float(static_cast<unsigned>(w[u])));
+    }
+    __syncthreads();  // (dscr: the group combine above may still read it)
+    dscr[p * 128 + ch] = a;
+    __syncthreads();
+    if (p == 0) {
+        const double tot = dscr[ch] + dscr[128 + ch];
+        sm.ss[ch] = static_cast<float>(tot / static_cast<double>(n));
+        if (c == 0) {
             if (ch < 64) dbeta[ch] = static_cast<float>(tot);
             else dgamma[ch - 64] = static_cast<float>(tot);
         }
-        if (tid == 0) __hip_atomic_store(pub, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        mark(tr, 4);
     }
-    await_tagged(cnt.ss + l * 128, tag, sm.ss, sync, 0x200u + l);
+    __syncthreads();
     mark(tr, 5);
 }
 
@@ -906,15 +1051,16 @@ __global__ __launch_bounds__(256, 2) void gin_pair_bwd_k(const scgib_pair_bwd_ar
     const int64_t c = blockIdx.x - (e ? nch0 : 0);
     const int64_t nch = n_chunks(E.n_cap), ngr = n_groups(E.n_cap);
     const int L = A.n_layers, F = A.n_feat;
-    const Ws ws = ws_of(E.ws, E.n_cap, L);
-    const Cnt cnt = cnt_of(E.counters, ngr);
+    float *ws = ws_of(E.ws);
+    const Cnt cnt = cnt_of(E.counters);
     const unsigned tag = __hip_atomic_load(cnt.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
     const int64_t n = E.dims ? static_cast<int64_t>(E.dims[0]) : E.n_cap;
     uint64_t *tr = A.trace ? A.trace + static_cast<int64_t>(blockIdx.x) * 64 : nullptr;
     mark(tr, 56);
 
-    const Chunk ck = load_chunk(E.rowptr, E.col, E.comp_ptr, comp_count(E.comp_dims, E.n_comp),
-                                nch, c, A.sync, sm);
+    const Chunk ck = E.chunk_rec ? load_chunk_rec(E.chunk_rec + c * kRec, sm)
+                                 : load_chunk(E.rowptr, E.col, E.comp_ptr, comp_count(E.comp_dims, E.n_comp),
+                                              nch, c, A.sync, sm);
     const int rb0 = ck.rb0, nr = ck.nr, nrb = ck.nrb, ns = (ck.nr + 3) / 4;
     const int q4 = tid & 15, rs = tid >> 4;  // thread-row-wise roles: float4 slot, rows rs + 16 k
     float *P = sm.buf0, *Q = sm.buf1;
@@ -930,6 +1076,13 @@ __global__ __launch_bounds__(256, 2) void gin_pair_bwd_k(const scgib_pair_bwd_ar
             *reinterpret_cast<float4 *>(P + sidx(v, 4 * q4)) = keep4(ok, fi);
         }
         load_frag_col<64, 64>(E.lin_w, 16 * wv, fw);
+        // g_out rows in flight during the dW0 product
+        float4 go[kNrb];
+        {
+            const Rsrc rg = rows_rsrc(E.g_out, E.g_out ? E.n_cap : 0, 64);
+#pragma unroll
+            for (int k = 0; k < kNrb; ++k) go[k] = ld_row(rg, rb0 + rs + 16 * k, 64, 4 * q4);
+        }
         __syncthreads();
         f32x4 aw[4] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f},
                        f32x4{0.f, 0.f, 0.f, 0.f}};
@@ -943,13 +1096,19 @@ __global__ __launch_bounds__(256, 2) void gin_pair_bwd_k(const scgib_pair_bwd_ar
         cs += __shfl_xor(cs, 16, kWave);
         cs += __shfl_xor(cs, 32, kWave);
         if (g == 0) sl[64 * 64 + 16 * wv + r16] = cs;
-        __syncthreads();  // every read of P (f) done: d out = g_out + g_t W0 -> P
+        __syncthreads();  // every read of P (f) done: g_out -> P, then P += g_t W0
+#pragma unroll
+        for (int k = 0; k < kNrb; ++k) {
+            const int v = rs + 16 * k;
+            if (v < 16 * nrb) *reinterpret_cast<float4 *>(P + sidx(v, 4 * q4)) = keep4(v < nr, go[k]);
+        }
+        __syncthreads();
         gemm_each(Q, fw, nrb, 0, 1, [&](int rb, const f32x4 &d) {
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
                 const int row = acc_row16(rb, i), col = acc_col16();
-                const float go = E.g_out && row < nr ? E.g_out[static_cast<int64_t>(rb0 + row) * 64 + col] : 0.f;
-                P[sidx(row, col)] = row < nr ? d[i] + go : 0.f;
+                float *pp = P + sidx(row, col);
+                *pp = row < nr ? d[i] + *pp : 0.f;
             }
         });
     } else {
@@ -1024,7 +1183,7 @@ __global__ __launch_bounds__(256, 2) void gin_pair_bwd_k(const scgib_pair_bwd_ar
             }
             __syncthreads();
             if (tid < 128)
-                st_agent(ws.part + (static_cast<int64_t>(l) * nch + c) * kPart + tid,
+                st_agent(ws + (static_cast<int64_t>(l) * nch + c) * kPart + tid,
                          ((sm.red[0][tid] + sm.red[1][tid]) + sm.red[2][tid]) + sm.red[3][tid]);
         }
         // r rows in flight during the exchange
@@ -1158,13 +1317,11 @@ __global__ __launch_bounds__(256, 2) void gin_pair_bwd_k(const scgib_pair_bwd_ar
     }
 
     // ---- exit: the last workgroup advances both encoders' epochs (the next
-    // launch's tag) and re-arms the publisher counters (already zero unless a
-    // spin timed out)
+    // launch's tag)
     mark(tr, 60);
     if (arrive(A.sync, sm) == gridDim.x - 1) {
         for (int ee = 0; ee < 2; ++ee) {
-            const Cnt k = cnt_of(A.enc[ee].counters, n_groups(A.enc[ee].n_cap));
-            if (tid < kL) __hip_atomic_store(k.pub + tid, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const Cnt k = cnt_of(A.enc[ee].counters);
             if (tid == 64) {
                 const unsigned ep = __hip_atomic_load(k.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 __hip_atomic_store(k.epoch, ep + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1182,6 +1339,7 @@ using namespace scgib;
 extern "C" int64_t scgib_gin_pair_args_bytes(void) { return sizeof(scgib_pair_fwd_args); }
 extern "C" int32_t scgib_gin_pair_max_component(void) { return pair::kMaxComp; }
 extern "C" int64_t scgib_gin_pair_chunks(int64_t n_cap) { return n_cap > 0 ? pair::n_chunks(n_cap) : 0; }
+extern "C" int64_t scgib_gin_pair_chunk_rec_ints(void) { return pair::kRec; }
 extern "C" int64_t scgib_gin_pair_ws_bytes(int64_t n_cap, int32_t n_layers) {
     return pair::ws_bytes(n_cap, n_layers);
 }

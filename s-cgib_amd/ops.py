@@ -897,7 +897,8 @@ def _pair_backward_persistent(ctx, g_s, g_ro, g_f, g_t):
                          device=dev)
         keep.append(ws)
         E.ws = ws.data_ptr()
-        E.counters = counters(dev, ("gin_pair_bwd", e), int(_lib.query("scgib_gin_pair_counters", n, L))).data_ptr()
+        E.chunk_rec = sub.chunk_rec.data_ptr()
+        E.counters = scan_state(dev, ("gin_pair_bwd", e), int(_lib.query("scgib_gin_pair_counters", n, L))).data_ptr()
         if e == 1 and ctx.lin and g_t is not None:
             f, w0 = ctx.lin_saved
             g_t = _f32(g_t, "compressor.0 grad")
@@ -991,9 +992,13 @@ def _pair_forward_persistent(ctx, x, wt, w0, b0, nmap, ego, core, gin_ego, gin_c
                          device=dev)
         keep.append(ws)
         E.ws = ws.data_ptr()
-        E.counters = counters(dev, ("gin_pair", id(gin)),
-                              int(_lib.query("scgib_gin_pair_counters", n, L))).data_ptr()
+        E.counters = scan_state(dev, ("gin_pair", id(gin)),
+                                int(_lib.query("scgib_gin_pair_counters", n, L))).data_ptr()
+        rec = torch.empty(int(_lib.query("scgib_gin_pair_chunks", n)) *
+                          int(_lib.query("scgib_gin_pair_chunk_rec_ints")), dtype=torch.int32, device=dev)
+        E.chunk_rec = rec.data_ptr()
         sub = ctx.sub[e]
+        sub.chunk_rec = rec
         sub.save_for_backward(*saved, *prm, aggx)
         sub.graph, sub.L, sub.training, sub.pre = gr, L, True, True
         sub.n_feat = x.shape[1]

@@ -4,10 +4,9 @@ ops.PAIR_TRACE, summarised per layer.  python tools/pair_trace.py [workload batc
 
 forward stamps per layer l (slot 8 l + i): 0 start, 1 aggregation done,
 2 GEMM1 + r stored, 3 z2 stored (exchange entered), 4 group arrival counted,
-5 group partial published (group's last chunk), 6 (scale, shift) published
-(publisher), 7 (scale, shift) in LDS.  backward: 0 start, 1 sums stored,
-2 group arrival, 3 group partial, 4 published, 5 coefficients in LDS,
-6 dW2 / dz1 done.  56 start, 57 chunk loaded, 58 layer-0 gather, 60 exit."""
+5 group partial stored (group's last chunk), 6 every group partial seen,
+7 (scale, shift) in LDS.  backward: 0 start, 1 sums stored, 2 group arrival,
+3 group partial, 4 every group seen, 5 coefficients in LDS, 6 dW2 / dz1 done.  56 start, 57 chunk loaded, 58 layer-0 gather, 60 exit."""
 import importlib
 import os
 import statistics
@@ -81,8 +80,20 @@ def slowest(t, l, i0, i1, k=8):
     print(f"  phase {i0}->{i1} median {float(d.median()):.2f} p90 {float(d.quantile(0.9)):.2f} us")
 
 
-summary("forward", tr[0], ["start", "agg", "gemm1", "ready", "arrive", "group", "publish", "go"], range(5))
-summary("backward", tr[1], ["start", "sums", "arrive", "group", "publish", "go", "dz1"], range(4, -1, -1))
+summary("forward", tr[0], ["start", "agg", "gemm1", "ready", "arrive", "group", "seen", "go"], range(5))
+summary("backward", tr[1], ["start", "sums", "arrive", "group", "seen", "go", "dz1"], range(4, -1, -1))
+def prologue(name, t, stamps):
+    t = t.view(1024, 64).cpu()
+    t = t[t[:, 56] > 0].double()
+    parts = []
+    for a, b in zip(stamps[:-1], stamps[1:]):
+        d = (t[:, b] - t[:, a]) / 100.0
+        parts.append(f"{a}->{b} {float(d.median()):.2f}/{float(d.max()):.2f}")
+    print(f"  {name} prologue: " + " | ".join(parts))
+
+
+prologue("forward", tr[0], [56, 57, 58, 0])
+prologue("backward", tr[1], [56, 57, 8 * 4])
 slowest(tr[0], 1, 0, 1)
 slowest(tr[0], 1, 1, 2)
 slowest(tr[0], 1, 2, 3)

@@ -16,7 +16,7 @@ files = glob.glob(os.path.join(path, "**", "*kernel_trace.csv"), recursive=True)
 per = collections.defaultdict(list)
 for fn in files:
     for r in csv.DictReader(open(fn)):
-        name = r["Kernel_Name"].split("(")[0].replace("void ", "").replace("scgib::", "").strip()
+        name = r["Kernel_Name"].split("(")[0].replace("void ", "").replace("scgib::", "").replace("pair::", "").strip()
         per[(name, int(r["Grid_Size_X"]))].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
 print(f"{'kernel':60s} {'grid':>9s} {'calls':>6s} {'avg_us':>9s} {'min_us':>8s}")
 for (name, grid), ds in sorted(per.items(), key=lambda kv: -sum(kv[1])):

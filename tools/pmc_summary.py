@@ -22,7 +22,7 @@ def load(path, counter):
                 continue
             # keep template arguments: gin_bwd_k<64, true> (GIN) vs <128, false> (MLP)
             name = row["Kernel_Name"].split("(")[0]
-            name = name.replace("void ", "").replace("scgib::", "").strip()
+            name = name.replace("void ", "").replace("scgib::", "").replace("pair::", "").strip()
             per[name].append(float(row["Counter_Value"]) * 1024.0)  # KB -> bytes
     return per
 

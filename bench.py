@@ -385,6 +385,12 @@ def cpu_model():
     return "unknown"
 
 
+def progress(msg):
+    """A progress line on stderr (long phases: the driver and gpurun treat a
+    silent process as hung)."""
+    print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
 def cpu_baselines(pool_host, k, gin_layers, F_in, workload, seconds=20.0):
     """the CPU path at all the CPUs this process may run on
     (len(os.sched_getaffinity(0)) torch threads: `value`), at the box's CPU
@@ -402,6 +408,7 @@ def cpu_baselines(pool_host, k, gin_layers, F_in, workload, seconds=20.0):
         for name, nt, warm, mins in (("all_affinity", affinity, 2, 5), ("share", threads, 2, 5),
                                      ("one_core", 1, 1, 3)):
             torch.set_num_threads(nt)
+            progress(f"cpu baseline leg {name}: {nt} threads")
             legs[name] = cpu_baseline(pool_host, k, gin_layers, F_in, workload, leg, warmup=warm,
                                       min_steps=mins)
     finally:
@@ -465,6 +472,8 @@ def cpu_baseline(pool_host, k, gin_layers, F_in, workload, seconds=20.0, warmup=
             times.append(t3 - t2)
             ego_times.append(t1 - t0)
         i += 1
+        if t3 - t0 > 5.0:
+            progress(f"  cpu step {i}: {t3 - t2:.1f} s")
     B = gh.batch_size
     step = statistics.median(times)
     return {"value": round(B / step, 2), "unit": "graphs/s", "cores": torch.get_num_threads(),
@@ -598,10 +607,12 @@ def main():
             if SUM_LOSS:
                 loss = kl + rec + con
                 loss.backward()
-                out = loss
+                out = loss.detach()
             else:
                 torch.autograd.backward((kl, rec, con), (one, one, one))
-                out = (kl, rec, con)
+                out = (kl.detach(), rec.detach(), con.detach())
+            # detached aliases (the replays refresh their storage): the step's
+            # autograd graph is not kept alive past the capture
             return out
 
         side = torch.cuda.Stream()
@@ -668,6 +679,7 @@ def main():
 
     for i in range(a.warmup):
         step(i)
+    progress(f"warm-up done ({a.warmup} steps); timing {a.steps} steps")
 
     def barrier():
         if world > 1:
@@ -711,10 +723,13 @@ def main():
             r = timer.kernel_summary(spec, timed_steps)
             if r is not None:
                 kernels[name] = roofline_entry(name, spec["desc"], r, spec["pmc"])
+    progress("timed steps and kernel timer done")
     # the dominant kernel = the largest summed time per step (kernel-timer pass)
     dominant = max(kernels, key=lambda k: kernels[k]["per_step_us"]) if kernels else None
 
     sb = None if a.no_superbatch or rank != 0 else superbatch_roofline(dev)
+    if sb is not None:
+        progress("superbatch roofline done")
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         cpu = cpu_baselines(pool_host[:2], a.k, a.gin_layers, F_in, a.workload, a.cpu_seconds)

@@ -683,7 +683,10 @@ class _GinEncoderPair(torch.autograd.Function):
             t = torch.empty_like(f)
             _lib.call("scgib_linear_fwd", _p(f), f.shape[0], _p(w0), _p(b0), _p(t),
                       _p(core.dims), _stream())
-            ctx.lin_saved = (f, w0)
+            # (an alias, not the output object itself: ctx -> output -> its
+            # grad_fn -> ctx would be a reference cycle that keeps this step's
+            # graph, AccumulateGrad nodes included, alive until a gc pass)
+            ctx.lin_saved = (f.detach(), w0)
             ctx.core_dims = core.dims
             outs = (s, ro, f, t)
         main.wait_stream(side)
@@ -986,7 +989,7 @@ def _pair_forward_persistent(ctx, x, wt, w0, b0, nmap, ego, core, gin_ego, gin_c
             keep += [w0c, b0c]
             t = torch.empty(n, HIDDEN, dtype=torch.float32, device=dev)
             E.lin_w, E.lin_b, E.lin_out = w0c.data_ptr(), b0c.data_ptr(), t.data_ptr()
-            ctx.lin_saved = (out, w0c)
+            ctx.lin_saved = (out.detach(), w0c)  # (an alias: no ctx -> output cycle)
             ctx.core_dims = gr.dims
         ws = torch.empty(int(_lib.query("scgib_gin_pair_ws_bytes", n, L)), dtype=torch.uint8,
                          device=dev)

@@ -391,12 +391,43 @@ def progress(msg):
     print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
 
 
-def cpu_baselines(pool_host, k, gin_layers, F_in, workload, seconds=20.0):
+# CPU legs run in child processes (a fresh OpenMP pool per thread count, and
+# a leg that cannot finish — e.g. hundreds of threads on a small CPU share —
+# is stopped at its time limit and reported as such)
+LEG_TIMEOUT = {"all_affinity": 120.0, "share": 120.0, "one_core": 150.0}
+
+
+def _run_leg(name, spec):
+    import subprocess
+    progress(f"cpu baseline leg {name}: {spec['threads']} threads")
+    env = dict(os.environ, HIP_VISIBLE_DEVICES="", CUDA_VISIBLE_DEVICES="",
+               OMP_NUM_THREADS=str(spec["threads"]))
+    p = subprocess.Popen([sys.executable, os.path.abspath(__file__), "--cpu-leg", json.dumps(spec)],
+                         stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, env=env)
+    t0 = time.perf_counter()
+    while True:
+        try:
+            out, err = p.communicate(timeout=20)
+            break
+        except subprocess.TimeoutExpired:
+            if time.perf_counter() - t0 > LEG_TIMEOUT[name]:
+                p.kill()
+                p.communicate()
+                progress(f"cpu baseline leg {name}: stopped at {LEG_TIMEOUT[name]:.0f} s")
+                return None
+            progress(f"cpu baseline leg {name}: running ({time.perf_counter() - t0:.0f} s)")
+    if p.returncode != 0:
+        progress(f"cpu baseline leg {name} failed: {err.strip()[-300:]}")
+        return None
+    return json.loads(out.strip().splitlines()[-1])
+
+
+def cpu_baselines(k, gin_layers, workload, batch, seconds=20.0):
     """the CPU path at all the CPUs this process may run on
     (len(os.sched_getaffinity(0)) torch threads: `value`), at the box's CPU
     share (torch's default thread count, OMP_NUM_THREADS) and at 1 core, with
     the CPU model, nproc and the thread counts.  Each leg is a bounded sample
-    of ~seconds/2 of CPU work."""
+    of ~seconds/2 of CPU work in its own process."""
     threads = torch.get_num_threads()
     try:
         affinity = len(os.sched_getaffinity(0))
@@ -404,27 +435,43 @@ def cpu_baselines(pool_host, k, gin_layers, F_in, workload, seconds=20.0):
         affinity = os.cpu_count() or threads
     leg = max(seconds / 2, 5.0)
     legs = {}
-    try:
-        for name, nt, warm, mins in (("all_affinity", affinity, 2, 5), ("share", threads, 2, 5),
-                                     ("one_core", 1, 1, 3)):
-            torch.set_num_threads(nt)
-            progress(f"cpu baseline leg {name}: {nt} threads")
-            legs[name] = cpu_baseline(pool_host, k, gin_layers, F_in, workload, leg, warmup=warm,
-                                      min_steps=mins)
-    finally:
-        torch.set_num_threads(threads)
-    allc = legs["all_affinity"]
-    out = dict(allc)
-    out.update({"cores": allc["cores"], "cpu_model": cpu_model(), "nproc": os.cpu_count(),
-                "sched_affinity_cpus": affinity, "torch_default_threads": threads,
-                "value_share_threads": legs["share"]["value"],
-                "ms_per_step_share_threads": legs["share"]["ms_per_step"],
-                "value_1core": legs["one_core"]["value"],
-                "ms_per_step_1core": legs["one_core"]["ms_per_step"],
-                "sample": allc["sample"] + f"; legs: {affinity} threads (value), {threads} "
-                                           f"threads ({legs['share']['steps']} steps), 1 thread "
-                                           f"({legs['one_core']['steps']} steps)"})
+    for name, nt, warm, mins in (("all_affinity", affinity, 2, 5), ("share", threads, 2, 5),
+                                 ("one_core", 1, 1, 3)):
+        legs[name] = _run_leg(name, {"threads": nt, "k": k, "gin_layers": gin_layers,
+                                     "workload": workload, "batch": batch, "seconds": leg,
+                                     "warmup": warm, "min_steps": mins})
+    base = legs["all_affinity"] or legs["share"] or legs["one_core"]
+    if base is None:
+        return None
+    out = dict(base)
+    out.update({"cores": affinity if legs["all_affinity"] else base["cores"],
+                "cpu_model": cpu_model(), "nproc": os.cpu_count(),
+                "sched_affinity_cpus": affinity, "torch_default_threads": threads})
+    for name, tag in (("all_affinity", "all_affinity"), ("share", "share_threads"),
+                      ("one_core", "1core")):
+        r = legs[name]
+        out[f"value_{tag}"] = r["value"] if r else None
+        out[f"ms_per_step_{tag}"] = r["ms_per_step"] if r else None
+        out[f"steps_{tag}"] = r["steps"] if r else None
+    if legs["all_affinity"] is None:
+        out["note"] = (f"the {affinity}-thread leg did not finish within "
+                       f"{LEG_TIMEOUT['all_affinity']:.0f} s (threads far above this process's CPU "
+                       "share); value is the best finished leg")
+    out["sample"] = base["sample"] + (f"; legs in child processes: {affinity} threads (value), "
+                                      f"{threads} threads, 1 thread")
     return out
+
+
+def _cpu_leg_main(spec_json):
+    """Child of _run_leg: one CPU leg, its result as a JSON line."""
+    spec = json.loads(spec_json)
+    torch.set_num_threads(spec["threads"])
+    pool = [pkg.graph.collate_pyg(pkg.synth.molecules(spec["batch"], spec["workload"], seed=i))[0]
+            for i in range(2)]
+    F_in = pkg.synth.WORKLOADS[spec["workload"]][2]
+    r = cpu_baseline(pool, spec["k"], spec["gin_layers"], F_in, spec["workload"], spec["seconds"],
+                     warmup=spec["warmup"], min_steps=spec["min_steps"])
+    print(json.dumps(r), flush=True)
 
 
 def cpu_baseline(pool_host, k, gin_layers, F_in, workload, seconds=20.0, warmup=1,
@@ -732,7 +779,7 @@ def main():
         progress("superbatch roofline done")
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
-        cpu = cpu_baselines(pool_host[:2], a.k, a.gin_layers, F_in, a.workload, a.cpu_seconds)
+        cpu = cpu_baselines(a.k, a.gin_layers, a.workload, a.batch, a.cpu_seconds)
 
     if rank == 0:
         total_graphs = world * a.batch * a.steps
@@ -788,4 +835,7 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    if len(sys.argv) == 3 and sys.argv[1] == "--cpu-leg":
+        _cpu_leg_main(sys.argv[2])
+    else:
+        main()

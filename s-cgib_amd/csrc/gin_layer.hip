@@ -1584,8 +1584,11 @@ extern "C" int scgib_trace_set(void *buf) {
 // largest per-workgroup count at one workgroup per CU: the same finish time
 // as the full two-per-CU grid (measured), half the slabs.
 static int64_t bwd5_subtiles(int64_t n_nodes) { return (n_nodes + SM - 1) / SM; }
+#ifndef SCGIB_BWD5_SLOTS  // (build-time A/B hook: tools/build_ab_lib.sh EXTRA=-DSCGIB_BWD5_SLOTS=n)
+#define SCGIB_BWD5_SLOTS kCUs
+#endif
 static int bwd5_grid(int64_t nsub) {
-    constexpr int64_t slots = kCUs;
+    constexpr int64_t slots = SCGIB_BWD5_SLOTS;
     const int64_t per = (nsub + slots - 1) / slots;
     return static_cast<int>((nsub + per - 1) / per);
 }

@@ -54,13 +54,18 @@ def _traffic():
 
 
 TRAFFIC = _traffic()
+RUN_CONFIG = None  # {"workload", "batch", "k"} of this run (main)
 
 
 def traffic_of(variants):
     """Dispatch-weighted mean HBM bytes per launch over the template
     instantiations whose names start with one of ``variants`` (e.g. the GIN
     variants of gin_bwd_k, not the MLP one); None when none is in the file."""
-    got = [t for k, t in TRAFFIC.items() if any(k.startswith(v) for v in variants)]
+    cfg = TRAFFIC.get("_config")
+    if cfg is not None and cfg != RUN_CONFIG:
+        return None  # measured on another configuration
+    got = [t for k, t in TRAFFIC.items()
+           if not k.startswith("_") and any(k.startswith(v) for v in variants)]
     n = sum(g["dispatches"] for g in got)
     if not n:
         return None
@@ -278,8 +283,12 @@ def roofline_entry(kernel, desc, r, variants):
            "avg_bytes_per_launch": int(r["avg_bytes"]),
            "avg_flops_per_launch": int(r["avg_flops"]), "launches_timed": r["launches"]}
     if traffic is None:
-        out["traffic_note"] = (f"no PMC entry for {variants} in {out['traffic_file']}: "
-                               "run tools/gpu_round.sh on this code")
+        cfg = TRAFFIC.get("_config")
+        out["traffic_note"] = (
+            f"{out['traffic_file']} holds PMC passes of {cfg}, not of this configuration "
+            f"{RUN_CONFIG}" if cfg is not None and cfg != RUN_CONFIG else
+            f"no PMC entry for {variants} in {out['traffic_file']}: run tools/gpu_round.sh on "
+            "this code")
     else:
         out["traffic_over_algorithmic"] = round(traffic / r["avg_bytes"], 3)
     return out
@@ -589,6 +598,8 @@ def main():
     dev = torch.device("cuda", local % max(torch.cuda.device_count(), 1))
     torch.cuda.set_device(dev)
     torch.manual_seed(1234 + rank)
+    global RUN_CONFIG
+    RUN_CONFIG = {"workload": a.workload, "batch": a.batch, "k": a.k}
     F_in = pkg.synth.WORKLOADS[a.workload][2]
 
     # per-rank pool of distinct batches, resident in HBM

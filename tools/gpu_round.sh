@@ -17,7 +17,7 @@ for C in FETCH_SIZE WRITE_SIZE; do
   timeout -s KILL 300 rocprofv3 --pmc $C --output-format csv -d "$O/pmc/$C" -o pmc \
     -- python bench.py $ARGS > "$O/pmc_$C.log" 2>&1 || { echo "pmc $C failed"; exit 1; }
 done
-python tools/pmc_summary.py "$O/pmc" > "$O/traffic.json" && echo traffic ok
+python tools/pmc_summary.py "$O/pmc" qm9,512,1 > "$O/traffic.json" && echo traffic ok
 SCGIB_TRAFFIC_FILE=$O/traffic.json timeout -k 10 600 python bench.py --steps 300 --warmup 20 --cpu-seconds 20 > $O/bench.log 2>&1 || { echo bench failed; tail -5 $O/bench.log; exit 1; }
 tail -1 $O/bench.log | cut -c1-400
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -T --output-format csv -d $O/prof_kt -o kt \

@@ -27,7 +27,7 @@ def load(path, counter):
     return per
 
 
-def main(out):
+def main(out, config=None):
     fetch, write = load(out, "FETCH_SIZE"), load(out, "WRITE_SIZE")
     res = {}
     for k in sorted(set(fetch) | set(write)):
@@ -36,8 +36,11 @@ def main(out):
         res[k] = {"dispatches": max(len(fetch.get(k, [])), len(write.get(k, []))),
                   "fetch_bytes": round(2 * f), "write_bytes": round(w),
                   "traffic_bytes": round(2 * f + w)}
+    if config:  # the bench configuration the passes ran ("qm9,512,1")
+        wl, b, k = config.split(",")
+        res["_config"] = {"workload": wl, "batch": int(b), "k": int(k)}
     print(json.dumps(res, indent=1))
 
 
 if __name__ == "__main__":
-    main(sys.argv[1])
+    main(sys.argv[1], sys.argv[2] if len(sys.argv) > 2 else None)

@@ -543,12 +543,6 @@ def cpu_baseline(pool_host, k, gin_layers, F_in, workload, seconds=20.0, warmup=
             "ms_per_step": round(step * 1e3, 2), "steps": len(times)}
 
 
-SUM_LOSS = os.environ.get("SCGIB_BENCH_SUM_LOSS", "0") != "0"
-# N > 1: capture the RCCL all-reduce inside the replayed step graph (falls back
-# to all-reduce between two replays if the capture raises)
-GRAPH_ALLREDUCE = os.environ.get("SCGIB_GRAPH_ALLREDUCE", "1") != "0"
-
-
 WORKLOAD_DESC = {"qm9": "QM9-like", "molpcba": "ogbg-molpcba-like", "pcqm4mv2": "PCQM4Mv2-like",
                  "zinc": "ZINC-like", "mutagenicity": "Mutagenicity-like",
                  "molhiv": "ogbg-molhiv-like"}
@@ -662,13 +656,8 @@ def main():
             # loss = KL + contrastive + recon (exp_pretraining.py:321): d loss / d part = 1,
             # so the parts are backpropagated directly with a resident ones scalar (no sum
             # kernels, no ones fill in the replayed step); the total is formed after timing
-            if SUM_LOSS:
-                loss = kl + rec + con
-                loss.backward()
-                out = loss.detach()
-            else:
-                torch.autograd.backward((kl, rec, con), (one, one, one))
-                out = (kl.detach(), rec.detach(), con.detach())
+            torch.autograd.backward((kl, rec, con), (one, one, one))
+            out = (kl.detach(), rec.detach(), con.detach())
             # detached aliases (the replays refresh their storage): the step's
             # autograd graph is not kept alive past the capture
             return out
@@ -690,7 +679,9 @@ def main():
         graph2 = None
         graph = torch.cuda.CUDAGraph()
         opt.zero_grad(set_to_none=True)
-        capture_ok = GRAPH_ALLREDUCE and dist.is_initialized() and dist.get_backend() == "nccl"
+        # N > 1: the RCCL all-reduce captured inside the replayed step graph
+        # (falls back to the all-reduce between two replays if the capture raises)
+        capture_ok = dist.is_initialized() and dist.get_backend() == "nccl"
         if collective and capture_ok:  # (gloo's all-reduce is a host round trip: not capturable)
             # the whole step incl. the RCCL all-reduce of the bucket in ONE graph:
             # no host enqueue between the backward and the optimizer step

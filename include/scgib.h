@@ -482,6 +482,16 @@ int scgib_noise_uniform(float *u_gate, float *u_feat, int64_t n_rows, uint64_t *
 int scgib_bn_running_update(const float *stats, const int32_t *graph_ptr, int64_t n_graphs,
                             float momentum, float *running_mean, float *running_var,
                             int64_t *num_batches_tracked, scgib_stream_t stream);
+/* The same update as an argument block, for launches that run it in an
+ * extra workgroup beside their own work (scgib_mlp2_recon_contrastive_fwd). */
+typedef struct {
+    const float *stats;           /* scgib_interaction_fwd's per-graph statistics */
+    const int32_t *graph_ptr;
+    int64_t n_graphs;
+    float momentum;
+    float *running_mean, *running_var;
+    int64_t *num_batches_tracked;
+} scgib_running_update;
 /* Backward of scgib_interaction_fwd.  The KL gradient is g_kl [2 n_last, 64],
  * or g_klmean (device scalar, gradient of kl_mean), or neither (both NULL).
  * pad_rows: zero rows [graph_ptr[B], n_nodes) of df, dt, ds.
@@ -600,7 +610,10 @@ int scgib_mlp2_recon_bwd(const float *x, const float *r, const float *out, const
  * workgroups of the MLP launches — one launch on the step's critical chain
  * instead of two each way.  d_in must be 128 (the pretraining head).
  * Forward also writes *closs; backward takes d loss / d contrastive =
- * *g_con and writes dz1, dz2. */
+ * *g_con and writes dz1, dz2.  ru (forward, or NULL): the compressor
+ * BatchNorm's running-stat update (scgib_bn_running_update) in one more
+ * workgroup of the loss-finishing launch, off the critical path without a
+ * second stream. */
 int scgib_mlp2_recon_contrastive_fwd(const float *x, int32_t d_in, int64_t n_nodes,
                                      const float *w1, const float *b1, const float *w2,
                                      const float *b2, float *r, float *out,
@@ -608,7 +621,8 @@ int scgib_mlp2_recon_contrastive_fwd(const float *x, int32_t d_in, int64_t n_nod
                                      float *ws, uint32_t *counter, float *loss,
                                      const int32_t *dims, const float *z1, const float *z2,
                                      int64_t n_graphs, float *cws, float *closs,
-                                     uint32_t *ccounters, scgib_stream_t stream);
+                                     uint32_t *ccounters, const scgib_running_update *ru,
+                                     scgib_stream_t stream);
 int scgib_mlp2_recon_contrastive_bwd(const float *x, const float *r, const float *out,
                                      const float *ws, int32_t d_in, const float *w1,
                                      const float *w2, int64_t n_nodes, const int32_t *rowptr,

@@ -60,7 +60,7 @@ SIGNATURES = {
                                             _P, _P, _P, _P, _P, _P]),
     "scgib_mlp2_recon_contrastive_fwd": (ctypes.c_int, [_P, _I32, _I64, _P, _P, _P, _P, _P, _P,
                                                         _P, _P, _I64, _P, _P, _P, _P, _P, _P,
-                                                        _I64, _P, _P, _P, _P]),
+                                                        _I64, _P, _P, _P, _P, _P]),
     "scgib_mlp2_recon_contrastive_bwd": (ctypes.c_int, [_P, _P, _P, _P, _I32, _P, _P, _I64, _P,
                                                         _P, _P, _P, _P, _P, _P, _P, _P, _P, _P,
                                                         _I64, _P, _P, _P, _P, _P, _P]),
@@ -156,6 +156,14 @@ class GradSlice(ctypes.Structure):
     _fields_ = [("data", ctypes.c_void_p), ("numel", ctypes.c_int64), ("offset", ctypes.c_int64)]
 
 
+class RunningUpdate(ctypes.Structure):
+    """scgib_running_update (include/scgib.h)."""
+    _fields_ = [("stats", ctypes.c_void_p), ("graph_ptr", ctypes.c_void_p),
+                ("n_graphs", ctypes.c_int64), ("momentum", ctypes.c_float),
+                ("running_mean", ctypes.c_void_p), ("running_var", ctypes.c_void_p),
+                ("num_batches_tracked", ctypes.c_void_p)]
+
+
 PAIR_MAX_LAYERS = 6  # SCGIB_PAIR_MAX_LAYERS
 
 
@@ -217,7 +225,7 @@ class PairBwdArgs(ctypes.Structure):
                 ("trace", ctypes.c_void_p)]
 
 
-ABI_VERSION = 8
+ABI_VERSION = 9
 STATS_STRIDE = 260
 PGRAD_STRIDE = 324
 HIDDEN = 64

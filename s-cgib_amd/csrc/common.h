@@ -115,9 +115,12 @@ int launch_slab_reduce(const float *slab, int nslab, int64_t width, float *out, 
 
 // Fused recon loss, forward finish (recon.hip): Gram reduce over the head
 // MLP's tile partials + edge term + last-arriver loss.  wsd: 512 doubles.
+// ru (or NULL): the compressor BatchNorm's running update in one more
+// workgroup of the same launch.
 int launch_recon_fin(const float *gslab, const float *im, const int32_t *rowptr,
                      const int32_t *col, int64_t n_nodes, int64_t n_edges, float *gram,
-                     double *wsd, unsigned *cnt, float *loss, const int32_t *dims, hipStream_t st);
+                     double *wsd, unsigned *cnt, float *loss, const int32_t *dims,
+                     const scgib_running_update *ru, hipStream_t st);
 
 // Phase tracing (debug build only, `make trace` -> libscgib_trace.so):
 // thread 0 of each workgroup stamps the 100 MHz wall clock at phase marks

@@ -1972,7 +1972,8 @@ static int mlp2_recon_fwd(const float *x, int32_t d_in, int64_t n_nodes, const f
                           const float *b1, const float *w2, const float *b2, float *r,
                           float *out, const int32_t *rowptr, const int32_t *col, int64_t n_edges,
                           float *ws, uint32_t *counter, float *loss, const int32_t *dims,
-                          const ContrastArgs &con, scgib_stream_t stream) {
+                          const ContrastArgs &con, const scgib_running_update *ru,
+                          scgib_stream_t stream) {
     if (n_nodes <= 0 || n_edges < 0 || (d_in != 64 && d_in != 128)) return SCGIB_EINVAL;
     if (!x || !w1 || !b1 || !w2 || !b2 || !r || !out || !rowptr || (n_edges > 0 && !col) || !ws ||
         !counter || !loss)
@@ -1993,7 +1994,7 @@ static int mlp2_recon_fwd(const float *x, int32_t d_in, int64_t n_nodes, const f
     const int rc = launch_status();
     if (rc != SCGIB_OK) return rc;
     return launch_recon_fin(ws, out, rowptr, col, n_nodes, n_edges, gram, wsd, counter, loss, dims,
-                            st);
+                            ru, st);
 }
 
 extern "C" int scgib_mlp2_recon_fwd(const float *x, int32_t d_in, int64_t n_nodes,
@@ -2003,7 +2004,7 @@ extern "C" int scgib_mlp2_recon_fwd(const float *x, int32_t d_in, int64_t n_node
                                     float *ws, uint32_t *counter, float *loss,
                                     const int32_t *dims, scgib_stream_t stream) {
     return mlp2_recon_fwd(x, d_in, n_nodes, w1, b1, w2, b2, r, out, rowptr, col, n_edges, ws,
-                          counter, loss, dims, ContrastArgs{}, stream);
+                          counter, loss, dims, ContrastArgs{}, nullptr, stream);
 }
 
 static bool contrast_ok(const float *z1, const float *z2, int64_t n_graphs, const float *cws,
@@ -2017,8 +2018,10 @@ extern "C" int scgib_mlp2_recon_contrastive_fwd(
     const float *w2, const float *b2, float *r, float *out, const int32_t *rowptr,
     const int32_t *col, int64_t n_edges, float *ws, uint32_t *counter, float *loss,
     const int32_t *dims, const float *z1, const float *z2, int64_t n_graphs, float *cws,
-    float *closs, uint32_t *ccounters, scgib_stream_t stream) {
+    float *closs, uint32_t *ccounters, const scgib_running_update *ru, scgib_stream_t stream) {
     if (!contrast_ok(z1, z2, n_graphs, cws, ccounters, d_in) || !closs) return SCGIB_EINVAL;
+    if (ru && ru->n_graphs > 0 && (!ru->stats || !ru->graph_ptr || !ru->running_mean || !ru->running_var))
+        return SCGIB_EINVAL;
     ContrastArgs con{z1, z2, n_graphs, cws, closs, nullptr, nullptr, nullptr,
                      reinterpret_cast<unsigned *>(ccounters), contrast_splits(n_graphs), 0};
     // the head tiles hold one CU each (101 KB LDS): the contrastive
@@ -2035,7 +2038,7 @@ extern "C" int scgib_mlp2_recon_contrastive_fwd(
         con.nsplit = static_cast<int>(fit);
     }
     return mlp2_recon_fwd(x, d_in, n_nodes, w1, b1, w2, b2, r, out, rowptr, col, n_edges, ws,
-                          counter, loss, dims, con, stream);
+                          counter, loss, dims, con, ru, stream);
 }
 
 static int mlp2_recon_bwd(const float *x, const float *r, const float *out, const float *ws,

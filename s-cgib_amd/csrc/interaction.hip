@@ -25,6 +25,7 @@
 //
 // Latency-bound VALU/shuffle work (a few hundred FLOP per row): no MFMA.
 #include "common.h"
+#include "running_update.h"
 
 namespace scgib {
 
@@ -382,90 +383,11 @@ __global__ __launch_bounds__(64) void interaction_fwd_k(
     }
 }
 
-// Closed form of the B sequential momentum updates of the per-graph
-// compressor BatchNorm (one nn.BatchNorm1d call per graph, models.py:642):
-//   r_B = (1-m)^B r_0 + sum_i m (1-m)^(B-1-i) x_i
-// in fp64.  1024 threads = 64 contiguous graph partitions x 16 lanes (float4
-// channel quads): partition p runs the recurrence S = (1-m) S + m x_i over its
-// graphs (Horner form, all of a round's loads in flight: one load round for
-// B <= 512), then 64 threads (one per channel) chain the partitions in order,
-// T = (1-m)^len_p T + S_p, and apply the decay of r_0.  Deterministic; closer
-// to the exact recurrence than an fp32 sequential loop.
-constexpr int kRuParts = 64, kRuRound = 8;
+// the compressor BatchNorm's running-stat update (running_update.h)
+static_assert(kStMeanT == kRuMeanOff && kStSsqT == kRuSsqOff, "stats slab layout");
 
-struct D4 {
-    double x, y, z, w;
-};
-
-__device__ __forceinline__ void horner4(D4 &a, double keep, double m, float4 v, float scale) {
-    a.x = keep * a.x + m * (static_cast<double>(v.x) * scale);
-    a.y = keep * a.y + m * (static_cast<double>(v.y) * scale);
-    a.z = keep * a.z + m * (static_cast<double>(v.z) * scale);
-    a.w = keep * a.w + m * (static_cast<double>(v.w) * scale);
-}
-
-
-__global__ __launch_bounds__(1024) void bn_running_update_k(const float *__restrict__ stats,
-                                                            const int32_t *__restrict__ gptr,
-                                                            int64_t B, float momentum,
-                                                            float *__restrict__ rm,
-                                                            float *__restrict__ rv,
-                                                            int64_t *__restrict__ nbt) {
-    const int c4 = threadIdx.x & 15, part = threadIdx.x >> 4;
-    const double m = momentum, keep = 1.0 - static_cast<double>(momentum);
-    const int64_t chunk = (B + kRuParts - 1) / kRuParts;
-    const int64_t i0 = part * chunk, i1 = i0 + chunk < B ? i0 + chunk : B;
-    __shared__ double sPow[3];  // keep^chunk, keep^(last partial length), keep^B
-    if (threadIdx.x == 1023) {
-        const int64_t last = B - (B - 1) / chunk * chunk;
-        sPow[0] = pow(keep, static_cast<double>(chunk));
-        sPow[1] = pow(keep, static_cast<double>(last));
-        sPow[2] = pow(keep, static_cast<double>(B));
-    }
-    D4 am{0.0, 0.0, 0.0, 0.0}, av{0.0, 0.0, 0.0, 0.0};
-    for (int64_t ib = i0; ib < i1; ib += kRuRound) {
-        float4 xm[kRuRound], xs[kRuRound];
-        int32_t g0[kRuRound], g1[kRuRound];
-#pragma unroll
-        for (int u = 0; u < kRuRound; ++u) {
-            const int64_t i = ib + u < i1 ? ib + u : i1 - 1;  // clamped: loads stay unconditional
-            const float *sl = stats + i * SCGIB_STATS_STRIDE;
-            xm[u] = ld4(sl + kStMeanT + 4 * c4);
-            xs[u] = ld4(sl + kStSsqT + 4 * c4);
-            g0[u] = gptr[i];
-            g1[u] = gptr[i + 1];
-        }
-#pragma unroll
-        for (int u = 0; u < kRuRound; ++u) {
-            if (ib + u < i1) {
-                horner4(am, keep, m, xm[u], 1.f);
-                // unbiased variance = centred sum of squares / (n - 1)
-                const double inv = 1.0 / static_cast<double>(g1[u] - g0[u] - 1);
-                av.x = keep * av.x + m * (static_cast<double>(xs[u].x) * inv);
-                av.y = keep * av.y + m * (static_cast<double>(xs[u].y) * inv);
-                av.z = keep * av.z + m * (static_cast<double>(xs[u].z) * inv);
-                av.w = keep * av.w + m * (static_cast<double>(xs[u].w) * inv);
-            }
-        }
-    }
-    __shared__ double pm[kRuParts][65], pv[kRuParts][65];
-    pm[part][4 * c4] = am.x; pm[part][4 * c4 + 1] = am.y; pm[part][4 * c4 + 2] = am.z; pm[part][4 * c4 + 3] = am.w;
-    pv[part][4 * c4] = av.x; pv[part][4 * c4 + 1] = av.y; pv[part][4 * c4 + 2] = av.z; pv[part][4 * c4 + 3] = av.w;
-    __syncthreads();
-    if (threadIdx.x < 64) {
-        const int c = threadIdx.x;
-        double sm = 0.0, sv = 0.0;
-        for (int p = 0; p < kRuParts; ++p) {
-            const int64_t b0 = p * chunk, b1 = b0 + chunk < B ? b0 + chunk : B;
-            if (b1 <= b0) break;  // partitions past B are empty (and so are all later ones)
-            const double d = b1 - b0 == chunk ? sPow[0] : sPow[1];
-            sm = d * sm + pm[p][c];
-            sv = d * sv + pv[p][c];
-        }
-        rm[c] = static_cast<float>(sPow[2] * rm[c] + sm);
-        rv[c] = static_cast<float>(sPow[2] * rv[c] + sv);
-        if (c == 0 && nbt) *nbt += B;
-    }
+__global__ __launch_bounds__(1024) void bn_running_update_k(const scgib_running_update a) {
+    running_update_body<1024>(a);
 }
 
 __global__ __launch_bounds__(64) void interaction_bwd_k(
@@ -734,9 +656,8 @@ extern "C" int scgib_bn_running_update(const float *stats, const int32_t *graph_
     if (n_graphs < 0) return SCGIB_EINVAL;
     if (n_graphs == 0) return SCGIB_OK;
     if (!stats || !graph_ptr || !running_mean || !running_var) return SCGIB_EINVAL;
-    bn_running_update_k<<<1, 1024, 0, as_stream(stream)>>>(stats, graph_ptr, n_graphs, momentum,
-                                                           running_mean, running_var,
-                                                           num_batches_tracked);
+    bn_running_update_k<<<1, 1024, 0, as_stream(stream)>>>(scgib_running_update{
+        stats, graph_ptr, n_graphs, momentum, running_mean, running_var, num_batches_tracked});
     return launch_status();
 }
 

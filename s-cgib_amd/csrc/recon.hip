@@ -20,6 +20,7 @@
 // recon_bwd_k: grad_v = (g/N) (4 (IM G)_v - 2 ((A + A^T) IM)_v), G staged in
 //   LDS, the row of IM broadcast from LDS.
 #include "mfma_tile.h"
+#include "running_update.h"
 
 namespace scgib {
 
@@ -218,7 +219,12 @@ __global__ __launch_bounds__(256) void recon_fin_k(const float *__restrict__ gsl
                                                    double *__restrict__ wsd,
                                                    unsigned *__restrict__ cnt,
                                                    float *__restrict__ loss,
-                                                   const int32_t *__restrict__ dims) {
+                                                   const int32_t *__restrict__ dims,
+                                                   const scgib_running_update ru) {
+    if (blockIdx.x == kFinBlocks) {  // (block-uniform) the extra workgroup: the running update
+        running_update_body<256>(ru);
+        return;
+    }
     const int64_t n = eff_count(dims, 0, ncap), n_edges = eff_count(dims, 1, ecap);
     const int64_t ntiles = (n + TM - 1) / TM;
     const int tid = threadIdx.x;
@@ -302,9 +308,12 @@ __global__ __launch_bounds__(256) void recon_fin_k(const float *__restrict__ gsl
 
 int launch_recon_fin(const float *gslab, const float *im, const int32_t *rowptr,
                      const int32_t *col, int64_t n_nodes, int64_t n_edges, float *gram,
-                     double *wsd, unsigned *cnt, float *loss, const int32_t *dims, hipStream_t st) {
-    recon_fin_k<<<kFinBlocks, 256, 0, st>>>(gslab, im, rowptr, col, n_nodes, n_edges, gram, wsd,
-                                            cnt, loss, dims);
+                     double *wsd, unsigned *cnt, float *loss, const int32_t *dims,
+                     const scgib_running_update *ru, hipStream_t st) {
+    const bool with_ru = ru && ru->n_graphs > 0;
+    recon_fin_k<<<kFinBlocks + (with_ru ? 1 : 0), 256, 0, st>>>(
+        gslab, im, rowptr, col, n_nodes, n_edges, gram, wsd, cnt, loss, dims,
+        with_ru ? *ru : scgib_running_update{});
     return launch_status();
 }
 

@@ -61,6 +61,9 @@ FOLD_SLABS = True
 # join_aside()); elsewhere aside work is enqueued at once.
 _AUX_DEFERRED = []
 _DEFER_DEPTH = [0]
+# the interaction forward's running-stat update, waiting for the loss head's
+# launch (take_running_update) or for join_aside
+_PENDING_RU = [None]
 
 
 # Loss-section weight-gradient reduces deferred into the encoder pair's
@@ -216,6 +219,7 @@ def discard_aside():
     never enqueued (replaying it with the next batch would apply that batch's
     running-stat update twice) and join what already ran on the aux stream."""
     _SLAB_SCOPE[0] = None
+    _PENDING_RU[0] = None
     _AUX_DEFERRED.clear()
     if _AUX_PENDING:
         main = torch.cuda.current_stream()
@@ -240,8 +244,18 @@ def aside_guard(fn):
     return wrapper
 
 
+def take_running_update():
+    """The compressor BatchNorm running update left by the interaction forward
+    (a scgib_running_update for the loss head's launch), or None."""
+    pend, _PENDING_RU[0] = _PENDING_RU[0], None
+    return pend
+
+
 def join_aside():
     _SLAB_SCOPE[0] = None  # end of a model forward: later standalone ops never defer
+    pend = take_running_update()
+    if pend is not None:  # no loss-head launch took it: the aux stream
+        launch_aside(pend[1], *pend[2])
     if not _AUX_PENDING:
         return
     main = torch.cuda.current_stream()
@@ -1123,10 +1137,18 @@ def _interaction_forward(ctx, f, t, s, u_gate, u_feat, gamma, beta, w2, b2, w_at
         def upd():  # B sequential momentum updates in closed form
             _lib.call("scgib_bn_running_update", _p(stats), _p(graph.graph_ptr), B,
                       float(bn.momentum), _p(rm), _p(rv), _p(nbt), _stream())
-        # nothing in the step reads them: beside the critical path (the
-        # 16-workgroup form inline measured 10 us slower than the aside
-        # launch's fork / join edges, round 2)
-        launch_aside(upd, stats, graph.graph_ptr)
+        # nothing in the step reads them.  Inside a model forward the loss
+        # head's launch runs it in one extra workgroup of its finishing kernel
+        # (scgib_mlp2_recon_contrastive_fwd: no second stream, no fork / join
+        # edges); if no such launch follows, join_aside puts it on the aux
+        # stream.  A standalone op call updates inline.
+        if _DEFER_DEPTH[0] > 0:
+            ru = _lib.RunningUpdate(stats.data_ptr(), graph.graph_ptr.data_ptr(), B,
+                                    float(bn.momentum), rm.data_ptr(), rv.data_ptr(),
+                                    nbt.data_ptr())
+            _PENDING_RU[0] = (ru, upd, (stats, graph.graph_ptr))
+        else:
+            upd()
     ctx.graph, ctx.training, ctx.pad, ctx.n_last = graph, training, pad, n_last
     ctx.bn_eps = float(bn.eps)
     ctx.rm, ctx.rv = (None, None) if training else (rm.clone(), rv.clone())
@@ -1553,11 +1575,13 @@ class _Mlp2ReconContrastive(torch.autograd.Function):
         closs = torch.empty((), dtype=torch.float32, device=dev)
         cnt = counters(dev, "mlp2_recon", 1)
         ccnt = counters(dev, "contrastive", int(_lib.query("scgib_contrastive_counters", B)))
+        ru = take_running_update()
         _launch("scgib_mlp2_recon_contrastive_fwd", {"n": n, "d_in": d_in, "B": B}, _p(x), d_in, n,
                 _p(w1), _p(b1), _p(w2),
                   _p(b2), _p(r), _p(out), _p(graph.rowptr), _p(graph.col),
                   graph.edge_capacity(), _p(ws), _p(cnt), _p(loss), _p(graph.dims), _p(z1),
-                  _p(z2), B, _p(cws), _p(closs), _p(ccnt), _stream())
+                  _p(z2), B, _p(cws), _p(closs), _p(ccnt), _byref(ru[0] if ru else None),
+                  _stream())
         ctx.save_for_backward(x, r, out, ws, w1, w2, z1, z2, cws)
         ctx.graph = graph
         return loss, closs

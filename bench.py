@@ -409,8 +409,10 @@ LEG_TIMEOUT = {"all_affinity": 120.0, "share": 120.0, "one_core": 150.0}
 def _run_leg(name, spec):
     import subprocess
     progress(f"cpu baseline leg {name}: {spec['threads']} threads")
+    # (passive OpenMP waits: a thread count far above the CPU share must not
+    # spin the share away)
     env = dict(os.environ, HIP_VISIBLE_DEVICES="", CUDA_VISIBLE_DEVICES="",
-               OMP_NUM_THREADS=str(spec["threads"]))
+               OMP_NUM_THREADS=str(spec["threads"]), OMP_WAIT_POLICY="PASSIVE")
     p = subprocess.Popen([sys.executable, os.path.abspath(__file__), "--cpu-leg", json.dumps(spec)],
                          stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, env=env)
     t0 = time.perf_counter()

@@ -451,11 +451,15 @@ def cpu_baselines(k, gin_layers, workload, batch, seconds=20.0):
         legs[name] = _run_leg(name, {"threads": nt, "k": k, "gin_layers": gin_layers,
                                      "workload": workload, "batch": batch, "seconds": leg,
                                      "warmup": warm, "min_steps": mins})
-    base = legs["all_affinity"] or legs["share"] or legs["one_core"]
-    if base is None:
+    done = {k: v for k, v in legs.items() if v is not None}
+    if not done:
         return None
+    # value: the fastest leg (the CPU path at its best thread count on this
+    # host's CPU share); every leg is reported beside it
+    best = max(done, key=lambda k: done[k]["value"])
+    base = done[best]
     out = dict(base)
-    out.update({"cores": affinity if legs["all_affinity"] else base["cores"],
+    out.update({"cores": base["cores"], "value_leg": best,
                 "cpu_model": cpu_model(), "nproc": os.cpu_count(),
                 "sched_affinity_cpus": affinity, "torch_default_threads": threads})
     for name, tag in (("all_affinity", "all_affinity"), ("share", "share_threads"),
@@ -467,9 +471,10 @@ def cpu_baselines(k, gin_layers, workload, batch, seconds=20.0):
     if legs["all_affinity"] is None:
         out["note"] = (f"the {affinity}-thread leg did not finish within "
                        f"{LEG_TIMEOUT['all_affinity']:.0f} s (threads far above this process's CPU "
-                       "share); value is the best finished leg")
-    out["sample"] = base["sample"] + (f"; legs in child processes: {affinity} threads (value), "
-                                      f"{threads} threads, 1 thread")
+                       "share)")
+    out["sample"] = base["sample"] + (f"; legs in child processes: {affinity} threads (all "
+                                      f"affinity CPUs), {threads} threads (CPU share), 1 thread; "
+                                      f"value = the fastest leg ({best})")
     return out
 
 

@@ -568,6 +568,8 @@ __global__ __launch_bounds__(kK1One) void egonet_k1_onepass_k(
     const int32_t *__restrict__ dims, int32_t *__restrict__ ego_dims) {
     const int nblk = gridDim.x, tid = threadIdx.x;
     int blk = blockIdx.x;
+    SCGIB_MARK(0);
+    SCGIB_MARK_HWID();
     if (nblk > kK1Resident) {  // block-uniform: the logical index from the ticket
         __shared__ int sTicket;
         if (tid == 0)
@@ -609,6 +611,7 @@ __global__ __launch_bounds__(kK1One) void egonet_k1_onepass_k(
         }
     }
     __syncthreads();
+    SCGIB_MARK(1);
     const K1Lds acc{rowptr, col, sRp, sCol, lo, c0, static_cast<uint32_t>(nc),
                     static_cast<uint32_t>(kWin)};
     // with the window in LDS the loops run over the actual members and
@@ -638,6 +641,7 @@ __global__ __launch_bounds__(kK1One) void egonet_k1_onepass_k(
                 ne += k1_index(b, acc.cl(e, true, 0)) >= 0 ? 1 : 0;
         }
     }
+    SCGIB_MARK(2);
     int32_t in_n = nb, in_e = ne;  // inclusive within the wave, then the block
     wave_scan2(in_n, in_e);
     int32_t agg_n = __shfl(in_n, 63, kWave), agg_e = __shfl(in_e, 63, kWave);
@@ -736,6 +740,7 @@ __global__ __launch_bounds__(kK1One) void egonet_k1_onepass_k(
             if (i < n_ego_cap) ego_nodes[i] = 0;
         }
     }
+    SCGIB_MARK(3);
     if (live) {  // members ascending (DGL order), each row's columns in CSR order
         int32_t r = 0;
         for (uint64_t m0 = b.w[0], m1 = b.w[1]; m0 | m1; ++r) {
@@ -752,6 +757,7 @@ __global__ __launch_bounds__(kK1One) void egonet_k1_onepass_k(
             }
         }
     }
+    SCGIB_MARK(4);
     // every look-back of this block is done: count it in; the last one resets
     // (wave 0 only: its look-back is the block's)
     if (wave == 0) {
@@ -949,3 +955,10 @@ extern "C" int scgib_egonet_fill(const int32_t *rowptr, const int32_t *col,
 #undef SCGIB_EGO_FILL
     return launch_status();
 }
+
+#ifdef SCGIB_TRACE
+// debug build only: this translation unit's phase-stamp buffer (common.h)
+extern "C" int scgib_trace_set_egonet(void *buf) {
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_trace), &buf, sizeof(buf)) == hipSuccess ? 0 : 1;
+}
+#endif

@@ -483,7 +483,7 @@ def _egonet_k1(g, ego_ptr, ego_eptr, ws, x, max_in_degree=12):
     if EGO_K1_ONEPASS:
         from . import ops  # (ops imports this module)
         state = ops.scan_state(dev, "egonet_k1_scan", int(_lib.query("scgib_egonet_k1_scan_words", n)))
-        _lib.call("scgib_egonet_k1_build_onepass", _ptr(g.rowptr), _ptr(g.col), n,
+        ops._launch("scgib_egonet_k1_build_onepass", {"n": n}, _ptr(g.rowptr), _ptr(g.col), n,
                   int(max_in_degree), _ptr(ego_ptr), _ptr(ego_eptr), _ptr(state), _ptr(ego_nodes),
                   _ptr(sub_rowptr), _ptr(sub_col), n_s, _ptr(g.dims), _ptr(ego_dims), _stream())
     else:

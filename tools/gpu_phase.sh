@@ -1,0 +1,7 @@
+#!/bin/bash
+# phase trace of the GIN / ego-build kernels (trace build of the library)
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"
+mkdir -p gpurun_out/phase
+SCGIB_LIB=$PWD/s-cgib_amd/libscgib_trace.so timeout -k 10 300 python tools/phase_trace.py > gpurun_out/phase/trace.txt 2>&1; rc=$?
+grep -v amdgpu.ids gpurun_out/phase/trace.txt | head -60; exit $rc

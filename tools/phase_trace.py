@@ -23,6 +23,7 @@ pkg = importlib.import_module("s-cgib_amd")
 import bench  # noqa: E402
 
 PHASES = {
+    "scgib_egonet_k1_build_onepass": ["window", "count", "lookback", "fill"],
     "scgib_gin_layer_fwd_bn": ["gather", "gemm1", "gemm2+st", "tilestat", "bn_hier"],
     "scgib_gin_layer0_fwd": ["gather", "gemm1", "gemm2+st", "tilestat", "bn_hier"],
     # gin_bwd5_k: marks of the first sub-tile, then the remaining sub-tiles
@@ -75,6 +76,9 @@ def main():
     pkg.ops.OBSERVER = None
     for name, meta, t in recs:
         nb = int((t[:, 0] != 0).sum())
+        if nb == 0:
+            print(f"{name}: no stamps")
+            continue
         t = t[:nb]
         ph = PHASES[name]
         start = t[:, 0]

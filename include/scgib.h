@@ -587,14 +587,19 @@ int scgib_mlp2_bwd(const float *dout, const float *x, const float *r, int32_t d_
  * forward with recons_type 'adj'; replaces scgib_mlp2_fwd + scgib_recon_fwd
  * and their backward).  Forward: out (= IM), r, and loss; `ws` holds
  * scgib_mlp2_recon_ws_floats(n) floats (per-tile Gram partials, G, loss
- * partials) and must be passed unchanged to the backward; `counter` is one
- * zeroed uint32, left zero.  Backward: dx = d loss / d x and wgrad as
+ * partials) and must be passed unchanged to the backward; `counter` is three
+ * zeroed uint32, left zero.  When the launch's workgroups are all co-resident
+ * the MLP tiles also finish the loss (no second launch; the same bits either
+ * way).  Backward: dx = d loss / d x and wgrad as
  * scgib_mlp2_bwd, for d loss / d recon = *g_loss; rowptr_t/col_t NULL for a
  * symmetric graph (A = A^T).  wgrad NULL: the per-workgroup slabs
  * (scgib_mlp2_slab_floats(n, d_in) floats, width 64*64 + 64*d_in + 128) are
  * left for the caller's scgib_slab_reduce(_multi) — the model path defers
  * them into an encoder chain's final reduce, off the loss section. */
 int64_t scgib_mlp2_recon_ws_floats(int64_t n_nodes);
+/* Testing hook: 0 = always finish the recon loss in its own launch; returns
+ * the previous setting (default 1). */
+int scgib_set_recon_fold(int on);
 int scgib_mlp2_recon_fwd(const float *x, int32_t d_in, int64_t n_nodes, const float *w1,
                          const float *b1, const float *w2, const float *b2, float *r, float *out,
                          const int32_t *rowptr, const int32_t *col, int64_t n_edges, float *ws,

@@ -18,6 +18,7 @@ _P, _I64, _I32, _F, _D = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32, ctypes
 # name -> (restype, argtypes); mirrors include/scgib.h exactly
 SIGNATURES = {
     "scgib_abi_version": (ctypes.c_int, []),
+    "scgib_set_recon_fold": (ctypes.c_int, [ctypes.c_int]),
     "scgib_strerror": (ctypes.c_char_p, [ctypes.c_int]),
     "scgib_gin_aggregate": (ctypes.c_int, [_P, _P, _P, _I64, _I32, _F, _P, _P, _P]),
     "scgib_segment_sum": (ctypes.c_int, [_P, _P, _I64, _I32, _P, _P, _P]),
@@ -225,7 +226,7 @@ class PairBwdArgs(ctypes.Structure):
                 ("trace", ctypes.c_void_p)]
 
 
-ABI_VERSION = 9
+ABI_VERSION = 10
 STATS_STRIDE = 260
 PGRAD_STRIDE = 324
 HIDDEN = 64

@@ -217,7 +217,7 @@ extern "C" int scgib_segment_broadcast(const float *g, const int32_t *ptr, int64
     return launch_status();
 }
 
-extern "C" int scgib_abi_version(void) { return 9; }
+extern "C" int scgib_abi_version(void) { return 10; }
 
 extern "C" const char *scgib_strerror(int code) {
     if (code == SCGIB_OK) return "ok";

@@ -35,6 +35,8 @@
 // columns of one row) bank-conflict free for ds_read_b32.
 #include "mfma_tile.h"
 #include "contrast_body.h"
+#include "recon_fin.h"
+#include "running_update.h"
 
 namespace scgib {
 
@@ -480,7 +482,16 @@ struct ReconArgs {
     // MLP's (con.B = 0: none): it reads only z1 / z2, so it runs beside the
     // MLP instead of as its own launch on the critical chain
     ContrastArgs con;
+    // fwd, fin_on: the tiles finish the loss themselves (recon_fin.h) once
+    // every tile has published its Gram partial and output rows (write-through
+    // stores + one arrival each); the host sets it only when the whole grid is
+    // co-resident (one workgroup per CU).  ru_block >= 0: that workgroup runs
+    // the compressor BatchNorm's running update (running_update.h)
+    ReconFin fin;
+    int fin_on, ru_block;
+    scgib_running_update ru;
 };
+constexpr uint64_t kFinWaitTicks = 20000000;  // 0.2 s of the 100 MHz wall clock
 
 // GATHER = false is the dense two-layer MLP of the head (models.py:1055-1057,
 // applied at :1174): the tile's input rows are staged directly, agg_out and
@@ -521,6 +532,10 @@ __global__ __launch_bounds__(256, (kFwdAlias<DIN, GATHER, PRE> ? 3 : 1)) void gi
     __shared__ float sPre[PRE ? (TM + 32) * kPreLD : 1];  // aggx tile | Wt
     if constexpr (RECON && DIN == 128) {  // the pretraining head (interaction map width)
         static_assert(TM * LDA >= CT * CLD, "contrastive tiles in sA / sW1");
+        if (static_cast<int>(blockIdx.x) == rec.ru_block) {  // block-uniform
+            running_update_body<256>(rec.ru);
+            return;
+        }
         if (rec.con.B > 0 && static_cast<int>(blockIdx.x) >= rec.con.nmain) {  // block-uniform
             const int64_t b = blockIdx.x - rec.con.nmain, nrb = contrast_row_blocks(rec.con.B);
             SCGIB_MARK(0);
@@ -688,7 +703,10 @@ __global__ __launch_bounds__(256, (kFwdAlias<DIN, GATHER, PRE> ? 3 : 1)) void gi
         const int row = wr * 32 + acc_row(reg, l);
         acc[reg] += bias2;
         if (row < nv) {
-            z2_out[(row0 + row) * 64 + ccol] = acc[reg];
+            if constexpr (RECON)  // write-through: the fused finish reads it from other CUs
+                st_agent(&z2_out[(row0 + row) * 64 + ccol], acc[reg]);
+            else
+                z2_out[(row0 + row) * 64 + ccol] = acc[reg];
             s += acc[reg];
         }
     }
@@ -704,7 +722,34 @@ __global__ __launch_bounds__(256, (kFwdAlias<DIN, GATHER, PRE> ? 3 : 1)) void gi
             const f32x16 g = mma_pf<TM, true, true>(sA + wr * 32, LDH, sA + wc * 32, LDH, zero16());
             float *gs = rec.gslab + tile * 4096;
 #pragma unroll
-            for (int reg = 0; reg < 16; ++reg) gs[(wr * 32 + acc_row(reg, l)) * 64 + ccol] = g[reg];
+            for (int reg = 0; reg < 16; ++reg) st_agent(&gs[(wr * 32 + acc_row(reg, l)) * 64 + ccol], g[reg]);
+            if (rec.fin_on) {  // block-uniform
+                // publish: every wave's write-through stores drained, one arrival
+                const unsigned ntiles = static_cast<unsigned>((n + TM - 1) / TM);
+                block_arrive(rec.fin.cnt + 1, ntiles);
+                SCGIB_MARK(6);
+                // tiles past the virtual blocks (d_in = 64 past 256 tiles) only publish:
+                // they never read the counter again, which the last virtual block resets
+                if (tile >= kFinBlocks) return;
+                if (tid == 0) {  // every tile published (bounded wait), then one acquire
+                    const uint64_t t0 = wall_clock64();
+                    while (__hip_atomic_load(rec.fin.cnt + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < ntiles) {
+                        __builtin_amdgcn_s_sleep(1);
+                        if (wall_clock64() - t0 > kFinWaitTicks) {  // loss -> NaN (recon_fin_block)
+                            __hip_atomic_store(rec.fin.cnt + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                            break;
+                        }
+                    }
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                }
+                __syncthreads();
+                SCGIB_MARK(7);
+                ReconFin f = rec.fin;
+                f.im = z2_out;  // (this kernel's own output, read through the pointer it wrote)
+                recon_fin_block(static_cast<int>(tile), f, ncap, dims, true);
+                SCGIB_MARK(10);
+            }
         }
         return;
     }
@@ -1970,6 +2015,30 @@ extern "C" int64_t scgib_mlp2_recon_ws_floats(int64_t n_nodes) {
     return n_nodes <= 0 ? 0 : scgib_gin_tiles(n_nodes) * 4096 + 4096 + 2 * 512;
 }
 
+static bool g_recon_fold = true;  // scgib_set_recon_fold (tests: both paths bit-equal)
+extern "C" int scgib_set_recon_fold(int on) {
+    const int prev = g_recon_fold ? 1 : 0;
+    g_recon_fold = on != 0;
+    return prev;
+}
+
+// co-resident workgroups of the head MLP launch on the current device (the
+// fused loss finish makes its tiles wait on each other)
+template <int DIN>
+static int64_t recon_fold_slots() {
+    static int64_t slots = -1;
+    if (slots < 0) {
+        int dev = 0, cus = 0, per = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(
+                &per, gin_fwd_k<DIN, false, false, false, true>, 256, 0) != hipSuccess)
+            return 0;
+        slots = static_cast<int64_t>(cus) * per;
+    }
+    return slots;
+}
+
 static int mlp2_recon_fwd(const float *x, int32_t d_in, int64_t n_nodes, const float *w1,
                           const float *b1, const float *w2, const float *b2, float *r,
                           float *out, const int32_t *rowptr, const int32_t *col, int64_t n_edges,
@@ -1987,14 +2056,32 @@ static int mlp2_recon_fwd(const float *x, int32_t d_in, int64_t n_nodes, const f
     rec.gslab = ws;
     rec.con = con;
     rec.con.nmain = static_cast<int>(nt);
+    rec.ru_block = -1;
     const int64_t ncon = con.B > 0 ? contrast_row_blocks(con.B) * con.nsplit : 0;
+    const bool with_ru = ru && ru->n_graphs > 0;
     hipStream_t st = as_stream(stream);
+    // the loss finish inside this launch when every workgroup is co-resident
+    // (the head tiles hold one CU each, 101 + 27 KB of LDS): the tiles wait for
+    // each other, so a grid past the co-resident slots would not finish — two
+    // launches then
+    const int64_t grid = nt + ncon + (with_ru && d_in == 128 ? 1 : 0);
+    const bool fold = g_recon_fold && (!with_ru || d_in == 128) &&
+                      grid <= (d_in == 128 ? recon_fold_slots<128>() : recon_fold_slots<64>());
+    if (fold) {
+        rec.fin = ReconFin{ws, out, rowptr, col, n_edges, gram, wsd,
+                           reinterpret_cast<unsigned *>(counter), loss};
+        rec.fin_on = 1;
+        if (with_ru) {
+            rec.ru_block = static_cast<int>(nt + ncon);
+            rec.ru = *ru;
+        }
+    }
     if (d_in == 128)
-        gin_fwd_k<128, false, false, false, true><<<(unsigned)(nt + ncon), 256, 0, st>>>(x, nullptr, nullptr, nullptr, nullptr, n_nodes, 0.f, w1, b1, w2, b2, nullptr, r, out, nullptr, dims, BnFwdFuse{}, PreArgs{}, scgib_bn_pending{}, rec);
+        gin_fwd_k<128, false, false, false, true><<<(unsigned)(fold ? grid : nt + ncon), 256, 0, st>>>(x, nullptr, nullptr, nullptr, nullptr, n_nodes, 0.f, w1, b1, w2, b2, nullptr, r, out, nullptr, dims, BnFwdFuse{}, PreArgs{}, scgib_bn_pending{}, rec);
     else
         gin_fwd_k<64, false, false, false, true><<<(unsigned)nt, 256, 0, st>>>(x, nullptr, nullptr, nullptr, nullptr, n_nodes, 0.f, w1, b1, w2, b2, nullptr, r, out, nullptr, dims, BnFwdFuse{}, PreArgs{}, scgib_bn_pending{}, rec);
     const int rc = launch_status();
-    if (rc != SCGIB_OK) return rc;
+    if (rc != SCGIB_OK || fold) return rc;
     return launch_recon_fin(ws, out, rowptr, col, n_nodes, n_edges, gram, wsd, counter, loss, dims,
                             ru, st);
 }
@@ -2031,7 +2118,10 @@ extern "C" int scgib_mlp2_recon_contrastive_fwd(
     // (each over more column tiles) rather than a second wave behind the
     // tiles; the loss does not depend on the split count (per-tile partials)
     const int64_t nrb = contrast_row_blocks(n_graphs);
-    const int64_t fit = n_nodes > 0 ? (kCUs - scgib_gin_tiles(n_nodes)) / nrb : con.nsplit;
+    // (one CU kept for the running-update workgroup, so that the grid stays
+    // within the CUs and the loss finish can run inside the launch)
+    const int64_t ru_wg = ru && ru->n_graphs > 0 ? 1 : 0;
+    const int64_t fit = n_nodes > 0 ? (kCUs - scgib_gin_tiles(n_nodes) - ru_wg) / nrb : con.nsplit;
     if (fit < 1) {  // not even one split fits beside the tiles: the two launches
         const int rc = scgib_contrastive_fwd(z1, z2, n_graphs, cws, closs, ccounters, stream);
         if (rc != SCGIB_OK) return rc;

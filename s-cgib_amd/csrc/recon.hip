@@ -19,14 +19,11 @@
 //   fence) forms the loss.  Deterministic for a given N.
 // recon_bwd_k: grad_v = (g/N) (4 (IM G)_v - 2 ((A + A^T) IM)_v), G staged in
 //   LDS, the row of IM broadcast from LDS.
-#include "mfma_tile.h"
+#include "recon_fin.h"
 #include "running_update.h"
 
 namespace scgib {
 
-constexpr int kGram = 64 * 64;
-// finalize: 256 workgroups x (16 Gram entries x 16 slab partitions)
-constexpr int kFinBlocks = kGram / 16;
 
 // ~64 rows per partial workgroup (short dependent MFMA/load chains, enough
 // workgroups to spread over the CUs), at most 1024 slabs
@@ -199,111 +196,22 @@ __global__ __launch_bounds__(256) void recon_bwd_k(const float *__restrict__ im,
 
 // ---------------------------------------------------------------------------
 // Fused path (the pretraining model's): the head MLP forward already wrote one
-// Gram partial per 64-row tile (gin_fwd_k<.., RECON>), so one kernel finishes
-// the forward loss:
-//   * workgroup b reduces Gram entries [16 b, 16 b + 16) over the tiles
-//     (16 partitions x 8 loads in flight, fp64, fixed order) -> G, ||G||^2_b;
-//   * and the edge term of its row range [b R, b R + R), R = ceil(N / 256):
-//     sum_v <im_v, sum_{u->v} im_u> with the latency-batched CSR gather
-//     (64 rows per pass, 16 lanes x float4 per row);
-//   * the last of the 256 workgroups (block_arrive: agent-scope data, no L2
-//     write-back fence) forms loss = (sum ||G||^2_b - 2 sum E_b + |E|) / N in
-//     fixed order and resets its counter.
+// Gram partial per 64-row tile (gin_fwd_k<.., RECON>).  When the MLP launch
+// cannot finish the loss itself (more tiles than fit the chip beside its other
+// workgroups, gin_layer.hip), this launch does: kFinBlocks workgroups, the
+// first V = min(tiles, 256) one virtual block each (recon_fin.h), plus
+// optionally one workgroup for the compressor BatchNorm's running update.
 // The backward is fused into the head MLP backward (gin_bwd_k<.., RECON>).
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void recon_fin_k(const float *__restrict__ gslab,
-                                                   const float *__restrict__ im,
-                                                   const int32_t *__restrict__ rowptr,
-                                                   const int32_t *__restrict__ col, int64_t ncap,
-                                                   int64_t ecap, float *__restrict__ gram,
-                                                   double *__restrict__ wsd,
-                                                   unsigned *__restrict__ cnt,
-                                                   float *__restrict__ loss,
+__global__ __launch_bounds__(256) void recon_fin_k(const ReconFin a, int64_t ncap,
                                                    const int32_t *__restrict__ dims,
                                                    const scgib_running_update ru) {
     if (blockIdx.x == kFinBlocks) {  // (block-uniform) the extra workgroup: the running update
         running_update_body<256>(ru);
         return;
     }
-    const int64_t n = eff_count(dims, 0, ncap), n_edges = eff_count(dims, 1, ecap);
-    const int64_t ntiles = (n + TM - 1) / TM;
-    const int tid = threadIdx.x;
-    // edge term: this workgroup's rows (issued first: three dependent load rounds)
-    const int64_t R = (n + kFinBlocks - 1) / kFinBlocks;
-    const int64_t rb = static_cast<int64_t>(blockIdx.x) * R;
-    const int64_t re = rb + R < n ? rb + R : n;
-    const float4 *im4 = reinterpret_cast<const float4 *>(im);
-    const float4 one = make_float4(1.f, 1.f, 1.f, 1.f), zero = make_float4(0.f, 0.f, 0.f, 0.f);
-    const int c = tid & 15, rbase = tid >> 4;
-    float e = 0.f;
-    for (int64_t r0 = rb; r0 < re; r0 += TM) {
-        const int nv = static_cast<int>(re - r0 < TM ? re - r0 : TM);
-        GatherHead<4> hd;
-        float4 nb[4];
-        gather_head<4, 16, 16>(im4, rowptr, r0, nv, rbase, c, hd);
-        gather_tail<4, 16, false>(im4, col, hd, c, 0.f, one, zero, nb);
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const float d = hd.self[k].x * nb[k].x + hd.self[k].y * nb[k].y +
-                            hd.self[k].z * nb[k].z + hd.self[k].w * nb[k].w;
-            e += rbase + 16 * k < nv ? d : 0.f;
-        }
-    }
-    // Gram entries over the tile partials
-    const int el = tid & 15, sp = tid >> 4;
-    const int ent = blockIdx.x * 16 + el;
-    double acc = 0.0;
-    for (int64_t b0 = sp; b0 < ntiles; b0 += 16 * 8) {
-        float v[8];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            const int64_t b = b0 + 16 * j < ntiles ? b0 + 16 * j : sp;  // clamped: unconditional
-            v[j] = gslab[b * kGram + ent];
-        }
-#pragma unroll
-        for (int j = 0; j < 8; ++j)
-            if (b0 + 16 * j < ntiles) acc += static_cast<double>(v[j]);
-    }
-    __shared__ double part[16][17];
-    __shared__ double sE[256];
-    __shared__ double red[16];
-    part[sp][el] = acc;
-    sE[tid] = static_cast<double>(e);
-    __syncthreads();
-    if (tid < 16) {
-        double g = 0.0;
-#pragma unroll
-        for (int k = 0; k < 16; ++k) g += part[k][tid];
-        gram[blockIdx.x * 16 + tid] = static_cast<float>(g);
-        red[tid] = g * g;
-    }
-    for (int off = 128; off >= 1; off >>= 1) {
-        if (tid < off) sE[tid] += sE[tid + off];
-        __syncthreads();
-    }
-    if (tid == 0) {
-        double q = 0.0;
-        for (int k = 0; k < 16; ++k) q += red[k];
-        st_agent(&wsd[blockIdx.x], q);
-        st_agent(&wsd[kFinBlocks + blockIdx.x], sE[0]);
-    }
-    if (!block_arrive(cnt, kFinBlocks)) return;
-    __shared__ double fin[2][256];
-    fin[0][tid] = ld_agent(&wsd[tid]);
-    fin[1][tid] = ld_agent(&wsd[kFinBlocks + tid]);
-    __syncthreads();
-    for (int off = 128; off >= 1; off >>= 1) {
-        if (tid < off) {
-            fin[0][tid] += fin[0][tid + off];
-            fin[1][tid] += fin[1][tid + off];
-        }
-        __syncthreads();
-    }
-    if (tid == 0) {
-        *loss = static_cast<float>((fin[0][0] - 2.0 * fin[1][0] + static_cast<double>(n_edges)) /
-                                   static_cast<double>(n));
-        *cnt = 0u;  // ready for the next launch / graph replay
-    }
+    if (static_cast<int>(blockIdx.x) >= recon_fin_vblocks(eff_count(dims, 0, ncap))) return;
+    recon_fin_block(static_cast<int>(blockIdx.x), a, ncap, dims, false);
 }
 
 int launch_recon_fin(const float *gslab, const float *im, const int32_t *rowptr,
@@ -311,9 +219,9 @@ int launch_recon_fin(const float *gslab, const float *im, const int32_t *rowptr,
                      double *wsd, unsigned *cnt, float *loss, const int32_t *dims,
                      const scgib_running_update *ru, hipStream_t st) {
     const bool with_ru = ru && ru->n_graphs > 0;
+    const ReconFin a{gslab, im, rowptr, col, n_edges, gram, wsd, cnt, loss};
     recon_fin_k<<<kFinBlocks + (with_ru ? 1 : 0), 256, 0, st>>>(
-        gslab, im, rowptr, col, n_nodes, n_edges, gram, wsd, cnt, loss, dims,
-        with_ru ? *ru : scgib_running_update{});
+        a, n_nodes, dims, with_ru ? *ru : scgib_running_update{});
     return launch_status();
 }
 

@@ -1512,7 +1512,7 @@ class _Mlp2Recon(torch.autograd.Function):
         ws = torch.empty(int(_lib.query("scgib_mlp2_recon_ws_floats", n)), dtype=torch.float32,
                          device=dev)
         loss = torch.empty((), dtype=torch.float32, device=dev)
-        cnt = counters(dev, "mlp2_recon", 1)
+        cnt = counters(dev, "mlp2_recon", 3)
         _lib.call("scgib_mlp2_recon_fwd", _p(x), d_in, n, _p(w1), _p(b1), _p(w2), _p(b2), _p(r),
                   _p(out), _p(graph.rowptr), _p(graph.col), graph.edge_capacity(), _p(ws),
                   _p(cnt), _p(loss), _p(graph.dims), _stream())
@@ -1573,7 +1573,7 @@ class _Mlp2ReconContrastive(torch.autograd.Function):
                           dtype=torch.float32, device=dev)
         loss = torch.empty((), dtype=torch.float32, device=dev)
         closs = torch.empty((), dtype=torch.float32, device=dev)
-        cnt = counters(dev, "mlp2_recon", 1)
+        cnt = counters(dev, "mlp2_recon", 3)
         ccnt = counters(dev, "contrastive", int(_lib.query("scgib_contrastive_counters", B)))
         ru = take_running_update()
         _launch("scgib_mlp2_recon_contrastive_fwd", {"n": n, "d_in": d_in, "B": B}, _p(x), d_in, n,

@@ -3,6 +3,8 @@
 Integer work (ego-nets) must be bit-exact; fp32 losses within 1e-4 relative
 (BASELINE.json north_star); activations/gradients within the tolerances
 written next to each check (fp32 reordering through 5-layer encoders)."""
+import math
+
 import numpy as np
 import pytest
 import torch
@@ -590,6 +592,53 @@ def test_mlp2_recon_contrastive_fused(pkg, dev, n_mols, n_graphs):
     (3.0 * loss_c).backward()
     assert rel_err(ca, loss_c.item()) < LOSS_TOL
     assert rel_l2(z1a, z1r.grad) < 1e-5 and rel_l2(z2a, z2r.grad) < 1e-5
+
+
+@pytest.mark.parametrize("n_mols", [7, 300, 900, 1100])
+def test_recon_fold_bit_equal(pkg, dev, n_mols):
+    """The recon loss finished inside the head MLP launch (the tiles publish
+    their Gram partials and output rows, wait for each other, then run
+    recon_fin.h's virtual blocks) against its own launch (recon_fin_k): the
+    same virtual-block sums in the same order, so the loss bits match, and so
+    do G and every gradient.  900 molecules (16.2 K atoms): 254 head tiles,
+    the contrastive workgroups no longer fit beside them, the fused finish
+    waits across 254 workgroups; 1100 (310 tiles): past the co-resident grid
+    at d_in = 128, both runs take the two launches there (the fallback), while
+    the d_in = 64 head (two workgroups per CU) still folds."""
+    g, _ = rand_graph(pkg, n_mols, "qm9", 11, dev)
+    n = g.num_nodes()
+    torch.manual_seed(n_mols + 1)
+    mlp = torch.nn.Sequential(torch.nn.Linear(128, 64), torch.nn.ReLU(),
+                              torch.nn.Linear(64, 64)).to(dev)
+    x = (0.3 * torch.randn(n, 128)).to(dev)
+    z1 = torch.randn(n_mols, 64).to(dev)
+    z2 = torch.randn(n_mols, 64).to(dev)
+    mlp64 = torch.nn.Sequential(torch.nn.Linear(64, 64), torch.nn.ReLU(),
+                                torch.nn.Linear(64, 64)).to(dev)
+    outs = []
+    for fold in (1, 0):
+        prev = pkg._lib.query("scgib_set_recon_fold", fold)
+        try:
+            for p_ in mlp.parameters():
+                p_.grad = None
+            xa = x.clone().requires_grad_(True)
+            rec, con = pkg.ops.mlp2_recon_contrastive(xa, mlp, g, z1, z2)
+            (2.0 * rec + con).backward()
+            # the d_in = 64 head (scgib_mlp2_recon_fwd, two workgroups per CU)
+            x64 = x[:, :64].contiguous().requires_grad_(True)
+            rec64 = pkg.ops.mlp2_recon(x64, mlp64, g)
+            rec64.backward()
+            torch.cuda.synchronize()
+            outs.append((rec.item(), con.item(), rec64.item(), xa.grad.cpu(), x64.grad.cpu(),
+                         [p_.grad.cpu() for p_ in mlp.parameters()]))
+        finally:
+            pkg._lib.query("scgib_set_recon_fold", prev)
+    (ra, ca, r64a, xa_, x64a, pa), (rb, cb, r64b, xb, x64b, pb) = outs
+    assert math.isfinite(ra) and ra == rb and ca == cb
+    assert math.isfinite(r64a) and r64a == r64b
+    assert torch.equal(xa_, xb) and torch.equal(x64a, x64b)
+    for u, v in zip(pa, pb):
+        assert torch.equal(u, v)
 
 
 # ---------------------------------------------------------------------------

@@ -34,7 +34,10 @@ PHASES = {
     "scgib_gin_bwd_stats_bn": ["gather+dy", "bn_hier"],
     "scgib_gin_bwd_stats_bn_fold": ["gather+dy", "bn_hier"],
     # head MLP (+ recon) tiles mark 1..3, the contrastive workgroups 5
-    "scgib_mlp2_recon_contrastive_fwd": ["load", "gemm1", "-", "-", "contrast"],
+    # (+ the fused loss finish: published, waited + acquire, then recon_fin.h's
+    # edge gather, Gram chunks, arrival / last-arrival loss)
+    "scgib_mlp2_recon_contrastive_fwd": ["load", "gemm1", "-", "-", "contrast", "gemm2+pub",
+                                         "wait+acq", "fin:edges", "fin:gram", "fin:arrive"],
     "scgib_mlp2_recon_contrastive_bwd": ["dz2(recon)", "dW2,dr,dz1", "dW1,dx", "-", "contrast"],
 }
 MAXB = 4096

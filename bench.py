@@ -748,6 +748,9 @@ def main():
         loss = step(a.warmup + i)
     barrier()
     elapsed = time.perf_counter() - t0
+    xq_to = pkg.ops.xq_timeouts(dev)
+    if xq_to:  # a hand-off wait gave up: its queue ran ahead of the data
+        raise SystemExit(f"bench: {xq_to} cross-queue hand-off waits timed out (ops.XQ_FLAGS)")
     if world > 1:
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)

@@ -67,6 +67,15 @@ enum {
 #define SCGIB_PGRAD_STRIDE 324 /* floats per graph in the parameter-gradient slab */
 
 int scgib_abi_version(void);
+/* Cross-queue hand-off without a stream/graph dependency: `words` is four
+ * zeroed uint32 shared by one producer/consumer pair.  scgib_stream_signal
+ * (producer stream, after the work to hand over) counts one signal;
+ * scgib_stream_wait (consumer stream) returns once a signal it has not yet
+ * consumed is there, so the consumer stream's later kernels see the
+ * producer's data.  Calls must pair up in order (n-th wait <-> n-th signal).
+ * A wait that sees no signal for 0.2 s gives up and counts words[2]. */
+int scgib_stream_signal(uint32_t *words, scgib_stream_t stream);
+int scgib_stream_wait(uint32_t *words, scgib_stream_t stream);
 const char *scgib_strerror(int code);
 
 /* ---- A5: GIN neighbourhood aggregation (DGL GINConv, sum aggregator) ------

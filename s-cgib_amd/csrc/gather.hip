@@ -160,6 +160,33 @@ __global__ __launch_bounds__(256) void segment_broadcast_scalar_k(
         }                                                                                   \
     } while (0)
 
+// Cross-queue hand-off without a graph edge (ops._GinEncoderPair): a graph
+// edge between the step's two chains costs the waiting queue several us even
+// when the producer finished long before; a one-wave
+// kernel pair does not.  words: [0] signals, [1] waits consumed, [2] wait
+// timeouts.  The producer queue's signal kernel runs after its chain (the
+// kernel boundary writes that chain's data back); the consumer queue's wait
+// kernel returns once a signal it has not consumed is there, so the next
+// kernel on its queue (whose start invalidates the caches) reads the data.
+__global__ void stream_signal_k(unsigned *w) {
+    if (threadIdx.x == 0) __hip_atomic_fetch_add(w, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__global__ void stream_wait_k(unsigned *w) {
+    if (threadIdx.x == 0) {
+        const unsigned a = __hip_atomic_load(w + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint64_t t0 = wall_clock64();
+        while (__hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - a - 1u >= 0x80000000u) {
+            __builtin_amdgcn_s_sleep(2);
+            if (wall_clock64() - t0 > 20000000) {  // 0.2 s of the 100 MHz clock: counted, not hung
+                __hip_atomic_fetch_add(w + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                break;
+            }
+        }
+        __hip_atomic_store(w + 1, a + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
 static bool dim_ok(int32_t dim) {
     return dim >= 4 && dim <= 256 && dim % 4 == 0 && ((dim / 4) & (dim / 4 - 1)) == 0;
 }
@@ -214,6 +241,18 @@ extern "C" int scgib_segment_broadcast(const float *g, const int32_t *ptr, int64
     }
     SCGIB_DISPATCH_LPR(dim, segment_broadcast_k, n_seg, reinterpret_cast<const float4 *>(g),
                        ptr, n_seg, reinterpret_cast<float4 *>(out), n_rows, dims);
+    return launch_status();
+}
+
+extern "C" int scgib_stream_signal(uint32_t *words, scgib_stream_t stream) {
+    if (!words) return SCGIB_EINVAL;
+    stream_signal_k<<<1, 64, 0, as_stream(stream)>>>(words);
+    return launch_status();
+}
+
+extern "C" int scgib_stream_wait(uint32_t *words, scgib_stream_t stream) {
+    if (!words) return SCGIB_EINVAL;
+    stream_wait_k<<<1, 64, 0, as_stream(stream)>>>(words);
     return launch_status();
 }
 

@@ -641,6 +641,37 @@ class _Ctx:
         self.saved_tensors = t
 
 
+# The encoder pair's two mid-step cross-queue hand-offs (forward join, backward
+# fork) as a signal / wait kernel pair instead of a stream dependency: in the
+# replayed graph a cross-queue edge stalls the waiting queue several us even
+# when the producer finished long before (tools/xq_probe.hip).  The
+# step's final join stays a stream dependency (the capture must end joined).
+XQ_FLAGS = True
+
+
+def _xq_words(device, key):
+    """Four zeroed uint32 for one signal / wait pair: the same words whichever
+    stream asks (counters() keys by stream)."""
+    with torch.cuda.stream(torch.cuda.default_stream(device)):
+        return counters(device, ("xq", key), 4)
+
+
+def _xq_handoff(producer, consumer, key):
+    """Order ``consumer``'s later work after ``producer``'s work so far
+    (scgib_stream_signal on producer, scgib_stream_wait on consumer)."""
+    w = _xq_words(producer.device, key)
+    with torch.cuda.stream(producer):
+        _lib.call("scgib_stream_signal", _p(w), _stream())
+    with torch.cuda.stream(consumer):
+        _lib.call("scgib_stream_wait", _p(w), _stream())
+
+
+def xq_timeouts(device):
+    """Waits of the encoder pair's hand-offs that gave up (0 = every wait saw
+    its signal; a non-zero count means the two kernels shared a queue)."""
+    return sum(int(_xq_words(device, k)[2].item()) for k in ("pair_fwd", "pair_bwd"))
+
+
 class _GinEncoderPair(torch.autograd.Function):
     """Encoder2 (ego-net batch, on ``side``) and Encoder1 (core batch, on the
     current stream) with transfer_d folded into both first layers, as ONE
@@ -703,7 +734,10 @@ class _GinEncoderPair(torch.autograd.Function):
             ctx.lin_saved = (f.detach(), w0)
             ctx.core_dims = core.dims
             outs = (s, ro, f, t)
-        main.wait_stream(side)
+        if XQ_FLAGS:
+            _xq_handoff(side, main, "pair_fwd")
+        else:
+            main.wait_stream(side)
         s.record_stream(main)
         ro.record_stream(main)
         return outs
@@ -719,7 +753,10 @@ class _GinEncoderPair(torch.autograd.Function):
         # by compressor[0]'s backward (d f += d t W0, dW0, db0)
         main, side = _torch_stream(), ctx.side
         check_fork(main)
-        side.wait_stream(main)
+        if XQ_FLAGS:
+            _xq_handoff(main, side, "pair_bwd")
+        else:
+            side.wait_stream(main)
         # Encoder1's final weight-gradient reduce runs beside the ego chain's
         # last layers; it also sums the loss section's deferred slabs
         # (SlabScope: the head MLP's and the interaction's, enqueued on the

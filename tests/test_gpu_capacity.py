@@ -134,6 +134,7 @@ def test_graph_replay_matches_exact_over_batches(pkg, dev, k, fork_losses, monke
         loss.backward()
         static_losses = torch.stack([kl, con, rec, loss]).detach()
 
+    t0 = pkg.ops.xq_timeouts(dev)
     for i in (0, 1, 2, 3, 1):  # includes a batch seen before (replay is stateless)
         gh = hosts[i]
         n = gh.num_nodes()
@@ -146,6 +147,9 @@ def test_graph_replay_matches_exact_over_batches(pkg, dev, k, fork_losses, monke
         graph.replay()
         torch.cuda.synchronize()
         _compare(exact_m, cap_m, le, static_losses.clone())
+    # the encoder pair's signal / wait hand-offs (ops.XQ_FLAGS): every wait saw
+    # its signal in the replayed graph (the kernels landed on different queues)
+    assert pkg.ops.xq_timeouts(dev) == t0
 
 
 def test_static_batch_rejects_oversized(pkg, dev):

@@ -8,6 +8,7 @@ from __future__ import annotations
 
 import contextlib
 import ctypes
+import os
 import weakref
 
 import numpy as np
@@ -646,7 +647,20 @@ class _Ctx:
 # replayed graph a cross-queue edge stalls the waiting queue several us even
 # when the producer finished long before (tools/xq_probe.hip).  The
 # step's final join stays a stream dependency (the capture must end joined).
-XQ_FLAGS = True
+# A replayed graph may order a wait before its signal on the same queue, and
+# then only concurrent queues let the signal run: off where kernel dispatch is
+# serialised device-wide (PMC counter collection, AMD_SERIALIZE_KERNEL, launch
+# blocking) — there a wait would time out (counted, xq_timeouts) instead.
+
+
+def _dispatch_serialised():
+    env = os.environ
+    return any(env.get(k, "0") not in ("", "0") for k in (
+        "ROCPROF_COUNTER_COLLECTION", "AMD_SERIALIZE_KERNEL", "HIP_LAUNCH_BLOCKING",
+        "CUDA_LAUNCH_BLOCKING"))
+
+
+XQ_FLAGS = not _dispatch_serialised()
 
 
 def _xq_words(device, key):

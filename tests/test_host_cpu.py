@@ -461,3 +461,20 @@ def test_bench_kernel_table_evaluates(pkg):
         f = bench._call_meta(spec["flops"], m)
         assert b > 0 and f >= 0, name
     assert bench.pair_fwd_bytes(pair) == sum(bench.agg_bytes(n, e, d) for n, e, d in pair["layers"])
+
+
+def test_xq_handoffs_off_under_serialised_dispatch(pkg, monkeypatch):
+    """ops.XQ_FLAGS's default: the signal / wait hand-offs need concurrent
+    queues, so they are off under PMC counter collection or serialised /
+    blocking launches (a replayed graph could order a wait before its signal
+    on one queue)."""
+    for k in ("ROCPROF_COUNTER_COLLECTION", "AMD_SERIALIZE_KERNEL", "HIP_LAUNCH_BLOCKING",
+              "CUDA_LAUNCH_BLOCKING"):
+        monkeypatch.delenv(k, raising=False)
+    assert not pkg.ops._dispatch_serialised()
+    monkeypatch.setenv("AMD_SERIALIZE_KERNEL", "0")
+    assert not pkg.ops._dispatch_serialised()
+    for k in ("ROCPROF_COUNTER_COLLECTION", "AMD_SERIALIZE_KERNEL", "HIP_LAUNCH_BLOCKING"):
+        monkeypatch.setenv(k, "1")
+        assert pkg.ops._dispatch_serialised()
+        monkeypatch.delenv(k)

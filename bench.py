@@ -634,9 +634,10 @@ def main():
             opt.step()
             return loss
     else:
-        # capacity mode + HIP graph: one capture of (ego build, forward,
-        # backward[, Adam]) on static buffers; each step copies the next batch
-        # in (5 device-to-device copies) and replays.  Every kernel reads the
+        # capacity mode + HIP graph: one capture of (batch load, ego build,
+        # forward, backward[, Adam]) on static buffers; each replay copies the
+        # pool's next resident batch in (one kernel inside the graph:
+        # StaticBatch.load_next) and steps on it.  Every kernel reads the
         # batch's actual sizes from the device.
         if a.torch_adam:
             opt = torch.optim.Adam(model.parameters(), lr=1e-4, weight_decay=5e-5,
@@ -652,12 +653,11 @@ def main():
             dict.__setitem__(gx.ndata, "x", F.normalize(gh.ndata["x"].float()))
             padded.append(static.pad(gx))
 
+        pool_dev = static.pool(padded)
         one = torch.ones((), dtype=torch.float32, device=dev)
 
-        def load(i):  # batch i into the step's static inputs
-            static.load(padded[i % len(padded)])
-
         def body():
+            static.load_next(pool_dev)  # the pool's next batch into the static inputs
             _, kl, con, rec = model(static.graph, static.x, None, None, None, 1, None, a.k, dev,
                                     a.batch)
             # loss = KL + contrastive + recon (exp_pretraining.py:321): d loss / d part = 1,
@@ -673,7 +673,6 @@ def main():
         side.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(side):  # warm-up (allocator, Adam state, RCCL comm) off the capture
             for i in range(3):
-                load(i)
                 opt.zero_grad(set_to_none=True)
                 body()
                 if collective:
@@ -726,7 +725,6 @@ def main():
             allreduce_mode = "between two graph replays"
 
         def step(i):
-            load(i)
             graph.replay()
             if graph2 is not None:  # RCCL all-reduce of the bucket between the two replays
                 reducer.reduce(force=True)

@@ -74,6 +74,12 @@ int scgib_abi_version(void);
  * consumed is there, so the consumer stream's later kernels see the
  * producer's data.  Calls must pair up in order (n-th wait <-> n-th signal).
  * A wait that sees no signal for 0.2 s gives up and counts words[2]. */
+/* The next batch of a resident pool into a static input buffer, for a
+ * replayed step graph: srcs = device table of n_src device pointers (each
+ * `bytes` long, bytes a multiple of 16); copies srcs[ctr[0] % n_src] to dst
+ * and advances ctr[0].  ctr: two uint32, ctr[1] zero on entry (left zero). */
+int scgib_pool_copy(const uint64_t *srcs, int32_t n_src, uint32_t *ctr, void *dst, int64_t bytes,
+                    scgib_stream_t stream);
 int scgib_stream_signal(uint32_t *words, scgib_stream_t stream);
 int scgib_stream_wait(uint32_t *words, scgib_stream_t stream);
 const char *scgib_strerror(int code);

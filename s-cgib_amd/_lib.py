@@ -19,6 +19,7 @@ _P, _I64, _I32, _F, _D = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32, ctypes
 SIGNATURES = {
     "scgib_abi_version": (ctypes.c_int, []),
     "scgib_set_recon_fold": (ctypes.c_int, [ctypes.c_int]),
+    "scgib_pool_copy": (ctypes.c_int, [_P, _I32, _P, _P, _I64, _P]),
     "scgib_stream_signal": (ctypes.c_int, [_P, _P]),
     "scgib_stream_wait": (ctypes.c_int, [_P, _P]),
     "scgib_strerror": (ctypes.c_char_p, [ctypes.c_int]),

@@ -187,6 +187,27 @@ __global__ void stream_wait_k(unsigned *w) {
     }
 }
 
+// One batch of a resident pool into a step's static input buffer from inside
+// a replayed graph (graph.StaticBatch.load_next): srcs is a device table of
+// n_src pointers; the launch copies srcs[ctr[0] % n_src] to dst, then the last
+// workgroup advances ctr[0] (ctr[1]: its arrival counter, left zero), so the
+// replays walk the pool with no host work between them.
+__global__ void pool_copy_k(const uint64_t *__restrict__ srcs, int32_t n_src, unsigned *ctr,
+                            float4 *__restrict__ dst, int64_t n16) {
+    __shared__ unsigned s_c;
+    if (threadIdx.x == 0) s_c = __hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    const unsigned c = s_c;
+    const float4 *src = reinterpret_cast<const float4 *>(srcs[c % static_cast<unsigned>(n_src)]);
+    const int64_t stride = static_cast<int64_t>(gridDim.x) * 256;
+    for (int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x; i < n16; i += stride)
+        dst[i] = src[i];
+    if (block_arrive(ctr + 1, gridDim.x) && threadIdx.x == 0) {
+        __hip_atomic_store(ctr + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(ctr, c + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
 static bool dim_ok(int32_t dim) {
     return dim >= 4 && dim <= 256 && dim % 4 == 0 && ((dim / 4) & (dim / 4 - 1)) == 0;
 }
@@ -253,6 +274,16 @@ extern "C" int scgib_stream_signal(uint32_t *words, scgib_stream_t stream) {
 extern "C" int scgib_stream_wait(uint32_t *words, scgib_stream_t stream) {
     if (!words) return SCGIB_EINVAL;
     stream_wait_k<<<1, 64, 0, as_stream(stream)>>>(words);
+    return launch_status();
+}
+
+extern "C" int scgib_pool_copy(const uint64_t *srcs, int32_t n_src, uint32_t *ctr, void *dst,
+                               int64_t bytes, scgib_stream_t stream) {
+    if (!srcs || n_src < 1 || !ctr || !dst || bytes < 0 || bytes % 16) return SCGIB_EINVAL;
+    const int64_t n16 = bytes / 16;
+    const int64_t grid = std::max<int64_t>(1, std::min<int64_t>((n16 + 255) / 256, 1024));
+    pool_copy_k<<<(unsigned)grid, 256, 0, as_stream(stream)>>>(
+        srcs, n_src, reinterpret_cast<unsigned *>(ctr), reinterpret_cast<float4 *>(dst), n16);
     return launch_status();
 }
 

@@ -607,6 +607,25 @@ class StaticBatch:
         """Copy a pad()-ed batch into the static buffers (one device copy)."""
         self.blob.copy_(padded["blob"], non_blocking=True)
 
+    def pool(self, padded):
+        """Device state for load_next over the pad()-ed batches ``padded``: the
+        table of their blobs and the cursor (kept alive by the caller along
+        with ``padded``)."""
+        dev = self.blob.device
+        for p in padded:
+            if p["blob"].numel() != self.blob.numel():
+                raise _lib.ScgibError("pool batch was padded for other capacities")
+        table = torch.tensor([p["blob"].data_ptr() for p in padded], dtype=torch.int64, device=dev)
+        return {"table": table, "cursor": torch.zeros(2, dtype=torch.int32, device=dev),
+                "n": len(padded), "batches": padded}
+
+    def load_next(self, pool):
+        """Copy the pool's next batch in (one kernel, capturable: the replays of
+        a graph holding it walk the pool in order, pool(...)[cursor] first)."""
+        _lib.call("scgib_pool_copy", ctypes.c_void_p(pool["table"].data_ptr()), pool["n"],
+                  ctypes.c_void_p(pool["cursor"].data_ptr()), ctypes.c_void_p(self.blob.data_ptr()),
+                  self.blob.numel(), ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
+
     def ego_error(self):
         """Error bits the ego-net build of the last step flagged (0 = none; see
         egonet_batch) — a device read, for checks outside the timed loop."""

@@ -271,3 +271,30 @@ def test_deferred_loss_reduce_partial_and_cast_backward(pkg, dev, mode, monkeypa
     for a, b in zip(got[False], got[True]):
         assert torch.isfinite(b).all()
         assert (a - b).norm() <= 1e-6 * a.norm() + 1e-12
+
+
+def test_pool_load_next_walks_the_pool(pkg, dev):
+    """StaticBatch.load_next (scgib_pool_copy, bench.py's in-graph batch load):
+    eager and captured in a HIP graph, each call / replay copies the pool's
+    next batch in, in order, byte for byte; the cursor's arrival word stays 0."""
+    hosts = _batches(pkg, (4, 5, 6))
+    n_cap, e_cap, mgn, caps = pkg.graph.StaticBatch.capacities(hosts, 1, slack=1.02)
+    static = pkg.graph.StaticBatch(B, n_cap, e_cap, F_IN, mgn, caps, dev)
+    padded = [static.pad(gh) for gh in hosts]
+    pool = static.pool(padded)
+    for i in range(4):
+        static.load_next(pool)
+        torch.cuda.synchronize()
+        assert torch.equal(static.blob, padded[i % 3]["blob"])
+    graph = torch.cuda.CUDAGraph()
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        with torch.cuda.graph(graph):
+            static.load_next(pool)
+    torch.cuda.synchronize()
+    for i in range(4, 9):
+        graph.replay()
+        torch.cuda.synchronize()
+        assert torch.equal(static.blob, padded[i % 3]["blob"])
+    assert pool["cursor"].tolist() == [9, 0]

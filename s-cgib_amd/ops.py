@@ -650,14 +650,18 @@ class _Ctx:
 # A replayed graph may order a wait before its signal on the same queue, and
 # then only concurrent queues let the signal run: off where kernel dispatch is
 # serialised device-wide (PMC counter collection, AMD_SERIALIZE_KERNEL, launch
-# blocking) — there a wait would time out (counted, xq_timeouts) instead.
+# blocking) — there a wait would time out (counted, xq_timeouts) instead — and
+# under rocprofv3 kernel tracing, whose per-dispatch callbacks submit the
+# replay's nodes one queue after the other, so a wait holds its queue until
+# the other queue's submission catches up (a 0.74 ms traced step; the kernels
+# are the same either way, only the synchronisation packets differ).
 
 
 def _dispatch_serialised():
     env = os.environ
     return any(env.get(k, "0") not in ("", "0") for k in (
-        "ROCPROF_COUNTER_COLLECTION", "AMD_SERIALIZE_KERNEL", "HIP_LAUNCH_BLOCKING",
-        "CUDA_LAUNCH_BLOCKING"))
+        "ROCPROF_COUNTER_COLLECTION", "ROCPROF_KERNEL_TRACE", "AMD_SERIALIZE_KERNEL",
+        "HIP_LAUNCH_BLOCKING", "CUDA_LAUNCH_BLOCKING"))
 
 
 XQ_FLAGS = not _dispatch_serialised()

@@ -465,16 +465,17 @@ def test_bench_kernel_table_evaluates(pkg):
 
 def test_xq_handoffs_off_under_serialised_dispatch(pkg, monkeypatch):
     """ops.XQ_FLAGS's default: the signal / wait hand-offs need concurrent
-    queues, so they are off under PMC counter collection or serialised /
-    blocking launches (a replayed graph could order a wait before its signal
-    on one queue)."""
-    for k in ("ROCPROF_COUNTER_COLLECTION", "AMD_SERIALIZE_KERNEL", "HIP_LAUNCH_BLOCKING",
-              "CUDA_LAUNCH_BLOCKING"):
+    queues, so they are off under PMC counter collection, kernel tracing or
+    serialised / blocking launches (a replayed graph could order a wait before
+    its signal on one queue)."""
+    for k in ("ROCPROF_COUNTER_COLLECTION", "ROCPROF_KERNEL_TRACE", "AMD_SERIALIZE_KERNEL",
+              "HIP_LAUNCH_BLOCKING", "CUDA_LAUNCH_BLOCKING"):
         monkeypatch.delenv(k, raising=False)
     assert not pkg.ops._dispatch_serialised()
     monkeypatch.setenv("AMD_SERIALIZE_KERNEL", "0")
     assert not pkg.ops._dispatch_serialised()
-    for k in ("ROCPROF_COUNTER_COLLECTION", "AMD_SERIALIZE_KERNEL", "HIP_LAUNCH_BLOCKING"):
+    for k in ("ROCPROF_COUNTER_COLLECTION", "ROCPROF_KERNEL_TRACE", "AMD_SERIALIZE_KERNEL",
+              "HIP_LAUNCH_BLOCKING"):
         monkeypatch.setenv(k, "1")
         assert pkg.ops._dispatch_serialised()
         monkeypatch.delenv(k)

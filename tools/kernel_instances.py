@@ -1,5 +1,11 @@
 """Per-instance kernel durations from a rocprofv3 kernel trace (csv):
-python tools/kernel_instances.py gpurun_out/TAG/prof_kt [max_grid]
+python tools/kernel_instances.py gpurun_out/TAG/prof_kt [--split KERNEL]
+
+--split KERNEL: two tables, the dispatches up to the last KERNEL dispatch
+(the bench's replayed steps, which end in adam_step_k) and those after it
+(the bench's kernel-timer pass: forward + backward, unforked, no optimizer
+step) — the second is the set of launches the bench's HIP-event timer
+averages.
 
 Groups dispatches by full kernel name (template arguments kept) and grid
 size, so the bench's roofline kernel (e.g. gin_fwd_k<64, true, true, ...>
@@ -11,15 +17,32 @@ import glob
 import os
 import sys
 
-path = sys.argv[1]
+args = sys.argv[1:]
+split = None
+if "--split" in args:
+    i = args.index("--split")
+    split = args[i + 1]
+    del args[i:i + 2]
+path = args[0]
 files = glob.glob(os.path.join(path, "**", "*kernel_trace.csv"), recursive=True) if os.path.isdir(path) else [path]
-per = collections.defaultdict(list)
+rows = []
 for fn in files:
     for r in csv.DictReader(open(fn)):
         name = r["Kernel_Name"].split("(")[0].replace("void ", "").replace("scgib::", "").replace("pair::", "").strip()
-        per[(name, int(r["Grid_Size_X"]))].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
-print(f"{'kernel':60s} {'grid':>9s} {'calls':>6s} {'avg_us':>9s} {'min_us':>8s}")
-for (name, grid), ds in sorted(per.items(), key=lambda kv: -sum(kv[1])):
-    if len(ds) < 2 and sum(ds) < 50_000:
-        continue
-    print(f"{name[:60]:60s} {grid:9d} {len(ds):6d} {sum(ds) / len(ds) / 1e3:9.2f} {min(ds) / 1e3:8.2f}")
+        rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), name, int(r["Grid_Size_X"])))
+rows.sort()
+parts = [("all dispatches", rows)]
+if split:
+    last = max((i for i, r in enumerate(rows) if r[2].startswith(split)), default=-1)
+    parts = [(f"up to the last {split} (replayed steps)", rows[:last + 1]),
+             (f"after it (kernel-timer pass)", rows[last + 1:])]
+for title, part in parts:
+    per = collections.defaultdict(list)
+    for t0, t1, name, grid in part:
+        per[(name, grid)].append(t1 - t0)
+    print(f"== {title}")
+    print(f"{'kernel':60s} {'grid':>9s} {'calls':>6s} {'avg_us':>9s} {'min_us':>8s}")
+    for (name, grid), ds in sorted(per.items(), key=lambda kv: -sum(kv[1])):
+        if len(ds) < 2 and sum(ds) < 50_000:
+            continue
+        print(f"{name[:60]:60s} {grid:9d} {len(ds):6d} {sum(ds) / len(ds) / 1e3:9.2f} {min(ds) / 1e3:8.2f}")

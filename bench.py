@@ -579,6 +579,9 @@ def main():
                     help="skip the event-timed kernel pass (PMC runs: only real step launches)")
     ap.add_argument("--eager", action="store_true",
                     help="launch every kernel from Python (no HIP-graph capture)")
+    ap.add_argument("--no-ego-prefetch", action="store_true",
+                    help="build each step's ego-nets at the head of the step instead of one "
+                         "batch ahead (graph.EgoPrefetch; A/B)")
     ap.add_argument("--torch-adam", action="store_true",
                     help="torch's fused Adam instead of the one-launch scgib Adam")
     a = ap.parse_args()
@@ -655,15 +658,25 @@ def main():
 
         pool_dev = static.pool(padded)
         one = torch.ones((), dtype=torch.float32, device=dev)
+        # k = 1: each step builds the NEXT batch's ego-nets (on the encoder
+        # pair's queue during the loss section) and its batch load moves them
+        # in with the batch: the build leaves the head of the critical path
+        prefetch = None
+        if a.k == 1 and not a.no_ego_prefetch:
+            prefetch = pkg.graph.EgoPrefetch(static, pool_dev)
+            prefetch.prime()  # the first batch's, before the first load
 
         def body():
-            static.load_next(pool_dev)  # the pool's next batch into the static inputs
+            # the pool's next batch (and its prefetched ego-nets) into the static inputs
+            static.load_next(pool_dev, prefetch)
             _, kl, con, rec = model(static.graph, static.x, None, None, None, 1, None, a.k, dev,
                                     a.batch)
             # loss = KL + contrastive + recon (exp_pretraining.py:321): d loss / d part = 1,
             # so the parts are backpropagated directly with a resident ones scalar (no sum
             # kernels, no ones fill in the replayed step); the total is formed after timing
             torch.autograd.backward((kl, rec, con), (one, one, one))
+            if prefetch is not None:
+                prefetch.join()  # (no-op: the encoder pair's backward joined it)
             out = (kl.detach(), rec.detach(), con.detach())
             # detached aliases (the replays refresh their storage): the step's
             # autograd graph is not kept alive past the capture
@@ -812,6 +825,9 @@ def main():
             "config": {"workload": f"{a.workload} pretrain step GIN-64x{a.gin_layers} "
                                    f"k={a.k}, batch {a.batch}/GPU, Mainmodel_continue + Adam",
                        "launch": "eager" if a.eager else "hip-graph replay (capacity mode)",
+                       "ego_build": ("in the step, for the batch the next step loads "
+                                     "(graph.EgoPrefetch)" if not a.eager and a.k == 1
+                                     and not a.no_ego_prefetch else "at the head of the step"),
                        "allreduce": None if not collective else
                        ("eager" if a.eager else allreduce_mode),
                        "global_batch": world * a.batch, "nodes_per_batch": round(n_nodes, 1),

@@ -80,6 +80,11 @@ int scgib_abi_version(void);
  * and advances ctr[0].  ctr: two uint32, ctr[1] zero on entry (left zero). */
 int scgib_pool_copy(const uint64_t *srcs, int32_t n_src, uint32_t *ctr, void *dst, int64_t bytes,
                     scgib_stream_t stream);
+/* ... and, in the same launch, bytes2 (a multiple of 16) from src2 to dst2
+ * (graph.EgoPrefetch: the ego-nets built for this batch during the previous
+ * step, staging -> the step's ego buffers). */
+int scgib_pool_copy2(const uint64_t *srcs, int32_t n_src, uint32_t *ctr, void *dst, int64_t bytes,
+                     const void *src2, void *dst2, int64_t bytes2, scgib_stream_t stream);
 int scgib_stream_signal(uint32_t *words, scgib_stream_t stream);
 int scgib_stream_wait(uint32_t *words, scgib_stream_t stream);
 const char *scgib_strerror(int code);
@@ -443,6 +448,19 @@ int scgib_egonet_k1_build_onepass(const int32_t *rowptr, const int32_t *col, int
                                   uint32_t *scan_state, int32_t *ego_nodes, int32_t *sub_rowptr,
                                   int32_t *sub_col, int64_t n_ego_cap, const int32_t *dims,
                                   int32_t *ego_dims, scgib_stream_t stream);
+/* The one-launch k = 1 build over the resident pool's batch srcs[ctr[0] % n_src]
+ * (srcs, ctr as in scgib_pool_copy; rowptr / col / dims at byte offsets
+ * o_rowptr / o_col / o_dims of each pool blob, capacity mode), resolved on
+ * the device when the kernel starts: the ego-nets of the batch the next
+ * replayed step loads, built inside the current step (graph.EgoPrefetch;
+ * replaces the in-step dgl.khop_in_subgraph pass, exp_pretraining.py:269-272). */
+int scgib_egonet_k1_build_onepass_pool(const uint64_t *srcs, int32_t n_src, const uint32_t *ctr,
+                                       int64_t o_rowptr, int64_t o_col, int64_t o_dims,
+                                       int64_t n_nodes, int32_t max_in_degree, int32_t *ego_ptr,
+                                       int32_t *ego_eptr, uint32_t *scan_state,
+                                       int32_t *ego_nodes, int32_t *sub_rowptr, int32_t *sub_col,
+                                       int64_t n_ego_cap, int32_t *ego_dims,
+                                       scgib_stream_t stream);
 int scgib_egonet_fill(const int32_t *rowptr, const int32_t *col, const int32_t *graph_ptr,
                       int64_t n_graphs, int64_t n_nodes, int32_t k, int32_t max_graph_nodes,
                       const int32_t *ego_ptr, const int32_t *ego_eptr, int32_t *ego_nodes,

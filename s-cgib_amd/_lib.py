@@ -20,6 +20,7 @@ SIGNATURES = {
     "scgib_abi_version": (ctypes.c_int, []),
     "scgib_set_recon_fold": (ctypes.c_int, [ctypes.c_int]),
     "scgib_pool_copy": (ctypes.c_int, [_P, _I32, _P, _P, _I64, _P]),
+    "scgib_pool_copy2": (ctypes.c_int, [_P, _I32, _P, _P, _I64, _P, _P, _I64, _P]),
     "scgib_stream_signal": (ctypes.c_int, [_P, _P]),
     "scgib_stream_wait": (ctypes.c_int, [_P, _P]),
     "scgib_strerror": (ctypes.c_char_p, [ctypes.c_int]),
@@ -36,6 +37,9 @@ SIGNATURES = {
     "scgib_egonet_k1_build_deg": (ctypes.c_int, [_P, _P, _I64, _I32, _P, _P, _P, _P, _P, _P, _I64,
                                                  _P, _P, _P]),
     "scgib_egonet_k1_scan_words": (_I64, [_I64]),
+    "scgib_egonet_k1_build_onepass_pool": (ctypes.c_int, [_P, _I32, _P, _I64, _I64, _I64, _I64,
+                                                           _I32, _P, _P, _P, _P, _P, _P, _I64,
+                                                           _P, _P]),
     "scgib_egonet_k1_build_onepass": (ctypes.c_int, [_P, _P, _I64, _I32, _P, _P, _P, _P, _P, _P,
                                                      _I64, _P, _P, _P]),
     "scgib_egonet_fill": (ctypes.c_int, [_P, _P, _P, _I64, _I64, _I32, _I32, _P, _P, _P, _P, _P,
@@ -229,7 +233,7 @@ class PairBwdArgs(ctypes.Structure):
                 ("trace", ctypes.c_void_p)]
 
 
-ABI_VERSION = 10
+ABI_VERSION = 11
 STATS_STRIDE = 260
 PGRAD_STRIDE = 324
 HIDDEN = 64

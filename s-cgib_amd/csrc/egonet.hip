@@ -565,9 +565,18 @@ __global__ __launch_bounds__(kK1One) void egonet_k1_onepass_k(
     int32_t *__restrict__ ego_ptr, int32_t *__restrict__ ego_eptr, uint64_t *__restrict__ state,
     uint32_t *__restrict__ done, int32_t *__restrict__ ego_nodes,
     int32_t *__restrict__ sub_rowptr, int32_t *__restrict__ sub_col, int64_t n_ego_cap,
-    const int32_t *__restrict__ dims, int32_t *__restrict__ ego_dims) {
+    const int32_t *__restrict__ dims, int32_t *__restrict__ ego_dims,
+    const uint64_t *__restrict__ srcs, int32_t n_src, const unsigned *ctr, int64_t o_rowptr,
+    int64_t o_col, int64_t o_dims) {
     const int nblk = gridDim.x, tid = threadIdx.x;
     int blk = blockIdx.x;
+    if (srcs) {  // pool form: the input batch is srcs[ctr[0] % n_src] (its CSR and dims sections)
+        const unsigned c = __hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const char *base = reinterpret_cast<const char *>(srcs[c % static_cast<unsigned>(n_src)]);
+        rowptr = reinterpret_cast<const int32_t *>(base + o_rowptr);
+        col = reinterpret_cast<const int32_t *>(base + o_col);
+        dims = reinterpret_cast<const int32_t *>(base + o_dims);
+    }
     SCGIB_MARK(0);
     SCGIB_MARK_HWID();
     if (nblk > kK1Resident) {  // block-uniform: the logical index from the ticket
@@ -880,15 +889,15 @@ extern "C" int64_t scgib_egonet_k1_scan_words(int64_t n_nodes) {
     return 2 * ((n_nodes + kK1Block - 1) / kK1Block) + 4;
 }
 
-extern "C" int scgib_egonet_k1_build_onepass(const int32_t *rowptr, const int32_t *col,
-                                             int64_t n_nodes, int32_t max_in_degree,
-                                             int32_t *ego_ptr, int32_t *ego_eptr,
-                                             uint32_t *scan_state, int32_t *ego_nodes,
-                                             int32_t *sub_rowptr, int32_t *sub_col,
-                                             int64_t n_ego_cap, const int32_t *dims,
-                                             int32_t *ego_dims, scgib_stream_t stream) {
-    if (n_nodes <= 0 || !rowptr || !col || !ego_ptr || !ego_eptr || !scan_state || !ego_nodes ||
-        !sub_rowptr || !sub_col || max_in_degree < 0)
+static int k1_onepass_launch(const int32_t *rowptr, const int32_t *col, int64_t n_nodes,
+                             int32_t max_in_degree, int32_t *ego_ptr, int32_t *ego_eptr,
+                             uint32_t *scan_state, int32_t *ego_nodes, int32_t *sub_rowptr,
+                             int32_t *sub_col, int64_t n_ego_cap, const int32_t *dims,
+                             int32_t *ego_dims, const uint64_t *srcs, int32_t n_src,
+                             const uint32_t *ctr, int64_t o_rowptr, int64_t o_col, int64_t o_dims,
+                             scgib_stream_t stream) {
+    if (n_nodes <= 0 || !ego_ptr || !ego_eptr || !scan_state || !ego_nodes || !sub_rowptr ||
+        !sub_col || max_in_degree < 0)
         return SCGIB_EINVAL;
     if (n_nodes >= (int64_t(1) << 31) || max_in_degree > 12) return SCGIB_EUNSUPPORTED;
     if (reinterpret_cast<uintptr_t>(scan_state) % 4) return SCGIB_EINVAL;
@@ -897,20 +906,47 @@ extern "C" int scgib_egonet_k1_build_onepass(const int32_t *rowptr, const int32_
     uint64_t *state = reinterpret_cast<uint64_t *>(
         (reinterpret_cast<uintptr_t>(scan_state) + 2 * sizeof(uint32_t) + 7) & ~uintptr_t(7));
     hipStream_t st = as_stream(stream);
-    if (max_in_degree <= 6)
-        egonet_k1_onepass_k<6><<<nblk, kK1One, 0, st>>>(rowptr, col, n_nodes, ego_ptr, ego_eptr,
-                                                          state, done, ego_nodes, sub_rowptr,
-                                                          sub_col, n_ego_cap, dims, ego_dims);
-    else if (max_in_degree <= 8)
-        egonet_k1_onepass_k<8><<<nblk, kK1One, 0, st>>>(rowptr, col, n_nodes, ego_ptr, ego_eptr,
-                                                          state, done, ego_nodes, sub_rowptr,
-                                                          sub_col, n_ego_cap, dims, ego_dims);
-    else
-        egonet_k1_onepass_k<12><<<nblk, kK1One, 0, st>>>(rowptr, col, n_nodes, ego_ptr,
-                                                           ego_eptr, state, done, ego_nodes,
-                                                           sub_rowptr, sub_col, n_ego_cap, dims,
-                                                           ego_dims);
+    const unsigned *c = reinterpret_cast<const unsigned *>(ctr);
+#define SCGIB_K1_ONEPASS(DD)                                                                     \
+    egonet_k1_onepass_k<DD><<<nblk, kK1One, 0, st>>>(rowptr, col, n_nodes, ego_ptr, ego_eptr,   \
+                                                     state, done, ego_nodes, sub_rowptr, sub_col, \
+                                                     n_ego_cap, dims, ego_dims, srcs, n_src, c,   \
+                                                     o_rowptr, o_col, o_dims)
+    if (max_in_degree <= 6) SCGIB_K1_ONEPASS(6);
+    else if (max_in_degree <= 8) SCGIB_K1_ONEPASS(8);
+    else SCGIB_K1_ONEPASS(12);
+#undef SCGIB_K1_ONEPASS
     return launch_status();
+}
+
+extern "C" int scgib_egonet_k1_build_onepass(const int32_t *rowptr, const int32_t *col,
+                                             int64_t n_nodes, int32_t max_in_degree,
+                                             int32_t *ego_ptr, int32_t *ego_eptr,
+                                             uint32_t *scan_state, int32_t *ego_nodes,
+                                             int32_t *sub_rowptr, int32_t *sub_col,
+                                             int64_t n_ego_cap, const int32_t *dims,
+                                             int32_t *ego_dims, scgib_stream_t stream) {
+    if (!rowptr || !col) return SCGIB_EINVAL;
+    return k1_onepass_launch(rowptr, col, n_nodes, max_in_degree, ego_ptr, ego_eptr, scan_state,
+                             ego_nodes, sub_rowptr, sub_col, n_ego_cap, dims, ego_dims, nullptr,
+                             0, nullptr, 0, 0, 0, stream);
+}
+
+// The same build over a resident pool's batch srcs[ctr[0] % n_src] (a
+// graph.StaticBatch blob: rowptr / col / dims at the given byte offsets),
+// resolved on the device at launch: a replayed step builds the ego-nets of the
+// batch the next step will load (graph.EgoPrefetch) with no host work.
+extern "C" int scgib_egonet_k1_build_onepass_pool(
+    const uint64_t *srcs, int32_t n_src, const uint32_t *ctr, int64_t o_rowptr, int64_t o_col,
+    int64_t o_dims, int64_t n_nodes, int32_t max_in_degree, int32_t *ego_ptr, int32_t *ego_eptr,
+    uint32_t *scan_state, int32_t *ego_nodes, int32_t *sub_rowptr, int32_t *sub_col,
+    int64_t n_ego_cap, int32_t *ego_dims, scgib_stream_t stream) {
+    if (!srcs || n_src < 1 || !ctr || o_rowptr < 0 || o_col < 0 || o_dims < 0 ||
+        (o_rowptr | o_col | o_dims) % 4)
+        return SCGIB_EINVAL;
+    return k1_onepass_launch(nullptr, nullptr, n_nodes, max_in_degree, ego_ptr, ego_eptr,
+                             scan_state, ego_nodes, sub_rowptr, sub_col, n_ego_cap, nullptr,
+                             ego_dims, srcs, n_src, ctr, o_rowptr, o_col, o_dims, stream);
 }
 
 extern "C" int scgib_egonet_k1_build(const int32_t *rowptr, const int32_t *col, int64_t n_nodes,

@@ -189,19 +189,25 @@ __global__ void stream_wait_k(unsigned *w) {
 
 // One batch of a resident pool into a step's static input buffer from inside
 // a replayed graph (graph.StaticBatch.load_next): srcs is a device table of
-// n_src pointers; the launch copies srcs[ctr[0] % n_src] to dst, then the last
-// workgroup advances ctr[0] (ctr[1]: its arrival counter, left zero), so the
-// replays walk the pool with no host work between them.
+// n_src pointers; the launch copies srcs[ctr[0] % n_src] to dst (n16 16-byte
+// words) and, in the same grid, src2 to dst2 (n16b words: the prefetched
+// ego-nets, graph.EgoPrefetch), then the last workgroup advances ctr[0] (ctr[1]:
+// its arrival counter, left zero), so the replays walk the pool with no host
+// work between them.
 __global__ void pool_copy_k(const uint64_t *__restrict__ srcs, int32_t n_src, unsigned *ctr,
-                            float4 *__restrict__ dst, int64_t n16) {
+                            float4 *__restrict__ dst, int64_t n16, const float4 *__restrict__ src2,
+                            float4 *__restrict__ dst2, int64_t n16b) {
     __shared__ unsigned s_c;
     if (threadIdx.x == 0) s_c = __hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __syncthreads();
     const unsigned c = s_c;
     const float4 *src = reinterpret_cast<const float4 *>(srcs[c % static_cast<unsigned>(n_src)]);
     const int64_t stride = static_cast<int64_t>(gridDim.x) * 256;
-    for (int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x; i < n16; i += stride)
-        dst[i] = src[i];
+    for (int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x; i < n16 + n16b;
+         i += stride) {
+        if (i < n16) dst[i] = src[i];
+        else dst2[i - n16] = src2[i - n16];
+    }
     if (block_arrive(ctr + 1, gridDim.x) && threadIdx.x == 0) {
         __hip_atomic_store(ctr + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(ctr, c + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -277,17 +283,26 @@ extern "C" int scgib_stream_wait(uint32_t *words, scgib_stream_t stream) {
     return launch_status();
 }
 
-extern "C" int scgib_pool_copy(const uint64_t *srcs, int32_t n_src, uint32_t *ctr, void *dst,
-                               int64_t bytes, scgib_stream_t stream) {
-    if (!srcs || n_src < 1 || !ctr || !dst || bytes < 0 || bytes % 16) return SCGIB_EINVAL;
-    const int64_t n16 = bytes / 16;
-    const int64_t grid = std::max<int64_t>(1, std::min<int64_t>((n16 + 255) / 256, 1024));
+extern "C" int scgib_pool_copy2(const uint64_t *srcs, int32_t n_src, uint32_t *ctr, void *dst,
+                                int64_t bytes, const void *src2, void *dst2, int64_t bytes2,
+                                scgib_stream_t stream) {
+    if (!srcs || n_src < 1 || !ctr || !dst || bytes < 0 || bytes % 16 || bytes2 < 0 ||
+        bytes2 % 16 || (bytes2 > 0 && (!src2 || !dst2)))
+        return SCGIB_EINVAL;
+    const int64_t n16 = bytes / 16, n16b = bytes2 / 16;
+    const int64_t grid = std::max<int64_t>(1, std::min<int64_t>((n16 + n16b + 255) / 256, 1024));
     pool_copy_k<<<(unsigned)grid, 256, 0, as_stream(stream)>>>(
-        srcs, n_src, reinterpret_cast<unsigned *>(ctr), reinterpret_cast<float4 *>(dst), n16);
+        srcs, n_src, reinterpret_cast<unsigned *>(ctr), reinterpret_cast<float4 *>(dst), n16,
+        reinterpret_cast<const float4 *>(src2), reinterpret_cast<float4 *>(dst2), n16b);
     return launch_status();
 }
 
-extern "C" int scgib_abi_version(void) { return 10; }
+extern "C" int scgib_pool_copy(const uint64_t *srcs, int32_t n_src, uint32_t *ctr, void *dst,
+                               int64_t bytes, scgib_stream_t stream) {
+    return scgib_pool_copy2(srcs, n_src, ctr, dst, bytes, nullptr, nullptr, 0, stream);
+}
+
+extern "C" int scgib_abi_version(void) { return 11; }
 
 extern "C" const char *scgib_strerror(int code) {
     if (code == SCGIB_OK) return "ok";

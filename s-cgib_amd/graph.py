@@ -606,6 +606,12 @@ class StaticBatch:
     def load(self, padded):
         """Copy a pad()-ed batch into the static buffers (one device copy)."""
         self.blob.copy_(padded["blob"], non_blocking=True)
+        self._unload_prefetch()
+
+    def _unload_prefetch(self):
+        pf = getattr(self.graph, "ego_prefetch", None)
+        if pf is not None:
+            pf.loaded = False  # its ego buffers no longer match the static batch
 
     def pool(self, padded):
         """Device state for load_next over the pad()-ed batches ``padded``: the
@@ -619,17 +625,115 @@ class StaticBatch:
         return {"table": table, "cursor": torch.zeros(2, dtype=torch.int32, device=dev),
                 "n": len(padded), "batches": padded}
 
-    def load_next(self, pool):
+    def load_next(self, pool, prefetch=None):
         """Copy the pool's next batch in (one kernel, capturable: the replays of
-        a graph holding it walk the pool in order, pool(...)[cursor] first)."""
-        _lib.call("scgib_pool_copy", ctypes.c_void_p(pool["table"].data_ptr()), pool["n"],
+        a graph holding it walk the pool in order, pool(...)[cursor] first).
+        With an EgoPrefetch the same launch also moves the ego-nets it built
+        for this batch into the step's ego buffers."""
+        src2 = dst2 = None
+        n2 = 0
+        self._unload_prefetch()
+        if prefetch is not None:
+            if prefetch.pool is not pool:
+                raise _lib.ScgibError("EgoPrefetch was made for another pool")
+            src2, dst2, n2 = _ptr(prefetch.staging), _ptr(prefetch.blob), prefetch.blob.numel()
+            prefetch.loaded = True
+        _lib.call("scgib_pool_copy2", ctypes.c_void_p(pool["table"].data_ptr()), pool["n"],
                   ctypes.c_void_p(pool["cursor"].data_ptr()), ctypes.c_void_p(self.blob.data_ptr()),
-                  self.blob.numel(), ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
+                  self.blob.numel(), src2, dst2, n2,
+                  ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
+
+    def blob_offsets(self):
+        """Byte offsets of (rowptr, col, dims) inside each blob."""
+        o = self._layout()
+        return o[0], o[1], o[3]
 
     def ego_error(self):
         """Error bits the ego-net build of the last step flagged (0 = none; see
         egonet_batch) — a device read, for checks outside the timed loop."""
         return int(self.err.item())
+
+
+class EgoPrefetch:
+    """The k = 1 ego-nets one batch ahead, for a replayed step over a
+    StaticBatch pool (bench.py): step t builds the ego-nets of the batch step
+    t + 1 will load — straight from that batch's pool blob, on the encoder
+    pair's queue while it would otherwise idle through the loss section
+    (models._encode_forked) — into a staging blob, and step t + 1's batch load
+    (StaticBatch.load_next) moves them into the ego buffers the step reads.
+    Every step still builds one batch's ego-nets (the reference's
+    khop_in_subgraph pass, exp_pretraining.py:269-272); the build leaves the
+    head of the step's critical path.
+
+    ``prime()`` builds the ego-nets of the pool's current batch once before
+    the first step (eager).  ``ego`` is the step's ego batch (capacity mode,
+    the same layout egonet_batch gives)."""
+
+    def __init__(self, static, pool):
+        g = static.graph
+        caps = g.ego_caps or ()
+        kmax = int(_lib.query("scgib_egonet_k1_max_degree"))
+        if static.k != 1 or len(caps) < 3 or caps[2] > kmax or \
+                g.max_graph_nodes > int(_lib.query("scgib_egonet_k1_max_graph_nodes")):
+            raise _lib.ScgibError("EgoPrefetch needs k = 1 within the one-pass builder's bounds")
+        self.static, self.pool, self.k = static, pool, 1
+        self.n = g.num_nodes()
+        self.n_s, self.e_cap, self.dmax = int(caps[0]), int(caps[1]), int(caps[2])
+        dev = static.blob.device
+        sizes = [4 * (self.n + 1), 4 * (self.n + 1), 4 * max(self.n_s, 1), 4 * (self.n_s + 1),
+                 4 * max(self.e_cap, 1), 8]
+        offs = [0]
+        for sz in sizes:
+            offs.append(offs[-1] + (sz + 255) // 256 * 256)
+        self._offs, self._sizes = offs, sizes
+        self.blob = torch.zeros(offs[-1], dtype=torch.uint8, device=dev)
+        self.staging = torch.zeros(offs[-1], dtype=torch.uint8, device=dev)
+        self.views = self._views(self.blob)
+        self.next_views = self._views(self.staging)
+        ego_ptr, _, ego_nodes, sub_rowptr, sub_col, ego_dims = self.views
+        self.ego = _ego_graph(g, sub_rowptr, sub_col, ego_ptr, ego_nodes, self.n_s, ego_dims)
+        self.loaded = False  # ego holds the static batch's ego-nets (load_next with this)
+        self._side = None  # stream of a prefetch not yet joined back (join())
+        g.ego_prefetch = self  # models._encode_forked takes ego from here when loaded
+
+    def _views(self, blob):
+        i32 = torch.int32
+        return tuple(blob[o:o + sz].view(i32) for o, sz in zip(self._offs, self._sizes))
+
+    def prefetch(self):
+        """Enqueue (current stream) the build of the ego-nets of the pool's
+        batch at the cursor — the one the next load_next copies in — into the
+        staging blob."""
+        from . import ops  # (ops imports this module)
+        ego_ptr, ego_eptr, ego_nodes, sub_rowptr, sub_col, ego_dims = self.next_views
+        state = ops.scan_state(self.blob.device, "egonet_k1_scan_prefetch",
+                               int(_lib.query("scgib_egonet_k1_scan_words", self.n)))
+        o_rp, o_col, o_dims = self.static.blob_offsets()
+        _lib.call("scgib_egonet_k1_build_onepass_pool", _ptr(self.pool["table"]), self.pool["n"],
+                  _ptr(self.pool["cursor"]), o_rp, o_col, o_dims, self.n, self.dmax, _ptr(ego_ptr),
+                  _ptr(ego_eptr), _ptr(state), _ptr(ego_nodes), _ptr(sub_rowptr), _ptr(sub_col),
+                  self.n_s, _ptr(ego_dims), _stream())
+
+    def prime(self):
+        """The ego-nets of the pool's batch at the cursor into staging, before
+        the first load_next (eager, current stream)."""
+        self.prefetch()
+
+    def __call__(self):
+        """The encoder pair's side tail: prefetch on the current stream, which
+        the pair's backward joins back (joined()) — else join() does."""
+        self.prefetch()
+        self._side = torch.cuda.current_stream()
+
+    def joined(self):
+        self._side = None
+
+    def join(self):
+        """Order the current stream after a prefetch that no backward joined
+        (e.g. a forward without backward); no-op otherwise."""
+        if self._side is not None:
+            torch.cuda.current_stream().wait_stream(self._side)
+            self._side = None
 
 
 # ---------------------------------------------------------------------------

@@ -280,8 +280,14 @@ class _SCGIBCore(nn.Module):
             # one autograd node for both encoders (ops._GinEncoderPair): the
             # ego chain is enqueued first on ``side`` in forward AND backward
             # (fork off: side is the current stream, the chains run in turn)
+            # graph.EgoPrefetch: this batch's ego-nets were built during the
+            # previous step; the next batch's are built on ``side`` after the
+            # ego chain (its idle stretch through the loss section)
+            pf = getattr(batch_g, "ego_prefetch", None)
+            if pf is not None and not (pf.loaded and pf.k == self.k_transition):
+                pf = None
             with torch.cuda.stream(side):
-                ego = G.egonet_batch(batch_g, self.k_transition)
+                ego = pf.ego if pf is not None else G.egonet_batch(batch_g, self.k_transition)
             lin0 = enc_owner.compressor[0] if LIN_IN_PAIR else None
             drawn = {}
             tail = None
@@ -290,7 +296,7 @@ class _SCGIBCore(nn.Module):
                     drawn["u"] = ops.device_noise(batch_g.num_nodes(), batch_x.device)
             outs = ops.gin_encoder_pair_x(
                 batch_x, ego, enc_owner.Encoder2, batch_g, enc_owner.Encoder1, self.transfer_d,
-                ego.ndata["_ID"], side, lin0, tail)
+                ego.ndata["_ID"], side, lin0, tail, pf)
             subgraphs_features, sub_readout, graph_features = outs[0], outs[1], outs[2]
             t = outs[3] if len(outs) > 3 else None
             return ego, (graph_features, subgraphs_features, sub_readout, t, drawn.get("u"))

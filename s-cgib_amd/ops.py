@@ -700,9 +700,11 @@ class _GinEncoderPair(torch.autograd.Function):
     overlap in both directions; d Wt = d Wt(ego) + d Wt(core)."""
 
     @staticmethod
-    def forward(ctx, x, wt, w0, b0, nmap, ego, core, gin_ego, gin_core, training, side, core_tail,
+    def forward(ctx, x, wt, w0, b0, nmap, ego, core, gin_ego, gin_core, training, side, tails,
                 *params):
         main = _torch_stream()
+        core_tail, side_tail = tails
+        ctx.side_tail = side_tail
         ne = 6 * len(gin_ego.ginlayers)
         ctx.set_materialize_grads(False)  # unused outputs (e.g. s) get no zero-fill launch
         # the loss-section reduces of this step are deferred into this node's
@@ -722,6 +724,9 @@ class _GinEncoderPair(torch.autograd.Function):
                 core_tail()
             main.wait_stream(side)
             ctx.persistent = True
+            if side_tail is not None:  # joined by its owner (EgoPrefetch.join)
+                with torch.cuda.stream(side):
+                    side_tail()
             return _pair_forward_persistent(ctx, x, wt, w0, b0, nmap, ego, core, gin_ego,
                                             gin_core, params)
         ctx.persistent = False
@@ -756,6 +761,11 @@ class _GinEncoderPair(torch.autograd.Function):
             _xq_handoff(side, main, "pair_fwd")
         else:
             main.wait_stream(side)
+        if side_tail is not None:
+            # after the hand-off: ``side`` idles through the loss section; the
+            # backward's core chain follows it there and joins main at its end
+            with torch.cuda.stream(side):
+                side_tail()
         s.record_stream(main)
         ro.record_stream(main)
         return outs
@@ -821,6 +831,8 @@ class _GinEncoderPair(torch.autograd.Function):
                 ctx.sub[1].extra_jobs = (jobs, keep)
             gc = _drain(_GinEncoder.backward_steps(ctx.sub[1], g_f))
         main.wait_stream(side)
+        if ctx.side_tail is not None and hasattr(ctx.side_tail, "joined"):
+            ctx.side_tail.joined()  # ordered before main's later work by the join above
         held = None  # after the join: main-stream reuse is ordered after side's reads
         for g in (*gc, dw0, db0):
             if isinstance(g, torch.Tensor):
@@ -1090,7 +1102,7 @@ def _pair_forward_persistent(ctx, x, wt, w0, b0, nmap, ego, core, gin_ego, gin_c
 
 
 def gin_encoder_pair_x(x, ego, gin_ego, core, gin_core, transfer, node_map, side, lin0=None,
-                       core_tail=None):
+                       core_tail=None, side_tail=None):
     """(s, sum_nodes(ego, s), f) with s = gin_ego(ego, transfer(x[node_map])) and
     f = gin_core(core, transfer(x)) — the two encoders of Mainmodel.forward
     with transfer_d folded, and the ego-net readout fused into Encoder2's last
@@ -1098,7 +1110,10 @@ def gin_encoder_pair_x(x, ego, gin_ego, core, gin_core, transfer, node_map, side
     compressor's Linear(64, 64), models.py:596) also returns
     t = lin0(gin_core(...)), computed at the end of the core chain;
     ``core_tail()`` (non-differentiable, e.g. the noise draw) runs first on
-    the core chain, beside the ego-net build."""
+    the core chain, beside the ego-net build; ``side_tail()`` (e.g.
+    graph.EgoPrefetch: the next batch's ego-net build) runs on ``side`` after
+    the ego chain's hand-off, and its ``joined()`` is called once the
+    backward has joined ``side`` back."""
     if ego.num_nodes() == 0 or core.num_nodes() == 0:
         raise _lib.ScgibError("gin_encoder on an empty graph")
     if transfer.bias is not None or transfer.weight.shape != (32, x.shape[1]) \
@@ -1110,7 +1125,8 @@ def gin_encoder_pair_x(x, ego, gin_ego, core, gin_core, transfer, node_map, side
         raise _lib.ScgibError("gin_encoder_pair_x: encoders in different train/eval modes")
     w0, b0 = (lin0.weight, lin0.bias) if lin0 is not None else (None, None)
     return _GinEncoderPair.apply(x, transfer.weight, w0, b0, node_map, ego, core, gin_ego,
-                                 gin_core, bool(gin_core.training), side, core_tail,
+                                 gin_core, bool(gin_core.training), side,
+                                 (core_tail, side_tail),
                                  *_gin_layer_params(gin_ego), *_gin_layer_params(gin_core))
 
 

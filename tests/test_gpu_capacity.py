@@ -298,3 +298,73 @@ def test_pool_load_next_walks_the_pool(pkg, dev):
         torch.cuda.synchronize()
         assert torch.equal(static.blob, padded[i % 3]["blob"])
     assert pool["cursor"].tolist() == [9, 0]
+
+
+def test_ego_prefetch_replay_bitwise(pkg, dev):
+    """graph.EgoPrefetch (bench.py's step): each replayed step builds the ego-nets
+    of the batch the next step loads (pool-indirect one-pass builder, on the
+    encoder pair's side stream) and the next load_next moves them in.  Against
+    the same step building its own ego-nets at its head: the same losses,
+    gradients and BN running statistics bit for bit over the pool, and the
+    moved-in ego buffers equal an eager egonet_batch of the loaded batch."""
+    hosts = _batches(pkg, (4, 5, 6, 7))
+    n_cap, e_cap, mgn, caps = pkg.graph.StaticBatch.capacities(hosts, 1, slack=1.02)
+    ug, uf = _noise(n_cap, dev, 300)
+    runs = {}
+    for mode in (False, True):
+        static = pkg.graph.StaticBatch(B, n_cap, e_cap, F_IN, mgn, caps, dev)
+        padded = [static.pad(gh) for gh in hosts]
+        pool = static.pool(padded)
+        pf = pkg.graph.EgoPrefetch(static, pool) if mode else None
+        model = _model(pkg, dev)
+
+        def body():
+            static.load_next(pool, pf)
+            _, kl, con, rec = model(static.graph, static.x, None, None, None, 1, None, 1, dev,
+                                    B, noise=(ug, uf))
+            (kl + rec + con).backward()
+            if pf is not None:
+                pf.join()
+            return torch.stack([kl, con, rec]).detach()
+
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            if pf is not None:
+                pf.prime()
+            for _ in range(2):  # eager steps (allocator warm-up), batches 0, 1
+                model.zero_grad(set_to_none=False)
+                body()
+        torch.cuda.current_stream().wait_stream(side)
+        graph = torch.cuda.CUDAGraph()
+        model.zero_grad(set_to_none=False)
+        with torch.cuda.graph(graph):
+            out = body()
+        got = []
+        for i in range(6):  # batches 2, 3, 0, 1, 2, 3
+            for p in model.parameters():
+                if p.grad is not None:
+                    p.grad.zero_()
+            graph.replay()
+            torch.cuda.synchronize()
+            grads = [p.grad.clone() for p in model.parameters() if p.grad is not None]
+            bufs = [b.clone() for n, b in model.named_buffers() if "running" in n]
+            got.append((out.clone(), grads, bufs))
+            if pf is not None:
+                ref = pkg.graph.egonet_batch(static.graph, 1)
+                torch.cuda.synchronize()
+                n_s = int(ref.dims[0])
+                e_s = int(ref.dims[1])
+                assert torch.equal(pf.ego.dims, ref.dims)
+                assert torch.equal(pf.ego.graph_ptr, ref.graph_ptr)
+                assert torch.equal(pf.ego.ndata["_ID"][:n_s], ref.ndata["_ID"][:n_s])
+                assert torch.equal(pf.ego.rowptr[: n_s + 1], ref.rowptr[: n_s + 1])
+                assert torch.equal(pf.ego.col[:e_s], ref.col[:e_s])
+        assert pkg.ops.xq_timeouts(dev) == 0
+        runs[mode] = got
+    for (la, ga, ba), (lb, gb, bb) in zip(runs[False], runs[True]):
+        assert torch.isfinite(la).all()
+        assert torch.equal(la, lb)
+        assert len(ga) == len(gb) > 0
+        assert all(torch.equal(x, y) for x, y in zip(ga, gb))
+        assert all(torch.equal(x, y) for x, y in zip(ba, bb))

@@ -5,7 +5,11 @@ import sys
 
 rows = list(csv.DictReader(open(sys.argv[1])))
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-starts = [i for i, r in enumerate(rows) if "egonet_" in r["Kernel_Name"] and ("count_k" in r["Kernel_Name"] or "onepass_k" in r["Kernel_Name"])]
+# a step starts with its batch load (pool_copy_k) when the bench loads in-graph,
+# else with its ego-net build
+starts = [i for i, r in enumerate(rows) if "pool_copy_k" in r["Kernel_Name"]]
+if len(starts) < 3:
+    starts = [i for i, r in enumerate(rows) if "egonet_" in r["Kernel_Name"] and ("count_k" in r["Kernel_Name"] or "onepass_k" in r["Kernel_Name"])]
 k = int(sys.argv[2]) if len(sys.argv) > 2 else len(starts) // 2
 i0, i1 = starts[k], starts[k + 1]
 t0 = int(rows[i0]["Start_Timestamp"])

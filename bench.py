@@ -658,11 +658,11 @@ def main():
 
         pool_dev = static.pool(padded)
         one = torch.ones((), dtype=torch.float32, device=dev)
-        # k = 1: each step builds the NEXT batch's ego-nets (on the encoder
+        # each step builds the NEXT batch's ego-nets (on the encoder
         # pair's queue during the loss section) and its batch load moves them
         # in with the batch: the build leaves the head of the critical path
         prefetch = None
-        if a.k == 1 and not a.no_ego_prefetch:
+        if not a.no_ego_prefetch:
             prefetch = pkg.graph.EgoPrefetch(static, pool_dev)
             prefetch.prime()  # the first batch's, before the first load
 
@@ -826,7 +826,7 @@ def main():
                                    f"k={a.k}, batch {a.batch}/GPU, Mainmodel_continue + Adam",
                        "launch": "eager" if a.eager else "hip-graph replay (capacity mode)",
                        "ego_build": ("in the step, for the batch the next step loads "
-                                     "(graph.EgoPrefetch)" if not a.eager and a.k == 1
+                                     "(graph.EgoPrefetch)" if not a.eager
                                      and not a.no_ego_prefetch else "at the head of the step"),
                        "allreduce": None if not collective else
                        ("eager" if a.eager else allreduce_mode),

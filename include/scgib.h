@@ -448,6 +448,21 @@ int scgib_egonet_k1_build_onepass(const int32_t *rowptr, const int32_t *col, int
                                   uint32_t *scan_state, int32_t *ego_nodes, int32_t *sub_rowptr,
                                   int32_t *sub_col, int64_t n_ego_cap, const int32_t *dims,
                                   int32_t *ego_dims, scgib_stream_t stream);
+/* scgib_egonet_count / scgib_egonet_fill (any k) over the resident pool's
+ * batch srcs[ctr[0] % n_src] (rowptr / col / graph_ptr / dims at byte offsets
+ * of each graph.StaticBatch blob, capacity mode; n_nodes = the capacity),
+ * resolved on the device when each kernel starts (graph.EgoPrefetch, k >= 2). */
+int scgib_egonet_count_pool(const uint64_t *srcs, int32_t n_src, const uint32_t *ctr,
+                            int64_t o_rowptr, int64_t o_col, int64_t o_gptr, int64_t o_dims,
+                            int64_t n_graphs, int64_t n_nodes, int32_t k, int32_t max_graph_nodes,
+                            int32_t *ego_ptr, int32_t *ego_eptr, void *workspace, int32_t *err,
+                            scgib_stream_t stream);
+int scgib_egonet_fill_pool(const uint64_t *srcs, int32_t n_src, const uint32_t *ctr,
+                           int64_t o_rowptr, int64_t o_col, int64_t o_gptr, int64_t o_dims,
+                           int64_t n_graphs, int64_t n_nodes, int32_t k, int32_t max_graph_nodes,
+                           const int32_t *ego_ptr, const int32_t *ego_eptr, int32_t *ego_nodes,
+                           int32_t *sub_rowptr, int32_t *sub_col, int32_t *err,
+                           int64_t n_ego_cap, int32_t *ego_dims, scgib_stream_t stream);
 /* The one-launch k = 1 build over the resident pool's batch srcs[ctr[0] % n_src]
  * (srcs, ctr as in scgib_pool_copy; rowptr / col / dims at byte offsets
  * o_rowptr / o_col / o_dims of each pool blob, capacity mode), resolved on

@@ -37,6 +37,10 @@ SIGNATURES = {
     "scgib_egonet_k1_build_deg": (ctypes.c_int, [_P, _P, _I64, _I32, _P, _P, _P, _P, _P, _P, _I64,
                                                  _P, _P, _P]),
     "scgib_egonet_k1_scan_words": (_I64, [_I64]),
+    "scgib_egonet_count_pool": (ctypes.c_int, [_P, _I32, _P, _I64, _I64, _I64, _I64, _I64, _I64,
+                                               _I32, _I32, _P, _P, _P, _P, _P]),
+    "scgib_egonet_fill_pool": (ctypes.c_int, [_P, _I32, _P, _I64, _I64, _I64, _I64, _I64, _I64,
+                                              _I32, _I32, _P, _P, _P, _P, _P, _P, _I64, _P, _P]),
     "scgib_egonet_k1_build_onepass_pool": (ctypes.c_int, [_P, _I32, _P, _I64, _I64, _I64, _I64,
                                                            _I32, _P, _P, _P, _P, _P, _P, _I64,
                                                            _P, _P]),
@@ -233,7 +237,7 @@ class PairBwdArgs(ctypes.Structure):
                 ("trace", ctypes.c_void_p)]
 
 
-ABI_VERSION = 11
+ABI_VERSION = 12
 STATS_STRIDE = 260
 PGRAD_STRIDE = 324
 HIDDEN = 64

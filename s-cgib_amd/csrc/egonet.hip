@@ -104,12 +104,36 @@ __device__ __forceinline__ void build_ball(int32_t lv, int32_t base, int32_t ng,
     }
 }
 
+// Pool form of the builders (graph.EgoPrefetch): the input batch is the
+// resident pool's blob srcs[ctr[0] % n_src] (graph.StaticBatch layout: CSR,
+// graph_ptr and dims at byte offsets), resolved when the kernel starts, so a
+// replayed step can build the ego-nets of the batch the next step loads.
+struct EgoSrc {
+    const uint64_t *srcs;  // nullptr: the plain pointers are used
+    const unsigned *ctr;
+    int64_t o_rowptr, o_col, o_gptr, o_dims;
+    int32_t n_src;
+};
+
+template <class P, class G>  // (P: the kernels' __restrict__ parameter type)
+__device__ __forceinline__ void ego_resolve(const EgoSrc &s, P &rowptr, P &col, G &gptr,
+                                            P &dims) {
+    if (!s.srcs) return;
+    const unsigned c = __hip_atomic_load(s.ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const char *base = reinterpret_cast<const char *>(s.srcs[c % static_cast<unsigned>(s.n_src)]);
+    rowptr = reinterpret_cast<const int32_t *>(base + s.o_rowptr);
+    col = reinterpret_cast<const int32_t *>(base + s.o_col);
+    gptr = reinterpret_cast<const int32_t *>(base + s.o_gptr);
+    dims = reinterpret_cast<const int32_t *>(base + s.o_dims);
+}
+
 template <int W>
 __global__ __launch_bounds__(256) void egonet_count_k(
     const int32_t *__restrict__ rowptr, const int32_t *__restrict__ col,
     const int32_t *__restrict__ gptr, int64_t n_graphs, int64_t n, int k,
     int32_t *__restrict__ ego_ptr, int32_t *__restrict__ ego_eptr,
-    int32_t *__restrict__ blk_tot, int32_t *err, const int32_t *__restrict__ dims) {
+    int32_t *__restrict__ blk_tot, int32_t *err, const int32_t *__restrict__ dims, EgoSrc ps) {
+    ego_resolve(ps, rowptr, col, gptr, dims);
     __shared__ int32_t sn[256], se[256];
     const int64_t v = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
     int32_t nb = 0, ne = 0;
@@ -202,7 +226,8 @@ __global__ __launch_bounds__(256) void egonet_fill_k(
     const int32_t *__restrict__ ego_ptr, const int32_t *__restrict__ ego_eptr,
     int32_t *__restrict__ ego_nodes, int32_t *__restrict__ sub_rowptr,
     int32_t *__restrict__ sub_col, int32_t *err, int64_t n_ego_cap,
-    const int32_t *__restrict__ dims, int32_t *__restrict__ ego_dims) {
+    const int32_t *__restrict__ dims, int32_t *__restrict__ ego_dims, EgoSrc ps) {
+    ego_resolve(ps, rowptr, col, gptr, dims);
     const int64_t v = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
     if (v == 0 && ego_dims) {  // the ego batch's actual [N_s, E_s], device-resident
         ego_dims[0] = ego_ptr[n];
@@ -565,17 +590,12 @@ __global__ __launch_bounds__(kK1One) void egonet_k1_onepass_k(
     int32_t *__restrict__ ego_ptr, int32_t *__restrict__ ego_eptr, uint64_t *__restrict__ state,
     uint32_t *__restrict__ done, int32_t *__restrict__ ego_nodes,
     int32_t *__restrict__ sub_rowptr, int32_t *__restrict__ sub_col, int64_t n_ego_cap,
-    const int32_t *__restrict__ dims, int32_t *__restrict__ ego_dims,
-    const uint64_t *__restrict__ srcs, int32_t n_src, const unsigned *ctr, int64_t o_rowptr,
-    int64_t o_col, int64_t o_dims) {
+    const int32_t *__restrict__ dims, int32_t *__restrict__ ego_dims, EgoSrc ps) {
     const int nblk = gridDim.x, tid = threadIdx.x;
     int blk = blockIdx.x;
-    if (srcs) {  // pool form: the input batch is srcs[ctr[0] % n_src] (its CSR and dims sections)
-        const unsigned c = __hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const char *base = reinterpret_cast<const char *>(srcs[c % static_cast<unsigned>(n_src)]);
-        rowptr = reinterpret_cast<const int32_t *>(base + o_rowptr);
-        col = reinterpret_cast<const int32_t *>(base + o_col);
-        dims = reinterpret_cast<const int32_t *>(base + o_dims);
+    {
+        const int32_t *gptr = nullptr;
+        ego_resolve(ps, rowptr, col, gptr, dims);
     }
     SCGIB_MARK(0);
     SCGIB_MARK_HWID();
@@ -807,14 +827,14 @@ extern "C" int64_t scgib_egonet_workspace_bytes(int64_t n_nodes) {
     return 2 * sizeof(int32_t) * (nblk > 0 ? nblk : 1);
 }
 
-extern "C" int scgib_egonet_count(const int32_t *rowptr, const int32_t *col,
-                                  const int32_t *graph_ptr, int64_t n_graphs, int64_t n_nodes,
-                                  int32_t k, int32_t max_graph_nodes, int32_t *ego_ptr,
-                                  int32_t *ego_eptr, void *workspace, int32_t *err,
-                                  const int32_t *dims, scgib_stream_t stream) {
+static int ego_count_launch(const int32_t *rowptr, const int32_t *col, const int32_t *graph_ptr,
+                            int64_t n_graphs, int64_t n_nodes, int32_t k, int32_t max_graph_nodes,
+                            int32_t *ego_ptr, int32_t *ego_eptr, void *workspace, int32_t *err,
+                            const int32_t *dims, EgoSrc ps, scgib_stream_t stream) {
     if (n_nodes < 0 || n_graphs < 0 || k < 0) return SCGIB_EINVAL;
     if (!ego_ptr || !ego_eptr || !err || !workspace) return SCGIB_EINVAL;
-    if (n_nodes > 0 && (!rowptr || !col || !graph_ptr || n_graphs == 0)) return SCGIB_EINVAL;
+    if (n_nodes > 0 && !ps.srcs && (!rowptr || !col || !graph_ptr || n_graphs == 0))
+        return SCGIB_EINVAL;
     if (n_nodes >= (int64_t(1) << 31)) return SCGIB_EUNSUPPORTED;
     const int W = words_for(max_graph_nodes);
     if (W == 0) return SCGIB_EUNSUPPORTED;
@@ -828,7 +848,7 @@ extern "C" int scgib_egonet_count(const int32_t *rowptr, const int32_t *col,
     int32_t *blk_tot = static_cast<int32_t *>(workspace);
 #define SCGIB_EGO_COUNT(WW)                                                                     \
     egonet_count_k<WW><<<nblk, 256, 0, st>>>(rowptr, col, graph_ptr, n_graphs, n_nodes, k,    \
-                                             ego_ptr, ego_eptr, blk_tot, err, dims)
+                                             ego_ptr, ego_eptr, blk_tot, err, dims, ps)
     switch (W) {
         case 1: SCGIB_EGO_COUNT(1); break;
         case 2: SCGIB_EGO_COUNT(2); break;
@@ -838,6 +858,36 @@ extern "C" int scgib_egonet_count(const int32_t *rowptr, const int32_t *col,
 #undef SCGIB_EGO_COUNT
     egonet_scan_fixup_k<<<nblk, 256, 0, st>>>(n_nodes, nblk, blk_tot, ego_ptr, ego_eptr);
     return launch_status();
+}
+
+static bool pool_src_ok(const uint64_t *srcs, int32_t n_src, const uint32_t *ctr,
+                        int64_t o_rowptr, int64_t o_col, int64_t o_gptr, int64_t o_dims) {
+    return srcs && n_src >= 1 && ctr && o_rowptr >= 0 && o_col >= 0 && o_gptr >= 0 &&
+           o_dims >= 0 && (o_rowptr | o_col | o_gptr | o_dims) % 4 == 0;
+}
+
+extern "C" int scgib_egonet_count(const int32_t *rowptr, const int32_t *col,
+                                  const int32_t *graph_ptr, int64_t n_graphs, int64_t n_nodes,
+                                  int32_t k, int32_t max_graph_nodes, int32_t *ego_ptr,
+                                  int32_t *ego_eptr, void *workspace, int32_t *err,
+                                  const int32_t *dims, scgib_stream_t stream) {
+    return ego_count_launch(rowptr, col, graph_ptr, n_graphs, n_nodes, k, max_graph_nodes,
+                            ego_ptr, ego_eptr, workspace, err, dims, EgoSrc{}, stream);
+}
+
+extern "C" int scgib_egonet_count_pool(const uint64_t *srcs, int32_t n_src, const uint32_t *ctr,
+                                       int64_t o_rowptr, int64_t o_col, int64_t o_gptr,
+                                       int64_t o_dims, int64_t n_graphs, int64_t n_nodes,
+                                       int32_t k, int32_t max_graph_nodes, int32_t *ego_ptr,
+                                       int32_t *ego_eptr, void *workspace, int32_t *err,
+                                       scgib_stream_t stream) {
+    if (!pool_src_ok(srcs, n_src, ctr, o_rowptr, o_col, o_gptr, o_dims) || n_nodes < 1 ||
+        n_graphs < 1)
+        return SCGIB_EINVAL;
+    const EgoSrc ps{srcs, reinterpret_cast<const unsigned *>(ctr), o_rowptr, o_col, o_gptr,
+                    o_dims, n_src};
+    return ego_count_launch(nullptr, nullptr, nullptr, n_graphs, n_nodes, k, max_graph_nodes,
+                            ego_ptr, ego_eptr, workspace, err, nullptr, ps, stream);
 }
 
 extern "C" int64_t scgib_egonet_k1_max_degree(void) { return 12; }
@@ -893,9 +943,7 @@ static int k1_onepass_launch(const int32_t *rowptr, const int32_t *col, int64_t 
                              int32_t max_in_degree, int32_t *ego_ptr, int32_t *ego_eptr,
                              uint32_t *scan_state, int32_t *ego_nodes, int32_t *sub_rowptr,
                              int32_t *sub_col, int64_t n_ego_cap, const int32_t *dims,
-                             int32_t *ego_dims, const uint64_t *srcs, int32_t n_src,
-                             const uint32_t *ctr, int64_t o_rowptr, int64_t o_col, int64_t o_dims,
-                             scgib_stream_t stream) {
+                             int32_t *ego_dims, EgoSrc ps, scgib_stream_t stream) {
     if (n_nodes <= 0 || !ego_ptr || !ego_eptr || !scan_state || !ego_nodes || !sub_rowptr ||
         !sub_col || max_in_degree < 0)
         return SCGIB_EINVAL;
@@ -906,12 +954,10 @@ static int k1_onepass_launch(const int32_t *rowptr, const int32_t *col, int64_t 
     uint64_t *state = reinterpret_cast<uint64_t *>(
         (reinterpret_cast<uintptr_t>(scan_state) + 2 * sizeof(uint32_t) + 7) & ~uintptr_t(7));
     hipStream_t st = as_stream(stream);
-    const unsigned *c = reinterpret_cast<const unsigned *>(ctr);
 #define SCGIB_K1_ONEPASS(DD)                                                                     \
     egonet_k1_onepass_k<DD><<<nblk, kK1One, 0, st>>>(rowptr, col, n_nodes, ego_ptr, ego_eptr,   \
                                                      state, done, ego_nodes, sub_rowptr, sub_col, \
-                                                     n_ego_cap, dims, ego_dims, srcs, n_src, c,   \
-                                                     o_rowptr, o_col, o_dims)
+                                                     n_ego_cap, dims, ego_dims, ps)
     if (max_in_degree <= 6) SCGIB_K1_ONEPASS(6);
     else if (max_in_degree <= 8) SCGIB_K1_ONEPASS(8);
     else SCGIB_K1_ONEPASS(12);
@@ -928,8 +974,8 @@ extern "C" int scgib_egonet_k1_build_onepass(const int32_t *rowptr, const int32_
                                              int32_t *ego_dims, scgib_stream_t stream) {
     if (!rowptr || !col) return SCGIB_EINVAL;
     return k1_onepass_launch(rowptr, col, n_nodes, max_in_degree, ego_ptr, ego_eptr, scan_state,
-                             ego_nodes, sub_rowptr, sub_col, n_ego_cap, dims, ego_dims, nullptr,
-                             0, nullptr, 0, 0, 0, stream);
+                             ego_nodes, sub_rowptr, sub_col, n_ego_cap, dims, ego_dims,
+                             EgoSrc{}, stream);
 }
 
 // The same build over a resident pool's batch srcs[ctr[0] % n_src] (a
@@ -941,12 +987,12 @@ extern "C" int scgib_egonet_k1_build_onepass_pool(
     int64_t o_dims, int64_t n_nodes, int32_t max_in_degree, int32_t *ego_ptr, int32_t *ego_eptr,
     uint32_t *scan_state, int32_t *ego_nodes, int32_t *sub_rowptr, int32_t *sub_col,
     int64_t n_ego_cap, int32_t *ego_dims, scgib_stream_t stream) {
-    if (!srcs || n_src < 1 || !ctr || o_rowptr < 0 || o_col < 0 || o_dims < 0 ||
-        (o_rowptr | o_col | o_dims) % 4)
-        return SCGIB_EINVAL;
+    if (!pool_src_ok(srcs, n_src, ctr, o_rowptr, o_col, 0, o_dims)) return SCGIB_EINVAL;
+    const EgoSrc ps{srcs, reinterpret_cast<const unsigned *>(ctr), o_rowptr, o_col, 0, o_dims,
+                    n_src};
     return k1_onepass_launch(nullptr, nullptr, n_nodes, max_in_degree, ego_ptr, ego_eptr,
                              scan_state, ego_nodes, sub_rowptr, sub_col, n_ego_cap, nullptr,
-                             ego_dims, srcs, n_src, ctr, o_rowptr, o_col, o_dims, stream);
+                             ego_dims, ps, stream);
 }
 
 extern "C" int scgib_egonet_k1_build(const int32_t *rowptr, const int32_t *col, int64_t n_nodes,
@@ -959,20 +1005,20 @@ extern "C" int scgib_egonet_k1_build(const int32_t *rowptr, const int32_t *col, 
                                      stream);
 }
 
-extern "C" int scgib_egonet_fill(const int32_t *rowptr, const int32_t *col,
-                                 const int32_t *graph_ptr, int64_t n_graphs, int64_t n_nodes,
-                                 int32_t k, int32_t max_graph_nodes, const int32_t *ego_ptr,
-                                 const int32_t *ego_eptr, int32_t *ego_nodes,
-                                 int32_t *sub_rowptr, int32_t *sub_col, int32_t *err,
-                                 int64_t n_ego_cap, const int32_t *dims, int32_t *ego_dims,
-                                 scgib_stream_t stream) {
+static int ego_fill_launch(const int32_t *rowptr, const int32_t *col, const int32_t *graph_ptr,
+                           int64_t n_graphs, int64_t n_nodes, int32_t k, int32_t max_graph_nodes,
+                           const int32_t *ego_ptr, const int32_t *ego_eptr, int32_t *ego_nodes,
+                           int32_t *sub_rowptr, int32_t *sub_col, int32_t *err, int64_t n_ego_cap,
+                           const int32_t *dims, int32_t *ego_dims, EgoSrc ps,
+                           scgib_stream_t stream) {
     if (n_nodes < 0 || n_graphs < 0 || k < 0) return SCGIB_EINVAL;
     if (!ego_ptr || !ego_eptr || !sub_rowptr || !err) return SCGIB_EINVAL;
     if (n_nodes == 0) {
         const hipError_t e = hipMemsetAsync(sub_rowptr, 0, sizeof(int32_t), as_stream(stream));
         return e == hipSuccess ? SCGIB_OK : static_cast<int>(e);
     }
-    if (!rowptr || !col || !graph_ptr || !ego_nodes || !sub_col) return SCGIB_EINVAL;
+    if ((!ps.srcs && (!rowptr || !col || !graph_ptr)) || !ego_nodes || !sub_col)
+        return SCGIB_EINVAL;
     const int W = words_for(max_graph_nodes);
     if (W == 0) return SCGIB_EUNSUPPORTED;
     hipStream_t st = as_stream(stream);
@@ -981,7 +1027,7 @@ extern "C" int scgib_egonet_fill(const int32_t *rowptr, const int32_t *col,
     egonet_fill_k<WW><<<dim3((unsigned)nblk), 256, 0, st>>>(rowptr, col, graph_ptr, n_graphs,  \
                                                             n_nodes, k, ego_ptr, ego_eptr,     \
                                                             ego_nodes, sub_rowptr, sub_col, err, \
-                                                            n_ego_cap, dims, ego_dims)
+                                                            n_ego_cap, dims, ego_dims, ps)
     switch (W) {
         case 1: SCGIB_EGO_FILL(1); break;
         case 2: SCGIB_EGO_FILL(2); break;
@@ -990,6 +1036,36 @@ extern "C" int scgib_egonet_fill(const int32_t *rowptr, const int32_t *col,
     }
 #undef SCGIB_EGO_FILL
     return launch_status();
+}
+
+extern "C" int scgib_egonet_fill(const int32_t *rowptr, const int32_t *col,
+                                 const int32_t *graph_ptr, int64_t n_graphs, int64_t n_nodes,
+                                 int32_t k, int32_t max_graph_nodes, const int32_t *ego_ptr,
+                                 const int32_t *ego_eptr, int32_t *ego_nodes,
+                                 int32_t *sub_rowptr, int32_t *sub_col, int32_t *err,
+                                 int64_t n_ego_cap, const int32_t *dims, int32_t *ego_dims,
+                                 scgib_stream_t stream) {
+    return ego_fill_launch(rowptr, col, graph_ptr, n_graphs, n_nodes, k, max_graph_nodes, ego_ptr,
+                           ego_eptr, ego_nodes, sub_rowptr, sub_col, err, n_ego_cap, dims,
+                           ego_dims, EgoSrc{}, stream);
+}
+
+extern "C" int scgib_egonet_fill_pool(const uint64_t *srcs, int32_t n_src, const uint32_t *ctr,
+                                      int64_t o_rowptr, int64_t o_col, int64_t o_gptr,
+                                      int64_t o_dims, int64_t n_graphs, int64_t n_nodes, int32_t k,
+                                      int32_t max_graph_nodes, const int32_t *ego_ptr,
+                                      const int32_t *ego_eptr, int32_t *ego_nodes,
+                                      int32_t *sub_rowptr, int32_t *sub_col, int32_t *err,
+                                      int64_t n_ego_cap, int32_t *ego_dims,
+                                      scgib_stream_t stream) {
+    if (!pool_src_ok(srcs, n_src, ctr, o_rowptr, o_col, o_gptr, o_dims) || n_nodes < 1 ||
+        n_graphs < 1)
+        return SCGIB_EINVAL;
+    const EgoSrc ps{srcs, reinterpret_cast<const unsigned *>(ctr), o_rowptr, o_col, o_gptr,
+                    o_dims, n_src};
+    return ego_fill_launch(nullptr, nullptr, nullptr, n_graphs, n_nodes, k, max_graph_nodes,
+                           ego_ptr, ego_eptr, ego_nodes, sub_rowptr, sub_col, err, n_ego_cap,
+                           nullptr, ego_dims, ps, stream);
 }
 
 #ifdef SCGIB_TRACE

@@ -644,9 +644,9 @@ class StaticBatch:
                   ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
 
     def blob_offsets(self):
-        """Byte offsets of (rowptr, col, dims) inside each blob."""
+        """Byte offsets of (rowptr, col, graph_ptr, dims) inside each blob."""
         o = self._layout()
-        return o[0], o[1], o[3]
+        return o[0], o[1], o[2], o[3]
 
     def ego_error(self):
         """Error bits the ego-net build of the last step flagged (0 = none; see
@@ -655,15 +655,17 @@ class StaticBatch:
 
 
 class EgoPrefetch:
-    """The k = 1 ego-nets one batch ahead, for a replayed step over a
-    StaticBatch pool (bench.py): step t builds the ego-nets of the batch step
-    t + 1 will load — straight from that batch's pool blob, on the encoder
-    pair's queue while it would otherwise idle through the loss section
+    """The ego-nets one batch ahead, for a replayed step over a StaticBatch
+    pool (bench.py): step t builds the ego-nets of the batch step t + 1 will
+    load — straight from that batch's pool blob, on the encoder pair's queue
+    while it would otherwise idle through the loss section
     (models._encode_forked) — into a staging blob, and step t + 1's batch load
     (StaticBatch.load_next) moves them into the ego buffers the step reads.
     Every step still builds one batch's ego-nets (the reference's
     khop_in_subgraph pass, exp_pretraining.py:269-272); the build leaves the
-    head of the step's critical path.
+    head of the step's critical path.  k = 1 within the one-pass builder's
+    bounds: scgib_egonet_k1_build_onepass_pool; otherwise (k >= 2) the
+    bitmap builder's count + fill, scgib_egonet_count_pool / _fill_pool.
 
     ``prime()`` builds the ego-nets of the pool's current batch once before
     the first step (eager).  ``ego`` is the step's ego batch (capacity mode,
@@ -673,15 +675,18 @@ class EgoPrefetch:
         g = static.graph
         caps = g.ego_caps or ()
         kmax = int(_lib.query("scgib_egonet_k1_max_degree"))
-        if static.k != 1 or len(caps) < 3 or caps[2] > kmax or \
-                g.max_graph_nodes > int(_lib.query("scgib_egonet_k1_max_graph_nodes")):
-            raise _lib.ScgibError("EgoPrefetch needs k = 1 within the one-pass builder's bounds")
-        self.static, self.pool, self.k = static, pool, 1
+        self.onepass = (static.k == 1 and EGO_K1_FAST and len(caps) > 2 and caps[2] <= kmax and
+                        g.max_graph_nodes <= int(_lib.query("scgib_egonet_k1_max_graph_nodes")))
+        if len(caps) < 2 or g.max_graph_nodes > 512:
+            raise _lib.ScgibError("EgoPrefetch needs ego capacities and molecules of <= 512 atoms")
+        self.static, self.pool, self.k = static, pool, static.k
         self.n = g.num_nodes()
-        self.n_s, self.e_cap, self.dmax = int(caps[0]), int(caps[1]), int(caps[2])
+        self.n_s, self.e_cap = int(caps[0]), int(caps[1])
+        self.dmax = int(caps[2]) if len(caps) > 2 else 0
         dev = static.blob.device
+        # ego_ptr | ego_eptr | ego_nodes | sub_rowptr | sub_col | (ego dims, error bits)
         sizes = [4 * (self.n + 1), 4 * (self.n + 1), 4 * max(self.n_s, 1), 4 * (self.n_s + 1),
-                 4 * max(self.e_cap, 1), 8]
+                 4 * max(self.e_cap, 1), 16]
         offs = [0]
         for sz in sizes:
             offs.append(offs[-1] + (sz + 255) // 256 * 256)
@@ -690,29 +695,48 @@ class EgoPrefetch:
         self.staging = torch.zeros(offs[-1], dtype=torch.uint8, device=dev)
         self.views = self._views(self.blob)
         self.next_views = self._views(self.staging)
-        ego_ptr, _, ego_nodes, sub_rowptr, sub_col, ego_dims = self.views
+        ego_ptr, _, ego_nodes, sub_rowptr, sub_col, ego_dims, self.err = self.views
         self.ego = _ego_graph(g, sub_rowptr, sub_col, ego_ptr, ego_nodes, self.n_s, ego_dims)
+        self.ws = None if self.onepass else torch.empty(
+            int(_lib.query("scgib_egonet_workspace_bytes", self.n)), dtype=torch.uint8, device=dev)
         self.loaded = False  # ego holds the static batch's ego-nets (load_next with this)
         self._side = None  # stream of a prefetch not yet joined back (join())
         g.ego_prefetch = self  # models._encode_forked takes ego from here when loaded
 
     def _views(self, blob):
         i32 = torch.int32
-        return tuple(blob[o:o + sz].view(i32) for o, sz in zip(self._offs, self._sizes))
+        v = [blob[o:o + sz].view(i32) for o, sz in zip(self._offs, self._sizes)]
+        tail = v.pop()
+        return (*v, tail[:2], tail[2:3])
 
     def prefetch(self):
         """Enqueue (current stream) the build of the ego-nets of the pool's
         batch at the cursor — the one the next load_next copies in — into the
         staging blob."""
-        from . import ops  # (ops imports this module)
-        ego_ptr, ego_eptr, ego_nodes, sub_rowptr, sub_col, ego_dims = self.next_views
-        state = ops.scan_state(self.blob.device, "egonet_k1_scan_prefetch",
-                               int(_lib.query("scgib_egonet_k1_scan_words", self.n)))
-        o_rp, o_col, o_dims = self.static.blob_offsets()
-        _lib.call("scgib_egonet_k1_build_onepass_pool", _ptr(self.pool["table"]), self.pool["n"],
-                  _ptr(self.pool["cursor"]), o_rp, o_col, o_dims, self.n, self.dmax, _ptr(ego_ptr),
-                  _ptr(ego_eptr), _ptr(state), _ptr(ego_nodes), _ptr(sub_rowptr), _ptr(sub_col),
-                  self.n_s, _ptr(ego_dims), _stream())
+        ego_ptr, ego_eptr, ego_nodes, sub_rowptr, sub_col, ego_dims, err = self.next_views
+        o_rp, o_col, o_gptr, o_dims = self.static.blob_offsets()
+        src = (_ptr(self.pool["table"]), self.pool["n"], _ptr(self.pool["cursor"]))
+        if self.onepass:
+            from . import ops  # (ops imports this module)
+            state = ops.scan_state(self.blob.device, "egonet_k1_scan_prefetch",
+                                   int(_lib.query("scgib_egonet_k1_scan_words", self.n)))
+            _lib.call("scgib_egonet_k1_build_onepass_pool", *src, o_rp, o_col, o_dims, self.n,
+                      self.dmax, _ptr(ego_ptr), _ptr(ego_eptr), _ptr(state), _ptr(ego_nodes),
+                      _ptr(sub_rowptr), _ptr(sub_col), self.n_s, _ptr(ego_dims), _stream())
+            return
+        g = self.static.graph
+        mgn = max(g.max_graph_nodes, 1)
+        _lib.call("scgib_egonet_count_pool", *src, o_rp, o_col, o_gptr, o_dims, g.batch_size,
+                  self.n, self.k, mgn, _ptr(ego_ptr), _ptr(ego_eptr), _ptr(self.ws), _ptr(err),
+                  _stream())
+        _lib.call("scgib_egonet_fill_pool", *src, o_rp, o_col, o_gptr, o_dims, g.batch_size,
+                  self.n, self.k, mgn, _ptr(ego_ptr), _ptr(ego_eptr), _ptr(ego_nodes),
+                  _ptr(sub_rowptr), _ptr(sub_col), _ptr(err), self.n_s, _ptr(ego_dims), _stream())
+
+    def error(self):
+        """Error bits any prefetched build flagged (sticky; 0 = none; see
+        egonet_batch) — a device read, for checks outside the timed loop."""
+        return int(self.err.item())
 
     def prime(self):
         """The ego-nets of the pool's batch at the cursor into staging, before

@@ -300,7 +300,8 @@ def test_pool_load_next_walks_the_pool(pkg, dev):
     assert pool["cursor"].tolist() == [9, 0]
 
 
-def test_ego_prefetch_replay_bitwise(pkg, dev):
+@pytest.mark.parametrize("k", [1, 2])
+def test_ego_prefetch_replay_bitwise(pkg, dev, k):
     """graph.EgoPrefetch (bench.py's step): each replayed step builds the ego-nets
     of the batch the next step loads (pool-indirect one-pass builder, on the
     encoder pair's side stream) and the next load_next moves them in.  Against
@@ -308,19 +309,21 @@ def test_ego_prefetch_replay_bitwise(pkg, dev):
     gradients and BN running statistics bit for bit over the pool, and the
     moved-in ego buffers equal an eager egonet_batch of the loaded batch."""
     hosts = _batches(pkg, (4, 5, 6, 7))
-    n_cap, e_cap, mgn, caps = pkg.graph.StaticBatch.capacities(hosts, 1, slack=1.02)
+    n_cap, e_cap, mgn, caps = pkg.graph.StaticBatch.capacities(hosts, k, slack=1.02)
     ug, uf = _noise(n_cap, dev, 300)
     runs = {}
     for mode in (False, True):
-        static = pkg.graph.StaticBatch(B, n_cap, e_cap, F_IN, mgn, caps, dev)
+        static = pkg.graph.StaticBatch(B, n_cap, e_cap, F_IN, mgn, caps, dev, k=k)
         padded = [static.pad(gh) for gh in hosts]
         pool = static.pool(padded)
         pf = pkg.graph.EgoPrefetch(static, pool) if mode else None
-        model = _model(pkg, dev)
+        if pf is not None:
+            assert pf.onepass == (k == 1)
+        model = _model(pkg, dev, k=k)
 
         def body():
             static.load_next(pool, pf)
-            _, kl, con, rec = model(static.graph, static.x, None, None, None, 1, None, 1, dev,
+            _, kl, con, rec = model(static.graph, static.x, None, None, None, 1, None, k, dev,
                                     B, noise=(ug, uf))
             (kl + rec + con).backward()
             if pf is not None:
@@ -351,7 +354,7 @@ def test_ego_prefetch_replay_bitwise(pkg, dev):
             bufs = [b.clone() for n, b in model.named_buffers() if "running" in n]
             got.append((out.clone(), grads, bufs))
             if pf is not None:
-                ref = pkg.graph.egonet_batch(static.graph, 1)
+                ref = pkg.graph.egonet_batch(static.graph, k)
                 torch.cuda.synchronize()
                 n_s = int(ref.dims[0])
                 e_s = int(ref.dims[1])
@@ -361,6 +364,8 @@ def test_ego_prefetch_replay_bitwise(pkg, dev):
                 assert torch.equal(pf.ego.rowptr[: n_s + 1], ref.rowptr[: n_s + 1])
                 assert torch.equal(pf.ego.col[:e_s], ref.col[:e_s])
         assert pkg.ops.xq_timeouts(dev) == 0
+        if pf is not None:
+            assert pf.error() == 0
         runs[mode] = got
     for (la, ga, ba), (lb, gb, bb) in zip(runs[False], runs[True]):
         assert torch.isfinite(la).all()

@@ -757,8 +757,11 @@ def main():
     t0 = time.perf_counter()
     for i in range(a.steps):
         loss = step(a.warmup + i)
+    t_enq = time.perf_counter() - t0  # host time to enqueue the K steps
     barrier()
     elapsed = time.perf_counter() - t0
+    progress(f"timed: {elapsed / a.steps * 1e3:.4f} ms/step, host enqueue "
+             f"{t_enq / a.steps * 1e3:.4f} ms/step")
     xq_to = pkg.ops.xq_timeouts(dev)
     if xq_to:  # a hand-off wait gave up: its queue ran ahead of the data
         raise SystemExit(f"bench: {xq_to} cross-queue hand-off waits timed out (ops.XQ_FLAGS)")

@@ -154,9 +154,13 @@ def test_config_step_exact_mode(pkg, dev, case):
     _check(c, model, _losses(kl, con, rec))
 
 
-def test_config_step_graph_replay(pkg, dev, case):
+@pytest.mark.parametrize("prefetch", [False, True])
+def test_config_step_graph_replay(pkg, dev, case, prefetch):
     """Capacity-sized static buffers (sized over this batch and another one),
-    one captured step, replayed on this batch — the bench's launch path."""
+    one captured step, replayed on this batch — the bench's launch path;
+    prefetch: the bench's step exactly (the batch loaded from a resident pool
+    inside the graph, its ego-nets built during the previous step,
+    graph.EgoPrefetch)."""
     c = case
     model = copy.deepcopy(c.model)
     hosts = [c.other, c.gh]
@@ -170,18 +174,27 @@ def test_config_step_graph_replay(pkg, dev, case):
         padded.append(static.pad(gx))
     s_ug = torch.zeros(n_cap, device=dev)
     s_uf = torch.zeros(n_cap, 64, device=dev)
+    pool = static.pool(padded) if prefetch else None
+    pf = pkg.graph.EgoPrefetch(static, pool) if prefetch else None
 
     def body():
+        if pf is not None:
+            static.load_next(pool, pf)
         _, kl, con, rec = model(static.graph, static.x, None, None, None, 1, None, c.k, dev, c.B,
                                 noise=(s_ug, s_uf))
         (kl + con + rec).backward()
+        if pf is not None:
+            pf.join()
         return torch.stack([kl, con, rec])
 
     snap = copy.deepcopy(model.state_dict())
     side = torch.cuda.Stream()
     side.wait_stream(torch.cuda.current_stream())
     with torch.cuda.stream(side):  # warm-up on the other batch (allocator)
-        static.load(padded[0])
+        if pf is not None:
+            pf.prime()  # the first batch's ego-nets; the step then builds this batch's
+        else:
+            static.load(padded[0])
         body()
     torch.cuda.current_stream().wait_stream(side)
     model.load_state_dict(snap)  # undo the warm-up's running-stat updates
@@ -192,8 +205,11 @@ def test_config_step_graph_replay(pkg, dev, case):
     n = c.gh.num_nodes()
     s_ug[:n].copy_(c.u_gate)
     s_uf[:n].copy_(c.u_feat)
-    static.load(padded[1])
-    graph.replay()
+    if pf is None:
+        static.load(padded[1])
+    graph.replay()  # (prefetch: loads pool[1] = this batch with its prefetched ego-nets)
     torch.cuda.synchronize()
+    if pf is not None:
+        assert pool["cursor"].tolist() == [2, 0] and pf.error() == 0
     kl, con, rec = out.tolist()
     _check(c, model, [kl, con, rec, kl + con + rec])

@@ -636,6 +636,9 @@ class StaticBatch:
         if prefetch is not None:
             if prefetch.pool is not pool:
                 raise _lib.ScgibError("EgoPrefetch was made for another pool")
+            # a prefetch no backward joined (a forward without backward) must
+            # be done with the staging blob before this copy reads it
+            prefetch.join()
             src2, dst2, n2 = _ptr(prefetch.staging), _ptr(prefetch.blob), prefetch.blob.numel()
             prefetch.loaded = True
         _lib.call("scgib_pool_copy2", ctypes.c_void_p(pool["table"].data_ptr()), pool["n"],

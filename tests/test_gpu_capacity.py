@@ -373,3 +373,28 @@ def test_ego_prefetch_replay_bitwise(pkg, dev, k):
         assert len(ga) == len(gb) > 0
         assert all(torch.equal(x, y) for x, y in zip(ga, gb))
         assert all(torch.equal(x, y) for x, y in zip(ba, bb))
+
+
+def test_ego_prefetch_forward_only_joins(pkg, dev):
+    """EgoPrefetch without a backward (no_grad forwards): the prefetch left on
+    the side stream is joined by the next load_next before it copies the
+    staging blob, so every loaded batch still carries its own ego-nets."""
+    hosts = _batches(pkg, (4, 5, 6))
+    n_cap, e_cap, mgn, caps = pkg.graph.StaticBatch.capacities(hosts, 1, slack=1.02)
+    static = pkg.graph.StaticBatch(B, n_cap, e_cap, F_IN, mgn, caps, dev)
+    pool = static.pool([static.pad(gh) for gh in hosts])
+    pf = pkg.graph.EgoPrefetch(static, pool)
+    model = _model(pkg, dev).eval()
+    ug, uf = _noise(n_cap, dev, 302)
+    pf.prime()
+    with torch.no_grad():
+        for _ in range(5):
+            static.load_next(pool, pf)
+            model(static.graph, static.x, None, None, None, 1, None, 1, dev, B, noise=(ug, uf))
+            ref = pkg.graph.egonet_batch(static.graph, 1)
+            torch.cuda.synchronize()
+            n_s, e_s = (int(v) for v in ref.dims.tolist())
+            assert torch.equal(pf.ego.ndata["_ID"][:n_s], ref.ndata["_ID"][:n_s])
+            assert torch.equal(pf.ego.col[:e_s], ref.col[:e_s])
+    pf.join()
+    assert pf.error() == 0

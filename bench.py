@@ -134,52 +134,14 @@ def layer_bwd_flops(n, e, d_in):
 
 
 def _call_meta(fn, m):
-    """bytes / flops of one launch from its meta: per-layer kernels take
-    (n, e, d_in); the persistent pair forward its own meta (layers list)."""
-    return fn(m) if "layers" in m else fn(m["n"], m["e"], m["d_in"])
-
-
-def pair_fwd_bytes(m):
-    """§8(d) aggregation bytes of every layer of both encoders (d = 32 for the
-    transfer_d-folded layer 0, 64 after): the algorithmic bytes of the
-    persistent encoder-pair forward launch."""
-    return sum(agg_bytes(n, e, d) for n, e, d in m["layers"])
-
-
-def pair_fwd_flops(m):
-    return sum(layer_fwd_flops(n, e, d) for n, e, d in m["layers"])
-
-
-def pair_bwd_bytes(m):
-    """Algorithmic bytes of the persistent encoder-pair backward launch: per
-    layer, the saved agg / r / z2 rows it must read, plus the transposed
-    aggregation of d(agg) (§8(d)'s figure) for every layer that propagates
-    to a previous one (d = 64; layer 0's input needs no gradient)."""
-    return sum(4 * n * (d + 2 * 64) + (agg_bytes(n, e, d) if d == 64 else 0)
-               for n, e, d in m["layers"])
-
-
-def pair_bwd_flops(m):
-    return sum(layer_bwd_flops(n, e, d) for n, e, d in m["layers"])
-
+    """bytes / flops of one launch from its meta (n, e, d_in)."""
+    return fn(m["n"], m["e"], m["d_in"])
 
 
 # The step's kernels timed by KernelTimer, by kernel (the C-ABI entries that
 # launch it, a filter on the launch sizes, §8(d) bytes, flops, and the PMC
 # name prefixes of its template instances in the traffic file)
 KERNELS = {
-    "gin_pair_fwd_k": dict(entries=("scgib_gin_pair_fwd",), keep=lambda m: True,
-                           bytes=pair_fwd_bytes, flops=pair_fwd_flops, pmc=["gin_pair_fwd_k"],
-                           desc="persistent encoder-pair forward: both GIN-64xL encoders "
-                                "(transfer_d folded, ego readout, compressor[0]) in one launch, "
-                                "chunk-resident rows, f32 MFMA 16x16x4, in-kernel BatchNorm "
-                                "exchange"),
-    "gin_pair_bwd_k": dict(entries=("scgib_gin_pair_bwd",), keep=lambda m: True,
-                           bytes=pair_bwd_bytes, flops=pair_bwd_flops, pmc=["gin_pair_bwd_k"],
-                           desc="persistent encoder-pair backward: compressor[0], every GIN "
-                                "layer of both encoders (BN backward exchanged in-kernel, 4 "
-                                "f32-MFMA GEMMs per layer, transposed aggregation in LDS), "
-                                "per-chunk weight-gradient partials"),
     "gin_fwd_k": dict(entries=("scgib_gin_layer0_fwd", "scgib_gin_layer_fwd_bn"),
                       keep=lambda m: True, bytes=agg_fwd_bytes, flops=layer_fwd_flops,
                       pmc=["gin_fwd_k<32, false, true, true,", "gin_fwd_k<64, true, true,",

@@ -73,7 +73,11 @@ int scgib_abi_version(void);
  * scgib_stream_wait (consumer stream) returns once a signal it has not yet
  * consumed is there, so the consumer stream's later kernels see the
  * producer's data.  Calls must pair up in order (n-th wait <-> n-th signal).
- * A wait that sees no signal for 0.2 s gives up and counts words[2]. */
+ * A wait that sees no signal for 0.2 s gives up, counts words[2] and sets the
+ * sticky *fault word (fault may be NULL): the step's loss kernels
+ * (scgib_mlp2_recon_fwd / _contrastive_fwd, given the same word) then report
+ * a NaN loss until the caller clears it, since some kernel of that step read
+ * data before it was written. */
 /* The next batch of a resident pool into a static input buffer, for a
  * replayed step graph: srcs = device table of n_src device pointers (each
  * `bytes` long, bytes a multiple of 16); copies srcs[ctr[0] % n_src] to dst
@@ -86,7 +90,7 @@ int scgib_pool_copy(const uint64_t *srcs, int32_t n_src, uint32_t *ctr, void *ds
 int scgib_pool_copy2(const uint64_t *srcs, int32_t n_src, uint32_t *ctr, void *dst, int64_t bytes,
                      const void *src2, void *dst2, int64_t bytes2, scgib_stream_t stream);
 int scgib_stream_signal(uint32_t *words, scgib_stream_t stream);
-int scgib_stream_wait(uint32_t *words, scgib_stream_t stream);
+int scgib_stream_wait(uint32_t *words, uint32_t *fault, scgib_stream_t stream);
 const char *scgib_strerror(int code);
 
 /* ---- A5: GIN neighbourhood aggregation (DGL GINConv, sum aggregator) ------
@@ -171,9 +175,10 @@ int scgib_bn_bwd_finalize(const float *tile_stats, int64_t n_nodes, int32_t trai
                           float *dgamma, float *dbeta, float *coef, const int32_t *dims,
                           scgib_stream_t stream);
 /* Training-mode fused variants: the BatchNorm finalize is folded into the
- * tile kernel (hierarchical last-arriver over 16-tile groups, fp64, fixed
- * order) — one launch per layer instead of two.  `bn_ws` holds
- * scgib_gin_bn_ws_floats(n) floats (tile statistics + group partials);
+ * tile kernel (hierarchical last-arriver over 16-tile groups, past 64 groups
+ * also over 64-group supergroups; fp64, fixed order) — one launch per layer
+ * instead of two.  `bn_ws` holds scgib_gin_bn_ws_floats(n) floats (tile
+ * statistics + group and supergroup partials);
  * `counters` holds scgib_gin_counters(n) uint32 that are zero on entry and
  * left zero (graph-replay safe; one set per concurrently running encoder).
  * scgib_gin_layer_fwd_bn = scgib_gin_layer_fwd + scgib_bn_finalize(training);
@@ -261,122 +266,6 @@ int scgib_gin_layer_bwd(const float *dy, const float *z2, const float *r, const 
                         const float *w2, int64_t n_nodes, float *dagg, float *slab,
                         float *wgrad, const int32_t *dims, const scgib_bn_bwd_pending *pending,
                         scgib_stream_t stream);
-/* ---- A4+A5+A6 persistent: both encoders' forward in ONE launch ----------------
- * Replaces, in training mode, the encoder pair of Mainmodel.extract_features
- * (models.py:702-716 / :1204-1213): h = transfer_d(x) (:668-669) and
- * Encoder1(batch_g, h), Encoder2(ego-nets, h[_ID]) — GIN-64 x L (models.py:
- * 52-72: GINConv(MLP) + BatchNorm1d (batch statistics) + ReLU per layer) —
- * the ego readout dgl.sum_nodes (:716) and compressor[0] on Encoder1's output
- * (:596).  Each workgroup owns one CHUNK of one encoder: the components
- * (molecules / ego-nets) whose first row lies in a 64-row window, at most
- * scgib_gin_pair_max_component() rows each, so every neighbour a row gathers
- * is a row the same workgroup computed; the chunk's rows stay in LDS across
- * the layers.  BatchNorm's batch statistics are exchanged per layer through
- * chunk -> group -> publisher partials (fp64, fixed order) with agent-scope
- * atomics; every spin is bounded (timeout: sync[1] != 0).  The grid holds
- * both encoders' chunks at once: valid only when scgib_gin_pair_chunks() of
- * both fits scgib_gin_pair_slots() (co-resident workgroups).
- * Writes exactly what the per-layer path saves for the backward (agg, r,
- * z2, stat per layer, aggx), updates the running statistics, and the
- * outputs: out = relu(BN(z2 of the last layer)), the per-component readout
- * and row -> component map (readout != NULL), lin_out = Linear(out)
- * (lin_w != NULL).  Capacity mode: dims = device [n, e], rows past n zeroed. */
-#define SCGIB_PAIR_MAX_LAYERS 6
-typedef struct {
-    const int32_t *rowptr, *col;  /* symmetric CSR (components closed) */
-    const int32_t *comp_ptr;      /* [n_comp + 1] component starts (only the first
-                                     actual count + 1 entries are read) */
-    int64_t n_comp;               /* components (capacity) */
-    const int32_t *comp_dims;     /* device: [0] = the actual component count
-                                     (capacity mode), or NULL: n_comp */
-    const int32_t *dims;          /* device [n, e] or NULL */
-    int64_t n_cap;                /* rows (capacity) */
-    const int32_t *node_map;      /* layer-0 row -> row of x, or NULL (identity) */
-    const float *w1[SCGIB_PAIR_MAX_LAYERS], *b1[SCGIB_PAIR_MAX_LAYERS];
-    const float *w2[SCGIB_PAIR_MAX_LAYERS], *b2[SCGIB_PAIR_MAX_LAYERS];
-    const float *gamma[SCGIB_PAIR_MAX_LAYERS], *beta[SCGIB_PAIR_MAX_LAYERS];
-    float one_plus_eps[SCGIB_PAIR_MAX_LAYERS], bn_eps[SCGIB_PAIR_MAX_LAYERS];
-    float momentum[SCGIB_PAIR_MAX_LAYERS];
-    float *running_mean[SCGIB_PAIR_MAX_LAYERS], *running_var[SCGIB_PAIR_MAX_LAYERS];
-    int64_t *num_batches_tracked[SCGIB_PAIR_MAX_LAYERS];
-    float *agg[SCGIB_PAIR_MAX_LAYERS], *r[SCGIB_PAIR_MAX_LAYERS];
-    float *z2[SCGIB_PAIR_MAX_LAYERS], *stat[SCGIB_PAIR_MAX_LAYERS];
-    float *aggx;                  /* [n][16] layer-0 gathered raw features */
-    float *out;                   /* [n][64] */
-    float *readout;               /* [n_comp][64] or NULL */
-    int32_t *seg;                 /* [n] with readout */
-    const float *lin_w, *lin_b;   /* Linear(64, 64) on out, or NULL */
-    float *lin_out;
-    void *ws;                     /* scgib_gin_pair_ws_bytes(n_cap, n_layers) bytes */
-    int32_t *chunk_rec;           /* [chunks][scgib_gin_pair_chunk_rec_ints()]: each chunk's
-                                     bounds and local CSR, written for the backward; or NULL */
-    uint32_t *counters;           /* scgib_gin_pair_counters(n_cap, n_layers) ZEROED words,
-                                     left zeroed */
-} scgib_pair_encoder;
-typedef struct {
-    scgib_pair_encoder enc[2];    /* enc[0] (the ego-nets) takes the first chunks */
-    const float *x;               /* [*][n_feat] raw (normalised) features */
-    int32_t n_feat;               /* <= 16 */
-    const float *wt;              /* transfer_d.weight [32][n_feat] */
-    int32_t n_layers;             /* <= SCGIB_PAIR_MAX_LAYERS */
-    uint32_t *sync;               /* 4 ZEROED words: [0] exit count (left zeroed),
-                                     [1] timeout code (0: none) */
-    uint64_t *trace;              /* diagnostics: NULL, or [grid][64] wall-clock stamps
-                                     of each workgroup's phases */
-} scgib_pair_fwd_args;
-/* The backward of scgib_gin_pair_fwd, the same way: one workgroup per chunk,
- * d h of the chunk's rows kept in LDS from layer to layer (the transposed
- * aggregation never leaves the chunk), per layer the BatchNorm-backward sums
- * (dbeta = sum dy, dgamma = sum dy xhat) exchanged as in the forward, then
- * dz2 = scale (dy - dbeta/N - xhat dgamma/N), dW2 += dz2^T r, dr = dz2 W2,
- * dz1 = dr [r > 0], dW1 += dz1^T agg, d(agg) = dz1 W1, and for layer 0
- * dWt += d(agg0)^T aggx (models.py:52-72, :668-669 under autograd).  Incoming:
- * g_out [n][64] and / or g_readout [n_comp][64] (the ego readout's gradient,
- * broadcast to the component's rows); with lin_g, compressor[0]'s backward
- * first: d out = g_out + lin_g W0, dW0 += lin_g^T lin_in (models.py:596).
- * Weight gradients: one partial per chunk in slab[l] (row c at c * stride[l]:
- * dW2[64*64] | dW1[64*d_in] | db2[64] | db1[64] | layer 0: dWt[32*16] at
- * 64*64 + 64*32 + 128, i.e. scgib_gin_layer_bwd's wgrad layout), lin_slab
- * (dW0[64*64] | db0[64]); summed afterwards by scgib_slab_reduce_multi. */
-typedef struct {
-    const int32_t *rowptr, *col, *comp_ptr;
-    int64_t n_comp;
-    const int32_t *comp_dims;     /* as scgib_pair_encoder */
-    const int32_t *dims;
-    int64_t n_cap;
-    const float *agg[SCGIB_PAIR_MAX_LAYERS], *r[SCGIB_PAIR_MAX_LAYERS];
-    const float *z2[SCGIB_PAIR_MAX_LAYERS], *stat[SCGIB_PAIR_MAX_LAYERS];
-    const float *w1[SCGIB_PAIR_MAX_LAYERS], *w2[SCGIB_PAIR_MAX_LAYERS];
-    float one_plus_eps[SCGIB_PAIR_MAX_LAYERS];
-    const float *aggx;
-    const float *g_out, *g_readout;
-    const float *lin_g, *lin_w, *lin_in;
-    float *dgamma[SCGIB_PAIR_MAX_LAYERS], *dbeta[SCGIB_PAIR_MAX_LAYERS];
-    float *slab[SCGIB_PAIR_MAX_LAYERS];
-    int64_t slab_stride[SCGIB_PAIR_MAX_LAYERS];
-    float *lin_slab;
-    void *ws;                     /* scgib_gin_pair_ws_bytes(n_cap, n_layers) bytes */
-    const int32_t *chunk_rec;     /* the forward's chunk records, or NULL (derived again) */
-    uint32_t *counters;           /* scgib_gin_pair_counters(...) ZEROED words, left zeroed */
-} scgib_pair_bwd_encoder;
-typedef struct {
-    scgib_pair_bwd_encoder enc[2];
-    int32_t n_layers;
-    int32_t n_feat;
-    uint32_t *sync;               /* as scgib_pair_fwd_args.sync */
-    uint64_t *trace;              /* as scgib_pair_fwd_args.trace */
-} scgib_pair_bwd_args;
-int64_t scgib_gin_pair_bwd_args_bytes(void);
-int scgib_gin_pair_bwd(const scgib_pair_bwd_args *args, scgib_stream_t stream);
-int64_t scgib_gin_pair_args_bytes(void);  /* sizeof(scgib_pair_fwd_args): binding check */
-int32_t scgib_gin_pair_max_component(void);
-int64_t scgib_gin_pair_chunks(int64_t n_cap);
-int64_t scgib_gin_pair_slots(void);
-int64_t scgib_gin_pair_ws_bytes(int64_t n_cap, int32_t n_layers);
-int64_t scgib_gin_pair_counters(int64_t n_cap, int32_t n_layers);
-int64_t scgib_gin_pair_chunk_rec_ints(void);
-int scgib_gin_pair_fwd(const scgib_pair_fwd_args *args, scgib_stream_t stream);
-
 /* ---- A6: per-segment readouts (dgl.sum_nodes) -------------------------------
  * out[s,:] = sum_{i in [ptr[s], ptr[s+1])} x[i,:]   (models.py:716, 725, 733)
  * segment_broadcast is its adjoint: out[i,:] = g[s,:] for every row i of s.
@@ -441,13 +330,16 @@ int scgib_egonet_k1_build_deg(const int32_t *rowptr, const int32_t *col, int64_t
  * decoupled look-back over the preceding blocks instead of a second launch.
  * scan_state: scgib_egonet_k1_scan_words(n) ZEROED uint32 words, 4-byte
  * aligned, left zeroed by the launch (reusable by the next one; one launch in
- * flight per scan_state).  Output identical to scgib_egonet_k1_build_deg. */
+ * flight per scan_state).  Output identical to scgib_egonet_k1_build_deg.
+ * e_cap: sub_col's capacity; a ball that would write past n_ego_cap rows or
+ * e_cap columns is dropped and sets bit 4 of *err (err may be NULL). */
 int64_t scgib_egonet_k1_scan_words(int64_t n_nodes);
 int scgib_egonet_k1_build_onepass(const int32_t *rowptr, const int32_t *col, int64_t n_nodes,
                                   int32_t max_in_degree, int32_t *ego_ptr, int32_t *ego_eptr,
                                   uint32_t *scan_state, int32_t *ego_nodes, int32_t *sub_rowptr,
-                                  int32_t *sub_col, int64_t n_ego_cap, const int32_t *dims,
-                                  int32_t *ego_dims, scgib_stream_t stream);
+                                  int32_t *sub_col, int64_t n_ego_cap, int64_t e_cap,
+                                  int32_t *err, const int32_t *dims, int32_t *ego_dims,
+                                  scgib_stream_t stream);
 /* scgib_egonet_count / scgib_egonet_fill (any k) over the resident pool's
  * batch srcs[ctr[0] % n_src] (rowptr / col / graph_ptr / dims at byte offsets
  * of each graph.StaticBatch blob, capacity mode; n_nodes = the capacity),
@@ -474,8 +366,8 @@ int scgib_egonet_k1_build_onepass_pool(const uint64_t *srcs, int32_t n_src, cons
                                        int64_t n_nodes, int32_t max_in_degree, int32_t *ego_ptr,
                                        int32_t *ego_eptr, uint32_t *scan_state,
                                        int32_t *ego_nodes, int32_t *sub_rowptr, int32_t *sub_col,
-                                       int64_t n_ego_cap, int32_t *ego_dims,
-                                       scgib_stream_t stream);
+                                       int64_t n_ego_cap, int64_t e_cap, int32_t *err,
+                                       int32_t *ego_dims, scgib_stream_t stream);
 int scgib_egonet_fill(const int32_t *rowptr, const int32_t *col, const int32_t *graph_ptr,
                       int64_t n_graphs, int64_t n_nodes, int32_t k, int32_t max_graph_nodes,
                       const int32_t *ego_ptr, const int32_t *ego_eptr, int32_t *ego_nodes,
@@ -636,7 +528,8 @@ int scgib_mlp2_bwd(const float *dout, const float *x, const float *r, int32_t d_
  * and their backward).  Forward: out (= IM), r, and loss; `ws` holds
  * scgib_mlp2_recon_ws_floats(n) floats (per-tile Gram partials, G, loss
  * partials) and must be passed unchanged to the backward; `counter` is three
- * zeroed uint32, left zero.  When the launch's workgroups are all co-resident
+ * zeroed uint32, left zero; `fault` (or NULL) is scgib_stream_wait's sticky
+ * hand-off fault word: while it is set, *loss is NaN.  When the launch's workgroups are all co-resident
  * the MLP tiles also finish the loss (no second launch; the same bits either
  * way).  Backward: dx = d loss / d x and wgrad as
  * scgib_mlp2_bwd, for d loss / d recon = *g_loss; rowptr_t/col_t NULL for a
@@ -652,7 +545,7 @@ int scgib_mlp2_recon_fwd(const float *x, int32_t d_in, int64_t n_nodes, const fl
                          const float *b1, const float *w2, const float *b2, float *r, float *out,
                          const int32_t *rowptr, const int32_t *col, int64_t n_edges, float *ws,
                          uint32_t *counter, float *loss, const int32_t *dims,
-                         scgib_stream_t stream);
+                         const uint32_t *fault, scgib_stream_t stream);
 int scgib_mlp2_recon_bwd(const float *x, const float *r, const float *out, const float *ws,
                          int32_t d_in, const float *w1, const float *w2, int64_t n_nodes,
                          const int32_t *rowptr, const int32_t *col, const int32_t *rowptr_t,
@@ -675,7 +568,7 @@ int scgib_mlp2_recon_contrastive_fwd(const float *x, int32_t d_in, int64_t n_nod
                                      const int32_t *dims, const float *z1, const float *z2,
                                      int64_t n_graphs, float *cws, float *closs,
                                      uint32_t *ccounters, const scgib_running_update *ru,
-                                     scgib_stream_t stream);
+                                     const uint32_t *fault, scgib_stream_t stream);
 int scgib_mlp2_recon_contrastive_bwd(const float *x, const float *r, const float *out,
                                      const float *ws, int32_t d_in, const float *w1,
                                      const float *w2, int64_t n_nodes, const int32_t *rowptr,

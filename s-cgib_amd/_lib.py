@@ -22,7 +22,7 @@ SIGNATURES = {
     "scgib_pool_copy": (ctypes.c_int, [_P, _I32, _P, _P, _I64, _P]),
     "scgib_pool_copy2": (ctypes.c_int, [_P, _I32, _P, _P, _I64, _P, _P, _I64, _P]),
     "scgib_stream_signal": (ctypes.c_int, [_P, _P]),
-    "scgib_stream_wait": (ctypes.c_int, [_P, _P]),
+    "scgib_stream_wait": (ctypes.c_int, [_P, _P, _P]),
     "scgib_strerror": (ctypes.c_char_p, [ctypes.c_int]),
     "scgib_gin_aggregate": (ctypes.c_int, [_P, _P, _P, _I64, _I32, _F, _P, _P, _P]),
     "scgib_segment_sum": (ctypes.c_int, [_P, _P, _I64, _I32, _P, _P, _P]),
@@ -43,9 +43,9 @@ SIGNATURES = {
                                               _I32, _I32, _P, _P, _P, _P, _P, _P, _I64, _P, _P]),
     "scgib_egonet_k1_build_onepass_pool": (ctypes.c_int, [_P, _I32, _P, _I64, _I64, _I64, _I64,
                                                            _I32, _P, _P, _P, _P, _P, _P, _I64,
-                                                           _P, _P]),
+                                                           _I64, _P, _P, _P]),
     "scgib_egonet_k1_build_onepass": (ctypes.c_int, [_P, _P, _I64, _I32, _P, _P, _P, _P, _P, _P,
-                                                     _I64, _P, _P, _P]),
+                                                     _I64, _I64, _P, _P, _P, _P]),
     "scgib_egonet_fill": (ctypes.c_int, [_P, _P, _P, _I64, _I64, _I32, _I32, _P, _P, _P, _P, _P,
                                          _P, _I64, _P, _P, _P]),
     "scgib_interaction_fwd": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _I64, _I64, _P, _P, _P, _P,
@@ -67,12 +67,12 @@ SIGNATURES = {
     "scgib_mlp2_bwd": (ctypes.c_int, [_P, _P, _P, _I32, _P, _P, _I64, _P, _P, _P, _P, _P]),
     "scgib_mlp2_recon_ws_floats": (_I64, [_I64]),
     "scgib_mlp2_recon_fwd": (ctypes.c_int, [_P, _I32, _I64, _P, _P, _P, _P, _P, _P, _P, _P, _I64,
-                                            _P, _P, _P, _P, _P]),
+                                            _P, _P, _P, _P, _P, _P]),
     "scgib_mlp2_recon_bwd": (ctypes.c_int, [_P, _P, _P, _P, _I32, _P, _P, _I64, _P, _P, _P, _P,
                                             _P, _P, _P, _P, _P, _P]),
     "scgib_mlp2_recon_contrastive_fwd": (ctypes.c_int, [_P, _I32, _I64, _P, _P, _P, _P, _P, _P,
                                                         _P, _P, _I64, _P, _P, _P, _P, _P, _P,
-                                                        _I64, _P, _P, _P, _P, _P]),
+                                                        _I64, _P, _P, _P, _P, _P, _P]),
     "scgib_mlp2_recon_contrastive_bwd": (ctypes.c_int, [_P, _P, _P, _P, _I32, _P, _P, _I64, _P,
                                                         _P, _P, _P, _P, _P, _P, _P, _P, _P, _P,
                                                         _I64, _P, _P, _P, _P, _P, _P]),
@@ -122,16 +122,6 @@ SIGNATURES = {
     "scgib_grad_pack_max_tensors": (_I64, []),
     "scgib_grad_pack": (ctypes.c_int, [_P, _I32, _P, _P]),
     "scgib_grad_unpack": (ctypes.c_int, [_P, _I32, _P, _F, _P]),
-    "scgib_gin_pair_args_bytes": (_I64, []),
-    "scgib_gin_pair_bwd_args_bytes": (_I64, []),
-    "scgib_gin_pair_bwd": (ctypes.c_int, [_P, _P]),
-    "scgib_gin_pair_max_component": (_I32, []),
-    "scgib_gin_pair_chunks": (_I64, [_I64]),
-    "scgib_gin_pair_chunk_rec_ints": (_I64, []),
-    "scgib_gin_pair_slots": (_I64, []),
-    "scgib_gin_pair_ws_bytes": (_I64, [_I64, _I32]),
-    "scgib_gin_pair_counters": (_I64, [_I64, _I32]),
-    "scgib_gin_pair_fwd": (ctypes.c_int, [_P, _P]),
     "scgib_adam_max_tensors": (_I64, []),
     "scgib_adam_step": (ctypes.c_int, [_P, _I32, _D, _D, _D, _D, _D, _P, _P]),
 }
@@ -176,68 +166,7 @@ class RunningUpdate(ctypes.Structure):
                 ("num_batches_tracked", ctypes.c_void_p)]
 
 
-PAIR_MAX_LAYERS = 6  # SCGIB_PAIR_MAX_LAYERS
-
-
-class PairEncoder(ctypes.Structure):
-    """scgib_pair_encoder (include/scgib.h)."""
-    _L = PAIR_MAX_LAYERS
-    _fields_ = [("rowptr", ctypes.c_void_p), ("col", ctypes.c_void_p),
-                ("comp_ptr", ctypes.c_void_p), ("n_comp", ctypes.c_int64),
-                ("comp_dims", ctypes.c_void_p),
-                ("dims", ctypes.c_void_p), ("n_cap", ctypes.c_int64),
-                ("node_map", ctypes.c_void_p),
-                ("w1", ctypes.c_void_p * _L), ("b1", ctypes.c_void_p * _L),
-                ("w2", ctypes.c_void_p * _L), ("b2", ctypes.c_void_p * _L),
-                ("gamma", ctypes.c_void_p * _L), ("beta", ctypes.c_void_p * _L),
-                ("one_plus_eps", ctypes.c_float * _L), ("bn_eps", ctypes.c_float * _L),
-                ("momentum", ctypes.c_float * _L),
-                ("running_mean", ctypes.c_void_p * _L), ("running_var", ctypes.c_void_p * _L),
-                ("num_batches_tracked", ctypes.c_void_p * _L),
-                ("agg", ctypes.c_void_p * _L), ("r", ctypes.c_void_p * _L),
-                ("z2", ctypes.c_void_p * _L), ("stat", ctypes.c_void_p * _L),
-                ("aggx", ctypes.c_void_p), ("out", ctypes.c_void_p),
-                ("readout", ctypes.c_void_p), ("seg", ctypes.c_void_p),
-                ("lin_w", ctypes.c_void_p), ("lin_b", ctypes.c_void_p),
-                ("lin_out", ctypes.c_void_p), ("ws", ctypes.c_void_p),
-                ("chunk_rec", ctypes.c_void_p), ("counters", ctypes.c_void_p)]
-
-
-class PairFwdArgs(ctypes.Structure):
-    """scgib_pair_fwd_args (include/scgib.h)."""
-    _fields_ = [("enc", PairEncoder * 2), ("x", ctypes.c_void_p), ("n_feat", ctypes.c_int32),
-                ("wt", ctypes.c_void_p), ("n_layers", ctypes.c_int32), ("sync", ctypes.c_void_p),
-                ("trace", ctypes.c_void_p)]
-
-
-class PairBwdEncoder(ctypes.Structure):
-    """scgib_pair_bwd_encoder (include/scgib.h)."""
-    _L = PAIR_MAX_LAYERS
-    _fields_ = [("rowptr", ctypes.c_void_p), ("col", ctypes.c_void_p),
-                ("comp_ptr", ctypes.c_void_p), ("n_comp", ctypes.c_int64),
-                ("comp_dims", ctypes.c_void_p),
-                ("dims", ctypes.c_void_p), ("n_cap", ctypes.c_int64),
-                ("agg", ctypes.c_void_p * _L), ("r", ctypes.c_void_p * _L),
-                ("z2", ctypes.c_void_p * _L), ("stat", ctypes.c_void_p * _L),
-                ("w1", ctypes.c_void_p * _L), ("w2", ctypes.c_void_p * _L),
-                ("one_plus_eps", ctypes.c_float * _L),
-                ("aggx", ctypes.c_void_p), ("g_out", ctypes.c_void_p),
-                ("g_readout", ctypes.c_void_p), ("lin_g", ctypes.c_void_p),
-                ("lin_w", ctypes.c_void_p), ("lin_in", ctypes.c_void_p),
-                ("dgamma", ctypes.c_void_p * _L), ("dbeta", ctypes.c_void_p * _L),
-                ("slab", ctypes.c_void_p * _L), ("slab_stride", ctypes.c_int64 * _L),
-                ("lin_slab", ctypes.c_void_p), ("ws", ctypes.c_void_p),
-                ("chunk_rec", ctypes.c_void_p), ("counters", ctypes.c_void_p)]
-
-
-class PairBwdArgs(ctypes.Structure):
-    """scgib_pair_bwd_args (include/scgib.h)."""
-    _fields_ = [("enc", PairBwdEncoder * 2), ("n_layers", ctypes.c_int32),
-                ("n_feat", ctypes.c_int32), ("sync", ctypes.c_void_p),
-                ("trace", ctypes.c_void_p)]
-
-
-ABI_VERSION = 12
+ABI_VERSION = 13
 STATS_STRIDE = 260
 PGRAD_STRIDE = 324
 HIDDEN = 64

@@ -120,7 +120,7 @@ int launch_slab_reduce(const float *slab, int nslab, int64_t width, float *out, 
 int launch_recon_fin(const float *gslab, const float *im, const int32_t *rowptr,
                      const int32_t *col, int64_t n_nodes, int64_t n_edges, float *gram,
                      double *wsd, unsigned *cnt, float *loss, const int32_t *dims,
-                     const scgib_running_update *ru, hipStream_t st);
+                     const scgib_running_update *ru, const unsigned *fault, hipStream_t st);
 
 // Phase tracing (debug build only, `make trace` -> libscgib_trace.so):
 // thread 0 of each workgroup stamps the 100 MHz wall clock at phase marks

@@ -63,7 +63,7 @@ __device__ __forceinline__ int64_t graph_of(const int32_t *__restrict__ gptr, in
     return lo;
 }
 
-enum : int32_t { kErrEdgeLeavesGraph = 1, kErrGraphTooLarge = 2 };
+enum : int32_t { kErrEdgeLeavesGraph = 1, kErrGraphTooLarge = 2, kErrCapacity = 4 };
 
 template <int W>
 __device__ __forceinline__ void build_ball(int32_t lv, int32_t base, int32_t ng, int k,
@@ -590,7 +590,8 @@ __global__ __launch_bounds__(kK1One) void egonet_k1_onepass_k(
     int32_t *__restrict__ ego_ptr, int32_t *__restrict__ ego_eptr, uint64_t *__restrict__ state,
     uint32_t *__restrict__ done, int32_t *__restrict__ ego_nodes,
     int32_t *__restrict__ sub_rowptr, int32_t *__restrict__ sub_col, int64_t n_ego_cap,
-    const int32_t *__restrict__ dims, int32_t *__restrict__ ego_dims, EgoSrc ps) {
+    int64_t e_cap, int32_t *__restrict__ err, const int32_t *__restrict__ dims,
+    int32_t *__restrict__ ego_dims, EgoSrc ps) {
     const int nblk = gridDim.x, tid = threadIdx.x;
     int blk = blockIdx.x;
     {
@@ -771,18 +772,24 @@ __global__ __launch_bounds__(kK1One) void egonet_k1_onepass_k(
     }
     SCGIB_MARK(3);
     if (live) {  // members ascending (DGL order), each row's columns in CSR order
-        int32_t r = 0;
-        for (uint64_t m0 = b.w[0], m1 = b.w[1]; m0 | m1; ++r) {
-            const int32_t i = m0 ? __ffsll(static_cast<unsigned long long>(m0)) - 1
-                                 : 64 + __ffsll(static_cast<unsigned long long>(m1)) - 1;
-            if (m0) m0 &= m0 - 1ull;
-            else m1 &= m1 - 1ull;
-            const int32_t u = b.v - 64 + i;
-            ego_nodes[noff + r] = u;
-            sub_rowptr[noff + r] = eo;
-            for (int32_t e = acc.rp(u), e1 = acc.rp(u + 1); e < e1; ++e) {
-                const int32_t j = k1_index(b, acc.cl(e, true, 0));
-                if (j >= 0) sub_col[eo++] = noff + k1_rank(b, j);
+        // (a ball past the buffers' capacities — a batch larger than the
+        // capacity it was sized for — is flagged and its writes dropped)
+        if (noff + nb > n_ego_cap || eo + ne > e_cap) {
+            if (err) atomicOr(err, kErrCapacity);
+        } else {
+            int32_t r = 0;
+            for (uint64_t m0 = b.w[0], m1 = b.w[1]; m0 | m1; ++r) {
+                const int32_t i = m0 ? __ffsll(static_cast<unsigned long long>(m0)) - 1
+                                     : 64 + __ffsll(static_cast<unsigned long long>(m1)) - 1;
+                if (m0) m0 &= m0 - 1ull;
+                else m1 &= m1 - 1ull;
+                const int32_t u = b.v - 64 + i;
+                ego_nodes[noff + r] = u;
+                sub_rowptr[noff + r] = eo;
+                for (int32_t e = acc.rp(u), e1 = acc.rp(u + 1); e < e1; ++e) {
+                    const int32_t j = k1_index(b, acc.cl(e, true, 0));
+                    if (j >= 0) sub_col[eo++] = noff + k1_rank(b, j);
+                }
             }
         }
     }
@@ -942,10 +949,11 @@ extern "C" int64_t scgib_egonet_k1_scan_words(int64_t n_nodes) {
 static int k1_onepass_launch(const int32_t *rowptr, const int32_t *col, int64_t n_nodes,
                              int32_t max_in_degree, int32_t *ego_ptr, int32_t *ego_eptr,
                              uint32_t *scan_state, int32_t *ego_nodes, int32_t *sub_rowptr,
-                             int32_t *sub_col, int64_t n_ego_cap, const int32_t *dims,
-                             int32_t *ego_dims, EgoSrc ps, scgib_stream_t stream) {
+                             int32_t *sub_col, int64_t n_ego_cap, int64_t e_cap, int32_t *err,
+                             const int32_t *dims, int32_t *ego_dims, EgoSrc ps,
+                             scgib_stream_t stream) {
     if (n_nodes <= 0 || !ego_ptr || !ego_eptr || !scan_state || !ego_nodes || !sub_rowptr ||
-        !sub_col || max_in_degree < 0)
+        !sub_col || max_in_degree < 0 || n_ego_cap < 0 || e_cap < 0)
         return SCGIB_EINVAL;
     if (n_nodes >= (int64_t(1) << 31) || max_in_degree > 12) return SCGIB_EUNSUPPORTED;
     if (reinterpret_cast<uintptr_t>(scan_state) % 4) return SCGIB_EINVAL;
@@ -957,7 +965,7 @@ static int k1_onepass_launch(const int32_t *rowptr, const int32_t *col, int64_t 
 #define SCGIB_K1_ONEPASS(DD)                                                                     \
     egonet_k1_onepass_k<DD><<<nblk, kK1One, 0, st>>>(rowptr, col, n_nodes, ego_ptr, ego_eptr,   \
                                                      state, done, ego_nodes, sub_rowptr, sub_col, \
-                                                     n_ego_cap, dims, ego_dims, ps)
+                                                     n_ego_cap, e_cap, err, dims, ego_dims, ps)
     if (max_in_degree <= 6) SCGIB_K1_ONEPASS(6);
     else if (max_in_degree <= 8) SCGIB_K1_ONEPASS(8);
     else SCGIB_K1_ONEPASS(12);
@@ -970,12 +978,13 @@ extern "C" int scgib_egonet_k1_build_onepass(const int32_t *rowptr, const int32_
                                              int32_t *ego_ptr, int32_t *ego_eptr,
                                              uint32_t *scan_state, int32_t *ego_nodes,
                                              int32_t *sub_rowptr, int32_t *sub_col,
-                                             int64_t n_ego_cap, const int32_t *dims,
-                                             int32_t *ego_dims, scgib_stream_t stream) {
+                                             int64_t n_ego_cap, int64_t e_cap, int32_t *err,
+                                             const int32_t *dims, int32_t *ego_dims,
+                                             scgib_stream_t stream) {
     if (!rowptr || !col) return SCGIB_EINVAL;
     return k1_onepass_launch(rowptr, col, n_nodes, max_in_degree, ego_ptr, ego_eptr, scan_state,
-                             ego_nodes, sub_rowptr, sub_col, n_ego_cap, dims, ego_dims,
-                             EgoSrc{}, stream);
+                             ego_nodes, sub_rowptr, sub_col, n_ego_cap, e_cap, err, dims,
+                             ego_dims, EgoSrc{}, stream);
 }
 
 // The same build over a resident pool's batch srcs[ctr[0] % n_src] (a
@@ -986,13 +995,13 @@ extern "C" int scgib_egonet_k1_build_onepass_pool(
     const uint64_t *srcs, int32_t n_src, const uint32_t *ctr, int64_t o_rowptr, int64_t o_col,
     int64_t o_dims, int64_t n_nodes, int32_t max_in_degree, int32_t *ego_ptr, int32_t *ego_eptr,
     uint32_t *scan_state, int32_t *ego_nodes, int32_t *sub_rowptr, int32_t *sub_col,
-    int64_t n_ego_cap, int32_t *ego_dims, scgib_stream_t stream) {
+    int64_t n_ego_cap, int64_t e_cap, int32_t *err, int32_t *ego_dims, scgib_stream_t stream) {
     if (!pool_src_ok(srcs, n_src, ctr, o_rowptr, o_col, 0, o_dims)) return SCGIB_EINVAL;
     const EgoSrc ps{srcs, reinterpret_cast<const unsigned *>(ctr), o_rowptr, o_col, 0, o_dims,
                     n_src};
     return k1_onepass_launch(nullptr, nullptr, n_nodes, max_in_degree, ego_ptr, ego_eptr,
-                             scan_state, ego_nodes, sub_rowptr, sub_col, n_ego_cap, nullptr,
-                             ego_dims, ps, stream);
+                             scan_state, ego_nodes, sub_rowptr, sub_col, n_ego_cap, e_cap, err,
+                             nullptr, ego_dims, ps, stream);
 }
 
 extern "C" int scgib_egonet_k1_build(const int32_t *rowptr, const int32_t *col, int64_t n_nodes,

@@ -172,7 +172,7 @@ __global__ void stream_signal_k(unsigned *w) {
     if (threadIdx.x == 0) __hip_atomic_fetch_add(w, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-__global__ void stream_wait_k(unsigned *w) {
+__global__ void stream_wait_k(unsigned *w, unsigned *fault) {
     if (threadIdx.x == 0) {
         const unsigned a = __hip_atomic_load(w + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const uint64_t t0 = wall_clock64();
@@ -180,6 +180,8 @@ __global__ void stream_wait_k(unsigned *w) {
             __builtin_amdgcn_s_sleep(2);
             if (wall_clock64() - t0 > 20000000) {  // 0.2 s of the 100 MHz clock: counted, not hung
                 __hip_atomic_fetch_add(w + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                // sticky: the step's loss kernels report NaN while it is set
+                if (fault) __hip_atomic_store(fault, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 break;
             }
         }
@@ -277,9 +279,9 @@ extern "C" int scgib_stream_signal(uint32_t *words, scgib_stream_t stream) {
     return launch_status();
 }
 
-extern "C" int scgib_stream_wait(uint32_t *words, scgib_stream_t stream) {
+extern "C" int scgib_stream_wait(uint32_t *words, uint32_t *fault, scgib_stream_t stream) {
     if (!words) return SCGIB_EINVAL;
-    stream_wait_k<<<1, 64, 0, as_stream(stream)>>>(words);
+    stream_wait_k<<<1, 64, 0, as_stream(stream)>>>(words, fault);
     return launch_status();
 }
 
@@ -302,7 +304,7 @@ extern "C" int scgib_pool_copy(const uint64_t *srcs, int32_t n_src, uint32_t *ct
     return scgib_pool_copy2(srcs, n_src, ctr, dst, bytes, nullptr, nullptr, 0, stream);
 }
 
-extern "C" int scgib_abi_version(void) { return 12; }
+extern "C" int scgib_abi_version(void) { return 13; }
 
 extern "C" const char *scgib_strerror(int code) {
     if (code == SCGIB_OK) return "ok";

@@ -135,10 +135,12 @@ __device__ __forceinline__ double quad_sum(double a) {
 // n_g = kGroup * 64 for every group but possibly the last, and dividing by a power
 // of two equals multiplying by its reciprocal exactly, so only the last
 // group's term (added last by its owner, the same order) divides.
-template <bool AGENT>
+// UNIT: rows of every entry but possibly the last (kGroup tiles; a 64-group
+// supergroup at the third level of bn_fwd_hier).  S (or nullptr): the sum.
+template <bool AGENT, int64_t UNIT = int64_t(kGroup) * TM>
 __device__ void bn_fwd_final(const double *__restrict__ gpart, int64_t n, int ngr, FwdFin &f,
-                             double &mean, double &M2) {
-    constexpr double kFull = kGroup * TM, kInvFull = 1.0 / kFull;
+                             double &mean, double &M2, double *S = nullptr) {
+    constexpr double kFull = static_cast<double>(UNIT), kInvFull = 1.0 / kFull;
     const int p = (threadIdx.x & 63) >> 4;
     double a = 0.0;
     for (int g0 = 0; g0 < ngr; g0 += kFinG) {
@@ -147,9 +149,11 @@ __device__ void bn_fwd_final(const double *__restrict__ gpart, int64_t n, int ng
         for (int u = 0; u < kFinR; ++u)
             if (g0 + 4 * u < ngr) a += g0 + p + 4 * u < ngr ? f.vs[u] : 0.0;
     }
-    mean = quad_sum(a) / static_cast<double>(n);
+    const double sum = quad_sum(a);
+    if (S) *S = sum;
+    mean = sum / static_cast<double>(n);
     const int glast = ngr - 1;
-    const double nlast = rows_in(n, int64_t(glast) * kGroup * TM, kGroup * TM);
+    const double nlast = rows_in(n, int64_t(glast) * UNIT, UNIT);
     const bool last_partial = nlast != kFull;
     double q = 0.0, last_vq = 0.0, last_d = 0.0;
     bool owns_last = false;
@@ -282,9 +286,40 @@ __device__ void bn_fwd_hier(const float *__restrict__ part, int64_t n, int64_t t
         if (threadIdx.x == 0) fz.counters[g] = 0u;
     }
     if (fz.defer) return;  // the consumer kernel finishes (bn_fwd_final there)
-    if (!block_arrive(&fz.counters[fz.ngr_cap], ngr)) return;
     double mean, M2;
     FwdFin fin;
+    if (ngr > kFinG) {  // block-uniform
+        // more groups than one load round: a third level, so that no single
+        // workgroup walks every group partial in series at the end of the
+        // kernel (1172 groups at 1.2 M rows: ~74 us of dependent load rounds).
+        // The last group of each 64-group supergroup combines its groups
+        // (one round), the last supergroup combines the supergroups.
+        constexpr int64_t kSupRows = int64_t(kFinG) * kGroup * TM;
+        const int s = g / kFinG, nsup = (ngr + kFinG - 1) / kFinG;
+        const int ssize = ngr - s * kFinG < kFinG ? ngr - s * kFinG : kFinG;
+        unsigned *scnt = &fz.counters[fz.ngr_cap + 1 + s];
+        if (!block_arrive(scnt, ssize)) return;
+        const double *gp = fz.gpart + int64_t(s) * kFinG * 128;
+        double *sp = fz.gpart + int64_t(fz.ngr_cap) * 128;
+        const int64_t ns = static_cast<int64_t>(rows_in(n, s * kSupRows, kSupRows));
+        double S;
+        bn_fwd_fin_load<true>(gp, ssize, 0, fin);
+        bn_fwd_final<true>(gp, ns, ssize, fin, mean, M2, &S);
+        if ((threadIdx.x & 63) < 16) {
+            st_agent(sp + int64_t(s) * 128 + fin_channel(), S);
+            st_agent(sp + int64_t(s) * 128 + 64 + fin_channel(), M2);
+        }
+        if (threadIdx.x == 0) *scnt = 0u;
+        if (!block_arrive(&fz.counters[fz.ngr_cap], nsup)) return;
+        const float gam = fz.gamma[fin_channel()], bet = fz.beta[fin_channel()];
+        bn_fwd_fin_load<true>(sp, nsup, 0, fin);
+        bn_fwd_final<true, kSupRows>(sp, n, nsup, fin, mean, M2);
+        bn_fwd_publish(fin_channel(), mean, M2, n, gam, bet, fz.eps, fz.momentum, fz.rmean,
+                       fz.rvar, fz.nbt, fz.stat, (threadIdx.x & 63) < 16);
+        if (threadIdx.x == 0) fz.counters[fz.ngr_cap] = 0u;
+        return;
+    }
+    if (!block_arrive(&fz.counters[fz.ngr_cap], ngr)) return;
     const float gam = fz.gamma[fin_channel()], bet = fz.beta[fin_channel()];
     bn_fwd_fin_load<true>(fz.gpart, ngr, 0, fin);
     bn_fwd_final<true>(fz.gpart, n, ngr, fin, mean, M2);
@@ -369,8 +404,27 @@ __device__ void bn_bwd_hier_s(const float *__restrict__ part, int64_t n, int64_t
         if (threadIdx.x == 0) bz.counters[g] = 0u;
     }
     if (bz.defer) return;  // the layer's gin_bwd_k finishes (bn_bwd_final there)
-    if (!block_arrive(&bz.counters[bz.ngr_cap], ngr)) return;
     BwdFin fin;
+    if (ngr > kFinG) {  // block-uniform: the third level, as in bn_fwd_hier
+        const int s = g / kFinG, nsup = (ngr + kFinG - 1) / kFinG;
+        const int ssize = ngr - s * kFinG < kFinG ? ngr - s * kFinG : kFinG;
+        unsigned *scnt = &bz.counters[bz.ngr_cap + 1 + s];
+        if (!block_arrive(scnt, ssize)) return;
+        const double *gp = bz.gpart + int64_t(s) * kFinG * 128;
+        double *sp = bz.gpart + int64_t(bz.ngr_cap) * 128;
+        bn_bwd_fin_load<true>(gp, ssize, 0, fin);
+        const double st = bn_bwd_final<true>(gp, ssize, fin);
+        if ((threadIdx.x & 63) < 32) st_agent(sp + int64_t(s) * 128 + bfin_index(), st);
+        if (threadIdx.x == 0) *scnt = 0u;
+        if (!block_arrive(&bz.counters[bz.ngr_cap], nsup)) return;
+        bn_bwd_fin_load<true>(sp, nsup, 0, fin);
+        const double tot = bn_bwd_final<true>(sp, nsup, fin);
+        if ((threadIdx.x & 63) < 32)
+            bn_bwd_publish(bfin_index(), tot, n, bz.training, bz.dgamma, bz.dbeta, bz.coef);
+        if (threadIdx.x == 0) bz.counters[bz.ngr_cap] = 0u;
+        return;
+    }
+    if (!block_arrive(&bz.counters[bz.ngr_cap], ngr)) return;
     bn_bwd_fin_load<true>(bz.gpart, ngr, 0, fin);
     const double tot = bn_bwd_final<true>(bz.gpart, ngr, fin);
     if ((threadIdx.x & 63) < 32)
@@ -1701,15 +1755,23 @@ extern "C" int scgib_gin_layer_fwd(const float *h_in, int32_t d_in, const float 
 }
 
 static int64_t bn_groups(int64_t n_nodes) { return (scgib_gin_tiles(n_nodes) + kGroup - 1) / kGroup; }
+// 64-group supergroups (the third statistics level past one load round of groups)
+static int64_t bn_supergroups(int64_t n_nodes) {
+    const int64_t g = bn_groups(n_nodes);
+    return g > kFinG ? (g + kFinG - 1) / kFinG : 0;
+}
 
 extern "C" int64_t scgib_gin_bn_ws_floats(int64_t n_nodes) {
     if (n_nodes <= 0) return 0;
     // tile stats [tiles][128] f32 | (8-byte aligned) group partials [groups][128] f64
-    return ((scgib_gin_tiles(n_nodes) * 128 + 1) & ~int64_t(1)) + 2 * 128 * bn_groups(n_nodes);
+    // | supergroup partials [supergroups][128] f64
+    return ((scgib_gin_tiles(n_nodes) * 128 + 1) & ~int64_t(1)) +
+           2 * 128 * (bn_groups(n_nodes) + bn_supergroups(n_nodes));
 }
 
+// [groups] group counters | [1] the layer counter | [supergroups] supergroup counters
 extern "C" int64_t scgib_gin_counters(int64_t n_nodes) {
-    return n_nodes <= 0 ? 0 : bn_groups(n_nodes) + 1;
+    return n_nodes <= 0 ? 0 : bn_groups(n_nodes) + 1 + bn_supergroups(n_nodes);
 }
 
 extern "C" int64_t scgib_gin_bn_gpart_offset(int64_t n_nodes) {
@@ -2044,7 +2106,7 @@ static int mlp2_recon_fwd(const float *x, int32_t d_in, int64_t n_nodes, const f
                           float *out, const int32_t *rowptr, const int32_t *col, int64_t n_edges,
                           float *ws, uint32_t *counter, float *loss, const int32_t *dims,
                           const ContrastArgs &con, const scgib_running_update *ru,
-                          scgib_stream_t stream) {
+                          const uint32_t *fault, scgib_stream_t stream) {
     if (n_nodes <= 0 || n_edges < 0 || (d_in != 64 && d_in != 128)) return SCGIB_EINVAL;
     if (!x || !w1 || !b1 || !w2 || !b2 || !r || !out || !rowptr || (n_edges > 0 && !col) || !ws ||
         !counter || !loss)
@@ -2069,7 +2131,8 @@ static int mlp2_recon_fwd(const float *x, int32_t d_in, int64_t n_nodes, const f
                       grid <= (d_in == 128 ? recon_fold_slots<128>() : recon_fold_slots<64>());
     if (fold) {
         rec.fin = ReconFin{ws, out, rowptr, col, n_edges, gram, wsd,
-                           reinterpret_cast<unsigned *>(counter), loss};
+                           reinterpret_cast<unsigned *>(counter), loss,
+                           reinterpret_cast<const unsigned *>(fault)};
         rec.fin_on = 1;
         if (with_ru) {
             rec.ru_block = static_cast<int>(nt + ncon);
@@ -2083,7 +2146,7 @@ static int mlp2_recon_fwd(const float *x, int32_t d_in, int64_t n_nodes, const f
     const int rc = launch_status();
     if (rc != SCGIB_OK || fold) return rc;
     return launch_recon_fin(ws, out, rowptr, col, n_nodes, n_edges, gram, wsd, counter, loss, dims,
-                            ru, st);
+                            ru, reinterpret_cast<const unsigned *>(fault), st);
 }
 
 extern "C" int scgib_mlp2_recon_fwd(const float *x, int32_t d_in, int64_t n_nodes,
@@ -2091,9 +2154,10 @@ extern "C" int scgib_mlp2_recon_fwd(const float *x, int32_t d_in, int64_t n_node
                                     const float *b2, float *r, float *out,
                                     const int32_t *rowptr, const int32_t *col, int64_t n_edges,
                                     float *ws, uint32_t *counter, float *loss,
-                                    const int32_t *dims, scgib_stream_t stream) {
+                                    const int32_t *dims, const uint32_t *fault,
+                                    scgib_stream_t stream) {
     return mlp2_recon_fwd(x, d_in, n_nodes, w1, b1, w2, b2, r, out, rowptr, col, n_edges, ws,
-                          counter, loss, dims, ContrastArgs{}, nullptr, stream);
+                          counter, loss, dims, ContrastArgs{}, nullptr, fault, stream);
 }
 
 static bool contrast_ok(const float *z1, const float *z2, int64_t n_graphs, const float *cws,
@@ -2107,7 +2171,8 @@ extern "C" int scgib_mlp2_recon_contrastive_fwd(
     const float *w2, const float *b2, float *r, float *out, const int32_t *rowptr,
     const int32_t *col, int64_t n_edges, float *ws, uint32_t *counter, float *loss,
     const int32_t *dims, const float *z1, const float *z2, int64_t n_graphs, float *cws,
-    float *closs, uint32_t *ccounters, const scgib_running_update *ru, scgib_stream_t stream) {
+    float *closs, uint32_t *ccounters, const scgib_running_update *ru, const uint32_t *fault,
+    scgib_stream_t stream) {
     if (!contrast_ok(z1, z2, n_graphs, cws, ccounters, d_in) || !closs) return SCGIB_EINVAL;
     if (ru && ru->n_graphs > 0 && (!ru->stats || !ru->graph_ptr || !ru->running_mean || !ru->running_var))
         return SCGIB_EINVAL;
@@ -2130,7 +2195,7 @@ extern "C" int scgib_mlp2_recon_contrastive_fwd(
         con.nsplit = static_cast<int>(fit);
     }
     return mlp2_recon_fwd(x, d_in, n_nodes, w1, b1, w2, b2, r, out, rowptr, col, n_edges, ws,
-                          counter, loss, dims, con, ru, stream);
+                          counter, loss, dims, con, ru, fault, stream);
 }
 
 static int mlp2_recon_bwd(const float *x, const float *r, const float *out, const float *ws,

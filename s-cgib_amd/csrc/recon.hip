@@ -217,9 +217,9 @@ __global__ __launch_bounds__(256) void recon_fin_k(const ReconFin a, int64_t nca
 int launch_recon_fin(const float *gslab, const float *im, const int32_t *rowptr,
                      const int32_t *col, int64_t n_nodes, int64_t n_edges, float *gram,
                      double *wsd, unsigned *cnt, float *loss, const int32_t *dims,
-                     const scgib_running_update *ru, hipStream_t st) {
+                     const scgib_running_update *ru, const unsigned *fault, hipStream_t st) {
     const bool with_ru = ru && ru->n_graphs > 0;
-    const ReconFin a{gslab, im, rowptr, col, n_edges, gram, wsd, cnt, loss};
+    const ReconFin a{gslab, im, rowptr, col, n_edges, gram, wsd, cnt, loss, fault};
     recon_fin_k<<<kFinBlocks + (with_ru ? 1 : 0), 256, 0, st>>>(
         a, n_nodes, dims, with_ru ? *ru : scgib_running_update{});
     return launch_status();

@@ -38,6 +38,8 @@ struct ReconFin {
     unsigned *cnt;           // [0] arrivals of the virtual blocks, [1] (fused) tile arrivals,
                              // [2] (fused) wait-timeout flag; all left zero
     float *loss;
+    const unsigned *fault;   // sticky hand-off fault word (scgib_stream_wait), or nullptr:
+                             // while it is set the loss is NaN
 };
 
 __device__ __forceinline__ int recon_fin_vblocks(int64_t n) {
@@ -139,6 +141,10 @@ __device__ void recon_fin_block(int vb, const ReconFin &a, int64_t ncap, const i
             __hip_atomic_store(&a.cnt[1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_store(&a.cnt[2], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
+        // a cross-queue hand-off of this or an earlier step gave up waiting:
+        // some kernel read data before it was written, so no loss is reported
+        if (a.fault && __hip_atomic_load(a.fault, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u)
+            timed_out = true;
         *a.loss = timed_out ? __builtin_nanf("") : static_cast<float>(l);
         __hip_atomic_store(&a.cnt[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // next launch / replay
     }

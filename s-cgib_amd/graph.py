@@ -485,7 +485,8 @@ def _egonet_k1(g, ego_ptr, ego_eptr, ws, x, max_in_degree=12):
         state = ops.scan_state(dev, "egonet_k1_scan", int(_lib.query("scgib_egonet_k1_scan_words", n)))
         ops._launch("scgib_egonet_k1_build_onepass", {"n": n}, _ptr(g.rowptr), _ptr(g.col), n,
                   int(max_in_degree), _ptr(ego_ptr), _ptr(ego_eptr), _ptr(state), _ptr(ego_nodes),
-                  _ptr(sub_rowptr), _ptr(sub_col), n_s, _ptr(g.dims), _ptr(ego_dims), _stream())
+                  _ptr(sub_rowptr), _ptr(sub_col), n_s, max(e_cap, 1),
+                  _ptr(getattr(g, "err_buf", None)), _ptr(g.dims), _ptr(ego_dims), _stream())
     else:
         _lib.call("scgib_egonet_k1_build_deg", _ptr(g.rowptr), _ptr(g.col), n,
                   int(max_in_degree), _ptr(ego_ptr), _ptr(ego_eptr), _ptr(ws), _ptr(ego_nodes),
@@ -725,7 +726,8 @@ class EgoPrefetch:
                                    int(_lib.query("scgib_egonet_k1_scan_words", self.n)))
             _lib.call("scgib_egonet_k1_build_onepass_pool", *src, o_rp, o_col, o_dims, self.n,
                       self.dmax, _ptr(ego_ptr), _ptr(ego_eptr), _ptr(state), _ptr(ego_nodes),
-                      _ptr(sub_rowptr), _ptr(sub_col), self.n_s, _ptr(ego_dims), _stream())
+                      _ptr(sub_rowptr), _ptr(sub_col), self.n_s, max(self.e_cap, 1), _ptr(err),
+                      _ptr(ego_dims), _stream())
             return
         g = self.static.graph
         mgn = max(g.max_graph_nodes, 1)

@@ -405,7 +405,9 @@ class _GinEncoder(torch.autograd.Function):
         bn_wss = [torch.empty(ws_floats, dtype=torch.float32, device=dev)
                   for _ in range(2 if defer_ok else 1)]
         gpart_off = 4 * int(_lib.query("scgib_gin_bn_gpart_offset", n))
-        cnt = counters(dev, ("gin", id(gin)), int(_lib.query("scgib_gin_counters", n))) \
+        # (keyed by call site and stream: concurrent encoders run on different
+        # streams, launches on one stream are ordered and leave the words zero)
+        cnt = scan_state(dev, "gin_fwd", int(_lib.query("scgib_gin_counters", n))) \
             if fused else None
         saved, h, stat_prev, aggx, pend = [], h0, None, None, None
         for l in range(L):
@@ -477,7 +479,7 @@ class _GinEncoder(torch.autograd.Function):
         ctx.graph, ctx.L, ctx.training, ctx.pre = graph, L, training, pre
         ctx.n_feat = x.shape[1] if pre else None
         ctx.opes = [c._one_plus_eps for c in gin.ginlayers]
-        ctx.cnt_key = ("gin_bwd", id(gin))
+        ctx.cnt_key = "gin_bwd"
         return out if ro is None else (out, ro)
 
     @staticmethod
@@ -504,7 +506,7 @@ class _GinEncoder(torch.autograd.Function):
         st = _stream()
         bn_ws = torch.empty(int(_lib.query("scgib_gin_bn_ws_floats", n)), dtype=torch.float32,
                             device=dev)
-        cnt = counters(dev, ctx.cnt_key, int(_lib.query("scgib_gin_counters", n)))
+        cnt = scan_state(dev, ctx.cnt_key, int(_lib.query("scgib_gin_counters", n)))
         # deferred BN-backward finalize: each layer's gin_bwd_k finishes the sums
         defer = int(DEFER_BN and n <= int(_lib.query("scgib_gin_defer_max_nodes")))
         gpart = bn_ws.data_ptr() + 4 * int(_lib.query("scgib_gin_bn_gpart_offset", n))
@@ -674,14 +676,34 @@ def _xq_words(device, key):
         return counters(device, ("xq", key), 4)
 
 
+def handoff_fault_word(device):
+    """The device's sticky hand-off fault word: a wait that gave up sets it,
+    and the pretraining loss kernels (scgib_mlp2_recon(_contrastive)_fwd)
+    report a NaN recon loss while it is set — a step whose kernels may have
+    read unwritten data never yields a finite loss.  One word per device,
+    whichever stream asks."""
+    with torch.cuda.stream(torch.cuda.default_stream(device)):
+        return counters(device, "handoff_fault", 1)
+
+
+def handoff_fault(device):
+    """True once a hand-off wait on ``device`` has given up (sticky)."""
+    return bool(handoff_fault_word(device).item())
+
+
+def clear_handoff_fault(device):
+    handoff_fault_word(device).zero_()
+
+
 def _xq_handoff(producer, consumer, key):
     """Order ``consumer``'s later work after ``producer``'s work so far
     (scgib_stream_signal on producer, scgib_stream_wait on consumer)."""
     w = _xq_words(producer.device, key)
+    fault = handoff_fault_word(producer.device)
     with torch.cuda.stream(producer):
         _lib.call("scgib_stream_signal", _p(w), _stream())
     with torch.cuda.stream(consumer):
-        _lib.call("scgib_stream_wait", _p(w), _stream())
+        _lib.call("scgib_stream_wait", _p(w), _p(fault), _stream())
 
 
 def xq_timeouts(device):
@@ -717,19 +739,6 @@ class _GinEncoderPair(torch.autograd.Function):
         check_fork(main)
         ctx.lin = w0 is not None
         ctx.lin_leaves = (w0, b0)
-        if _pair_persistent_ok(x, ego, core, gin_ego, gin_core, training, w0):
-            # both encoders in ONE persistent launch on the current stream,
-            # after the ego-net build (``side``) and the noise draw (here)
-            if core_tail is not None:
-                core_tail()
-            main.wait_stream(side)
-            ctx.persistent = True
-            if side_tail is not None:  # joined by its owner (EgoPrefetch.join)
-                with torch.cuda.stream(side):
-                    side_tail()
-            return _pair_forward_persistent(ctx, x, wt, w0, b0, nmap, ego, core, gin_ego,
-                                            gin_core, params)
-        ctx.persistent = False
         side.wait_stream(main)
         if core_tail is not None:  # beside the ego-net build
             core_tail()
@@ -772,8 +781,6 @@ class _GinEncoderPair(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, g_s, g_ro, g_f, g_t=None):
-        if ctx.persistent:
-            return _pair_backward_persistent(ctx, g_s, g_ro, g_f, g_t)
         # backward: the ego chain (the longer one) stays on the current stream,
         # where its weight-gradient reduces can fork to the aux stream (a fork
         # from an already-forked stream breaks HIP-graph capture on this
@@ -848,257 +855,6 @@ class _GinEncoderPair(torch.autograd.Function):
 
 def _torch_stream():
     return torch.cuda.current_stream()
-
-
-# The encoder pair's forward as ONE persistent launch (scgib_gin_pair_fwd,
-# gin_pair.hip) when it applies: training with batch statistics, both graphs
-# made of closed components of <= scgib_gin_pair_max_component() rows, and
-# both encoders' chunks co-resident on the device.  Otherwise the per-layer
-# kernels.  (A module attribute: the tests run both paths.)
-PAIR_PERSISTENT = False  # (on once validated on the GPU)
-# diagnostics (tools/pair_trace.py): None, or two int64 device tensors
-# [grid * 64] receiving the forward's / backward's per-workgroup phase stamps
-PAIR_TRACE = None
-
-
-def pair_sync_error(device):
-    """The persistent pair forward's timeout word (0: none; a bounded spin
-    that gave up writes its code) — read by the tests, not in the step."""
-    return int(counters(device, ("gin_pair_sync",), 4)[1].item())
-
-
-def _pair_persistent_ok(x, ego, core, gin_ego, gin_core, training, w0):
-    L = len(gin_ego.ginlayers)
-    if not (PAIR_PERSISTENT and training and L == len(gin_core.ginlayers)
-            and 1 <= L <= _lib.PAIR_MAX_LAYERS and x.shape[1] <= 16):
-        return False
-    if w0 is not None and tuple(w0.shape) != (HIDDEN, HIDDEN):
-        return False
-    for gr, gin in ((ego, gin_ego), (core, gin_core)):
-        if not (getattr(gr, "components_closed", False) and gr.symmetric and gr.num_nodes() > 0
-                and gr.batch_size > 0):
-            return False
-        if not 1 <= gr.max_graph_nodes <= int(_lib.query("scgib_gin_pair_max_component")):
-            return False
-        for conv, bn in zip(gin.ginlayers, gin.batch_norms):
-            mlp = conv.apply_func.mlp
-            if not (bn.track_running_stats and bn.momentum is not None and bn.affine):
-                return False
-            if mlp[2].weight.shape != (HIDDEN, HIDDEN):
-                return False
-    chunks = sum(int(_lib.query("scgib_gin_pair_chunks", gr.num_nodes())) for gr in (ego, core))
-    return chunks <= int(_lib.query("scgib_gin_pair_slots"))
-
-
-def _comp_dims(gr):
-    """Device count of gr's valid components in capacity mode: an ego batch
-    has one ego-net per actual molecule node (its seg_dims[0]); its
-    graph_ptr entries past that count are not maintained."""
-    sd = getattr(gr, "seg_dims", None)
-    return sd.data_ptr() if (gr.dims is not None and sd is not None) else None
-
-
-def _pair_backward_persistent(ctx, g_s, g_ro, g_f, g_t):
-    """_GinEncoderPair.backward through scgib_gin_pair_bwd (one launch, both
-    encoders, compressor[0]'s backward first on Encoder1's chunks), then ONE
-    fixed-order reduce of every layer's per-chunk weight-gradient partials —
-    both encoders' transfer_d partials summed as one job (no add of two
-    d Wt), the loss section's deferred slabs (SlabScope) in the same launch."""
-    dev = ctx.sub[0].saved_tensors[2].device
-    L = ctx.sub[0].L
-    F = ctx.sub[0].n_feat
-    args = _lib.PairBwdArgs()
-    args.n_layers, args.n_feat = L, F
-    args.sync = counters(dev, ("gin_pair_sync",), 4).data_ptr()
-    if PAIR_TRACE is not None:
-        args.trace = PAIR_TRACE[1].data_ptr()
-    keep, jobs = [], []
-    nchs = [int(_lib.query("scgib_gin_pair_chunks", ctx.sub[e].saved_tensors[2].shape[0]))
-            for e in (0, 1)]
-    w0_width = HIDDEN * HIDDEN + HIDDEN * 32 + 2 * HIDDEN      # layer 0: W2 | W1 | b2 | b1
-    l0_stride = int(_lib.query("scgib_gin_layer0_slab_width"))  # + the 32 x 16 dWt tail
-    slab0 = torch.empty((nchs[0] + nchs[1]) * l0_stride, dtype=torch.float32, device=dev)
-    keep.append(slab0)
-    dwt = torch.empty(32, F, dtype=torch.float32, device=dev)
-    jobs.append(_lib.SlabJob(slab0.data_ptr() + 4 * w0_width, dwt.data_ptr(), 32 * F,
-                             nchs[0] + nchs[1], l0_stride))
-    grads = ([None] * (6 * L), [None] * (6 * L))
-    dw0 = db0 = None
-    g_in = ((g_s, g_ro), (g_f, None))
-    for e in (0, 1):
-        sub = ctx.sub[e]
-        t = sub.saved_tensors
-        saved, params, aggx = t[: 4 * L], t[4 * L: 4 * L + 6 * L], t[-1]
-        gr = sub.graph
-        n = saved[2].shape[0]
-        E = args.enc[e]
-        E.rowptr, E.col = gr.rowptr.data_ptr(), gr.col.data_ptr()
-        E.comp_ptr, E.n_comp = gr.graph_ptr.data_ptr(), gr.batch_size
-        E.comp_dims = _comp_dims(gr)
-        E.dims = gr.dims.data_ptr() if gr.dims is not None else None
-        E.n_cap = n
-        E.aggx = aggx.data_ptr()
-        g_out, g_read = g_in[e]
-        if g_out is not None:
-            g_out = _f32(g_out, "gin_encoder_pair.backward")
-            keep.append(g_out)
-            E.g_out = g_out.data_ptr()
-        if g_read is not None:
-            g_read = _f32(g_read, "gin_encoder_pair.backward readout")
-            keep.append(g_read)
-            E.g_readout = g_read.data_ptr()
-        for l in range(L):
-            agg, r, z2, stat = saved[4 * l: 4 * l + 4]
-            w1, w2 = _f32(params[6 * l], "w1"), _f32(params[6 * l + 2], "w2")
-            keep += [w1, w2]
-            E.agg[l], E.r[l], E.z2[l], E.stat[l] = (x.data_ptr() for x in (agg, r, z2, stat))
-            E.w1[l], E.w2[l] = w1.data_ptr(), w2.data_ptr()
-            E.one_plus_eps[l] = sub.opes[l]
-            bn_g = torch.empty(2, HIDDEN, dtype=torch.float32, device=dev)
-            E.dgamma[l], E.dbeta[l] = bn_g[0].data_ptr(), bn_g[1].data_ptr()
-            d_in = agg.shape[1]
-            width = HIDDEN * HIDDEN + HIDDEN * d_in + 2 * HIDDEN
-            wgrad = torch.empty(width, dtype=torch.float32, device=dev)
-            if l == 0:
-                E.slab[l] = slab0.data_ptr() + 4 * (nchs[0] * l0_stride if e else 0)
-                E.slab_stride[l] = l0_stride
-                jobs.append(_lib.SlabJob(E.slab[l], wgrad.data_ptr(), width, nchs[e], l0_stride))
-            else:
-                slab = torch.empty(nchs[e] * width, dtype=torch.float32, device=dev)
-                keep.append(slab)
-                E.slab[l], E.slab_stride[l] = slab.data_ptr(), width
-                jobs.append(_lib.SlabJob(slab.data_ptr(), wgrad.data_ptr(), width, nchs[e], 0))
-            o = HIDDEN * HIDDEN
-            gl = grads[e]
-            gl[6 * l + 2] = wgrad[:o].view(HIDDEN, HIDDEN)
-            gl[6 * l + 0] = wgrad[o:o + HIDDEN * d_in].view(HIDDEN, d_in)
-            o += HIDDEN * d_in
-            gl[6 * l + 3] = wgrad[o:o + HIDDEN]
-            gl[6 * l + 1] = wgrad[o + HIDDEN:o + 2 * HIDDEN]
-            gl[6 * l + 4] = bn_g[0]
-            gl[6 * l + 5] = bn_g[1]
-        ws = torch.empty(int(_lib.query("scgib_gin_pair_ws_bytes", n, L)), dtype=torch.uint8,
-                         device=dev)
-        keep.append(ws)
-        E.ws = ws.data_ptr()
-        E.chunk_rec = sub.chunk_rec.data_ptr()
-        E.counters = scan_state(dev, ("gin_pair_bwd", e), int(_lib.query("scgib_gin_pair_counters", n, L))).data_ptr()
-        if e == 1 and ctx.lin and g_t is not None:
-            f, w0 = ctx.lin_saved
-            g_t = _f32(g_t, "compressor.0 grad")
-            keep.append(g_t)
-            E.lin_g, E.lin_w, E.lin_in = g_t.data_ptr(), w0.data_ptr(), f.data_ptr()
-            lin_slab = torch.empty(nchs[1] * (HIDDEN * HIDDEN + HIDDEN), dtype=torch.float32,
-                                   device=dev)
-            keep.append(lin_slab)
-            E.lin_slab = lin_slab.data_ptr()
-            wg0 = torch.empty(HIDDEN * HIDDEN + HIDDEN, dtype=torch.float32, device=dev)
-            jobs.append(_lib.SlabJob(lin_slab.data_ptr(), wg0.data_ptr(), wg0.numel(), nchs[1], 0))
-            dw0, db0 = wg0[: HIDDEN * HIDDEN].view(HIDDEN, HIDDEN), wg0[HIDDEN * HIDDEN:]
-    meta = None if OBSERVER is None else {
-        "layers": [(ctx.sub[e].graph.num_nodes(), ctx.sub[e].graph.edge_capacity(),
-                    32 if l == 0 else HIDDEN) for e in (0, 1) for l in range(L)]}
-    _launch("scgib_gin_pair_bwd", meta, ctypes.cast(ctypes.pointer(args), ctypes.c_void_p),
-            _stream())
-    scope = ctx.scope if (ctx.scope is not None and ctx.scope.open) else None
-    if scope is not None:  # the loss section's deferred slabs: the same reduce launch
-        sj, sk = scope.take()
-        jobs += sj
-        keep += sk
-    _reduce_jobs(jobs, _stream())
-    del keep  # (slabs stay allocated until the reduce is enqueued)
-    return (None, dwt, dw0, db0, None, None, None, None, None, None, None, None, *grads[0],
-            *grads[1])
-
-
-def _pair_forward_persistent(ctx, x, wt, w0, b0, nmap, ego, core, gin_ego, gin_core, params):
-    """_GinEncoderPair.forward through scgib_gin_pair_fwd: fills ctx.sub[0]
-    (Encoder2, ego-nets) and ctx.sub[1] (Encoder1) with exactly what the
-    per-layer forward saves, so the backward is the same."""
-    x = _f32(x, "gin_encoder x")
-    wt = _f32(wt, "transfer_d.weight")
-    dev = x.device
-    L = len(gin_ego.ginlayers)
-    ne = 6 * L
-    args = _lib.PairFwdArgs()
-    args.x, args.n_feat, args.wt, args.n_layers = x.data_ptr(), x.shape[1], wt.data_ptr(), L
-    args.sync = counters(dev, ("gin_pair_sync",), 4).data_ptr()
-    if PAIR_TRACE is not None:
-        args.trace = PAIR_TRACE[0].data_ptr()
-    keep = [x, wt]
-    outs = []
-    for e, (gr, gin, prm) in enumerate(((ego, gin_ego, params[:ne]), (core, gin_core, params[ne:]))):
-        n = gr.num_nodes()
-        E = args.enc[e]
-        E.rowptr, E.col = gr.rowptr.data_ptr(), gr.col.data_ptr()
-        E.comp_ptr, E.n_comp = gr.graph_ptr.data_ptr(), gr.batch_size
-        E.comp_dims = _comp_dims(gr)
-        E.dims = gr.dims.data_ptr() if gr.dims is not None else None
-        E.n_cap = n
-        E.node_map = nmap.data_ptr() if (e == 0 and nmap is not None) else None
-        saved = []
-        for l in range(L):
-            conv, bn = gin.ginlayers[l], gin.batch_norms[l]
-            w1, b1, w2, b2, gamma, beta = (_f32(p, "gin param") for p in prm[6 * l: 6 * l + 6])
-            d_in = 32 if l == 0 else HIDDEN
-            if w1.shape != (HIDDEN, d_in):
-                raise _lib.ScgibError(f"fused GIN layer {l} needs Linear({d_in}, 64)")
-            keep += [w1, b1, w2, b2, gamma, beta]
-            E.w1[l], E.b1[l], E.w2[l], E.b2[l] = (t.data_ptr() for t in (w1, b1, w2, b2))
-            E.gamma[l], E.beta[l] = gamma.data_ptr(), beta.data_ptr()
-            E.one_plus_eps[l] = conv._one_plus_eps
-            E.bn_eps[l], E.momentum[l] = float(bn.eps), float(bn.momentum)
-            E.running_mean[l] = bn.running_mean.data_ptr()
-            E.running_var[l] = bn.running_var.data_ptr()
-            E.num_batches_tracked[l] = bn.num_batches_tracked.data_ptr()
-            agg = torch.empty(n, d_in, dtype=torch.float32, device=dev)
-            r = torch.empty(n, HIDDEN, dtype=torch.float32, device=dev)
-            z2 = torch.empty(n, HIDDEN, dtype=torch.float32, device=dev)
-            stat = torch.empty(4, HIDDEN, dtype=torch.float32, device=dev)
-            E.agg[l], E.r[l], E.z2[l], E.stat[l] = (t.data_ptr() for t in (agg, r, z2, stat))
-            saved += [agg, r, z2, stat]
-        aggx = torch.empty(n, 16, dtype=torch.float32, device=dev)
-        out = torch.empty(n, HIDDEN, dtype=torch.float32, device=dev)
-        E.aggx, E.out = aggx.data_ptr(), out.data_ptr()
-        ro = seg = t = None
-        if e == 0:
-            ro = torch.empty(gr.batch_size, HIDDEN, dtype=torch.float32, device=dev)
-            seg = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
-            E.readout, E.seg = ro.data_ptr(), seg.data_ptr()
-        elif w0 is not None:
-            w0c, b0c = _f32(w0, "compressor.0.weight"), _f32(b0, "compressor.0.bias")
-            keep += [w0c, b0c]
-            t = torch.empty(n, HIDDEN, dtype=torch.float32, device=dev)
-            E.lin_w, E.lin_b, E.lin_out = w0c.data_ptr(), b0c.data_ptr(), t.data_ptr()
-            ctx.lin_saved = (out.detach(), w0c)  # (an alias: no ctx -> output cycle)
-            ctx.core_dims = gr.dims
-        ws = torch.empty(int(_lib.query("scgib_gin_pair_ws_bytes", n, L)), dtype=torch.uint8,
-                         device=dev)
-        keep.append(ws)
-        E.ws = ws.data_ptr()
-        E.counters = scan_state(dev, ("gin_pair", id(gin)),
-                                int(_lib.query("scgib_gin_pair_counters", n, L))).data_ptr()
-        rec = torch.empty(int(_lib.query("scgib_gin_pair_chunks", n)) *
-                          int(_lib.query("scgib_gin_pair_chunk_rec_ints")), dtype=torch.int32, device=dev)
-        E.chunk_rec = rec.data_ptr()
-        sub = ctx.sub[e]
-        sub.chunk_rec = rec
-        sub.save_for_backward(*saved, *prm, aggx)
-        sub.graph, sub.L, sub.training, sub.pre = gr, L, True, True
-        sub.n_feat = x.shape[1]
-        sub.opes = [c._one_plus_eps for c in gin.ginlayers]
-        sub.cnt_key = ("gin_bwd", id(gin))
-        sub.seg = seg
-        outs += [out, ro] if e == 0 else [out] + ([t] if t is not None else [])
-    # (the sizes only for the bench's kernel timer: an exact-mode ego batch's
-    # edge count is a device read)
-    meta = None if OBSERVER is None else {
-        "layers": [(gr.num_nodes(), gr.edge_capacity(), 32 if l == 0 else HIDDEN)
-                   for gr in (ego, core) for l in range(L)]}
-    _launch("scgib_gin_pair_fwd", meta, ctypes.cast(ctypes.pointer(args), ctypes.c_void_p),
-            _stream())
-    del keep  # (every pointer is read into the kernel arguments at the launch)
-    return tuple(outs)
 
 
 def gin_encoder_pair_x(x, ego, gin_ego, core, gin_core, transfer, node_map, side, lin0=None,
@@ -1425,18 +1181,24 @@ _SCAN_RETIRED = []  # outgrown scan states: a captured graph may still point at 
 
 
 def scan_state(device, key, n):
-    """``n`` zeroed int32 words of O(n) scan state (the one-pass ego builder's
-    look-back words) for call site ``key`` on ``device`` and the current
-    stream, separate from the O(1) counter pool: it grows on demand (a new
-    zeroed tensor; the outgrown one is kept alive, since a captured graph may
-    reference it) and the kernels leave it zeroed for the next launch."""
+    """``n`` zeroed int32 words of O(n) state (the one-pass ego builder's
+    look-back words, a GIN encoder's BatchNorm arrival counters) for call
+    site ``key`` on ``device`` and the current stream, separate from the O(1)
+    counter pool: it grows on demand to the next power of two (a new zeroed
+    tensor; the outgrown one is kept alive, since a captured graph may
+    reference it — at most log2 of the largest size per key) and the kernels
+    leave it zeroed for the next launch.  Keys name call sites, never objects,
+    so a long-lived process that builds new modules reuses the same words."""
     idx = torch.device(device).index or 0
     rk = (idx, key, torch.cuda.current_stream(device).cuda_stream)
     buf = _SCAN_STATES.get(rk)
     if buf is None or buf.numel() < n:
         if buf is not None:
             _SCAN_RETIRED.append(buf)
-        buf = _SCAN_STATES[rk] = torch.zeros(max(n, 1024), dtype=torch.int32, device=device)
+        size = 1024
+        while size < n:
+            size *= 2
+        buf = _SCAN_STATES[rk] = torch.zeros(size, dtype=torch.int32, device=device)
     return buf[:n]
 
 
@@ -1586,7 +1348,7 @@ class _Mlp2Recon(torch.autograd.Function):
         cnt = counters(dev, "mlp2_recon", 3)
         _lib.call("scgib_mlp2_recon_fwd", _p(x), d_in, n, _p(w1), _p(b1), _p(w2), _p(b2), _p(r),
                   _p(out), _p(graph.rowptr), _p(graph.col), graph.edge_capacity(), _p(ws),
-                  _p(cnt), _p(loss), _p(graph.dims), _stream())
+                  _p(cnt), _p(loss), _p(graph.dims), _p(handoff_fault_word(dev)), _stream())
         ctx.save_for_backward(x, r, out, ws, w1, w2)
         ctx.graph = graph
         return loss
@@ -1652,7 +1414,7 @@ class _Mlp2ReconContrastive(torch.autograd.Function):
                   _p(b2), _p(r), _p(out), _p(graph.rowptr), _p(graph.col),
                   graph.edge_capacity(), _p(ws), _p(cnt), _p(loss), _p(graph.dims), _p(z1),
                   _p(z2), B, _p(cws), _p(closs), _p(ccnt), _byref(ru[0] if ru else None),
-                  _stream())
+                  _p(handoff_fault_word(dev)), _stream())
         ctx.save_for_backward(x, r, out, ws, w1, w2, z1, z2, cws)
         ctx.graph = graph
         return loss, closs

@@ -71,7 +71,9 @@ class Adam(torch.optim.Optimizer):
             for li, i0 in enumerate(range(0, len(ent), self._max)):
                 chunk = ent[i0:i0 + self._max]
                 table = (_lib.AdamTensor * len(chunk))(*chunk)
-                cnt = ops.counters(dev, ("adam", id(self), gi, li), 1)
+                # one word per stream (launches on a stream are ordered, and each
+                # leaves it zero): not per optimizer, so new optimizers reuse it
+                cnt = ops.counters(dev, "adam", 1)
                 _lib.call("scgib_adam_step", ctypes.cast(table, ctypes.c_void_p), len(chunk),
                           float(group["lr"]), float(b1), float(b2), float(group["eps"]),
                           float(group["weight_decay"]), ops._p(cnt), st)

@@ -62,14 +62,34 @@ def pickle_globals(path):
         if len(pk) != 1:
             raise RefCheckpointError(f"{path}: not a torch zip checkpoint")
         data = z.read(pk[0])
-    out, strs = set(), []
+    # STACK_GLOBAL takes module and name from the stack: they are the two
+    # values pushed just before it, each a unicode literal or a memo fetch of
+    # one (BINGET after MEMOIZE / BINPUT).  Every other opcode is recorded as an
+    # unknown value, so a STACK_GLOBAL whose operands cannot be resolved here
+    # is refused rather than misnamed.
+    out, pushed, memo = set(), [], {}
     for op, arg, _ in pickletools.genops(io.BytesIO(data)):
-        if op.name in ("SHORT_BINUNICODE", "BINUNICODE", "UNICODE", "BINUNICODE8"):
-            strs.append(arg)
-        elif op.name == "GLOBAL":
+        name = op.name
+        if name in ("SHORT_BINUNICODE", "BINUNICODE", "UNICODE", "BINUNICODE8"):
+            pushed.append(arg)
+        elif name == "MEMOIZE":
+            memo[len(memo)] = pushed[-1] if pushed else None
+        elif name in ("PUT", "BINPUT", "LONG_BINPUT"):
+            memo[arg] = pushed[-1] if pushed else None
+        elif name in ("GET", "BINGET", "LONG_BINGET"):
+            pushed.append(memo.get(arg))
+        elif name == "GLOBAL":
             out.add(arg.replace(" ", "."))
-        elif op.name == "STACK_GLOBAL":
-            out.add(f"{strs[-2]}.{strs[-1]}")
+            pushed.append(None)
+        elif name == "STACK_GLOBAL":
+            mod, nm = (pushed[-2], pushed[-1]) if len(pushed) >= 2 else (None, None)
+            if not (isinstance(mod, str) and isinstance(nm, str)):
+                raise RefCheckpointError(f"{path}: a STACK_GLOBAL whose module / name are not "
+                                         "string literals or memo references to them; refused")
+            out.add(f"{mod}.{nm}")
+            pushed.append(None)
+        else:
+            pushed.append(None)
     return out
 
 

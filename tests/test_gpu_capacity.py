@@ -398,3 +398,28 @@ def test_ego_prefetch_forward_only_joins(pkg, dev):
             assert torch.equal(pf.ego.col[:e_s], ref.col[:e_s])
     pf.join()
     assert pf.error() == 0
+
+
+def test_handoff_timeout_poisons_loss(pkg, dev):
+    """A cross-queue hand-off wait that gives up (here: a wait with no signal
+    at all) sets the device's sticky fault word, and from then on the
+    pretraining step reports a NaN recon loss — not finite losses computed
+    from data that may not have been written — until the caller clears it."""
+    ops = pkg.ops
+    ops.clear_handoff_fault(dev)
+    gh = _batches(pkg, (21,))[0]
+    g = gh.to(dev)
+    m = _model(pkg, dev)
+    ug, uf = _noise(g.num_nodes(), dev, 7)
+    ok = _step(m, g, g.ndata["x"], (ug, uf), dev)
+    assert torch.isfinite(ok).all()
+    w = ops._xq_words(dev, "test_orphan_wait")
+    ops._lib.call("scgib_stream_wait", ops._p(w), ops._p(ops.handoff_fault_word(dev)),
+                  ops._stream())
+    torch.cuda.synchronize()
+    assert int(w[2].item()) == 1 and ops.handoff_fault(dev)
+    bad = _step(m, g, g.ndata["x"], (ug, uf), dev)
+    assert torch.isnan(bad[2]) and torch.isnan(bad[3])  # recon, and so the total
+    ops.clear_handoff_fault(dev)
+    again = _step(m, g, g.ndata["x"], (ug, uf), dev)
+    assert torch.isfinite(again).all()

@@ -1,0 +1,58 @@
+"""Arrival-counter and scan-state lifetime:
+counters are keyed by call site and stream, never by module or optimizer
+object, so a long-lived process that keeps building modules (fine-tune sweeps,
+the three runs of exp_tudataset.py:150) reuses the same words instead of
+exhausting the fixed pool.  The kernels leave every word zeroed, which the
+repeated results check: the same module on the same inputs gives bitwise the
+same output whichever stream or word range ran it."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def dev():
+    if not torch.cuda.is_available():
+        pytest.skip("needs a GPU")
+    return torch.device("cuda", 0)
+
+
+def _pool_used(ops, idx=0):
+    return max((o + s for (d, _, _), (o, s) in ops._COUNTER_RANGES.items() if d == idx),
+               default=0)
+
+
+def test_fresh_modules_and_streams_reuse_counters(pkg, dev):
+    ops = pkg.ops
+    mols = pkg.synth.molecules(40, "qm9", seed=3)
+    g = pkg.graph.collate_pyg(mols)[0].to(dev)
+    h0 = torch.randn(g.num_nodes(), 32, device=dev)
+    streams = [torch.cuda.Stream(dev) for _ in range(8)]
+
+    def run(seed, stream):
+        torch.manual_seed(seed)
+        gin = pkg.models.GIN(32, 64, 5).to(dev).train()
+        opt = pkg.optim.Adam(gin.parameters(), lr=1e-3)
+        stream.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(stream):
+            out = gin(g, h0)
+            (out * out).mean().backward()
+            opt.step()
+            res = torch.cat([out.detach().flatten(), gin.ginlayers[0].apply_func.mlp[0].weight
+                             .detach().flatten()])
+        torch.cuda.current_stream().wait_stream(stream)
+        return res
+
+    first = run(0, streams[0])  # allocates this call site's words on every path
+    for s in streams[1:]:
+        run(1, s)
+    torch.cuda.synchronize()
+    used, n_scan = _pool_used(ops), len(ops._SCAN_STATES)
+    for i in range(300):
+        run(1000 + i, streams[i % 8])
+    again = run(0, streams[5])
+    torch.cuda.synchronize()
+    assert _pool_used(ops) == used  # no new counter ranges after the first round
+    assert len(ops._SCAN_STATES) == n_scan
+    assert torch.equal(first, again)  # words left zeroed: the same bits on another stream

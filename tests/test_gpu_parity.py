@@ -183,6 +183,45 @@ def test_egonet_rejects_oversized_graph(pkg, dev):
         pkg.graph.egonet_batch(gh.to(dev), 1)
 
 
+def test_egonet_k1_onepass_flags_capacity_overflow(pkg, dev):
+    """The one-launch k = 1 builder given buffers smaller than the ego batch
+    (a batch past the capacity it was sized for) writes nothing past them and
+    sets error bit 4; with the right capacities it flags nothing, and the scan
+    state comes back zeroed either way (the next launch is exact)."""
+    _, gh = rand_graph(pkg, 64, "qm9", 5, dev)
+    g = gh.to(dev)
+    n = g.num_nodes()
+    info = gh.host_info
+    ball = 1 + info["deg"] - info["selfloops"]
+    n_s, e_s = int(ball.sum()), int((info["deg"] * ball).sum())
+    i32 = torch.int32
+    lib, ops = pkg._lib, pkg.ops
+    state = ops.scan_state(dev, "test_k1_overflow", int(lib.query("scgib_egonet_k1_scan_words", n)))
+
+    def build(ncap, ecap):
+        guard = 64
+        ego_ptr = torch.empty(n + 1, dtype=i32, device=dev)
+        ego_eptr = torch.empty(n + 1, dtype=i32, device=dev)
+        nodes = torch.full((ncap + guard,), -7, dtype=i32, device=dev)
+        rp = torch.full((ncap + 1 + guard,), -7, dtype=i32, device=dev)
+        col = torch.full((ecap + guard,), -7, dtype=i32, device=dev)
+        err = torch.zeros(1, dtype=i32, device=dev)
+        lib.call("scgib_egonet_k1_build_onepass", ops._p(g.rowptr), ops._p(g.col), n, 12,
+                 ops._p(ego_ptr), ops._p(ego_eptr), ops._p(state), ops._p(nodes), ops._p(rp),
+                 ops._p(col), ncap, ecap, ops._p(err), None, None, ops._stream())
+        torch.cuda.synchronize()
+        for t, cap in ((nodes, ncap), (rp, ncap + 1), (col, ecap)):
+            assert (t[cap:] == -7).all()  # nothing written past the capacity
+        return int(err.item()), nodes[:n_s].cpu(), col[:e_s].cpu()
+
+    e_ok, nodes_ok, col_ok = build(n_s, e_s)
+    assert e_ok == 0
+    e_small, _, _ = build(n_s // 2, e_s // 2)
+    assert e_small & 4
+    e_again, nodes2, col2 = build(n_s, e_s)
+    assert e_again == 0 and torch.equal(nodes2, nodes_ok) and torch.equal(col2, col_ok)
+
+
 # ---------------------------------------------------------------------------
 # A12: reconstruction loss (Gram form vs dense N x N)
 # ---------------------------------------------------------------------------
@@ -361,7 +400,10 @@ def test_pretrain_step_matches_reference(pkg, dev, name, device_ego):
 # A5 fused: GIN encoder (fused HIP layers) vs the oracle's GIN
 # ---------------------------------------------------------------------------
 @pytest.mark.parametrize("training", [True, False])
-@pytest.mark.parametrize("layers,n_mols", [(5, 300), (4, 37), (2, 1)])
+# (2, 6000): ~108 k rows, 106 BatchNorm statistics groups — past one load
+# round, so the statistics take the third (supergroup) level of bn_fwd_hier /
+# bn_bwd_hier, with a partial last supergroup
+@pytest.mark.parametrize("layers,n_mols", [(5, 300), (4, 37), (2, 1), (2, 6000)])
 def test_fused_gin_encoder(pkg, dev, training, layers, n_mols):
     torch.manual_seed(layers)
     g, gh = rand_graph(pkg, n_mols, "qm9", 11, dev)

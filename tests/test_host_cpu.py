@@ -32,10 +32,6 @@ def test_library_exports_every_header_symbol(pkg):
     loaded = lib_mod.load()
     assert loaded.scgib_abi_version() == lib_mod.ABI_VERSION
     assert loaded.scgib_strerror(-1).decode().startswith("invalid")
-    # the persistent pair forward takes its arguments as one struct: its ctypes
-    # mirror must have the C layout's size
-    assert loaded.scgib_gin_pair_args_bytes() == ctypes.sizeof(lib_mod.PairFwdArgs)
-    assert loaded.scgib_gin_pair_bwd_args_bytes() == ctypes.sizeof(lib_mod.PairBwdArgs)
 
 
 def test_argument_errors_do_not_launch(pkg):
@@ -446,21 +442,44 @@ def test_checkpoint_levels_roundtrip(pkg, tmp_path):
         pkg.refckpt.read(bad)
 
 
+def test_pickle_globals_resolves_memo_references(pkg, tmp_path):
+    """STACK_GLOBAL operands fetched from the memo (protocol 4 memoizes the
+    module string and BINGETs it for the next class of the same module) are
+    resolved, not taken from the last two literals; an operand that is not a
+    string is refused.  The pickle bytes are built by hand (disassembled only)."""
+    import pickletools
+    import zipfile
+
+    def zipped(name, payload):
+        p = str(tmp_path / name)
+        with zipfile.ZipFile(p, "w") as z:
+            z.writestr("archive/data.pkl", payload)
+        return p
+
+    # [models.Mainmodel, models.GIN] with 'models' memoized once and fetched
+    u = lambda s: b"\x8c" + bytes([len(s)]) + s.encode()  # SHORT_BINUNICODE
+    payload = (b"\x80\x04]\x94(" + u("models") + b"\x94" + u("Mainmodel") + b"\x94\x93\x94"
+               + b"h\x01" + u("GIN") + b"\x94\x93\x94e.")
+    pickletools.dis(payload, out=open(os.devnull, "w"))  # well-formed
+    assert pkg.refckpt.pickle_globals(zipped("memo.pt", payload)) == {"models.Mainmodel",
+                                                                       "models.GIN"}
+    bad = b"\x80\x04]\x94(" + u("models") + b"\x94K\x05\x93\x94e."  # name = BININT1 5
+    with pytest.raises(pkg.refckpt.RefCheckpointError):
+        pkg.refckpt.pickle_globals(zipped("bad_sg.pt", bad))
+
+
 def test_bench_kernel_table_evaluates(pkg):
     """bench.py imports on a CPU host and every KERNELS entry's bytes / flops
-    evaluate on a launch meta of its shape (per-layer or persistent pair)."""
+    evaluate on a per-layer launch meta."""
     import importlib
     import sys
     sys.path.insert(0, ROOT)
     bench = importlib.import_module("bench")
     layer = {"n": 1000, "e": 2000, "d_in": 64}
-    pair = {"layers": [(1000, 2000, 32)] + [(1000, 2000, 64)] * 4}
     for name, spec in bench.KERNELS.items():
-        m = pair if "pair" in name else layer
-        b = bench._call_meta(spec["bytes"], m)
-        f = bench._call_meta(spec["flops"], m)
+        b = bench._call_meta(spec["bytes"], layer)
+        f = bench._call_meta(spec["flops"], layer)
         assert b > 0 and f >= 0, name
-    assert bench.pair_fwd_bytes(pair) == sum(bench.agg_bytes(n, e, d) for n, e, d in pair["layers"])
 
 
 def test_xq_handoffs_off_under_serialised_dispatch(pkg, monkeypatch):

@@ -55,6 +55,37 @@ def _traffic():
 
 TRAFFIC = _traffic()
 RUN_CONFIG = None  # {"workload", "batch", "k"} of this run (main)
+# Replay-derived launch times: the same bench command traced by rocprofv3
+# (tools/gpu_round.sh: kernel_instances.py --json over the replayed steps of
+# its traced run), per kernel template instance — the timer pass below times
+# each kernel isolated and cache-warm, the replayed step runs it beside the
+# other encoder chain.
+REPLAY_FILE = os.environ.get("SCGIB_REPLAY_FILE",
+                             os.path.join(ROOT, "profiles", "replay_current.json"))
+
+
+def _replay():
+    try:
+        with open(REPLAY_FILE) as fh:
+            return json.load(fh)
+    except (OSError, ValueError):
+        return {}
+
+
+REPLAY = _replay()
+
+
+def replay_of(variants):
+    """(dispatches, dispatch-weighted mean duration in us) of the replayed
+    launches whose kernel names start with one of ``variants``; None when the
+    file is of another configuration or holds none."""
+    if REPLAY.get("_config") != RUN_CONFIG:
+        return None
+    got = [v for k, v in REPLAY.get("kernels", {}).items() if any(k.startswith(p) for p in variants)]
+    n = sum(g["dispatches"] for g in got)
+    if not n:
+        return None
+    return n, sum(g["avg_us"] * g["dispatches"] for g in got) / n
 
 
 def traffic_of(variants):
@@ -244,6 +275,19 @@ def roofline_entry(kernel, desc, r, variants):
            "launches_per_step": round(r["launches_per_step"], 2),
            "avg_bytes_per_launch": int(r["avg_bytes"]),
            "avg_flops_per_launch": int(r["avg_flops"]), "launches_timed": r["launches"]}
+    rep = replay_of(variants)
+    out["replay_file"] = os.path.relpath(REPLAY_FILE, ROOT)
+    if rep is None:
+        out["replay_avg_us"] = out["replay_frac"] = None
+        out["replay_note"] = (f"no replayed-step trace of {RUN_CONFIG} for {variants} in "
+                              f"{out['replay_file']}: run tools/gpu_round.sh on this code")
+    else:
+        d, us = rep
+        rate = (r["avg_flops"] / (us * 1e-6) / 1e12 if bound == "mfma" else
+                r["avg_bytes"] / (us * 1e-6) / 1e9)
+        out["replay_avg_us"] = round(us, 3)
+        out["replay_dispatches"] = d
+        out["replay_frac"] = round(rate / peak, 4)  # same bytes / flops, replayed launch time
     if traffic is None:
         cfg = TRAFFIC.get("_config")
         out["traffic_note"] = (
@@ -546,7 +590,16 @@ def main():
                          "batch ahead (graph.EgoPrefetch; A/B)")
     ap.add_argument("--torch-adam", action="store_true",
                     help="torch's fused Adam instead of the one-launch scgib Adam")
+    ap.add_argument("--finetune", choices=["molhiv"], default=None,
+                    help="time the fine-tune step of BASELINE.json configs[4] instead "
+                         "(finetune_bench.py; --batch defaults to 32 there)")
     a = ap.parse_args()
+    if a.finetune:
+        import finetune_bench
+        dev = torch.device("cuda", 0)
+        torch.cuda.set_device(dev)
+        finetune_bench.main_line(sys.modules[__name__], a, dev)
+        return
 
     rank, world, local = pkg.dist.init_from_env()
     if a.force_allreduce and world == 1 and not dist.is_initialized():

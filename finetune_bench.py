@@ -1,0 +1,223 @@
+"""BASELINE.json configs[4] on the device: the ogbg-molhiv fine-tune step from
+pre_training_v1_GIN_64_5_1.pt (bench.py --finetune molhiv).
+
+One step = the batch load + on-device ego-nets (the reference extracts them
+in its data loader, exp_molhiv.py) + Mainmodel_finetuning.forward in train
+mode (models.py:501-520: transfer_d, the pretrained Mainmodel_continue's
+extract_features with the reference's freezing quirk, MLP, Set2Set, predict,
+sigmoid) + BCE loss (models.py:522-523) + backward + Adam(lr 1e-3, weight
+decay 1e-5) over the model's parameters (exp_molhiv.py:160,
+train_molhiv.py:107-152), captured as ONE HIP graph in capacity mode and
+replayed over a pool of resident synthetic molhiv-shaped batches of B = 32
+(the reference's default batch size for this driver; --batch to change).
+
+The pretrained weights are the shipped checkpoint's 544 tensors as read
+weights-only by s-cgib_amd/refckpt.py into tests/golden/ (no pickle is loaded
+here); the fine-tune head's own weights are seeded random; targets are seeded
+random {0, 1} labels per batch.  The CPU baseline is the oracle's fine-tune
+step (oracle/scgib_ref.py finetune_forward + backward + Adam, ego-nets
+pre-extracted as the reference's loader does) on a bounded sample.
+"""
+from __future__ import annotations
+
+import json
+import os
+import statistics
+import time
+from types import SimpleNamespace
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+CKPT = os.path.join(ROOT, "tests", "golden", "ckpt_pre_training_v1_GIN_64_5_1.npz")
+
+
+def load_pretrained(pkg, args):
+    """The shipped checkpoint's module chain (4 levels, 544 tensors) from the
+    committed weights-only fixture."""
+    with np.load(CKPT, allow_pickle=False) as d:
+        levels = [(s.split(":")[0], int(s.split(":")[1])) for s in d["levels"].tolist()]
+        cfg = {k[4:]: (d[k].item() if d[k].dtype.kind in "iuf" else str(d[k]))
+               for k in d.files if k.startswith("cfg_")}
+        sd = {k[3:]: torch.tensor(d[k]) for k in d.files if k.startswith("sd/")}
+    return pkg.models.model_from_state(levels, cfg, sd, args), levels, cfg
+
+
+def make_finetune_model(pkg, F_in, B, dev, seed=0):
+    args = SimpleNamespace(recons_type="adj", useAtt=1, readout_f="sum", d_transfer=32,
+                           batch_size=B, gin_layers=5, task="graph_classification",
+                           dataset="ogbg-molhiv", device=dev)
+    torch.manual_seed(seed)
+    pre, levels, cfg = load_pretrained(pkg, args)
+    k = int(cfg["k_transition"])
+    ft = pkg.models.Mainmodel_finetuning(args, F_in, 64, 4, 4, k, 1, pre, "GIN")
+    return ft.to(dev).train(), k
+
+
+def oracle_params(pkg, ft):
+    """fp32 CPU leaves of the fine-tune model for the oracle: only the
+    parameters the step trains require grad (the freezing quirk)."""
+    from oracle import scgib_ref as R
+    trainable = {n for n, p in ft.named_parameters() if p.requires_grad}
+    p = R.make_params({k: v.detach().cpu().numpy() for k, v in ft.state_dict().items()},
+                      requires_grad=False)
+    for k, v in p.items():
+        if k in trainable:
+            v.requires_grad_(True)
+    return p
+
+
+def cpu_baseline(pkg, ft, host_batches, targets, seconds):
+    """The oracle's fine-tune step on this host's cores (torch's default
+    thread count = the CPU share), bounded sample."""
+    from oracle import egonet
+    from oracle import scgib_ref as R
+    p = oracle_params(pkg, ft)
+    opt = torch.optim.Adam([v for v in p.values() if v.requires_grad], lr=1e-3, weight_decay=1e-5)
+    buffers = {k: v for k, v in p.items() if "running" in k or "num_batches" in k}
+    k = int(ft.k_transition)
+    times = []
+    t_end = time.perf_counter() + seconds
+    i = 0
+    while time.perf_counter() < t_end or i < 3:
+        gh = host_batches[i % len(host_batches)]
+        t0 = time.perf_counter()
+        sizes, ecount, nodes, esrc, edst = egonet.egonets(gh.rowptr.numpy(), gh.col.numpy(), k)
+        off = np.repeat(np.concatenate([[0], np.cumsum(sizes)[:-1]]), ecount)
+        src, dst = gh.edges()
+        batch = {"src": src, "dst": dst, "counts": torch.from_numpy(gh.batch_num_nodes_host())}
+        ego = {"src": torch.from_numpy(esrc + off), "dst": torch.from_numpy(edst + off),
+               "counts": torch.from_numpy(sizes)}
+        x = F.normalize(gh.ndata["x"].float())
+        n = x.shape[0]
+        opt.zero_grad(set_to_none=True)
+        scores = R.finetune_forward(p, batch, ego, x, x[torch.from_numpy(nodes)],
+                                    torch.rand(n), torch.rand(n, 64), "ogbg-molhiv", buffers)
+        loss = F.binary_cross_entropy(scores, targets[i % len(targets)].cpu())
+        loss.backward()
+        opt.step()
+        if i >= 1:
+            times.append(time.perf_counter() - t0)
+        i += 1
+    B = host_batches[0].batch_size
+    ms = statistics.mean(times) * 1e3
+    return {"value": round(B / (ms * 1e-3), 1), "unit": "graphs/s", "ms_per_step": round(ms, 3),
+            "steps": len(times), "cores": torch.get_num_threads(), "kind": "port",
+            "sample": f"{len(times)} oracle fine-tune steps (finetune_forward + BCE + backward + "
+                      f"Adam, fp32, per-graph loops; ego-nets by oracle/egonet.py in the step) "
+                      f"of B={B} molhiv-like molecules after 1 warm-up, ~{seconds:.0f} s"}
+
+
+def run(bench, a, dev):
+    """bench.py --finetune molhiv: returns the JSON line (dict)."""
+    pkg = bench.pkg
+    workload = "molhiv"
+    F_in = pkg.synth.WORKLOADS[workload][2]
+    B = a.batch if a.batch != 512 else 32  # (bench's pretrain default 512 -> the fine-tune's 32)
+    ft, k = make_finetune_model(pkg, F_in, B, dev)
+    gen = torch.Generator().manual_seed(7)
+    host, padded_src = [], []
+    for i in range(a.pool):
+        gh, _ = pkg.graph.collate_pyg(pkg.synth.molecules(B, workload, seed=500 + i))
+        host.append(gh)
+    targets = [torch.randint(0, 2, (B, 1), generator=gen).float() for _ in range(a.pool)]
+    bench.RUN_CONFIG = {"workload": "molhiv-finetune", "batch": B, "k": k}
+    opt = pkg.optim.Adam(ft.parameters(), lr=1e-3, weight_decay=1e-5)
+    n_cap, e_cap, mgn, caps = pkg.graph.StaticBatch.capacities(host, k, slack=1.02)
+    static = pkg.graph.StaticBatch(B, n_cap, e_cap, F_in, mgn, caps, dev, k=k)
+    padded = []
+    for gh in host:
+        gx = pkg.graph.GraphBatch.from_edges(*[t.numpy() for t in gh.edges()], gh.num_nodes(), True,
+                                             gh.batch_num_nodes_host())
+        dict.__setitem__(gx.ndata, "x", F.normalize(gh.ndata["x"].float()))
+        padded.append(static.pad(gx))
+    pool = static.pool(padded)
+    tpool = torch.stack(targets).to(dev)  # [pool, B, 1]
+
+    def body():
+        static.load_next(pool)
+        # the batch just loaded: the cursor the copy kernel advanced, minus one
+        idx = torch.remainder(pool["cursor"][:1].long() - 1, pool["n"])
+        tg = tpool.index_select(0, idx)[0]
+        scores, *_ = ft(static.graph, static.x, None, None, 1, None, 2, dev, B)
+        loss = ft.loss(scores, tg)
+        loss.backward()
+        return loss.detach()
+
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):  # warm-up: allocator, Adam state
+        for _ in range(3):
+            opt.zero_grad(set_to_none=True)
+            body()
+            opt.step()
+    torch.cuda.current_stream().wait_stream(side)
+    torch.cuda.synchronize()
+    opt.zero_grad(set_to_none=True)
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        static_loss = body()
+        opt.step()
+    for _ in range(a.warmup):
+        graph.replay()
+    bench.progress(f"fine-tune warm-up done; timing {a.steps} steps")
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        graph.replay()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if pkg.ops.xq_timeouts(dev) or pkg.ops.handoff_fault(dev):
+        raise SystemExit("bench: a cross-queue hand-off wait timed out (ops.XQ_FLAGS)")
+    final_loss = float(static_loss.item())
+    # kernel timer: eager fine-tune steps on one stream, HIP events per launch
+    kernels = {}
+    if not a.no_kernel_timer:
+        entries = [e for spec in bench.KERNELS.values() for e in spec["entries"]]
+        steps_t = min(a.steps, 10)
+        pkg.models.FORK_ENCODERS = False
+        try:
+            with bench.KernelTimer(*entries) as timer:
+                for i in range(steps_t):
+                    gh = host[i % len(host)]
+                    g = gh.to(dev)
+                    x = F.normalize(g.ndata["x"].float())
+                    ft.zero_grad(set_to_none=True)
+                    scores, *_ = ft(g, x, None, None, 1, None, 2, dev, B)
+                    ft.loss(scores, targets[i % len(targets)].to(dev)).backward()
+        finally:
+            pkg.models.FORK_ENCODERS = True
+        for name, spec in bench.KERNELS.items():
+            r = timer.kernel_summary(spec, steps_t)
+            if r is not None:
+                kernels[name] = bench.roofline_entry(name, spec["desc"], r, spec["pmc"])
+    dominant = max(kernels, key=lambda kk: kernels[kk]["per_step_us"]) if kernels else None
+    cpu = None if a.no_cpu_baseline else cpu_baseline(pkg, ft, host, targets, a.cpu_seconds / 2)
+    n_nodes = statistics.mean(g.num_nodes() for g in host)
+    return {
+        "metric": "graphs/sec (ogbg-molhiv fine-tune step from pre_training_v1_GIN_64_5_1, "
+                  "GIN-64x5) on 1 MI355X",
+        "value": round(B * a.steps / elapsed, 1), "unit": "graphs/s", "n_gpus": 1,
+        "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(elapsed / a.steps * 1e3, 4),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
+        "data": "synthetic (seeded molhiv-like molecules, F=9 OGB features, random {0,1} "
+                "targets); pretrained weights: the shipped checkpoint's tensors (weights-only "
+                "fixture), head weights seeded random",
+        "config": {"workload": f"molhiv fine-tune step, batch {B}, k={k} (BASELINE.json "
+                               "configs[4]), Mainmodel_finetuning + BCE + Adam(1e-3, wd 1e-5)",
+                   "launch": "hip-graph replay (capacity mode)",
+                   "ego_build": "at the head of the step (device k-hop builder)",
+                   "trainable": sum(p.numel() for p in ft.parameters() if p.requires_grad),
+                   "nodes_per_batch": round(n_nodes, 1), "parallelism": "dp1",
+                   "final_loss": round(final_loss, 4)},
+        "roofline": kernels.get(dominant),
+        "roofline_kernels": kernels or None,
+        "cpu_baseline": cpu,
+    }
+
+
+def main_line(bench, a, dev):
+    line = run(bench, a, dev)
+    print(json.dumps(line), flush=True)

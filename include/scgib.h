@@ -186,6 +186,13 @@ int scgib_bn_bwd_finalize(const float *tile_stats, int64_t n_nodes, int32_t trai
  * scgib_gin_bwd_stats_bn = scgib_gin_bwd_stats + scgib_bn_bwd_finalize. */
 int64_t scgib_gin_bn_ws_floats(int64_t n_nodes);
 int64_t scgib_gin_counters(int64_t n_nodes);
+/* d_in = 64 layers of many more tiles than the device holds (>= 2048 tiles,
+ * BatchNorm not deferred) run a walking form of the layer kernel: each
+ * workgroup a contiguous run of tiles, weights staged once, the next tile's
+ * gather in flight under the current tile's GEMMs; bitwise the same outputs.
+ * Testing hook: 0 = never walk, 1 = from the threshold (default), 2 = whenever
+ * eligible; returns the previous setting. */
+int scgib_set_fwd_walk(int mode);
 int scgib_gin_layer_fwd_bn(const float *h_in, int32_t d_in, const float *in_stat,
                            const int32_t *rowptr, const int32_t *col, int64_t n_nodes,
                            float one_plus_eps, const float *w1, const float *b1, const float *w2,
@@ -266,6 +273,23 @@ int scgib_gin_layer_bwd(const float *dy, const float *z2, const float *r, const 
                         const float *w2, int64_t n_nodes, float *dagg, float *slab,
                         float *wgrad, const int32_t *dims, const scgib_bn_bwd_pending *pending,
                         scgib_stream_t stream);
+/* ---- (f)1/(f)4: Set2Set attention readout (DGL Set2Set, models.py:565) ----
+ * One round's per-graph half of Set2Set as Mainmodel_finetuning.forward
+ * (models.py:515) and Mainmodel_domainadapt (:271-272) run it: for graph g
+ * (rows [graph_ptr[g], graph_ptr[g+1]) of x [*][dim], dim <= 64),
+ *   e_v = <x_v, q_g>, alpha = softmax_g(e), out_g = sum_v alpha_v x_v;
+ * stat [2 n_graphs] receives (max_g e, softmax denominator) for the backward.
+ * Backward: dx_v = alpha_v g_g + de_v q_g, dq_g = sum_v de_v x_v with
+ * de_v = alpha_v (<g_g, x_v> - sum_u alpha_u <g_g, x_u>); rows of dx past
+ * graph_ptr[n_graphs] (up to n_rows: capacity padding) are zeroed.  The LSTM
+ * cell between rounds is the caller's.  No host sync: graph-capturable. */
+int scgib_set2set_fwd(const float *x, const float *q, const int32_t *graph_ptr,
+                      int64_t n_graphs, int32_t dim, float *stat, float *out,
+                      scgib_stream_t stream);
+int scgib_set2set_bwd(const float *x, const float *q, const int32_t *graph_ptr,
+                      int64_t n_graphs, int32_t dim, const float *stat, const float *g_out,
+                      float *dx, float *dq, int64_t n_rows, scgib_stream_t stream);
+
 /* ---- A6: per-segment readouts (dgl.sum_nodes) -------------------------------
  * out[s,:] = sum_{i in [ptr[s], ptr[s+1])} x[i,:]   (models.py:716, 725, 733)
  * segment_broadcast is its adjoint: out[i,:] = g[s,:] for every row i of s.

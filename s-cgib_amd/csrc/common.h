@@ -82,14 +82,15 @@ __device__ __forceinline__ float4 ld_agent4(const float *p) {
 // `expected` arrivals.  Every wave first waits for its stores to be
 // acknowledged (vmcnt(0)); the barrier collects the waves; one thread counts
 // the workgroup in.  Data exchanged this way must use st_agent / ld_agent.
-__device__ __forceinline__ bool block_arrive(unsigned *counter, unsigned expected) {
+__device__ __forceinline__ bool block_arrive(unsigned *counter, unsigned expected,
+                                             unsigned count = 1u) {
     __shared__ unsigned s_ticket;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0)
-        s_ticket = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s_ticket = __hip_atomic_fetch_add(counter, count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __syncthreads();
-    return s_ticket == expected - 1;
+    return s_ticket + count == expected;  // (count: arrivals this workgroup makes at once)
 }
 
 // Batched loads: a load written as `ok ? p[i] : 0` is compiled into its own

@@ -120,6 +120,33 @@ __device__ __forceinline__ void gather_head(const float4 *__restrict__ h4,
     }
 }
 
+// one round of up to 4 neighbours per row: acc += x[u] (slots past the
+// row's degree enter with weight 0), and the self term acc = ope x[v] + acc
+// (shared by gather_tail and the walking forward, so both are bitwise equal)
+template <int RPT, bool XFORM>
+__device__ __forceinline__ void gather_round(const float4 (&a)[RPT][4], int j0,
+                                             const int32_t (&deg)[RPT], float4 sc, float4 sh,
+                                             float4 (&acc)[RPT]) {
+#pragma unroll
+    for (int k = 0; k < RPT; ++k)
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            const float w = j0 + t < deg[k] ? 1.f : 0.f;
+            acc[k] = fma4(XFORM ? xform4(a[k][t], sc, sh) : a[k][t], w, acc[k]);
+        }
+}
+
+template <int RPT, bool XFORM>
+__device__ __forceinline__ void gather_self(const float4 (&self)[RPT], float ope, float4 sc,
+                                            float4 sh, float4 (&acc)[RPT]) {
+#pragma unroll
+    for (int k = 0; k < RPT; ++k) {
+        const float4 x = XFORM ? xform4(self[k], sc, sh) : self[k];
+        acc[k] = make_float4(ope * x.x + acc[k].x, ope * x.y + acc[k].y, ope * x.z + acc[k].z,
+                             ope * x.w + acc[k].w);
+    }
+}
+
 template <int RPT, int LPR, bool XFORM>
 __device__ __forceinline__ void gather_tail(const float4 *__restrict__ h4,
                                             const int32_t *__restrict__ col, GatherHead<RPT> &hd,
@@ -147,20 +174,9 @@ __device__ __forceinline__ void gather_tail(const float4 *__restrict__ h4,
         for (int k = 0; k < RPT; ++k)
 #pragma unroll
             for (int t = 0; t < 4; ++t) a[k][t] = h4[static_cast<int64_t>(u[k][t]) * LPR + c];
-#pragma unroll
-        for (int k = 0; k < RPT; ++k)
-#pragma unroll
-            for (int t = 0; t < 4; ++t) {
-                const float w = j0 + t < hd.deg[k] ? 1.f : 0.f;
-                acc[k] = fma4(XFORM ? xform4(a[k][t], sc, sh) : a[k][t], w, acc[k]);
-            }
+        gather_round<RPT, XFORM>(a, j0, hd.deg, sc, sh, acc);
     }
-#pragma unroll
-    for (int k = 0; k < RPT; ++k) {
-        const float4 x = XFORM ? xform4(hd.self[k], sc, sh) : hd.self[k];
-        acc[k] = make_float4(ope * x.x + acc[k].x, ope * x.y + acc[k].y, ope * x.z + acc[k].z,
-                             ope * x.w + acc[k].w);
-    }
+    gather_self<RPT, XFORM>(hd.self, ope, sc, sh, acc);
 }
 
 // Sum aggregation of RPT rows (row0 + rbase + k * RPP) for one 4-channel
@@ -404,6 +420,17 @@ __device__ __forceinline__ void mma_kk4x2(const float *pa, const float *pb1, con
         mma_step_fence();
     }
     asm volatile("" ::"v"(c1[0]), "v"(c2[0]));
+}
+
+// s_waitcnt through the builtin (the compiler's wait model sees it, an asm
+// statement it does not): vmcnt(0) = 0x0F70, lgkmcnt(0) alone = 0xC07F (gfx9
+// encoding: vmcnt [3:0] + [15:14], expcnt [6:4], lgkmcnt [11:8])
+__device__ __forceinline__ void vm_wait_all() { __builtin_amdgcn_s_waitcnt(0x0F70); }
+// barrier without the vmcnt(0) of a __syncthreads fence (global stores and
+// prefetch loads stay in flight across it)
+__device__ __forceinline__ void lds_barrier() {
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    __builtin_amdgcn_s_barrier();
 }
 
 // row of accumulator register `reg` of the 32x32 output tile held by lane l

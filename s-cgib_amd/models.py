@@ -106,32 +106,36 @@ class GIN(nn.Module):
 
 
 class Set2Set(nn.Module):
-    """DGL Set2Set (LSTM(2d -> d), n_iters rounds) — held for state_dict parity
-    with the reference (models.py:565); not on the pretraining hot path."""
+    """DGL Set2Set (LSTM(2d -> d), n_iters rounds; reference models.py:565,
+    the fine-tune and domain-adaptation readout).  Each round: one LSTM cell
+    step on q_star (torch ops, PyTorch gate order i, f, g, o — the reference's
+    single-layer nn.LSTM), then the per-graph softmax attention readout on
+    the device (ops.set2set_attend, one wavefront per graph).  No host sync
+    and no host->device copy, so a fine-tune step holding it is capturable.
+    ``lstm`` keeps nn.LSTM's parameters (state_dict parity)."""
 
     def __init__(self, input_dim, n_iters, n_layers):
         super().__init__()
+        if n_layers != 1:
+            raise NotImplementedError("Set2Set: the reference uses one LSTM layer")
         self.input_dim, self.output_dim = input_dim, 2 * input_dim
         self.n_iters, self.n_layers = n_iters, n_layers
         self.lstm = nn.LSTM(self.output_dim, self.input_dim, n_layers)
 
     def forward(self, graph, feat):
-        bs = graph.batch_size
-        h = (feat.new_zeros((self.n_layers, bs, self.input_dim)),
-             feat.new_zeros((self.n_layers, bs, self.input_dim)))
+        bs, d = graph.batch_size, self.input_dim
+        lstm = self.lstm
+        hx = feat.new_zeros(bs, d)
+        cx = feat.new_zeros(bs, d)
         q_star = feat.new_zeros(bs, self.output_dim)
-        seg = torch.repeat_interleave(torch.arange(bs, device=feat.device),
-                                      graph.batch_num_nodes().to(feat.device))
         for _ in range(self.n_iters):
-            q, h = self.lstm(q_star.unsqueeze(0), h)
-            q = q.view(bs, self.input_dim)
-            e = (feat * q[seg]).sum(dim=-1, keepdim=True)
-            emax = torch.full((bs, 1), float("-inf"), device=feat.device).scatter_reduce(
-                0, seg.view(-1, 1), e, "amax")
-            a = torch.exp(e - emax[seg])
-            den = torch.zeros(bs, 1, device=feat.device).index_add(0, seg, a)
-            readout = ops.sum_nodes_graph(graph, feat * (a / den[seg]))
-            q_star = torch.cat([q, readout], dim=-1)
+            gates = F.linear(q_star, lstm.weight_ih_l0, lstm.bias_ih_l0) + \
+                F.linear(hx, lstm.weight_hh_l0, lstm.bias_hh_l0)
+            i, f, g, o = gates.chunk(4, dim=1)
+            cx = torch.sigmoid(f) * cx + torch.sigmoid(i) * torch.tanh(g)
+            hx = torch.sigmoid(o) * torch.tanh(cx)
+            readout = ops.set2set_attend(feat, hx, graph)
+            q_star = torch.cat([hx, readout], dim=-1)
         return q_star
 
 

@@ -919,6 +919,38 @@ def sum_nodes_graph(graph, x):
     return segment_sum(x, graph.graph_ptr, graph.batch_size)
 
 
+class _Set2SetAttend(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, q, ptr, nseg):
+        x, q = _f32(x, "set2set x"), _f32(q, "set2set q")
+        if x.dim() != 2 or q.shape != (nseg, x.shape[1]) or x.shape[1] > 64:
+            raise _lib.ScgibError(f"set2set: x {tuple(x.shape)}, q {tuple(q.shape)}, "
+                                  f"{nseg} graphs (width <= 64)")
+        out = torch.empty(nseg, x.shape[1], dtype=torch.float32, device=x.device)
+        stat = torch.empty(max(2 * nseg, 1), dtype=torch.float32, device=x.device)
+        _lib.call("scgib_set2set_fwd", _p(x), _p(q), _p(ptr), nseg, x.shape[1], _p(stat),
+                  _p(out), _stream())
+        ctx.save_for_backward(x, q, stat)
+        ctx.ptr, ctx.nseg = ptr, nseg
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        x, q, stat = ctx.saved_tensors
+        g = _f32(g, "set2set.backward")
+        dx, dq = torch.empty_like(x), torch.empty_like(q)
+        _lib.call("scgib_set2set_bwd", _p(x), _p(q), _p(ctx.ptr), ctx.nseg, x.shape[1], _p(stat),
+                  _p(g), _p(dx), _p(dq), x.shape[0], _stream())
+        return dx, dq, None, None
+
+
+def set2set_attend(x, q, graph):
+    """One Set2Set round's attention readout on the device (DGL Set2Set,
+    models.py:565): softmax over each graph's rows of <x_v, q_g>, then the
+    alpha-weighted row sum per graph."""
+    return _Set2SetAttend.apply(x, q, graph.graph_ptr, int(graph.batch_size))
+
+
 # ---------------------------------------------------------------------------
 # A6-A8: fused core <-> subgraph interaction
 # ---------------------------------------------------------------------------

@@ -1,8 +1,9 @@
 #!/bin/bash
-# Round measurement: GPU tests, smoke, the PMC traffic passes, the full bench
-# line (its roofline.traffic read from this run's PMC summary), then the
-# rocprofv3 kernel-trace summary.  Every GPU step has its own limit and the
-# first failure ends the script.  Usage: bash tools/gpu_round.sh TAG
+# Round measurement: GPU tests, smoke, the PMC traffic passes, a rocprofv3
+# kernel trace of the bench (replayed steps + kernel-timer pass: the replay
+# file), then the full bench line (its roofline.traffic from this run's PMC
+# summary, roofline.replay_* from this run's trace).  Every GPU step has its
+# own limit and the first failure ends the script.  Usage: bash tools/gpu_round.sh TAG
 set -o pipefail
 TAG=${1:-round}
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
@@ -18,11 +19,11 @@ for C in FETCH_SIZE WRITE_SIZE; do
     -- python bench.py $ARGS > "$O/pmc_$C.log" 2>&1 || { echo "pmc $C failed"; exit 1; }
 done
 python tools/pmc_summary.py "$O/pmc" qm9,512,1 > "$O/traffic.json" && echo traffic ok
-SCGIB_TRAFFIC_FILE=$O/traffic.json timeout -k 10 600 python bench.py --steps 300 --warmup 20 --cpu-seconds 20 > $O/bench.log 2>&1 || { echo bench failed; tail -5 $O/bench.log; exit 1; }
-tail -1 $O/bench.log | cut -c1-400
 # the bench with its kernel-timer pass: kernel_instances.py --split separates
 # the replayed steps from the timer pass (the launches the timer averages)
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -T --output-format csv -d $O/prof_kt -o kt \
   -- python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-superbatch > $O/prof_bench.log 2>&1 || { echo rocprof failed; exit 1; }
-python tools/kernel_instances.py $O/prof_kt --split adam_step_k > $O/kernel_instances.txt 2>&1
+python tools/kernel_instances.py $O/prof_kt --split adam_step_k --json $O/replay.json --config qm9,512,1 > $O/kernel_instances.txt 2>&1 && echo replay ok
+SCGIB_TRAFFIC_FILE=$O/traffic.json SCGIB_REPLAY_FILE=$O/replay.json timeout -k 10 600 python bench.py --steps 300 --warmup 20 --cpu-seconds 20 > $O/bench.log 2>&1 || { echo bench failed; tail -5 $O/bench.log; exit 1; }
+tail -1 $O/bench.log | cut -c1-400
 echo done

@@ -10,7 +10,13 @@ averages.
 Groups dispatches by full kernel name (template arguments kept) and grid
 size, so the bench's roofline kernel (e.g. gin_fwd_k<64, true, true, ...>
 at the step's grid) can be checked against rocprof's own durations; rows
-with a grid above max_grid (the ZINC-scale superbatch) are listed apart."""
+with a grid above max_grid (the ZINC-scale superbatch) are listed apart.
+
+--json OUT --config WORKLOAD,BATCH,K: also write the replayed steps' per-kernel
+(full template name) dispatch count and average duration to OUT, tagged with
+the bench configuration — bench.py reads it (SCGIB_REPLAY_FILE, default
+profiles/replay_current.json) to report each roofline kernel's replay-derived
+launch time beside its isolated kernel-timer time."""
 import collections
 import csv
 import glob
@@ -18,6 +24,16 @@ import os
 import sys
 
 args = sys.argv[1:]
+json_out = config = None
+for flag in ("--json", "--config"):
+    if flag in args:
+        i = args.index(flag)
+        if flag == "--json":
+            json_out = args[i + 1]
+        else:
+            w, b, k = args[i + 1].split(",")
+            config = {"workload": w, "batch": int(b), "k": int(k)}
+        del args[i:i + 2]
 split = None
 if "--split" in args:
     i = args.index("--split")
@@ -46,3 +62,14 @@ for title, part in parts:
         if len(ds) < 2 and sum(ds) < 50_000:
             continue
         print(f"{name[:60]:60s} {grid:9d} {len(ds):6d} {sum(ds) / len(ds) / 1e3:9.2f} {min(ds) / 1e3:8.2f}")
+
+if json_out:
+    import json
+    replayed = parts[0][1]
+    per = collections.defaultdict(list)
+    for t0, t1, name, grid in replayed:
+        per[name].append(t1 - t0)
+    with open(json_out, "w") as fh:
+        json.dump({"_config": config, "_source": os.path.abspath(path),
+                   "kernels": {name: {"dispatches": len(ds), "avg_us": round(sum(ds) / len(ds) / 1e3, 3)}
+                               for name, ds in per.items()}}, fh, indent=1, sort_keys=True)

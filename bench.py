@@ -780,10 +780,21 @@ def main():
     xq_to = pkg.ops.xq_timeouts(dev)
     if xq_to:  # a hand-off wait gave up: its queue ran ahead of the data
         raise SystemExit(f"bench: {xq_to} cross-queue hand-off waits timed out (ops.XQ_FLAGS)")
+    replica_diff = None
     if world > 1:
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+        # replica mode's invariant after the timed steps: every rank holds the
+        # same parameters and BatchNorm statistics (the averaged bucket is
+        # applied identically) — the largest difference to rank 0's, any rank
+        flat = torch.cat([p.detach().reshape(-1) for p in model.parameters()] +
+                         [b.reshape(-1) for b in pkg.dist.bn_buffers(model)])
+        ref = flat.clone()
+        dist.broadcast(ref, 0)
+        d = (flat - ref).abs().max().reshape(1).double()
+        dist.all_reduce(d, op=dist.ReduceOp.MAX)
+        replica_diff = float(d.item())
     final_loss = float(sum(loss).item()) if isinstance(loss, tuple) else float(loss.item())
 
     # instrumented eager pass over the same batches: HIP events around every
@@ -850,6 +861,7 @@ def main():
                        ("eager" if a.eager else allreduce_mode),
                        "global_batch": world * a.batch, "nodes_per_batch": round(n_nodes, 1),
                        "parallelism": f"dp{world}", "final_loss": round(final_loss, 4),
+                       "replica_max_abs_diff": replica_diff,
                        "bn_semantics": ("single rank: BatchNorm statistics over the whole batch"
                                         if world == 1 else
                                         "replica mode (DESIGN.md §6): each rank's BatchNorm, "

@@ -102,8 +102,16 @@ __device__ __forceinline__ double ld_part(const double *p) {
 // groups p, p + 4, ... (fp64, fixed order); the four partitions combine as
 // (p0 + p1) + (p2 + p3) through two xor shuffles (identical in every lane).
 // Split into the load (issue early, registers) and the combine, so other
-// loads can be in flight meanwhile; one load round for ngr <= kFinG.
-constexpr int kFinR = 16, kFinG = 4 * kFinR;
+// loads can be in flight meanwhile; one load round for ngr <= kFinG.  (8:
+// the QM9 B512 ego layers' 28 groups in one round, and 32 fewer VGPRs than
+// 16 in the forward kernel, which then keeps its first neighbour-index round
+// in flight across the finish)
+constexpr int kFinR = 8, kFinG = 4 * kFinR;
+// backward consumers: 2 partitions x kBFinR groups per load round
+constexpr int kBFinR = 16;
+// past one round of 64 groups the last-arriver statistics take a third
+// level: 64-group supergroups (bn_fwd_hier / bn_bwd_hier)
+constexpr int kSuper = 64;
 
 struct FwdFin {
     double vs[kFinR], vq[kFinR];
@@ -290,18 +298,18 @@ __device__ void bn_fwd_hier(const float *__restrict__ part, int64_t n, int64_t t
     if (fz.defer) return;  // the consumer kernel finishes (bn_fwd_final there)
     double mean, M2;
     FwdFin fin;
-    if (ngr > kFinG) {  // block-uniform
+    if (ngr > kSuper) {  // block-uniform
         // more groups than one load round: a third level, so that no single
         // workgroup walks every group partial in series at the end of the
         // kernel (1172 groups at 1.2 M rows: ~74 us of dependent load rounds).
         // The last group of each 64-group supergroup combines its groups
         // (one round), the last supergroup combines the supergroups.
-        constexpr int64_t kSupRows = int64_t(kFinG) * kGroup * TM;
-        const int s = g / kFinG, nsup = (ngr + kFinG - 1) / kFinG;
-        const int ssize = ngr - s * kFinG < kFinG ? ngr - s * kFinG : kFinG;
+        constexpr int64_t kSupRows = int64_t(kSuper) * kGroup * TM;
+        const int s = g / kSuper, nsup = (ngr + kSuper - 1) / kSuper;
+        const int ssize = ngr - s * kSuper < kSuper ? ngr - s * kSuper : kSuper;
         unsigned *scnt = &fz.counters[fz.ngr_cap + 1 + s];
         if (!block_arrive(scnt, ssize)) return;
-        const double *gp = fz.gpart + int64_t(s) * kFinG * 128;
+        const double *gp = fz.gpart + int64_t(s) * kSuper * 128;
         double *sp = fz.gpart + int64_t(fz.ngr_cap) * 128;
         const int64_t ns = static_cast<int64_t>(rows_in(n, s * kSupRows, kSupRows));
         double S;
@@ -334,7 +342,7 @@ __device__ void bn_fwd_hier(const float *__restrict__ part, int64_t n, int64_t t
 // barrier-free: lane l of wave w owns sum index cs = 32 w + (l & 31) and
 // partition p = l >> 5 (groups p, p + 2, ...); p0 + p1 via one xor shuffle.
 struct BwdFin {
-    double v[kFinR];
+    double v[kBFinR];
 };
 
 __device__ __forceinline__ int bfin_index() { return 32 * (threadIdx.x >> 6) + (threadIdx.x & 31); }
@@ -344,7 +352,7 @@ __device__ __forceinline__ void bn_bwd_fin_load(const double *__restrict__ gpart
                                                 BwdFin &f) {
     const int cs = bfin_index(), p = (threadIdx.x & 63) >> 5;
 #pragma unroll
-    for (int u = 0; u < kFinR; ++u) {
+    for (int u = 0; u < kBFinR; ++u) {
         if (g0 + 2 * u < ngr) {  // wave-uniform
             const int64_t gg = g0 + p + 2 * u < ngr ? g0 + p + 2 * u : 0;  // group 0 always exists
             f.v[u] = ld_part<AGENT>(gpart + gg * 128 + cs);
@@ -356,10 +364,10 @@ template <bool AGENT>
 __device__ double bn_bwd_final(const double *__restrict__ gpart, int ngr, BwdFin &f) {
     const int p = (threadIdx.x & 63) >> 5;
     double a = 0.0;
-    for (int g0 = 0; g0 < ngr; g0 += 2 * kFinR) {
+    for (int g0 = 0; g0 < ngr; g0 += 2 * kBFinR) {
         if (g0 > 0) bn_bwd_fin_load<AGENT>(gpart, ngr, g0, f);
 #pragma unroll
-        for (int u = 0; u < kFinR; ++u)
+        for (int u = 0; u < kBFinR; ++u)
             if (g0 + 2 * u < ngr) a += g0 + p + 2 * u < ngr ? f.v[u] : 0.0;
     }
     return a + __shfl_xor(a, 32, kWave);
@@ -407,12 +415,12 @@ __device__ void bn_bwd_hier_s(const float *__restrict__ part, int64_t n, int64_t
     }
     if (bz.defer) return;  // the layer's gin_bwd_k finishes (bn_bwd_final there)
     BwdFin fin;
-    if (ngr > kFinG) {  // block-uniform: the third level, as in bn_fwd_hier
-        const int s = g / kFinG, nsup = (ngr + kFinG - 1) / kFinG;
-        const int ssize = ngr - s * kFinG < kFinG ? ngr - s * kFinG : kFinG;
+    if (ngr > kSuper) {  // block-uniform: the third level, as in bn_fwd_hier
+        const int s = g / kSuper, nsup = (ngr + kSuper - 1) / kSuper;
+        const int ssize = ngr - s * kSuper < kSuper ? ngr - s * kSuper : kSuper;
         unsigned *scnt = &bz.counters[bz.ngr_cap + 1 + s];
         if (!block_arrive(scnt, ssize)) return;
-        const double *gp = bz.gpart + int64_t(s) * kFinG * 128;
+        const double *gp = bz.gpart + int64_t(s) * kSuper * 128;
         double *sp = bz.gpart + int64_t(bz.ngr_cap) * 128;
         bn_bwd_fin_load<true>(gp, ssize, 0, fin);
         const double st = bn_bwd_final<true>(gp, ssize, fin);
@@ -692,6 +700,11 @@ __global__ __launch_bounds__(256, (kFwdAlias<DIN, GATHER, PRE> ? 3 : 1)) void gi
         float4 acc[RPT];
         GatherHead<RPT> hd;
         gather_head<RPT, RPP, LPR>(h4, rowptr, row0, nv, rbase, c, hd);  // in flight meanwhile
+        // with a deferred BatchNorm finish ahead, the first neighbour-index
+        // round goes out before it too (it needs only the row pointers)
+        int32_t u0[RPT][4];
+        const bool idx_early = XFORM && pend.gpart != nullptr;  // block-uniform
+        if (idx_early) gather_idx0<RPT>(col, hd, u0);
         if (XFORM) {
             if (pend.gpart) {  // finish the previous layer's deferred BatchNorm statistics
                 __shared__ float sScSh[128];
@@ -719,7 +732,10 @@ __global__ __launch_bounds__(256, (kFwdAlias<DIN, GATHER, PRE> ? 3 : 1)) void gi
                 sh = ld4(in_shift + 4 * c);
             }
         }
-        gather_tail<RPT, LPR, XFORM>(h4, col, hd, c, ope, sc, sh, acc);
+        if (idx_early)
+            gather_tail<RPT, LPR, XFORM, true>(h4, col, hd, c, ope, sc, sh, acc, u0);
+        else
+            gather_tail<RPT, LPR, XFORM>(h4, col, hd, c, ope, sc, sh, acc);
         if (late_w) load_weights<DIN>(w1, w2, wregs);  // before the agg stores (in-order vmcnt)
 #pragma unroll
         for (int k = 0; k < RPT; ++k) {
@@ -960,7 +976,16 @@ __device__ __forceinline__ void walk_finish(const float4 *__restrict__ h4,
     gather_self<4, XFORM>(g.self, ope, sc, sh, acc);
 }
 
-constexpr int kWalkPerCU = 1;
+// DEEP: the gather pipelined two tiles deep (tile t + 1's rows in flight
+// through all of tile t) at one workgroup per CU (the prefetch needs > 256
+// VGPRs); shallow: one tile deep (tile t + 1's rows issued after tile t's
+// second GEMM) at two workgroups per CU
+template <bool DEEP>
+constexpr int kWalkPerCU = DEEP ? 1 : 2;
+#ifndef SCGIB_WALK_DEEP
+#define SCGIB_WALK_DEEP 0
+#endif
+constexpr bool kWalkDeep = SCGIB_WALK_DEEP != 0;
 
 // trace build: per-workgroup wall-clock time summed over the run's tiles per
 // phase (tools/superbatch_trace.py, TRACE_ENTRY walk)
@@ -983,8 +1008,8 @@ constexpr int kWalkPerCU = 1;
 #define WALK_END() do {} while (0)
 #endif
 
-template <bool XFORM>
-__global__ __launch_bounds__(256, kWalkPerCU) void gin_fwd_walk_k(
+template <bool XFORM, bool DEEP>
+__global__ __launch_bounds__(256, kWalkPerCU<DEEP>) void gin_fwd_walk_k(
     const float *__restrict__ h, const float *__restrict__ in_scale,
     const float *__restrict__ in_shift, const int32_t *__restrict__ rowptr,
     const int32_t *__restrict__ col, int64_t ncap, float ope, const float *__restrict__ w1,
@@ -1026,9 +1051,11 @@ __global__ __launch_bounds__(256, kWalkPerCU) void gin_fwd_walk_k(
     walk_head(rowptr, t_beg * TM, nvs, tid >> 4, x.beg, x.end);
     walk_idx(col, x);
     walk_rows(h4, t_beg * TM, nvs, tid >> 4, tid & 15, x, g);
-    walk_head(rowptr, (nv1 > 0 ? t_beg + 1 : t_beg) * TM, nv1 > 0 ? nv1 : nvs, tid >> 4, x.beg,
-              x.end);
-    walk_idx(col, x);
+    if constexpr (DEEP) {
+        walk_head(rowptr, (nv1 > 0 ? t_beg + 1 : t_beg) * TM, nv1 > 0 ? nv1 : nvs, tid >> 4,
+                  x.beg, x.end);
+        walk_idx(col, x);
+    }
     store_weights<64>(wregs, sW1, sW2);
     WALK_PH(7);
     for (int64_t tile = t_beg; tile < t_end; ++tile) {
@@ -1060,13 +1087,17 @@ __global__ __launch_bounds__(256, kWalkPerCU) void gin_fwd_walk_k(
         // for the row pointers, not for the rows
         const int nvn = rows_of(tile + 1), nvn2 = rows_of(tile + 2);
         const int64_t tn = nvn > 0 ? tile + 1 : tile, tn2 = nvn2 > 0 ? tile + 2 : tile;
-        int32_t hb[4], he[4];
-        walk_head(rowptr, tn2 * TM, nvn2 > 0 ? nvn2 : nv, rbase, hb, he);
-        walk_rows(h4, tn * TM, nvn > 0 ? nvn : nv, rbase, c, x, g);
+        if constexpr (DEEP) {
+            int32_t hb[4], he[4];
+            walk_head(rowptr, tn2 * TM, nvn2 > 0 ? nvn2 : nv, rbase, hb, he);
+            walk_rows(h4, tn * TM, nvn > 0 ? nvn : nv, rbase, c, x, g);
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            x.beg[k] = hb[k];
-            x.end[k] = he[k];
+            for (int k = 0; k < 4; ++k) {
+                x.beg[k] = hb[k];
+                x.end[k] = he[k];
+            }
+        } else {  // tile + 1's row pointers (its indices after GEMM1, rows after GEMM2)
+            walk_head(rowptr, tn * TM, nvn > 0 ? nvn : nv, rbase, x.beg, x.end);
         }
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
@@ -1090,11 +1121,12 @@ __global__ __launch_bounds__(256, kWalkPerCU) void gin_fwd_walk_k(
             }
         }
         WALK_PH(2);
-        walk_idx(col, x);  // tile + 2's first-round indices
+        walk_idx(col, x);  // the first-round indices of tile + 2 (DEEP) / tile + 1
         lds_barrier();
         WALK_PH(3);
         f32x16 a2 = mma_pf<64, false, false>(sA + wr * 32 * LDH, LDH, sW2 + wc * 32 * LDH, LDH,
                                              zero16());
+        if constexpr (!DEEP) walk_rows(h4, tn * TM, nvn > 0 ? nvn : nv, rbase, c, x, g);
         float s = 0.f;
 #pragma unroll
         for (int reg = 0; reg < 16; ++reg) {
@@ -2034,13 +2066,13 @@ static int launch_gin_fwd(const float *h_in, int32_t d_in, const float *in_stat,
     const float *isc = in_stat ? in_stat + 128 : nullptr, *ish = in_stat ? in_stat + 192 : nullptr;
     const scgib_bn_pending pd = pend ? *pend : scgib_bn_pending{};
     if (d_in == 64 && !pend && !fz.defer && fwd_walk(nt)) {
-        const int64_t slots = int64_t(kWalkPerCU) * kCUs;
+        const int64_t slots = int64_t(kWalkPerCU<kWalkDeep>) * kCUs;
         const int64_t run = (nt + (nt < slots ? nt : slots) - 1) / (nt < slots ? nt : slots);
         const unsigned grid = static_cast<unsigned>((nt + run - 1) / run);
         if (in_stat)
-            gin_fwd_walk_k<true><<<grid, 256, 0, st>>>(h_in, isc, ish, rowptr, col, n_nodes, one_plus_eps, w1, b1, w2, b2, agg, r, z2, tile_stats, dims, fz, run);
+            gin_fwd_walk_k<true, kWalkDeep><<<grid, 256, 0, st>>>(h_in, isc, ish, rowptr, col, n_nodes, one_plus_eps, w1, b1, w2, b2, agg, r, z2, tile_stats, dims, fz, run);
         else
-            gin_fwd_walk_k<false><<<grid, 256, 0, st>>>(h_in, isc, ish, rowptr, col, n_nodes, one_plus_eps, w1, b1, w2, b2, agg, r, z2, tile_stats, dims, fz, run);
+            gin_fwd_walk_k<false, kWalkDeep><<<grid, 256, 0, st>>>(h_in, isc, ish, rowptr, col, n_nodes, one_plus_eps, w1, b1, w2, b2, agg, r, z2, tile_stats, dims, fz, run);
         return launch_status();
     }
     if (d_in == 32)
@@ -2083,7 +2115,7 @@ static int64_t bn_groups(int64_t n_nodes) { return (scgib_gin_tiles(n_nodes) + k
 // 64-group supergroups (the third statistics level past one load round of groups)
 static int64_t bn_supergroups(int64_t n_nodes) {
     const int64_t g = bn_groups(n_nodes);
-    return g > kFinG ? (g + kFinG - 1) / kFinG : 0;
+    return g > kSuper ? (g + kSuper - 1) / kSuper : 0;
 }
 
 extern "C" int64_t scgib_gin_bn_ws_floats(int64_t n_nodes) {

@@ -147,11 +147,37 @@ __device__ __forceinline__ void gather_self(const float4 (&self)[RPT], float ope
     }
 }
 
-template <int RPT, int LPR, bool XFORM>
+// the first neighbour round's indices of gather_tail (the same clamped
+// addresses), loaded ahead so they are in flight across other work (the
+// forward's deferred BatchNorm finish); rows with no in-edges: not loaded
+template <int RPT>
+__device__ __forceinline__ void gather_idx0(const int32_t *__restrict__ col,
+                                            const GatherHead<RPT> &hd, int32_t (&u)[RPT][4]) {
+    int maxdeg = 0, maxend = 0;
+#pragma unroll
+    for (int k = 0; k < RPT; ++k) {
+        maxend = hd.deg[k] > maxend ? hd.deg[k] : maxend;
+        const int d = hd.deg[k] - hd.beg[k];
+        maxdeg = d > maxdeg ? d : maxdeg;
+    }
+    if (maxdeg > 0) {
+#pragma unroll
+        for (int k = 0; k < RPT; ++k)
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                const int32_t e = hd.beg[k] + t;
+                u[k][t] = col[e < maxend ? e : maxend - 1];
+            }
+    }
+}
+
+// U0: round 0's indices come from gather_idx0 (u0) instead of being loaded here
+template <int RPT, int LPR, bool XFORM, bool U0 = false>
 __device__ __forceinline__ void gather_tail(const float4 *__restrict__ h4,
                                             const int32_t *__restrict__ col, GatherHead<RPT> &hd,
                                             int c, float ope, float4 sc, float4 sh,
-                                            float4 (&acc)[RPT]) {
+                                            float4 (&acc)[RPT],
+                                            const int32_t (*u0)[4] = nullptr) {
     int maxdeg = 0, maxend = 0;
 #pragma unroll
     for (int k = 0; k < RPT; ++k) {
@@ -167,7 +193,7 @@ __device__ __forceinline__ void gather_tail(const float4 *__restrict__ h4,
 #pragma unroll
             for (int t = 0; t < 4; ++t) {
                 const int32_t e = hd.beg[k] + j0 + t;
-                u[k][t] = col[e < maxend ? e : maxend - 1];
+                u[k][t] = (U0 && j0 == 0) ? u0[k][t] : col[e < maxend ? e : maxend - 1];
             }
         float4 a[RPT][4];
 #pragma unroll

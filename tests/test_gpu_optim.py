@@ -169,6 +169,10 @@ def test_bench_two_ranks_gloo_on_one_gpu(tmp_path, strong):
     assert line["scaling"] == ("strong" if strong else "weak")
     assert line["config"]["allreduce"] == "between two graph replays"
     assert line["config"]["final_loss"] == line["config"]["final_loss"]  # finite (not NaN)
+    # replica mode: after the timed steps both ranks hold bitwise the same
+    # parameters and BatchNorm statistics (the one averaged bucket applied by
+    # both); the step itself is parity-tested in tests/test_gpu_dp.py
+    assert line["config"]["replica_max_abs_diff"] == 0.0
 
 
 def test_bench_allreduce_captured_one_rank_rccl():

@@ -1184,3 +1184,68 @@ def test_finetune_from_shipped_checkpoint(pkg, dev):
     check_grads_model({k[5:]: v for k, v in g.items() if k.startswith("grad_")},
                       lambda n: params[n].grad, tol=1e-3)
     assert all(p.grad is None for n, p in params.items() if n not in trainable)
+
+
+def test_finetune_from_shipped_checkpoint_captured(pkg, dev):
+    """The fine-tune step as bench.py --finetune runs it — capacity-sized
+    static buffers, the batch loaded from a resident pool inside the graph,
+    forward (device Set2Set) + BCE + backward captured as one HIP graph and
+    replayed — against the reference's own run on the shipped checkpoint
+    (finetune_molhiv_ckpt): scores and loss 1e-4, the trainable gradients as
+    in the eager test."""
+    import copy
+    from types import SimpleNamespace
+    g = load_golden("finetune_molhiv_ckpt")
+    levels, cfg, sd = checkpoint_fixture(pkg)
+    args = SimpleNamespace(recons_type="adj", useAtt=1, readout_f="sum", d_transfer=32,
+                           batch_size=int(g["B"]), gin_layers=int(g["L"]),
+                           task="graph_classification", dataset=str(g["dataset"]), device=dev)
+    pre = pkg.models.model_from_state(levels, cfg, sd, args)
+    F_in, B, k = int(g["F"]), int(g["B"]), int(cfg["k_transition"])
+    ft = pkg.models.Mainmodel_finetuning(args, F_in, 64, 4, 4, int(g["k"]), 1, pre, "GIN")
+    ft.load_state_dict({k_[6:]: torch.tensor(v) for k_, v in g.items() if k_.startswith("param_")},
+                       strict=False)
+    ft = ft.to(dev).train()
+    gx = pkg.graph.GraphBatch.from_edges(g["src"], g["dst"], len(g["x_raw"]), True,
+                                         g["batch_num_nodes"])
+    dict.__setitem__(gx.ndata, "x", F.normalize(torch.tensor(g["x_raw"]).float()))
+    other, _ = pkg.graph.collate_pyg(pkg.synth.molecules(B, "molhiv", seed=3))
+    dict.__setitem__(other.ndata, "x", F.normalize(other.ndata["x"].float()))
+    hosts = [other, gx]
+    n_cap, e_cap, mgn, caps = pkg.graph.StaticBatch.capacities(hosts, k, slack=1.05)
+    static = pkg.graph.StaticBatch(B, n_cap, e_cap, F_in, mgn, caps, dev, k=k)
+    pool = static.pool([static.pad(h) for h in hosts])
+    s_ug = torch.zeros(n_cap, device=dev)
+    s_uf = torch.zeros(n_cap, 64, device=dev)
+    tg = torch.tensor(g["targets"], device=dev).float()
+
+    def body():
+        static.load_next(pool)
+        scores, *_ = ft(static.graph, static.x, None, None, 1, None, 2, dev, B, noise=(s_ug, s_uf))
+        loss = ft.loss(scores, tg)
+        loss.backward()
+        return scores.detach(), loss.detach()
+
+    snap = copy.deepcopy(ft.state_dict())
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):  # warm-up on pool[0] (allocator)
+        body()
+    torch.cuda.current_stream().wait_stream(side)
+    torch.cuda.synchronize()
+    ft.load_state_dict(snap)
+    ft.zero_grad(set_to_none=True)
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        scores, loss = body()
+    n = len(g["x_raw"])
+    s_ug[:n].copy_(torch.tensor(g["train_u_gate"]))
+    s_uf[:n].copy_(torch.tensor(g["train_u_feat"]))
+    graph.replay()  # loads pool[1] = the golden batch (the warm-up took pool[0])
+    torch.cuda.synchronize()
+    assert pool["cursor"].tolist()[0] == 2
+    assert rel_err(scores.cpu(), g["train_scores"]) < 1e-4
+    assert rel_err(loss.item(), g["loss"]) < 1e-4
+    params = dict(ft.named_parameters())
+    check_grads_model({k_[5:]: v for k_, v in g.items() if k_.startswith("grad_")},
+                      lambda n_: params[n_].grad, tol=1e-3)

@@ -186,13 +186,7 @@ int scgib_bn_bwd_finalize(const float *tile_stats, int64_t n_nodes, int32_t trai
  * scgib_gin_bwd_stats_bn = scgib_gin_bwd_stats + scgib_bn_bwd_finalize. */
 int64_t scgib_gin_bn_ws_floats(int64_t n_nodes);
 int64_t scgib_gin_counters(int64_t n_nodes);
-/* d_in = 64 layers of many more tiles than the device holds (>= 2048 tiles,
- * BatchNorm not deferred) run a walking form of the layer kernel: each
- * workgroup a contiguous run of tiles, weights staged once, the next tile's
- * gather in flight under the current tile's GEMMs; bitwise the same outputs.
- * Testing hook: 0 = never walk, 1 = from the threshold (default), 2 = whenever
- * eligible; returns the previous setting. */
-int scgib_set_fwd_walk(int mode);
+
 int scgib_gin_layer_fwd_bn(const float *h_in, int32_t d_in, const float *in_stat,
                            const int32_t *rowptr, const int32_t *col, int64_t n_nodes,
                            float one_plus_eps, const float *w1, const float *b1, const float *w2,

@@ -246,7 +246,8 @@ __device__ __forceinline__ void bn_pending_finish(const scgib_bn_pending &pend, 
 // Per-tile (S, M2) -> group (S_g, M2_g) -> layer (mean, M2); exact
 // decomposition M2 = sum_b [M2_b + (S_b - n_b mean)^2 / n_b] at each level.
 // arrivals = tiles of group g whose statistics this workgroup contributes
-// (1: a tile kernel; the walking kernel arrives once per group it touched)
+// (1 per tile kernel; a workgroup running several tiles of one group may
+// arrive for all of them at once)
 __device__ void bn_fwd_hier(const float *__restrict__ part, int64_t n, int64_t tile,
                             const BnFwdFuse &fz, unsigned arrivals = 1u) {
     const int64_t nt = (n + TM - 1) / TM;
@@ -851,330 +852,6 @@ __global__ __launch_bounds__(256, (kFwdAlias<DIN, GATHER, PRE> ? 3 : 1)) void gi
         bn_fwd_hier(part, n, tile, fz);
         SCGIB_MARK(5);
     }
-}
-
-// ---------------------------------------------------------------------------
-// gin_fwd_walk_k: the d_in = 64 gathering layer for batches of many more
-// tiles than the chip holds (the ZINC-scale superbatch: 18.7 k tiles for 768
-// resident slots; BatchNorm not deferred there).  gin_fwd_k's per-tile
-// workgroups each reload 32 KB of weights and spend ~8.6 of a tile's ~18.7 us
-// in the gather's three dependent memory hops (row pointers -> neighbour
-// indices -> rows; tools/superbatch_trace.py): the chip's bytes in flight
-// come from the ~46 % of workgroups that are gathering at any moment.  Here a
-// workgroup walks a contiguous run of tiles with the weights staged in LDS
-// once, and the gather is pipelined two tiles deep: while tile t's GEMMs,
-// stores and statistics run, tile t + 1's rows (self + first neighbour round)
-// are in flight (issued at the top of iteration t from indices fetched during
-// t - 1), and tile t + 2's row pointers and indices are fetched.  Barriers
-// inside the loop wait for LDS only (lds_barrier), so those loads and the
-// agg / r / z2 stores stay in flight across them; the statistics arrivals
-// are made once per BatchNorm group after the loop.  Per tile the same gather
-// arithmetic (gather_round / gather_self), GEMMs and statistics as gin_fwd_k:
-// every output, tile statistic and BatchNorm record is bitwise gin_fwd_k's.
-// ---------------------------------------------------------------------------
-struct WalkIdx {     // a tile's CSR ranges and first-round neighbour indices
-    int32_t beg[4], end[4];
-    int32_t u[4][4];
-};
-struct WalkRows {    // a tile's self rows and first-round neighbour rows
-    int32_t beg[4], end[4];
-    float4 self[4];
-    float4 a[4][4];
-};
-
-__device__ __forceinline__ void walk_head(const int32_t *__restrict__ rowptr, int64_t row0,
-                                          int nv, int rbase, int32_t (&beg)[4], int32_t (&end)[4]) {
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        const int rr = rbase + 16 * k;
-        const int64_t v = row0 + (rr < nv ? rr : nv - 1);
-        beg[k] = rowptr[v];
-        end[k] = rowptr[v + 1];
-    }
-}
-
-__device__ __forceinline__ int walk_maxend(const int32_t (&beg)[4], const int32_t (&end)[4],
-                                           int &maxdeg) {
-    int me = 0;
-    maxdeg = 0;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        me = end[k] > me ? end[k] : me;
-        const int d = end[k] - beg[k];
-        maxdeg = d > maxdeg ? d : maxdeg;
-    }
-    return me;
-}
-
-// The first round's neighbour indices.  Unconditional loads from clamped
-// addresses (a conditional write would keep an older tile's values live
-// around the loop): with no in-edges in this thread's rows the index reads
-// col[0] (the caller's col holds >= 1 word) and is replaced by row 0;
-// gather_round weighs such slots 0.
-__device__ __forceinline__ void walk_idx(const int32_t *__restrict__ col, WalkIdx &x) {
-    int maxdeg;
-    const int me = walk_maxend(x.beg, x.end, maxdeg);
-    const int last = me > 0 ? me - 1 : 0;
-#pragma unroll
-    for (int k = 0; k < 4; ++k)
-#pragma unroll
-        for (int t = 0; t < 4; ++t) {
-            const int32_t e = x.beg[k] + t;
-            const int32_t u = col[e < me ? e : last];
-            x.u[k][t] = maxdeg > 0 ? u : 0;
-        }
-}
-
-__device__ __forceinline__ void walk_rows(const float4 *__restrict__ h4, int64_t row0, int nv,
-                                          int rbase, int c, const WalkIdx &x, WalkRows &g) {
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        const int rr = rbase + 16 * k;
-        const int64_t v = row0 + (rr < nv ? rr : nv - 1);
-        g.beg[k] = x.beg[k];
-        g.end[k] = x.end[k];
-        g.self[k] = h4[v * 16 + c];
-    }
-#pragma unroll
-    for (int k = 0; k < 4; ++k)
-#pragma unroll
-        for (int t = 0; t < 4; ++t) g.a[k][t] = h4[static_cast<int64_t>(x.u[k][t]) * 16 + c];
-}
-
-// agg of the four rows: the prefetched first round, any further rounds of
-// 4 (loaded here), the self term — gather_tail's arithmetic, in its order
-template <bool XFORM>
-__device__ __forceinline__ void walk_finish(const float4 *__restrict__ h4,
-                                            const int32_t *__restrict__ col, const WalkRows &g,
-                                            int c, float ope, float4 sc, float4 sh,
-                                            float4 (&acc)[4]) {
-    int maxdeg;
-    const int me = walk_maxend(g.beg, g.end, maxdeg);
-    int32_t deg[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        acc[k] = make_float4(0.f, 0.f, 0.f, 0.f);
-        deg[k] = g.end[k] - g.beg[k];
-    }
-    gather_round<4, XFORM>(g.a, 0, deg, sc, sh, acc);  // (maxdeg 0: every weight 0)
-    for (int j0 = 4; j0 < maxdeg; j0 += 4) {
-        int32_t u[4][4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k)
-#pragma unroll
-            for (int t = 0; t < 4; ++t) {
-                const int32_t e = g.beg[k] + j0 + t;
-                u[k][t] = col[e < me ? e : me - 1];
-            }
-        float4 a[4][4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k)
-#pragma unroll
-            for (int t = 0; t < 4; ++t) a[k][t] = h4[static_cast<int64_t>(u[k][t]) * 16 + c];
-        gather_round<4, XFORM>(a, j0, deg, sc, sh, acc);
-    }
-    gather_self<4, XFORM>(g.self, ope, sc, sh, acc);
-}
-
-// DEEP: the gather pipelined two tiles deep (tile t + 1's rows in flight
-// through all of tile t) at one workgroup per CU (the prefetch needs > 256
-// VGPRs); shallow: one tile deep (tile t + 1's rows issued after tile t's
-// second GEMM) at two workgroups per CU
-template <bool DEEP>
-constexpr int kWalkPerCU = DEEP ? 1 : 2;
-#ifndef SCGIB_WALK_DEEP
-#define SCGIB_WALK_DEEP 0
-#endif
-constexpr bool kWalkDeep = SCGIB_WALK_DEEP != 0;
-
-// trace build: per-workgroup wall-clock time summed over the run's tiles per
-// phase (tools/superbatch_trace.py, TRACE_ENTRY walk)
-#ifdef SCGIB_TRACE
-#define WALK_T0() uint64_t wt_prev = wall_clock64(), wt_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}
-#define WALK_PH(k)                                \
-    do {                                          \
-        const uint64_t t_ = wall_clock64();       \
-        wt_acc[k] += t_ - wt_prev;                \
-        wt_prev = t_;                             \
-    } while (0)
-#define WALK_END()                                                                       \
-    do {                                                                                 \
-        if (threadIdx.x == 0 && g_trace)                                                 \
-            for (int k_ = 0; k_ < 8; ++k_) g_trace[blockIdx.x * 32 + k_] = wt_acc[k_];    \
-    } while (0)
-#else
-#define WALK_T0() do {} while (0)
-#define WALK_PH(k) do {} while (0)
-#define WALK_END() do {} while (0)
-#endif
-
-template <bool XFORM, bool DEEP>
-__global__ __launch_bounds__(256, kWalkPerCU<DEEP>) void gin_fwd_walk_k(
-    const float *__restrict__ h, const float *__restrict__ in_scale,
-    const float *__restrict__ in_shift, const int32_t *__restrict__ rowptr,
-    const int32_t *__restrict__ col, int64_t ncap, float ope, const float *__restrict__ w1,
-    const float *__restrict__ b1, const float *__restrict__ w2, const float *__restrict__ b2,
-    float *__restrict__ agg_out, float *__restrict__ r_out, float *__restrict__ z2_out,
-    float *__restrict__ part, const int32_t *__restrict__ dims, BnFwdFuse fz, int64_t run) {
-    constexpr int LDA = 65;
-    __shared__ float sA[TM * LDA];  // the agg tile, then r
-    __shared__ float sW1[64 * LDA];
-    __shared__ float sW2[64 * LDH];
-    __shared__ float sRed[2][64];
-    const int64_t n = eff_count(dims, 0, ncap);
-    const int64_t ntc = (ncap + TM - 1) / TM;
-    const float4 *h4 = reinterpret_cast<const float4 *>(h);
-    int tid = threadIdx.x;
-    const int64_t t_beg = static_cast<int64_t>(blockIdx.x) * run;
-    const int64_t t_end = t_beg + run < ntc ? t_beg + run : ntc;
-    if (t_beg >= t_end) return;
-    WALK_T0();
-    WeightRegs<64> wregs;
-    load_weights<64>(w1, w2, wregs);
-    const int bcol = (tid >> 6 & 1) * 32 + (tid & 31);
-    const float bias1 = b1[bcol], bias2 = b2[bcol];
-    float4 sc = make_float4(1.f, 1.f, 1.f, 1.f), sh = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (XFORM) {
-        sc = ld4(in_scale + 4 * (tid & 15));
-        sh = ld4(in_shift + 4 * (tid & 15));
-    }
-    auto rows_of = [&](int64_t t) -> int {  // valid rows of tile t (0 past the batch)
-        const int64_t r = n - t * TM;
-        return static_cast<int>(t < t_end ? (r < TM ? (r > 0 ? r : 0) : TM) : 0);
-    };
-    // prologue: tile t_beg's rows, tile t_beg + 1's indices (a tile with no
-    // rows loads the first tile's addresses again: valid, unused)
-    WalkIdx x;
-    WalkRows g;
-    int nv = rows_of(t_beg), nv1 = rows_of(t_beg + 1);
-    const int nvs = nv > 0 ? nv : 1;
-    walk_head(rowptr, t_beg * TM, nvs, tid >> 4, x.beg, x.end);
-    walk_idx(col, x);
-    walk_rows(h4, t_beg * TM, nvs, tid >> 4, tid & 15, x, g);
-    if constexpr (DEEP) {
-        walk_head(rowptr, (nv1 > 0 ? t_beg + 1 : t_beg) * TM, nv1 > 0 ? nv1 : nvs, tid >> 4,
-                  x.beg, x.end);
-        walk_idx(col, x);
-    }
-    store_weights<64>(wregs, sW1, sW2);
-    WALK_PH(7);
-    for (int64_t tile = t_beg; tile < t_end; ++tile) {
-        // the lane's indices, derived again in every iteration: values hoisted
-        // out of the loop as invariants (addresses, offsets) would stay live
-        // across the whole tile beside the prefetched gather and spill
-        asm volatile("" : "+v"(tid));
-        const int l = tid & 63, w = tid >> 6, c = tid & 15, rbase = tid >> 4;
-        const int wr = w >> 1, wc = w & 1, ccol = wc * 32 + (l & 31);
-        const int64_t row0 = tile * TM;
-        if (dims) {  // capacity mode: zero this tile's padded rows [nv, rows in capacity)
-            const int ncr = static_cast<int>(ncap - row0 < TM ? ncap - row0 : TM);
-            for (int idx = nv * 64 + tid; idx < ncr * 64; idx += 256) {
-                r_out[row0 * 64 + idx] = 0.f;
-                z2_out[row0 * 64 + idx] = 0.f;
-                agg_out[row0 * 64 + idx] = 0.f;
-            }
-        }
-        if (nv == 0) {  // past the batch (block-uniform): so are the later tiles
-            if (tid < 128) part[tile * 128 + tid] = 0.f;
-            continue;
-        }
-        float4 acc[4];
-        walk_finish<XFORM>(h4, col, g, c, ope, sc, sh, acc);
-        WALK_PH(0);
-        // tile + 2's row pointers, then tile + 1's rows (its indices came
-        // during the previous tile) — in this order: the hardware retires
-        // loads in issue order, so tile + 2's indices (after GEMM1) wait only
-        // for the row pointers, not for the rows
-        const int nvn = rows_of(tile + 1), nvn2 = rows_of(tile + 2);
-        const int64_t tn = nvn > 0 ? tile + 1 : tile, tn2 = nvn2 > 0 ? tile + 2 : tile;
-        if constexpr (DEEP) {
-            int32_t hb[4], he[4];
-            walk_head(rowptr, tn2 * TM, nvn2 > 0 ? nvn2 : nv, rbase, hb, he);
-            walk_rows(h4, tn * TM, nvn > 0 ? nvn : nv, rbase, c, x, g);
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                x.beg[k] = hb[k];
-                x.end[k] = he[k];
-            }
-        } else {  // tile + 1's row pointers (its indices after GEMM1, rows after GEMM2)
-            walk_head(rowptr, tn * TM, nvn > 0 ? nvn : nv, rbase, x.beg, x.end);
-        }
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const int rr = rbase + 16 * k;
-            if (rr < nv) st4(agg_out + (row0 + rr) * 64 + 4 * c, acc[k]);
-            float *d = sA + rr * LDA + 4 * c;
-            d[0] = acc[k].x; d[1] = acc[k].y; d[2] = acc[k].z; d[3] = acc[k].w;
-        }
-        lds_barrier();
-        WALK_PH(1);
-        {
-            const f32x16 a1 = mma_pf<64, false, false>(sA + wr * 32 * LDA, LDA, sW1 + wc * 32 * LDA,
-                                                       LDA, zero16());
-            lds_barrier();  // every wave's reads of the agg tile are done: r takes its buffer
-#pragma unroll
-            for (int reg = 0; reg < 16; ++reg) {
-                const int row = wr * 32 + acc_row(reg, l);
-                const float v = fmaxf(a1[reg] + bias1, 0.f);
-                sA[row * LDH + ccol] = v;
-                if (row < nv) r_out[(row0 + row) * 64 + ccol] = v;
-            }
-        }
-        WALK_PH(2);
-        walk_idx(col, x);  // the first-round indices of tile + 2 (DEEP) / tile + 1
-        lds_barrier();
-        WALK_PH(3);
-        f32x16 a2 = mma_pf<64, false, false>(sA + wr * 32 * LDH, LDH, sW2 + wc * 32 * LDH, LDH,
-                                             zero16());
-        if constexpr (!DEEP) walk_rows(h4, tn * TM, nvn > 0 ? nvn : nv, rbase, c, x, g);
-        float s = 0.f;
-#pragma unroll
-        for (int reg = 0; reg < 16; ++reg) {
-            const int row = wr * 32 + acc_row(reg, l);
-            a2[reg] += bias2;
-            if (row < nv) {
-                z2_out[(row0 + row) * 64 + ccol] = a2[reg];
-                s += a2[reg];
-            }
-        }
-        s += __shfl_xor(s, 32, kWave);
-        if (l < 32) sRed[wr][ccol] = s;
-        lds_barrier();
-        const float csum = sRed[0][ccol] + sRed[1][ccol];
-        const float cmean = csum / nv;
-        float m2 = 0.f;
-#pragma unroll
-        for (int reg = 0; reg < 16; ++reg) {
-            const int row = wr * 32 + acc_row(reg, l);
-            const float d = a2[reg] - cmean;
-            if (row < nv) m2 += d * d;
-        }
-        m2 += __shfl_xor(m2, 32, kWave);
-        lds_barrier();
-        if (l < 32) sRed[wr][ccol] = m2;
-        lds_barrier();
-        if (wr == 0 && l < 32) {
-            st_agent(part + tile * 128 + ccol, csum);
-            st_agent(part + tile * 128 + 64 + ccol, sRed[0][ccol] + sRed[1][ccol]);
-        }
-        nv = nvn;
-        WALK_PH(4);
-    }
-    // the statistics arrivals of every tile this workgroup ran, one per
-    // BatchNorm group it touched (a run of ~37 tiles spans 3-4 groups); the
-    // last arriver of each group combines it as gin_fwd_k's would
-    if (fz.counters) {
-        const int64_t nt = (n + TM - 1) / TM;
-        const int64_t last = t_end < nt ? t_end : nt;
-        for (int64_t t0 = t_beg; t0 < last;) {
-            const int64_t gend = (t0 / kGroup + 1) * kGroup;
-            const int64_t t1 = gend < last ? gend : last;
-            bn_fwd_hier(part, n, t0, fz, static_cast<unsigned>(t1 - t0));
-            t0 = t1;
-        }
-    }
-    WALK_PH(5);
-    WALK_END();
 }
 
 // Batch mean / biased variance from the per-tile (sum, centred M2), fp64,
@@ -2041,21 +1718,6 @@ extern "C" int64_t scgib_gin_bwd_slabs(int64_t n_nodes) {
     return n_nodes <= 0 ? 0 : bwd_grid(scgib_gin_tiles(n_nodes));
 }
 
-// The walking forward (gin_fwd_walk_k) from this many tiles on (a batch
-// several times the chip's resident slots); scgib_set_fwd_walk: 0 = never,
-// 1 = from the threshold (default), 2 = whenever eligible (tests: both paths
-// bitwise equal)
-constexpr int64_t kWalkMinTiles = 2048;
-static int g_fwd_walk = 1;
-extern "C" int scgib_set_fwd_walk(int mode) {
-    const int prev = g_fwd_walk;
-    if (mode >= 0 && mode <= 2) g_fwd_walk = mode;
-    return prev;
-}
-static bool fwd_walk(int64_t nt) {
-    return g_fwd_walk == 2 || (g_fwd_walk == 1 && nt >= kWalkMinTiles);
-}
-
 static int launch_gin_fwd(const float *h_in, int32_t d_in, const float *in_stat,
                           const int32_t *rowptr, const int32_t *col, int64_t n_nodes,
                           float one_plus_eps, const float *w1, const float *b1, const float *w2,
@@ -2065,16 +1727,6 @@ static int launch_gin_fwd(const float *h_in, int32_t d_in, const float *in_stat,
     const int64_t nt = scgib_gin_tiles(n_nodes);
     const float *isc = in_stat ? in_stat + 128 : nullptr, *ish = in_stat ? in_stat + 192 : nullptr;
     const scgib_bn_pending pd = pend ? *pend : scgib_bn_pending{};
-    if (d_in == 64 && !pend && !fz.defer && fwd_walk(nt)) {
-        const int64_t slots = int64_t(kWalkPerCU<kWalkDeep>) * kCUs;
-        const int64_t run = (nt + (nt < slots ? nt : slots) - 1) / (nt < slots ? nt : slots);
-        const unsigned grid = static_cast<unsigned>((nt + run - 1) / run);
-        if (in_stat)
-            gin_fwd_walk_k<true, kWalkDeep><<<grid, 256, 0, st>>>(h_in, isc, ish, rowptr, col, n_nodes, one_plus_eps, w1, b1, w2, b2, agg, r, z2, tile_stats, dims, fz, run);
-        else
-            gin_fwd_walk_k<false, kWalkDeep><<<grid, 256, 0, st>>>(h_in, isc, ish, rowptr, col, n_nodes, one_plus_eps, w1, b1, w2, b2, agg, r, z2, tile_stats, dims, fz, run);
-        return launch_status();
-    }
     if (d_in == 32)
         gin_fwd_k<32, false><<<dim3((unsigned)nt), 256, 0, st>>>(h_in, isc, ish, rowptr, col, n_nodes, one_plus_eps, w1, b1, w2, b2, agg, r, z2, tile_stats, dims, fz, PreArgs{}, pd, ReconArgs{});
     else if (in_stat || pend)

@@ -51,8 +51,6 @@ def main():
         recs.append((meta, buf[: tiles * 32].view(tiles, 32).cpu().numpy().copy()))
         return out
 
-    walk = int(os.environ.get("FWD_WALK", "0"))  # 0: gin_fwd_k (per-tile marks); 1/2: the walk
-    lib.scgib_set_fwd_walk(walk)
     with torch.no_grad():
         for it in range(2):
             recs.clear()
@@ -61,20 +59,6 @@ def main():
             torch.cuda.synchronize()
     pkg.ops.OBSERVER = None
     print(f"superbatch n={n} e={g.num_edges()} tiles={tiles}")
-    if walk:  # gin_fwd_walk_k: per-workgroup phase sums over its run of tiles
-        names = ["finish", "head+rows+agg st", "gemm1+r st", "idx", "gemm2+z2+stats",
-                 "arrivals", "-", "prologue"]
-        for li, (meta, t) in enumerate(recs):
-            nb = int((t[:, :8].sum(axis=1) != 0).sum())
-            t = t[:nb, :8] / 100.0  # us
-            run = (tiles + nb - 1) // nb
-            print(f"layer {li}: {nb} workgroups x {run} tiles; per workgroup total "
-                  f"p50={np.percentile(t.sum(axis=1), 50):.1f} max={t.sum(axis=1).max():.1f} us")
-            for k, nm in enumerate(names):
-                if nm != "-":
-                    print(f"    {nm:18s} per tile {t[:, k].mean() / run:6.2f} us "
-                          f"(workgroup sum p50 {np.percentile(t[:, k], 50):7.1f})")
-        return
     for li, (meta, t) in enumerate(recs):
         nb = int((t[:, 0] != 0).sum())
         t = t[t[:, 0] != 0]

@@ -261,7 +261,8 @@ class _SCGIBCore(nn.Module):
         noisy = im[:, : self.hidden_dim]
         return im, kl, noisy, z2, z1
 
-    def _encode_forked(self, enc_owner, batch_g, batch_x, fork=True, draw_noise=False):
+    def _encode_forked(self, enc_owner, batch_g, batch_x, fork=True, draw_noise=False,
+                       transfer=None):
         """Fast path of forward() when the ego-nets are built on the device:
         the ego branch (ego-net build, x_subs gather, transfer_d, Encoder2,
         readout) runs on a second HIP stream, concurrently with Encoder1 on the
@@ -272,9 +273,11 @@ class _SCGIBCore(nn.Module):
         main = torch.cuda.current_stream(batch_x.device)
         side = _side_stream(batch_x.device) if fork else main
         # transfer_d folded into both encoders' first layer (raw features are
-        # gathered in-kernel, through the ego -> parent map for Encoder2)
+        # gathered in-kernel, through the ego -> parent map for Encoder2);
+        # ``transfer``: another module's transfer_d (the fine-tune head's)
+        td = self.transfer_d if transfer is None else transfer
         fold = (enc_owner.Encoder1.fused and enc_owner.Encoder2.fused
-                and self.transfer_d.bias is None and self.transfer_d.out_features == 32
+                and td.bias is None and td.out_features == 32
                 and batch_x.shape[1] <= 16 and not batch_x.requires_grad)
         if fork:
             ops.check_fork(main)  # never a nested fork while capturing (ops.check_fork)
@@ -299,7 +302,7 @@ class _SCGIBCore(nn.Module):
                 def tail():  # the interaction's noise, drawn beside the ego chain
                     drawn["u"] = ops.device_noise(batch_g.num_nodes(), batch_x.device)
             outs = ops.gin_encoder_pair_x(
-                batch_x, ego, enc_owner.Encoder2, batch_g, enc_owner.Encoder1, self.transfer_d,
+                batch_x, ego, enc_owner.Encoder2, batch_g, enc_owner.Encoder1, td,
                 ego.ndata["_ID"], side, lin0, tail, pf)
             subgraphs_features, sub_readout, graph_features = outs[0], outs[1], outs[2]
             t = outs[3] if len(outs) > 3 else None
@@ -308,17 +311,16 @@ class _SCGIBCore(nn.Module):
             if fold:
                 ego = G.egonet_batch(batch_g, self.k_transition)
                 subgraphs_features = ops.gin_encoder_x(batch_x, ego, enc_owner.Encoder2,
-                                                       self.transfer_d, ego.ndata["_ID"])
+                                                       td, ego.ndata["_ID"])
             else:
                 ego, x_subs = self._prepare_ego(batch_g, None, batch_x, None)
-                subgraphs_features = enc_owner.Encoder2(ego, self.transfer_d(x_subs))
+                subgraphs_features = enc_owner.Encoder2(ego, td(x_subs))
             sub_readout = ops.segment_sum(subgraphs_features, ego.graph_ptr, ego.batch_size,
                                           ego.seg_dims)
         if fold:
-            graph_features = ops.gin_encoder_x(batch_x, batch_g, enc_owner.Encoder1,
-                                               self.transfer_d)
+            graph_features = ops.gin_encoder_x(batch_x, batch_g, enc_owner.Encoder1, td)
         else:
-            graph_features = enc_owner.Encoder1(batch_g, self.transfer_d(batch_x))
+            graph_features = enc_owner.Encoder1(batch_g, td(batch_x))
         main.wait_stream(side)
         subgraphs_features.record_stream(main)
         sub_readout.record_stream(main)
@@ -688,12 +690,24 @@ class Mainmodel_finetuning(nn.Module):
                 edge_index=None, k_transition=None, device=None, batch_size=2, noise=None):
         self.batch_size = batch_size
         self.device = device
-        if flatten_batch_subgraphs is None:  # ego-nets built on the device
-            flatten_batch_subgraphs, x_subs = self._prepare_ego(batch_g, batch_x, x_subs)
-        batch_x = self.transfer_d(batch_x)
-        x_subs = self.transfer_d(x_subs)
-        im = self.model.extract_features(None, batch_g, batch_x, flatten_batch_subgraphs, x_subs,
-                                         device, noise)[0]
+        inner = self.model
+        if flatten_batch_subgraphs is None and x_subs is None and batch_x.is_cuda and \
+                isinstance(inner, _SCGIBCore):
+            # ego-nets built on the device: this head's transfer_d folded into the
+            # pretrained model's encoders, the ego branch forked (as the
+            # pretraining step and Mainmodel_domainadapt run them) — the same
+            # maths as transfer_d then extract_features (models.py:510-513)
+            ego, enc = inner._encode_forked(inner, batch_g, batch_x, FORK_ENCODERS,
+                                            noise is None, transfer=self.transfer_d)
+            im = inner._extract(inner, batch_g, None, ego, None, noise, enc)[0]
+            _drop_graph_refs(inner)
+        else:
+            if flatten_batch_subgraphs is None:  # ego-nets built on the device
+                flatten_batch_subgraphs, x_subs = self._prepare_ego(batch_g, batch_x, x_subs)
+            batch_x = self.transfer_d(batch_x)
+            x_subs = self.transfer_d(x_subs)
+            im = inner.extract_features(None, batch_g, batch_x, flatten_batch_subgraphs, x_subs,
+                                        device, noise)[0]
         im = ops.mlp2(im, self.MLP, batch_g.dims)
         im = self.s2s(batch_g, im)
         scores = self.predict(im)

@@ -192,6 +192,9 @@ int64_t scgib_gin_counters(int64_t n_nodes);
  * 0 = the per-neighbour gather, 1 = the window (default); bitwise the same
  * outputs; returns the previous setting. */
 int scgib_set_fwd_window(int on);
+/* The same for the transposed gather of scgib_gin_bwd_stats(_bn)(_fold)
+ * (testing hook, default 1). */
+int scgib_set_bwd_window(int on);
 
 int scgib_gin_layer_fwd_bn(const float *h_in, int32_t d_in, const float *in_stat,
                            const int32_t *rowptr, const int32_t *col, int64_t n_nodes,

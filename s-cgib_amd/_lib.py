@@ -20,6 +20,7 @@ SIGNATURES = {
     "scgib_abi_version": (ctypes.c_int, []),
     "scgib_set_recon_fold": (ctypes.c_int, [ctypes.c_int]),
     "scgib_set_fwd_window": (ctypes.c_int, [ctypes.c_int]),
+    "scgib_set_bwd_window": (ctypes.c_int, [ctypes.c_int]),
     "scgib_set2set_fwd": (ctypes.c_int, [_P, _P, _P, _I64, _I32, _P, _P, _P]),
     "scgib_set2set_bwd": (ctypes.c_int, [_P, _P, _P, _I64, _I32, _P, _P, _P, _P, _I64, _P]),
     "scgib_pool_copy": (ctypes.c_int, [_P, _I32, _P, _P, _I64, _P]),

@@ -1288,7 +1288,92 @@ __device__ __forceinline__ void slab_fold_block(const scgib_slab_job &J, int b, 
                                       red[192 + el]);
 }
 
-template <bool GATHER, bool SEG = false>
+// The transposed gather of gin_bwd_stats_k through the LDS row window (as
+// gin_fwd_win_k's forward gather, no input transform): rows [row0 - 32,
+// row0 + 96) of h in one contiguous load beside the row pointers, the first
+// index round after them, the sum from LDS (gather_tail's order; a neighbour
+// outside the window from global memory).  sWin: kWinRows x 64 floats.
+__device__ __forceinline__ void win_gather_rows(const float4 *__restrict__ h4,
+                                                const int32_t *__restrict__ rowptr,
+                                                const int32_t *__restrict__ col, int64_t row0,
+                                                int nv, int64_t n, int rbase, int c, float ope,
+                                                float *sWin, float4 (&acc)[4]) {
+    const int tid = threadIdx.x;
+    const int64_t w0 = row0 - kWinLead;
+    int32_t beg[4], end[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int rr = rbase + 16 * k;
+        const int64_t v = row0 + (rr < nv ? rr : nv - 1);
+        beg[k] = rowptr[v];
+        end[k] = rowptr[v + 1];
+    }
+    float4 wv[kWinRows * 16 / 256];
+#pragma unroll
+    for (int k = 0; k < kWinRows * 16 / 256; ++k) {
+        const int64_t g = w0 + ((tid + 256 * k) >> 4);
+        wv[k] = h4[(g < 0 ? 0 : (g < n ? g : n - 1)) * 16 + c];
+    }
+    int maxdeg = 0, maxend = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        maxend = end[k] > maxend ? end[k] : maxend;
+        const int d = end[k] - beg[k];
+        maxdeg = d > maxdeg ? d : maxdeg;
+    }
+    int32_t u0[4][4];
+    if (maxdeg > 0) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                const int32_t e = beg[k] + t;
+                u0[k][t] = col[e < maxend ? e : maxend - 1];
+            }
+    }
+#pragma unroll
+    for (int k = 0; k < kWinRows * 16 / 256; ++k)
+        *reinterpret_cast<float4 *>(sWin + (((tid + 256 * k) >> 4) * 64) + 4 * c) = wv[k];
+    lds_barrier();
+    auto rowval = [&](int32_t u) -> float4 {
+        const int64_t o = static_cast<int64_t>(u) - w0;
+        const bool in = o >= 0 && o < kWinRows;
+        float4 v = *reinterpret_cast<const float4 *>(sWin + (in ? o : 0) * 64 + 4 * c);
+        if (!in) v = h4[static_cast<int64_t>(u) * 16 + c];
+        return v;
+    };
+    int32_t deg[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        acc[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+        deg[k] = end[k] - beg[k];
+    }
+    for (int j0 = 0; j0 < maxdeg; j0 += 4) {
+        int32_t u[4][4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                const int32_t e = beg[k] + j0 + t;
+                u[k][t] = j0 == 0 ? u0[k][t] : col[e < maxend ? e : maxend - 1];
+            }
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+#pragma unroll
+            for (int t = 0; t < 4; ++t)
+                acc[k] = fma4(rowval(u[k][t]), j0 + t < deg[k] ? 1.f : 0.f, acc[k]);
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int rr = rbase + 16 * k;
+        const float4 x = *reinterpret_cast<const float4 *>(
+            sWin + ((rr < nv ? rr : nv - 1) + kWinLead) * 64 + 4 * c);
+        acc[k] = make_float4(ope * x.x + acc[k].x, ope * x.y + acc[k].y, ope * x.z + acc[k].z,
+                             ope * x.w + acc[k].w);
+    }
+}
+
+template <bool GATHER, bool SEG = false, bool WIN = false>
 __global__ __launch_bounds__(256) void gin_bwd_stats_k(
     const float *__restrict__ dh, const int32_t *__restrict__ rowptr_t,
     const int32_t *__restrict__ col_t, float ope, const float *__restrict__ z2,
@@ -1317,7 +1402,10 @@ __global__ __launch_bounds__(256) void gin_bwd_stats_k(
     SCGIB_MARK(0);
     SCGIB_MARK_HWID();
     float4 g[4];
-    if (GATHER) {
+    if (GATHER && WIN) {
+        __shared__ __attribute__((aligned(16))) float sWin[kWinRows * 64];
+        win_gather_rows(g4, rowptr_t, col_t, row0, nv, n, slot, c, ope, sWin, g);
+    } else if (GATHER) {
         gather_rows<4, 16, 16, false>(g4, rowptr_t, col_t, row0, nv, slot, c, ope, sc, sh, g);
     } else if (SEG) {
         int32_t sg[4];
@@ -2151,6 +2239,15 @@ extern "C" int scgib_bn_relu_apply(const float *z, const float *stat, int64_t n_
     return launch_status();
 }
 
+// the transposed gather of the statistics kernel through the LDS row window
+// (win_gather_rows); scgib_set_bwd_window: 0 = per-neighbour, 1 = window (default)
+static int g_bwd_window = 1;
+extern "C" int scgib_set_bwd_window(int on) {
+    const int prev = g_bwd_window;
+    if (on == 0 || on == 1) g_bwd_window = on;
+    return prev;
+}
+
 static int launch_gin_bwd_stats(const float *dh, const int32_t *rowptr_t, const int32_t *col_t,
                                 float one_plus_eps, const float *z2, const float *stat,
                                 int64_t n_nodes, float *dy, float *tile_stats,
@@ -2159,7 +2256,9 @@ static int launch_gin_bwd_stats(const float *dh, const int32_t *rowptr_t, const 
                                 const scgib_slab_job *fold = nullptr) {
     const scgib_slab_job fj = fold ? *fold : scgib_slab_job{};
     const unsigned grid = static_cast<unsigned>(scgib_gin_tiles(n_nodes) + slab_fold_blocks(fj));
-    if (rowptr_t)
+    if (rowptr_t && g_bwd_window)
+        gin_bwd_stats_k<true, false, true><<<dim3(grid), 256, 0, st>>>(dh, rowptr_t, col_t, one_plus_eps, z2, stat, n_nodes, dy, tile_stats, dims, bz, nullptr, nullptr, fj);
+    else if (rowptr_t)
         gin_bwd_stats_k<true><<<dim3(grid), 256, 0, st>>>(dh, rowptr_t, col_t, one_plus_eps, z2, stat, n_nodes, dy, tile_stats, dims, bz, nullptr, nullptr, fj);
     else if (g_seg)
         gin_bwd_stats_k<false, true><<<dim3(grid), 256, 0, st>>>(dh, rowptr_t, col_t, one_plus_eps, z2, stat, n_nodes, dy, tile_stats, dims, bz, g_seg, seg, fj);

@@ -916,12 +916,27 @@ def _fwd_window(pkg, on):
     return pkg._lib.load().scgib_set_fwd_window(on)
 
 
+def _windows(pkg, on):
+    """Both row-window gathers (forward layer, backward statistics) on / off;
+    returns the previous settings for _windows_restore."""
+    lib = pkg._lib.load()
+    return lib.scgib_set_fwd_window(on), lib.scgib_set_bwd_window(on)
+
+
+def _windows_restore(pkg, prev):
+    lib = pkg._lib.load()
+    lib.scgib_set_fwd_window(prev[0])
+    lib.scgib_set_bwd_window(prev[1])
+
+
 @pytest.mark.parametrize("workload,n_mols,mu", [("qm9", 300, None), ("qm9", 6000, None),
                                                  ("qm9", 150, 60.0)])
 def test_gin_encoder_window_forward_bitwise(pkg, dev, workload, n_mols, mu):
-    """The LDS row-window forward layer (gin_fwd_win_k) against the
-    per-neighbour gather (gin_fwd_k) on the same inputs: outputs, every
-    gradient and the BatchNorm running statistics bitwise equal — 300
+    """The LDS row-window gathers (the forward layer gin_fwd_win_k, the
+    backward statistics' transposed gather win_gather_rows) against the
+    per-neighbour gathers (gin_fwd_k, gather_rows) on the same inputs:
+    outputs, every gradient and the BatchNorm running statistics bitwise
+    equal — 300
     molecules (deferred BN), 6000 (~108 k rows: BN in-kernel, third
     statistics level) and molecules of ~60 atoms (neighbours outside the
     window: the global-memory fallback)."""
@@ -943,14 +958,14 @@ def test_gin_encoder_window_forward_bitwise(pkg, dev, workload, n_mols, mu):
     outs = []
     for on in (0, 1):
         gin_c = copy.deepcopy(gin)
-        prev = _fwd_window(pkg, on)
+        prev = _windows(pkg, on)
         try:
             x = h0.clone().requires_grad_(True)
             h = gin_c(g, x)
             (h * w).sum().backward()
             torch.cuda.synchronize()
         finally:
-            _fwd_window(pkg, prev)
+            _windows_restore(pkg, prev)
         outs.append((h.detach(), x.grad, {k: p.grad for k, p in gin_c.named_parameters()},
                      {k: b.clone() for k, b in gin_c.named_buffers()}))
     (ha, xa, ga, ba), (hb, xb, gb, bb) = outs

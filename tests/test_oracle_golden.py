@@ -138,3 +138,30 @@ def test_trans_logM_matches_reference_targets(pkg):
                                              True)
         got = pkg.graph.trans_logM(gi, k).numpy()
         np.testing.assert_array_equal(got, want)
+
+
+def test_oracle_recon_gram_form_equals_dense():
+    """The Gram form of loss_recon_adj that the config-size oracle runs use
+    above B = 512 (scgib_ref.pretrain_forward(dense_recon=False):
+    (||IM^T IM||^2 - 2 sum_{(u,v) in E} <im_u, im_v> + |E|) / N) against the
+    dense N x N restatement of models.py:762-768, in float64: loss and its
+    gradient w.r.t. IM, on a 3000-node graph with directed edges (A != A^T)
+    and self-loops — the restatement the large parity tests rely on."""
+    import torch
+    from oracle import scgib_ref as R
+    gen = torch.Generator().manual_seed(3)
+    n = 3000
+    src = torch.randint(0, n, (9000,), generator=gen)
+    dst = torch.randint(0, n, (9000,), generator=gen)
+    pairs = sorted(set(zip(src.tolist(), dst.tolist())) | {(i, i) for i in range(0, n, 97)})
+    src = torch.tensor([p[0] for p in pairs])
+    dst = torch.tensor([p[1] for p in pairs])
+    im = (0.2 * torch.randn(n, 64, generator=gen, dtype=torch.float64)).requires_grad_(True)
+    dense = R.recon_adj_dense(im, src, dst)
+    (gd,) = torch.autograd.grad(dense, im)
+    g = im.t() @ im
+    e = (im[src] * im[dst]).sum()
+    gram = (torch.sum(g * g) - 2 * e + len(src)) / n
+    (gg,) = torch.autograd.grad(gram, im)
+    assert abs(gram.item() - dense.item()) <= 1e-10 * abs(dense.item())
+    assert float((gg - gd).abs().max()) <= 1e-10 * float(gd.abs().max())

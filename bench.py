@@ -632,6 +632,9 @@ def main():
         pool.append(g)
 
     model = make_model(F_in, a.k, a.gin_layers, dev)
+    # rank 0's initial weights everywhere (each rank's seed still drives its
+    # own Gumbel / noise draws): replicas from the first step on
+    pkg.dist.broadcast_replicas(model)
     # gradients + the BN running statistics, averaged in one bucket per step
     reducer = pkg.dist.GradAllReducer(model.parameters(), buffers=pkg.dist.bn_buffers(model))
 

@@ -572,6 +572,20 @@ constexpr bool kLateWeights = true;  // (early: 0.4372 vs 0.4355 ms, round 2)
 template <int DIN, bool GATHER, bool PRE>
 constexpr bool kFwdAlias = ((DIN == 64 && GATHER && !PRE) || (DIN == 32 && GATHER && PRE));
 
+// blockIdx -> 64-row tile of a gathering layer.  The dispatcher deals
+// workgroups round-robin over the 8 XCDs (MI355X_MICROARCH.md, "Workgroup
+// dispatch"), so with tile = blockIdx consecutive tiles — which share rows:
+// the neighbours across a tile edge, the row window's halo — sit in
+// different L2s.  SCGIB_XCD_TILES = 1 gives each XCD a contiguous run of
+// tiles instead (xcd_remap): speed only, every tile computes the same bits
+// wherever it runs.
+#ifndef SCGIB_XCD_TILES  // (build-time A/B hook: tools/build_ab_lib.sh EXTRA=-DSCGIB_XCD_TILES=n)
+#define SCGIB_XCD_TILES 0
+#endif
+__device__ __forceinline__ int64_t tile_of_block(int64_t ntiles) {
+    return SCGIB_XCD_TILES ? xcd_remap(blockIdx.x, ntiles) : static_cast<int64_t>(blockIdx.x);
+}
+
 template <int DIN, bool XFORM, bool GATHER = true, bool PRE = false, bool RECON = false>
 __global__ __launch_bounds__(256, (kFwdAlias<DIN, GATHER, PRE> ? 3 : 1)) void gin_fwd_k(
     const float *__restrict__ h, const float *__restrict__ in_scale,
@@ -610,7 +624,8 @@ __global__ __launch_bounds__(256, (kFwdAlias<DIN, GATHER, PRE> ? 3 : 1)) void gi
         }
     }
     const int tid = threadIdx.x, l = tid & 63, w = tid >> 6;
-    const int64_t tile = blockIdx.x;
+    // (the head MLP's grid carries extra workgroups past its tiles: identity there)
+    const int64_t tile = GATHER ? tile_of_block(gridDim.x) : static_cast<int64_t>(blockIdx.x);
     const int64_t row0 = tile * TM;
     const int nv = static_cast<int>(n - row0 < TM ? (n - row0 > 0 ? n - row0 : 0) : TM);  // valid rows
     if (dims) {  // capacity mode: zero this tile's padded rows [nv, rows in capacity)
@@ -917,7 +932,7 @@ __global__ __launch_bounds__(256, 3) void gin_fwd_win_k(
     const int64_t n = eff_count(dims, 0, ncap);
     const int tid = threadIdx.x, l = tid & 63, w = tid >> 6;
     const int c = tid & 15, rbase = tid >> 4;
-    const int64_t tile = blockIdx.x, row0 = tile * TM;
+    const int64_t tile = tile_of_block(gridDim.x), row0 = tile * TM;
     const int nv = static_cast<int>(n - row0 < TM ? (n - row0 > 0 ? n - row0 : 0) : TM);
     if (dims) {  // capacity mode: zero this tile's padded rows [nv, rows in capacity)
         const int ncr = static_cast<int>(ncap - row0 < TM ? ncap - row0 : TM);
@@ -1389,7 +1404,8 @@ __global__ __launch_bounds__(256) void gin_bwd_stats_k(
     }
     const int64_t n = eff_count(dims, 0, ncap);
     const int tid = threadIdx.x, c = tid & 15, slot = tid >> 4;
-    const int64_t tile = blockIdx.x, row0 = tile * TM;
+    const int64_t tile = GATHER ? tile_of_block(ntile) : static_cast<int64_t>(blockIdx.x);
+    const int64_t row0 = tile * TM;
     const float4 mean = ld4(stat + 4 * c), istd = ld4(stat + 64 + 4 * c);
     const float4 sc = ld4(stat + 128 + 4 * c), sh = ld4(stat + 192 + 4 * c);
     const float4 *g4 = reinterpret_cast<const float4 *>(dh);

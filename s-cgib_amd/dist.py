@@ -144,6 +144,18 @@ class GradAllReducer:
         self.unpack()
 
 
+def broadcast_replicas(model, src=0, group=None):
+    """Rank ``src``'s parameters and buffers to every rank of ``group`` (the
+    construction-time sync of a data-parallel replica set): the replicas start
+    identical whatever each rank's seed, and the one averaged update per step
+    keeps them identical.  No-op in a 1-rank world."""
+    if not dist.is_initialized() or dist.get_world_size(group) == 1:
+        return
+    with torch.no_grad():
+        for t in list(model.parameters()) + list(model.buffers()):
+            dist.broadcast(t.data, src, group=group)
+
+
 def bn_buffers(model):
     """The BatchNorm running means / variances of ``model`` (float buffers the
     replicas average each step; num_batches_tracked is equal on every rank)."""

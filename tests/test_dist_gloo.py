@@ -159,3 +159,46 @@ def test_bn_buffers_identical_across_ranks(pkg):
     for k in got[0]:
         np.testing.assert_array_equal(got[0][k], got[1][k], err_msg=k)
         assert torch.allclose(torch.from_numpy(got[0][k]), expect[k], rtol=1e-6, atol=1e-7), k
+
+
+def _bcast_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    sys.path.insert(0, ROOT)
+    import importlib
+    from types import SimpleNamespace
+    pkg = importlib.import_module("s-cgib_amd")
+    pkg.dist.init_from_env(backend="gloo")
+    torch.manual_seed(1234 + rank)  # the bench's per-rank seed: different initial weights
+    args = SimpleNamespace(recons_type="adj", useAtt=1, readout_f="sum", d_transfer=32,
+                           gin_layers=2)
+    model = pkg.models.Mainmodel(args, 11, 64, 4, 4, 1, "GIN")
+    with torch.no_grad():  # a rank-dependent buffer too
+        next(iter(b for n, b in model.named_buffers() if n.endswith("running_mean"))).fill_(rank)
+    before = {k: v.numpy().copy() for k, v in model.state_dict().items()}
+    pkg.dist.broadcast_replicas(model)
+    q.put((rank, before, {k: v.numpy().copy() for k, v in model.state_dict().items()}))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_broadcast_replicas_makes_ranks_identical(pkg):
+    """bench.py's replica sync: differently seeded ranks hold rank 0's
+    parameters and buffers, bitwise, after broadcast_replicas."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_bcast_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = dict((r, (b, a)) for r, b, a in (q.get(timeout=240) for _ in range(world)))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    (b0, a0), (b1, a1) = got[0], got[1]
+    assert any(not np.array_equal(b0[k], b1[k]) for k in b0)  # they did differ
+    for k in a0:
+        np.testing.assert_array_equal(a0[k], b0[k], err_msg=k)  # rank 0 kept its own
+        np.testing.assert_array_equal(a1[k], a0[k], err_msg=k)

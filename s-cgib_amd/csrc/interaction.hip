@@ -243,6 +243,15 @@ __global__ __launch_bounds__(64) void interaction_fwd_k(
             }
         }
     };
+    // the first chunk's noise (independent of pass A): in flight with its rows
+    float4 uk[CH];
+    float ugk[CH];
+#pragma unroll
+    for (int j = 0; j < CH; ++j) {
+        const int64_t r = r0 + L.q + 4 * j, rr = r < r1 ? r : r0;
+        uk[j] = ld4(u_feat + rr * 64 + L.ch);
+        ugk[j] = u_gate[rr];
+    }
     pass_a(r0, fk, tk, sk);
     for (int64_t cb = r0 + 4 * CH; cb < r1; cb += 4 * CH) {
         float4 fv[CH], tv[CH], sv[CH];
@@ -284,14 +293,14 @@ __global__ __launch_bounds__(64) void interaction_fwd_k(
     float4 zacc = f4(0.f), qacc = f4(0.f);
     float lmk[CH];  // first chunk's lambda, kept for the KL store pass
     auto pass_b = [&](int64_t cb, const float4 *fv, const float4 *tv, const float4 *sv,
-                      float *lmo) {
+                      float *lmo, const float4 *upre, const float *gpre) {
         float4 uv[CH];
         float ug[CH];
 #pragma unroll
         for (int j = 0; j < CH; ++j) {
             const int64_t r = cb + L.q + 4 * j, rr = r < r1 ? r : r0;
-            uv[j] = ld4(u_feat + rr * 64 + L.ch);
-            ug[j] = u_gate[rr];
+            uv[j] = upre ? upre[j] : ld4(u_feat + rr * 64 + L.ch);
+            ug[j] = gpre ? gpre[j] : u_gate[rr];
         }
 #pragma unroll
         for (int j = 0; j < CH; ++j) {
@@ -316,7 +325,7 @@ __global__ __launch_bounds__(64) void interaction_fwd_k(
             }
         }
     };
-    pass_b(r0, fk, tk, sk, lmk);
+    pass_b(r0, fk, tk, sk, lmk, uk, ugk);
     for (int64_t cb = r0 + 4 * CH; cb < r1; cb += 4 * CH) {
         float4 fv[CH], tv[CH], sv[CH];
 #pragma unroll
@@ -326,7 +335,7 @@ __global__ __launch_bounds__(64) void interaction_fwd_k(
             tv[j] = ld4(t + rr * 64 + L.ch);
             sv[j] = ld4(s + rr * 64 + L.ch);
         }
-        pass_b(cb, fv, tv, sv, nullptr);
+        pass_b(cb, fv, tv, sv, nullptr, nullptr, nullptr);
     }
     zacc = red_q4(zacc);
     if (L.q == 0) st4(z1 + gi * 64 + L.ch, zacc);

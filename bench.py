@@ -176,9 +176,8 @@ KERNELS = {
     "gin_fwd_k": dict(entries=("scgib_gin_layer0_fwd", "scgib_gin_layer_fwd_bn"),
                       keep=lambda m: True, bytes=agg_fwd_bytes, flops=layer_fwd_flops,
                       pmc=["gin_fwd_k<32, false, true, true,", "gin_fwd_k<64, true, true,",
-                           "gin_fwd_k<64, false, true,", "gin_fwd_win_k<"],
-                      desc="fused GIN layer forward: gather (+ previous BN + ReLU on load; "
-                           "d_in = 64 through the LDS row window, gin_fwd_win_k) + "
+                           "gin_fwd_k<64, false, true,"],
+                      desc="fused GIN layer forward: gather (+ previous BN + ReLU on load) + "
                            "2 f32-MFMA GEMMs + BN tile statistics"),
     "gin_bwd5_k": dict(entries=("scgib_gin_layer_bwd",), keep=lambda m: m["d_in"] == 64,
                        bytes=layer_bwd_bytes, flops=layer_bwd_flops, pmc=["gin_bwd5_k<64>"],
@@ -589,9 +588,6 @@ def main():
     ap.add_argument("--no-ego-prefetch", action="store_true",
                     help="build each step's ego-nets at the head of the step instead of one "
                          "batch ahead (graph.EgoPrefetch; A/B)")
-    ap.add_argument("--row-window", choices=("both", "fwd", "bwd", "none"), default="both",
-                    help="which d = 64 gathers read through the LDS row window "
-                         "(scgib_set_fwd_window / scgib_set_bwd_window; A/B)")
     ap.add_argument("--torch-adam", action="store_true",
                     help="torch's fused Adam instead of the one-launch scgib Adam")
     ap.add_argument("--finetune", choices=["molhiv"], default=None,
@@ -605,9 +601,6 @@ def main():
         finetune_bench.main_line(sys.modules[__name__], a, dev)
         return
 
-    lib = pkg._lib.load()
-    lib.scgib_set_fwd_window(int(a.row_window in ("both", "fwd")))
-    lib.scgib_set_bwd_window(int(a.row_window in ("both", "bwd")))
     rank, world, local = pkg.dist.init_from_env()
     if a.force_allreduce and world == 1 and not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")

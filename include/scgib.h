@@ -186,15 +186,6 @@ int scgib_bn_bwd_finalize(const float *tile_stats, int64_t n_nodes, int32_t trai
  * scgib_gin_bwd_stats_bn = scgib_gin_bwd_stats + scgib_bn_bwd_finalize. */
 int64_t scgib_gin_bn_ws_floats(int64_t n_nodes);
 int64_t scgib_gin_counters(int64_t n_nodes);
-/* d_in = 64 gathering layers read their neighbour rows from an LDS window of
- * rows [row0 - 32, row0 + 96) loaded as one contiguous block per 64-row tile
- * (neighbours outside it from global memory: any graph).  Testing hook:
- * 0 = the per-neighbour gather, 1 = the window (default); bitwise the same
- * outputs; returns the previous setting. */
-int scgib_set_fwd_window(int on);
-/* The same for the transposed gather of scgib_gin_bwd_stats(_bn)(_fold)
- * (testing hook, default 1). */
-int scgib_set_bwd_window(int on);
 
 int scgib_gin_layer_fwd_bn(const float *h_in, int32_t d_in, const float *in_stat,
                            const int32_t *rowptr, const int32_t *col, int64_t n_nodes,

@@ -576,11 +576,13 @@ constexpr bool kFwdAlias = ((DIN == 64 && GATHER && !PRE) || (DIN == 32 && GATHE
 // workgroups round-robin over the 8 XCDs (MI355X_MICROARCH.md, "Workgroup
 // dispatch"), so with tile = blockIdx consecutive tiles — which share rows:
 // the neighbours across a tile edge, the row window's halo — sit in
-// different L2s.  SCGIB_XCD_TILES = 1 gives each XCD a contiguous run of
-// tiles instead (xcd_remap): speed only, every tile computes the same bits
-// wherever it runs.
+// different L2s.  SCGIB_XCD_TILES = 1 (default) gives each XCD a contiguous
+// run of tiles instead (xcd_remap): speed only, every tile computes the same
+// bits wherever it runs.  Measured (profiles/r04_window/xcd_tiles.txt): the
+// superbatch backward statistics 258.9 -> 236.5 us (0.76 -> 0.83 of HBM),
+// the forward layer 437.9 -> 435.4 us, the QM9 B512 step unchanged.
 #ifndef SCGIB_XCD_TILES  // (build-time A/B hook: tools/build_ab_lib.sh EXTRA=-DSCGIB_XCD_TILES=n)
-#define SCGIB_XCD_TILES 0
+#define SCGIB_XCD_TILES 1
 #endif
 __device__ __forceinline__ int64_t tile_of_block(int64_t ntiles) {
     return SCGIB_XCD_TILES ? xcd_remap(blockIdx.x, ntiles) : static_cast<int64_t>(blockIdx.x);
@@ -869,288 +871,6 @@ __global__ __launch_bounds__(256, (kFwdAlias<DIN, GATHER, PRE> ? 3 : 1)) void gi
     }
 }
 
-// ---------------------------------------------------------------------------
-// gin_fwd_win_k: the d_in = 64 gathering layer with an LDS row window.
-//
-// Molecules (and ego-nets) are contiguous row ranges, so the rows a 64-row
-// tile gathers lie within a few dozen rows of it.  gin_fwd_k fetches them
-// through three dependent memory hops (row pointers -> neighbour indices ->
-// rows: 8.6 of a tile's ~18.7 us on the superbatch, tools/superbatch_trace.py);
-// here the tile's window of rows [row0 - 32, row0 + 96) is loaded as ONE
-// contiguous block (coalesced float4, no dependence on the indices) beside
-// the row pointers, the indices follow the row pointers, and the aggregation
-// reads the rows from LDS — the window already BN+ReLU-transformed when the
-// layer has an input transform.  A neighbour outside the window (a molecule
-// of > 33 atoms across the tile's edge, or any non-molecular graph) is read
-// from global memory: correct for every graph.  With a deferred BatchNorm
-// ahead (scgib_bn_pending) the window, row pointers and first index round are
-// all in flight across its finish.
-//
-// LDS: the window (32 KB; the agg tile, then r, after the aggregation) + W1;
-// W2 is held in registers (each wave's 32-column block, 32 VGPRs) — 53 KB,
-// three workgroups per CU.  Same gather order (gather_tail's rounds, then the
-// self term), same GEMM k order and statistics as gin_fwd_k: every output is
-// bitwise gin_fwd_k's (tests: test_gin_layer_window_forward_bitwise).
-// ---------------------------------------------------------------------------
-constexpr int kWinRows = 128, kWinLead = 32;
-
-// acc += A B^T, K = 64: A from LDS (mma_pf's NT operand), B from registers
-// (b[s] = B(j = lane & 31, k = 2 s + (lane >> 5))) — mma_pf<64, false, false>'s
-// k order, so the same bits
-__device__ __forceinline__ f32x16 mma_nt_breg64(const float *As, int lda, const float (&b)[32],
-                                                f32x16 acc) {
-    constexpr int S = 32, D = 4, R = D + 1;
-    const float *pa = mma_base<false>(As, lda);
-    float a[R];
-#pragma unroll
-    for (int s = 0; s < D; ++s) a[s] = pa[2 * s];
-#pragma unroll
-    for (int s = 0; s < S; ++s) {
-        if (s + D < S) a[(s + D) % R] = pa[2 * (s + D)];
-        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[s % R], b[s], acc, 0, 0, 0);
-        mma_step_fence();
-    }
-    return acc;
-}
-
-template <bool XFORM>
-__global__ __launch_bounds__(256, 3) void gin_fwd_win_k(
-    const float *__restrict__ h, const float *__restrict__ in_scale,
-    const float *__restrict__ in_shift, const int32_t *__restrict__ rowptr,
-    const int32_t *__restrict__ col, int64_t ncap, float ope, const float *__restrict__ w1,
-    const float *__restrict__ b1, const float *__restrict__ w2, const float *__restrict__ b2,
-    float *__restrict__ agg_out, float *__restrict__ r_out, float *__restrict__ z2_out,
-    float *__restrict__ part, const int32_t *__restrict__ dims, BnFwdFuse fz,
-    scgib_bn_pending pend) {
-    constexpr int LDA = 65;
-    static_assert(TM * LDA <= kWinRows * 64, "the agg tile takes the window's buffer");
-    __shared__ __attribute__((aligned(16))) float sWin[kWinRows * 64];  // window, then agg / r
-    __shared__ float sW1[64 * LDA];
-    __shared__ float sRed[2][64];
-    __shared__ float sScSh[128];
-    float *const sA = sWin;
-    const int64_t n = eff_count(dims, 0, ncap);
-    const int tid = threadIdx.x, l = tid & 63, w = tid >> 6;
-    const int c = tid & 15, rbase = tid >> 4;
-    const int64_t tile = tile_of_block(gridDim.x), row0 = tile * TM;
-    const int nv = static_cast<int>(n - row0 < TM ? (n - row0 > 0 ? n - row0 : 0) : TM);
-    if (dims) {  // capacity mode: zero this tile's padded rows [nv, rows in capacity)
-        const int ncr = static_cast<int>(ncap - row0 < TM ? ncap - row0 : TM);
-        for (int idx = nv * 64 + tid; idx < ncr * 64; idx += 256) {
-            r_out[row0 * 64 + idx] = 0.f;
-            z2_out[row0 * 64 + idx] = 0.f;
-            agg_out[row0 * 64 + idx] = 0.f;
-        }
-        if (nv == 0) {
-            if (tid < 128) part[tile * 128 + tid] = 0.f;
-            return;
-        }
-    }
-    SCGIB_MARK(0);
-    SCGIB_MARK_HWID();
-    // the previous layer's deferred BN statistics: partial loads go out first
-    FwdFin fin;
-    float pend_gam = 0.f, pend_bet = 0.f;
-    const int pend_ngr = static_cast<int>(((n + TM - 1) / TM + kGroup - 1) / kGroup);
-    if (XFORM && pend.gpart) {
-        pend_gam = pend.gamma[fin_channel()];
-        pend_bet = pend.beta[fin_channel()];
-        bn_fwd_fin_load<false>(pend.gpart, pend_ngr, 0, fin);
-    }
-    // row pointers of the thread's 4 rows and the window (no dependence between them)
-    const float4 *h4 = reinterpret_cast<const float4 *>(h);
-    const int64_t w0 = row0 - kWinLead;
-    int32_t beg[4], end[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        const int rr = rbase + 16 * k;
-        const int64_t v = row0 + (rr < nv ? rr : nv - 1);
-        beg[k] = rowptr[v];
-        end[k] = rowptr[v + 1];
-    }
-    float4 wv[kWinRows * 16 / 256];
-#pragma unroll
-    for (int k = 0; k < kWinRows * 16 / 256; ++k) {
-        const int64_t g = w0 + ((tid + 256 * k) >> 4);
-        wv[k] = h4[(g < 0 ? 0 : (g < n ? g : n - 1)) * 16 + c];
-    }
-    // the first neighbour round's indices (gather_tail's clamped addresses)
-    int maxdeg = 0, maxend = 0;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        maxend = end[k] > maxend ? end[k] : maxend;
-        const int d = end[k] - beg[k];
-        maxdeg = d > maxdeg ? d : maxdeg;
-    }
-    int32_t u0[4][4];
-    if (maxdeg > 0) {
-#pragma unroll
-        for (int k = 0; k < 4; ++k)
-#pragma unroll
-            for (int t = 0; t < 4; ++t) {
-                const int32_t e = beg[k] + t;
-                u0[k][t] = col[e < maxend ? e : maxend - 1];
-            }
-    }
-    WeightRegs<64> wr1;  // (W1 only: its b half is unused)
-    {
-        constexpr int N1 = 64 * 64 / 4 / 256;
-#pragma unroll
-        for (int k = 0; k < N1; ++k) wr1.a[k] = reinterpret_cast<const float4 *>(w1)[tid + 256 * k];
-    }
-    float4 sc = make_float4(1.f, 1.f, 1.f, 1.f), sh = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (XFORM) {
-        if (pend.gpart) {  // finish the previous layer's deferred BatchNorm statistics
-            double mean, M2;
-            bn_fwd_final<false>(pend.gpart, n, pend_ngr, fin, mean, M2);
-            const int fc = fin_channel();
-            const bool lead = (tid & 63) < 16;
-            const float2 ss = bn_fwd_publish(fc, mean, M2, n, pend_gam, pend_bet, pend.eps,
-                                             pend.momentum, pend.running_mean, pend.running_var,
-                                             pend.num_batches_tracked, pend.stat,
-                                             blockIdx.x == 0 && lead);
-            if (lead) {
-                sScSh[fc] = ss.x;
-                sScSh[64 + fc] = ss.y;
-            }
-            lds_barrier();
-            sc = make_float4(sScSh[4 * c], sScSh[4 * c + 1], sScSh[4 * c + 2], sScSh[4 * c + 3]);
-            sh = make_float4(sScSh[64 + 4 * c], sScSh[65 + 4 * c], sScSh[66 + 4 * c],
-                             sScSh[67 + 4 * c]);
-        } else {
-            sc = ld4(in_scale + 4 * c);
-            sh = ld4(in_shift + 4 * c);
-        }
-    }
-    // the window into LDS (transformed once), W1 into LDS
-#pragma unroll
-    for (int k = 0; k < kWinRows * 16 / 256; ++k) {
-        const float4 v = XFORM ? xform4(wv[k], sc, sh) : wv[k];
-        *reinterpret_cast<float4 *>(sWin + (((tid + 256 * k) >> 4) * 64) + 4 * c) = v;
-    }
-    {
-        constexpr int N1 = 64 * 64 / 4 / 256;
-#pragma unroll
-        for (int k = 0; k < N1; ++k) {
-            const int idx = 4 * (tid + 256 * k), row = idx >> 6, cc = idx & 63;
-            float *d = sW1 + row * LDA + cc;
-            d[0] = wr1.a[k].x; d[1] = wr1.a[k].y; d[2] = wr1.a[k].z; d[3] = wr1.a[k].w;
-        }
-    }
-    // W2: this wave's 32 output columns, in registers for GEMM2 (in flight
-    // through the aggregation and GEMM1)
-    const int wr = w >> 1, wc = w & 1, ccol = wc * 32 + (l & 31);
-    float w2r[32];
-#pragma unroll
-    for (int s = 0; s < 32; ++s) w2r[s] = w2[ccol * 64 + 2 * s + (l >> 5)];
-    const float bias1 = b1[ccol], bias2 = b2[ccol];
-    lds_barrier();
-    SCGIB_MARK(8);
-    // aggregation from the window: gather_tail's rounds and order, the self
-    // term last; a neighbour outside the window comes from global memory
-    auto rowval = [&](int32_t u) -> float4 {
-        const int64_t o = static_cast<int64_t>(u) - w0;
-        const bool in = o >= 0 && o < kWinRows;
-        float4 v = *reinterpret_cast<const float4 *>(sWin + (in ? o : 0) * 64 + 4 * c);
-        if (!in) {
-            const float4 g = h4[static_cast<int64_t>(u) * 16 + c];
-            v = XFORM ? xform4(g, sc, sh) : g;
-        }
-        return v;
-    };
-    float4 acc[4];
-    int32_t deg[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        acc[k] = make_float4(0.f, 0.f, 0.f, 0.f);
-        deg[k] = end[k] - beg[k];
-    }
-    for (int j0 = 0; j0 < maxdeg; j0 += 4) {
-        int32_t u[4][4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k)
-#pragma unroll
-            for (int t = 0; t < 4; ++t) {
-                const int32_t e = beg[k] + j0 + t;
-                u[k][t] = j0 == 0 ? u0[k][t] : col[e < maxend ? e : maxend - 1];
-            }
-#pragma unroll
-        for (int k = 0; k < 4; ++k)
-#pragma unroll
-            for (int t = 0; t < 4; ++t)
-                acc[k] = fma4(rowval(u[k][t]), j0 + t < deg[k] ? 1.f : 0.f, acc[k]);
-    }
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {  // self: the tile's own rows are always in the window
-        const int rr = rbase + 16 * k;
-        const float4 x = *reinterpret_cast<const float4 *>(
-            sWin + ((rr < nv ? rr : nv - 1) + kWinLead) * 64 + 4 * c);
-        acc[k] = make_float4(ope * x.x + acc[k].x, ope * x.y + acc[k].y, ope * x.z + acc[k].z,
-                             ope * x.w + acc[k].w);
-    }
-    lds_barrier();  // every thread's window reads are done: the agg tile takes the buffer
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        const int rr = rbase + 16 * k;
-        if (rr < nv) st4(agg_out + (row0 + rr) * 64 + 4 * c, acc[k]);
-        float *d = sA + rr * LDA + 4 * c;
-        d[0] = acc[k].x; d[1] = acc[k].y; d[2] = acc[k].z; d[3] = acc[k].w;
-    }
-    lds_barrier();
-    SCGIB_MARK(1);
-    {  // z1 = agg W1^T + b1 ; r = relu(z1) (into the agg tile's buffer)
-        const f32x16 a1 = mma_pf<64, false, false>(sA + wr * 32 * LDA, LDA, sW1 + wc * 32 * LDA,
-                                                   LDA, zero16());
-        lds_barrier();
-#pragma unroll
-        for (int reg = 0; reg < 16; ++reg) {
-            const int row = wr * 32 + acc_row(reg, l);
-            const float v = fmaxf(a1[reg] + bias1, 0.f);
-            sA[row * LDH + ccol] = v;
-            if (row < nv) r_out[(row0 + row) * 64 + ccol] = v;
-        }
-    }
-    lds_barrier();
-    SCGIB_MARK(2);
-    f32x16 a2 = mma_nt_breg64(sA + wr * 32 * LDH, LDH, w2r, zero16());
-    float s = 0.f;
-#pragma unroll
-    for (int reg = 0; reg < 16; ++reg) {
-        const int row = wr * 32 + acc_row(reg, l);
-        a2[reg] += bias2;
-        if (row < nv) {
-            z2_out[(row0 + row) * 64 + ccol] = a2[reg];
-            s += a2[reg];
-        }
-    }
-    SCGIB_MARK(3);
-    s += __shfl_xor(s, 32, kWave);
-    if (l < 32) sRed[wr][ccol] = s;
-    lds_barrier();
-    const float csum = sRed[0][ccol] + sRed[1][ccol];
-    const float cmean = csum / nv;
-    float m2 = 0.f;
-#pragma unroll
-    for (int reg = 0; reg < 16; ++reg) {
-        const int row = wr * 32 + acc_row(reg, l);
-        const float d = a2[reg] - cmean;
-        if (row < nv) m2 += d * d;
-    }
-    m2 += __shfl_xor(m2, 32, kWave);
-    lds_barrier();
-    if (l < 32) sRed[wr][ccol] = m2;
-    lds_barrier();
-    if (wr == 0 && l < 32) {
-        st_agent(part + tile * 128 + ccol, csum);
-        st_agent(part + tile * 128 + 64 + ccol, sRed[0][ccol] + sRed[1][ccol]);
-    }
-    SCGIB_MARK(4);
-    if (fz.counters) {
-        bn_fwd_hier(part, n, tile, fz);
-        SCGIB_MARK(5);
-    }
-}
-
 // Batch mean / biased variance from the per-tile (sum, centred M2), fp64,
 // two passes over the tile statistics with 8 tiles' loads in flight per
 // thread (16 partitions x 64 channels, partitions combined in fixed order):
@@ -1303,92 +1023,7 @@ __device__ __forceinline__ void slab_fold_block(const scgib_slab_job &J, int b, 
                                       red[192 + el]);
 }
 
-// The transposed gather of gin_bwd_stats_k through the LDS row window (as
-// gin_fwd_win_k's forward gather, no input transform): rows [row0 - 32,
-// row0 + 96) of h in one contiguous load beside the row pointers, the first
-// index round after them, the sum from LDS (gather_tail's order; a neighbour
-// outside the window from global memory).  sWin: kWinRows x 64 floats.
-__device__ __forceinline__ void win_gather_rows(const float4 *__restrict__ h4,
-                                                const int32_t *__restrict__ rowptr,
-                                                const int32_t *__restrict__ col, int64_t row0,
-                                                int nv, int64_t n, int rbase, int c, float ope,
-                                                float *sWin, float4 (&acc)[4]) {
-    const int tid = threadIdx.x;
-    const int64_t w0 = row0 - kWinLead;
-    int32_t beg[4], end[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        const int rr = rbase + 16 * k;
-        const int64_t v = row0 + (rr < nv ? rr : nv - 1);
-        beg[k] = rowptr[v];
-        end[k] = rowptr[v + 1];
-    }
-    float4 wv[kWinRows * 16 / 256];
-#pragma unroll
-    for (int k = 0; k < kWinRows * 16 / 256; ++k) {
-        const int64_t g = w0 + ((tid + 256 * k) >> 4);
-        wv[k] = h4[(g < 0 ? 0 : (g < n ? g : n - 1)) * 16 + c];
-    }
-    int maxdeg = 0, maxend = 0;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        maxend = end[k] > maxend ? end[k] : maxend;
-        const int d = end[k] - beg[k];
-        maxdeg = d > maxdeg ? d : maxdeg;
-    }
-    int32_t u0[4][4];
-    if (maxdeg > 0) {
-#pragma unroll
-        for (int k = 0; k < 4; ++k)
-#pragma unroll
-            for (int t = 0; t < 4; ++t) {
-                const int32_t e = beg[k] + t;
-                u0[k][t] = col[e < maxend ? e : maxend - 1];
-            }
-    }
-#pragma unroll
-    for (int k = 0; k < kWinRows * 16 / 256; ++k)
-        *reinterpret_cast<float4 *>(sWin + (((tid + 256 * k) >> 4) * 64) + 4 * c) = wv[k];
-    lds_barrier();
-    auto rowval = [&](int32_t u) -> float4 {
-        const int64_t o = static_cast<int64_t>(u) - w0;
-        const bool in = o >= 0 && o < kWinRows;
-        float4 v = *reinterpret_cast<const float4 *>(sWin + (in ? o : 0) * 64 + 4 * c);
-        if (!in) v = h4[static_cast<int64_t>(u) * 16 + c];
-        return v;
-    };
-    int32_t deg[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        acc[k] = make_float4(0.f, 0.f, 0.f, 0.f);
-        deg[k] = end[k] - beg[k];
-    }
-    for (int j0 = 0; j0 < maxdeg; j0 += 4) {
-        int32_t u[4][4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k)
-#pragma unroll
-            for (int t = 0; t < 4; ++t) {
-                const int32_t e = beg[k] + j0 + t;
-                u[k][t] = j0 == 0 ? u0[k][t] : col[e < maxend ? e : maxend - 1];
-            }
-#pragma unroll
-        for (int k = 0; k < 4; ++k)
-#pragma unroll
-            for (int t = 0; t < 4; ++t)
-                acc[k] = fma4(rowval(u[k][t]), j0 + t < deg[k] ? 1.f : 0.f, acc[k]);
-    }
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        const int rr = rbase + 16 * k;
-        const float4 x = *reinterpret_cast<const float4 *>(
-            sWin + ((rr < nv ? rr : nv - 1) + kWinLead) * 64 + 4 * c);
-        acc[k] = make_float4(ope * x.x + acc[k].x, ope * x.y + acc[k].y, ope * x.z + acc[k].z,
-                             ope * x.w + acc[k].w);
-    }
-}
-
-template <bool GATHER, bool SEG = false, bool WIN = false>
+template <bool GATHER, bool SEG = false>
 __global__ __launch_bounds__(256) void gin_bwd_stats_k(
     const float *__restrict__ dh, const int32_t *__restrict__ rowptr_t,
     const int32_t *__restrict__ col_t, float ope, const float *__restrict__ z2,
@@ -1418,10 +1053,7 @@ __global__ __launch_bounds__(256) void gin_bwd_stats_k(
     SCGIB_MARK(0);
     SCGIB_MARK_HWID();
     float4 g[4];
-    if (GATHER && WIN) {
-        __shared__ __attribute__((aligned(16))) float sWin[kWinRows * 64];
-        win_gather_rows(g4, rowptr_t, col_t, row0, nv, n, slot, c, ope, sWin, g);
-    } else if (GATHER) {
+    if (GATHER) {
         gather_rows<4, 16, 16, false>(g4, rowptr_t, col_t, row0, nv, slot, c, ope, sc, sh, g);
     } else if (SEG) {
         int32_t sg[4];
@@ -2104,16 +1736,6 @@ extern "C" int64_t scgib_gin_bwd_slabs(int64_t n_nodes) {
     return n_nodes <= 0 ? 0 : bwd_grid(scgib_gin_tiles(n_nodes));
 }
 
-// d_in = 64 gathering layers through the LDS row window (gin_fwd_win_k);
-// scgib_set_fwd_window: 0 = the per-neighbour gather of gin_fwd_k (tests: the
-// two are bitwise equal), 1 = the window (default)
-static int g_fwd_window = 1;
-extern "C" int scgib_set_fwd_window(int on) {
-    const int prev = g_fwd_window;
-    if (on == 0 || on == 1) g_fwd_window = on;
-    return prev;
-}
-
 static int launch_gin_fwd(const float *h_in, int32_t d_in, const float *in_stat,
                           const int32_t *rowptr, const int32_t *col, int64_t n_nodes,
                           float one_plus_eps, const float *w1, const float *b1, const float *w2,
@@ -2123,13 +1745,6 @@ static int launch_gin_fwd(const float *h_in, int32_t d_in, const float *in_stat,
     const int64_t nt = scgib_gin_tiles(n_nodes);
     const float *isc = in_stat ? in_stat + 128 : nullptr, *ish = in_stat ? in_stat + 192 : nullptr;
     const scgib_bn_pending pd = pend ? *pend : scgib_bn_pending{};
-    if (d_in == 64 && g_fwd_window) {  // the LDS row-window gather (gin_fwd_win_k)
-        if (in_stat || pend)
-            gin_fwd_win_k<true><<<dim3((unsigned)nt), 256, 0, st>>>(h_in, isc, ish, rowptr, col, n_nodes, one_plus_eps, w1, b1, w2, b2, agg, r, z2, tile_stats, dims, fz, pd);
-        else
-            gin_fwd_win_k<false><<<dim3((unsigned)nt), 256, 0, st>>>(h_in, isc, ish, rowptr, col, n_nodes, one_plus_eps, w1, b1, w2, b2, agg, r, z2, tile_stats, dims, fz, pd);
-        return launch_status();
-    }
     if (d_in == 32)
         gin_fwd_k<32, false><<<dim3((unsigned)nt), 256, 0, st>>>(h_in, isc, ish, rowptr, col, n_nodes, one_plus_eps, w1, b1, w2, b2, agg, r, z2, tile_stats, dims, fz, PreArgs{}, pd, ReconArgs{});
     else if (in_stat || pend)
@@ -2255,15 +1870,6 @@ extern "C" int scgib_bn_relu_apply(const float *z, const float *stat, int64_t n_
     return launch_status();
 }
 
-// the transposed gather of the statistics kernel through the LDS row window
-// (win_gather_rows); scgib_set_bwd_window: 0 = per-neighbour, 1 = window (default)
-static int g_bwd_window = 1;
-extern "C" int scgib_set_bwd_window(int on) {
-    const int prev = g_bwd_window;
-    if (on == 0 || on == 1) g_bwd_window = on;
-    return prev;
-}
-
 static int launch_gin_bwd_stats(const float *dh, const int32_t *rowptr_t, const int32_t *col_t,
                                 float one_plus_eps, const float *z2, const float *stat,
                                 int64_t n_nodes, float *dy, float *tile_stats,
@@ -2272,9 +1878,7 @@ static int launch_gin_bwd_stats(const float *dh, const int32_t *rowptr_t, const 
                                 const scgib_slab_job *fold = nullptr) {
     const scgib_slab_job fj = fold ? *fold : scgib_slab_job{};
     const unsigned grid = static_cast<unsigned>(scgib_gin_tiles(n_nodes) + slab_fold_blocks(fj));
-    if (rowptr_t && g_bwd_window)
-        gin_bwd_stats_k<true, false, true><<<dim3(grid), 256, 0, st>>>(dh, rowptr_t, col_t, one_plus_eps, z2, stat, n_nodes, dy, tile_stats, dims, bz, nullptr, nullptr, fj);
-    else if (rowptr_t)
+    if (rowptr_t)
         gin_bwd_stats_k<true><<<dim3(grid), 256, 0, st>>>(dh, rowptr_t, col_t, one_plus_eps, z2, stat, n_nodes, dy, tile_stats, dims, bz, nullptr, nullptr, fj);
     else if (g_seg)
         gin_bwd_stats_k<false, true><<<dim3(grid), 256, 0, st>>>(dh, rowptr_t, col_t, one_plus_eps, z2, stat, n_nodes, dy, tile_stats, dims, bz, g_seg, seg, fj);

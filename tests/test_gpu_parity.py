@@ -912,119 +912,6 @@ def test_set2set_device_vs_oracle(pkg, dev, dim, n_mols):
         assert rel_err(v.grad.cpu(), p["s2s." + k].grad) < 1e-4, k
 
 
-def _fwd_window(pkg, on):
-    return pkg._lib.load().scgib_set_fwd_window(on)
-
-
-def _windows(pkg, on):
-    """Both row-window gathers (forward layer, backward statistics) on / off;
-    returns the previous settings for _windows_restore."""
-    lib = pkg._lib.load()
-    return lib.scgib_set_fwd_window(on), lib.scgib_set_bwd_window(on)
-
-
-def _windows_restore(pkg, prev):
-    lib = pkg._lib.load()
-    lib.scgib_set_fwd_window(prev[0])
-    lib.scgib_set_bwd_window(prev[1])
-
-
-@pytest.mark.parametrize("workload,n_mols,mu", [("qm9", 300, None), ("qm9", 6000, None),
-                                                 ("qm9", 150, 60.0)])
-def test_gin_encoder_window_forward_bitwise(pkg, dev, workload, n_mols, mu):
-    """The LDS row-window gathers (the forward layer gin_fwd_win_k, the
-    backward statistics' transposed gather win_gather_rows) against the
-    per-neighbour gathers (gin_fwd_k, gather_rows) on the same inputs:
-    outputs, every gradient and the BatchNorm running statistics bitwise
-    equal — 300
-    molecules (deferred BN), 6000 (~108 k rows: BN in-kernel, third
-    statistics level) and molecules of ~60 atoms (neighbours outside the
-    window: the global-memory fallback)."""
-    import copy
-    torch.manual_seed(n_mols)
-    kw = {} if mu is None else {"mu": mu, "sigma": 8.0}
-    mols = pkg.synth.molecules(n_mols, workload, seed=17, **kw)
-    gh, _ = pkg.graph.collate_pyg(mols)
-    g = gh.to(dev)
-    if mu is not None:
-        assert gh.max_graph_nodes > 40
-    gin = pkg.models.GIN(64, 64, 3).to(dev).train()
-    with torch.no_grad():
-        for bn in gin.batch_norms:
-            bn.weight.add_(0.2 * torch.randn(64, device=dev))
-            bn.bias.add_(0.2 * torch.randn(64, device=dev))
-    h0 = torch.randn(g.num_nodes(), 64, device=dev)
-    w = torch.randn(g.num_nodes(), 64, device=dev)
-    outs = []
-    for on in (0, 1):
-        gin_c = copy.deepcopy(gin)
-        prev = _windows(pkg, on)
-        try:
-            x = h0.clone().requires_grad_(True)
-            h = gin_c(g, x)
-            (h * w).sum().backward()
-            torch.cuda.synchronize()
-        finally:
-            _windows_restore(pkg, prev)
-        outs.append((h.detach(), x.grad, {k: p.grad for k, p in gin_c.named_parameters()},
-                     {k: b.clone() for k, b in gin_c.named_buffers()}))
-    (ha, xa, ga, ba), (hb, xb, gb, bb) = outs
-    assert torch.equal(ha, hb) and torch.equal(xa, xb)
-    for k in ga:
-        assert torch.equal(ga[k], gb[k]), k
-    for k in ba:
-        assert torch.equal(ba[k], bb[k]), k
-
-
-@pytest.mark.parametrize("xform", [False, True])
-def test_gin_layer_window_forward_capacity_bitwise(pkg, dev, xform):
-    """One layer through the C-ABI in capacity mode (dims: 70 k actual rows of
-    a 90 k-row capacity): the window and the per-neighbour forward write the
-    same agg / r / z2 (padding rows zero), tile statistics, BN record and
-    running statistics, bit for bit; counters left zero."""
-    lib, ops = pkg._lib, pkg.ops
-    torch.manual_seed(7)
-    _, gh = rand_graph(pkg, 4000, "qm9", 14, dev)
-    n = gh.num_nodes()
-    ncap = n + 20000
-    rowptr = torch.full((ncap + 1,), int(gh.rowptr[-1]), dtype=torch.int32)
-    rowptr[: n + 1] = gh.rowptr
-    e = int(gh.rowptr[-1])
-    col = torch.zeros(e + 64, dtype=torch.int32)
-    col[:e] = gh.col
-    rowptr, col = rowptr.to(dev), col.to(dev)
-    dims = torch.tensor([n, e], dtype=torch.int32, device=dev)
-    h = torch.randn(ncap, 64, device=dev)
-    w1, w2 = 0.2 * torch.randn(64, 64, device=dev), 0.2 * torch.randn(64, 64, device=dev)
-    b1, b2 = 0.1 * torch.randn(64, device=dev), 0.1 * torch.randn(64, device=dev)
-    gamma, beta = 1 + 0.2 * torch.randn(64, device=dev), 0.2 * torch.randn(64, device=dev)
-    in_stat = torch.randn(4, 64, device=dev) if xform else None
-    res = []
-    for on in (0, 1):
-        agg, r, z2 = (torch.full((ncap, 64), 7.0, device=dev) for _ in range(3))
-        stat = torch.empty(4, 64, device=dev)
-        rm, rv = torch.zeros(64, device=dev), torch.ones(64, device=dev)
-        nbt = torch.zeros((), dtype=torch.int64, device=dev)
-        ws = torch.zeros(int(lib.query("scgib_gin_bn_ws_floats", ncap)), device=dev)
-        cnt = torch.zeros(int(lib.query("scgib_gin_counters", ncap)), dtype=torch.int32, device=dev)
-        prev = _fwd_window(pkg, on)
-        try:
-            lib.call("scgib_gin_layer_fwd_bn", ops._p(h), 64, ops._p(in_stat), ops._p(rowptr),
-                     ops._p(col), ncap, 1.0, ops._p(w1), ops._p(b1), ops._p(w2), ops._p(b2),
-                     ops._p(agg), ops._p(r), ops._p(z2), ops._p(gamma), ops._p(beta), 1e-5, 0.1,
-                     ops._p(rm), ops._p(rv), ops._p(nbt), ops._p(stat), ops._p(ws), ops._p(cnt),
-                     ops._p(dims), None, 0, ops._stream())
-            torch.cuda.synchronize()
-        finally:
-            _fwd_window(pkg, prev)
-        assert int(cnt.abs().sum()) == 0
-        ntile = (n + 63) // 64
-        res.append([agg, r, z2, stat, rm, rv, nbt, ws[: ntile * 128]])
-    for a, b in zip(*res):
-        assert torch.equal(a, b)
-    assert float(res[1][2][n:].abs().max()) == 0.0
-
-
 # ---------------------------------------------------------------------------
 # Domain adaptation (SURVEY.md §8(f) #4) and fine-tuning on the adapted model
 # ---------------------------------------------------------------------------

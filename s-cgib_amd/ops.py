@@ -1208,8 +1208,30 @@ def counters(device, key, n):
     return buf[off: off + n]
 
 
-_SCAN_STATES = {}  # (device index, key, stream) -> int32 tensor
-_SCAN_RETIRED = []  # outgrown scan states: a captured graph may still point at one
+_SCAN_STATES = {}  # (device index, key, stream) -> int32 tensor (a range of an arena)
+_SCAN_ARENAS = {}  # device index -> [int32 tensors]: zeroed at creation, never freed
+_SCAN_NEXT = {}    # device index -> next free word of the newest arena
+_SCAN_ARENA_WORDS = 1 << 20  # 4 MB: every key and stream of a process, captures included
+
+
+def _scan_carve(idx, device, size):
+    """``size`` zeroed words from the device's arena.  The arena is made by the
+    first request (an eager step, before any capture), so a key first seen
+    while a graph is being captured — a capture runs on its own stream, a new
+    key — is carved from memory that is already zero instead of allocating
+    (and zero-filling) inside the graph, where the fill would replay every
+    step (a 5 us fill at the head of each encoder chain, round 4)."""
+    arenas = _SCAN_ARENAS.setdefault(idx, [])
+    off = _SCAN_NEXT.get(idx, 0)
+    if arenas and off + size <= arenas[-1].numel():
+        _SCAN_NEXT[idx] = off + ((size + 63) // 64) * 64  # 256-B aligned ranges
+        return arenas[-1][off: off + size]
+    words = _SCAN_ARENA_WORDS
+    while words < size:
+        words *= 2
+    arenas.append(torch.zeros(words, dtype=torch.int32, device=device))
+    _SCAN_NEXT[idx] = ((size + 63) // 64) * 64
+    return arenas[-1][:size]
 
 
 def scan_state(device, key, n):
@@ -1217,20 +1239,19 @@ def scan_state(device, key, n):
     look-back words, a GIN encoder's BatchNorm arrival counters) for call
     site ``key`` on ``device`` and the current stream, separate from the O(1)
     counter pool: it grows on demand to the next power of two (a new zeroed
-    tensor; the outgrown one is kept alive, since a captured graph may
-    reference it — at most log2 of the largest size per key) and the kernels
-    leave it zeroed for the next launch.  Keys name call sites, never objects,
-    so a long-lived process that builds new modules reuses the same words."""
+    range of the device's arena; the outgrown one stays allocated, since a
+    captured graph may reference it — at most log2 of the largest size per
+    key) and the kernels leave it zeroed for the next launch.  Keys name call
+    sites, never objects, so a long-lived process that builds new modules
+    reuses the same words."""
     idx = torch.device(device).index or 0
     rk = (idx, key, torch.cuda.current_stream(device).cuda_stream)
     buf = _SCAN_STATES.get(rk)
     if buf is None or buf.numel() < n:
-        if buf is not None:
-            _SCAN_RETIRED.append(buf)
         size = 1024
         while size < n:
             size *= 2
-        buf = _SCAN_STATES[rk] = torch.zeros(size, dtype=torch.int32, device=device)
+        buf = _SCAN_STATES[rk] = _scan_carve(idx, device, size)
     return buf[:n]
 
 

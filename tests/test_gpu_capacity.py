@@ -126,6 +126,7 @@ def test_graph_replay_matches_exact_over_batches(pkg, dev, k, fork_losses, monke
     torch.cuda.current_stream().wait_stream(side)
     cap_m.load_state_dict(snap)  # undo the warm-up's BN running updates
     cap_m.zero_grad(set_to_none=True)
+    arenas = len(pkg.ops._SCAN_ARENAS[dev.index or 0])
     graph = torch.cuda.CUDAGraph()
     with torch.cuda.graph(graph):
         _, kl, con, rec = cap_m(static.graph, static.x, None, None, None, 1, None, k, dev, B,
@@ -133,6 +134,9 @@ def test_graph_replay_matches_exact_over_batches(pkg, dev, k, fork_losses, monke
         loss = kl + rec + con
         loss.backward()
         static_losses = torch.stack([kl, con, rec, loss]).detach()
+    # the capture's stream is new to every scan-state call site: their words
+    # came from the pre-zeroed arena, no zero-fill was captured into the step
+    assert len(pkg.ops._SCAN_ARENAS[dev.index or 0]) == arenas
 
     t0 = pkg.ops.xq_timeouts(dev)
     for i in (0, 1, 2, 3, 1):  # includes a batch seen before (replay is stateless)

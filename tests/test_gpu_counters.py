@@ -56,3 +56,4 @@ def test_fresh_modules_and_streams_reuse_counters(pkg, dev):
     assert _pool_used(ops) == used  # no new counter ranges after the first round
     assert len(ops._SCAN_STATES) == n_scan
     assert torch.equal(first, again)  # words left zeroed: the same bits on another stream
+

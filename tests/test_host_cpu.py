@@ -498,3 +498,25 @@ def test_xq_handoffs_off_under_serialised_dispatch(pkg, monkeypatch):
         monkeypatch.setenv(k, "1")
         assert pkg.ops._dispatch_serialised()
         monkeypatch.delenv(k)
+
+
+def test_scan_arena_carves_disjoint_zeroed_ranges(pkg):
+    """ops._scan_carve (the scan-state arena): disjoint, 256-B aligned, zeroed
+    ranges from one arena; a request past its end opens a new arena (the old
+    ranges stay valid)."""
+    import torch
+    ops = pkg.ops
+    key = 977  # a device index no real device uses
+    try:
+        a = ops._scan_carve(key, "cpu", 1024)
+        b = ops._scan_carve(key, "cpu", 100)
+        c = ops._scan_carve(key, "cpu", 1024)
+        assert a.data_ptr() + 1024 * 4 == b.data_ptr()
+        assert c.data_ptr() == b.data_ptr() + 128 * 4  # 100 words rounded to 64-word ranges
+        assert int(a.abs().sum() + b.abs().sum() + c.abs().sum()) == 0
+        big = ops._scan_carve(key, "cpu", ops._SCAN_ARENA_WORDS)
+        assert len(ops._SCAN_ARENAS[key]) == 2 and big.numel() == ops._SCAN_ARENA_WORDS
+        assert int(big.abs().sum()) == 0
+    finally:
+        ops._SCAN_ARENAS.pop(key, None)
+        ops._SCAN_NEXT.pop(key, None)

@@ -21,7 +21,7 @@ done
 python tools/pmc_summary.py "$O/pmc" qm9,512,1 > "$O/traffic.json" && echo traffic ok
 # the bench with its kernel-timer pass: kernel_instances.py --split separates
 # the replayed steps from the timer pass (the launches the timer averages)
-timeout -k 10 600 rocprofv3 --kernel-trace --stats -T --output-format csv -d $O/prof_kt -o kt \
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_kt -o kt \
   -- python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-superbatch > $O/prof_bench.log 2>&1 || { echo rocprof failed; exit 1; }
 python tools/kernel_instances.py $O/prof_kt --split adam_step_k --json $O/replay.json --config qm9,512,1 > $O/kernel_instances.txt 2>&1 && echo replay ok
 SCGIB_TRAFFIC_FILE=$O/traffic.json SCGIB_REPLAY_FILE=$O/replay.json timeout -k 10 600 python bench.py --steps 300 --warmup 20 --cpu-seconds 20 > $O/bench.log 2>&1 || { echo bench failed; tail -5 $O/bench.log; exit 1; }

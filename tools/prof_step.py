@@ -17,7 +17,12 @@ last = 0
 for r in rows[i0:i1]:
     s = int(r["Start_Timestamp"]) - t0
     e = int(r["End_Timestamp"]) - t0
+    name = r["Kernel_Name"].replace("void ", "").replace("scgib::", "")
+    if "at::" in name:  # a torch kernel: its functor says which op it is
+        name = name.split("(")[0][:150]
+    else:
+        name = name.split("(")[0].split("<")[0][:48]
     print(f"{s/1000:8.2f} {e/1000:8.2f} {(e-s)/1000:7.2f} gap{(s-last)/1000:7.2f} "
-          f"q{r['Queue_Id']} {r['Kernel_Name'][:48]} g{r['Grid_Size_X']}")
+          f"q{r['Queue_Id']} {name} g{r['Grid_Size_X']}")
     last = max(last, e)
 print("span", (int(rows[i1]["Start_Timestamp"]) - t0) / 1000)

@@ -267,22 +267,28 @@ int scgib_gin_layer_bwd(const float *dy, const float *z2, const float *r, const 
                         const float *w2, int64_t n_nodes, float *dagg, float *slab,
                         float *wgrad, const int32_t *dims, const scgib_bn_bwd_pending *pending,
                         scgib_stream_t stream);
-/* ---- (f)1/(f)4: Set2Set attention readout (DGL Set2Set, models.py:565) ----
- * One round's per-graph half of Set2Set as Mainmodel_finetuning.forward
- * (models.py:515) and Mainmodel_domainadapt (:271-272) run it: for graph g
- * (rows [graph_ptr[g], graph_ptr[g+1]) of x [*][dim], dim <= 64),
- *   e_v = <x_v, q_g>, alpha = softmax_g(e), out_g = sum_v alpha_v x_v;
- * stat [2 n_graphs] receives (max_g e, softmax denominator) for the backward.
- * Backward: dx_v = alpha_v g_g + de_v q_g, dq_g = sum_v de_v x_v with
- * de_v = alpha_v (<g_g, x_v> - sum_u alpha_u <g_g, x_u>); rows of dx past
- * graph_ptr[n_graphs] (up to n_rows: capacity padding) are zeroed.  The LSTM
- * cell between rounds is the caller's.  No host sync: graph-capturable. */
-int scgib_set2set_fwd(const float *x, const float *q, const int32_t *graph_ptr,
-                      int64_t n_graphs, int32_t dim, float *stat, float *out,
+/* ---- (f)1/(f)4: Set2Set readout (DGL Set2Set(dim, n_iters, 1), models.py:565) ----
+ * The whole readout as Mainmodel_finetuning.forward (models.py:515) and
+ * Mainmodel_domainadapt (:271-272) run it, all n_iters rounds in one launch:
+ * for graph g (rows [graph_ptr[g], graph_ptr[g+1]) of x [*][dim], dim <= 64),
+ * from h = c = 0, q* = 0:
+ *   gates = W_ih q* + b_ih + W_hh h + b_hh  (w_ih [4 dim][2 dim], w_hh [4 dim][dim],
+ *           PyTorch LSTM gate order i, f, g, o);  c = sig(f) c + sig(i) tanh(g);
+ *   h = sig(o) tanh(c);  e_v = <x_v, h>;  alpha = softmax_g(e);  r = sum_v alpha_v x_v;
+ *   q* = [h, r];   out [n_graphs][2 dim] = the last q*.
+ * save [scgib_set2set_save_floats]: the per-round state the backward reads.
+ * Backward: d out -> dx (rows past graph_ptr[n_graphs], up to n_rows:
+ * capacity padding, zeroed), dw_ih, dw_hh, db_ih = db_hh; dgates
+ * [n_graphs * n_iters * 4 dim] is scratch.  No host sync: graph-capturable. */
+int64_t scgib_set2set_save_floats(int64_t n_graphs, int32_t dim, int32_t n_iters);
+int scgib_set2set_fwd(const float *x, const int32_t *graph_ptr, int64_t n_graphs, int32_t dim,
+                      int32_t n_iters, const float *w_ih, const float *b_ih, const float *w_hh,
+                      const float *b_hh, float *save, float *out, scgib_stream_t stream);
+int scgib_set2set_bwd(const float *x, const int32_t *graph_ptr, int64_t n_graphs, int32_t dim,
+                      int32_t n_iters, const float *w_ih, const float *w_hh, const float *save,
+                      const float *g_out, float *dx, int64_t n_rows, float *dgates,
+                      float *dw_ih, float *dw_hh, float *db_ih, float *db_hh,
                       scgib_stream_t stream);
-int scgib_set2set_bwd(const float *x, const float *q, const int32_t *graph_ptr,
-                      int64_t n_graphs, int32_t dim, const float *stat, const float *g_out,
-                      float *dx, float *dq, int64_t n_rows, scgib_stream_t stream);
 
 /* ---- A6: per-segment readouts (dgl.sum_nodes) -------------------------------
  * out[s,:] = sum_{i in [ptr[s], ptr[s+1])} x[i,:]   (models.py:716, 725, 733)

@@ -19,8 +19,10 @@ _P, _I64, _I32, _F, _D = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32, ctypes
 SIGNATURES = {
     "scgib_abi_version": (ctypes.c_int, []),
     "scgib_set_recon_fold": (ctypes.c_int, [ctypes.c_int]),
-    "scgib_set2set_fwd": (ctypes.c_int, [_P, _P, _P, _I64, _I32, _P, _P, _P]),
-    "scgib_set2set_bwd": (ctypes.c_int, [_P, _P, _P, _I64, _I32, _P, _P, _P, _P, _I64, _P]),
+    "scgib_set2set_save_floats": (_I64, [_I64, _I32, _I32]),
+    "scgib_set2set_fwd": (ctypes.c_int, [_P, _P, _I64, _I32, _I32, _P, _P, _P, _P, _P, _P, _P]),
+    "scgib_set2set_bwd": (ctypes.c_int, [_P, _P, _I64, _I32, _I32, _P, _P, _P, _P, _P, _I64, _P,
+                                         _P, _P, _P, _P, _P]),
     "scgib_pool_copy": (ctypes.c_int, [_P, _I32, _P, _P, _I64, _P]),
     "scgib_pool_copy2": (ctypes.c_int, [_P, _I32, _P, _P, _I64, _P, _P, _I64, _P]),
     "scgib_stream_signal": (ctypes.c_int, [_P, _P]),
@@ -168,7 +170,7 @@ class RunningUpdate(ctypes.Structure):
                 ("num_batches_tracked", ctypes.c_void_p)]
 
 
-ABI_VERSION = 14
+ABI_VERSION = 15
 STATS_STRIDE = 260
 PGRAD_STRIDE = 324
 HIDDEN = 64

@@ -1,23 +1,29 @@
-// Set2Set attention readout (gfx950): the per-graph half of DGL's Set2Set
-// (reference models.py:565, used by Mainmodel_finetuning.forward :515 and
-// Mainmodel_domainadapt :271-272; DGL 1.1 nn/pytorch/glob.py semantics):
+// Set2Set readout (gfx950): DGL Set2Set(d, n_iters, 1) as the reference
+// builds it (models.py:565; used by Mainmodel_finetuning.forward :515 and
+// Mainmodel_domainadapt :271-272; DGL 1.1 nn/pytorch/glob.py semantics), ALL
+// n_iters rounds in one launch per direction:
 //
-//   e_v = <x_v, q_g>;  alpha_v = exp(e_v - max_g e) / sum_g exp(. - max);
-//   readout_g = sum_{v in g} x_v alpha_v
+//   gates = W_ih q* + b_ih + W_hh h + b_hh      (PyTorch LSTM gate order i, f, g, o)
+//   c = sig(f) c + sig(i) tanh(g);  h = sig(o) tanh(c)
+//   e_v = <x_v, h_g>;  alpha = softmax over the graph's rows;  r_g = sum_v alpha_v x_v
+//   q* = [h, r]
 //
-// and its backward.  The LSTM cell between the rounds stays with the host
-// (models.Set2Set: four [B, 4d] products on rocBLAS, no host sync); this
-// kernel replaces the per-round scatter_reduce / exp / index_add / segment
-// sum chain of the eager form and its host->device copy of the segment ids,
-// so the fine-tune step is capturable in a HIP graph.
+// Every graph's recurrence is independent of the others' (the LSTM runs on
+// the B graph rows, one row each), so one 256-thread workgroup per graph runs
+// the whole recurrence: thread j < 4d owns gate j (its dot products over the
+// 2d + d inputs, held in LDS), wave 0 runs the attention over the graph's rows
+// (lane = 16 q + j: row group q takes rows p0 + q, p0 + q + 4, ...; lane j
+// holds channels j, j + 16, j + 32, j + 48, d <= 64).  This replaces the
+// ~13 torch launches per round of the LSTM cell + attention (two GEMMs,
+// eight elementwise ops, the readout, the concatenation) and their backward.
 //
-// One wavefront per graph.  Lane l = 16 q + j: row group q (0..3) takes rows
-// p0 + q, p0 + q + 4, ...; lane j holds channels j, j + 16, j + 32, j + 48
-// (< d, d <= 64: the MLP output d = 64 and the raw feature widths of
-// s2s_rev, e.g. 9).  A row dot is a 16-lane butterfly; a per-channel sum
-// over the graph's rows is a per-lane accumulator folded over the four row
-// groups at the end.  Latency-bound VALU/shuffle work (a few hundred flops
-// per row): no MFMA.
+// Saved per graph and round (the backward's inputs), s2s_save(d) floats:
+//   q*_prev [2d] | h_prev [d] | c_prev [d] | act [4d] (sig i, sig f, tanh g, sig o) |
+//   c [d] | (max_g e, softmax denominator)
+// The backward (one workgroup per graph, rounds in reverse) writes the gates'
+// pre-activation gradients dG [B][T][4d]; set2set_wgrad_k then forms
+// dW_ih = dG^T q*_prev, dW_hh = dG^T h_prev and db = sum dG (fixed order).
+// Latency-bound VALU/shuffle work: no MFMA.
 #include "common.h"
 
 namespace scgib {
@@ -25,6 +31,8 @@ namespace scgib {
 namespace {
 
 constexpr int kS2SMaxD = 64;
+
+__host__ __device__ constexpr int s2s_save(int d) { return 9 * d + 2; }
 
 __device__ __forceinline__ float s2s_red16(float v) {
     v += __shfl_xor(v, 1, kWave);
@@ -43,27 +51,10 @@ __device__ __forceinline__ float s2s_max_all(float v) {
     for (int o = 1; o < 64; o <<= 1) v = fmaxf(v, __shfl_xor(v, o, kWave));
     return v;
 }
+__device__ __forceinline__ float s2s_sigmoid(float v) { return 1.f / (1.f + expf(-v)); }
 
-// rows [p0, p1) of graph g (capacity mode: graphs past dims-counted rows are
-// empty only if their ptr entries say so; graph_ptr is always maintained)
-__device__ __forceinline__ void s2s_rows(const int32_t *__restrict__ ptr, int64_t g, int64_t &p0,
-                                         int64_t &p1) {
-    p0 = ptr[g];
-    p1 = ptr[g + 1];
-}
-
-// zero rows [ptr[nseg], nrows) of out (the capacity padding of dfeat)
-__device__ __forceinline__ void s2s_zero_tail(const int32_t *__restrict__ ptr, int64_t nseg,
-                                              int64_t nrows, int d, float *__restrict__ out,
-                                              int64_t blk, int64_t nblk) {
-    const int64_t r0 = ptr[nseg];
-    for (int64_t i = r0 * d + blk * 64 + threadIdx.x; i < nrows * d; i += nblk * 64) out[i] = 0.f;
-}
-
-}  // namespace
-
-// the logit e_r = <x_r, q> of row r for the 16 lanes of its row group (every
-// lane of the group returns it)
+// the logit <x_r, q> of row r for the 16 lanes of its row group (every lane
+// of the group returns it)
 __device__ __forceinline__ float s2s_logit(const float *__restrict__ x, int64_t r, int d, int j,
                                            const float (&qv)[4]) {
     float dot = 0.f;
@@ -75,96 +66,80 @@ __device__ __forceinline__ float s2s_logit(const float *__restrict__ x, int64_t 
     return s2s_red16(dot);
 }
 
-// stat[2 g] = max_g e, stat[2 g + 1] = the softmax denominator.  The logits
-// are recomputed in each pass (a 16-lane dot per row) rather than kept: a
-// graph may hold any number of rows, and registers / LDS would bound it.
-__global__ __launch_bounds__(64) void set2set_fwd_k(const float *__restrict__ x,
-                                                    const float *__restrict__ q,
-                                                    const int32_t *__restrict__ ptr, int64_t nseg,
-                                                    int d, float *__restrict__ stat,
-                                                    float *__restrict__ out) {
-    const int64_t g = blockIdx.x;
+// wave 0: the attention readout of rows [p0, p1) with query q (LDS, d
+// floats) into r (LDS) and (max, denominator) into st.  The logits are
+// recomputed in each pass (a 16-lane dot per row) rather than kept: a graph
+// may hold any number of rows.
+__device__ void s2s_attend_fwd(const float *__restrict__ x, int64_t p0, int64_t p1, int d,
+                               const float *q, float *r, float *st) {
     const int l = threadIdx.x, rq = l >> 4, j = l & 15;
-    int64_t p0, p1;
-    s2s_rows(ptr, g, p0, p1);
     float qv[4];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        const int c = j + 16 * k;
-        qv[k] = c < d ? q[g * d + c] : 0.f;
-    }
+    for (int k = 0; k < 4; ++k) qv[k] = j + 16 * k < d ? q[j + 16 * k] : 0.f;
     // (a row group's 16 lanes run a row together: the butterflies stay
     // within active lanes whatever the other groups do)
     float mx = -INFINITY;
-    for (int64_t r = p0 + rq; r < p1; r += 4) mx = fmaxf(mx, s2s_logit(x, r, d, j, qv));
+    for (int64_t v = p0 + rq; v < p1; v += 4) mx = fmaxf(mx, s2s_logit(x, v, d, j, qv));
     mx = s2s_max_all(mx);
     float den = 0.f;
-    for (int64_t r = p0 + rq; r < p1; r += 4) {
-        const float a = expf(s2s_logit(x, r, d, j, qv) - mx);
+    for (int64_t v = p0 + rq; v < p1; v += 4) {
+        const float a = expf(s2s_logit(x, v, d, j, qv) - mx);
         den += j == 0 ? a : 0.f;
     }
     den = s2s_red_q(s2s_red16(den));
-    // readout_c = sum_r x_rc (a_r / den), as feat * (a / den) summed per graph
     float acc[4] = {0.f, 0.f, 0.f, 0.f};
-    for (int64_t r = p0 + rq; r < p1; r += 4) {
-        const float alpha = expf(s2s_logit(x, r, d, j, qv) - mx) / den;
+    for (int64_t v = p0 + rq; v < p1; v += 4) {
+        const float alpha = expf(s2s_logit(x, v, d, j, qv) - mx) / den;
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             const int c = j + 16 * k;
-            acc[k] = fmaf(c < d ? x[r * d + c] : 0.f, alpha, acc[k]);
+            acc[k] = fmaf(c < d ? x[v * d + c] : 0.f, alpha, acc[k]);
         }
     }
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
         const float s = s2s_red_q(acc[k]);
         const int c = j + 16 * k;
-        if (rq == 0 && c < d) out[g * d + c] = s;
+        if (rq == 0 && c < d) r[c] = s;
     }
     if (l == 0) {
-        stat[2 * g] = mx;
-        stat[2 * g + 1] = den;
+        st[0] = mx;
+        st[1] = den;
     }
 }
 
-// d readout -> d x, d q:  dalpha_v = <g_g, x_v>;  s = sum alpha dalpha;
-// de_v = alpha_v (dalpha_v - s);  dx_v = alpha_v g_g + de_v q_g;  dq_g = sum de_v x_v
-__global__ __launch_bounds__(64) void set2set_bwd_k(
-    const float *__restrict__ x, const float *__restrict__ q, const int32_t *__restrict__ ptr,
-    int64_t nseg, int d, const float *__restrict__ stat, const float *__restrict__ gout,
-    float *__restrict__ dx, float *__restrict__ dq, int64_t nrows) {
-    if (static_cast<int64_t>(blockIdx.x) >= nseg) {  // block-uniform: the padding rows
-        s2s_zero_tail(ptr, nseg, nrows, d, dx, blockIdx.x - nseg, gridDim.x - nseg);
-        return;
-    }
-    const int64_t g = blockIdx.x;
+// wave 0: the attention backward for d r = gr (LDS) with query q (LDS):
+//   dalpha_v = <gr, x_v>;  s = sum alpha dalpha;  de_v = alpha_v (dalpha_v - s)
+//   dx_v (+)= alpha_v gr + de_v q;  dq = sum de_v x_v  (into dq, LDS)
+__device__ void s2s_attend_bwd(const float *__restrict__ x, int64_t p0, int64_t p1, int d,
+                               const float *q, const float *gr, float mx, float den,
+                               float *__restrict__ dx, bool accumulate, float *dq) {
     const int l = threadIdx.x, rq = l >> 4, j = l & 15;
-    int64_t p0, p1;
-    s2s_rows(ptr, g, p0, p1);
-    const float mx = stat[2 * g], den = stat[2 * g + 1];
     float gv[4], qv[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
         const int c = j + 16 * k;
-        gv[k] = c < d ? gout[g * d + c] : 0.f;
-        qv[k] = c < d ? q[g * d + c] : 0.f;
+        gv[k] = c < d ? gr[c] : 0.f;
+        qv[k] = c < d ? q[c] : 0.f;
     }
     float s = 0.f;
-    for (int64_t r = p0 + rq; r < p1; r += 4) {
-        const float alpha = expf(s2s_logit(x, r, d, j, qv) - mx) / den;
-        const float da = s2s_logit(x, r, d, j, gv);
+    for (int64_t v = p0 + rq; v < p1; v += 4) {
+        const float alpha = expf(s2s_logit(x, v, d, j, qv) - mx) / den;
+        const float da = s2s_logit(x, v, d, j, gv);
         s += j == 0 ? alpha * da : 0.f;
     }
     s = s2s_red_q(s2s_red16(s));
     float acc[4] = {0.f, 0.f, 0.f, 0.f};
-    for (int64_t r = p0 + rq; r < p1; r += 4) {
-        const float alpha = expf(s2s_logit(x, r, d, j, qv) - mx) / den;
-        const float de = alpha * (s2s_logit(x, r, d, j, gv) - s);
+    for (int64_t v = p0 + rq; v < p1; v += 4) {
+        const float alpha = expf(s2s_logit(x, v, d, j, qv) - mx) / den;
+        const float de = alpha * (s2s_logit(x, v, d, j, gv) - s);
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             const int c = j + 16 * k;
             if (c < d) {
-                dx[r * d + c] = fmaf(de, qv[k], alpha * gv[k]);
-                acc[k] = fmaf(de, x[r * d + c], acc[k]);
+                const float t = fmaf(de, qv[k], alpha * gv[k]);
+                dx[v * d + c] = accumulate ? dx[v * d + c] + t : t;
+                acc[k] = fmaf(de, x[v * d + c], acc[k]);
             }
         }
     }
@@ -172,35 +147,194 @@ __global__ __launch_bounds__(64) void set2set_bwd_k(
     for (int k = 0; k < 4; ++k) {
         const float t = s2s_red_q(acc[k]);
         const int c = j + 16 * k;
-        if (rq == 0 && c < d) dq[g * d + c] = t;
+        if (rq == 0 && c < d) dq[c] = t;
     }
+}
+
+}  // namespace
+
+// One workgroup per graph: all n_iters rounds.  out [B][2d] = the last q*.
+__global__ __launch_bounds__(256) void set2set_fwd_k(
+    const float *__restrict__ x, const int32_t *__restrict__ ptr, int d, int T,
+    const float *__restrict__ w_ih, const float *__restrict__ b_ih,
+    const float *__restrict__ w_hh, const float *__restrict__ b_hh, float *__restrict__ save,
+    float *__restrict__ out) {
+    __shared__ float sQ[2 * kS2SMaxD], sH[kS2SMaxD], sC[kS2SMaxD], sA[4 * kS2SMaxD];
+    const int64_t g = blockIdx.x;
+    const int tid = threadIdx.x, D2 = 2 * d, G4 = 4 * d, S = s2s_save(d);
+    const int64_t p0 = ptr[g], p1 = ptr[g + 1];
+    if (tid < D2) sQ[tid] = 0.f;
+    if (tid < d) sH[tid] = sC[tid] = 0.f;
+    // this thread's gate biases (b_ih + b_hh added after the two products, as
+    // F.linear(q, W_ih, b_ih) + F.linear(h, W_hh, b_hh))
+    const float bi = tid < G4 ? b_ih[tid] : 0.f, bh = tid < G4 ? b_hh[tid] : 0.f;
+    __syncthreads();
+    for (int t = 0; t < T; ++t) {
+        float *sv = save + (g * T + t) * S;
+        if (tid < D2) sv[tid] = sQ[tid];
+        if (tid < d) {
+            sv[D2 + tid] = sH[tid];
+            sv[3 * d + tid] = sC[tid];
+        }
+        if (tid < G4) {  // gate tid
+            const float *wi = w_ih + static_cast<int64_t>(tid) * D2;
+            const float *wh = w_hh + static_cast<int64_t>(tid) * d;
+            float a = 0.f, b = 0.f;
+            for (int k = 0; k < D2; ++k) a = fmaf(wi[k], sQ[k], a);
+            for (int k = 0; k < d; ++k) b = fmaf(wh[k], sH[k], b);
+            const float z = (a + bi) + (b + bh);
+            const int kind = tid / d;  // 0 i, 1 f, 2 g, 3 o
+            const float act = kind == 2 ? tanhf(z) : s2s_sigmoid(z);
+            sA[tid] = act;
+            sv[4 * d + tid] = act;
+        }
+        __syncthreads();
+        if (tid < d) {
+            const float c = sA[d + tid] * sC[tid] + sA[tid] * sA[2 * d + tid];
+            const float h = sA[3 * d + tid] * tanhf(c);
+            sC[tid] = c;
+            sH[tid] = h;
+            sQ[tid] = h;
+            sv[8 * d + tid] = c;
+        }
+        __syncthreads();
+        if (tid < kWave) s2s_attend_fwd(x, p0, p1, d, sH, sQ + d, sv + 9 * d);
+        __syncthreads();
+    }
+    if (tid < D2) out[g * D2 + tid] = sQ[tid];
+}
+
+// One workgroup per graph, rounds in reverse: d q*_T = g_out -> dx (rows of
+// the graph; capacity rows past ptr[B] are zeroed by the extra workgroups)
+// and dG [B][T][4d] for set2set_wgrad_k.
+__global__ __launch_bounds__(256) void set2set_bwd_k(
+    const float *__restrict__ x, const int32_t *__restrict__ ptr, int64_t nseg, int d, int T,
+    const float *__restrict__ w_ih, const float *__restrict__ w_hh,
+    const float *__restrict__ save, const float *__restrict__ g_out, float *__restrict__ dx,
+    float *__restrict__ dG, int64_t nrows) {
+    if (static_cast<int64_t>(blockIdx.x) >= nseg) {  // block-uniform: the padding rows
+        const int64_t r0 = ptr[nseg], nb = gridDim.x - nseg;
+        for (int64_t i = r0 * d + (blockIdx.x - nseg) * 256 + threadIdx.x; i < nrows * d;
+             i += nb * 256)
+            dx[i] = 0.f;
+        return;
+    }
+    __shared__ float sDQ[2 * kS2SMaxD], sDH[kS2SMaxD], sDC[kS2SMaxD], sDG[4 * kS2SMaxD];
+    __shared__ float sHq[kS2SMaxD], sAtt[kS2SMaxD];
+    const int64_t g = blockIdx.x;
+    const int tid = threadIdx.x, D2 = 2 * d, G4 = 4 * d, S = s2s_save(d);
+    const int64_t p0 = ptr[g], p1 = ptr[g + 1];
+    if (tid < D2) sDQ[tid] = g_out[g * D2 + tid];
+    if (tid < d) sDH[tid] = sDC[tid] = 0.f;  // from round t + 1 (none after the last)
+    __syncthreads();
+    for (int t = T - 1; t >= 0; --t) {
+        const float *sv = save + (g * T + t) * S;
+        // h_t (the round's query) = q*_t's first half: the next round's q*_prev,
+        // or recomputed for the last round from its saved act / c
+        if (tid < d) {
+            const float c = sv[8 * d + tid];
+            sHq[tid] = sv[7 * d + tid] * tanhf(c);
+        }
+        __syncthreads();
+        if (tid < kWave)
+            s2s_attend_bwd(x, p0, p1, d, sHq, sDQ + d, sv[9 * d], sv[9 * d + 1], dx, t < T - 1,
+                           sAtt);
+        __syncthreads();
+        if (tid < d) {  // the cell: dh_t = d q*_t[:d] + the attention's d query + from round t + 1
+            const float dh = (sDQ[tid] + sAtt[tid]) + sDH[tid];
+            const float ig = sv[4 * d + tid], fg = sv[5 * d + tid], gg = sv[6 * d + tid],
+                        og = sv[7 * d + tid], c = sv[8 * d + tid], cp = sv[3 * d + tid];
+            const float tc = tanhf(c);
+            const float dc = sDC[tid] + dh * og * (1.f - tc * tc);
+            sDG[tid] = dc * gg * ig * (1.f - ig);             // i
+            sDG[d + tid] = dc * cp * fg * (1.f - fg);         // f
+            sDG[2 * d + tid] = dc * ig * (1.f - gg * gg);     // g
+            sDG[3 * d + tid] = dh * tc * og * (1.f - og);     // o
+            sDC[tid] = dc * fg;                               // -> c_{t-1}
+        }
+        __syncthreads();
+        if (tid < G4) dG[(g * T + t) * G4 + tid] = sDG[tid];
+        // d q*_{t-1} = W_ih^T dG, d h_{t-1} (gates path) = W_hh^T dG
+        float a = 0.f;
+        if (tid < D2)
+            for (int j = 0; j < G4; ++j) a = fmaf(w_ih[static_cast<int64_t>(j) * D2 + tid], sDG[j], a);
+        float b = 0.f;
+        if (tid < d)
+            for (int j = 0; j < G4; ++j) b = fmaf(w_hh[static_cast<int64_t>(j) * d + tid], sDG[j], b);
+        __syncthreads();
+        if (tid < D2) sDQ[tid] = a;
+        if (tid < d) sDH[tid] = b;
+        __syncthreads();
+    }
+}
+
+// dW_ih [4d][2d], dW_hh [4d][d], db_ih = db_hh [4d] (two outputs: two parameters):
+// workgroup k < 3d forms column k of [dW_ih | dW_hh] over the R = B T saved
+// rounds in order; workgroup 3d the bias.  Thread j = gate.
+__global__ __launch_bounds__(256) void set2set_wgrad_k(const float *__restrict__ save,
+                                                       const float *__restrict__ dG, int64_t R,
+                                                       int d, float *__restrict__ dw_ih,
+                                                       float *__restrict__ dw_hh,
+                                                       float *__restrict__ db_ih,
+                                                       float *__restrict__ db_hh) {
+    const int k = blockIdx.x, j = threadIdx.x, D2 = 2 * d, G4 = 4 * d, S = s2s_save(d);
+    if (j >= G4) return;
+    float acc = 0.f;
+    if (k == 3 * d) {
+        for (int64_t r = 0; r < R; ++r) acc += dG[r * G4 + j];
+        db_ih[j] = acc;
+        db_hh[j] = acc;
+        return;
+    }
+    // save row r starts with [q*_prev (2d) | h_prev (d)]: column k of both inputs
+    for (int64_t r = 0; r < R; ++r) acc = fmaf(dG[r * G4 + j], save[r * S + k], acc);
+    if (k < D2)
+        dw_ih[static_cast<int64_t>(j) * D2 + k] = acc;
+    else
+        dw_hh[static_cast<int64_t>(j) * d + (k - D2)] = acc;
 }
 
 }  // namespace scgib
 
 using namespace scgib;
 
-extern "C" int scgib_set2set_fwd(const float *x, const float *q, const int32_t *graph_ptr,
-                                 int64_t n_graphs, int32_t dim, float *stat, float *out,
-                                 scgib_stream_t stream) {
-    if (n_graphs < 0 || dim < 1 || dim > kS2SMaxD) return SCGIB_EINVAL;
+extern "C" int64_t scgib_set2set_save_floats(int64_t n_graphs, int32_t dim, int32_t n_iters) {
+    return n_graphs * n_iters * s2s_save(dim);
+}
+
+extern "C" int scgib_set2set_fwd(const float *x, const int32_t *graph_ptr, int64_t n_graphs,
+                                 int32_t dim, int32_t n_iters, const float *w_ih,
+                                 const float *b_ih, const float *w_hh, const float *b_hh,
+                                 float *save, float *out, scgib_stream_t stream) {
+    if (n_graphs < 0 || dim < 1 || dim > kS2SMaxD || n_iters < 1) return SCGIB_EINVAL;
     if (n_graphs == 0) return SCGIB_OK;
-    if (!x || !q || !graph_ptr || !stat || !out) return SCGIB_EINVAL;
-    set2set_fwd_k<<<static_cast<unsigned>(n_graphs), 64, 0, as_stream(stream)>>>(
-        x, q, graph_ptr, n_graphs, dim, stat, out);
+    if (!x || !graph_ptr || !w_ih || !b_ih || !w_hh || !b_hh || !save || !out)
+        return SCGIB_EINVAL;
+    set2set_fwd_k<<<static_cast<unsigned>(n_graphs), 256, 0, as_stream(stream)>>>(
+        x, graph_ptr, dim, n_iters, w_ih, b_ih, w_hh, b_hh, save, out);
     return launch_status();
 }
 
-extern "C" int scgib_set2set_bwd(const float *x, const float *q, const int32_t *graph_ptr,
-                                 int64_t n_graphs, int32_t dim, const float *stat,
-                                 const float *g_out, float *dx, float *dq, int64_t n_rows,
+extern "C" int scgib_set2set_bwd(const float *x, const int32_t *graph_ptr, int64_t n_graphs,
+                                 int32_t dim, int32_t n_iters, const float *w_ih,
+                                 const float *w_hh, const float *save, const float *g_out,
+                                 float *dx, int64_t n_rows, float *dgates, float *dw_ih,
+                                 float *dw_hh, float *db_ih, float *db_hh,
                                  scgib_stream_t stream) {
-    if (n_graphs < 0 || dim < 1 || dim > kS2SMaxD || n_rows < 0) return SCGIB_EINVAL;
+    if (n_graphs < 0 || dim < 1 || dim > kS2SMaxD || n_iters < 1 || n_rows < 0)
+        return SCGIB_EINVAL;
     if (n_graphs == 0) return SCGIB_OK;
-    if (!x || !q || !graph_ptr || !stat || !g_out || !dx || !dq) return SCGIB_EINVAL;
-    const int64_t tail = (n_rows * dim + 64 * 64 - 1) / (64 * 64);  // padding-zero blocks (<= 64 rows of work each)
+    if (!x || !graph_ptr || !w_ih || !w_hh || !save || !g_out || !dx || !dgates || !dw_ih ||
+        !dw_hh || !db_ih || !db_hh)
+        return SCGIB_EINVAL;
+    hipStream_t st = as_stream(stream);
+    const int64_t tail = (n_rows * dim + 256 * 16 - 1) / (256 * 16);  // padding-zero blocks
     const int64_t extra = tail < 1 ? 1 : (tail > 256 ? 256 : tail);
-    set2set_bwd_k<<<static_cast<unsigned>(n_graphs + extra), 64, 0, as_stream(stream)>>>(
-        x, q, graph_ptr, n_graphs, dim, stat, g_out, dx, dq, n_rows);
+    set2set_bwd_k<<<static_cast<unsigned>(n_graphs + extra), 256, 0, st>>>(
+        x, graph_ptr, n_graphs, dim, n_iters, w_ih, w_hh, save, g_out, dx, dgates, n_rows);
+    int rc = launch_status();
+    if (rc != SCGIB_OK) return rc;
+    set2set_wgrad_k<<<static_cast<unsigned>(3 * dim + 1), 256, 0, st>>>(
+        save, dgates, n_graphs * n_iters, dim, dw_ih, dw_hh, db_ih, db_hh);
     return launch_status();
 }

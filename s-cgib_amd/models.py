@@ -107,12 +107,12 @@ class GIN(nn.Module):
 
 class Set2Set(nn.Module):
     """DGL Set2Set (LSTM(2d -> d), n_iters rounds; reference models.py:565,
-    the fine-tune and domain-adaptation readout).  Each round: one LSTM cell
-    step on q_star (torch ops, PyTorch gate order i, f, g, o — the reference's
-    single-layer nn.LSTM), then the per-graph softmax attention readout on
-    the device (ops.set2set_attend, one wavefront per graph).  No host sync
-    and no host->device copy, so a fine-tune step holding it is capturable.
-    ``lstm`` keeps nn.LSTM's parameters (state_dict parity)."""
+    the fine-tune and domain-adaptation readout): the LSTM recurrence (PyTorch
+    gate order i, f, g, o — the reference's single-layer nn.LSTM) and the
+    per-graph softmax attention readouts of all rounds in ONE device launch
+    per direction (ops.set2set, csrc/set2set.hip; one workgroup per graph).
+    No host sync and no host->device copy, so a fine-tune step holding it is
+    capturable.  ``lstm`` keeps nn.LSTM's parameters (state_dict parity)."""
 
     def __init__(self, input_dim, n_iters, n_layers):
         super().__init__()
@@ -123,20 +123,7 @@ class Set2Set(nn.Module):
         self.lstm = nn.LSTM(self.output_dim, self.input_dim, n_layers)
 
     def forward(self, graph, feat):
-        bs, d = graph.batch_size, self.input_dim
-        lstm = self.lstm
-        hx = feat.new_zeros(bs, d)
-        cx = feat.new_zeros(bs, d)
-        q_star = feat.new_zeros(bs, self.output_dim)
-        for _ in range(self.n_iters):
-            gates = F.linear(q_star, lstm.weight_ih_l0, lstm.bias_ih_l0) + \
-                F.linear(hx, lstm.weight_hh_l0, lstm.bias_hh_l0)
-            i, f, g, o = gates.chunk(4, dim=1)
-            cx = torch.sigmoid(f) * cx + torch.sigmoid(i) * torch.tanh(g)
-            hx = torch.sigmoid(o) * torch.tanh(cx)
-            readout = ops.set2set_attend(feat, hx, graph)
-            q_star = torch.cat([hx, readout], dim=-1)
-        return q_star
+        return ops.set2set(feat, graph, self.lstm, self.n_iters)
 
 
 _SIDE_STREAMS = {}

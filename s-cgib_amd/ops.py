@@ -919,36 +919,50 @@ def sum_nodes_graph(graph, x):
     return segment_sum(x, graph.graph_ptr, graph.batch_size)
 
 
-class _Set2SetAttend(torch.autograd.Function):
+class _Set2Set(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, q, ptr, nseg):
-        x, q = _f32(x, "set2set x"), _f32(q, "set2set q")
-        if x.dim() != 2 or q.shape != (nseg, x.shape[1]) or x.shape[1] > 64:
-            raise _lib.ScgibError(f"set2set: x {tuple(x.shape)}, q {tuple(q.shape)}, "
-                                  f"{nseg} graphs (width <= 64)")
-        out = torch.empty(nseg, x.shape[1], dtype=torch.float32, device=x.device)
-        stat = torch.empty(max(2 * nseg, 1), dtype=torch.float32, device=x.device)
-        _lib.call("scgib_set2set_fwd", _p(x), _p(q), _p(ptr), nseg, x.shape[1], _p(stat),
-                  _p(out), _stream())
-        ctx.save_for_backward(x, q, stat)
-        ctx.ptr, ctx.nseg = ptr, nseg
+    def forward(ctx, x, w_ih, b_ih, w_hh, b_hh, ptr, nseg, n_iters):
+        x = _f32(x, "set2set x")
+        d = x.shape[1] if x.dim() == 2 else -1
+        w_ih, w_hh = _f32(w_ih, "lstm.weight_ih_l0"), _f32(w_hh, "lstm.weight_hh_l0")
+        b_ih, b_hh = _f32(b_ih, "lstm.bias_ih_l0"), _f32(b_hh, "lstm.bias_hh_l0")
+        if not (1 <= d <= 64) or tuple(w_ih.shape) != (4 * d, 2 * d) or \
+                tuple(w_hh.shape) != (4 * d, d) or b_ih.numel() != 4 * d or b_hh.numel() != 4 * d:
+            raise _lib.ScgibError(f"set2set: x {tuple(x.shape)} (width <= 64), w_ih "
+                                  f"{tuple(w_ih.shape)}, w_hh {tuple(w_hh.shape)}")
+        save = torch.empty(max(int(_lib.query("scgib_set2set_save_floats", nseg, d, n_iters)), 1),
+                           dtype=torch.float32, device=x.device)
+        out = torch.empty(nseg, 2 * d, dtype=torch.float32, device=x.device)
+        _lib.call("scgib_set2set_fwd", _p(x), _p(ptr), nseg, d, n_iters, _p(w_ih), _p(b_ih),
+                  _p(w_hh), _p(b_hh), _p(save), _p(out), _stream())
+        ctx.save_for_backward(x, w_ih, w_hh, save)
+        ctx.ptr, ctx.nseg, ctx.n_iters = ptr, nseg, n_iters
         return out
 
     @staticmethod
     def backward(ctx, g):
-        x, q, stat = ctx.saved_tensors
+        x, w_ih, w_hh, save = ctx.saved_tensors
         g = _f32(g, "set2set.backward")
-        dx, dq = torch.empty_like(x), torch.empty_like(q)
-        _lib.call("scgib_set2set_bwd", _p(x), _p(q), _p(ctx.ptr), ctx.nseg, x.shape[1], _p(stat),
-                  _p(g), _p(dx), _p(dq), x.shape[0], _stream())
-        return dx, dq, None, None
+        d = x.shape[1]
+        dx = torch.empty_like(x)
+        dgates = torch.empty(max(ctx.nseg * ctx.n_iters * 4 * d, 1), dtype=torch.float32,
+                             device=x.device)
+        dw_ih, dw_hh = torch.empty_like(w_ih), torch.empty_like(w_hh)
+        db_ih = torch.empty(4 * d, dtype=torch.float32, device=x.device)
+        db_hh = torch.empty_like(db_ih)
+        _lib.call("scgib_set2set_bwd", _p(x), _p(ctx.ptr), ctx.nseg, d, ctx.n_iters, _p(w_ih),
+                  _p(w_hh), _p(save), _p(g), _p(dx), x.shape[0], _p(dgates), _p(dw_ih),
+                  _p(dw_hh), _p(db_ih), _p(db_hh), _stream())
+        return dx, dw_ih, db_ih, dw_hh, db_hh, None, None, None
 
 
-def set2set_attend(x, q, graph):
-    """One Set2Set round's attention readout on the device (DGL Set2Set,
-    models.py:565): softmax over each graph's rows of <x_v, q_g>, then the
-    alpha-weighted row sum per graph."""
-    return _Set2SetAttend.apply(x, q, graph.graph_ptr, int(graph.batch_size))
+def set2set(x, graph, lstm, n_iters):
+    """DGL Set2Set(d, n_iters, 1) (models.py:565) on the device: the LSTM
+    recurrence and the per-graph softmax attention readouts of all n_iters
+    rounds in one launch (scgib_set2set_fwd); ``lstm`` = the module's
+    nn.LSTM (its parameters)."""
+    return _Set2Set.apply(x, lstm.weight_ih_l0, lstm.bias_ih_l0, lstm.weight_hh_l0,
+                          lstm.bias_hh_l0, graph.graph_ptr, int(graph.batch_size), int(n_iters))
 
 
 # ---------------------------------------------------------------------------

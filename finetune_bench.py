@@ -134,13 +134,17 @@ def run(bench, a, dev):
         dict.__setitem__(gx.ndata, "x", F.normalize(gh.ndata["x"].float()))
         padded.append(static.pad(gx))
     pool = static.pool(padded)
-    tpool = torch.stack(targets).to(dev)  # [pool, B, 1]
+    # the targets walk their own resident pool in step with the batches: one
+    # pool-copy launch per step (its own cursor, advanced like the batch's)
+    tdev = [t.to(dev).contiguous() for t in targets]
+    ttable = torch.tensor([t.data_ptr() for t in tdev], dtype=torch.int64, device=dev)
+    tcursor = torch.zeros(2, dtype=torch.int32, device=dev)
+    tg = torch.empty(B, 1, dtype=torch.float32, device=dev)
 
     def body():
         static.load_next(pool)
-        # the batch just loaded: the cursor the copy kernel advanced, minus one
-        idx = torch.remainder(pool["cursor"][:1].long() - 1, pool["n"])
-        tg = tpool.index_select(0, idx)[0]
+        pkg._lib.call("scgib_pool_copy", pkg.ops._p(ttable), len(tdev), pkg.ops._p(tcursor),
+                      pkg.ops._p(tg), tg.numel() * 4, pkg.ops._stream())
         scores, *_ = ft(static.graph, static.x, None, None, 1, None, 2, dev, B)
         loss = ft.loss(scores, tg)
         loss.backward()

@@ -457,7 +457,8 @@ typedef struct {
     int64_t *num_batches_tracked;
 } scgib_running_update;
 /* Backward of scgib_interaction_fwd.  The KL gradient is g_kl [2 n_last, 64],
- * or g_klmean (device scalar, gradient of kl_mean), or neither (both NULL).
+ * or g_klmean (device scalar, gradient of kl_mean), or neither (both NULL);
+ * g_z1 / g_z2 may be NULL (readouts that feed no loss: zero gradient).
  * pad_rows: zero rows [graph_ptr[B], n_nodes) of df, dt, ds.
  * Outputs df, dt, ds [N,64] and per-graph parameter-gradient partials
  * pgrad[B, SCGIB_PGRAD_STRIDE] laid out as

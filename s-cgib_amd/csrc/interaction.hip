@@ -497,8 +497,9 @@ __global__ __launch_bounds__(64) void interaction_bwd_k(
     }
     dwhi = red_q4(dwhi);
     const float dc = red_q(dcq);
-    const float4 gb = ld4(g_z1 + gi * 64 + L.ch) + dc * wlo;  // d z-bar -> every node's noisy
-    const float4 gz2 = ld4(g_z2 + gi * 64 + L.ch);            // d readout(f) -> every node's f
+    // (a NULL g_z1 / g_z2: the readouts feed no loss, e.g. in the fine-tune head)
+    const float4 gb = (g_z1 ? ld4(g_z1 + gi * 64 + L.ch) : f4(0.f)) + dc * wlo;  // d z-bar -> every node's noisy
+    const float4 gz2 = g_z2 ? ld4(g_z2 + gi * 64 + L.ch) : f4(0.f);  // d readout(f) -> every node's f
 
     // ---- KL (last graph) ----
     // gradient of the KL term: a tensor g_kl [2n, 64] (both copies), or the
@@ -681,8 +682,7 @@ extern "C" int scgib_interaction_bwd(
     if (n_graphs < 0 || n_nodes < 0) return SCGIB_EINVAL;
     if (n_graphs == 0) return SCGIB_OK;
     if (n_graphs > 0x7fffffff) return SCGIB_EUNSUPPORTED;
-    if (!graph_ptr || !g_z1 || !g_z2 || !bn_gamma || !bn_beta || !w2 || !w_att || !z1 ||
-        !stats || !pgrad)
+    if (!graph_ptr || !bn_gamma || !bn_beta || !w2 || !w_att || !z1 || !stats || !pgrad)
         return SCGIB_EINVAL;
     if (n_nodes > 0 && (!g_im || !f || !t || !s || !u_feat || !lam || !logit || !df || !dt ||
                         !ds))

@@ -53,15 +53,60 @@ __device__ __forceinline__ float s2s_max_all(float v) {
 }
 __device__ __forceinline__ float s2s_sigmoid(float v) { return 1.f / (1.f + expf(-v)); }
 
+// <w[0, n), v[0, n)>, w a weight row in global memory, v in LDS: float4 loads
+// when the row is a multiple of 4 floats (it is then 16-B aligned: row j
+// starts at j n), four accumulators, unrolled so the row's loads are in
+// flight together (a latency-bound dot: one thread per gate)
+__device__ __forceinline__ float s2s_dot(const float *__restrict__ w, const float *v, int n) {
+    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+    if ((n & 3) == 0) {
+        const float4 *w4 = reinterpret_cast<const float4 *>(w);
+#pragma unroll 16
+        for (int k = 0; k < n / 4; ++k) {
+            const float4 x = w4[k];
+            a0 = fmaf(x.x, v[4 * k], a0);
+            a1 = fmaf(x.y, v[4 * k + 1], a1);
+            a2 = fmaf(x.z, v[4 * k + 2], a2);
+            a3 = fmaf(x.w, v[4 * k + 3], a3);
+        }
+    } else {
+#pragma unroll 4
+        for (int k = 0; k < n; ++k) a0 = fmaf(w[k], v[k], a0);
+    }
+    return (a0 + a1) + (a2 + a3);
+}
+
+// The graph's rows: the first kS2SRows staged in LDS by the workgroup (every
+// round and pass re-reads them), the rest read from global memory.
+constexpr int kS2SRows = 64;
+struct S2SRows {
+    const float *__restrict__ x;  // global [*][d]
+    const float *xs;              // LDS copy of rows [p0, p0 + ns)
+    int64_t p0;
+    int ns, d;
+    __device__ __forceinline__ float at(int64_t v, int c) const {
+        const int64_t o = v - p0;
+        return o < ns ? xs[o * d + c] : x[v * d + c];
+    }
+};
+
+// all threads: stage rows [p0, p0 + min(n, kS2SRows)) of x into xs (then a barrier)
+__device__ __forceinline__ int s2s_stage(const float *__restrict__ x, int64_t p0, int64_t p1,
+                                         int d, float *xs) {
+    const int ns = static_cast<int>(p1 - p0 < kS2SRows ? p1 - p0 : kS2SRows);
+    for (int i = threadIdx.x; i < ns * d; i += blockDim.x) xs[i] = x[p0 * d + i];
+    return ns;
+}
+
 // the logit <x_r, q> of row r for the 16 lanes of its row group (every lane
 // of the group returns it)
-__device__ __forceinline__ float s2s_logit(const float *__restrict__ x, int64_t r, int d, int j,
+__device__ __forceinline__ float s2s_logit(const S2SRows &X, int64_t r, int j,
                                            const float (&qv)[4]) {
     float dot = 0.f;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
         const int c = j + 16 * k;
-        dot = fmaf(c < d ? x[r * d + c] : 0.f, qv[k], dot);
+        dot = fmaf(c < X.d ? X.at(r, c) : 0.f, qv[k], dot);
     }
     return s2s_red16(dot);
 }
@@ -70,8 +115,10 @@ __device__ __forceinline__ float s2s_logit(const float *__restrict__ x, int64_t 
 // floats) into r (LDS) and (max, denominator) into st.  The logits are
 // recomputed in each pass (a 16-lane dot per row) rather than kept: a graph
 // may hold any number of rows.
-__device__ void s2s_attend_fwd(const float *__restrict__ x, int64_t p0, int64_t p1, int d,
-                               const float *q, float *r, float *st) {
+__device__ void s2s_attend_fwd(const S2SRows &X, int64_t p1, const float *q, float *r,
+                               float *st) {
+    const int64_t p0 = X.p0;
+    const int d = X.d;
     const int l = threadIdx.x, rq = l >> 4, j = l & 15;
     float qv[4];
 #pragma unroll
@@ -79,21 +126,21 @@ __device__ void s2s_attend_fwd(const float *__restrict__ x, int64_t p0, int64_t 
     // (a row group's 16 lanes run a row together: the butterflies stay
     // within active lanes whatever the other groups do)
     float mx = -INFINITY;
-    for (int64_t v = p0 + rq; v < p1; v += 4) mx = fmaxf(mx, s2s_logit(x, v, d, j, qv));
+    for (int64_t v = p0 + rq; v < p1; v += 4) mx = fmaxf(mx, s2s_logit(X, v, j, qv));
     mx = s2s_max_all(mx);
     float den = 0.f;
     for (int64_t v = p0 + rq; v < p1; v += 4) {
-        const float a = expf(s2s_logit(x, v, d, j, qv) - mx);
+        const float a = expf(s2s_logit(X, v, j, qv) - mx);
         den += j == 0 ? a : 0.f;
     }
     den = s2s_red_q(s2s_red16(den));
     float acc[4] = {0.f, 0.f, 0.f, 0.f};
     for (int64_t v = p0 + rq; v < p1; v += 4) {
-        const float alpha = expf(s2s_logit(x, v, d, j, qv) - mx) / den;
+        const float alpha = expf(s2s_logit(X, v, j, qv) - mx) / den;
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             const int c = j + 16 * k;
-            acc[k] = fmaf(c < d ? x[v * d + c] : 0.f, alpha, acc[k]);
+            acc[k] = fmaf(c < d ? X.at(v, c) : 0.f, alpha, acc[k]);
         }
     }
 #pragma unroll
@@ -110,10 +157,16 @@ __device__ void s2s_attend_fwd(const float *__restrict__ x, int64_t p0, int64_t 
 
 // wave 0: the attention backward for d r = gr (LDS) with query q (LDS):
 //   dalpha_v = <gr, x_v>;  s = sum alpha dalpha;  de_v = alpha_v (dalpha_v - s)
-//   dx_v (+)= alpha_v gr + de_v q;  dq = sum de_v x_v  (into dq, LDS)
-__device__ void s2s_attend_bwd(const float *__restrict__ x, int64_t p0, int64_t p1, int d,
-                               const float *q, const float *gr, float mx, float den,
-                               float *__restrict__ dx, bool accumulate, float *dq) {
+//   dx_v (+)= alpha_v gr + de_v q (dxs: the staged rows' LDS accumulator);
+//   dq = sum de_v x_v  (into dq, LDS)
+// (not inlined: inlined into set2set_bwd_k, hipcc 7.2 rejects the staged
+// accumulator's LDS read-modify-write, "Operand has incorrect register class")
+__device__ __noinline__ void s2s_attend_bwd(const S2SRows X, int64_t p1, const float *q,
+                                             const float *gr, float mx, float den,
+                                             float *__restrict__ dx, float *dxs, bool accumulate,
+                                             float *dq) {
+    const int64_t p0 = X.p0;
+    const int d = X.d;
     const int l = threadIdx.x, rq = l >> 4, j = l & 15;
     float gv[4], qv[4];
 #pragma unroll
@@ -124,22 +177,30 @@ __device__ void s2s_attend_bwd(const float *__restrict__ x, int64_t p0, int64_t 
     }
     float s = 0.f;
     for (int64_t v = p0 + rq; v < p1; v += 4) {
-        const float alpha = expf(s2s_logit(x, v, d, j, qv) - mx) / den;
-        const float da = s2s_logit(x, v, d, j, gv);
+        const float alpha = expf(s2s_logit(X, v, j, qv) - mx) / den;
+        const float da = s2s_logit(X, v, j, gv);
         s += j == 0 ? alpha * da : 0.f;
     }
     s = s2s_red_q(s2s_red16(s));
     float acc[4] = {0.f, 0.f, 0.f, 0.f};
     for (int64_t v = p0 + rq; v < p1; v += 4) {
-        const float alpha = expf(s2s_logit(x, v, d, j, qv) - mx) / den;
-        const float de = alpha * (s2s_logit(x, v, d, j, gv) - s);
+        const float alpha = expf(s2s_logit(X, v, j, qv) - mx) / den;
+        const float de = alpha * (s2s_logit(X, v, j, gv) - s);
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             const int c = j + 16 * k;
             if (c < d) {
                 const float t = fmaf(de, qv[k], alpha * gv[k]);
-                dx[v * d + c] = accumulate ? dx[v * d + c] + t : t;
-                acc[k] = fmaf(de, x[v * d + c], acc[k]);
+                // staged rows accumulate in LDS (written out once, after the
+                // last round), the rest in global memory
+                const int64_t o = v - p0;
+                if (o < X.ns) {
+                    const float prev = accumulate ? dxs[o * d + c] : 0.f;
+                    dxs[o * d + c] = prev + t;
+                } else {
+                    dx[v * d + c] = accumulate ? dx[v * d + c] + t : t;
+                }
+                acc[k] = fmaf(de, X.at(v, c), acc[k]);
             }
         }
     }
@@ -160,9 +221,11 @@ __global__ __launch_bounds__(256) void set2set_fwd_k(
     const float *__restrict__ w_hh, const float *__restrict__ b_hh, float *__restrict__ save,
     float *__restrict__ out) {
     __shared__ float sQ[2 * kS2SMaxD], sH[kS2SMaxD], sC[kS2SMaxD], sA[4 * kS2SMaxD];
+    __shared__ float sX[kS2SRows * kS2SMaxD];
     const int64_t g = blockIdx.x;
     const int tid = threadIdx.x, D2 = 2 * d, G4 = 4 * d, S = s2s_save(d);
     const int64_t p0 = ptr[g], p1 = ptr[g + 1];
+    const S2SRows X{x, sX, p0, s2s_stage(x, p0, p1, d, sX), d};
     if (tid < D2) sQ[tid] = 0.f;
     if (tid < d) sH[tid] = sC[tid] = 0.f;
     // this thread's gate biases (b_ih + b_hh added after the two products, as
@@ -177,11 +240,8 @@ __global__ __launch_bounds__(256) void set2set_fwd_k(
             sv[3 * d + tid] = sC[tid];
         }
         if (tid < G4) {  // gate tid
-            const float *wi = w_ih + static_cast<int64_t>(tid) * D2;
-            const float *wh = w_hh + static_cast<int64_t>(tid) * d;
-            float a = 0.f, b = 0.f;
-            for (int k = 0; k < D2; ++k) a = fmaf(wi[k], sQ[k], a);
-            for (int k = 0; k < d; ++k) b = fmaf(wh[k], sH[k], b);
+            const float a = s2s_dot(w_ih + static_cast<int64_t>(tid) * D2, sQ, D2);
+            const float b = s2s_dot(w_hh + static_cast<int64_t>(tid) * d, sH, d);
             const float z = (a + bi) + (b + bh);
             const int kind = tid / d;  // 0 i, 1 f, 2 g, 3 o
             const float act = kind == 2 ? tanhf(z) : s2s_sigmoid(z);
@@ -198,7 +258,7 @@ __global__ __launch_bounds__(256) void set2set_fwd_k(
             sv[8 * d + tid] = c;
         }
         __syncthreads();
-        if (tid < kWave) s2s_attend_fwd(x, p0, p1, d, sH, sQ + d, sv + 9 * d);
+        if (tid < kWave) s2s_attend_fwd(X, p1, sH, sQ + d, sv + 9 * d);
         __syncthreads();
     }
     if (tid < D2) out[g * D2 + tid] = sQ[tid];
@@ -220,10 +280,12 @@ __global__ __launch_bounds__(256) void set2set_bwd_k(
         return;
     }
     __shared__ float sDQ[2 * kS2SMaxD], sDH[kS2SMaxD], sDC[kS2SMaxD], sDG[4 * kS2SMaxD];
-    __shared__ float sHq[kS2SMaxD], sAtt[kS2SMaxD];
+    __shared__ float sHq[kS2SMaxD], sAtt[kS2SMaxD], sPart[4][3 * kS2SMaxD];
+    __shared__ float sX[kS2SRows * kS2SMaxD], sDX[kS2SRows * kS2SMaxD];
     const int64_t g = blockIdx.x;
     const int tid = threadIdx.x, D2 = 2 * d, G4 = 4 * d, S = s2s_save(d);
     const int64_t p0 = ptr[g], p1 = ptr[g + 1];
+    const S2SRows X{x, sX, p0, s2s_stage(x, p0, p1, d, sX), d};
     if (tid < D2) sDQ[tid] = g_out[g * D2 + tid];
     if (tid < d) sDH[tid] = sDC[tid] = 0.f;  // from round t + 1 (none after the last)
     __syncthreads();
@@ -237,7 +299,7 @@ __global__ __launch_bounds__(256) void set2set_bwd_k(
         }
         __syncthreads();
         if (tid < kWave)
-            s2s_attend_bwd(x, p0, p1, d, sHq, sDQ + d, sv[9 * d], sv[9 * d + 1], dx, t < T - 1,
+            s2s_attend_bwd(X, p1, sHq, sDQ + d, sv[9 * d], sv[9 * d + 1], dx, sDX, t < T - 1,
                            sAtt);
         __syncthreads();
         if (tid < d) {  // the cell: dh_t = d q*_t[:d] + the attention's d query + from round t + 1
@@ -254,18 +316,41 @@ __global__ __launch_bounds__(256) void set2set_bwd_k(
         }
         __syncthreads();
         if (tid < G4) dG[(g * T + t) * G4 + tid] = sDG[tid];
-        // d q*_{t-1} = W_ih^T dG, d h_{t-1} (gates path) = W_hh^T dG
-        float a = 0.f;
-        if (tid < D2)
-            for (int j = 0; j < G4; ++j) a = fmaf(w_ih[static_cast<int64_t>(j) * D2 + tid], sDG[j], a);
-        float b = 0.f;
-        if (tid < d)
-            for (int j = 0; j < G4; ++j) b = fmaf(w_hh[static_cast<int64_t>(j) * d + tid], sDG[j], b);
+        // [d q*_{t-1} | d h_{t-1} (gates path)] = [W_ih | W_hh]^T dG: wave w sums
+        // the gates of its quarter, lane l the outputs l, l + 64, l + 128 < 3d
+        // (coalesced along the weight rows); the quarters combine in fixed order
+        {
+            const int w = tid >> 6, l = tid & 63, D3 = 3 * d;
+            const int j0 = (G4 * w) / 4, j1 = (G4 * (w + 1)) / 4;
+            float acc[3] = {0.f, 0.f, 0.f};
+#pragma unroll 8
+            for (int j = j0; j < j1; ++j) {
+                const float gj = sDG[j];
+#pragma unroll
+                for (int u = 0; u < 3; ++u) {
+                    const int o = l + 64 * u;
+                    if (o < D3) {
+                        const float wv = o < D2 ? w_ih[static_cast<int64_t>(j) * D2 + o]
+                                                : w_hh[static_cast<int64_t>(j) * d + (o - D2)];
+                        acc[u] = fmaf(wv, gj, acc[u]);
+                    }
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < 3; ++u)
+                if (l + 64 * u < D3) sPart[w][l + 64 * u] = acc[u];
+        }
         __syncthreads();
-        if (tid < D2) sDQ[tid] = a;
-        if (tid < d) sDH[tid] = b;
+        if (tid < 3 * d) {
+            const float v = (sPart[0][tid] + sPart[1][tid]) + (sPart[2][tid] + sPart[3][tid]);
+            if (tid < D2)
+                sDQ[tid] = v;
+            else
+                sDH[tid - D2] = v;
+        }
         __syncthreads();
     }
+    for (int i = tid; i < X.ns * d; i += 256) dx[p0 * d + i] = sDX[i];
 }
 
 // dW_ih [4d][2d], dW_hh [4d][d], db_ih = db_hh [4d] (two outputs: two parameters):
@@ -279,15 +364,21 @@ __global__ __launch_bounds__(256) void set2set_wgrad_k(const float *__restrict__
                                                        float *__restrict__ db_hh) {
     const int k = blockIdx.x, j = threadIdx.x, D2 = 2 * d, G4 = 4 * d, S = s2s_save(d);
     if (j >= G4) return;
-    float acc = 0.f;
+    // (four accumulators over r mod 4, combined in fixed order: the loads of
+    // the unrolled rows are in flight together)
+    float a[4] = {0.f, 0.f, 0.f, 0.f};
     if (k == 3 * d) {
-        for (int64_t r = 0; r < R; ++r) acc += dG[r * G4 + j];
+#pragma unroll 8
+        for (int64_t r = 0; r < R; ++r) a[r & 3] += dG[r * G4 + j];
+        const float acc = (a[0] + a[1]) + (a[2] + a[3]);
         db_ih[j] = acc;
         db_hh[j] = acc;
         return;
     }
     // save row r starts with [q*_prev (2d) | h_prev (d)]: column k of both inputs
-    for (int64_t r = 0; r < R; ++r) acc = fmaf(dG[r * G4 + j], save[r * S + k], acc);
+#pragma unroll 8
+    for (int64_t r = 0; r < R; ++r) a[r & 3] = fmaf(dG[r * G4 + j], save[r * S + k], a[r & 3]);
+    const float acc = (a[0] + a[1]) + (a[2] + a[3]);
     if (k < D2)
         dw_ih[static_cast<int64_t>(j) * D2 + k] = acc;
     else

@@ -1040,8 +1040,9 @@ def _interaction_backward(ctx, saved, g_im, g_z1, g_z2, g_kl, g_klmean):
     dev = f.device
     zeros = lambda *shape: torch.zeros(*shape, dtype=torch.float32, device=dev)  # noqa: E731
     g_im = zeros(n, 2 * HIDDEN) if g_im is None else _f32(g_im, "g_im")
-    g_z1 = zeros(B, HIDDEN) if g_z1 is None else _f32(g_z1, "g_z1")
-    g_z2 = zeros(B, HIDDEN) if g_z2 is None else _f32(g_z2, "g_z2")
+    # (no gradient for a readout: the kernel reads NULL as zero, no fill launch)
+    g_z1 = None if g_z1 is None else _f32(g_z1, "g_z1")
+    g_z2 = None if g_z2 is None else _f32(g_z2, "g_z2")
     if g_kl is not None and g_kl.numel() == 0:
         g_kl = None
     if g_kl is not None:
@@ -1074,6 +1075,7 @@ class _Interaction(torch.autograd.Function):
     @staticmethod
     def forward(ctx, f, t, s, u_gate, u_feat, gamma, beta, w2, b2, w_att, b_att, graph, bn,
                 training):
+        ctx.set_materialize_grads(False)  # outputs no loss reads (fine-tune: z1, z2, KL): no fills
         ctx.leaves = (gamma, beta, w2, b2, w_att, b_att)
         ctx.scope = _slab_scope_for(ctx.leaves)
         f = _f32(f, "interaction")
@@ -1098,6 +1100,7 @@ class _InteractionLin(torch.autograd.Function):
     @staticmethod
     def forward(ctx, f, w0, b0, s, u_gate, u_feat, gamma, beta, w2, b2, w_att, b_att, graph, bn,
                 training):
+        ctx.set_materialize_grads(False)  # outputs no loss reads (fine-tune: z1, z2, KL): no fills
         f = _f32(f, "interaction")
         s = _f32(s, "interaction")
         w0, b0 = _f32(w0, "compressor.0.weight"), _f32(b0, "compressor.0.bias")

@@ -7,7 +7,10 @@ rows = list(csv.DictReader(open(sys.argv[1])))
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
 # a step starts with its batch load (pool_copy_k) when the bench loads in-graph,
 # else with its ego-net build
-starts = [i for i, r in enumerate(rows) if "pool_copy_k" in r["Kernel_Name"]]
+# (the largest pool copy: the fine-tune bench also copies its targets in one)
+copies = [(i, int(r["Grid_Size_X"])) for i, r in enumerate(rows) if "pool_copy_k" in r["Kernel_Name"]]
+gmax = max((gsz for _, gsz in copies), default=0)
+starts = [i for i, gsz in copies if gsz == gmax]
 if len(starts) < 3:
     starts = [i for i, r in enumerate(rows) if "egonet_" in r["Kernel_Name"] and ("count_k" in r["Kernel_Name"] or "onepass_k" in r["Kernel_Name"])]
 k = int(sys.argv[2]) if len(sys.argv) > 2 else len(starts) // 2

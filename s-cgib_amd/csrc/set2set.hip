@@ -53,6 +53,29 @@ __device__ __forceinline__ float s2s_max_all(float v) {
 }
 __device__ __forceinline__ float s2s_sigmoid(float v) { return 1.f / (1.f + expf(-v)); }
 
+// <w[0, n), v[0, n)>, w a weight row in global memory, v in LDS: float4 loads
+// when the row is a multiple of 4 floats (it is then 16-B aligned: row j
+// starts at j n), four accumulators, unrolled so the row's loads are in
+// flight together (a latency-bound dot: one thread per gate)
+__device__ __forceinline__ float s2s_dot(const float *__restrict__ w, const float *v, int n) {
+    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+    if ((n & 3) == 0) {
+        const float4 *w4 = reinterpret_cast<const float4 *>(w);
+#pragma unroll 16
+        for (int k = 0; k < n / 4; ++k) {
+            const float4 x = w4[k];
+            a0 = fmaf(x.x, v[4 * k], a0);
+            a1 = fmaf(x.y, v[4 * k + 1], a1);
+            a2 = fmaf(x.z, v[4 * k + 2], a2);
+            a3 = fmaf(x.w, v[4 * k + 3], a3);
+        }
+    } else {
+#pragma unroll 4
+        for (int k = 0; k < n; ++k) a0 = fmaf(w[k], v[k], a0);
+    }
+    return (a0 + a1) + (a2 + a3);
+}
+
 // The graph's rows: the first kS2SRows staged in LDS by the workgroup (every
 // round and pass re-reads them), the rest read from global memory.
 constexpr int kS2SRows = 64;
@@ -199,10 +222,8 @@ __global__ __launch_bounds__(256) void set2set_fwd_k(
     float *__restrict__ out) {
     __shared__ float sQ[2 * kS2SMaxD], sH[kS2SMaxD], sC[kS2SMaxD], sA[4 * kS2SMaxD];
     __shared__ float sX[kS2SRows * kS2SMaxD];
-    __shared__ float sRed[4 * 64 * 65];  // per wave: [gate][lane] partials, rows padded
     const int64_t g = blockIdx.x;
-    const int tid = threadIdx.x, D2 = 2 * d, D3 = 3 * d, G4 = 4 * d, S = s2s_save(d);
-    const int per = (G4 + 3) / 4;  // gates per wave
+    const int tid = threadIdx.x, D2 = 2 * d, G4 = 4 * d, S = s2s_save(d);
     const int64_t p0 = ptr[g], p1 = ptr[g + 1];
     const S2SRows X{x, sX, p0, s2s_stage(x, p0, p1, d, sX), d};
     if (tid < D2) sQ[tid] = 0.f;
@@ -218,44 +239,10 @@ __global__ __launch_bounds__(256) void set2set_fwd_k(
             sv[D2 + tid] = sH[tid];
             sv[3 * d + tid] = sC[tid];
         }
-        {   // gate partials: wave w takes gates [jb, je), lane l the inputs l, l + 64,
-            // l + 128 of [q* | h] (weight rows read coalesced); the partials go
-            // to sRed [gate][lane] and thread j sums gate j's row below
-            const int w = tid >> 6, l = tid & 63, jb = w * per, je = jb + per < G4 ? jb + per : G4;
-            float in[3];
-#pragma unroll
-            for (int u = 0; u < 3; ++u) {
-                const int o = l + 64 * u;
-                in[u] = o < D2 ? sQ[o] : (o < D3 ? sH[o - D2] : 0.f);
-            }
-#pragma unroll 8
-            for (int j = jb; j < je; ++j) {
-                float pj = 0.f;
-#pragma unroll
-                for (int u = 0; u < 3; ++u) {
-                    const int o = l + 64 * u;
-                    if (o < D3) {
-                        const float wv = o < D2 ? w_ih[static_cast<int64_t>(j) * D2 + o]
-                                                : w_hh[static_cast<int64_t>(j) * d + (o - D2)];
-                        pj = fmaf(wv, in[u], pj);
-                    }
-                }
-                sRed[(j - jb) * 65 + w * 64 * 65 + l] = pj;
-            }
-        }
-        __syncthreads();
         if (tid < G4) {  // gate tid
-            const int w = tid / per, jl = tid - w * per;
-            const float *row = sRed + w * 64 * 65 + jl * 65;
-            float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
-#pragma unroll
-            for (int m = 0; m < 64; m += 4) {
-                a0 += row[m];
-                a1 += row[m + 1];
-                a2 += row[m + 2];
-                a3 += row[m + 3];
-            }
-            const float z = ((a0 + a1) + (a2 + a3)) + (bi + bh);
+            const float a = s2s_dot(w_ih + static_cast<int64_t>(tid) * D2, sQ, D2);
+            const float b = s2s_dot(w_hh + static_cast<int64_t>(tid) * d, sH, d);
+            const float z = (a + bi) + (b + bh);
             const int kind = tid / d;  // 0 i, 1 f, 2 g, 3 o
             const float act = kind == 2 ? tanhf(z) : s2s_sigmoid(z);
             sA[tid] = act;
@@ -336,7 +323,7 @@ __global__ __launch_bounds__(256) void set2set_bwd_k(
             const int w = tid >> 6, l = tid & 63, D3 = 3 * d;
             const int j0 = (G4 * w) / 4, j1 = (G4 * (w + 1)) / 4;
             float acc[3] = {0.f, 0.f, 0.f};
-#pragma unroll 16
+#pragma unroll 8
             for (int j = j0; j < j1; ++j) {
                 const float gj = sDG[j];
 #pragma unroll

@@ -11,9 +11,10 @@
 // Every graph's recurrence is independent of the others' (the LSTM runs on
 // the B graph rows, one row each), so one 256-thread workgroup per graph runs
 // the whole recurrence: thread j < 4d owns gate j (its dot products over the
-// 2d + d inputs, held in LDS), wave 0 runs the attention over the graph's rows
-// (lane = 16 q + j: row group q takes rows p0 + q, p0 + q + 4, ...; lane j
-// holds channels j, j + 16, j + 32, j + 48, d <= 64).  This replaces the
+// 2d + d inputs, held in LDS), and all four waves run the attention over the
+// graph's rows (16 row groups of 16 lanes: group G takes rows p0 + G,
+// p0 + G + 16, ...; lane j of a group holds channels j, j + 16, j + 32,
+// j + 48, d <= 64), the first 64 rows staged in LDS.  This replaces the
 // ~13 torch launches per round of the LSTM cell + attention (two GEMMs,
 // eight elementwise ops, the readout, the concatenation) and their backward.
 //
@@ -111,63 +112,76 @@ __device__ __forceinline__ float s2s_logit(const S2SRows &X, int64_t r, int j,
     return s2s_red16(dot);
 }
 
-// wave 0: the attention readout of rows [p0, p1) with query q (LDS, d
-// floats) into r (LDS) and (max, denominator) into st.  The logits are
-// recomputed in each pass (a 16-lane dot per row) rather than kept: a graph
-// may hold any number of rows.
+// All four waves: the attention readout of rows [p0, p1) with query q (LDS,
+// d floats) into r (LDS) and (max, denominator) into st.  Row group G = 4 w +
+// (lane >> 4) of the 16 takes rows p0 + G, p0 + G + 16, ...; the logits are
+// recomputed in the second pass (a 16-lane dot per row) rather than kept: a
+// graph may hold any number of rows.  red: LDS scratch, kS2SRed floats; the
+// waves' partials combine in fixed order.  Call from every thread.
+constexpr int kS2SRed = 8 + 4 * kS2SMaxD;
 __device__ void s2s_attend_fwd(const S2SRows &X, int64_t p1, const float *q, float *r,
-                               float *st) {
+                               float *st, float *red) {
     const int64_t p0 = X.p0;
     const int d = X.d;
-    const int l = threadIdx.x, rq = l >> 4, j = l & 15;
+    const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, j = l & 15;
+    const int G = 4 * w + (l >> 4);
     float qv[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) qv[k] = j + 16 * k < d ? q[j + 16 * k] : 0.f;
     // (a row group's 16 lanes run a row together: the butterflies stay
     // within active lanes whatever the other groups do)
     float mx = -INFINITY;
-    for (int64_t v = p0 + rq; v < p1; v += 4) mx = fmaxf(mx, s2s_logit(X, v, j, qv));
+    for (int64_t v = p0 + G; v < p1; v += 16) mx = fmaxf(mx, s2s_logit(X, v, j, qv));
     mx = s2s_max_all(mx);
-    float den = 0.f;
-    for (int64_t v = p0 + rq; v < p1; v += 4) {
+    if (l == 0) red[w] = mx;
+    __syncthreads();
+    mx = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+    // denominator and the unnormalised readout sum_v exp(e_v - max) x_v in one pass
+    float den = 0.f, acc[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int64_t v = p0 + G; v < p1; v += 16) {
         const float a = expf(s2s_logit(X, v, j, qv) - mx);
         den += j == 0 ? a : 0.f;
-    }
-    den = s2s_red_q(s2s_red16(den));
-    float acc[4] = {0.f, 0.f, 0.f, 0.f};
-    for (int64_t v = p0 + rq; v < p1; v += 4) {
-        const float alpha = expf(s2s_logit(X, v, j, qv) - mx) / den;
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             const int c = j + 16 * k;
-            acc[k] = fmaf(c < d ? X.at(v, c) : 0.f, alpha, acc[k]);
+            acc[k] = fmaf(c < d ? X.at(v, c) : 0.f, a, acc[k]);
         }
     }
+    den = s2s_red_q(s2s_red16(den));
+    if (l == 0) red[4 + w] = den;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-        const float s = s2s_red_q(acc[k]);
+        const float t = s2s_red_q(acc[k]);
         const int c = j + 16 * k;
-        if (rq == 0 && c < d) r[c] = s;
+        if (l < 16 && c < d) red[8 + w * kS2SMaxD + c] = t;
     }
-    if (l == 0) {
+    __syncthreads();
+    const float D = (red[4] + red[5]) + (red[6] + red[7]);
+    if (tid < d) {
+        const float t = (red[8 + tid] + red[8 + kS2SMaxD + tid]) +
+                        (red[8 + 2 * kS2SMaxD + tid] + red[8 + 3 * kS2SMaxD + tid]);
+        r[tid] = D > 0.f ? t / D : 0.f;  // (an empty graph reads out zero)
+    }
+    if (tid == 0) {
         st[0] = mx;
-        st[1] = den;
+        st[1] = D;
     }
 }
 
-// wave 0: the attention backward for d r = gr (LDS) with query q (LDS):
+// All four waves: the attention backward for d r = gr (LDS) with query q (LDS):
 //   dalpha_v = <gr, x_v>;  s = sum alpha dalpha;  de_v = alpha_v (dalpha_v - s)
 //   dx_v (+)= alpha_v gr + de_v q (dxs: the staged rows' LDS accumulator);
-//   dq = sum de_v x_v  (into dq, LDS)
+//   dq = sum de_v x_v  (into dq, LDS).  Row groups and red as s2s_attend_fwd.
 // (not inlined: inlined into set2set_bwd_k, hipcc 7.2 rejects the staged
 // accumulator's LDS read-modify-write, "Operand has incorrect register class")
 __device__ __noinline__ void s2s_attend_bwd(const S2SRows X, int64_t p1, const float *q,
                                              const float *gr, float mx, float den,
                                              float *__restrict__ dx, float *dxs, bool accumulate,
-                                             float *dq) {
+                                             float *dq, float *red) {
     const int64_t p0 = X.p0;
     const int d = X.d;
-    const int l = threadIdx.x, rq = l >> 4, j = l & 15;
+    const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, j = l & 15;
+    const int G = 4 * w + (l >> 4);
     float gv[4], qv[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
@@ -176,14 +190,17 @@ __device__ __noinline__ void s2s_attend_bwd(const S2SRows X, int64_t p1, const f
         qv[k] = c < d ? q[c] : 0.f;
     }
     float s = 0.f;
-    for (int64_t v = p0 + rq; v < p1; v += 4) {
+    for (int64_t v = p0 + G; v < p1; v += 16) {
         const float alpha = expf(s2s_logit(X, v, j, qv) - mx) / den;
         const float da = s2s_logit(X, v, j, gv);
         s += j == 0 ? alpha * da : 0.f;
     }
     s = s2s_red_q(s2s_red16(s));
+    if (l == 0) red[w] = s;
+    __syncthreads();
+    s = (red[0] + red[1]) + (red[2] + red[3]);
     float acc[4] = {0.f, 0.f, 0.f, 0.f};
-    for (int64_t v = p0 + rq; v < p1; v += 4) {
+    for (int64_t v = p0 + G; v < p1; v += 16) {
         const float alpha = expf(s2s_logit(X, v, j, qv) - mx) / den;
         const float de = alpha * (s2s_logit(X, v, j, gv) - s);
 #pragma unroll
@@ -208,8 +225,12 @@ __device__ __noinline__ void s2s_attend_bwd(const S2SRows X, int64_t p1, const f
     for (int k = 0; k < 4; ++k) {
         const float t = s2s_red_q(acc[k]);
         const int c = j + 16 * k;
-        if (rq == 0 && c < d) dq[c] = t;
+        if (l < 16 && c < d) red[8 + w * kS2SMaxD + c] = t;
     }
+    __syncthreads();
+    if (tid < d)
+        dq[tid] = (red[8 + tid] + red[8 + kS2SMaxD + tid]) +
+                  (red[8 + 2 * kS2SMaxD + tid] + red[8 + 3 * kS2SMaxD + tid]);
 }
 
 }  // namespace
@@ -221,7 +242,7 @@ __global__ __launch_bounds__(256) void set2set_fwd_k(
     const float *__restrict__ w_hh, const float *__restrict__ b_hh, float *__restrict__ save,
     float *__restrict__ out) {
     __shared__ float sQ[2 * kS2SMaxD], sH[kS2SMaxD], sC[kS2SMaxD], sA[4 * kS2SMaxD];
-    __shared__ float sX[kS2SRows * kS2SMaxD];
+    __shared__ float sX[kS2SRows * kS2SMaxD], sRedA[kS2SRed];
     const int64_t g = blockIdx.x;
     const int tid = threadIdx.x, D2 = 2 * d, G4 = 4 * d, S = s2s_save(d);
     const int64_t p0 = ptr[g], p1 = ptr[g + 1];
@@ -258,7 +279,7 @@ __global__ __launch_bounds__(256) void set2set_fwd_k(
             sv[8 * d + tid] = c;
         }
         __syncthreads();
-        if (tid < kWave) s2s_attend_fwd(X, p1, sH, sQ + d, sv + 9 * d);
+        s2s_attend_fwd(X, p1, sH, sQ + d, sv + 9 * d, sRedA);
         __syncthreads();
     }
     if (tid < D2) out[g * D2 + tid] = sQ[tid];
@@ -281,7 +302,7 @@ __global__ __launch_bounds__(256) void set2set_bwd_k(
     }
     __shared__ float sDQ[2 * kS2SMaxD], sDH[kS2SMaxD], sDC[kS2SMaxD], sDG[4 * kS2SMaxD];
     __shared__ float sHq[kS2SMaxD], sAtt[kS2SMaxD], sPart[4][3 * kS2SMaxD];
-    __shared__ float sX[kS2SRows * kS2SMaxD], sDX[kS2SRows * kS2SMaxD];
+    __shared__ float sX[kS2SRows * kS2SMaxD], sDX[kS2SRows * kS2SMaxD], sRedA[kS2SRed];
     const int64_t g = blockIdx.x;
     const int tid = threadIdx.x, D2 = 2 * d, G4 = 4 * d, S = s2s_save(d);
     const int64_t p0 = ptr[g], p1 = ptr[g + 1];
@@ -298,9 +319,8 @@ __global__ __launch_bounds__(256) void set2set_bwd_k(
             sHq[tid] = sv[7 * d + tid] * tanhf(c);
         }
         __syncthreads();
-        if (tid < kWave)
-            s2s_attend_bwd(X, p1, sHq, sDQ + d, sv[9 * d], sv[9 * d + 1], dx, sDX, t < T - 1,
-                           sAtt);
+        s2s_attend_bwd(X, p1, sHq, sDQ + d, sv[9 * d], sv[9 * d + 1], dx, sDX, t < T - 1,
+                           sAtt, sRedA);
         __syncthreads();
         if (tid < d) {  // the cell: dh_t = d q*_t[:d] + the attention's d query + from round t + 1
             const float dh = (sDQ[tid] + sAtt[tid]) + sDH[tid];

@@ -252,7 +252,9 @@ __global__ __launch_bounds__(256) void set2set_fwd_k(
     // this thread's gate biases (b_ih + b_hh added after the two products, as
     // F.linear(q, W_ih, b_ih) + F.linear(h, W_hh, b_hh))
     const float bi = tid < G4 ? b_ih[tid] : 0.f, bh = tid < G4 ? b_hh[tid] : 0.f;
+    SCGIB_MARK(0);
     __syncthreads();
+    SCGIB_MARK(1);
     for (int t = 0; t < T; ++t) {
         float *sv = save + (g * T + t) * S;
         if (tid < D2) sv[tid] = sQ[tid];
@@ -270,6 +272,7 @@ __global__ __launch_bounds__(256) void set2set_fwd_k(
             sv[4 * d + tid] = act;
         }
         __syncthreads();
+        if (t == 0) SCGIB_MARK(2);
         if (tid < d) {
             const float c = sA[d + tid] * sC[tid] + sA[tid] * sA[2 * d + tid];
             const float h = sA[3 * d + tid] * tanhf(c);
@@ -279,9 +282,12 @@ __global__ __launch_bounds__(256) void set2set_fwd_k(
             sv[8 * d + tid] = c;
         }
         __syncthreads();
+        if (t == 0) SCGIB_MARK(3);
         s2s_attend_fwd(X, p1, sH, sQ + d, sv + 9 * d, sRedA);
         __syncthreads();
+        if (t == 0) SCGIB_MARK(4);
     }
+    SCGIB_MARK(5);
     if (tid < D2) out[g * D2 + tid] = sQ[tid];
 }
 
@@ -309,8 +315,12 @@ __global__ __launch_bounds__(256) void set2set_bwd_k(
     const S2SRows X{x, sX, p0, s2s_stage(x, p0, p1, d, sX), d};
     if (tid < D2) sDQ[tid] = g_out[g * D2 + tid];
     if (tid < d) sDH[tid] = sDC[tid] = 0.f;  // from round t + 1 (none after the last)
+    SCGIB_MARK(0);
     __syncthreads();
+    SCGIB_MARK(1);
     for (int t = T - 1; t >= 0; --t) {
+        const int mk = t == T - 1 ? 2 : 7;  // (trace build: the first two rounds' phases)
+        (void)mk;
         const float *sv = save + (g * T + t) * S;
         // h_t (the round's query) = q*_t's first half: the next round's q*_prev,
         // or recomputed for the last round from its saved act / c
@@ -319,9 +329,11 @@ __global__ __launch_bounds__(256) void set2set_bwd_k(
             sHq[tid] = sv[7 * d + tid] * tanhf(c);
         }
         __syncthreads();
+        if (t >= T - 2) SCGIB_MARK(mk);
         s2s_attend_bwd(X, p1, sHq, sDQ + d, sv[9 * d], sv[9 * d + 1], dx, sDX, t < T - 1,
                            sAtt, sRedA);
         __syncthreads();
+        if (t >= T - 2) SCGIB_MARK(mk + 1);
         if (tid < d) {  // the cell: dh_t = d q*_t[:d] + the attention's d query + from round t + 1
             const float dh = (sDQ[tid] + sAtt[tid]) + sDH[tid];
             const float ig = sv[4 * d + tid], fg = sv[5 * d + tid], gg = sv[6 * d + tid],
@@ -335,6 +347,7 @@ __global__ __launch_bounds__(256) void set2set_bwd_k(
             sDC[tid] = dc * fg;                               // -> c_{t-1}
         }
         __syncthreads();
+        if (t >= T - 2) SCGIB_MARK(mk + 2);
         if (tid < G4) dG[(g * T + t) * G4 + tid] = sDG[tid];
         // [d q*_{t-1} | d h_{t-1} (gates path)] = [W_ih | W_hh]^T dG: wave w sums
         // the gates of its quarter, lane l the outputs l, l + 64, l + 128 < 3d
@@ -342,18 +355,33 @@ __global__ __launch_bounds__(256) void set2set_bwd_k(
         {
             const int w = tid >> 6, l = tid & 63, D3 = 3 * d;
             const int j0 = (G4 * w) / 4, j1 = (G4 * (w + 1)) / 4;
-            float acc[3] = {0.f, 0.f, 0.f};
-#pragma unroll 8
-            for (int j = j0; j < j1; ++j) {
-                const float gj = sDG[j];
+            // per output slot u: its weight column (base, row stride), chosen
+            // once, so the loads below are unconditional and the unrolled
+            // rows' loads go out together (a branch per load made hipcc wait
+            // for each one: 21 us of a round, tools/s2s_trace.py)
+            const float *col[3];
+            int64_t rs[3];
 #pragma unroll
-                for (int u = 0; u < 3; ++u) {
-                    const int o = l + 64 * u;
-                    if (o < D3) {
-                        const float wv = o < D2 ? w_ih[static_cast<int64_t>(j) * D2 + o]
-                                                : w_hh[static_cast<int64_t>(j) * d + (o - D2)];
-                        acc[u] = fmaf(wv, gj, acc[u]);
-                    }
+            for (int u = 0; u < 3; ++u) {
+                const int o = l + 64 * u;
+                col[u] = o < D2 ? w_ih + o : (o < D3 ? w_hh + (o - D2) : w_ih);
+                rs[u] = o < D2 ? D2 : (o < D3 ? d : 0);
+            }
+            float acc[3] = {0.f, 0.f, 0.f};
+            constexpr int kB = 16;  // rows per batch: 3 kB loads issued before their uses
+            for (int jb = j0; jb < j1; jb += kB) {
+                float wv[kB][3];
+#pragma unroll
+                for (int i = 0; i < kB; ++i) {
+                    const int jc = jb + i < j1 ? jb + i : j1 - 1;  // (clamped: no branch)
+#pragma unroll
+                    for (int u = 0; u < 3; ++u) wv[i][u] = col[u][jc * rs[u]];
+                }
+#pragma unroll
+                for (int i = 0; i < kB; ++i) {
+                    const float gj = jb + i < j1 ? sDG[jb + i] : 0.f;
+#pragma unroll
+                    for (int u = 0; u < 3; ++u) acc[u] = fmaf(wv[i][u], gj, acc[u]);
                 }
             }
 #pragma unroll
@@ -361,6 +389,7 @@ __global__ __launch_bounds__(256) void set2set_bwd_k(
                 if (l + 64 * u < D3) sPart[w][l + 64 * u] = acc[u];
         }
         __syncthreads();
+        if (t >= T - 2) SCGIB_MARK(mk + 3);
         if (tid < 3 * d) {
             const float v = (sPart[0][tid] + sPart[1][tid]) + (sPart[2][tid] + sPart[3][tid]);
             if (tid < D2)
@@ -370,7 +399,9 @@ __global__ __launch_bounds__(256) void set2set_bwd_k(
         }
         __syncthreads();
     }
+    SCGIB_MARK(12);
     for (int i = tid; i < X.ns * d; i += 256) dx[p0 * d + i] = sDX[i];
+    SCGIB_MARK(13);
 }
 
 // dW_ih [4d][2d], dW_hh [4d][d], db_ih = db_hh [4d] (two outputs: two parameters):
@@ -449,3 +480,10 @@ extern "C" int scgib_set2set_bwd(const float *x, const int32_t *graph_ptr, int64
         save, dgates, n_graphs * n_iters, dim, dw_ih, dw_hh, db_ih, db_hh);
     return launch_status();
 }
+
+#ifdef SCGIB_TRACE
+// debug build only: this file's own g_trace (see common.h; scgib_trace_set)
+extern "C" int scgib_trace_set_set2set(void *buf) {
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_trace), &buf, sizeof(buf)) == hipSuccess ? 0 : 1;
+}
+#endif

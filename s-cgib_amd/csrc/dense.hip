@@ -97,17 +97,25 @@ __global__ __launch_bounds__(256) void linear_bwd_k(
             a[0] = va[k].x; a[1] = va[k].y; a[2] = va[k].z; a[3] = va[k].w;
         }
         __syncthreads();
+        const int ccol = wc * 32 + (l & 31);
+        // the addend rows, loaded unconditionally (clamped rows) ahead of the
+        // products: behind the store's row predicate each load was waited for
+        // on its own
+        float addv[16];
+        if (add) {
+#pragma unroll
+            for (int reg = 0; reg < 16; ++reg) {
+                const int row = wr * 32 + acc_row(reg, l);
+                addv[reg] = add[(row0 + (row < nv ? row : nv - 1)) * 64 + ccol];
+            }
+        }
         accW = mma_tn<TM>(sD + wr * 32, LDH, sA + wc * 32, LDH, accW);
         db = col_sum16(db, sD + q * LDH + ch, 4 * LDH);
         f32x16 g = mma_nn<64>(sD + wr * 32 * LDH, LDH, sW + wc * 32, LDH, zero16());
-        const int ccol = wc * 32 + (l & 31);
 #pragma unroll
         for (int reg = 0; reg < 16; ++reg) {
             const int row = wr * 32 + acc_row(reg, l);
-            if (row < nv) {
-                const int64_t o = (row0 + row) * 64 + ccol;
-                dx[o] = add ? add[o] + g[reg] : g[reg];
-            }
+            if (row < nv) dx[(row0 + row) * 64 + ccol] = add ? addv[reg] + g[reg] : g[reg];
         }
     }
     float *sl = slab + static_cast<int64_t>(blockIdx.x) * kLinSlab;

@@ -290,21 +290,6 @@ int scgib_set2set_bwd(const float *x, const int32_t *graph_ptr, int64_t n_graphs
                       float *dw_ih, float *dw_hh, float *db_ih, float *db_hh,
                       scgib_stream_t stream);
 
-/* ---- (f)1: the fine-tune prediction head (models.py:386-396, :515-520) ----
- * out [n_rows][n_out] = [sigmoid](relu(x W1^T + b1) W2^T + b2) for x
- * [n_rows][d_in] (d_in <= 128, d_hidden <= 64, n_out <= 64): one workgroup;
- * hidden [n_rows][d_hidden] (the ReLU output) is saved for the backward.
- * Backward: g_out -> dx, dw1 [d_hidden][d_in], db1, dw2 [n_out][d_hidden], db2,
- * sums in fixed order.  No host sync: graph-capturable. */
-int scgib_predict_fwd(const float *x, int64_t n_rows, int32_t d_in, const float *w1,
-                      const float *b1, int32_t d_hidden, const float *w2, const float *b2,
-                      int32_t n_out, int32_t sigmoid, float *hidden, float *out,
-                      scgib_stream_t stream);
-int scgib_predict_bwd(const float *x, int64_t n_rows, int32_t d_in, const float *w1,
-                      int32_t d_hidden, const float *w2, int32_t n_out, int32_t sigmoid,
-                      const float *hidden, const float *out, const float *g_out, float *dx,
-                      float *dw1, float *db1, float *dw2, float *db2, scgib_stream_t stream);
-
 /* ---- A6: per-segment readouts (dgl.sum_nodes) -------------------------------
  * out[s,:] = sum_{i in [ptr[s], ptr[s+1])} x[i,:]   (models.py:716, 725, 733)
  * segment_broadcast is its adjoint: out[i,:] = g[s,:] for every row i of s.

@@ -20,10 +20,6 @@ SIGNATURES = {
     "scgib_abi_version": (ctypes.c_int, []),
     "scgib_set_recon_fold": (ctypes.c_int, [ctypes.c_int]),
     "scgib_set2set_save_floats": (_I64, [_I64, _I32, _I32]),
-    "scgib_predict_fwd": (ctypes.c_int, [_P, _I64, _I32, _P, _P, _I32, _P, _P, _I32, _I32, _P, _P,
-                                         _P]),
-    "scgib_predict_bwd": (ctypes.c_int, [_P, _I64, _I32, _P, _I32, _P, _I32, _I32, _P, _P, _P, _P,
-                                         _P, _P, _P, _P, _P]),
     "scgib_set2set_fwd": (ctypes.c_int, [_P, _P, _I64, _I32, _I32, _P, _P, _P, _P, _P, _P, _P]),
     "scgib_set2set_bwd": (ctypes.c_int, [_P, _P, _I64, _I32, _I32, _P, _P, _P, _P, _P, _I64, _P,
                                          _P, _P, _P, _P, _P]),
@@ -174,7 +170,7 @@ class RunningUpdate(ctypes.Structure):
                 ("num_batches_tracked", ctypes.c_void_p)]
 
 
-ABI_VERSION = 16
+ABI_VERSION = 15
 STATS_STRIDE = 260
 PGRAD_STRIDE = 324
 HIDDEN = 64

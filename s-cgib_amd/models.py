@@ -697,10 +697,11 @@ class Mainmodel_finetuning(nn.Module):
                                         device, noise)[0]
         im = ops.mlp2(im, self.MLP, batch_g.dims)
         im = self.s2s(batch_g, im)
-        # predict [+ sigmoid] (models.py:516-520) as one device op
-        scores = ops.predict_head(im, self.predict, self.dataset not in self.tasks)
+        scores = self.predict(im)
         ops.join_aside()
-        return scores, 0, 0, 0
+        if self.dataset in self.tasks:
+            return scores, 0, 0, 0
+        return torch.sigmoid(scores), 0, 0, 0
 
     def _prepare_ego(self, batch_g, batch_x, x_subs):
         k = getattr(self.model, "k_transition", self.k_transition)

@@ -956,52 +956,6 @@ class _Set2Set(torch.autograd.Function):
         return dx, dw_ih, db_ih, dw_hh, db_hh, None, None, None
 
 
-class _PredictHead(torch.autograd.Function):
-    @staticmethod
-    def forward(ctx, x, w1, b1, w2, b2, sigmoid):
-        x = _f32(x, "predict x")
-        w1, b1 = _f32(w1, "predict.0.weight"), _f32(b1, "predict.0.bias")
-        w2, b2 = _f32(w2, "predict.2.weight"), _f32(b2, "predict.2.bias")
-        B, din = x.shape
-        dh, C = w1.shape[0], w2.shape[0]
-        if tuple(w1.shape) != (dh, din) or tuple(w2.shape) != (C, dh) or din > 128 or dh > 64 \
-                or C > 64:
-            raise _lib.ScgibError(f"predict head: x {tuple(x.shape)}, W1 {tuple(w1.shape)}, "
-                                  f"W2 {tuple(w2.shape)} (d_in <= 128, hidden <= 64, out <= 64)")
-        hid = torch.empty(B, dh, dtype=torch.float32, device=x.device)
-        out = torch.empty(B, C, dtype=torch.float32, device=x.device)
-        _lib.call("scgib_predict_fwd", _p(x), B, din, _p(w1), _p(b1), dh, _p(w2), _p(b2), C,
-                  int(sigmoid), _p(hid), _p(out), _stream())
-        ctx.save_for_backward(x, w1, w2, hid, out)
-        ctx.sigmoid = bool(sigmoid)
-        return out
-
-    @staticmethod
-    def backward(ctx, g):
-        x, w1, w2, hid, out = ctx.saved_tensors
-        g = _f32(g, "predict.backward")
-        B, din = x.shape
-        dh, C = w1.shape[0], w2.shape[0]
-        dx, dw1, dw2 = torch.empty_like(x), torch.empty_like(w1), torch.empty_like(w2)
-        db1 = torch.empty(dh, dtype=torch.float32, device=x.device)
-        db2 = torch.empty(C, dtype=torch.float32, device=x.device)
-        _lib.call("scgib_predict_bwd", _p(x), B, din, _p(w1), dh, _p(w2), C, int(ctx.sigmoid),
-                  _p(hid), _p(out), _p(g), _p(dx), _p(dw1), _p(db1), _p(dw2), _p(db2),
-                  _stream())
-        return dx, dw1, db1, dw2, db2, None
-
-
-def predict_head(x, predict, sigmoid):
-    """The fine-tune head ``predict`` = Sequential(Linear, ReLU, Linear)
-    (models.py:386-396) [+ sigmoid, :520] on the device, one launch per
-    direction (csrc/head.hip)."""
-    lin1, act, lin2 = predict
-    if not (isinstance(lin1, torch.nn.Linear) and isinstance(act, torch.nn.ReLU)
-            and isinstance(lin2, torch.nn.Linear)):
-        raise _lib.ScgibError("predict_head: expects Sequential(Linear, ReLU, Linear)")
-    return _PredictHead.apply(x, lin1.weight, lin1.bias, lin2.weight, lin2.bias, bool(sigmoid))
-
-
 def set2set(x, graph, lstm, n_iters):
     """DGL Set2Set(d, n_iters, 1) (models.py:565) on the device: the LSTM
     recurrence and the per-graph softmax attention readouts of all n_iters

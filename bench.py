@@ -616,6 +616,11 @@ def main():
     # (more ranks than devices only in local gloo rehearsals: ranks share GPUs)
     dev = torch.device("cuda", local % max(torch.cuda.device_count(), 1))
     torch.cuda.set_device(dev)
+    if world > torch.cuda.device_count():
+        # processes sharing a GPU are time-sliced, so one process's two queues
+        # are not guaranteed to run concurrently: the encoder pair's signal /
+        # wait hand-offs (which need that) become ordinary stream edges
+        pkg.ops.XQ_FLAGS = False
     torch.manual_seed(1234 + rank)
     global RUN_CONFIG
     RUN_CONFIG = {"workload": a.workload, "batch": a.batch, "k": a.k}

@@ -488,7 +488,15 @@ __device__ __forceinline__ void gather_x_rows(const PreArgs &pre, const int32_t 
         vrow[k] = row0 + (rr < nv ? rr : nv - 1);
         beg[k] = rowptr[vrow[k]];
         deg[k] = rowptr[vrow[k] + 1];
-        sid[k] = pre.nmap ? static_cast<int64_t>(pre.nmap[vrow[k]]) : vrow[k];
+    }
+    // (the uniform branch outside the rows: as a per-row select, each
+    // node-map load sat in its own branch and was waited for alone)
+    if (pre.nmap) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) sid[k] = pre.nmap[vrow[k]];
+    } else {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) sid[k] = vrow[k];
     }
     float self[4];
 #pragma unroll

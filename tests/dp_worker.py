@@ -57,6 +57,9 @@ def main(out_dir):
     rank, world, local = pkg.dist.init_from_env()
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
+    # both ranks share one GPU (time-sliced processes): no signal / wait
+    # hand-offs between one process's queues (as bench.py does in that case)
+    pkg.ops.XQ_FLAGS = False
     F_in = pkg.synth.WORKLOADS[WORKLOAD][2]
     B = B_TOTAL // world
     gh, u_gate, u_feat = shard_and_noise(pkg, rank, world)

@@ -126,26 +126,28 @@ def agg_fwd_bytes(n, e, d_in):
     return agg_bytes(n, e, d_in)
 
 
-def layer_fwd_bytes_inclusive(n, e, d_in):
+def layer_fwd_bytes_inclusive(n, e, d_in, store_r=False):
     """Everything one gin_fwd_k launch moves: the gather (neighbour + self
-    rows, col + rowptr), W1/b1/W2/b2, the agg / r / z2 writes and the per-tile
-    BN statistics (reported beside the §8(d) figure as frac_inclusive)."""
+    rows, col + rowptr), W1/b1/W2/b2, the agg / z2 writes (+ r's when the
+    forward stores it, ops.STORE_R) and the per-tile BN statistics (reported
+    beside the §8(d) figure as frac_inclusive)."""
     return (4 * d_in * (e + n) + 4 * e + 4 * (n + 1)
             + 4 * (64 * d_in + 64 + 64 * 64 + 64)
-            + 4 * n * (d_in + 64 + 64) + 512 * ((n + 63) // 64))
+            + 4 * n * (d_in + 64 + (64 if store_r else 0)) + 512 * ((n + 63) // 64))
 
 
 def layer_fwd_flops(n, e, d_in):
     return 2 * n * 64 * (d_in + 64)
 
 
-def layer_bwd_bytes(n, e, d_in):
-    """Algorithmic bytes of one GIN layer backward launch (gin_bwd5_k, DESIGN.md
-    §4): the dy, z2, r and agg rows read, W1/W2 + BN coefficients, d(agg)
-    written.  The per-workgroup dW slabs are NOT counted: they are partials of
-    a 33 KB gradient, not bytes the layer needs (their cost shows in
-    `traffic`)."""
-    return 4 * n * (3 * 64 + d_in) + 4 * (64 * d_in + 64 * 64 + 6 * 64) + 4 * n * d_in
+def layer_bwd_bytes(n, e, d_in, store_r=False):
+    """Algorithmic bytes of one GIN layer backward launch (gin_bwd5r_k /
+    gin_bwd5_k): the dy, z2 and agg rows read (+ r's when the
+    forward stored it), W1/b1/W2 + BN coefficients, d(agg) written.  The
+    per-workgroup dW slabs are NOT counted: they are partials of a 33 KB
+    gradient, not bytes the layer needs (their cost shows in `traffic`)."""
+    return (4 * n * ((3 if store_r else 2) * 64 + d_in) + 4 * (64 * d_in + 64 * 64 + 7 * 64)
+            + 4 * n * d_in)
 
 
 def stats_bytes(n, e, d):
@@ -165,7 +167,9 @@ def layer_bwd_flops(n, e, d_in):
 
 
 def _call_meta(fn, m):
-    """bytes / flops of one launch from its meta (n, e, d_in)."""
+    """bytes / flops of one launch from its meta (n, e, d_in[, r stored])."""
+    if fn in (layer_fwd_bytes_inclusive, layer_bwd_bytes):
+        return fn(m["n"], m["e"], m["d_in"], m.get("r", False))
     return fn(m["n"], m["e"], m["d_in"])
 
 
@@ -180,9 +184,11 @@ KERNELS = {
                       desc="fused GIN layer forward: gather (+ previous BN + ReLU on load) + "
                            "2 f32-MFMA GEMMs + BN tile statistics"),
     "gin_bwd5_k": dict(entries=("scgib_gin_layer_bwd",), keep=lambda m: m["d_in"] == 64,
-                       bytes=layer_bwd_bytes, flops=layer_bwd_flops, pmc=["gin_bwd5_k<64>"],
+                       bytes=layer_bwd_bytes, flops=layer_bwd_flops,
+                       pmc=["gin_bwd5r_k<64>", "gin_bwd5_k<64>"],
                        desc="fused GIN layer backward (d_in = 64): BN-backward apply + 4 "
-                            "f32-MFMA GEMMs on 32-row sub-tiles"),
+                            "f32-MFMA GEMMs on 32-row sub-tiles (gin_bwd5r_k: + the hidden "
+                            "activation r recomputed, not read; flops count the 4 GEMMs)"),
     "gin_bwd_stats_k": dict(entries=("scgib_gin_bwd_stats_bn_fold", "scgib_gin_bwd_stats_seg_bn",
                                      "scgib_gin_bwd_stats_bn"),
                             keep=lambda m: True, bytes=stats_bytes, flops=no_flops,
@@ -351,7 +357,7 @@ def superbatch_roofline(dev, n_target=1_200_000, reps=20):
     torch.cuda.synchronize()
     # gin_fwd_k over its d = 64 layers: frac on §8(d)'s aggregation bytes;
     # frac_inclusive counts everything the launch moves (its own saved
-    # agg / r / z2 writes and the weights too); mfma_frac on its two GEMMs
+    # agg / z2 (and r, if stored) writes and the weights too); mfma_frac on its two GEMMs
     fwd = [rec for rec in fwd if rec[2]["d_in"] == 64]
     for key, recs, fn in (("gin_fwd_k", fwd, agg_fwd_bytes), ("gin_bwd_stats_k", st, stats_bytes)):
         if recs:
@@ -360,7 +366,8 @@ def superbatch_roofline(dev, n_target=1_200_000, reps=20):
             res[key] = _frac_entry(fn(m["n"], m["e"], m["d_in"]), ms_k)
             res[key]["launches"] = len(recs)
             if key == "gin_fwd_k":
-                inc = layer_fwd_bytes_inclusive(m["n"], m["e"], m["d_in"])
+                inc = layer_fwd_bytes_inclusive(m["n"], m["e"], m["d_in"], m.get("r", False))
+                res[key]["stores_r"] = bool(m.get("r", False))
                 res[key]["bytes_inclusive"] = int(inc)
                 res[key]["frac_inclusive"] = round(inc / (ms_k * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
                 fl = layer_fwd_flops(m["n"], m["e"], m["d_in"])
@@ -373,7 +380,8 @@ def superbatch_roofline(dev, n_target=1_200_000, reps=20):
         ms_k = statistics.mean(a.elapsed_time(b) / KernelTimer.REPEAT for a, b, _ in bw)
         m = bw[0][2]
         fl = layer_bwd_flops(m["n"], m["e"], m["d_in"])
-        ent = _frac_entry(layer_bwd_bytes(m["n"], m["e"], m["d_in"]), ms_k)
+        ent = _frac_entry(layer_bwd_bytes(m["n"], m["e"], m["d_in"], m.get("r", False)), ms_k)
+        ent["recomputes_r"] = not m.get("r", False)
         ent["tflops"] = round(fl / (ms_k * 1e-3) / 1e12, 2)
         ent["mfma_frac"] = round(fl / (ms_k * 1e-3) / 1e12 / F32_MFMA_PEAK_TFLOPS, 4)
         ent["launches"] = len(bw)
@@ -590,10 +598,14 @@ def main():
                          "batch ahead (graph.EgoPrefetch; A/B)")
     ap.add_argument("--torch-adam", action="store_true",
                     help="torch's fused Adam instead of the one-launch scgib Adam")
+    ap.add_argument("--recompute-r", action="store_true",
+                    help="the GIN forward does not store r, the backward recomputes it "
+                         "(ops.STORE_R = False; A/B, same bits: profiles/r05_recompute)")
     ap.add_argument("--finetune", choices=["molhiv"], default=None,
                     help="time the fine-tune step of BASELINE.json configs[4] instead "
                          "(finetune_bench.py; --batch defaults to 32 there)")
     a = ap.parse_args()
+    pkg.ops.STORE_R = not a.recompute_r
     if a.finetune:
         import finetune_bench
         dev = torch.device("cuda", 0)
@@ -616,11 +628,14 @@ def main():
     # (more ranks than devices only in local gloo rehearsals: ranks share GPUs)
     dev = torch.device("cuda", local % max(torch.cuda.device_count(), 1))
     torch.cuda.set_device(dev)
-    if world > torch.cuda.device_count():
-        # processes sharing a GPU are time-sliced, so one process's two queues
-        # are not guaranteed to run concurrently: the encoder pair's signal /
-        # wait hand-offs (which need that) become ordinary stream edges
-        pkg.ops.XQ_FLAGS = False
+    # the encoder pair's signal / wait hand-offs need one process's two
+    # queues to run concurrently (ops.handoff_rule: e.g. ranks sharing a GPU
+    # are time-sliced processes); where the rule refuses, ordinary stream edges
+    xq_env = dict(os.environ)
+    xq_env.setdefault("LOCAL_WORLD_SIZE", str(world))
+    xq_ok, xq_why = pkg.ops.handoff_rule(torch.cuda.device_count(), xq_env)
+    if not xq_ok:
+        pkg.ops.XQ_FLAGS, pkg.ops.XQ_REASON = False, xq_why
     torch.manual_seed(1234 + rank)
     global RUN_CONFIG
     RUN_CONFIG = {"workload": a.workload, "batch": a.batch, "k": a.k}
@@ -788,6 +803,7 @@ def main():
     xq_to = pkg.ops.xq_timeouts(dev)
     if xq_to:  # a hand-off wait gave up: its queue ran ahead of the data
         raise SystemExit(f"bench: {xq_to} cross-queue hand-off waits timed out (ops.XQ_FLAGS)")
+    pkg.ops.check_handoff(dev)
     replica_diff = None
     if world > 1:
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
@@ -867,6 +883,8 @@ def main():
                                      and not a.no_ego_prefetch else "at the head of the step"),
                        "allreduce": None if not collective else
                        ("eager" if a.eager else allreduce_mode),
+                       "handoffs": ("signal / wait kernels" if pkg.ops.XQ_FLAGS else
+                                    f"stream edges ({pkg.ops.XQ_REASON})"),
                        "global_batch": world * a.batch, "nodes_per_batch": round(n_nodes, 1),
                        "parallelism": f"dp{world}", "final_loss": round(final_loss, 4),
                        "replica_max_abs_diff": replica_diff,
@@ -888,7 +906,8 @@ def main():
                      "the on-path gather kernels gin_fwd_k and gin_bwd_stats_k; "
                      "gin_aggregate_k is a reference kernel, not in the step); gin_fwd_k frac "
                      "on §8(d) aggregation bytes, frac_inclusive on everything the launch moves "
-                     "(its saved agg / r / z2 writes too); gin_bwd5_k at this scale (~146 "
+                     "(its saved agg / z2 writes too; r is recomputed by the backward, "
+                     "stores_r); gin_bwd5_k (gin_bwd5r_k) at this scale (~146 "
                      "sub-tiles per workgroup, its start-of-kernel chain amortised), mfma_frac "
                      "= flops / time / 157.3 TF/s"),
             "cpu_baseline": cpu,

@@ -176,6 +176,7 @@ def run(bench, a, dev):
     elapsed = time.perf_counter() - t0
     if pkg.ops.xq_timeouts(dev) or pkg.ops.handoff_fault(dev):
         raise SystemExit("bench: a cross-queue hand-off wait timed out (ops.XQ_FLAGS)")
+    pkg.ops.check_handoff(dev)
     final_loss = float(static_loss.item())
     # kernel timer: eager fine-tune steps on one stream, HIP events per launch
     kernels = {}

@@ -75,9 +75,15 @@ int scgib_abi_version(void);
  * producer's data.  Calls must pair up in order (n-th wait <-> n-th signal).
  * A wait that sees no signal for 0.2 s gives up, counts words[2] and sets the
  * sticky *fault word (fault may be NULL): the step's loss kernels
- * (scgib_mlp2_recon_fwd / _contrastive_fwd, given the same word) then report
- * a NaN loss until the caller clears it, since some kernel of that step read
- * data before it was written. */
+ * (scgib_mlp2_recon_fwd / _contrastive_fwd, given the same word) then
+ * report a NaN loss until the caller clears it, since some kernel of that
+ * step read data before it was written.  It also sets *host_fault (may be
+ * NULL): a host-visible pinned word the host reads without a sync (the
+ * Python mirror raises on it at the next model forward / optimizer step,
+ * ops.check_handoff — the fine-tune and domain-adaptation heads' losses are
+ * torch ops, and NaN scores would trip binary_cross_entropy's range assert).
+ * Correctness needs the signal and the wait on queues the device runs
+ * concurrently ("Cross-queue hand-offs"). */
 /* The next batch of a resident pool into a static input buffer, for a
  * replayed step graph: srcs = device table of n_src device pointers (each
  * `bytes` long, bytes a multiple of 16); copies srcs[ctr[0] % n_src] to dst
@@ -90,7 +96,8 @@ int scgib_pool_copy(const uint64_t *srcs, int32_t n_src, uint32_t *ctr, void *ds
 int scgib_pool_copy2(const uint64_t *srcs, int32_t n_src, uint32_t *ctr, void *dst, int64_t bytes,
                      const void *src2, void *dst2, int64_t bytes2, scgib_stream_t stream);
 int scgib_stream_signal(uint32_t *words, scgib_stream_t stream);
-int scgib_stream_wait(uint32_t *words, uint32_t *fault, scgib_stream_t stream);
+int scgib_stream_wait(uint32_t *words, uint32_t *fault, uint32_t *host_fault,
+                      scgib_stream_t stream);
 const char *scgib_strerror(int code);
 
 /* ---- A5: GIN neighbourhood aggregation (DGL GINConv, sum aggregator) ------
@@ -114,7 +121,9 @@ int scgib_gin_aggregate(const float *h, const int32_t *rowptr, const int32_t *co
  *   x = relu(in_stat.scale * h_in + in_stat.shift) when in_stat != NULL
  *   (the previous layer's BN+ReLU applied on load; d_in must be 64);
  *   r = relu(agg W1^T + b1); z2 = r W2^T + b2; per-tile (sum, centred M2).
- *   d_in in {32, 64}; hidden 64.  Outputs agg [n,d_in], r, z2 [n,64].
+ *   d_in in {32, 64}; hidden 64.  Outputs agg [n,d_in], r, z2 [n,64];
+ *   r may be NULL (also in scgib_gin_layer_fwd_bn / scgib_gin_layer0_fwd): it
+ *   is then not stored and the backward recomputes it (below).
  * scgib_bn_finalize: training: batch mean/var from the tile stats (fp64
  *   Chan combine), running stats updated (momentum, unbiased var,
  *   num_batches_tracked += 1); eval: running stats.  Writes `stat`.
@@ -131,6 +140,14 @@ int scgib_gin_aggregate(const float *h, const int32_t *rowptr, const int32_t *co
  *   total; d_in = 64: 32-row sub-tiles, up to two workgroups per CU each
  *   walking its sub-tiles), reduced in a fixed order.  With wgrad NULL the slabs are left for the
  *   caller's scgib_slab_reduce (so the GEMM kernel can be timed alone).
+ *   r NULL (d_in = 64, and scgib_gin_layer0_bwd): the forward did not store r
+ *   (a third of the forward's HBM writes); the kernel
+ *   recomputes r = relu(agg W1^T + b1) from the saved agg with the forward's
+ *   own MFMA chain — bitwise the r it would have stored, so every output is
+ *   bitwise the stored-r kernel's.  b1 is read only then (may be NULL with r).
+ * scgib_gin_hidden: r = relu(agg W1^T + b1) [n,64] with that same chain
+ *   (inspection / tests: the hidden ReLU decisions of a step that did not
+ *   store r).
  * scgib_slab_reduce: out[w] = sum_s slab[s*width + w], fixed order. */
 int64_t scgib_gin_tiles(int64_t n_nodes);
 int64_t scgib_gin_slab_floats(int64_t n_nodes, int32_t d_in);
@@ -259,14 +276,16 @@ int scgib_gin_bwd_stats_bn_fold(const float *dh, const int32_t *rowptr_t, const 
  * scgib_gin_bwd_stats_bn of the same layer (coef may then be NULL). */
 int scgib_gin_layer0_bwd(const float *dy, const float *z2, const float *r, const float *agg,
                          const float *aggx, int32_t n_feat, const float *stat,
-                         const float *coef, const float *w1, const float *w2, int64_t n_nodes,
-                         float *slab, const int32_t *dims, const scgib_bn_bwd_pending *pending,
-                         scgib_stream_t stream);
+                         const float *coef, const float *w1, const float *b1, const float *w2,
+                         int64_t n_nodes, float *slab, const int32_t *dims,
+                         const scgib_bn_bwd_pending *pending, scgib_stream_t stream);
 int scgib_gin_layer_bwd(const float *dy, const float *z2, const float *r, const float *agg,
                         int32_t d_in, const float *stat, const float *coef, const float *w1,
-                        const float *w2, int64_t n_nodes, float *dagg, float *slab,
-                        float *wgrad, const int32_t *dims, const scgib_bn_bwd_pending *pending,
-                        scgib_stream_t stream);
+                        const float *b1, const float *w2, int64_t n_nodes, float *dagg,
+                        float *slab, float *wgrad, const int32_t *dims,
+                        const scgib_bn_bwd_pending *pending, scgib_stream_t stream);
+int scgib_gin_hidden(const float *agg, int32_t d_in, const float *w1, const float *b1,
+                     int64_t n_nodes, float *r, scgib_stream_t stream);
 /* ---- (f)1/(f)4: Set2Set readout (DGL Set2Set(dim, n_iters, 1), models.py:565) ----
  * The whole readout as Mainmodel_finetuning.forward (models.py:515) and
  * Mainmodel_domainadapt (:271-272) run it, all n_iters rounds in one launch:

@@ -26,7 +26,7 @@ SIGNATURES = {
     "scgib_pool_copy": (ctypes.c_int, [_P, _I32, _P, _P, _I64, _P]),
     "scgib_pool_copy2": (ctypes.c_int, [_P, _I32, _P, _P, _I64, _P, _P, _I64, _P]),
     "scgib_stream_signal": (ctypes.c_int, [_P, _P]),
-    "scgib_stream_wait": (ctypes.c_int, [_P, _P, _P]),
+    "scgib_stream_wait": (ctypes.c_int, [_P, _P, _P, _P]),
     "scgib_strerror": (ctypes.c_char_p, [ctypes.c_int]),
     "scgib_gin_aggregate": (ctypes.c_int, [_P, _P, _P, _I64, _I32, _F, _P, _P, _P]),
     "scgib_segment_sum": (ctypes.c_int, [_P, _P, _I64, _I32, _P, _P, _P]),
@@ -88,8 +88,9 @@ SIGNATURES = {
     "scgib_gin_layer0_fwd": (ctypes.c_int, [_P, _I32, _P, _P, _P, _P, _I64, _F, _P, _P, _P, _P,
                                             _P, _P, _P, _P, _P, _P, _F, _F, _P, _P, _P, _P, _P,
                                             _P, _P, _I32, _P]),
-    "scgib_gin_layer0_bwd": (ctypes.c_int, [_P, _P, _P, _P, _P, _I32, _P, _P, _P, _P, _I64, _P,
-                                            _P, _P, _P]),
+    "scgib_gin_layer0_bwd": (ctypes.c_int, [_P, _P, _P, _P, _P, _I32, _P, _P, _P, _P, _P, _I64,
+                                            _P, _P, _P, _P]),
+    "scgib_gin_hidden": (ctypes.c_int, [_P, _I32, _P, _P, _I64, _P, _P]),
     "scgib_gin_bn_gpart_offset": (_I64, [_I64]),
     "scgib_gin_defer_max_nodes": (_I64, []),
     "scgib_gin_bn_ws_floats": (_I64, [_I64]),
@@ -115,8 +116,8 @@ SIGNATURES = {
                                                  _P]),
     "scgib_gin_bwd_stats": (ctypes.c_int, [_P, _P, _P, _F, _P, _P, _I64, _P, _P, _P, _P]),
     "scgib_bn_bwd_finalize": (ctypes.c_int, [_P, _I64, _I32, _P, _P, _P, _P, _P]),
-    "scgib_gin_layer_bwd": (ctypes.c_int, [_P, _P, _P, _P, _I32, _P, _P, _P, _P, _I64, _P, _P,
-                                           _P, _P, _P, _P]),
+    "scgib_gin_layer_bwd": (ctypes.c_int, [_P, _P, _P, _P, _I32, _P, _P, _P, _P, _P, _I64, _P,
+                                           _P, _P, _P, _P, _P]),
     "scgib_recon_partials_floats": (_I64, [_I64]),
     "scgib_recon_fwd": (ctypes.c_int, [_P, _P, _P, _I64, _I64, _P, _P, _P, _P, _P]),
     "scgib_recon_bwd": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _I64, _P, _P, _P, _P]),
@@ -170,7 +171,7 @@ class RunningUpdate(ctypes.Structure):
                 ("num_batches_tracked", ctypes.c_void_p)]
 
 
-ABI_VERSION = 15
+ABI_VERSION = 16
 STATS_STRIDE = 260
 PGRAD_STRIDE = 324
 HIDDEN = 64

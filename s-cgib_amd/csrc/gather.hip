@@ -172,7 +172,7 @@ __global__ void stream_signal_k(unsigned *w) {
     if (threadIdx.x == 0) __hip_atomic_fetch_add(w, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-__global__ void stream_wait_k(unsigned *w, unsigned *fault) {
+__global__ void stream_wait_k(unsigned *w, unsigned *fault, unsigned *host_fault) {
     if (threadIdx.x == 0) {
         const unsigned a = __hip_atomic_load(w + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const uint64_t t0 = wall_clock64();
@@ -182,6 +182,10 @@ __global__ void stream_wait_k(unsigned *w, unsigned *fault) {
                 __hip_atomic_fetch_add(w + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 // sticky: the step's loss kernels report NaN while it is set
                 if (fault) __hip_atomic_store(fault, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                // and the host's pinned copy, which the host checks without a
+                // sync (ops.check_handoff: models' forwards, optim.Adam.step)
+                if (host_fault)
+                    __hip_atomic_store(host_fault, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                 break;
             }
         }
@@ -279,9 +283,10 @@ extern "C" int scgib_stream_signal(uint32_t *words, scgib_stream_t stream) {
     return launch_status();
 }
 
-extern "C" int scgib_stream_wait(uint32_t *words, uint32_t *fault, scgib_stream_t stream) {
+extern "C" int scgib_stream_wait(uint32_t *words, uint32_t *fault, uint32_t *host_fault,
+                                 scgib_stream_t stream) {
     if (!words) return SCGIB_EINVAL;
-    stream_wait_k<<<1, 64, 0, as_stream(stream)>>>(words, fault);
+    stream_wait_k<<<1, 64, 0, as_stream(stream)>>>(words, fault, host_fault);
     return launch_status();
 }
 
@@ -304,7 +309,7 @@ extern "C" int scgib_pool_copy(const uint64_t *srcs, int32_t n_src, uint32_t *ct
     return scgib_pool_copy2(srcs, n_src, ctr, dst, bytes, nullptr, nullptr, 0, stream);
 }
 
-extern "C" int scgib_abi_version(void) { return 15; }
+extern "C" int scgib_abi_version(void) { return 16; }
 
 extern "C" const char *scgib_strerror(int code) {
     if (code == SCGIB_OK) return "ok";

@@ -641,7 +641,7 @@ __global__ __launch_bounds__(256, (kFwdAlias<DIN, GATHER, PRE> ? 3 : 1)) void gi
     if (dims) {  // capacity mode: zero this tile's padded rows [nv, rows in capacity)
         const int ncr = static_cast<int>(ncap - row0 < TM ? ncap - row0 : TM);
         for (int idx = nv * 64 + tid; idx < ncr * 64; idx += 256) {
-            r_out[row0 * 64 + idx] = 0.f;
+            if (r_out) r_out[row0 * 64 + idx] = 0.f;
             z2_out[row0 * 64 + idx] = 0.f;
         }
         if (GATHER)
@@ -777,7 +777,10 @@ __global__ __launch_bounds__(256, (kFwdAlias<DIN, GATHER, PRE> ? 3 : 1)) void gi
 
     const int wr = w >> 1, wc = w & 1;
     const int ccol = wc * 32 + (l & 31);
-    // z1 = agg W1^T + b1 ; r = relu(z1)
+    // z1 = agg W1^T + b1 ; r = relu(z1).  r_out NULL (the model path): r is
+    // not stored — the backward recomputes it bit for bit from the saved agg
+    // (gin_bwd5r_k, gin_bwd_k<.., RC>: this same MFMA chain, k pairs (2s,
+    // 2s + 1) in order from zero, + b1, fmaxf)
     {
         f32x16 acc = mma_pf<DIN, false, false>(sA + wr * 32 * LDA, LDA, sW1 + wc * 32 * LDA, LDA, zero16());
         const float bias = b1[ccol];
@@ -787,7 +790,7 @@ __global__ __launch_bounds__(256, (kFwdAlias<DIN, GATHER, PRE> ? 3 : 1)) void gi
             const int row = wr * 32 + acc_row(reg, l);
             const float v = fmaxf(acc[reg] + bias, 0.f);
             sR[row * LDH + ccol] = v;
-            if (row < nv) r_out[(row0 + row) * 64 + ccol] = v;
+            if (r_out && row < nv) r_out[(row0 + row) * 64 + ccol] = v;
         }
     }
     __syncthreads();
@@ -1173,15 +1176,21 @@ __global__ __launch_bounds__(1024) void bn_bwd_finalize_k(const float *__restric
 // of the MLP output); z2 / stat / coef are not read.
 // PRE: layer 0 with transfer_d folded in (see gather_x_rows): d(agg0) is not
 // stored; dWt += d(agg0)^T aggx is accumulated (slab tail of 32 x 16 floats).
-template <int DIN, bool BN = true, bool PRE = false, bool RECON = false>
+// RC (PRE only): r is not read — the forward did not store it — but
+// recomputed per tile from the agg tile (staged in the d(agg0) buffer, dead
+// until the tile's last products) with the forward's own call, mma_pf<32>
+// over the same [64][33] layouts, + b1, fmaxf: bitwise the forward's r;
+// rows past the tile's valid rows are 0, as the stored path loads them.
+template <int DIN, bool BN = true, bool PRE = false, bool RECON = false, bool RC = false>
 __global__ __launch_bounds__(256, (DIN <= 64 && !RECON ? 2 : 1)) void gin_bwd_k(
     const float *__restrict__ dy, const float *__restrict__ z2, const float *__restrict__ r,
     const float *__restrict__ agg, const float *__restrict__ stat,
     const float *__restrict__ coef, const float *__restrict__ w1, const float *__restrict__ w2,
     int64_t ncap, int64_t ntiles, float *__restrict__ dagg_out, float *__restrict__ slab,
     const int32_t *__restrict__ dims, const float *__restrict__ aggx, scgib_bn_bwd_pending pend,
-    ReconArgs rec, int pre_f = kPreF) {
+    ReconArgs rec, int pre_f = kPreF, const float *__restrict__ b1 = nullptr) {
     static_assert(!PRE || DIN == 32, "transfer_d fold: layer 0 only");
+    static_assert(!RC || PRE, "r recomputed in the layer-0 backward only (gin_bwd5r_k: d_in = 64)");
     static_assert(!RECON || !BN, "the recon backward is fused into the dense head MLP");
     const int64_t n = eff_count(dims, 0, ncap);
     constexpr int LDA = DIN + 1;
@@ -1218,6 +1227,7 @@ __global__ __launch_bounds__(256, (DIN <= 64 && !RECON ? 2 : 1)) void gin_bwd_k(
     const int wr = w >> 1, wc = w & 1;
     SCGIB_MARK(0);
     SCGIB_MARK_HWID();
+    [[maybe_unused]] const float rc_bias = RC ? b1[wc * 32 + (l & 31)] : 0.f;
     [[maybe_unused]] float rscale = 0.f;  // recon: g / N
     if constexpr (RECON) {
         stage_matrix<64>(rec.gram, sG);
@@ -1264,7 +1274,7 @@ __global__ __launch_bounds__(256, (DIN <= 64 && !RECON ? 2 : 1)) void gin_bwd_k(
             if (BN) vz[k] = ld_ok(reinterpret_cast<const float4 *>(z2), o, so, rr < m, zero);
             else vz[k] = zero;
             if (!RECON) vd[k] = ld_ok(reinterpret_cast<const float4 *>(dy), o, so, rr < m, zero);
-            vr[k] = ld_ok(reinterpret_cast<const float4 *>(r), o, so, rr < m, zero);
+            if (!RC) vr[k] = ld_ok(reinterpret_cast<const float4 *>(r), o, so, rr < m, zero);
         }
         if (PRE)
             vx = ld_ok(reinterpret_cast<const float4 *>(aggx), (r0 + (tid >> 2)) * 4 + (tid & 3),
@@ -1346,6 +1356,15 @@ __global__ __launch_bounds__(256, (DIN <= 64 && !RECON ? 2 : 1)) void gin_bwd_k(
             float *px = sPX + (tid >> 2) * LDP + 4 * (tid & 3);
             px[0] = vx.x; px[1] = vx.y; px[2] = vx.z; px[3] = vx.w;
         }
+        if constexpr (RC) {  // the agg tile for the r recompute (in the d(agg0) buffer)
+            static_assert(LDP == LDA, "the forward's agg tile layout");
+#pragma unroll
+            for (int k = 0; k < AK; ++k) {
+                const int idx = tid + 256 * k, rr = idx / AQ, cq = idx % AQ;
+                float *pa = sPD + rr * LDP + 4 * cq;
+                pa[0] = va[k].x; pa[1] = va[k].y; pa[2] = va[k].z; pa[3] = va[k].w;
+            }
+        }
         // dz2 = scale (dy - c1 - xhat c2); rows past n are zero
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
@@ -1361,9 +1380,19 @@ __global__ __launch_bounds__(256, (DIN <= 64 && !RECON ? 2 : 1)) void gin_bwd_k(
             }
             float *pd = sD + rr * LDH + 4 * c4, *pr = sR + rr * LDH + 4 * c4;
             pd[0] = d.x; pd[1] = d.y; pd[2] = d.z; pd[3] = d.w;
-            pr[0] = vr[k].x; pr[1] = vr[k].y; pr[2] = vr[k].z; pr[3] = vr[k].w;
+            if (!RC) { pr[0] = vr[k].x; pr[1] = vr[k].y; pr[2] = vr[k].z; pr[3] = vr[k].w; }
         }
         __syncthreads();
+        if constexpr (RC) {  // r = relu(agg W1^T + b1): the forward's GEMM1, rows >= nv zero
+            const f32x16 z = mma_pf<DIN, false, false>(sPD + wr * 32 * LDP, LDP, sW1 + wc * 32 * LDA, LDA, zero16());
+            const int cc = wc * 32 + (l & 31);
+#pragma unroll
+            for (int reg = 0; reg < 16; ++reg) {
+                const int row = wr * 32 + acc_row(reg, l);
+                sR[row * LDH + cc] = row < nv ? fmaxf(z[reg] + rc_bias, 0.f) : 0.f;
+            }
+            __syncthreads();
+        }
         if constexpr (RECON) {  // sD = IM tile -> dz2 = d IM = (g/N) (4 IM G - 2 nb)
             const f32x16 p = mma_pf<64, false, true>(sD + wr * 32 * LDH, LDH, sG + wc * 32, LDH, zero16());
             __syncthreads();
@@ -1398,13 +1427,18 @@ __global__ __launch_bounds__(256, (DIN <= 64 && !RECON ? 2 : 1)) void gin_bwd_k(
         }
         __syncthreads();  // r is dead: the agg tile (held in registers) takes its buffer
         if (tile == blockIdx.x) SCGIB_MARK(2);
+        // RC: the agg tile is already in the d(agg0) buffer (the r recompute's
+        // operand), the dead r buffer takes d(agg0) instead — same layouts
+        float *const aggT = RC ? sPD : sA, *const daggT = RC ? sRA : sPD;
+        if constexpr (!RC) {
 #pragma unroll
-        for (int k = 0; k < AK; ++k) {
-            const int idx = tid + 256 * k, rr = idx / AQ, cq = idx % AQ;
-            float *pa = sA + rr * LDA + 4 * cq;
-            pa[0] = va[k].x; pa[1] = va[k].y; pa[2] = va[k].z; pa[3] = va[k].w;
+            for (int k = 0; k < AK; ++k) {
+                const int idx = tid + 256 * k, rr = idx / AQ, cq = idx % AQ;
+                float *pa = sA + rr * LDA + 4 * cq;
+                pa[0] = va[k].x; pa[1] = va[k].y; pa[2] = va[k].z; pa[3] = va[k].w;
+            }
+            __syncthreads();
         }
-        __syncthreads();
         db1 = col_sum16(db1, sD + q * LDH + ch, 4 * LDH);
         // dW1 += dz1^T agg  (64 x DIN) ; d(agg) = dz1 W1  (TM x DIN)
 #pragma unroll
@@ -1413,19 +1447,19 @@ __global__ __launch_bounds__(256, (DIN <= 64 && !RECON ? 2 : 1)) void gin_bwd_k(
             if (sub < NSUB1) {
                 const int jb = sub & 1, kb = sub >> 1;  // j-block (rows of dW1 / d(agg)), k-block
                 f32x16 da = zero16();
-                mma_pf2<64, true, true, false, true>(sD + jb * 32, LDH, sA + kb * 32, LDA, accW1[q1],
+                mma_pf2<64, true, true, false, true>(sD + jb * 32, LDH, aggT + kb * 32, LDA, accW1[q1],
                                                      sD + jb * 32 * LDH, LDH, sW1 + kb * 32, LDA, da);
 #pragma unroll
                 for (int reg = 0; reg < 16; ++reg) {
                     const int row = jb * 32 + acc_row(reg, l);
-                    if (PRE) sPD[row * LDP + kb * 32 + (l & 31)] = da[reg];
+                    if (PRE) daggT[row * LDP + kb * 32 + (l & 31)] = da[reg];
                     else if (row < nv) dagg_out[(row0 + row) * DIN + kb * 32 + (l & 31)] = da[reg];
                 }
             }
         }
         if (PRE) {  // dWt += d(agg0)^T aggx (32 x 32, columns >= 16 are zero)
             __syncthreads();
-            if (w == 0) accWt = mma_tn<TM>(sPD, LDP, sPX, LDP, accWt);
+            if (w == 0) accWt = mma_tn<TM>(daggT, LDP, sPX, LDP, accWt);
         }
         if (tile == blockIdx.x) SCGIB_MARK(3);
     }
@@ -1690,6 +1724,285 @@ __global__ __launch_bounds__(256, 2) void gin_bwd5_k(
     SCGIB_MARK(6);
 }
 
+// ---------------------------------------------------------------------------
+// gin_bwd5r_k: gin_bwd5_k without the saved r.  The
+// forward no longer writes r = relu(agg W1^T + b1) — one of the three [N,64]
+// row sets gin_fwd_k stored, a third of its HBM writes — and this kernel
+// recomputes it per sub-tile from the agg rows it stages anyway, with the
+// forward's own MFMA chain (v_mfma_f32_32x32x2_f32, step s = k pair (2 s,
+// 2 s + 1), s = 0..31 in order from zero, then + b1 and fmaxf 0), so every r
+// element is bitwise the one the forward would have stored; every other
+// product is one of gin_bwd5_k's chains unchanged (same operands, same order
+// per output element), so dW1 / dW2 / db / d(agg) are bitwise gin_bwd5_k's
+// (tests/test_gpu_parity.py::test_gin_layer_bwd_recompute_bitwise).
+// Roles, 80 MFMAs per wave and sub-tile (gin_bwd5_k: 64) in three phases:
+//   1: waves 0,1: r block q = agg W1[32q.., :]^T + b1, relu -> r^T image
+//                 (and the block's ReLU mask, 16 bits in one register)
+//      waves 2,3: dr block q = dz2 W2[:, 32q..] -> the dz1^T image
+//   2: waves 0,1: dz1 = dr [r > 0] (their own block) -> dz1 / dz1^T images
+//      every wave: dW2 block (q, w >> 1) += dz2^T r (db2: waves 0,1)
+//   3: waves 0,1: d(agg) block q = dz1 W1[:, 32q..] -> staging
+//      waves 2,3: dW1 rows 32q.. += dz1^T agg (db1)
+//   (+ the next sub-tile's dz2 staged during phase 3: three barriers)
+// Registers: waves 0,1 hold W1 rows (r) and W1 columns (d(agg)), waves 2,3
+// W2 columns (dr) and two dW1 accumulators — the second weight block and
+// those accumulators are the same two f32x16.  LDS: gin_bwd5_k's images
+// (r^T now written by phase 1) + the agg rows with each row's k split
+// even | odd (lane half kk reads k = 2 s + kk, s = 0..31, as one run: b128
+// operand reads) = 72 KB, two workgroups per CU.
+// ---------------------------------------------------------------------------
+constexpr int kEO = 32;  // even | odd split: k -> (k & 1) * 32 + (k >> 1)
+
+template <int DIN>
+__global__ __launch_bounds__(256, 2) void gin_bwd5r_k(
+    const float *__restrict__ dy, const float *__restrict__ z2, const float *__restrict__ agg,
+    const float *__restrict__ stat, const float *__restrict__ coef, const float *__restrict__ w1,
+    const float *__restrict__ b1, const float *__restrict__ w2, int64_t ncap, int64_t nsub,
+    float *__restrict__ dagg_out, float *__restrict__ slab, const int32_t *__restrict__ dims,
+    scgib_bn_bwd_pending pend) {
+    static_assert(DIN == 64 && SM == 32, "64-wide rows, 32-row sub-tiles");
+    constexpr int SLAB = 64 * 64 + 64 * DIN + 128;
+    __shared__ __attribute__((aligned(16))) float sD[SM * LDR];   // dz2 [row][k]
+    __shared__ __attribute__((aligned(16))) float sDT[64 * LDT];  // dz2 [col][row]
+    __shared__ __attribute__((aligned(16))) float sE[SM * LDR];   // dz1
+    __shared__ __attribute__((aligned(16))) float sET[64 * LDT];
+    __shared__ __attribute__((aligned(16))) float sRT[64 * LDT];  // r [col][row] (recomputed)
+    __shared__ __attribute__((aligned(16))) float sAT[DIN * LDT]; // agg [col][row]
+    __shared__ __attribute__((aligned(16))) float sAR[SM * LDR];  // agg [row][even | odd k]
+    __shared__ float sG[SM * LDH];                                 // d(agg) staging
+    __shared__ float sCoef[128];
+    const int64_t n = eff_count(dims, 0, ncap);
+    const int tid = threadIdx.x, l = tid & 63, w = tid >> 6;
+    const int kk = l >> 5, li = l & 31;
+    const bool ra = w < 2;  // wave-uniform role: r, d(agg) (waves 0,1) or dr, dW1 (2,3)
+    const int q = w & 1;    // the role's 32-wide block
+    const int c = l;        // elementwise: column c, rows 8 w .. 8 w + 7
+    const int64_t last = ncap - 1;
+    const int64_t G = gridDim.x;
+    SCGIB_MARK(0);
+    SCGIB_MARK_HWID();
+    BwdFin bfin;
+    const int pend_ngr = static_cast<int>(((n + TM - 1) / TM + kGroup - 1) / kGroup);
+    if (pend.gpart) bn_bwd_fin_load<false>(pend.gpart, pend_ngr, 0, bfin);
+    const float s_mean = stat[c], s_istd = stat[64 + c], s_sc = stat[128 + c];
+    float c1 = 0.f, c2 = 0.f;
+    if (!pend.gpart) {
+        c1 = coef[c];
+        c2 = coef[64 + c];
+    }
+    // wa: waves 0,1 W1[32q + li][2 s + kk] (r, the forward's k order);
+    //     waves 2,3 W2[kperm(s, kk)][32q + li] (dr)
+    // X0 | X1: waves 0,1 W1[kperm(s, kk)][32q + li] (d(agg));
+    //          waves 2,3 the dW1 accumulators (q, 0) | (q, 1)
+    float wa[32];
+    f32x16 X0 = zero16(), X1 = zero16();
+    float bias1 = 0.f;
+    if (ra) {
+#pragma unroll
+        for (int s = 0; s < 32; ++s) wa[s] = w1[(q * 32 + li) * DIN + 2 * s + kk];
+#pragma unroll
+        for (int s = 0; s < 16; ++s) {
+            X0[s] = w1[kperm(s, kk) * DIN + q * 32 + li];
+            X1[s] = w1[kperm(s + 16, kk) * DIN + q * 32 + li];
+        }
+        bias1 = b1[q * 32 + li];
+    } else {
+#pragma unroll
+        for (int s = 0; s < 32; ++s) wa[s] = w2[kperm(s, kk) * 64 + q * 32 + li];
+    }
+    // a sub-tile's column c, rows 8 w + i: [0] dy, [1] z2, [2] agg.  The next
+    // sub-tile's agg rows are loaded a whole sub-tile ahead (its r^T / agg
+    // images are written after this one's barriers 1 and 3), its dy / z2 only
+    // after barrier 1 (staged in phase 3): fewer registers live across phase 1
+    float nx[3][8];
+    auto load_agg = [&](int64_t s) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            int64_t row = s * SM + 8 * w + i;
+            row = row < last ? row : last;
+            nx[2][i] = agg[row * DIN + c];
+        }
+    };
+    auto load_dz = [&](int64_t s) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            int64_t row = s * SM + 8 * w + i;
+            row = row < last ? row : last;
+            nx[0][i] = dy[row * 64 + c];
+            nx[1][i] = z2[row * 64 + c];
+        }
+    };
+    auto load_sub = [&](int64_t s) {
+        load_agg(s);
+        load_dz(s);
+    };
+    auto put_at = [&]() {  // agg column c, rows 8w..8w+7 -> [c][row]
+        float4 *p = reinterpret_cast<float4 *>(sAT + c * LDT + 8 * w);
+        p[0] = make_float4(nx[2][0], nx[2][1], nx[2][2], nx[2][3]);
+        p[1] = make_float4(nx[2][4], nx[2][5], nx[2][6], nx[2][7]);
+    };
+    auto put_ar = [&]() {  // agg column c -> position (c & 1) * 32 + (c >> 1) of rows 8w..
+        const int pos = (c & 1) * kEO + (c >> 1);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) sAR[(8 * w + i) * LDR + pos] = nx[2][i];
+    };
+    auto rows_of = [&](int64_t s) {
+        const int64_t v = n - s * SM;
+        return static_cast<int>(v < SM ? (v > 0 ? v : 0) : SM);
+    };
+    auto zero_pad = [&](int64_t s, int from) {
+        const int64_t row0 = s * SM;
+        const int ncr = static_cast<int>(ncap - row0 < SM ? ncap - row0 : SM);
+        for (int idx = from * DIN + tid; idx < ncr * DIN; idx += 256) dagg_out[row0 * DIN + idx] = 0.f;
+    };
+    float k1 = 0.f;
+    // dz2 = sc (dy - c1 - (z2 - mean) istd c2), rows past nv zero -> sD, sDT
+    auto stage_dz2 = [&](int nvs) {
+        float d[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const float v = s_sc * (nx[0][i] - c1 - (nx[1][i] - s_mean) * k1);
+            d[i] = 8 * w + i < nvs ? v : 0.f;
+            sD[(8 * w + i) * LDR + c] = d[i];
+        }
+        float4 *p = reinterpret_cast<float4 *>(sDT + c * LDT + 8 * w);
+        p[0] = make_float4(d[0], d[1], d[2], d[3]);
+        p[1] = make_float4(d[4], d[5], d[6], d[7]);
+    };
+    int64_t s = blockIdx.x;
+    int nv = s < nsub ? rows_of(s) : 0;
+    if (nv > 0) load_sub(s);
+    if (pend.gpart) {  // finish the BN-backward sums; workgroup 0 writes dgamma, dbeta
+        const double tot = bn_bwd_final<false>(pend.gpart, pend_ngr, bfin);
+        const int cs = bfin_index();
+        const bool lead = (tid & 63) < 32, w0 = blockIdx.x == 0 && lead;
+        const float cf = bn_bwd_publish(cs, tot, n, pend.training, w0 ? pend.dgamma : nullptr,
+                                        w0 ? pend.dbeta : nullptr, nullptr);
+        if (lead) sCoef[cs] = cf;
+        __syncthreads();
+        c1 = sCoef[c];
+        c2 = sCoef[64 + c];
+    }
+    k1 = s_istd * c2;
+    if (nv > 0) {
+        put_at();
+        put_ar();
+        stage_dz2(nv);
+    }
+    // the weight registers complete here (see gin_bwd5_k)
+    vm_wait_all();
+    __syncthreads();
+    // the second sub-tile's agg rows: in flight during the first one's phase 1
+    if (nv > 0 && s + G < nsub && rows_of(s + G) > 0) load_agg(s + G);
+    SCGIB_MARK(1);
+    f32x16 acc0 = zero16();  // waves 0,1: dW2 block (q, 0); waves 2,3: dW2 block (q, 1)
+    float dbias = 0.f;       // waves 0,1: db2 [32q + li]; waves 2,3: db1
+    for (int it = 0; s < nsub; s += G, ++it) {
+        if (nv == 0) {  // capacity tail: this and every later sub-tile is padding
+            for (int64_t t = s; t < nsub; t += G) zero_pad(t, rows_of(t));
+            break;
+        }
+        const int64_t next = s + G;
+        const int next_nv = next < nsub ? rows_of(next) : 0;  // block-uniform
+        // the element (row 8 g + 4 kk + t, column 32 q + li) of block q sits in
+        // register 4 g + t of every role: one b128 per g in the [col][row] images
+        const int col = q * 32 + li;
+        unsigned rmask = 0u;  // waves 0,1: bit 4 g + t = [r > 0] of their r block
+        if (ra) {  // phase 1: r block q (the forward's chain), relu -> sRT as [col][row]
+            const f32x16 z = mma_rk4<8, 4>(sAR + li * LDR + kk * kEO, wa, zero16());
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                float v[4];
+#pragma unroll
+                for (int t = 0; t < 4; ++t) {
+                    v[t] = fmaxf(z[4 * g + t] + bias1, 0.f);
+                    rmask |= (v[t] > 0.f ? 1u : 0u) << (4 * g + t);
+                }
+                *reinterpret_cast<float4 *>(sRT + col * LDT + 8 * g + 4 * kk) = make_float4(v[0], v[1], v[2], v[3]);
+            }
+        } else {   // phase 1: dr block q -> sET [col][row] (masked in phase 2 by waves 0,1)
+            const f32x16 dr = mma_rk4<8>(sD + li * LDR + 4 * kk, wa, zero16());
+#pragma unroll
+            for (int g = 0; g < 4; ++g)
+                *reinterpret_cast<float4 *>(sET + col * LDT + 8 * g + 4 * kk) =
+                    make_float4(dr[4 * g], dr[4 * g + 1], dr[4 * g + 2], dr[4 * g + 3]);
+        }
+        lds_barrier();  // r^T and dr complete; the agg rows consumed
+        if (it == 0) SCGIB_MARK(2);
+        if (next_nv > 0) {
+            put_ar();
+            load_dz(next);  // staged in phase 3
+        }
+        if (ra) {  // phase 2: dz1 = dr [r > 0] -> sE, sET in place (mask by multiplication)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                float4 *pt = reinterpret_cast<float4 *>(sET + col * LDT + 8 * g + 4 * kk);
+                const float4 d = *pt;
+                const float4 v = make_float4(d.x * ((rmask >> (4 * g)) & 1u ? 1.f : 0.f),
+                                             d.y * ((rmask >> (4 * g + 1)) & 1u ? 1.f : 0.f),
+                                             d.z * ((rmask >> (4 * g + 2)) & 1u ? 1.f : 0.f),
+                                             d.w * ((rmask >> (4 * g + 3)) & 1u ? 1.f : 0.f));
+                const int row = 8 * g + 4 * kk;
+                sE[row * LDR + col] = v.x;
+                sE[(row + 1) * LDR + col] = v.y;
+                sE[(row + 2) * LDR + col] = v.z;
+                sE[(row + 3) * LDR + col] = v.w;
+                *pt = v;
+            }
+        }
+        // phase 2: dW2 rows 32q.., columns 32 (w >> 1).. += dz2^T r (db2 on waves 0,1)
+        if (ra)
+            mma_kk4<4, true>(sDT + (q * 32 + li) * LDT + 4 * kk, sRT + li * LDT + 4 * kk, acc0, dbias);
+        else
+            mma_kk4<4, false>(sDT + (q * 32 + li) * LDT + 4 * kk, sRT + (32 + li) * LDT + 4 * kk, acc0, dbias);
+        lds_barrier();  // dz1 complete; dz2 and r consumed
+        if (it == 0) SCGIB_MARK(3);
+        if (ra) {  // phase 3: d(agg) block q = dz1 W1[:, 32q..] -> staging
+            const f32x16 da = mma_rk4<8>(sE + li * LDR + 4 * kk, W32{X0, X1}, zero16());
+#pragma unroll
+            for (int reg = 0; reg < 16; ++reg) sG[acc_row(reg, l) * LDH + q * 32 + li] = da[reg];
+        } else {   // phase 3: dW1 rows 32q.. += dz1^T agg (db1 from the A operand)
+            mma_kk4x2<4>(sET + (q * 32 + li) * LDT + 4 * kk, sAT + li * LDT + 4 * kk,
+                         sAT + (32 + li) * LDT + 4 * kk, X0, X1, dbias);
+        }
+        if (next_nv > 0) stage_dz2(next_nv);  // dz2 and its images are free since the barrier
+        lds_barrier();  // d(agg) staged, next dz2 staged; agg^T and dz1 consumed
+        if (it == 0) SCGIB_MARK(4);
+        if (next_nv > 0) {
+            put_at();
+            const int64_t nn = next + G;  // the sub-tile after: in flight during the next one
+            if (nn < nsub && rows_of(nn) > 0) load_agg(nn);
+        }
+        {   // d(agg) rows: full-row float4 stores (after the loads: in-order vmcnt)
+            const int c4 = tid & 15, rs = tid >> 4;
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+                const int rr = rs + 16 * k;
+                const float *pg = sG + rr * LDH + 4 * c4;
+                const float4 v = make_float4(pg[0], pg[1], pg[2], pg[3]);
+                if (rr < nv) st4(dagg_out + (s * SM + rr) * DIN + 4 * c4, v);
+            }
+        }
+        if (dims) zero_pad(s, nv);
+        nv = next_nv;
+    }
+    SCGIB_MARK(5);
+    // per-workgroup slab: dW2 | dW1 | db2 | db1 (gin_bwd_k layout)
+    float *sl = slab + static_cast<int64_t>(blockIdx.x) * SLAB;
+#pragma unroll
+    for (int reg = 0; reg < 16; ++reg) {
+        const int j = q * 32 + acc_row(reg, l);
+        sl[j * 64 + (ra ? 0 : 32) + li] = acc0[reg];
+        if (!ra) {
+            sl[64 * 64 + j * DIN + li] = X0[reg];
+            sl[64 * 64 + j * DIN + 32 + li] = X1[reg];
+        }
+    }
+    dbias += __shfl_xor(dbias, 32, kWave);
+    if (l < 32) sl[64 * 64 + 64 * DIN + (ra ? 0 : 64) + q * 32 + l] = dbias;
+    SCGIB_MARK(6);
+}
+
 // up to two workgroups per CU (66.5 KB LDS each): one tile per workgroup for
 // batches up to kBwdGridCap tiles, so every tile of
 // an encoder layer runs at once; larger batches loop over tiles
@@ -1770,8 +2083,8 @@ static int gin_fwd_args_ok(const float *h_in, int32_t d_in, const float *in_stat
                            const float *tile_stats) {
     if (n_nodes < 0 || (d_in != 32 && d_in != 64)) return SCGIB_EINVAL;
     if (n_nodes == 0) return SCGIB_OK;
-    if (!h_in || !rowptr || !col || !w1 || !b1 || !w2 || !b2 || !agg || !r || !z2 || !tile_stats)
-        return SCGIB_EINVAL;
+    if (!h_in || !rowptr || !col || !w1 || !b1 || !w2 || !b2 || !agg || !z2 || !tile_stats)
+        return SCGIB_EINVAL;  // (r may be NULL: not stored)
     if (in_stat && d_in != 64) return SCGIB_EUNSUPPORTED;
     return 1;  // go
 }
@@ -2044,13 +2357,14 @@ extern "C" int scgib_bn_bwd_finalize(const float *tile_stats, int64_t n_nodes, i
 
 extern "C" int scgib_gin_layer_bwd(const float *dy, const float *z2, const float *r,
                                    const float *agg, int32_t d_in, const float *stat,
-                                   const float *coef, const float *w1, const float *w2,
-                                   int64_t n_nodes, float *dagg, float *slab, float *wgrad,
-                                   const int32_t *dims, const scgib_bn_bwd_pending *pending,
-                                   scgib_stream_t stream) {
+                                   const float *coef, const float *w1, const float *b1,
+                                   const float *w2, int64_t n_nodes, float *dagg, float *slab,
+                                   float *wgrad, const int32_t *dims,
+                                   const scgib_bn_bwd_pending *pending, scgib_stream_t stream) {
     if (n_nodes <= 0 || (d_in != 32 && d_in != 64)) return SCGIB_EINVAL;
-    if (!dy || !z2 || !r || !agg || !stat || (!coef && !pending) || !w1 || !w2 || !dagg || !slab)
+    if (!dy || !z2 || !agg || !stat || (!coef && !pending) || !w1 || !w2 || !dagg || !slab)
         return SCGIB_EINVAL;
+    if (!r && (d_in != 64 || !b1)) return SCGIB_EINVAL;  // recompute: d_in = 64, needs b1
     if (pending && (!pending->gpart || !pending->dgamma || !pending->dbeta)) return SCGIB_EINVAL;
     const scgib_bn_bwd_pending pd = pending ? *pending : scgib_bn_bwd_pending{};
     const int64_t nt = scgib_gin_tiles(n_nodes);
@@ -2058,8 +2372,10 @@ extern "C" int scgib_gin_layer_bwd(const float *dy, const float *z2, const float
     hipStream_t st = as_stream(stream);
     if (d_in == 32)
         gin_bwd_k<32><<<grid, 256, 0, st>>>(dy, z2, r, agg, stat, coef, w1, w2, n_nodes, nt, dagg, slab, dims, nullptr, pd, ReconArgs{});
-    else
+    else if (r)
         gin_bwd5_k<64><<<grid, 256, 0, st>>>(dy, z2, r, agg, stat, coef, w1, w2, n_nodes, bwd5_subtiles(n_nodes), dagg, slab, dims, pd);
+    else
+        gin_bwd5r_k<64><<<grid, 256, 0, st>>>(dy, z2, agg, stat, coef, w1, b1, w2, n_nodes, bwd5_subtiles(n_nodes), dagg, slab, dims, pd);
     const int rc = launch_status();
     if (rc != SCGIB_OK || !wgrad) return rc;  // wgrad NULL: the caller reduces the slabs
     return launch_slab_reduce(slab, grid, 64 * 64 + 64 * static_cast<int64_t>(d_in) + 128, wgrad, st);
@@ -2321,9 +2637,8 @@ extern "C" int scgib_gin_layer0_fwd(const float *x, int32_t n_feat, const int32_
                                     uint32_t *counters, const int32_t *dims, int32_t defer,
                                     scgib_stream_t stream) {
     if (n_nodes <= 0 || n_feat < 1 || n_feat > kPreF) return n_nodes == 0 ? SCGIB_OK : SCGIB_EINVAL;
-    if (!x || !wt || !rowptr || !col || !w1 || !b1 || !w2 || !b2 || !agg || !aggx || !r || !z2 ||
-        !bn_ws)
-        return SCGIB_EINVAL;
+    if (!x || !wt || !rowptr || !col || !w1 || !b1 || !w2 || !b2 || !agg || !aggx || !z2 || !bn_ws)
+        return SCGIB_EINVAL;  // (r may be NULL: not stored)
     if (counters && (!gamma || !beta || !stat || ((running_mean == nullptr) != (running_var == nullptr))))
         return SCGIB_EINVAL;
     BnFwdFuse fz{};
@@ -2342,17 +2657,60 @@ extern "C" int scgib_gin_layer0_fwd(const float *x, int32_t n_feat, const int32_
 extern "C" int scgib_gin_layer0_bwd(const float *dy, const float *z2, const float *r,
                                     const float *agg, const float *aggx, int32_t n_feat,
                                     const float *stat, const float *coef, const float *w1,
-                                    const float *w2, int64_t n_nodes, float *slab,
+                                    const float *b1, const float *w2, int64_t n_nodes, float *slab,
                                     const int32_t *dims, const scgib_bn_bwd_pending *pending,
                                     scgib_stream_t stream) {
-    if (n_nodes <= 0 || !dy || !z2 || !r || !agg || !aggx || !stat || (!coef && !pending) || !w1 ||
-        !w2 || !slab || n_feat < 1 || n_feat > kPreF)
+    if (n_nodes <= 0 || !dy || !z2 || (!r && !b1) || !agg || !aggx || !stat || (!coef && !pending) ||
+        !w1 || !w2 || !slab || n_feat < 1 || n_feat > kPreF)
         return SCGIB_EINVAL;
     if (pending && (!pending->gpart || !pending->dgamma || !pending->dbeta)) return SCGIB_EINVAL;
     const scgib_bn_bwd_pending pd = pending ? *pending : scgib_bn_bwd_pending{};
     const int64_t nt = scgib_gin_tiles(n_nodes);
-    gin_bwd_k<32, true, true><<<bwd_grid(nt), 256, 0, as_stream(stream)>>>(
-        dy, z2, r, agg, stat, coef, w1, w2, n_nodes, nt, nullptr, slab, dims, aggx, pd, ReconArgs{},
-        n_feat);
+    if (r)
+        gin_bwd_k<32, true, true><<<bwd_grid(nt), 256, 0, as_stream(stream)>>>(
+            dy, z2, r, agg, stat, coef, w1, w2, n_nodes, nt, nullptr, slab, dims, aggx, pd, ReconArgs{},
+            n_feat);
+    else
+        gin_bwd_k<32, true, true, false, true><<<bwd_grid(nt), 256, 0, as_stream(stream)>>>(
+            dy, z2, nullptr, agg, stat, coef, w1, w2, n_nodes, nt, nullptr, slab, dims, aggx, pd,
+            ReconArgs{}, n_feat, b1);
+    return launch_status();
+}
+
+// r = relu(agg W1^T + b1) with the forward's MFMA chain, i.e. bitwise the r
+// gin_fwd_k computes (and the backward recomputes): one wave per 32 x 32
+// block, operands straight from global memory (the chain, not the operand
+// path, fixes the bits).  Inspection / tests: the ReLU decisions of a model
+// step whose forward did not store r.
+__global__ __launch_bounds__(256) void gin_hidden_k(const float *__restrict__ agg, int din,
+                                                    const float *__restrict__ w1,
+                                                    const float *__restrict__ b1, int64_t n,
+                                                    float *__restrict__ r) {
+    const int l = threadIdx.x & 63, li = l & 31, kk = l >> 5;
+    const int64_t blk = static_cast<int64_t>(blockIdx.x) * 4 + (threadIdx.x >> 6);  // 32 rows x 32 cols
+    const int64_t row0 = (blk >> 1) * 32;
+    const int col = static_cast<int>(blk & 1) * 32 + li;
+    if (row0 >= n) return;  // wave-uniform
+    const int64_t arow = row0 + li < n ? row0 + li : n - 1;
+    f32x16 acc = zero16();
+    for (int s = 0; s < din / 2; ++s)
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(agg[arow * din + 2 * s + kk],
+                                                  w1[col * din + 2 * s + kk], acc, 0, 0, 0);
+    const float bias = b1[col];
+#pragma unroll
+    for (int reg = 0; reg < 16; ++reg) {
+        const int64_t row = row0 + acc_row(reg, l);
+        if (row < n) r[row * 64 + col] = fmaxf(acc[reg] + bias, 0.f);
+    }
+}
+
+extern "C" int scgib_gin_hidden(const float *agg, int32_t d_in, const float *w1, const float *b1,
+                                int64_t n_nodes, float *r, scgib_stream_t stream) {
+    if (n_nodes < 0 || (d_in != 32 && d_in != 64)) return SCGIB_EINVAL;
+    if (n_nodes == 0) return SCGIB_OK;
+    if (!agg || !w1 || !b1 || !r) return SCGIB_EINVAL;
+    const int64_t blocks = ((n_nodes + 31) / 32) * 2;
+    gin_hidden_k<<<dim3(static_cast<unsigned>((blocks + 3) / 4)), 256, 0, as_stream(stream)>>>(
+        agg, d_in, w1, b1, n_nodes, r);
     return launch_status();
 }

@@ -399,20 +399,60 @@ __device__ __forceinline__ float f4at(const float4 &v, int t) {
 // acc += A B over K = 8 NB: A k-contiguous per lane (pa = this lane's row
 // start + 4 kk), B in registers (b[s] = B(kperm(s, kk), lane's column)).
 // One accumulation chain (64-cycle issue = dependent latency of the f32 MFMA).
-template <int NB>
-__device__ __forceinline__ f32x16 mma_rk4(const float *pa, const float (&b)[4 * NB], f32x16 acc) {
+// STRIDE: floats between the lane's consecutive 4-step blocks — 8 for the
+// kperm order; 4 for an image whose lane half kk holds k = 2 s + kk as one
+// contiguous run (the even | odd split of gin_bwd5r_k's agg rows), which
+// feeds step s the forward's own k pair (2 s, 2 s + 1): mma_nt's order.
+// The weights come either as a float array or as two f32x16 (b0: steps
+// 0..15, b1: 16..31 — registers a wave of another role uses as accumulators).
+__device__ __forceinline__ float wsel(const float *b, int s) { return b[s]; }
+struct W32 {
+    const f32x16 &lo, &hi;
+};
+__device__ __forceinline__ float wsel(const W32 &b, int s) { return s < 16 ? b.lo[s] : b.hi[s - 16]; }
+
+template <int NB, int STRIDE = 8, class WB>
+__device__ __forceinline__ f32x16 mma_rk4(const float *pa, const WB &b, f32x16 acc) {
     float4 a[2];
     a[0] = *reinterpret_cast<const float4 *>(pa);
 #pragma unroll
     for (int qb = 0; qb < NB; ++qb) {
-        if (qb + 1 < NB) a[(qb + 1) & 1] = *reinterpret_cast<const float4 *>(pa + 8 * (qb + 1));
+        if (qb + 1 < NB) a[(qb + 1) & 1] = *reinterpret_cast<const float4 *>(pa + STRIDE * (qb + 1));
         if (kMmaPrefetchPin) __builtin_amdgcn_sched_barrier(0);  // the next block's read goes out first
 #pragma unroll
         for (int t = 0; t < 4; ++t)
-            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(f4at(a[qb & 1], t), b[4 * qb + t], acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(f4at(a[qb & 1], t), wsel(b, 4 * qb + t), acc, 0, 0, 0);
         mma_step_fence();
     }
     return acc;
+}
+
+// one product of mma_kk4x2 (the same per-element chain as its c1 / c2):
+// c += A B over K = 8 NB, both operands k-contiguous per lane; asum += the
+// lane's A values when SUM
+template <int NB, bool SUM>
+__device__ __forceinline__ void mma_kk4(const float *pa, const float *pb, f32x16 &c, float &asum) {
+    float4 a[2], b[2];
+    a[0] = *reinterpret_cast<const float4 *>(pa);
+    b[0] = *reinterpret_cast<const float4 *>(pb);
+#pragma unroll
+    for (int qb = 0; qb < NB; ++qb) {
+        if (qb + 1 < NB) {
+            const int o = 8 * (qb + 1), x = (qb + 1) & 1;
+            a[x] = *reinterpret_cast<const float4 *>(pa + o);
+            b[x] = *reinterpret_cast<const float4 *>(pb + o);
+        }
+        if (kMmaPrefetchPin) __builtin_amdgcn_sched_barrier(0);
+        const int x = qb & 1;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            const float av = f4at(a[x], t);
+            c = __builtin_amdgcn_mfma_f32_32x32x2f32(av, f4at(b[x], t), c, 0, 0, 0);
+            if (SUM) asum += av;
+        }
+        mma_step_fence();
+    }
+    asm volatile("" ::"v"(c[0]));
 }
 
 // two products sharing the A operand, K = 8 NB, both operands k-contiguous

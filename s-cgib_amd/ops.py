@@ -51,6 +51,17 @@ DEFER_BN_FWD = True
 # the chain's final reduce launch; only layer 0's slabs are left for the end
 # (bench.py's superbatch pass turns it off to time the statistics kernel alone)
 FOLD_SLABS = True
+# the GIN layers' hidden activation r = relu(agg W1^T + b1): stored by the
+# forward and read by the backward (True), or not stored and recomputed bit
+# for bit by the backward from the saved agg (False: scgib_gin_layer_bwd /
+# _layer0_bwd with r NULL, gin_bwd5r_k).  Same bits
+# either way (test_gin_r_recompute_bitwise).  Measured (profiles/r05_recompute):
+# recomputing costs 8192 flop per row on f32 MFMA, more than the 512 B of
+# r traffic it saves — step 0.398 -> 0.421 ms, superbatch forward -39 us but
+# backward +145 us per layer — so r is stored; False saves 256 B per row and
+# layer of saved activations.  (A d_in = 32 layer fed by a given h0, i.e. not
+# the transfer_d fold, always stores r.)
+STORE_R = True
 
 
 # LATE_FORK (always): launch_aside records an event on the current stream now
@@ -232,11 +243,13 @@ def discard_aside():
 def aside_guard(fn):
     """Decorator for model forwards that end with join_aside(): an exception
     raised between the deferred launch and the join discards the deferred
-    work instead of leaving it for the next forward."""
+    work instead of leaving it for the next forward.  Each call first runs
+    check_handoff() (host-side, no sync)."""
     import functools
 
     @functools.wraps(fn)
     def wrapper(*args, **kwargs):
+        check_handoff()  # an earlier step's hand-off wait gave up: raise, loud
         try:
             return fn(*args, **kwargs)
         except BaseException:
@@ -418,9 +431,11 @@ class _GinEncoder(torch.autograd.Function):
                 raise _lib.ScgibError(f"fused GIN layer needs Linear({d_in},64)/Linear(64,64), got "
                                       f"{tuple(w1.shape)}/{tuple(w2.shape)}")
             agg = torch.empty(n, d_in, dtype=torch.float32, device=dev)
-            r = torch.empty(n, HIDDEN, dtype=torch.float32, device=dev)
+            # r only where the backward cannot recompute it (or STORE_R)
+            keep_r = STORE_R or (d_in != HIDDEN and not (pre and l == 0))
+            r = torch.empty(n, HIDDEN, dtype=torch.float32, device=dev) if keep_r else None
             z2 = torch.empty(n, HIDDEN, dtype=torch.float32, device=dev)
-            meta = {"n": n, "e": graph.edge_capacity(), "d_in": d_in}
+            meta = {"n": n, "e": graph.edge_capacity(), "d_in": d_in, "r": r is not None}
             stat = torch.empty(4, HIDDEN, dtype=torch.float32, device=dev)
             track = training and bn.track_running_stats
             momentum = float(bn.momentum if bn.momentum is not None else 0.1)
@@ -518,8 +533,8 @@ class _GinEncoder(torch.autograd.Function):
         fold_slab = None  # its slab: released once that launch is enqueued (the
         # allocator may then reuse the block for later tensors of this stream)
         for l in reversed(range(L)):
-            agg, r, z2, stat = saved[4 * l: 4 * l + 4]
-            w1, _, w2 = params[6 * l], params[6 * l + 1], params[6 * l + 2]
+            agg, r, z2, stat = saved[4 * l: 4 * l + 4]  # r None: recomputed by the kernel
+            w1, b1, w2 = params[6 * l], params[6 * l + 1], params[6 * l + 2]
             d_in = agg.shape[1]
             # (the previous layer's dy and slab are no longer read by anything
             # not yet enqueued: released before the new allocations, whose
@@ -554,14 +569,15 @@ class _GinEncoder(torch.autograd.Function):
                 fold = fold_slab = dagg_next = None
             bpend = _lib.BnBwdPending(gpart, bn_g[0].data_ptr(), bn_g[1].data_ptr(),
                                       int(ctx.training)) if defer else None
-            meta = {"n": n, "e": gr.edge_capacity(), "d_in": d_in}
+            meta = {"n": n, "e": gr.edge_capacity(), "d_in": d_in, "r": r is not None}
             w1c, w2c = _f32(w1, "w1"), _f32(w2, "w2")
+            b1c = _f32(b1, "b1") if r is None else None
             if pre and l == 0:
                 width = int(_lib.query("scgib_gin_layer0_slab_width"))
                 slab = torch.empty(nslab * width, dtype=torch.float32, device=dev)
                 _launch("scgib_gin_layer0_bwd", meta, _p(dy), _p(z2), _p(r), _p(agg), _p(aggx),
-                        ctx.n_feat, _p(stat), _p(coef), _p(w1c), _p(w2c), n, _p(slab), _p(gr.dims),
-                        _byref(bpend), st)
+                        ctx.n_feat, _p(stat), _p(coef), _p(w1c), _p(b1c), _p(w2c), n, _p(slab),
+                        _p(gr.dims), _byref(bpend), st)
                 dagg = None
             else:
                 width = HIDDEN * HIDDEN + HIDDEN * d_in + 2 * HIDDEN
@@ -569,8 +585,8 @@ class _GinEncoder(torch.autograd.Function):
                                    dtype=torch.float32, device=dev)
                 dagg = torch.empty(n, d_in, dtype=torch.float32, device=dev)
                 _launch("scgib_gin_layer_bwd", meta, _p(dy), _p(z2), _p(r), _p(agg), d_in,
-                        _p(stat), _p(coef), _p(w1c), _p(w2c), n, _p(dagg), _p(slab), _NULL,
-                        _p(gr.dims), _byref(bpend), st)
+                        _p(stat), _p(coef), _p(w1c), _p(b1c), _p(w2c), n, _p(dagg), _p(slab),
+                        _NULL, _p(gr.dims), _byref(bpend), st)
             wgrad = torch.empty(width, dtype=torch.float32, device=dev)
             if pre and l == 0:  # dWt occupies 32 * F of its 512 columns
                 used = HIDDEN * HIDDEN + HIDDEN * d_in + 2 * HIDDEN + 32 * ctx.n_feat
@@ -636,6 +652,21 @@ def gin_encoder_x(x, graph, gin, transfer, node_map=None):
                              node_map, *_gin_layer_params(gin))
 
 
+def gin_hidden(agg, w1, b1):
+    """r = relu(agg W1^T + b1) [n, 64] with the GIN forward's own MFMA chain
+    (scgib_gin_hidden): bitwise the r a fused layer computes, and the r its
+    backward recomputes when the forward did not store it (STORE_R False).
+    Inspection / tests (the hidden ReLU decisions of a step)."""
+    agg = _f32(agg, "gin_hidden agg")
+    w1, b1 = _f32(w1, "gin_hidden w1"), _f32(b1, "gin_hidden b1")
+    n, d_in = agg.shape
+    if tuple(w1.shape) != (HIDDEN, d_in) or b1.numel() != HIDDEN:
+        raise _lib.ScgibError(f"gin_hidden: agg {tuple(agg.shape)}, w1 {tuple(w1.shape)}")
+    r = torch.empty(n, HIDDEN, dtype=torch.float32, device=agg.device)
+    _lib.call("scgib_gin_hidden", _p(agg), d_in, _p(w1), _p(b1), n, _p(r), _stream())
+    return r
+
+
 class _Ctx:
     """Stand-in ctx so _GinEncoder's forward/backward can run inside another
     Function (the tensors it saves stay referenced by the outer node)."""
@@ -659,14 +690,63 @@ class _Ctx:
 # are the same either way, only the synchronisation packets differ).
 
 
-def _dispatch_serialised():
-    env = os.environ
+def _dispatch_serialised(env=None):
+    env = os.environ if env is None else env
     return any(env.get(k, "0") not in ("", "0") for k in (
         "ROCPROF_COUNTER_COLLECTION", "ROCPROF_KERNEL_TRACE", "AMD_SERIALIZE_KERNEL",
         "HIP_LAUNCH_BLOCKING", "CUDA_LAUNCH_BLOCKING"))
 
 
-XQ_FLAGS = not _dispatch_serialised()
+def _env_int(env, name, default):
+    try:
+        return int(env.get(name, "") or default)
+    except ValueError:
+        return default
+
+
+def handoff_rule(device_count=None, env=None):
+    """(ok, reason): may the encoder pair use the signal / wait hand-offs?
+
+    A wait kernel spins until its signal kernel has run, so the two must sit
+    on hardware queues the device runs CONCURRENTLY — a replayed graph may
+    order the wait before the signal on one in-order queue, and then the wait
+    only ends at its 0.2 s bound (counted, the sticky fault set, an error at
+    the next host check: check_handoff).  What the hand-offs rely on
+    ("Cross-queue hand-offs"): eagerly, `side` and the current
+    stream are distinct HIP streams; a replayed graph runs its parallel
+    branches (the two encoder chains) on distinct streams the runtime creates
+    per device for graph execution (capped by DEBUG_HIP_FORCE_GRAPH_QUEUES);
+    the runtime gives each stream one of the process's GPU_MAX_HW_QUEUES
+    hardware queues (4 on the pool's boxes), spreading streams over them; the
+    command processor runs distinct hardware queues concurrently.  So the
+    rule refuses exactly the settings that break one of those links:
+      * dispatch serialised device-wide (PMC counter collection, kernel-trace
+        callbacks, AMD_SERIALIZE_KERNEL, blocking launches);
+      * GPU_MAX_HW_QUEUES < 2 (every stream of the process on one queue);
+      * DEBUG_HIP_FORCE_GRAPH_QUEUES < 2 (a replayed graph on one stream);
+      * more local ranks than devices (ranks sharing a GPU are time-sliced
+        processes: their queues need not run at the same time) —
+        LOCAL_WORLD_SIZE against the local device count, not the global
+        world size (a multi-node job keeps its hand-offs).
+    Measured support for the rest: every replay of the GPU suite and of the
+    benches asserts zero timed-out waits (ops.xq_timeouts)."""
+    env = os.environ if env is None else env
+    if _dispatch_serialised(env):
+        return False, "kernel dispatch is serialised device-wide (profiling / blocking launches)"
+    hw = _env_int(env, "GPU_MAX_HW_QUEUES", 4)
+    if hw < 2:
+        return False, f"GPU_MAX_HW_QUEUES={hw}: every stream shares one hardware queue"
+    gq = _env_int(env, "DEBUG_HIP_FORCE_GRAPH_QUEUES", 0)
+    if 0 < gq < 2:
+        return False, f"DEBUG_HIP_FORCE_GRAPH_QUEUES={gq}: a replayed graph runs on one stream"
+    local = _env_int(env, "LOCAL_WORLD_SIZE", 1)
+    if device_count is not None and local > max(int(device_count), 1):
+        return False, (f"{local} local ranks on {device_count} device(s): ranks sharing a GPU "
+                       "are time-sliced, their queues need not run concurrently")
+    return True, f"{hw} hardware queues per process, graph branches on distinct streams"
+
+
+XQ_FLAGS, XQ_REASON = handoff_rule()
 
 
 def _xq_words(device, key):
@@ -679,11 +759,49 @@ def _xq_words(device, key):
 def handoff_fault_word(device):
     """The device's sticky hand-off fault word: a wait that gave up sets it,
     and the pretraining loss kernels (scgib_mlp2_recon(_contrastive)_fwd)
-    report a NaN recon loss while it is set — a step whose kernels may have
-    read unwritten data never yields a finite loss.  One word per device,
-    whichever stream asks."""
+    report a NaN recon loss while it is set — a pretraining step whose
+    kernels may have read unwritten data never yields a finite loss.  The
+    fine-tune and domain-adaptation heads end in torch losses (NaN scores
+    would trip binary_cross_entropy's device-side range assert): they rely
+    on the host check instead (check_handoff, at the next forward / optimizer
+    step).  One word per device, whichever stream asks."""
     with torch.cuda.stream(torch.cuda.default_stream(device)):
         return counters(device, "handoff_fault", 1)
+
+
+_HOST_FAULT = {}  # device index -> pinned int32 [1]: set by a wait that gave up
+
+
+def _host_fault_word(device):
+    """A pinned host word the wait kernel also sets when it gives up (a
+    system-scope store): the host reads it without synchronising."""
+    idx = torch.device(device).index or 0
+    w = _HOST_FAULT.get(idx)
+    if w is None:
+        if torch.cuda.is_current_stream_capturing():
+            raise _lib.ScgibError("hand-off fault words must be created outside graph capture "
+                                  "(run one eager step first)")
+        w = _HOST_FAULT[idx] = torch.zeros(1, dtype=torch.int32).pin_memory()
+    return w
+
+
+def check_handoff(device=None):
+    """Raise ScgibError if a cross-queue hand-off wait has given up on
+    ``device`` (every device used so far when None).  Host-side and free (a
+    pinned word, no sync), so it runs at every model forward
+    (ops.aside_guard) and optimizer step (optim.Adam.step): the first of them
+    after a step whose wait timed out raises — that step's own loss is
+    already NaN.  After fixing the cause, clear_handoff_fault()."""
+    idx = None if device is None else (torch.device(device).index or 0)
+    for d, w in _HOST_FAULT.items():
+        if (idx is None or d == idx) and int(w[0]) != 0:
+            raise _lib.ScgibError(
+                f"cuda:{d}: a cross-queue hand-off wait of the GIN encoder pair (ops._xq_handoff: "
+                "scgib_stream_signal / scgib_stream_wait) gave up after 0.2 s — its signal "
+                "kernel was not scheduled concurrently, so kernels of that step may have read "
+                "data before it was written (its loss is NaN).  Hand-off rule: "
+                f"{handoff_rule()[1]}; run with ops.XQ_FLAGS = False if this setup time-slices "
+                "the queues, then ops.clear_handoff_fault(device)")
 
 
 def handoff_fault(device):
@@ -693,6 +811,7 @@ def handoff_fault(device):
 
 def clear_handoff_fault(device):
     handoff_fault_word(device).zero_()
+    _host_fault_word(device).zero_()
 
 
 def _xq_handoff(producer, consumer, key):
@@ -700,10 +819,11 @@ def _xq_handoff(producer, consumer, key):
     (scgib_stream_signal on producer, scgib_stream_wait on consumer)."""
     w = _xq_words(producer.device, key)
     fault = handoff_fault_word(producer.device)
+    host = _host_fault_word(producer.device)
     with torch.cuda.stream(producer):
         _lib.call("scgib_stream_signal", _p(w), _stream())
     with torch.cuda.stream(consumer):
-        _lib.call("scgib_stream_wait", _p(w), _p(fault), _stream())
+        _lib.call("scgib_stream_wait", _p(w), _p(fault), _p(host), _stream())
 
 
 def xq_timeouts(device):
@@ -1213,7 +1333,7 @@ def counters(device, key, n):
     idx = torch.device(device).index or 0
     buf = _COUNTERS.get(idx)
     if buf is None:
-        buf = _COUNTERS[idx] = torch.zeros(_COUNTER_CAP, dtype=torch.int32, device=device)
+        buf = _COUNTERS[idx] = _zeroed_words(_COUNTER_CAP, device)
     rk = (idx, key, torch.cuda.current_stream(device).cuda_stream)
     off, size = _COUNTER_RANGES.get(rk, (None, 0))
     if size < n:
@@ -1231,6 +1351,25 @@ _SCAN_NEXT = {}    # device index -> next free word of the newest arena
 _SCAN_ARENA_WORDS = 1 << 20  # 4 MB: every key and stream of a process, captures included
 
 
+def _zeroed_words(n, device):
+    """n zeroed int32 on ``device``, the fill COMPLETE before this returns.
+    The pool / arena it makes is carved into ranges that kernels on other
+    streams use with no ordering edge to the fill (a later carve
+    for another stream could otherwise race the memset — e.g. the encoder's
+    BatchNorm arrival counters on the main stream against a fill enqueued on
+    the side stream, leaving a counter non-zero and every later last-arriver
+    reduction miscounting).  Made once per device, before any capture (a
+    capture would record the fill into the replayed step instead)."""
+    dev = torch.device(device)
+    if dev.type == "cuda" and torch.cuda.is_current_stream_capturing():
+        raise _lib.ScgibError("arrival-counter / scan-state memory must be created outside "
+                              "graph capture (run one eager step first)")
+    buf = torch.zeros(n, dtype=torch.int32, device=dev)
+    if dev.type == "cuda":
+        torch.cuda.current_stream(dev).synchronize()
+    return buf
+
+
 def _scan_carve(idx, device, size):
     """``size`` zeroed words from the device's arena.  The arena is made by the
     first request (an eager step, before any capture), so a key first seen
@@ -1246,7 +1385,7 @@ def _scan_carve(idx, device, size):
     words = _SCAN_ARENA_WORDS
     while words < size:
         words *= 2
-    arenas.append(torch.zeros(words, dtype=torch.int32, device=device))
+    arenas.append(_zeroed_words(words, device))
     _SCAN_NEXT[idx] = ((size + 63) // 64) * 64
     return arenas[-1][:size]
 

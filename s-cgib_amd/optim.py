@@ -58,6 +58,7 @@ class Adam(torch.optim.Optimizer):
     @torch.no_grad()
     def step(self, closure=None):
         loss = None
+        ops.check_handoff()  # an earlier step's hand-off wait gave up: raise before updating
         if closure is not None:
             with torch.enable_grad():
                 loss = closure()

@@ -75,11 +75,17 @@ def gin_relu_masks(out, layers):
     output `out` (ops._GinEncoder): r > 0 from the saved r, and
     scale z2 + shift > 0 from the saved z2 and BN record — for the oracle's
     relu_masks (scgib_ref.gin_encoder).  The latter in fp64: the exact
-    product plus one rounding has the sign of the kernels' fused multiply-add."""
+    product plus one rounding has the sign of the kernels' fused multiply-add.
+    A layer whose forward did not store r (ops.STORE_R off) gets it from
+    ops.gin_hidden — the forward's own chain, so the same decisions."""
+    ops = importlib.import_module("s-cgib_amd").ops
     t = out.grad_fn.saved_tensors
+    params = t[4 * layers: 10 * layers]
     masks = []
     for l in range(layers):
-        _, r, z2, stat = t[4 * l: 4 * l + 4]
+        agg, r, z2, stat = t[4 * l: 4 * l + 4]
+        if r is None:
+            r = ops.gin_hidden(agg, params[6 * l], params[6 * l + 1])
         stat = stat.double()
         m2 = (stat[2] * z2.double() + stat[3]) > 0
         masks.append(((r > 0).cpu(), m2.cpu()))

@@ -57,8 +57,10 @@ def main(out_dir):
     rank, world, local = pkg.dist.init_from_env()
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
-    # both ranks share one GPU (time-sliced processes): no signal / wait
-    # hand-offs between one process's queues (as bench.py does in that case)
+    # both ranks share one GPU (time-sliced processes): the hand-off rule
+    # refuses the signal / wait kernels (as in bench.py)
+    ok, why = pkg.ops.handoff_rule(torch.cuda.device_count())
+    assert not ok, why
     pkg.ops.XQ_FLAGS = False
     F_in = pkg.synth.WORKLOADS[WORKLOAD][2]
     B = B_TOTAL // world

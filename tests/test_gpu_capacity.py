@@ -156,6 +156,36 @@ def test_graph_replay_matches_exact_over_batches(pkg, dev, k, fork_losses, monke
     assert pkg.ops.xq_timeouts(dev) == t0
 
 
+def test_capacity_step_r_recompute_bitwise(pkg, dev, monkeypatch):
+    """The whole pretrain step in capacity mode (padded rows, device dims:
+    the recompute kernels' zero-padding and clamped-row paths) with the
+    hidden activation r recomputed in the backward vs stored by the forward
+    (ops.STORE_R): losses, every gradient and BN buffer bitwise equal."""
+    hosts = _batches(pkg, (21, 22))
+    n_cap, e_cap, mgn, caps = pkg.graph.StaticBatch.capacities(hosts, 1, slack=1.05)
+    static = pkg.graph.StaticBatch(B, n_cap, e_cap, F_IN, mgn, caps, dev)
+    base = _model(pkg, dev)
+    res = []
+    for store in (True, False):
+        monkeypatch.setattr(pkg.ops, "STORE_R", store)
+        m = copy.deepcopy(base)
+        losses = []
+        for i, gh in enumerate(hosts):
+            static.load(static.pad(gh))
+            losses.append(_step(m, static.graph, static.x, _noise(n_cap, dev, 300 + i), dev))
+        torch.cuda.synchronize()
+        res.append((torch.stack(losses), {k: p.grad.clone() for k, p in m.named_parameters()
+                                          if p.grad is not None},
+                    {k: b.clone() for k, b in m.named_buffers()}))
+    (la, ga, ba), (lb, gb, bb) = res
+    assert torch.equal(la, lb)
+    assert ga.keys() == gb.keys()
+    for k in ga:
+        assert torch.equal(ga[k], gb[k]), k
+    for k in ba:
+        assert torch.equal(ba[k], bb[k]), k
+
+
 def test_static_batch_rejects_oversized(pkg, dev):
     small, big = _batches(pkg, (8,)), None
     n_cap, e_cap, mgn, caps = pkg.graph.StaticBatch.capacities(small, 1)
@@ -419,11 +449,45 @@ def test_handoff_timeout_poisons_loss(pkg, dev):
     assert torch.isfinite(ok).all()
     w = ops._xq_words(dev, "test_orphan_wait")
     ops._lib.call("scgib_stream_wait", ops._p(w), ops._p(ops.handoff_fault_word(dev)),
-                  ops._stream())
+                  ops._p(ops._host_fault_word(dev)), ops._stream())
     torch.cuda.synchronize()
     assert int(w[2].item()) == 1 and ops.handoff_fault(dev)
+    # loud: the pinned host word is set too, so the next
+    # model forward / optimizer step raises, naming the hand-off
+    assert int(ops._host_fault_word(dev)[0]) == 1
+    with pytest.raises(ops._lib.ScgibError, match="hand-off"):
+        _step(m, g, g.ndata["x"], (ug, uf), dev)
+    opt = pkg.optim.Adam(m.parameters(), lr=1e-4)
+    with pytest.raises(ops._lib.ScgibError, match="hand-off"):
+        opt.step()
+    # the device word alone (a caller that bypasses the host check): the
+    # step's recon loss, and so the total, is NaN
+    ops._host_fault_word(dev).zero_()
     bad = _step(m, g, g.ndata["x"], (ug, uf), dev)
-    assert torch.isnan(bad[2]) and torch.isnan(bad[3])  # recon, and so the total
+    assert torch.isnan(bad[2]) and torch.isnan(bad[3])
     ops.clear_handoff_fault(dev)
     again = _step(m, g, g.ndata["x"], (ug, uf), dev)
     assert torch.isfinite(again).all()
+
+
+def test_handoff_fault_raises_in_finetune(pkg, dev):
+    """the fine-tune head ends in torch's BCE (NaN scores would
+    trip its device-side range assert), so a hand-off fault reaches it as the
+    host check: with the pinned host word set, the next fine-tune forward
+    raises a ScgibError naming the hand-off; cleared, the step is finite."""
+    import finetune_bench
+    ops = pkg.ops
+    ops.clear_handoff_fault(dev)
+    ft, _ = finetune_bench.make_finetune_model(pkg, 9, 8, dev)
+    gh, _ = pkg.graph.collate_pyg(pkg.synth.molecules(8, "molhiv", seed=3))
+    g = gh.to(dev)
+    x = F.normalize(g.ndata["x"].float())
+    tgt = torch.randint(0, 2, (8, 1), device=dev).float()
+    scores, *_ = ft(g, x, None, None, 1, None, 2, dev, 8)
+    assert torch.isfinite(ft.loss(scores, tgt))
+    ops._host_fault_word(dev).fill_(1)  # as a wait that gave up sets it
+    with pytest.raises(ops._lib.ScgibError, match="hand-off"):
+        ft(g, x, None, None, 1, None, 2, dev, 8)
+    ops.clear_handoff_fault(dev)
+    scores, *_ = ft(g, x, None, None, 1, None, 2, dev, 8)
+    assert torch.isfinite(ft.loss(scores, tgt))

@@ -500,6 +500,46 @@ def test_xq_handoffs_off_under_serialised_dispatch(pkg, monkeypatch):
         monkeypatch.delenv(k)
 
 
+def test_handoff_rule(pkg):
+    """ops.handoff_rule — the signal / wait hand-offs only
+    where the step's two chains can be on hardware queues the device runs
+    concurrently: not under serialised dispatch, not with one hardware queue
+    per process or one graph-execution stream, not with more local ranks than
+    devices (LOCAL_WORLD_SIZE, not the global world: a multi-node job with one
+    rank per GPU keeps them)."""
+    rule = pkg.ops.handoff_rule
+    assert rule(1, {})[0]
+    assert rule(8, {"LOCAL_WORLD_SIZE": "8", "WORLD_SIZE": "16"})[0]   # 2 nodes x 8 GPUs
+    assert rule(None, {"LOCAL_WORLD_SIZE": "2"})[0]                    # device count unknown
+    assert rule(1, {"GPU_MAX_HW_QUEUES": "4", "DEBUG_HIP_FORCE_GRAPH_QUEUES": "4"})[0]
+    for env, dc in (({"LOCAL_WORLD_SIZE": "2"}, 1), ({"LOCAL_WORLD_SIZE": "9"}, 8),
+                    ({"GPU_MAX_HW_QUEUES": "1"}, 1), ({"DEBUG_HIP_FORCE_GRAPH_QUEUES": "1"}, 1),
+                    ({"AMD_SERIALIZE_KERNEL": "3"}, 1), ({"ROCPROF_KERNEL_TRACE": "1"}, 8)):
+        ok, why = rule(dc, env)
+        assert not ok and why, env
+    # the module default follows the process environment
+    assert pkg.ops.XQ_FLAGS == rule()[0]
+
+
+def test_check_handoff_raises_on_host_fault_word(pkg):
+    """The host half of the hand-off fault: a set pinned word makes
+    ops.check_handoff (run by every model forward and optimizer step) raise a
+    ScgibError that names the hand-off; clean words pass."""
+    import torch
+    ops = pkg.ops
+    key = 977  # a device index no real device uses
+    ops._HOST_FAULT[key] = torch.zeros(1, dtype=torch.int32)
+    try:
+        ops.check_handoff()
+        ops._HOST_FAULT[key][0] = 1
+        with pytest.raises(pkg._lib.ScgibError, match="hand-off"):
+            ops.check_handoff()
+        with pytest.raises(pkg._lib.ScgibError, match="hand-off"):
+            ops.aside_guard(lambda: None)()
+    finally:
+        ops._HOST_FAULT.pop(key, None)
+
+
 def test_scan_arena_carves_disjoint_zeroed_ranges(pkg):
     """ops._scan_carve (the scan-state arena): disjoint, 256-B aligned, zeroed
     ranges from one arena; a request past its end opens a new arena (the old

@@ -140,14 +140,15 @@ def layer_fwd_flops(n, e, d_in):
     return 2 * n * 64 * (d_in + 64)
 
 
-def layer_bwd_bytes(n, e, d_in, store_r=False):
+def layer_bwd_bytes(n, e, d_in, store_r=False, wg=True):
     """Algorithmic bytes of one GIN layer backward launch (gin_bwd5r_k /
     gin_bwd5_k): the dy, z2 and agg rows read (+ r's when the
     forward stored it), W1/b1/W2 + BN coefficients, d(agg) written.  The
     per-workgroup dW slabs are NOT counted: they are partials of a 33 KB
-    gradient, not bytes the layer needs (their cost shows in `traffic`)."""
-    return (4 * n * ((3 if store_r else 2) * 64 + d_in) + 4 * (64 * d_in + 64 * 64 + 7 * 64)
-            + 4 * n * d_in)
+    gradient, not bytes the layer needs (their cost shows in `traffic`).
+    wg False (a frozen layer, need_w = 0): the agg rows are not read."""
+    return (4 * n * ((3 if store_r else 2) * 64 + (d_in if wg else 0))
+            + 4 * (64 * d_in + 64 * 64 + 7 * 64) + 4 * n * d_in)
 
 
 def stats_bytes(n, e, d):
@@ -162,14 +163,18 @@ def no_flops(n, e, d):
     return 0
 
 
-def layer_bwd_flops(n, e, d_in):
-    return 4 * n * 64 * (64 + d_in)  # dW2, dr, dW1, d(agg)
+def layer_bwd_flops(n, e, d_in, wg=True):
+    return (4 if wg else 2) * n * 64 * (64 + d_in)  # dW2, dr, dW1, d(agg) (frozen: dr, d(agg))
 
 
 def _call_meta(fn, m):
     """bytes / flops of one launch from its meta (n, e, d_in[, r stored])."""
-    if fn in (layer_fwd_bytes_inclusive, layer_bwd_bytes):
+    if fn is layer_fwd_bytes_inclusive:
         return fn(m["n"], m["e"], m["d_in"], m.get("r", False))
+    if fn is layer_bwd_bytes:
+        return fn(m["n"], m["e"], m["d_in"], m.get("r", False), m.get("wg", True))
+    if fn is layer_bwd_flops:
+        return fn(m["n"], m["e"], m["d_in"], m.get("wg", True))
     return fn(m["n"], m["e"], m["d_in"])
 
 
@@ -569,6 +574,25 @@ WORKLOAD_DESC = {"qm9": "QM9-like", "molpcba": "ogbg-molpcba-like", "pcqm4mv2": 
                  "molhiv": "ogbg-molhiv-like"}
 
 
+def finetune_leg(a, dev):
+    """BASELINE.json configs[4] in the same run (finetune_bench.run: the molhiv
+    fine-tune step from the shipped checkpoint's weights, B = 32, captured and
+    replayed, a.steps timed after a.warmup), its dominant kernel's roofline and
+    its oracle CPU baseline (half the pretrain leg's CPU budget)."""
+    import finetune_bench
+    global RUN_CONFIG
+    keep = RUN_CONFIG
+    ns = SimpleNamespace(batch=32, pool=a.pool, steps=a.steps, warmup=a.warmup,
+                         no_kernel_timer=a.no_kernel_timer, no_cpu_baseline=a.no_cpu_baseline,
+                         cpu_seconds=a.cpu_seconds, no_ego_prefetch=a.no_ego_prefetch)
+    try:
+        line = finetune_bench.run(sys.modules[__name__], ns, dev)
+    finally:
+        RUN_CONFIG = keep
+    return {k: line[k] for k in ("metric", "value", "unit", "ms_per_step", "steps", "warmup",
+                                 "dtype", "data", "config", "roofline", "cpu_baseline")}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -604,6 +628,8 @@ def main():
     ap.add_argument("--finetune", choices=["molhiv"], default=None,
                     help="time the fine-tune step of BASELINE.json configs[4] instead "
                          "(finetune_bench.py; --batch defaults to 32 there)")
+    ap.add_argument("--no-finetune", action="store_true",
+                    help="skip the fine-tune leg (configs[4]) the N = 1 line carries in 'finetune'")
     a = ap.parse_args()
     pkg.ops.STORE_R = not a.recompute_r
     if a.finetune:
@@ -856,6 +882,10 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         cpu = cpu_baselines(a.k, a.gin_layers, a.workload, a.batch, a.cpu_seconds)
+    ft = None
+    if rank == 0 and world == 1 and not a.no_finetune:
+        ft = finetune_leg(a, dev)
+        progress("fine-tune leg done")
 
     if rank == 0:
         total_graphs = world * a.batch * a.steps
@@ -911,6 +941,9 @@ def main():
                      "sub-tiles per workgroup, its start-of-kernel chain amortised), mfma_frac "
                      "= flops / time / 157.3 TF/s"),
             "cpu_baseline": cpu,
+            # BASELINE.json configs[4] (molhiv fine-tune from the shipped
+            # checkpoint, B = 32, 1 GPU): its own timed replay after this leg
+            "finetune": ft,
         }
         print(json.dumps(line), flush=True)
     if world > 1:

@@ -45,14 +45,17 @@ def load_pretrained(pkg, args):
     return pkg.models.model_from_state(levels, cfg, sd, args), levels, cfg
 
 
-def make_finetune_model(pkg, F_in, B, dev, seed=0):
+def make_finetune_model(pkg, F_in, B, dev, seed=0, dataset="ogbg-molhiv", num_classes=1):
+    """Mainmodel_finetuning around the shipped checkpoint's chain: molhiv's
+    BCE head (exp_molhiv.py, num_classes 1) by default; Mutagenicity's CE
+    head with dataset="Mutagenicity", num_classes=2 (exp_tudataset.py)."""
     args = SimpleNamespace(recons_type="adj", useAtt=1, readout_f="sum", d_transfer=32,
                            batch_size=B, gin_layers=5, task="graph_classification",
-                           dataset="ogbg-molhiv", device=dev)
+                           dataset=dataset, device=dev)
     torch.manual_seed(seed)
     pre, levels, cfg = load_pretrained(pkg, args)
     k = int(cfg["k_transition"])
-    ft = pkg.models.Mainmodel_finetuning(args, F_in, 64, 4, 4, k, 1, pre, "GIN")
+    ft = pkg.models.Mainmodel_finetuning(args, F_in, 64, 4, 4, k, num_classes, pre, "GIN")
     return ft.to(dev).train(), k
 
 
@@ -134,6 +137,13 @@ def run(bench, a, dev):
         dict.__setitem__(gx.ndata, "x", F.normalize(gh.ndata["x"].float()))
         padded.append(static.pad(gx))
     pool = static.pool(padded)
+    # the ego-nets one batch ahead, as the pretrain bench (graph.EgoPrefetch):
+    # each step builds the next batch's on the encoder pair's idle queue during
+    # the loss section, and the next batch load moves them in with the batch
+    prefetch = None
+    if not a.no_ego_prefetch:
+        prefetch = pkg.graph.EgoPrefetch(static, pool)
+        prefetch.prime()
     # the targets walk their own resident pool in step with the batches: one
     # pool-copy launch per step (its own cursor, advanced like the batch's)
     tdev = [t.to(dev).contiguous() for t in targets]
@@ -143,12 +153,14 @@ def run(bench, a, dev):
     one = torch.ones((), dtype=torch.float32, device=dev)  # d loss / d loss, resident (no fill per step)
 
     def body():
-        static.load_next(pool)
+        static.load_next(pool, prefetch)
         pkg._lib.call("scgib_pool_copy", pkg.ops._p(ttable), len(tdev), pkg.ops._p(tcursor),
                       pkg.ops._p(tg), tg.numel() * 4, pkg.ops._stream())
         scores, *_ = ft(static.graph, static.x, None, None, 1, None, 2, dev, B)
         loss = ft.loss(scores, tg)
         torch.autograd.backward(loss, one)
+        if prefetch is not None:
+            prefetch.join()  # (no-op: the encoder pair's backward joined it)
         return loss.detach()
 
     side = torch.cuda.Stream()
@@ -214,7 +226,9 @@ def run(bench, a, dev):
         "config": {"workload": f"molhiv fine-tune step, batch {B}, k={k} (BASELINE.json "
                                "configs[4]), Mainmodel_finetuning + BCE + Adam(1e-3, wd 1e-5)",
                    "launch": "hip-graph replay (capacity mode)",
-                   "ego_build": "at the head of the step (device k-hop builder)",
+                   "ego_build": ("in the step, for the batch the next step loads "
+                                 "(graph.EgoPrefetch)" if prefetch is not None
+                                 else "at the head of the step (device k-hop builder)"),
                    "trainable": sum(p.numel() for p in ft.parameters() if p.requires_grad),
                    "nodes_per_batch": round(n_nodes, 1), "parallelism": "dp1",
                    "final_loss": round(final_loss, 4)},

@@ -274,15 +274,20 @@ int scgib_gin_bwd_stats_bn_fold(const float *dh, const int32_t *rowptr_t, const 
                                 scgib_stream_t stream);
 /* layer backward: `pending` (NULL: coef is read) finishes the deferred
  * scgib_gin_bwd_stats_bn of the same layer (coef may then be NULL). */
+/* need_w = 0: the layer's W1 / b1 / W2 / b2 take no gradient (frozen: the
+ * fine-tune freezing quirk, models.py:424-434) — only d(agg) (layer 0: dWt)
+ * is formed, by the same chains (bitwise the need_w = 1 values); the dW
+ * products and slabs are skipped (layer 0: only its dWt slab part is
+ * written; agg may then be NULL; r must be given). */
 int scgib_gin_layer0_bwd(const float *dy, const float *z2, const float *r, const float *agg,
                          const float *aggx, int32_t n_feat, const float *stat,
                          const float *coef, const float *w1, const float *b1, const float *w2,
-                         int64_t n_nodes, float *slab, const int32_t *dims,
+                         int64_t n_nodes, float *slab, int32_t need_w, const int32_t *dims,
                          const scgib_bn_bwd_pending *pending, scgib_stream_t stream);
 int scgib_gin_layer_bwd(const float *dy, const float *z2, const float *r, const float *agg,
                         int32_t d_in, const float *stat, const float *coef, const float *w1,
                         const float *b1, const float *w2, int64_t n_nodes, float *dagg,
-                        float *slab, float *wgrad, const int32_t *dims,
+                        float *slab, float *wgrad, int32_t need_w, const int32_t *dims,
                         const scgib_bn_bwd_pending *pending, scgib_stream_t stream);
 int scgib_gin_hidden(const float *agg, int32_t d_in, const float *w1, const float *b1,
                      int64_t n_nodes, float *r, scgib_stream_t stream);

@@ -89,7 +89,7 @@ SIGNATURES = {
                                             _P, _P, _P, _P, _P, _P, _F, _F, _P, _P, _P, _P, _P,
                                             _P, _P, _I32, _P]),
     "scgib_gin_layer0_bwd": (ctypes.c_int, [_P, _P, _P, _P, _P, _I32, _P, _P, _P, _P, _P, _I64,
-                                            _P, _P, _P, _P]),
+                                            _P, _I32, _P, _P, _P]),
     "scgib_gin_hidden": (ctypes.c_int, [_P, _I32, _P, _P, _I64, _P, _P]),
     "scgib_gin_bn_gpart_offset": (_I64, [_I64]),
     "scgib_gin_defer_max_nodes": (_I64, []),
@@ -117,7 +117,7 @@ SIGNATURES = {
     "scgib_gin_bwd_stats": (ctypes.c_int, [_P, _P, _P, _F, _P, _P, _I64, _P, _P, _P, _P]),
     "scgib_bn_bwd_finalize": (ctypes.c_int, [_P, _I64, _I32, _P, _P, _P, _P, _P]),
     "scgib_gin_layer_bwd": (ctypes.c_int, [_P, _P, _P, _P, _I32, _P, _P, _P, _P, _P, _I64, _P,
-                                           _P, _P, _P, _P, _P]),
+                                           _P, _P, _I32, _P, _P, _P]),
     "scgib_recon_partials_floats": (_I64, [_I64]),
     "scgib_recon_fwd": (ctypes.c_int, [_P, _P, _P, _I64, _I64, _P, _P, _P, _P, _P]),
     "scgib_recon_bwd": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _I64, _P, _P, _P, _P]),

@@ -1181,7 +1181,12 @@ __global__ __launch_bounds__(1024) void bn_bwd_finalize_k(const float *__restric
 // until the tile's last products) with the forward's own call, mma_pf<32>
 // over the same [64][33] layouts, + b1, fmaxf: bitwise the forward's r;
 // rows past the tile's valid rows are 0, as the stored path loads them.
-template <int DIN, bool BN = true, bool PRE = false, bool RECON = false, bool RC = false>
+// WG = false (PRE only): the layer's W1 / W2 / biases are frozen (the
+// fine-tune freezing quirk) — dr and d(agg0) by the same chains as with WG
+// (mma_pf instead of mma_pf2: one product per call, the same k order), no
+// dW1 / dW2 / db products or slab part, no agg tile; dWt is still formed.
+template <int DIN, bool BN = true, bool PRE = false, bool RECON = false, bool RC = false,
+          bool WG = true>
 __global__ __launch_bounds__(256, (DIN <= 64 && !RECON ? 2 : 1)) void gin_bwd_k(
     const float *__restrict__ dy, const float *__restrict__ z2, const float *__restrict__ r,
     const float *__restrict__ agg, const float *__restrict__ stat,
@@ -1191,6 +1196,7 @@ __global__ __launch_bounds__(256, (DIN <= 64 && !RECON ? 2 : 1)) void gin_bwd_k(
     ReconArgs rec, int pre_f = kPreF, const float *__restrict__ b1 = nullptr) {
     static_assert(!PRE || DIN == 32, "transfer_d fold: layer 0 only");
     static_assert(!RC || PRE, "r recomputed in the layer-0 backward only (gin_bwd5r_k: d_in = 64)");
+    static_assert(WG || (PRE && !RC), "frozen weights: the layer-0 stored-r backward only");
     static_assert(!RECON || !BN, "the recon backward is fused into the dense head MLP");
     const int64_t n = eff_count(dims, 0, ncap);
     constexpr int LDA = DIN + 1;
@@ -1281,6 +1287,7 @@ __global__ __launch_bounds__(256, (DIN <= 64 && !RECON ? 2 : 1)) void gin_bwd_k(
                        r0 * 4 + (tid & 3), (tid >> 2) < m, zero);
     };
     auto load_agg = [&](int64_t t) {
+        if constexpr (!WG) return;  // agg is read only by dW1
         const int64_t r0 = t * TM;
         const int m = static_cast<int>(n - r0 < TM ? (n - r0 > 0 ? n - r0 : 0) : TM);
 #pragma unroll
@@ -1415,9 +1422,13 @@ __global__ __launch_bounds__(256, (DIN <= 64 && !RECON ? 2 : 1)) void gin_bwd_k(
         // dW2 += dz2^T r  (sub-tile j-block wr, k-block wc)
         // dr = dz2 W2  (rows wr, cols wc); the two products alternate
         f32x16 dr = zero16();
-        mma_pf2<64, true, true, false, true>(sD + wr * 32, LDH, sR + wc * 32, LDH, accW2,
-                                             sD + wr * 32 * LDH, LDH, sW2 + wc * 32, LDH, dr);
-        db2 = col_sum16(db2, sD + q * LDH + ch, 4 * LDH);
+        if constexpr (WG) {
+            mma_pf2<64, true, true, false, true>(sD + wr * 32, LDH, sR + wc * 32, LDH, accW2,
+                                                 sD + wr * 32 * LDH, LDH, sW2 + wc * 32, LDH, dr);
+            db2 = col_sum16(db2, sD + q * LDH + ch, 4 * LDH);
+        } else {
+            dr = mma_pf<64, false, true>(sD + wr * 32 * LDH, LDH, sW2 + wc * 32, LDH, zero16());
+        }
         __syncthreads();  // all reads of dz2 done
         // dz1 = dr * [r > 0]  -> sD
 #pragma unroll
@@ -1430,7 +1441,7 @@ __global__ __launch_bounds__(256, (DIN <= 64 && !RECON ? 2 : 1)) void gin_bwd_k(
         // RC: the agg tile is already in the d(agg0) buffer (the r recompute's
         // operand), the dead r buffer takes d(agg0) instead — same layouts
         float *const aggT = RC ? sPD : sA, *const daggT = RC ? sRA : sPD;
-        if constexpr (!RC) {
+        if constexpr (!RC && WG) {
 #pragma unroll
             for (int k = 0; k < AK; ++k) {
                 const int idx = tid + 256 * k, rr = idx / AQ, cq = idx % AQ;
@@ -1439,7 +1450,7 @@ __global__ __launch_bounds__(256, (DIN <= 64 && !RECON ? 2 : 1)) void gin_bwd_k(
             }
             __syncthreads();
         }
-        db1 = col_sum16(db1, sD + q * LDH + ch, 4 * LDH);
+        if (WG) db1 = col_sum16(db1, sD + q * LDH + ch, 4 * LDH);
         // dW1 += dz1^T agg  (64 x DIN) ; d(agg) = dz1 W1  (TM x DIN)
 #pragma unroll
         for (int q1 = 0; q1 < NW1; ++q1) {
@@ -1447,8 +1458,11 @@ __global__ __launch_bounds__(256, (DIN <= 64 && !RECON ? 2 : 1)) void gin_bwd_k(
             if (sub < NSUB1) {
                 const int jb = sub & 1, kb = sub >> 1;  // j-block (rows of dW1 / d(agg)), k-block
                 f32x16 da = zero16();
-                mma_pf2<64, true, true, false, true>(sD + jb * 32, LDH, aggT + kb * 32, LDA, accW1[q1],
-                                                     sD + jb * 32 * LDH, LDH, sW1 + kb * 32, LDA, da);
+                if constexpr (WG)
+                    mma_pf2<64, true, true, false, true>(sD + jb * 32, LDH, aggT + kb * 32, LDA, accW1[q1],
+                                                         sD + jb * 32 * LDH, LDH, sW1 + kb * 32, LDA, da);
+                else
+                    da = mma_pf<64, false, true>(sD + jb * 32 * LDH, LDH, sW1 + kb * 32, LDA, zero16());
 #pragma unroll
                 for (int reg = 0; reg < 16; ++reg) {
                     const int row = jb * 32 + acc_row(reg, l);
@@ -1465,6 +1479,17 @@ __global__ __launch_bounds__(256, (DIN <= 64 && !RECON ? 2 : 1)) void gin_bwd_k(
     }
     // per-workgroup slab
     float *sl = slab + static_cast<int64_t>(blockIdx.x) * SLAB;
+    if constexpr (!WG) {  // frozen W1 / W2: only the dWt part
+        if (w == 0) {
+#pragma unroll
+            for (int reg = 0; reg < 16; ++reg) {
+                const int i = acc_row(reg, l), j = l & 31;
+                if (j < pre_f) sl[64 * 64 + 64 * DIN + 128 + i * pre_f + j] = accWt[reg];
+            }
+        }
+        SCGIB_MARK(4);
+        return;
+    }
 #pragma unroll
     for (int reg = 0; reg < 16; ++reg) {
         const int j = wr * 32 + acc_row(reg, l), k = wc * 32 + (l & 31);
@@ -1537,7 +1562,12 @@ constexpr int SM = 32;   // rows per sub-tile
 constexpr int LDR = 68;  // row-major 64-wide images (= 4 mod 64: b128 reads conflict free)
 constexpr int LDT = 36;  // transposed [64][32] images (rows k-contiguous)
 
-template <int DIN>
+// WG = false: a frozen layer (the fine-tune freezing quirk, models.py:424-434:
+// no parameter of it takes a gradient) — only the data-gradient chains run,
+// dr and d(agg), each exactly as with WG (bitwise the same d(agg)); the
+// dW products, the agg rows (read only by dW1), the transposed dz images
+// and the slab are skipped.
+template <int DIN, bool WG = true>
 __global__ __launch_bounds__(256, 2) void gin_bwd5_k(
     const float *__restrict__ dy, const float *__restrict__ z2, const float *__restrict__ r,
     const float *__restrict__ agg, const float *__restrict__ stat,
@@ -1588,11 +1618,13 @@ __global__ __launch_bounds__(256, 2) void gin_bwd5_k(
             row = row < last ? row : last;
             nx[2][i] = r[row * 64 + c];
         }
+        if constexpr (WG) {
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            int64_t row = s * SM + 8 * w + i;
-            row = row < last ? row : last;
-            nx[3][i] = agg[row * DIN + c];
+            for (int i = 0; i < 8; ++i) {
+                int64_t row = s * SM + 8 * w + i;
+                row = row < last ? row : last;
+                nx[3][i] = agg[row * DIN + c];
+            }
         }
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
@@ -1629,7 +1661,7 @@ __global__ __launch_bounds__(256, 2) void gin_bwd5_k(
     }
     if (nv > 0) {
         put_t(sRT, 2);
-        put_t(sAT, 3);
+        if (WG) put_t(sAT, 3);
     }
     // the weight registers complete here: a load still counted at the loop
     // entry makes hipcc wait vmcnt(0..3) at their uses in EVERY iteration
@@ -1658,9 +1690,11 @@ __global__ __launch_bounds__(256, 2) void gin_bwd5_k(
                 d[i] = 8 * w + i < nv ? v : 0.f;
                 sD[(8 * w + i) * LDR + c] = d[i];
             }
-            float4 *p = reinterpret_cast<float4 *>(sDT + c * LDT + 8 * w);
-            p[0] = make_float4(d[0], d[1], d[2], d[3]);
-            p[1] = make_float4(d[4], d[5], d[6], d[7]);
+            if constexpr (WG) {
+                float4 *p = reinterpret_cast<float4 *>(sDT + c * LDT + 8 * w);
+                p[0] = make_float4(d[0], d[1], d[2], d[3]);
+                p[1] = make_float4(d[4], d[5], d[6], d[7]);
+            }
         }
         const int64_t next = s + G;
         const int next_nv = next < nsub ? rows_of(next) : 0;  // block-uniform
@@ -1674,9 +1708,9 @@ __global__ __launch_bounds__(256, 2) void gin_bwd5_k(
                 const int row = acc_row(reg, l), col = q * 32 + li;
                 const float v = dr[reg] * (sRT[col * LDT + row] > 0.f ? 1.f : 0.f);
                 sE[row * LDR + col] = v;
-                sET[col * LDT + row] = v;
+                if (WG) sET[col * LDT + row] = v;
             }
-        } else {   // dW2 rows 32q.. += dz2^T r (db2 from the A operand)
+        } else if constexpr (WG) {   // dW2 rows 32q.. += dz2^T r (db2 from the A operand)
             mma_kk4x2<4>(sDT + (q * 32 + li) * LDT + 4 * kk, sRT + li * LDT + 4 * kk,
                          sRT + (32 + li) * LDT + 4 * kk, accA, accB, dbias);
         }
@@ -1684,8 +1718,9 @@ __global__ __launch_bounds__(256, 2) void gin_bwd5_k(
         if (it == 0) SCGIB_MARK(3);
         if (next_nv > 0) put_t(sRT, 2);
         if (nw) {  // dW1 rows 32q.. += dz1^T agg (db1 from the A operand)
-            mma_kk4x2<4>(sET + (q * 32 + li) * LDT + 4 * kk, sAT + li * LDT + 4 * kk,
-                         sAT + (32 + li) * LDT + 4 * kk, accA, accB, dbias);
+            if constexpr (WG)
+                mma_kk4x2<4>(sET + (q * 32 + li) * LDT + 4 * kk, sAT + li * LDT + 4 * kk,
+                             sAT + (32 + li) * LDT + 4 * kk, accA, accB, dbias);
         } else {   // d(agg) block q = dz1 W1[:, 32q..] -> staging
             const f32x16 da = mma_rk4<8>(sE + li * LDR + 4 * kk, wreg, zero16());
 #pragma unroll
@@ -1693,7 +1728,7 @@ __global__ __launch_bounds__(256, 2) void gin_bwd5_k(
         }
         lds_barrier();  // d(agg) staged; agg and dz1 consumed
         if (it == 0) SCGIB_MARK(4);
-        if (next_nv > 0) put_t(sAT, 3);
+        if (WG && next_nv > 0) put_t(sAT, 3);
         // d(agg) rows: full-row float4 stores (after the loads: in-order vmcnt)
         {
             const int c4 = tid & 15, rs = tid >> 4;
@@ -1709,6 +1744,7 @@ __global__ __launch_bounds__(256, 2) void gin_bwd5_k(
         nv = next_nv;
     }
     SCGIB_MARK(5);
+    if constexpr (!WG) return;
     // per-workgroup slab: dW2 | dW1 | db2 | db1 (gin_bwd_k layout)
     float *sl = slab + static_cast<int64_t>(blockIdx.x) * SLAB;
     float *dw = nw ? sl + 64 * 64 : sl;  // N: dW1 [64][DIN], T: dW2 [64][64]
@@ -2359,12 +2395,14 @@ extern "C" int scgib_gin_layer_bwd(const float *dy, const float *z2, const float
                                    const float *agg, int32_t d_in, const float *stat,
                                    const float *coef, const float *w1, const float *b1,
                                    const float *w2, int64_t n_nodes, float *dagg, float *slab,
-                                   float *wgrad, const int32_t *dims,
+                                   float *wgrad, int32_t need_w, const int32_t *dims,
                                    const scgib_bn_bwd_pending *pending, scgib_stream_t stream) {
     if (n_nodes <= 0 || (d_in != 32 && d_in != 64)) return SCGIB_EINVAL;
-    if (!dy || !z2 || !agg || !stat || (!coef && !pending) || !w1 || !w2 || !dagg || !slab)
+    if (!dy || !z2 || !stat || (!coef && !pending) || !w1 || !w2 || !dagg)
         return SCGIB_EINVAL;
-    if (!r && (d_in != 64 || !b1)) return SCGIB_EINVAL;  // recompute: d_in = 64, needs b1
+    if (need_w && (!agg || !slab)) return SCGIB_EINVAL;
+    if (!r && (d_in != 64 || !b1 || !agg)) return SCGIB_EINVAL;  // recompute: d_in = 64, needs b1
+    if (!need_w && (d_in != 64 || !r)) return SCGIB_EUNSUPPORTED;  // frozen: stored-r d_in = 64
     if (pending && (!pending->gpart || !pending->dgamma || !pending->dbeta)) return SCGIB_EINVAL;
     const scgib_bn_bwd_pending pd = pending ? *pending : scgib_bn_bwd_pending{};
     const int64_t nt = scgib_gin_tiles(n_nodes);
@@ -2372,12 +2410,14 @@ extern "C" int scgib_gin_layer_bwd(const float *dy, const float *z2, const float
     hipStream_t st = as_stream(stream);
     if (d_in == 32)
         gin_bwd_k<32><<<grid, 256, 0, st>>>(dy, z2, r, agg, stat, coef, w1, w2, n_nodes, nt, dagg, slab, dims, nullptr, pd, ReconArgs{});
+    else if (!need_w)
+        gin_bwd5_k<64, false><<<grid, 256, 0, st>>>(dy, z2, r, agg, stat, coef, w1, w2, n_nodes, bwd5_subtiles(n_nodes), dagg, slab, dims, pd);
     else if (r)
         gin_bwd5_k<64><<<grid, 256, 0, st>>>(dy, z2, r, agg, stat, coef, w1, w2, n_nodes, bwd5_subtiles(n_nodes), dagg, slab, dims, pd);
     else
         gin_bwd5r_k<64><<<grid, 256, 0, st>>>(dy, z2, agg, stat, coef, w1, b1, w2, n_nodes, bwd5_subtiles(n_nodes), dagg, slab, dims, pd);
     const int rc = launch_status();
-    if (rc != SCGIB_OK || !wgrad) return rc;  // wgrad NULL: the caller reduces the slabs
+    if (rc != SCGIB_OK || !wgrad || !need_w) return rc;  // wgrad NULL: the caller reduces the slabs
     return launch_slab_reduce(slab, grid, 64 * 64 + 64 * static_cast<int64_t>(d_in) + 128, wgrad, st);
 }
 
@@ -2658,15 +2698,21 @@ extern "C" int scgib_gin_layer0_bwd(const float *dy, const float *z2, const floa
                                     const float *agg, const float *aggx, int32_t n_feat,
                                     const float *stat, const float *coef, const float *w1,
                                     const float *b1, const float *w2, int64_t n_nodes, float *slab,
-                                    const int32_t *dims, const scgib_bn_bwd_pending *pending,
-                                    scgib_stream_t stream) {
-    if (n_nodes <= 0 || !dy || !z2 || (!r && !b1) || !agg || !aggx || !stat || (!coef && !pending) ||
+                                    int32_t need_w, const int32_t *dims,
+                                    const scgib_bn_bwd_pending *pending, scgib_stream_t stream) {
+    if (n_nodes <= 0 || !dy || !z2 || (!r && !b1) || !aggx || !stat || (!coef && !pending) ||
         !w1 || !w2 || !slab || n_feat < 1 || n_feat > kPreF)
         return SCGIB_EINVAL;
+    if ((need_w || !r) && !agg) return SCGIB_EINVAL;
+    if (!need_w && !r) return SCGIB_EUNSUPPORTED;  // frozen weights: the stored-r kernel
     if (pending && (!pending->gpart || !pending->dgamma || !pending->dbeta)) return SCGIB_EINVAL;
     const scgib_bn_bwd_pending pd = pending ? *pending : scgib_bn_bwd_pending{};
     const int64_t nt = scgib_gin_tiles(n_nodes);
-    if (r)
+    if (!need_w)
+        gin_bwd_k<32, true, true, false, false, false><<<bwd_grid(nt), 256, 0, as_stream(stream)>>>(
+            dy, z2, r, agg, stat, coef, w1, w2, n_nodes, nt, nullptr, slab, dims, aggx, pd, ReconArgs{},
+            n_feat);
+    else if (r)
         gin_bwd_k<32, true, true><<<bwd_grid(nt), 256, 0, as_stream(stream)>>>(
             dy, z2, r, agg, stat, coef, w1, w2, n_nodes, nt, nullptr, slab, dims, aggx, pd, ReconArgs{},
             n_feat);

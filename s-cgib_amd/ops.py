@@ -499,6 +499,8 @@ class _GinEncoder(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, g_out, g_readout=None):
+        if not isinstance(ctx, _Ctx):  # (the encoder pair sets its sub-contexts' own)
+            ctx.need = ctx.needs_input_grad[7:]
         return _drain(_GinEncoder.backward_steps(ctx, g_out, g_readout))
 
     @staticmethod
@@ -526,6 +528,11 @@ class _GinEncoder(torch.autograd.Function):
         defer = int(DEFER_BN and n <= int(_lib.query("scgib_gin_defer_max_nodes")))
         gpart = bn_ws.data_ptr() + 4 * int(_lib.query("scgib_gin_bn_gpart_offset", n))
         grads = [None] * (6 * L)
+        # which parameters take a gradient (the fine-tune freezing quirk,
+        # models.py:424-434, leaves most GIN layers frozen): a layer none of
+        # whose W1 / b1 / W2 / b2 does runs its backward without the weight
+        # products (scgib_gin_layer_bwd need_w = 0; same data gradients, bitwise)
+        need = getattr(ctx, "need", None)
         dagg_next, dwt = None, None
         nslab = int(_lib.query("scgib_gin_bwd_slabs", n))
         jobs, keep = [], []
@@ -572,21 +579,38 @@ class _GinEncoder(torch.autograd.Function):
             meta = {"n": n, "e": gr.edge_capacity(), "d_in": d_in, "r": r is not None}
             w1c, w2c = _f32(w1, "w1"), _f32(w2, "w2")
             b1c = _f32(b1, "b1") if r is None else None
+            # (frozen-weight kernels: stored r, d_in = 64 or the layer-0 fold)
+            wg = need is None or any(need[6 * l: 6 * l + 4]) or r is None or \
+                (d_in != HIDDEN and not (pre and l == 0))
+            meta["wg"] = wg
             if pre and l == 0:
                 width = int(_lib.query("scgib_gin_layer0_slab_width"))
                 slab = torch.empty(nslab * width, dtype=torch.float32, device=dev)
                 _launch("scgib_gin_layer0_bwd", meta, _p(dy), _p(z2), _p(r), _p(agg), _p(aggx),
                         ctx.n_feat, _p(stat), _p(coef), _p(w1c), _p(b1c), _p(w2c), n, _p(slab),
-                        _p(gr.dims), _byref(bpend), st)
+                        int(wg), _p(gr.dims), _byref(bpend), st)
                 dagg = None
             else:
                 width = HIDDEN * HIDDEN + HIDDEN * d_in + 2 * HIDDEN
                 slab = torch.empty(int(_lib.query("scgib_gin_slab_floats", n, d_in)),
-                                   dtype=torch.float32, device=dev)
+                                   dtype=torch.float32, device=dev) if wg else None
                 dagg = torch.empty(n, d_in, dtype=torch.float32, device=dev)
                 _launch("scgib_gin_layer_bwd", meta, _p(dy), _p(z2), _p(r), _p(agg), d_in,
                         _p(stat), _p(coef), _p(w1c), _p(b1c), _p(w2c), n, _p(dagg), _p(slab),
-                        _NULL, _p(gr.dims), _byref(bpend), st)
+                        _NULL, int(wg), _p(gr.dims), _byref(bpend), st)
+            grads[6 * l + 4] = bn_g[0]
+            grads[6 * l + 5] = bn_g[1]
+            if not wg:  # no weight gradients: only layer 0's dWt (its slab's tail)
+                if pre and l == 0:
+                    o = HIDDEN * HIDDEN + HIDDEN * d_in + 2 * HIDDEN
+                    dwt = torch.empty(32 * ctx.n_feat, dtype=torch.float32, device=dev)
+                    jobs.append(_lib.SlabJob(slab.data_ptr() + 4 * o, dwt.data_ptr(),
+                                             32 * ctx.n_feat, nslab, width))
+                    keep.append(slab)
+                    dwt = dwt.view(32, ctx.n_feat)
+                dagg_next = dagg
+                yield
+                continue
             wgrad = torch.empty(width, dtype=torch.float32, device=dev)
             if pre and l == 0:  # dWt occupies 32 * F of its 512 columns
                 used = HIDDEN * HIDDEN + HIDDEN * d_in + 2 * HIDDEN + 32 * ctx.n_feat
@@ -609,8 +633,6 @@ class _GinEncoder(torch.autograd.Function):
             if pre and l == 0:
                 o += 2 * HIDDEN
                 dwt = wgrad[o:o + 32 * ctx.n_feat].view(32, ctx.n_feat)
-            grads[6 * l + 4] = bn_g[0]
-            grads[6 * l + 5] = bn_g[1]
             dagg_next = dagg
             yield
         extra = getattr(ctx, "extra_jobs", None)
@@ -919,6 +941,8 @@ class _GinEncoderPair(torch.autograd.Function):
         # chain ends well before the ego chain's, so they leave the critical path
         scope = ctx.scope if (ctx.scope is not None and ctx.scope.open) else None
         held = None
+        need = ctx.needs_input_grad[12:]  # the two encoders' parameters (frozen ones skip dW)
+        ctx.sub[0].need, ctx.sub[1].need = need[:ctx.ne], need[ctx.ne:]
         dw0 = db0 = None
         g_f_in = g_f
         # the critical ego chain is captured first: the replayed graph then

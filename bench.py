@@ -628,10 +628,14 @@ def main():
     ap.add_argument("--finetune", choices=["molhiv"], default=None,
                     help="time the fine-tune step of BASELINE.json configs[4] instead "
                          "(finetune_bench.py; --batch defaults to 32 there)")
+    ap.add_argument("--torch-head", action="store_true",
+                    help="fine-tune: torch's predict head / sigmoid / BCE instead of csrc/head.hip "
+                         "(models.FUSE_HEAD; A/B)")
     ap.add_argument("--no-finetune", action="store_true",
                     help="skip the fine-tune leg (configs[4]) the N = 1 line carries in 'finetune'")
     a = ap.parse_args()
     pkg.ops.STORE_R = not a.recompute_r
+    pkg.models.FUSE_HEAD = not a.torch_head
     if a.finetune:
         import finetune_bench
         dev = torch.device("cuda", 0)

@@ -23,6 +23,11 @@ SIGNATURES = {
     "scgib_set2set_fwd": (ctypes.c_int, [_P, _P, _I64, _I32, _I32, _P, _P, _P, _P, _P, _P, _P]),
     "scgib_set2set_bwd": (ctypes.c_int, [_P, _P, _I64, _I32, _I32, _P, _P, _P, _P, _P, _I64, _P,
                                          _P, _P, _P, _P, _P]),
+    "scgib_head_fwd": (ctypes.c_int, [_P, _I64, _I32, _P, _P, _P, _P, _I32, _I32, _P, _P, _P]),
+    "scgib_head_bwd": (ctypes.c_int, [_P, _P, _P, _P, _I64, _I32, _P, _P, _I32, _I32, _P, _P,
+                                      _P, _P, _P, _P]),
+    "scgib_bce_fwd": (ctypes.c_int, [_P, _P, _I64, _P, _P]),
+    "scgib_bce_bwd": (ctypes.c_int, [_P, _P, _I64, _P, _P, _P]),
     "scgib_pool_copy": (ctypes.c_int, [_P, _I32, _P, _P, _I64, _P]),
     "scgib_pool_copy2": (ctypes.c_int, [_P, _I32, _P, _P, _I64, _P, _P, _I64, _P]),
     "scgib_stream_signal": (ctypes.c_int, [_P, _P]),

@@ -147,6 +147,9 @@ FUSE_CONTRAST = True
 # gate / feature noise drawn by one Philox kernel (ops.device_noise) on the
 # core encoder's chain instead of two torch.rand launches on the critical path
 DEVICE_NOISE = True
+# fine-tune head: predict (+ sigmoid) and the BCE loss on csrc/head.hip (four
+# launches per step instead of ~19 torch ones; tests cover both sides)
+FUSE_HEAD = True
 
 
 _GRAPH_ATTRS = ("graph_features", "subgraphs_features", "_last_z1", "_last_kl_mean")
@@ -697,11 +700,14 @@ class Mainmodel_finetuning(nn.Module):
                                         device, noise)[0]
         im = ops.mlp2(im, self.MLP, batch_g.dims)
         im = self.s2s(batch_g, im)
-        scores = self.predict(im)
+        sig = self.dataset not in self.tasks  # models.py:517-520
+        if FUSE_HEAD and ops.predict_head_ok(im, self.predict):
+            scores = ops.predict_head(im, self.predict, sig)  # predict (+ sigmoid), one launch
+        else:
+            scores = self.predict(im)
+            scores = torch.sigmoid(scores) if sig else scores
         ops.join_aside()
-        if self.dataset in self.tasks:
-            return scores, 0, 0, 0
-        return torch.sigmoid(scores), 0, 0, 0
+        return scores, 0, 0, 0
 
     def _prepare_ego(self, batch_g, batch_x, x_subs):
         k = getattr(self.model, "k_transition", self.k_transition)
@@ -712,6 +718,8 @@ class Mainmodel_finetuning(nn.Module):
 
     # losses (models.py:522-543)
     def loss(self, scores, targets):
+        if FUSE_HEAD and scores.is_cuda and scores.shape == targets.shape:
+            return ops.bce_mean(scores.float(), targets.float())  # one launch each way
         return F.binary_cross_entropy(scores.float(), targets.float())
 
     def loss_CrossEntropy(self, scores, targets):

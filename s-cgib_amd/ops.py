@@ -1110,6 +1110,87 @@ def set2set(x, graph, lstm, n_iters):
 
 
 # ---------------------------------------------------------------------------
+# (f)1: fine-tune prediction head + BCE (models.py:510-523), csrc/head.hip
+# ---------------------------------------------------------------------------
+class _PredictHead(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w1, b1, w2, b2, sigmoid):
+        x = _f32(x, "predict head x")
+        w1, b1, w2, b2 = (_f32(t, "predict head params") for t in (w1, b1, w2, b2))
+        n, k = x.shape
+        c = w2.shape[0]
+        hid = torch.empty(n, HIDDEN, dtype=torch.float32, device=x.device)
+        out = torch.empty(n, c, dtype=torch.float32, device=x.device)
+        _lib.call("scgib_head_fwd", _p(x), n, k, _p(w1), _p(b1), _p(w2), _p(b2), c, int(sigmoid),
+                  _p(hid), _p(out), _stream())
+        ctx.save_for_backward(x, hid, out, w1, w2)
+        ctx.sigmoid = bool(sigmoid)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        x, hid, out, w1, w2 = ctx.saved_tensors
+        g = _f32(g, "predict head grad")
+        n, k = x.shape
+        c = w2.shape[0]
+        dx, dw1, dw2 = torch.empty_like(x), torch.empty_like(w1), torch.empty_like(w2)
+        db1 = torch.empty(HIDDEN, dtype=torch.float32, device=x.device)
+        db2 = torch.empty(c, dtype=torch.float32, device=x.device)
+        _lib.call("scgib_head_bwd", _p(x), _p(hid), _p(out), _p(g), n, k, _p(w1), _p(w2), c,
+                  int(ctx.sigmoid), _p(dx), _p(dw1), _p(db1), _p(dw2), _p(db2), _stream())
+        return dx, dw1, db1, dw2, db2, None
+
+
+def predict_head_ok(x, seq):
+    """Whether ``seq`` is the fine-tune head the kernels implement:
+    Sequential(Linear(K <= 128, 64), ReLU, Linear(64, C <= 16)) on a [B, K]
+    HIP tensor."""
+    import torch.nn as nn
+    return (x.is_cuda and x.dim() == 2 and len(seq) == 3 and isinstance(seq[0], nn.Linear)
+            and isinstance(seq[1], nn.ReLU) and isinstance(seq[2], nn.Linear)
+            and seq[0].bias is not None and seq[2].bias is not None
+            and seq[0].out_features == HIDDEN and seq[2].in_features == HIDDEN
+            and x.shape[1] == seq[0].in_features and 1 <= x.shape[1] <= 128
+            and 1 <= seq[2].out_features <= 16)
+
+
+def predict_head(x, seq, sigmoid):
+    """``sigmoid(seq(x))`` (or ``seq(x)``) for the fine-tune head
+    Sequential(Linear, ReLU, Linear) (models.py:510-520: predict, then the
+    sigmoid unless the dataset is a regression one) in one launch forward
+    and one backward (scgib_head_fwd / _bwd) instead of ~12 torch launches."""
+    return _PredictHead.apply(x, seq[0].weight, seq[0].bias, seq[2].weight, seq[2].bias,
+                              bool(sigmoid))
+
+
+class _BceMean(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, s, t):
+        s, t = _f32(s, "bce scores"), _f32(t, "bce targets")
+        loss = torch.empty((), dtype=torch.float32, device=s.device)
+        _lib.call("scgib_bce_fwd", _p(s), _p(t), s.numel(), _p(loss), _stream())
+        ctx.save_for_backward(s, t)
+        return loss
+
+    @staticmethod
+    def backward(ctx, g):
+        s, t = ctx.saved_tensors
+        ds = torch.empty_like(s)
+        _lib.call("scgib_bce_bwd", _p(s), _p(t), s.numel(), _p(_f32(g.reshape(1), "bce grad")),
+                  _p(ds), _stream())
+        return ds, None
+
+
+def bce_mean(scores, targets):
+    """F.binary_cross_entropy(scores, targets) (mean) in one launch each way
+    (scgib_bce_fwd / _bwd: torch's per-element formula, its log clamp at
+    -100 and its backward's 1e-12 floor; fp64 fixed-order sum)."""
+    if scores.shape != targets.shape:
+        raise _lib.ScgibError(f"bce: scores {tuple(scores.shape)} vs targets {tuple(targets.shape)}")
+    return _BceMean.apply(scores, targets)
+
+
+# ---------------------------------------------------------------------------
 # A6-A8: fused core <-> subgraph interaction
 # ---------------------------------------------------------------------------
 def _interaction_forward(ctx, f, t, s, u_gate, u_feat, gamma, beta, w2, b2, w_att, b_att, graph,

@@ -220,3 +220,41 @@ def test_frozen_layers_skip_weight_grads_bitwise(pkg, dev, case):
     for n in tr:
         if ga[n] is not None:
             assert torch.equal(ga[n], gb[n]), n
+
+
+@pytest.mark.parametrize("n,k,c,sig", [(32, 128, 1, True), (32, 128, 2, True), (1, 128, 1, True),
+                                       (33, 64, 3, False), (100, 128, 1, True), (7, 9, 16, False)])
+def test_predict_head_and_bce_vs_torch(pkg, dev, n, k, c, sig):
+    """csrc/head.hip against torch in float64: the head's output (and its
+    sigmoid), every gradient, and the BCE loss and its gradient (the tail of
+    Mainmodel_finetuning, models.py:510-523).  n = 100: backward row chunks
+    of 32 with a partial last one; k = 9 / 64: K padding of the float4 runs."""
+    import torch.nn as nn
+    gen = torch.Generator().manual_seed(n * 1000 + k + c)
+    seq = nn.Sequential(nn.Linear(k, 64), nn.ReLU(), nn.Linear(64, c))
+    x = torch.randn(n, k, generator=gen)
+    up = torch.rand(n, c, generator=gen)
+    tg = torch.randint(0, 2, (n, c), generator=gen).float()
+    seq64 = copy.deepcopy(seq).double()
+    x64 = x.double().requires_grad_(True)
+    ref = seq64(x64)
+    ref = torch.sigmoid(ref) if sig else ref
+    (ref * up.double()).sum().backward()
+    seqd = copy.deepcopy(seq).to(dev)
+    xd = x.to(dev).requires_grad_(True)
+    assert pkg.ops.predict_head_ok(xd, seqd)
+    out = pkg.ops.predict_head(xd, seqd, sig)
+    (out * up.to(dev)).sum().backward()
+    assert rel_err(out.detach().cpu(), ref.detach()) < 1e-5
+    assert rel_err(xd.grad.cpu(), x64.grad) < 1e-5
+    for (na, pa), (_, pb) in zip(seqd.named_parameters(), seq64.named_parameters()):
+        assert rel_err(pa.grad.cpu(), pb.grad) < 1e-5, na
+    if sig:  # BCE on the scores
+        s = out.detach().clamp(1e-6, 1 - 1e-6).requires_grad_(True)
+        s64 = s.detach().cpu().double().requires_grad_(True)
+        lr = F.binary_cross_entropy(s64, tg.double())
+        lr.backward()
+        l = pkg.ops.bce_mean(s, tg.to(dev))
+        l.backward()
+        assert rel_err(l.item(), lr.item()) < 1e-5
+        assert rel_err(s.grad.cpu(), s64.grad) < 1e-4

@@ -582,7 +582,8 @@ int scgib_contrastive_bwd(const float *z1, const float *z2, int64_t n_graphs, fl
  * Mainmodel_continue (models.py:569-571 / :1055-1057, applied at :676 /
  * :1174).  Forward saves r = relu(x W1^T + b1) [N][64] for backward.
  * Backward: dx [N][d_in] and wgrad = dW2[64*64] | dW1[64*d_in] | db2 | db1
- * (fixed-order, deterministic); `slab` holds scgib_mlp2_slab_floats(n, d_in).
+ * (fixed-order, deterministic); `slab` holds scgib_mlp2_slab_floats(n, d_in);
+ * wgrad NULL: the slabs are left for the caller's reduce (a deferred one).
  * linear: out = x W^T (+ b), 64 -> 64 — compressor[0] (models.py:589-592 /
  * :1081-1084, applied at :596 / :1092).  Backward writes dx = add + dy W
  * (`add` may be NULL) and wgrad = dW[64*64] | db[64]; `slab` holds

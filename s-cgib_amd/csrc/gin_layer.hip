@@ -2445,7 +2445,7 @@ extern "C" int scgib_mlp2_bwd(const float *dout, const float *x, const float *r,
                               float *slab, float *wgrad, const int32_t *dims,
                               scgib_stream_t stream) {
     if (n_nodes <= 0 || (d_in != 64 && d_in != 128)) return SCGIB_EINVAL;
-    if (!dout || !x || !r || !w1 || !w2 || !dx || !slab || !wgrad) return SCGIB_EINVAL;
+    if (!dout || !x || !r || !w1 || !w2 || !dx || !slab) return SCGIB_EINVAL;
     const int64_t nt = scgib_gin_tiles(n_nodes);
     const int grid = bwd_grid(nt);
     hipStream_t st = as_stream(stream);
@@ -2454,7 +2454,7 @@ extern "C" int scgib_mlp2_bwd(const float *dout, const float *x, const float *r,
     else
         gin_bwd_k<64, false><<<grid, 256, 0, st>>>(dout, nullptr, r, x, nullptr, nullptr, w1, w2, n_nodes, nt, dx, slab, dims, nullptr, scgib_bn_bwd_pending{}, ReconArgs{});
     const int rc = launch_status();
-    if (rc != SCGIB_OK) return rc;
+    if (rc != SCGIB_OK || !wgrad) return rc;  // wgrad NULL: the caller reduces the slabs
     return launch_slab_reduce(slab, grid, 64 * 64 + 64 * static_cast<int64_t>(d_in) + 128, wgrad, st);
 }
 

@@ -235,7 +235,29 @@ __device__ __noinline__ void s2s_attend_bwd(const S2SRows X, int64_t p1, const f
 
 }  // namespace
 
+// the gate dot of s2s_dot's float4 path with the weight row in registers
+// (same four accumulators, same k order: the same bits)
+template <int N4>
+__device__ __forceinline__ float s2s_dot_reg(const float4 (&w)[N4], const float *v) {
+    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+#pragma unroll
+    for (int k = 0; k < N4; ++k) {
+        a0 = fmaf(w[k].x, v[4 * k], a0);
+        a1 = fmaf(w[k].y, v[4 * k + 1], a1);
+        a2 = fmaf(w[k].z, v[4 * k + 2], a2);
+        a3 = fmaf(w[k].w, v[4 * k + 3], a3);
+    }
+    return (a0 + a1) + (a2 + a3);
+}
+
 // One workgroup per graph: all n_iters rounds.  out [B][2d] = the last q*.
+// Round 0 starts from q* = h = 0, so its gate products are exactly +0 and
+// z = (0 + b_ih) + (0 + b_hh) is formed without them (the round-0 dots were
+// 6 of the kernel's ~20 us, phase trace r04).  REG (d = 64: thread j owns
+// gate j of 256): the thread's W_ih / W_hh rows (192 floats) are loaded into
+// registers at the kernel's start — their latency hides under round 0 — and
+// every later round's dots read them there instead of reloading the rows.
+template <bool REG>
 __global__ __launch_bounds__(256) void set2set_fwd_k(
     const float *__restrict__ x, const int32_t *__restrict__ ptr, int d, int T,
     const float *__restrict__ w_ih, const float *__restrict__ b_ih,
@@ -245,6 +267,16 @@ __global__ __launch_bounds__(256) void set2set_fwd_k(
     __shared__ float sX[kS2SRows * kS2SMaxD], sRedA[kS2SRed];
     const int64_t g = blockIdx.x;
     const int tid = threadIdx.x, D2 = 2 * d, G4 = 4 * d, S = s2s_save(d);
+    constexpr int NI = REG ? 2 * kS2SMaxD / 4 : 1, NH = REG ? kS2SMaxD / 4 : 1;
+    float4 wi[NI], wh[NH];
+    if constexpr (REG) {  // d = 64, G4 = 256: every thread owns a gate
+        const float4 *ri = reinterpret_cast<const float4 *>(w_ih + static_cast<int64_t>(tid) * D2);
+        const float4 *rh = reinterpret_cast<const float4 *>(w_hh + static_cast<int64_t>(tid) * d);
+#pragma unroll
+        for (int k = 0; k < NI; ++k) wi[k] = ri[k];
+#pragma unroll
+        for (int k = 0; k < NH; ++k) wh[k] = rh[k];
+    }
     const int64_t p0 = ptr[g], p1 = ptr[g + 1];
     const S2SRows X{x, sX, p0, s2s_stage(x, p0, p1, d, sX), d};
     if (tid < D2) sQ[tid] = 0.f;
@@ -263,8 +295,16 @@ __global__ __launch_bounds__(256) void set2set_fwd_k(
             sv[3 * d + tid] = sC[tid];
         }
         if (tid < G4) {  // gate tid
-            const float a = s2s_dot(w_ih + static_cast<int64_t>(tid) * D2, sQ, D2);
-            const float b = s2s_dot(w_hh + static_cast<int64_t>(tid) * d, sH, d);
+            float a = 0.f, b = 0.f;  // round 0: q* = h = 0
+            if (t > 0) {
+                if constexpr (REG) {
+                    a = s2s_dot_reg(wi, sQ);
+                    b = s2s_dot_reg(wh, sH);
+                } else {
+                    a = s2s_dot(w_ih + static_cast<int64_t>(tid) * D2, sQ, D2);
+                    b = s2s_dot(w_hh + static_cast<int64_t>(tid) * d, sH, d);
+                }
+            }
             const float z = (a + bi) + (b + bh);
             const int kind = tid / d;  // 0 i, 1 f, 2 g, 3 o
             const float act = kind == 2 ? tanhf(z) : s2s_sigmoid(z);
@@ -349,6 +389,10 @@ __global__ __launch_bounds__(256) void set2set_bwd_k(
         __syncthreads();
         if (t >= T - 2) SCGIB_MARK(mk + 2);
         if (tid < G4) dG[(g * T + t) * G4 + tid] = sDG[tid];
+        // round 0's [d q*_{-1} | d h_{-1}] would be the gradient of the initial
+        // state, the constant zeros: nothing reads it (the products were
+        // 3.6 us of the kernel, phase trace r04)
+        if (t == 0) break;
         // [d q*_{t-1} | d h_{t-1} (gates path)] = [W_ih | W_hh]^T dG: wave w sums
         // the gates of its quarter, lane l the outputs l, l + 64, l + 128 < 3d
         // (coalesced along the weight rows); the quarters combine in fixed order
@@ -452,8 +496,12 @@ extern "C" int scgib_set2set_fwd(const float *x, const int32_t *graph_ptr, int64
     if (n_graphs == 0) return SCGIB_OK;
     if (!x || !graph_ptr || !w_ih || !b_ih || !w_hh || !b_hh || !save || !out)
         return SCGIB_EINVAL;
-    set2set_fwd_k<<<static_cast<unsigned>(n_graphs), 256, 0, as_stream(stream)>>>(
-        x, graph_ptr, dim, n_iters, w_ih, b_ih, w_hh, b_hh, save, out);
+    if (dim == kS2SMaxD)
+        set2set_fwd_k<true><<<static_cast<unsigned>(n_graphs), 256, 0, as_stream(stream)>>>(
+            x, graph_ptr, dim, n_iters, w_ih, b_ih, w_hh, b_hh, save, out);
+    else
+        set2set_fwd_k<false><<<static_cast<unsigned>(n_graphs), 256, 0, as_stream(stream)>>>(
+            x, graph_ptr, dim, n_iters, w_ih, b_ih, w_hh, b_hh, save, out);
     return launch_status();
 }
 

@@ -1605,6 +1605,11 @@ class _Mlp2(torch.autograd.Function):
         n, d_in = x.shape
         if tuple(w1.shape) != (HIDDEN, d_in) or tuple(w2.shape) != (HIDDEN, HIDDEN):
             raise _lib.ScgibError(f"mlp2: expects Linear({d_in},64) - Linear(64,64)")
+        # (the fine-tune head's MLP: its weight-gradient reduce is deferred into
+        # the encoder pair's backward, off the loss chain, as the pretraining
+        # head's is — SlabScope)
+        ctx.leaves = (w1, b1, w2, b2)
+        ctx.scope = _slab_scope_for(ctx.leaves)
         w1, b1, w2, b2 = (_f32(t, "mlp2 params") for t in (w1, b1, w2, b2))
         r = torch.empty(n, HIDDEN, dtype=torch.float32, device=x.device)
         out = torch.empty(n, HIDDEN, dtype=torch.float32, device=x.device)
@@ -1624,8 +1629,11 @@ class _Mlp2(torch.autograd.Function):
                            dtype=torch.float32, device=x.device)
         wg = torch.empty(HIDDEN * HIDDEN + HIDDEN * d_in + 2 * HIDDEN, dtype=torch.float32,
                          device=x.device)
+        defer = ctx.scope is not None and ctx.scope.usable(ctx.leaves)
         _lib.call("scgib_mlp2_bwd", _p(g), _p(x), _p(r), d_in, _p(w1), _p(w2), n, _p(dx),
-                  _p(slab), _p(wg), _p(ctx.dims), _stream())
+                  _p(slab), None if defer else _p(wg), _p(ctx.dims), _stream())
+        if defer:  # reduced by the encoder pair's backward (SlabScope)
+            ctx.scope.add(slab, wg, wg.numel(), slab.numel() // wg.numel())
         o = HIDDEN * HIDDEN
         dw2 = wg[:o].view(HIDDEN, HIDDEN)
         dw1 = wg[o: o + HIDDEN * d_in].view(HIDDEN, d_in)

@@ -64,6 +64,20 @@ REPLAY_FILE = os.environ.get("SCGIB_REPLAY_FILE",
                              os.path.join(ROOT, "profiles", "replay_current.json"))
 
 
+SB_FILE = os.environ.get("SCGIB_SB_EVIDENCE_FILE") or os.path.join(
+    ROOT, "profiles", "sb_evidence_current.json")
+
+
+def _sb_evidence():
+    """rocprofv3 evidence of the superbatch launches (tools/sb_evidence.py):
+    per kernel the traced average duration and the PMC HBM bytes per launch."""
+    try:
+        with open(SB_FILE) as fh:
+            return json.load(fh)
+    except (OSError, ValueError):
+        return {}
+
+
 def _replay():
     try:
         with open(REPLAY_FILE) as fh:
@@ -392,6 +406,28 @@ def superbatch_roofline(dev, n_target=1_200_000, reps=20):
         ent["launches"] = len(bw)
         res["gin_bwd5_k"] = ent
     del y, x, h, gin
+    # rocprofv3 evidence of these launches (same program, separate runs):
+    # the traced average duration beside the event time, and the PMC HBM
+    # bytes per launch beside the algorithmic bytes
+    ev = _sb_evidence()
+    for key in ("gin_fwd_k", "gin_bwd_stats_k", "gin_bwd5_k", "gin_aggregate_k"):
+        e = ev.get(key)
+        if key not in res or not e:
+            continue
+        r = res[key]
+        r["trace_avg_us"] = e.get("trace_avg_us")
+        if e.get("trace_avg_us"):
+            r["trace_vs_event"] = round(e["trace_avg_us"] / r["us"], 4)
+        r["traffic"] = e.get("traffic_bytes")
+        r["traffic_fetch"] = e.get("fetch_bytes")
+        r["traffic_write"] = e.get("write_bytes")
+        if e.get("traffic_bytes"):
+            r["traffic_over_algorithmic"] = round(e["traffic_bytes"] / r["bytes"], 4)
+            r["hbm_frac_measured"] = round(e["traffic_bytes"] / (r["us"] * 1e-6) / 1e9
+                                           / HBM_PEAK_GBS, 4)
+    if ev:
+        res["evidence_file"] = os.path.relpath(SB_FILE, ROOT)
+        res["evidence_nodes"] = ev.get("_nodes")
     return res
 
 
@@ -613,6 +649,9 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=20.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-superbatch", action="store_true")
+    ap.add_argument("--superbatch-only", action="store_true",
+                    help="only the superbatch pass (a program for rocprofv3 kernel-trace / PMC "
+                         "passes over exactly those launches: tools/sb_evidence.py)")
     ap.add_argument("--no-kernel-timer", action="store_true",
                     help="skip the event-timed kernel pass (PMC runs: only real step launches)")
     ap.add_argument("--eager", action="store_true",
@@ -635,6 +674,11 @@ def main():
                     help="skip the fine-tune leg (configs[4]) the N = 1 line carries in 'finetune'")
     a = ap.parse_args()
     pkg.ops.STORE_R = not a.recompute_r
+    if a.superbatch_only:
+        dev = torch.device("cuda", 0)
+        torch.cuda.set_device(dev)
+        print(json.dumps({"roofline_superbatch": superbatch_roofline(dev)}), flush=True)
+        return
     pkg.models.FUSE_HEAD = not a.torch_head
     if a.finetune:
         import finetune_bench

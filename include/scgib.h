@@ -403,7 +403,8 @@ int scgib_egonet_k1_build_deg(const int32_t *rowptr, const int32_t *col, int64_t
  * aligned, left zeroed by the launch (reusable by the next one; one launch in
  * flight per scan_state).  Output identical to scgib_egonet_k1_build_deg.
  * e_cap: sub_col's capacity; a ball that would write past n_ego_cap rows or
- * e_cap columns is dropped and sets bit 4 of *err (err may be NULL). */
+ * e_cap columns is dropped and ORs the flag value 4 (bit 2; flags 1 and 2
+ * as above) into *err (err may be NULL). */
 int64_t scgib_egonet_k1_scan_words(int64_t n_nodes);
 int scgib_egonet_k1_build_onepass(const int32_t *rowptr, const int32_t *col, int64_t n_nodes,
                                   int32_t max_in_degree, int32_t *ego_ptr, int32_t *ego_eptr,

@@ -118,6 +118,12 @@ class Set2Set(nn.Module):
         super().__init__()
         if n_layers != 1:
             raise NotImplementedError("Set2Set: the reference uses one LSTM layer")
+        if not 1 <= input_dim <= 64:
+            # (the device kernels hold a graph's features, 64 lanes wide; a
+            # domain-adaptation model over raw features wider than 64 is
+            # refused when it is built, not at its first step)
+            raise NotImplementedError(f"Set2Set: input width {input_dim} (the device readout "
+                                      "supports 1..64: the hidden width, or raw features)")
         self.input_dim, self.output_dim = input_dim, 2 * input_dim
         self.n_iters, self.n_layers = n_iters, n_layers
         self.lstm = nn.LSTM(self.output_dim, self.input_dim, n_layers)

@@ -940,15 +940,24 @@ def test_gin_r_recompute_bitwise(pkg, dev, via_ego, n_mols):
         assert torch.equal(ba[k], bb[k]), k
 
 
-@pytest.mark.parametrize("dim,n_mols", [(64, 32), (9, 32), (64, 300), (9, 1)])
-def test_set2set_device_vs_oracle(pkg, dev, dim, n_mols):
-    """models.Set2Set (LSTM cell in torch ops + the device attention readout,
-    scgib_set2set_fwd / _bwd) against the oracle's fp64 DGL Set2Set
-    (models.py:565): output and the gradients of the features and of every
-    LSTM parameter; dim 9 = s2s_rev over raw OGB features (odd width).  The
-    features get rows past the batch (capacity padding): their gradient is 0."""
+@pytest.mark.parametrize("dim,n_mols,mu", [(64, 32, None), (9, 32, None), (64, 300, None),
+                                           (9, 1, None), (64, 6, 150.0), (9, 4, 150.0)])
+def test_set2set_device_vs_oracle(pkg, dev, dim, n_mols, mu):
+    """models.Set2Set (the LSTM recurrence and every round's attention
+    readout in one device launch per direction, scgib_set2set_fwd / _bwd)
+    against the oracle's fp64 DGL Set2Set (models.py:565): output and the
+    gradients of the features and of every LSTM parameter; dim 9 = s2s_rev
+    over raw OGB features (odd width); mu = 150 atoms: graphs past the 64 rows
+    the kernels stage in LDS (the global-row path).  The features get rows
+    past the batch (capacity padding): their gradient is 0."""
     torch.manual_seed(dim + n_mols)
-    g, gh = rand_graph(pkg, n_mols, "molhiv", 5, dev)
+    if mu is None:
+        g, gh = rand_graph(pkg, n_mols, "molhiv", 5, dev)
+    else:
+        gh, _ = pkg.graph.collate_pyg(pkg.synth.molecules(n_mols, "molhiv", seed=5, mu=mu,
+                                                          sigma=20.0))
+        assert gh.batch_num_nodes_host().max() > 64
+        g = gh.to(dev)
     n = g.num_nodes()
     s2s = pkg.models.Set2Set(dim, 2, 1).to(dev)
     feat_full = torch.randn(n + 37, dim, device=dev)

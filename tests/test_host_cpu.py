@@ -560,3 +560,13 @@ def test_scan_arena_carves_disjoint_zeroed_ranges(pkg):
     finally:
         ops._SCAN_ARENAS.pop(key, None)
         ops._SCAN_NEXT.pop(key, None)
+
+
+def test_set2set_rejects_widths_past_the_device_readout(pkg):
+    """ADVICE r04: the device Set2Set holds a graph's features 64 lanes wide;
+    a wider one (domain adaptation over raw features wider than 64) is refused
+    when the model is built, with a message, not at its first step."""
+    pkg.models.Set2Set(64, 2, 1)
+    pkg.models.Set2Set(9, 2, 1)
+    with pytest.raises(NotImplementedError, match="width 65"):
+        pkg.models.Set2Set(65, 2, 1)

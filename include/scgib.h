@@ -291,28 +291,6 @@ int scgib_gin_layer_bwd(const float *dy, const float *z2, const float *r, const 
                         const scgib_bn_bwd_pending *pending, scgib_stream_t stream);
 int scgib_gin_hidden(const float *agg, int32_t d_in, const float *w1, const float *b1,
                      int64_t n_nodes, float *r, scgib_stream_t stream);
-/* ---- (f)1: fine-tune prediction head + BCE (models.py:510-523) ------------
- * scgib_head_fwd: hid = relu(x W1^T + b1) [n,64] (saved), out = hid W2^T + b2
- *   [n,C], sigmoid applied when `sigmoid` (the reference's scores unless the
- *   dataset is a regression one, models.py:517-520); x [n,K], K <= 128, C <= 16.
- * scgib_head_bwd: from d_out [n,C] (and out = the sigmoid output when
- *   `sigmoid`): dx [n,K], dW1 [64][K], db1 [64], dW2 [C][64], db2 [C]; one
- *   workgroup, fixed order.
- * scgib_bce_fwd / _bwd: F.binary_cross_entropy(scores, targets), mean over n
- *   elements (torch's per-element formula and log clamp at -100; fp64 fixed
- *   order sum), and d scores = g (s - t) / max((1 - s) s, 1e-12) / n with g the
- *   device scalar d loss (models.py:522-523). */
-int scgib_head_fwd(const float *x, int64_t n_rows, int32_t k_in, const float *w1, const float *b1,
-                   const float *w2, const float *b2, int32_t n_out, int32_t sigmoid, float *hid,
-                   float *out, scgib_stream_t stream);
-int scgib_head_bwd(const float *x, const float *hid, const float *out, const float *d_out,
-                   int64_t n_rows, int32_t k_in, const float *w1, const float *w2, int32_t n_out,
-                   int32_t sigmoid, float *dx, float *dw1, float *db1, float *dw2, float *db2,
-                   scgib_stream_t stream);
-int scgib_bce_fwd(const float *scores, const float *targets, int64_t n, float *loss,
-                  scgib_stream_t stream);
-int scgib_bce_bwd(const float *scores, const float *targets, int64_t n, const float *g_loss,
-                  float *d_scores, scgib_stream_t stream);
 
 /* ---- (f)1/(f)4: Set2Set readout (DGL Set2Set(dim, n_iters, 1), models.py:565) ----
  * The whole readout as Mainmodel_finetuning.forward (models.py:515) and
@@ -504,6 +482,35 @@ typedef struct {
     float *running_mean, *running_var;
     int64_t *num_batches_tracked;
 } scgib_running_update;
+
+/* ---- (f)1: fine-tune prediction head + BCE (models.py:510-523) ------------
+ * scgib_head_fwd: hid = relu(x W1^T + b1) [n,64] (saved), out = hid W2^T + b2
+ *   [n,C], sigmoid applied when `sigmoid` (the reference's scores unless the
+ *   dataset is a regression one, models.py:517-520); x [n,K], K <= 128 and a
+ *   multiple of 4, C <= 16; x and w1 16-byte aligned (else SCGIB_EUNSUPPORTED).
+ *   ru (may be NULL): the compressor BatchNorm's running update
+ *   (scgib_running_update, below), run in one extra workgroup of the launch —
+ *   nothing in the fine-tune step reads the running statistics, so it needs no
+ *   launch of its own.
+ * scgib_head_bwd: from d_out [n,C] (and out = the sigmoid output when
+ *   `sigmoid`): dx [n,K], dW1 [64][K], db1 [64], dW2 [C][64], db2 [C]; four
+ *   workgroups (dW1 row quarters, dx column quarters), each output summed in a
+ *   fixed order.
+ * scgib_bce_fwd / _bwd: F.binary_cross_entropy(scores, targets), mean over n
+ *   elements (torch's per-element formula and log clamp at -100; fp64 fixed
+ *   order sum), and d scores = g (s - t) / max((1 - s) s, 1e-12) / n with g the
+ *   device scalar d loss (models.py:522-523). */
+int scgib_head_fwd(const float *x, int64_t n_rows, int32_t k_in, const float *w1, const float *b1,
+                   const float *w2, const float *b2, int32_t n_out, int32_t sigmoid, float *hid,
+                   float *out, const scgib_running_update *ru, scgib_stream_t stream);
+int scgib_head_bwd(const float *x, const float *hid, const float *out, const float *d_out,
+                   int64_t n_rows, int32_t k_in, const float *w1, const float *w2, int32_t n_out,
+                   int32_t sigmoid, float *dx, float *dw1, float *db1, float *dw2, float *db2,
+                   scgib_stream_t stream);
+int scgib_bce_fwd(const float *scores, const float *targets, int64_t n, float *loss,
+                  scgib_stream_t stream);
+int scgib_bce_bwd(const float *scores, const float *targets, int64_t n, const float *g_loss,
+                  float *d_scores, scgib_stream_t stream);
 /* Backward of scgib_interaction_fwd.  The KL gradient is g_kl [2 n_last, 64],
  * or g_klmean (device scalar, gradient of kl_mean), or neither (both NULL);
  * g_z1 / g_z2 may be NULL (readouts that feed no loss: zero gradient).

@@ -23,7 +23,8 @@ SIGNATURES = {
     "scgib_set2set_fwd": (ctypes.c_int, [_P, _P, _I64, _I32, _I32, _P, _P, _P, _P, _P, _P, _P]),
     "scgib_set2set_bwd": (ctypes.c_int, [_P, _P, _I64, _I32, _I32, _P, _P, _P, _P, _P, _I64, _P,
                                          _P, _P, _P, _P, _P]),
-    "scgib_head_fwd": (ctypes.c_int, [_P, _I64, _I32, _P, _P, _P, _P, _I32, _I32, _P, _P, _P]),
+    "scgib_head_fwd": (ctypes.c_int, [_P, _I64, _I32, _P, _P, _P, _P, _I32, _I32, _P, _P, _P,
+                                      _P]),
     "scgib_head_bwd": (ctypes.c_int, [_P, _P, _P, _P, _I64, _I32, _P, _P, _I32, _I32, _P, _P,
                                       _P, _P, _P, _P]),
     "scgib_bce_fwd": (ctypes.c_int, [_P, _P, _I64, _P, _P]),
@@ -176,7 +177,7 @@ class RunningUpdate(ctypes.Structure):
                 ("num_batches_tracked", ctypes.c_void_p)]
 
 
-ABI_VERSION = 16
+ABI_VERSION = 17
 STATS_STRIDE = 260
 PGRAD_STRIDE = 324
 HIDDEN = 64

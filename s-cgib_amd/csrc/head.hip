@@ -10,6 +10,7 @@
 // operand is staged in LDS once, each thread owns a fixed set of outputs and
 // sums its terms in a fixed order (deterministic, no atomics).
 #include "common.h"
+#include "running_update.h"
 
 namespace scgib {
 
@@ -18,31 +19,72 @@ constexpr int kHeadKMax = 128;  // input width (2 * hidden: the Set2Set output)
 constexpr int kHeadCMax = 16;   // classes
 constexpr int kHeadRows = 16;   // forward: rows per workgroup
 constexpr int kHeadChunk = 32;  // backward: rows per chunk
+constexpr int kHeadG = 4;       // backward: workgroups (dW1 row / dx column slices)
+
+__device__ __forceinline__ float4 hld4(const float *p) { return *reinterpret_cast<const float4 *>(p); }
+// K is a multiple of 4 (float4 staging); every operand's loads are issued
+// together before its LDS stores (a store-after-load loop waits on each load)
 
 // forward: workgroup = 16 rows; thread (r = tid >> 4, u = tid & 15) owns the
 // hidden units u, u + 16, u + 32, u + 48 of row r (LDS W1 rows at stride
 // K + 1: the 16 lanes of a row read 16 different banks), then output c of
-// row r for c = u, u + 16, ... < C.
+// row r for c = u, u + 16, ... < C.  with_ru: one more workgroup runs the
+// compressor BatchNorm's running update (running_update.h), which nothing in
+// the step reads — instead of its own launch on an aux stream.
 __global__ __launch_bounds__(256) void head_fwd_k(const float *__restrict__ x, int64_t B, int K,
                                                   const float *__restrict__ w1,
                                                   const float *__restrict__ b1,
                                                   const float *__restrict__ w2,
                                                   const float *__restrict__ b2, int C, int act,
                                                   float *__restrict__ hid,
-                                                  float *__restrict__ out) {
+                                                  float *__restrict__ out,
+                                                  const scgib_running_update ru, int with_ru) {
+    if (with_ru && blockIdx.x == gridDim.x - 1) {
+        running_update_body<256>(ru);
+        return;
+    }
     __shared__ float sW1[kHeadH * (kHeadKMax + 1)];
     __shared__ float sX[kHeadRows * (kHeadKMax + 1)];
     __shared__ float sH[kHeadRows * (kHeadH + 1)];
     __shared__ float sW2[kHeadCMax * (kHeadH + 1)];
-    const int tid = threadIdx.x, LK = K + 1;
+    const int tid = threadIdx.x, LK = K + 1, K4 = K >> 2;
     const int64_t row0 = static_cast<int64_t>(blockIdx.x) * kHeadRows;
     const int nv = static_cast<int>(B - row0 < kHeadRows ? B - row0 : kHeadRows);
-    for (int i = tid; i < kHeadH * K; i += 256) sW1[(i / K) * LK + i % K] = w1[i];
-    for (int i = tid; i < kHeadRows * K; i += 256) {
-        const int r = i / K;
-        sX[r * LK + i % K] = x[(row0 + (r < nv ? r : nv - 1)) * K + i % K];
+    // loads: W1 (64 K / 4 <= 2048 float4: 8 per thread), x (16 K / 4: 2), W2 (C 64: 4)
+    float4 vw[8], vx[2];
+    float vw2[4];
+    const int nw = kHeadH * K4, nx = kHeadRows * K4, nw2 = C * kHeadH;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+        const int i = tid + 256 * u;
+        vw[u] = hld4(w1 + 4 * (i < nw ? i : nw - 1));
     }
-    for (int i = tid; i < C * kHeadH; i += 256) sW2[(i / kHeadH) * (kHeadH + 1) + i % kHeadH] = w2[i];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+        const int i = tid + 256 * u, ic = i < nx ? i : nx - 1, r = ic / K4;
+        vx[u] = hld4(x + (row0 + (r < nv ? r : nv - 1)) * K + 4 * (ic - r * K4));
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const int i = tid + 256 * u;
+        vw2[u] = w2[i < nw2 ? i : nw2 - 1];
+    }
+    auto put4 = [](float *d, const float4 v) { d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w; };
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+        const int i = tid + 256 * u, j = i / K4;
+        if (i < nw) put4(sW1 + j * LK + 4 * (i - j * K4), vw[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+        const int i = tid + 256 * u, r = i / K4;
+        if (i < nx) put4(sX + r * LK + 4 * (i - r * K4), vx[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const int i = tid + 256 * u;
+        if (i < nw2) sW2[(i / kHeadH) * (kHeadH + 1) + i % kHeadH] = vw2[u];
+    }
     __syncthreads();
     const int r = tid >> 4, u = tid & 15;
     float acc[4];
@@ -70,16 +112,19 @@ __global__ __launch_bounds__(256) void head_fwd_k(const float *__restrict__ x, i
     }
 }
 
-// backward, one workgroup, rows in chunks of 32:
+// backward, kHeadG workgroups, rows in chunks of 32:
 //   do = ds * (act ? s (1 - s) : 1)                      [rows][C]
-//   dh = (do W2) [hid > 0]                               [rows][64]
-//   dW2 += do^T hid, db2 += sum do, dW1 += dh^T x, db1 += sum dh, dx = dh W1
+//   dh = (do W2) [hid > 0]                               [rows][64]  (every workgroup)
+//   dW1 += dh^T x, db1 += sum dh   rows j in [16 q, 16 q + 16) of workgroup q
+//   dx = dh W1                     columns [kb, ke) of workgroup q (a quarter of the float4 columns)
+//   dW2 += do^T hid, db2 += sum do (workgroup 0)
 // Output ownership (each thread sums its terms in row / chunk order):
-//   dW1[j][k]: j = tid >> 2, k in [32 (tid & 3), +32)  (8 float4 x reads per row)
-//   dx[r][k]:  r = tid >> 3, k in [16 (tid & 7), +16)  (4 float4 W1 reads per j)
-//   dh[r][j]:  r = tid >> 3, j = (tid & 7) + 8 m;  db1 / dW2 column j = tid < 64
-// LDS rows of x and W1 at stride K + 4 (16-byte aligned float4 runs).
-constexpr int kHeadLK = kHeadKMax + 4;
+//   dW1[j][k]: j = 16 q + (tid >> 4), k = (tid & 15) + 16 m
+//   dx[r][k]:  r = tid >> 3, k = kb + (tid & 7) + 8 m
+//   dh[r][j]:  r = tid >> 3, j = (tid & 7) + 8 m;  db1 row j = 16 q + tid (tid < 16);
+//   dW2 / db2 column j = tid < 64 (workgroup 0)
+// LDS: x rows at stride K + 1, the W1 column slice at stride 33.
+constexpr int kHeadSlice = kHeadKMax / kHeadG;  // widest dx column slice
 
 __global__ __launch_bounds__(256) void head_bwd_k(
     const float *__restrict__ x, const float *__restrict__ hid, const float *__restrict__ s,
@@ -87,54 +132,100 @@ __global__ __launch_bounds__(256) void head_bwd_k(
     const float *__restrict__ w2, int C, int act, float *__restrict__ dx,
     float *__restrict__ dw1, float *__restrict__ db1, float *__restrict__ dw2,
     float *__restrict__ db2) {
-    __shared__ __attribute__((aligned(16))) float sW1[kHeadH * kHeadLK];
-    __shared__ __attribute__((aligned(16))) float sX[kHeadChunk * kHeadLK];
+    __shared__ float sX[kHeadChunk * (kHeadKMax + 1)];
+    __shared__ float sW1[kHeadH * (kHeadSlice + 1)];
     __shared__ float sH[kHeadChunk * (kHeadH + 1)];    // hid, then dh
     __shared__ float sDo[kHeadChunk * kHeadCMax];
     __shared__ float sW2[kHeadCMax * kHeadH];
-    const int tid = threadIdx.x;
-    // K padded to a multiple of 32 with zero columns (x and W1), so every
-    // thread's k runs are whole float4s
-    const int KP = (K + 31) & ~31;
-    for (int i = tid; i < kHeadH * KP; i += 256) {
-        const int j = i / KP, k = i % KP;
-        sW1[j * kHeadLK + k] = k < K ? w1[j * K + k] : 0.f;
-    }
-    for (int i = tid; i < C * kHeadH; i += 256) sW2[i] = w2[i];
-    const int jw = tid >> 2, kb = (tid & 3) * 32;   // dW1 ownership
-    const int xr = tid >> 3, kx = (tid & 7) * 16;   // dx / dh ownership
-    const bool w_on = kb < KP, x_on = kx < KP;      // (wave-divergent only for K < 128)
-    float4 aW1[8];
+    const int q = blockIdx.x, tid = threadIdx.x, K4 = K >> 2, LK = K + 1;
+    constexpr int LS = kHeadSlice + 1;
+    // this workgroup's dx columns: float4 columns [q K4 / G, (q + 1) K4 / G)
+    const int kb = 4 * ((q * K4) / kHeadG), ke = 4 * (((q + 1) * K4) / kHeadG), s4 = (ke - kb) >> 2;
+    auto put4 = [](float *d, const float4 v) { d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w; };
+    {   // once: the W1 column slice (64 x <= 8 float4: 2 per thread) and W2 (C 64: 4)
+        const int nw = kHeadH * s4, nw2 = C * kHeadH;
+        float4 vw[2];
+        float vw2[4];
 #pragma unroll
-    for (int m = 0; m < 8; ++m) aW1[m] = make_float4(0.f, 0.f, 0.f, 0.f);
+        for (int u = 0; u < 2; ++u) {
+            const int i = tid + 256 * u, ic = i < nw ? i : (nw > 0 ? nw - 1 : 0), j = s4 > 0 ? ic / s4 : 0;
+            vw[u] = s4 > 0 ? hld4(w1 + j * K + kb + 4 * (ic - j * s4)) : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int i = tid + 256 * u;
+            vw2[u] = w2[i < nw2 ? i : nw2 - 1];
+        }
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const int i = tid + 256 * u;
+            if (i < nw) {
+                const int j = i / s4;
+                put4(sW1 + j * LS + 4 * (i - j * s4), vw[u]);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int i = tid + 256 * u;
+            if (i < nw2) sW2[i] = vw2[u];
+        }
+    }
+    const int jw = 16 * q + (tid >> 4), kw = tid & 15;  // dW1 ownership
+    const int xr = tid >> 3, kx = tid & 7;              // dx / dh ownership
+    float aW1[8];
+#pragma unroll
+    for (int m = 0; m < 8; ++m) aW1[m] = 0.f;
     float aB1 = 0.f, aB2 = 0.f, aW2[kHeadCMax];
 #pragma unroll
     for (int c = 0; c < kHeadCMax; ++c) aW2[c] = 0.f;
     for (int64_t c0 = 0; c0 < B; c0 += kHeadChunk) {
         const int nv = static_cast<int>(B - c0 < kHeadChunk ? B - c0 : kHeadChunk);
+        // the chunk's loads: x (32 K / 4 <= 1024 float4: 4 per thread), hid (512: 2),
+        // ds / s (32 C <= 512: 2)
+        const int nx = nv * K4;
+        float4 vx[4], vh[2];
+        float vd[2], vs[2];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int i = tid + 256 * u, ic = i < nx ? i : nx - 1, r = ic / K4;
+            vx[u] = hld4(x + (c0 + r) * K + 4 * (ic - r * K4));
+        }
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const int i = tid + 256 * u, r = i >> 4;
+            vh[u] = hld4(hid + (c0 + (r < nv ? r : nv - 1)) * kHeadH + 4 * (i & 15));
+        }
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const int i = tid + 256 * u, ic = i < nv * C ? i : nv * C - 1;
+            vd[u] = ds[c0 * C + ic];
+            vs[u] = act ? s[c0 * C + ic] : 0.f;
+        }
         __syncthreads();  // the previous chunk's reads are done
-        for (int i = tid; i < kHeadChunk * KP; i += 256) {
-            const int r = i / KP, k = i % KP;
-            sX[r * kHeadLK + k] = (r < nv && k < K) ? x[(c0 + r) * K + k] : 0.f;
-        }
-        for (int i = tid; i < kHeadChunk * kHeadH; i += 256) {
-            const int r = i >> 6;
-            sH[r * (kHeadH + 1) + (i & 63)] = r < nv ? hid[(c0 + r) * kHeadH + (i & 63)] : 0.f;
-        }
-        for (int i = tid; i < kHeadChunk * C; i += 256) {
-            const int r = i / C, c = i % C;
-            float d = 0.f;
-            if (r < nv) {
-                d = ds[(c0 + r) * C + c];
-                if (act) {
-                    const float sv = s[(c0 + r) * C + c];
-                    d = d * (sv * (1.f - sv));
-                }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int i = tid + 256 * u, r = i / K4;
+            if (i < kHeadChunk * K4) {
+                float *d = sX + r * LK + 4 * (i - r * K4);
+                if (i < nx) put4(d, vx[u]);
+                else put4(d, make_float4(0.f, 0.f, 0.f, 0.f));
             }
-            sDo[r * kHeadCMax + c] = d;
+        }
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const int i = tid + 256 * u, r = i >> 4;
+            put4(sH + r * (kHeadH + 1) + 4 * (i & 15), r < nv ? vh[u] : make_float4(0.f, 0.f, 0.f, 0.f));
+        }
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const int i = tid + 256 * u;
+            if (i < kHeadChunk * C) {
+                const int r = i / C, c = i - r * C;
+                sDo[r * kHeadCMax + c] = i < nv * C ? (act ? vd[u] * (vs[u] * (1.f - vs[u])) : vd[u]) : 0.f;
+            }
         }
         __syncthreads();
-        if (tid < kHeadH) {  // dW2[c][j] += sum_r do[r][c] hid[r][j] (column j = tid); db2 by thread c
+        if (q == 0 && tid < kHeadH) {  // dW2[c][j] += sum_r do[r][c] hid[r][j] (column j = tid); db2 by thread c
 #pragma unroll
             for (int c = 0; c < kHeadCMax; ++c) {
                 if (c < C) {
@@ -162,66 +253,47 @@ __global__ __launch_bounds__(256) void head_bwd_k(
 #pragma unroll
         for (int m = 0; m < 8; ++m) sH[xr * (kHeadH + 1) + (tid & 7) + 8 * m] = dh[m];
         __syncthreads();
-        if (w_on) {  // dW1[jw][kb..kb+31] += sum_r dh[r][jw] x[r][kb..]
-            for (int r = 0; r < kHeadChunk; ++r) {
-                const float d = sH[r * (kHeadH + 1) + jw];
-                const float4 *xp = reinterpret_cast<const float4 *>(sX + r * kHeadLK + kb);
+        for (int r = 0; r < kHeadChunk; ++r) {  // dW1[jw][k] += dh[r][jw] x[r][k]
+            const float d = sH[r * (kHeadH + 1) + jw];
 #pragma unroll
-                for (int m = 0; m < 8; ++m) {
-                    const float4 v = xp[m];
-                    aW1[m] = make_float4(fmaf(d, v.x, aW1[m].x), fmaf(d, v.y, aW1[m].y),
-                                         fmaf(d, v.z, aW1[m].z), fmaf(d, v.w, aW1[m].w));
-                }
+            for (int m = 0; m < 8; ++m) {
+                const int k = kw + 16 * m;
+                if (k < K) aW1[m] = fmaf(d, sX[r * LK + k], aW1[m]);
             }
         }
-        if (tid < kHeadH) {
+        if (tid < 16) {
             float a = 0.f;
-            for (int r = 0; r < kHeadChunk; ++r) a += sH[r * (kHeadH + 1) + tid];
+            for (int r = 0; r < kHeadChunk; ++r) a += sH[r * (kHeadH + 1) + 16 * q + tid];
             aB1 += a;
         }
-        if (x_on && xr < nv) {  // dx[xr][kx..kx+15] = sum_j dh[xr][j] W1[j][kx..]
-            float4 a[4];
+        if (xr < nv) {  // dx[xr][k] = sum_j dh[xr][j] W1[j][k], k in [kb, ke)
+            float a[4];
 #pragma unroll
-            for (int m = 0; m < 4; ++m) a[m] = make_float4(0.f, 0.f, 0.f, 0.f);
+            for (int m = 0; m < 4; ++m) a[m] = 0.f;
             for (int j = 0; j < kHeadH; ++j) {
                 const float d = sH[xr * (kHeadH + 1) + j];
-                const float4 *wp = reinterpret_cast<const float4 *>(sW1 + j * kHeadLK + kx);
 #pragma unroll
-                for (int m = 0; m < 4; ++m) {
-                    const float4 v = wp[m];
-                    a[m] = make_float4(fmaf(d, v.x, a[m].x), fmaf(d, v.y, a[m].y),
-                                       fmaf(d, v.z, a[m].z), fmaf(d, v.w, a[m].w));
-                }
+                for (int m = 0; m < 4; ++m) a[m] = fmaf(d, sW1[j * LS + kx + 8 * m], a[m]);
             }
 #pragma unroll
             for (int m = 0; m < 4; ++m) {
-                const float v[4] = {a[m].x, a[m].y, a[m].z, a[m].w};
-#pragma unroll
-                for (int t = 0; t < 4; ++t) {
-                    const int k = kx + 4 * m + t;
-                    if (k < K) dx[(c0 + xr) * K + k] = v[t];
-                }
+                const int k = kb + kx + 8 * m;
+                if (k < ke) dx[(c0 + xr) * K + k] = a[m];
             }
         }
     }
-    if (w_on) {
 #pragma unroll
-        for (int m = 0; m < 8; ++m) {
-            const float v[4] = {aW1[m].x, aW1[m].y, aW1[m].z, aW1[m].w};
-#pragma unroll
-            for (int t = 0; t < 4; ++t) {
-                const int k = kb + 4 * m + t;
-                if (k < K) dw1[jw * K + k] = v[t];
-            }
-        }
+    for (int m = 0; m < 8; ++m) {
+        const int k = kw + 16 * m;
+        if (k < K) dw1[jw * K + k] = aW1[m];
     }
-    if (tid < kHeadH) {
-        db1[tid] = aB1;
+    if (tid < 16) db1[16 * q + tid] = aB1;
+    if (q == 0 && tid < kHeadH) {
 #pragma unroll
         for (int c = 0; c < kHeadCMax; ++c)
             if (c < C) dw2[c * kHeadH + tid] = aW2[c];
     }
-    if (tid < C) db2[tid] = aB2;
+    if (q == 0 && tid < C) db2[tid] = aB2;
 }
 
 // BCE, mean reduction, as torch's binary_cross_entropy: per element
@@ -262,16 +334,24 @@ __global__ __launch_bounds__(256) void bce_bwd_k(const float *__restrict__ s,
 
 using namespace scgib;
 
+static bool head_aligned(const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
 extern "C" int scgib_head_fwd(const float *x, int64_t n_rows, int32_t k_in, const float *w1,
                               const float *b1, const float *w2, const float *b2, int32_t n_out,
-                              int32_t sigmoid, float *hid, float *out, scgib_stream_t stream) {
+                              int32_t sigmoid, float *hid, float *out,
+                              const scgib_running_update *ru, scgib_stream_t stream) {
     if (n_rows < 0 || k_in < 1 || k_in > kHeadKMax || n_out < 1 || n_out > kHeadCMax)
         return SCGIB_EINVAL;
     if (n_rows == 0) return SCGIB_OK;
     if (!x || !w1 || !b1 || !w2 || !b2 || !hid || !out) return SCGIB_EINVAL;
-    const unsigned grid = static_cast<unsigned>((n_rows + kHeadRows - 1) / kHeadRows);
+    if (k_in % 4 || !head_aligned(x) || !head_aligned(w1)) return SCGIB_EUNSUPPORTED;
+    if (ru && (ru->n_graphs < 1 || !ru->stats || !ru->graph_ptr || !ru->running_mean ||
+               !ru->running_var))
+        return SCGIB_EINVAL;
+    const unsigned grid = static_cast<unsigned>((n_rows + kHeadRows - 1) / kHeadRows + (ru ? 1 : 0));
     head_fwd_k<<<grid, 256, 0, as_stream(stream)>>>(x, n_rows, k_in, w1, b1, w2, b2, n_out,
-                                                    sigmoid ? 1 : 0, hid, out);
+                                                    sigmoid ? 1 : 0, hid, out,
+                                                    ru ? *ru : scgib_running_update{}, ru ? 1 : 0);
     return launch_status();
 }
 
@@ -284,7 +364,9 @@ extern "C" int scgib_head_bwd(const float *x, const float *hid, const float *out
         return SCGIB_EINVAL;
     if (!x || !hid || !out || !d_out || !w1 || !w2 || !dx || !dw1 || !db1 || !dw2 || !db2)
         return SCGIB_EINVAL;
-    head_bwd_k<<<1, 256, 0, as_stream(stream)>>>(x, hid, out, d_out, n_rows, k_in, w1, w2, n_out,
+    if (k_in % 4 || !head_aligned(x) || !head_aligned(w1) || !head_aligned(hid))
+        return SCGIB_EUNSUPPORTED;
+    head_bwd_k<<<kHeadG, 256, 0, as_stream(stream)>>>(x, hid, out, d_out, n_rows, k_in, w1, w2, n_out,
                                                  sigmoid ? 1 : 0, dx, dw1, db1, dw2, db2);
     return launch_status();
 }

@@ -1121,8 +1121,11 @@ class _PredictHead(torch.autograd.Function):
         c = w2.shape[0]
         hid = torch.empty(n, HIDDEN, dtype=torch.float32, device=x.device)
         out = torch.empty(n, c, dtype=torch.float32, device=x.device)
+        # the compressor BN running update left by the interaction forward (inside
+        # a model forward): one extra workgroup of this launch, not an aux launch
+        ru = take_running_update()
         _lib.call("scgib_head_fwd", _p(x), n, k, _p(w1), _p(b1), _p(w2), _p(b2), c, int(sigmoid),
-                  _p(hid), _p(out), _stream())
+                  _p(hid), _p(out), _byref(ru[0] if ru else None), _stream())
         ctx.save_for_backward(x, hid, out, w1, w2)
         ctx.sigmoid = bool(sigmoid)
         return out
@@ -1144,14 +1147,14 @@ class _PredictHead(torch.autograd.Function):
 def predict_head_ok(x, seq):
     """Whether ``seq`` is the fine-tune head the kernels implement:
     Sequential(Linear(K <= 128, 64), ReLU, Linear(64, C <= 16)) on a [B, K]
-    HIP tensor."""
+    HIP tensor, K a multiple of 4."""
     import torch.nn as nn
     return (x.is_cuda and x.dim() == 2 and len(seq) == 3 and isinstance(seq[0], nn.Linear)
             and isinstance(seq[1], nn.ReLU) and isinstance(seq[2], nn.Linear)
             and seq[0].bias is not None and seq[2].bias is not None
             and seq[0].out_features == HIDDEN and seq[2].in_features == HIDDEN
             and x.shape[1] == seq[0].in_features and 1 <= x.shape[1] <= 128
-            and 1 <= seq[2].out_features <= 16)
+            and x.shape[1] % 4 == 0 and 1 <= seq[2].out_features <= 16)
 
 
 def predict_head(x, seq, sigmoid):

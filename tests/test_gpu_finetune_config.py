@@ -223,12 +223,14 @@ def test_frozen_layers_skip_weight_grads_bitwise(pkg, dev, case):
 
 
 @pytest.mark.parametrize("n,k,c,sig", [(32, 128, 1, True), (32, 128, 2, True), (1, 128, 1, True),
-                                       (33, 64, 3, False), (100, 128, 1, True), (7, 9, 16, False)])
+                                       (33, 64, 3, False), (100, 128, 1, True), (7, 12, 16, False),
+                                       (5, 36, 2, True)])
 def test_predict_head_and_bce_vs_torch(pkg, dev, n, k, c, sig):
     """csrc/head.hip against torch in float64: the head's output (and its
     sigmoid), every gradient, and the BCE loss and its gradient (the tail of
     Mainmodel_finetuning, models.py:510-523).  n = 100: backward row chunks
-    of 32 with a partial last one; k = 9 / 64: K padding of the float4 runs."""
+    of 32 with a partial last one; k = 12 / 36 / 64: dx column slices of the
+    four backward workgroups that are empty / uneven / half width."""
     import torch.nn as nn
     gen = torch.Generator().manual_seed(n * 1000 + k + c)
     seq = nn.Sequential(nn.Linear(k, 64), nn.ReLU(), nn.Linear(64, c))
@@ -258,3 +260,15 @@ def test_predict_head_and_bce_vs_torch(pkg, dev, n, k, c, sig):
         l.backward()
         assert rel_err(l.item(), lr.item()) < 1e-5
         assert rel_err(s.grad.cpu(), s64.grad) < 1e-4
+
+
+def test_predict_head_refuses_k_not_multiple_of_4(pkg, dev):
+    """The head kernels stage float4 runs: K % 4 != 0 is not the fused head
+    (predict_head_ok False: the model keeps torch's head) and the C-ABI
+    refuses it loudly."""
+    import torch.nn as nn
+    seq = nn.Sequential(nn.Linear(9, 64), nn.ReLU(), nn.Linear(64, 1)).to(dev)
+    x = torch.randn(4, 9, device=dev)
+    assert not pkg.ops.predict_head_ok(x, seq)
+    with pytest.raises(pkg._lib.ScgibError):
+        pkg.ops.predict_head(x, seq, True)

@@ -14,8 +14,10 @@ if [ -z "$NO_TESTS" ]; then
 fi
 for i in $(seq ${ROUNDS:-3}); do
   for cfg in "$@"; do
-    timeout -k 10 200 python bench.py --finetune molhiv --steps 300 --warmup 20 --no-cpu-baseline \
-      --no-kernel-timer $cfg > $O/ft_last.log 2>&1 || { echo "ft [$cfg] failed"; tail -5 $O/ft_last.log; exit 1; }
+    dir=.; args="$cfg"
+    if [[ "$cfg" == DIR=* ]]; then dir=${cfg#DIR=}; args=""; fi  # another revision (tools/make_ab_tree.sh)
+    (cd $dir && timeout -k 10 200 python bench.py --finetune molhiv --steps 300 --warmup 20 --no-cpu-baseline \
+      --no-kernel-timer $args) > $O/ft_last.log 2>&1 || { echo "ft [$cfg] failed"; tail -5 $O/ft_last.log; exit 1; }
     tail -1 $O/ft_last.log | python -c "import sys,json; d=json.loads(sys.stdin.read()); print('[$cfg]', d['ms_per_step'], d['value'])" | tee -a $O/ft_ab.txt
   done
 done

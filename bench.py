@@ -866,12 +866,24 @@ def main():
         torch.cuda.synchronize()
 
     barrier()
+    # SCGIB_STEP_PROBE=1 (diagnostics only, tools/gpu_steps_probe.sh): HIP events
+    # around every timed step
+    probe = [] if os.environ.get("SCGIB_STEP_PROBE") == "1" else None
     t0 = time.perf_counter()
     for i in range(a.steps):
+        if probe is not None:
+            probe.append(torch.cuda.Event(enable_timing=True))
+            probe[-1].record()
         loss = step(a.warmup + i)
+    if probe is not None:
+        probe.append(torch.cuda.Event(enable_timing=True))
+        probe[-1].record()
     t_enq = time.perf_counter() - t0  # host time to enqueue the K steps
     barrier()
     elapsed = time.perf_counter() - t0
+    if probe is not None:
+        progress("step probe (ms): " + " ".join(
+            f"{probe[i].elapsed_time(probe[i + 1]):.4f}" for i in range(len(probe) - 1)))
     progress(f"timed: {elapsed / a.steps * 1e3:.4f} ms/step, host enqueue "
              f"{t_enq / a.steps * 1e3:.4f} ms/step")
     xq_to = pkg.ops.xq_timeouts(dev)

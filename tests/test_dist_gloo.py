@@ -110,8 +110,15 @@ def test_grad_allreduce_matches_mean_of_shards(pkg, world):
         for k, v in gr.items():
             expect[k] = expect.get(k, 0) + v / world
     assert set(got) == set(expect)
+    # absolute floor on the model's gradient scale: some tensors' true gradient
+    # is exactly zero (a GIN MLP's last bias feeds a BatchNorm, which removes
+    # it), so both sides hold fp32 summation-order noise there (CPU threads
+    # differ between the workers and this process); an all-reduce or sharding
+    # error is of the gradients' own size
+    scale = max(float(v.abs().max()) for v in expect.values())
     for k in expect:
-        assert torch.allclose(torch.from_numpy(got[k]), expect[k], rtol=1e-5, atol=1e-7), k
+        assert torch.allclose(torch.from_numpy(got[k]), expect[k], rtol=1e-5,
+                              atol=1e-5 * scale), k
 
 
 def test_shard_covers_everything_once(pkg):

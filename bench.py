@@ -780,7 +780,9 @@ def main():
 
         def body():
             # the pool's next batch (and its prefetched ego-nets) into the static inputs
+            pkg.ops.stamp("step_start")
             static.load_next(pool_dev, prefetch)
+            pkg.ops.stamp("loaded")
             _, kl, con, rec = model(static.graph, static.x, None, None, None, 1, None, a.k, dev,
                                     a.batch)
             # loss = KL + contrastive + recon (exp_pretraining.py:321): d loss / d part = 1,
@@ -808,6 +810,8 @@ def main():
         torch.cuda.current_stream().wait_stream(side)
         torch.cuda.synchronize()
         graph2 = None
+        if os.environ.get("SCGIB_STAMPS"):  # diagnostics: wall-clock stamps in the captured step
+            pkg.ops.stamps_enable(dev, int(os.environ["SCGIB_STAMPS"]))
         graph = torch.cuda.CUDAGraph()
         opt.zero_grad(set_to_none=True)
         # N > 1: the RCCL all-reduce captured inside the replayed step graph
@@ -881,6 +885,9 @@ def main():
     t_enq = time.perf_counter() - t0  # host time to enqueue the K steps
     barrier()
     elapsed = time.perf_counter() - t0
+    if os.environ.get("SCGIB_STAMPS"):
+        for lab, us in pkg.ops.stamps_read():
+            progress(f"stamp {us:9.2f} us  {lab}")
     if probe is not None:
         progress("step probe (ms): " + " ".join(
             f"{probe[i].elapsed_time(probe[i + 1]):.4f}" for i in range(len(probe) - 1)))

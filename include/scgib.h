@@ -98,6 +98,10 @@ int scgib_pool_copy2(const uint64_t *srcs, int32_t n_src, uint32_t *ctr, void *d
 int scgib_stream_signal(uint32_t *words, scgib_stream_t stream);
 int scgib_stream_wait(uint32_t *words, uint32_t *fault, uint32_t *host_fault,
                       scgib_stream_t stream);
+/* Diagnostics: writes the 100 MHz device wall clock (s_memrealtime) to
+ * buf[slot] when the stream reaches this point (ops.stamps: the timeline of
+ * a replayed step with its hand-offs on; not on the product path). */
+int scgib_stamp(uint64_t *buf, int32_t slot, scgib_stream_t stream);
 const char *scgib_strerror(int code);
 
 /* ---- A5: GIN neighbourhood aggregation (DGL GINConv, sum aggregator) ------

@@ -32,6 +32,7 @@ SIGNATURES = {
     "scgib_pool_copy": (ctypes.c_int, [_P, _I32, _P, _P, _I64, _P]),
     "scgib_pool_copy2": (ctypes.c_int, [_P, _I32, _P, _P, _I64, _P, _P, _I64, _P]),
     "scgib_stream_signal": (ctypes.c_int, [_P, _P]),
+    "scgib_stamp": (ctypes.c_int, [_P, _I32, _P]),
     "scgib_stream_wait": (ctypes.c_int, [_P, _P, _P, _P]),
     "scgib_strerror": (ctypes.c_char_p, [ctypes.c_int]),
     "scgib_gin_aggregate": (ctypes.c_int, [_P, _P, _P, _I64, _I32, _F, _P, _P, _P]),

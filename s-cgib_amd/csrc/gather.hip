@@ -283,6 +283,19 @@ extern "C" int scgib_stream_signal(uint32_t *words, scgib_stream_t stream) {
     return launch_status();
 }
 
+// Diagnostics (ops.stamps): the 100 MHz wall clock into buf[slot] when this
+// point of the stream is reached — a replayed step's timeline with the
+// hand-offs on (a kernel trace turns them off, ops.handoff_rule).
+__global__ void stamp_k(uint64_t *buf, int32_t slot) {
+    if (threadIdx.x == 0) buf[slot] = wall_clock64();
+}
+
+extern "C" int scgib_stamp(uint64_t *buf, int32_t slot, scgib_stream_t stream) {
+    if (!buf || slot < 0) return SCGIB_EINVAL;
+    stamp_k<<<1, 64, 0, as_stream(stream)>>>(buf, slot);
+    return launch_status();
+}
+
 extern "C" int scgib_stream_wait(uint32_t *words, uint32_t *fault, uint32_t *host_fault,
                                  scgib_stream_t stream) {
     if (!words) return SCGIB_EINVAL;

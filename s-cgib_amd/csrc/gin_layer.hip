@@ -766,7 +766,7 @@ __global__ __launch_bounds__(256, (kFwdAlias<DIN, GATHER, PRE> ? 3 : 1)) void gi
 #pragma unroll
         for (int k = 0; k < RPT; ++k) {
             const int rr = rbase + k * RPP;
-            if (rr < nv) st4(agg_out + (row0 + rr) * DIN + 4 * c, acc[k]);
+            if (rr < nv) st4_saved(agg_out + (row0 + rr) * DIN + 4 * c, acc[k]);
             float *d = sA + rr * LDA + 4 * c;
             d[0] = acc[k].x; d[1] = acc[k].y; d[2] = acc[k].z; d[3] = acc[k].w;
         }
@@ -790,7 +790,7 @@ __global__ __launch_bounds__(256, (kFwdAlias<DIN, GATHER, PRE> ? 3 : 1)) void gi
             const int row = wr * 32 + acc_row(reg, l);
             const float v = fmaxf(acc[reg] + bias, 0.f);
             sR[row * LDH + ccol] = v;
-            if (r_out && row < nv) r_out[(row0 + row) * 64 + ccol] = v;
+            if (r_out && row < nv) st_saved(&r_out[(row0 + row) * 64 + ccol], v);
         }
     }
     __syncthreads();
@@ -807,7 +807,7 @@ __global__ __launch_bounds__(256, (kFwdAlias<DIN, GATHER, PRE> ? 3 : 1)) void gi
             if constexpr (RECON)  // write-through: the fused finish reads it from other CUs
                 st_agent(&z2_out[(row0 + row) * 64 + ccol], acc[reg]);
             else
-                z2_out[(row0 + row) * 64 + ccol] = acc[reg];
+                st_saved(&z2_out[(row0 + row) * 64 + ccol], acc[reg]);
             s += acc[reg];
         }
     }

@@ -21,6 +21,24 @@ __device__ __forceinline__ f32x16 zero16() {
 
 __device__ __forceinline__ float4 ld4(const float *p) { return *reinterpret_cast<const float4 *>(p); }
 __device__ __forceinline__ void st4(float *p, float4 v) { *reinterpret_cast<float4 *>(p) = v; }
+
+// The forward layer's saved activations (agg, r, z2: read next by the
+// backward, or by the next layer's gather): plain stores, or with
+// SCGIB_NT_SAVED=1 (build-time A/B hook) non-temporal ones.
+#ifndef SCGIB_NT_SAVED
+#define SCGIB_NT_SAVED 0
+#endif
+typedef float scgib_f4v __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void st_saved(float *p, float v) {
+    if constexpr (SCGIB_NT_SAVED != 0) __builtin_nontemporal_store(v, p);
+    else *p = v;
+}
+__device__ __forceinline__ void st4_saved(float *p, float4 v) {
+    if constexpr (SCGIB_NT_SAVED != 0)
+        __builtin_nontemporal_store(scgib_f4v{v.x, v.y, v.z, v.w}, reinterpret_cast<scgib_f4v *>(p));
+    else
+        *reinterpret_cast<float4 *>(p) = v;
+}
 __device__ __forceinline__ float4 add4(float4 a, float4 b) { return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w); }
 __device__ __forceinline__ float4 xform4(float4 z, float4 a, float4 b) {
     return make_float4(fmaxf(a.x * z.x + b.x, 0.f), fmaxf(a.y * z.y + b.y, 0.f),

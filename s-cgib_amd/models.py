@@ -251,6 +251,7 @@ class _SCGIBCore(nn.Module):
                                                               enc_owner.compressor,
                                                               enc_owner.attn_layer, batch_g,
                                                               enc_owner.training)
+        ops.stamp("interaction_end")
         enc_owner._last_kl_mean = kl_mean
         # the draws when noise was None (replayable via noise=)
         enc_owner._last_noise = (u_gate, u_feat) if noise is None else None
@@ -511,6 +512,7 @@ class Mainmodel_continue(_SCGIBCore):
         kl_loss, con, rec = self._losses(batch_g, im, self.model._last_kl_mean,
                                          self.model._last_z1, z2, self.MLP, batch_size,
                                          batch_logMs)
+        ops.stamp("losses_end")
         ops.join_aside()
         _drop_graph_refs(self, self.model)
         return None, kl_loss, con, rec

@@ -352,13 +352,56 @@ def _gin_layer_params(gin):
     return out
 
 
-def _drain(gen):
-    """Run a step generator to completion and return its value."""
+def _drain(gen, tag=None):
+    """Run a step generator to completion and return its value (``tag``:
+    stamps at each of its yields, at stamp level 2)."""
+    i = 0
     while True:
         try:
             next(gen)
         except StopIteration as stop:
             return stop.value
+        if tag is not None and _STAMPS["level"] >= 2:
+            stamp(f"{tag}.{i}")
+        i += 1
+
+
+# ---------------------------------------------------------------------------
+# Diagnostics: device wall-clock stamps (scgib_stamp) at the step's chain
+# boundaries, for the timeline of a REPLAYED step with its hand-offs on (a
+# rocprofv3 kernel trace serialises the queues' submission, so the hand-offs
+# are off there: ops.handoff_rule).  Off unless stamps_enable() was called
+# (bench.py: SCGIB_STAMPS=1 coarse, =2 also one per GIN layer); each stamp is
+# one more 1-thread launch on its stream.
+# ---------------------------------------------------------------------------
+_STAMPS = {"buf": None, "labels": [], "level": 0}
+
+
+def stamps_enable(device, level=1, slots=256):
+    _STAMPS["buf"] = torch.zeros(slots, dtype=torch.int64, device=device)
+    _STAMPS["labels"] = []
+    _STAMPS["level"] = int(level)
+
+
+def stamp(label):
+    """The device wall clock when the current stream reaches this point (when
+    stamps are enabled; a no-op otherwise)."""
+    buf = _STAMPS["buf"]
+    if buf is None or len(_STAMPS["labels"]) >= buf.numel():
+        return
+    _STAMPS["labels"].append(label)
+    _lib.call("scgib_stamp", _p(buf), len(_STAMPS["labels"]) - 1, _stream())
+
+
+def stamps_read():
+    """[(label, us after the first stamp)] of the last replay / run, in time order."""
+    buf = _STAMPS["buf"]
+    if buf is None or not _STAMPS["labels"]:
+        return []
+    t = buf[:len(_STAMPS["labels"])].cpu().tolist()
+    t0 = min(t)
+    return sorted(((lab, (v - t0) / 100.0) for lab, v in zip(_STAMPS["labels"], t)),
+                  key=lambda e: e[1])
 
 
 def _reduce_jobs(jobs, st, max_wg=0):
@@ -501,7 +544,8 @@ class _GinEncoder(torch.autograd.Function):
     def backward(ctx, g_out, g_readout=None):
         if not isinstance(ctx, _Ctx):  # (the encoder pair sets its sub-contexts' own)
             ctx.need = ctx.needs_input_grad[7:]
-        return _drain(_GinEncoder.backward_steps(ctx, g_out, g_readout))
+        return _drain(_GinEncoder.backward_steps(ctx, g_out, g_readout),
+                      getattr(ctx, "stamp_tag", None))
 
     @staticmethod
     def backward_steps(ctx, g_out, g_readout=None):
@@ -882,6 +926,9 @@ class _GinEncoderPair(torch.autograd.Function):
         ctx.lin = w0 is not None
         ctx.lin_leaves = (w0, b0)
         side.wait_stream(main)
+        stamp("fwd.fork[main]")
+        with torch.cuda.stream(side):
+            stamp("fwd.start[side]")
         if core_tail is not None:  # beside the ego-net build
             core_tail()
         # Encoder2 + its readout (dgl.sum_nodes per ego-net) on ``side``,
@@ -892,8 +939,10 @@ class _GinEncoderPair(torch.autograd.Function):
         core_steps = _GinEncoder.forward_steps(ctx.sub[1], None, core, gin_core, training, x, wt,
                                                None, *params[ne:])
         with torch.cuda.stream(side):
-            s, ro = _drain(ego_steps)
-        f = _drain(core_steps)
+            s, ro = _drain(ego_steps, "fwd.ego")
+            stamp("fwd.ego_end[side]")
+        f = _drain(core_steps, "fwd.core")
+        stamp("fwd.core_end[main]")
         outs = (s, ro, f)
         if ctx.lin:  # compressor[0] on the (shorter) core chain, before the join
             w0, b0 = _f32(w0, "compressor.0.weight"), _f32(b0, "compressor.0.bias")
@@ -912,6 +961,7 @@ class _GinEncoderPair(torch.autograd.Function):
             _xq_handoff(side, main, "pair_fwd")
         else:
             main.wait_stream(side)
+        stamp("fwd.joined[main]")
         if side_tail is not None:
             # after the hand-off: ``side`` idles through the loss section; the
             # backward's core chain follows it there and joins main at its end
@@ -930,10 +980,13 @@ class _GinEncoderPair(torch.autograd.Function):
         # by compressor[0]'s backward (d f += d t W0, dW0, db0)
         main, side = _torch_stream(), ctx.side
         check_fork(main)
+        stamp("bwd.start[main]")
         if XQ_FLAGS:
             _xq_handoff(main, side, "pair_bwd")
         else:
             side.wait_stream(main)
+        with torch.cuda.stream(side):
+            stamp("bwd.start[side]")
         # Encoder1's final weight-gradient reduce runs beside the ego chain's
         # last layers; it also sums the loss section's deferred slabs
         # (SlabScope: the head MLP's and the interaction's, enqueued on the
@@ -947,7 +1000,9 @@ class _GinEncoderPair(torch.autograd.Function):
         g_f_in = g_f
         # the critical ego chain is captured first: the replayed graph then
         # puts it on the interaction's queue (round 2: 0.4381 -> 0.4326 ms)
+        ctx.sub[0].stamp_tag = "bwd.ego"
         ge = _GinEncoder.backward(ctx.sub[0], g_s, g_ro)
+        stamp("bwd.ego_end[main]")
         with torch.cuda.stream(side):
             if ctx.lin and g_t is not None:
                 f, w0 = ctx.lin_saved
@@ -980,8 +1035,10 @@ class _GinEncoderPair(torch.autograd.Function):
                     jobs = jobs[:big] + jobs[big + 1:]
                     keep = keep[:2 * big] + keep[2 * big + 2:]
                 ctx.sub[1].extra_jobs = (jobs, keep)
-            gc = _drain(_GinEncoder.backward_steps(ctx.sub[1], g_f))
+            gc = _drain(_GinEncoder.backward_steps(ctx.sub[1], g_f), "bwd.core")
+            stamp("bwd.core_end[side]")
         main.wait_stream(side)
+        stamp("bwd.joined[main]")
         if ctx.side_tail is not None and hasattr(ctx.side_tail, "joined"):
             ctx.side_tail.joined()  # ordered before main's later work by the join above
         held = None  # after the join: main-stream reuse is ordered after side's reads

@@ -78,4 +78,5 @@ class Adam(torch.optim.Optimizer):
                 _lib.call("scgib_adam_step", ctypes.cast(table, ctypes.c_void_p), len(chunk),
                           float(group["lr"]), float(b1), float(b2), float(group["eps"]),
                           float(group["weight_decay"]), ops._p(cnt), st)
+        ops.stamp("adam_end")
         return loss

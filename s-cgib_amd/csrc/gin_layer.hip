@@ -2090,8 +2090,20 @@ extern "C" int64_t scgib_gin_slab_floats(int64_t n_nodes, int32_t d_in) {
     return scgib_gin_layer_bwd_slabs(n_nodes, d_in) * (64 * 64 + 64 * d_in + 128);
 }
 
+// layer 0 (transfer_d folded): one tile per workgroup up to SCGIB_BWD0_CAP
+// workgroups; past it, the fewest workgroups with the same per-workgroup tile
+// count (build-time A/B hook: tools/build_ab_lib.sh EXTRA=-DSCGIB_BWD0_CAP=n)
+#ifndef SCGIB_BWD0_CAP
+#define SCGIB_BWD0_CAP kBwdGridCap
+#endif
+static int bwd0_grid(int64_t nt) {
+    constexpr int64_t cap = SCGIB_BWD0_CAP;
+    const int64_t per = (nt + cap - 1) / cap;
+    return static_cast<int>((nt + per - 1) / per);
+}
+
 extern "C" int64_t scgib_gin_bwd_slabs(int64_t n_nodes) {
-    return n_nodes <= 0 ? 0 : bwd_grid(scgib_gin_tiles(n_nodes));
+    return n_nodes <= 0 ? 0 : bwd0_grid(scgib_gin_tiles(n_nodes));
 }
 
 static int launch_gin_fwd(const float *h_in, int32_t d_in, const float *in_stat,
@@ -2709,15 +2721,15 @@ extern "C" int scgib_gin_layer0_bwd(const float *dy, const float *z2, const floa
     const scgib_bn_bwd_pending pd = pending ? *pending : scgib_bn_bwd_pending{};
     const int64_t nt = scgib_gin_tiles(n_nodes);
     if (!need_w)
-        gin_bwd_k<32, true, true, false, false, false><<<bwd_grid(nt), 256, 0, as_stream(stream)>>>(
+        gin_bwd_k<32, true, true, false, false, false><<<bwd0_grid(nt), 256, 0, as_stream(stream)>>>(
             dy, z2, r, agg, stat, coef, w1, w2, n_nodes, nt, nullptr, slab, dims, aggx, pd, ReconArgs{},
             n_feat);
     else if (r)
-        gin_bwd_k<32, true, true><<<bwd_grid(nt), 256, 0, as_stream(stream)>>>(
+        gin_bwd_k<32, true, true><<<bwd0_grid(nt), 256, 0, as_stream(stream)>>>(
             dy, z2, r, agg, stat, coef, w1, w2, n_nodes, nt, nullptr, slab, dims, aggx, pd, ReconArgs{},
             n_feat);
     else
-        gin_bwd_k<32, true, true, false, true><<<bwd_grid(nt), 256, 0, as_stream(stream)>>>(
+        gin_bwd_k<32, true, true, false, true><<<bwd0_grid(nt), 256, 0, as_stream(stream)>>>(
             dy, z2, nullptr, agg, stat, coef, w1, w2, n_nodes, nt, nullptr, slab, dims, aggx, pd,
             ReconArgs{}, n_feat, b1);
     return launch_status();

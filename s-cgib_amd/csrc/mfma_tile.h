@@ -23,10 +23,11 @@ __device__ __forceinline__ float4 ld4(const float *p) { return *reinterpret_cast
 __device__ __forceinline__ void st4(float *p, float4 v) { *reinterpret_cast<float4 *>(p) = v; }
 
 // The forward layer's saved activations (agg, r, z2: read next by the
-// backward, or by the next layer's gather): plain stores, or with
-// SCGIB_NT_SAVED=1 (build-time A/B hook) non-temporal ones.
+// backward, or by the next layer's gather) as non-temporal stores (1.6 % off
+// the 1.2 M-row superbatch layer, neutral at QM9 B512: profiles/r05_nt);
+// SCGIB_NT_SAVED=0 (build-time A/B hook) for plain ones.
 #ifndef SCGIB_NT_SAVED
-#define SCGIB_NT_SAVED 0
+#define SCGIB_NT_SAVED 1
 #endif
 typedef float scgib_f4v __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ void st_saved(float *p, float v) {

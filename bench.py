@@ -204,7 +204,9 @@ KERNELS = {
                            "2 f32-MFMA GEMMs + BN tile statistics"),
     "gin_bwd5_k": dict(entries=("scgib_gin_layer_bwd",), keep=lambda m: m["d_in"] == 64,
                        bytes=layer_bwd_bytes, flops=layer_bwd_flops,
-                       pmc=["gin_bwd5r_k<64>", "gin_bwd5_k<64>"],
+                       # (the instance with weight products: <64, true>; <64, false>
+                       # is the frozen-layer fine-tune kernel)
+                       pmc=["gin_bwd5r_k<64>", "gin_bwd5_k<64, true>", "gin_bwd5_k<64>"],
                        desc="fused GIN layer backward (d_in = 64): BN-backward apply + 4 "
                             "f32-MFMA GEMMs on 32-row sub-tiles (gin_bwd5r_k: + the hidden "
                             "activation r recomputed, not read; flops count the 4 GEMMs)"),

@@ -173,6 +173,8 @@ def run(bench, a, dev):
     torch.cuda.current_stream().wait_stream(side)
     torch.cuda.synchronize()
     opt.zero_grad(set_to_none=True)
+    if os.environ.get("SCGIB_STAMPS"):  # diagnostics: wall-clock stamps in the captured step
+        pkg.ops.stamps_enable(dev, int(os.environ["SCGIB_STAMPS"]))
     graph = torch.cuda.CUDAGraph()
     with torch.cuda.graph(graph):
         static_loss = body()
@@ -189,6 +191,11 @@ def run(bench, a, dev):
     if pkg.ops.xq_timeouts(dev) or pkg.ops.handoff_fault(dev):
         raise SystemExit("bench: a cross-queue hand-off wait timed out (ops.XQ_FLAGS)")
     pkg.ops.check_handoff(dev)
+    if os.environ.get("SCGIB_STAMPS"):
+        for lab, us in pkg.ops.stamps_read():
+            bench.progress(f"stamp {us:9.2f} us  {lab}")
+        pkg.ops.stamps_enable(dev, 0)
+        pkg.ops._STAMPS["buf"] = None
     final_loss = float(static_loss.item())
     # kernel timer: eager fine-tune steps on one stream, HIP events per launch
     kernels = {}

@@ -308,7 +308,11 @@ int scgib_gin_hidden(const float *agg, int32_t d_in, const float *w1, const floa
  * save [scgib_set2set_save_floats]: the per-round state the backward reads.
  * Backward: d out -> dx (rows past graph_ptr[n_graphs], up to n_rows:
  * capacity padding, zeroed), dw_ih, dw_hh, db_ih = db_hh; dgates
- * [n_graphs * n_iters * 4 dim] is scratch.  No host sync: graph-capturable. */
+ * [n_graphs * n_iters * 4 dim] is scratch.  No host sync: graph-capturable.
+ * With dw_ih, dw_hh, db_ih and db_hh all NULL, scgib_set2set_bwd writes dx and
+ * dgates only, and scgib_set2set_wgrad (the same save / dgates) forms the
+ * weight gradients later — the fine-tune step runs it off the critical
+ * chain (ops.SlabScope). */
 int64_t scgib_set2set_save_floats(int64_t n_graphs, int32_t dim, int32_t n_iters);
 int scgib_set2set_fwd(const float *x, const int32_t *graph_ptr, int64_t n_graphs, int32_t dim,
                       int32_t n_iters, const float *w_ih, const float *b_ih, const float *w_hh,
@@ -318,6 +322,9 @@ int scgib_set2set_bwd(const float *x, const int32_t *graph_ptr, int64_t n_graphs
                       const float *g_out, float *dx, int64_t n_rows, float *dgates,
                       float *dw_ih, float *dw_hh, float *db_ih, float *db_hh,
                       scgib_stream_t stream);
+int scgib_set2set_wgrad(const float *save, const float *dgates, int64_t n_graphs, int32_t dim,
+                        int32_t n_iters, float *dw_ih, float *dw_hh, float *db_ih, float *db_hh,
+                        scgib_stream_t stream);
 
 /* ---- A6: per-segment readouts (dgl.sum_nodes) -------------------------------
  * out[s,:] = sum_{i in [ptr[s], ptr[s+1])} x[i,:]   (models.py:716, 725, 733)

@@ -23,6 +23,7 @@ SIGNATURES = {
     "scgib_set2set_fwd": (ctypes.c_int, [_P, _P, _I64, _I32, _I32, _P, _P, _P, _P, _P, _P, _P]),
     "scgib_set2set_bwd": (ctypes.c_int, [_P, _P, _I64, _I32, _I32, _P, _P, _P, _P, _P, _I64, _P,
                                          _P, _P, _P, _P, _P]),
+    "scgib_set2set_wgrad": (ctypes.c_int, [_P, _P, _I64, _I32, _I32, _P, _P, _P, _P, _P]),
     "scgib_head_fwd": (ctypes.c_int, [_P, _I64, _I32, _P, _P, _P, _P, _I32, _I32, _P, _P, _P,
                                       _P]),
     "scgib_head_bwd": (ctypes.c_int, [_P, _P, _P, _P, _I64, _I32, _P, _P, _I32, _I32, _P, _P,
@@ -178,7 +179,7 @@ class RunningUpdate(ctypes.Structure):
                 ("num_batches_tracked", ctypes.c_void_p)]
 
 
-ABI_VERSION = 17
+ABI_VERSION = 18
 STATS_STRIDE = 260
 PGRAD_STRIDE = 324
 HIDDEN = 64

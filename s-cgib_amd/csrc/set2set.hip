@@ -514,8 +514,11 @@ extern "C" int scgib_set2set_bwd(const float *x, const int32_t *graph_ptr, int64
     if (n_graphs < 0 || dim < 1 || dim > kS2SMaxD || n_iters < 1 || n_rows < 0)
         return SCGIB_EINVAL;
     if (n_graphs == 0) return SCGIB_OK;
-    if (!x || !graph_ptr || !w_ih || !w_hh || !save || !g_out || !dx || !dgates || !dw_ih ||
-        !dw_hh || !db_ih || !db_hh)
+    // the four weight gradients all NULL: the data gradient only (dgates kept
+    // for a later scgib_set2set_wgrad)
+    const bool wg = dw_ih || dw_hh || db_ih || db_hh;
+    if (!x || !graph_ptr || !w_ih || !w_hh || !save || !g_out || !dx || !dgates ||
+        (wg && (!dw_ih || !dw_hh || !db_ih || !db_hh)))
         return SCGIB_EINVAL;
     hipStream_t st = as_stream(stream);
     const int64_t tail = (n_rows * dim + 256 * 16 - 1) / (256 * 16);  // padding-zero blocks
@@ -523,8 +526,19 @@ extern "C" int scgib_set2set_bwd(const float *x, const int32_t *graph_ptr, int64
     set2set_bwd_k<<<static_cast<unsigned>(n_graphs + extra), 256, 0, st>>>(
         x, graph_ptr, n_graphs, dim, n_iters, w_ih, w_hh, save, g_out, dx, dgates, n_rows);
     int rc = launch_status();
-    if (rc != SCGIB_OK) return rc;
+    if (rc != SCGIB_OK || !wg) return rc;
     set2set_wgrad_k<<<static_cast<unsigned>(3 * dim + 1), 256, 0, st>>>(
+        save, dgates, n_graphs * n_iters, dim, dw_ih, dw_hh, db_ih, db_hh);
+    return launch_status();
+}
+
+extern "C" int scgib_set2set_wgrad(const float *save, const float *dgates, int64_t n_graphs,
+                                   int32_t dim, int32_t n_iters, float *dw_ih, float *dw_hh,
+                                   float *db_ih, float *db_hh, scgib_stream_t stream) {
+    if (n_graphs < 0 || dim < 1 || dim > kS2SMaxD || n_iters < 1) return SCGIB_EINVAL;
+    if (n_graphs == 0) return SCGIB_OK;
+    if (!save || !dgates || !dw_ih || !dw_hh || !db_ih || !db_hh) return SCGIB_EINVAL;
+    set2set_wgrad_k<<<static_cast<unsigned>(3 * dim + 1), 256, 0, as_stream(stream)>>>(
         save, dgates, n_graphs * n_iters, dim, dw_ih, dw_hh, db_ih, db_hh);
     return launch_status();
 }

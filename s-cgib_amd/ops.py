@@ -104,7 +104,7 @@ class SlabScope:
     _device_ok = staticmethod(lambda p: p.is_cuda)
 
     def __init__(self):
-        self.jobs, self.keep = [], []
+        self.jobs, self.keep, self.later = [], [], []
         self.open, self.ok, self.callback, self.stream = True, True, False, None
         for other in list(SlabScope._live):
             if other.open:  # two forwards awaiting one backward: defer nothing
@@ -130,7 +130,18 @@ class SlabScope:
     def add(self, slab, wgrad, width, n_slabs):
         self.jobs.append(_lib.SlabJob(slab.data_ptr(), wgrad.data_ptr(), width, n_slabs, 0))
         self.keep += [slab, wgrad]
-        self.stream = torch.cuda.current_stream() if slab.is_cuda else None
+        self._arm(slab)
+
+    def defer(self, launch, *tensors):
+        """A weight-gradient launch nothing before the optimizer reads (the
+        Set2Set LSTM's, scgib_set2set_wgrad): enqueued by the encoder pair's
+        backward on the current stream after the ego chain's backward, off the
+        loss section's serial chain; ``tensors`` stay referenced until then."""
+        self.later.append((launch, tensors))
+        self._arm(tensors[0])
+
+    def _arm(self, t):
+        self.stream = torch.cuda.current_stream() if t.is_cuda else None
         if not self.callback:
             # a backward that never reaches the encoder pair (autograd.grad over
             # the loss-section parameters only, backward(inputs=...)) would never
@@ -142,12 +153,20 @@ class SlabScope:
                 pass
 
     def _flush(self):
-        if not self.open or not self.jobs:
+        if not self.open or not (self.jobs or self.later):
             return
+        later = self.take_later()
         jobs, keep = self.take()
         with torch.cuda.stream(self.stream):
-            _reduce_jobs(jobs, _stream())
-        del keep  # the slabs stay allocated until the launch is enqueued
+            for launch, _ in later:
+                launch()
+            if jobs:
+                _reduce_jobs(jobs, _stream())
+        del keep, later  # the slabs stay allocated until the launches are enqueued
+
+    def take_later(self):
+        later, self.later = self.later, []
+        return later
 
     def take(self):
         self.open = False
@@ -1001,7 +1020,11 @@ class _GinEncoderPair(torch.autograd.Function):
         # the critical ego chain is captured first: the replayed graph then
         # puts it on the interaction's queue (round 2: 0.4381 -> 0.4326 ms)
         ctx.sub[0].stamp_tag = "bwd.ego"
+        later = scope.take_later() if scope is not None else []
         ge = _GinEncoder.backward(ctx.sub[0], g_s, g_ro)
+        for launch, _ in later:  # deferred weight-gradient launches, after the ego chain
+            launch()
+        later = None
         stamp("bwd.ego_end[main]")
         with torch.cuda.stream(side):
             if ctx.lin and g_t is not None:
@@ -1131,6 +1154,8 @@ class _Set2Set(torch.autograd.Function):
                 tuple(w_hh.shape) != (4 * d, d) or b_ih.numel() != 4 * d or b_hh.numel() != 4 * d:
             raise _lib.ScgibError(f"set2set: x {tuple(x.shape)} (width <= 64), w_ih "
                                   f"{tuple(w_ih.shape)}, w_hh {tuple(w_hh.shape)}")
+        ctx.leaves = (w_ih, b_ih, w_hh, b_hh)
+        ctx.scope = _slab_scope_for(ctx.leaves)
         save = torch.empty(max(int(_lib.query("scgib_set2set_save_floats", nseg, d, n_iters)), 1),
                            dtype=torch.float32, device=x.device)
         out = torch.empty(nseg, 2 * d, dtype=torch.float32, device=x.device)
@@ -1148,12 +1173,29 @@ class _Set2Set(torch.autograd.Function):
         dx = torch.empty_like(x)
         dgates = torch.empty(max(ctx.nseg * ctx.n_iters * 4 * d, 1), dtype=torch.float32,
                              device=x.device)
-        dw_ih, dw_hh = torch.empty_like(w_ih), torch.empty_like(w_hh)
-        db_ih = torch.empty(4 * d, dtype=torch.float32, device=x.device)
-        db_hh = torch.empty_like(db_ih)
+        # the four weight gradients as views of one buffer: autograd then takes
+        # the views themselves as .grad (a gradient tensor referenced elsewhere
+        # is copied at accumulation), while the deferred launch keeps the buffer
+        n_ih, n_hh = 4 * d * 2 * d, 4 * d * d
+        wbuf = torch.empty(n_ih + n_hh + 8 * d, dtype=torch.float32, device=x.device)
+        dw_ih = wbuf[:n_ih].view(4 * d, 2 * d)
+        dw_hh = wbuf[n_ih:n_ih + n_hh].view(4 * d, d)
+        db_ih = wbuf[n_ih + n_hh:n_ih + n_hh + 4 * d]
+        db_hh = wbuf[n_ih + n_hh + 4 * d:]
+        ptrs = (dw_ih.data_ptr(), dw_hh.data_ptr(), db_ih.data_ptr(), db_hh.data_ptr())
+        # the LSTM weight gradients: deferred past the encoders' backward when
+        # the encoder pair's scope can take them (nothing reads them before the
+        # optimizer), else in the same call
+        scope = getattr(ctx, "scope", None)
+        defer = scope is not None and scope.usable(ctx.leaves)
+        wg = (None,) * 4 if defer else tuple(ctypes.c_void_p(v) for v in ptrs)
         _lib.call("scgib_set2set_bwd", _p(x), _p(ctx.ptr), ctx.nseg, d, ctx.n_iters, _p(w_ih),
-                  _p(w_hh), _p(save), _p(g), _p(dx), x.shape[0], _p(dgates), _p(dw_ih),
-                  _p(dw_hh), _p(db_ih), _p(db_hh), _stream())
+                  _p(w_hh), _p(save), _p(g), _p(dx), x.shape[0], _p(dgates), *wg, _stream())
+        if defer:
+            args = (_p(save), _p(dgates), ctx.nseg, d, ctx.n_iters,
+                    *(ctypes.c_void_p(v) for v in ptrs))
+            scope.defer(lambda: _lib.call("scgib_set2set_wgrad", *args, _stream()),
+                        save, dgates, wbuf)
         return dx, dw_ih, db_ih, dw_hh, db_hh, None, None, None
 
 

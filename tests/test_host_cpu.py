@@ -540,6 +540,31 @@ def test_check_handoff_raises_on_host_fault_word(pkg):
         ops._HOST_FAULT.pop(key, None)
 
 
+def test_slab_scope_defers_launches_once(pkg):
+    """ops.SlabScope.defer (the Set2Set LSTM weight gradients): a deferred
+    launch runs exactly once — taken by the encoder pair's backward
+    (take_later), or by the scope's end-of-backward flush when no pair
+    backward takes it — and its tensors stay referenced until then."""
+    import torch
+    ops = pkg.ops
+    calls = []
+    sc = ops.SlabScope()
+    t = torch.zeros(3)
+    sc.defer(lambda: calls.append("a"), t)
+    sc.defer(lambda: calls.append("b"), t)
+    assert len(sc.later) == 2 and sc.later[0][1][0] is t
+    later = sc.take_later()
+    assert [f() for f, _ in later] and calls == ["a", "b"] and not sc.later
+    sc._flush()  # nothing left: no launch twice
+    assert calls == ["a", "b"]
+    sc2 = ops.SlabScope()
+    sc2.defer(lambda: calls.append("c"), t)
+    sc2._flush()  # no pair backward took it: the flush runs it
+    assert calls == ["a", "b", "c"] and not sc2.later and not sc2.open
+    sc2._flush()
+    assert calls == ["a", "b", "c"]
+
+
 def test_scan_arena_carves_disjoint_zeroed_ranges(pkg):
     """ops._scan_carve (the scan-state arena): disjoint, 256-B aligned, zeroed
     ranges from one arena; a request past its end opens a new arena (the old

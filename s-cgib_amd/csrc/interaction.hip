@@ -169,7 +169,55 @@ __device__ __forceinline__ Lanes lanes() {
     return {l >> 4, l & 15, (l & 15) * 4};
 }
 
-__global__ __launch_bounds__(64) void interaction_fwd_k(
+// Waves per graph (build-time A/B hook SCGIB_INT_NW): a graph's rows are
+// spread over 4 NW row groups (row group qg = 4 wave + lane / 16), CH / NW
+// rows per lane per 32-row chunk; sums over row groups go through the wave's
+// shuffles, then (NW > 1) one LDS exchange in fixed wave order.  The kernels
+// are latency-bound per wave (phase trace: two ~5 us passes of dependent
+// VALU / shuffle chains at NW = 1), so a shorter chain per wave is what pays.
+#ifndef SCGIB_INT_NW
+#define SCGIB_INT_NW 4
+#endif
+constexpr int kIntNW = SCGIB_INT_NW;
+static_assert(kIntNW == 1 || kIntNW == 2 || kIntNW == 4, "waves per graph");
+
+// cross-wave sums of per-wave float4 totals (identical in every lane of a
+// wave's channel quad): v[i] <- sum over waves 0..NW-1, fixed order
+template <int NW, int K>
+__device__ __forceinline__ void wave_sum4(float4 (&v)[K], float4 (*sx)[4][16], int w, int q, int c4) {
+    if constexpr (NW > 1) {
+        if (q == 0) {
+#pragma unroll
+            for (int i = 0; i < K; ++i) sx[i][w][c4] = v[i];
+        }
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < K; ++i) {
+            float4 a = sx[i][0][c4];
+#pragma unroll
+            for (int k = 1; k < NW; ++k) a = a + sx[i][k][c4];
+            v[i] = a;
+        }
+        __syncthreads();
+    }
+}
+
+template <int NW>
+__device__ __forceinline__ float wave_sum1(float v, float *sx, int w) {
+    if constexpr (NW > 1) {
+        if ((threadIdx.x & 63) == 0) sx[w] = v;
+        __syncthreads();
+        float a = sx[0];
+#pragma unroll
+        for (int k = 1; k < NW; ++k) a += sx[k];
+        __syncthreads();
+        return a;
+    }
+    return v;
+}
+
+template <int NW>
+__global__ __launch_bounds__(64 * NW) void interaction_fwd_k(
     const float *__restrict__ f, const float *__restrict__ t, const float *__restrict__ s,
     const float *__restrict__ u_gate, const float *__restrict__ u_feat,
     const int32_t *__restrict__ gptr, int64_t B, const float *__restrict__ gamma,
@@ -180,8 +228,14 @@ __global__ __launch_bounds__(64) void interaction_fwd_k(
     float *__restrict__ z2, float *__restrict__ lam, float *__restrict__ logit,
     float *__restrict__ stats, float *__restrict__ kl, float *__restrict__ kl_mean,
     int64_t n_rows_cap, int pad) {
+    constexpr int RS = 4 * NW, CN = CH / NW;  // row stride, rows per lane per chunk
+    static_assert(RS * CN == 4 * CH, "32-row chunks");
+    __shared__ float4 sX[6][4][16];  // cross-wave exchanges (NW > 1)
+    __shared__ float sM[4], sS[4], sK[4];
     const Lanes L = lanes();
+    const int w = threadIdx.x >> 6, qg = 4 * w + L.q;
     const int64_t gi = blockIdx.x;
+    SCGIB_MARK(0);
     if (gi >= B) {  // padding blocks: zero rows [N, n_rows_cap) of im, lam, logit
         const int64_t r_beg = gptr[B];
         for (int64_t r = r_beg + (gi - B); r < n_rows_cap; r += gridDim.x - B) {
@@ -193,14 +247,15 @@ __global__ __launch_bounds__(64) void interaction_fwd_k(
     const int64_t r0 = gptr[gi], r1 = gptr[gi + 1];
     const int n = static_cast<int>(r1 - r0);
     if (n <= 0) {
-        if (L.q == 0) {
+        if (qg == 0) {
             st4(z1 + gi * 64 + L.ch, f4(0.f));
             st4(z2 + gi * 64 + L.ch, f4(0.f));
         }
         if (gi == B - 1 && kl_mean && threadIdx.x == 0) *kl_mean = 0.f;
         return;
     }
-    // Two load passes (the first chunk of CH rows per row group — a whole
+    SCGIB_MARK(1);
+    // Two load passes (the first chunk of CN rows per row group — a whole
     // typical molecule — stays in registers between them):
     //   pass A: f / t sums and shifted second moments; the attention logit
     //           w_hi . s_v and its online softmax (the per-graph constant
@@ -212,28 +267,28 @@ __global__ __launch_bounds__(64) void interaction_fwd_k(
     //   registers, later chunks recomputed).
     const float4 f0 = ld4(f + r0 * 64 + L.ch), t0 = ld4(t + r0 * 64 + L.ch);
     const float4 whi = ld4(watt + 64 + L.ch);
-    float4 zf = f4(0.f), zt = f4(0.f), sf = f4(0.f), st = f4(0.f), qf = f4(0.f), qt = f4(0.f);
+    float4 acc6[6] = {f4(0.f), f4(0.f), f4(0.f), f4(0.f), f4(0.f), f4(0.f)};  // zf zt sf st qf qt
     float M = -INFINITY, S = 0.f;  // per row group, merged below
-    float4 fk[CH], tk[CH], sk[CH];  // first chunk, kept
+    float4 fk[CN], tk[CN], sk[CN];  // first chunk, kept
     auto pass_a = [&](int64_t cb, float4 *fv, float4 *tv, float4 *sv) {
 #pragma unroll
-        for (int j = 0; j < CH; ++j) {
-            const int64_t r = cb + L.q + 4 * j, rr = r < r1 ? r : r0;
+        for (int j = 0; j < CN; ++j) {
+            const int64_t r = cb + qg + RS * j, rr = r < r1 ? r : r0;
             fv[j] = ld4(f + rr * 64 + L.ch);
             tv[j] = ld4(t + rr * 64 + L.ch);
             sv[j] = ld4(s + rr * 64 + L.ch);
         }
 #pragma unroll
-        for (int j = 0; j < CH; ++j) {
-            const int64_t r = cb + L.q + 4 * j;
-            const float w = r < r1 ? 1.f : 0.f;
-            zf = macc(fv[j], w, zf);
-            zt = macc(tv[j], w, zt);
+        for (int j = 0; j < CN; ++j) {
+            const int64_t r = cb + qg + RS * j;
+            const float wt = r < r1 ? 1.f : 0.f;
+            acc6[0] = macc(fv[j], wt, acc6[0]);
+            acc6[1] = macc(tv[j], wt, acc6[1]);
             const float4 df = fv[j] - f0, dt = tv[j] - t0;
-            sf = macc(df, w, sf);
-            st = macc(dt, w, st);
-            qf = macc(df * df, w, qf);
-            qt = macc(dt * dt, w, qt);
+            acc6[2] = macc(df, wt, acc6[2]);
+            acc6[3] = macc(dt, wt, acc6[3]);
+            acc6[4] = macc(df * df, wt, acc6[4]);
+            acc6[5] = macc(dt * dt, wt, acc6[5]);
             const float lg = red16(dot4(whi, sv[j]));
             if (r < r1) {
                 if (L.c4 == 0) logit[r] = lg;
@@ -244,28 +299,46 @@ __global__ __launch_bounds__(64) void interaction_fwd_k(
         }
     };
     // the first chunk's noise (independent of pass A): in flight with its rows
-    float4 uk[CH];
-    float ugk[CH];
+    float4 uk[CN];
+    float ugk[CN];
 #pragma unroll
-    for (int j = 0; j < CH; ++j) {
-        const int64_t r = r0 + L.q + 4 * j, rr = r < r1 ? r : r0;
+    for (int j = 0; j < CN; ++j) {
+        const int64_t r = r0 + qg + RS * j, rr = r < r1 ? r : r0;
         uk[j] = ld4(u_feat + rr * 64 + L.ch);
         ugk[j] = u_gate[rr];
     }
     pass_a(r0, fk, tk, sk);
-    for (int64_t cb = r0 + 4 * CH; cb < r1; cb += 4 * CH) {
-        float4 fv[CH], tv[CH], sv[CH];
+    for (int64_t cb = r0 + RS * CN; cb < r1; cb += RS * CN) {
+        float4 fv[CN], tv[CN], sv[CN];
         pass_a(cb, fv, tv, sv);
     }
-    zf = red_q4(zf); zt = red_q4(zt); sf = red_q4(sf); st = red_q4(st);
-    qf = red_q4(qf); qt = red_q4(qt);
 #pragma unroll
-    for (int off = 16; off <= 32; off <<= 1) {  // merge the four row groups' softmax
+    for (int i = 0; i < 6; ++i) acc6[i] = red_q4(acc6[i]);
+    wave_sum4<NW>(acc6, sX, w, L.q, L.c4);
+#pragma unroll
+    for (int off = 16; off <= 32; off <<= 1) {  // merge the wave's four row groups' softmax
         const float Mo = __shfl_xor(M, off, kWave), So = __shfl_xor(S, off, kWave);
         const float Mn = fmaxf(M, Mo);
         S = (S == 0.f ? 0.f : S * expf(M - Mn)) + (So == 0.f ? 0.f : So * expf(Mo - Mn));
         M = Mn;
     }
+    if constexpr (NW > 1) {  // ... and the waves', in wave order
+        if ((threadIdx.x & 63) == 0) {
+            sM[w] = M;
+            sS[w] = S;
+        }
+        __syncthreads();
+        M = sM[0];
+        S = sS[0];
+#pragma unroll
+        for (int k = 1; k < NW; ++k) {
+            const float Mo = sM[k], So = sS[k], Mn = fmaxf(M, Mo);
+            S = (S == 0.f ? 0.f : S * expf(M - Mn)) + (So == 0.f ? 0.f : So * expf(Mo - Mn));
+            M = Mn;
+        }
+    }
+    const float4 zf = acc6[0], zt = acc6[1], sf = acc6[2], st = acc6[3], qf = acc6[4], qt = acc6[5];
+    SCGIB_MARK(2);
     const float invS = 1.f / S;
     const float inv_n = 1.f / n;
     const float4 mu = inv_n * zf, mt = inv_n * zt;
@@ -280,42 +353,43 @@ __global__ __launch_bounds__(64) void interaction_fwd_k(
     const float4 gm = ld4(gamma + L.ch), bt = ld4(beta + L.ch), w2c = ld4(w2 + L.ch);
     const float b2 = *b2p;
     float *sl = stats + gi * SCGIB_STATS_STRIDE;
-    if (L.q == 0) {
+    if (qg == 0) {
         st4(z2 + gi * 64 + L.ch, zf);
         st4(sl + kStMeanT + L.ch, mt);
         st4(sl + kStSsqT + L.ch, ctp);
         st4(sl + kStMu + L.ch, mu);
         st4(sl + kStSigma + L.ch, sig);
     }
+    SCGIB_MARK(3);
     // ---- pass B: compressor logit p, gate lambda, noisy features, attention ----
     const bool last = gi == B - 1;
     const float4 se = sig + f4(kKlEps);
-    float4 zacc = f4(0.f), qacc = f4(0.f);
-    float lmk[CH];  // first chunk's lambda, kept for the KL store pass
+    float4 acc2[2] = {f4(0.f), f4(0.f)};  // zacc, qacc
+    float lmk[CN];  // first chunk's lambda, kept for the KL store pass
     auto pass_b = [&](int64_t cb, const float4 *fv, const float4 *tv, const float4 *sv,
                       float *lmo, const float4 *upre, const float *gpre) {
-        float4 uv[CH];
-        float ug[CH];
+        float4 uv[CN];
+        float ug[CN];
 #pragma unroll
-        for (int j = 0; j < CH; ++j) {
-            const int64_t r = cb + L.q + 4 * j, rr = r < r1 ? r : r0;
+        for (int j = 0; j < CN; ++j) {
+            const int64_t r = cb + qg + RS * j, rr = r < r1 ? r : r0;
             uv[j] = upre ? upre[j] : ld4(u_feat + rr * 64 + L.ch);
             ug[j] = gpre ? gpre[j] : u_gate[rr];
         }
 #pragma unroll
-        for (int j = 0; j < CH; ++j) {
-            const int64_t r = cb + L.q + 4 * j;
-            const float w = r < r1 ? 1.f : 0.f;
+        for (int j = 0; j < CN; ++j) {
+            const int64_t r = cb + qg + RS * j;
+            const float wt = r < r1 ? 1.f : 0.f;
             const float4 y = gm * ((tv[j] - m_use) * rstd) + bt;
             const float p = red16(dot4(w2c, relu4(y))) + b2;
             const float lm = gate_lambda(ug[j], p), ln = 1.f - lm;
             if (lmo) lmo[j] = lm;
             const float4 nz = (lm * fv[j] + ln * mu) + uv[j] * (ln * sig);
-            zacc = macc(nz, w, zacc);
+            acc2[0] = macc(nz, wt, acc2[0]);
             if (last) {
                 const float4 d = (lm * fv[j] + ln * mu) - mu;
                 const float4 z = make_float4(d.x / se.x, d.y / se.y, d.z / se.z, d.w / se.w);
-                qacc = macc(z * z, w, qacc);
+                acc2[1] = macc(z * z, wt, acc2[1]);
             }
             const float lg = red16(dot4(whi, sv[j]));
             if (r < r1) {
@@ -326,31 +400,34 @@ __global__ __launch_bounds__(64) void interaction_fwd_k(
         }
     };
     pass_b(r0, fk, tk, sk, lmk, uk, ugk);
-    for (int64_t cb = r0 + 4 * CH; cb < r1; cb += 4 * CH) {
-        float4 fv[CH], tv[CH], sv[CH];
+    for (int64_t cb = r0 + RS * CN; cb < r1; cb += RS * CN) {
+        float4 fv[CN], tv[CN], sv[CN];
 #pragma unroll
-        for (int j = 0; j < CH; ++j) {
-            const int64_t r = cb + L.q + 4 * j, rr = r < r1 ? r : r0;
+        for (int j = 0; j < CN; ++j) {
+            const int64_t r = cb + qg + RS * j, rr = r < r1 ? r : r0;
             fv[j] = ld4(f + rr * 64 + L.ch);
             tv[j] = ld4(t + rr * 64 + L.ch);
             sv[j] = ld4(s + rr * 64 + L.ch);
         }
         pass_b(cb, fv, tv, sv, nullptr, nullptr, nullptr);
     }
-    zacc = red_q4(zacc);
-    if (L.q == 0) st4(z1 + gi * 64 + L.ch, zacc);
+    acc2[0] = red_q4(acc2[0]);
+    acc2[1] = red_q4(acc2[1]);
+    wave_sum4<NW>(acc2, sX, w, L.q, L.c4);  // (qacc: only the last graph uses it)
+    const float4 zacc = acc2[0], qacc = acc2[1];
+    SCGIB_MARK(4);
+    if (qg == 0) st4(z1 + gi * 64 + L.ch, zacc);
     // the z-bar half of the attention logit (constant per graph; kept for the
     // record, the softmax above and its backward do not depend on it)
     const float cst = red16(dot4(ld4(watt + L.ch), zacc)) + *battp;
     // ---- KL of the last graph only, duplicated (models.py:657-659) ----
-    if (last) {
-        qacc = red_q4(qacc);
+    if (last) {  // (block-uniform)
         const float4 den = se * se;
         float ksum = 0.f;
         auto kl_store = [&](int64_t cb, const float *lmv) {
 #pragma unroll
-            for (int j = 0; j < CH; ++j) {
-                const int64_t r = cb + L.q + 4 * j;
+            for (int j = 0; j < CN; ++j) {
+                const int64_t r = cb + qg + RS * j;
                 const float4 ns = (1.f - lmv[j]) * sig;
                 const float4 nn = ns * ns;
                 const float4 v = f4(0.5f) * make_float4(nn.x / den.x, nn.y / den.y, nn.z / den.z,
@@ -365,24 +442,24 @@ __global__ __launch_bounds__(64) void interaction_fwd_k(
             }
         };
         kl_store(r0, lmk);
-        for (int64_t cb = r0 + 4 * CH; cb < r1; cb += 4 * CH) {
-            float4 tv[CH];
-            float ug[CH], lmv[CH];
+        for (int64_t cb = r0 + RS * CN; cb < r1; cb += RS * CN) {
+            float4 tv[CN];
+            float ug[CN], lmv[CN];
 #pragma unroll
-            for (int j = 0; j < CH; ++j) {
-                const int64_t r = cb + L.q + 4 * j, rr = r < r1 ? r : r0;
+            for (int j = 0; j < CN; ++j) {
+                const int64_t r = cb + qg + RS * j, rr = r < r1 ? r : r0;
                 tv[j] = ld4(t + rr * 64 + L.ch);
                 ug[j] = u_gate[rr];
             }
 #pragma unroll
-            for (int j = 0; j < CH; ++j) {
+            for (int j = 0; j < CN; ++j) {
                 const float4 y = gm * ((tv[j] - m_use) * rstd) + bt;
                 lmv[j] = gate_lambda(ug[j], red16(dot4(w2c, relu4(y))) + b2);
             }
             kl_store(cb, lmv);
         }
         // mean over the duplicated [2n, 64] tensor == mean over [n, 64]
-        ksum = red_q(red16(ksum));
+        ksum = wave_sum1<NW>(red_q(red16(ksum)), sK, w);
         if (kl_mean && threadIdx.x == 0) *kl_mean = ksum / (static_cast<float>(n) * 64.f);
     }
     if (threadIdx.x == 0) {
@@ -390,6 +467,7 @@ __global__ __launch_bounds__(64) void interaction_fwd_k(
         sl[kStSoftSum] = S;
         sl[kStConst] = cst;
     }
+    SCGIB_MARK(5);
 }
 
 // the compressor BatchNorm's running-stat update (running_update.h)
@@ -424,6 +502,7 @@ __global__ __launch_bounds__(64) void interaction_bwd_k(
         }
         return;
     }
+    SCGIB_MARK(0);
     const int64_t r0 = gptr[gi], r1 = gptr[gi + 1];
     const int n = static_cast<int>(r1 - r0);
     float *pg = pgrad + gi * SCGIB_PGRAD_STRIDE;
@@ -441,6 +520,7 @@ __global__ __launch_bounds__(64) void interaction_bwd_k(
     const float4 rstd = rcp_sqrt4(v_use + f4(bn_eps));
     const float4 gm = ld4(gamma + L.ch), bt = ld4(beta + L.ch), w2c = ld4(w2 + L.ch);
     const float4 wlo = ld4(watt + L.ch), whi = ld4(watt + 64 + L.ch), zb = ld4(z1 + gi * 64 + L.ch);
+    SCGIB_MARK(1);
 
     // ---- attention backward: a_v = alpha_v s_v, alpha = softmax(logit) ----
     // The first chunk (all rows of a typical molecule's ego-net batch slice)
@@ -497,6 +577,7 @@ __global__ __launch_bounds__(64) void interaction_bwd_k(
     }
     dwhi = red_q4(dwhi);
     const float dc = red_q(dcq);
+    SCGIB_MARK(2);
     // (a NULL g_z1 / g_z2: the readouts feed no loss, e.g. in the fine-tune head)
     const float4 gb = (g_z1 ? ld4(g_z1 + gi * 64 + L.ch) : f4(0.f)) + dc * wlo;  // d z-bar -> every node's noisy
     const float4 gz2 = g_z2 ? ld4(g_z2 + gi * 64 + L.ch) : f4(0.f);  // d readout(f) -> every node's f
@@ -579,6 +660,7 @@ __global__ __launch_bounds__(64) void interaction_bwd_k(
     dg = red_q4(dg);
     dbe = red_q4(dbe);
     const float db2 = red_q(db2q);
+    SCGIB_MARK(3);
     // BatchNorm backward (this graph's batch statistics, or running stats);
     // chunk 0 from registers, later chunks re-read the dt entries this lane wrote
     const float4 gr = gm * rstd;
@@ -615,6 +697,7 @@ __global__ __launch_bounds__(64) void interaction_bwd_k(
         pg[SCGIB_PGRAD_STRIDE - 2] = 0.f;
         pg[SCGIB_PGRAD_STRIDE - 1] = 0.f;
     }
+    SCGIB_MARK(4);
 }
 
 }  // namespace scgib
@@ -638,7 +721,7 @@ extern "C" int scgib_interaction_fwd(
         return SCGIB_EINVAL;
     if (!training && (!bn_running_mean || !bn_running_var)) return SCGIB_EINVAL;
     const unsigned grid = static_cast<unsigned>(n_graphs + (pad_rows ? 64 : 0));
-    interaction_fwd_k<<<dim3(grid), 64, 0, as_stream(stream)>>>(
+    interaction_fwd_k<kIntNW><<<dim3(grid), 64 * kIntNW, 0, as_stream(stream)>>>(
         f, t, s, u_gate, u_feat, graph_ptr, n_graphs, bn_gamma, bn_beta, bn_running_mean,
         bn_running_var, bn_eps, training, w2, b2, w_att, b_att, im, z1, z2, lam, logit, stats,
         kl_tensor, kl_mean, n_nodes, pad_rows);
@@ -701,3 +784,10 @@ extern "C" int scgib_interaction_bwd(
     }
     return launch_status();
 }
+
+#ifdef SCGIB_TRACE
+// debug build only: this file's own g_trace (see common.h; scgib_trace_set)
+extern "C" int scgib_trace_set_interaction(void *buf) {
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_trace), &buf, sizeof(buf)) == hipSuccess ? 0 : 1;
+}
+#endif

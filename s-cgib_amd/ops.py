@@ -1327,7 +1327,7 @@ def _interaction_forward(ctx, f, t, s, u_gate, u_feat, gamma, beta, w2, b2, w_at
     w_att, b_att = _f32(w_att, "w_att"), _f32(b_att, "b_att")
     rm, rv = bn.running_mean, bn.running_var
     st = _stream()
-    _lib.call("scgib_interaction_fwd", _p(f), _p(t), _p(s), _p(u_gate), _p(u_feat),
+    _launch("scgib_interaction_fwd", {"n": n, "B": B}, _p(f), _p(t), _p(s), _p(u_gate), _p(u_feat),
               _p(graph.graph_ptr), B, n, _p(gamma), _p(beta), _p(rm), _p(rv), float(bn.eps),
               int(training), _p(w2), _p(b2), _p(w_att), _p(b_att), _p(im), _p(z1), _p(z2),
               _p(lam), _p(logit), _p(stats), _p(kl), _p(kl_mean), int(pad), st)
@@ -1386,7 +1386,7 @@ def _interaction_backward(ctx, saved, g_im, g_z1, g_z2, g_kl, g_klmean):
     pg = torch.empty(PGRAD_STRIDE, dtype=torch.float32, device=dev)
     scope = getattr(ctx, "scope", None)
     defer = B > 0 and scope is not None and scope.usable(ctx.leaves)
-    _lib.call("scgib_interaction_bwd", _p(g_im), _p(g_z1), _p(g_z2), _p(g_kl), _p(f), _p(t),
+    _launch("scgib_interaction_bwd", {"n": n, "B": B}, _p(g_im), _p(g_z1), _p(g_z2), _p(g_kl), _p(f), _p(t),
               _p(s), _p(u_feat), _p(ctx.graph.graph_ptr), B, n, _p(gamma), _p(beta),
               _p(ctx.rm), _p(ctx.rv), ctx.bn_eps, int(ctx.training), _p(w2), _p(w_att),
               _p(z1), _p(lam), _p(logit), _p(stats), _p(df), _p(dt), _p(ds), _p(pgrad),

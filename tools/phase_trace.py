@@ -39,6 +39,9 @@ PHASES = {
     "scgib_mlp2_recon_contrastive_fwd": ["load", "gemm1", "-", "-", "contrast", "gemm2+pub",
                                          "wait+acq", "fin:edges", "fin:gram", "fin:arrive"],
     "scgib_mlp2_recon_contrastive_bwd": ["dz2(recon)", "dW2,dr,dz1", "dW1,dx", "-", "contrast"],
+    # one wave per graph (padding blocks carry no marks)
+    "scgib_interaction_fwd": ["gptr", "passA+red", "stats", "passB", "end"],
+    "scgib_interaction_bwd": ["ld stats", "attention", "compress", "bn bwd"],
 }
 MAXB = 4096
 

@@ -477,7 +477,8 @@ __global__ __launch_bounds__(1024) void bn_running_update_k(const scgib_running_
     running_update_body<1024>(a);
 }
 
-__global__ __launch_bounds__(64) void interaction_bwd_k(
+template <int NW>
+__global__ __launch_bounds__(64 * NW) void interaction_bwd_k(
     const float *__restrict__ g_im, const float *__restrict__ g_z1,
     const float *__restrict__ g_z2, const float *__restrict__ g_kl,
     const float *__restrict__ f, const float *__restrict__ t, const float *__restrict__ s,
@@ -489,7 +490,11 @@ __global__ __launch_bounds__(64) void interaction_bwd_k(
     const float *__restrict__ logit, const float *__restrict__ stats, float *__restrict__ df,
     float *__restrict__ dt, float *__restrict__ ds, float *__restrict__ pgrad,
     const float *__restrict__ g_klmean, int64_t n_rows_cap) {
+    constexpr int RS = 4 * NW, CN = CH / NW;  // row stride, rows per lane per chunk
+    __shared__ float4 sX[6][4][16];  // cross-wave exchanges (NW > 1)
+    __shared__ float sK[4];
     const Lanes L = lanes();
+    const int wvi = threadIdx.x >> 6, qg = 4 * wvi + L.q;
     const int64_t gi = blockIdx.x;
     if (gi >= B) {  // padding blocks: zero rows [N, n_rows_cap) of df, dt, ds
         const int64_t r_beg = gptr[B];
@@ -507,7 +512,7 @@ __global__ __launch_bounds__(64) void interaction_bwd_k(
     const int n = static_cast<int>(r1 - r0);
     float *pg = pgrad + gi * SCGIB_PGRAD_STRIDE;
     if (n <= 0) {
-        for (int j = threadIdx.x; j < SCGIB_PGRAD_STRIDE; j += 64) pg[j] = 0.f;
+        for (int j = threadIdx.x; j < SCGIB_PGRAD_STRIDE; j += 64 * NW) pg[j] = 0.f;
         return;
     }
     const float *sl = stats + gi * SCGIB_STATS_STRIDE;
@@ -527,38 +532,38 @@ __global__ __launch_bounds__(64) void interaction_bwd_k(
     // stays in registers across the passes; later chunks are re-loaded.
     auto att_load = [&](int64_t cb, float4 *ga, float4 *sv, float *lg) {
 #pragma unroll
-        for (int j = 0; j < CH; ++j) {
-            const int64_t r = cb + L.q + 4 * j, rr = r < r1 ? r : r0;
+        for (int j = 0; j < CN; ++j) {
+            const int64_t r = cb + qg + RS * j, rr = r < r1 ? r : r0;
             ga[j] = ld4(g_im + rr * 128 + 64 + L.ch);
             sv[j] = ld4(s + rr * 64 + L.ch);
             lg[j] = logit[rr];
         }
     };
-    float4 ga0[CH], sv0[CH];
-    float lg0[CH];
+    float4 ga0[CN], sv0[CN];
+    float lg0[CN];
     att_load(r0, ga0, sv0, lg0);
     float sa = 0.f;  // sum alpha * dalpha of this row group (uniform over its lanes)
     auto att_sum = [&](int64_t cb, const float4 *ga, const float4 *sv, const float *lg) {
 #pragma unroll
-        for (int j = 0; j < CH; ++j) {
+        for (int j = 0; j < CN; ++j) {
             const float da = red16(dot4(ga[j], sv[j]));
-            sa = fmaf(expf(lg[j] - M) * invS * da, cb + L.q + 4 * j < r1 ? 1.f : 0.f, sa);
+            sa = fmaf(expf(lg[j] - M) * invS * da, cb + qg + RS * j < r1 ? 1.f : 0.f, sa);
         }
     };
     att_sum(r0, ga0, sv0, lg0);
-    for (int64_t cb = r0 + 4 * CH; cb < r1; cb += 4 * CH) {
-        float4 ga[CH], sv[CH];
-        float lg[CH];
+    for (int64_t cb = r0 + RS * CN; cb < r1; cb += RS * CN) {
+        float4 ga[CN], sv[CN];
+        float lg[CN];
         att_load(cb, ga, sv, lg);
         att_sum(cb, ga, sv, lg);
     }
-    const float SA = red_q(sa);
+    const float SA = wave_sum1<NW>(red_q(sa), sK, wvi);
     float4 dwhi = f4(0.f);
     float dcq = 0.f;
     auto att_grad = [&](int64_t cb, const float4 *ga, const float4 *sv, const float *lg) {
 #pragma unroll
-        for (int j = 0; j < CH; ++j) {
-            const int64_t r = cb + L.q + 4 * j;
+        for (int j = 0; j < CN; ++j) {
+            const int64_t r = cb + qg + RS * j;
             const float w = r < r1 ? 1.f : 0.f;
             const float da = red16(dot4(ga[j], sv[j]));
             const float al = expf(lg[j] - M) * invS;
@@ -569,14 +574,16 @@ __global__ __launch_bounds__(64) void interaction_bwd_k(
         }
     };
     att_grad(r0, ga0, sv0, lg0);
-    for (int64_t cb = r0 + 4 * CH; cb < r1; cb += 4 * CH) {
-        float4 ga[CH], sv[CH];
-        float lg[CH];
+    for (int64_t cb = r0 + RS * CN; cb < r1; cb += RS * CN) {
+        float4 ga[CN], sv[CN];
+        float lg[CN];
         att_load(cb, ga, sv, lg);
         att_grad(cb, ga, sv, lg);
     }
-    dwhi = red_q4(dwhi);
-    const float dc = red_q(dcq);
+    float4 dwv[1] = {red_q4(dwhi)};
+    wave_sum4<NW>(dwv, sX, wvi, L.q, L.c4);
+    dwhi = dwv[0];
+    const float dc = wave_sum1<NW>(red_q(dcq), sK, wvi);
     SCGIB_MARK(2);
     // (a NULL g_z1 / g_z2: the readouts feed no loss, e.g. in the fine-tune head)
     const float4 gb = (g_z1 ? ld4(g_z1 + gi * 64 + L.ch) : f4(0.f)) + dc * wlo;  // d z-bar -> every node's noisy
@@ -589,11 +596,13 @@ __global__ __launch_bounds__(64) void interaction_bwd_k(
     const float gk_uniform = g_klmean ? *g_klmean / (static_cast<float>(n) * 64.f) : 0.f;
     float4 Gc = f4(0.f);
     if (has_kl && g_kl) {
-        for (int base = 0; base < n; base += 4) {
-            const int rl = base + L.q;
+        for (int base = 0; base < n; base += RS) {
+            const int rl = base + qg;
             if (rl < n) Gc = Gc + ld4(g_kl + rl * 64 + L.ch) + ld4(g_kl + (rl + n) * 64 + L.ch);
         }
-        Gc = red_q4(Gc);
+        float4 gv[1] = {red_q4(Gc)};
+        wave_sum4<NW>(gv, sX, wvi, L.q, L.c4);  // (block-uniform branch: the last graph)
+        Gc = gv[0];
     }
     if (has_kl && !g_kl) Gc = f4(gk_uniform * n);
     const float4 se = sig + f4(kKlEps);
@@ -603,13 +612,13 @@ __global__ __launch_bounds__(64) void interaction_bwd_k(
     // ---- compression backward ----
     float4 dw2 = f4(0.f), dg = f4(0.f), dbe = f4(0.f);
     float db2q = 0.f;
-    float4 dy0[CH], xh0[CH];  // first chunk's BN-input gradient and normalised input
+    float4 dy0[CN], xh0[CN];  // first chunk's BN-input gradient and normalised input
     auto comp = [&](int64_t cb, float4 *dyo, float4 *xho) {
-        float lm[CH];
-        float4 fv[CH], gn[CH], uv[CH], tv[CH], gk[CH];
+        float lm[CN];
+        float4 fv[CN], gn[CN], uv[CN], tv[CN], gk[CN];
 #pragma unroll
-        for (int j = 0; j < CH; ++j) {
-            const int64_t r = cb + L.q + 4 * j, rr = r < r1 ? r : r0;
+        for (int j = 0; j < CN; ++j) {
+            const int64_t r = cb + qg + RS * j, rr = r < r1 ? r : r0;
             lm[j] = lam[rr];
             fv[j] = ld4(f + rr * 64 + L.ch);
             gn[j] = ld4(g_im + rr * 128 + L.ch);
@@ -623,8 +632,8 @@ __global__ __launch_bounds__(64) void interaction_bwd_k(
             }
         }
 #pragma unroll
-        for (int j = 0; j < CH; ++j) {
-            const int64_t r = cb + L.q + 4 * j;
+        for (int j = 0; j < CN; ++j) {
+            const int64_t r = cb + qg + RS * j;
             const float w = r < r1 ? 1.f : 0.f;
             const float4 g = gn[j] + gb;
             const float4 fm = fv[j] - mu;
@@ -655,36 +664,38 @@ __global__ __launch_bounds__(64) void interaction_bwd_k(
         }
     };
     comp(r0, dy0, xh0);
-    for (int64_t cb = r0 + 4 * CH; cb < r1; cb += 4 * CH) comp(cb, nullptr, nullptr);
-    dw2 = red_q4(dw2);
-    dg = red_q4(dg);
-    dbe = red_q4(dbe);
-    const float db2 = red_q(db2q);
+    for (int64_t cb = r0 + RS * CN; cb < r1; cb += RS * CN) comp(cb, nullptr, nullptr);
+    float4 dv[3] = {red_q4(dw2), red_q4(dg), red_q4(dbe)};
+    wave_sum4<NW>(dv, sX, wvi, L.q, L.c4);
+    dw2 = dv[0];
+    dg = dv[1];
+    dbe = dv[2];
+    const float db2 = wave_sum1<NW>(red_q(db2q), sK, wvi);
     SCGIB_MARK(3);
     // BatchNorm backward (this graph's batch statistics, or running stats);
     // chunk 0 from registers, later chunks re-read the dt entries this lane wrote
     const float4 gr = gm * rstd;
     auto bn_bwd = [&](int64_t cb, const float4 *dy, const float4 *xh) {
 #pragma unroll
-        for (int j = 0; j < CH; ++j) {
-            const int64_t r = cb + L.q + 4 * j;
+        for (int j = 0; j < CN; ++j) {
+            const int64_t r = cb + qg + RS * j;
             if (r < r1)
                 st4(dt + r * 64 + L.ch,
                     training ? gr * (dy[j] - inv_n * dbe - xh[j] * (inv_n * dg)) : gr * dy[j]);
         }
     };
     bn_bwd(r0, dy0, xh0);
-    for (int64_t cb = r0 + 4 * CH; cb < r1; cb += 4 * CH) {
-        float4 dy[CH], xh[CH];
+    for (int64_t cb = r0 + RS * CN; cb < r1; cb += RS * CN) {
+        float4 dy[CN], xh[CN];
 #pragma unroll
-        for (int j = 0; j < CH; ++j) {
-            const int64_t r = cb + L.q + 4 * j, rr = r < r1 ? r : r0;
+        for (int j = 0; j < CN; ++j) {
+            const int64_t r = cb + qg + RS * j, rr = r < r1 ? r : r0;
             dy[j] = ld4(dt + rr * 64 + L.ch);  // valid rows: written by this lane above
             xh[j] = (ld4(t + rr * 64 + L.ch) - m_use) * rstd;
         }
         bn_bwd(cb, dy, xh);
     }
-    if (L.q == 0) {
+    if (qg == 0) {
         st4(pg + kPgW2 + L.ch, dw2);
         st4(pg + kPgGamma + L.ch, dg);
         st4(pg + kPgBeta + L.ch, dbe);
@@ -772,7 +783,7 @@ extern "C" int scgib_interaction_bwd(
         return SCGIB_EINVAL;
     if (!training && (!bn_running_mean || !bn_running_var)) return SCGIB_EINVAL;
     const unsigned grid = static_cast<unsigned>(n_graphs + (pad_rows ? 64 : 0));
-    interaction_bwd_k<<<dim3(grid), 64, 0, as_stream(stream)>>>(
+    interaction_bwd_k<kIntNW><<<dim3(grid), 64 * kIntNW, 0, as_stream(stream)>>>(
         g_im, g_z1, g_z2, g_kl, f, t, s, u_feat, graph_ptr, n_graphs, bn_gamma, bn_beta,
         bn_running_mean, bn_running_var, bn_eps, training, w2, w_att, z1, lam, logit, stats,
         df, dt, ds, pgrad, g_klmean, n_nodes);

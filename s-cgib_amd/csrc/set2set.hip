@@ -78,17 +78,19 @@ __device__ __forceinline__ float s2s_dot(const float *__restrict__ w, const floa
 }
 
 // The graph's rows: the first kS2SRows staged in LDS by the workgroup (every
-// round and pass re-reads them), the rest read from global memory.
+// round and pass re-reads them), the rest read from global memory.  Row group
+// G (of 16) takes rows p0 + G, p0 + G + 16, ...: its staged rows are the
+// kS2SPer slots G + 16 i, read into registers once per attention pass with
+// plain LDS loads (a per-element LDS-or-global select made every read a flat
+// load, and the second pass recomputed every logit: phase trace r05_s2s); rows
+// past kS2SRows go through their own global-memory loop.
 constexpr int kS2SRows = 64;
+constexpr int kS2SPer = kS2SRows / 16;
 struct S2SRows {
     const float *__restrict__ x;  // global [*][d]
     const float *xs;              // LDS copy of rows [p0, p0 + ns)
     int64_t p0;
     int ns, d;
-    __device__ __forceinline__ float at(int64_t v, int c) const {
-        const int64_t o = v - p0;
-        return o < ns ? xs[o * d + c] : x[v * d + c];
-    }
 };
 
 // all threads: stage rows [p0, p0 + min(n, kS2SRows)) of x into xs (then a barrier)
@@ -99,28 +101,53 @@ __device__ __forceinline__ int s2s_stage(const float *__restrict__ x, int64_t p0
     return ns;
 }
 
-// the logit <x_r, q> of row r for the 16 lanes of its row group (every lane
-// of the group returns it)
-__device__ __forceinline__ float s2s_logit(const S2SRows &X, int64_t r, int j,
-                                           const float (&qv)[4]) {
-    float dot = 0.f;
+// lane j's channels j + 16 k of the row group's staged slots G + 16 i, 0 past
+// ns or d.  The index is clamped into the staging array (ns <= 64, d <= 64),
+// so the loads are unconditional and go out together.
+__device__ __forceinline__ void s2s_rows_lds(const S2SRows &X, int G, int j,
+                                             float (&xv)[kS2SPer][4]) {
+#pragma unroll
+    for (int i = 0; i < kS2SPer; ++i) {
+        const int o = G + 16 * i;
+        const bool ok = o < X.ns;
+        const int oc = ok ? o : 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int c = j + 16 * k;
+            const float v = X.xs[oc * X.d + (c < X.d ? c : 0)];
+            xv[i][k] = ok && c < X.d ? v : 0.f;
+        }
+    }
+}
+
+// lane j's channels j + 16 k of global row v, 0 past d
+__device__ __forceinline__ void s2s_row_glb(const float *__restrict__ x, int64_t v, int d, int j,
+                                            float (&xv)[4]) {
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
         const int c = j + 16 * k;
-        dot = fmaf(c < X.d ? X.at(r, c) : 0.f, qv[k], dot);
+        xv[k] = c < d ? x[v * d + c] : 0.f;
     }
+}
+
+// the row's logit-style dot <x_v, q> for the 16 lanes of its row group (every
+// lane of the group returns it)
+__device__ __forceinline__ float s2s_dot16(const float (&xv)[4], const float (&qv)[4]) {
+    float dot = 0.f;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) dot = fmaf(xv[k], qv[k], dot);
     return s2s_red16(dot);
 }
 
 // All four waves: the attention readout of rows [p0, p1) with query q (LDS,
-// d floats) into r (LDS) and (max, denominator) into st.  Row group G = 4 w +
-// (lane >> 4) of the 16 takes rows p0 + G, p0 + G + 16, ...; the logits are
-// recomputed in the second pass (a 16-lane dot per row) rather than kept: a
-// graph may hold any number of rows.  red: LDS scratch, kS2SRed floats; the
-// waves' partials combine in fixed order.  Call from every thread.
+// d floats) into r (LDS) and (max, denominator) into st.  The staged rows'
+// logits stay in registers between the two passes; rows past kS2SRows are
+// re-read and their logits recomputed (a graph may hold any number of rows).
+// red: LDS scratch, kS2SRed floats; the waves' partials combine in fixed
+// order.  Call from every thread.
 constexpr int kS2SRed = 8 + 4 * kS2SMaxD;
-__device__ void s2s_attend_fwd(const S2SRows &X, int64_t p1, const float *q, float *r,
-                               float *st, float *red) {
+__device__ __forceinline__ void s2s_attend_fwd(const S2SRows &X, int64_t p1, const float *q,
+                                               float *r, float *st, float *red) {
     const int64_t p0 = X.p0;
     const int d = X.d;
     const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, j = l & 15;
@@ -130,22 +157,42 @@ __device__ void s2s_attend_fwd(const S2SRows &X, int64_t p1, const float *q, flo
     for (int k = 0; k < 4; ++k) qv[k] = j + 16 * k < d ? q[j + 16 * k] : 0.f;
     // (a row group's 16 lanes run a row together: the butterflies stay
     // within active lanes whatever the other groups do)
+    float xv[kS2SPer][4], e[kS2SPer];
+    s2s_rows_lds(X, G, j, xv);
     float mx = -INFINITY;
-    for (int64_t v = p0 + G; v < p1; v += 16) mx = fmaxf(mx, s2s_logit(X, v, j, qv));
+#pragma unroll
+    for (int i = 0; i < kS2SPer; ++i) {
+        e[i] = s2s_dot16(xv[i], qv);
+        if (G + 16 * i < X.ns) mx = fmaxf(mx, e[i]);
+    }
+    for (int64_t v = p0 + kS2SRows + G; v < p1; v += 16) {
+        float xg[4];
+        s2s_row_glb(X.x, v, d, j, xg);
+        mx = fmaxf(mx, s2s_dot16(xg, qv));
+    }
     mx = s2s_max_all(mx);
     if (l == 0) red[w] = mx;
     __syncthreads();
     mx = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
-    // denominator and the unnormalised readout sum_v exp(e_v - max) x_v in one pass
+    // denominator and the unnormalised readout sum_v exp(e_v - max) x_v in one
+    // pass, rows in the first pass's order
     float den = 0.f, acc[4] = {0.f, 0.f, 0.f, 0.f};
-    for (int64_t v = p0 + G; v < p1; v += 16) {
-        const float a = expf(s2s_logit(X, v, j, qv) - mx);
+#pragma unroll
+    for (int i = 0; i < kS2SPer; ++i) {
+        if (G + 16 * i < X.ns) {
+            const float a = expf(e[i] - mx);
+            den += j == 0 ? a : 0.f;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) acc[k] = fmaf(xv[i][k], a, acc[k]);
+        }
+    }
+    for (int64_t v = p0 + kS2SRows + G; v < p1; v += 16) {
+        float xg[4];
+        s2s_row_glb(X.x, v, d, j, xg);
+        const float a = expf(s2s_dot16(xg, qv) - mx);
         den += j == 0 ? a : 0.f;
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const int c = j + 16 * k;
-            acc[k] = fmaf(c < d ? X.at(v, c) : 0.f, a, acc[k]);
-        }
+        for (int k = 0; k < 4; ++k) acc[k] = fmaf(xg[k], a, acc[k]);
     }
     den = s2s_red_q(s2s_red16(den));
     if (l == 0) red[4 + w] = den;
@@ -171,13 +218,12 @@ __device__ void s2s_attend_fwd(const S2SRows &X, int64_t p1, const float *q, flo
 // All four waves: the attention backward for d r = gr (LDS) with query q (LDS):
 //   dalpha_v = <gr, x_v>;  s = sum alpha dalpha;  de_v = alpha_v (dalpha_v - s)
 //   dx_v (+)= alpha_v gr + de_v q (dxs: the staged rows' LDS accumulator);
-//   dq = sum de_v x_v  (into dq, LDS).  Row groups and red as s2s_attend_fwd.
-// (not inlined: inlined into set2set_bwd_k, hipcc 7.2 rejects the staged
-// accumulator's LDS read-modify-write, "Operand has incorrect register class")
-__device__ __noinline__ void s2s_attend_bwd(const S2SRows X, int64_t p1, const float *q,
-                                             const float *gr, float mx, float den,
-                                             float *__restrict__ dx, float *dxs, bool accumulate,
-                                             float *dq, float *red) {
+//   dq = sum de_v x_v  (into dq, LDS).  Row groups and red as s2s_attend_fwd;
+// the staged rows' alpha and dalpha stay in registers between the passes.
+__device__ __forceinline__ void s2s_attend_bwd(const S2SRows &X, int64_t p1, const float *q,
+                                               const float *gr, float mx, float den,
+                                               float *__restrict__ dx, float *dxs,
+                                               bool accumulate, float *dq, float *red) {
     const int64_t p0 = X.p0;
     const int d = X.d;
     const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, j = l & 15;
@@ -189,35 +235,58 @@ __device__ __noinline__ void s2s_attend_bwd(const S2SRows X, int64_t p1, const f
         gv[k] = c < d ? gr[c] : 0.f;
         qv[k] = c < d ? q[c] : 0.f;
     }
+    float xv[kS2SPer][4], al[kS2SPer], da[kS2SPer];
+    s2s_rows_lds(X, G, j, xv);
     float s = 0.f;
-    for (int64_t v = p0 + G; v < p1; v += 16) {
-        const float alpha = expf(s2s_logit(X, v, j, qv) - mx) / den;
-        const float da = s2s_logit(X, v, j, gv);
-        s += j == 0 ? alpha * da : 0.f;
+#pragma unroll
+    for (int i = 0; i < kS2SPer; ++i) {
+        al[i] = expf(s2s_dot16(xv[i], qv) - mx) / den;
+        da[i] = s2s_dot16(xv[i], gv);
+        if (G + 16 * i < X.ns) s += j == 0 ? al[i] * da[i] : 0.f;
+    }
+    for (int64_t v = p0 + kS2SRows + G; v < p1; v += 16) {
+        float xg[4];
+        s2s_row_glb(X.x, v, d, j, xg);
+        const float alpha = expf(s2s_dot16(xg, qv) - mx) / den;
+        const float dalpha = s2s_dot16(xg, gv);  // (all 16 lanes: outside the select)
+        s += j == 0 ? alpha * dalpha : 0.f;
     }
     s = s2s_red_q(s2s_red16(s));
     if (l == 0) red[w] = s;
     __syncthreads();
     s = (red[0] + red[1]) + (red[2] + red[3]);
     float acc[4] = {0.f, 0.f, 0.f, 0.f};
-    for (int64_t v = p0 + G; v < p1; v += 16) {
-        const float alpha = expf(s2s_logit(X, v, j, qv) - mx) / den;
-        const float de = alpha * (s2s_logit(X, v, j, gv) - s);
+#pragma unroll
+    for (int i = 0; i < kS2SPer; ++i) {
+        const int o = G + 16 * i;
+        if (o < X.ns) {
+            const float de = al[i] * (da[i] - s);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int c = j + 16 * k;
+                if (c < d) {
+                    // staged rows accumulate in LDS (written out once, after the
+                    // last round)
+                    const float t = fmaf(de, qv[k], al[i] * gv[k]);
+                    const float prev = accumulate ? dxs[o * d + c] : 0.f;
+                    dxs[o * d + c] = prev + t;
+                    acc[k] = fmaf(de, xv[i][k], acc[k]);
+                }
+            }
+        }
+    }
+    for (int64_t v = p0 + kS2SRows + G; v < p1; v += 16) {
+        float xg[4];
+        s2s_row_glb(X.x, v, d, j, xg);
+        const float alpha = expf(s2s_dot16(xg, qv) - mx) / den;
+        const float de = alpha * (s2s_dot16(xg, gv) - s);
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             const int c = j + 16 * k;
             if (c < d) {
                 const float t = fmaf(de, qv[k], alpha * gv[k]);
-                // staged rows accumulate in LDS (written out once, after the
-                // last round), the rest in global memory
-                const int64_t o = v - p0;
-                if (o < X.ns) {
-                    const float prev = accumulate ? dxs[o * d + c] : 0.f;
-                    dxs[o * d + c] = prev + t;
-                } else {
-                    dx[v * d + c] = accumulate ? dx[v * d + c] + t : t;
-                }
-                acc[k] = fmaf(de, X.at(v, c), acc[k]);
+                dx[v * d + c] = accumulate ? dx[v * d + c] + t : t;
+                acc[k] = fmaf(de, xg[k], acc[k]);
             }
         }
     }
@@ -333,7 +402,13 @@ __global__ __launch_bounds__(256) void set2set_fwd_k(
 
 // One workgroup per graph, rounds in reverse: d q*_T = g_out -> dx (rows of
 // the graph; capacity rows past ptr[B] are zeroed by the extra workgroups)
-// and dG [B][T][4d] for set2set_wgrad_k.
+// and dG [B][T][4d] for set2set_wgrad_k.  REG (d = 64): the transposed gate
+// products' weights (lane l of wave w: columns l, l + 64 of W_ih and l of
+// W_hh over gate rows 64 w ..) are loaded into registers at the kernel's
+// start, their latency hidden under the last round's attention (loaded at
+// the products, four dependent 16-row batches: 3.8 us of the kernel, phase
+// trace r05_s2s).
+template <bool REG>
 __global__ __launch_bounds__(256) void set2set_bwd_k(
     const float *__restrict__ x, const int32_t *__restrict__ ptr, int64_t nseg, int d, int T,
     const float *__restrict__ w_ih, const float *__restrict__ w_hh,
@@ -351,6 +426,19 @@ __global__ __launch_bounds__(256) void set2set_bwd_k(
     __shared__ float sX[kS2SRows * kS2SMaxD], sDX[kS2SRows * kS2SMaxD], sRedA[kS2SRed];
     const int64_t g = blockIdx.x;
     const int tid = threadIdx.x, D2 = 2 * d, G4 = 4 * d, S = s2s_save(d);
+    float wT[REG ? kS2SMaxD : 1][3];
+    if constexpr (REG) {
+        if (T > 1) {
+            const int64_t w0 = 64 * (tid >> 6);
+            const int l = tid & 63;
+#pragma unroll
+            for (int i = 0; i < kS2SMaxD; ++i) {
+                wT[i][0] = w_ih[(w0 + i) * 128 + l];
+                wT[i][1] = w_ih[(w0 + i) * 128 + 64 + l];
+                wT[i][2] = w_hh[(w0 + i) * 64 + l];
+            }
+        }
+    }
     const int64_t p0 = ptr[g], p1 = ptr[g + 1];
     const S2SRows X{x, sX, p0, s2s_stage(x, p0, p1, d, sX), d};
     if (tid < D2) sDQ[tid] = g_out[g * D2 + tid];
@@ -396,7 +484,18 @@ __global__ __launch_bounds__(256) void set2set_bwd_k(
         // [d q*_{t-1} | d h_{t-1} (gates path)] = [W_ih | W_hh]^T dG: wave w sums
         // the gates of its quarter, lane l the outputs l, l + 64, l + 128 < 3d
         // (coalesced along the weight rows); the quarters combine in fixed order
-        {
+        if constexpr (REG) {  // (the same row order as below: the same bits)
+            const int w = tid >> 6, l = tid & 63;
+            float acc[3] = {0.f, 0.f, 0.f};
+#pragma unroll
+            for (int i = 0; i < kS2SMaxD; ++i) {
+                const float gj = sDG[64 * w + i];
+#pragma unroll
+                for (int u = 0; u < 3; ++u) acc[u] = fmaf(wT[i][u], gj, acc[u]);
+            }
+#pragma unroll
+            for (int u = 0; u < 3; ++u) sPart[w][l + 64 * u] = acc[u];
+        } else {
             const int w = tid >> 6, l = tid & 63, D3 = 3 * d;
             const int j0 = (G4 * w) / 4, j1 = (G4 * (w + 1)) / 4;
             // per output slot u: its weight column (base, row stride), chosen
@@ -523,8 +622,12 @@ extern "C" int scgib_set2set_bwd(const float *x, const int32_t *graph_ptr, int64
     hipStream_t st = as_stream(stream);
     const int64_t tail = (n_rows * dim + 256 * 16 - 1) / (256 * 16);  // padding-zero blocks
     const int64_t extra = tail < 1 ? 1 : (tail > 256 ? 256 : tail);
-    set2set_bwd_k<<<static_cast<unsigned>(n_graphs + extra), 256, 0, st>>>(
-        x, graph_ptr, n_graphs, dim, n_iters, w_ih, w_hh, save, g_out, dx, dgates, n_rows);
+    if (dim == kS2SMaxD)
+        set2set_bwd_k<true><<<static_cast<unsigned>(n_graphs + extra), 256, 0, st>>>(
+            x, graph_ptr, n_graphs, dim, n_iters, w_ih, w_hh, save, g_out, dx, dgates, n_rows);
+    else
+        set2set_bwd_k<false><<<static_cast<unsigned>(n_graphs + extra), 256, 0, st>>>(
+            x, graph_ptr, n_graphs, dim, n_iters, w_ih, w_hh, save, g_out, dx, dgates, n_rows);
     int rc = launch_status();
     if (rc != SCGIB_OK || !wg) return rc;
     set2set_wgrad_k<<<static_cast<unsigned>(3 * dim + 1), 256, 0, st>>>(

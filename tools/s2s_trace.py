@@ -17,8 +17,9 @@ pkg = importlib.import_module("s-cgib_amd")
 
 FWD = ["prologue", "stage+bias", "r0 gates", "r0 cell", "r0 attention", "r1 + out"]
 BWD = ["-", "stage", "r1 h", "r1 attention", "r1 cell", "r1 products", "r1 comb + r0 h",
-       "r0 attention", "r0 cell", "r0 products", "r0 combine", "dx out"]
-BWD_MARKS = [0, 1, 2, 3, 4, 5, 7, 8, 9, 10, 12, 13]
+       "r0 attention", "r0 cell", "r0 dG out", "dx out"]
+# (round 0 leaves the loop before its products: mark 10 is never written)
+BWD_MARKS = [0, 1, 2, 3, 4, 5, 7, 8, 9, 12, 13]
 
 
 def summary(buf, nblk, marks, names):

@@ -872,15 +872,25 @@ def main():
         torch.cuda.synchronize()
 
     barrier()
+    if os.environ.get("SCGIB_STAMPS_FIRST"):  # diagnostics: the stamps of one step from idle
+        step(a.warmup)
+        barrier()
+        for lab, us in pkg.ops.stamps_read():
+            progress(f"first-step stamp {us:9.2f} us  {lab}")
+        barrier()
     # SCGIB_STEP_PROBE=1 (diagnostics only, tools/gpu_steps_probe.sh): HIP events
     # around every timed step
     probe = [] if os.environ.get("SCGIB_STEP_PROBE") == "1" else None
+    host_us = [] if probe is not None else None
     t0 = time.perf_counter()
     for i in range(a.steps):
         if probe is not None:
             probe.append(torch.cuda.Event(enable_timing=True))
             probe[-1].record()
+            th = time.perf_counter()
         loss = step(a.warmup + i)
+        if probe is not None:
+            host_us.append((time.perf_counter() - th) * 1e6)
     if probe is not None:
         probe.append(torch.cuda.Event(enable_timing=True))
         probe[-1].record()
@@ -893,6 +903,7 @@ def main():
     if probe is not None:
         progress("step probe (ms): " + " ".join(
             f"{probe[i].elapsed_time(probe[i + 1]):.4f}" for i in range(len(probe) - 1)))
+        progress("host replay (us): " + " ".join(f"{u:.0f}" for u in host_us))
     progress(f"timed: {elapsed / a.steps * 1e3:.4f} ms/step, host enqueue "
              f"{t_enq / a.steps * 1e3:.4f} ms/step")
     xq_to = pkg.ops.xq_timeouts(dev)

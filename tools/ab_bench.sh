@@ -12,8 +12,8 @@ for i in $(seq ${ROUNDS:-3}); do
       elif [[ "$w" == --* ]]; then args="$args $w"
       else envs="$envs $w"; fi
     done
-    (cd $dir && env $envs timeout -k 10 200 python bench.py --steps 300 --warmup 20 --no-cpu-baseline \
-      --no-superbatch --no-kernel-timer $args 2>/dev/null) | tail -1 | \
+    (cd $dir && env $envs timeout -k 10 200 python bench.py --steps ${STEPS:-300} --warmup ${WARMUP:-20} --no-cpu-baseline \
+      --no-superbatch --no-kernel-timer --no-finetune $args 2>/dev/null) | tail -1 | \
       python -c "import sys,json; d=json.loads(sys.stdin.read()); print('$cfg', d['ms_per_step'], d['value'])" || exit 1
   done
 done

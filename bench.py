@@ -669,6 +669,9 @@ def main():
     ap.add_argument("--finetune", choices=["molhiv"], default=None,
                     help="time the fine-tune step of BASELINE.json configs[4] instead "
                          "(finetune_bench.py; --batch defaults to 32 there)")
+    ap.add_argument("--no-handoffs", action="store_true",
+                    help="the encoder pair joins its streams with ordinary stream edges instead "
+                         "of signal / wait kernels (ops.XQ_FLAGS = False; A/B)")
     ap.add_argument("--torch-head", action="store_true",
                     help="fine-tune: torch's predict head / sigmoid / BCE instead of csrc/head.hip "
                          "(models.FUSE_HEAD; A/B)")
@@ -712,6 +715,8 @@ def main():
     xq_ok, xq_why = pkg.ops.handoff_rule(torch.cuda.device_count(), xq_env)
     if not xq_ok:
         pkg.ops.XQ_FLAGS, pkg.ops.XQ_REASON = False, xq_why
+    elif a.no_handoffs:
+        pkg.ops.XQ_FLAGS, pkg.ops.XQ_REASON = False, "--no-handoffs"
     torch.manual_seed(1234 + rank)
     global RUN_CONFIG
     RUN_CONFIG = {"workload": a.workload, "batch": a.batch, "k": a.k}

@@ -648,7 +648,11 @@ class _GinEncoder(torch.autograd.Function):
             meta["wg"] = wg
             if pre and l == 0:
                 width = int(_lib.query("scgib_gin_layer0_slab_width"))
-                slab = torch.empty(nslab * width, dtype=torch.float32, device=dev)
+                # (dwt_row: one spare row whose d Wt columns another encoder's
+                # reduce fills — the pair's core chain — so this encoder's
+                # final reduce returns the sum of both, _GinEncoderPair)
+                xrow = int(getattr(ctx, "dwt_row", False))
+                slab = torch.empty((nslab + xrow) * width, dtype=torch.float32, device=dev)
                 _launch("scgib_gin_layer0_bwd", meta, _p(dy), _p(z2), _p(r), _p(agg), _p(aggx),
                         ctx.n_feat, _p(stat), _p(coef), _p(w1c), _p(b1c), _p(w2c), n, _p(slab),
                         int(wg), _p(gr.dims), _byref(bpend), st)
@@ -666,18 +670,35 @@ class _GinEncoder(torch.autograd.Function):
             if not wg:  # no weight gradients: only layer 0's dWt (its slab's tail)
                 if pre and l == 0:
                     o = HIDDEN * HIDDEN + HIDDEN * d_in + 2 * HIDDEN
-                    dwt = torch.empty(32 * ctx.n_feat, dtype=torch.float32, device=dev)
-                    jobs.append(_lib.SlabJob(slab.data_ptr() + 4 * o, dwt.data_ptr(),
-                                             32 * ctx.n_feat, nslab, width))
+                    into = getattr(ctx, "dwt_into", None)
+                    if into is None:
+                        dwt = torch.empty(32 * ctx.n_feat, dtype=torch.float32, device=dev)
+                    jobs.append(_lib.SlabJob(slab.data_ptr() + 4 * o,
+                                             into if into is not None else dwt.data_ptr(),
+                                             32 * ctx.n_feat, nslab + xrow, width))
                     keep.append(slab)
-                    dwt = dwt.view(32, ctx.n_feat)
+                    if xrow:
+                        ctx.dwt_row_ptr = slab.data_ptr() + 4 * (nslab * width + o)
+                        ctx.dwt_row_slab = slab
+                    dwt = dwt.view(32, ctx.n_feat) if into is None else None
                 dagg_next = dagg
                 yield
                 continue
             wgrad = torch.empty(width, dtype=torch.float32, device=dev)
             if pre and l == 0:  # dWt occupies 32 * F of its 512 columns
-                used = HIDDEN * HIDDEN + HIDDEN * d_in + 2 * HIDDEN + 32 * ctx.n_feat
-                jobs.append(_lib.SlabJob(slab.data_ptr(), wgrad.data_ptr(), used, nslab, width))
+                o = HIDDEN * HIDDEN + HIDDEN * d_in + 2 * HIDDEN
+                into = getattr(ctx, "dwt_into", None)
+                if into is None and not xrow:
+                    jobs.append(_lib.SlabJob(slab.data_ptr(), wgrad.data_ptr(),
+                                             o + 32 * ctx.n_feat, nslab, width))
+                else:  # dWt as its own job: into another encoder's row / over the spare row
+                    jobs.append(_lib.SlabJob(slab.data_ptr(), wgrad.data_ptr(), o, nslab, width))
+                    jobs.append(_lib.SlabJob(slab.data_ptr() + 4 * o,
+                                             into if into is not None else wgrad.data_ptr() + 4 * o,
+                                             32 * ctx.n_feat, nslab + xrow, width))
+                if xrow:
+                    ctx.dwt_row_ptr = slab.data_ptr() + 4 * (nslab * width + o)
+                    ctx.dwt_row_slab = slab
                 keep.append(slab)
             else:  # reduced by the next stats launch, or together at the end
                 ns = int(_lib.query("scgib_gin_layer_bwd_slabs", n, d_in))
@@ -693,7 +714,7 @@ class _GinEncoder(torch.autograd.Function):
             o += HIDDEN * d_in
             grads[6 * l + 3] = wgrad[o:o + HIDDEN]
             grads[6 * l + 1] = wgrad[o + HIDDEN:o + 2 * HIDDEN]
-            if pre and l == 0:
+            if pre and l == 0 and getattr(ctx, "dwt_into", None) is None:
                 o += 2 * HIDDEN
                 dwt = wgrad[o:o + 32 * ctx.n_feat].view(32, ctx.n_feat)
             dagg_next = dagg
@@ -703,7 +724,9 @@ class _GinEncoder(torch.autograd.Function):
             ctx.extra_jobs = None
             jobs.extend(extra[0])
             keep.extend(extra[1])
-        if jobs:  # every layer's weight-gradient slabs, one fixed-order reduce launch
+        if jobs and getattr(ctx, "defer_final", False):  # enqueued by the caller (the pair)
+            ctx.final = (jobs, keep)
+        elif jobs:  # every layer's weight-gradient slabs, one fixed-order reduce launch
             _reduce_jobs(jobs, st)
             del keep  # slabs stay allocated until the launch is enqueued
         if pre:
@@ -1020,12 +1043,22 @@ class _GinEncoderPair(torch.autograd.Function):
         # the critical ego chain is captured first: the replayed graph then
         # puts it on the interaction's queue (round 2: 0.4381 -> 0.4326 ms)
         ctx.sub[0].stamp_tag = "bwd.ego"
+        # d Wt = d Wt(ego) + d Wt(core) without a separate add after the join:
+        # the core chain's reduce writes its d Wt into a spare row of the ego
+        # layer-0 slab, and the ego chain's final reduce — enqueued after the
+        # join, which costs nothing there (the core chain ends first) — sums
+        # it with the ego's rows
+        ctx.sub[0].dwt_row = ctx.sub[0].defer_final = True
         later = scope.take_later() if scope is not None else []
         ge = _GinEncoder.backward(ctx.sub[0], g_s, g_ro)
         for launch, _ in later:  # deferred weight-gradient launches, after the ego chain
             launch()
         later = None
         stamp("bwd.ego_end[main]")
+        row = getattr(ctx.sub[0], "dwt_row_ptr", None)
+        if row is not None:
+            ctx.sub[1].dwt_into = row
+            ctx.sub[0].dwt_row_slab.record_stream(side)
         with torch.cuda.stream(side):
             if ctx.lin and g_t is not None:
                 f, w0 = ctx.lin_saved
@@ -1062,6 +1095,12 @@ class _GinEncoderPair(torch.autograd.Function):
             stamp("bwd.core_end[side]")
         main.wait_stream(side)
         stamp("bwd.joined[main]")
+        final = getattr(ctx.sub[0], "final", None)
+        if final is not None:  # the ego chain's weight-gradient reduce, d Wt(core) included
+            ctx.sub[0].final = None
+            _reduce_jobs(final[0], _stream())
+            final = None
+        ctx.sub[0].dwt_row_slab = None
         if ctx.side_tail is not None and hasattr(ctx.side_tail, "joined"):
             ctx.side_tail.joined()  # ordered before main's later work by the join above
         held = None  # after the join: main-stream reuse is ordered after side's reads
@@ -1072,7 +1111,7 @@ class _GinEncoderPair(torch.autograd.Function):
             g_f_in.record_stream(side)
         if g_t is not None:
             g_t.record_stream(side)
-        dwt = ge[5] if gc[5] is None else ge[5] + gc[5]
+        dwt = ge[5] if gc[5] is None else ge[5] + gc[5]  # (gc[5] None: summed by the reduce)
         return (None, dwt, dw0, db0, None, None, None, None, None, None, None, None, *ge[7:],
                 *gc[7:])
 

@@ -2060,9 +2060,10 @@ extern "C" int64_t scgib_gin_tiles(int64_t n_nodes) { return (n_nodes + TM - 1) 
 extern "C" int scgib_trace_set_egonet(void *buf);   // (egonet.hip's own g_trace)
 extern "C" int scgib_trace_set_set2set(void *buf);  // (set2set.hip's)
 extern "C" int scgib_trace_set_interaction(void *buf);  // (interaction.hip's)
+extern "C" int scgib_trace_set_head(void *buf);  // (head.hip's)
 extern "C" int scgib_trace_set(void *buf) {
     if (scgib_trace_set_egonet(buf) != 0 || scgib_trace_set_set2set(buf) != 0 ||
-        scgib_trace_set_interaction(buf) != 0)
+        scgib_trace_set_interaction(buf) != 0 || scgib_trace_set_head(buf) != 0)
         return 1;
     return hipMemcpyToSymbol(HIP_SYMBOL(g_trace), &buf, sizeof(buf)) == hipSuccess ? 0 : 1;
 }

@@ -49,6 +49,7 @@ __global__ __launch_bounds__(256) void head_fwd_k(const float *__restrict__ x, i
     __shared__ float sW2[kHeadCMax * (kHeadH + 1)];
     const int tid = threadIdx.x, LK = K + 1, K4 = K >> 2;
     const int64_t row0 = static_cast<int64_t>(blockIdx.x) * kHeadRows;
+    SCGIB_MARK(0);
     const int nv = static_cast<int>(B - row0 < kHeadRows ? B - row0 : kHeadRows);
     // loads: W1 (64 K / 4 <= 2048 float4: 8 per thread), x (16 K / 4: 2), W2 (C 64: 4)
     float4 vw[8], vx[2];
@@ -86,6 +87,7 @@ __global__ __launch_bounds__(256) void head_fwd_k(const float *__restrict__ x, i
         if (i < nw2) sW2[(i / kHeadH) * (kHeadH + 1) + i % kHeadH] = vw2[u];
     }
     __syncthreads();
+    SCGIB_MARK(1);
     const int r = tid >> 4, u = tid & 15;
     float acc[4];
 #pragma unroll
@@ -103,6 +105,7 @@ __global__ __launch_bounds__(256) void head_fwd_k(const float *__restrict__ x, i
         if (r < nv) hid[(row0 + r) * kHeadH + j] = h;
     }
     __syncthreads();
+    SCGIB_MARK(2);
     for (int c = u; c < C; c += 16) {
         float o = 0.f;
         for (int j = 0; j < kHeadH; ++j) o = fmaf(sH[r * (kHeadH + 1) + j], sW2[c * (kHeadH + 1) + j], o);
@@ -110,6 +113,7 @@ __global__ __launch_bounds__(256) void head_fwd_k(const float *__restrict__ x, i
         if (act) o = 1.f / (1.f + expf(-o));
         if (r < nv) out[(row0 + r) * C + c] = o;
     }
+    SCGIB_MARK(3);
 }
 
 // backward, kHeadG workgroups, rows in chunks of 32:
@@ -142,6 +146,7 @@ __global__ __launch_bounds__(256) void head_bwd_k(
     // this workgroup's dx columns: float4 columns [q K4 / G, (q + 1) K4 / G)
     const int kb = 4 * ((q * K4) / kHeadG), ke = 4 * (((q + 1) * K4) / kHeadG), s4 = (ke - kb) >> 2;
     auto put4 = [](float *d, const float4 v) { d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w; };
+    SCGIB_MARK(0);
     {   // once: the W1 column slice (64 x <= 8 float4: 2 per thread) and W2 (C 64: 4)
         const int nw = kHeadH * s4, nw2 = C * kHeadH;
         float4 vw[2];
@@ -170,6 +175,7 @@ __global__ __launch_bounds__(256) void head_bwd_k(
             if (i < nw2) sW2[i] = vw2[u];
         }
     }
+    SCGIB_MARK(1);
     const int jw = 16 * q + (tid >> 4), kw = tid & 15;  // dW1 ownership
     const int xr = tid >> 3, kx = tid & 7;              // dx / dh ownership
     float aW1[8];
@@ -225,6 +231,7 @@ __global__ __launch_bounds__(256) void head_bwd_k(
             }
         }
         __syncthreads();
+        if (c0 == 0) SCGIB_MARK(2);
         if (q == 0 && tid < kHeadH) {  // dW2[c][j] += sum_r do[r][c] hid[r][j] (column j = tid); db2 by thread c
 #pragma unroll
             for (int c = 0; c < kHeadCMax; ++c) {
@@ -249,10 +256,12 @@ __global__ __launch_bounds__(256) void head_bwd_k(
             for (int c = 0; c < C; ++c) a = fmaf(sDo[xr * kHeadCMax + c], sW2[c * kHeadH + j], a);
             dh[m] = sH[xr * (kHeadH + 1) + j] > 0.f ? a : 0.f;
         }
+        if (c0 == 0) SCGIB_MARK(3);
         __syncthreads();  // every read of hid is done: dh replaces it
 #pragma unroll
         for (int m = 0; m < 8; ++m) sH[xr * (kHeadH + 1) + (tid & 7) + 8 * m] = dh[m];
         __syncthreads();
+        if (c0 == 0) SCGIB_MARK(4);
         for (int r = 0; r < kHeadChunk; ++r) {  // dW1[jw][k] += dh[r][jw] x[r][k]
             const float d = sH[r * (kHeadH + 1) + jw];
 #pragma unroll
@@ -266,6 +275,7 @@ __global__ __launch_bounds__(256) void head_bwd_k(
             for (int r = 0; r < kHeadChunk; ++r) a += sH[r * (kHeadH + 1) + 16 * q + tid];
             aB1 += a;
         }
+        if (c0 == 0) SCGIB_MARK(5);
         if (xr < nv) {  // dx[xr][k] = sum_j dh[xr][j] W1[j][k], k in [kb, ke)
             float a[4];
 #pragma unroll
@@ -281,6 +291,7 @@ __global__ __launch_bounds__(256) void head_bwd_k(
                 if (k < ke) dx[(c0 + xr) * K + k] = a[m];
             }
         }
+        if (c0 == 0) SCGIB_MARK(6);
     }
 #pragma unroll
     for (int m = 0; m < 8; ++m) {
@@ -294,6 +305,7 @@ __global__ __launch_bounds__(256) void head_bwd_k(
             if (c < C) dw2[c * kHeadH + tid] = aW2[c];
     }
     if (q == 0 && tid < C) db2[tid] = aB2;
+    SCGIB_MARK(7);
 }
 
 // BCE, mean reduction, as torch's binary_cross_entropy: per element
@@ -386,3 +398,10 @@ extern "C" int scgib_bce_bwd(const float *scores, const float *targets, int64_t 
         scores, targets, n, g_loss, d_scores);
     return launch_status();
 }
+
+#ifdef SCGIB_TRACE
+// debug build only: this file's own g_trace (see common.h; scgib_trace_set)
+extern "C" int scgib_trace_set_head(void *buf) {
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_trace), &buf, sizeof(buf)) == hipSuccess ? 0 : 1;
+}
+#endif

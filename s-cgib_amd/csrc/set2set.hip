@@ -93,11 +93,41 @@ struct S2SRows {
     int ns, d;
 };
 
-// all threads: stage rows [p0, p0 + min(n, kS2SRows)) of x into xs (then a barrier)
+// all 256 threads: stage rows [p0, p0 + min(n, kS2SRows)) of x into xs (then a
+// barrier).  Every thread's loads (<= 4 float4, or <= 16 floats for a width
+// not a multiple of 4) are issued before its LDS stores: a load / wait /
+// store loop paid one memory latency per element, before the kernels' first
+// phase mark (8 of set2set_fwd_k's 17.6 us in the kernel trace).  Call it
+// before issuing other loads whose wait it would otherwise share.
 __device__ __forceinline__ int s2s_stage(const float *__restrict__ x, int64_t p0, int64_t p1,
                                          int d, float *xs) {
     const int ns = static_cast<int>(p1 - p0 < kS2SRows ? p1 - p0 : kS2SRows);
-    for (int i = threadIdx.x; i < ns * d; i += blockDim.x) xs[i] = x[p0 * d + i];
+    const int tid = threadIdx.x, total = ns * d;
+    if ((d & 3) == 0) {  // rows 16-B aligned (row r at r d floats)
+        constexpr int K = kS2SRows * kS2SMaxD / 4 / 256;
+        const float4 *x4 = reinterpret_cast<const float4 *>(x + p0 * d);
+        float4 *xs4 = reinterpret_cast<float4 *>(xs);
+        float4 v[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const int i = tid + 256 * k;
+            v[k] = i < total / 4 ? x4[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+            if (tid + 256 * k < total / 4) xs4[tid + 256 * k] = v[k];
+    } else {
+        constexpr int K = kS2SRows * kS2SMaxD / 256;
+        float v[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const int i = tid + 256 * k;
+            v[k] = i < total ? x[p0 * d + i] : 0.f;
+        }
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+            if (tid + 256 * k < total) xs[tid + 256 * k] = v[k];
+    }
     return ns;
 }
 
@@ -337,6 +367,8 @@ __global__ __launch_bounds__(256) void set2set_fwd_k(
     const int64_t g = blockIdx.x;
     const int tid = threadIdx.x, D2 = 2 * d, G4 = 4 * d, S = s2s_save(d);
     constexpr int NI = REG ? 2 * kS2SMaxD / 4 : 1, NH = REG ? kS2SMaxD / 4 : 1;
+    const int64_t p0 = ptr[g], p1 = ptr[g + 1];
+    const S2SRows X{x, sX, p0, s2s_stage(x, p0, p1, d, sX), d};
     float4 wi[NI], wh[NH];
     if constexpr (REG) {  // d = 64, G4 = 256: every thread owns a gate
         const float4 *ri = reinterpret_cast<const float4 *>(w_ih + static_cast<int64_t>(tid) * D2);
@@ -346,8 +378,6 @@ __global__ __launch_bounds__(256) void set2set_fwd_k(
 #pragma unroll
         for (int k = 0; k < NH; ++k) wh[k] = rh[k];
     }
-    const int64_t p0 = ptr[g], p1 = ptr[g + 1];
-    const S2SRows X{x, sX, p0, s2s_stage(x, p0, p1, d, sX), d};
     if (tid < D2) sQ[tid] = 0.f;
     if (tid < d) sH[tid] = sC[tid] = 0.f;
     // this thread's gate biases (b_ih + b_hh added after the two products, as
@@ -426,6 +456,8 @@ __global__ __launch_bounds__(256) void set2set_bwd_k(
     __shared__ float sX[kS2SRows * kS2SMaxD], sDX[kS2SRows * kS2SMaxD], sRedA[kS2SRed];
     const int64_t g = blockIdx.x;
     const int tid = threadIdx.x, D2 = 2 * d, G4 = 4 * d, S = s2s_save(d);
+    const int64_t p0 = ptr[g], p1 = ptr[g + 1];
+    const S2SRows X{x, sX, p0, s2s_stage(x, p0, p1, d, sX), d};
     float wT[REG ? kS2SMaxD : 1][3];
     if constexpr (REG) {
         if (T > 1) {
@@ -439,8 +471,6 @@ __global__ __launch_bounds__(256) void set2set_bwd_k(
             }
         }
     }
-    const int64_t p0 = ptr[g], p1 = ptr[g + 1];
-    const S2SRows X{x, sX, p0, s2s_stage(x, p0, p1, d, sX), d};
     if (tid < D2) sDQ[tid] = g_out[g * D2 + tid];
     if (tid < d) sDH[tid] = sDC[tid] = 0.f;  // from round t + 1 (none after the last)
     SCGIB_MARK(0);

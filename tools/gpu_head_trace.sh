@@ -1,0 +1,8 @@
+#!/bin/bash
+# Fine-tune head phase stamps (trace build of the library, built here)
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"
+mkdir -p gpurun_out/head
+make -s -j16 -C s-cgib_amd/csrc trace > gpurun_out/head/build.log 2>&1 || { echo "trace build failed"; exit 3; }
+SCGIB_LIB=$PWD/s-cgib_amd/libscgib_trace.so timeout -k 10 300 python tools/head_trace.py > gpurun_out/head/trace.txt 2>&1; rc=$?
+grep -v amdgpu.ids gpurun_out/head/trace.txt | head -60; exit $rc

@@ -26,9 +26,11 @@ __device__ __forceinline__ float4 hld4(const float *p) { return *reinterpret_cas
 // together before its LDS stores (a store-after-load loop waits on each load)
 
 // forward: workgroup = 16 rows; thread (r = tid >> 4, u = tid & 15) owns the
-// hidden units u, u + 16, u + 32, u + 48 of row r (LDS W1 rows at stride
-// K + 1: the 16 lanes of a row read 16 different banks), then output c of
-// row r for c = u, u + 16, ... < C.  with_ru: one more workgroup runs the
+// hidden units u, u + 16, u + 32, u + 48 of row r, then output c of row r for
+// c = u, u + 16, ... < C.  LDS rows at stride K + 4 (hidden at 68), read as
+// float4 (16-B aligned; lane u's four banks start at 4 u: conflict-free), the
+// k order of every sum unchanged (scalar reads at stride K + 1 left ~one LDS
+// wait per read: 4.3 us for the hidden units, tools/head_trace.py).  with_ru: one more workgroup runs the
 // compressor BatchNorm's running update (running_update.h), which nothing in
 // the step reads — instead of its own launch on an aux stream.
 __global__ __launch_bounds__(256) void head_fwd_k(const float *__restrict__ x, int64_t B, int K,
@@ -43,11 +45,12 @@ __global__ __launch_bounds__(256) void head_fwd_k(const float *__restrict__ x, i
         running_update_body<256>(ru);
         return;
     }
-    __shared__ float sW1[kHeadH * (kHeadKMax + 1)];
-    __shared__ float sX[kHeadRows * (kHeadKMax + 1)];
-    __shared__ float sH[kHeadRows * (kHeadH + 1)];
-    __shared__ float sW2[kHeadCMax * (kHeadH + 1)];
-    const int tid = threadIdx.x, LK = K + 1, K4 = K >> 2;
+    constexpr int LH = kHeadH + 4;
+    __shared__ float4 sW1[kHeadH * (kHeadKMax + 4) / 4];
+    __shared__ float4 sX[kHeadRows * (kHeadKMax + 4) / 4];
+    __shared__ float4 sH[kHeadRows * LH / 4];
+    __shared__ float4 sW2[kHeadCMax * LH / 4];
+    const int tid = threadIdx.x, K4 = K >> 2, L4 = K4 + 1;  // row strides in float4
     const int64_t row0 = static_cast<int64_t>(blockIdx.x) * kHeadRows;
     SCGIB_MARK(0);
     const int nv = static_cast<int>(B - row0 < kHeadRows ? B - row0 : kHeadRows);
@@ -70,21 +73,21 @@ __global__ __launch_bounds__(256) void head_fwd_k(const float *__restrict__ x, i
         const int i = tid + 256 * u;
         vw2[u] = w2[i < nw2 ? i : nw2 - 1];
     }
-    auto put4 = [](float *d, const float4 v) { d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w; };
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
         const int i = tid + 256 * u, j = i / K4;
-        if (i < nw) put4(sW1 + j * LK + 4 * (i - j * K4), vw[u]);
+        if (i < nw) sW1[j * L4 + (i - j * K4)] = vw[u];
     }
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
         const int i = tid + 256 * u, r = i / K4;
-        if (i < nx) put4(sX + r * LK + 4 * (i - r * K4), vx[u]);
+        if (i < nx) sX[r * L4 + (i - r * K4)] = vx[u];
     }
+    float *sW2f = reinterpret_cast<float *>(sW2), *sHf = reinterpret_cast<float *>(sH);
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
         const int i = tid + 256 * u;
-        if (i < nw2) sW2[(i / kHeadH) * (kHeadH + 1) + i % kHeadH] = vw2[u];
+        if (i < nw2) sW2f[(i / kHeadH) * LH + i % kHeadH] = vw2[u];
     }
     __syncthreads();
     SCGIB_MARK(1);
@@ -92,23 +95,37 @@ __global__ __launch_bounds__(256) void head_fwd_k(const float *__restrict__ x, i
     float acc[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) acc[i] = 0.f;
-    for (int k = 0; k < K; ++k) {
-        const float xv = sX[r * LK + k];
+#pragma unroll 4
+    for (int k4 = 0; k4 < K4; ++k4) {
+        const float4 xv = sX[r * L4 + k4];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) acc[i] = fmaf(xv, sW1[(u + 16 * i) * LK + k], acc[i]);
+        for (int i = 0; i < 4; ++i) {
+            const float4 w = sW1[(u + 16 * i) * L4 + k4];
+            acc[i] = fmaf(xv.x, w.x, acc[i]);
+            acc[i] = fmaf(xv.y, w.y, acc[i]);
+            acc[i] = fmaf(xv.z, w.z, acc[i]);
+            acc[i] = fmaf(xv.w, w.w, acc[i]);
+        }
     }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         const int j = u + 16 * i;
         const float h = fmaxf(acc[i] + b1[j], 0.f);
-        sH[r * (kHeadH + 1) + j] = h;
+        sHf[r * LH + j] = h;
         if (r < nv) hid[(row0 + r) * kHeadH + j] = h;
     }
     __syncthreads();
     SCGIB_MARK(2);
     for (int c = u; c < C; c += 16) {
         float o = 0.f;
-        for (int j = 0; j < kHeadH; ++j) o = fmaf(sH[r * (kHeadH + 1) + j], sW2[c * (kHeadH + 1) + j], o);
+#pragma unroll 4
+        for (int j4 = 0; j4 < kHeadH / 4; ++j4) {
+            const float4 h = sH[r * (LH / 4) + j4], w = sW2[c * (LH / 4) + j4];
+            o = fmaf(h.x, w.x, o);
+            o = fmaf(h.y, w.y, o);
+            o = fmaf(h.z, w.z, o);
+            o = fmaf(h.w, w.w, o);
+        }
         o += b2[c];
         if (act) o = 1.f / (1.f + expf(-o));
         if (r < nv) out[(row0 + r) * C + c] = o;
@@ -262,13 +279,17 @@ __global__ __launch_bounds__(256) void head_bwd_k(
         for (int m = 0; m < 8; ++m) sH[xr * (kHeadH + 1) + (tid & 7) + 8 * m] = dh[m];
         __syncthreads();
         if (c0 == 0) SCGIB_MARK(4);
-        for (int r = 0; r < kHeadChunk; ++r) {  // dW1[jw][k] += dh[r][jw] x[r][k]
+        // dW1[jw][k] += dh[r][jw] x[r][k].  Unconditional: a lane-dependent
+        // `k < K` here put each FMA and its LDS read in its own exec-masked
+        // branch with its own wait (9.3 us of the kernel, tools/head_trace.py);
+        // r LK + k < kHeadChunk (kHeadKMax + 1) for every K <= kHeadKMax, and
+        // columns k >= K are never written out.  (Rows 4 at a time: fully
+        // unrolled, hipcc hoisted all 256 reads into registers and spilled.)
+#pragma unroll 4
+        for (int r = 0; r < kHeadChunk; ++r) {
             const float d = sH[r * (kHeadH + 1) + jw];
 #pragma unroll
-            for (int m = 0; m < 8; ++m) {
-                const int k = kw + 16 * m;
-                if (k < K) aW1[m] = fmaf(d, sX[r * LK + k], aW1[m]);
-            }
+            for (int m = 0; m < 8; ++m) aW1[m] = fmaf(d, sX[r * LK + kw + 16 * m], aW1[m]);
         }
         if (tid < 16) {
             float a = 0.f;

@@ -601,13 +601,15 @@ int scgib_contrastive_bwd(const float *z1, const float *z2, int64_t n_graphs, fl
  * Mainmodel_continue (models.py:569-571 / :1055-1057, applied at :676 /
  * :1174).  Forward saves r = relu(x W1^T + b1) [N][64] for backward.
  * Backward: dx [N][d_in] and wgrad = dW2[64*64] | dW1[64*d_in] | db2 | db1
- * (fixed-order, deterministic); `slab` holds scgib_mlp2_slab_floats(n, d_in);
+ * (fixed-order, deterministic); `slab` holds scgib_mlp2_slab_floats(n, d_in)
+ * (d_in = 128 on few tiles: two workgroups, two slab rows, per tile — ABI 19);
  * wgrad NULL: the slabs are left for the caller's reduce (a deferred one).
  * linear: out = x W^T (+ b), 64 -> 64 — compressor[0] (models.py:589-592 /
  * :1081-1084, applied at :596 / :1092).  Backward writes dx = add + dy W
  * (`add` may be NULL) and wgrad = dW[64*64] | db[64]; `slab` holds
  * scgib_linear_slab_floats(n).  Capacity mode as above (dims). */
 int64_t scgib_mlp2_slab_floats(int64_t n_nodes, int32_t d_in);
+int64_t scgib_mlp2_recon_slab_floats(int64_t n_nodes, int32_t d_in);
 int scgib_mlp2_fwd(const float *x, int32_t d_in, int64_t n_nodes, const float *w1,
                    const float *b1, const float *w2, const float *b2, float *r, float *out,
                    const int32_t *dims, scgib_stream_t stream);
@@ -626,7 +628,7 @@ int scgib_mlp2_bwd(const float *dout, const float *x, const float *r, int32_t d_
  * way).  Backward: dx = d loss / d x and wgrad as
  * scgib_mlp2_bwd, for d loss / d recon = *g_loss; rowptr_t/col_t NULL for a
  * symmetric graph (A = A^T).  wgrad NULL: the per-workgroup slabs
- * (scgib_mlp2_slab_floats(n, d_in) floats, width 64*64 + 64*d_in + 128) are
+ * (scgib_mlp2_recon_slab_floats(n, d_in) floats, width 64*64 + 64*d_in + 128) are
  * left for the caller's scgib_slab_reduce(_multi) — the model path defers
  * them into an encoder chain's final reduce, off the loss section. */
 int64_t scgib_mlp2_recon_ws_floats(int64_t n_nodes);

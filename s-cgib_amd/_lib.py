@@ -75,6 +75,7 @@ SIGNATURES = {
     "scgib_contrastive_fwd": (ctypes.c_int, [_P, _P, _I64, _P, _P, _P, _P]),
     "scgib_contrastive_bwd": (ctypes.c_int, [_P, _P, _I64, _P, _P, _P, _P, _P, _P]),
     "scgib_mlp2_slab_floats": (_I64, [_I64, _I32]),
+    "scgib_mlp2_recon_slab_floats": (_I64, [_I64, _I32]),
     "scgib_mlp2_fwd": (ctypes.c_int, [_P, _I32, _I64, _P, _P, _P, _P, _P, _P, _P, _P]),
     "scgib_mlp2_bwd": (ctypes.c_int, [_P, _P, _P, _I32, _P, _P, _I64, _P, _P, _P, _P, _P]),
     "scgib_mlp2_recon_ws_floats": (_I64, [_I64]),
@@ -179,7 +180,7 @@ class RunningUpdate(ctypes.Structure):
                 ("num_batches_tracked", ctypes.c_void_p)]
 
 
-ABI_VERSION = 18
+ABI_VERSION = 19
 STATS_STRIDE = 260
 PGRAD_STRIDE = 324
 HIDDEN = 64

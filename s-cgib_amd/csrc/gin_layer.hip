@@ -1193,7 +1193,7 @@ __global__ __launch_bounds__(256, (DIN <= 64 && !RECON ? 2 : 1)) void gin_bwd_k(
     const float *__restrict__ coef, const float *__restrict__ w1, const float *__restrict__ w2,
     int64_t ncap, int64_t ntiles, float *__restrict__ dagg_out, float *__restrict__ slab,
     const int32_t *__restrict__ dims, const float *__restrict__ aggx, scgib_bn_bwd_pending pend,
-    ReconArgs rec, int pre_f = kPreF, const float *__restrict__ b1 = nullptr) {
+    ReconArgs rec, int pre_f = kPreF, const float *__restrict__ b1 = nullptr, int nsplit = 1) {
     static_assert(!PRE || DIN == 32, "transfer_d fold: layer 0 only");
     static_assert(!RC || PRE, "r recomputed in the layer-0 backward only (gin_bwd5r_k: d_in = 64)");
     static_assert(WG || (PRE && !RC), "frozen weights: the layer-0 stored-r backward only");
@@ -1231,6 +1231,12 @@ __global__ __launch_bounds__(256, (DIN <= 64 && !RECON ? 2 : 1)) void gin_bwd_k(
     }
     const int tid = threadIdx.x, l = tid & 63, w = tid >> 6;
     const int wr = w >> 1, wc = w & 1;
+    // nsplit 2 (the dense d_in = 128 MLP on few tiles: scgib_mlp2_bwd): two
+    // workgroups per tile, each forming half of the dW1 / d(agg) column blocks
+    // (its q1 = half), after the same dz2 / dz1 (the same bits: mma_pf is
+    // mma_pf2's second product); half 0 alone adds dW2 / db2 / db1.  Every
+    // workgroup writes its whole slab row (zeros where the other half adds).
+    const int half = static_cast<int>(blockIdx.x) % nsplit;
     SCGIB_MARK(0);
     SCGIB_MARK_HWID();
     [[maybe_unused]] const float rc_bias = RC ? b1[wc * 32 + (l & 31)] : 0.f;
@@ -1319,7 +1325,7 @@ __global__ __launch_bounds__(256, (DIN <= 64 && !RECON ? 2 : 1)) void gin_bwd_k(
                              sCoef[67 + 4 * c4]);
         }
     }
-    for (int64_t tile = blockIdx.x; tile < ntiles; tile += gsz) {
+    for (int64_t tile = blockIdx.x / nsplit; tile < ntiles; tile += gsz / nsplit) {
         const int64_t row0 = tile * TM;
         const int nv = static_cast<int>(n - row0 < TM ? (n - row0 > 0 ? n - row0 : 0) : TM);
         if (dims) {  // capacity mode: zero this tile's padded rows of d(agg)
@@ -1418,11 +1424,11 @@ __global__ __launch_bounds__(256, (DIN <= 64 && !RECON ? 2 : 1)) void gin_bwd_k(
             }
             __syncthreads();
         }
-        if (tile == blockIdx.x) SCGIB_MARK(1);
+        if (tile == blockIdx.x / nsplit) SCGIB_MARK(1);
         // dW2 += dz2^T r  (sub-tile j-block wr, k-block wc)
         // dr = dz2 W2  (rows wr, cols wc); the two products alternate
         f32x16 dr = zero16();
-        if constexpr (WG) {
+        if (WG && half == 0) {
             mma_pf2<64, true, true, false, true>(sD + wr * 32, LDH, sR + wc * 32, LDH, accW2,
                                                  sD + wr * 32 * LDH, LDH, sW2 + wc * 32, LDH, dr);
             db2 = col_sum16(db2, sD + q * LDH + ch, 4 * LDH);
@@ -1437,7 +1443,7 @@ __global__ __launch_bounds__(256, (DIN <= 64 && !RECON ? 2 : 1)) void gin_bwd_k(
             sD[row * LDH + cc] = sR[row * LDH + cc] > 0.f ? dr[reg] : 0.f;
         }
         __syncthreads();  // r is dead: the agg tile (held in registers) takes its buffer
-        if (tile == blockIdx.x) SCGIB_MARK(2);
+        if (tile == blockIdx.x / nsplit) SCGIB_MARK(2);
         // RC: the agg tile is already in the d(agg0) buffer (the r recompute's
         // operand), the dead r buffer takes d(agg0) instead — same layouts
         float *const aggT = RC ? sPD : sA, *const daggT = RC ? sRA : sPD;
@@ -1450,12 +1456,12 @@ __global__ __launch_bounds__(256, (DIN <= 64 && !RECON ? 2 : 1)) void gin_bwd_k(
             }
             __syncthreads();
         }
-        if (WG) db1 = col_sum16(db1, sD + q * LDH + ch, 4 * LDH);
+        if (WG && half == 0) db1 = col_sum16(db1, sD + q * LDH + ch, 4 * LDH);
         // dW1 += dz1^T agg  (64 x DIN) ; d(agg) = dz1 W1  (TM x DIN)
 #pragma unroll
         for (int q1 = 0; q1 < NW1; ++q1) {
             const int sub = w + 4 * q1;
-            if (sub < NSUB1) {
+            if (sub < NSUB1 && (nsplit == 1 || q1 == half)) {  // (wave-uniform)
                 const int jb = sub & 1, kb = sub >> 1;  // j-block (rows of dW1 / d(agg)), k-block
                 f32x16 da = zero16();
                 if constexpr (WG)
@@ -1475,7 +1481,7 @@ __global__ __launch_bounds__(256, (DIN <= 64 && !RECON ? 2 : 1)) void gin_bwd_k(
             __syncthreads();
             if (w == 0) accWt = mma_tn<TM>(daggT, LDP, sPX, LDP, accWt);
         }
-        if (tile == blockIdx.x) SCGIB_MARK(3);
+        if (tile == blockIdx.x / nsplit) SCGIB_MARK(3);
     }
     // per-workgroup slab
     float *sl = slab + static_cast<int64_t>(blockIdx.x) * SLAB;
@@ -2437,7 +2443,22 @@ extern "C" int scgib_gin_layer_bwd(const float *dy, const float *z2, const float
     return launch_slab_reduce(slab, grid, 64 * 64 + 64 * static_cast<int64_t>(d_in) + 128, wgrad, st);
 }
 
+// workgroups per tile of scgib_mlp2_bwd: 2 for d_in = 128 while the doubled
+// grid fits the chip (the fine-tune MLP's ~13 tiles: each workgroup's dW1 /
+// d(agg) MFMA chain halves, tools/mlp_trace.py), else 1
+static int mlp2_split(int64_t nt, int32_t d_in) {
+    return d_in == 128 && 2 * static_cast<int64_t>(bwd_grid(nt)) <= kCUs ? 2 : 1;
+}
+
 extern "C" int64_t scgib_mlp2_slab_floats(int64_t n_nodes, int32_t d_in) {
+    const int64_t nt = scgib_gin_tiles(n_nodes);
+    return static_cast<int64_t>(bwd_grid(nt)) * mlp2_split(nt, d_in) * (64 * 64 + 64 * d_in + 128);
+}
+
+// the recon heads' backward (scgib_mlp2_recon_bwd / _contrastive_bwd): one
+// slab per tile workgroup, no split (their grid also holds the contrastive
+// workgroups)
+extern "C" int64_t scgib_mlp2_recon_slab_floats(int64_t n_nodes, int32_t d_in) {
     return static_cast<int64_t>(bwd_grid(scgib_gin_tiles(n_nodes))) * (64 * 64 + 64 * d_in + 128);
 }
 
@@ -2463,10 +2484,10 @@ extern "C" int scgib_mlp2_bwd(const float *dout, const float *x, const float *r,
     if (n_nodes <= 0 || (d_in != 64 && d_in != 128)) return SCGIB_EINVAL;
     if (!dout || !x || !r || !w1 || !w2 || !dx || !slab) return SCGIB_EINVAL;
     const int64_t nt = scgib_gin_tiles(n_nodes);
-    const int grid = bwd_grid(nt);
+    const int ns = mlp2_split(nt, d_in), grid = bwd_grid(nt) * ns;
     hipStream_t st = as_stream(stream);
     if (d_in == 128)
-        gin_bwd_k<128, false><<<grid, 256, 0, st>>>(dout, nullptr, r, x, nullptr, nullptr, w1, w2, n_nodes, nt, dx, slab, dims, nullptr, scgib_bn_bwd_pending{}, ReconArgs{});
+        gin_bwd_k<128, false><<<grid, 256, 0, st>>>(dout, nullptr, r, x, nullptr, nullptr, w1, w2, n_nodes, nt, dx, slab, dims, nullptr, scgib_bn_bwd_pending{}, ReconArgs{}, kPreF, nullptr, ns);
     else
         gin_bwd_k<64, false><<<grid, 256, 0, st>>>(dout, nullptr, r, x, nullptr, nullptr, w1, w2, n_nodes, nt, dx, slab, dims, nullptr, scgib_bn_bwd_pending{}, ReconArgs{});
     const int rc = launch_status();

@@ -1823,7 +1823,7 @@ class _Mlp2Recon(torch.autograd.Function):
         g_loss = _f32(g_loss.reshape(1), "g_loss")
         n, d_in = x.shape
         dx = torch.empty_like(x)
-        slab = torch.empty(int(_lib.query("scgib_mlp2_slab_floats", n, d_in)),
+        slab = torch.empty(int(_lib.query("scgib_mlp2_recon_slab_floats", n, d_in)),
                            dtype=torch.float32, device=x.device)
         wg = torch.empty(HIDDEN * HIDDEN + HIDDEN * d_in + 2 * HIDDEN, dtype=torch.float32,
                          device=x.device)
@@ -1895,7 +1895,7 @@ class _Mlp2ReconContrastive(torch.autograd.Function):
         B = z1.shape[0]
         dx = torch.empty_like(x)
         dz1, dz2 = torch.empty_like(z1), torch.empty_like(z2)
-        slab = torch.empty(int(_lib.query("scgib_mlp2_slab_floats", n, d_in)),
+        slab = torch.empty(int(_lib.query("scgib_mlp2_recon_slab_floats", n, d_in)),
                            dtype=torch.float32, device=dev)
         wg = torch.empty(HIDDEN * HIDDEN + HIDDEN * d_in + 2 * HIDDEN, dtype=torch.float32,
                          device=dev)

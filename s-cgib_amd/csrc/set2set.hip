@@ -456,6 +456,20 @@ __global__ __launch_bounds__(256) void set2set_bwd_k(
     __shared__ float sX[kS2SRows * kS2SMaxD], sDX[kS2SRows * kS2SMaxD], sRedA[kS2SRed];
     const int64_t g = blockIdx.x;
     const int tid = threadIdx.x, D2 = 2 * d, G4 = 4 * d, S = s2s_save(d);
+    // a round's saved values this thread reads (its act / c / c_prev slice,
+    // the attention's max and denominator), loaded one round ahead — the last
+    // round's before the staging — so no phase waits on a save load (at the
+    // point of use they were a load round in each round's first phase and cell)
+    struct SvRound {
+        float i, f, gg, o, c, cp, mx, den;
+    };
+    auto sv_load = [&](int t) {
+        const float *sv = save + (g * T + t) * S;
+        const int k = tid < d ? tid : 0;
+        return SvRound{sv[4 * d + k], sv[5 * d + k], sv[6 * d + k], sv[7 * d + k],
+                       sv[8 * d + k], sv[3 * d + k], sv[9 * d], sv[9 * d + 1]};
+    };
+    SvRound cur = sv_load(T - 1);
     const int64_t p0 = ptr[g], p1 = ptr[g + 1];
     const S2SRows X{x, sX, p0, s2s_stage(x, p0, p1, d, sX), d};
     float wT[REG ? kS2SMaxD : 1][3];
@@ -479,23 +493,18 @@ __global__ __launch_bounds__(256) void set2set_bwd_k(
     for (int t = T - 1; t >= 0; --t) {
         const int mk = t == T - 1 ? 2 : 7;  // (trace build: the first two rounds' phases)
         (void)mk;
-        const float *sv = save + (g * T + t) * S;
+        const SvRound nxt = t > 0 ? sv_load(t - 1) : cur;  // in flight through this round
         // h_t (the round's query) = q*_t's first half: the next round's q*_prev,
         // or recomputed for the last round from its saved act / c
-        if (tid < d) {
-            const float c = sv[8 * d + tid];
-            sHq[tid] = sv[7 * d + tid] * tanhf(c);
-        }
+        if (tid < d) sHq[tid] = cur.o * tanhf(cur.c);
         __syncthreads();
         if (t >= T - 2) SCGIB_MARK(mk);
-        s2s_attend_bwd(X, p1, sHq, sDQ + d, sv[9 * d], sv[9 * d + 1], dx, sDX, t < T - 1,
-                           sAtt, sRedA);
+        s2s_attend_bwd(X, p1, sHq, sDQ + d, cur.mx, cur.den, dx, sDX, t < T - 1, sAtt, sRedA);
         __syncthreads();
         if (t >= T - 2) SCGIB_MARK(mk + 1);
         if (tid < d) {  // the cell: dh_t = d q*_t[:d] + the attention's d query + from round t + 1
             const float dh = (sDQ[tid] + sAtt[tid]) + sDH[tid];
-            const float ig = sv[4 * d + tid], fg = sv[5 * d + tid], gg = sv[6 * d + tid],
-                        og = sv[7 * d + tid], c = sv[8 * d + tid], cp = sv[3 * d + tid];
+            const float ig = cur.i, fg = cur.f, gg = cur.gg, og = cur.o, c = cur.c, cp = cur.cp;
             const float tc = tanhf(c);
             const float dc = sDC[tid] + dh * og * (1.f - tc * tc);
             sDG[tid] = dc * gg * ig * (1.f - ig);             // i
@@ -571,6 +580,7 @@ __global__ __launch_bounds__(256) void set2set_bwd_k(
                 sDH[tid - D2] = v;
         }
         __syncthreads();
+        cur = nxt;
     }
     SCGIB_MARK(12);
     for (int i = tid; i < X.ns * d; i += 256) dx[p0 * d + i] = sDX[i];

@@ -82,6 +82,44 @@ __device__ void recon_fin_block(int vb, const ReconFin &a, int64_t ncap, const i
     // Gram chunks over the tile partials
     const int el = tid & 15, sp = tid >> 4;
     double q = 0.0;  // (thread 0) this block's share of ||G||^2, chunks in order
+    if (ntiles >= 8 && ntiles <= 64) {  // block-uniform
+        // few tiles, so each block has up to 32 chunks: each thread owns whole
+        // entries with their tile partials in flight NB at a time, instead of
+        // one chunk per load round trip (B = 32: 29 rounds, 21 us).  The same
+        // sums in the same order as the loop below: partition k = tiles k,
+        // k + 16, k + 32, k + 48 from 0.0, then the 16 partitions in order;
+        // ||G||^2 over (chunk, entry) in order
+        __shared__ double sq[512];
+        const int nent = (kFinBlocks - vb + V - 1) / V * 16;  // <= 32 chunks (V >= 8)
+        auto entries = [&](auto nbc) {
+            constexpr int NB = decltype(nbc)::value;
+            for (int e = tid; e < nent; e += 256) {
+                const int ent = (vb + (e >> 4) * V) * 16 + (e & 15);
+                double p[16];
+#pragma unroll
+                for (int k = 0; k < 16; ++k) p[k] = 0.0;
+                for (int b0 = 0; b0 < ntiles; b0 += NB) {
+                    float v[NB];
+#pragma unroll
+                    for (int b = 0; b < NB; ++b)
+                        v[b] = a.gslab[(b0 + b < ntiles ? b0 + b : 0) * kGram + ent];
+#pragma unroll
+                    for (int b = 0; b < NB; ++b)
+                        if (b0 + b < ntiles) p[b % 16] += static_cast<double>(v[b]);
+                }
+                double g = 0.0;
+#pragma unroll
+                for (int k = 0; k < 16; ++k) g += p[k];
+                a.gram[ent] = static_cast<float>(g);
+                sq[e] = g * g;
+            }
+        };
+        if (ntiles <= 16) entries(std::integral_constant<int, 16>{});
+        else entries(std::integral_constant<int, 32>{});
+        __syncthreads();
+        if (tid == 0)
+            for (int e = 0; e < nent; ++e) q += sq[e];
+    } else
     for (int ch = vb; ch < kFinBlocks; ch += V) {
         const int ent = ch * 16 + el;
         double acc = 0.0;

@@ -225,7 +225,8 @@ def test_egonet_k1_onepass_flags_capacity_overflow(pkg, dev):
 # ---------------------------------------------------------------------------
 # A12: reconstruction loss (Gram form vs dense N x N)
 # ---------------------------------------------------------------------------
-@pytest.mark.parametrize("n_mols", [1, 7, 512])
+# (32 / 80 / 128 molecules: ~10 / ~23 / ~36 tiles, recon_fin.h's few-tile Gram path)
+@pytest.mark.parametrize("n_mols", [1, 7, 32, 80, 128, 512])
 def test_recon_adj_fwd_bwd(pkg, dev, n_mols):
     g, gh = rand_graph(pkg, n_mols, "qm9", 3, dev)
     im = (0.3 * torch.randn(g.num_nodes(), 64, device=dev)).requires_grad_(True)
@@ -524,7 +525,8 @@ def _dense_adj(src, dst, n):
     return a
 
 
-@pytest.mark.parametrize("n_mols,symmetric", [(1, True), (7, True), (512, True), (40, False)])
+@pytest.mark.parametrize("n_mols,symmetric", [(1, True), (7, True), (32, True), (512, True),
+                                              (40, False)])
 def test_mlp2_recon_fused(pkg, dev, n_mols, symmetric):
     if symmetric:
         g, gh = rand_graph(pkg, n_mols, "qm9", 5, dev)
@@ -636,7 +638,7 @@ def test_mlp2_recon_contrastive_fused(pkg, dev, n_mols, n_graphs):
     assert rel_l2(z1a, z1r.grad) < 1e-5 and rel_l2(z2a, z2r.grad) < 1e-5
 
 
-@pytest.mark.parametrize("n_mols", [7, 300, 900, 1100])
+@pytest.mark.parametrize("n_mols", [7, 32, 80, 128, 300, 900, 1100])
 def test_recon_fold_bit_equal(pkg, dev, n_mols):
     """The recon loss finished inside the head MLP launch (the tiles publish
     their Gram partials and output rows, wait for each other, then run

@@ -2,6 +2,7 @@
 
     make -C s-cgib_amd/csrc trace
     SCGIB_LIB=$PWD/s-cgib_amd/libscgib_trace.so python tools/phase_trace.py
+    (PT_BATCH=32: the same step at the fine-tune batch size)
 
 Runs one eager pretrain step of the bench workload on one stream; every
 launch routed through ops._launch is synchronised and its [grid][8] wall-clock
@@ -55,7 +56,8 @@ def main():
     lib.scgib_trace_set.argtypes = [ctypes.c_void_p]
     assert lib.scgib_trace_set(ctypes.c_void_p(buf.data_ptr())) == 0
     F_in = pkg.synth.WORKLOADS["qm9"][2]
-    mols = pkg.synth.molecules(512, "qm9", seed=0)
+    B = int(os.environ.get("PT_BATCH", "512"))  # e.g. 32: the fine-tune batch size
+    mols = pkg.synth.molecules(B, "qm9", seed=0)
     gh, _ = pkg.graph.collate_pyg(mols)
     g = gh.to(dev)
     dict.__setitem__(g.ndata, "x", F.normalize(g.ndata["x"].float()))
@@ -76,7 +78,7 @@ def main():
     for it in range(2):  # second iteration: warm caches / allocator
         recs.clear()
         pkg.ops.OBSERVER = observe if it == 1 else None
-        _, kl, con, rec = model(g, g.ndata["x"], None, None, None, 1, None, 1, dev, 512)
+        _, kl, con, rec = model(g, g.ndata["x"], None, None, None, 1, None, 1, dev, B)
         (kl + con + rec).backward()
         torch.cuda.synchronize()
     pkg.ops.OBSERVER = None

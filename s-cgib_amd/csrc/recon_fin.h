@@ -119,33 +119,34 @@ __device__ void recon_fin_block(int vb, const ReconFin &a, int64_t ncap, const i
         __syncthreads();
         if (tid == 0)
             for (int e = 0; e < nent; ++e) q += sq[e];
-    } else
-    for (int ch = vb; ch < kFinBlocks; ch += V) {
-        const int ent = ch * 16 + el;
-        double acc = 0.0;
-        for (int64_t b0 = sp; b0 < ntiles; b0 += 16 * 8) {
-            float v[8];
+    } else {  // one chunk at a time, 16 partitions x 8 tile loads in flight
+        for (int ch = vb; ch < kFinBlocks; ch += V) {
+            const int ent = ch * 16 + el;
+            double acc = 0.0;
+            for (int64_t b0 = sp; b0 < ntiles; b0 += 16 * 8) {
+                float v[8];
 #pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                const int64_t b = b0 + 16 * j < ntiles ? b0 + 16 * j : sp;  // clamped: unconditional
-                v[j] = a.gslab[b * kGram + ent];
+                for (int j = 0; j < 8; ++j) {
+                    const int64_t b = b0 + 16 * j < ntiles ? b0 + 16 * j : sp;  // clamped: unconditional
+                    v[j] = a.gslab[b * kGram + ent];
+                }
+#pragma unroll
+                for (int j = 0; j < 8; ++j)
+                    if (b0 + 16 * j < ntiles) acc += static_cast<double>(v[j]);
             }
+            part[sp][el] = acc;
+            __syncthreads();
+            if (tid < 16) {
+                double g = 0.0;
 #pragma unroll
-            for (int j = 0; j < 8; ++j)
-                if (b0 + 16 * j < ntiles) acc += static_cast<double>(v[j]);
+                for (int k = 0; k < 16; ++k) g += part[k][tid];
+                a.gram[ch * 16 + tid] = static_cast<float>(g);
+                red[tid] = g * g;
+            }
+            __syncthreads();
+            if (tid == 0)
+                for (int k = 0; k < 16; ++k) q += red[k];
         }
-        part[sp][el] = acc;
-        __syncthreads();
-        if (tid < 16) {
-            double g = 0.0;
-#pragma unroll
-            for (int k = 0; k < 16; ++k) g += part[k][tid];
-            a.gram[ch * 16 + tid] = static_cast<float>(g);
-            red[tid] = g * g;
-        }
-        __syncthreads();
-        if (tid == 0)
-            for (int k = 0; k < 16; ++k) q += red[k];
     }
     SCGIB_MARK(9);
     for (int off = 128; off >= 1; off >>= 1) {

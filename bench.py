@@ -43,17 +43,21 @@ F32_MFMA_PEAK_TFLOPS = 157.3  # dense fp32 MFMA (MI355X_MICROARCH.md)
 # without an entry there is reported with traffic null and a traffic_note.
 TRAFFIC_FILE = os.environ.get("SCGIB_TRAFFIC_FILE",
                               os.path.join(ROOT, "profiles", "traffic_current.json"))
+# the same passes over the fine-tune step (bench.py --finetune molhiv)
+FT_TRAFFIC_FILE = os.environ.get("SCGIB_FT_TRAFFIC_FILE",
+                                 os.path.join(ROOT, "profiles", "traffic_finetune_current.json"))
 
 
-def _traffic():
+def _load_json(path):
     try:
-        with open(TRAFFIC_FILE) as fh:
+        with open(path) as fh:
             return json.load(fh)
     except (OSError, ValueError):
         return {}
 
 
-TRAFFIC = _traffic()
+TRAFFIC_SETS = [(TRAFFIC_FILE, _load_json(TRAFFIC_FILE)),
+                (FT_TRAFFIC_FILE, _load_json(FT_TRAFFIC_FILE))]
 RUN_CONFIG = None  # {"workload", "batch", "k"} of this run (main)
 # Replay-derived launch times: the same bench command traced by rocprofv3
 # (tools/gpu_round.sh: kernel_instances.py --json over the replayed steps of
@@ -62,6 +66,19 @@ RUN_CONFIG = None  # {"workload", "batch", "k"} of this run (main)
 # other encoder chain.
 REPLAY_FILE = os.environ.get("SCGIB_REPLAY_FILE",
                              os.path.join(ROOT, "profiles", "replay_current.json"))
+FT_REPLAY_FILE = os.environ.get("SCGIB_FT_REPLAY_FILE",
+                                os.path.join(ROOT, "profiles", "replay_finetune_current.json"))
+REPLAY_SETS = [(REPLAY_FILE, _load_json(REPLAY_FILE)),
+               (FT_REPLAY_FILE, _load_json(FT_REPLAY_FILE))]
+
+
+def _for_run(sets):
+    """(path, data) of the evidence file measured on this run's
+    configuration; the first file (for its note) when none is."""
+    for path, data in sets:
+        if data.get("_config") == RUN_CONFIG:
+            return path, data
+    return sets[0]
 
 
 SB_FILE = os.environ.get("SCGIB_SB_EVIDENCE_FILE") or os.path.join(
@@ -78,24 +95,14 @@ def _sb_evidence():
         return {}
 
 
-def _replay():
-    try:
-        with open(REPLAY_FILE) as fh:
-            return json.load(fh)
-    except (OSError, ValueError):
-        return {}
-
-
-REPLAY = _replay()
-
-
 def replay_of(variants):
     """(dispatches, dispatch-weighted mean duration in us) of the replayed
     launches whose kernel names start with one of ``variants``; None when the
     file is of another configuration or holds none."""
-    if REPLAY.get("_config") != RUN_CONFIG:
+    _, rep = _for_run(REPLAY_SETS)
+    if rep.get("_config") != RUN_CONFIG:
         return None
-    got = [v for k, v in REPLAY.get("kernels", {}).items() if any(k.startswith(p) for p in variants)]
+    got = [v for k, v in rep.get("kernels", {}).items() if any(k.startswith(p) for p in variants)]
     n = sum(g["dispatches"] for g in got)
     if not n:
         return None
@@ -106,10 +113,11 @@ def traffic_of(variants):
     """Dispatch-weighted mean HBM bytes per launch over the template
     instantiations whose names start with one of ``variants`` (e.g. the GIN
     variants of gin_bwd_k, not the MLP one); None when none is in the file."""
-    cfg = TRAFFIC.get("_config")
+    _, tr = _for_run(TRAFFIC_SETS)
+    cfg = tr.get("_config")
     if cfg is not None and cfg != RUN_CONFIG:
         return None  # measured on another configuration
-    got = [t for k, t in TRAFFIC.items()
+    got = [t for k, t in tr.items()
            if not k.startswith("_") and any(k.startswith(v) for v in variants)]
     n = sum(g["dispatches"] for g in got)
     if not n:
@@ -291,9 +299,11 @@ def roofline_entry(kernel, desc, r, variants):
     else:
         bound, ach, peak, unit = "hbm", r["gbs"], HBM_PEAK_GBS, "GB/s"
     traffic = traffic_of(variants)
+    t_path, t_data = _for_run(TRAFFIC_SETS)
+    r_path, _ = _for_run(REPLAY_SETS)
     out = {"bound": bound, "kernel": kernel, "kernel_desc": desc, "achieved": round(ach, 2),
            "peak": peak, "unit": unit, "frac": round(ach / peak, 4), "traffic": traffic,
-           "traffic_file": os.path.relpath(TRAFFIC_FILE, ROOT),
+           "traffic_file": os.path.relpath(t_path, ROOT),
            "hbm_gbs": round(r["gbs"], 1), "hbm_frac": round(r["hbm_frac"], 4),
            "hbm_frac_vs_measured_copy": round(r["gbs"] / HBM_MEASURED_GBS, 4),
            "mfma_f32_tflops": round(r["tflops"], 2), "mfma_frac": round(r["mfma_frac"], 4),
@@ -303,7 +313,7 @@ def roofline_entry(kernel, desc, r, variants):
            "avg_bytes_per_launch": int(r["avg_bytes"]),
            "avg_flops_per_launch": int(r["avg_flops"]), "launches_timed": r["launches"]}
     rep = replay_of(variants)
-    out["replay_file"] = os.path.relpath(REPLAY_FILE, ROOT)
+    out["replay_file"] = os.path.relpath(r_path, ROOT)
     if rep is None:
         out["replay_avg_us"] = out["replay_frac"] = None
         out["replay_note"] = (f"no replayed-step trace of {RUN_CONFIG} for {variants} in "
@@ -316,7 +326,7 @@ def roofline_entry(kernel, desc, r, variants):
         out["replay_dispatches"] = d
         out["replay_frac"] = round(rate / peak, 4)  # same bytes / flops, replayed launch time
     if traffic is None:
-        cfg = TRAFFIC.get("_config")
+        cfg = t_data.get("_config")
         out["traffic_note"] = (
             f"{out['traffic_file']} holds PMC passes of {cfg}, not of this configuration "
             f"{RUN_CONFIG}" if cfg is not None and cfg != RUN_CONFIG else
@@ -460,7 +470,9 @@ def progress(msg):
 # CPU legs run in child processes (a fresh OpenMP pool per thread count, and
 # a leg that cannot finish — e.g. hundreds of threads on a small CPU share —
 # is stopped at its time limit and reported as such)
-LEG_TIMEOUT = {"all_affinity": 120.0, "share": 120.0, "one_core": 150.0}
+LEG_TIMEOUT = {"all_affinity": 150.0, "share": 120.0, "one_core": 150.0}
+# BASELINE.md §2's protocol: 3 warm-up steps, then the median of >= 10
+CPU_WARMUP, CPU_MIN_STEPS = 3, 10
 
 
 def _run_leg(name, spec):
@@ -503,11 +515,10 @@ def cpu_baselines(k, gin_layers, workload, batch, seconds=20.0):
         affinity = os.cpu_count() or threads
     leg = max(seconds / 2, 5.0)
     legs = {}
-    for name, nt, warm, mins in (("all_affinity", affinity, 2, 5), ("share", threads, 2, 5),
-                                 ("one_core", 1, 1, 3)):
+    for name, nt in (("all_affinity", affinity), ("share", threads), ("one_core", 1)):
         legs[name] = _run_leg(name, {"threads": nt, "k": k, "gin_layers": gin_layers,
                                      "workload": workload, "batch": batch, "seconds": leg,
-                                     "warmup": warm, "min_steps": mins})
+                                     "warmup": CPU_WARMUP, "min_steps": CPU_MIN_STEPS})
     done = {k: v for k, v in legs.items() if v is not None}
     if not done:
         return None
@@ -547,8 +558,8 @@ def _cpu_leg_main(spec_json):
     print(json.dumps(r), flush=True)
 
 
-def cpu_baseline(pool_host, k, gin_layers, F_in, workload, seconds=20.0, warmup=1,
-                 min_steps=2):
+def cpu_baseline(pool_host, k, gin_layers, F_in, workload, seconds=20.0, warmup=CPU_WARMUP,
+                 min_steps=CPU_MIN_STEPS):
     """The oracle (literal restatement of the reference's CPU path: per-graph
     loops, dense N x N recon) timed on this host's cores, bounded sample."""
     from oracle import egonet
@@ -628,7 +639,143 @@ def finetune_leg(a, dev):
     finally:
         RUN_CONFIG = keep
     return {k: line[k] for k in ("metric", "value", "unit", "ms_per_step", "steps", "warmup",
-                                 "dtype", "data", "config", "roofline", "cpu_baseline")}
+                                 "dtype", "data", "config", "roofline", "critical_path_us",
+                                 "cpu_baseline")}
+
+
+def build_replay_step(model, opt, pool_host, k, batch, dev, prefetch=True, noise=None,
+                      collective=False, reducer=None, warm=3):
+    """The bench's pretrain step (exp_pretraining.py:290-333) as ONE captured
+    HIP graph in capacity mode: the pool's next resident batch (and the ego-nets
+    the previous step built for it) loaded inside the graph, forward, backward,
+    [the RCCL all-reduce of the gradient bucket,] Adam.  ``warm`` eager steps
+    on a side stream first (allocator, Adam state, RCCL communicator).
+    ``noise`` = (u_gate [n_cap], u_feat [n_cap, 64]) static device buffers the
+    step reads instead of drawing its own (tests/test_gpu_trajectory.py fills
+    them before each replay); None = the device Philox draws of every replay.
+    Returns step(i), the static losses (kl, rec, con), the static batch, the
+    device pool and its prefetch, the all-reduce mode and the node count of
+    the captured graph."""
+    n_cap, e_cap, mgn, ego_caps = pkg.graph.StaticBatch.capacities(pool_host, k, slack=1.02)
+    F_in = pool_host[0].ndata["x"].shape[1]
+    static = pkg.graph.StaticBatch(batch, n_cap, e_cap, F_in, mgn, ego_caps, dev, k=k)
+    padded = []
+    for gh in pool_host:
+        gx = pkg.graph.GraphBatch.from_edges(*[t.numpy() for t in gh.edges()], gh.num_nodes(),
+                                             True, gh.batch_num_nodes_host())
+        dict.__setitem__(gx.ndata, "x", F.normalize(gh.ndata["x"].float()))
+        padded.append(static.pad(gx))
+
+    pool_dev = static.pool(padded)
+    one = torch.ones((), dtype=torch.float32, device=dev)
+    # each step builds the NEXT batch's ego-nets (on the encoder
+    # pair's queue during the loss section) and its batch load moves them
+    # in with the batch: the build leaves the head of the critical path
+    pf = None
+    if prefetch:
+        pf = pkg.graph.EgoPrefetch(static, pool_dev)
+        pf.prime()  # the first batch's, before the first load
+
+    def body():
+        # the pool's next batch (and its prefetched ego-nets) into the static inputs
+        pkg.ops.stamp("step_start")
+        static.load_next(pool_dev, pf)
+        pkg.ops.stamp("loaded")
+        _, kl, con, rec = model(static.graph, static.x, None, None, None, 1, None, k, dev,
+                                batch, noise=noise)
+        # loss = KL + contrastive + recon (exp_pretraining.py:321): d loss / d part = 1,
+        # so the parts are backpropagated directly with a resident ones scalar (no sum
+        # kernels, no ones fill in the replayed step); the total is formed after timing
+        torch.autograd.backward((kl, rec, con), (one, one, one))
+        if pf is not None:
+            pf.join()  # (no-op: the encoder pair's backward joined it)
+        # detached aliases (the replays refresh their storage): the step's
+        # autograd graph is not kept alive past the capture
+        return (kl.detach(), rec.detach(), con.detach())
+
+    def bucket():
+        reducer.pack()
+        reducer.reduce(force=True)
+        reducer.unpack()
+
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):  # warm-up (allocator, Adam state, RCCL comm) off the capture
+        for i in range(warm):
+            opt.zero_grad(set_to_none=True)
+            body()
+            if collective:
+                bucket()
+            opt.step()
+    torch.cuda.current_stream().wait_stream(side)
+    torch.cuda.synchronize()
+    graph2 = None
+    if os.environ.get("SCGIB_STAMPS"):  # diagnostics: wall-clock stamps in the captured step
+        pkg.ops.stamps_enable(dev, int(os.environ["SCGIB_STAMPS"]))
+    # keep_graph: the captured graph stays queryable for its node count
+    # (graph_node_counts) and is instantiated explicitly below
+    graph = torch.cuda.CUDAGraph(keep_graph=True)
+    opt.zero_grad(set_to_none=True)
+    # N > 1: the RCCL all-reduce captured inside the replayed step graph
+    # (falls back to the all-reduce between two replays if the capture raises)
+    capture_ok = dist.is_initialized() and dist.get_backend() == "nccl"
+    allreduce_mode = None
+    if collective and capture_ok:  # (gloo's all-reduce is a host round trip: not capturable)
+        # the whole step incl. the RCCL all-reduce of the bucket in ONE graph:
+        # no host enqueue between the backward and the optimizer step
+        try:
+            # thread_local: the process group's watchdog thread queries the
+            # warm-up all-reduce's event while this thread captures; under
+            # the default global mode that query invalidates the capture
+            with torch.cuda.graph(graph, capture_error_mode="thread_local"):
+                static_loss = body()
+                bucket()
+                opt.step()
+            allreduce_mode = "captured in the step graph"
+        except Exception as exc:  # RCCL without graph-capture support: two graphs
+            print(f"bench: all-reduce capture failed ({exc!r}); two-graph fallback",
+                  file=sys.stderr, flush=True)
+            torch.cuda.synchronize()
+            graph = torch.cuda.CUDAGraph(keep_graph=True)
+            opt.zero_grad(set_to_none=True)
+            graph2 = "fallback"
+    if not collective:
+        with torch.cuda.graph(graph):
+            static_loss = body()
+            opt.step()
+    elif graph2 is not None or not capture_ok:
+        with torch.cuda.graph(graph):  # gradients -> the flat bucket, one launch
+            static_loss = body()
+            reducer.pack()
+        graph2 = torch.cuda.CUDAGraph()  # 1/world unpack + Adam, after the all-reduce
+        with torch.cuda.graph(graph2):
+            reducer.unpack()
+            opt.step()
+        allreduce_mode = "between two graph replays"
+    nodes = graph_node_counts(graph)
+    graph.instantiate()
+
+    def step(i):
+        graph.replay()
+        if graph2 is not None:  # RCCL all-reduce of the bucket between the two replays
+            reducer.reduce(force=True)
+            graph2.replay()
+        return static_loss
+
+    return SimpleNamespace(step=step, loss=static_loss, static=static, pool=pool_dev,
+                           padded=padded, prefetch=pf, allreduce_mode=allreduce_mode,
+                           graph=graph, graph_nodes=nodes)
+
+
+def graph_node_counts(graph):
+    """{kernel, memcpy, memset, other, total} nodes of a captured torch
+    CUDAGraph (hipGraphGetNodes + hipGraphNodeGetType through ops), or None
+    where the runtime does not expose the graph."""
+    try:
+        return pkg.ops.graph_node_counts(graph)
+    except Exception as exc:  # noqa: BLE001 (diagnostic field only)
+        progress(f"graph node count unavailable: {exc!r}")
+        return None
 
 
 def main():
@@ -713,9 +860,8 @@ def main():
     xq_env = dict(os.environ)
     xq_env.setdefault("LOCAL_WORLD_SIZE", str(world))
     xq_ok, xq_why = pkg.ops.handoff_rule(torch.cuda.device_count(), xq_env)
-    if not xq_ok:
-        pkg.ops.XQ_FLAGS, pkg.ops.XQ_REASON = False, xq_why
-    elif a.no_handoffs:
+    pkg.ops.XQ_FLAGS, pkg.ops.XQ_REASON = xq_ok, xq_why
+    if xq_ok and a.no_handoffs:
         pkg.ops.XQ_FLAGS, pkg.ops.XQ_REASON = False, "--no-handoffs"
     torch.manual_seed(1234 + rank)
     global RUN_CONFIG
@@ -739,6 +885,7 @@ def main():
     # gradients + the BN running statistics, averaged in one bucket per step
     reducer = pkg.dist.GradAllReducer(model.parameters(), buffers=pkg.dist.bn_buffers(model))
 
+    graph_nodes = None
     if a.eager:
         opt = (torch.optim.Adam(model.parameters(), lr=1e-4, weight_decay=5e-5, fused=True)
                if a.torch_adam else pkg.optim.Adam(model.parameters(), lr=1e-4, weight_decay=5e-5))
@@ -756,116 +903,15 @@ def main():
             opt.step()
             return loss
     else:
-        # capacity mode + HIP graph: one capture of (batch load, ego build,
-        # forward, backward[, Adam]) on static buffers; each replay copies the
-        # pool's next resident batch in (one kernel inside the graph:
-        # StaticBatch.load_next) and steps on it.  Every kernel reads the
-        # batch's actual sizes from the device.
         if a.torch_adam:
             opt = torch.optim.Adam(model.parameters(), lr=1e-4, weight_decay=5e-5,
                                    capturable=True, fused=True)
         else:  # one-launch device Adam, same arithmetic (tests/test_gpu_optim.py)
             opt = pkg.optim.Adam(model.parameters(), lr=1e-4, weight_decay=5e-5)
-        n_cap, e_cap, mgn, ego_caps = pkg.graph.StaticBatch.capacities(pool_host, a.k, slack=1.02)
-        static = pkg.graph.StaticBatch(a.batch, n_cap, e_cap, F_in, mgn, ego_caps, dev, k=a.k)
-        padded = []
-        for gh in pool_host:
-            gx = pkg.graph.GraphBatch.from_edges(*[t.numpy() for t in gh.edges()], gh.num_nodes(),
-                                                 True, gh.batch_num_nodes_host())
-            dict.__setitem__(gx.ndata, "x", F.normalize(gh.ndata["x"].float()))
-            padded.append(static.pad(gx))
-
-        pool_dev = static.pool(padded)
-        one = torch.ones((), dtype=torch.float32, device=dev)
-        # each step builds the NEXT batch's ego-nets (on the encoder
-        # pair's queue during the loss section) and its batch load moves them
-        # in with the batch: the build leaves the head of the critical path
-        prefetch = None
-        if not a.no_ego_prefetch:
-            prefetch = pkg.graph.EgoPrefetch(static, pool_dev)
-            prefetch.prime()  # the first batch's, before the first load
-
-        def body():
-            # the pool's next batch (and its prefetched ego-nets) into the static inputs
-            pkg.ops.stamp("step_start")
-            static.load_next(pool_dev, prefetch)
-            pkg.ops.stamp("loaded")
-            _, kl, con, rec = model(static.graph, static.x, None, None, None, 1, None, a.k, dev,
-                                    a.batch)
-            # loss = KL + contrastive + recon (exp_pretraining.py:321): d loss / d part = 1,
-            # so the parts are backpropagated directly with a resident ones scalar (no sum
-            # kernels, no ones fill in the replayed step); the total is formed after timing
-            torch.autograd.backward((kl, rec, con), (one, one, one))
-            if prefetch is not None:
-                prefetch.join()  # (no-op: the encoder pair's backward joined it)
-            out = (kl.detach(), rec.detach(), con.detach())
-            # detached aliases (the replays refresh their storage): the step's
-            # autograd graph is not kept alive past the capture
-            return out
-
-        side = torch.cuda.Stream()
-        side.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(side):  # warm-up (allocator, Adam state, RCCL comm) off the capture
-            for i in range(3):
-                opt.zero_grad(set_to_none=True)
-                body()
-                if collective:
-                    reducer.pack()
-                    reducer.reduce(force=True)
-                    reducer.unpack()
-                opt.step()
-        torch.cuda.current_stream().wait_stream(side)
-        torch.cuda.synchronize()
-        graph2 = None
-        if os.environ.get("SCGIB_STAMPS"):  # diagnostics: wall-clock stamps in the captured step
-            pkg.ops.stamps_enable(dev, int(os.environ["SCGIB_STAMPS"]))
-        graph = torch.cuda.CUDAGraph()
-        opt.zero_grad(set_to_none=True)
-        # N > 1: the RCCL all-reduce captured inside the replayed step graph
-        # (falls back to the all-reduce between two replays if the capture raises)
-        capture_ok = dist.is_initialized() and dist.get_backend() == "nccl"
-        if collective and capture_ok:  # (gloo's all-reduce is a host round trip: not capturable)
-            # the whole step incl. the RCCL all-reduce of the bucket in ONE graph:
-            # no host enqueue between the backward and the optimizer step
-            try:
-                # thread_local: the process group's watchdog thread queries the
-                # warm-up all-reduce's event while this thread captures; under
-                # the default global mode that query invalidates the capture
-                with torch.cuda.graph(graph, capture_error_mode="thread_local"):
-                    static_loss = body()
-                    reducer.pack()
-                    reducer.reduce(force=True)
-                    reducer.unpack()
-                    opt.step()
-                allreduce_mode = "captured in the step graph"
-            except Exception as exc:  # RCCL without graph-capture support: two graphs
-                print(f"bench: all-reduce capture failed ({exc!r}); two-graph fallback",
-                      file=sys.stderr, flush=True)
-                torch.cuda.synchronize()
-                graph = torch.cuda.CUDAGraph()
-                opt.zero_grad(set_to_none=True)
-                graph2 = "fallback"
-        if not collective:
-            with torch.cuda.graph(graph):
-                static_loss = body()
-                opt.step()
-            allreduce_mode = None
-        elif graph2 is not None or not capture_ok:
-            with torch.cuda.graph(graph):  # gradients -> the flat bucket, one launch
-                static_loss = body()
-                reducer.pack()
-            graph2 = torch.cuda.CUDAGraph()  # 1/world unpack + Adam, after the all-reduce
-            with torch.cuda.graph(graph2):
-                reducer.unpack()
-                opt.step()
-            allreduce_mode = "between two graph replays"
-
-        def step(i):
-            graph.replay()
-            if graph2 is not None:  # RCCL all-reduce of the bucket between the two replays
-                reducer.reduce(force=True)
-                graph2.replay()
-            return static_loss
+        rs = build_replay_step(model, opt, pool_host, a.k, a.batch, dev,
+                               prefetch=not a.no_ego_prefetch, collective=collective,
+                               reducer=reducer)
+        step, allreduce_mode, graph_nodes = rs.step, rs.allreduce_mode, rs.graph_nodes
 
     for i in range(a.warmup):
         step(i)
@@ -998,9 +1044,13 @@ def main():
                                      and not a.no_ego_prefetch else "at the head of the step"),
                        "allreduce": None if not collective else
                        ("eager" if a.eager else allreduce_mode),
-                       "handoffs": ("signal / wait kernels" if pkg.ops.XQ_FLAGS else
+                       "handoffs": ("signal / wait kernels" if pkg.ops.xq_enabled() else
                                     f"stream edges ({pkg.ops.XQ_REASON})"),
                        "global_batch": world * a.batch, "nodes_per_batch": round(n_nodes, 1),
+                       # the replayed step graph's nodes by kind (each is host
+                       # enqueue work) and the host's enqueue time per timed step
+                       "graph_nodes": graph_nodes,
+                       "host_enqueue_ms": round(t_enq / a.steps * 1e3, 4),
                        "parallelism": f"dp{world}", "final_loss": round(final_loss, 4),
                        "replica_max_abs_diff": replica_diff,
                        "bn_semantics": ("single rank: BatchNorm statistics over the whole batch"

@@ -51,10 +51,15 @@ def _linear(x, p, name, bias=True):
     return F.linear(x, w, b)
 
 
-def _batchnorm_train(x, p, name, buffers):
+def _batchnorm_train(x, p, name, buffers, training=True):
     """nn.BatchNorm1d in train mode (torch's own batch_norm kernel, as the
     reference): batch stats for the output, unbiased var into the running
-    estimate, momentum 0.1, eps 1e-5."""
+    estimate, momentum 0.1, eps 1e-5.  training False: eval mode (the running
+    estimates normalise, nothing is updated), as evaluate_network's
+    model.eval() (train_molhiv.py:161-162) runs every BatchNorm."""
+    if not training:
+        return F.batch_norm(x, buffers[name + ".running_mean"], buffers[name + ".running_var"],
+                            p[name + ".weight"], p[name + ".bias"], False, BN_MOMENTUM, BN_EPS)
     if x.shape[0] <= 1:
         raise ValueError("Expected more than 1 value per channel when training")
     if buffers is not None:
@@ -76,7 +81,8 @@ def _relu(x, mask, tie):
     return torch.where(amb, x * mask.to(x.dtype), F.relu(x))
 
 
-def gin_encoder(p, prefix, src, dst, h, buffers, num_layers, relu_masks=None, tie=1e-5):
+def gin_encoder(p, prefix, src, dst, h, buffers, num_layers, relu_masks=None, tie=1e-5,
+                training=True):
     """GIN.forward with DGL GINConv semantics (sum aggregation, (1+eps)*h).
     relu_masks (test use): per layer (hidden ReLU mask, output ReLU mask) of
     the fp32 implementation under test, applied only at pre-activations
@@ -90,7 +96,7 @@ def gin_encoder(p, prefix, src, dst, h, buffers, num_layers, relu_masks=None, ti
         m1, m2 = relu_masks[i] if relu_masks is not None else (None, None)
         z = _relu(_linear(rst, p, lp + ".apply_func.mlp.0"), m1, tie)
         z = _linear(z, p, lp + ".apply_func.mlp.2")
-        z = _batchnorm_train(z, p, f"{prefix}.batch_norms.{i}", buffers)
+        z = _batchnorm_train(z, p, f"{prefix}.batch_norms.{i}", buffers, training)
         h = _relu(z, m2, tie)
     return h
 
@@ -107,7 +113,7 @@ def sum_nodes(x, counts):
     return torch.zeros(len(counts), x.shape[1], dtype=x.dtype).index_add(0, seg, x)
 
 
-def compression(p, graph_features, counts, u_gate, u_feat, buffers):
+def compression(p, graph_features, counts, u_gate, u_feat, buffers, training=True):
     """Per-graph loop of models.py:631-660 with explicit noise."""
     noisy_all, p_all, kl_all = [], [], None
     off = 0
@@ -115,7 +121,7 @@ def compression(p, graph_features, counts, u_gate, u_feat, buffers):
         feats = graph_features[off:off + n_i]
         # compress(): compressor = Linear-BN-ReLU-Linear (models.py:589-596)
         t = _linear(feats, p, "compressor.0")
-        t = _batchnorm_train(t, p, "compressor.1", buffers)
+        t = _batchnorm_train(t, p, "compressor.1", buffers, training)
         pv = _linear(F.relu(t), p, "compressor.3")
         bias = 0.0 + 0.0001
         eps = (bias - (1 - bias)) * u_gate[off:off + n_i].reshape(-1, 1) + (1 - bias)
@@ -184,12 +190,12 @@ def recon_logm(im, logms, counts, kstep):
     return loss / kstep
 
 
-def extract_features(p, batch, ego, h0, hs0, u_gate, u_feat, buffers):
+def extract_features(p, batch, ego, h0, hs0, u_gate, u_feat, buffers, training=True):
     L = num_gin_layers(p)
-    gf = gin_encoder(p, "Encoder1", batch["src"], batch["dst"], h0, buffers, L)
-    sf = gin_encoder(p, "Encoder2", ego["src"], ego["dst"], hs0, buffers, L)
+    gf = gin_encoder(p, "Encoder1", batch["src"], batch["dst"], h0, buffers, L, training=training)
+    sf = gin_encoder(p, "Encoder2", ego["src"], ego["dst"], hs0, buffers, L, training=training)
     readout = sum_nodes(gf, batch["counts"])
-    noisy, _, kl_tensor = compression(p, gf, batch["counts"], u_gate, u_feat, buffers)
+    noisy, _, kl_tensor = compression(p, gf, batch["counts"], u_gate, u_feat, buffers, training)
     sub_readout = sum_nodes(sf, ego["counts"])
     im = attention(p, noisy, sub_readout, batch["counts"])
     return {"graph_features": gf, "subgraph_features": sf, "graph_readout": readout,
@@ -288,16 +294,20 @@ def domainadapt_forward(p, batch, ego, x, x_subs, u_gate, u_feat, buffers=None):
     return torch.sum((rec - org) ** 2)
 
 
-def finetune_forward(p, batch, ego, x, x_subs, u_gate, u_feat, dataset, buffers=None):
+def finetune_forward(p, batch, ego, x, x_subs, u_gate, u_feat, dataset, buffers=None,
+                     training=True):
     """Mainmodel_finetuning.forward: own transfer_d -> the pretrained model's
     extract_features (its wrapper-level encoders, "model." prefix) -> own MLP
-    -> Set2Set -> predict -> sigmoid (unless a regression dataset)."""
+    -> Set2Set -> predict -> sigmoid (unless a regression dataset).  training
+    False: evaluate_network's eval mode (train_molhiv.py:161-193) — every
+    BatchNorm on its running estimates; the compression noise is still drawn
+    (models.py:650 does not look at self.training)."""
     h0 = _linear(x, p, "transfer_d", bias=False)
     hs0 = _linear(x_subs, p, "transfer_d", bias=False)
     pre = {k[6:]: v for k, v in p.items() if k.startswith("model.")}
     bufs = None if buffers is None else {k[6:]: v for k, v in buffers.items()
                                          if k.startswith("model.")}
-    acts = extract_features(pre, batch, ego, h0, hs0, u_gate, u_feat, bufs)
+    acts = extract_features(pre, batch, ego, h0, hs0, u_gate, u_feat, bufs, training)
     im = _linear(F.relu(_linear(acts["interaction_map"], p, "MLP.0")), p, "MLP.2")
     g = set2set(p, "s2s", im, batch["counts"])
     scores = _linear(F.relu(_linear(g, p, "predict.0")), p, "predict.2")

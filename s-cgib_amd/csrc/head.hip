@@ -393,8 +393,17 @@ extern "C" int scgib_head_bwd(const float *x, const float *hid, const float *out
                               const float *w2, int32_t n_out, int32_t sigmoid, float *dx,
                               float *dw1, float *db1, float *dw2, float *db2,
                               scgib_stream_t stream) {
-    if (n_rows < 1 || k_in < 1 || k_in > kHeadKMax || n_out < 1 || n_out > kHeadCMax)
+    if (n_rows < 0 || k_in < 1 || k_in > kHeadKMax || n_out < 1 || n_out > kHeadCMax)
         return SCGIB_EINVAL;
+    if (n_rows == 0) {  // an empty batch (the forward accepted it): zero weight gradients
+        if (!dw1 || !db1 || !dw2 || !db2) return SCGIB_EINVAL;
+        hipStream_t st = as_stream(stream);
+        hipError_t e = hipMemsetAsync(dw1, 0, sizeof(float) * kHeadH * k_in, st);
+        if (e == hipSuccess) e = hipMemsetAsync(db1, 0, sizeof(float) * kHeadH, st);
+        if (e == hipSuccess) e = hipMemsetAsync(dw2, 0, sizeof(float) * kHeadH * n_out, st);
+        if (e == hipSuccess) e = hipMemsetAsync(db2, 0, sizeof(float) * n_out, st);
+        return e == hipSuccess ? SCGIB_OK : static_cast<int>(e);
+    }
     if (!x || !hid || !out || !d_out || !w1 || !w2 || !dx || !dw1 || !db1 || !dw2 || !db2)
         return SCGIB_EINVAL;
     if (k_in % 4 || !head_aligned(x) || !head_aligned(w1) || !head_aligned(hid))

@@ -103,7 +103,9 @@ __device__ __forceinline__ int s2s_stage(const float *__restrict__ x, int64_t p0
                                          int d, float *xs) {
     const int ns = static_cast<int>(p1 - p0 < kS2SRows ? p1 - p0 : kS2SRows);
     const int tid = threadIdx.x, total = ns * d;
-    if ((d & 3) == 0) {  // rows 16-B aligned (row r at r d floats)
+    // float4 staging needs 16-B aligned rows: d % 4 == 0 AND a 16-B aligned
+    // base (a tensor view with a storage offset may not be): else scalar loads
+    if ((d & 3) == 0 && (reinterpret_cast<uintptr_t>(x) & 15) == 0) {
         constexpr int K = kS2SRows * kS2SMaxD / 4 / 256;
         const float4 *x4 = reinterpret_cast<const float4 *>(x + p0 * d);
         float4 *xs4 = reinterpret_cast<float4 *>(xs);

@@ -423,6 +423,34 @@ def stamps_read():
                   key=lambda e: e[1])
 
 
+# hipGraphNodeType (hip_runtime_api.h): the node kinds a replayed step holds
+_NODE_TYPES = {0: "kernel", 1: "memcpy", 2: "memset", 5: "empty", 6: "wait_event",
+               7: "event_record"}
+
+
+def graph_node_counts(graph):
+    """Nodes of a captured torch CUDAGraph made with keep_graph=True, by
+    hipGraphNodeType ({"kernel": .., "memcpy": .., "memset": .., ..., "total"}):
+    each node of a replayed graph is host enqueue work (~1.6 us
+    per node), so this is the step's launch-overhead count."""
+    hip = ctypes.CDLL("libamdhip64.so")
+    g = ctypes.c_void_p(graph.raw_cuda_graph())
+    n = ctypes.c_size_t(0)
+    if hip.hipGraphGetNodes(g, None, ctypes.byref(n)) != 0:
+        raise _lib.ScgibError("hipGraphGetNodes failed")
+    nodes = (ctypes.c_void_p * max(n.value, 1))()
+    if hip.hipGraphGetNodes(g, nodes, ctypes.byref(n)) != 0:
+        raise _lib.ScgibError("hipGraphGetNodes failed")
+    out = {"total": int(n.value)}
+    t = ctypes.c_int(0)
+    for i in range(n.value):
+        if hip.hipGraphNodeGetType(ctypes.c_void_p(nodes[i]), ctypes.byref(t)) != 0:
+            raise _lib.ScgibError("hipGraphNodeGetType failed")
+        key = _NODE_TYPES.get(t.value, f"type{t.value}")
+        out[key] = out.get(key, 0) + 1
+    return out
+
+
 def _reduce_jobs(jobs, st, max_wg=0):
     cap = int(_lib.query("scgib_slab_reduce_max_jobs"))
     for i0 in range(0, len(jobs), cap):
@@ -854,7 +882,21 @@ def handoff_rule(device_count=None, env=None):
     return True, f"{hw} hardware queues per process, graph branches on distinct streams"
 
 
-XQ_FLAGS, XQ_REASON = handoff_rule()
+# None: resolved on first use by xq_enabled() — with the local device count,
+# so that ranks sharing a GPU (LOCAL_WORLD_SIZE > devices) get stream edges
+# whatever entry point they came in by; True / False set by a caller (bench
+# --no-handoffs, tests) stands
+XQ_FLAGS, XQ_REASON = None, "not resolved yet (xq_enabled)"
+
+
+def xq_enabled():
+    """Whether the encoder pair's hand-offs are signal / wait kernels: the
+    rule (handoff_rule) with this process's environment and local device
+    count, resolved once, unless a caller set XQ_FLAGS."""
+    global XQ_FLAGS, XQ_REASON
+    if XQ_FLAGS is None:
+        XQ_FLAGS, XQ_REASON = handoff_rule(torch.cuda.device_count())
+    return XQ_FLAGS
 
 
 def _xq_words(device, key):
@@ -999,7 +1041,7 @@ class _GinEncoderPair(torch.autograd.Function):
             ctx.lin_saved = (f.detach(), w0)
             ctx.core_dims = core.dims
             outs = (s, ro, f, t)
-        if XQ_FLAGS:
+        if xq_enabled():
             _xq_handoff(side, main, "pair_fwd")
         else:
             main.wait_stream(side)
@@ -1023,7 +1065,7 @@ class _GinEncoderPair(torch.autograd.Function):
         main, side = _torch_stream(), ctx.side
         check_fork(main)
         stamp("bwd.start[main]")
-        if XQ_FLAGS:
+        if xq_enabled():
             _xq_handoff(main, side, "pair_bwd")
         else:
             side.wait_stream(main)

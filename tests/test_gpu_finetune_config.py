@@ -217,9 +217,15 @@ def test_frozen_layers_skip_weight_grads_bitwise(pkg, dev, case):
     (sa, ga, tr), (sb, gb, _) = out
     assert torch.equal(sa, sb)
     assert {n for n, v in ga.items() if v is not None} <= tr
+    checked = 0
     for n in tr:
-        if ga[n] is not None:
+        # a trainable tensor the all-trainable step gives a gradient must get
+        # one with the freezing too (a dropped need_w slice would lose it)
+        assert (ga[n] is None) == (gb[n] is None), n
+        if gb[n] is not None:
             assert torch.equal(ga[n], gb[n]), n
+            checked += 1
+    assert checked > 0
 
 
 @pytest.mark.parametrize("n,k,c,sig", [(32, 128, 1, True), (32, 128, 2, True), (1, 128, 1, True),
@@ -260,6 +266,21 @@ def test_predict_head_and_bce_vs_torch(pkg, dev, n, k, c, sig):
         l.backward()
         assert rel_err(l.item(), lr.item()) < 1e-5
         assert rel_err(s.grad.cpu(), s64.grad) < 1e-4
+
+
+def test_predict_head_empty_batch(pkg, dev):
+    """an empty batch through the fused head — the forward
+    returns [0, C], the backward zero weight gradients (as torch's head)."""
+    import torch.nn as nn
+    seq = nn.Sequential(nn.Linear(128, 64), nn.ReLU(), nn.Linear(64, 1)).to(dev)
+    x = torch.zeros(0, 128, device=dev, requires_grad=True)
+    out = pkg.ops.predict_head(x, seq, True)
+    assert out.shape == (0, 1)
+    out.sum().backward()
+    torch.cuda.synchronize()
+    assert x.grad.shape == (0, 128)
+    for p in seq.parameters():
+        assert p.grad is not None and float(p.grad.abs().max()) == 0.0
 
 
 def test_predict_head_refuses_k_not_multiple_of_4(pkg, dev):

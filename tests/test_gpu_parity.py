@@ -980,6 +980,29 @@ def test_set2set_device_vs_oracle(pkg, dev, dim, n_mols, mu):
         assert rel_err(v.grad.cpu(), p["s2s." + k].grad) < 1e-4, k
 
 
+def test_set2set_misaligned_feature_view(pkg, dev):
+    """a contiguous feature view whose storage offset is not a
+    multiple of 4 floats (base not 16-B aligned) takes the scalar staging
+    path of set2set.hip — bitwise the result of an aligned copy."""
+    g, gh = rand_graph(pkg, 40, "molhiv", 6, dev)
+    n = g.num_nodes()
+    s2s = pkg.models.Set2Set(64, 2, 1).to(dev)
+    base = torch.randn(n * 64 + 1, device=dev)
+    outs = []
+    for view in (True, False):
+        f = base[1:].view(n, 64) if view else base[1:].view(n, 64).clone()
+        assert (f.data_ptr() % 16 != 0) == view
+        f = f.detach().requires_grad_(True)
+        s2s.zero_grad(set_to_none=True)
+        out = s2s(g, f)
+        out.sum().backward()
+        torch.cuda.synchronize()
+        outs.append((out.detach(), f.grad, [p.grad.clone() for p in s2s.parameters()]))
+    (oa, ga, pa), (ob, gb, pb) = outs
+    assert torch.equal(oa, ob) and torch.equal(ga, gb)
+    assert all(torch.equal(a, b) for a, b in zip(pa, pb))
+
+
 # ---------------------------------------------------------------------------
 # Domain adaptation (SURVEY.md §8(f) #4) and fine-tuning on the adapted model
 # ---------------------------------------------------------------------------

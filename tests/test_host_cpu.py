@@ -517,8 +517,16 @@ def test_handoff_rule(pkg):
                     ({"AMD_SERIALIZE_KERNEL": "3"}, 1), ({"ROCPROF_KERNEL_TRACE": "1"}, 8)):
         ok, why = rule(dc, env)
         assert not ok and why, env
-    # the module default follows the process environment
-    assert pkg.ops.XQ_FLAGS == rule()[0]
+    # the module default follows the process environment and the local device
+    # count, resolved on first use (every entry point gets it)
+    import torch
+    keep = pkg.ops.XQ_FLAGS, pkg.ops.XQ_REASON
+    try:
+        pkg.ops.XQ_FLAGS = None
+        assert pkg.ops.xq_enabled() == rule(torch.cuda.device_count())[0]
+        assert pkg.ops.XQ_FLAGS is not None and pkg.ops.XQ_REASON
+    finally:
+        pkg.ops.XQ_FLAGS, pkg.ops.XQ_REASON = keep
 
 
 def test_check_handoff_raises_on_host_fault_word(pkg):

@@ -1071,10 +1071,10 @@ def main():
                      "the on-path gather kernels gin_fwd_k and gin_bwd_stats_k; "
                      "gin_aggregate_k is a reference kernel, not in the step); gin_fwd_k frac "
                      "on §8(d) aggregation bytes, frac_inclusive on everything the launch moves "
-                     "(its saved agg / z2 writes too; r is recomputed by the backward, "
-                     "stores_r); gin_bwd5_k (gin_bwd5r_k) at this scale (~146 "
-                     "sub-tiles per workgroup, its start-of-kernel chain amortised), mfma_frac "
-                     "= flops / time / 157.3 TF/s"),
+                     "(its saved-activation writes too: agg, z2 and — stores_r — r); "
+                     "gin_bwd5_k at this scale (~146 sub-tiles per workgroup, its "
+                     "start-of-kernel chain amortised; recomputes_r: the gin_bwd5r_k variant), "
+                     "mfma_frac = flops / time / 157.3 TF/s"),
             "cpu_baseline": cpu,
             # BASELINE.json configs[4] (molhiv fine-tune from the shipped
             # checkpoint, B = 32, 1 GPU): its own timed replay after this leg

@@ -285,7 +285,7 @@ def test_interaction_fwd_bwd(pkg, dev, training):
         # eval-mode compressor BN: the oracle's train-mode helper is replaced
         # by running statistics
         orig = R._batchnorm_train
-        R._batchnorm_train = lambda x, pp, name, buf: F.batch_norm(
+        R._batchnorm_train = lambda x, pp, name, buf, *_: F.batch_norm(
             x, bn_state[name + ".running_mean"], bn_state[name + ".running_var"],
             pp[name + ".weight"], pp[name + ".bias"], False, 0.1, 1e-5)
     try:
@@ -438,7 +438,7 @@ def test_fused_gin_encoder(pkg, dev, training, layers, n_mols):
         ref = R.gin_encoder(p, "Encoder1", src, dst, h0c, bufs, layers, relu_masks=masks)
     else:
         orig = R._batchnorm_train
-        R._batchnorm_train = lambda x, pp, name, buf: F.batch_norm(
+        R._batchnorm_train = lambda x, pp, name, buf, *_: F.batch_norm(
             x, bufs[name + ".running_mean"], bufs[name + ".running_var"], pp[name + ".weight"],
             pp[name + ".bias"], False, 0.1, 1e-5)
         try:
@@ -771,7 +771,7 @@ def _fold_case(pkg, dev, n_mols, training, via_ego, seed=7):
         h64 = R.gin_encoder(p64, "Encoder1", src, dst, h0, bufs, 5)
     else:
         orig = R._batchnorm_train
-        R._batchnorm_train = lambda xx, pp, name, buf: F.batch_norm(
+        R._batchnorm_train = lambda xx, pp, name, buf, *_: F.batch_norm(
             xx, pp[name + ".running_mean"], pp[name + ".running_var"], pp[name + ".weight"],
             pp[name + ".bias"], False, 0.1, 1e-5)
         try:

@@ -148,14 +148,16 @@ def agg_fwd_bytes(n, e, d_in):
     return agg_bytes(n, e, d_in)
 
 
-def layer_fwd_bytes_inclusive(n, e, d_in, store_r=False):
+def layer_fwd_bytes_inclusive(n, e, d_in, store_r=False, store_agg=True):
     """Everything one gin_fwd_k launch moves: the gather (neighbour + self
-    rows, col + rowptr), W1/b1/W2/b2, the agg / z2 writes (+ r's when the
-    forward stores it, ops.STORE_R) and the per-tile BN statistics (reported
-    beside the §8(d) figure as frac_inclusive)."""
+    rows, col + rowptr), W1/b1/W2/b2, the z2 writes (+ r's when the forward
+    stores it, ops.STORE_R; + agg's unless the layer is agg-free, ops.AGG_FREE)
+    and the per-tile BN statistics (reported beside the §8(d) figure as
+    frac_inclusive)."""
     return (4 * d_in * (e + n) + 4 * e + 4 * (n + 1)
             + 4 * (64 * d_in + 64 + 64 * 64 + 64)
-            + 4 * n * (d_in + 64 + (64 if store_r else 0)) + 512 * ((n + 63) // 64))
+            + 4 * n * ((d_in if store_agg else 0) + 64 + (64 if store_r else 0))
+            + 512 * ((n + 63) // 64))
 
 
 def layer_fwd_flops(n, e, d_in):
@@ -171,6 +173,28 @@ def layer_bwd_bytes(n, e, d_in, store_r=False, wg=True):
     wg False (a frozen layer, need_w = 0): the agg rows are not read."""
     return (4 * n * ((3 if store_r else 2) * 64 + (d_in if wg else 0))
             + 4 * (64 * d_in + 64 * 64 + 7 * 64) + 4 * n * d_in)
+
+
+def bwdz_bytes(n, e, d_in, wg=True):
+    """Algorithmic bytes of one gin_bwd5z_k launch (the agg-free layer
+    backward, ops.AGG_FREE): the dy, z2 and r rows read, W2 + BN coefficients,
+    dz1 written (slabs not counted, as layer_bwd_bytes)."""
+    return 4 * n * 3 * 64 + 4 * (64 * 64 + 7 * 64) + 4 * n * 64
+
+
+def bwdz_flops(n, e, d_in, wg=True):
+    return (4 if wg else 2) * n * 64 * 64  # dW2 and dr (frozen: dr)
+
+
+def statsz_bytes(n, e, d, wg=True):
+    """Algorithmic bytes of one gin_bwd_statsz_k launch: gin_bwd_stats_k's
+    (the transposed gather of dz1, z2 read, dy written) + W1 (its dW1
+    partials not counted, as the layer kernels' slabs)."""
+    return stats_bytes(n, e, d) + 4 * 64 * 64
+
+
+def statsz_flops(n, e, d, wg=True):
+    return (4 if wg else 2) * n * 64 * 64  # dh = g W1 and dW1 += g^T h (frozen: dh)
 
 
 def stats_bytes(n, e, d):
@@ -192,7 +216,9 @@ def layer_bwd_flops(n, e, d_in, wg=True):
 def _call_meta(fn, m):
     """bytes / flops of one launch from its meta (n, e, d_in[, r stored])."""
     if fn is layer_fwd_bytes_inclusive:
-        return fn(m["n"], m["e"], m["d_in"], m.get("r", False))
+        return fn(m["n"], m["e"], m["d_in"], m.get("r", False), m.get("agg", True))
+    if fn in (bwdz_bytes, bwdz_flops, statsz_bytes, statsz_flops):
+        return fn(m["n"], m["e"], m["d_in"], m.get("wg", True))
     if fn is layer_bwd_bytes:
         return fn(m["n"], m["e"], m["d_in"], m.get("r", False), m.get("wg", True))
     if fn is layer_bwd_flops:
@@ -224,6 +250,17 @@ KERNELS = {
                             pmc=["gin_bwd_stats_k<"],
                             desc="GIN backward statistics: transposed gather of d(agg) + ReLU "
                                  "mask + BN-backward sums"),
+    "gin_bwd5z_k": dict(entries=("scgib_gin_layer_bwd_z",), keep=lambda m: m.get("wg", True),
+                        bytes=bwdz_bytes, flops=bwdz_flops, pmc=["gin_bwd5z_k<true>"],
+                        desc="agg-free GIN layer backward (layers 1..4, ops.AGG_FREE): BN-backward "
+                             "apply + dW2 and dr on f32 MFMA, dz1 written (dW1 moves to "
+                             "gin_bwd_statsz_k)"),
+    "gin_bwd_statsz_k": dict(entries=("scgib_gin_bwd_stats_z",), keep=lambda m: m.get("wg", True),
+                             bytes=statsz_bytes, flops=statsz_flops,
+                             pmc=["gin_bwd_statsz_k<true>"],
+                             desc="GIN backward statistics below an agg-free layer: transposed "
+                                  "gather of dz1, dh = g W1 and dW1 += g^T h on f32 MFMA, ReLU "
+                                  "mask + BN-backward sums"),
     "gin_bwd_k": dict(entries=("scgib_gin_layer0_bwd",), keep=lambda m: True,
                       bytes=layer_bwd_bytes, flops=layer_bwd_flops,
                       pmc=["gin_bwd_k<32, true, true,"],
@@ -377,7 +414,8 @@ def superbatch_roofline(dev, n_target=1_200_000, reps=20):
     pkg.ops.FOLD_SLABS = False
     try:
         with KernelTimer("scgib_gin_layer_fwd_bn", "scgib_gin_bwd_stats_bn",
-                         "scgib_gin_bwd_stats_bn_fold", "scgib_gin_layer_bwd") as timer:
+                         "scgib_gin_bwd_stats_bn_fold", "scgib_gin_layer_bwd",
+                         "scgib_gin_layer_bwd_z", "scgib_gin_bwd_stats_z") as timer:
             y = gin(g, x)
             y.sum().backward()
     finally:
@@ -385,23 +423,38 @@ def superbatch_roofline(dev, n_target=1_200_000, reps=20):
     fwd = timer.records["scgib_gin_layer_fwd_bn"]
     st = [rec for name in ("scgib_gin_bwd_stats_bn", "scgib_gin_bwd_stats_bn_fold")
           for rec in timer.records[name] if rec[2]["e"] > 0]
+    stz = timer.records["scgib_gin_bwd_stats_z"]
     torch.cuda.synchronize()
     # gin_fwd_k over its d = 64 layers: frac on §8(d)'s aggregation bytes;
     # frac_inclusive counts everything the launch moves (its own saved
-    # agg / z2 (and r, if stored) writes and the weights too); mfma_frac on its two GEMMs
+    # z2 (+ r if stored, + agg unless agg-free) writes and the weights too);
+    # mfma_frac on its two GEMMs.  This GIN runs on a given h0, so its layer 0
+    # is a d_in = 64 layer that stores agg (the step's layer 0 is the
+    # transfer_d fold, d_in = 32): gin_fwd_k averages all five, and
+    # gin_fwd_k_agg_free the four agg-free ones — the step's d = 64 layers
     fwd = [rec for rec in fwd if rec[2]["d_in"] == 64]
-    for key, recs, fn in (("gin_fwd_k", fwd, agg_fwd_bytes), ("gin_bwd_stats_k", st, stats_bytes)):
+    fwd_free = [rec for rec in fwd if not rec[2].get("agg", True)]
+    for key, recs, fn in (("gin_fwd_k", fwd, agg_fwd_bytes),
+                          ("gin_fwd_k_agg_free", fwd_free, agg_fwd_bytes),
+                          ("gin_bwd_stats_k", st, stats_bytes),
+                          ("gin_bwd_statsz_k", stz, statsz_bytes)):
         if recs:
             ms_k = statistics.mean(a.elapsed_time(b) / KernelTimer.REPEAT for a, b, _ in recs)
             m = recs[0][2]
             res[key] = _frac_entry(fn(m["n"], m["e"], m["d_in"]), ms_k)
             res[key]["launches"] = len(recs)
-            if key == "gin_fwd_k":
-                inc = layer_fwd_bytes_inclusive(m["n"], m["e"], m["d_in"], m.get("r", False))
+            if key.startswith("gin_fwd_k"):
+                inc = statistics.mean(layer_fwd_bytes_inclusive(
+                    r[2]["n"], r[2]["e"], r[2]["d_in"], r[2].get("r", False), r[2].get("agg", True))
+                    for r in recs)
                 res[key]["stores_r"] = bool(m.get("r", False))
+                res[key]["stores_agg"] = sum(bool(r[2].get("agg", True)) for r in recs)
                 res[key]["bytes_inclusive"] = int(inc)
                 res[key]["frac_inclusive"] = round(inc / (ms_k * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
                 fl = layer_fwd_flops(m["n"], m["e"], m["d_in"])
+                res[key]["mfma_frac"] = round(fl / (ms_k * 1e-3) / 1e12 / F32_MFMA_PEAK_TFLOPS, 4)
+            if key == "gin_bwd_statsz_k":
+                fl = statsz_flops(m["n"], m["e"], m["d_in"])
                 res[key]["mfma_frac"] = round(fl / (ms_k * 1e-3) / 1e12 / F32_MFMA_PEAK_TFLOPS, 4)
     # the step's dominant kernel (gin_bwd5_k, d_in = 64 layers) at this scale:
     # ~37 k sub-tiles, ~146 per workgroup, so its start-of-kernel chain is
@@ -417,12 +470,28 @@ def superbatch_roofline(dev, n_target=1_200_000, reps=20):
         ent["mfma_frac"] = round(fl / (ms_k * 1e-3) / 1e12 / F32_MFMA_PEAK_TFLOPS, 4)
         ent["launches"] = len(bw)
         res["gin_bwd5_k"] = ent
+    bz = timer.records["scgib_gin_layer_bwd_z"]
+    if bz:
+        ms_k = statistics.mean(a.elapsed_time(b) / KernelTimer.REPEAT for a, b, _ in bz)
+        m = bz[0][2]
+        fl = bwdz_flops(m["n"], m["e"], m["d_in"])
+        ent = _frac_entry(bwdz_bytes(m["n"], m["e"], m["d_in"]), ms_k)
+        ent["tflops"] = round(fl / (ms_k * 1e-3) / 1e12, 2)
+        ent["mfma_frac"] = round(fl / (ms_k * 1e-3) / 1e12 / F32_MFMA_PEAK_TFLOPS, 4)
+        ent["launches"] = len(bz)
+        res["gin_bwd5z_k"] = ent
+    if "gin_bwd5z_k" in res and "gin_bwd_statsz_k" in res:
+        # an agg-free layer's whole backward (the statistics launch below it
+        # and its own): against gin_bwd_stats_k + gin_bwd5_k of a stored-agg layer
+        res["agg_free_layer_bwd_us"] = round(res["gin_bwd5z_k"]["us"]
+                                             + res["gin_bwd_statsz_k"]["us"], 2)
     del y, x, h, gin
     # rocprofv3 evidence of these launches (same program, separate runs):
     # the traced average duration beside the event time, and the PMC HBM
     # bytes per launch beside the algorithmic bytes
     ev = _sb_evidence()
-    for key in ("gin_fwd_k", "gin_bwd_stats_k", "gin_bwd5_k", "gin_aggregate_k"):
+    for key in ("gin_fwd_k", "gin_fwd_k_agg_free", "gin_bwd_stats_k", "gin_bwd_statsz_k",
+                "gin_bwd5_k", "gin_bwd5z_k", "gin_aggregate_k"):
         e = ev.get(key)
         if key not in res or not e:
             continue
@@ -813,6 +882,12 @@ def main():
     ap.add_argument("--recompute-r", action="store_true",
                     help="the GIN forward does not store r, the backward recomputes it "
                          "(ops.STORE_R = False; A/B, same bits: profiles/r05_recompute)")
+    ap.add_argument("--no-agg-free", action="store_true",
+                    help="every GIN layer stores agg and runs the stored-agg backward "
+                         "(ops.AGG_FREE = False; A/B)")
+    ap.add_argument("--agg-free-min-rows", type=int, default=None,
+                    help="encoders of at least this many rows run agg-free "
+                         "(ops.AGG_FREE_MIN_ROWS; 0: every encoder; A/B)")
     ap.add_argument("--finetune", choices=["molhiv"], default=None,
                     help="time the fine-tune step of BASELINE.json configs[4] instead "
                          "(finetune_bench.py; --batch defaults to 32 there)")
@@ -826,6 +901,9 @@ def main():
                     help="skip the fine-tune leg (configs[4]) the N = 1 line carries in 'finetune'")
     a = ap.parse_args()
     pkg.ops.STORE_R = not a.recompute_r
+    pkg.ops.AGG_FREE = not a.no_agg_free
+    if a.agg_free_min_rows is not None:
+        pkg.ops.AGG_FREE_MIN_ROWS = a.agg_free_min_rows
     if a.superbatch_only:
         dev = torch.device("cuda", 0)
         torch.cuda.set_device(dev)

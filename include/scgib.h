@@ -295,6 +295,48 @@ int scgib_gin_layer_bwd(const float *dy, const float *z2, const float *r, const 
                         const scgib_bn_bwd_pending *pending, scgib_stream_t stream);
 int scgib_gin_hidden(const float *agg, int32_t d_in, const float *w1, const float *b1,
                      int64_t n_nodes, float *r, scgib_stream_t stream);
+/* ---- A5: the agg-free backward of a d_in = 64 layer l >= 1 (ABI 20) ----
+ * Replaces the agg half of DGL GINConv's backward (models.py:63-71, the
+ * GINConv(MLP) + BatchNorm1d of GIN.forward): for a symmetric molecule graph
+ * dW1 = dz1^T agg = g^T h_{l-1} and d h_{l-1} = g W1 with g = (I + A)^T dz1,
+ * so the forward stores no agg for such a layer (scgib_gin_layer_fwd[_bn]
+ * with agg NULL) and:
+ *   scgib_gin_layer_bwd_z   dz2 (BN backward) -> dW2 += dz2^T r, dr = dz2 W2,
+ *                           dz1 = dr [r > 0] written to dz1 [n][64]; one slab
+ *                           per workgroup: dW2 [64][64] | db2 [64] | db1 [64]
+ *                           (scgib_gin_layer_bwd_z_width floats; count
+ *                           scgib_gin_layer_bwd_z_slabs); `fold`, `fold2`
+ *                           (or NULL): slab jobs reduced in extra workgroups
+ *                           (fold: 32 columns x 8 slab partitions each, for
+ *                           the previous statistics launch's many dW1
+ *                           partials; fold2: as scgib_gin_bwd_stats_bn_fold's);
+ *   scgib_gin_bwd_stats_z   layer l-1's statistics from dz1 of layer l:
+ *                           g gathered over the transposed CSR (one_plus_eps
+ *                           of layer l), dh = g W1 (W1 of layer l), dy = dh
+ *                           [scale z2 + shift > 0], BN sums as
+ *                           scgib_gin_bwd_stats_bn_fold; dW1 of layer l as
+ *                           one [64][64] partial per workgroup in wslab
+ *                           (scgib_gin_bwd_stats_z_slabs of them); up to two
+ *                           fold jobs reduced in extra workgroups.
+ * need_w = 0 (a frozen layer l, resp. l + 1 for the statistics): the same
+ * data chains (bitwise the need_w = 1 dz1 / dy), no weight products, no
+ * slab (slab / wslab may be NULL).  Results equal the stored-agg path to
+ * fp32 rounding (different association of the same sums), deterministic run
+ * to run. */
+int64_t scgib_gin_layer_bwd_z_slabs(int64_t n_nodes);
+int64_t scgib_gin_layer_bwd_z_width(void);
+int scgib_gin_layer_bwd_z(const float *dy, const float *z2, const float *r, const float *stat,
+                          const float *coef, const float *w2, int64_t n_nodes, float *dz1,
+                          float *slab, int32_t need_w, const int32_t *dims,
+                          const scgib_bn_bwd_pending *pending, const scgib_slab_job *fold,
+                          const scgib_slab_job *fold2, scgib_stream_t stream);
+int64_t scgib_gin_bwd_stats_z_slabs(int64_t n_nodes);
+int scgib_gin_bwd_stats_z(const float *dz1, const int32_t *rowptr_t, const int32_t *col_t,
+                          float one_plus_eps, const float *w1, const float *z2, const float *stat,
+                          int64_t n_nodes, int32_t training, float *dy, float *dgamma,
+                          float *dbeta, float *coef, float *bn_ws, uint32_t *counters,
+                          const int32_t *dims, int32_t defer, float *wslab, int32_t need_w,
+                          const scgib_slab_job *fold, int32_t n_fold, scgib_stream_t stream);
 
 /* ---- (f)1/(f)4: Set2Set readout (DGL Set2Set(dim, n_iters, 1), models.py:565) ----
  * The whole readout as Mainmodel_finetuning.forward (models.py:515) and

@@ -127,6 +127,13 @@ SIGNATURES = {
     "scgib_bn_bwd_finalize": (ctypes.c_int, [_P, _I64, _I32, _P, _P, _P, _P, _P]),
     "scgib_gin_layer_bwd": (ctypes.c_int, [_P, _P, _P, _P, _I32, _P, _P, _P, _P, _P, _I64, _P,
                                            _P, _P, _I32, _P, _P, _P]),
+    "scgib_gin_layer_bwd_z_slabs": (_I64, [_I64]),
+    "scgib_gin_layer_bwd_z_width": (_I64, []),
+    "scgib_gin_layer_bwd_z": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _I64, _P, _P, _I32, _P, _P,
+                                             _P, _P, _P]),
+    "scgib_gin_bwd_stats_z_slabs": (_I64, [_I64]),
+    "scgib_gin_bwd_stats_z": (ctypes.c_int, [_P, _P, _P, _F, _P, _P, _P, _I64, _I32, _P, _P, _P,
+                                             _P, _P, _P, _P, _I32, _P, _I32, _P, _I32, _P]),
     "scgib_recon_partials_floats": (_I64, [_I64]),
     "scgib_recon_fwd": (ctypes.c_int, [_P, _P, _P, _I64, _I64, _P, _P, _P, _P, _P]),
     "scgib_recon_bwd": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _I64, _P, _P, _P, _P]),
@@ -180,7 +187,7 @@ class RunningUpdate(ctypes.Structure):
                 ("num_batches_tracked", ctypes.c_void_p)]
 
 
-ABI_VERSION = 19
+ABI_VERSION = 20
 STATS_STRIDE = 260
 PGRAD_STRIDE = 324
 HIDDEN = 64

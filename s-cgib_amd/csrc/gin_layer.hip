@@ -390,13 +390,13 @@ __device__ __forceinline__ float bn_bwd_publish(int c, double tot, int64_t n, in
 // backward: tile (sum dy, sum dy xhat) -> group -> layer sums (fp64);
 // sh: 2 KB of LDS scratch (the caller's, so a kernel near its LDS limit can
 // lend a dead tile image)
-__device__ void bn_bwd_hier_s(const float *__restrict__ part, int64_t n, int64_t tile,
-                              const BnBwdFuse &bz, double (*sh)[128]) {
+// (group g, `count` of its tiles arriving at once: gin_bwd_statsz_k's walk)
+__device__ __forceinline__ void bn_bwd_hier_gs(const float *__restrict__ part, int64_t n, int g, unsigned count,
+                               const BnBwdFuse &bz, double (*sh)[128]) {
     const int64_t nt = (n + TM - 1) / TM;
     const int ngr = static_cast<int>((nt + kGroup - 1) / kGroup);
-    const int g = static_cast<int>(tile / kGroup);
     const int gsize = static_cast<int>(nt - int64_t(g) * kGroup < kGroup ? nt - int64_t(g) * kGroup : kGroup);
-    if (!block_arrive(&bz.counters[g], gsize)) return;
+    if (!block_arrive(&bz.counters[g], gsize, count)) return;
     const int c = threadIdx.x & 127, p = threadIdx.x >> 7;  // 128 sums x 2 partitions
     {
         constexpr int U = kGroup / 2;
@@ -441,6 +441,11 @@ __device__ void bn_bwd_hier_s(const float *__restrict__ part, int64_t n, int64_t
     if ((threadIdx.x & 63) < 32)
         bn_bwd_publish(bfin_index(), tot, n, bz.training, bz.dgamma, bz.dbeta, bz.coef);
     if (threadIdx.x == 0) bz.counters[bz.ngr_cap] = 0u;
+}
+
+__device__ void bn_bwd_hier_s(const float *__restrict__ part, int64_t n, int64_t tile,
+                              const BnBwdFuse &bz, double (*sh)[128]) {
+    bn_bwd_hier_gs(part, n, static_cast<int>(tile / kGroup), 1u, bz, sh);
 }
 
 __device__ void bn_bwd_hier(const float *__restrict__ part, int64_t n, int64_t tile,
@@ -644,7 +649,7 @@ __global__ __launch_bounds__(256, (kFwdAlias<DIN, GATHER, PRE> ? 3 : 1)) void gi
             if (r_out) r_out[row0 * 64 + idx] = 0.f;
             z2_out[row0 * 64 + idx] = 0.f;
         }
-        if (GATHER)
+        if (GATHER && agg_out)
             for (int idx = nv * DIN + tid; idx < ncr * DIN; idx += 256) agg_out[row0 * DIN + idx] = 0.f;
         if (PRE)
             for (int idx = nv * kPreF + tid; idx < ncr * kPreF; idx += 256) pre.aggx[row0 * kPreF + idx] = 0.f;
@@ -766,7 +771,9 @@ __global__ __launch_bounds__(256, (kFwdAlias<DIN, GATHER, PRE> ? 3 : 1)) void gi
 #pragma unroll
         for (int k = 0; k < RPT; ++k) {
             const int rr = rbase + k * RPP;
-            if (rr < nv) st4_saved(agg_out + (row0 + rr) * DIN + 4 * c, acc[k]);
+            // agg_out NULL (an agg-free layer: its backward never reads agg,
+            // gin_bwd_statsz_k forms dW1 from the gathered dz1 instead)
+            if (agg_out && rr < nv) st4_saved(agg_out + (row0 + rr) * DIN + 4 * c, acc[k]);
             float *d = sA + rr * LDA + 4 * c;
             d[0] = acc[k].x; d[1] = acc[k].y; d[2] = acc[k].z; d[3] = acc[k].w;
         }
@@ -1032,6 +1039,42 @@ __device__ __forceinline__ void slab_fold_block(const scgib_slab_job &J, int b, 
     if (sp == 0 && e < J.width)
         J.out[e] = static_cast<float>(((static_cast<double>(red[el]) + red[64 + el]) + red[128 + el]) +
                                       red[192 + el]);
+}
+
+// The same over 32 columns x 8 slab partitions per block (partials combined
+// in fp64, fixed order): for a job of many slabs — the agg-free statistics
+// walk's dW1 partials, one per tile at small batches — folded into
+// gin_bwd5z_k, whose grid leaves the CUs room for these blocks.
+constexpr int kFold8Cols = 32;
+
+__host__ __device__ inline int slab_fold8_blocks(const scgib_slab_job &J) {
+    return J.n_slabs > 0 ? static_cast<int>((J.width + kFold8Cols - 1) / kFold8Cols) : 0;
+}
+
+__device__ __forceinline__ void slab_fold8_block(const scgib_slab_job &J, int b, float *red) {
+    const int el = threadIdx.x & 31, sp = threadIdx.x >> 5;
+    const int64_t e = static_cast<int64_t>(b) * kFold8Cols + el;
+    const int64_t stride = J.stride > 0 ? J.stride : J.width;
+    const int64_t ec = e < J.width ? e : J.width - 1;  // clamped: loads stay unconditional
+    float acc = 0.f;
+    for (int b0 = sp; b0 < J.n_slabs; b0 += 8 * 16) {
+        float v[16];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {
+            const int sb = b0 + 8 * u;
+            v[u] = J.slab[static_cast<int64_t>(sb < J.n_slabs ? sb : sp) * stride + ec];
+        }
+#pragma unroll
+        for (int u = 0; u < 16; ++u) acc += b0 + 8 * u < J.n_slabs ? v[u] : 0.f;
+    }
+    red[sp * 32 + el] = acc;
+    __syncthreads();
+    if (sp == 0 && e < J.width) {
+        double t = red[el];
+#pragma unroll
+        for (int p = 1; p < 8; ++p) t += red[32 * p + el];
+        J.out[e] = static_cast<float>(t);
+    }
 }
 
 template <bool GATHER, bool SEG = false>
@@ -1767,6 +1810,394 @@ __global__ __launch_bounds__(256, 2) void gin_bwd5_k(
 }
 
 // ---------------------------------------------------------------------------
+// The agg-free backward of a d_in = 64 GIN layer l >= 1.
+// agg_l = (I + A) h_{l-1} is read by exactly one product of the layer's
+// backward, dW1 = dz1^T agg.  A is symmetric (the reference's bidirected
+// molecule graphs), so with g = (I + A)^T dz1 — the transposed gather the
+// NEXT statistics kernel runs anyway, now over dz1 instead of d(agg):
+//   dW1_l      = dz1^T (I + A) h_{l-1} = g^T h_{l-1}
+//   d h_{l-1}  = (I + A)^T (dz1 W1) = g W1
+// and h_{l-1} = relu(scale z2_{l-1} + shift) comes elementwise from the z2
+// rows that kernel reads for layer l-1's BatchNorm backward.  So the forward
+// stores no agg for these layers (256 B per row less of the 768 B it wrote,
+// gin_fwd_k), gin_bwd5z_k runs two of gin_bwd5_k's four products (dr, dW2)
+// and writes dz1 where gin_bwd5_k wrote d(agg), reading no agg; and
+// gin_bwd_statsz_k gathers dz1 and adds the two products it moved (g W1 and
+// g^T h, f32 MFMA), leaving dW1 as per-workgroup partials.  No flops are
+// added, only moved; the sums associate differently, so results match the
+// stored-agg path to rounding, not bitwise (ops.AGG_FREE selects the path).
+// ---------------------------------------------------------------------------
+constexpr int kZSlab = 64 * 64 + 128;  // gin_bwd5z_k slab: dW2 [64][64] | db2 | db1
+
+// gin_bwd5z_k: gin_bwd5_k's sub-tile walk with its first product pair only —
+//   waves 0,1 (N): dr block q = dz2 W2[:, 32q..] (K = 64), dz1 = dr [r > 0]
+//                  -> dz1 staging (row-major) and db1 (column sums of dz1);
+//   waves 2,3 (T): dW2 rows 32q.. += dz2^T r (two blocks, K = 32 rows) + db2
+// — then the dz1 rows go out as full-row float4 stores: two barriers per
+// sub-tile (gin_bwd5_k: three), no agg rows loaded, no W1.
+// WG = false: a frozen layer (the fine-tune freezing quirk) — dz1 by the same
+// dr chain, no dW2 / db products, no slab.
+template <bool WG = true>
+__global__ __launch_bounds__(256, 2) void gin_bwd5z_k(
+    const float *__restrict__ dy, const float *__restrict__ z2, const float *__restrict__ r,
+    const float *__restrict__ stat, const float *__restrict__ coef, const float *__restrict__ w2,
+    int64_t ncap, int64_t nsub, int64_t G, float *__restrict__ dz1_out, float *__restrict__ slab,
+    const int32_t *__restrict__ dims, scgib_bn_bwd_pending pend, scgib_slab_job fold,
+    scgib_slab_job fold2) {
+    static_assert(SM == 32, "32-row sub-tiles");
+    __shared__ __attribute__((aligned(16))) float sD[SM * LDR];   // dz2 [row][k]
+    __shared__ __attribute__((aligned(16))) float sDT[64 * LDT];  // dz2 [col][row]
+    __shared__ __attribute__((aligned(16))) float sRT[64 * LDT];  // r [col][row]
+    __shared__ float sE[SM * LDH];                                 // dz1 staging
+    __shared__ float sCoef[128];
+    if (static_cast<int64_t>(blockIdx.x) >= G) {  // block-uniform: a folded reduce block
+        const int b = static_cast<int>(blockIdx.x - G), f1 = slab_fold8_blocks(fold);
+        if (b < f1) slab_fold8_block(fold, b, sD);
+        else slab_fold_block(fold2, b - f1, sD);
+        return;
+    }
+    const int64_t n = eff_count(dims, 0, ncap);
+    const int tid = threadIdx.x, l = tid & 63, w = tid >> 6;
+    const int kk = l >> 5, li = l & 31;
+    const bool nw = w < 2;  // wave-uniform role: N (dr, dz1, db1) or T (dW2, db2)
+    const int q = w & 1;    // the role's 32-wide block
+    const int c = l;        // elementwise: column c, rows 8 w .. 8 w + 7
+    const int64_t last = ncap - 1;
+    SCGIB_MARK(0);
+    SCGIB_MARK_HWID();
+    BwdFin bfin;
+    const int pend_ngr = static_cast<int>(((n + TM - 1) / TM + kGroup - 1) / kGroup);
+    if (pend.gpart) bn_bwd_fin_load<false>(pend.gpart, pend_ngr, 0, bfin);
+    const float s_mean = stat[c], s_istd = stat[64 + c], s_sc = stat[128 + c];
+    float c1 = 0.f, c2 = 0.f;
+    if (!pend.gpart) {
+        c1 = coef[c];
+        c2 = coef[64 + c];
+    }
+    float wreg[32];  // N waves: W2[:, 32q..] (k in kperm order); T waves: unused
+#pragma unroll
+    for (int s = 0; s < 32; ++s) wreg[s] = nw ? w2[kperm(s, kk) * 64 + q * 32 + li] : 0.f;
+    float nx[3][8];  // a sub-tile's column c, rows 8 w + i: [0] dy, [1] z2, [2] r
+    auto load_sub = [&](int64_t s) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {  // in order of use: r, then dy / z2
+            int64_t row = s * SM + 8 * w + i;
+            row = row < last ? row : last;
+            nx[2][i] = r[row * 64 + c];
+        }
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            int64_t row = s * SM + 8 * w + i;
+            row = row < last ? row : last;
+            nx[0][i] = dy[row * 64 + c];
+            nx[1][i] = z2[row * 64 + c];
+        }
+    };
+    auto put_rt = [&]() {  // r: column c, rows 8w..8w+7 -> [c][row]
+        float4 *p = reinterpret_cast<float4 *>(sRT + c * LDT + 8 * w);
+        p[0] = make_float4(nx[2][0], nx[2][1], nx[2][2], nx[2][3]);
+        p[1] = make_float4(nx[2][4], nx[2][5], nx[2][6], nx[2][7]);
+    };
+    auto rows_of = [&](int64_t s) {
+        const int64_t v = n - s * SM;
+        return static_cast<int>(v < SM ? (v > 0 ? v : 0) : SM);
+    };
+    auto zero_pad = [&](int64_t s, int from) {
+        const int64_t row0 = s * SM;
+        const int ncr = static_cast<int>(ncap - row0 < SM ? ncap - row0 : SM);
+        for (int idx = from * 64 + tid; idx < ncr * 64; idx += 256) dz1_out[row0 * 64 + idx] = 0.f;
+    };
+    int64_t s = blockIdx.x;
+    int nv = s < nsub ? rows_of(s) : 0;
+    if (nv > 0) load_sub(s);
+    if (pend.gpart) {  // finish the BN-backward sums; workgroup 0 writes dgamma, dbeta
+        const double tot = bn_bwd_final<false>(pend.gpart, pend_ngr, bfin);
+        const int cs = bfin_index();
+        const bool lead = (tid & 63) < 32, w0 = blockIdx.x == 0 && lead;
+        const float cf = bn_bwd_publish(cs, tot, n, pend.training, w0 ? pend.dgamma : nullptr,
+                                        w0 ? pend.dbeta : nullptr, nullptr);
+        if (lead) sCoef[cs] = cf;
+    }
+    if (nv > 0) put_rt();
+    vm_wait_all();  // the weight registers complete before the loop (gin_bwd5_k)
+    __syncthreads();
+    if (pend.gpart) {
+        c1 = sCoef[c];
+        c2 = sCoef[64 + c];
+    }
+    const float k1 = s_istd * c2;  // dz2 = sc (dy - c1 - (z2 - mean) istd c2)
+    SCGIB_MARK(1);
+    f32x16 accA = zero16(), accB = zero16();  // T waves: dW2 blocks (q, 0), (q, 1)
+    float dbias = 0.f;                         // N: db1 (column q*32 + li), T: db2
+    for (int it = 0; s < nsub; s += G, ++it) {
+        if (nv == 0) {  // capacity tail: this and every later sub-tile is padding
+            for (int64_t t = s; t < nsub; t += G) zero_pad(t, rows_of(t));
+            break;
+        }
+        {   // dz2 (rows past nv zero) -> sD row-major and sDT transposed
+            float d[8];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const float v = s_sc * (nx[0][i] - c1 - (nx[1][i] - s_mean) * k1);
+                d[i] = 8 * w + i < nv ? v : 0.f;
+                sD[(8 * w + i) * LDR + c] = d[i];
+            }
+            float4 *p = reinterpret_cast<float4 *>(sDT + c * LDT + 8 * w);
+            p[0] = make_float4(d[0], d[1], d[2], d[3]);
+            p[1] = make_float4(d[4], d[5], d[6], d[7]);
+        }
+        const int64_t next = s + G;
+        const int next_nv = next < nsub ? rows_of(next) : 0;  // block-uniform
+        if (next_nv > 0) load_sub(next);  // in flight during the products
+        lds_barrier();  // dz2 complete
+        if (it == 0) SCGIB_MARK(2);
+        if (nw) {  // dr block q, dz1 = dr [r > 0] (mask by multiplication) -> staging
+            const f32x16 dr = mma_rk4<8>(sD + li * LDR + 4 * kk, wreg, zero16());
+#pragma unroll
+            for (int reg = 0; reg < 16; ++reg) {
+                const int row = acc_row(reg, l), col = q * 32 + li;
+                const float v = dr[reg] * (sRT[col * LDT + row] > 0.f ? 1.f : 0.f);
+                sE[row * LDH + col] = v;
+                dbias += v;
+            }
+        } else if constexpr (WG) {   // dW2 rows 32q.. += dz2^T r (db2 from the A operand)
+            mma_kk4x2<4>(sDT + (q * 32 + li) * LDT + 4 * kk, sRT + li * LDT + 4 * kk,
+                         sRT + (32 + li) * LDT + 4 * kk, accA, accB, dbias);
+        }
+        lds_barrier();  // dz1 staged; r and dz2 consumed
+        if (it == 0) SCGIB_MARK(3);
+        if (next_nv > 0) put_rt();
+        {   // dz1 rows: full-row float4 stores
+            const int c4 = tid & 15, rs = tid >> 4;
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+                const int rr = rs + 16 * k;
+                const float *pg = sE + rr * LDH + 4 * c4;
+                const float4 v = make_float4(pg[0], pg[1], pg[2], pg[3]);
+                if (rr < nv) st4(dz1_out + (s * SM + rr) * 64 + 4 * c4, v);
+            }
+        }
+        if (dims) zero_pad(s, nv);
+        nv = next_nv;
+    }
+    SCGIB_MARK(5);
+    if constexpr (!WG) return;
+    // per-workgroup slab: dW2 [64][64] | db2 [64] | db1 [64]
+    float *sl = slab + static_cast<int64_t>(blockIdx.x) * kZSlab;
+    if (!nw) {
+#pragma unroll
+        for (int reg = 0; reg < 16; ++reg) {
+            const int j = q * 32 + acc_row(reg, l);
+            sl[j * 64 + li] = accA[reg];
+            sl[j * 64 + 32 + li] = accB[reg];
+        }
+    }
+    dbias += __shfl_xor(dbias, 32, kWave);
+    if (l < 32) sl[64 * 64 + (nw ? 64 : 0) + q * 32 + l] = dbias;
+    SCGIB_MARK(6);
+}
+
+// gin_bwd_statsz_k: the backward statistics of layer l below an agg-free layer
+// l + 1 — gin_bwd_stats_k<GATHER>'s work with the transposed gather taken over
+// dz1_{l+1} and the two products moved out of gin_bwd5z_k:
+//   g = ope dz1[v] + sum_{v->u} dz1[u]       (gather_rows, as gin_bwd_stats_k)
+//   dh = g W1_{l+1}     (f32 MFMA, W1 staged in LDS once per workgroup)
+//   dW1_{l+1} += g^T h, h = relu(scale z2 + shift) (rows past nv: 0)
+//   dy = dh [scale z2 + shift > 0]; tile sums of dy and dy xhat -> BN hier
+// Each workgroup walks a run of `per` consecutive tiles (the fewest workgroups
+// reaching ceil(tiles / kZStatSlots) tiles each) and keeps its 64 x 64 dW1
+// block in MFMA accumulators (wave w: rows 32 (w >> 1).., columns 32 (w & 1)..),
+// one partial slab per workgroup — per-tile partials would write as many
+// bytes as the agg rows this path saves.  Workgroups past the walk reduce up
+// to two slab jobs.  LDS: the g, h and z tiles row-major at stride 65 (the
+// stats layout's 4-channel runs store conflict free, and both products read
+// their operands by column or by row conflict free, mma_pf), W1, the sums.
+constexpr int kZStatSlots = 512;    // two walking workgroups per CU
+
+// WG = false: layer l + 1 is frozen — dh and dy exactly as with WG, no h
+// image, no dW1 product, no slab.
+template <bool WG = true>
+__global__ __launch_bounds__(256, 2) void gin_bwd_statsz_k(
+    const float *__restrict__ dz1, const int32_t *__restrict__ rowptr_t,
+    const int32_t *__restrict__ col_t, float ope, const float *__restrict__ w1,
+    const float *__restrict__ z2, const float *__restrict__ stat, int64_t ncap, int per,
+    float *__restrict__ dy_out, float *__restrict__ part, const int32_t *__restrict__ dims,
+    BnBwdFuse bz, float *__restrict__ wslab, scgib_slab_job fold1, scgib_slab_job fold2) {
+    __shared__ float sG[TM * LDH];   // g [row][o]; then dh [row][in] (staging)
+    __shared__ float sH[TM * LDH];   // h [row][in]
+    __shared__ float sZ[TM * LDH];   // z2 [row][c] (not held in registers across the products)
+    __shared__ float sW1[64 * LDH];  // W1 [o][in]
+    __shared__ float sRed[2][16][64];
+    const int64_t ntc = (ncap + TM - 1) / TM;
+    const int64_t G = (ntc + per - 1) / per;
+    if (static_cast<int64_t>(blockIdx.x) >= G) {  // block-uniform: a folded reduce block
+        const int b = static_cast<int>(blockIdx.x - G), f1 = slab_fold_blocks(fold1);
+        if (b < f1) slab_fold_block(fold1, b, &sRed[0][0][0]);
+        else slab_fold_block(fold2, b - f1, &sRed[0][0][0]);
+        return;
+    }
+    const int64_t n = eff_count(dims, 0, ncap);
+    const int rw = (threadIdx.x >> 6) >> 1, cq = (threadIdx.x >> 6) & 1;  // the wave's 32 x 32
+    // block of dh and of dW1 (wave-uniform)
+    SCGIB_MARK(0);
+    SCGIB_MARK_HWID();
+    const float4 *g4 = reinterpret_cast<const float4 *>(dz1);
+    f32x16 accW = zero16();
+    const int64_t vb = SCGIB_XCD_TILES ? xcd_remap(blockIdx.x, G) : static_cast<int64_t>(blockIdx.x);
+    const int64_t t0 = vb * per, t1 = t0 + per < ntc ? t0 + per : ntc;
+    bool w1_staged = false;
+    for (int64_t tile = t0; tile < t1; ++tile) {
+        // lane indices laundered per tile: every LDS / global address below is
+        // then formed inside the loop, not hoisted out of it and held in
+        // registers across the walk (which ran the kernel out of VGPRs)
+        int tid = threadIdx.x;
+        asm volatile("" : "+v"(tid));
+        const int c = tid & 15, slot = tid >> 4, l = tid & 63;
+        const int64_t row0 = tile * TM;
+        const int nv = static_cast<int>(n - row0 < TM ? (n - row0 > 0 ? n - row0 : 0) : TM);
+        if (nv == 0) {  // capacity mode: a tile of padding rows (block-uniform)
+            for (int rr = slot; rr < TM && row0 + rr < ncap; rr += 16)
+                st4(dy_out + (row0 + rr) * 64 + 4 * c, make_float4(0.f, 0.f, 0.f, 0.f));
+            continue;
+        }
+        float4 g[4], z[4];
+        {
+            const float4 one4 = make_float4(1.f, 1.f, 1.f, 1.f), zero4 = make_float4(0.f, 0.f, 0.f, 0.f);
+            // W1 once per workgroup: its loads go out first, then the gather's
+            // first round and the z rows; W1 goes to LDS before the gather's
+            // neighbour rounds (in-order completion: waiting for W1 does not
+            // wait for the loads behind it), so its registers are free again
+            // where the gather holds the most
+            GatherHead<4> hd;
+            if (!w1_staged) {  // block-uniform
+                float4 wv[4];
+#pragma unroll
+                for (int k = 0; k < 4; ++k) wv[k] = reinterpret_cast<const float4 *>(w1)[tid + 256 * k];
+                gather_head<4, 16, 16>(g4, rowptr_t, row0, nv, slot, c, hd);
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const int rr = slot + 16 * k;
+                    z[k] = ld4(z2 + (row0 + (rr < nv ? rr : nv - 1)) * 64 + 4 * c);
+                }
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {  // (sW1 is read only after the image barrier)
+                    const int idx = 4 * (tid + 256 * k), row = idx >> 6, cc = idx & 63;
+                    float *d = sW1 + row * LDH + cc;
+                    d[0] = wv[k].x; d[1] = wv[k].y; d[2] = wv[k].z; d[3] = wv[k].w;
+                }
+                w1_staged = true;
+            } else {
+                gather_head<4, 16, 16>(g4, rowptr_t, row0, nv, slot, c, hd);
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const int rr = slot + 16 * k;
+                    z[k] = ld4(z2 + (row0 + (rr < nv ? rr : nv - 1)) * 64 + 4 * c);
+                }
+            }
+            gather_tail<4, 16, false>(g4, col_t, hd, c, ope, one4, zero4, g);
+            __syncthreads();  // the previous tile's readers of sG (dh) / sH / sZ are done
+        }
+        {
+            const float4 sc = ld4(stat + 128 + 4 * c), sh = ld4(stat + 192 + 4 * c);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {  // g, h (rows past nv: 0), z rows
+                const int rr = slot + 16 * k;
+                const float valid = rr < nv ? 1.f : 0.f;
+                float *pg = sG + rr * LDH + 4 * c, *pz = sZ + rr * LDH + 4 * c;
+                pg[0] = g[k].x; pg[1] = g[k].y; pg[2] = g[k].z; pg[3] = g[k].w;
+                pz[0] = z[k].x; pz[1] = z[k].y; pz[2] = z[k].z; pz[3] = z[k].w;
+                if constexpr (WG) {
+                    float *ph = sH + rr * LDH + 4 * c;
+                    ph[0] = fmaxf(sc.x * z[k].x + sh.x, 0.f) * valid;
+                    ph[1] = fmaxf(sc.y * z[k].y + sh.y, 0.f) * valid;
+                    ph[2] = fmaxf(sc.z * z[k].z + sh.z, 0.f) * valid;
+                    ph[3] = fmaxf(sc.w * z[k].w + sh.w, 0.f) * valid;
+                }
+            }
+        }
+        __syncthreads();
+        SCGIB_MARK(1);
+        // dh block (rw, cq) = g W1: A(i = row, k = o) = sG[row][o], B(k = o, j = in) = sW1[o][in]
+        f32x16 dh = mma_pf<64, false, true, 2>(sG + 32 * rw * LDH, LDH, sW1 + 32 * cq, LDH, zero16());
+        // dW1 block (rw, cq) += g^T h over the tile's rows: A(i = o, k = row) = sG[row][o],
+        // B(k = row, j = in) = sH[row][in]
+        if constexpr (WG) accW = mma_pf<64, true, true, 2>(sG + 32 * rw, LDH, sH + 32 * cq, LDH, accW);
+        __syncthreads();  // every read of the g tile done: it stages dh now
+#pragma unroll
+        for (int reg = 0; reg < 16; ++reg)
+            sG[(32 * rw + acc_row(reg, l)) * LDH + 32 * cq + (l & 31)] = dh[reg];
+        __syncthreads();
+        SCGIB_MARK(2);
+        {
+            const float4 mean = ld4(stat + 4 * c), istd = ld4(stat + 64 + 4 * c);
+            const float4 sc = ld4(stat + 128 + 4 * c), sh = ld4(stat + 192 + 4 * c);
+            float4 sdy = make_float4(0.f, 0.f, 0.f, 0.f), sdx = sdy;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int rr = slot + 16 * k;
+                const int64_t v = row0 + rr;
+                const float valid = rr < nv ? 1.f : 0.f;
+                const float *pd = sG + rr * LDH + 4 * c, *pz = sZ + rr * LDH + 4 * c;
+                const float4 gg = make_float4(pd[0], pd[1], pd[2], pd[3]);
+                const float4 zz = make_float4(pz[0], pz[1], pz[2], pz[3]);
+                const float4 dyv = make_float4((sc.x * zz.x + sh.x > 0.f ? gg.x : 0.f) * valid,
+                                               (sc.y * zz.y + sh.y > 0.f ? gg.y : 0.f) * valid,
+                                               (sc.z * zz.z + sh.z > 0.f ? gg.z : 0.f) * valid,
+                                               (sc.w * zz.w + sh.w > 0.f ? gg.w : 0.f) * valid);
+                if (v < ncap) st4(dy_out + v * 64 + 4 * c, dyv);
+                sdy = add4(sdy, dyv);
+                sdx = add4(sdx, make_float4(dyv.x * (zz.x - mean.x) * istd.x,
+                                            dyv.y * (zz.y - mean.y) * istd.y,
+                                            dyv.z * (zz.z - mean.z) * istd.z,
+                                            dyv.w * (zz.w - mean.w) * istd.w));
+            }
+            float *pa = &sRed[0][slot][4 * c];
+            pa[0] = sdy.x; pa[1] = sdy.y; pa[2] = sdy.z; pa[3] = sdy.w;
+            float *pb = &sRed[1][slot][4 * c];
+            pb[0] = sdx.x; pb[1] = sdx.y; pb[2] = sdx.z; pb[3] = sdx.w;
+        }
+        __syncthreads();
+        if (tid < 128) {
+            const int which = tid >> 6, ch = tid & 63;
+            float s = 0.f;
+            for (int k = 0; k < 16; ++k) s += sRed[which][k][ch];
+            st_agent(part + tile * 128 + which * 64 + ch, s);
+        }
+        SCGIB_MARK(3);
+        __syncthreads();  // sRed's readers done before the next tile writes it
+    }
+    // the BatchNorm statistics: this workgroup's tiles arrive at their groups
+    // at once, one arrival per group its run touches (the hierarchy inlined
+    // in the tile loop held its registers beside the walk's and spilled); the
+    // dW1 slab is written after (an arrival waits for every store issued
+    // before it)
+    // (accW waits in LDS meanwhile — each lane its own 16 slots of the dead
+    // g tile — so its registers are free for the hierarchy's)
+    if constexpr (WG) {
+#pragma unroll
+        for (int reg = 0; reg < 16; ++reg) sG[threadIdx.x * 16 + reg] = accW[reg];
+    }
+    if (bz.counters) {
+        __shared__ double shh[2][128];
+        const int64_t ntv = (n + TM - 1) / TM, e = t1 < ntv ? t1 : ntv;
+        for (int64_t gg = t0 / kGroup; gg * kGroup < e; ++gg) {
+            const int64_t lo = t0 > gg * kGroup ? t0 : gg * kGroup;
+            const int64_t hi = e < (gg + 1) * kGroup ? e : (gg + 1) * kGroup;
+            if (hi <= lo) continue;  // (a run of padding tiles only: no arrival)
+            bn_bwd_hier_gs(part, n, static_cast<int>(gg), static_cast<unsigned>(hi - lo), bz, shh);
+        }
+    }
+    if constexpr (WG) {  // this workgroup's dW1 partial
+        const int l = threadIdx.x & 63, li = l & 31;
+        float *sl = wslab + static_cast<int64_t>(blockIdx.x) * 4096;
+#pragma unroll
+        for (int reg = 0; reg < 16; ++reg)
+            sl[(32 * rw + acc_row(reg, l)) * 64 + 32 * cq + li] = sG[threadIdx.x * 16 + reg];
+    }
+    SCGIB_MARK(4);
+}
+
+// ---------------------------------------------------------------------------
 // gin_bwd5r_k: gin_bwd5_k without the saved r.  The
 // forward no longer writes r = relu(agg W1^T + b1) — one of the three [N,64]
 // row sets gin_fwd_k stored, a third of its HBM writes — and this kernel
@@ -2141,8 +2572,9 @@ static int gin_fwd_args_ok(const float *h_in, int32_t d_in, const float *in_stat
                            const float *tile_stats) {
     if (n_nodes < 0 || (d_in != 32 && d_in != 64)) return SCGIB_EINVAL;
     if (n_nodes == 0) return SCGIB_OK;
-    if (!h_in || !rowptr || !col || !w1 || !b1 || !w2 || !b2 || !agg || !z2 || !tile_stats)
+    if (!h_in || !rowptr || !col || !w1 || !b1 || !w2 || !b2 || !z2 || !tile_stats)
         return SCGIB_EINVAL;  // (r may be NULL: not stored)
+    if (!agg && d_in != 64) return SCGIB_EINVAL;  // (agg NULL: an agg-free d_in = 64 layer)
     if (in_stat && d_in != 64) return SCGIB_EUNSUPPORTED;
     return 1;  // go
 }
@@ -2441,6 +2873,86 @@ extern "C" int scgib_gin_layer_bwd(const float *dy, const float *z2, const float
     const int rc = launch_status();
     if (rc != SCGIB_OK || !wgrad || !need_w) return rc;  // wgrad NULL: the caller reduces the slabs
     return launch_slab_reduce(slab, grid, 64 * 64 + 64 * static_cast<int64_t>(d_in) + 128, wgrad, st);
+}
+
+// ---------------------------------------------------------------------------
+// agg-free backward entries (gin_bwd5z_k / gin_bwd_statsz_k)
+// ---------------------------------------------------------------------------
+extern "C" int64_t scgib_gin_layer_bwd_z_slabs(int64_t n_nodes) {
+    return n_nodes <= 0 ? 0 : bwd5_grid(bwd5_subtiles(n_nodes));
+}
+
+extern "C" int64_t scgib_gin_layer_bwd_z_width(void) { return kZSlab; }
+
+extern "C" int scgib_gin_layer_bwd_z(const float *dy, const float *z2, const float *r,
+                                     const float *stat, const float *coef, const float *w2,
+                                     int64_t n_nodes, float *dz1, float *slab, int32_t need_w,
+                                     const int32_t *dims, const scgib_bn_bwd_pending *pending,
+                                     const scgib_slab_job *fold, const scgib_slab_job *fold2,
+                                     scgib_stream_t stream) {
+    if (n_nodes <= 0 || !dy || !z2 || !r || !stat || (!coef && !pending) || !w2 || !dz1 ||
+        (need_w && !slab))
+        return SCGIB_EINVAL;
+    if (pending && (!pending->gpart || !pending->dgamma || !pending->dbeta)) return SCGIB_EINVAL;
+    if (!fold_ok(fold) || !fold_ok(fold2)) return SCGIB_EINVAL;
+    const scgib_bn_bwd_pending pd = pending ? *pending : scgib_bn_bwd_pending{};
+    const scgib_slab_job fj = fold ? *fold : scgib_slab_job{};
+    const scgib_slab_job fj2 = fold2 ? *fold2 : scgib_slab_job{};
+    const int64_t G = scgib_gin_layer_bwd_z_slabs(n_nodes);
+    const int grid = static_cast<int>(G + slab_fold8_blocks(fj) + slab_fold_blocks(fj2));
+    if (need_w)
+        gin_bwd5z_k<true><<<grid, 256, 0, as_stream(stream)>>>(
+            dy, z2, r, stat, coef, w2, n_nodes, bwd5_subtiles(n_nodes), G, dz1, slab, dims, pd, fj,
+            fj2);
+    else
+        gin_bwd5z_k<false><<<grid, 256, 0, as_stream(stream)>>>(
+            dy, z2, r, stat, coef, w2, n_nodes, bwd5_subtiles(n_nodes), G, dz1, slab, dims, pd, fj,
+            fj2);
+    return launch_status();
+}
+
+static int statsz_per(int64_t n_nodes) {
+    const int64_t nt = scgib_gin_tiles(n_nodes);
+    return static_cast<int>((nt + kZStatSlots - 1) / kZStatSlots);
+}
+
+extern "C" int64_t scgib_gin_bwd_stats_z_slabs(int64_t n_nodes) {
+    if (n_nodes <= 0) return 0;
+    const int64_t nt = scgib_gin_tiles(n_nodes), per = statsz_per(n_nodes);
+    return (nt + per - 1) / per;
+}
+
+extern "C" int scgib_gin_bwd_stats_z(const float *dz1, const int32_t *rowptr_t,
+                                     const int32_t *col_t, float one_plus_eps, const float *w1,
+                                     const float *z2, const float *stat, int64_t n_nodes,
+                                     int32_t training, float *dy, float *dgamma, float *dbeta,
+                                     float *coef, float *bn_ws, uint32_t *counters,
+                                     const int32_t *dims, int32_t defer, float *wslab,
+                                     int32_t need_w, const scgib_slab_job *fold, int32_t n_fold,
+                                     scgib_stream_t stream) {
+    if (n_nodes <= 0 || !dz1 || !rowptr_t || !col_t || !w1 || !z2 || !stat || !dy || !bn_ws ||
+        !counters || (need_w && !wslab))
+        return SCGIB_EINVAL;
+    if (!defer && (!dgamma || !dbeta || !coef)) return SCGIB_EINVAL;
+    if (n_fold < 0 || n_fold > 2 || (n_fold > 0 && !fold)) return SCGIB_EINVAL;
+    for (int i = 0; i < n_fold; ++i)
+        if (!fold_ok(&fold[i])) return SCGIB_EINVAL;
+    BnBwdFuse bz{counters, bn_gpart(bn_ws, n_nodes), dgamma, dbeta, coef, training,
+                 static_cast<int>(bn_groups(n_nodes)), defer ? 1 : 0};
+    const scgib_slab_job f1 = n_fold > 0 ? fold[0] : scgib_slab_job{};
+    const scgib_slab_job f2 = n_fold > 1 ? fold[1] : scgib_slab_job{};
+    const int per = statsz_per(n_nodes);
+    const unsigned grid = static_cast<unsigned>(scgib_gin_bwd_stats_z_slabs(n_nodes) +
+                                                slab_fold_blocks(f1) + slab_fold_blocks(f2));
+    if (need_w)
+        gin_bwd_statsz_k<true><<<dim3(grid), 256, 0, as_stream(stream)>>>(
+            dz1, rowptr_t, col_t, one_plus_eps, w1, z2, stat, n_nodes, per, dy, bn_ws, dims, bz,
+            wslab, f1, f2);
+    else
+        gin_bwd_statsz_k<false><<<dim3(grid), 256, 0, as_stream(stream)>>>(
+            dz1, rowptr_t, col_t, one_plus_eps, w1, z2, stat, n_nodes, per, dy, bn_ws, dims, bz,
+            wslab, f1, f2);
+    return launch_status();
 }
 
 // workgroups per tile of scgib_mlp2_bwd: 2 for d_in = 128 while the doubled

@@ -62,6 +62,23 @@ FOLD_SLABS = True
 # layer of saved activations.  (A d_in = 32 layer fed by a given h0, i.e. not
 # the transfer_d fold, always stores r.)
 STORE_R = True
+# the d_in = 64 GIN layers l >= 1 without a saved agg:
+# the forward writes only r and z2, the layer backward (scgib_gin_layer_bwd_z)
+# writes dz1 instead of d(agg), and the layer below's statistics launch
+# (scgib_gin_bwd_stats_z) gathers dz1 and forms d h = g W1 and dW1 = g^T h
+# there (g = (I + A)^T dz1, A symmetric).  Needs STORE_R (the recompute path
+# reads agg).  False: every layer stores agg (the round-5 path).
+AGG_FREE = True
+# ... for encoders of at least this many rows: below it the layer's agg rows
+# stay in the Infinity Cache / L2 between the forward and the backward, the
+# store + reload costs little, and the agg-free statistics launch's two
+# dependent GEMM phases lengthen the latency-bound chain instead (QM9 B512,
+# ego-nets of 27.9 k rows: 0.389 -> 0.416 ms per step); from molpcba B1024's
+# 80 k-row ego-nets up it is neutral to faster (0.907 -> 0.903 ms; PCQM B2048
+# k2: 1.432 -> 1.425 ms), and at ZINC scale the agg rows go to HBM and back
+# (the d = 64 forward 0.35 -> 0.40 of HBM, the layer backward 715 -> 711 us).
+# DESIGN.md §5 "Agg-free layers" has the A/B.
+AGG_FREE_MIN_ROWS = 1 << 16
 
 
 # LATE_FORK (always): launch_aside records an event on the current stream now
@@ -451,6 +468,13 @@ def graph_node_counts(graph):
     return out
 
 
+# the agg-free layer's weight-gradient row: dW2 [64][64] | db2 | db1 (the
+# scgib_gin_layer_bwd_z slab, reduced as one job) | dW1 [64][64] (the
+# scgib_gin_bwd_stats_z slab of the layer below)
+_Z_SLAB = HIDDEN * HIDDEN + 2 * HIDDEN
+_Z_W1_OFF = _Z_SLAB
+
+
 def _reduce_jobs(jobs, st, max_wg=0):
     cap = int(_lib.query("scgib_slab_reduce_max_jobs"))
     for i0 in range(0, len(jobs), cap):
@@ -520,12 +544,18 @@ class _GinEncoder(torch.autograd.Function):
             if w1.shape != (HIDDEN, d_in) or w2.shape != (HIDDEN, HIDDEN):
                 raise _lib.ScgibError(f"fused GIN layer needs Linear({d_in},64)/Linear(64,64), got "
                                       f"{tuple(w1.shape)}/{tuple(w2.shape)}")
-            agg = torch.empty(n, d_in, dtype=torch.float32, device=dev)
+            # agg only where a backward reads it: layer 0, and every layer
+            # without AGG_FREE (the agg-free layers' dW1 comes from the layer
+            # below's statistics launch, a frozen layer's backward reads none)
+            agg_free = AGG_FREE and STORE_R and l >= 1 and d_in == HIDDEN and \
+                n >= AGG_FREE_MIN_ROWS
+            agg = None if agg_free else torch.empty(n, d_in, dtype=torch.float32, device=dev)
             # r only where the backward cannot recompute it (or STORE_R)
             keep_r = STORE_R or (d_in != HIDDEN and not (pre and l == 0))
             r = torch.empty(n, HIDDEN, dtype=torch.float32, device=dev) if keep_r else None
             z2 = torch.empty(n, HIDDEN, dtype=torch.float32, device=dev)
-            meta = {"n": n, "e": graph.edge_capacity(), "d_in": d_in, "r": r is not None}
+            meta = {"n": n, "e": graph.edge_capacity(), "d_in": d_in, "r": r is not None,
+                    "agg": agg is not None}
             stat = torch.empty(4, HIDDEN, dtype=torch.float32, device=dev)
             track = training and bn.track_running_stats
             momentum = float(bn.momentum if bn.momentum is not None else 0.1)
@@ -625,15 +655,28 @@ class _GinEncoder(torch.autograd.Function):
         # products (scgib_gin_layer_bwd need_w = 0; same data gradients, bitwise)
         need = getattr(ctx, "need", None)
         dagg_next, dwt = None, None
+        # an agg-free layer l + 1 hands layer l's statistics launch its dz1,
+        # W1 and the row of its weight gradient dW1 lands in
+        dz1_next = w1_next = wgrad_next = None  # (wgrad_next None: layer l + 1 is frozen)
         nslab = int(_lib.query("scgib_gin_bwd_slabs", n))
         jobs, keep = [], []
-        fold = None  # the previous layer's slab job, reduced by the next stats launch
-        fold_slab = None  # its slab: released once that launch is enqueued (the
-        # allocator may then reuse the block for later tensors of this stream)
+        # slab jobs waiting to be reduced by the next statistics launch's extra
+        # workgroups (one for scgib_gin_bwd_stats_bn_fold, two for
+        # scgib_gin_bwd_stats_z), with their slabs: released once that launch
+        # is enqueued (the allocator may then reuse the blocks for later
+        # tensors of this stream); whatever is left goes to the final reduce
+        pend_jobs = []
+        w1_fold = None  # the dW1 partials job for the agg-free layer backward next
+
+        def take_folds(k):
+            got = pend_jobs[:k]
+            del pend_jobs[:k]
+            return got
+
         for l in reversed(range(L)):
             agg, r, z2, stat = saved[4 * l: 4 * l + 4]  # r None: recomputed by the kernel
             w1, b1, w2 = params[6 * l], params[6 * l + 1], params[6 * l + 2]
-            d_in = agg.shape[1]
+            d_in = agg.shape[1] if agg is not None else HIDDEN  # (agg None: an agg-free layer)
             # (the previous layer's dy and slab are no longer read by anything
             # not yet enqueued: released before the new allocations, whose
             # blocks the captured step can then reuse)
@@ -642,13 +685,13 @@ class _GinEncoder(torch.autograd.Function):
             bn_g = torch.empty(2, HIDDEN, dtype=torch.float32, device=dev)  # dgamma, dbeta
             coef = torch.empty(2, HIDDEN, dtype=torch.float32, device=dev)
             # dy, tile sums and the BN-backward finalize in one launch
-            if dagg_next is None and g_readout is not None:
+            if dagg_next is None and dz1_next is None and g_readout is not None:
                 # the readout's broadcast backward folded into the last layer
                 _launch("scgib_gin_bwd_stats_seg_bn", {"n": n, "e": 0, "d_in": HIDDEN}, _p(g_out), _p(g_readout),
                         _p(ctx.seg), _p(z2), _p(stat), n, int(ctx.training), _p(dy),
                         _p(bn_g[0]), _p(bn_g[1]), _p(coef), _p(bn_ws), _p(cnt), _p(gr.dims),
                         defer, st)
-            elif dagg_next is None:
+            elif dagg_next is None and dz1_next is None:
                 # (first_fold: a loss-section slab job handed over by the encoder
                 # pair — reduced in extra workgroups here, its slab then released)
                 ff = getattr(ctx, "first_fold", None)
@@ -658,13 +701,49 @@ class _GinEncoder(torch.autograd.Function):
                         _p(bn_g[0]), _p(bn_g[1]), _p(coef), _p(bn_ws), _p(cnt), _p(gr.dims),
                         defer, _byref(ff[0] if ff else None), st)
                 ff = None
+            elif dz1_next is not None:
+                # layer l + 1 is agg-free: gather its dz1, d h_l = g W1_{l+1},
+                # and dW1_{l+1} = g^T h_l as per-workgroup partials
+                nz = int(_lib.query("scgib_gin_bwd_stats_z_slabs", n))
+                wgn = wgrad_next is not None
+                wslab = torch.empty(nz * HIDDEN * HIDDEN, dtype=torch.float32,
+                                    device=dev) if wgn else None
+                # (no folds when the walk fills the chip's two slots per CU: the
+                # extra workgroups would wait for a second wave; the pending jobs
+                # then go to the next agg-free layer backward, or the final reduce)
+                room = 2 * 256 - nz
+                folds = []
+                while pend_jobs and room >= (pend_jobs[0][0].width + 63) // 64:
+                    room -= (pend_jobs[0][0].width + 63) // 64
+                    folds += take_folds(1)
+                table = (_lib.SlabJob * max(len(folds), 1))(*[j for j, _ in folds])
+                _launch("scgib_gin_bwd_stats_z", {"n": n, "e": gr.edge_capacity(), "d_in": HIDDEN,
+                                                  "z": True, "wg": wgn},
+                        _p(dz1_next), _p(gr.rowptr_t), _p(gr.col_t), ctx.opes[l + 1],
+                        _p(w1_next), _p(z2), _p(stat), n, int(ctx.training), _p(dy), _p(bn_g[0]),
+                        _p(bn_g[1]), _p(coef), _p(bn_ws), _p(cnt), _p(gr.dims), defer,
+                        _p(wslab), int(wgn), ctypes.cast(table, ctypes.c_void_p), len(folds), st)
+                folds = table = None
+                if wgn:  # dW1_{l+1} lands after its dW2 | db2 | db1 (wgrad_next's layout)
+                    job = _lib.SlabJob(wslab.data_ptr(), wgrad_next.data_ptr() + 4 * _Z_W1_OFF,
+                                       HIDDEN * HIDDEN, nz, 0)
+                    # (one partial per walking workgroup — per tile at small batches:
+                    # reduced by this layer's agg-free backward, the next launch,
+                    # whose grid leaves room; else with the chain's final reduce)
+                    if FOLD_SLABS and agg is None:
+                        w1_fold = (job, wslab)
+                    else:
+                        jobs.append(job)
+                        keep.append(wslab)
+                wslab = dz1_next = w1_next = wgrad_next = None
             else:
+                folds = take_folds(1)
                 _launch("scgib_gin_bwd_stats_bn_fold", {"n": n, "e": gr.edge_capacity(), "d_in": HIDDEN},
                         _p(dagg_next), _p(gr.rowptr_t),
                         _p(gr.col_t), ctx.opes[l + 1], _p(z2), _p(stat), n, int(ctx.training),
                         _p(dy), _p(bn_g[0]), _p(bn_g[1]), _p(coef), _p(bn_ws), _p(cnt),
-                        _p(gr.dims), defer, _byref(fold), st)
-                fold = fold_slab = dagg_next = None
+                        _p(gr.dims), defer, _byref(folds[0][0] if folds else None), st)
+                folds = dagg_next = None
             bpend = _lib.BnBwdPending(gpart, bn_g[0].data_ptr(), bn_g[1].data_ptr(),
                                       int(ctx.training)) if defer else None
             meta = {"n": n, "e": gr.edge_capacity(), "d_in": d_in, "r": r is not None}
@@ -674,6 +753,36 @@ class _GinEncoder(torch.autograd.Function):
             wg = need is None or any(need[6 * l: 6 * l + 4]) or r is None or \
                 (d_in != HIDDEN and not (pre and l == 0))
             meta["wg"] = wg
+            grads[6 * l + 4] = bn_g[0]
+            grads[6 * l + 5] = bn_g[1]
+            if agg is None:
+                # agg-free: dz1 out, dW2 | db2 | db1 here, dW1 from layer l - 1's
+                # statistics launch (always one: l >= 1); a frozen layer (not
+                # wg): the same dz1 chain, no weight products
+                meta["z"] = True
+                nsz = int(_lib.query("scgib_gin_layer_bwd_z_slabs", n))
+                slab = torch.empty(nsz * _Z_SLAB, dtype=torch.float32, device=dev) if wg else None
+                dz1 = torch.empty(n, HIDDEN, dtype=torch.float32, device=dev)
+                f2 = take_folds(1)  # the previous agg-free layer's dW2 | db slab (pend)
+                _launch("scgib_gin_layer_bwd_z", meta, _p(dy), _p(z2), _p(r), _p(stat), _p(coef),
+                        _p(w2c), n, _p(dz1), _p(slab), int(wg), _p(gr.dims), _byref(bpend),
+                        _byref(w1_fold[0] if w1_fold else None), _byref(f2[0][0] if f2 else None),
+                        st)
+                w1_fold = f2 = None
+                wgrad = None
+                if wg:
+                    wgrad = torch.empty(_Z_SLAB + HIDDEN * HIDDEN, dtype=torch.float32,
+                                        device=dev)
+                    pend_jobs.append((_lib.SlabJob(slab.data_ptr(), wgrad.data_ptr(), _Z_SLAB,
+                                                   nsz, 0), slab))
+                    grads[6 * l + 2] = wgrad[:HIDDEN * HIDDEN].view(HIDDEN, HIDDEN)
+                    grads[6 * l + 3] = wgrad[HIDDEN * HIDDEN:HIDDEN * HIDDEN + HIDDEN]
+                    grads[6 * l + 1] = wgrad[HIDDEN * HIDDEN + HIDDEN:_Z_SLAB]
+                    grads[6 * l + 0] = wgrad[_Z_W1_OFF:].view(HIDDEN, HIDDEN)
+                dz1_next, w1_next, wgrad_next = dz1, w1c, wgrad
+                slab = dz1 = wgrad = None
+                yield
+                continue
             if pre and l == 0:
                 width = int(_lib.query("scgib_gin_layer0_slab_width"))
                 # (dwt_row: one spare row whose d Wt columns another encoder's
@@ -693,8 +802,6 @@ class _GinEncoder(torch.autograd.Function):
                 _launch("scgib_gin_layer_bwd", meta, _p(dy), _p(z2), _p(r), _p(agg), d_in,
                         _p(stat), _p(coef), _p(w1c), _p(b1c), _p(w2c), n, _p(dagg), _p(slab),
                         _NULL, int(wg), _p(gr.dims), _byref(bpend), st)
-            grads[6 * l + 4] = bn_g[0]
-            grads[6 * l + 5] = bn_g[1]
             if not wg:  # no weight gradients: only layer 0's dWt (its slab's tail)
                 if pre and l == 0:
                     o = HIDDEN * HIDDEN + HIDDEN * d_in + 2 * HIDDEN
@@ -732,7 +839,7 @@ class _GinEncoder(torch.autograd.Function):
                 ns = int(_lib.query("scgib_gin_layer_bwd_slabs", n, d_in))
                 job = _lib.SlabJob(slab.data_ptr(), wgrad.data_ptr(), width, ns, 0)
                 if FOLD_SLABS and l > 0:
-                    fold, fold_slab = job, slab  # reduced by the next layer's launch
+                    pend_jobs.append((job, slab))
                 else:
                     jobs.append(job)
                     keep.append(slab)
@@ -747,6 +854,10 @@ class _GinEncoder(torch.autograd.Function):
                 dwt = wgrad[o:o + 32 * ctx.n_feat].view(32, ctx.n_feat)
             dagg_next = dagg
             yield
+        for job, sl in pend_jobs:  # (none past layer 0's statistics launch as a rule)
+            jobs.append(job)
+            keep.append(sl)
+        pend_jobs = None
         extra = getattr(ctx, "extra_jobs", None)
         if extra is not None:  # deferred loss-section slabs (SlabScope), same launch
             ctx.extra_jobs = None

@@ -17,7 +17,7 @@ import pytest
 import torch
 import torch.nn.functional as F
 
-from conftest import check_grads_model, rel_err
+from conftest import CANCELLED, check_grads_model, rel_err, rel_l2
 
 pytestmark = pytest.mark.gpu
 
@@ -160,7 +160,9 @@ def test_capacity_step_r_recompute_bitwise(pkg, dev, monkeypatch):
     """The whole pretrain step in capacity mode (padded rows, device dims:
     the recompute kernels' zero-padding and clamped-row paths) with the
     hidden activation r recomputed in the backward vs stored by the forward
-    (ops.STORE_R): losses, every gradient and BN buffer bitwise equal."""
+    (ops.STORE_R): losses, every gradient and BN buffer bitwise equal.  (Both
+    on the stored-agg backward, ops.AGG_FREE off: the recompute reads agg.)"""
+    monkeypatch.setattr(pkg.ops, "AGG_FREE", False)
     hosts = _batches(pkg, (21, 22))
     n_cap, e_cap, mgn, caps = pkg.graph.StaticBatch.capacities(hosts, 1, slack=1.05)
     static = pkg.graph.StaticBatch(B, n_cap, e_cap, F_IN, mgn, caps, dev)
@@ -182,6 +184,47 @@ def test_capacity_step_r_recompute_bitwise(pkg, dev, monkeypatch):
     assert ga.keys() == gb.keys()
     for k in ga:
         assert torch.equal(ga[k], gb[k]), k
+    for k in ba:
+        assert torch.equal(ba[k], bb[k]), k
+
+
+def test_capacity_step_agg_free_matches_stored_agg(pkg, dev, monkeypatch):
+    """the agg-free layers (ops.AGG_FREE: no agg stored,
+    dz1 out of the layer backward, dW1 = g^T h and d h = g W1 in the layer
+    below's statistics launch) against the stored-agg backward, on the whole
+    pretrain step in capacity mode over two batches: the forward is the same
+    kernels minus a store, so losses and every BatchNorm buffer are bitwise
+    equal; the gradients associate the same sums differently — every tensor
+    within 2e-5 relative L2 (the rounding-only bound; a wrong product or
+    index is O(1))."""
+    monkeypatch.setattr(pkg.ops, "AGG_FREE_MIN_ROWS", 0)  # (every encoder, whatever its size)
+    hosts = _batches(pkg, (23, 24))
+    n_cap, e_cap, mgn, caps = pkg.graph.StaticBatch.capacities(hosts, 1, slack=1.05)
+    static = pkg.graph.StaticBatch(B, n_cap, e_cap, F_IN, mgn, caps, dev)
+    base = _model(pkg, dev)
+    res = []
+    for free in (True, False):
+        monkeypatch.setattr(pkg.ops, "AGG_FREE", free)
+        m = copy.deepcopy(base)
+        losses = []
+        for i, gh in enumerate(hosts):
+            static.load(static.pad(gh))
+            losses.append(_step(m, static.graph, static.x, _noise(n_cap, dev, 400 + i), dev))
+        torch.cuda.synchronize()
+        res.append((torch.stack(losses), {k: p.grad.clone() for k, p in m.named_parameters()
+                                          if p.grad is not None},
+                    {k: b.clone() for k, b in m.named_buffers()}))
+    (la, ga, ba), (lb, gb, bb) = res
+    assert torch.equal(la, lb)
+    assert ga.keys() == gb.keys()
+    worst = 0.0
+    for k in ga:
+        if k.endswith(CANCELLED):  # rounding noise on both sides
+            continue
+        e = rel_l2(ga[k].cpu(), gb[k].cpu())
+        worst = max(worst, e)
+        assert e < 2e-5, (k, e)
+    print(f"agg-free vs stored agg: worst gradient rel-L2 {worst:.2e}")
     for k in ba:
         assert torch.equal(ba[k], bb[k]), k
 

@@ -193,12 +193,17 @@ def test_finetune_config_graph_replay(pkg, dev, case):
     _check(c, ft, scores, loss.item())
 
 
-def test_frozen_layers_skip_weight_grads_bitwise(pkg, dev, case):
+@pytest.mark.parametrize("agg_free", [False, True])
+def test_frozen_layers_skip_weight_grads_bitwise(pkg, dev, case, agg_free, monkeypatch):
     """The frozen GIN layers' backward skips the weight products
     (scgib_gin_layer_bwd / _layer0_bwd need_w = 0): the
     trainable gradients (transfer_d through layer 0, ginlayers.2, the head)
     are bitwise those of the same step with every parameter trainable, and
-    the frozen ones still get none."""
+    the frozen ones still get none.  agg_free: the agg-free layers forced on
+    at this size (ops.AGG_FREE_MIN_ROWS = 0): a frozen layer runs
+    scgib_gin_layer_bwd_z / scgib_gin_bwd_stats_z with need_w = 0."""
+    if agg_free:
+        monkeypatch.setattr(pkg.ops, "AGG_FREE_MIN_ROWS", 0)
     c = case
     g = c["gh"].to(dev)
     x = F.normalize(g.ndata["x"].float())

@@ -914,8 +914,9 @@ def test_gin_r_recompute_bitwise(pkg, dev, via_ego, n_mols):
     outs = []
     for store in (True, False):
         gin_c, lin_c = copy.deepcopy(gin), copy.deepcopy(lin)
-        old = pkg.ops.STORE_R
-        pkg.ops.STORE_R = store
+        old = pkg.ops.STORE_R, pkg.ops.AGG_FREE
+        # (both on the stored-agg backward: the recompute reads agg)
+        pkg.ops.STORE_R, pkg.ops.AGG_FREE = store, False
         try:
             h = pkg.ops.gin_encoder_x(x, target, gin_c, lin_c, nmap)
             t = h.grad_fn.saved_tensors
@@ -929,7 +930,7 @@ def test_gin_r_recompute_bitwise(pkg, dev, via_ego, n_mols):
                 assert all(t[4 * l + 1] is None for l in range(5))
             (h * w).sum().backward()
         finally:
-            pkg.ops.STORE_R = old
+            pkg.ops.STORE_R, pkg.ops.AGG_FREE = old
         torch.cuda.synchronize()
         outs.append((h.detach(), {k: p.grad for k, p in list(gin_c.named_parameters())
                                   + [("wt", lin_c.weight)]},
@@ -938,6 +939,60 @@ def test_gin_r_recompute_bitwise(pkg, dev, via_ego, n_mols):
     assert torch.equal(ha, hb)
     for k in ga:
         assert torch.equal(ga[k], gb[k]), k
+    for k in ba:
+        assert torch.equal(ba[k], bb[k]), k
+
+
+@pytest.mark.parametrize("fold,n_mols", [(False, 40), (True, 40), (True, 200), (True, 1500)])
+def test_gin_agg_free_matches_stored_agg(pkg, dev, fold, n_mols, monkeypatch):
+    """VERDICT r05 item 3 at the encoder: ops.AGG_FREE (layers 1..4 store no
+    agg; scgib_gin_layer_bwd_z + scgib_gin_bwd_stats_z) against the stored-agg
+    backward — with transfer_d folded (fold: the ego-net chain of the step;
+    1500 molecules: ~80 k rows, the statistics walk takes 3 tiles per
+    workgroup) and on a plain GIN over given h0 (layer 0 then a regular d_in =
+    64 layer whose d(agg) feeds the final transposed aggregation).  Output and
+    BN buffers bitwise (the forward differs by a store), gradients (dWt / dh0
+    included) within 2e-5 relative L2."""
+    import copy
+    monkeypatch.setattr(pkg.ops, "AGG_FREE_MIN_ROWS", 0)  # (every encoder, whatever its size)
+    torch.manual_seed(19)
+    g, _ = rand_graph(pkg, n_mols, "qm9", 17, dev)
+    target = pkg.graph.egonet_batch(g, 1) if fold else g
+    nmap = target.ndata["_ID"] if fold else None
+    n = target.num_nodes()
+    x = F.normalize(torch.rand(g.num_nodes(), 11)).to(dev)
+    h0 = torch.randn(n, 64, device=dev)
+    lin = torch.nn.Linear(11, 32, bias=False).to(dev)
+    gin = pkg.models.GIN(32 if fold else 64, 64, 5).to(dev).train()
+    with torch.no_grad():
+        for bn in gin.batch_norms:
+            bn.weight.add_(0.2 * torch.randn(64, device=dev))
+            bn.bias.add_(0.2 * torch.randn(64, device=dev))
+    w = torch.randn(n, 64, device=dev)
+    outs = []
+    for free in (True, False):
+        gin_c, lin_c = copy.deepcopy(gin), copy.deepcopy(lin)
+        old = pkg.ops.AGG_FREE
+        pkg.ops.AGG_FREE = free
+        try:
+            hin = None if fold else h0.clone().requires_grad_(True)
+            h = (pkg.ops.gin_encoder_x(x, target, gin_c, lin_c, nmap) if fold
+                 else pkg.ops.gin_encoder(hin, target, gin_c))
+            t = h.grad_fn.saved_tensors
+            assert all((t[4 * l] is None) == (free and l >= 1) for l in range(5))
+            (h * w).sum().backward()
+        finally:
+            pkg.ops.AGG_FREE = old
+        torch.cuda.synchronize()
+        grads = {k: p.grad for k, p in gin_c.named_parameters()}
+        grads["in"] = lin_c.weight.grad if fold else hin.grad
+        outs.append((h.detach(), grads, {k: b.clone() for k, b in gin_c.named_buffers()}))
+    (ha, ga, ba), (hb, gb, bb) = outs
+    assert torch.equal(ha, hb)
+    for k in ga:
+        if k.endswith(CANCELLED):
+            continue
+        assert rel_l2(ga[k].cpu(), gb[k].cpu()) < 2e-5, (k, rel_l2(ga[k].cpu(), gb[k].cpu()))
     for k in ba:
         assert torch.equal(ba[k], bb[k]), k
 

@@ -19,6 +19,6 @@ python tools/sb_evidence.py $O/kt $O/pmc $O/sb_evidence.json > $O/sb_evidence.tx
 SCGIB_SB_EVIDENCE_FILE=$O/sb_evidence.json timeout -k 10 300 python bench.py --superbatch-only > $O/sb_line.log 2>&1 || { echo "sb line failed"; exit 1; }
 tail -1 $O/sb_line.log | python -c "
 import sys,json; sb=json.loads(sys.stdin.read())['roofline_superbatch']
-for k in ('gin_fwd_k','gin_bwd_stats_k','gin_bwd5_k','gin_aggregate_k'):
+for k in ('gin_fwd_k','gin_fwd_k_agg_free','gin_bwd_stats_k','gin_bwd_statsz_k','gin_bwd5_k','gin_bwd5z_k','gin_aggregate_k'):
     e=sb.get(k) or {}; print(k, {kk: e.get(kk) for kk in ('us','trace_avg_us','trace_vs_event','frac','bytes','traffic','traffic_over_algorithmic','hbm_frac_measured')})"
 echo done

@@ -33,6 +33,10 @@ PHASES = {
     "scgib_gin_layer_bwd_fused": ["prologue", "dz2", "pairA", "pairB", "rest", "stats", "bn_hier"],
     "scgib_gin_layer0_bwd": ["ld+dz2", "dW2,dr", "dW1,dagg", "slab"],
     "scgib_gin_bwd_stats_bn": ["gather+dy", "bn_hier"],
+    # the agg-free pair (ops.AGG_FREE): the statistics walk's first tile, then
+    # its dW1 slab + BN arrivals; the layer backward as gin_bwd5_k (no pair B)
+    "scgib_gin_bwd_stats_z": ["gather+img", "gemms+stage", "stats", "slab+hier"],
+    "scgib_gin_layer_bwd_z": ["prologue", "dz2", "pairA", "-", "rest", "slab"],
     "scgib_gin_bwd_stats_bn_fold": ["gather+dy", "bn_hier"],
     # head MLP (+ recon) tiles mark 1..3, the contrastive workgroups 5
     # (+ the fused loss finish: published, waited + acquire, then recon_fin.h's

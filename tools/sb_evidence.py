@@ -22,10 +22,15 @@ import sys
 # bench.superbatch_roofline's kernels -> the trace-name prefixes of the launches
 # it times (gin_bwd_stats_k: the gathering instance only, as the bench keeps
 # the launches with e > 0)
+# (a launch may count for two keys: gin_fwd_k averages all five d = 64
+# layers, gin_fwd_k_agg_free the four XFORM ones, which are agg-free)
 KERNELS = {
     "gin_fwd_k": ("gin_fwd_k<64,",),
+    "gin_fwd_k_agg_free": ("gin_fwd_k<64, true,",),
     "gin_bwd_stats_k": ("gin_bwd_stats_k<true,",),
+    "gin_bwd_statsz_k": ("gin_bwd_statsz_k<true>",),
     "gin_bwd5_k": ("gin_bwd5_k<64", "gin_bwd5r_k<64"),
+    "gin_bwd5z_k": ("gin_bwd5z_k<true>",),
     "gin_aggregate_k": ("gin_aggregate_k<",),
 }
 
@@ -34,19 +39,15 @@ def _name(raw):
     return raw.split("(")[0].replace("void ", "").replace("scgib::", "").strip()
 
 
-def _kernel_of(name):
-    for key, prefixes in KERNELS.items():
-        if name.startswith(prefixes):
-            return key
-    return None
+def _kernels_of(name):
+    return [key for key, prefixes in KERNELS.items() if name.startswith(prefixes)]
 
 
 def trace(path):
     per = collections.defaultdict(list)
     for fn in glob.glob(os.path.join(path, "**", "*kernel_trace.csv"), recursive=True):
         for r in csv.DictReader(open(fn)):
-            k = _kernel_of(_name(r["Kernel_Name"]))
-            if k:
+            for k in _kernels_of(_name(r["Kernel_Name"])):
                 per[k].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
     return per
 
@@ -58,8 +59,7 @@ def pmc(path, counter):
         for r in csv.DictReader(open(fn)):
             if r.get("Counter_Name") != counter:
                 continue
-            k = _kernel_of(_name(r["Kernel_Name"]))
-            if k:
+            for k in _kernels_of(_name(r["Kernel_Name"])):
                 per[k].append(float(r["Counter_Value"]) * 1024.0)  # KB -> bytes
     return per
 

@@ -836,6 +836,26 @@ def build_replay_step(model, opt, pool_host, k, batch, dev, prefetch=True, noise
                            graph=graph, graph_nodes=nodes)
 
 
+def set_side_cu_mask(dev, k):
+    """The encoder pair's side stream (models._side_stream) as a HIP stream
+    restricted to the device's last k CUs (hipExtStreamCreateWithCUMask;
+    tools/cumask_probe.hip: a captured node keeps its stream's mask when the
+    graph is replayed on another stream, as torch replays it)."""
+    import ctypes
+    hip = ctypes.CDLL("libamdhip64.so")
+    ncu = torch.cuda.get_device_properties(dev).multi_processor_count
+    words = (ncu + 31) // 32
+    mask = (ctypes.c_uint32 * words)()
+    for i in range(ncu - k, ncu):
+        mask[i // 32] |= 1 << (i % 32)
+    s = ctypes.c_void_p()
+    if hip.hipExtStreamCreateWithCUMask(ctypes.byref(s), words, mask) != 0:
+        raise SystemExit("hipExtStreamCreateWithCUMask failed")
+    ext = torch.cuda.ExternalStream(s.value, device=dev)
+    pkg.models._SIDE_STREAMS[dev.index] = pkg.ops.register_fork_stream(ext)
+    progress(f"side stream on CUs [{ncu - k}, {ncu})")
+
+
 def graph_node_counts(graph):
     """{kernel, memcpy, memset, other, total} nodes of a captured torch
     CUDAGraph (hipGraphGetNodes + hipGraphNodeGetType through ops), or None
@@ -888,6 +908,9 @@ def main():
     ap.add_argument("--agg-free-min-rows", type=int, default=None,
                     help="encoders of at least this many rows run agg-free "
                          "(ops.AGG_FREE_MIN_ROWS; 0: every encoder; A/B)")
+    ap.add_argument("--side-cu-mask", type=int, default=0,
+                    help="probe (VERDICT r05 item 4): the encoder pair's side stream made with "
+                         "hipExtStreamCreateWithCUMask on the last K CUs (0: an ordinary stream)")
     ap.add_argument("--finetune", choices=["molhiv"], default=None,
                     help="time the fine-tune step of BASELINE.json configs[4] instead "
                          "(finetune_bench.py; --batch defaults to 32 there)")
@@ -941,6 +964,8 @@ def main():
     pkg.ops.XQ_FLAGS, pkg.ops.XQ_REASON = xq_ok, xq_why
     if xq_ok and a.no_handoffs:
         pkg.ops.XQ_FLAGS, pkg.ops.XQ_REASON = False, "--no-handoffs"
+    if a.side_cu_mask:
+        set_side_cu_mask(dev, a.side_cu_mask)
     torch.manual_seed(1234 + rank)
     global RUN_CONFIG
     RUN_CONFIG = {"workload": a.workload, "batch": a.batch, "k": a.k}

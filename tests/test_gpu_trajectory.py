@@ -42,10 +42,11 @@ pretrain run (lr 1e-4, 8 steps) is held to the 1e-4 loss bar free-running too.
 Bars (written here): losses and scores within 1e-4 relative (north star);
 parameters within 2e-3 per-tensor relative L2; the step's update (theta_new -
 theta_old) of the well-conditioned elements within 2e-2 (COND below); the
-gradient each Adam took (from its first moment) by check_grads_model's rule
-(5e-3 per tensor of >= 4096 elements, cosine 0.999 on every tensor, 1e-3 over
-all tensors together: GRAD_TOL's note); the second moment within 2e-3 per tensor of >= 4096 elements, 5e-3
-per smaller one; both moments within 1e-3 over all tensors together; every BatchNorm running statistic within 1e-4
+gradient each Adam took (from its first moment) within 1e-2 per tensor of >=
+4096 elements, cosine 0.999 on every tensor and 3e-3 over all tensors
+together (ReLU-tie bars: GRAD_TOL's note); the second moment within 2e-3 per
+tensor of >= 4096 elements, 5e-3 per smaller one; both moments within 1e-3
+over all tensors together; every BatchNorm running statistic within 1e-4
 relative; num_batches_tracked and Adam's step exact; the eval ROC-AUC within
 1e-6 of the oracle's, widened only by the pairs whose oracle scores lie within
 the score tolerance of each other (a swap there is a tie of two correct fp32
@@ -78,17 +79,19 @@ PARAM_TOL = 2e-3
 # fine-tune weight whose gradient matched to 3e-4), so the moments are held
 # per tensor only where they are the better-conditioned quantity (exp_avg_sq,
 # MOMENT_TOL) and together (MOMENT_TOL_ALL, every tensor concatenated)
-# Per tensor the bars are conftest.check_grads_model's whole-model rule
-# (5e-3 on the >= 4096-element matrices, cosine 0.999 on every tensor, 1e-3
-# over all tensors together): over 20 fine-tune steps of 32 molecules a
-# hidden unit whose pre-activation sits within rounding of 0 for one row
-# decides differently in two correct fp32 evaluations now and then (measured:
-# 3.0e-3 on both weight matrices of Encoder2.ginlayers.2 at step 13, every
-# other step and tensor <= 1.3e-3); the single-step config tests hold their
-# fixed seeds to 2e-3
-GRAD_TOL = 5e-3
+# The gradient each Adam took is held to bars for ReLU-tie noise, not for
+# rounding: a hidden unit whose pre-activation sits within rounding of 0 for a
+# row decides differently in two correct fp32 evaluations, moving that
+# layer's weight gradients by one row's contribution — at the fine-tune's 32
+# molecules, where only ginlayers.2 trains, by up to 6.1e-3 per tensor and
+# 1.8e-3 over all tensors in one step (measured, step 1; the pretrain step at
+# B512: 1.4e-3 over all tensors).  The single-step config tests hold fixed
+# seeds to 2e-3; here 28 steps of fresh parameters sample many more ties.
+# A structural error (a misaligned batch, a stale BatchNorm record, a wrong
+# Adam state) moves a gradient by O(1) and its cosine far below 0.999.
+GRAD_TOL = 1e-2
 GRAD_TOL_SMALL = None  # (under BIG elements: the cosine and the concatenation only)
-GRAD_TOL_ALL = 1e-3
+GRAD_TOL_ALL = 3e-3
 COS_MIN = 0.999
 MOMENT_TOL = 2e-3
 # a tensor under BIG elements (the 64-element biases, BatchNorm affines): one

@@ -713,7 +713,7 @@ def finetune_leg(a, dev):
 
 
 def build_replay_step(model, opt, pool_host, k, batch, dev, prefetch=True, noise=None,
-                      collective=False, reducer=None, warm=3):
+                      collective=False, reducer=None, warm=3, split=True):
     """The bench's pretrain step (exp_pretraining.py:290-333) as ONE captured
     HIP graph in capacity mode: the pool's next resident batch (and the ego-nets
     the previous step built for it) loaded inside the graph, forward, backward,
@@ -722,9 +722,12 @@ def build_replay_step(model, opt, pool_host, k, batch, dev, prefetch=True, noise
     ``noise`` = (u_gate [n_cap], u_feat [n_cap, 64]) static device buffers the
     step reads instead of drawing its own (tests/test_gpu_trajectory.py fills
     them before each replay); None = the device Philox draws of every replay.
+    ``split``: replay the captured graph as two linear lanes (ops.SplitGraph:
+    ~6 us of host enqueue per lane instead of ~3 us per node) where the
+    hand-off rule allows and the graph is one launch.
     Returns step(i), the static losses (kl, rec, con), the static batch, the
-    device pool and its prefetch, the all-reduce mode and the node count of
-    the captured graph."""
+    device pool and its prefetch, the all-reduce mode, the node count of the
+    captured graph and the split (None: the captured graph is replayed)."""
     n_cap, e_cap, mgn, ego_caps = pkg.graph.StaticBatch.capacities(pool_host, k, slack=1.02)
     F_in = pool_host[0].ndata["x"].shape[1]
     static = pkg.graph.StaticBatch(batch, n_cap, e_cap, F_in, mgn, ego_caps, dev, k=k)
@@ -822,18 +825,41 @@ def build_replay_step(model, opt, pool_host, k, batch, dev, prefetch=True, noise
             opt.step()
         allreduce_mode = "between two graph replays"
     nodes = graph_node_counts(graph)
-    graph.instantiate()
+    lanes = split_graph(graph, dev) if (split and graph2 is None) else None
+    if lanes is None:
+        graph.instantiate()
 
     def step(i):
+        if lanes is not None:
+            lanes.replay()
+            return static_loss
         graph.replay()
         if graph2 is not None:  # RCCL all-reduce of the bucket between the two replays
             reducer.reduce(force=True)
             graph2.replay()
         return static_loss
 
+    # `one` is read by the captured backward through its device pointer only:
+    # the namespace holds it, or the allocator would hand its block to the next
+    # allocation and the replays would seed the backward with whatever lands there
     return SimpleNamespace(step=step, loss=static_loss, static=static, pool=pool_dev,
                            padded=padded, prefetch=pf, allreduce_mode=allreduce_mode,
-                           graph=graph, graph_nodes=nodes)
+                           graph=graph, graph_nodes=nodes, split=lanes, one=one)
+
+
+def split_graph(graph, dev):
+    """ops.SplitGraph of a captured step (two linear lanes), or None where the
+    hand-offs are off (serialised dispatch: a kernel trace, PMC) or the graph
+    does not split (a non-kernel node, e.g. a captured RCCL all-reduce)."""
+    if not pkg.ops.xq_enabled():
+        return None
+    try:
+        lanes = pkg.ops.SplitGraph(graph, dev)
+    except pkg.ops.SplitUnsupported as exc:
+        progress(f"graph replayed whole: {exc}")
+        return None
+    progress(f"graph split into two lanes: {lanes.info}")
+    return lanes
 
 
 def set_side_cu_mask(dev, k):
@@ -894,6 +920,9 @@ def main():
                     help="skip the event-timed kernel pass (PMC runs: only real step launches)")
     ap.add_argument("--eager", action="store_true",
                     help="launch every kernel from Python (no HIP-graph capture)")
+    ap.add_argument("--no-split", action="store_true",
+                    help="replay the captured step graph whole instead of as two linear lanes "
+                         "(ops.SplitGraph; A/B of the host enqueue)")
     ap.add_argument("--no-ego-prefetch", action="store_true",
                     help="build each step's ego-nets at the head of the step instead of one "
                          "batch ahead (graph.EgoPrefetch; A/B)")
@@ -1013,8 +1042,12 @@ def main():
             opt = pkg.optim.Adam(model.parameters(), lr=1e-4, weight_decay=5e-5)
         rs = build_replay_step(model, opt, pool_host, a.k, a.batch, dev,
                                prefetch=not a.no_ego_prefetch, collective=collective,
-                               reducer=reducer)
+                               reducer=reducer, split=not a.no_split)
         step, allreduce_mode, graph_nodes = rs.step, rs.allreduce_mode, rs.graph_nodes
+        if graph_nodes is not None:  # the replayed lanes (ops.SplitGraph), or the whole graph
+            graph_nodes = dict(graph_nodes, replay=(
+                {k: rs.split.info[k] for k in ("lane0_nodes", "lane1_nodes", "handoffs")}
+                if rs.split is not None else "whole graph"))
 
     for i in range(a.warmup):
         step(i)
@@ -1141,7 +1174,10 @@ def main():
                     f"SURVEY.md §8(d)); random-init weights",
             "config": {"workload": f"{a.workload} pretrain step GIN-64x{a.gin_layers} "
                                    f"k={a.k}, batch {a.batch}/GPU, Mainmodel_continue + Adam",
-                       "launch": "eager" if a.eager else "hip-graph replay (capacity mode)",
+                       "launch": "eager" if a.eager else (
+                           "hip-graph replay (capacity mode)" + (
+                               ", two linear lanes" if isinstance((graph_nodes or {}).get("replay"), dict)
+                               else "")),
                        "ego_build": ("in the step, for the batch the next step loads "
                                      "(graph.EgoPrefetch)" if not a.eager
                                      and not a.no_ego_prefetch else "at the head of the step"),

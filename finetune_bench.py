@@ -116,7 +116,7 @@ def cpu_baseline(bench, ft, host_batches, targets, seconds):
 
 
 def build_finetune_step(pkg, ft, opt, host, targets, k, B, dev, prefetch=True, noise=None,
-                        warm=3):
+                        warm=3, split=True):
     """The fine-tune step (train_molhiv.py:107-152: forward, BCE, backward,
     Adam) as ONE captured HIP graph in capacity mode over a resident pool of
     the host batches ``host`` and their ``targets`` ([B, 1] each): the pool's
@@ -124,8 +124,10 @@ def build_finetune_step(pkg, ft, opt, host, targets, k, B, dev, prefetch=True, n
     it loaded inside the graph.  ``warm`` eager steps on a side stream first
     (allocator, Adam state).  ``noise`` = (u_gate [n_cap], u_feat [n_cap, 64])
     static device buffers the step reads instead of its own device draws
-    (tests/test_gpu_trajectory.py).  Returns the graph, the static scores and
-    loss, the static batch, the device pool and its prefetch."""
+    (tests/test_gpu_trajectory.py).  ``split``: replay as two linear lanes
+    (ops.SplitGraph) where the hand-off rule allows.  Returns replay() (one
+    step), the captured graph, the static scores and loss, the static batch,
+    the device pool and its prefetch."""
     n_cap, e_cap, mgn, caps = pkg.graph.StaticBatch.capacities(host, k, slack=1.02)
     F_in = host[0].ndata["x"].shape[1]
     static = pkg.graph.StaticBatch(B, n_cap, e_cap, F_in, mgn, caps, dev, k=k)
@@ -182,10 +184,23 @@ def build_finetune_step(pkg, ft, opt, host, targets, k, B, dev, prefetch=True, n
         nodes = pkg.ops.graph_node_counts(graph)
     except Exception:  # noqa: BLE001 (diagnostic field only)
         nodes = None
-    graph.instantiate()
-    return SimpleNamespace(graph=graph, scores=scores, loss=loss, static=static, pool=pool,
-                           padded=padded, prefetch=pf, targets=(tdev, ttable, tcursor, tg),
-                           graph_nodes=nodes)
+    lanes = None
+    if split and pkg.ops.xq_enabled():
+        try:
+            lanes = pkg.ops.SplitGraph(graph, dev)
+        except pkg.ops.SplitUnsupported:
+            lanes = None
+    if lanes is None:
+        graph.instantiate()
+    if nodes is not None:
+        nodes = dict(nodes, replay=(
+            {k: lanes.info[k] for k in ("lane0_nodes", "lane1_nodes", "handoffs")}
+            if lanes is not None else "whole graph"))
+    # (`one` held for the captured backward, as bench.build_replay_step does)
+    return SimpleNamespace(replay=lanes.replay if lanes is not None else graph.replay,
+                           graph=graph, split=lanes, scores=scores, loss=loss, static=static,
+                           pool=pool, padded=padded, prefetch=pf,
+                           targets=(tdev, ttable, tcursor, tg), graph_nodes=nodes, one=one)
 
 
 FT_STAMPS_FILE = os.environ.get("SCGIB_FT_STAMPS_FILE",
@@ -241,15 +256,15 @@ def run(bench, a, dev):
     bench.RUN_CONFIG = {"workload": "molhiv-finetune", "batch": B, "k": k}
     opt = pkg.optim.Adam(ft.parameters(), lr=1e-3, weight_decay=1e-5)
     fs = build_finetune_step(pkg, ft, opt, host, targets, k, B, dev,
-                             prefetch=not a.no_ego_prefetch)
-    graph, static_loss, prefetch = fs.graph, fs.loss, fs.prefetch
+                             prefetch=not a.no_ego_prefetch, split=not a.no_split)
+    replay, static_loss, prefetch = fs.replay, fs.loss, fs.prefetch
     for _ in range(a.warmup):
-        graph.replay()
+        replay()
     bench.progress(f"fine-tune warm-up done; timing {a.steps} steps")
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(a.steps):
-        graph.replay()
+        replay()
     t_enq = time.perf_counter() - t0
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0

@@ -98,6 +98,33 @@ int scgib_pool_copy2(const uint64_t *srcs, int32_t n_src, uint32_t *ctr, void *d
 int scgib_stream_signal(uint32_t *words, scgib_stream_t stream);
 int scgib_stream_wait(uint32_t *words, uint32_t *fault, uint32_t *host_fault,
                       scgib_stream_t stream);
+/* Two-lane replay of a captured step graph (ABI 21; DESIGN.md §3, "Host
+ * enqueue"): hipGraphLaunch of a graph with parallel branches costs the host
+ * ~2.5-3 us per node, a linear graph ~6 us in all.  scgib_graph_split takes a
+ * captured hipGraph_t (`graph`; kernel nodes only, else SCGIB_EUNSUPPORTED)
+ * whose DAG is at most two chains wide, assigns its nodes to two lanes along
+ * the captured chains, and builds one linear graph per lane (the kernel nodes
+ * copied; each cross-lane edge becomes a scgib_stream_signal /
+ * scgib_stream_wait kernel pair on its own 4-uint32 slot of `words`,
+ * n_slots slots, zeroed, alive as long as the split; the last 8 slots are
+ * for the queue check below).  `fault` / `host_fault` are the waits' sticky
+ * fault words as for scgib_stream_wait.  `stream`: the caller's stream, the
+ * one every replay must use — the split's non-blocking side stream is
+ * checked at creation to run on another hardware queue than it (a
+ * wait / signal pair across the two; up to 8 streams tried, else
+ * SCGIB_EUNSUPPORTED).  *out receives an opaque handle; info (8 int32, may be
+ * NULL): captured nodes, lane-0 kernels, lane-1 kernels, hand-offs added,
+ * lane-0 nodes, lane-1 nodes, nodes serialised beyond two chains, slots used.
+ * The captured graph's memory must stay alive while the split is used.
+ * scgib_graph_split_launch replays lane 0 on `stream` (the creation stream,
+ * else SCGIB_EINVAL) and lane 1 on the side stream, with one launch's stream
+ * semantics: ordered after earlier work on `stream`, later work on `stream`
+ * ordered after both lanes.  scgib_graph_split_destroy waits for the side
+ * lane and frees it. */
+int scgib_graph_split(void *graph, uint32_t *words, int32_t n_slots, uint32_t *fault,
+                      uint32_t *host_fault, scgib_stream_t stream, void **out, int32_t *info);
+int scgib_graph_split_launch(void *split, scgib_stream_t stream);
+int scgib_graph_split_destroy(void *split);
 /* Diagnostics: writes the 100 MHz device wall clock (s_memrealtime) to
  * buf[slot] when the stream reaches this point (ops.stamps: the timeline of
  * a replayed step with its hand-offs on; not on the product path). */

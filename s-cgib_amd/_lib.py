@@ -35,6 +35,9 @@ SIGNATURES = {
     "scgib_stream_signal": (ctypes.c_int, [_P, _P]),
     "scgib_stamp": (ctypes.c_int, [_P, _I32, _P]),
     "scgib_stream_wait": (ctypes.c_int, [_P, _P, _P, _P]),
+    "scgib_graph_split": (ctypes.c_int, [_P, _P, _I32, _P, _P, _P, _P, _P]),
+    "scgib_graph_split_launch": (ctypes.c_int, [_P, _P]),
+    "scgib_graph_split_destroy": (ctypes.c_int, [_P]),
     "scgib_strerror": (ctypes.c_char_p, [ctypes.c_int]),
     "scgib_gin_aggregate": (ctypes.c_int, [_P, _P, _P, _I64, _I32, _F, _P, _P, _P]),
     "scgib_segment_sum": (ctypes.c_int, [_P, _P, _I64, _I32, _P, _P, _P]),
@@ -187,7 +190,7 @@ class RunningUpdate(ctypes.Structure):
                 ("num_batches_tracked", ctypes.c_void_p)]
 
 
-ABI_VERSION = 20
+ABI_VERSION = 21
 STATS_STRIDE = 260
 PGRAD_STRIDE = 324
 HIDDEN = 64

@@ -220,6 +220,14 @@ __global__ void pool_copy_k(const uint64_t *__restrict__ srcs, int32_t n_src, un
     }
 }
 
+// the hand-off kernels' launch handles, for the two-lane graph split
+// (graph_split.hip), which adds them as kernel nodes and recognises the
+// encoder pair's in-graph ones by them
+void handoff_kernels(const void **signal, const void **wait) {
+    *signal = reinterpret_cast<const void *>(&stream_signal_k);
+    *wait = reinterpret_cast<const void *>(&stream_wait_k);
+}
+
 static bool dim_ok(int32_t dim) {
     return dim >= 4 && dim <= 256 && dim % 4 == 0 && ((dim / 4) & (dim / 4 - 1)) == 0;
 }
@@ -322,7 +330,7 @@ extern "C" int scgib_pool_copy(const uint64_t *srcs, int32_t n_src, uint32_t *ct
     return scgib_pool_copy2(srcs, n_src, ctr, dst, bytes, nullptr, nullptr, 0, stream);
 }
 
-extern "C" int scgib_abi_version(void) { return 20; }
+extern "C" int scgib_abi_version(void) { return 21; }
 
 extern "C" const char *scgib_strerror(int code) {
     if (code == SCGIB_OK) return "ok";

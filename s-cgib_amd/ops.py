@@ -468,6 +468,70 @@ def graph_node_counts(graph):
     return out
 
 
+class SplitUnsupported(_lib.ScgibError):
+    """scgib_graph_split refused the graph (a non-kernel node, or an in-graph
+    hand-off the two lanes cannot keep): replay the captured graph instead."""
+
+
+_SPLIT_SLOTS = 64  # hand-off slots per split (the pretraining step uses 2-3)
+_LIVE_SPLITS = weakref.WeakSet()
+
+
+class SplitGraph:
+    """A captured step graph replayed as two linear lanes (csrc/graph_split.hip,
+    include/scgib.h scgib_graph_split): the host enqueues ~6 us per lane
+    instead of ~3 us per node of a two-branch graph (tools/graph_launch_probe.hip,
+    DESIGN.md §3 "Host enqueue").  Built from a torch.cuda.CUDAGraph captured
+    with keep_graph=True; the torch graph is kept (its memory pool holds the
+    step's buffers) and never replayed.  Replays go on the stream current at
+    construction (the side stream was checked against its hardware queue).  The lanes' waits rely on two
+    concurrently running queues like the encoder pair's hand-offs, so callers
+    split only when xq_enabled() holds (a kernel trace serialises dispatch)."""
+
+    def __init__(self, graph, device):
+        dev = torch.device(device)
+        self.graph = graph
+        self.words = torch.zeros(4 * _SPLIT_SLOTS, dtype=torch.int32, device=dev)
+        self._fault = handoff_fault_word(dev)
+        self._host = _host_fault_word(dev)
+        # the side lane reads its slots at once: the zero fill must have landed
+        torch.cuda.synchronize(dev)
+        handle = ctypes.c_void_p()
+        info = (ctypes.c_int32 * 8)()
+        rc = _lib.load().scgib_graph_split(
+            ctypes.c_void_p(graph.raw_cuda_graph()), _p(self.words), _SPLIT_SLOTS, _p(self._fault),
+            _p(self._host), _stream(), ctypes.byref(handle), info)
+        if rc == -2:
+            raise SplitUnsupported("scgib_graph_split: graph not splittable into two lanes")
+        if rc != 0:
+            raise _lib.ScgibError(f"scgib_graph_split failed: {_lib.load().scgib_strerror(rc).decode()}"
+                                  f" (code {rc})")
+        self._handle = handle
+        self.device = dev
+        keys = ("captured", "lane0_kernels", "lane1_kernels", "handoffs", "lane0_nodes",
+                "lane1_nodes", "serialised", "slots")
+        self.info = dict(zip(keys, (int(v) for v in info)))
+        _LIVE_SPLITS.add(self)
+
+    def replay(self):
+        _lib.call("scgib_graph_split_launch", self._handle, _stream())
+
+    def timeouts(self):
+        """Waits of the added hand-offs that gave up (0 when the lanes overlapped)."""
+        return int(self.words.view(-1, 4)[:self.info["slots"], 2].sum().item())
+
+    def close(self):
+        if self._handle:
+            _lib.call("scgib_graph_split_destroy", self._handle)
+            self._handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001 (interpreter shutdown)
+            pass
+
+
 # the agg-free layer's weight-gradient row: dW2 [64][64] | db2 | db1 (the
 # scgib_gin_layer_bwd_z slab, reduced as one job) | dW1 [64][64] (the
 # scgib_gin_bwd_stats_z slab of the layer below)
@@ -1090,7 +1154,10 @@ def _xq_handoff(producer, consumer, key):
 def xq_timeouts(device):
     """Waits of the encoder pair's hand-offs that gave up (0 = every wait saw
     its signal; a non-zero count means the two kernels shared a queue)."""
-    return sum(int(_xq_words(device, k)[2].item()) for k in ("pair_fwd", "pair_bwd"))
+    idx = torch.device(device).index or 0
+    split = sum(s.timeouts() for s in list(_LIVE_SPLITS)
+                if s._handle and (s.device.index or 0) == idx)
+    return split + sum(int(_xq_words(device, k)[2].item()) for k in ("pair_fwd", "pair_bwd"))
 
 
 class _GinEncoderPair(torch.autograd.Function):

@@ -276,7 +276,7 @@ def _lockstep(name, model, opt, replay, oracle_step, plan, names, key_of, lr, wd
 # ---------------------------------------------------------------------------
 # pretrain (configs[1])
 # ---------------------------------------------------------------------------
-K_PRE, POOL_PRE, B_PRE = 8, 3, 512
+K_PRE, POOL_PRE = 8, 3
 
 
 def _pretrain_model(pkg, F_in, k, B, dev):
@@ -294,11 +294,15 @@ def _pretrain_model(pkg, F_in, k, B, dev):
     return model.to(dev).train()
 
 
-def test_pretrain_trajectory_replayed(pkg, dev):
+@pytest.mark.parametrize("B_PRE,split,seed", [(512, True, 70), (512, False, 70), (128, True, 70),
+                                              (128, False, 70), (128, True, 30), (128, False, 30)],
+                         ids=["B512-lanes", "B512-whole", "B128-lanes", "B128-whole",
+                              "B128-lanes-s30", "B128-whole-s30"])
+def test_pretrain_trajectory_replayed(pkg, dev, B_PRE, split, seed):
     import bench
     from oracle import scgib_ref as R
     k, F_in = 1, pkg.synth.WORKLOADS["qm9"][2]
-    hosts = [pkg.graph.collate_pyg(pkg.synth.molecules(B_PRE, "qm9", seed=70 + i))[0]
+    hosts = [pkg.graph.collate_pyg(pkg.synth.molecules(B_PRE, "qm9", seed=seed + i))[0]
              for i in range(POOL_PRE)]
     model = _pretrain_model(pkg, F_in, k, B_PRE, dev)
     opt = pkg.optim.Adam(model.parameters(), lr=1e-4, weight_decay=5e-5)
@@ -306,7 +310,8 @@ def test_pretrain_trajectory_replayed(pkg, dev):
     s_ug = torch.zeros(n_cap, device=dev)
     s_uf = torch.zeros(n_cap, 64, device=dev)
     rs = bench.build_replay_step(model, opt, hosts, k, B_PRE, dev, prefetch=True,
-                                 noise=(s_ug, s_uf))
+                                 noise=(s_ug, s_uf), split=split)
+    assert (rs.split is not None) == (split and pkg.ops.xq_enabled())
     c0 = int(rs.pool["cursor"][0])
     assert c0 == 3  # the builder's three eager warm-up steps loaded pool[0..2]
     gen = torch.Generator().manual_seed(4242)
@@ -392,7 +397,7 @@ def test_finetune_trajectory_and_eval_rocauc(pkg, dev):
         n = len(ug)
         s_ug[:n].copy_(ug)
         s_uf[:n].copy_(uf)
-        fs.graph.replay()
+        fs.replay()
         return {"losses": [fs.loss.item()], "scores": fs.scores.cpu().double()}
 
     def oracle_step(orc, item):

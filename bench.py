@@ -702,7 +702,8 @@ def finetune_leg(a, dev):
     keep = RUN_CONFIG
     ns = SimpleNamespace(batch=32, pool=a.pool, steps=a.steps, warmup=a.warmup,
                          no_kernel_timer=a.no_kernel_timer, no_cpu_baseline=a.no_cpu_baseline,
-                         cpu_seconds=a.cpu_seconds, no_ego_prefetch=a.no_ego_prefetch)
+                         cpu_seconds=a.cpu_seconds, no_ego_prefetch=a.no_ego_prefetch,
+                         no_split=a.no_split)
     try:
         line = finetune_bench.run(sys.modules[__name__], ns, dev)
     finally:
@@ -825,7 +826,9 @@ def build_replay_step(model, opt, pool_host, k, batch, dev, prefetch=True, noise
             opt.step()
         allreduce_mode = "between two graph replays"
     nodes = graph_node_counts(graph)
-    lanes = split_graph(graph, dev) if (split and graph2 is None) else None
+    # (one process per GPU with the RCCL all-reduce in the graph keeps the whole
+    # graph: its collective nodes are not exercised by the split's tests here)
+    lanes = split_graph(graph, dev) if (split and not collective) else None
     if lanes is None:
         graph.instantiate()
 

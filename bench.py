@@ -1210,13 +1210,17 @@ def main():
                 sb, bound="hbm", peak=HBM_PEAK_GBS, unit="GB/s",
                 note="ZINC-like superbatch, [N,64] fp32 > 256 MiB Infinity Cache; frac = "
                      "algorithmic bytes / launch time / 8.0 TB/s (north_star target >= 0.40 on "
-                     "the on-path gather kernels gin_fwd_k and gin_bwd_stats_k; "
-                     "gin_aggregate_k is a reference kernel, not in the step); gin_fwd_k frac "
-                     "on §8(d) aggregation bytes, frac_inclusive on everything the launch moves "
-                     "(its saved-activation writes too: agg, z2 and — stores_r — r); "
-                     "gin_bwd5_k at this scale (~146 sub-tiles per workgroup, its "
-                     "start-of-kernel chain amortised; recomputes_r: the gin_bwd5r_k variant), "
-                     "mfma_frac = flops / time / 157.3 TF/s"),
+                     "the on-path gather kernels; gin_aggregate_k is a reference kernel, not in "
+                     "the step).  At this size layers 1-4 run agg-free "
+                     "(ops.AGG_FREE_MIN_ROWS): gin_fwd_k_agg_free = those four forward launches "
+                     "(no aggregate store, the step's d = 64 layers), gin_fwd_k = all five "
+                     "(this GIN's layer 0 is a d_in = 64 layer that stores its aggregate); "
+                     "the backward pair is gin_bwd_statsz_k (gather of dz1, dh = g W1, "
+                     "dW1 = g^T h, BN-backward sums) + gin_bwd5z_k (dz1, dW2, db2, db1); "
+                     "gin_bwd_stats_k / gin_bwd5_k appear when the stored-agg path runs "
+                     "(--no-agg-free).  gin_fwd_k frac on §8(d) aggregation bytes, "
+                     "frac_inclusive on everything the launch moves (its saved-activation "
+                     "writes too); mfma_frac = flops / time / 157.3 TF/s"),
             "cpu_baseline": cpu,
             # BASELINE.json configs[4] (molhiv fine-tune from the shipped
             # checkpoint, B = 32, 1 GPU): its own timed replay after this leg

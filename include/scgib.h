@@ -124,6 +124,19 @@ int scgib_stream_wait(uint32_t *words, uint32_t *fault, uint32_t *host_fault,
 int scgib_graph_split(void *graph, uint32_t *words, int32_t n_slots, uint32_t *fault,
                       uint32_t *host_fault, scgib_stream_t stream, void **out, int32_t *info);
 int scgib_graph_split_launch(void *split, scgib_stream_t stream);
+/* The lane plan scgib_graph_split makes, on the host alone (no device): n
+ * nodes, m edges from[k] -> to[k], n_hidden in-graph hand-off pairs
+ * (signal node -> wait node).  Per node (n int32 each, may be NULL): lane,
+ * position in it, the slot of the wait placed before it and of the signal
+ * placed after it (-1: none); info (4 int32): slots, the start hand-off's
+ * slot (a signal before lane 0's first node, a wait before lane 1's), the
+ * end hand-off's slot (a signal after lane 1's last node, a wait after lane
+ * 0's last), nodes serialised beyond two chains (-1: no such hand-off).
+ * SCGIB_EUNSUPPORTED where scgib_graph_split refuses the graph. */
+int scgib_graph_split_plan(int32_t n, int32_t m, const int32_t *from, const int32_t *to,
+                           int32_t n_hidden, const int32_t *hidden_signal,
+                           const int32_t *hidden_wait, int32_t *lane, int32_t *pos,
+                           int32_t *wait_slot, int32_t *signal_slot, int32_t *info);
 int scgib_graph_split_destroy(void *split);
 /* Diagnostics: writes the 100 MHz device wall clock (s_memrealtime) to
  * buf[slot] when the stream reaches this point (ops.stamps: the timeline of

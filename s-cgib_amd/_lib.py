@@ -38,6 +38,8 @@ SIGNATURES = {
     "scgib_graph_split": (ctypes.c_int, [_P, _P, _I32, _P, _P, _P, _P, _P]),
     "scgib_graph_split_launch": (ctypes.c_int, [_P, _P]),
     "scgib_graph_split_destroy": (ctypes.c_int, [_P]),
+    "scgib_graph_split_plan": (ctypes.c_int, [_I32, _I32, _P, _P, _I32, _P, _P, _P, _P, _P, _P,
+                                              _P]),
     "scgib_strerror": (ctypes.c_char_p, [ctypes.c_int]),
     "scgib_gin_aggregate": (ctypes.c_int, [_P, _P, _P, _I64, _I32, _F, _P, _P, _P]),
     "scgib_segment_sum": (ctypes.c_int, [_P, _P, _I64, _I32, _P, _P, _P]),

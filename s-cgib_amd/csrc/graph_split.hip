@@ -92,6 +92,119 @@ struct Lane {
 
 }  // namespace
 
+// The lane plan of a DAG of n nodes (preds[v]: v's predecessors; hidden:
+// (signal, wait) node pairs ordered by hand-off words, not by edges): one
+// topological order (ties by node index) with the hidden pairs as edges, each
+// node on the lane whose tail is its direct predecessor (lane 0 first), and
+// the cross-lane waits pruned to the latest predecessor in the other lane,
+// plus the start / end hand-offs (header comment).  Host-only: tested on the
+// CPU through scgib_graph_split_plan.
+struct Plan {
+    std::vector<int> lane, pos, wait_slot, signal_slot;
+    std::vector<int> seq[2];
+    int slots = 0, start_slot = -1, end_slot = -1, loose = 0;
+};
+
+static int plan_lanes(int n, const std::vector<std::vector<int>> &preds,
+                      const std::vector<std::pair<int, int>> &hidden, Plan &pl) {
+    // topological order, ties broken by the runtime's node order (capture order)
+    std::priority_queue<int, std::vector<int>, std::greater<int>> ready;
+    std::vector<std::vector<int>> after(n);
+    std::vector<int> indeg(n, 0);
+    for (int v = 0; v < n; ++v)
+        for (int u : preds[v]) {
+            after[u].push_back(v);
+            ++indeg[v];
+        }
+    for (const auto &h : hidden) {
+        after[h.first].push_back(h.second);
+        ++indeg[h.second];
+    }
+    for (int i = 0; i < n; ++i)
+        if (indeg[i] == 0) ready.push(i);
+    std::vector<int> order;
+    order.reserve(n);
+    while (!ready.empty()) {
+        const int u = ready.top();
+        ready.pop();
+        order.push_back(u);
+        for (int v : after[u])
+            if (--indeg[v] == 0) ready.push(v);
+    }
+    if (static_cast<int>(order.size()) != n) return SCGIB_EUNSUPPORTED;  // a hand-off against the graph's order
+    // ancestor bitsets (a step graph has tens to a few hundred nodes)
+    const size_t wds = (static_cast<size_t>(n) + 63) / 64;
+    std::vector<uint64_t> anc(static_cast<size_t>(n) * wds, 0ull);
+    for (int v : order)
+        for (int u : preds[v]) {
+            for (size_t w = 0; w < wds; ++w) anc[v * wds + w] |= anc[u * wds + w];
+            anc[v * wds + u / 64] |= 1ull << (u % 64);
+        }
+    auto is_anc = [&](int u, int v) { return (anc[v * wds + u / 64] >> (u % 64)) & 1ull; };
+    // lanes: follow the captured chains (a node joins the lane whose tail is
+    // its direct predecessor), a fork's second child opens the other lane
+    std::vector<int> &lane = pl.lane, &pos = pl.pos;
+    std::vector<int> *seq = pl.seq;
+    lane.assign(n, -1);
+    pos.assign(n, -1);
+    int &loose = pl.loose;
+    loose = 0;
+    std::vector<int> nsucc(n, 0);
+    for (int v = 0; v < n; ++v)
+        for (int u : preds[v]) ++nsucc[u];
+    for (int v : order) {
+        // both tails direct predecessors (a join, or a mid-capture stream
+        // dependency): the tail with the fewer successors is the one whose
+        // chain ends in v; the other one's stream continues past it
+        int pick = -1;
+        for (int l = 0; l < 2; ++l)
+            if (!seq[l].empty() &&
+                std::find(preds[v].begin(), preds[v].end(), seq[l].back()) != preds[v].end() &&
+                (pick < 0 || nsucc[seq[l].back()] < nsucc[seq[pick].back()]))
+                pick = l;
+        if (pick < 0) {
+            if (seq[0].empty()) pick = 0;
+            else if (seq[1].empty()) pick = 1;
+            else if (is_anc(seq[1].back(), v)) pick = 1;
+            else if (is_anc(seq[0].back(), v)) pick = 0;
+            else {
+                pick = 1;  // a third concurrent chain: serialised behind lane 1
+                ++loose;
+            }
+        }
+        lane[v] = pick;
+        pos[v] = static_cast<int>(seq[pick].size());
+        seq[pick].push_back(v);
+    }
+    for (const auto &h : hidden)  // (both ends on one lane: in order by construction)
+        if (lane[h.first] == lane[h.second] && pos[h.first] > pos[h.second]) return SCGIB_EUNSUPPORTED;
+    // cross-lane waits, pruned to the latest predecessor in the other lane
+    std::vector<int> &wait_slot = pl.wait_slot, &signal_slot = pl.signal_slot;
+    wait_slot.assign(n, -1);
+    signal_slot.assign(n, -1);
+    int &slots = pl.slots, &start_slot = pl.start_slot, &end_slot = pl.end_slot;
+    slots = 0;
+    start_slot = end_slot = -1;
+    for (int l = 0; l < 2; ++l) {
+        int waited = -1;
+        for (int v : seq[l]) {
+            int need = -1;
+            for (int u : preds[v])
+                if (lane[u] != l) need = std::max(need, pos[u]);
+            if (need > waited) {
+                const int src = seq[1 - l][need];
+                if (signal_slot[src] >= 0) return SCGIB_EINVAL;  // one wait per source by construction
+                signal_slot[src] = wait_slot[v] = slots++;
+                waited = need;
+            }
+        }
+        if (l == 0 && !seq[1].empty() && waited < static_cast<int>(seq[1].size()) - 1)
+            end_slot = slots++;  // lane 0 ends waiting for lane 1's last node
+    }
+    if (!seq[1].empty() && wait_slot[seq[1][0]] < 0) start_slot = slots++;
+    return SCGIB_OK;
+}
+
 // words: n_slots * 4 zeroed uint32 (one slot per added hand-off, the last 8
 // for the queue check; kept for the lifetime of the split); fault /
 // host_fault: the encoder pair's sticky fault words (ops.handoff_fault_word /
@@ -129,14 +242,8 @@ extern "C" int scgib_graph_split(void *graph, uint32_t *words, int32_t n_slots, 
     std::vector<hipGraphNode_t> from(m), to(m);
     if (m && (e = hipGraphGetEdges(g, from.data(), to.data(), &m)) != hipSuccess)
         return static_cast<int>(e);
-    std::vector<std::vector<int>> preds(n), succs(n);
-    std::vector<int> indeg(n, 0);
-    for (size_t k = 0; k < m; ++k) {
-        const int u = index.at(from[k]), v = index.at(to[k]);
-        preds[v].push_back(u);
-        succs[u].push_back(v);
-        ++indeg[v];
-    }
+    std::vector<std::vector<int>> preds(n);
+    for (size_t k = 0; k < m; ++k) preds[index.at(to[k])].push_back(index.at(from[k]));
     // the encoder pair's in-graph hand-offs (a stream_signal_k and the
     // stream_wait_k on the same words): a dependency the graph does not show,
     // added to the topological order below so that it too points backwards
@@ -158,83 +265,12 @@ extern "C" int scgib_graph_split(void *graph, uint32_t *words, int32_t n_slots, 
         for (const auto &kv : pairs)
             if (kv.second.first >= 0 && kv.second.second >= 0) hidden.push_back(kv.second);
     }
-    // topological order, ties broken by the runtime's node order (capture order)
-    std::priority_queue<int, std::vector<int>, std::greater<int>> ready;
-    std::vector<std::vector<int>> after(succs);
-    for (const auto &h : hidden) {
-        after[h.first].push_back(h.second);
-        ++indeg[h.second];
-    }
-    for (size_t i = 0; i < n; ++i)
-        if (indeg[i] == 0) ready.push(static_cast<int>(i));
-    std::vector<int> order;
-    order.reserve(n);
-    while (!ready.empty()) {
-        const int u = ready.top();
-        ready.pop();
-        order.push_back(u);
-        for (int v : after[u])
-            if (--indeg[v] == 0) ready.push(v);
-    }
-    if (order.size() != n) return SCGIB_EUNSUPPORTED;  // a hand-off against the graph's order
-    // ancestor bitsets (a step graph has tens to a few hundred nodes)
-    const size_t wds = (n + 63) / 64;
-    std::vector<uint64_t> anc(n * wds, 0ull);
-    for (int v : order)
-        for (int u : preds[v]) {
-            for (size_t w = 0; w < wds; ++w) anc[v * wds + w] |= anc[u * wds + w];
-            anc[v * wds + u / 64] |= 1ull << (u % 64);
-        }
-    auto is_anc = [&](int u, int v) { return (anc[v * wds + u / 64] >> (u % 64)) & 1ull; };
-    // lanes: follow the captured chains (a node joins the lane whose tail is
-    // its direct predecessor; lane 0 at a join), a fork's second child opens
-    // the other lane
-    std::vector<int> lane(n, -1), pos(n, -1);
-    std::vector<int> seq[2];
-    int loose = 0;
-    for (int v : order) {
-        int pick = -1;
-        for (int l = 0; l < 2 && pick < 0; ++l)
-            if (!seq[l].empty() &&
-                std::find(preds[v].begin(), preds[v].end(), seq[l].back()) != preds[v].end())
-                pick = l;
-        if (pick < 0) {
-            if (seq[0].empty()) pick = 0;
-            else if (seq[1].empty()) pick = 1;
-            else if (is_anc(seq[1].back(), v)) pick = 1;
-            else if (is_anc(seq[0].back(), v)) pick = 0;
-            else {
-                pick = 1;  // a third concurrent chain: serialised behind lane 1
-                ++loose;
-            }
-        }
-        lane[v] = pick;
-        pos[v] = static_cast<int>(seq[pick].size());
-        seq[pick].push_back(v);
-    }
-    for (const auto &h : hidden)  // (both ends on one lane: in order by construction)
-        if (lane[h.first] == lane[h.second] && pos[h.first] > pos[h.second]) return SCGIB_EUNSUPPORTED;
-    // cross-lane waits, pruned to the latest predecessor in the other lane
-    std::vector<int> wait_slot(n, -1), signal_slot(n, -1);
-    int slots = 0;
-    int start_slot = -1, end_slot = -1;
-    for (int l = 0; l < 2; ++l) {
-        int waited = -1;
-        for (int v : seq[l]) {
-            int need = -1;
-            for (int u : preds[v])
-                if (lane[u] != l) need = std::max(need, pos[u]);
-            if (need > waited) {
-                const int src = seq[1 - l][need];
-                if (signal_slot[src] >= 0) return SCGIB_EINVAL;  // one wait per source by construction
-                signal_slot[src] = wait_slot[v] = slots++;
-                waited = need;
-            }
-        }
-        if (l == 0 && !seq[1].empty() && waited < static_cast<int>(seq[1].size()) - 1)
-            end_slot = slots++;  // lane 0 ends waiting for lane 1's last node
-    }
-    if (!seq[1].empty() && wait_slot[seq[1][0]] < 0) start_slot = slots++;
+    Plan pl;
+    const int prc = plan_lanes(static_cast<int>(n), preds, hidden, pl);
+    if (prc != SCGIB_OK) return prc;
+    const std::vector<int> &wait_slot = pl.wait_slot, &signal_slot = pl.signal_slot;
+    const std::vector<int> *seq = pl.seq;
+    const int slots = pl.slots, start_slot = pl.start_slot, end_slot = pl.end_slot, loose = pl.loose;
     if (slots > n_slots - kQueueTries) return SCGIB_EINVAL;
     // the two linear graphs
     auto handoff = [&](bool signal) {
@@ -339,5 +375,49 @@ extern "C" int scgib_graph_split_launch(void *split, scgib_stream_t stream) {
 extern "C" int scgib_graph_split_destroy(void *split) {
     if (!split) return SCGIB_EINVAL;
     release(reinterpret_cast<Split *>(split));
+    return SCGIB_OK;
+}
+
+// The lane plan alone, for tests on the host (no device needed): n nodes,
+// m edges from[k] -> to[k], n_hidden signal -> wait pairs.  Outputs (n int32
+// each, may be NULL): lane, position in the lane, wait slot before the node
+// (-1: none), signal slot after it (-1: none); info (4 int32): slots, the
+// start hand-off's slot (a signal before lane 0's first node, a wait before
+// lane 1's; -1: none), the end hand-off's slot (a signal after lane 1's last
+// node, a wait after lane 0's last; -1: none), nodes serialised beyond two
+// chains.  Returns SCGIB_EUNSUPPORTED where scgib_graph_split would.
+extern "C" int scgib_graph_split_plan(int32_t n, int32_t m, const int32_t *from, const int32_t *to,
+                                      int32_t n_hidden, const int32_t *hidden_signal,
+                                      const int32_t *hidden_wait, int32_t *lane, int32_t *pos,
+                                      int32_t *wait_slot, int32_t *signal_slot, int32_t *info) {
+    if (n < 1 || m < 0 || n_hidden < 0 || (m > 0 && (!from || !to)) ||
+        (n_hidden > 0 && (!hidden_signal || !hidden_wait)))
+        return SCGIB_EINVAL;
+    std::vector<std::vector<int>> preds(n);
+    for (int k = 0; k < m; ++k) {
+        if (from[k] < 0 || from[k] >= n || to[k] < 0 || to[k] >= n) return SCGIB_EINVAL;
+        preds[to[k]].push_back(from[k]);
+    }
+    std::vector<std::pair<int, int>> hidden;
+    for (int k = 0; k < n_hidden; ++k) {
+        if (hidden_signal[k] < 0 || hidden_signal[k] >= n || hidden_wait[k] < 0 || hidden_wait[k] >= n)
+            return SCGIB_EINVAL;
+        hidden.emplace_back(hidden_signal[k], hidden_wait[k]);
+    }
+    Plan pl;
+    const int rc = plan_lanes(n, preds, hidden, pl);
+    if (rc != SCGIB_OK) return rc;
+    for (int v = 0; v < n; ++v) {
+        if (lane) lane[v] = pl.lane[v];
+        if (pos) pos[v] = pl.pos[v];
+        if (wait_slot) wait_slot[v] = pl.wait_slot[v];
+        if (signal_slot) signal_slot[v] = pl.signal_slot[v];
+    }
+    if (info) {
+        info[0] = pl.slots;
+        info[1] = pl.start_slot;
+        info[2] = pl.end_slot;
+        info[3] = pl.loose;
+    }
     return SCGIB_OK;
 }

@@ -508,12 +508,16 @@ class SplitGraph:
                                   f" (code {rc})")
         self._handle = handle
         self.device = dev
+        self._stream_id = torch.cuda.current_stream(dev).cuda_stream
         keys = ("captured", "lane0_kernels", "lane1_kernels", "handoffs", "lane0_nodes",
                 "lane1_nodes", "serialised", "slots")
         self.info = dict(zip(keys, (int(v) for v in info)))
         _LIVE_SPLITS.add(self)
 
     def replay(self):
+        if torch.cuda.current_stream(self.device).cuda_stream != self._stream_id:
+            raise _lib.ScgibError("SplitGraph.replay: replay on the stream the split was made on "
+                                  "(its side stream's hardware queue was checked against that one)")
         _lib.call("scgib_graph_split_launch", self._handle, _stream())
 
     def timeouts(self):

@@ -1052,6 +1052,15 @@ def main():
                 {k: rs.split.info[k] for k in ("lane0_nodes", "lane1_nodes", "handoffs")}
                 if rs.split is not None else "whole graph"))
 
+    if os.environ.get("SCGIB_PRELOAD_MS"):  # diagnostics only (DESIGN §5 "Round 6"): busy
+        # the GPU for that long before the warm-up, to tell a clock ramp from
+        # a per-launch effect in the first timed steps; never set by the driver
+        t_end = time.perf_counter() + float(os.environ["SCGIB_PRELOAD_MS"]) / 1e3
+        m = torch.randn(2048, 2048, device=dev)
+        while time.perf_counter() < t_end:
+            for _ in range(8):
+                m = torch.tanh(m @ m * 1e-3)
+            torch.cuda.synchronize()
     for i in range(a.warmup):
         step(i)
     progress(f"warm-up done ({a.warmup} steps); timing {a.steps} steps")

@@ -1061,9 +1061,18 @@ def main():
             for _ in range(8):
                 m = torch.tanh(m @ m * 1e-3)
             torch.cuda.synchronize()
+    if os.environ.get("SCGIB_PRELAUNCH"):  # diagnostics only: that many one-element
+        # kernel launches before the warm-up (a per-launch effect, not a clock one)
+        t = torch.zeros(1, device=dev)
+        for _ in range(int(os.environ["SCGIB_PRELAUNCH"])):
+            t.add_(1.0)
+        torch.cuda.synchronize()
     for i in range(a.warmup):
         step(i)
     progress(f"warm-up done ({a.warmup} steps); timing {a.steps} steps")
+    if os.environ.get("SCGIB_IDLE_MS"):  # diagnostics only: the GPU idle that long
+        torch.cuda.synchronize()  # between the warm-up and the timed steps
+        time.sleep(float(os.environ["SCGIB_IDLE_MS"]) / 1e3)
 
     def barrier():
         if world > 1:

@@ -714,7 +714,7 @@ def finetune_leg(a, dev):
 
 
 def build_replay_step(model, opt, pool_host, k, batch, dev, prefetch=True, noise=None,
-                      collective=False, reducer=None, warm=3, split=True):
+                      collective=False, reducer=None, warm=3, split=True, noise_prefetch=True):
     """The bench's pretrain step (exp_pretraining.py:290-333) as ONE captured
     HIP graph in capacity mode: the pool's next resident batch (and the ego-nets
     the previous step built for it) loaded inside the graph, forward, backward,
@@ -722,13 +722,17 @@ def build_replay_step(model, opt, pool_host, k, batch, dev, prefetch=True, noise
     on a side stream first (allocator, Adam state, RCCL communicator).
     ``noise`` = (u_gate [n_cap], u_feat [n_cap, 64]) static device buffers the
     step reads instead of drawing its own (tests/test_gpu_trajectory.py fills
-    them before each replay); None = the device Philox draws of every replay.
+    them before each replay); None = the device Philox draws of every replay,
+    with ``noise_prefetch`` one step ahead (ops.NoisePrefetch: each step's
+    backward draws the next step's noise at the end of its core chain, off
+    the forward's critical path; the same draws in the same order).
     ``split``: replay the captured graph as two linear lanes (ops.SplitGraph:
     ~6 us of host enqueue per lane instead of ~3 us per node) where the
     hand-off rule allows and the graph is one launch.
     Returns step(i), the static losses (kl, rec, con), the static batch, the
     device pool and its prefetch, the all-reduce mode, the node count of the
-    captured graph and the split (None: the captured graph is replayed)."""
+    captured graph, the split (None: the captured graph is replayed) and the
+    noise prefetch (None: drawn in the forward, or passed in)."""
     n_cap, e_cap, mgn, ego_caps = pkg.graph.StaticBatch.capacities(pool_host, k, slack=1.02)
     F_in = pool_host[0].ndata["x"].shape[1]
     static = pkg.graph.StaticBatch(batch, n_cap, e_cap, F_in, mgn, ego_caps, dev, k=k)
@@ -748,6 +752,10 @@ def build_replay_step(model, opt, pool_host, k, batch, dev, prefetch=True, noise
     if prefetch:
         pf = pkg.graph.EgoPrefetch(static, pool_dev)
         pf.prime()  # the first batch's, before the first load
+    nf = None
+    if noise is None and noise_prefetch:  # the device noise one step ahead (ops.NoisePrefetch)
+        nf = pkg.ops.NoisePrefetch(static.graph, dev)
+        nf.prime()
 
     def body():
         # the pool's next batch (and its prefetched ego-nets) into the static inputs
@@ -847,7 +855,8 @@ def build_replay_step(model, opt, pool_host, k, batch, dev, prefetch=True, noise
     # allocation and the replays would seed the backward with whatever lands there
     return SimpleNamespace(step=step, loss=static_loss, static=static, pool=pool_dev,
                            padded=padded, prefetch=pf, allreduce_mode=allreduce_mode,
-                           graph=graph, graph_nodes=nodes, split=lanes, one=one)
+                           graph=graph, graph_nodes=nodes, split=lanes, one=one,
+                           noise_prefetch=nf)
 
 
 def split_graph(graph, dev):
@@ -923,6 +932,9 @@ def main():
                     help="skip the event-timed kernel pass (PMC runs: only real step launches)")
     ap.add_argument("--eager", action="store_true",
                     help="launch every kernel from Python (no HIP-graph capture)")
+    ap.add_argument("--no-noise-prefetch", action="store_true",
+                    help="draw each step's compression noise at the head of its forward core "
+                         "chain instead of in the step before's backward (ops.NoisePrefetch; A/B)")
     ap.add_argument("--no-split", action="store_true",
                     help="replay the captured step graph whole instead of as two linear lanes "
                          "(ops.SplitGraph; A/B of the host enqueue)")
@@ -1021,6 +1033,7 @@ def main():
     reducer = pkg.dist.GradAllReducer(model.parameters(), buffers=pkg.dist.bn_buffers(model))
 
     graph_nodes = None
+    noise_draw = "in the step's forward, head of the core chain"
     if a.eager:
         opt = (torch.optim.Adam(model.parameters(), lr=1e-4, weight_decay=5e-5, fused=True)
                if a.torch_adam else pkg.optim.Adam(model.parameters(), lr=1e-4, weight_decay=5e-5))
@@ -1045,8 +1058,11 @@ def main():
             opt = pkg.optim.Adam(model.parameters(), lr=1e-4, weight_decay=5e-5)
         rs = build_replay_step(model, opt, pool_host, a.k, a.batch, dev,
                                prefetch=not a.no_ego_prefetch, collective=collective,
-                               reducer=reducer, split=not a.no_split)
+                               reducer=reducer, split=not a.no_split,
+                               noise_prefetch=not a.no_noise_prefetch)
         step, allreduce_mode, graph_nodes = rs.step, rs.allreduce_mode, rs.graph_nodes
+        if rs.noise_prefetch is not None:
+            noise_draw = "in the step before's backward, core chain end (ops.NoisePrefetch)"
         if graph_nodes is not None:  # the replayed lanes (ops.SplitGraph), or the whole graph
             graph_nodes = dict(graph_nodes, replay=(
                 {k: rs.split.info[k] for k in ("lane0_nodes", "lane1_nodes", "handoffs")}
@@ -1202,6 +1218,7 @@ def main():
                        "ego_build": ("in the step, for the batch the next step loads "
                                      "(graph.EgoPrefetch)" if not a.eager
                                      and not a.no_ego_prefetch else "at the head of the step"),
+                       "noise_draw": noise_draw,
                        "allreduce": None if not collective else
                        ("eager" if a.eager else allreduce_mode),
                        "handoffs": ("signal / wait kernels" if pkg.ops.xq_enabled() else

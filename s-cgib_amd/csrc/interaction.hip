@@ -137,8 +137,13 @@ __device__ __forceinline__ float4 noise_feat(const NoiseGen &ng, int64_t r, int 
 
 // one thread per (row, channel quad); 256 threads = 16 rows per workgroup per
 // pass, grid-stride over at most kNoiseWG workgroups: the kernel runs
-// beside Encoder2's last layer, so it should hold few CU slots
-constexpr int kNoiseWG = 64;
+// beside Encoder2's last layer, so it should hold few CU slots (build-time
+// A/B hook SCGIB_NOISE_WG: the draws depend only on (row, quad, offset), so
+// the grid does not change a bit)
+#ifndef SCGIB_NOISE_WG
+#define SCGIB_NOISE_WG 64
+#endif
+constexpr int kNoiseWG = SCGIB_NOISE_WG;
 __global__ __launch_bounds__(256) void noise_uniform_k(float *__restrict__ u_gate,
                                                        float *__restrict__ u_feat, int64_t n,
                                                        uint64_t *__restrict__ rng,

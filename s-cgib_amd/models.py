@@ -20,7 +20,8 @@ Differences from the reference, all deliberate:
     generator per graph (models.py:599, 650); here it is drawn on the device
     (counter-based Philox4x32-10 keyed by a device seed/offset,
     ops.device_noise / ops.seed_noise; the draws are kept in
-    ``_last_noise``), or passed explicitly with
+    ``_last_noise`` — under ops.NoisePrefetch the static buffers, which the
+    step's backward refills with the next step's draw), or passed explicitly with
     ``noise=(u_gate[N], u_feat[N,64])`` for parity with a recorded run;
   * ``flatten_batch_subgraphs`` may be ``None``: the ego-nets are then built
     on the device from ``batch_g`` (scgib_egonet_*), replacing the offline
@@ -294,13 +295,22 @@ class _SCGIBCore(nn.Module):
                 ego = pf.ego if pf is not None else G.egonet_batch(batch_g, self.k_transition)
             lin0 = enc_owner.compressor[0] if LIN_IN_PAIR else None
             drawn = {}
-            tail = None
+            tail = bwd_tail = None
             if draw_noise and DEVICE_NOISE and self.hidden_dim == 64:
-                def tail():  # the interaction's noise, drawn beside the ego chain
-                    drawn["u"] = ops.device_noise(batch_g.num_nodes(), batch_x.device)
+                # ops.NoisePrefetch (a training step with a backward): this
+                # step's noise was drawn by the previous step's backward, and
+                # this step's backward draws the next one's
+                nf = getattr(batch_g, "noise_prefetch", None)
+                if (nf is not None and nf.n == batch_g.num_nodes() and enc_owner.training
+                        and torch.is_grad_enabled()):
+                    drawn["u"] = (nf.u_gate, nf.u_feat)
+                    bwd_tail = nf.draw
+                else:
+                    def tail():  # the interaction's noise, drawn beside the ego chain
+                        drawn["u"] = ops.device_noise(batch_g.num_nodes(), batch_x.device)
             outs = ops.gin_encoder_pair_x(
                 batch_x, ego, enc_owner.Encoder2, batch_g, enc_owner.Encoder1, td,
-                ego.ndata["_ID"], side, lin0, tail, pf)
+                ego.ndata["_ID"], side, lin0, tail, pf, bwd_tail)
             subgraphs_features, sub_readout, graph_features = outs[0], outs[1], outs[2]
             t = outs[3] if len(outs) > 3 else None
             return ego, (graph_features, subgraphs_features, sub_readout, t, drawn.get("u"))

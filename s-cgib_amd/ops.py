@@ -1177,8 +1177,8 @@ class _GinEncoderPair(torch.autograd.Function):
     def forward(ctx, x, wt, w0, b0, nmap, ego, core, gin_ego, gin_core, training, side, tails,
                 *params):
         main = _torch_stream()
-        core_tail, side_tail = tails
-        ctx.side_tail = side_tail
+        core_tail, side_tail, bwd_tail = tails
+        ctx.side_tail, ctx.bwd_tail = side_tail, bwd_tail
         ne = 6 * len(gin_ego.ginlayers)
         ctx.set_materialize_grads(False)  # unused outputs (e.g. s) get no zero-fill launch
         # the loss-section reduces of this step are deferred into this node's
@@ -1316,6 +1316,8 @@ class _GinEncoderPair(torch.autograd.Function):
                     keep = keep[:2 * big] + keep[2 * big + 2:]
                 ctx.sub[1].extra_jobs = (jobs, keep)
             gc = _drain(_GinEncoder.backward_steps(ctx.sub[1], g_f), "bwd.core")
+            if ctx.bwd_tail is not None:  # e.g. NoisePrefetch.draw: the next step's noise
+                ctx.bwd_tail()
             stamp("bwd.core_end[side]")
         main.wait_stream(side)
         stamp("bwd.joined[main]")
@@ -1345,7 +1347,7 @@ def _torch_stream():
 
 
 def gin_encoder_pair_x(x, ego, gin_ego, core, gin_core, transfer, node_map, side, lin0=None,
-                       core_tail=None, side_tail=None):
+                       core_tail=None, side_tail=None, bwd_tail=None):
     """(s, sum_nodes(ego, s), f) with s = gin_ego(ego, transfer(x[node_map])) and
     f = gin_core(core, transfer(x)) — the two encoders of Mainmodel.forward
     with transfer_d folded, and the ego-net readout fused into Encoder2's last
@@ -1356,7 +1358,9 @@ def gin_encoder_pair_x(x, ego, gin_ego, core, gin_core, transfer, node_map, side
     the core chain, beside the ego-net build; ``side_tail()`` (e.g.
     graph.EgoPrefetch: the next batch's ego-net build) runs on ``side`` after
     the ego chain's hand-off, and its ``joined()`` is called once the
-    backward has joined ``side`` back."""
+    backward has joined ``side`` back; ``bwd_tail()`` (e.g.
+    NoisePrefetch.draw) runs on ``side`` at the end of the backward's core
+    chain, before that join."""
     if ego.num_nodes() == 0 or core.num_nodes() == 0:
         raise _lib.ScgibError("gin_encoder on an empty graph")
     if transfer.bias is not None or transfer.weight.shape != (32, x.shape[1]) \
@@ -1369,7 +1373,7 @@ def gin_encoder_pair_x(x, ego, gin_ego, core, gin_core, transfer, node_map, side
     w0, b0 = (lin0.weight, lin0.bias) if lin0 is not None else (None, None)
     return _GinEncoderPair.apply(x, transfer.weight, w0, b0, node_map, ego, core, gin_ego,
                                  gin_core, bool(gin_core.training), side,
-                                 (core_tail, side_tail),
+                                 (core_tail, side_tail, bwd_tail),
                                  *_gin_layer_params(gin_ego), *_gin_layer_params(gin_core))
 
 
@@ -1919,6 +1923,33 @@ def device_noise(n, device):
     _lib.call("scgib_noise_uniform", _p(u_gate), _p(u_feat), n, _p(noise_state(device)),
               _p(counters(device, "noise", 1)), _stream())
     return u_gate, u_feat
+
+
+class NoisePrefetch:
+    """The compression noise one step ahead, for a replayed step (bench.py):
+    the step reads (u_gate, u_feat) from these static buffers and its
+    backward draws the next step's into them at the end of the encoder
+    pair's core chain — on ``side``, after the interaction backward (the
+    buffers' last reader) and beside the longer ego chain — instead of at
+    the head of the forward core chain.  The same Philox draws in the same
+    order as device_noise per step (one draw of ``n`` rows per step), so a
+    replayed step reads the values the inline draw would have given it.
+    ``prime()`` draws the first step's (eager); models._encode_forked takes
+    the buffers from ``batch_g.noise_prefetch``."""
+
+    def __init__(self, graph, device):
+        self.n = graph.num_nodes()
+        self.device = torch.device(device)
+        self.u_gate = torch.zeros(self.n, dtype=torch.float32, device=device)
+        self.u_feat = torch.zeros(self.n, HIDDEN, dtype=torch.float32, device=device)
+        graph.noise_prefetch = self
+
+    def draw(self):
+        """The next step's noise into the buffers, on the current stream."""
+        _lib.call("scgib_noise_uniform", _p(self.u_gate), _p(self.u_feat), self.n,
+                  _p(noise_state(self.device)), _p(counters(self.device, "noise", 1)), _stream())
+
+    prime = draw
 
 
 # ---------------------------------------------------------------------------

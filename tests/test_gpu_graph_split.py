@@ -137,6 +137,39 @@ def test_split_pretrain_step_matches_whole_replay(pkg, dev):
     _assert_bitwise(runs[0][1], runs[1][1])
 
 
+def test_noise_prefetch_matches_inline_draw(pkg, dev):
+    """ops.NoisePrefetch: the bench's replayed step with its compression
+    noise drawn one step ahead (by the step before's backward, at the end of
+    the core chain) computes bitwise what the step drawing it at the head of
+    its forward computes — the same Philox draws in the same order."""
+    import bench
+    from test_gpu_trajectory import _pretrain_model
+    k, B, K, POOL = 1, 128, 6, 3
+    F_in = pkg.synth.WORKLOADS["qm9"][2]
+    hosts = [pkg.graph.collate_pyg(pkg.synth.molecules(B, "qm9", seed=40 + i))[0]
+             for i in range(POOL)]
+    runs = []
+    for ahead in (False, True):
+        model = _pretrain_model(pkg, F_in, k, B, dev)
+        opt = pkg.optim.Adam(model.parameters(), lr=1e-4, weight_decay=5e-5)
+        pkg.ops.seed_noise(dev, 2024)
+        rs = bench.build_replay_step(model, opt, hosts, k, B, dev, prefetch=True,
+                                     noise_prefetch=ahead)
+        assert (rs.noise_prefetch is not None) == ahead
+        losses = []
+        for j in range(K):
+            kl, rec, con = rs.step(j)
+            losses.append(torch.stack([kl, rec, con]).clone())
+        torch.cuda.synchronize()
+        assert pkg.ops.xq_timeouts(dev) == 0
+        runs.append((torch.stack(losses), _state(model, opt)))
+        if rs.split is not None:
+            rs.split.close()
+    assert torch.isfinite(runs[0][0]).all()
+    assert torch.equal(runs[0][0], runs[1][0]), (runs[0][0], runs[1][0])
+    _assert_bitwise(runs[0][1], runs[1][1])
+
+
 def test_split_finetune_step_matches_whole_replay(pkg, dev):
     import finetune_bench
     if not pkg.ops.xq_enabled():

@@ -933,8 +933,9 @@ def main():
     ap.add_argument("--eager", action="store_true",
                     help="launch every kernel from Python (no HIP-graph capture)")
     ap.add_argument("--no-noise-prefetch", action="store_true",
-                    help="draw each step's compression noise at the head of its forward core "
-                         "chain instead of in the step before's backward (ops.NoisePrefetch; A/B)")
+                    help="pretrain: draw each step's compression noise at the head of its forward "
+                         "core chain instead of in the step before's backward (ops.NoisePrefetch; "
+                         "A/B; the fine-tune step draws it in its forward)")
     ap.add_argument("--no-split", action="store_true",
                     help="replay the captured step graph whole instead of as two linear lanes "
                          "(ops.SplitGraph; A/B of the host enqueue)")

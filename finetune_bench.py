@@ -116,7 +116,7 @@ def cpu_baseline(bench, ft, host_batches, targets, seconds):
 
 
 def build_finetune_step(pkg, ft, opt, host, targets, k, B, dev, prefetch=True, noise=None,
-                        warm=3, split=True):
+                        warm=3, split=True, noise_prefetch=False):
     """The fine-tune step (train_molhiv.py:107-152: forward, BCE, backward,
     Adam) as ONE captured HIP graph in capacity mode over a resident pool of
     the host batches ``host`` and their ``targets`` ([B, 1] each): the pool's
@@ -125,9 +125,14 @@ def build_finetune_step(pkg, ft, opt, host, targets, k, B, dev, prefetch=True, n
     (allocator, Adam state).  ``noise`` = (u_gate [n_cap], u_feat [n_cap, 64])
     static device buffers the step reads instead of its own device draws
     (tests/test_gpu_trajectory.py).  ``split``: replay as two linear lanes
-    (ops.SplitGraph) where the hand-off rule allows.  Returns replay() (one
-    step), the captured graph, the static scores and loss, the static batch,
-    the device pool and its prefetch."""
+    (ops.SplitGraph) where the hand-off rule allows.  ``noise_prefetch``
+    (noise None): the device noise one step ahead, as the pretrain bench
+    (ops.NoisePrefetch) — off by default here: with the lower GIN layers
+    frozen the fine-tune's backward core chain is the longer one, and the
+    draw at its end measured 0.2876-0.2890 vs 0.2854-0.2855 ms per step
+    (profiles/r06_noise/finetune_ab.txt).  Returns replay() (one step), the captured graph,
+    the static scores and loss, the static batch, the device pool and its
+    prefetches."""
     n_cap, e_cap, mgn, caps = pkg.graph.StaticBatch.capacities(host, k, slack=1.02)
     F_in = host[0].ndata["x"].shape[1]
     static = pkg.graph.StaticBatch(B, n_cap, e_cap, F_in, mgn, caps, dev, k=k)
@@ -145,6 +150,10 @@ def build_finetune_step(pkg, ft, opt, host, targets, k, B, dev, prefetch=True, n
     if prefetch:
         pf = pkg.graph.EgoPrefetch(static, pool)
         pf.prime()
+    nf = None
+    if noise is None and noise_prefetch:
+        nf = pkg.ops.NoisePrefetch(static.graph, dev)
+        nf.prime()
     # the targets walk their own resident pool in step with the batches: one
     # pool-copy launch per step (its own cursor, advanced like the batch's)
     tdev = [t.to(dev).contiguous() for t in targets]
@@ -199,7 +208,7 @@ def build_finetune_step(pkg, ft, opt, host, targets, k, B, dev, prefetch=True, n
     # (`one` held for the captured backward, as bench.build_replay_step does)
     return SimpleNamespace(replay=lanes.replay if lanes is not None else graph.replay,
                            graph=graph, split=lanes, scores=scores, loss=loss, static=static,
-                           pool=pool, padded=padded, prefetch=pf,
+                           pool=pool, padded=padded, prefetch=pf, noise_prefetch=nf,
                            targets=(tdev, ttable, tcursor, tg), graph_nodes=nodes, one=one)
 
 

@@ -136,12 +136,15 @@ __device__ __forceinline__ float4 noise_feat(const NoiseGen &ng, int64_t r, int 
 
 
 // one thread per (row, channel quad); 256 threads = 16 rows per workgroup per
-// pass, grid-stride over at most kNoiseWG workgroups: the kernel runs
-// beside Encoder2's last layer, so it should hold few CU slots (build-time
-// A/B hook SCGIB_NOISE_WG: the draws depend only on (row, quad, offset), so
-// the grid does not change a bit)
+// pass, grid-stride over at most kNoiseWG workgroups.  The bench's step
+// draws one step ahead (ops.NoisePrefetch), at the end of the backward's
+// core chain beside the ego chain's last layers: 256 workgroups there
+// (B = 512: 588 row groups in 3 passes instead of 10) measured 0.3872–0.3882
+// vs 0.3886–0.3902 ms per step, B = 32 unchanged (profiles/r06_noise/).
+// Build-time A/B hook SCGIB_NOISE_WG: the draws depend only on (row, quad,
+// offset), so the grid does not change a bit.
 #ifndef SCGIB_NOISE_WG
-#define SCGIB_NOISE_WG 64
+#define SCGIB_NOISE_WG 256
 #endif
 constexpr int kNoiseWG = SCGIB_NOISE_WG;
 __global__ __launch_bounds__(256) void noise_uniform_k(float *__restrict__ u_gate,

@@ -301,8 +301,12 @@ class _SCGIBCore(nn.Module):
                 # step's noise was drawn by the previous step's backward, and
                 # this step's backward draws the next one's
                 nf = getattr(batch_g, "noise_prefetch", None)
+                # (only when the pair will run a backward: a trainable encoder
+                # or transfer_d parameter — a fully frozen pair never redraws)
                 if (nf is not None and nf.n == batch_g.num_nodes() and enc_owner.training
-                        and torch.is_grad_enabled()):
+                        and torch.is_grad_enabled()
+                        and any(p.requires_grad for m in (enc_owner.Encoder1, enc_owner.Encoder2, td)
+                                for p in m.parameters())):
                     drawn["u"] = (nf.u_gate, nf.u_feat)
                     bwd_tail = nf.draw
                 else:

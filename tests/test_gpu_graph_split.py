@@ -207,3 +207,35 @@ def test_split_finetune_step_matches_whole_replay(pkg, dev):
             fs.split.close()
     assert torch.equal(runs[0][0], runs[1][0])
     _assert_bitwise(runs[0][1], runs[1][1])
+
+
+def test_finetune_noise_prefetch_matches_inline_draw(pkg, dev):
+    """The fine-tune step (frozen lower GIN layers, as finetune_bench builds
+    it) with ops.NoisePrefetch computes bitwise what the inline draw gives."""
+    import finetune_bench
+    B, K, POOL = 32, 6, 3
+    F_in = pkg.synth.WORKLOADS["molhiv"][2]
+    hosts = [pkg.graph.collate_pyg(pkg.synth.molecules(B, "molhiv", seed=70 + i))[0]
+             for i in range(POOL)]
+    gen = torch.Generator().manual_seed(6)
+    targets = [torch.randint(0, 2, (B, 1), generator=gen).float() for _ in range(POOL)]
+    runs = []
+    for ahead in (False, True):
+        ft, k = finetune_bench.make_finetune_model(pkg, F_in, B, dev, seed=12)
+        opt = pkg.optim.Adam(ft.parameters(), lr=1e-3, weight_decay=1e-5)
+        pkg.ops.seed_noise(dev, 77)
+        fs = finetune_bench.build_finetune_step(pkg, ft, opt, hosts, targets, k, B, dev,
+                                                prefetch=True, noise_prefetch=ahead)
+        assert (fs.noise_prefetch is not None) == ahead
+        losses = []
+        for _ in range(K):
+            fs.replay()
+            losses.append(torch.cat([fs.loss.reshape(1), fs.scores.reshape(-1)]).clone())
+        torch.cuda.synchronize()
+        assert pkg.ops.xq_timeouts(dev) == 0
+        runs.append((torch.stack(losses), _state(ft, opt)))
+        if fs.split is not None:
+            fs.split.close()
+    assert torch.isfinite(runs[0][0]).all()
+    assert torch.equal(runs[0][0], runs[1][0]), (runs[0][0], runs[1][0])
+    _assert_bitwise(runs[0][1], runs[1][1])

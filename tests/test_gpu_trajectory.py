@@ -13,7 +13,9 @@ noise, fed through the steps' static noise buffers:
   * pretrain: ``bench.build_replay_step`` (exp_pretraining.py:290-333, the
     bench's configs[1] step: QM9 B512 k1, pool load + ego prefetch + forward
     + backward + Adam(1e-4, wd 5e-5) in ONE graph), K = 8 replays over a pool
-    of 3 batches (the cursor wraps twice);
+    of 3 batches (the cursor wraps twice); and K = 4 replays of configs[2] /
+    configs[3]'s per-GPU steps (molpcba B1024 k1, PCQM4Mv2 B2048 k2), whose
+    ego layers take the agg-free backward and, at k = 2, the bitmap builder;
   * fine-tune: ``finetune_bench.build_finetune_step`` (train_molhiv.py:107-152,
     configs[4]: molhiv B32 from the shipped checkpoint, BCE, Adam(1e-3, wd
     1e-5)), K = 20 replays over a pool of 4 batches, then
@@ -294,15 +296,23 @@ def _pretrain_model(pkg, F_in, k, B, dev):
     return model.to(dev).train()
 
 
-@pytest.mark.parametrize("B_PRE,split,seed", [(512, True, 70), (512, False, 70), (128, True, 70),
-                                              (128, False, 70), (128, True, 30), (128, False, 30)],
+@pytest.mark.parametrize("B_PRE,split,seed,wl,k,n_steps",
+                         [(512, True, 70, "qm9", 1, K_PRE), (512, False, 70, "qm9", 1, K_PRE),
+                          (128, True, 70, "qm9", 1, K_PRE), (128, False, 70, "qm9", 1, K_PRE),
+                          (128, True, 30, "qm9", 1, K_PRE), (128, False, 30, "qm9", 1, K_PRE),
+                          (1024, True, 50, "molpcba", 1, 4), (2048, True, 60, "pcqm4mv2", 2, 4)],
                          ids=["B512-lanes", "B512-whole", "B128-lanes", "B128-whole",
-                              "B128-lanes-s30", "B128-whole-s30"])
-def test_pretrain_trajectory_replayed(pkg, dev, B_PRE, split, seed):
+                              "B128-lanes-s30", "B128-whole-s30", "molpcba-B1024-aggfree",
+                              "pcqm-B2048-k2-aggfree"])
+def test_pretrain_trajectory_replayed(pkg, dev, B_PRE, split, seed, wl, k, n_steps):
+    """(molpcba B1024 k1 and PCQM4Mv2 B2048 k2 = configs[2] / configs[3]'s
+    per-GPU steps: their ego layers run above ops.AGG_FREE_MIN_ROWS, so the
+    agg-free backward is on the replayed path, and k = 2 takes the bitmap
+    ego builder)"""
     import bench
     from oracle import scgib_ref as R
-    k, F_in = 1, pkg.synth.WORKLOADS["qm9"][2]
-    hosts = [pkg.graph.collate_pyg(pkg.synth.molecules(B_PRE, "qm9", seed=seed + i))[0]
+    F_in = pkg.synth.WORKLOADS[wl][2]
+    hosts = [pkg.graph.collate_pyg(pkg.synth.molecules(B_PRE, wl, seed=seed + i))[0]
              for i in range(POOL_PRE)]
     model = _pretrain_model(pkg, F_in, k, B_PRE, dev)
     opt = pkg.optim.Adam(model.parameters(), lr=1e-4, weight_decay=5e-5)
@@ -316,7 +326,10 @@ def test_pretrain_trajectory_replayed(pkg, dev, B_PRE, split, seed):
     assert c0 == 3  # the builder's three eager warm-up steps loaded pool[0..2]
     gen = torch.Generator().manual_seed(4242)
     plan = []
-    for j in range(K_PRE):
+    if wl != "qm9":  # the agg-free layers are on this step's path
+        n_ego = pkg.graph.StaticBatch.capacities(hosts, k, slack=1.02)[3][0]
+        assert pkg.ops.AGG_FREE and n_ego >= pkg.ops.AGG_FREE_MIN_ROWS, n_ego
+    for j in range(n_steps):
         b = (c0 + j) % POOL_PRE
         n = hosts[b].num_nodes()
         plan.append((b, torch.rand(n, generator=gen), torch.rand(n, 64, generator=gen)))
@@ -349,7 +362,7 @@ def test_pretrain_trajectory_replayed(pkg, dev, B_PRE, split, seed):
     # parity and stay untouched: only the HOT modules are the oracle's)
     outs, first, _ = _lockstep("pretrain", model, opt, replay, oracle_step, plan, names, key_of,
                                1e-4, 5e-5, HOT)
-    assert int(rs.pool["cursor"][0]) == c0 + K_PRE
+    assert int(rs.pool["cursor"][0]) == c0 + n_steps
     assert rs.prefetch.error() == 0 and rs.static.ego_error() == 0
     pkg.ops.check_handoff(dev)
     # free-running: the fp64 oracle's own trajectory from the first state

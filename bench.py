@@ -16,6 +16,7 @@ Prints ONE JSON line on rank 0 (see README/DESIGN.md for the fields).
 from __future__ import annotations
 
 import argparse
+import contextlib
 import importlib
 import json
 import os
@@ -714,7 +715,8 @@ def finetune_leg(a, dev):
 
 
 def build_replay_step(model, opt, pool_host, k, batch, dev, prefetch=True, noise=None,
-                      collective=False, reducer=None, warm=3, split=True, noise_prefetch=True):
+                      collective=False, reducer=None, warm=3, split=True, noise_prefetch=True,
+                      fuse_adam=True):
     """The bench's pretrain step (exp_pretraining.py:290-333) as ONE captured
     HIP graph in capacity mode: the pool's next resident batch (and the ego-nets
     the previous step built for it) loaded inside the graph, forward, backward,
@@ -732,7 +734,9 @@ def build_replay_step(model, opt, pool_host, k, batch, dev, prefetch=True, noise
     Returns step(i), the static losses (kl, rec, con), the static batch, the
     device pool and its prefetch, the all-reduce mode, the node count of the
     captured graph, the split (None: the captured graph is replayed) and the
-    noise prefetch (None: drawn in the forward, or passed in)."""
+    noise prefetch (None: drawn in the forward, or passed in).  ``fuse_adam``
+    (no collective): the ego chain's final weight-gradient reduce and Adam
+    as one launch (ops.fuse_final_into_step; the same bits)."""
     n_cap, e_cap, mgn, ego_caps = pkg.graph.StaticBatch.capacities(pool_host, k, slack=1.02)
     F_in = pool_host[0].ndata["x"].shape[1]
     static = pkg.graph.StaticBatch(batch, n_cap, e_cap, F_in, mgn, ego_caps, dev, k=k)
@@ -779,15 +783,20 @@ def build_replay_step(model, opt, pool_host, k, batch, dev, prefetch=True, noise
         reducer.reduce(force=True)
         reducer.unpack()
 
+    def fused():  # (a collective reads the gradients between the backward and the step)
+        return (pkg.ops.fuse_final_into_step() if fuse_adam and not collective
+                else contextlib.nullcontext())
+
     side = torch.cuda.Stream()
     side.wait_stream(torch.cuda.current_stream())
     with torch.cuda.stream(side):  # warm-up (allocator, Adam state, RCCL comm) off the capture
         for i in range(warm):
             opt.zero_grad(set_to_none=True)
-            body()
-            if collective:
-                bucket()
-            opt.step()
+            with fused():
+                body()
+                if collective:
+                    bucket()
+                opt.step()
     torch.cuda.current_stream().wait_stream(side)
     torch.cuda.synchronize()
     graph2 = None
@@ -821,7 +830,7 @@ def build_replay_step(model, opt, pool_host, k, batch, dev, prefetch=True, noise
             opt.zero_grad(set_to_none=True)
             graph2 = "fallback"
     if not collective:
-        with torch.cuda.graph(graph):
+        with torch.cuda.graph(graph), fused():
             static_loss = body()
             opt.step()
     elif graph2 is not None or not capture_ok:
@@ -932,6 +941,9 @@ def main():
                     help="skip the event-timed kernel pass (PMC runs: only real step launches)")
     ap.add_argument("--eager", action="store_true",
                     help="launch every kernel from Python (no HIP-graph capture)")
+    ap.add_argument("--no-fuse-adam", action="store_true",
+                    help="launch the ego chain's final weight-gradient reduce and Adam "
+                         "separately (ops.fuse_final_into_step; A/B)")
     ap.add_argument("--no-noise-prefetch", action="store_true",
                     help="pretrain: draw each step's compression noise at the head of its forward "
                          "core chain instead of in the step before's backward (ops.NoisePrefetch; "
@@ -1060,7 +1072,8 @@ def main():
         rs = build_replay_step(model, opt, pool_host, a.k, a.batch, dev,
                                prefetch=not a.no_ego_prefetch, collective=collective,
                                reducer=reducer, split=not a.no_split,
-                               noise_prefetch=not a.no_noise_prefetch)
+                               noise_prefetch=not a.no_noise_prefetch,
+                               fuse_adam=not a.no_fuse_adam)
         step, allreduce_mode, graph_nodes = rs.step, rs.allreduce_mode, rs.graph_nodes
         if rs.noise_prefetch is not None:
             noise_draw = "in the step before's backward, core chain end (ops.NoisePrefetch)"
@@ -1220,6 +1233,10 @@ def main():
                                      "(graph.EgoPrefetch)" if not a.eager
                                      and not a.no_ego_prefetch else "at the head of the step"),
                        "noise_draw": noise_draw,
+                       "adam": ("one launch with the ego chain's final weight-gradient reduce "
+                                "(scgib_adam_step_reduce)" if not (a.eager or collective
+                                                                  or a.no_fuse_adam)
+                                else "its own launch"),
                        "allreduce": None if not collective else
                        ("eager" if a.eager else allreduce_mode),
                        "handoffs": ("signal / wait kernels" if pkg.ops.xq_enabled() else

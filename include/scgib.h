@@ -787,6 +787,19 @@ int64_t scgib_adam_max_tensors(void);
 int scgib_adam_step(const scgib_adam_tensor *tensors, int32_t n_tensors, double lr,
                     double beta1, double beta2, double eps, double weight_decay,
                     uint32_t *counter, scgib_stream_t stream);
+/* scgib_slab_reduce_multi(jobs) followed by scgib_adam_step(tensors) in ONE
+ * launch, with the same bits: a tensor whose gradient lies inside a job's
+ * output is updated by the reduce's workgroups from the value they produce
+ * (the replayed pretraining step's last weight-gradient reduce and its Adam
+ * step, models.py's training loop exp_pretraining.py:321-323 — no reference
+ * counterpart of its own; ABI 22).  n_jobs <= scgib_adam_reduce_max_jobs();
+ * a gradient that straddles a job output's edge, or two tensors' gradients
+ * overlapping inside one: SCGIB_EINVAL. */
+int64_t scgib_adam_reduce_max_jobs(void);
+int scgib_adam_step_reduce(const scgib_adam_tensor *tensors, int32_t n_tensors,
+                           const scgib_slab_job *jobs, int32_t n_jobs, double lr, double beta1,
+                           double beta2, double eps, double weight_decay, uint32_t *counter,
+                           scgib_stream_t stream);
 
 
 /* ---- data parallelism: gradient bucket (dist.GradAllReducer) --------------

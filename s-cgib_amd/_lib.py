@@ -150,6 +150,8 @@ SIGNATURES = {
     "scgib_grad_unpack": (ctypes.c_int, [_P, _I32, _P, _F, _P]),
     "scgib_adam_max_tensors": (_I64, []),
     "scgib_adam_step": (ctypes.c_int, [_P, _I32, _D, _D, _D, _D, _D, _P, _P]),
+    "scgib_adam_reduce_max_jobs": (_I64, []),
+    "scgib_adam_step_reduce": (ctypes.c_int, [_P, _I32, _P, _I32, _D, _D, _D, _D, _D, _P, _P]),
 }
 
 
@@ -192,7 +194,7 @@ class RunningUpdate(ctypes.Structure):
                 ("num_batches_tracked", ctypes.c_void_p)]
 
 
-ABI_VERSION = 21
+ABI_VERSION = 22
 STATS_STRIDE = 260
 PGRAD_STRIDE = 324
 HIDDEN = 64

@@ -45,6 +45,29 @@ struct AdamRef {
 // hyper-parameters are doubles, so the weight decay, both moment updates and
 // eps enter in double and round to fp32 on assignment; the bias corrections
 // are computed in double and rounded to fp32; the final update is fp32.
+// One element (shared by adam_chunk and the fused reduce + Adam launch, so
+// both give the same bits).
+__device__ __forceinline__ void adam_elem(float p, float g, float m, float v, float step_size,
+                                          float bc2_sqrt, double beta1, double beta2, double eps,
+                                          double wd, float &pp, float &mm, float &vv) {
+    float gg = g;
+    if (wd != 0.0) gg = static_cast<float>(gg + p * wd);
+    mm = static_cast<float>(beta1 * m + (1 - beta1) * gg);
+    vv = static_cast<float>(beta2 * v + (1 - beta2) * gg * gg);
+    const float denom = static_cast<float>(sqrtf(vv) / bc2_sqrt + eps);
+    pp = p - step_size * mm / denom;
+}
+
+// the tensor's bias corrections at its step t = *step + 1
+__device__ __forceinline__ void adam_coef(const float *step, double lr, double beta1,
+                                          double beta2, float &step_size, float &bc2_sqrt) {
+    const float t = *step + 1.f;
+    const float bc1 = static_cast<float>(1 - pow(beta1, static_cast<double>(t)));
+    bc2_sqrt = static_cast<float>(sqrt(1 - pow(beta2, static_cast<double>(t))));
+    step_size = static_cast<float>(lr / bc1);
+}
+
+template <int NT>  // threads per workgroup; a chunk is 4 NT elements
 __device__ __forceinline__ void adam_chunk(const AdamRef &T, int64_t base,
                                            float step_size, float bc2_sqrt, double beta1,
                                            double beta2, double eps, double wd) {
@@ -52,7 +75,7 @@ __device__ __forceinline__ void adam_chunk(const AdamRef &T, int64_t base,
     int64_t idx[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {  // clamped loads (all in flight), masked stores
-        const int64_t j = base + threadIdx.x + 256 * k;
+        const int64_t j = base + threadIdx.x + NT * k;
         idx[k] = j < T.numel ? j : T.numel - 1;
         p[k] = T.param[idx[k]];
         g[k] = T.grad[idx[k]];
@@ -61,13 +84,9 @@ __device__ __forceinline__ void adam_chunk(const AdamRef &T, int64_t base,
     }
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-        float gg = g[k];
-        if (wd != 0.0) gg = static_cast<float>(gg + p[k] * wd);
-        const float mm = static_cast<float>(beta1 * m[k] + (1 - beta1) * gg);
-        const float vv = static_cast<float>(beta2 * v[k] + (1 - beta2) * gg * gg);
-        const float denom = static_cast<float>(sqrtf(vv) / bc2_sqrt + eps);
-        const float pp = p[k] - step_size * mm / denom;
-        if (base + threadIdx.x + 256 * k < T.numel) {
+        float pp, mm, vv;
+        adam_elem(p[k], g[k], m[k], v[k], step_size, bc2_sqrt, beta1, beta2, eps, wd, pp, mm, vv);
+        if (base + threadIdx.x + NT * k < T.numel) {
             T.param[idx[k]] = pp;
             T.exp_avg[idx[k]] = mm;
             T.exp_avg_sq[idx[k]] = vv;
@@ -90,12 +109,10 @@ __global__ __launch_bounds__(256) void adam_step_k(const AdamTable tab, double l
         i += __popcll(__ballot(le));
     }
     const AdamRef T{tab.param[i], tab.grad[i], tab.exp_avg[i], tab.exp_avg_sq[i], tab.numel[i]};
-    const float t = *tab.step[i] + 1.f;
-    const float bc1 = static_cast<float>(1 - pow(beta1, static_cast<double>(t)));
-    const float bc2_sqrt = static_cast<float>(sqrt(1 - pow(beta2, static_cast<double>(t))));
-    const float step_size = static_cast<float>(lr / bc1);
+    float step_size, bc2_sqrt;
+    adam_coef(tab.step[i], lr, beta1, beta2, step_size, bc2_sqrt);
     const int64_t base = static_cast<int64_t>(b - tab.chunk0[i]) * kAdamChunk;
-    if (T.numel > 0) adam_chunk(T, base, step_size, bc2_sqrt, beta1, beta2, eps, wd);
+    if (T.numel > 0) adam_chunk<256>(T, base, step_size, bc2_sqrt, beta1, beta2, eps, wd);
     __shared__ unsigned s_last;
     __syncthreads();
     if (threadIdx.x == 0)
@@ -103,6 +120,120 @@ __global__ __launch_bounds__(256) void adam_step_k(const AdamTable tab, double l
                  gridDim.x - 1;
     __syncthreads();
     if (s_last) {  // every workgroup has read its step: advance all of them at once
+        if (threadIdx.x < tab.n) *tab.step[threadIdx.x] += 1.f;
+        if (threadIdx.x == 0) *counter = 0u;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// The step's last weight-gradient reduce and the Adam step in ONE launch
+// (scgib_adam_step_reduce): the reduce's column blocks (slab_reduce_multi_k's
+// decomposition and fixed order, so every gradient has the same bits) apply
+// Adam to the elements of the tensors whose gradients they produce, right
+// where the reduced value is in a register; the other tensors' Adam chunks
+// run as the launch's remaining workgroups, beside them.  The replayed
+// pretraining step ended with the two launches back to back (the ego chain's
+// final reduce after the join, then Adam): one launch boundary and the Adam
+// launch's latency leave its tail.
+// ---------------------------------------------------------------------------
+constexpr int kFuseJobs = 8;
+constexpr int kFuseSegs = 16;
+constexpr int kFuseChunk = 4 * 1024;  // Adam elements per 1024-thread workgroup
+
+struct FuseTable {
+    scgib_slab_job j[kFuseJobs];
+    int32_t blk0[kFuseJobs + 1];  // first column block of job i; blk0[nj] = reduce blocks
+    int32_t nj;
+    // reduced tensors: table entry t's gradient = elements [o0, o0 + numel) of job's output
+    int32_t seg_t[kFuseSegs], seg_job[kFuseSegs], seg_o0[kFuseSegs];
+    int32_t ns;
+};
+
+__global__ __launch_bounds__(1024) void adam_reduce_k(const AdamTable tab, const FuseTable ft,
+                                                      double lr, double beta1, double beta2,
+                                                      double eps, double wd,
+                                                      unsigned *__restrict__ counter) {
+    const int b = blockIdx.x;
+    const int lane = threadIdx.x & 63;
+    const int nred = ft.blk0[ft.nj];
+    __shared__ float red[16][64];
+    if (b < nred) {  // block-uniform: one column block of one reduce job
+        const int el = threadIdx.x & 63, sp = threadIdx.x >> 6;
+        const bool le = lane < ft.nj && ft.blk0[lane < ft.nj ? lane : 0] <= b;
+        const int i = __popcll(__ballot(le)) - 1;
+        const scgib_slab_job &J = ft.j[i];
+        const int64_t e = static_cast<int64_t>(b - ft.blk0[i]) * 64 + el;
+        const int64_t stride = J.stride > 0 ? J.stride : J.width;
+        // the Adam tensor of this element's gradient, its bias corrections and
+        // operands: independent of the sums, so in flight with the slab loads
+        int t = -1;
+        int64_t o = 0;
+        float step_size = 0.f, bc2_sqrt = 1.f, p0 = 0.f, m0 = 0.f, v0 = 0.f;
+        if (sp == 0 && e < J.width) {
+            for (int q = 0; q < ft.ns; ++q) {
+                const int64_t oq = e - ft.seg_o0[q];
+                if (ft.seg_job[q] == i && oq >= 0 && oq < tab.numel[ft.seg_t[q]]) {
+                    t = ft.seg_t[q];
+                    o = oq;
+                }
+            }
+            if (t >= 0) {
+                p0 = tab.param[t][o];
+                m0 = tab.exp_avg[t][o];
+                v0 = tab.exp_avg_sq[t][o];
+                adam_coef(tab.step[t], lr, beta1, beta2, step_size, bc2_sqrt);
+            }
+        }
+        float acc = 0.f;
+        if (e < J.width) {
+            for (int b0 = sp; b0 < J.n_slabs; b0 += 16 * 8) {
+                float v[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u)
+                    v[u] = ld_ok(J.slab, static_cast<int64_t>(b0 + 16 * u) * stride + e, e,
+                                 b0 + 16 * u < J.n_slabs, 0.f);
+#pragma unroll
+                for (int u = 0; u < 8; ++u) acc += v[u];
+            }
+        }
+        red[sp][el] = acc;
+        __syncthreads();
+        if (sp == 0 && e < J.width) {
+            double sum = 0.0;
+#pragma unroll
+            for (int k = 0; k < 16; ++k) sum += static_cast<double>(red[k][el]);
+            const float g = static_cast<float>(sum);
+            J.out[e] = g;
+            if (t >= 0) {
+                float pp, mm, vv;
+                adam_elem(p0, g, m0, v0, step_size, bc2_sqrt, beta1, beta2, eps, wd, pp, mm, vv);
+                tab.param[t][o] = pp;
+                tab.exp_avg[t][o] = mm;
+                tab.exp_avg_sq[t][o] = vv;
+            }
+        }
+    } else {  // an Adam chunk of a tensor whose gradient is already complete
+        const int c = b - nred;
+        int i = -1;
+#pragma unroll
+        for (int r = 0; r < (kAdamMax + 63) / 64; ++r) {
+            const int q = 64 * r + lane;
+            const bool le = q < tab.n && tab.chunk0[q < tab.n ? q : 0] <= c;
+            i += __popcll(__ballot(le));
+        }
+        const AdamRef T{tab.param[i], tab.grad[i], tab.exp_avg[i], tab.exp_avg_sq[i], tab.numel[i]};
+        float step_size, bc2_sqrt;
+        adam_coef(tab.step[i], lr, beta1, beta2, step_size, bc2_sqrt);
+        const int64_t base = static_cast<int64_t>(c - tab.chunk0[i]) * kFuseChunk;
+        if (T.numel > 0) adam_chunk<1024>(T, base, step_size, bc2_sqrt, beta1, beta2, eps, wd);
+    }
+    __shared__ unsigned s_last;
+    __syncthreads();
+    if (threadIdx.x == 0)
+        s_last = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                 gridDim.x - 1;
+    __syncthreads();
+    if (s_last) {  // every workgroup has read its steps: advance all of them at once
         if (threadIdx.x < tab.n) *tab.step[threadIdx.x] += 1.f;
         if (threadIdx.x == 0) *counter = 0u;
     }
@@ -229,4 +360,78 @@ extern "C" int scgib_grad_unpack(const scgib_grad_slice *tensors, int32_t n_tens
                                  const float *flat, float scale, scgib_stream_t stream) {
     return launch_pack(tensors, n_tensors, const_cast<float *>(flat), scale, true,
                        as_stream(stream));
+}
+
+extern "C" int64_t scgib_adam_reduce_max_jobs(void) { return scgib::kFuseJobs; }
+
+extern "C" int scgib_adam_step_reduce(const scgib_adam_tensor *tensors, int32_t n_tensors,
+                                      const scgib_slab_job *jobs, int32_t n_jobs, double lr,
+                                      double beta1, double beta2, double eps, double weight_decay,
+                                      uint32_t *counter, scgib_stream_t stream) {
+    using namespace scgib;
+    if (n_tensors < 0 || n_tensors > kAdamMax || n_jobs < 0 || n_jobs > kFuseJobs) return SCGIB_EINVAL;
+    if (n_jobs == 0) return scgib_adam_step(tensors, n_tensors, lr, beta1, beta2, eps, weight_decay,
+                                            counter, stream);
+    if (!jobs || !counter || (n_tensors > 0 && !tensors)) return SCGIB_EINVAL;
+    FuseTable ft{};
+    ft.nj = n_jobs;
+    int64_t blocks = 0;
+    for (int i = 0; i < n_jobs; ++i) {
+        const scgib_slab_job &J = jobs[i];
+        if (J.n_slabs <= 0 || J.width <= 0 || !J.slab || !J.out) return SCGIB_EINVAL;
+        if (J.stride < 0 || (J.stride > 0 && J.stride < J.width)) return SCGIB_EINVAL;
+        ft.j[i] = J;
+        ft.blk0[i] = static_cast<int32_t>(blocks);
+        blocks += (J.width + 63) / 64;
+        if (blocks > 0x3fffffff) return SCGIB_EUNSUPPORTED;
+    }
+    ft.blk0[n_jobs] = static_cast<int32_t>(blocks);
+    AdamTable tab{};
+    tab.n = n_tensors;
+    int64_t chunks = 0;
+    for (int t = 0; t < n_tensors; ++t) {
+        const scgib_adam_tensor &T = tensors[t];
+        if (T.numel < 0 || !T.step || (T.numel > 0 && (!T.param || !T.grad || !T.exp_avg ||
+                                                       !T.exp_avg_sq)))
+            return SCGIB_EINVAL;
+        if (T.numel > 0x7fffffff) return SCGIB_EUNSUPPORTED;
+        tab.param[t] = T.param;
+        tab.grad[t] = T.grad;
+        tab.exp_avg[t] = T.exp_avg;
+        tab.exp_avg_sq[t] = T.exp_avg_sq;
+        tab.step[t] = T.step;
+        tab.numel[t] = static_cast<int32_t>(T.numel);
+        tab.chunk0[t] = static_cast<int32_t>(chunks);
+        // a gradient inside a job's output: Adam in the reduce (no chunks of its own);
+        // one that straddles an output's edge is refused
+        int seg = -1;
+        for (int i = 0; i < n_jobs && T.numel > 0; ++i) {
+            const float *o0 = jobs[i].out, *o1 = jobs[i].out + jobs[i].width;
+            const float *g0 = T.grad, *g1 = T.grad + T.numel;
+            if (g0 >= o0 && g1 <= o1) {
+                seg = i;
+                break;
+            }
+            if (g0 < o1 && g1 > o0) return SCGIB_EINVAL;
+        }
+        if (seg >= 0) {
+            if (ft.ns == kFuseSegs) return SCGIB_EUNSUPPORTED;
+            ft.seg_t[ft.ns] = t;
+            ft.seg_job[ft.ns] = seg;
+            ft.seg_o0[ft.ns] = static_cast<int32_t>(T.grad - jobs[seg].out);
+            ++ft.ns;
+        } else {
+            chunks += (T.numel + kFuseChunk - 1) / kFuseChunk;
+        }
+    }
+    for (int a = 0; a < ft.ns; ++a)  // each reduced element updates one tensor
+        for (int c = a + 1; c < ft.ns; ++c)
+            if (ft.seg_job[a] == ft.seg_job[c] &&
+                ft.seg_o0[a] < ft.seg_o0[c] + tab.numel[ft.seg_t[c]] &&
+                ft.seg_o0[c] < ft.seg_o0[a] + tab.numel[ft.seg_t[a]])
+                return SCGIB_EINVAL;
+    tab.chunk0[n_tensors] = static_cast<int32_t>(chunks);
+    adam_reduce_k<<<dim3(static_cast<unsigned>(blocks + chunks)), 1024, 0, as_stream(stream)>>>(
+        tab, ft, lr, beta1, beta2, eps, weight_decay, counter);
+    return launch_status();
 }

@@ -330,7 +330,7 @@ extern "C" int scgib_pool_copy(const uint64_t *srcs, int32_t n_src, uint32_t *ct
     return scgib_pool_copy2(srcs, n_src, ctr, dst, bytes, nullptr, nullptr, 0, stream);
 }
 
-extern "C" int scgib_abi_version(void) { return 21; }
+extern "C" int scgib_abi_version(void) { return 22; }
 
 extern "C" const char *scgib_strerror(int code) {
     if (code == SCGIB_OK) return "ok";

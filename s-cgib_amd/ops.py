@@ -543,6 +543,42 @@ _Z_SLAB = HIDDEN * HIDDEN + 2 * HIDDEN
 _Z_W1_OFF = _Z_SLAB
 
 
+# The ego chain's final weight-gradient reduce (after the encoder pair's
+# backward join) and the optimizer step right after it as ONE launch
+# (scgib_adam_step_reduce, optim.Adam.step): inside fuse_final_into_step() the
+# pair's backward leaves its final reduce jobs here instead of launching them,
+# and the step takes them; whatever no step took is reduced when the context
+# ends.  Only where nothing reads the gradients between the backward and the
+# step (the benches' replayed steps without a collective).
+FUSE_FINAL_ADAM = True
+# ... from this many slabs in the largest final job (the ego layer-0 weight-
+# gradient slabs): QM9 B = 512 (452 slabs) 0.3850-0.3857 vs 0.3869-0.3888 ms,
+# B = 128 (111) unchanged, B = 32 (28) 0.2541-0.2553 vs 0.2527-0.2535 ms
+# (profiles/r06_noise/fuse_adam_ab.txt): below it the Adam chunks on the
+# reduce's 1024-thread workgroups outlast the small reduce they hide behind
+FUSE_FINAL_MIN_SLABS = 256
+_FINAL_ARMED = [False]
+_FINAL_PENDING = {}  # device index -> [(jobs, keep)]
+
+
+@contextlib.contextmanager
+def fuse_final_into_step():
+    prev = _FINAL_ARMED[0]
+    _FINAL_ARMED[0] = FUSE_FINAL_ADAM
+    try:
+        yield
+    finally:
+        _FINAL_ARMED[0] = prev
+        for idx in list(_FINAL_PENDING):
+            for jobs, _keep in _FINAL_PENDING.pop(idx):
+                _reduce_jobs(jobs, _stream())
+
+
+def take_final(device):
+    """The pending final reduces of ``device`` (consumed: the caller launches them)."""
+    return _FINAL_PENDING.pop(torch.device(device).index or 0, [])
+
+
 def _reduce_jobs(jobs, st, max_wg=0):
     cap = int(_lib.query("scgib_slab_reduce_max_jobs"))
     for i0 in range(0, len(jobs), cap):
@@ -1324,7 +1360,10 @@ class _GinEncoderPair(torch.autograd.Function):
         final = getattr(ctx.sub[0], "final", None)
         if final is not None:  # the ego chain's weight-gradient reduce, d Wt(core) included
             ctx.sub[0].final = None
-            _reduce_jobs(final[0], _stream())
+            if _FINAL_ARMED[0]:  # left to the optimizer step that follows (fuse_final_into_step)
+                _FINAL_PENDING.setdefault(main.device_index or 0, []).append(final)
+            else:
+                _reduce_jobs(final[0], _stream())
             final = None
         ctx.sub[0].dwt_row_slab = None
         if ctx.side_tail is not None and hasattr(ctx.side_tail, "joined"):

@@ -62,6 +62,10 @@ class Adam(torch.optim.Optimizer):
         if closure is not None:
             with torch.enable_grad():
                 loss = closure()
+        pending = []  # the final weight-gradient reduces left to this step (ops.fuse_final_into_step)
+        for group in self.param_groups:
+            pending += ops.take_final(group["params"][0].device) if group["params"] else []
+        fused = False
         for gi, group in enumerate(self.param_groups):
             ent = self._entries(group)
             if not ent:
@@ -69,6 +73,23 @@ class Adam(torch.optim.Optimizer):
             dev = group["params"][0].device
             b1, b2 = group["betas"]
             st = ops._stream()
+            jobs = [j for jl, _ in pending for j in jl]
+            if (jobs and not fused and len(self.param_groups) == 1 and len(ent) <= self._max
+                    and len(jobs) <= int(_lib.query("scgib_adam_reduce_max_jobs"))
+                    and max(j.n_slabs for j in jobs) >= ops.FUSE_FINAL_MIN_SLABS):
+                # the reduce and this step in one launch (same bits)
+                table = (_lib.AdamTensor * len(ent))(*ent)
+                jt = (_lib.SlabJob * len(jobs))(*jobs)
+                _lib.call("scgib_adam_step_reduce", ctypes.cast(table, ctypes.c_void_p), len(ent),
+                          ctypes.cast(jt, ctypes.c_void_p), len(jobs), float(group["lr"]),
+                          float(b1), float(b2), float(group["eps"]), float(group["weight_decay"]),
+                          ops._p(ops.counters(dev, "adam", 1)), st)
+                fused = True
+                continue
+            if pending and not fused:  # not fusable here: the reduces first, as unfused
+                for jl, _ in pending:
+                    ops._reduce_jobs(jl, st)
+                fused = True
             for li, i0 in enumerate(range(0, len(ent), self._max)):
                 chunk = ent[i0:i0 + self._max]
                 table = (_lib.AdamTensor * len(chunk))(*chunk)
@@ -78,5 +99,9 @@ class Adam(torch.optim.Optimizer):
                 _lib.call("scgib_adam_step", ctypes.cast(table, ctypes.c_void_p), len(chunk),
                           float(group["lr"]), float(b1), float(b2), float(group["eps"]),
                           float(group["weight_decay"]), ops._p(cnt), st)
+        if pending and not fused:  # (no gradients here at all)
+            for jl, _ in pending:
+                ops._reduce_jobs(jl, ops._stream())
+        pending = None  # the slabs stay referenced until the launches are enqueued
         ops.stamp("adam_end")
         return loss

@@ -239,3 +239,36 @@ def test_finetune_noise_prefetch_matches_inline_draw(pkg, dev):
     assert torch.isfinite(runs[0][0]).all()
     assert torch.equal(runs[0][0], runs[1][0]), (runs[0][0], runs[1][0])
     _assert_bitwise(runs[0][1], runs[1][1])
+
+
+def test_fused_final_reduce_adam_matches_separate(pkg, dev, monkeypatch):
+    """scgib_adam_step_reduce (ops.fuse_final_into_step): the bench's replayed
+    step with the ego chain's final weight-gradient reduce and Adam in one
+    launch computes bitwise what the two launches compute — losses, every
+    parameter, Adam's moments and steps — over 6 replays."""
+    import bench
+    from test_gpu_trajectory import _pretrain_model
+    k, B, K, POOL = 1, 128, 6, 3
+    monkeypatch.setattr(pkg.ops, "FUSE_FINAL_MIN_SLABS", 0)  # (B = 128: 111 slabs, under the gate)
+    F_in = pkg.synth.WORKLOADS["qm9"][2]
+    hosts = [pkg.graph.collate_pyg(pkg.synth.molecules(B, "qm9", seed=80 + i))[0]
+             for i in range(POOL)]
+    runs = []
+    for fuse in (False, True):
+        model = _pretrain_model(pkg, F_in, k, B, dev)
+        opt = pkg.optim.Adam(model.parameters(), lr=1e-4, weight_decay=5e-5)
+        pkg.ops.seed_noise(dev, 99)
+        rs = bench.build_replay_step(model, opt, hosts, k, B, dev, prefetch=True, fuse_adam=fuse)
+        assert not pkg.ops._FINAL_PENDING and not pkg.ops._FINAL_ARMED[0]
+        losses = []
+        for j in range(K):
+            kl, rec, con = rs.step(j)
+            losses.append(torch.stack([kl, rec, con]).clone())
+        torch.cuda.synchronize()
+        assert pkg.ops.xq_timeouts(dev) == 0
+        runs.append((torch.stack(losses), _state(model, opt)))
+        if rs.split is not None:
+            rs.split.close()
+    assert torch.isfinite(runs[0][0]).all()
+    assert torch.equal(runs[0][0], runs[1][0]), (runs[0][0], runs[1][0])
+    _assert_bitwise(runs[0][1], runs[1][1])

@@ -193,3 +193,74 @@ def test_bench_allreduce_captured_one_rank_rccl():
     line = json.loads(out.stdout.strip().splitlines()[-1])
     assert line["config"]["allreduce"] == "captured in the step graph", out.stderr[-2000:]
     assert line["value"] > 0 and line["config"]["final_loss"] == line["config"]["final_loss"]
+
+
+def test_adam_step_reduce_matches_reduce_then_step(pkg, dev):
+    """scgib_adam_step_reduce: the slab reduce of two jobs (one with a column
+    stride) and the Adam step in one launch, bitwise the reduce launch
+    followed by scgib_adam_step — for tensors inside a job's output (several
+    per job, one not at its start), tensors outside, a reduced output no
+    tensor covers, and a tensor larger than one fused chunk; a gradient
+    straddling an output's edge is refused."""
+    import ctypes
+    L, ops = pkg._lib, pkg.ops
+    gen = torch.Generator().manual_seed(5)
+    nslab, w0, w1, stride1 = 37, 64 * 64 + 64 + 96, 1000, 1200
+    slab0 = torch.randn(nslab, w0, generator=gen).to(dev)
+    slab1 = torch.randn(nslab + 2, stride1, generator=gen).to(dev)
+    shapes = [(64, 64), (64,), (96,), (3, 7), (9000,), (700,)]
+
+    def run(fused):
+        out0 = torch.zeros(w0, device=dev)
+        out1 = torch.zeros(w1, device=dev)
+        ps = [torch.randn(s, generator=torch.Generator().manual_seed(i)).to(dev)
+              for i, s in enumerate(shapes)]
+        grads = [out0[:4096].view(64, 64), out0[4096:4160], out1[200:296],
+                 torch.randn(3, 7, generator=torch.Generator().manual_seed(9)).to(dev),
+                 torch.randn(9000, generator=torch.Generator().manual_seed(10)).to(dev),
+                 out1[300:1000]]  # (out0's last 96 columns, out1[:200] and [296:300]: no tensor)
+        mg = torch.Generator().manual_seed(21)
+        steps = [torch.full((), 3.0, device=dev) for _ in shapes]
+        ms = [(torch.rand(s, generator=mg).to(dev), torch.rand(s, generator=mg).to(dev))
+              for s in shapes]
+        ent = [L.AdamTensor(p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr(), s.data_ptr(),
+                            p.numel()) for p, g, s, (m, v) in zip(ps, grads, steps, ms)]
+        jobs = [L.SlabJob(slab0.data_ptr(), out0.data_ptr(), w0, nslab, 0),
+                L.SlabJob(slab1.data_ptr(), out1.data_ptr(), w1, nslab + 2, stride1)]
+        tab = (L.AdamTensor * len(ent))(*ent)
+        jt = (L.SlabJob * 2)(*jobs)
+        cnt = ops.counters(dev, "adam", 1)
+        args = (1e-3, 0.9, 0.999, 1e-8, 5e-5, ops._p(cnt), ops._stream())
+        if fused:
+            L.call("scgib_adam_step_reduce", ctypes.cast(tab, ctypes.c_void_p), len(ent),
+                   ctypes.cast(jt, ctypes.c_void_p), 2, *args)
+        else:
+            L.call("scgib_slab_reduce_multi", ctypes.cast(jt, ctypes.c_void_p), 2, ops._stream())
+            L.call("scgib_adam_step", ctypes.cast(tab, ctypes.c_void_p), len(ent), *args)
+        torch.cuda.synchronize()
+        return [out0, out1] + ps + steps + [t for mv in ms for t in mv]
+
+    a, b = run(False), run(True)
+    assert all(torch.equal(x, y) for x, y in zip(a, b))
+    assert float(b[2 + len(shapes)]) == 4.0  # steps advanced once
+    # a gradient straddling the end of a job's output
+    out0 = torch.zeros(w0, device=dev)
+    p = torch.zeros(128, device=dev)
+    m, v, s = torch.zeros(128, device=dev), torch.zeros(128, device=dev), torch.zeros((), device=dev)
+    bad = (L.AdamTensor * 1)(L.AdamTensor(p.data_ptr(), out0.data_ptr() + 4 * (w0 - 64),
+                                          m.data_ptr(), v.data_ptr(), s.data_ptr(), 128))
+    jt = (L.SlabJob * 1)(L.SlabJob(slab0.data_ptr(), out0.data_ptr(), w0, nslab, 0))
+    with pytest.raises(L.ScgibError):
+        L.call("scgib_adam_step_reduce", ctypes.cast(bad, ctypes.c_void_p), 1,
+               ctypes.cast(jt, ctypes.c_void_p), 1, 1e-3, 0.9, 0.999, 1e-8, 0.0,
+               ops._p(ops.counters(dev, "adam", 1)), ops._stream())
+    # two tensors' gradients overlapping inside one output
+    q = torch.zeros(128, device=dev)
+    two = (L.AdamTensor * 2)(L.AdamTensor(p.data_ptr(), out0.data_ptr(), m.data_ptr(), v.data_ptr(),
+                                          s.data_ptr(), 128),
+                             L.AdamTensor(q.data_ptr(), out0.data_ptr() + 4 * 64, m.data_ptr(),
+                                          v.data_ptr(), s.data_ptr(), 128))
+    with pytest.raises(L.ScgibError):
+        L.call("scgib_adam_step_reduce", ctypes.cast(two, ctypes.c_void_p), 2,
+               ctypes.cast(jt, ctypes.c_void_p), 1, 1e-3, 0.9, 0.999, 1e-8, 0.0,
+               ops._p(ops.counters(dev, "adam", 1)), ops._stream())

@@ -29,7 +29,7 @@ python tools/pmc_summary.py "$O/pmc" qm9,512,1 > "$O/traffic.json" && echo traff
 # the replayed steps from the timer pass (the launches the timer averages)
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_kt -o kt \
   -- python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-superbatch --no-finetune > $O/prof_bench.log 2>&1 || { echo rocprof failed; exit 1; }
-python tools/kernel_instances.py $O/prof_kt --split adam_step_k --json $O/replay.json --config qm9,512,1 > $O/kernel_instances.txt 2>&1 && echo replay ok
+python tools/kernel_instances.py $O/prof_kt --split adam_step_k,adam_reduce_k --json $O/replay.json --config qm9,512,1 > $O/kernel_instances.txt 2>&1 && echo replay ok
 # the fine-tune step (bench.py --finetune molhiv): PMC passes, kernel trace, stamps
 FARGS="--finetune molhiv --steps 5 --warmup 2 --no-cpu-baseline --no-kernel-timer"
 for C in FETCH_SIZE WRITE_SIZE; do

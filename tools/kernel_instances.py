@@ -2,7 +2,7 @@
 python tools/kernel_instances.py gpurun_out/TAG/prof_kt [--split KERNEL]
 
 --split KERNEL: two tables, the dispatches up to the last KERNEL dispatch
-(the bench's replayed steps, which end in adam_step_k) and those after it
+(the bench's replayed steps, which end in adam_step_k or adam_reduce_k) and those after it
 (the bench's kernel-timer pass: forward + backward, unforked, no optimizer
 step) — the second is the set of launches the bench's HIP-event timer
 averages.
@@ -49,7 +49,10 @@ for fn in files:
 rows.sort()
 parts = [("all dispatches", rows)]
 if split:
-    last = max((i for i, r in enumerate(rows) if r[2].startswith(split)), default=-1)
+    # (comma-separated: the last dispatch of any, e.g. adam_step_k,adam_reduce_k —
+    # the replayed pretraining step ends in the fused reduce + Adam launch)
+    last = max((i for i, r in enumerate(rows) if r[2].startswith(tuple(split.split(",")))),
+               default=-1)
     parts = [(f"up to the last {split} (replayed steps)", rows[:last + 1]),
              (f"after it (kernel-timer pass)", rows[last + 1:])]
 for title, part in parts:

@@ -25,7 +25,7 @@ for C in "${CONFIGS[@]}"; do
   python tools/pmc_summary.py "$D/pmc" $W,$B,$K > "$D/traffic.json" && echo "$W traffic ok"
   timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $D/kt -o kt \
     -- python bench.py $A --steps 20 --warmup 5 --no-cpu-baseline --no-superbatch --no-finetune > $D/kt_bench.log 2>&1 || { echo "$W trace failed"; exit 1; }
-  python tools/kernel_instances.py $D/kt --split adam_step_k --json $D/replay.json --config $W,$B,$K > $D/kernel_instances.txt 2>&1 && echo "$W replay ok"
+  python tools/kernel_instances.py $D/kt --split adam_step_k,adam_reduce_k --json $D/replay.json --config $W,$B,$K > $D/kernel_instances.txt 2>&1 && echo "$W replay ok"
   SCGIB_TRAFFIC_FILE=$D/traffic.json SCGIB_REPLAY_FILE=$D/replay.json timeout -k 10 600 \
     python bench.py $A --steps 100 --warmup 10 --no-cpu-baseline --no-superbatch --no-finetune > $D/bench.log 2>&1 || { echo "$W bench failed"; exit 1; }
   tail -1 $D/bench.log | python -c "

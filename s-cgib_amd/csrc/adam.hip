@@ -67,14 +67,14 @@ __device__ __forceinline__ void adam_coef(const float *step, double lr, double b
     step_size = static_cast<float>(lr / bc1);
 }
 
-template <int NT>  // threads per workgroup; a chunk is 4 NT elements
+template <int NT, int EPT = 4>  // threads per workgroup; a chunk is EPT * NT elements
 __device__ __forceinline__ void adam_chunk(const AdamRef &T, int64_t base,
                                            float step_size, float bc2_sqrt, double beta1,
                                            double beta2, double eps, double wd) {
-    float p[4], g[4], m[4], v[4];
-    int64_t idx[4];
+    float p[EPT], g[EPT], m[EPT], v[EPT];
+    int64_t idx[EPT];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {  // clamped loads (all in flight), masked stores
+    for (int k = 0; k < EPT; ++k) {  // clamped loads (all in flight), masked stores
         const int64_t j = base + threadIdx.x + NT * k;
         idx[k] = j < T.numel ? j : T.numel - 1;
         p[k] = T.param[idx[k]];
@@ -83,7 +83,7 @@ __device__ __forceinline__ void adam_chunk(const AdamRef &T, int64_t base,
         v[k] = T.exp_avg_sq[idx[k]];
     }
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
+    for (int k = 0; k < EPT; ++k) {
         float pp, mm, vv;
         adam_elem(p[k], g[k], m[k], v[k], step_size, bc2_sqrt, beta1, beta2, eps, wd, pp, mm, vv);
         if (base + threadIdx.x + NT * k < T.numel) {
@@ -138,7 +138,15 @@ __global__ __launch_bounds__(256) void adam_step_k(const AdamTable tab, double l
 // ---------------------------------------------------------------------------
 constexpr int kFuseJobs = 8;
 constexpr int kFuseSegs = 16;
-constexpr int kFuseChunk = 4 * 1024;  // Adam elements per 1024-thread workgroup
+// Adam elements per thread in the fused launch: one (a chunk per 1024
+// elements, ~96 workgroups for the pretraining model) — with four, QM9
+// B = 32 ran 0.2537–0.2552 ms against 0.2519–0.2527 (B = 512 unchanged,
+// profiles/r06_noise/fuse_ept_ab.txt).  Build-time A/B hook SCGIB_FUSE_EPT.
+#ifndef SCGIB_FUSE_EPT
+#define SCGIB_FUSE_EPT 1
+#endif
+constexpr int kFuseEPT = SCGIB_FUSE_EPT;
+constexpr int kFuseChunk = kFuseEPT * 1024;  // Adam elements per 1024-thread workgroup
 
 struct FuseTable {
     scgib_slab_job j[kFuseJobs];
@@ -225,7 +233,7 @@ __global__ __launch_bounds__(1024) void adam_reduce_k(const AdamTable tab, const
         float step_size, bc2_sqrt;
         adam_coef(tab.step[i], lr, beta1, beta2, step_size, bc2_sqrt);
         const int64_t base = static_cast<int64_t>(c - tab.chunk0[i]) * kFuseChunk;
-        if (T.numel > 0) adam_chunk<1024>(T, base, step_size, bc2_sqrt, beta1, beta2, eps, wd);
+        if (T.numel > 0) adam_chunk<1024, kFuseEPT>(T, base, step_size, bc2_sqrt, beta1, beta2, eps, wd);
     }
     __shared__ unsigned s_last;
     __syncthreads();

@@ -552,11 +552,11 @@ _Z_W1_OFF = _Z_SLAB
 # step (the benches' replayed steps without a collective).
 FUSE_FINAL_ADAM = True
 # ... from this many slabs in the largest final job (the ego layer-0 weight-
-# gradient slabs): QM9 B = 512 (452 slabs) 0.3850-0.3857 vs 0.3869-0.3888 ms,
-# B = 128 (111) unchanged, B = 32 (28) 0.2541-0.2553 vs 0.2527-0.2535 ms
-# (profiles/r06_noise/fuse_adam_ab.txt): below it the Adam chunks on the
-# reduce's 1024-thread workgroups outlast the small reduce they hide behind
-FUSE_FINAL_MIN_SLABS = 256
+# gradient slabs).  0: always.  With four Adam elements per thread in the
+# fused launch QM9 B = 32 (28 slabs) was slower fused and this stood at 256;
+# with one (SCGIB_FUSE_EPT) B = 32 is faster fused too
+# (profiles/r06_noise/fuse_adam_ab.txt, fuse_ept_ab.txt)
+FUSE_FINAL_MIN_SLABS = 0
 _FINAL_ARMED = [False]
 _FINAL_PENDING = {}  # device index -> [(jobs, keep)]
 
